@@ -1,0 +1,123 @@
+/*
+ * orbfe.h — C-ABI of the MI355X-native ORB front-end (liborbfe.so).
+ *
+ * Drop-in boundary for the Tracking-thread hot path of ORB-SLAM3 as vendored in
+ * giltchcity/orb_slam3_ros. Every entry point names the reference interface it replaces
+ * (paths under orb_slam3/). Plain pointers and sizes only; no exceptions cross the ABI; every
+ * call returns an int status (>= 0 ok, see ORBFE_E_*). Handles are not re-entrant (like one
+ * ORBextractor instance, whose mvImagePyramid is per-call state); distinct handles may be used
+ * concurrently from different host threads. Matcher entry points are stateless and re-entrant.
+ *
+ * Keypoints use the 28-byte cv::KeyPoint layout (pt.x, pt.y, size, angle, response, octave,
+ * class_id) so a shim can memcpy them into std::vector<cv::KeyPoint>; descriptors are n x 32 u8
+ * rows (cv::Mat CV_8U, continuous).
+ */
+#ifndef ORBFE_H
+#define ORBFE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORBFE_OK 0
+#define ORBFE_E_EMPTY (-1)      /* empty image: ORBextractor::operator() returns -1 (ORBextractor.cc:1090-1091) */
+#define ORBFE_E_ARG (-2)        /* bad type / size / argument (the reference asserts CV_8UC1, :1094) */
+#define ORBFE_E_DEVICE (-3)     /* HIP runtime error */
+#define ORBFE_E_CAPACITY (-4)   /* caller buffer too small */
+
+typedef struct orbfe_keypoint {  /* == cv::KeyPoint */
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} orbfe_keypoint;
+
+typedef struct orbfe_extractor orbfe_extractor;
+
+/* ---------------------------------------------------------------------------------------------
+ * Extractor — replaces ORB_SLAM3::ORBextractor (include/ORBextractor.h:43-112)
+ * ------------------------------------------------------------------------------------------- */
+
+/* ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST)
+ * (ORBextractor.h:49-50, ORBextractor.cc:409-469). Binds to the current HIP device. */
+int orbfe_extractor_create(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST,
+                           orbfe_extractor** out);
+void orbfe_extractor_destroy(orbfe_extractor* h);
+
+/* GetLevels / GetScaleFactors / GetInverseScaleFactors / GetScaleSigmaSquares /
+ * GetInverseScaleSigmaSquares (ORBextractor.h:61-81). Arrays have nlevels entries; any may be NULL.
+ * features_per_level: mnFeaturesPerLevel (ORBextractor.cc:434-445). */
+int orbfe_extractor_levels(const orbfe_extractor* h);
+int orbfe_extractor_scale_info(const orbfe_extractor* h, float* scale, float* inv_scale, float* sigma2,
+                               float* inv_sigma2, int* features_per_level);
+
+/* Max keypoints one image can yield (sum over levels of the octree bound); size caller buffers with it. */
+int orbfe_extractor_capacity(orbfe_extractor* h, int width, int height);
+
+/* int ORBextractor::operator()(InputArray image, InputArray mask, vector<KeyPoint>& kps,
+ *                              OutputArray desc, vector<int>& vLappingArea)   (ORBextractor.h:57-59)
+ * Host buffers: img is width x height u8 with row stride `stride` bytes. The mask is ignored, as in
+ * the reference. lap0/lap1 = vLappingArea[0..1]. On success returns monoIndex (>= 0) and writes
+ * *n keypoints / descriptors; returns ORBFE_E_EMPTY for an empty image. */
+int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int width, int height, int stride, int lap0, int lap1,
+                  orbfe_keypoint* kps, uint8_t* desc, int cap, int* n);
+
+/* The public std::vector<cv::Mat> mvImagePyramid (ORBextractor.h:83), read by
+ * Frame::ComputeStereoMatches (Frame.cc:818,908,918,923): copies level `level` of image `image`
+ * of the last call to dst (row pitch dst_pitch) and reports its size. dst may be NULL. */
+int orbfe_pyramid_level(orbfe_extractor* h, int image, int level, uint8_t* dst, int dst_pitch, int* width,
+                        int* height);
+
+/* Batched device path (multi-camera / multi-frame; Frame.cc:122-125 runs two extractors on two
+ * threads per stereo frame — here one launch sequence covers nimg images). d_imgs: nimg device
+ * pointers (host array) to width x height u8 images with row pitch `pitch`. stream: hipStream_t
+ * (NULL = the handle's own stream). Outputs stay on the device: see orbfe_batch_outputs. */
+int orbfe_extract_batch(orbfe_extractor* h, int nimg, const uint8_t* const* d_imgs, int width, int height,
+                        int pitch, int lap0, int lap1, void* stream);
+/* Device pointers of the last batch: kps[nimg][cap], desc[nimg][cap][32], counts[nimg][2] =
+ * {n, monoIndex}. Valid until the next call on this handle. */
+int orbfe_batch_outputs(orbfe_extractor* h, orbfe_keypoint** d_kps, uint8_t** d_desc, int** d_counts, int* cap);
+
+/* Per-kernel HIP-event timing of the next orbfe_extract_batch call (for bench.py's roofline).
+ * ms[0..ORBFE_NUM_STAGES) after that call: resize, blur, fast, octree, describe. */
+#define ORBFE_NUM_STAGES 5
+int orbfe_set_stage_timing(orbfe_extractor* h, int enable);
+int orbfe_get_stage_timing(orbfe_extractor* h, float* ms);
+
+/* ---------------------------------------------------------------------------------------------
+ * Stereo — replaces Frame::ComputeStereoMatches (include/Frame.h:116, src/Frame.cc:811-981)
+ * ------------------------------------------------------------------------------------------- */
+
+/* Rectified pinhole stereo for nframes frames: frame f's left image is image (lbase + f*lstep) of
+ * the last batch of `left`, its right image is image (rbase + f*rstep) of the last batch of
+ * `right` (left == right allowed, e.g. interleaved L/R). bf = mbf, fx = K(0,0) (the reference
+ * reads mb = mbf/fx). Device outputs: uright/depth[nframes][cap] (-1 = no match, Frame.cc:813-814),
+ * nmatch[nframes] (matches before the median cut). */
+int orbfe_stereo_match_batch(orbfe_extractor* left, int lbase, int lstep, orbfe_extractor* right, int rbase,
+                             int rstep, int nframes, float bf, float fx, float* d_uright, float* d_depth,
+                             int* d_nmatch, void* stream);
+
+/* Host convenience for one frame: uses the last orbfe_extract call of `left` and `right` and writes
+ * host arrays uright[n_left], depth[n_left]. Returns the pre-cut match count. */
+int orbfe_stereo_match(orbfe_extractor* left, orbfe_extractor* right, float bf, float fx, float* uright,
+                       float* depth);
+
+/* ---------------------------------------------------------------------------------------------
+ * ORBmatcher — replaces ORB_SLAM3::ORBmatcher::DescriptorDistance (ORBmatcher.cc:2058-2074)
+ * ------------------------------------------------------------------------------------------- */
+int orbfe_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* Debug/inspection (tests only): copy an intermediate of image `image`, level `level` of the last
+ * batch to host memory. what: 0 = per-cell FAST key counts (int32[n_cells]),
+ * 1 = per-cell FAST key slots (uint32[n_cells * cell_cap], x_rel | y_rel << 12 | score << 24),
+ * 2 = DistributeOctTree output (uint32[n], x | y << 12 | score << 24) followed by nothing,
+ * 3 = per-level info int32[4] {n, n_lap, n_mono, n_raw}. Returns the element count. */
+int orbfe_debug_copy(orbfe_extractor* h, int what, int image, int level, void* dst, int cap_bytes);
+
+/* Library identification (build string). */
+const char* orbfe_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORBFE_H */

@@ -1,0 +1,123 @@
+"""ctypes wrapper of the CPU ORACLE (oracle/liborb_oracle.so) — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module. It
+is the checker (and the timed CPU baseline), never the product path. Parity status: see the
+header of oracle/orb_oracle.cpp ("parity unpinned" w.r.t. the real OpenCV-based reference).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(_HERE, "liborb_oracle.so")
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+
+def build(force: bool = False) -> str:
+    srcs = [os.path.join(_HERE, f) for f in ("orb_oracle.cpp", "orb_oracle_match.cpp", "Makefile")]
+    if force or not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in srcs):
+        subprocess.run(["make", "-C", _HERE, "-B" if force else "-s"], check=True)
+    return LIB
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        vp, ci, cf = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+        L.oro_create.restype = vp
+        L.oro_create.argtypes = [ci, cf, ci, ci, ci]
+        L.oro_destroy.argtypes = [vp]
+        L.oro_set_model.argtypes = [vp, ci, ci]
+        L.oro_level_info.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        L.oro_extract.argtypes = [vp, vp, ci, ci, ci, ci, ci, vp, ci, vp, ctypes.POINTER(ci)]
+        L.oro_pyramid_level.argtypes = [vp, ci, vp, ci, ctypes.POINTER(ci), ctypes.POINTER(ci)]
+        L.oro_debug_keys.argtypes = [vp, ci, ci, vp, ci]
+        L.oro_resize.argtypes = [vp, ci, ci, vp, ci, ci, ci]
+        L.oro_blur.argtypes = [vp, ci, ci, vp, ci]
+        L.oro_fast.argtypes = [vp, ci, ci, ci, ci, vp, ci]
+        L.oro_fast_atan2.restype = cf
+        L.oro_fast_atan2.argtypes = [cf, cf]
+        L.oro_hamming.argtypes = [vp, vp]
+        L.oro_stereo_match.argtypes = [vp, vp, vp, vp, ci, vp, vp, ci, cf, cf, vp, vp]
+        L.oro_bench_extract.restype = ctypes.c_double
+        L.oro_bench_extract.argtypes = [vp, ci, ci, ci, ci, cf, ci, ci, ci, ci, ctypes.POINTER(ci)]
+        _lib = L
+    return _lib
+
+
+class OracleExtractor:
+    """CPU restatement of ORB_SLAM3::ORBextractor (see oracle/orb_oracle.cpp)."""
+
+    def __init__(self, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, resize_simd_lanes=16, blur_variant=0):
+        self._l = lib()
+        self.h = self._l.oro_create(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
+        self._l.oro_set_model(self.h, resize_simd_lanes, blur_variant)
+        self.nlevels = nlevels
+
+    def level_info(self):
+        n = self.nlevels
+        out = [np.zeros(n, np.float32) for _ in range(4)] + [np.zeros(n, np.int32), np.zeros(16, np.int32)]
+        self._l.oro_level_info(self.h, *[a.ctypes.data for a in out])
+        return dict(zip(("scale", "inv_scale", "sigma2", "inv_sigma2", "per_level", "umax"), out))
+
+    def __call__(self, img, lap=(0, 0)):
+        img = np.ascontiguousarray(img, np.uint8)
+        h, w = img.shape
+        cap = 20000
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = ctypes.c_int()
+        mono = self._l.oro_extract(self.h, img.ctypes.data, w, h, w, lap[0], lap[1], kps.ctypes.data, cap,
+                                   desc.ctypes.data, ctypes.byref(n))
+        return mono, kps[: n.value].copy(), desc[: n.value].copy()
+
+    def pyramid_level(self, level):
+        w, h = ctypes.c_int(), ctypes.c_int()
+        self._l.oro_pyramid_level(self.h, level, None, 0, ctypes.byref(w), ctypes.byref(h))
+        out = np.zeros((h.value, w.value), np.uint8)
+        self._l.oro_pyramid_level(self.h, level, out.ctypes.data, out.size, ctypes.byref(w), ctypes.byref(h))
+        return out
+
+    def debug_keys(self, level, which):
+        """which=0: raw FAST keys of the level (vToDistributeKeys, coords relative to minBorder);
+        which=1: DistributeOctTree output (level coords, before scaling)."""
+        n = self._l.oro_debug_keys(self.h, level, which, None, 0)
+        out = np.zeros(n, KEYPOINT_DTYPE)
+        self._l.oro_debug_keys(self.h, level, which, out.ctypes.data, n)
+        return out
+
+    def close(self):
+        if self.h:
+            self._l.oro_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def stereo_match(ext_l: OracleExtractor, ext_r: OracleExtractor, kl, dl, kr, dr, bf, fx):
+    L = lib()
+    n = len(kl)
+    ur = np.zeros(max(n, 1), np.float32)
+    dp = np.zeros(max(n, 1), np.float32)
+    kl = np.ascontiguousarray(kl)
+    kr = np.ascontiguousarray(kr)
+    dl = np.ascontiguousarray(dl)
+    dr = np.ascontiguousarray(dr)
+    nm = L.oro_stereo_match(ext_l.h, ext_r.h, kl.ctypes.data, dl.ctypes.data, n, kr.ctypes.data, dr.ctypes.data,
+                            len(kr), bf, fx, ur.ctypes.data, dp.ctypes.data)
+    return ur[:n], dp[:n], nm

@@ -1,0 +1,90 @@
+"""ctypes binding of liborbfe.so (the C-ABI declared in include/orbfe.h).
+
+The library is built in-tree by orb_slam3_ros_amd.build.build_library() (hipcc, gfx950). There is
+no CPU fallback: if the shared object is missing or fails to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liborbfe.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "orbfe.h")
+
+ORBFE_OK = 0
+ORBFE_E_EMPTY = -1
+ORBFE_E_ARG = -2
+ORBFE_E_DEVICE = -3
+ORBFE_E_CAPACITY = -4
+ORBFE_NUM_STAGES = 5
+STAGE_NAMES = ("resize", "blur", "fast", "octree", "describe")
+
+
+class OrbKeyPoint(ctypes.Structure):
+    """cv::KeyPoint byte layout (28 B)."""
+    _fields_ = [("x", ctypes.c_float), ("y", ctypes.c_float), ("size", ctypes.c_float),
+                ("angle", ctypes.c_float), ("response", ctypes.c_float),
+                ("octave", ctypes.c_int32), ("class_id", ctypes.c_int32)]
+
+
+_c_int, _c_float, _vp = ctypes.c_int, ctypes.c_float, ctypes.c_void_p
+_P_int, _P_float = ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_float)
+
+_SIGS = {
+    "orbfe_extractor_create": (_c_int, [_c_int, _c_float, _c_int, _c_int, _c_int, ctypes.POINTER(_vp)]),
+    "orbfe_extractor_destroy": (None, [_vp]),
+    "orbfe_extractor_levels": (_c_int, [_vp]),
+    "orbfe_extractor_scale_info": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "orbfe_extractor_capacity": (_c_int, [_vp, _c_int, _c_int]),
+    "orbfe_extract": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _P_int]),
+    "orbfe_pyramid_level": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _P_int, _P_int]),
+    "orbfe_extract_batch": (_c_int, [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp]),
+    "orbfe_batch_outputs": (_c_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp), _P_int]),
+    "orbfe_set_stage_timing": (_c_int, [_vp, _c_int]),
+    "orbfe_get_stage_timing": (_c_int, [_vp, _vp]),
+    "orbfe_stereo_match_batch": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_float, _c_float,
+                                          _vp, _vp, _vp, _vp]),
+    "orbfe_stereo_match": (_c_int, [_vp, _vp, _c_float, _c_float, _vp, _vp]),
+    "orbfe_descriptor_distance": (_c_int, [_vp, _vp]),
+    "orbfe_debug_copy": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _c_int]),
+    "orbfe_version": (ctypes.c_char_p, []),
+}
+
+_lib = None
+
+
+class OrbfeError(RuntimeError):
+    pass
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load liborbfe.so (raises OrbfeError if it is missing: there is no fallback path)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    # One HIP runtime per process: torch ships its own libamdhip64.so with the same soname as
+    # /opt/rocm's. Import torch first (when present) so liborbfe.so binds to that runtime too;
+    # loading ours first would put two runtimes in the process and break device calls.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    if not os.path.exists(p):
+        raise OrbfeError(f"liborbfe.so not found at {p}; build it with orb_slam3_ros_amd.build.build_library()")
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> int:
+    if rc < 0 and rc != ORBFE_E_EMPTY:
+        names = {ORBFE_E_ARG: "bad argument", ORBFE_E_DEVICE: "HIP device error", ORBFE_E_CAPACITY: "capacity"}
+        raise OrbfeError(f"{what} failed: {names.get(rc, rc)}")
+    return rc

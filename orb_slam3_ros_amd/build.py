@@ -1,0 +1,37 @@
+"""In-tree build of liborbfe.so (hipcc, gfx950). The .so travels to the GPU box with the snapshot."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(_HERE, "csrc")
+LIB = os.path.join(_HERE, "liborbfe.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+SOURCES = ["orbfe_engine.hip"]
+DEPS = ["orbfe_engine.hip", "orbfe_kernels.hip", "orbfe_types.h", "glibc_sincosf.h", "stl_sort.h",
+        "brief_pattern.h", "orbfe_matcher.hip"]
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+         "-fno-fast-math", "-Wall", "-Wno-unused-function"]
+
+
+def _stale(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    hdr = os.path.join(os.path.dirname(_HERE), "include", "orbfe.h")
+    return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps + [hdr])
+
+
+def build_library(force: bool = False, verbose: bool = False) -> str:
+    deps = [os.path.join(CSRC, d) for d in DEPS]
+    if force or _stale(LIB, deps):
+        cmd = [HIPCC] + FLAGS + ["-o", LIB] + [os.path.join(CSRC, s) for s in SOURCES]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build_library(force=True, verbose=True))

@@ -1,0 +1,570 @@
+// Host engine + C-ABI of liborbfe.so (declared in include/orbfe.h).
+// Owns the device buffers of one extractor handle (sized for the largest batch seen so far),
+// derives the per-level geometry with the reference's exact expressions, and launches the
+// kernel sequence of orbfe_kernels.hip on one HIP stream.
+#pragma clang fp contract(off)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/orbfe.h"
+#include "orbfe_types.h"
+
+// Single translation unit: the kernels are compiled together with their launchers.
+#include "orbfe_kernels.hip"
+
+using namespace orbfe;
+
+#define HIPCHK(x)                                                                                 \
+    do {                                                                                          \
+        hipError_t e_ = (x);                                                                      \
+        if (e_ != hipSuccess) {                                                                   \
+            fprintf(stderr, "orbfe: HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+            return ORBFE_E_DEVICE;                                                                \
+        }                                                                                         \
+    } while (0)
+
+namespace {
+
+inline int cv_round(float v) { return (int)std::lrintf(v); }
+inline int cv_floor(float v) { int i = (int)v; return i - (i > v); }
+inline short sat_s16(float v) {
+    int iv = cv_round(v);
+    return (short)std::min(32767, std::max(-32768, iv));
+}
+inline int round_up(int v, int a) { return (v + a - 1) / a * a; }
+
+// blur kernel quantisation (see oracle header): 0 = OpenCV >= 3.4.6 error-diffusion (default)
+const int kBlurED[7] = {18, 34, 48, 56, 48, 34, 18};
+const int kBlurRound[7] = {18, 34, 49, 55, 49, 34, 18};
+
+size_t octree_lds_bytes(const OrbGeom& g) {
+    auto a16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    const size_t NC = g.node_cap;
+    size_t s = a16(sizeof(int) * (g.max_cells_level + 1));
+    s += 2 * (4 * a16(2 * NC) + a16(4 * NC));
+    s += 2 * a16(16 * NC);
+    s += a16(8 * NC) + a16(2 * NC) + a16(4 * NC) * 5;
+    s += a16(12 * NC) + a16(8 * NC);
+    return s;
+}
+
+}  // namespace
+
+struct orbfe_extractor {
+    int nfeatures, nlevels, ini_th, min_th;
+    float scale_factor_f;
+    double scale_factor;
+    int resize_simd_lanes = 16;
+    int blur_variant = 0;
+    std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
+    std::vector<int> per_level;
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    // geometry of the current allocation
+    int W = 0, H = 0, cap_b = 0;
+    OrbGeom g{};
+    std::vector<int16_t> tab;
+    int roi_max = 0;
+    size_t oct_lds = 0;
+    // device buffers
+    int16_t* d_tab = nullptr;
+    uint8_t* d_pyr = nullptr;
+    uint8_t* d_blur = nullptr;
+    uint32_t* d_cellkeys = nullptr;
+    int* d_cellcnt = nullptr;
+    uint32_t* d_lkeys = nullptr;
+    uint16_t* d_nodeof = nullptr;
+    uint32_t* d_outkeys = nullptr;
+    int* d_lvinfo = nullptr;
+    int* d_ranks = nullptr;
+    OrbKeyPoint* d_kps = nullptr;
+    uint8_t* d_desc = nullptr;
+    int* d_counts = nullptr;
+    const uint8_t** d_ptrs = nullptr;
+    uint8_t* d_stage = nullptr;    // host-API input staging (one image)
+    size_t stage_bytes = 0;
+    float* d_uright = nullptr;
+    float* d_depth = nullptr;
+    int* d_nmatch = nullptr;
+    int stereo_cap_frames = 0;
+    // last batch description
+    int last_nimg = 0, last_pitch = 0;
+    std::vector<const uint8_t*> last_ptrs;
+    // stage timing
+    bool timing = false;
+    hipEvent_t ev[ORBFE_NUM_STAGES + 1] = {};
+    float stage_ms[ORBFE_NUM_STAGES] = {};
+    std::mutex mu;
+};
+
+static void free_buffers(orbfe_extractor* h) {
+    void** bufs[] = {(void**)&h->d_tab, (void**)&h->d_pyr, (void**)&h->d_blur, (void**)&h->d_cellkeys,
+                     (void**)&h->d_cellcnt, (void**)&h->d_lkeys, (void**)&h->d_nodeof, (void**)&h->d_outkeys,
+                     (void**)&h->d_lvinfo, (void**)&h->d_ranks, (void**)&h->d_kps, (void**)&h->d_desc,
+                     (void**)&h->d_counts, (void**)&h->d_ptrs};
+    for (void** p : bufs) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+    }
+    h->cap_b = 0;
+}
+
+// Per-level geometry with the reference's expressions (see orbfe_types.h).
+static int build_geom(orbfe_extractor* h, int W, int H) {
+    OrbGeom& g = h->g;
+    memset(&g, 0, sizeof(g));
+    g.nlevels = h->nlevels;
+    g.width = W;
+    g.height = H;
+    g.ini_th = std::min(std::max(h->ini_th, 0), 255);
+    g.min_th = std::min(std::max(h->min_th, 0), 255);
+    h->tab.clear();
+    int cell_base = 0, cellkey_off = 0, out_off = 0, pyr_off = 0, blur_off = 0, tile_base = 0;
+    int max_cells = 0, node_cap = 0, roi_max = 0;
+    int pw = W, ph = H;
+    for (int l = 0; l < h->nlevels; l++) {
+        OrbLevel& L = g.lv[l];
+        L.w = cv_round((float)W * h->inv_scale[l]);
+        L.h = cv_round((float)H * h->inv_scale[l]);
+        if (L.w < 2 * ORBFE_MINB + ORBFE_CELL + 6 || L.h < 2 * ORBFE_MINB + ORBFE_CELL + 6 || L.w > 4096 + 32 ||
+            L.h > 4096 + 32)
+            return ORBFE_E_ARG;
+        L.scale = h->scale[l];
+        L.inv_scale = h->inv_scale[l];
+        L.patch_size = (int)(31 * h->scale[l]);
+        L.pitch = round_up(L.w, 16);
+        L.pyr_off = l == 0 ? 0 : pyr_off;
+        if (l > 0) pyr_off += round_up(L.pitch * L.h, 256);
+        L.blur_off = blur_off;
+        blur_off += round_up(L.pitch * L.h, 256);
+        // FAST cell grid (ORBextractor.cc:789-803)
+        const int minB = ORBFE_MINB, maxBX = L.w - ORBFE_MINB, maxBY = L.h - ORBFE_MINB;
+        const float width = (float)(maxBX - minB), height = (float)(maxBY - minB);
+        const float Wc = ORBFE_CELL;
+        L.n_cols = (int)(width / Wc);
+        L.n_rows = (int)(height / Wc);
+        L.w_cell = (int)std::ceil(width / L.n_cols);
+        L.h_cell = (int)std::ceil(height / L.n_rows);
+        L.cell_base = cell_base;
+        const int ncell = L.n_cols * L.n_rows;
+        cell_base += ncell;
+        max_cells = std::max(max_cells, ncell);
+        L.cell_cap = ((L.w_cell + 1) / 2) * ((L.h_cell + 1) / 2);
+        L.cellkey_off = cellkey_off;
+        cellkey_off += ncell * L.cell_cap;
+        roi_max = std::max(roi_max, round_up((L.w_cell + 6) * (L.h_cell + 6), 16));
+        // octree
+        L.budget = h->per_level[l];
+        L.n_ini = (int)std::round((float)(maxBX - minB) / (maxBY - minB));
+        if (L.n_ini < 1) return ORBFE_E_ARG;   // the reference indexes an empty node vector here
+        L.hx = (float)(maxBX - minB) / L.n_ini;
+        L.out_cap = std::max(L.budget + 3, 4 * L.n_ini);
+        L.out_off = out_off;
+        out_off += L.out_cap;
+        node_cap = std::max(node_cap, L.out_cap + 4);
+        // resize tables (cv::resize INTER_LINEAR, dsize given, from level l-1)
+        if (l > 0) {
+            const double inv_x = (double)L.w / pw, inv_y = (double)L.h / ph;
+            const double scale_x = 1. / inv_x, scale_y = 1. / inv_y;
+            L.tab_x = (int)h->tab.size();
+            int xmax = L.w;
+            for (int dx = 0; dx < L.w; dx++) {
+                float fx = (float)((dx + 0.5) * scale_x - 0.5);
+                int sx = cv_floor(fx);
+                fx -= sx;
+                if (sx < 0) { fx = 0; sx = 0; }
+                if (sx + 1 >= pw) {
+                    xmax = std::min(xmax, dx);
+                    if (sx >= pw - 1) { fx = 0; sx = pw - 1; }
+                }
+                h->tab.push_back((int16_t)sx);
+                h->tab.push_back(sat_s16((1.f - fx) * 2048));
+                h->tab.push_back(sat_s16(fx * 2048));
+            }
+            L.xmax = xmax;
+            L.tab_y = (int)h->tab.size();
+            for (int dy = 0; dy < L.h; dy++) {
+                float fy = (float)((dy + 0.5) * scale_y - 0.5);
+                int sy = cv_floor(fy);
+                fy -= sy;
+                auto clip = [&](int v) { return v < 0 ? 0 : (v >= ph ? ph - 1 : v); };
+                h->tab.push_back((int16_t)clip(sy));
+                h->tab.push_back((int16_t)clip(sy + 1));
+                h->tab.push_back(sat_s16((1.f - fy) * 2048));
+                h->tab.push_back(sat_s16(fy * 2048));
+            }
+            int x = 0;
+            const int lanes = h->resize_simd_lanes;
+            if (lanes > 0) {
+                for (; x <= L.w - lanes; x += lanes) {}
+                for (; x < L.w - lanes / 2; x += lanes / 2) {}
+            }
+            L.simd_end = x;
+            L.resize_row_blocks = (L.h + 3) / 4;
+        }
+        L.blur_tiles_x = (L.w + 63) / 64;
+        L.blur_tiles_y = (L.h + 15) / 16;
+        L.blur_tile_base = tile_base;
+        tile_base += L.blur_tiles_x * L.blur_tiles_y;
+        pw = L.w;
+        ph = L.h;
+    }
+    g.total_cells = cell_base;
+    g.cellkeys_per_img = cellkey_off;
+    g.out_per_img = out_off;
+    g.kp_cap = out_off;
+    g.pyr_bytes = round_up(std::max(pyr_off, 256), 256);
+    g.blur_bytes = round_up(blur_off, 256);
+    g.blur_tiles = tile_base;
+    g.max_cells_level = max_cells;
+    g.node_cap = node_cap;
+    h->roi_max = roi_max;
+    h->oct_lds = octree_lds_bytes(g);
+    return ORBFE_OK;
+}
+
+static int ensure(orbfe_extractor* h, int W, int H, int B) {
+    if (W == h->W && H == h->H && B <= h->cap_b) return ORBFE_OK;
+    HIPCHK(hipSetDevice(h->device));
+    if (W != h->W || H != h->H) {
+        free_buffers(h);
+        int rc = build_geom(h, W, H);
+        if (rc) return rc;
+        h->W = W;
+        h->H = H;
+    } else {
+        free_buffers(h);
+    }
+    if (h->oct_lds > 160 * 1024) return ORBFE_E_ARG;
+    B = std::max(B, 1);
+    const OrbGeom& g = h->g;
+    HIPCHK(hipMalloc(&h->d_tab, std::max<size_t>(2, h->tab.size() * 2)));
+    HIPCHK(hipMemcpy(h->d_tab, h->tab.data(), h->tab.size() * 2, hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&h->d_pyr, (size_t)B * g.pyr_bytes));
+    HIPCHK(hipMalloc(&h->d_blur, (size_t)B * g.blur_bytes));
+    HIPCHK(hipMalloc(&h->d_cellkeys, (size_t)B * g.cellkeys_per_img * 4));
+    HIPCHK(hipMalloc(&h->d_cellcnt, (size_t)B * g.total_cells * 4));
+    HIPCHK(hipMalloc(&h->d_lkeys, (size_t)B * g.cellkeys_per_img * 4));
+    HIPCHK(hipMalloc(&h->d_nodeof, (size_t)B * g.cellkeys_per_img * 2));
+    HIPCHK(hipMalloc(&h->d_outkeys, (size_t)B * g.out_per_img * 4));
+    HIPCHK(hipMalloc(&h->d_lvinfo, (size_t)B * g.nlevels * 4 * 4));
+    HIPCHK(hipMalloc(&h->d_ranks, (size_t)B * g.out_per_img * 4));
+    HIPCHK(hipMalloc(&h->d_kps, (size_t)B * g.kp_cap * sizeof(OrbKeyPoint)));
+    HIPCHK(hipMalloc(&h->d_desc, (size_t)B * g.kp_cap * 32));
+    HIPCHK(hipMalloc(&h->d_counts, (size_t)B * 2 * 4));
+    HIPCHK(hipMalloc(&h->d_ptrs, (size_t)B * sizeof(void*)));
+    h->cap_b = B;
+    h->last_ptrs.clear();
+    return ORBFE_OK;
+}
+
+static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs, int pitch, int lap0, int lap1,
+                     hipStream_t s) {
+    const OrbGeom& g = h->g;
+    bool same = (int)h->last_ptrs.size() == B;
+    for (int i = 0; same && i < B; i++) same = h->last_ptrs[i] == host_ptrs[i];
+    if (!same) {
+        h->last_ptrs.assign(host_ptrs, host_ptrs + B);
+        HIPCHK(hipMemcpyAsync(h->d_ptrs, h->last_ptrs.data(), (size_t)B * sizeof(void*), hipMemcpyHostToDevice, s));
+    }
+    h->last_nimg = B;
+    h->last_pitch = pitch;
+    const uint8_t* const* P = h->d_ptrs;
+    const bool tm = h->timing;
+    if (tm) HIPCHK(hipEventRecord(h->ev[0], s));
+    for (int l = 1; l < g.nlevels; l++) {
+        dim3 grid(g.lv[l].resize_row_blocks, B);
+        hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, s, P, pitch, h->d_pyr, g.pyr_bytes, h->d_tab, g, l);
+    }
+    if (tm) HIPCHK(hipEventRecord(h->ev[1], s));
+    BlurKernel bk;
+    memcpy(bk.k, h->blur_variant == 1 ? kBlurRound : kBlurED, sizeof(bk.k));
+    hipLaunchKernelGGL(k_blur, dim3(g.blur_tiles, B), dim3(256), 0, s, P, pitch, h->d_pyr, g.pyr_bytes, h->d_blur,
+                       g.blur_bytes, g, bk);
+    if (tm) HIPCHK(hipEventRecord(h->ev[2], s));
+    hipLaunchKernelGGL(k_fast, dim3((g.total_cells + 3) / 4, B), dim3(256), (size_t)4 * 2 * h->roi_max, s, P, pitch,
+                       h->d_pyr, g.pyr_bytes, g, h->roi_max, h->d_cellkeys, h->d_cellcnt);
+    if (tm) HIPCHK(hipEventRecord(h->ev[3], s));
+    hipLaunchKernelGGL(k_octree, dim3(g.nlevels, B), dim3(64), h->oct_lds, s, g, h->d_cellkeys, h->d_cellcnt,
+                       h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, lap0, lap1);
+    if (tm) HIPCHK(hipEventRecord(h->ev[4], s));
+    hipLaunchKernelGGL(k_describe, dim3((g.out_per_img + 3) / 4, B), dim3(256), 0, s, P, pitch, h->d_pyr,
+                       g.pyr_bytes, h->d_blur, g.blur_bytes, g, h->d_outkeys, h->d_lvinfo, h->d_ranks, h->d_kps,
+                       h->d_desc, h->d_counts);
+    if (tm) HIPCHK(hipEventRecord(h->ev[5], s));
+    HIPCHK(hipGetLastError());
+    if (tm) {
+        HIPCHK(hipEventSynchronize(h->ev[5]));
+        for (int i = 0; i < ORBFE_NUM_STAGES; i++) HIPCHK(hipEventElapsedTime(&h->stage_ms[i], h->ev[i], h->ev[i + 1]));
+    }
+    return ORBFE_OK;
+}
+
+static hipStream_t pick_stream(orbfe_extractor* h, void* stream) {
+    return stream ? (hipStream_t)stream : h->own_stream;
+}
+
+extern "C" {
+
+const char* orbfe_version(void) { return "orbfe 0.1 (gfx950, HIP)"; }
+
+int orbfe_extractor_create(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST,
+                           orbfe_extractor** out) {
+    if (!out || nfeatures <= 0 || nlevels <= 0 || nlevels > ORBFE_MAX_LEVELS || !(scaleFactor > 1.0f))
+        return ORBFE_E_ARG;
+    orbfe_extractor* h = new orbfe_extractor();
+    h->nfeatures = nfeatures;
+    h->nlevels = nlevels;
+    h->ini_th = iniThFAST;
+    h->min_th = minThFAST;
+    h->scale_factor_f = scaleFactor;
+    h->scale_factor = scaleFactor;   // double member initialised from the float argument (ORBextractor.h:96)
+    // ORBextractor.cc:414-445
+    h->scale.resize(nlevels);
+    h->sigma2.resize(nlevels);
+    h->scale[0] = 1.0f;
+    h->sigma2[0] = 1.0f;
+    for (int i = 1; i < nlevels; i++) {
+        h->scale[i] = (float)(h->scale[i - 1] * h->scale_factor);
+        h->sigma2[i] = h->scale[i] * h->scale[i];
+    }
+    h->inv_scale.resize(nlevels);
+    h->inv_sigma2.resize(nlevels);
+    for (int i = 0; i < nlevels; i++) {
+        h->inv_scale[i] = 1.0f / h->scale[i];
+        h->inv_sigma2[i] = 1.0f / h->sigma2[i];
+    }
+    h->per_level.resize(nlevels);
+    const float factor = (float)(1.0f / h->scale_factor);
+    float nDesired = nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)nlevels));
+    int sum = 0;
+    for (int l = 0; l < nlevels - 1; l++) {
+        h->per_level[l] = cv_round(nDesired);
+        sum += h->per_level[l];
+        nDesired *= factor;
+    }
+    h->per_level[nlevels - 1] = std::max(nfeatures - sum, 0);
+    hipError_t e = hipGetDevice(&h->device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
+    for (int i = 0; e == hipSuccess && i <= ORBFE_NUM_STAGES; i++) e = hipEventCreate(&h->ev[i]);
+    if (e != hipSuccess) {
+        fprintf(stderr, "orbfe: extractor_create: HIP error %s\n", hipGetErrorString(e));
+        delete h;
+        return ORBFE_E_DEVICE;
+    }
+    *out = h;
+    return ORBFE_OK;
+}
+
+void orbfe_extractor_destroy(orbfe_extractor* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    (void)hipDeviceSynchronize();
+    free_buffers(h);
+    if (h->d_stage) (void)hipFree(h->d_stage);
+    if (h->d_uright) (void)hipFree(h->d_uright);
+    if (h->d_depth) (void)hipFree(h->d_depth);
+    if (h->d_nmatch) (void)hipFree(h->d_nmatch);
+    for (int i = 0; i <= ORBFE_NUM_STAGES; i++)
+        if (h->ev[i]) (void)hipEventDestroy(h->ev[i]);
+    if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+    delete h;
+}
+
+int orbfe_extractor_levels(const orbfe_extractor* h) { return h ? h->nlevels : ORBFE_E_ARG; }
+
+int orbfe_extractor_scale_info(const orbfe_extractor* h, float* scale, float* inv_scale, float* sigma2,
+                               float* inv_sigma2, int* per_level) {
+    if (!h) return ORBFE_E_ARG;
+    for (int l = 0; l < h->nlevels; l++) {
+        if (scale) scale[l] = h->scale[l];
+        if (inv_scale) inv_scale[l] = h->inv_scale[l];
+        if (sigma2) sigma2[l] = h->sigma2[l];
+        if (inv_sigma2) inv_sigma2[l] = h->inv_sigma2[l];
+        if (per_level) per_level[l] = h->per_level[l];
+    }
+    return ORBFE_OK;
+}
+
+int orbfe_extractor_capacity(orbfe_extractor* h, int width, int height) {
+    if (!h) return ORBFE_E_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (width != h->W || height != h->H) {
+        int rc = ensure(h, width, height, std::max(h->cap_b, 1));
+        if (rc) return rc;
+    }
+    return h->g.kp_cap;
+}
+
+int orbfe_extract_batch(orbfe_extractor* h, int nimg, const uint8_t* const* d_imgs, int width, int height, int pitch,
+                        int lap0, int lap1, void* stream) {
+    if (!h || nimg <= 0 || !d_imgs || pitch < width) return ORBFE_E_ARG;
+    if (width <= 0 || height <= 0) return ORBFE_E_EMPTY;
+    std::lock_guard<std::mutex> lk(h->mu);
+    int rc = ensure(h, width, height, nimg);
+    if (rc) return rc;
+    return run_batch(h, nimg, d_imgs, pitch, lap0, lap1, pick_stream(h, stream));
+}
+
+int orbfe_batch_outputs(orbfe_extractor* h, orbfe_keypoint** d_kps, uint8_t** d_desc, int** d_counts, int* cap) {
+    if (!h || !h->cap_b) return ORBFE_E_ARG;
+    if (d_kps) *d_kps = (orbfe_keypoint*)h->d_kps;
+    if (d_desc) *d_desc = h->d_desc;
+    if (d_counts) *d_counts = h->d_counts;
+    if (cap) *cap = h->g.kp_cap;
+    return ORBFE_OK;
+}
+
+int orbfe_set_stage_timing(orbfe_extractor* h, int enable) {
+    if (!h) return ORBFE_E_ARG;
+    h->timing = enable != 0;
+    return ORBFE_OK;
+}
+int orbfe_get_stage_timing(orbfe_extractor* h, float* ms) {
+    if (!h || !ms) return ORBFE_E_ARG;
+    memcpy(ms, h->stage_ms, sizeof(h->stage_ms));
+    return ORBFE_OK;
+}
+
+int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int width, int height, int stride, int lap0, int lap1,
+                  orbfe_keypoint* kps, uint8_t* desc, int cap, int* n) {
+    if (!h || !n) return ORBFE_E_ARG;
+    *n = 0;
+    if (!img || width <= 0 || height <= 0) return ORBFE_E_EMPTY;
+    if (stride < width) return ORBFE_E_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    int rc = ensure(h, width, height, 1);
+    if (rc) return rc;
+    hipStream_t s = h->own_stream;
+    const size_t bytes = (size_t)width * height;
+    if (h->stage_bytes < bytes) {
+        if (h->d_stage) HIPCHK(hipFree(h->d_stage));
+        HIPCHK(hipMalloc(&h->d_stage, bytes));
+        h->stage_bytes = bytes;
+    }
+    HIPCHK(hipMemcpy2DAsync(h->d_stage, width, img, stride, width, height, hipMemcpyHostToDevice, s));
+    const uint8_t* ptrs[1] = {h->d_stage};
+    rc = run_batch(h, 1, ptrs, width, lap0, lap1, s);
+    if (rc) return rc;
+    int cnt[2];
+    HIPCHK(hipMemcpyAsync(cnt, h->d_counts, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    *n = cnt[0];
+    if (cnt[0] > cap) return ORBFE_E_CAPACITY;
+    if (cnt[0] > 0) {
+        if (kps) HIPCHK(hipMemcpyAsync(kps, h->d_kps, (size_t)cnt[0] * sizeof(OrbKeyPoint), hipMemcpyDeviceToHost, s));
+        if (desc) HIPCHK(hipMemcpyAsync(desc, h->d_desc, (size_t)cnt[0] * 32, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    return cnt[1];
+}
+
+int orbfe_pyramid_level(orbfe_extractor* h, int image, int level, uint8_t* dst, int dst_pitch, int* width,
+                        int* height) {
+    if (!h || level < 0 || level >= h->nlevels || !h->cap_b || image < 0 || image >= h->last_nimg) return ORBFE_E_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    const OrbLevel& L = h->g.lv[level];
+    if (width) *width = L.w;
+    if (height) *height = L.h;
+    if (!dst) return ORBFE_OK;
+    if (dst_pitch < L.w) return ORBFE_E_CAPACITY;
+    HIPCHK(hipStreamSynchronize(h->own_stream));
+    HIPCHK(hipDeviceSynchronize());
+    const uint8_t* src;
+    int sp;
+    if (level == 0) { src = h->last_ptrs[image]; sp = h->last_pitch; }
+    else { src = h->d_pyr + (size_t)image * h->g.pyr_bytes + L.pyr_off; sp = L.pitch; }
+    HIPCHK(hipMemcpy2D(dst, dst_pitch, src, sp, L.w, L.h, hipMemcpyDeviceToHost));
+    return ORBFE_OK;
+}
+
+int orbfe_stereo_match_batch(orbfe_extractor* left, int lbase, int lstep, orbfe_extractor* right, int rbase,
+                             int rstep, int nframes, float bf, float fx, float* d_uright, float* d_depth,
+                             int* d_nmatch, void* stream) {
+    if (!left || !right || nframes <= 0 || !left->cap_b || !right->cap_b) return ORBFE_E_ARG;
+    if (left->W != right->W || left->H != right->H || left->nlevels != right->nlevels ||
+        left->nfeatures != right->nfeatures || left->scale_factor_f != right->scale_factor_f)
+        return ORBFE_E_ARG;
+    if (lbase + (nframes - 1) * lstep >= left->last_nimg || rbase + (nframes - 1) * rstep >= right->last_nimg)
+        return ORBFE_E_ARG;
+    const OrbGeom& g = left->g;
+    StereoSide SL{left->d_ptrs, left->last_pitch, left->d_pyr, g.pyr_bytes, left->d_kps, left->d_desc,
+                  left->d_counts, lbase, lstep};
+    StereoSide SR{right->d_ptrs, right->last_pitch, right->d_pyr, right->g.pyr_bytes, right->d_kps, right->d_desc,
+                  right->d_counts, rbase, rstep};
+    StereoArgs sa{bf, fx, g.kp_cap};
+    const size_t lds = (size_t)g.kp_cap * (32 + 4 * 6);
+    if (lds > 160 * 1024) return ORBFE_E_ARG;
+    hipStream_t s = pick_stream(left, stream);
+    hipLaunchKernelGGL(k_stereo, dim3(nframes), dim3(256), lds, s, g, SL, SR, sa, d_uright, d_depth, d_nmatch);
+    HIPCHK(hipGetLastError());
+    return ORBFE_OK;
+}
+
+int orbfe_stereo_match(orbfe_extractor* left, orbfe_extractor* right, float bf, float fx, float* uright,
+                       float* depth) {
+    if (!left || !right) return ORBFE_E_ARG;
+    std::lock_guard<std::mutex> lk(left->mu);
+    if (!left->d_uright || left->stereo_cap_frames < 1) {
+        HIPCHK(hipMalloc(&left->d_uright, (size_t)left->g.kp_cap * 4));
+        HIPCHK(hipMalloc(&left->d_depth, (size_t)left->g.kp_cap * 4));
+        HIPCHK(hipMalloc(&left->d_nmatch, 4));
+        left->stereo_cap_frames = 1;
+    }
+    HIPCHK(hipStreamSynchronize(right->own_stream));
+    int rc = orbfe_stereo_match_batch(left, 0, 1, right, 0, 1, 1, bf, fx, left->d_uright, left->d_depth,
+                                      left->d_nmatch, nullptr);
+    if (rc) return rc;
+    hipStream_t s = left->own_stream;
+    int cnt[2], nm = 0;
+    HIPCHK(hipMemcpyAsync(cnt, left->d_counts, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&nm, left->d_nmatch, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (cnt[0] > 0) {
+        HIPCHK(hipMemcpyAsync(uright, left->d_uright, (size_t)cnt[0] * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(depth, left->d_depth, (size_t)cnt[0] * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    return nm;
+}
+
+int orbfe_debug_copy(orbfe_extractor* h, int what, int image, int level, void* dst, int cap_bytes) {
+    if (!h || !h->cap_b || image < 0 || image >= h->last_nimg || level < 0 || level >= h->nlevels) return ORBFE_E_ARG;
+    HIPCHK(hipDeviceSynchronize());
+    const OrbGeom& g = h->g;
+    const OrbLevel& L = g.lv[level];
+    const int ncell = L.n_cols * L.n_rows;
+    const void* src = nullptr;
+    size_t bytes = 0;
+    int count = 0;
+    int info[4];
+    HIPCHK(hipMemcpy(info, h->d_lvinfo + ((size_t)image * g.nlevels + level) * 4, 16, hipMemcpyDeviceToHost));
+    if (what == 0) { src = h->d_cellcnt + (size_t)image * g.total_cells + L.cell_base; count = ncell; bytes = 4 * count; }
+    else if (what == 1) { src = h->d_cellkeys + (size_t)image * g.cellkeys_per_img + L.cellkey_off; count = ncell * L.cell_cap; bytes = 4 * (size_t)count; }
+    else if (what == 2) { src = h->d_outkeys + (size_t)image * g.out_per_img + L.out_off; count = info[0]; bytes = 4 * (size_t)count; }
+    else if (what == 3) { if (cap_bytes < 16) return ORBFE_E_CAPACITY; memcpy(dst, info, 16); return 4; }
+    else return ORBFE_E_ARG;
+    if (!dst) return count;
+    if ((size_t)cap_bytes < bytes) return ORBFE_E_CAPACITY;
+    if (bytes) HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return count;
+}
+
+int orbfe_descriptor_distance(const uint8_t* a, const uint8_t* b) {
+    int d = 0;
+    for (int i = 0; i < 8; i++) {
+        uint32_t x, y;
+        memcpy(&x, a + 4 * i, 4);
+        memcpy(&y, b + 4 * i, 4);
+        d += __builtin_popcount(x ^ y);
+    }
+    return d;
+}
+
+}  // extern "C"
