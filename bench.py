@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""bench.py — ORB front-end throughput on MI355X (BASELINE.json metric).
+
+A step = one pass of the hot path over one batch of synthetic stereo frames resident in HBM:
+ORBextractor::operator() on every left and right image (pyramid, FAST cells, octree,
+orientation, blur, rBRIEF) + Frame::ComputeStereoMatches per frame, all on the GPU (liborbfe.so).
+With N > 1 GPUs (torchrun, one process per GPU) every rank processes its own shard of frames
+(weak scaling) and the per-image feature slots are all-gathered over RCCL at the end of the step.
+
+Prints ONE JSON line (rank 0). See DESIGN.md §Measurement for the roofline bytes.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "frames/sec ORB extract+match (752×480, 1000 kp) at 1/2/4/8 GPU; % HBM roofline"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# Algorithmic bytes of the pyramid+FAST pass per 752x480 image: every level read
+# once + levels 1..7 written once.
+PYR_FAST_BYTES = {(752, 480): 1873774, (1241, 376): 2421578, (512, 512): 1361776}
+
+
+def level_sizes(w, h, nlevels=8, sf=1.2):
+    s = [np.float32(1.0)]
+    for i in range(1, nlevels):
+        s.append(np.float32(np.float64(s[-1]) * np.float64(np.float32(sf))))
+    inv = [np.float32(1.0) / v for v in s]
+    return [(int(np.rint(np.float32(w) * v)), int(np.rint(np.float32(h) * v))) for v in inv]
+
+
+def algorithmic_bytes(w, h):
+    lv = level_sizes(w, h)
+    return sum(a * b for a, b in lv) + sum(a * b for a, b in lv[1:])
+
+
+def cpu_baseline(pairs_l, pairs_r, w, h, nfeatures, bf, fx):
+    """Oracle CPU path (C++ restatement, kind='port') on a bounded sample, host cores."""
+    from oracle import oracle
+    oracle.build()
+    L = oracle.lib()
+    threads = max(1, min(16, os.cpu_count() or 1))
+    # bounded sample: ~10-30 s of CPU work (the oracle needs ~90 ms per stereo frame per core)
+    n = min(max(160, 8 * threads), 400)
+    idx = [i % len(pairs_l) for i in range(n)]
+    Ls = np.ascontiguousarray(np.stack([pairs_l[i] for i in idx]))
+    Rs = np.ascontiguousarray(np.stack([pairs_r[i] for i in idx]))
+    t0 = time.perf_counter()
+    L.oro_bench_stereo(Ls.ctypes.data, Rs.ctypes.data, n, w, h, nfeatures, 1.2, 8, 20, 7, bf, fx, threads)
+    dt = time.perf_counter() - t0
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(n / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{n} stereo frames {w}x{h} (extract L+R + ComputeStereoMatches), {threads} threads, "
+                      f"frame-parallel, oracle/orb_oracle.cpp -O3 -march=native; host CPU: {cpu}",
+            "seconds": round(dt, 3)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--frames", type=int, default=256, help="stereo frames per GPU per step")
+    ap.add_argument("--width", type=int, default=752)
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--nfeatures", type=int, default=1000)
+    ap.add_argument("--unique", type=int, default=16, help="distinct synthetic frames (tiled over the batch)")
+    ap.add_argument("--no-allgather", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--stage-steps", type=int, default=10, help="extra steps with per-stage HIP events")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from orb_slam3_ros_amd.frontend import StereoFrontEnd
+    from orb_slam3_ros_amd.synth import synth_stereo
+    from orb_slam3_ros_amd import distributed as odist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    W, H, F = args.width, args.height, args.frames
+    bf, fx = 0.110078 * 458.654, 458.654   # EuRoC stereo baseline x fx
+    U = min(args.unique, F)
+    pairs = [synth_stereo(1000 * rank + i, W, H) for i in range(U)]
+    host = np.empty((2 * F, H, W), np.uint8)
+    for f in range(F):
+        host[2 * f], host[2 * f + 1] = pairs[f % U]
+    images = torch.from_numpy(host).to(dev)
+    fe = StereoFrontEnd(F, W, H, nfeatures=args.nfeatures, bf=bf, fx=fx, device=dev)
+    gather = world > 1 and not args.no_allgather
+    if gather:
+        sb = odist.slot_bytes(fe.cap)
+        local_slots = torch.empty((2 * F, sb), dtype=torch.uint8, device=dev)
+        all_slots = torch.empty((world * 2 * F, sb), dtype=torch.uint8, device=dev)
+
+    def step():
+        fe.run(images)
+        if gather:
+            odist.pack_slots(fe.counts, fe.kps, fe.desc, local_slots)
+            odist.allgather_slots(local_slots, all_slots)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    ms_per_step = 1000.0 * elapsed / args.steps
+    value = world * F * args.steps / elapsed
+
+    # per-stage HIP-event timing on the launch stream (separate steps, same workload)
+    fe.set_stage_timing(True)
+    for _ in range(args.stage_steps):
+        fe.run(images)
+    torch.cuda.synchronize()
+    stages, nrec = fe.stage_timing()
+    fe.set_stage_timing(False)
+    counts = fe.counts.cpu().numpy()
+    nm = fe.nmatch.cpu().numpy()
+
+    if rank == 0:
+        n_img = 2 * F
+        pyr_fast_ms = stages["resize"] + stages["fast"]
+        bytes_img = algorithmic_bytes(W, H)
+        achieved = n_img * bytes_img / (pyr_fast_ms * 1e-3) / 1e9
+        dominant = max(stages, key=stages.get)
+        result = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {
+                "workload": "EuRoC-MH01-like stereo 752x480 (BASELINE config 2): ORBextractor L+R "
+                            "(nFeatures=%d, scale 1.2, 8 levels, FAST 20/7) + ComputeStereoMatches" % args.nfeatures,
+                "frames_per_gpu_per_step": F,
+                "images_per_gpu_per_step": 2 * F,
+                "width": W, "height": H,
+                "allgather": gather,
+                "parallelism": f"frame-sharded x{world}",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "pyramid+FAST pass (k_resize x7 + k_fast)",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "bytes_per_image": bytes_img,
+                "images_per_launch": n_img,
+                "kernel_ms_per_launch": round(pyr_fast_ms, 4),
+            },
+            "stage_ms": {k: round(v, 4) for k, v in stages.items()},
+            "dominant_stage": dominant,
+            "keypoints_per_image_mean": float(counts[:, 0].mean()),
+            "stereo_matches_per_frame_mean": float(nm.mean()),
+        }
+        if not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline([p[0] for p in pairs], [p[1] for p in pairs], W, H,
+                                                  args.nfeatures, bf, fx)
+        print(json.dumps(result), flush=True)
+    fe.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

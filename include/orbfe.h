@@ -78,8 +78,16 @@ int orbfe_extract_batch(orbfe_extractor* h, int nimg, const uint8_t* const* d_im
  * {n, monoIndex}. Valid until the next call on this handle. */
 int orbfe_batch_outputs(orbfe_extractor* h, orbfe_keypoint** d_kps, uint8_t** d_desc, int** d_counts, int* cap);
 
-/* Per-kernel HIP-event timing of the next orbfe_extract_batch call (for bench.py's roofline).
- * ms[0..ORBFE_NUM_STAGES) after that call: resize, blur, fast, octree, describe. */
+/* Make later orbfe_extract_batch calls write their outputs into caller-owned device buffers
+ * (kps[cap_images][cap], desc[cap_images][cap][32], counts[cap_images][2]) instead of the
+ * handle's own; cap = orbfe_extractor_capacity(). Pass NULLs to revert. */
+int orbfe_set_batch_outputs(orbfe_extractor* h, orbfe_keypoint* d_kps, uint8_t* d_desc, int* d_counts,
+                            int cap_images);
+
+/* Per-kernel HIP-event timing (for bench.py's roofline). While enabled, every batch records
+ * events around each stage on the stream it runs on (no host sync). orbfe_get_stage_timing waits
+ * for the recorded batches, writes the MEAN ms per batch of each stage to ms[0..ORBFE_NUM_STAGES)
+ * = {resize (all levels), blur, fast, octree, describe}, resets, and returns the batch count. */
 #define ORBFE_NUM_STAGES 5
 int orbfe_set_stage_timing(orbfe_extractor* h, int enable);
 int orbfe_get_stage_timing(orbfe_extractor* h, float* ms);

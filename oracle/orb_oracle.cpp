@@ -800,4 +800,36 @@ double oro_bench_extract(const uint8_t* imgs, int nimg, int w, int h, int nfeatu
     return 0.0;
 }
 
+// CPU baseline for the bench's workload (config 2): per frame extract(L) + extract(R) on two
+// threads (Frame.cc:122-125) then ComputeStereoMatches, with `nthreads` frames in flight.
+// Returns the total number of stereo matches (so the work cannot be optimised away).
+long oro_bench_stereo(const uint8_t* L, const uint8_t* R, int nframes, int w, int h, int nfeatures, float sf,
+                      int nlevels, int ini, int mn, float bf, float fx, int nthreads) {
+    std::vector<std::thread> th;
+    std::vector<long> tot(nthreads, 0);
+    for (int t = 0; t < nthreads; t++) {
+        th.emplace_back([&, t]() {
+            Extractor el(nfeatures, sf, nlevels, ini, mn), er(nfeatures, sf, nlevels, ini, mn);
+            std::vector<KeyPoint> kl, kr;
+            std::vector<uint8_t> dl, dr;
+            std::vector<float> ur, dp;
+            for (int f = t; f < nframes; f += nthreads) {
+                Image a, b;
+                a.w = b.w = w; a.h = b.h = h;
+                a.px.assign(L + (size_t)f * w * h, L + (size_t)(f + 1) * w * h);
+                b.px.assign(R + (size_t)f * w * h, R + (size_t)(f + 1) * w * h);
+                el.extract(a, 0, 0, kl, dl);
+                er.extract(b, 0, 0, kr, dr);
+                ur.resize(kl.size() + 1); dp.resize(kl.size() + 1);
+                tot[t] += oro_stereo_match(&el, &er, kl.data(), dl.data(), (int)kl.size(), kr.data(), dr.data(),
+                                           (int)kr.size(), bf, fx, ur.data(), dp.data());
+            }
+        });
+    }
+    for (auto& x : th) x.join();
+    long s = 0;
+    for (long v : tot) s += v;
+    return s;
+}
+
 }  // extern "C"

@@ -42,6 +42,7 @@ _SIGS = {
     "orbfe_extract_batch": (_c_int, [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp]),
     "orbfe_batch_outputs": (_c_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp), _P_int]),
     "orbfe_set_stage_timing": (_c_int, [_vp, _c_int]),
+    "orbfe_set_batch_outputs": (_c_int, [_vp, _vp, _vp, _vp, _c_int]),
     "orbfe_get_stage_timing": (_c_int, [_vp, _vp]),
     "orbfe_stereo_match_batch": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_float, _c_float,
                                           _vp, _vp, _vp, _vp]),

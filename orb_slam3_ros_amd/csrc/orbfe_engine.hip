@@ -98,8 +98,18 @@ struct orbfe_extractor {
     std::vector<const uint8_t*> last_ptrs;
     // stage timing
     bool timing = false;
-    hipEvent_t ev[ORBFE_NUM_STAGES + 1] = {};
+    hipEvent_t ev[ORBFE_NUM_STAGES + 1] = {};   // spare set (host API)
+    std::vector<std::vector<hipEvent_t>> ev_ring;  // one event set per timed batch, read lazily
+    int ev_used = 0;
     float stage_ms[ORBFE_NUM_STAGES] = {};
+    // optional caller-owned outputs (orbfe_set_batch_outputs)
+    OrbKeyPoint* ext_kps = nullptr;
+    uint8_t* ext_desc = nullptr;
+    int* ext_counts = nullptr;
+    int ext_cap_images = 0;
+    OrbKeyPoint* last_kps = nullptr;
+    uint8_t* last_desc = nullptr;
+    int* last_counts = nullptr;
     std::mutex mu;
 };
 
@@ -277,32 +287,45 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
     h->last_pitch = pitch;
     const uint8_t* const* P = h->d_ptrs;
     const bool tm = h->timing;
-    if (tm) HIPCHK(hipEventRecord(h->ev[0], s));
+    hipEvent_t* ev = nullptr;
+    if (tm) {
+        if (h->ev_used == (int)h->ev_ring.size()) {
+            if (h->ev_ring.size() >= 1024) return ORBFE_E_CAPACITY;
+            std::vector<hipEvent_t> set(ORBFE_NUM_STAGES + 1);
+            for (auto& e : set) HIPCHK(hipEventCreate(&e));
+            h->ev_ring.push_back(set);
+        }
+        ev = h->ev_ring[h->ev_used++].data();
+        HIPCHK(hipEventRecord(ev[0], s));
+    }
+    const bool ext = h->ext_kps && B <= h->ext_cap_images;
+    OrbKeyPoint* o_kps = ext ? h->ext_kps : h->d_kps;
+    uint8_t* o_desc = ext ? h->ext_desc : h->d_desc;
+    int* o_counts = ext ? h->ext_counts : h->d_counts;
     for (int l = 1; l < g.nlevels; l++) {
         dim3 grid(g.lv[l].resize_row_blocks, B);
         hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, s, P, pitch, h->d_pyr, g.pyr_bytes, h->d_tab, g, l);
     }
-    if (tm) HIPCHK(hipEventRecord(h->ev[1], s));
+    if (tm) HIPCHK(hipEventRecord(ev[1], s));
     BlurKernel bk;
     memcpy(bk.k, h->blur_variant == 1 ? kBlurRound : kBlurED, sizeof(bk.k));
     hipLaunchKernelGGL(k_blur, dim3(g.blur_tiles, B), dim3(256), 0, s, P, pitch, h->d_pyr, g.pyr_bytes, h->d_blur,
                        g.blur_bytes, g, bk);
-    if (tm) HIPCHK(hipEventRecord(h->ev[2], s));
+    if (tm) HIPCHK(hipEventRecord(ev[2], s));
     hipLaunchKernelGGL(k_fast, dim3((g.total_cells + 3) / 4, B), dim3(256), (size_t)4 * 2 * h->roi_max, s, P, pitch,
                        h->d_pyr, g.pyr_bytes, g, h->roi_max, h->d_cellkeys, h->d_cellcnt);
-    if (tm) HIPCHK(hipEventRecord(h->ev[3], s));
+    if (tm) HIPCHK(hipEventRecord(ev[3], s));
     hipLaunchKernelGGL(k_octree, dim3(g.nlevels, B), dim3(64), h->oct_lds, s, g, h->d_cellkeys, h->d_cellcnt,
                        h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, lap0, lap1);
-    if (tm) HIPCHK(hipEventRecord(h->ev[4], s));
+    if (tm) HIPCHK(hipEventRecord(ev[4], s));
     hipLaunchKernelGGL(k_describe, dim3((g.out_per_img + 3) / 4, B), dim3(256), 0, s, P, pitch, h->d_pyr,
-                       g.pyr_bytes, h->d_blur, g.blur_bytes, g, h->d_outkeys, h->d_lvinfo, h->d_ranks, h->d_kps,
-                       h->d_desc, h->d_counts);
-    if (tm) HIPCHK(hipEventRecord(h->ev[5], s));
+                       g.pyr_bytes, h->d_blur, g.blur_bytes, g, h->d_outkeys, h->d_lvinfo, h->d_ranks, o_kps,
+                       o_desc, o_counts);
+    if (tm) HIPCHK(hipEventRecord(ev[5], s));
     HIPCHK(hipGetLastError());
-    if (tm) {
-        HIPCHK(hipEventSynchronize(h->ev[5]));
-        for (int i = 0; i < ORBFE_NUM_STAGES; i++) HIPCHK(hipEventElapsedTime(&h->stage_ms[i], h->ev[i], h->ev[i + 1]));
-    }
+    h->last_kps = o_kps;
+    h->last_desc = o_desc;
+    h->last_counts = o_counts;
     return ORBFE_OK;
 }
 
@@ -414,9 +437,9 @@ int orbfe_extract_batch(orbfe_extractor* h, int nimg, const uint8_t* const* d_im
 
 int orbfe_batch_outputs(orbfe_extractor* h, orbfe_keypoint** d_kps, uint8_t** d_desc, int** d_counts, int* cap) {
     if (!h || !h->cap_b) return ORBFE_E_ARG;
-    if (d_kps) *d_kps = (orbfe_keypoint*)h->d_kps;
-    if (d_desc) *d_desc = h->d_desc;
-    if (d_counts) *d_counts = h->d_counts;
+    if (d_kps) *d_kps = (orbfe_keypoint*)(h->last_kps ? h->last_kps : h->d_kps);
+    if (d_desc) *d_desc = h->last_desc ? h->last_desc : h->d_desc;
+    if (d_counts) *d_counts = h->last_counts ? h->last_counts : h->d_counts;
     if (cap) *cap = h->g.kp_cap;
     return ORBFE_OK;
 }
@@ -428,7 +451,28 @@ int orbfe_set_stage_timing(orbfe_extractor* h, int enable) {
 }
 int orbfe_get_stage_timing(orbfe_extractor* h, float* ms) {
     if (!h || !ms) return ORBFE_E_ARG;
-    memcpy(ms, h->stage_ms, sizeof(h->stage_ms));
+    const int n = h->ev_used;
+    for (int i = 0; i < ORBFE_NUM_STAGES; i++) ms[i] = 0.f;
+    for (int r = 0; r < n; r++) {
+        HIPCHK(hipEventSynchronize(h->ev_ring[r][ORBFE_NUM_STAGES]));
+        for (int i = 0; i < ORBFE_NUM_STAGES; i++) {
+            float t = 0.f;
+            HIPCHK(hipEventElapsedTime(&t, h->ev_ring[r][i], h->ev_ring[r][i + 1]));
+            ms[i] += t;
+        }
+    }
+    if (n) for (int i = 0; i < ORBFE_NUM_STAGES; i++) ms[i] /= n;
+    h->ev_used = 0;
+    return n;
+}
+
+int orbfe_set_batch_outputs(orbfe_extractor* h, orbfe_keypoint* d_kps, uint8_t* d_desc, int* d_counts,
+                            int cap_images) {
+    if (!h) return ORBFE_E_ARG;
+    h->ext_kps = (OrbKeyPoint*)d_kps;
+    h->ext_desc = d_desc;
+    h->ext_counts = d_counts;
+    h->ext_cap_images = (d_kps && d_desc && d_counts) ? cap_images : 0;
     return ORBFE_OK;
 }
 
@@ -453,13 +497,13 @@ int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int width, int height,
     rc = run_batch(h, 1, ptrs, width, lap0, lap1, s);
     if (rc) return rc;
     int cnt[2];
-    HIPCHK(hipMemcpyAsync(cnt, h->d_counts, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(cnt, h->last_counts, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     *n = cnt[0];
     if (cnt[0] > cap) return ORBFE_E_CAPACITY;
     if (cnt[0] > 0) {
-        if (kps) HIPCHK(hipMemcpyAsync(kps, h->d_kps, (size_t)cnt[0] * sizeof(OrbKeyPoint), hipMemcpyDeviceToHost, s));
-        if (desc) HIPCHK(hipMemcpyAsync(desc, h->d_desc, (size_t)cnt[0] * 32, hipMemcpyDeviceToHost, s));
+        if (kps) HIPCHK(hipMemcpyAsync(kps, h->last_kps, (size_t)cnt[0] * sizeof(OrbKeyPoint), hipMemcpyDeviceToHost, s));
+        if (desc) HIPCHK(hipMemcpyAsync(desc, h->last_desc, (size_t)cnt[0] * 32, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
     }
     return cnt[1];
@@ -494,10 +538,10 @@ int orbfe_stereo_match_batch(orbfe_extractor* left, int lbase, int lstep, orbfe_
     if (lbase + (nframes - 1) * lstep >= left->last_nimg || rbase + (nframes - 1) * rstep >= right->last_nimg)
         return ORBFE_E_ARG;
     const OrbGeom& g = left->g;
-    StereoSide SL{left->d_ptrs, left->last_pitch, left->d_pyr, g.pyr_bytes, left->d_kps, left->d_desc,
-                  left->d_counts, lbase, lstep};
-    StereoSide SR{right->d_ptrs, right->last_pitch, right->d_pyr, right->g.pyr_bytes, right->d_kps, right->d_desc,
-                  right->d_counts, rbase, rstep};
+    StereoSide SL{left->d_ptrs, left->last_pitch, left->d_pyr, g.pyr_bytes, left->last_kps, left->last_desc,
+                  left->last_counts, lbase, lstep};
+    StereoSide SR{right->d_ptrs, right->last_pitch, right->d_pyr, right->g.pyr_bytes, right->last_kps,
+                  right->last_desc, right->last_counts, rbase, rstep};
     StereoArgs sa{bf, fx, g.kp_cap};
     const size_t lds = (size_t)g.kp_cap * (32 + 4 * 6);
     if (lds > 160 * 1024) return ORBFE_E_ARG;
@@ -523,7 +567,7 @@ int orbfe_stereo_match(orbfe_extractor* left, orbfe_extractor* right, float bf, 
     if (rc) return rc;
     hipStream_t s = left->own_stream;
     int cnt[2], nm = 0;
-    HIPCHK(hipMemcpyAsync(cnt, left->d_counts, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(cnt, left->last_counts, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(&nm, left->d_nmatch, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     if (cnt[0] > 0) {

@@ -1,0 +1,90 @@
+"""Batched device front-end: extract(L) + extract(R) + ComputeStereoMatches for many stereo frames
+per launch sequence (the multi-frame / multi-camera path of BASELINE config 2-4).
+
+Frame f of a batch is images (2f, 2f+1) of one interleaved [2F, H, W] u8 device tensor: this is
+the batched form of Frame::Frame(stereo) (Frame.cc:101-197), which runs ORBextractor::operator()
+on the left and right image on two threads (Frame.cc:122-125) and then ComputeStereoMatches
+(Frame.cc:141, :811-981). Outputs are device tensors in the reference's order (mvKeys,
+mDescriptors, mvuRight, mvDepth per frame, padded to `cap`).
+
+torch is used only for device memory and streams; all compute is in liborbfe.so.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .extractor import KEYPOINT_DTYPE
+
+
+class StereoFrontEnd:
+    def __init__(self, frames: int, width: int, height: int, nfeatures: int = 1000, scale_factor: float = 1.2,
+                 nlevels: int = 8, ini_th: int = 20, min_th: int = 7, bf: float = 0.110078 * 458.654,
+                 fx: float = 458.654, device=None):
+        import torch
+        self.torch = torch
+        self.lib = _lib.load()
+        self.F, self.W, self.H = int(frames), int(width), int(height)
+        self.bf, self.fx = float(bf), float(fx)
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.orbfe_extractor_create(nfeatures, scale_factor, nlevels, ini_th, min_th, ctypes.byref(h)),
+                   "create")
+        self.h = h
+        self.cap = _lib.check(self.lib.orbfe_extractor_capacity(h, self.W, self.H), "capacity")
+        n = 2 * self.F
+        t = torch
+        self.kps = t.zeros((n, self.cap, 7), dtype=t.int32, device=self.device)        # cv::KeyPoint records
+        self.desc = t.zeros((n, self.cap, 32), dtype=t.uint8, device=self.device)
+        self.counts = t.zeros((n, 2), dtype=t.int32, device=self.device)
+        self.uright = t.zeros((self.F, self.cap), dtype=t.float32, device=self.device)
+        self.depth = t.zeros((self.F, self.cap), dtype=t.float32, device=self.device)
+        self.nmatch = t.zeros((self.F,), dtype=t.int32, device=self.device)
+        _lib.check(self.lib.orbfe_set_batch_outputs(h, self.kps.data_ptr(), self.desc.data_ptr(),
+                                                    self.counts.data_ptr(), n), "set_batch_outputs")
+        self._ptrs = None
+        self._ptr_key = None
+
+    def _pointer_array(self, images):
+        key = (images.data_ptr(), tuple(images.shape), tuple(images.stride()))
+        if key != self._ptr_key:
+            base, st = images.data_ptr(), images.stride(0)
+            self._ptrs = (ctypes.c_void_p * images.shape[0])(*[base + i * st for i in range(images.shape[0])])
+            self._ptr_key = key
+        return self._ptrs
+
+    def run(self, images, stream=None):
+        """images: [2F, H, W] uint8 CUDA tensor, contiguous rows (left = even, right = odd)."""
+        assert images.dtype == self.torch.uint8 and images.dim() == 3 and images.is_cuda
+        n = images.shape[0]
+        assert n == 2 * self.F and images.shape[1] == self.H and images.shape[2] == self.W
+        assert images.stride(2) == 1 and images.stride(1) >= self.W
+        s = stream if stream is not None else self.torch.cuda.current_stream(self.device).cuda_stream
+        ptrs = self._pointer_array(images)
+        _lib.check(self.lib.orbfe_extract_batch(self.h, n, ptrs, self.W, self.H, images.stride(1), 0, 0, s),
+                   "extract_batch")
+        _lib.check(self.lib.orbfe_stereo_match_batch(self.h, 0, 2, self.h, 1, 2, self.F, self.bf, self.fx,
+                                                     self.uright.data_ptr(), self.depth.data_ptr(),
+                                                     self.nmatch.data_ptr(), s), "stereo_match_batch")
+
+    def set_stage_timing(self, on: bool):
+        self.lib.orbfe_set_stage_timing(self.h, 1 if on else 0)
+
+    def stage_timing(self):
+        ms = np.zeros(_lib.ORBFE_NUM_STAGES, np.float32)
+        n = self.lib.orbfe_get_stage_timing(self.h, ms.ctypes.data)
+        return dict(zip(_lib.STAGE_NAMES, ms.tolist())), n
+
+    def host_frame(self, f: int):
+        """(kps_left structured, desc_left, uright, depth) of frame f, copied to the host."""
+        c = self.counts[2 * f].cpu().numpy()
+        n = int(c[0])
+        kp = self.kps[2 * f, :n].cpu().numpy().view(KEYPOINT_DTYPE).reshape(n)
+        return kp, self.desc[2 * f, :n].cpu().numpy(), self.uright[f, :n].cpu().numpy(), self.depth[f, :n].cpu().numpy()
+
+    def close(self):
+        if self.h:
+            self.lib.orbfe_extractor_destroy(self.h)
+            self.h = None
