@@ -51,6 +51,7 @@ size_t octree_lds_bytes(const OrbGeom& g) {
     s += 2 * a16(16 * NC);
     s += a16(8 * NC) + a16(2 * NC) + a16(4 * NC) * 5;
     s += a16(12 * NC) + a16(8 * NC);
+    s += a16(sizeof(StSeg) * ORBFE_SORT_STACK);
     return s;
 }
 
@@ -93,6 +94,9 @@ struct orbfe_extractor {
     float* d_depth = nullptr;
     int* d_nmatch = nullptr;
     int stereo_cap_frames = 0;
+    int* d_sdist = nullptr;       // per left kp SAD distance of accepted stereo matches
+    int sdist_frames = 0;
+    std::mutex mu_stereo;
     // last batch description
     int last_nimg = 0, last_pitch = 0;
     std::vector<const uint8_t*> last_ptrs;
@@ -168,7 +172,7 @@ static int build_geom(orbfe_extractor* h, int W, int H) {
         L.cell_cap = ((L.w_cell + 1) / 2) * ((L.h_cell + 1) / 2);
         L.cellkey_off = cellkey_off;
         cellkey_off += ncell * L.cell_cap;
-        roi_max = std::max(roi_max, round_up((L.w_cell + 6) * (L.h_cell + 6), 16));
+        roi_max = std::max(roi_max, round_up((L.w_cell + 12) * (L.h_cell + 6), 16));   // RS <= cols + 6
         // octree
         L.budget = h->per_level[l];
         L.n_ini = (int)std::round((float)(maxBX - minB) / (maxBY - minB));
@@ -177,7 +181,7 @@ static int build_geom(orbfe_extractor* h, int W, int H) {
         L.out_cap = std::max(L.budget + 3, 4 * L.n_ini);
         L.out_off = out_off;
         out_off += L.out_cap;
-        node_cap = std::max(node_cap, L.out_cap + 4);
+        node_cap = std::max(node_cap, L.out_cap + 8);
         // resize tables (cv::resize INTER_LINEAR, dsize given, from level l-1)
         if (l > 0) {
             const double inv_x = (double)L.w / pw, inv_y = (double)L.h / ph;
@@ -216,10 +220,12 @@ static int build_geom(orbfe_extractor* h, int W, int H) {
                 for (; x < L.w - lanes / 2; x += lanes / 2) {}
             }
             L.simd_end = x;
-            L.resize_row_blocks = (L.h + 3) / 4;
+            // block geometry so the staged source window fits s_src[RZ_SROWS][RZ_SCOLS]
+            L.rz_rows = std::max(1, std::min(RZ_ROWS, (int)((RZ_SROWS - 3) / scale_y) + 1));
+            L.rz_cols = std::max(4, std::min(RZ_COLS, ((int)((RZ_SCOLS - 12) / scale_x)) & ~3));
         }
-        L.blur_tiles_x = (L.w + 63) / 64;
-        L.blur_tiles_y = (L.h + 15) / 16;
+        L.blur_tiles_x = (L.w + BL_TW - 1) / BL_TW;
+        L.blur_tiles_y = (L.h + BL_TH - 1) / BL_TH;
         L.blur_tile_base = tile_base;
         tile_base += L.blur_tiles_x * L.blur_tiles_y;
         pw = L.w;
@@ -303,7 +309,7 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
     uint8_t* o_desc = ext ? h->ext_desc : h->d_desc;
     int* o_counts = ext ? h->ext_counts : h->d_counts;
     for (int l = 1; l < g.nlevels; l++) {
-        dim3 grid(g.lv[l].resize_row_blocks, B);
+        dim3 grid((g.lv[l].w + g.lv[l].rz_cols - 1) / g.lv[l].rz_cols, (g.lv[l].h + g.lv[l].rz_rows - 1) / g.lv[l].rz_rows, B);
         hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, s, P, pitch, h->d_pyr, g.pyr_bytes, h->d_tab, g, l);
     }
     if (tm) HIPCHK(hipEventRecord(ev[1], s));
@@ -312,7 +318,7 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
     hipLaunchKernelGGL(k_blur, dim3(g.blur_tiles, B), dim3(256), 0, s, P, pitch, h->d_pyr, g.pyr_bytes, h->d_blur,
                        g.blur_bytes, g, bk);
     if (tm) HIPCHK(hipEventRecord(ev[2], s));
-    hipLaunchKernelGGL(k_fast, dim3((g.total_cells + 3) / 4, B), dim3(256), (size_t)4 * 2 * h->roi_max, s, P, pitch,
+    hipLaunchKernelGGL(k_fast, dim3((g.total_cells + 3) / 4, B), dim3(256), (size_t)4 * 4 * h->roi_max, s, P, pitch,
                        h->d_pyr, g.pyr_bytes, g, h->roi_max, h->d_cellkeys, h->d_cellcnt);
     if (tm) HIPCHK(hipEventRecord(ev[3], s));
     hipLaunchKernelGGL(k_octree, dim3(g.nlevels, B), dim3(64), h->oct_lds, s, g, h->d_cellkeys, h->d_cellcnt,
@@ -394,6 +400,7 @@ void orbfe_extractor_destroy(orbfe_extractor* h) {
     if (h->d_uright) (void)hipFree(h->d_uright);
     if (h->d_depth) (void)hipFree(h->d_depth);
     if (h->d_nmatch) (void)hipFree(h->d_nmatch);
+    if (h->d_sdist) (void)hipFree(h->d_sdist);
     for (int i = 0; i <= ORBFE_NUM_STAGES; i++)
         if (h->ev[i]) (void)hipEventDestroy(h->ev[i]);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
@@ -543,10 +550,19 @@ int orbfe_stereo_match_batch(orbfe_extractor* left, int lbase, int lstep, orbfe_
     StereoSide SR{right->d_ptrs, right->last_pitch, right->d_pyr, right->g.pyr_bytes, right->last_kps,
                   right->last_desc, right->last_counts, rbase, rstep};
     StereoArgs sa{bf, fx, g.kp_cap};
-    const size_t lds = (size_t)g.kp_cap * (32 + 4 * 6);
-    if (lds > 160 * 1024) return ORBFE_E_ARG;
+    const size_t lds = (size_t)g.kp_cap * (32 + sizeof(RightRec)) + 4 * 512 + 4 * 128 * 4;
+    if (lds > 160 * 1024 || g.kp_cap > ST_SORT || g.kp_cap > 65535) return ORBFE_E_ARG;
     hipStream_t s = pick_stream(left, stream);
-    hipLaunchKernelGGL(k_stereo, dim3(nframes), dim3(256), lds, s, g, SL, SR, sa, d_uright, d_depth, d_nmatch);
+    std::lock_guard<std::mutex> lk(left->mu_stereo);
+    if (left->sdist_frames < nframes) {
+        if (left->d_sdist) HIPCHK(hipFree(left->d_sdist));
+        HIPCHK(hipMalloc(&left->d_sdist, (size_t)nframes * g.kp_cap * 4));
+        left->sdist_frames = nframes;
+    }
+    hipLaunchKernelGGL(k_stereo, dim3((g.kp_cap + ST_LK - 1) / ST_LK, nframes), dim3(256), lds, s, g, SL, SR, sa,
+                       d_uright, d_depth, left->d_sdist);
+    hipLaunchKernelGGL(k_stereo_cut, dim3(nframes), dim3(256), 0, s, g, SL, sa, d_uright, d_depth, left->d_sdist,
+                       d_nmatch);
     HIPCHK(hipGetLastError());
     return ORBFE_OK;
 }

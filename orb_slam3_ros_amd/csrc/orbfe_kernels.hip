@@ -68,96 +68,211 @@ __device__ __forceinline__ const uint8_t* level_base(const uint8_t* const* imgs,
     return pyr + (size_t)b * pyr_stride + g.lv[l].pyr_off;
 }
 
-__device__ __forceinline__ uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
-
-// ---------------------------------------------------------------------------------------------
-// K1: level l from level l-1 (chained pyramid). tab: per-level int16 coefficient tables computed
-// on the host with OpenCV's exact float/double expressions. Vertical pass: columns < simd_end use
-// the universal-intrinsic rounding ((H>>4)*b>>16 summed, +2 >>2), the rest the scalar >>22 form.
-// ---------------------------------------------------------------------------------------------
-#define RESIZE_ROWS 4
-__global__ __launch_bounds__(256) void k_resize(const uint8_t* const* imgs, int in_pitch, uint8_t* pyr, int pyr_stride,
-                                                const int16_t* __restrict__ tab, OrbGeom g, int l) {
-    const OrbLevel& L = g.lv[l];
-    const int b = blockIdx.y;
-    int spitch;
-    const uint8_t* src = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l - 1, &spitch);
-    uint8_t* dst = pyr + (size_t)b * pyr_stride + L.pyr_off;
-    const int16_t* tx = tab + L.tab_x;
-    const int16_t* ty = tab + L.tab_y;
-    for (int r = 0; r < RESIZE_ROWS; r++) {
-        const int dy = blockIdx.x * RESIZE_ROWS + r;
-        if (dy >= L.h) break;
-        const int sy0 = ty[4 * dy], sy1 = ty[4 * dy + 1], b0 = ty[4 * dy + 2], b1 = ty[4 * dy + 3];
-        const uint8_t* S0 = src + (size_t)sy0 * spitch;
-        const uint8_t* S1 = src + (size_t)sy1 * spitch;
-        for (int dx = threadIdx.x; dx < L.w; dx += blockDim.x) {
-            const int sx = tx[3 * dx], a0 = tx[3 * dx + 1], a1 = tx[3 * dx + 2];
-            int h0, h1;
-            if (dx < L.xmax) {
-                h0 = S0[sx] * a0 + S0[sx + 1] * a1;
-                h1 = S1[sx] * a0 + S1[sx + 1] * a1;
-            } else {
-                h0 = S0[sx] * 2048;
-                h1 = S1[sx] * 2048;
-            }
-            int v;
-            if (dx < L.simd_end) v = ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2) >> 2;
-            else v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
-            dst[(size_t)dy * L.pitch + dx] = sat_u8(v);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// K2: 7x7 Gaussian, separable fixed point: row pass Q8 (exact), column pass Q16, (v+2^15)>>16.
-// One 64x16 output tile per block; halo 3 with reflect-101 at the level edges.
-// ---------------------------------------------------------------------------------------------
-#define BT_W 64
-#define BT_H 16
 __device__ __forceinline__ int reflect101(int p, int n) {
     if (p < 0) p = -p;
     if (p >= n) p = 2 * n - 2 - p;
     return p;
 }
+
+__device__ __forceinline__ uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+
+// ---------------------------------------------------------------------------------------------
+// K1: level l from level l-1 (chained pyramid, cv::resize INTER_LINEAR 8U fixed point).
+// tab: per-level int16 coefficient tables computed on the host with OpenCV's exact float/double
+// expressions. Vertical pass: columns < simd_end use the universal-intrinsic rounding
+// ((H>>4)*b>>16 summed, +2 >>2), the rest the scalar >>22 form.
+// One block = RZ_ROWS output rows x RZ_COLS output columns; the source rows it needs are staged
+// in LDS with dword loads; each thread produces 4 adjacent output pixels (one dword store).
+// ---------------------------------------------------------------------------------------------
+#define RZ_ROWS 8
+#define RZ_COLS 1024
+#define RZ_SROWS 14           // >= ceil(RZ_ROWS * scale_y) + 2 source rows (host clamps rz_rows)
+#define RZ_SCOLS (RZ_COLS * 3 / 2 + 16)
+__global__ __launch_bounds__(256) void k_resize(const uint8_t* const* imgs, int in_pitch, uint8_t* pyr, int pyr_stride,
+                                                const int16_t* __restrict__ tab, OrbGeom g, int l) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_src[RZ_SROWS][RZ_SCOLS];
+    __shared__ int s_ty[RZ_ROWS][4];
+    const OrbLevel& L = g.lv[l];
+    const OrbLevel& Ps = g.lv[l - 1];
+    const int b = blockIdx.z;
+    const int y0 = blockIdx.y * L.rz_rows, x0 = blockIdx.x * L.rz_cols;
+    int spitch;
+    const uint8_t* src = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l - 1, &spitch);
+    uint8_t* dst = pyr + (size_t)b * pyr_stride + L.pyr_off;
+    const int16_t* tx = tab + L.tab_x;
+    const int16_t* ty = tab + L.tab_y;
+    const int y1 = min(y0 + L.rz_rows, L.h), x1 = min(x0 + L.rz_cols, L.w);
+    const int sr0 = ty[4 * y0], sr1 = ty[4 * (y1 - 1) + 1];              // source rows [sr0, sr1]
+    const int sc0 = tx[3 * x0] & ~3;
+    const int sc1 = min((int)tx[3 * (x1 - 1)] + 2, Ps.w);                 // source cols [sc0, sc1)
+    const int nsr = sr1 - sr0 + 1, nsc4 = (sc1 - sc0 + 3) >> 2;
+    const bool aligned = ((spitch & 3) == 0) && ((((uintptr_t)src) & 3) == 0);
+    // every global load of the block is issued up front: source window, row and column coefficients
+    const int xq = x0 + 4 * threadIdx.x;     // first of this thread's 4 output columns
+    int sx[4], a0[4], a1[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int dx = min(xq + q, x1 - 1);
+        sx[q] = tx[3 * dx];
+        a0[q] = tx[3 * dx + 1];
+        a1[q] = tx[3 * dx + 2];
+    }
+    int tyv = 0;
+    if (threadIdx.x < 4 * (y1 - y0)) tyv = ty[4 * y0 + threadIdx.x];
+    uint32_t v[RZ_SROWS][2];
+#pragma unroll
+    for (int r = 0; r < RZ_SROWS; r++)
+#pragma unroll
+        for (int cc = 0; cc < 2; cc++) {
+            const int c = threadIdx.x + 256 * cc;
+            v[r][cc] = 0;
+            if (r < nsr && c < nsc4) {
+                const uint8_t* sp = src + (size_t)(sr0 + r) * spitch + sc0 + 4 * c;
+                if (aligned && sc0 + 4 * c + 4 <= spitch) {
+                    v[r][cc] = *(const uint32_t*)sp;
+                } else {
+                    for (int k = 0; k < 4; k++)
+                        if (sc0 + 4 * c + k < Ps.w) v[r][cc] |= (uint32_t)sp[k] << (8 * k);
+                }
+            }
+        }
+#pragma unroll
+    for (int r = 0; r < RZ_SROWS; r++)
+#pragma unroll
+        for (int cc = 0; cc < 2; cc++) {
+            const int c = threadIdx.x + 256 * cc;
+            if (r < nsr && c < nsc4) *(uint32_t*)&s_src[r][4 * c] = v[r][cc];
+        }
+    if (threadIdx.x < 4 * (y1 - y0)) (&s_ty[0][0])[threadIdx.x] = tyv;
+    SYNC();
+    if (xq >= x1) return;
+    bool lin[4], vec[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int dx = min(xq + q, x1 - 1);
+        sx[q] -= sc0;
+        lin[q] = dx < L.xmax;
+        vec[q] = dx < L.simd_end;
+    }
+    for (int dy = y0; dy < y1; dy++) {
+        const int r0 = s_ty[dy - y0][0] - sr0, r1 = s_ty[dy - y0][1] - sr0;
+        const int b0 = s_ty[dy - y0][2], b1 = s_ty[dy - y0][3];
+        uint32_t packed = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            int h0, h1;
+            if (lin[q]) {
+                h0 = s_src[r0][sx[q]] * a0[q] + s_src[r0][sx[q] + 1] * a1[q];
+                h1 = s_src[r1][sx[q]] * a0[q] + s_src[r1][sx[q] + 1] * a1[q];
+            } else {
+                h0 = s_src[r0][sx[q]] * 2048;
+                h1 = s_src[r1][sx[q]] * 2048;
+            }
+            int vv;
+            if (vec[q]) vv = ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2) >> 2;
+            else vv = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+            packed |= (uint32_t)sat_u8(vv) << (8 * q);
+        }
+        uint8_t* dp = dst + (size_t)dy * L.pitch + xq;
+        if (xq + 4 <= x1) {
+            *(uint32_t*)dp = packed;
+        } else {
+            for (int q = 0; q < 4 && xq + q < x1; q++) dp[q] = (uint8_t)(packed >> (8 * q));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K2: 7x7 Gaussian (symmetric kernel k0..k3..k0), separable fixed point: row pass Q8 (exact),
+// column pass Q16, (v + 2^15) >> 16, reflect-101 at the level edges. A block covers a 256 x 64
+// output tile: the (64+6) x (256+8) input window is staged in LDS with dword loads; each thread
+// owns 4 adjacent columns x 16 rows and slides a 7-row window of Q8 row sums in registers.
+// ---------------------------------------------------------------------------------------------
+#define BL_TW 256
+#define BL_TH 64
+#define BL_LW ((BL_TW + 8) / 4)     // LDS row in dwords: x from tx0-4 to tx0+TW+4
 struct BlurKernel { int k[7]; };
 __global__ __launch_bounds__(256) void k_blur(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                               int pyr_stride, uint8_t* blur, int blur_stride, OrbGeom g,
                                               BlurKernel bk) {
-    __shared__ uint8_t s_in[BT_H + 6][BT_W + 8];
-    __shared__ uint32_t s_row[BT_H + 6][BT_W];
+    __shared__ uint32_t s_in[BL_TH + 6][BL_LW];
     const int b = blockIdx.y;
     int l = 0;
     while (l + 1 < g.nlevels && (int)blockIdx.x >= g.lv[l + 1].blur_tile_base) l++;
     const OrbLevel& L = g.lv[l];
     const int t = blockIdx.x - L.blur_tile_base;
-    const int tx0 = (t % L.blur_tiles_x) * BT_W, ty0 = (t / L.blur_tiles_x) * BT_H;
+    const int tx0 = (t % L.blur_tiles_x) * BL_TW, ty0 = (t / L.blur_tiles_x) * BL_TH;
     int pitch;
     const uint8_t* src = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l, &pitch);
-    for (int i = threadIdx.x; i < (BT_H + 6) * (BT_W + 6); i += blockDim.x) {
-        const int r = i / (BT_W + 6), c = i % (BT_W + 6);
-        const int y = reflect101(ty0 + r - 3, L.h), x = reflect101(tx0 + c - 3, L.w);
-        s_in[r][c] = src[(size_t)y * pitch + x];
-    }
-    SYNC();
-    for (int i = threadIdx.x; i < (BT_H + 6) * BT_W; i += blockDim.x) {
-        const int r = i / BT_W, c = i % BT_W;
-        uint32_t s = 0;
+    const bool interior = tx0 - 4 >= 0 && tx0 + BL_TW + 4 <= L.w && (pitch & 3) == 0 && ((((uintptr_t)src) & 3) == 0);
+    constexpr int NLD = (BL_TH + 6) * BL_LW;
+    constexpr int PER = (NLD + 255) / 256;   // dwords per thread
+    uint32_t v[PER];
 #pragma unroll
-        for (int k = 0; k < 7; k++) s += (uint32_t)bk.k[k] * s_in[r][c + k];
-        s_row[r][c] = s;
+    for (int u = 0; u < PER; u++) {
+        const int i = threadIdx.x + 256 * u;
+        v[u] = 0;
+        if (i < NLD) {
+            const int r = i / BL_LW, c = i - r * BL_LW;
+            const int y = reflect101(ty0 + r - 3, L.h);
+            const uint8_t* row = src + (size_t)y * pitch;
+            const int x = tx0 - 4 + 4 * c;
+            if (interior) {
+                v[u] = *(const uint32_t*)(row + x);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int xx = x + k;
+                    const uint32_t pv = (xx >= -3 && xx < L.w + 3) ? row[reflect101(xx, L.w)] : 0u;
+                    v[u] |= pv << (8 * k);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < PER; u++) {
+        const int i = threadIdx.x + 256 * u;
+        if (i < NLD) (&s_in[0][0])[i] = v[u];
     }
     SYNC();
+    const int cg = threadIdx.x & 63, rg = threadIdx.x >> 6;
+    const uint32_t k0 = bk.k[0], k1 = bk.k[1], k2 = bk.k[2], k3 = bk.k[3];
     uint8_t* dst = blur + (size_t)b * blur_stride + L.blur_off;
-    for (int i = threadIdx.x; i < BT_H * BT_W; i += blockDim.x) {
-        const int r = i / BT_W, c = i % BT_W;
-        const int y = ty0 + r, x = tx0 + c;
-        if (y < L.h && x < L.w) {
-            uint32_t s = 0;
+    const int xo = tx0 + 4 * cg;
+    if (xo >= L.w) return;
+    uint32_t win[7][4];
 #pragma unroll
-            for (int k = 0; k < 7; k++) s += (uint32_t)bk.k[k] * s_row[r + k][c];
-            const uint32_t v = (s + 32768u) >> 16;
-            dst[(size_t)y * L.pitch + x] = (uint8_t)(v > 255 ? 255 : v);
+    for (int r = 0; r < 16 + 6; r++) {
+        const int R = rg * 16 + r;
+        const uint32_t w0 = s_in[R][cg], w1 = s_in[R][cg + 1], w2 = s_in[R][cg + 2];
+        uint32_t by[12];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            by[k] = (w0 >> (8 * k)) & 255u;
+            by[4 + k] = (w1 >> (8 * k)) & 255u;
+            by[8 + k] = (w2 >> (8 * k)) & 255u;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            win[r % 7][q] = k0 * (by[q + 1] + by[q + 7]) + k1 * (by[q + 2] + by[q + 6]) + k2 * (by[q + 3] + by[q + 5]) +
+                            k3 * by[q + 4];
+        if (r >= 6) {
+            const int y = ty0 + rg * 16 + (r - 6);
+            if (y < L.h) {
+                uint32_t packed = 0;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t s = k0 * (win[(r - 6) % 7][q] + win[r % 7][q]) +
+                                       k1 * (win[(r - 5) % 7][q] + win[(r - 1) % 7][q]) +
+                                       k2 * (win[(r - 4) % 7][q] + win[(r - 2) % 7][q]) + k3 * win[(r - 3) % 7][q];
+                    uint32_t v = (s + 32768u) >> 16;
+                    packed |= (v > 255u ? 255u : v) << (8 * q);
+                }
+                uint8_t* dp = dst + (size_t)y * L.pitch + xo;
+                if (xo + 4 <= L.w) *(uint32_t*)dp = packed;
+                else
+                    for (int q = 0; q < 4 && xo + q < L.w; q++) dp[q] = (uint8_t)(packed >> (8 * q));
+            }
         }
     }
 }
@@ -165,31 +280,38 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* const* imgs, int in
 // ---------------------------------------------------------------------------------------------
 // K3: FAST-9/16 per cell. One wave per cell (4 cells per 256-thread block). The cell ROI
 // (wCell+6)x(hCell+6) is staged in LDS; the score of every detection pixel is computed ONCE at
-// minThFAST (score = M-1 where M = max over 9-arcs of the arc-min contrast, corner iff M > th), and
-// per-cell NMS is exact because the ROI ring outside the detection rect is zero. A cell emits its
-// survivors with score >= iniThFAST, or all survivors when there are none (the reference's
-// FAST(iniTh) -> FAST(minTh) fallback, ORBextractor.cc:826-846). Keys are packed
+// minThFAST (score = M-1 where M = max over 9-arcs of the arc-min contrast, corner iff M > th),
+// and per-cell NMS is exact because the ROI ring outside the detection rect is zero. A cell
+// emits its survivors with score >= iniThFAST, or all survivors when there are none (the
+// reference's FAST(iniTh) -> FAST(minTh) fallback, ORBextractor.cc:826-846). Keys are packed
 // x_rel | y_rel<<12 | score<<24 in row-major order (FAST emission order).
+// Pass 1 runs FAST's exact necessary test (every 9-arc holds one pixel of each opposite pair
+// (k, k+8), k = 0,2,4,6) on all pixels and compacts the candidates; pass 2 scores candidates only.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ int fast_M(const uint8_t* im, int cols, int x, int y) {
-    const int v = im[y * cols + x];
-    int d[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) d[k] = v - (int)im[(y + c_ring_dy[k]) * cols + x + c_ring_dx[k]];
-    int mn2[16], mx2[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) { mn2[k] = min(d[k], d[(k + 1) & 15]); mx2[k] = max(d[k], d[(k + 1) & 15]); }
-    int mn4[16], mx4[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) { mn4[k] = min(mn2[k], mn2[(k + 2) & 15]); mx4[k] = max(mx2[k], mx2[(k + 2) & 15]); }
-    int M = -1000;
+typedef short orbfe_short2 __attribute__((ext_vector_type(2)));
+// M = max over the 16 arcs of 9 contiguous ring pixels of max(min d, min -d), d_k = v - ring_k.
+// Both signs ride in one packed int16x2 lane so every min/max is one v_pk_{min,max}_i16.
+__device__ __forceinline__ int fast_M(const uint8_t* im, int stride, int x, int y) {
+    const uint8_t* q = im + y * stride + x;
+    const int v = q[0];
+    orbfe_short2 P[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        const int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
-        const int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
-        M = max(M, max(mn9, -mx9));
+        const short d = (short)(v - (int)q[c_ring_dy[k] * stride + c_ring_dx[k]]);
+        P[k] = orbfe_short2{d, (short)-d};
     }
-    return M;
+    orbfe_short2 m2[16], m4[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(P[k], P[(k + 1) & 15]);
+#pragma unroll
+    for (int k = 0; k < 16; k++) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
+    orbfe_short2 best = orbfe_short2{(short)-1000, (short)-1000};
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const orbfe_short2 m9 = __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]), P[(k + 8) & 15]);
+        best = __builtin_elementwise_max(best, m9);
+    }
+    return max((int)best.x, (int)best.y);
 }
 
 __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
@@ -199,8 +321,9 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
     const int wave = threadIdx.x >> 6, lane = lane_id();
     const int c = blockIdx.x * 4 + wave;
     const int b = blockIdx.y;
-    uint8_t* s_img = smem_fast + wave * 2 * roi_max;
+    uint8_t* s_img = smem_fast + wave * 4 * roi_max;
     uint8_t* s_sc = s_img + roi_max;
+    uint16_t* s_cand = (uint16_t*)(s_sc + roi_max);
     const bool active = c < g.total_cells;
     int l = 0;
     if (active)
@@ -216,50 +339,106 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
     const int rows = skip ? 0 : r1 - r0, cols = skip ? 0 : c1 - c0;
     int pitch;
     const uint8_t* src = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l, &pitch);
-    for (int i = lane; i < rows * cols; i += 64) {
-        const int y = i / cols, x = i - y * cols;
-        s_img[i] = src[(size_t)(r0 + y) * pitch + c0 + x];
-        s_sc[i] = 0;
+    // LDS image rows have stride RS (dwords cover [c0 & ~3, c1)); pixel (y, x) of the ROI lives at
+    // s_img[y * RS + x] after shifting the base by (c0 & 3).
+    const int sh = c0 & 3;
+    const int RS = (cols + sh + 3) & ~3, nd = RS >> 2;
+    const bool al = (pitch & 3) == 0 && ((((uintptr_t)src) & 3) == 0);
+    {
+        const int total = rows * nd;
+        for (int base = lane; base < total; base += 64 * 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int i = base + 64 * u;
+                v[u] = 0;
+                if (i < total) {
+                    const int y = i / nd, cdw = i - y * nd;
+                    const int gx = (c0 & ~3) + 4 * cdw;
+                    const uint8_t* sp = src + (size_t)(r0 + y) * pitch + gx;
+                    if (al && gx + 4 <= L.w) v[u] = *(const uint32_t*)sp;
+                    else
+                        for (int k = 0; k < 4; k++)
+                            if (gx + k < L.w) v[u] |= (uint32_t)sp[k] << (8 * k);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int i = base + 64 * u;
+                if (i < total) ((uint32_t*)s_img)[i] = v[u];
+            }
+        }
+        for (int i = lane; i < rows * nd; i += 64) ((uint32_t*)s_sc)[i] = 0u;
     }
     SYNC();
-    const int dw = cols - 6, dh = rows - 6;
-    const int ndet = (dw > 0 && dh > 0) ? dw * dh : 0;
-    for (int p = lane; p < ndet; p += 64) {
-        const int dy = p / dw, dx = p - dy * dw;
-        const int M = fast_M(s_img, cols, dx + 3, dy + 3);
-        s_sc[(dy + 3) * cols + dx + 3] = (uint8_t)(M > g.min_th ? M - 1 : 0);
+    const uint8_t* s_px = s_img + sh;   // ROI pixel (y, x) = s_px[y * RS + x]
+    const int dw = cols - 6, dh = rows - 6;    const int ndet = (dw > 0 && dh > 0) ? dw * dh : 0;
+    const int th = g.min_th;
+    // p -> (dy, dx): floor((p + 0.5) * (1/dw)) is exact for p < 2^16 (error << 0.5/dw)
+    const float inv_dw = dw > 0 ? 1.0f / (float)dw : 0.f;
+    // pass 1: necessary test on opposite pairs, compact candidates as (dy << 8 | dx)
+    int ncand = 0;
+    for (int p0 = 0; p0 < ndet; p0 += 64) {
+        const int p = p0 + lane;
+        bool cand = false;
+        int packed = 0;
+        if (p < ndet) {
+            const int dy = (int)(((float)p + 0.5f) * inv_dw), dx = p - dy * dw;
+            packed = (dy << 8) | dx;
+            const uint8_t* q = s_px + (dy + 3) * RS + dx + 3;
+            const int v = q[0];
+            const int lo = v - th, hi = v + th;
+            auto tb = [&](int k) -> int {
+                const int x = q[c_ring_dy[k] * RS + c_ring_dx[k]];
+                return x < lo ? 1 : (x > hi ? 2 : 0);
+            };
+            const int d = (tb(0) | tb(8)) & (tb(2) | tb(10)) & (tb(4) | tb(12)) & (tb(6) | tb(14));
+            cand = d != 0;
+        }
+        const unsigned long long m = __ballot(cand);
+        if (cand) s_cand[ncand + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)packed;
+        ncand += __popcll(m);
     }
     SYNC();
-    // NMS: survivors written into s_img (the pixels are no longer needed)
+    // pass 2: exact score for candidates only
+    for (int i = lane; i < ncand; i += 64) {
+        const int p = s_cand[i];
+        const int dy = p >> 8, dx = p & 255;
+        const int M = fast_M(s_px, RS, dx + 3, dy + 3);
+        s_sc[(dy + 3) * RS + dx + 3] = (uint8_t)(M > th ? M - 1 : 0);
+    }
+    SYNC();
+    // NMS (candidates only: every other pixel has score 0); survivors marked in s_img
     int nhi = 0;
-    for (int p = lane; p < ndet; p += 64) {
-        const int dy = p / dw, dx = p - dy * dw;
-        const int y = dy + 3, x = dx + 3;
-        const uint8_t* q = s_sc + y * cols + x;
+    for (int i = lane; i < ncand; i += 64) {
+        const int p = s_cand[i];
+        const int dy = p >> 8, dx = p & 255;
+        const uint8_t* q = s_sc + (dy + 3) * RS + dx + 3;
         const int s = q[0];
-        const bool surv = s > 0 && s > q[-1] && s > q[1] && s > q[-cols - 1] && s > q[-cols] && s > q[-cols + 1] &&
-                          s > q[cols - 1] && s > q[cols] && s > q[cols + 1];
+        const bool surv = s > 0 && s > q[-1] && s > q[1] && s > q[-RS - 1] && s > q[-RS] && s > q[-RS + 1] &&
+                          s > q[RS - 1] && s > q[RS] && s > q[RS + 1];
         nhi += (surv && s >= g.ini_th) ? 1 : 0;
-        // s_img row y is read only through s_sc now; store survivor score in place
-        s_img[y * cols + x] = surv ? (uint8_t)s : 0;
+        s_cand[i] = surv ? (uint16_t)p : (uint16_t)0xFFFF;
     }
     nhi = wave_sum(nhi);
     SYNC();
+    // emission in row-major order == candidate order (candidates were compacted in pixel order)
     const int thr = nhi > 0 ? g.ini_th : 1;
     int base = 0;
     uint32_t* out = cellkeys + (size_t)b * g.cellkeys_per_img + L.cellkey_off + (size_t)local * L.cell_cap;
     const int xr0 = c0 - ORBFE_MINB + 3, yr0 = r0 - ORBFE_MINB + 3;
-    for (int dy = 0; dy < dh; dy++) {
-        for (int dx0 = 0; dx0 < dw; dx0 += 64) {
-            const int dx = dx0 + lane;
-            int s = 0;
-            if (dx < dw) s = s_img[(dy + 3) * cols + dx + 3];
-            const bool f = s >= thr && s > 0;
-            const unsigned long long m = __ballot(f);
-            const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
-            if (f) out[pos] = (uint32_t)(xr0 + dx) | ((uint32_t)(yr0 + dy) << 12) | ((uint32_t)s << 24);
-            base += __popcll(m);
+    for (int i0 = 0; i0 < ncand; i0 += 64) {
+        const int i = i0 + lane;
+        int s = 0, p = 0;
+        if (i < ncand) {
+            p = s_cand[i];
+            if (p != 0xFFFF) s = s_sc[((p >> 8) + 3) * RS + (p & 255) + 3];
         }
+        const bool f = s >= thr && s > 0;
+        const unsigned long long m = __ballot(f);
+        const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
+        if (f) out[pos] = (uint32_t)(xr0 + (p & 255)) | ((uint32_t)(yr0 + (p >> 8)) << 12) | ((uint32_t)s << 24);
+        base += __popcll(m);
     }
     if (active && lane == 0) cellcnt[(size_t)b * g.total_cells + c] = base;
 }
@@ -279,10 +458,6 @@ struct ExpLess {
         if (a.size > b.size) return false;
         return a.x0 < b.x0;
     }
-};
-struct NodeTab {
-    int16_t *x0, *x1, *y0, *y1;
-    int* size;
 };
 __device__ __forceinline__ int quadrant(uint32_t key, int x0, int x1, int y0, int y1) {
     const int halfX = (int)ceilf((float)(x1 - x0) / 2.f);
@@ -313,13 +488,15 @@ __global__ __launch_bounds__(64) void k_octree(OrbGeom g, const uint32_t* __rest
     uint8_t* p = smem_oct;
     auto carve = [&](size_t bytes) { uint8_t* r = p; p += (bytes + 15) & ~(size_t)15; return r; };
     int* cellpre = (int*)carve(sizeof(int) * (g.max_cells_level + 1));
-    NodeTab T[2];
-    for (int k = 0; k < 2; k++) {
-        T[k].x0 = (int16_t*)carve(2 * NC); T[k].x1 = (int16_t*)carve(2 * NC);
-        T[k].y0 = (int16_t*)carve(2 * NC); T[k].y1 = (int16_t*)carve(2 * NC);
-        T[k].size = (int*)carve(4 * NC);
-    }
-    int* cnt[2] = {(int*)carve(16 * NC), (int*)carve(16 * NC)};
+    // current (C*) and next (X*) node tables; swapped by pointer after each rebuild
+    int16_t *Cx0 = (int16_t*)carve(2 * NC), *Cx1 = (int16_t*)carve(2 * NC);
+    int16_t *Cy0 = (int16_t*)carve(2 * NC), *Cy1 = (int16_t*)carve(2 * NC);
+    int* Csz = (int*)carve(4 * NC);
+    int16_t *Xx0 = (int16_t*)carve(2 * NC), *Xx1 = (int16_t*)carve(2 * NC);
+    int16_t *Xy0 = (int16_t*)carve(2 * NC), *Xy1 = (int16_t*)carve(2 * NC);
+    int* Xsz = (int*)carve(4 * NC);
+    int* Ccnt = (int*)carve(16 * NC);
+    int* Xcnt = (int*)carve(16 * NC);
     int16_t* childpos = (int16_t*)carve(8 * NC);
     int16_t* newpos = (int16_t*)carve(2 * NC);
     int* divorder = (int*)carve(4 * NC);
@@ -329,6 +506,7 @@ __global__ __launch_bounds__(64) void k_octree(OrbGeom g, const uint32_t* __rest
     int* procp = (int*)carve(4 * NC);
     ExpEnt* expv = (ExpEnt*)carve(sizeof(ExpEnt) * NC);
     unsigned long long* best = (unsigned long long*)carve(8 * NC);
+    StSeg* sstack = (StSeg*)carve(sizeof(StSeg) * ORBFE_SORT_STACK);
     __shared__ int s_misc[8];
 
     // ---- gather this level's cell key lists in cell order (vToDistributeKeys order) ----
@@ -369,29 +547,28 @@ __global__ __launch_bounds__(64) void k_octree(OrbGeom g, const uint32_t* __rest
         atomicAdd(&tmpA[r], 1);
     }
     SYNC();
-    int cur = 0;
-    for (int i = lane; i < nIni; i += 64) tmpB[i] = tmpA[i] > 0 ? 1 : 0;
+        for (int i = lane; i < nIni; i += 64) tmpB[i] = tmpA[i] > 0 ? 1 : 0;
     SYNC();
     int n = wave_excl_scan_lds(tmpB, nIni);   // position of each non-empty root
     for (int i = lane; i < nIni; i += 64) {
         if (tmpA[i] > 0) {
             const int q = tmpB[i];
-            T[cur].x0[q] = (int16_t)(int)(hX * (float)i);
-            T[cur].x1[q] = (int16_t)(int)(hX * (float)(i + 1));
-            T[cur].y0[q] = 0;
-            T[cur].y1[q] = (int16_t)H;
-            T[cur].size[q] = tmpA[i];
+            Cx0[q] = (int16_t)(int)(hX * (float)i);
+            Cx1[q] = (int16_t)(int)(hX * (float)(i + 1));
+            Cy0[q] = 0;
+            Cy1[q] = (int16_t)H;
+            Csz[q] = tmpA[i];
         }
     }
-    for (int i = lane; i < 4 * NC; i += 64) cnt[cur][i] = 0;
+    for (int i = lane; i < 4 * NC; i += 64) Ccnt[i] = 0;
     SYNC();
     for (int k = lane; k < K; k += 64) {
         const uint32_t key = keys[k];
         const int r = (int)((float)(key & 0xfff) / hX);
         const int q = tmpB[r];
         nof[k] = (uint16_t)q;
-        if (T[cur].size[q] > 1)
-            atomicAdd(&cnt[cur][4 * q + quadrant(key, T[cur].x0[q], T[cur].x1[q], T[cur].y0[q], T[cur].y1[q])], 1);
+        if (Csz[q] > 1)
+            atomicAdd(&Ccnt[4 * q + quadrant(key, Cx0[q], Cx1[q], Cy0[q], Cy1[q])], 1);
     }
     SYNC();
 
@@ -407,7 +584,7 @@ __global__ __launch_bounds__(64) void k_octree(OrbGeom g, const uint32_t* __rest
         if (!phase2) {
             // every node with >1 keys divides, in list order
             for (int i = lane; i < n; i += 64) {
-                const bool dv = T[cur].size[i] > 1;
+                const bool dv = Csz[i] > 1;
                 divorder[i] = dv ? 1 : -1;
                 tmpA[i] = dv ? 1 : 0;
             }
@@ -418,12 +595,12 @@ __global__ __launch_bounds__(64) void k_octree(OrbGeom g, const uint32_t* __rest
             SYNC();
         } else {
             if (lane == 0) {
-                stl_sort(expv, m, ExpLess());
+                stl_sort_with_stack(expv, m, ExpLess(), sstack);
                 int Lsz = n, t = 0;
                 for (int j = m - 1; j >= 0; j--) {
                     const int q = expv[j].pos;
                     int c = 0;
-                    for (int k = 0; k < 4; k++) c += cnt[cur][4 * q + k] > 0;
+                    for (int k = 0; k < 4; k++) c += Ccnt[4 * q + k] > 0;
                     divorder[q] = t;
                     procp[t] = q;
                     t++;
@@ -439,39 +616,38 @@ __global__ __launch_bounds__(64) void k_octree(OrbGeom g, const uint32_t* __rest
         for (int t = lane; t < T_div; t += 64) {
             const int q = procp[t];
             int c = 0, e = 0;
-            for (int k = 0; k < 4; k++) { const int v = cnt[cur][4 * q + k]; c += v > 0; e += v > 1; }
+            for (int k = 0; k < 4; k++) { const int v = Ccnt[4 * q + k]; c += v > 0; e += v > 1; }
             tmpB[t] = c;
             tmpC[t] = e;
         }
         SYNC();
         const int Ctot = wave_excl_scan_lds(tmpB, T_div);
         const int Etot = wave_excl_scan_lds(tmpC, T_div);
-        const int nxt = cur ^ 1;
         // children: block of t starts at sum_{t'>t} c_t' = Ctot - (excl_t + c_t); order n4,n3,n2,n1
         for (int t = lane; t < T_div; t += 64) {
             const int q = procp[t];
             int c = 0;
-            for (int k = 0; k < 4; k++) c += cnt[cur][4 * q + k] > 0;
+            for (int k = 0; k < 4; k++) c += Ccnt[4 * q + k] > 0;
             const int start = Ctot - (tmpB[t] + c);
             int kk = 0;
-            const int px0 = T[cur].x0[q], px1 = T[cur].x1[q], py0 = T[cur].y0[q], py1 = T[cur].y1[q];
+            const int px0 = Cx0[q], px1 = Cx1[q], py0 = Cy0[q], py1 = Cy1[q];
             for (int ch = 3; ch >= 0; ch--) {
-                const int v = cnt[cur][4 * q + ch];
+                const int v = Ccnt[4 * q + ch];
                 if (v > 0) {
                     const int np = start + kk++;
                     childpos[4 * q + ch] = (int16_t)np;
                     int a0, a1, b0, b1;
                     child_rect(ch, px0, px1, py0, py1, &a0, &a1, &b0, &b1);
-                    T[nxt].x0[np] = (int16_t)a0; T[nxt].x1[np] = (int16_t)a1;
-                    T[nxt].y0[np] = (int16_t)b0; T[nxt].y1[np] = (int16_t)b1;
-                    T[nxt].size[np] = v;
+                    Xx0[np] = (int16_t)a0; Xx1[np] = (int16_t)a1;
+                    Xy0[np] = (int16_t)b0; Xy1[np] = (int16_t)b1;
+                    Xsz[np] = v;
                 } else {
                     childpos[4 * q + ch] = -1;
                 }
             }
             int e = tmpC[t];
             for (int ch = 0; ch < 4; ch++) {
-                const int v = cnt[cur][4 * q + ch];
+                const int v = Ccnt[4 * q + ch];
                 if (v > 1) {
                     int a0, a1, b0, b1;
                     child_rect(ch, px0, px1, py0, py1, &a0, &a1, &b0, &b1);
@@ -488,29 +664,33 @@ __global__ __launch_bounds__(64) void k_octree(OrbGeom g, const uint32_t* __rest
             if (divorder[i] < 0) {
                 const int np = Ctot + tmpA[i];
                 newpos[i] = (int16_t)np;
-                T[nxt].x0[np] = T[cur].x0[i]; T[nxt].x1[np] = T[cur].x1[i];
-                T[nxt].y0[np] = T[cur].y0[i]; T[nxt].y1[np] = T[cur].y1[i];
-                T[nxt].size[np] = T[cur].size[i];
+                Xx0[np] = Cx0[i]; Xx1[np] = Cx1[i];
+                Xy0[np] = Cy0[i]; Xy1[np] = Cy1[i];
+                Xsz[np] = Csz[i];
             }
         }
         const int newN = Ctot + nKeep;
-        for (int i = lane; i < 4 * newN; i += 64) cnt[nxt][i] = 0;
+        for (int i = lane; i < 4 * newN; i += 64) Xcnt[i] = 0;
         SYNC();
         // key sweep: move keys to their new node positions and count the next split
         for (int k = lane; k < K; k += 64) {
             const uint32_t key = keys[k];
             const int q = nof[k];
             int np;
-            if (divorder[q] >= 0) np = childpos[4 * q + quadrant(key, T[cur].x0[q], T[cur].x1[q], T[cur].y0[q], T[cur].y1[q])];
+            if (divorder[q] >= 0) np = childpos[4 * q + quadrant(key, Cx0[q], Cx1[q], Cy0[q], Cy1[q])];
             else np = newpos[q];
             nof[k] = (uint16_t)np;
-            if (T[nxt].size[np] > 1)
-                atomicAdd(&cnt[nxt][4 * np + quadrant(key, T[nxt].x0[np], T[nxt].x1[np], T[nxt].y0[np], T[nxt].y1[np])], 1);
+            if (Xsz[np] > 1)
+                atomicAdd(&Xcnt[4 * np + quadrant(key, Xx0[np], Xx1[np], Xy0[np], Xy1[np])], 1);
         }
         for (int i = lane; i < NC; i += 64) divorder[i] = -1;
         SYNC();
-        cur = nxt;
+        { int16_t* t; int* ti;
+          t = Cx0; Cx0 = Xx0; Xx0 = t; t = Cx1; Cx1 = Xx1; Xx1 = t;
+          t = Cy0; Cy0 = Xy0; Xy0 = t; t = Cy1; Cy1 = Xy1; Xy1 = t;
+          ti = Csz; Csz = Xsz; Xsz = ti; ti = Ccnt; Ccnt = Xcnt; Xcnt = ti; }
         n = newN;
+        if (n > NC - 4) { n = NC - 4; finish = true; }   // capacity guard (bound: n <= max(N+2, 4*nIni) = NC-8-1)
         m = Etot;
         if (n >= N || n == prevN) finish = true;
         else if (!phase2 && n + 3 * m > N) phase2 = true;
@@ -695,142 +875,185 @@ __device__ __forceinline__ int hamming32(const uint32_t* a, const uint32_t* b) {
     for (int i = 0; i < 8; i++) d += __popc(a[i] ^ b[i]);
     return d;
 }
+// Stage 1: one wave per left keypoint (4 per block), ST_LK left keypoints per block; the right
+// keypoints (x, row band, octave) and descriptors of the frame are staged in LDS once per block.
+// Writes per left kp: uRight, depth (-1 = none) and the SAD distance of an accepted match (-1).
+#define ST_LK 64
+struct RightRec { float x; int minr, maxr, oct; };
 __global__ __launch_bounds__(256) void k_stereo(OrbGeom g, StereoSide SL, StereoSide SR, StereoArgs sa,
-                                                float* uright, float* depth, int* nmatch) {
+                                                float* uright, float* depth, int* sdist) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_st[];
-    const int f = blockIdx.x;
+    const int f = blockIdx.y;
     const int bL = SL.base + f * SL.step, bR = SR.base + f * SR.step;
     const int wave = threadIdx.x >> 6, lane = lane_id();
     const int N = SL.counts[2 * bL], Nr = SR.counts[2 * bR];
-    uint32_t* s_descR = (uint32_t*)smem_st;                               // Nr * 8 words
-    float* s_xR = (float*)(s_descR + 8 * sa.max_kp);
-    int* s_oct = (int*)(s_xR + sa.max_kp);
-    int* s_minr = s_oct + sa.max_kp;
-    int* s_maxr = s_minr + sa.max_kp;
-    int* s_list = s_maxr + sa.max_kp;                                     // accepted (dist) per left kp
-    int* s_idx = s_list + sa.max_kp;
-    __shared__ int s_nacc;
+    const int i0 = blockIdx.x * ST_LK;
+    if (i0 >= N) return;
+    uint32_t* s_descR = (uint32_t*)smem_st;                        // sa.max_kp * 8 words
+    RightRec* s_rec = (RightRec*)(s_descR + 8 * sa.max_kp);        // sa.max_kp records
+    uint8_t* s_win = (uint8_t*)(s_rec + sa.max_kp) + wave * 512;   // per wave: IL 11x11 @0, IR 11x21 @128
+    int* s_part = (int*)((uint8_t*)(s_rec + sa.max_kp) + 4 * 512) + wave * 128;
     const OrbKeyPoint* kR = SR.kps + (size_t)bR * g.kp_cap;
     const OrbKeyPoint* kL = SL.kps + (size_t)bL * g.kp_cap;
-    const uint32_t* dR = (const uint32_t*)(SR.desc + (size_t)bR * g.kp_cap * 32);
+    const uint4* dR = (const uint4*)(SR.desc + (size_t)bR * g.kp_cap * 32);
     const uint32_t* dL = (const uint32_t*)(SL.desc + (size_t)bL * g.kp_cap * 32);
-    for (int i = threadIdx.x; i < Nr * 8; i += blockDim.x) s_descR[i] = dR[i];
+    for (int i = threadIdx.x; i < Nr * 2; i += blockDim.x) ((uint4*)s_descR)[i] = dR[i];
     for (int i = threadIdx.x; i < Nr; i += blockDim.x) {
         const OrbKeyPoint kp = kR[i];
         const float r = 2.0f * g.lv[kp.octave].scale;
-        s_xR[i] = kp.x;
-        s_oct[i] = kp.octave;
-        s_maxr[i] = (int)ceilf(kp.y + r);
-        s_minr[i] = (int)floorf(kp.y - r);
+        RightRec rr;
+        rr.x = kp.x;
+        rr.oct = kp.octave;
+        rr.maxr = (int)ceilf(kp.y + r);
+        rr.minr = (int)floorf(kp.y - r);
+        s_rec[i] = rr;
     }
-    if (threadIdx.x == 0) s_nacc = 0;
+    SYNC();
     float* uR_out = uright + (size_t)f * g.kp_cap;
     float* dp_out = depth + (size_t)f * g.kp_cap;
-    for (int i = threadIdx.x; i < N; i += blockDim.x) { uR_out[i] = -1.0f; dp_out[i] = -1.0f; }
-    SYNC();
-    const float mb = sa.bf / sa.fx;
+    int* sd_out = sdist + (size_t)f * g.kp_cap;
+    const float mb = sa.bf / sa.fx;   // intended mb = mbf/fx (the reference reads it uninitialised)
     const float minZ = mb, minD = 0.f, maxD = sa.bf / minZ;
-    for (int iL = wave; iL < N; iL += 4) {
+    const int iend = min(N, i0 + ST_LK);
+    for (int iL = i0 + wave; iL < iend; iL += 4) {
+        float outU = -1.0f, outD = -1.0f;
+        int outS = -1;
         const OrbKeyPoint kpL = kL[iL];
         const int levelL = kpL.octave;
         const float vL = kpL.y, uL = kpL.x;
         const int row = (int)vL;
         const float minU = uL - maxD, maxU = uL - minD;
-        if (maxU < 0) continue;
         uint32_t dl[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) dl[k] = dL[(size_t)iL * 8 + k];
-        int bestKey = 0x7fffffff;   // (dist << 16) | iR, min
+        int bestKey = 0x7fffffff;   // (dist << 16) | iR: the first best in iR order
         bool anyCand = false;
         for (int iR = lane; iR < Nr; iR += 64) {
-            if (s_minr[iR] <= row && row <= s_maxr[iR]) {
+            const RightRec rr = s_rec[iR];
+            if (rr.minr <= row && row <= rr.maxr) {
                 anyCand = true;
-                const int o = s_oct[iR];
-                if (o < levelL - 1 || o > levelL + 1) continue;
-                const float uR = s_xR[iR];
-                if (uR >= minU && uR <= maxU) {
+                if (rr.oct >= levelL - 1 && rr.oct <= levelL + 1 && rr.x >= minU && rr.x <= maxU) {
                     const int dist = hamming32(dl, s_descR + 8 * iR);
-                    const int kk = (dist << 16) | iR;
-                    bestKey = min(bestKey, kk);
+                    bestKey = min(bestKey, (dist << 16) | iR);
                 }
             }
         }
-        if (!__any(anyCand)) continue;   // vCandidates.empty()
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) bestKey = min(bestKey, __shfl_xor(bestKey, d, 64));
+        const bool cand = __any(anyCand) && !(maxU < 0);
         const int bestDist = bestKey == 0x7fffffff ? 100 : min(100, bestKey >> 16);
-        if (!(bestDist < 75)) continue;   // thOrbDist = (TH_HIGH+TH_LOW)/2
-        const int bestIdxR = bestKey & 0xffff;
-        const float uR0 = s_xR[bestIdxR];
-        const float sf = g.lv[levelL].inv_scale;
-        const float scaleduL = roundf(kpL.x * sf);
-        const float scaledvL = roundf(kpL.y * sf);
-        const float scaleduR0 = roundf(uR0 * sf);
-        const int w = 5, Lr = 5;
-        const float iniu = scaleduR0 + Lr - w;
-        const float endu = scaleduR0 + Lr + w + 1;
-        const OrbLevel& LV = g.lv[levelL];
-        if (iniu < 0 || endu >= LV.w) continue;
-        int pL, pR;
-        const uint8_t* IL = level_base(SL.imgs, SL.in_pitch, SL.pyr, SL.pyr_stride, g, bL, levelL, &pL);
-        const uint8_t* IR = level_base(SR.imgs, SR.in_pitch, SR.pyr, SR.pyr_stride, g, bR, levelL, &pR);
-        const int r0 = (int)(scaledvL - w), c0L = (int)(scaleduL - w);
-        // lanes: pixel (yy, xx) of the 11x11 window, 121 = 64 + 57
-        float dists[11];
-        int bestD = 0x7fffffff, bestinc = 0;
-        for (int inc = -Lr; inc <= Lr; inc++) {
-            const int c0R = (int)(scaleduR0 + inc - w);
-            int s = 0;
-            for (int pix = lane; pix < 121; pix += 64) {
-                const int yy = pix / 11, xx = pix - yy * 11;
-                s += abs((int)IL[(size_t)(r0 + yy) * pL + c0L + xx] - (int)IR[(size_t)(r0 + yy) * pR + c0R + xx]);
+        if (cand && bestDist < 75) {   // thOrbDist = (TH_HIGH + TH_LOW) / 2
+            const int bestIdxR = bestKey & 0xffff;
+            const float uR0 = s_rec[bestIdxR].x;
+            const float sf = g.lv[levelL].inv_scale;
+            const float scaleduL = roundf(kpL.x * sf);
+            const float scaledvL = roundf(kpL.y * sf);
+            const float scaleduR0 = roundf(uR0 * sf);
+            const int w = 5, Lr = 5;
+            const float iniu = scaleduR0 + Lr - w;
+            const float endu = scaleduR0 + Lr + w + 1;
+            const OrbLevel& LV = g.lv[levelL];
+            if (!(iniu < 0 || endu >= LV.w)) {
+                int pL, pR;
+                const uint8_t* IL = level_base(SL.imgs, SL.in_pitch, SL.pyr, SL.pyr_stride, g, bL, levelL, &pL);
+                const uint8_t* IR = level_base(SR.imgs, SR.in_pitch, SR.pyr, SR.pyr_stride, g, bR, levelL, &pR);
+                const int r0 = (int)(scaledvL - w), c0L = (int)(scaleduL - w), c0R = (int)(scaleduR0 - Lr - w);
+                // stage IL 11x11 and IR 11x21 windows
+                for (int i = lane; i < 121 + 231; i += 64) {
+                    if (i < 121) {
+                        const int yy = i / 11, xx = i - yy * 11;
+                        s_win[i] = IL[(size_t)(r0 + yy) * pL + c0L + xx];
+                    } else {
+                        const int j = i - 121, yy = j / 21, xx = j - yy * 21;
+                        s_win[128 + j] = IR[(size_t)(r0 + yy) * pR + c0R + xx];
+                    }
+                }
+                // lanes: (shift inc, window row) pairs -> row SAD over 11 columns
+                for (int pidx = lane; pidx < 121; pidx += 64) {
+                    const int inc = pidx / 11, yy = pidx - inc * 11;
+                    int sad = 0;
+#pragma unroll
+                    for (int xx = 0; xx < 11; xx++)
+                        sad += abs((int)s_win[yy * 11 + xx] - (int)s_win[128 + yy * 21 + inc + xx]);
+                    s_part[pidx] = sad;
+                }
+                int dsum = 0;
+                if (lane < 11)
+                    for (int yy = 0; yy < 11; yy++) dsum += s_part[lane * 11 + yy];
+                float dists[11];
+                int bestD = 0x7fffffff, bestinc = 0;
+#pragma unroll
+                for (int k = 0; k < 11; k++) {
+                    const float dist = (float)__shfl(dsum, k, 64);   // cv::norm(NORM_L1) of shift k - Lr
+                    dists[k] = dist;
+                    if (dist < (float)bestD) { bestD = (int)dist; bestinc = k - Lr; }
+                }
+                if (!(bestinc == -Lr || bestinc == Lr)) {
+                    const float dist1 = dists[Lr + bestinc - 1], dist2 = dists[Lr + bestinc], dist3 = dists[Lr + bestinc + 1];
+                    const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+                    if (!(deltaR < -1 || deltaR > 1)) {
+                        float bestuR = LV.scale * ((float)scaleduR0 + (float)bestinc + deltaR);
+                        float disparity = (uL - bestuR);
+                        if (disparity >= minD && disparity < maxD) {
+                            if (disparity <= 0) { disparity = (float)0.01; bestuR = (float)((double)uL - 0.01); }
+                            outD = sa.bf / disparity;
+                            outU = bestuR;
+                            outS = bestD;
+                        }
+                    }
+                }
             }
-            s = wave_sum(s);
-            const float dist = (float)s;
-            if (dist < (float)bestD) { bestD = (int)dist; bestinc = inc; }
-            dists[Lr + inc] = dist;
         }
-        if (bestinc == -Lr || bestinc == Lr) continue;
-        const float dist1 = dists[Lr + bestinc - 1], dist2 = dists[Lr + bestinc], dist3 = dists[Lr + bestinc + 1];
-        const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
-        if (deltaR < -1 || deltaR > 1) continue;
-        float bestuR = g.lv[levelL].scale * ((float)scaleduR0 + (float)bestinc + deltaR);
-        float disparity = (uL - bestuR);
-        if (disparity >= minD && disparity < maxD) {
-            if (disparity <= 0) { disparity = (float)0.01; bestuR = (float)((double)uL - 0.01); }
-            if (lane == 0) {
-                dp_out[iL] = sa.bf / disparity;
-                uR_out[iL] = bestuR;
-                const int slot = atomicAdd(&s_nacc, 1);
-                s_list[slot] = bestD;
-                s_idx[slot] = iL;
-            }
-        }
+        if (lane == 0) { uR_out[iL] = outU; dp_out[iL] = outD; sd_out[iL] = outS; }
+    }
+}
+
+// Stage 2 (one block per frame): the median outlier cut of ComputeStereoMatches (Frame.cc:966-980):
+// sort the accepted (dist, iL) pairs, median = the (n/2)-th dist, drop every match with
+// dist >= 1.5f*1.4f*median. Bitonic sort of the accepted distances in LDS.
+#define ST_SORT 2048
+__global__ __launch_bounds__(256) void k_stereo_cut(OrbGeom g, StereoSide SL, StereoArgs sa, float* uright,
+                                                    float* depth, const int* sdist, int* nmatch) {
+    __shared__ int s_v[ST_SORT];
+    __shared__ int s_n;
+    const int f = blockIdx.x;
+    const int bL = SL.base + f * SL.step;
+    const int N = SL.counts[2 * bL];
+    const int* sd = sdist + (size_t)f * g.kp_cap;
+    if (threadIdx.x == 0) s_n = 0;
+    SYNC();
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+        const int d = sd[i];
+        if (d >= 0) s_v[atomicAdd(&s_n, 1)] = d;
     }
     SYNC();
-    const int nacc = s_nacc;
-    if (nacc == 0) { if (threadIdx.x == 0) nmatch[f] = 0; return; }
-    // median of the (dist, iL)-sorted list = the (nacc/2)-th smallest dist: rank selection
-    __shared__ int s_med;
-    for (int i = threadIdx.x; i < nacc; i += blockDim.x) {
-        const int di = s_list[i], ii = s_idx[i];
-        int rank = 0;
-        for (int j = 0; j < nacc; j++) {
-            const int dj = s_list[j];
-            rank += (dj < di) || (dj == di && s_idx[j] < ii);
-        }
-        if (rank == nacc / 2) s_med = di;
-    }
+    const int n = s_n;
+    int P = 1;
+    while (P < n) P <<= 1;
+    for (int i = n + threadIdx.x; i < P; i += blockDim.x) s_v[i] = 0x7fffffff;
     SYNC();
-    const float median = (float)s_med;
+    for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < P; i += blockDim.x) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const int a = s_v[i], c = s_v[ixj];
+                    const bool up = (i & k) == 0;
+                    if ((a > c) == up) { s_v[i] = c; s_v[ixj] = a; }
+                }
+            }
+            SYNC();
+        }
+    if (threadIdx.x == 0) nmatch[f] = n;
+    if (n == 0) return;   // the reference indexes vDistIdx[size/2] unguarded here
+    const float median = (float)s_v[n / 2];
     const float thDist = 1.5f * 1.4f * median;
-    int kept = 0;
-    for (int i = threadIdx.x; i < nacc; i += blockDim.x) {
-        if (!((float)s_list[i] < thDist)) { uR_out[s_idx[i]] = -1; dp_out[s_idx[i]] = -1; }
-        else kept++;
+    float* uR = uright + (size_t)f * g.kp_cap;
+    float* dp = depth + (size_t)f * g.kp_cap;
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+        const int d = sd[i];
+        if (d >= 0 && !((float)d < thDist)) { uR[i] = -1; dp[i] = -1; }
     }
-    (void)kept;
-    if (threadIdx.x == 0) nmatch[f] = nacc;
 }
 
 }  // namespace orbfe

@@ -34,7 +34,7 @@ struct OrbLevel {
     int simd_end;             // first column handled by the scalar vertical tail
     // blur tiling
     int blur_tiles_x, blur_tiles_y, blur_tile_base;
-    int resize_row_blocks;
+    int rz_rows, rz_cols;     // output rows / cols per k_resize block (fit the LDS source window)
 };
 
 struct OrbGeom {

@@ -122,13 +122,16 @@ ORBFE_HD void st_insertion_sort(T* first, T* last, Cmp comp) {
 
 ORBFE_HD int st_lg(int n) { int r = 0; while (n >>= 1) r++; return r; }
 
+struct StSeg { int lo, hi, depth; };
+#define ORBFE_SORT_STACK 64
+
+// `stack` must hold ORBFE_SORT_STACK entries (the device passes an LDS buffer).
 template <typename T, typename Cmp>
-ORBFE_HD void stl_sort(T* first, int n, Cmp comp) {
+ORBFE_HD void stl_sort_with_stack(T* first, int n, Cmp comp, StSeg* stack) {
     if (n <= 1) return;
     const int kThreshold = 16;
     // __introsort_loop(first, last, 2*lg(n)): iterate on the left part, "recurse" on the right part.
-    struct Seg { int lo, hi, depth; };
-    Seg stack[64];
+    typedef StSeg Seg;
     int sp = 0;
     stack[sp++] = Seg{0, n, 2 * st_lg(n)};
     while (sp > 0) {
@@ -156,6 +159,12 @@ ORBFE_HD void stl_sort(T* first, int n, Cmp comp) {
     } else {
         st_insertion_sort(first, first + n, comp);
     }
+}
+
+template <typename T, typename Cmp>
+ORBFE_HD void stl_sort(T* first, int n, Cmp comp) {
+    StSeg stack[ORBFE_SORT_STACK];
+    stl_sort_with_stack(first, n, comp, stack);
 }
 
 }  // namespace orbfe
