@@ -81,6 +81,7 @@ def main():
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--nfeatures", type=int, default=1000)
     ap.add_argument("--unique", type=int, default=16, help="distinct synthetic frames (tiled over the batch)")
+    ap.add_argument("--pipelines", type=int, default=1, help="sub-batches on separate HIP streams")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stage-steps", type=int, default=10, help="extra steps with per-stage HIP events")
@@ -109,7 +110,7 @@ def main():
     for f in range(F):
         host[2 * f], host[2 * f + 1] = pairs[f % U]
     images = torch.from_numpy(host).to(dev)
-    fe = StereoFrontEnd(F, W, H, nfeatures=args.nfeatures, bf=bf, fx=fx, device=dev)
+    fe = StereoFrontEnd(F, W, H, nfeatures=args.nfeatures, bf=bf, fx=fx, device=dev, pipelines=args.pipelines)
     gather = world > 1 and not args.no_allgather
     if gather:
         sb = odist.slot_bytes(fe.cap)
@@ -142,13 +143,17 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
     value = world * F * args.steps / elapsed
 
-    # per-stage HIP-event timing on the launch stream (separate steps, same workload)
-    fe.set_stage_timing(True)
+    # per-stage HIP-event timing on the launch stream (separate steps, same workload, one pipeline
+    # so the events bracket kernels that run alone on the GPU)
+    fe_t = fe if args.pipelines == 1 else StereoFrontEnd(F, W, H, nfeatures=args.nfeatures, bf=bf, fx=fx, device=dev)
+    fe_t.set_stage_timing(True)
     for _ in range(args.stage_steps):
-        fe.run(images)
+        fe_t.run(images)
     torch.cuda.synchronize()
-    stages, nrec = fe.stage_timing()
-    fe.set_stage_timing(False)
+    stages, nrec = fe_t.stage_timing()
+    fe_t.set_stage_timing(False)
+    if fe_t is not fe:
+        fe_t.close()
     counts = fe.counts.cpu().numpy()
     nm = fe.nmatch.cpu().numpy()
 
@@ -178,6 +183,7 @@ def main():
                 "images_per_gpu_per_step": 2 * F,
                 "width": W, "height": H,
                 "allgather": gather,
+                "pipelines": args.pipelines,
                 "parallelism": f"frame-sharded x{world}",
             },
             "roofline": {

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -115,6 +116,7 @@ struct orbfe_extractor {
     uint8_t* last_desc = nullptr;
     int* last_counts = nullptr;
     std::mutex mu;
+    int ablate_fast = 0;   // ORBFE_ABLATE_FAST: timing-only builds of k_fast (outputs invalid when != 0)
 };
 
 static void free_buffers(orbfe_extractor* h) {
@@ -263,7 +265,6 @@ static int ensure(orbfe_extractor* h, int W, int H, int B) {
     HIPCHK(hipMalloc(&h->d_tab, std::max<size_t>(2, h->tab.size() * 2)));
     HIPCHK(hipMemcpy(h->d_tab, h->tab.data(), h->tab.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(hipMalloc(&h->d_pyr, (size_t)B * g.pyr_bytes));
-    HIPCHK(hipMalloc(&h->d_blur, (size_t)B * g.blur_bytes));
     HIPCHK(hipMalloc(&h->d_cellkeys, (size_t)B * g.cellkeys_per_img * 4));
     HIPCHK(hipMalloc(&h->d_cellcnt, (size_t)B * g.total_cells * 4));
     HIPCHK(hipMalloc(&h->d_lkeys, (size_t)B * g.cellkeys_per_img * 4));
@@ -315,18 +316,15 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
     if (tm) HIPCHK(hipEventRecord(ev[1], s));
     BlurKernel bk;
     memcpy(bk.k, h->blur_variant == 1 ? kBlurRound : kBlurED, sizeof(bk.k));
-    hipLaunchKernelGGL(k_blur, dim3(g.blur_tiles, B), dim3(256), 0, s, P, pitch, h->d_pyr, g.pyr_bytes, h->d_blur,
-                       g.blur_bytes, g, bk);
-    if (tm) HIPCHK(hipEventRecord(ev[2], s));
+    if (tm) HIPCHK(hipEventRecord(ev[2], s));   // the blur is fused into k_describe (stage kept for the layout)
     hipLaunchKernelGGL(k_fast, dim3((g.total_cells + 3) / 4, B), dim3(256), (size_t)4 * 4 * h->roi_max, s, P, pitch,
-                       h->d_pyr, g.pyr_bytes, g, h->roi_max, h->d_cellkeys, h->d_cellcnt);
+                       h->d_pyr, g.pyr_bytes, g, h->roi_max, h->d_cellkeys, h->d_cellcnt, h->ablate_fast);
     if (tm) HIPCHK(hipEventRecord(ev[3], s));
     hipLaunchKernelGGL(k_octree, dim3(g.nlevels, B), dim3(64), h->oct_lds, s, g, h->d_cellkeys, h->d_cellcnt,
                        h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, lap0, lap1);
     if (tm) HIPCHK(hipEventRecord(ev[4], s));
     hipLaunchKernelGGL(k_describe, dim3((g.out_per_img + 3) / 4, B), dim3(256), 0, s, P, pitch, h->d_pyr,
-                       g.pyr_bytes, h->d_blur, g.blur_bytes, g, h->d_outkeys, h->d_lvinfo, h->d_ranks, o_kps,
-                       o_desc, o_counts);
+                       g.pyr_bytes, g, h->d_outkeys, h->d_lvinfo, h->d_ranks, o_kps, o_desc, o_counts, bk);
     if (tm) HIPCHK(hipEventRecord(ev[5], s));
     HIPCHK(hipGetLastError());
     h->last_kps = o_kps;
@@ -354,6 +352,7 @@ int orbfe_extractor_create(int nfeatures, float scaleFactor, int nlevels, int in
     h->min_th = minThFAST;
     h->scale_factor_f = scaleFactor;
     h->scale_factor = scaleFactor;   // double member initialised from the float argument (ORBextractor.h:96)
+    if (const char* ab = getenv("ORBFE_ABLATE_FAST")) h->ablate_fast = atoi(ab);
     // ORBextractor.cc:414-445
     h->scale.resize(nlevels);
     h->sigma2.resize(nlevels);

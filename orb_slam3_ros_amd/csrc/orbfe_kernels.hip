@@ -22,6 +22,16 @@
 namespace orbfe {
 
 #define SYNC() __syncthreads()
+// Intra-wave LDS hand-off (producer and consumer lanes belong to one wave; other waves of the
+// block may already have exited, so no workgroup barrier): order the LDS accesses for the
+// compiler and wait for this wave's outstanding LDS operations.
+#define WAVE_SYNC()                                               \
+    do {                                                          \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");    \
+        __builtin_amdgcn_s_waitcnt(0xc07f);                       \
+        __builtin_amdgcn_wave_barrier();                          \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");    \
+    } while (0)
 
 __constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
 __constant__ signed char c_pattern[ORBFE_PATTERN_PAIRS * 4] = ORBFE_BRIEF_PATTERN_INIT;
@@ -61,11 +71,19 @@ __device__ int wave_excl_scan_lds(int* arr, int n) {
     return carry;
 }
 
-__device__ __forceinline__ const uint8_t* level_base(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
-                                                     int pyr_stride, const OrbGeom& g, int b, int l, int* pitch) {
-    if (l == 0) { *pitch = in_pitch; return imgs[b]; }
+// Image pointers come from a pointer table, so the compiler cannot prove they are global memory
+// and would emit flat_* loads (which also count against lgkmcnt and serialise with LDS traffic).
+// Every image access goes through an explicit address_space(1) pointer instead.
+#define ORBFE_GLOBAL __attribute__((address_space(1)))
+typedef const ORBFE_GLOBAL uint8_t* gptr_u8;
+typedef const ORBFE_GLOBAL uint32_t* gptr_u32;
+__device__ __forceinline__ gptr_u8 as_global(const uint8_t* p) { return (gptr_u8)p; }
+
+__device__ __forceinline__ gptr_u8 level_base(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
+                                              int pyr_stride, const OrbGeom& g, int b, int l, int* pitch) {
+    if (l == 0) { *pitch = in_pitch; return as_global(imgs[b]); }
     *pitch = g.lv[l].pitch;
-    return pyr + (size_t)b * pyr_stride + g.lv[l].pyr_off;
+    return as_global(pyr + (size_t)b * pyr_stride + g.lv[l].pyr_off);
 }
 
 __device__ __forceinline__ int reflect101(int p, int n) {
@@ -97,7 +115,7 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t* const* imgs, int 
     const int b = blockIdx.z;
     const int y0 = blockIdx.y * L.rz_rows, x0 = blockIdx.x * L.rz_cols;
     int spitch;
-    const uint8_t* src = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l - 1, &spitch);
+    gptr_u8 src = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l - 1, &spitch);
     uint8_t* dst = pyr + (size_t)b * pyr_stride + L.pyr_off;
     const int16_t* tx = tab + L.tab_x;
     const int16_t* ty = tab + L.tab_y;
@@ -120,22 +138,26 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t* const* imgs, int 
     int tyv = 0;
     if (threadIdx.x < 4 * (y1 - y0)) tyv = ty[4 * y0 + threadIdx.x];
     uint32_t v[RZ_SROWS][2];
+    if (aligned) {
+        // clamped addresses: every load is issued unconditionally, out-of-window lanes are dropped at the store
 #pragma unroll
-    for (int r = 0; r < RZ_SROWS; r++)
+        for (int r = 0; r < RZ_SROWS; r++)
 #pragma unroll
-        for (int cc = 0; cc < 2; cc++) {
-            const int c = threadIdx.x + 256 * cc;
-            v[r][cc] = 0;
-            if (r < nsr && c < nsc4) {
-                const uint8_t* sp = src + (size_t)(sr0 + r) * spitch + sc0 + 4 * c;
-                if (aligned && sc0 + 4 * c + 4 <= spitch) {
-                    v[r][cc] = *(const uint32_t*)sp;
-                } else {
-                    for (int k = 0; k < 4; k++)
-                        if (sc0 + 4 * c + k < Ps.w) v[r][cc] |= (uint32_t)sp[k] << (8 * k);
-                }
+            for (int cc = 0; cc < 2; cc++) {
+                const int rr = min(r, nsr - 1), c = min((int)threadIdx.x + 256 * cc, nsc4 - 1);
+                v[r][cc] = *(gptr_u32)(src + (size_t)(sr0 + rr) * spitch + sc0 + 4 * c);
             }
-        }
+    } else {
+        for (int r = 0; r < RZ_SROWS; r++)
+            for (int cc = 0; cc < 2; cc++) {
+                const int rr = min(r, nsr - 1), c = min((int)threadIdx.x + 256 * cc, nsc4 - 1);
+                gptr_u8 sp = src + (size_t)(sr0 + rr) * spitch + sc0 + 4 * c;
+                uint32_t x = 0;
+                for (int k = 0; k < 4; k++)
+                    if (sc0 + 4 * c + k < Ps.w) x |= (uint32_t)sp[k] << (8 * k);
+                v[r][cc] = x;
+            }
+    }
 #pragma unroll
     for (int r = 0; r < RZ_SROWS; r++)
 #pragma unroll
@@ -203,30 +225,33 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* const* imgs, int in
     const int t = blockIdx.x - L.blur_tile_base;
     const int tx0 = (t % L.blur_tiles_x) * BL_TW, ty0 = (t / L.blur_tiles_x) * BL_TH;
     int pitch;
-    const uint8_t* src = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l, &pitch);
+    gptr_u8 src = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l, &pitch);
     const bool interior = tx0 - 4 >= 0 && tx0 + BL_TW + 4 <= L.w && (pitch & 3) == 0 && ((((uintptr_t)src) & 3) == 0);
     constexpr int NLD = (BL_TH + 6) * BL_LW;
     constexpr int PER = (NLD + 255) / 256;   // dwords per thread
     uint32_t v[PER];
+    if (interior) {
 #pragma unroll
-    for (int u = 0; u < PER; u++) {
-        const int i = threadIdx.x + 256 * u;
-        v[u] = 0;
-        if (i < NLD) {
+        for (int u = 0; u < PER; u++) {
+            const int i = min((int)threadIdx.x + 256 * u, NLD - 1);
             const int r = i / BL_LW, c = i - r * BL_LW;
             const int y = reflect101(ty0 + r - 3, L.h);
-            const uint8_t* row = src + (size_t)y * pitch;
+            v[u] = *(gptr_u32)(src + (size_t)y * pitch + tx0 - 4 + 4 * c);
+        }
+    } else {
+        for (int u = 0; u < PER; u++) {
+            const int i = min((int)threadIdx.x + 256 * u, NLD - 1);
+            const int r = i / BL_LW, c = i - r * BL_LW;
+            const int y = reflect101(ty0 + r - 3, L.h);
+            gptr_u8 row = src + (size_t)y * pitch;
             const int x = tx0 - 4 + 4 * c;
-            if (interior) {
-                v[u] = *(const uint32_t*)(row + x);
-            } else {
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const int xx = x + k;
-                    const uint32_t pv = (xx >= -3 && xx < L.w + 3) ? row[reflect101(xx, L.w)] : 0u;
-                    v[u] |= pv << (8 * k);
-                }
+            uint32_t a = 0;
+            for (int k = 0; k < 4; k++) {
+                const int xx = x + k;
+                const uint32_t pv = (xx >= -3 && xx < L.w + 3) ? row[reflect101(xx, L.w)] : 0u;
+                a |= pv << (8 * k);
             }
+            v[u] = a;
         }
     }
 #pragma unroll
@@ -316,7 +341,7 @@ __device__ __forceinline__ int fast_M(const uint8_t* im, int stride, int x, int 
 
 __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                               int pyr_stride, OrbGeom g, int roi_max, uint32_t* cellkeys,
-                                              int* cellcnt) {
+                                              int* cellcnt, int ablate) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_fast[];
     const int wave = threadIdx.x >> 6, lane = lane_id();
     const int c = blockIdx.x * 4 + wave;
@@ -338,7 +363,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
     const bool skip = !active || (r0 >= maxBY - 3) || (c0 >= maxBX - 6);
     const int rows = skip ? 0 : r1 - r0, cols = skip ? 0 : c1 - c0;
     int pitch;
-    const uint8_t* src = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l, &pitch);
+    gptr_u8 src = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l, &pitch);
     // LDS image rows have stride RS (dwords cover [c0 & ~3, c1)); pixel (y, x) of the ROI lives at
     // s_img[y * RS + x] after shifting the base by (c0 & 3).
     const int sh = c0 & 3;
@@ -348,18 +373,23 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
         const int total = rows * nd;
         for (int base = lane; base < total; base += 64 * 8) {
             uint32_t v[8];
+            if (al) {
 #pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int i = base + 64 * u;
-                v[u] = 0;
-                if (i < total) {
+                for (int u = 0; u < 8; u++) {
+                    const int i = min(base + 64 * u, total - 1);
+                    const int y = i / nd, cdw = i - y * nd;
+                    v[u] = *(gptr_u32)(src + (size_t)(r0 + y) * pitch + (c0 & ~3) + 4 * cdw);
+                }
+            } else {
+                for (int u = 0; u < 8; u++) {
+                    const int i = min(base + 64 * u, total - 1);
                     const int y = i / nd, cdw = i - y * nd;
                     const int gx = (c0 & ~3) + 4 * cdw;
-                    const uint8_t* sp = src + (size_t)(r0 + y) * pitch + gx;
-                    if (al && gx + 4 <= L.w) v[u] = *(const uint32_t*)sp;
-                    else
-                        for (int k = 0; k < 4; k++)
-                            if (gx + k < L.w) v[u] |= (uint32_t)sp[k] << (8 * k);
+                    gptr_u8 sp = src + (size_t)(r0 + y) * pitch + gx;
+                    uint32_t a = 0;
+                    for (int k = 0; k < 4; k++)
+                        if (gx + k < L.w) a |= (uint32_t)sp[k] << (8 * k);
+                    v[u] = a;
                 }
             }
 #pragma unroll
@@ -376,6 +406,8 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
     const int th = g.min_th;
     // p -> (dy, dx): floor((p + 0.5) * (1/dw)) is exact for p < 2^16 (error << 0.5/dw)
     const float inv_dw = dw > 0 ? 1.0f / (float)dw : 0.f;
+    // timing-only ablation: stop after a phase, keep its results live, publish an empty cell
+    if (ablate == 1) { asm volatile("" ::"v"((int)s_px[lane])); if (active && lane == 0) cellcnt[(size_t)b * g.total_cells + c] = 0; return; }
     // pass 1: necessary test on opposite pairs, compact candidates as (dy << 8 | dx)
     int ncand = 0;
     for (int p0 = 0; p0 < ndet; p0 += 64) {
@@ -400,6 +432,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
         ncand += __popcll(m);
     }
     SYNC();
+    if (ablate == 2) { asm volatile("" ::"v"(ncand)); if (active && lane == 0) cellcnt[(size_t)b * g.total_cells + c] = 0; return; }
     // pass 2: exact score for candidates only
     for (int i = lane; i < ncand; i += 64) {
         const int p = s_cand[i];
@@ -408,6 +441,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
         s_sc[(dy + 3) * RS + dx + 3] = (uint8_t)(M > th ? M - 1 : 0);
     }
     SYNC();
+    if (ablate == 3) { asm volatile("" ::"v"((int)s_sc[lane])); if (active && lane == 0) cellcnt[(size_t)b * g.total_cells + c] = 0; return; }
     // NMS (candidates only: every other pixel has score 0); survivors marked in s_img
     int nhi = 0;
     for (int i = lane; i < ncand; i += 64) {
@@ -754,11 +788,24 @@ __device__ __forceinline__ float fast_atan2_dev(float y, float x) {
     return a;
 }
 
+// Fused per-keypoint pipeline, one wave per keypoint: the 43x43 patch of the UNBLURRED level
+// around the keypoint (reflect-101 outside the level) is staged in LDS once; IC_Angle reads it
+// directly; the 7x7 Gaussian of the level is evaluated on the 37x37 window the descriptor can
+// sample (|offset| <= 18) with the exact separable fixed-point arithmetic of k_blur's reference
+// semantics (GaussianBlur of the whole level, ORBextractor.cc:1132-1133, restricted to the pixels
+// the descriptor reads); rBRIEF samples that window. No blurred level ever touches HBM.
+#define DP_R 21                      // patch radius: 18 (pattern) + 3 (blur)
+#define DP_N (2 * DP_R + 1)          // 43
+#define DP_RAW_S 48                  // raw row stride (bytes)
+#define DP_Q_S 40                    // Q8 row-pass stride (u16 elements)
+#define DP_B_S 40                    // blurred row stride (bytes)
+#define DP_B 37                      // blurred window (2*18+1)
+#define DP_WAVE_LDS 7056   // >= 43*48 + 43*40*2 + 37*40, multiple of 16
 __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
-                                                  int pyr_stride, const uint8_t* blur, int blur_stride, OrbGeom g,
-                                                  const uint32_t* __restrict__ outkeys, const int* __restrict__ lvinfo,
-                                                  const int* __restrict__ ranks, OrbKeyPoint* kps, uint8_t* desc,
-                                                  int* counts) {
+                                                  int pyr_stride, OrbGeom g, const uint32_t* __restrict__ outkeys,
+                                                  const int* __restrict__ lvinfo, const int* __restrict__ ranks,
+                                                  OrbKeyPoint* kps, uint8_t* desc, int* counts, BlurKernel bk) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_dp[4][DP_WAVE_LDS];
     const int wave = threadIdx.x >> 6, lane = lane_id();
     const int b = blockIdx.y;
     const int flat = blockIdx.x * 4 + wave;   // index over all levels' output slots
@@ -778,50 +825,111 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
     if (i >= inf[4 * l]) return;
     const uint32_t key = outkeys[(size_t)b * g.out_per_img + flat];
     const int x = key & 0xfff, y = (key >> 12) & 0xfff;
-    // IC_Angle on the unblurred level
+    uint8_t* raw = s_dp[wave];
+    uint16_t* rowq = (uint16_t*)(raw + DP_N * DP_RAW_S);
+    uint8_t* blr = raw + DP_N * DP_RAW_S + DP_N * DP_Q_S * 2;
     int pitch;
-    const uint8_t* im = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l, &pitch);
-    const uint8_t* center = im + (size_t)y * pitch + x;
+    gptr_u8 im = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l, &pitch);
+    // ---- stage the raw patch: raw[r][c] = level(y - 21 + r, x - 21 + c), reflect-101 outside ----
+    const int px0 = x - DP_R, py0 = y - DP_R;
+    const int gx0 = px0 & ~3, sh = px0 - gx0;
+    const bool interior = px0 >= 0 && py0 >= 0 && py0 + DP_N <= L.h && gx0 + DP_RAW_S + 4 <= L.w &&
+                          (pitch & 3) == 0 && ((((uintptr_t)im) & 3) == 0);
+    if (interior) {
+        constexpr int ND = DP_N * (DP_RAW_S / 4);   // 516 dwords
+        uint32_t lo[9], hi[9];
+#pragma unroll
+        for (int u = 0; u < 9; u++) {
+            const int it = min(lane + 64 * u, ND - 1);
+            const int r = it / (DP_RAW_S / 4), k = it - r * (DP_RAW_S / 4);
+            gptr_u32 rp = (gptr_u32)(im + (size_t)(py0 + r) * pitch + gx0) + k;
+            lo[u] = rp[0];
+            hi[u] = rp[1];
+        }
+#pragma unroll
+        for (int u = 0; u < 9; u++) {
+            const int it = lane + 64 * u;
+            if (it < ND) ((uint32_t*)raw)[it] = __builtin_amdgcn_alignbyte(hi[u], lo[u], (unsigned)sh);
+        }
+    } else {
+        for (int it = lane; it < DP_N * DP_N; it += 64) {
+            const int r = it / DP_N, c = it - r * DP_N;
+            raw[r * DP_RAW_S + c] = im[(size_t)reflect101(py0 + r, L.h) * pitch + reflect101(px0 + c, L.w)];
+        }
+    }
+    WAVE_SYNC();
+    // ---- IC_Angle on the unblurred patch, centre (21, 21) ----
+    const uint8_t* center = raw + DP_R * DP_RAW_S + DP_R;
     const int u = (lane & 31) - 15;
-    const bool ucol = (lane & 31) < 31;
     int m10 = 0, m01 = 0;
-    if (ucol) {
-        if (lane < 32) {
-            m10 += u * (int)center[u];
-            for (int v = 1; v <= 8; v++) {
-                if (u >= -c_umax[v] && u <= c_umax[v]) {
-                    const int vp = center[u + v * pitch], vm = center[u - v * pitch];
-                    m10 += u * (vp + vm);
-                    m01 += v * (vp - vm);
-                }
-            }
-        } else {
-            for (int v = 9; v <= 15; v++) {
-                if (u >= -c_umax[v] && u <= c_umax[v]) {
-                    const int vp = center[u + v * pitch], vm = center[u - v * pitch];
-                    m10 += u * (vp + vm);
-                    m01 += v * (vp - vm);
-                }
+    if ((lane & 31) < 31) {
+        const int v0 = lane < 32 ? 1 : 9, v1 = lane < 32 ? 8 : 15;
+        if (lane < 32) m10 += u * (int)center[u];
+        for (int v = v0; v <= v1; v++) {
+            if (u >= -c_umax[v] && u <= c_umax[v]) {
+                const int vp = center[u + v * DP_RAW_S], vm = center[u - v * DP_RAW_S];
+                m10 += u * (vp + vm);
+                m01 += v * (vp - vm);
             }
         }
     }
     m10 = wave_sum(m10);
     m01 = wave_sum(m01);
     const float angle = fast_atan2_dev((float)m01, (float)m10);
-    // rBRIEF on the blurred level
+    // ---- 7x7 Gaussian on the 37x37 window: row pass (Q8, exact) then column pass ----
+    const uint32_t k0 = bk.k[0], k1 = bk.k[1], k2 = bk.k[2], k3 = bk.k[3];
+    for (int it = lane; it < DP_N * 10; it += 64) {   // 43 rows x 10 groups of 4 output columns
+        const int r = it / 10, gq = it - r * 10;
+        const uint32_t* rp = (const uint32_t*)(raw + r * DP_RAW_S) + gq;
+        const uint32_t w0 = rp[0], w1 = rp[1], w2 = rp[2];
+        uint32_t by[12];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            by[k] = (w0 >> (8 * k)) & 255u;
+            by[4 + k] = (w1 >> (8 * k)) & 255u;
+            by[8 + k] = (w2 >> (8 * k)) & 255u;
+        }
+        uint32_t h[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            h[q] = k0 * (by[q] + by[q + 6]) + k1 * (by[q + 1] + by[q + 5]) + k2 * (by[q + 2] + by[q + 4]) + k3 * by[q + 3];
+        uint2 pk;
+        pk.x = h[0] | (h[1] << 16);
+        pk.y = h[2] | (h[3] << 16);
+        *(uint2*)(rowq + r * DP_Q_S + 4 * gq) = pk;
+    }
+    WAVE_SYNC();
+    for (int it = lane; it < DP_B * 10; it += 64) {   // 37 rows x 10 groups of 4 columns
+        const int r = it / 10, gq = it - r * 10;
+        uint32_t a[7][4];
+#pragma unroll
+        for (int j = 0; j < 7; j++) {
+            const uint2 pk = *(const uint2*)(rowq + (r + j) * DP_Q_S + 4 * gq);
+            a[j][0] = pk.x & 0xffffu; a[j][1] = pk.x >> 16; a[j][2] = pk.y & 0xffffu; a[j][3] = pk.y >> 16;
+        }
+        uint32_t packed = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t sum = k0 * (a[0][q] + a[6][q]) + k1 * (a[1][q] + a[5][q]) + k2 * (a[2][q] + a[4][q]) + k3 * a[3][q];
+            const uint32_t v = (sum + 32768u) >> 16;
+            packed |= (v > 255u ? 255u : v) << (8 * q);
+        }
+        *(uint32_t*)(blr + r * DP_B_S + 4 * gq) = packed;
+    }
+    WAVE_SYNC();
+    // ---- rBRIEF on the blurred window, centre (18, 18) ----
     const float factorPI = (float)(M_PI / 180.f);
     const float ang = angle * factorPI;
     const float a = glibc_cosf(ang), bs = glibc_sinf(ang);
-    const uint8_t* bl = blur + (size_t)b * blur_stride + L.blur_off;
-    const uint8_t* bc = bl + (size_t)y * L.pitch + x;
+    const uint8_t* bc = blr + 18 * DP_B_S + 18;
     unsigned long long masks[4];
 #pragma unroll
     for (int mm = 0; mm < 4; mm++) {
         const int pr = 64 * mm + lane;
-        const float px0 = (float)c_pattern[4 * pr], py0 = (float)c_pattern[4 * pr + 1];
-        const float px1 = (float)c_pattern[4 * pr + 2], py1 = (float)c_pattern[4 * pr + 3];
-        const int t0 = bc[(int)rintf(px0 * bs + py0 * a) * L.pitch + (int)rintf(px0 * a - py0 * bs)];
-        const int t1 = bc[(int)rintf(px1 * bs + py1 * a) * L.pitch + (int)rintf(px1 * a - py1 * bs)];
+        const float px0f = (float)c_pattern[4 * pr], py0f = (float)c_pattern[4 * pr + 1];
+        const float px1f = (float)c_pattern[4 * pr + 2], py1f = (float)c_pattern[4 * pr + 3];
+        const int t0 = bc[(int)rintf(px0f * bs + py0f * a) * DP_B_S + (int)rintf(px0f * a - py0f * bs)];
+        const int t1 = bc[(int)rintf(px1f * bs + py1f * a) * DP_B_S + (int)rintf(px1f * a - py1f * bs)];
         masks[mm] = __ballot(t0 < t1);
     }
     const int rk = ranks[(size_t)b * g.out_per_img + flat];
@@ -955,8 +1063,8 @@ __global__ __launch_bounds__(256) void k_stereo(OrbGeom g, StereoSide SL, Stereo
             const OrbLevel& LV = g.lv[levelL];
             if (!(iniu < 0 || endu >= LV.w)) {
                 int pL, pR;
-                const uint8_t* IL = level_base(SL.imgs, SL.in_pitch, SL.pyr, SL.pyr_stride, g, bL, levelL, &pL);
-                const uint8_t* IR = level_base(SR.imgs, SR.in_pitch, SR.pyr, SR.pyr_stride, g, bR, levelL, &pR);
+                gptr_u8 IL = level_base(SL.imgs, SL.in_pitch, SL.pyr, SL.pyr_stride, g, bL, levelL, &pL);
+                gptr_u8 IR = level_base(SR.imgs, SR.in_pitch, SR.pyr, SR.pyr_stride, g, bR, levelL, &pR);
                 const int r0 = (int)(scaledvL - w), c0L = (int)(scaleduL - w), c0R = (int)(scaleduR0 - Lr - w);
                 // stage IL 11x11 and IR 11x21 windows
                 for (int i = lane; i < 121 + 231; i += 64) {

@@ -20,20 +20,33 @@ from .extractor import KEYPOINT_DTYPE
 
 
 class StereoFrontEnd:
+    """`pipelines` > 1 splits the frames into that many sub-batches, each with its own engine handle
+    and HIP stream, so the kernels of different sub-batches overlap on the GPU (the latency-bound
+    octree / stereo stages of one sub-batch run beside the streaming stages of another)."""
+
     def __init__(self, frames: int, width: int, height: int, nfeatures: int = 1000, scale_factor: float = 1.2,
                  nlevels: int = 8, ini_th: int = 20, min_th: int = 7, bf: float = 0.110078 * 458.654,
-                 fx: float = 458.654, device=None):
+                 fx: float = 458.654, device=None, pipelines: int = 1):
         import torch
         self.torch = torch
         self.lib = _lib.load()
         self.F, self.W, self.H = int(frames), int(width), int(height)
         self.bf, self.fx = float(bf), float(fx)
         self.device = device or torch.device("cuda", torch.cuda.current_device())
-        h = ctypes.c_void_p()
-        _lib.check(self.lib.orbfe_extractor_create(nfeatures, scale_factor, nlevels, ini_th, min_th, ctypes.byref(h)),
-                   "create")
-        self.h = h
-        self.cap = _lib.check(self.lib.orbfe_extractor_capacity(h, self.W, self.H), "capacity")
+        P = max(1, min(int(pipelines), self.F))
+        bounds = [self.F * i // P for i in range(P + 1)]
+        self.parts = [(bounds[i], bounds[i + 1]) for i in range(P) if bounds[i + 1] > bounds[i]]
+        self.handles, self.streams = [], []
+        for _ in self.parts:
+            h = ctypes.c_void_p()
+            _lib.check(self.lib.orbfe_extractor_create(nfeatures, scale_factor, nlevels, ini_th, min_th,
+                                                       ctypes.byref(h)), "create")
+            self.handles.append(h)
+            self.streams.append(torch.cuda.Stream(self.device) if len(self.parts) > 1 else None)
+        self.h = self.handles[0]
+        self.cap = _lib.check(self.lib.orbfe_extractor_capacity(self.h, self.W, self.H), "capacity")
+        for h in self.handles[1:]:
+            self.lib.orbfe_extractor_capacity(h, self.W, self.H)
         n = 2 * self.F
         t = torch
         self.kps = t.zeros((n, self.cap, 7), dtype=t.int32, device=self.device)        # cv::KeyPoint records
@@ -42,39 +55,61 @@ class StereoFrontEnd:
         self.uright = t.zeros((self.F, self.cap), dtype=t.float32, device=self.device)
         self.depth = t.zeros((self.F, self.cap), dtype=t.float32, device=self.device)
         self.nmatch = t.zeros((self.F,), dtype=t.int32, device=self.device)
-        _lib.check(self.lib.orbfe_set_batch_outputs(h, self.kps.data_ptr(), self.desc.data_ptr(),
-                                                    self.counts.data_ptr(), n), "set_batch_outputs")
+        for h, (a, b) in zip(self.handles, self.parts):
+            _lib.check(self.lib.orbfe_set_batch_outputs(h, self.kps[2 * a].data_ptr(), self.desc[2 * a].data_ptr(),
+                                                        self.counts[2 * a].data_ptr(), 2 * (b - a)),
+                       "set_batch_outputs")
         self._ptrs = None
         self._ptr_key = None
 
-    def _pointer_array(self, images):
+    def _pointer_arrays(self, images):
         key = (images.data_ptr(), tuple(images.shape), tuple(images.stride()))
         if key != self._ptr_key:
             base, st = images.data_ptr(), images.stride(0)
-            self._ptrs = (ctypes.c_void_p * images.shape[0])(*[base + i * st for i in range(images.shape[0])])
+            self._ptrs = [(ctypes.c_void_p * (2 * (b - a)))(*[base + i * st for i in range(2 * a, 2 * b)])
+                          for a, b in self.parts]
             self._ptr_key = key
         return self._ptrs
 
     def run(self, images, stream=None):
         """images: [2F, H, W] uint8 CUDA tensor, contiguous rows (left = even, right = odd)."""
-        assert images.dtype == self.torch.uint8 and images.dim() == 3 and images.is_cuda
+        torch = self.torch
+        assert images.dtype == torch.uint8 and images.dim() == 3 and images.is_cuda
         n = images.shape[0]
         assert n == 2 * self.F and images.shape[1] == self.H and images.shape[2] == self.W
         assert images.stride(2) == 1 and images.stride(1) >= self.W
-        s = stream if stream is not None else self.torch.cuda.current_stream(self.device).cuda_stream
-        ptrs = self._pointer_array(images)
-        _lib.check(self.lib.orbfe_extract_batch(self.h, n, ptrs, self.W, self.H, images.stride(1), 0, 0, s),
-                   "extract_batch")
-        _lib.check(self.lib.orbfe_stereo_match_batch(self.h, 0, 2, self.h, 1, 2, self.F, self.bf, self.fx,
-                                                     self.uright.data_ptr(), self.depth.data_ptr(),
-                                                     self.nmatch.data_ptr(), s), "stereo_match_batch")
+        main = torch.cuda.current_stream(self.device)
+        s_main = stream if stream is not None else main.cuda_stream
+        ptrs = self._pointer_arrays(images)
+        multi = len(self.parts) > 1
+        if multi:
+            ev0 = torch.cuda.Event()
+            ev0.record(main)
+        for h, st, p, (a, b) in zip(self.handles, self.streams, ptrs, self.parts):
+            if multi:
+                st.wait_event(ev0)
+                s = st.cuda_stream
+            else:
+                s = s_main
+            _lib.check(self.lib.orbfe_extract_batch(h, 2 * (b - a), p, self.W, self.H, images.stride(1), 0, 0, s),
+                       "extract_batch")
+            _lib.check(self.lib.orbfe_stereo_match_batch(h, 0, 2, h, 1, 2, b - a, self.bf, self.fx,
+                                                         self.uright[a].data_ptr(), self.depth[a].data_ptr(),
+                                                         self.nmatch[a:].data_ptr(), s), "stereo_match_batch")
+        if multi:
+            for st in self.streams:
+                main.wait_stream(st)
 
     def set_stage_timing(self, on: bool):
-        self.lib.orbfe_set_stage_timing(self.h, 1 if on else 0)
+        for h in self.handles:
+            self.lib.orbfe_set_stage_timing(h, 1 if on else 0)
 
     def stage_timing(self):
+        """Mean per-batch stage times of the first pipeline (its own stream)."""
         ms = np.zeros(_lib.ORBFE_NUM_STAGES, np.float32)
-        n = self.lib.orbfe_get_stage_timing(self.h, ms.ctypes.data)
+        n = self.lib.orbfe_get_stage_timing(self.handles[0], ms.ctypes.data)
+        for h in self.handles[1:]:
+            self.lib.orbfe_get_stage_timing(h, np.zeros(_lib.ORBFE_NUM_STAGES, np.float32).ctypes.data)
         return dict(zip(_lib.STAGE_NAMES, ms.tolist())), n
 
     def host_frame(self, f: int):
@@ -85,6 +120,8 @@ class StereoFrontEnd:
         return kp, self.desc[2 * f, :n].cpu().numpy(), self.uright[f, :n].cpu().numpy(), self.depth[f, :n].cpu().numpy()
 
     def close(self):
-        if self.h:
-            self.lib.orbfe_extractor_destroy(self.h)
-            self.h = None
+        for h in self.handles:
+            if h:
+                self.lib.orbfe_extractor_destroy(h)
+        self.handles = []
+        self.h = None
