@@ -119,8 +119,14 @@ int orbfe_descriptor_distance(const uint8_t* a, const uint8_t* b);
  * batch to host memory. what: 0 = per-cell FAST key counts (int32[n_cells]),
  * 1 = per-cell FAST key slots (uint32[n_cells * cell_cap], x_rel | y_rel << 12 | score << 24),
  * 2 = DistributeOctTree output (uint32[n], x | y << 12 | score << 24) followed by nothing,
- * 3 = per-level info int32[4] {n, n_lap, n_mono, n_raw}. Returns the element count. */
+ * 3 = per-level info int32[4] {n, n_lap, n_mono, n_raw},
+ * 4 = octree phase timestamps uint64[64] of image 0 (only with ORBFE_OCT_STAMPS set at create).
+ * Returns the element count. */
 int orbfe_debug_copy(orbfe_extractor* h, int what, int image, int level, void* dst, int cap_bytes);
+
+/* Test hook: sort n <= 4096 u64 values by their high 32 bits with the device's block-parallel
+ * replica of libstdc++ std::sort (used by DistributeOctTree); result must equal std::sort. */
+int orbfe_debug_block_sort(uint64_t* data, int n);
 
 /* Library identification (build string). */
 const char* orbfe_version(void);

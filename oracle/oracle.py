@@ -52,6 +52,7 @@ def lib() -> ctypes.CDLL:
         L.oro_stereo_match.argtypes = [vp, vp, vp, vp, ci, vp, vp, ci, cf, cf, vp, vp]
         L.oro_bench_extract.restype = ctypes.c_double
         L.oro_bench_extract.argtypes = [vp, ci, ci, ci, ci, cf, ci, ci, ci, ci, ctypes.POINTER(ci)]
+        L.oro_std_sort_u64_hi.argtypes = [vp, ci]
         L.oro_bench_stereo.restype = ctypes.c_long
         L.oro_bench_stereo.argtypes = [vp, vp, ci, ci, ci, ci, cf, ci, ci, ci, cf, cf, ci]
         _lib = L

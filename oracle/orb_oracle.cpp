@@ -800,6 +800,12 @@ double oro_bench_extract(const uint8_t* imgs, int nimg, int w, int h, int nfeatu
     return 0.0;
 }
 
+// std::sort of u64 values by their high 32 bits (the shape of DistributeOctTree's
+// compareNodes sort, ORBextractor.cc:700) — checker for the device block-parallel replica.
+void oro_std_sort_u64_hi(uint64_t* a, int n) {
+    std::sort(a, a + n, [](uint64_t x, uint64_t y) { return (x >> 32) < (y >> 32); });
+}
+
 // CPU baseline for the bench's workload (config 2): per frame extract(L) + extract(R) on two
 // threads (Frame.cc:122-125) then ComputeStereoMatches, with `nthreads` frames in flight.
 // Returns the total number of stereo matches (so the work cannot be optimised away).

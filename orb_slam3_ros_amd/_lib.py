@@ -49,6 +49,7 @@ _SIGS = {
     "orbfe_stereo_match": (_c_int, [_vp, _vp, _c_float, _c_float, _vp, _vp]),
     "orbfe_descriptor_distance": (_c_int, [_vp, _vp]),
     "orbfe_debug_copy": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _c_int]),
+    "orbfe_debug_block_sort": (_c_int, [_vp, _c_int]),
     "orbfe_version": (ctypes.c_char_p, []),
 }
 

@@ -51,8 +51,8 @@ size_t octree_lds_bytes(const OrbGeom& g) {
     s += 2 * (4 * a16(2 * NC) + a16(4 * NC));
     s += 2 * a16(16 * NC);
     s += a16(8 * NC) + a16(2 * NC) + a16(4 * NC) * 5;
-    s += a16(12 * NC) + a16(8 * NC);
-    s += a16(sizeof(StSeg) * ORBFE_SORT_STACK);
+    s += a16(8 * NC) + a16(8 * NC);
+    s += a16(4 * NC) + a16(16 * ORBFE_SORT_STACK);
     return s;
 }
 
@@ -117,6 +117,7 @@ struct orbfe_extractor {
     int* last_counts = nullptr;
     std::mutex mu;
     int ablate_fast = 0;   // ORBFE_ABLATE_FAST: timing-only builds of k_fast (outputs invalid when != 0)
+    unsigned long long* d_oct_ts = nullptr;   // ORBFE_OCT_STAMPS: per-phase s_memtime of the octree (image 0)
 };
 
 static void free_buffers(orbfe_extractor* h) {
@@ -320,8 +321,8 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
     hipLaunchKernelGGL(k_fast, dim3((g.total_cells + 3) / 4, B), dim3(256), (size_t)4 * 4 * h->roi_max, s, P, pitch,
                        h->d_pyr, g.pyr_bytes, g, h->roi_max, h->d_cellkeys, h->d_cellcnt, h->ablate_fast);
     if (tm) HIPCHK(hipEventRecord(ev[3], s));
-    hipLaunchKernelGGL(k_octree, dim3(g.nlevels, B), dim3(64), h->oct_lds, s, g, h->d_cellkeys, h->d_cellcnt,
-                       h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, lap0, lap1);
+    hipLaunchKernelGGL(k_octree, dim3(B, g.nlevels), dim3(OCT_NT), h->oct_lds, s, g, h->d_cellkeys, h->d_cellcnt,
+                       h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, lap0, lap1, h->d_oct_ts);
     if (tm) HIPCHK(hipEventRecord(ev[4], s));
     hipLaunchKernelGGL(k_describe, dim3((g.out_per_img + 3) / 4, B), dim3(256), 0, s, P, pitch, h->d_pyr,
                        g.pyr_bytes, g, h->d_outkeys, h->d_lvinfo, h->d_ranks, o_kps, o_desc, o_counts, bk);
@@ -353,6 +354,10 @@ int orbfe_extractor_create(int nfeatures, float scaleFactor, int nlevels, int in
     h->scale_factor_f = scaleFactor;
     h->scale_factor = scaleFactor;   // double member initialised from the float argument (ORBextractor.h:96)
     if (const char* ab = getenv("ORBFE_ABLATE_FAST")) h->ablate_fast = atoi(ab);
+    if (getenv("ORBFE_OCT_STAMPS")) {
+        if (hipMalloc(&h->d_oct_ts, 64 * 8 * ORBFE_MAX_LEVELS) != hipSuccess) { delete h; return ORBFE_E_DEVICE; }
+        (void)hipMemset(h->d_oct_ts, 0, 64 * 8 * ORBFE_MAX_LEVELS);
+    }
     // ORBextractor.cc:414-445
     h->scale.resize(nlevels);
     h->sigma2.resize(nlevels);
@@ -608,11 +613,29 @@ int orbfe_debug_copy(orbfe_extractor* h, int what, int image, int level, void* d
     else if (what == 1) { src = h->d_cellkeys + (size_t)image * g.cellkeys_per_img + L.cellkey_off; count = ncell * L.cell_cap; bytes = 4 * (size_t)count; }
     else if (what == 2) { src = h->d_outkeys + (size_t)image * g.out_per_img + L.out_off; count = info[0]; bytes = 4 * (size_t)count; }
     else if (what == 3) { if (cap_bytes < 16) return ORBFE_E_CAPACITY; memcpy(dst, info, 16); return 4; }
+    else if (what == 4) {
+        if (!h->d_oct_ts) return 0;
+        src = h->d_oct_ts + 64 * level; count = 64; bytes = 64 * 8;
+    }
     else return ORBFE_E_ARG;
     if (!dst) return count;
     if ((size_t)cap_bytes < bytes) return ORBFE_E_CAPACITY;
     if (bytes) HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
     return count;
+}
+
+int orbfe_debug_block_sort(uint64_t* data, int n) {
+    if (!data || n < 0 || n > 4096) return ORBFE_E_ARG;
+    if (n == 0) return 0;
+    unsigned long long* d = nullptr;
+    HIPCHK(hipMalloc(&d, (size_t)n * 8));
+    HIPCHK(hipMemcpy(d, data, (size_t)n * 8, hipMemcpyHostToDevice));
+    const size_t lds = (size_t)n * 16 + (size_t)n * 16 + 16 + 16 * ORBFE_SORT_STACK;
+    hipLaunchKernelGGL(k_debug_block_sort, dim3(1), dim3(OCT_NT), lds, 0, d, n);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(data, d, (size_t)n * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipFree(d));
+    return n;
 }
 
 int orbfe_descriptor_distance(const uint8_t* a, const uint8_t* b) {

@@ -478,19 +478,20 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
 }
 
 // ---------------------------------------------------------------------------------------------
-// K4: DistributeOctTree for one (image, level), one wave. Keys are swept in parallel (each key
-// carries the list position of its node); the ordered list/sort logic of the reference runs on
-// LDS tables: phase-1 rounds are rebuilt with scans (list order = push_front order), phase-2
-// passes sort the expandable nodes with the libstdc++ introsort replica (tie order matters) and
-// replay the reference's break-at-N walk. The per-node winner is the first max-response key in
-// key order, i.e. max(score) then min(index) (ORBextractor.cc:757-776).
+// K4: DistributeOctTree for one (image, level) per 256-thread block. Keys are swept in parallel
+// (each key carries the list position of its node, loads batched 4 deep); the ordered list/sort
+// logic of the reference runs on LDS tables: phase-1 rounds are rebuilt with block scans (list
+// order = push_front order), phase-2 passes sort the expandable nodes with the libstdc++
+// introsort replica (tie order matters) and replay the reference's break-at-N walk. The per-node
+// winner is the first max-response key in key order, i.e. max(score) then min(index)
+// (ORBextractor.cc:757-776).
 // ---------------------------------------------------------------------------------------------
-struct ExpEnt { int size; int x0; int pos; };
-struct ExpLess {
-    __device__ bool operator()(const ExpEnt& a, const ExpEnt& b) const {   // compareNodes
-        if (a.size < b.size) return true;
-        if (a.size > b.size) return false;
-        return a.x0 < b.x0;
+#define OCT_NT 256
+#define OCT_U 4
+// expandable node: (size << 44) | (UL.x << 32) | list position; compareNodes orders by the high 32 bits
+struct ExpLess64 {
+    __device__ bool operator()(const unsigned long long& a, const unsigned long long& b) const {
+        return (a >> 32) < (b >> 32);
     }
 };
 __device__ __forceinline__ int quadrant(uint32_t key, int x0, int x1, int y0, int y1) {
@@ -509,12 +510,184 @@ __device__ __forceinline__ void child_rect(int q, int x0, int x1, int y0, int y1
     *cy0 = (q & 2) ? my : y0;
     *cy1 = (q & 2) ? y1 : my;
 }
+// Block-wide (OCT_NT threads) in-place exclusive scan of arr[0..n); returns the total.
+__device__ int block_excl_scan(int* arr, int n, int* s_ws) {
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    int carry = 0;
+    for (int base = 0; base < n; base += OCT_NT) {
+        const int i = base + threadIdx.x;
+        const int v = i < n ? arr[i] : 0;
+        const int incl = wave_incl_scan(v);
+        if (lane == 63) s_ws[wave] = incl;
+        SYNC();
+        int woff = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < OCT_NT / 64; w++) {
+            const int t = s_ws[w];
+            woff += w < wave ? t : 0;
+            tot += t;
+        }
+        if (i < n) arr[i] = carry + woff + incl - v;
+        carry += tot;
+        SYNC();
+    }
+    return carry;
+}
 
-__global__ __launch_bounds__(64) void k_octree(OrbGeom g, const uint32_t* __restrict__ cellkeys,
-                                               const int* __restrict__ cellcnt, uint32_t* lkeys, uint16_t* nodeof,
-                                               uint32_t* outkeys, int* lvinfo, int* ranks, int lap0, int lap1) {
+// Block-parallel, element-for-element replica of libstdc++ std::sort on u64 elements ordered by
+// their high 32 bits (see stl_sort.h "Data-parallel formulation"). Segments are processed one at
+// a time by the whole block: median-of-three on one thread, then the unguarded partition as
+// stop-pairing with block scans; leaves (<= 16 elements) are stably sorted in parallel by rank;
+// depth-exhausted leaves fall back to the serial heapsort replica.
+// Scratch: fl, lpos, rpos, leaves: int[n]; tmp: u64[n]; segs: int4[ORBFE_SORT_STACK].
+// In-place exclusive scan of arr[0..n) by the calling wave only (no workgroup barrier).
+__device__ int wave_scan_lds(int* arr, int n) {
+    const int lane = lane_id();
+    int carry = 0;
+    for (int base = 0; base < n; base += 64) {
+        const int i = base + lane;
+        const int v = i < n ? arr[i] : 0;
+        const int incl = wave_incl_scan(v);
+        if (i < n) arr[i] = carry + incl - v;
+        carry += __shfl(incl, 63, 64);
+    }
+    WAVE_SYNC();
+    return carry;
+}
+
+__device__ void wave_introsort_impl(unsigned long long* a, int n, int* fl, int* lpos, int* rpos, int* leaves,
+                                unsigned long long* tmp, int4* segs, int* s_ws, int* s_ctl) {
+    const int tid = lane_id();
+    if (n <= 1) return;
+    if (tid == 0) {
+        segs[0] = make_int4(0, n, 2 * st_lg(n), 0);
+        s_ctl[0] = 1;   // stack size
+        s_ctl[1] = 0;   // leaf count
+    }
+    WAVE_SYNC();
+    while (true) {
+        if (s_ctl[0] == 0) break;
+        WAVE_SYNC();
+        if (tid == 0) {
+            const int4 sg = segs[--s_ctl[0]];
+            s_ctl[2] = sg.x; s_ctl[3] = sg.y; s_ctl[4] = sg.z;
+            if (sg.y - sg.x <= 16 || sg.z == 0) {
+                leaves[s_ctl[1]++] = sg.x | ((sg.y - sg.x <= 16) ? 0 : (int)0x80000000);
+            } else {
+                unsigned long long* f = a + sg.x;
+                st_move_median_to_first(f, f + 1, f + (sg.y - sg.x) / 2, a + sg.y - 1, ExpLess64());
+            }
+        }
+        WAVE_SYNC();
+        const int lo = s_ctl[2], hi = s_ctl[3], depth = s_ctl[4];
+        if (hi - lo <= 16 || depth == 0) continue;
+        const unsigned P = (unsigned)(a[lo] >> 32);
+        const int m = hi - lo - 1;
+        // left stops (scan rightwards over [lo+1, hi)): !(x < P)
+        for (int i = tid; i < m; i += 64) fl[i] = ((unsigned)(a[lo + 1 + i] >> 32) < P) ? 0 : 1;
+        WAVE_SYNC();
+        const int nl = wave_scan_lds(fl, m);
+        for (int i = tid; i < m; i += 64)
+            if (!((unsigned)(a[lo + 1 + i] >> 32) < P)) lpos[fl[i]] = lo + 1 + i;
+        WAVE_SYNC();
+        // right stops (scan leftwards from hi-1): !(P < x)
+        for (int j = tid; j < m; j += 64) fl[j] = (P < (unsigned)(a[hi - 1 - j] >> 32)) ? 0 : 1;
+        WAVE_SYNC();
+        const int nr = wave_scan_lds(fl, m);
+        for (int j = tid; j < m; j += 64)
+            if (!(P < (unsigned)(a[hi - 1 - j] >> 32))) rpos[fl[j]] = hi - 1 - j;
+        if (tid == 0) s_ctl[5] = 0;
+        WAVE_SYNC();
+        const int kmax = min(nl, nr);
+        int cntk = 0;
+        for (int k = tid; k < kmax; k += 64) cntk += lpos[k] < rpos[k] ? 1 : 0;
+        cntk = wave_sum(cntk);
+        if (tid == 0) s_ctl[5] = cntk;
+        WAVE_SYNC();
+        const int sw = s_ctl[5];   // lpos increasing, rpos decreasing: the pairs that swap are a prefix
+        for (int k = tid; k < sw; k += 64) {
+            const unsigned long long x = a[lpos[k]];
+            a[lpos[k]] = a[rpos[k]];
+            a[rpos[k]] = x;
+        }
+        if (tid == 0) {
+            int cut;
+            if (sw == 0) cut = lpos[0];
+            else cut = (sw < nl && lpos[sw] < rpos[sw - 1]) ? lpos[sw] : rpos[sw - 1];
+            segs[s_ctl[0]++] = make_int4(cut, hi, depth - 1, 0);
+            segs[s_ctl[0]++] = make_int4(lo, cut, depth - 1, 0);
+        }
+        WAVE_SYNC();
+    }
+    WAVE_SYNC();
+    // leaves were recorded left to right; stable rank sort inside each ordinary leaf
+    const int nleaf = s_ctl[1];
+    for (int i = tid; i < n; i += 64) {
+        int lo_i = 0, hi_i = nleaf - 1;   // last leaf with start <= i
+        while (lo_i < hi_i) {
+            const int mid = (lo_i + hi_i + 1) >> 1;
+            if ((leaves[mid] & 0x7fffffff) <= i) lo_i = mid; else hi_i = mid - 1;
+        }
+        const int ls = leaves[lo_i] & 0x7fffffff;
+        const int le = lo_i + 1 < nleaf ? (leaves[lo_i + 1] & 0x7fffffff) : n;
+        const unsigned long long x = a[i];
+        if (leaves[lo_i] & 0x80000000) { tmp[i] = x; continue; }
+        const unsigned kx = (unsigned)(x >> 32);
+        int r = 0;
+        for (int j = ls; j < le; j++) {
+            const unsigned kj = (unsigned)(a[j] >> 32);
+            r += (kj < kx || (kj == kx && j < i)) ? 1 : 0;
+        }
+        tmp[ls + r] = x;
+    }
+    WAVE_SYNC();
+    for (int i = tid; i < n; i += 64) a[i] = tmp[i];
+    WAVE_SYNC();
+    if (tid == 0)
+        for (int L = 0; L < nleaf; L++)
+            if (leaves[L] & 0x80000000) {
+                const int ls = leaves[L] & 0x7fffffff;
+                const int le = L + 1 < nleaf ? (leaves[L + 1] & 0x7fffffff) : n;
+                st_heap_sort(a + ls, le - ls, ExpLess64());
+            }
+    WAVE_SYNC();
+}
+
+// Block entry: the sort runs on wave 0 only (wave-level scans, no workgroup barriers inside);
+// the other waves wait at the closing barrier.
+__device__ void block_introsort(unsigned long long* a, int n, int* fl, int* lpos, int* rpos, int* leaves,
+                                unsigned long long* tmp, int4* segs, int* s_ws, int* s_ctl) {
+    (void)s_ws;
+    SYNC();
+    if ((threadIdx.x >> 6) == 0) wave_introsort_impl(a, n, fl, lpos, rpos, leaves, tmp, segs, s_ws, s_ctl);
+    SYNC();
+}
+
+// Debug/test entry: sort one array with the block sort (single block).
+__global__ __launch_bounds__(OCT_NT) void k_debug_block_sort(unsigned long long* a, int n) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_dbs[];
+    unsigned long long* la = (unsigned long long*)smem_dbs;
+    unsigned long long* tmp = la + n;
+    int* fl = (int*)(tmp + n);
+    int* lpos = fl + n;
+    int* rpos = lpos + n;
+    int* leaves = rpos + n;
+    int4* segs = (int4*)(((uintptr_t)(leaves + n) + 15) & ~(uintptr_t)15);
+    __shared__ int s_ws[OCT_NT / 64];
+    __shared__ int s_ctl[8];
+    for (int i = threadIdx.x; i < n; i += OCT_NT) la[i] = a[i];
+    SYNC();
+    block_introsort(la, n, fl, lpos, rpos, leaves, tmp, segs, s_ws, s_ctl);
+    for (int i = threadIdx.x; i < n; i += OCT_NT) a[i] = la[i];
+}
+
+__global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __restrict__ cellkeys,
+                                                   const int* __restrict__ cellcnt, uint32_t* lkeys,
+                                                   uint16_t* nodeof, uint32_t* outkeys, int* lvinfo, int* ranks,
+                                                   int lap0, int lap1, unsigned long long* tstamp) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_oct[];
-    const int l = blockIdx.x, b = blockIdx.y, lane = lane_id();
+    // grid (B, nlevels): level-0 blocks (the longest) are dispatched first
+    const int b = blockIdx.x, l = blockIdx.y, tid = threadIdx.x;
     const OrbLevel& L = g.lv[l];
     const int NC = g.node_cap;
     const int ncell = L.n_cols * L.n_rows;
@@ -538,53 +711,66 @@ __global__ __launch_bounds__(64) void k_octree(OrbGeom g, const uint32_t* __rest
     int* tmpB = (int*)carve(4 * NC);
     int* tmpC = (int*)carve(4 * NC);
     int* procp = (int*)carve(4 * NC);
-    ExpEnt* expv = (ExpEnt*)carve(sizeof(ExpEnt) * NC);
+    unsigned long long* expv = (unsigned long long*)carve(8 * NC);
     unsigned long long* best = (unsigned long long*)carve(8 * NC);
-    StSeg* sstack = (StSeg*)carve(sizeof(StSeg) * ORBFE_SORT_STACK);
+    int* leaves = (int*)carve(4 * NC);
+    int4* segs = (int4*)carve(sizeof(int4) * ORBFE_SORT_STACK);
+    __shared__ int s_ws[OCT_NT / 64];
     __shared__ int s_misc[8];
 
+    // diagnostic phase stamps (image 0 of the batch, every level), tstamp == nullptr in normal runs
+    unsigned long long* ts = (tstamp && b == 0) ? tstamp + 64 * l : nullptr;
+    int tsi = 0;
+#define OCT_STAMP() do { if (ts && tid == 0 && tsi < 62) ts[tsi] = __builtin_amdgcn_s_memtime(); tsi++; } while (0)
+    OCT_STAMP();
     // ---- gather this level's cell key lists in cell order (vToDistributeKeys order) ----
     const int* cc = cellcnt + (size_t)b * g.total_cells + L.cell_base;
-    {
-        int carry = 0;
-        for (int base = 0; base < ncell; base += 64) {
-            const int i = base + lane;
-            const int v = i < ncell ? cc[i] : 0;
-            const int incl = wave_incl_scan(v);
-            if (i < ncell) cellpre[i + 1] = carry + incl;
-            carry += __shfl(incl, 63, 64);
-        }
-        if (lane == 0) cellpre[0] = 0;
-    }
+    for (int i = tid; i < ncell; i += OCT_NT) cellpre[i] = cc[i];
     SYNC();
-    const int K = cellpre[ncell];
+    const int K = block_excl_scan(cellpre, ncell, s_ws);
+    if (tid == 0) cellpre[ncell] = K;
+    SYNC();
     const size_t kbase = (size_t)b * g.cellkeys_per_img + L.cellkey_off;
     uint32_t* keys = lkeys + kbase;
     uint16_t* nof = nodeof + kbase;
     const uint32_t* ck = cellkeys + kbase;
-    for (int k = lane; k < K; k += 64) {
-        int lo = 0, hi = ncell - 1;   // largest c with cellpre[c] <= k
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (cellpre[mid] <= k) lo = mid; else hi = mid - 1;
+    for (int k0 = tid; k0 < K; k0 += OCT_NT * OCT_U) {
+        uint32_t v[OCT_U];
+#pragma unroll
+        for (int u = 0; u < OCT_U; u++) {
+            const int k = min(k0 + OCT_NT * u, K - 1);
+            int lo = 0, hi = ncell - 1;   // largest c with cellpre[c] <= k
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (cellpre[mid] <= k) lo = mid; else hi = mid - 1;
+            }
+            v[u] = ck[(size_t)lo * L.cell_cap + (k - cellpre[lo])];
         }
-        keys[k] = ck[(size_t)lo * L.cell_cap + (k - cellpre[lo])];
+#pragma unroll
+        for (int u = 0; u < OCT_U; u++)
+            if (k0 + OCT_NT * u < K) keys[k0 + OCT_NT * u] = v[u];
     }
+    OCT_STAMP();
     // ---- initial nodes (ORBextractor.cc:559-601) ----
     const int nIni = L.n_ini;
     const float hX = L.hx;
     const int H = (L.h - ORBFE_MINB) - ORBFE_MINB;
-    for (int i = lane; i < nIni; i += 64) tmpA[i] = 0;
+    for (int i = tid; i < nIni; i += OCT_NT) tmpA[i] = 0;
+    for (int i = tid; i < 4 * NC; i += OCT_NT) Ccnt[i] = 0;
     SYNC();
-    for (int k = lane; k < K; k += 64) {
-        const int r = (int)((float)(keys[k] & 0xfff) / hX);
-        atomicAdd(&tmpA[r], 1);
+    for (int k0 = tid; k0 < K; k0 += OCT_NT * OCT_U) {
+        uint32_t v[OCT_U];
+#pragma unroll
+        for (int u = 0; u < OCT_U; u++) v[u] = keys[min(k0 + OCT_NT * u, K - 1)];
+#pragma unroll
+        for (int u = 0; u < OCT_U; u++)
+            if (k0 + OCT_NT * u < K) atomicAdd(&tmpA[(int)((float)(v[u] & 0xfff) / hX)], 1);
     }
     SYNC();
-        for (int i = lane; i < nIni; i += 64) tmpB[i] = tmpA[i] > 0 ? 1 : 0;
+    for (int i = tid; i < nIni; i += OCT_NT) tmpB[i] = tmpA[i] > 0 ? 1 : 0;
     SYNC();
-    int n = wave_excl_scan_lds(tmpB, nIni);   // position of each non-empty root
-    for (int i = lane; i < nIni; i += 64) {
+    int n = block_excl_scan(tmpB, nIni, s_ws);   // position of each non-empty root
+    for (int i = tid; i < nIni; i += OCT_NT) {
         if (tmpA[i] > 0) {
             const int q = tmpB[i];
             Cx0[q] = (int16_t)(int)(hX * (float)i);
@@ -594,60 +780,70 @@ __global__ __launch_bounds__(64) void k_octree(OrbGeom g, const uint32_t* __rest
             Csz[q] = tmpA[i];
         }
     }
-    for (int i = lane; i < 4 * NC; i += 64) Ccnt[i] = 0;
     SYNC();
-    for (int k = lane; k < K; k += 64) {
-        const uint32_t key = keys[k];
-        const int r = (int)((float)(key & 0xfff) / hX);
-        const int q = tmpB[r];
-        nof[k] = (uint16_t)q;
-        if (Csz[q] > 1)
-            atomicAdd(&Ccnt[4 * q + quadrant(key, Cx0[q], Cx1[q], Cy0[q], Cy1[q])], 1);
+    for (int k0 = tid; k0 < K; k0 += OCT_NT * OCT_U) {
+        uint32_t v[OCT_U];
+#pragma unroll
+        for (int u = 0; u < OCT_U; u++) v[u] = keys[min(k0 + OCT_NT * u, K - 1)];
+#pragma unroll
+        for (int u = 0; u < OCT_U; u++) {
+            const int k = k0 + OCT_NT * u;
+            if (k < K) {
+                const uint32_t key = v[u];
+                const int q = tmpB[(int)((float)(key & 0xfff) / hX)];
+                nof[k] = (uint16_t)q;
+                if (Csz[q] > 1) atomicAdd(&Ccnt[4 * q + quadrant(key, Cx0[q], Cx1[q], Cy0[q], Cy1[q])], 1);
+            }
+        }
     }
+    for (int i = tid; i < NC; i += OCT_NT) divorder[i] = -1;
     SYNC();
+    OCT_STAMP();
 
     const int N = L.budget;
     bool phase2 = false, finish = false;
     int m = 0;   // expandable-node count of the last rebuild (vSizeAndPointerToNode)
-    for (int i = lane; i < NC; i += 64) divorder[i] = -1;
-    SYNC();
     int guard = 0;
     while (!finish && guard++ < 100000) {
         const int prevN = n;
         int T_div;   // number of divided nodes in this step
         if (!phase2) {
             // every node with >1 keys divides, in list order
-            for (int i = lane; i < n; i += 64) {
-                const bool dv = Csz[i] > 1;
-                divorder[i] = dv ? 1 : -1;
-                tmpA[i] = dv ? 1 : 0;
-            }
+            for (int i = tid; i < n; i += OCT_NT) tmpA[i] = Csz[i] > 1 ? 1 : 0;
             SYNC();
-            T_div = wave_excl_scan_lds(tmpA, n);   // tmpA[i] = divider rank t (list order)
-            for (int i = lane; i < n; i += 64)
+            for (int i = tid; i < n; i += OCT_NT) divorder[i] = Csz[i] > 1 ? 1 : -1;
+            T_div = block_excl_scan(tmpA, n, s_ws);   // tmpA[i] = divider rank t (list order)
+            for (int i = tid; i < n; i += OCT_NT)
                 if (divorder[i] >= 0) { divorder[i] = tmpA[i]; procp[tmpA[i]] = i; }
             SYNC();
         } else {
-            if (lane == 0) {
-                stl_sort_with_stack(expv, m, ExpLess(), sstack);
-                int Lsz = n, t = 0;
-                for (int j = m - 1; j >= 0; j--) {
-                    const int q = expv[j].pos;
-                    int c = 0;
-                    for (int k = 0; k < 4; k++) c += Ccnt[4 * q + k] > 0;
-                    divorder[q] = t;
-                    procp[t] = q;
-                    t++;
-                    Lsz += c - 1;
-                    if (Lsz >= N) break;
-                }
-                s_misc[0] = t;
+            // std::sort(vPrevSizeAndPointerToNode, compareNodes) (ORBextractor.cc:700), exact replica
+            block_introsort(expv, m, tmpC, tmpA, tmpB, leaves, best, segs, s_ws, s_misc);
+            // walk from the back until the list reaches N (ORBextractor.cc:701-748): processed node t is
+            // expv[m-1-t]; the list grows by (children - 1) per division -> first t where it reaches N
+            for (int t = tid; t < m; t += OCT_NT) {
+                const int q = (int)(expv[m - 1 - t] & 0xffffffffull);
+                const int4 cq = *(const int4*)&Ccnt[4 * q];
+                tmpA[t] = (cq.x > 0) + (cq.y > 0) + (cq.z > 0) + (cq.w > 0) - 1;
+                procp[t] = q;
+            }
+            if (tid == 0) s_misc[6] = m;
+            SYNC();
+            (void)block_excl_scan(tmpA, m, s_ws);   // tmpA[t] = growth before processing t
+            for (int t = tid; t < m; t += OCT_NT) {
+                const int q = procp[t];
+                const int4 cq = *(const int4*)&Ccnt[4 * q];
+                const int grow = (cq.x > 0) + (cq.y > 0) + (cq.z > 0) + (cq.w > 0) - 1;
+                if (n + tmpA[t] + grow >= N) atomicMin(&s_misc[6], t + 1);
             }
             SYNC();
-            T_div = s_misc[0];
+            T_div = s_misc[6];
+            for (int t = tid; t < T_div; t += OCT_NT) divorder[procp[t]] = t;
+            SYNC();
         }
+        OCT_STAMP();
         // children counts per processed node (t order): tmpB = nonempty, tmpC = expandable (>1)
-        for (int t = lane; t < T_div; t += 64) {
+        for (int t = tid; t < T_div; t += OCT_NT) {
             const int q = procp[t];
             int c = 0, e = 0;
             for (int k = 0; k < 4; k++) { const int v = Ccnt[4 * q + k]; c += v > 0; e += v > 1; }
@@ -655,10 +851,10 @@ __global__ __launch_bounds__(64) void k_octree(OrbGeom g, const uint32_t* __rest
             tmpC[t] = e;
         }
         SYNC();
-        const int Ctot = wave_excl_scan_lds(tmpB, T_div);
-        const int Etot = wave_excl_scan_lds(tmpC, T_div);
+        const int Ctot = block_excl_scan(tmpB, T_div, s_ws);
+        const int Etot = block_excl_scan(tmpC, T_div, s_ws);
         // children: block of t starts at sum_{t'>t} c_t' = Ctot - (excl_t + c_t); order n4,n3,n2,n1
-        for (int t = lane; t < T_div; t += 64) {
+        for (int t = tid; t < T_div; t += OCT_NT) {
             const int q = procp[t];
             int c = 0;
             for (int k = 0; k < 4; k++) c += Ccnt[4 * q + k] > 0;
@@ -685,16 +881,17 @@ __global__ __launch_bounds__(64) void k_octree(OrbGeom g, const uint32_t* __rest
                 if (v > 1) {
                     int a0, a1, b0, b1;
                     child_rect(ch, px0, px1, py0, py1, &a0, &a1, &b0, &b1);
-                    expv[e].size = v; expv[e].x0 = a0; expv[e].pos = childpos[4 * q + ch];
+                    expv[e] = ((unsigned long long)v << 44) | ((unsigned long long)(a0 & 0xfff) << 32) |
+                              (unsigned long long)(uint16_t)childpos[4 * q + ch];
                     e++;
                 }
             }
         }
         // undivided nodes keep their relative order after the pushed children
-        for (int i = lane; i < n; i += 64) tmpA[i] = divorder[i] < 0 ? 1 : 0;
+        for (int i = tid; i < n; i += OCT_NT) tmpA[i] = divorder[i] < 0 ? 1 : 0;
         SYNC();
-        const int nKeep = wave_excl_scan_lds(tmpA, n);
-        for (int i = lane; i < n; i += 64) {
+        const int nKeep = block_excl_scan(tmpA, n, s_ws);
+        for (int i = tid; i < n; i += OCT_NT) {
             if (divorder[i] < 0) {
                 const int np = Ctot + tmpA[i];
                 newpos[i] = (int16_t)np;
@@ -704,63 +901,97 @@ __global__ __launch_bounds__(64) void k_octree(OrbGeom g, const uint32_t* __rest
             }
         }
         const int newN = Ctot + nKeep;
-        for (int i = lane; i < 4 * newN; i += 64) Xcnt[i] = 0;
+        for (int i = tid; i < 4 * newN; i += OCT_NT) Xcnt[i] = 0;
         SYNC();
+        OCT_STAMP();
         // key sweep: move keys to their new node positions and count the next split
-        for (int k = lane; k < K; k += 64) {
-            const uint32_t key = keys[k];
-            const int q = nof[k];
-            int np;
-            if (divorder[q] >= 0) np = childpos[4 * q + quadrant(key, Cx0[q], Cx1[q], Cy0[q], Cy1[q])];
-            else np = newpos[q];
-            nof[k] = (uint16_t)np;
-            if (Xsz[np] > 1)
-                atomicAdd(&Xcnt[4 * np + quadrant(key, Xx0[np], Xx1[np], Xy0[np], Xy1[np])], 1);
+        for (int k0 = tid; k0 < K; k0 += OCT_NT * OCT_U) {
+            uint32_t v[OCT_U];
+            int qv[OCT_U];
+#pragma unroll
+            for (int u = 0; u < OCT_U; u++) {
+                const int k = min(k0 + OCT_NT * u, K - 1);
+                v[u] = keys[k];
+                qv[u] = nof[k];
+            }
+#pragma unroll
+            for (int u = 0; u < OCT_U; u++) {
+                const int k = k0 + OCT_NT * u;
+                if (k < K) {
+                    const uint32_t key = v[u];
+                    const int q = qv[u];
+                    int np;
+                    if (divorder[q] >= 0) np = childpos[4 * q + quadrant(key, Cx0[q], Cx1[q], Cy0[q], Cy1[q])];
+                    else np = newpos[q];
+                    nof[k] = (uint16_t)np;
+                    if (Xsz[np] > 1)
+                        atomicAdd(&Xcnt[4 * np + quadrant(key, Xx0[np], Xx1[np], Xy0[np], Xy1[np])], 1);
+                }
+            }
         }
-        for (int i = lane; i < NC; i += 64) divorder[i] = -1;
         SYNC();
-        { int16_t* t; int* ti;
-          t = Cx0; Cx0 = Xx0; Xx0 = t; t = Cx1; Cx1 = Xx1; Xx1 = t;
-          t = Cy0; Cy0 = Xy0; Xy0 = t; t = Cy1; Cy1 = Xy1; Xy1 = t;
-          ti = Csz; Csz = Xsz; Xsz = ti; ti = Ccnt; Ccnt = Xcnt; Xcnt = ti; }
+        for (int i = tid; i < NC; i += OCT_NT) divorder[i] = -1;
+        {
+            int16_t* t;
+            int* ti;
+            t = Cx0; Cx0 = Xx0; Xx0 = t; t = Cx1; Cx1 = Xx1; Xx1 = t;
+            t = Cy0; Cy0 = Xy0; Xy0 = t; t = Cy1; Cy1 = Xy1; Xy1 = t;
+            ti = Csz; Csz = Xsz; Xsz = ti; ti = Ccnt; Ccnt = Xcnt; Xcnt = ti;
+        }
+        SYNC();
         n = newN;
-        if (n > NC - 4) { n = NC - 4; finish = true; }   // capacity guard (bound: n <= max(N+2, 4*nIni) = NC-8-1)
         m = Etot;
+        if (n > NC - 4) { n = NC - 4; finish = true; }   // capacity guard (bound: n <= max(N+2, 4*nIni) = NC-8-1)
         if (n >= N || n == prevN) finish = true;
         else if (!phase2 && n + 3 * m > N) phase2 = true;
     }
+    OCT_STAMP();
     // ---- retain the best key per node ----
-    for (int i = lane; i < n; i += 64) best[i] = 0ull;
+    for (int i = tid; i < n; i += OCT_NT) best[i] = 0ull;
     SYNC();
-    for (int k = lane; k < K; k += 64) {
-        const uint32_t key = keys[k];
-        const unsigned long long v = ((unsigned long long)(key >> 24) << 32) | (0xFFFFFFFFull - (unsigned)k);
-        atomicMax(&best[nof[k]], v);
+    for (int k0 = tid; k0 < K; k0 += OCT_NT * OCT_U) {
+        uint32_t v[OCT_U];
+        int qv[OCT_U];
+#pragma unroll
+        for (int u = 0; u < OCT_U; u++) {
+            const int k = min(k0 + OCT_NT * u, K - 1);
+            v[u] = keys[k];
+            qv[u] = nof[k];
+        }
+#pragma unroll
+        for (int u = 0; u < OCT_U; u++) {
+            const int k = k0 + OCT_NT * u;
+            if (k < K)
+                atomicMax(&best[qv[u]], ((unsigned long long)(v[u] >> 24) << 32) | (0xFFFFFFFFull - (unsigned)k));
+        }
     }
     SYNC();
     uint32_t* ok = outkeys + (size_t)b * g.out_per_img + L.out_off;
     int* rk = ranks + (size_t)b * g.out_per_img + L.out_off;
-    int carry_lap = 0, carry_mono = 0;
-    for (int base = 0; base < n; base += 64) {
-        const int i = base + lane;
-        bool lap = false;
-        if (i < n) {
-            const unsigned k = 0xFFFFFFFFu - (unsigned)(best[i] & 0xFFFFFFFFull);
-            const uint32_t key = keys[k];
-            const int x = (int)(key & 0xfff) + ORBFE_MINB, y = (int)((key >> 12) & 0xfff) + ORBFE_MINB;
-            ok[i] = (uint32_t)x | ((uint32_t)y << 12) | (key & 0xff000000u);
-            const float sx = (l == 0) ? (float)x : (float)x * L.scale;
-            lap = sx >= (float)lap0 && sx <= (float)lap1;
-        }
-        const int il = wave_incl_scan(lap ? 1 : 0);
-        const int im = wave_incl_scan((i < n && !lap) ? 1 : 0);
-        if (i < n) rk[i] = lap ? (int)(0x40000000 | (carry_lap + il - 1)) : (carry_mono + im - 1);
-        carry_lap += __shfl(il, 63, 64);
-        carry_mono += __shfl(im, 63, 64);
+    // lapping flag per output node, then ranks among lapping / non-lapping keys (block scans)
+    for (int i = tid; i < n; i += OCT_NT) {
+        const unsigned k = 0xFFFFFFFFu - (unsigned)(best[i] & 0xFFFFFFFFull);
+        const uint32_t key = keys[k];
+        const int x = (int)(key & 0xfff) + ORBFE_MINB, y = (int)((key >> 12) & 0xfff) + ORBFE_MINB;
+        ok[i] = (uint32_t)x | ((uint32_t)y << 12) | (key & 0xff000000u);
+        const float sx = (l == 0) ? (float)x : (float)x * L.scale;
+        const bool lap = sx >= (float)lap0 && sx <= (float)lap1;
+        tmpA[i] = lap ? 1 : 0;
+        tmpB[i] = lap ? 0 : 1;
     }
-    if (lane == 0) {
+    SYNC();
+    const int nlap = block_excl_scan(tmpA, n, s_ws);
+    const int nmono = block_excl_scan(tmpB, n, s_ws);
+    for (int i = tid; i < n; i += OCT_NT) {
+        const bool lap = (i + 1 < n ? tmpA[i + 1] : nlap) != tmpA[i];
+        rk[i] = lap ? (int)(0x40000000 | tmpA[i]) : tmpB[i];
+    }
+    OCT_STAMP();
+    if (ts && tid == 0) ts[63] = (unsigned long long)tsi;
+#undef OCT_STAMP
+    if (tid == 0) {
         int* inf = lvinfo + ((size_t)b * g.nlevels + l) * 4;
-        inf[0] = n; inf[1] = carry_lap; inf[2] = carry_mono; inf[3] = K;
+        inf[0] = n; inf[1] = nlap; inf[2] = nmono; inf[3] = K;
     }
 }
 

@@ -167,4 +167,35 @@ ORBFE_HD void stl_sort(T* first, int n, Cmp comp) {
     stl_sort_with_stack(first, n, comp, stack);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Data-parallel formulation of the SAME libstdc++ introsort (used by the octree kernel's block
+// sort). The result is element-for-element identical to stl_sort because:
+//  * __unguarded_partition(first, last, pivot) pairs the k-th "left stop" (scanning right, first
+//    element with !(x < P)) with the k-th "right stop" (scanning left, first element with
+//    !(P < x)) of the ORIGINAL segment for k = 1..s, s = #k with Lstop_k < Rstop_k; it returns
+//    cut = Lstop_{s+1} if that exists and lies left of Rstop_s, else Rstop_s (s >= 1), or Lstop_1.
+//  * after the introsort loop every leaf segment (<= 16 elements) holds only elements that are
+//    not-greater than everything to its right, so __final_insertion_sort never moves an element
+//    across a leaf boundary and acts as a STABLE sort inside each leaf; any stable sort gives the
+//    same order. Leaves whose depth budget ran out are heap-sorted by the serial replica.
+// partition_by_stops is the sequential statement of the first point (checked against
+// st_unguarded_partition in tests/native/check_stl_sort.cpp); the device version computes the
+// stops with block scans.
+template <typename T, typename Cmp>
+ORBFE_HD int partition_by_stops(T* a, int lo, int hi, Cmp comp, int* lstop, int* rstop) {
+    const T P = a[lo];
+    int nl = 0, nr = 0;
+    for (int i = lo + 1; i < hi; i++)
+        if (!comp(a[i], P)) lstop[nl++] = i;
+    for (int j = hi - 1; j > lo; j--)
+        if (!comp(P, a[j])) rstop[nr++] = j;
+    int s = 0;
+    while (s < nl && s < nr && lstop[s] < rstop[s]) s++;
+    int cut;
+    if (s == 0) cut = lstop[0];
+    else cut = (s < nl && lstop[s] < rstop[s - 1]) ? lstop[s] : rstop[s - 1];
+    for (int k = 0; k < s; k++) st_swap(&a[lstop[k]], &a[rstop[k]]);
+    return cut;
+}
+
 }  // namespace orbfe
