@@ -1,0 +1,34 @@
+"""CPU: liborbfe.so builds for gfx950, loads, and exports every function include/orbfe.h declares
+(no compute calls: there is no GPU here)."""
+import ctypes
+import os
+import re
+
+HDR = os.path.join(os.path.dirname(os.path.dirname(__file__)), "include", "orbfe.h")
+
+
+def _declared_functions():
+    src = open(HDR).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(orbfe_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_boundary():
+    fns = _declared_functions()
+    for required in ("orbfe_extractor_create", "orbfe_extract", "orbfe_extract_batch", "orbfe_pyramid_level",
+                     "orbfe_stereo_match", "orbfe_stereo_match_batch", "orbfe_descriptor_distance"):
+        assert required in fns
+
+
+def test_library_exports_every_declared_symbol(orbfe_lib):
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(os.path.dirname(__file__)), "orb_slam3_ros_amd", "liborbfe.so"))
+    missing = [f for f in _declared_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+
+
+def test_descriptor_distance_host_entry(orbfe_lib):
+    import numpy as np
+    a = np.zeros(32, np.uint8)
+    b = np.zeros(32, np.uint8)
+    b[0], b[31] = 0xFF, 0x01
+    assert orbfe_lib.orbfe_descriptor_distance(a.ctypes.data, b.ctypes.data) == 9
