@@ -67,7 +67,7 @@ def cpu_baseline(pairs_l, pairs_r, w, h, nfeatures, bf, fx):
         pass
     return {"value": round(n / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
             "sample": f"{n} stereo frames {w}x{h} (extract L+R + ComputeStereoMatches), {threads} threads, "
-                      f"frame-parallel, oracle/orb_oracle.cpp -O3 -march=native; host CPU: {cpu}",
+                      f"frame-parallel, oracle/orb_oracle.cpp -O3 -march=x86-64-v3; host CPU: {cpu}",
             "seconds": round(dt, 3)}
 
 
