@@ -111,9 +111,111 @@ int orbfe_stereo_match(orbfe_extractor* left, orbfe_extractor* right, float bf, 
                        float* depth);
 
 /* ---------------------------------------------------------------------------------------------
- * ORBmatcher — replaces ORB_SLAM3::ORBmatcher::DescriptorDistance (ORBmatcher.cc:2058-2074)
+ * ORBmatcher — replaces the Tracking-thread methods of ORB_SLAM3::ORBmatcher (include/ORBmatcher.h)
+ * and Frame::ComputeStereoFishEyeMatches' brute-force kNN. Stateless and re-entrant; every call
+ * takes host pointers, runs on the current HIP device, and returns nmatches (>= 0) or an error.
+ * The C++ objects the reference passes (Frame&, KeyFrame*, MapPoint*, FeatureVector) are
+ * flattened by the caller into the snapshot structs below under the objects' own locks
+ * (MapPoint::GetDescriptor / isBad / Observations, MapPoint.cc:210,302,405); MapPoint* results
+ * are returned as the caller's int32 handles (-1 = NULL).
  * ------------------------------------------------------------------------------------------- */
-int orbfe_descriptor_distance(const uint8_t* a, const uint8_t* b);
+int orbfe_descriptor_distance(const uint8_t* a, const uint8_t* b);   /* DescriptorDistance (ORBmatcher.cc:2058-2074) */
+
+#define ORBFE_GRID_COLS 64   /* FRAME_GRID_COLS (Frame.h:44) */
+#define ORBFE_GRID_ROWS 48   /* FRAME_GRID_ROWS (Frame.h:45) */
+
+/* The parts of a Frame the matchers read (Frame.h). Keypoints are mvKeysUn (== mvKeys for the
+ * rectified / undistorted case); the 64x48 grid (AssignFeaturesToGrid, Frame.cc:385-416) is
+ * rebuilt from them with the reference's PosInGrid arithmetic. */
+typedef struct orbfe_frame {
+    int32_t n;                       /* N */
+    const orbfe_keypoint* keys;      /* mvKeysUn [n] */
+    const uint8_t* desc;             /* mDescriptors [n][32] */
+    const float* uright;             /* mvuRight [n] or NULL (monocular) */
+    float min_x, max_x, min_y, max_y;   /* mnMinX, mnMaxX, mnMinY, mnMaxY (ComputeImageBounds) */
+    int32_t nlevels;
+    const float* scale_factors;      /* mvScaleFactors [nlevels] */
+    float mbf;                       /* mbf (stereo baseline * fx) */
+} orbfe_frame;
+
+/* MapPoint tracking snapshot for SearchByProjection(Frame&, vector<MapPoint*>, ...)
+ * (MapPoint.h:172-180; filled by Frame::isInFrustum, Tracking.cc:3407-3425). 80 bytes. */
+#define ORBFE_MP_IN_VIEW 1           /* mbTrackInView */
+#define ORBFE_MP_BAD 2               /* isBad() */
+typedef struct orbfe_map_point {
+    float proj_x, proj_y, proj_xr;   /* mTrackProjX, mTrackProjY, mTrackProjXR */
+    float view_cos;                  /* mTrackViewCos */
+    float depth;                     /* mTrackDepth */
+    int32_t scale_level;             /* mnTrackScaleLevel */
+    int32_t flags;                   /* ORBFE_MP_* */
+    int32_t observations;            /* Observations() */
+    int32_t id;                      /* handle stored into mvpMapPoints */
+    int32_t reserved[3];
+    uint8_t desc[32];                /* GetDescriptor() */
+} orbfe_map_point;
+
+/* ORBmatcher(nnratio).SearchByProjection(F, vpMapPoints, th, bFarPoints, thFarPoints)
+ * (ORBmatcher.cc:43-213, pinhole/rectified path). mvp: F.mvpMapPoints as handles [F.n], updated in
+ * place; mvp_obs: Observations() of the MapPoint currently in each slot (0 when empty). Points are
+ * processed in array order exactly as the reference loop (a keypoint already holding a point with
+ * Observations() > 0 is skipped). Returns nmatches. */
+int orbfe_search_by_projection_local(const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs,
+                                     const orbfe_map_point* mps, int32_t n_mps, float th, int32_t bFarPoints,
+                                     float thFarPoints, float nnratio);
+
+/* One projected point of the last frame for SearchByProjection(CurrentFrame, LastFrame, th, bMono)
+ * (ORBmatcher.cc:1676-1887): the caller projects LastFrame.mvpMapPoints[i] with Tcw
+ * (x3Dc = Tcw * X, invzc = 1/z, uv = K * x3Dc) and skips outliers / empty slots (valid = 0). */
+typedef struct orbfe_proj_point {
+    float u, v, invzc;
+    int32_t octave;                  /* LastFrame keypoint octave (nLastOctave) */
+    float angle;                     /* LastFrame keypoint angle (rotation histogram) */
+    int32_t valid;
+    int32_t observations;            /* Observations() of the MapPoint */
+    int32_t id;                      /* MapPoint handle */
+    uint8_t desc[32];
+} orbfe_proj_point;                  /* 64 bytes */
+
+/* Motion-model search: bForward / bBackward as computed by the reference from the poses
+ * (ORBmatcher.cc:1691-1693). Returns nmatches after the rotation-consistency filter. */
+int orbfe_search_by_projection_lastframe(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_obs,
+                                         const orbfe_proj_point* pts, int32_t n_pts, float th, int32_t bForward,
+                                         int32_t bBackward, int32_t checkOri);
+
+/* Relocalisation refinement SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
+ * (ORBmatcher.cc:1889-2010): one entry per KF map point that is not bad and not already found,
+ * projected by the caller; octave = PredictScale(...) (MapPoint.cc:531-546), angle =
+ * pKF->mvKeysUn[i].angle; valid = 0 when the reference's bounds / distance checks reject it.
+ * Any slot already holding a MapPoint is skipped. */
+int orbfe_search_by_projection_kf(const orbfe_frame* cur, int32_t* mvp, const orbfe_proj_point* pts,
+                                  int32_t n_pts, float th, int32_t ORBdist, int32_t checkOri);
+
+/* SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize) (ORBmatcher.cc:648-763).
+ * prev_matched: [F1.n][2] (x, y), updated in place; matches12: [F1.n] output. */
+int orbfe_search_for_initialization(const orbfe_frame* F1, const orbfe_frame* F2, float* prev_matched,
+                                    int32_t* matches12, int32_t windowSize, float nnratio, int32_t checkOri);
+
+/* DBoW2::FeatureVector (std::map<NodeId, vector<unsigned>>) flattened: node ids ascending,
+ * offsets[n_nodes + 1] into indices. */
+typedef struct orbfe_feature_vector {
+    int32_t n_nodes;
+    const uint32_t* node_ids;
+    const int32_t* offsets;
+    const uint32_t* indices;
+} orbfe_feature_vector;
+
+/* SearchByBoW(pKF, F, vpMapPointMatches) (ORBmatcher.cc:223-425, monocular/pinhole path).
+ * kf_mp: pKF->GetMapPointMatches() handles with bad points already mapped to -1; out: [F.n]. */
+int orbfe_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, const int32_t* kf_mp, int32_t kf_n,
+                        const orbfe_feature_vector* kf_fv, const orbfe_frame* F, const orbfe_feature_vector* f_fv,
+                        int32_t* out, float nnratio, int32_t checkOri);
+
+/* ComputeStereoFishEyeMatches' descriptor stage (Frame.cc:1126-1151): BFMatcher(NORM_HAMMING)
+ * knnMatch(k=2) of left rows [0, nl) against right rows [0, nr) and Lowe's 0.7 ratio. out_train[i]
+ * = best right row of left row i or -1; out_dist[i] its distance. The KannalaBrandt8
+ * TriangulateMatches post-filter stays with the camera model on the host. */
+int orbfe_stereo_knn_ratio(const uint8_t* left_desc, int32_t nl, const uint8_t* right_desc, int32_t nr,
+                           float ratio, int32_t* out_train, int32_t* out_dist);
 
 /* Debug/inspection (tests only): copy an intermediate of image `image`, level `level` of the last
  * batch to host memory. what: 0 = per-cell FAST key counts (int32[n_cells]),

@@ -1,1 +1,354 @@
-// matcher restatement (filled in later)
+// ============================================================================================
+// orb_oracle_match.cpp — CPU ORACLE of the Tracking-thread ORBmatcher methods (test
+// infrastructure only; see orb_oracle.cpp's header for the rules and the parity status).
+// Literal sequential restatements over the flattened snapshot structs of include/orbfe.h:
+//   Frame::AssignFeaturesToGrid / PosInGrid  Frame.cc:385-416, 725-735   -> Grid
+//   Frame::GetFeaturesInArea                 Frame.cc:657-723            -> Grid::area()
+//   ORBmatcher::SearchByProjection (local)   ORBmatcher.cc:43-213        -> oro_sbp_local()
+//   ORBmatcher::RadiusByViewingCos           ORBmatcher.cc:215-221
+//   ORBmatcher::SearchByBoW(KF, F)           ORBmatcher.cc:223-425       -> oro_search_by_bow()
+//   ORBmatcher::SearchForInitialization      ORBmatcher.cc:648-763       -> oro_search_for_init()
+//   ORBmatcher::SearchByProjection (frame)   ORBmatcher.cc:1676-1887     -> oro_sbp_lastframe()
+//   ORBmatcher::SearchByProjection (KF)      ORBmatcher.cc:1889-2010     -> oro_sbp_kf()
+//   ORBmatcher::ComputeThreeMaxima           ORBmatcher.cc:2012-2053     -> three_maxima()
+//   Frame::ComputeStereoFishEyeMatches kNN   Frame.cc:1126-1151          -> oro_stereo_knn_ratio()
+// Only the pinhole / rectified branches (F.Nleft == -1) are restated; the KannalaBrandt8
+// right-camera branches are out of scope.
+// ============================================================================================
+#include <climits>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <vector>
+
+#include "../include/orbfe.h"
+
+namespace oracle {
+int hamming(const uint8_t* a, const uint8_t* b);
+}
+
+namespace {
+
+const int TH_HIGH = 100, TH_LOW = 50, HISTO_LENGTH = 30;
+
+struct Grid {
+    const orbfe_frame* F;
+    float invw, invh;
+    std::vector<size_t> cell[ORBFE_GRID_COLS][ORBFE_GRID_ROWS];
+    explicit Grid(const orbfe_frame* f) : F(f) {
+        invw = static_cast<float>(ORBFE_GRID_COLS) / (F->max_x - F->min_x);
+        invh = static_cast<float>(ORBFE_GRID_ROWS) / (F->max_y - F->min_y);
+        for (int i = 0; i < F->n; i++) {
+            const orbfe_keypoint& kp = F->keys[i];
+            int px = (int)std::round((kp.x - F->min_x) * invw);
+            int py = (int)std::round((kp.y - F->min_y) * invh);
+            if (px < 0 || px >= ORBFE_GRID_COLS || py < 0 || py >= ORBFE_GRID_ROWS) continue;
+            cell[px][py].push_back(i);
+        }
+    }
+    std::vector<size_t> area(float x, float y, float r, int minLevel, int maxLevel) const {
+        std::vector<size_t> v;
+        const float fx = r, fy = r;
+        const int nMinCellX = std::max(0, (int)std::floor((x - F->min_x - fx) * invw));
+        if (nMinCellX >= ORBFE_GRID_COLS) return v;
+        const int nMaxCellX = std::min(ORBFE_GRID_COLS - 1, (int)std::ceil((x - F->min_x + fx) * invw));
+        if (nMaxCellX < 0) return v;
+        const int nMinCellY = std::max(0, (int)std::floor((y - F->min_y - fy) * invh));
+        if (nMinCellY >= ORBFE_GRID_ROWS) return v;
+        const int nMaxCellY = std::min(ORBFE_GRID_ROWS - 1, (int)std::ceil((y - F->min_y + fy) * invh));
+        if (nMaxCellY < 0) return v;
+        const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+        for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
+            for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+                const std::vector<size_t>& c = cell[ix][iy];
+                for (size_t j = 0; j < c.size(); j++) {
+                    const orbfe_keypoint& kp = F->keys[c[j]];
+                    if (bCheckLevels) {
+                        if (kp.octave < minLevel) continue;
+                        if (maxLevel >= 0 && kp.octave > maxLevel) continue;
+                    }
+                    const float distx = kp.x - x, disty = kp.y - y;
+                    if (std::fabs(distx) < fx && std::fabs(disty) < fy) v.push_back(c[j]);
+                }
+            }
+        return v;
+    }
+};
+
+void three_maxima(const std::vector<int>* histo, int L, int& ind1, int& ind2, int& ind3) {
+    int max1 = 0, max2 = 0, max3 = 0;
+    for (int i = 0; i < L; i++) {
+        const int s = (int)histo[i].size();
+        if (s > max1) {
+            max3 = max2; max2 = max1; max1 = s;
+            ind3 = ind2; ind2 = ind1; ind1 = i;
+        } else if (s > max2) {
+            max3 = max2; max2 = s;
+            ind3 = ind2; ind2 = i;
+        } else if (s > max3) {
+            max3 = s; ind3 = i;
+        }
+    }
+    if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+    else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+}
+
+int rot_bin(float a1, float a2) {
+    const float factor = 1.0f / HISTO_LENGTH;
+    float rot = a1 - a2;
+    if (rot < 0.0) rot += 360.0f;
+    int bin = (int)std::round(rot * factor);
+    if (bin == HISTO_LENGTH) bin = 0;
+    return bin;
+}
+
+float radius_by_viewing_cos(const float& viewCos) { return viewCos > 0.998 ? 2.5f : 4.0f; }
+
+}  // namespace
+
+extern "C" {
+
+int oro_sbp_local(const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs_in, const orbfe_map_point* mps,
+                  int32_t n_mps, float th, int32_t bFarPoints, float thFarPoints, float nnratio) {
+    Grid grid(F);
+    std::vector<int32_t> obs(mvp_obs_in, mvp_obs_in + F->n);
+    int nmatches = 0;
+    const bool bFactor = th != 1.0;
+    for (int iMP = 0; iMP < n_mps; iMP++) {
+        const orbfe_map_point& mp = mps[iMP];
+        if (!(mp.flags & ORBFE_MP_IN_VIEW)) continue;
+        if (bFarPoints && mp.depth > thFarPoints) continue;
+        if (mp.flags & ORBFE_MP_BAD) continue;
+        const int nPredictedLevel = mp.scale_level;
+        float r = radius_by_viewing_cos(mp.view_cos);
+        if (bFactor) r *= th;
+        const std::vector<size_t> vIndices =
+            grid.area(mp.proj_x, mp.proj_y, r * F->scale_factors[nPredictedLevel], nPredictedLevel - 1, nPredictedLevel);
+        if (vIndices.empty()) continue;
+        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+        for (size_t idx : vIndices) {
+            if (mvp[idx] >= 0 && obs[idx] > 0) continue;
+            if (F->uright && F->uright[idx] > 0) {
+                const float er = std::fabs(mp.proj_xr - F->uright[idx]);
+                if (er > r * F->scale_factors[nPredictedLevel]) continue;
+            }
+            const int dist = oracle::hamming(mp.desc, F->desc + idx * 32);
+            if (dist < bestDist) {
+                bestDist2 = bestDist; bestDist = dist;
+                bestLevel2 = bestLevel; bestLevel = F->keys[idx].octave;
+                bestIdx = (int)idx;
+            } else if (dist < bestDist2) {
+                bestLevel2 = F->keys[idx].octave;
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= TH_HIGH) {
+            if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
+            if (bestLevel != bestLevel2 || bestDist <= nnratio * bestDist2) {
+                mvp[bestIdx] = mp.id;
+                obs[bestIdx] = mp.observations;
+                nmatches++;
+            }
+        }
+    }
+    return nmatches;
+}
+
+int oro_sbp_lastframe(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_obs_in, const orbfe_proj_point* pts,
+                      int32_t n_pts, float th, int32_t bForward, int32_t bBackward, int32_t checkOri) {
+    Grid grid(cur);
+    std::vector<int32_t> obs(mvp_obs_in, mvp_obs_in + cur->n);
+    std::vector<int> rotHist[HISTO_LENGTH];
+    int nmatches = 0;
+    for (int i = 0; i < n_pts; i++) {
+        const orbfe_proj_point& p = pts[i];
+        if (!p.valid) continue;
+        if (p.invzc < 0) continue;
+        if (p.u < cur->min_x || p.u > cur->max_x) continue;
+        if (p.v < cur->min_y || p.v > cur->max_y) continue;
+        const int nLastOctave = p.octave;
+        const float radius = th * cur->scale_factors[nLastOctave];
+        std::vector<size_t> v2;
+        if (bForward) v2 = grid.area(p.u, p.v, radius, nLastOctave, -1);
+        else if (bBackward) v2 = grid.area(p.u, p.v, radius, 0, nLastOctave);
+        else v2 = grid.area(p.u, p.v, radius, nLastOctave - 1, nLastOctave + 1);
+        if (v2.empty()) continue;
+        int bestDist = 256, bestIdx2 = -1;
+        for (size_t i2 : v2) {
+            if (mvp[i2] >= 0 && obs[i2] > 0) continue;
+            if (cur->uright && cur->uright[i2] > 0) {
+                const float ur = p.u - cur->mbf * p.invzc;
+                const float er = std::fabs(ur - cur->uright[i2]);
+                if (er > radius) continue;
+            }
+            const int dist = oracle::hamming(p.desc, cur->desc + i2 * 32);
+            if (dist < bestDist) { bestDist = dist; bestIdx2 = (int)i2; }
+        }
+        if (bestDist <= TH_HIGH) {
+            mvp[bestIdx2] = p.id;
+            obs[bestIdx2] = p.observations;
+            nmatches++;
+            if (checkOri) rotHist[rot_bin(p.angle, cur->keys[bestIdx2].angle)].push_back(bestIdx2);
+        }
+    }
+    if (checkOri) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        three_maxima(rotHist, HISTO_LENGTH, ind1, ind2, ind3);
+        for (int i = 0; i < HISTO_LENGTH; i++)
+            if (i != ind1 && i != ind2 && i != ind3)
+                for (int k : rotHist[i]) { mvp[k] = -1; nmatches--; }
+    }
+    return nmatches;
+}
+
+int oro_sbp_kf(const orbfe_frame* cur, int32_t* mvp, const orbfe_proj_point* pts, int32_t n_pts, float th,
+               int32_t ORBdist, int32_t checkOri) {
+    Grid grid(cur);
+    std::vector<int> rotHist[HISTO_LENGTH];
+    int nmatches = 0;
+    for (int i = 0; i < n_pts; i++) {
+        const orbfe_proj_point& p = pts[i];
+        if (!p.valid) continue;
+        const int nPredictedLevel = p.octave;
+        const float radius = th * cur->scale_factors[nPredictedLevel];
+        const std::vector<size_t> v2 = grid.area(p.u, p.v, radius, nPredictedLevel - 1, nPredictedLevel + 1);
+        if (v2.empty()) continue;
+        int bestDist = 256, bestIdx2 = -1;
+        for (size_t i2 : v2) {
+            if (mvp[i2] >= 0) continue;
+            const int dist = oracle::hamming(p.desc, cur->desc + i2 * 32);
+            if (dist < bestDist) { bestDist = dist; bestIdx2 = (int)i2; }
+        }
+        if (bestDist <= ORBdist) {
+            mvp[bestIdx2] = p.id;
+            nmatches++;
+            if (checkOri) rotHist[rot_bin(p.angle, cur->keys[bestIdx2].angle)].push_back(bestIdx2);
+        }
+    }
+    if (checkOri) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        three_maxima(rotHist, HISTO_LENGTH, ind1, ind2, ind3);
+        for (int i = 0; i < HISTO_LENGTH; i++)
+            if (i != ind1 && i != ind2 && i != ind3)
+                for (int k : rotHist[i]) { mvp[k] = -1; nmatches--; }
+    }
+    return nmatches;
+}
+
+int oro_search_for_init(const orbfe_frame* F1, const orbfe_frame* F2, float* prev, int32_t* m12, int32_t windowSize,
+                        float nnratio, int32_t checkOri) {
+    Grid grid2(F2);
+    int nmatches = 0;
+    for (int i = 0; i < F1->n; i++) m12[i] = -1;
+    std::vector<int> rotHist[HISTO_LENGTH];
+    std::vector<int> vMatchedDistance(F2->n, INT_MAX), vnMatches21(F2->n, -1);
+    for (int i1 = 0; i1 < F1->n; i1++) {
+        const orbfe_keypoint& kp1 = F1->keys[i1];
+        const int level1 = kp1.octave;
+        if (level1 > 0) continue;
+        const std::vector<size_t> v2 = grid2.area(prev[2 * i1], prev[2 * i1 + 1], (float)windowSize, level1, level1);
+        if (v2.empty()) continue;
+        int bestDist = INT_MAX, bestDist2 = INT_MAX, bestIdx2 = -1;
+        for (size_t i2 : v2) {
+            const int dist = oracle::hamming(F1->desc + (size_t)i1 * 32, F2->desc + i2 * 32);
+            if (vMatchedDistance[i2] <= dist) continue;
+            if (dist < bestDist) { bestDist2 = bestDist; bestDist = dist; bestIdx2 = (int)i2; }
+            else if (dist < bestDist2) bestDist2 = dist;
+        }
+        if (bestDist <= TH_LOW) {
+            if (bestDist < (float)bestDist2 * nnratio) {
+                if (vnMatches21[bestIdx2] >= 0) { m12[vnMatches21[bestIdx2]] = -1; nmatches--; }
+                m12[i1] = bestIdx2;
+                vnMatches21[bestIdx2] = i1;
+                vMatchedDistance[bestIdx2] = bestDist;
+                nmatches++;
+                if (checkOri) rotHist[rot_bin(F1->keys[i1].angle, F2->keys[bestIdx2].angle)].push_back(i1);
+            }
+        }
+    }
+    if (checkOri) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        three_maxima(rotHist, HISTO_LENGTH, ind1, ind2, ind3);
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            if (i == ind1 || i == ind2 || i == ind3) continue;
+            for (int idx1 : rotHist[i])
+                if (m12[idx1] >= 0) { m12[idx1] = -1; nmatches--; }
+        }
+    }
+    for (int i1 = 0; i1 < F1->n; i1++)
+        if (m12[i1] >= 0) { prev[2 * i1] = F2->keys[m12[i1]].x; prev[2 * i1 + 1] = F2->keys[m12[i1]].y; }
+    return nmatches;
+}
+
+int oro_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, const int32_t* kf_mp, int32_t kf_n,
+                      const orbfe_feature_vector* kfv, const orbfe_frame* F, const orbfe_feature_vector* ffv,
+                      int32_t* out, float nnratio, int32_t checkOri) {
+    (void)kf_n;
+    for (int i = 0; i < F->n; i++) out[i] = -1;
+    std::vector<int> rotHist[HISTO_LENGTH];
+    int nmatches = 0;
+    // std::map iteration with lower_bound jumps == ordered merge-join on equal node ids
+    int a = 0, b = 0;
+    while (a < kfv->n_nodes && b < ffv->n_nodes) {
+        if (kfv->node_ids[a] == ffv->node_ids[b]) {
+            for (int ia = kfv->offsets[a]; ia < kfv->offsets[a + 1]; ia++) {
+                const unsigned realIdxKF = kfv->indices[ia];
+                const int mp = kf_mp[realIdxKF];
+                if (mp < 0) continue;
+                const uint8_t* dKF = kf_desc + (size_t)realIdxKF * 32;
+                int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
+                for (int ib = ffv->offsets[b]; ib < ffv->offsets[b + 1]; ib++) {
+                    const unsigned realIdxF = ffv->indices[ib];
+                    if (out[realIdxF] >= 0) continue;
+                    const int dist = oracle::hamming(dKF, F->desc + (size_t)realIdxF * 32);
+                    if (dist < bestDist1) { bestDist2 = bestDist1; bestDist1 = dist; bestIdxF = (int)realIdxF; }
+                    else if (dist < bestDist2) bestDist2 = dist;
+                }
+                if (bestDist1 <= TH_LOW) {
+                    if (static_cast<float>(bestDist1) < nnratio * static_cast<float>(bestDist2)) {
+                        out[bestIdxF] = mp;
+                        if (checkOri) rotHist[rot_bin(kf_keys[realIdxKF].angle, F->keys[bestIdxF].angle)].push_back(bestIdxF);
+                        nmatches++;
+                    }
+                }
+            }
+            a++;
+            b++;
+        } else if (kfv->node_ids[a] < ffv->node_ids[b]) {
+            while (a < kfv->n_nodes && kfv->node_ids[a] < ffv->node_ids[b]) a++;
+        } else {
+            while (b < ffv->n_nodes && ffv->node_ids[b] < kfv->node_ids[a]) b++;
+        }
+    }
+    if (checkOri) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        three_maxima(rotHist, HISTO_LENGTH, ind1, ind2, ind3);
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            if (i == ind1 || i == ind2 || i == ind3) continue;
+            for (int k : rotHist[i]) { out[k] = -1; nmatches--; }
+        }
+    }
+    return nmatches;
+}
+
+// BFMatcher(NORM_HAMMING).knnMatch(k=2): per query the two smallest distances, earlier train index
+// first on ties; accept when (float)d0 < (double)d1 * ratio (Frame.cc:1151 multiplies by 0.7).
+int oro_stereo_knn_ratio(const uint8_t* L, int32_t nl, const uint8_t* R, int32_t nr, float ratio, int32_t* out_train,
+                         int32_t* out_dist) {
+    int good = 0;
+    for (int i = 0; i < nl; i++) {
+        int d0 = INT_MAX, d1 = INT_MAX, t0 = -1;
+        for (int j = 0; j < nr; j++) {
+            const int d = oracle::hamming(L + (size_t)i * 32, R + (size_t)j * 32);
+            if (d < d0) { d1 = d0; d0 = d; t0 = j; }
+            else if (d < d1) d1 = d;
+        }
+        out_train[i] = -1;
+        out_dist[i] = -1;
+        if (nr >= 2 && (float)d0 < (float)d1 * (double)ratio) { out_train[i] = t0; out_dist[i] = d0; good++; }
+    }
+    return good;
+}
+
+}  // extern "C"

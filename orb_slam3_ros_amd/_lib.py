@@ -51,6 +51,12 @@ _SIGS = {
     "orbfe_debug_copy": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _c_int]),
     "orbfe_debug_block_sort": (_c_int, [_vp, _c_int]),
     "orbfe_version": (ctypes.c_char_p, []),
+    "orbfe_search_by_projection_local": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _c_float, _c_int, _c_float, _c_float]),
+    "orbfe_search_by_projection_lastframe": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _c_float, _c_int, _c_int, _c_int]),
+    "orbfe_search_by_projection_kf": (_c_int, [_vp, _vp, _vp, _c_int, _c_float, _c_int, _c_int]),
+    "orbfe_search_for_initialization": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _c_float, _c_int]),
+    "orbfe_search_by_bow": (_c_int, [_vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_float, _c_int]),
+    "orbfe_stereo_knn_ratio": (_c_int, [_vp, _c_int, _vp, _c_int, _c_float, _vp, _vp]),
 }
 
 _lib = None

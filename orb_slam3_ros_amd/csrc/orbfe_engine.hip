@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <cstddef>
 #include <mutex>
 #include <vector>
 
@@ -650,3 +651,6 @@ int orbfe_descriptor_distance(const uint8_t* a, const uint8_t* b) {
 }
 
 }  // extern "C"
+
+// ORBmatcher methods (kernels + host wrappers; uses HIPCHK above).
+#include "orbfe_matcher.hip"

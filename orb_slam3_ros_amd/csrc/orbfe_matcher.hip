@@ -1,0 +1,879 @@
+// ORBmatcher Tracking-thread methods on CDNA4 (included into orbfe_engine.hip's translation unit).
+//
+// The reference processes its queries strictly in order and later queries see earlier
+// assignments (a keypoint taken by a point with Observations() > 0 is skipped, a keypoint
+// "stolen" in SearchForInitialization, ...). Every such dependency is TRIANGULAR: query q only
+// reads state written by queries j < q. The kernels therefore evaluate all queries in parallel
+// against the state implied by the current assignment vector, recompute that state, and repeat
+// until no assignment changes. After iteration t the first t queries are exactly the sequential
+// result, so the loop reaches the reference's answer (in practice in 2-4 passes); no iteration
+// cap below n_queries + 1 is needed for correctness.
+//
+// Each query scans its candidates in Frame::GetFeaturesInArea order (cell ix outer, iy inner,
+// keypoint index inside a cell: the grid is rebuilt with a stable (cell, index) sort), so the
+// reference's strict-< "first best wins" and best/second-best bookkeeping are reproduced verbatim.
+#pragma once
+
+#define MT_NT 256
+#define MT_TH_HIGH 100
+#define MT_TH_LOW 50
+#define MT_HISTO 30
+#define MT_NCELL (ORBFE_GRID_COLS * ORBFE_GRID_ROWS)
+#define MT_INF 0x7fffffff
+
+struct FrameDev {
+    int n;
+    const OrbKeyPoint* keys;
+    const uint32_t* desc;   // n x 8 words
+    const float* uright;    // may be null
+    float minx, maxx, miny, maxy, invw, invh, mbf;
+    const float* scale;
+    const int* cstart;      // MT_NCELL + 1 offsets, cell = ix * ORBFE_GRID_ROWS + iy
+    const int* cidx;        // keypoint indices sorted by (cell, index)
+};
+
+__device__ __forceinline__ int mt_hamming(const uint8_t* a, const uint32_t* b) {
+    uint32_t w[8];
+    memcpy(w, a, 32);
+    int d = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) d += __popc(w[i] ^ b[i]);
+    return d;
+}
+
+// Frame::GetFeaturesInArea (Frame.cc:657-723), calling f(idx) in the reference's order.
+template <typename Fn>
+__device__ __forceinline__ void mt_for_area(const FrameDev& fr, float x, float y, float r, int minLevel, int maxLevel,
+                                            Fn&& f) {
+    const int nMinCellX = max(0, (int)floorf((x - fr.minx - r) * fr.invw));
+    if (nMinCellX >= ORBFE_GRID_COLS) return;
+    const int nMaxCellX = min(ORBFE_GRID_COLS - 1, (int)ceilf((x - fr.minx + r) * fr.invw));
+    if (nMaxCellX < 0) return;
+    const int nMinCellY = max(0, (int)floorf((y - fr.miny - r) * fr.invh));
+    if (nMinCellY >= ORBFE_GRID_ROWS) return;
+    const int nMaxCellY = min(ORBFE_GRID_ROWS - 1, (int)ceilf((y - fr.miny + r) * fr.invh));
+    if (nMaxCellY < 0) return;
+    const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+    for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
+        for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+            const int c = ix * ORBFE_GRID_ROWS + iy;
+            for (int j = fr.cstart[c]; j < fr.cstart[c + 1]; j++) {
+                const int idx = fr.cidx[j];
+                const OrbKeyPoint kp = fr.keys[idx];
+                if (bCheckLevels) {
+                    if (kp.octave < minLevel) continue;
+                    if (maxLevel >= 0 && kp.octave > maxLevel) continue;
+                }
+                if (fabsf(kp.x - x) < r && fabsf(kp.y - y) < r) f(idx, kp);
+            }
+        }
+}
+
+// AssignFeaturesToGrid (Frame.cc:385-416): stable (cell, index) order via a bitonic sort of
+// (cell << 16 | index) keys in LDS. One block per frame, n <= MT_GRID_MAXN.
+#define MT_GRID_MAXN 8192
+__global__ __launch_bounds__(1024) void k_mt_grid(const OrbKeyPoint* keys, int n, float minx, float miny, float invw,
+                                                  float invh, int* cstart, int* cidx) {
+    __shared__ uint32_t s_k[MT_GRID_MAXN];
+    int P = 1;
+    while (P < n) P <<= 1;
+    for (int i = threadIdx.x; i < P; i += blockDim.x) {
+        uint32_t key = 0xFFFFFFFFu;
+        if (i < n) {
+            const OrbKeyPoint kp = keys[i];
+            const int px = (int)roundf((kp.x - minx) * invw);
+            const int py = (int)roundf((kp.y - miny) * invh);
+            uint32_t cell = MT_NCELL;   // outside the grid: never a candidate (PosInGrid false)
+            if (!(px < 0 || px >= ORBFE_GRID_COLS || py < 0 || py >= ORBFE_GRID_ROWS))
+                cell = (uint32_t)(px * ORBFE_GRID_ROWS + py);
+            key = (cell << 16) | (uint32_t)i;
+        }
+        s_k[i] = key;
+    }
+    SYNC();
+    for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < P; i += blockDim.x) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const uint32_t a = s_k[i], c = s_k[ixj];
+                    if ((a > c) == ((i & k) == 0)) { s_k[i] = c; s_k[ixj] = a; }
+                }
+            }
+            SYNC();
+        }
+    for (int i = threadIdx.x; i < n; i += blockDim.x) cidx[i] = (int)(s_k[i] & 0xFFFFu);
+    for (int c = threadIdx.x; c <= MT_NCELL; c += blockDim.x) {
+        int lo = 0, hi = n;   // first position with cell >= c
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if ((int)(s_k[mid] >> 16) < c) lo = mid + 1; else hi = mid;
+        }
+        cstart[c] = lo;
+    }
+}
+
+// first[k] = min query index j with assign[j] == k (and Observations_j > 0 when need_obs); the
+// observation count is read from the query records (byte stride) in place.
+__global__ void k_mt_first_strided(const int* assign, const uint8_t* qobs, int stride, int nq, int need_obs,
+                                   int* first) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nq) return;
+    const int a = assign[j];
+    if (a >= 0 && (!need_obs || *(const int*)(qobs + (size_t)j * stride) > 0)) atomicMin(&first[a], j);
+}
+__global__ void k_mt_fill(int* p, int n, int v) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+// ---- SearchByProjection(Frame&, vector<MapPoint*>, th, bFarPoints, thFar) (ORBmatcher.cc:43-213) ----
+__global__ __launch_bounds__(MT_NT) void k_sbp_local(FrameDev fr, const orbfe_map_point* mps, int nq, float th,
+                                                     int bFar, float thFar, float nnratio, const int* blocked0,
+                                                     const int* first, int* assign, int* changed) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    const orbfe_map_point& mp = mps[q];
+    int result = -1;
+    const bool bFactor = th != 1.0f;
+    if ((mp.flags & ORBFE_MP_IN_VIEW) && !(bFar && mp.depth > thFar) && !(mp.flags & ORBFE_MP_BAD)) {
+        const int lvl = mp.scale_level;
+        float r = mp.view_cos > 0.998 ? 2.5f : 4.0f;   // RadiusByViewingCos (ORBmatcher.cc:215-221)
+        if (bFactor) r *= th;
+        const float R = r * fr.scale[lvl];
+        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+        mt_for_area(fr, mp.proj_x, mp.proj_y, R, lvl - 1, lvl, [&](int idx, const OrbKeyPoint& kp) {
+            if (blocked0[idx] || first[idx] < q) return;
+            if (fr.uright && fr.uright[idx] > 0) {
+                const float er = fabsf(mp.proj_xr - fr.uright[idx]);
+                if (er > R) return;
+            }
+            const int dist = mt_hamming(mp.desc, fr.desc + 8 * idx);
+            if (dist < bestDist) {
+                bestDist2 = bestDist; bestDist = dist;
+                bestLevel2 = bestLevel; bestLevel = kp.octave;
+                bestIdx = idx;
+            } else if (dist < bestDist2) {
+                bestLevel2 = kp.octave;
+                bestDist2 = dist;
+            }
+        });
+        if (bestDist <= MT_TH_HIGH) {
+            if (!(bestLevel == bestLevel2 && bestDist > nnratio * bestDist2)) result = bestIdx;
+        }
+    }
+    if (result != assign[q]) {
+        assign[q] = result;
+        atomicAdd(changed, 1);
+    }
+}
+
+// ---- SearchByProjection(CurrentFrame, LastFrame, ...) (ORBmatcher.cc:1676-1887) and
+//      SearchByProjection(CurrentFrame, pKF, ...) (:1889-2010): single best, then rotation filter ----
+__global__ __launch_bounds__(MT_NT) void k_sbp_proj(FrameDev fr, const orbfe_proj_point* pts, int nq, float th,
+                                                    int mode /*0 lastframe, 1 kf*/, int bForward, int bBackward,
+                                                    int maxDist, const int* blocked0, const int* first, int* assign,
+                                                    int* changed) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    const orbfe_proj_point& p = pts[q];
+    int result = -1;
+    bool ok = p.valid != 0;
+    if (ok && mode == 0) {
+        if (p.invzc < 0) ok = false;
+        else if (p.u < fr.minx || p.u > fr.maxx) ok = false;
+        else if (p.v < fr.miny || p.v > fr.maxy) ok = false;
+    }
+    if (ok) {
+        const int oct = p.octave;
+        const float radius = th * fr.scale[oct];
+        int minL, maxL;
+        if (mode == 1) { minL = oct - 1; maxL = oct + 1; }
+        else if (bForward) { minL = oct; maxL = -1; }
+        else if (bBackward) { minL = 0; maxL = oct; }
+        else { minL = oct - 1; maxL = oct + 1; }
+        int bestDist = 256, bestIdx2 = -1;
+        mt_for_area(fr, p.u, p.v, radius, minL, maxL, [&](int i2, const OrbKeyPoint&) {
+            if (blocked0[i2] || first[i2] < q) return;
+            if (mode == 0 && fr.uright && fr.uright[i2] > 0) {
+                const float ur = p.u - fr.mbf * p.invzc;
+                const float er = fabsf(ur - fr.uright[i2]);
+                if (er > radius) return;
+            }
+            const int dist = mt_hamming(p.desc, fr.desc + 8 * i2);
+            if (dist < bestDist) { bestDist = dist; bestIdx2 = i2; }
+        });
+        if (bestDist <= maxDist) result = bestIdx2;
+    }
+    if (result != assign[q]) {
+        assign[q] = result;
+        atomicAdd(changed, 1);
+    }
+}
+
+// rotation-histogram bin of an accepted match (ORBmatcher.cc:1775-1792): round(rot * (1/30)).
+__device__ __forceinline__ int mt_rot_bin(float a1, float a2) {
+    const float factor = 1.0f / MT_HISTO;
+    float rot = a1 - a2;
+    if (rot < 0.0) rot += 360.0f;
+    int bin = (int)roundf(rot * factor);
+    if (bin == MT_HISTO) bin = 0;
+    return bin;
+}
+
+// ComputeThreeMaxima (ORBmatcher.cc:2012-2053) on 30 bin counts -> keep mask.
+__device__ __forceinline__ unsigned mt_three_maxima_keep(const int* hist) {
+    int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+    for (int i = 0; i < MT_HISTO; i++) {
+        const int s = hist[i];
+        if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+        else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+        else if (s > max3) { max3 = s; ind3 = i; }
+    }
+    if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+    else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+    unsigned keep = 0;
+    if (ind1 >= 0) keep |= 1u << ind1;
+    if (ind2 >= 0) keep |= 1u << ind2;
+    if (ind3 >= 0) keep |= 1u << ind3;
+    return keep;
+}
+
+// Final write-back for slot-assigning searches: slot k gets the LAST query that chose it; with
+// checkOri, every entry of a dropped bin clears its slot and decrements nmatches
+// (ORBmatcher.cc:1860-1884). q_angle: the query-side angle per query; frame angle from keys.
+__global__ __launch_bounds__(1024) void k_mt_commit_slots(const OrbKeyPoint* keys, int n, const int* assign,
+                                                          const int* qid, const float* q_angle, int q_stride_bytes,
+                                                          int nq, int checkOri, int* mvp, int* result) {
+    __shared__ int s_hist[MT_HISTO];
+    __shared__ unsigned s_keep;
+    __shared__ int s_n;
+    if (threadIdx.x < MT_HISTO) s_hist[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_n = 0;
+    SYNC();
+    int cnt = 0;
+    for (int j = threadIdx.x; j < nq; j += blockDim.x) {
+        const int a = assign[j];
+        if (a < 0) continue;
+        cnt++;
+        if (checkOri) {
+            const float qa = *(const float*)((const uint8_t*)q_angle + (size_t)j * q_stride_bytes);
+            atomicAdd(&s_hist[mt_rot_bin(qa, keys[a].angle)], 1);
+        }
+    }
+    atomicAdd(&s_n, cnt);
+    SYNC();
+    if (threadIdx.x == 0) s_keep = checkOri ? mt_three_maxima_keep(s_hist) : 0xFFFFFFFFu;
+    SYNC();
+    // last assigner per slot: sequential order = query index; the largest j wins
+    for (int j = threadIdx.x; j < nq; j += blockDim.x) {
+        const int a = assign[j];
+        if (a >= 0) atomicMax(&result[2 + a], j);
+    }
+    SYNC();
+    int dropped = 0;
+    for (int j = threadIdx.x; j < nq; j += blockDim.x) {
+        const int a = assign[j];
+        if (a < 0 || !checkOri) continue;
+        const float qa = *(const float*)((const uint8_t*)q_angle + (size_t)j * q_stride_bytes);
+        if (!((s_keep >> mt_rot_bin(qa, keys[a].angle)) & 1u)) {
+            dropped++;
+            result[2 + a] = -2;   // cleared slot marker (cannot race with a winner write: written after SYNC)
+        }
+    }
+    SYNC();
+    atomicAdd(&s_n, -dropped);
+    SYNC();
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        const int w = result[2 + k];
+        if (w == -2) mvp[k] = -1;
+        else if (w >= 0) mvp[k] = *(const int*)((const uint8_t*)qid + (size_t)w * q_stride_bytes);
+    }
+    if (threadIdx.x == 0) result[0] = s_n;
+}
+
+// ---- SearchForInitialization (ORBmatcher.cc:648-763) ----
+// State seen by query q for candidate i2: vMatchedDistance[i2] = min distance of the queries j < q
+// that selected i2 (a new selection must beat the stored distance, so the last selector holds the
+// minimum). The state table is rebuilt every pass: (i2 << 16 | j) keys sorted + segmented
+// prefix-min of the selecting distances.
+#define MT_INIT_MAXQ 8192
+__global__ __launch_bounds__(1024) void k_init_state(const int* assign, const int* adist, int nq, uint32_t* skey,
+                                                     int* spmin, int* nsel) {
+    __shared__ uint32_t s_k[MT_INIT_MAXQ];
+    __shared__ int s_cnt;
+    if (threadIdx.x == 0) s_cnt = 0;
+    SYNC();
+    for (int j = threadIdx.x; j < nq; j += blockDim.x)
+        if (assign[j] >= 0) s_k[atomicAdd(&s_cnt, 1)] = ((uint32_t)assign[j] << 16) | (uint32_t)j;
+    SYNC();
+    const int m = s_cnt;
+    int P = 1;
+    while (P < m) P <<= 1;
+    for (int i = m + threadIdx.x; i < P; i += blockDim.x) s_k[i] = 0xFFFFFFFFu;
+    SYNC();
+    for (int k = 2; k <= P; k <<= 1)
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+            for (int i = threadIdx.x; i < P; i += blockDim.x) {
+                const int ixj = i ^ jj;
+                if (ixj > i) {
+                    const uint32_t a = s_k[i], c = s_k[ixj];
+                    if ((a > c) == ((i & k) == 0)) { s_k[i] = c; s_k[ixj] = a; }
+                }
+            }
+            SYNC();
+        }
+    // segmented prefix-min of distances (segments = equal i2); sequential per segment start
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        skey[i] = s_k[i];
+        if (i == 0 || (s_k[i - 1] >> 16) != (s_k[i] >> 16)) {
+            int cur = MT_INF;
+            for (int t = i; t < m && (s_k[t] >> 16) == (s_k[i] >> 16); t++) {
+                cur = min(cur, adist[s_k[t] & 0xFFFFu]);
+                spmin[t] = cur;
+            }
+        }
+    }
+    if (threadIdx.x == 0) *nsel = m;
+}
+
+__global__ __launch_bounds__(MT_NT) void k_init_eval(FrameDev f1, FrameDev f2, const float* prev, int windowSize,
+                                                     float nnratio, const uint32_t* skey, const int* spmin,
+                                                     const int* nsel, int* assign, int* adist, int* changed) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= f1.n) return;
+    int result = -1, rdist = 0;
+    const int m = *nsel;
+    const OrbKeyPoint kp1 = f1.keys[q];
+    if (kp1.octave <= 0) {
+        const int level1 = kp1.octave;
+        uint8_t d1[32];
+        memcpy(d1, f1.desc + 8 * q, 32);
+        int bestDist = MT_INF, bestDist2 = MT_INF, bestIdx2 = -1;
+        mt_for_area(f2, prev[2 * q], prev[2 * q + 1], (float)windowSize, level1, level1, [&](int i2, const OrbKeyPoint&) {
+            const int dist = mt_hamming(d1, f2.desc + 8 * i2);
+            // vMatchedDistance[i2] as seen by query q: last selector j < q of i2
+            int lo = 0, hi = m;   // first key >= (i2 << 16 | q)
+            const uint32_t target = ((uint32_t)i2 << 16) | (uint32_t)q;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (skey[mid] < target) lo = mid + 1; else hi = mid;
+            }
+            int md = MT_INF;
+            if (lo > 0 && (skey[lo - 1] >> 16) == (uint32_t)i2) md = spmin[lo - 1];
+            if (md <= dist) return;
+            if (dist < bestDist) { bestDist2 = bestDist; bestDist = dist; bestIdx2 = i2; }
+            else if (dist < bestDist2) bestDist2 = dist;
+        });
+        if (bestDist <= MT_TH_LOW && bestDist < (float)bestDist2 * nnratio) { result = bestIdx2; rdist = bestDist; }
+    }
+    if (result != assign[q] || (result >= 0 && rdist != adist[q])) {
+        assign[q] = result;
+        adist[q] = rdist;
+        atomicAdd(changed, 1);
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_init_commit(FrameDev f1, FrameDev f2, const int* assign, int checkOri,
+                                                      float* prev, int* m12, int* result) {
+    __shared__ int s_hist[MT_HISTO];
+    __shared__ unsigned s_keep;
+    __shared__ int s_n;
+    __shared__ int s_owner[MT_INIT_MAXQ];
+    if (threadIdx.x < MT_HISTO) s_hist[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_n = 0;
+    for (int i = threadIdx.x; i < f2.n && i < MT_INIT_MAXQ; i += blockDim.x) s_owner[i] = -1;
+    SYNC();
+    for (int j = threadIdx.x; j < f1.n; j += blockDim.x) {
+        const int a = assign[j];
+        if (a < 0) continue;
+        atomicMax(&s_owner[a], j);   // the last selector keeps i2; earlier ones were stolen
+        if (checkOri) atomicAdd(&s_hist[mt_rot_bin(f1.keys[j].angle, f2.keys[a].angle)], 1);
+    }
+    SYNC();
+    if (threadIdx.x == 0) s_keep = checkOri ? mt_three_maxima_keep(s_hist) : 0xFFFFFFFFu;
+    SYNC();
+    int cnt = 0;
+    for (int j = threadIdx.x; j < f1.n; j += blockDim.x) {
+        const int a = assign[j];
+        int out = -1;
+        if (a >= 0 && s_owner[a] == j) {
+            out = a;
+            if (checkOri && !((s_keep >> mt_rot_bin(f1.keys[j].angle, f2.keys[a].angle)) & 1u)) out = -1;
+        }
+        m12[j] = out;
+        if (out >= 0) {
+            cnt++;
+            prev[2 * j] = f2.keys[out].x;
+            prev[2 * j + 1] = f2.keys[out].y;
+        }
+    }
+    atomicAdd(&s_n, cnt);
+    SYNC();
+    if (threadIdx.x == 0) result[0] = s_n;
+}
+
+// ---- SearchByBoW(KF, F) (ORBmatcher.cc:223-425): one thread per node present in both vectors.
+// Every frame index belongs to exactly one vocabulary node, so the "already matched" skip is local
+// to the node and the node walks are independent (the reference's order inside a node is kept).
+__global__ __launch_bounds__(MT_NT) void k_bow_nodes(const int* pairs, int npairs, const int* kf_off,
+                                                     const uint32_t* kf_idx, const int* f_off, const uint32_t* f_idx,
+                                                     const int32_t* kf_mp, const uint32_t* kf_desc,
+                                                     const uint32_t* f_desc, float nnratio, int* out_src) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= npairs) return;
+    const int a = pairs[2 * t], b = pairs[2 * t + 1];
+    for (int ia = kf_off[a]; ia < kf_off[a + 1]; ia++) {
+        const unsigned realIdxKF = kf_idx[ia];
+        if (kf_mp[realIdxKF] < 0) continue;
+        uint32_t dk[8];
+#pragma unroll
+        for (int w = 0; w < 8; w++) dk[w] = kf_desc[8 * realIdxKF + w];
+        int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
+        for (int ib = f_off[b]; ib < f_off[b + 1]; ib++) {
+            const unsigned realIdxF = f_idx[ib];
+            if (out_src[realIdxF] >= 0) continue;
+            int dist = 0;
+#pragma unroll
+            for (int w = 0; w < 8; w++) dist += __popc(dk[w] ^ f_desc[8 * realIdxF + w]);
+            if (dist < bestDist1) { bestDist2 = bestDist1; bestDist1 = dist; bestIdxF = (int)realIdxF; }
+            else if (dist < bestDist2) bestDist2 = dist;
+        }
+        if (bestDist1 <= MT_TH_LOW && static_cast<float>(bestDist1) < nnratio * static_cast<float>(bestDist2))
+            out_src[bestIdxF] = (int)realIdxKF;
+    }
+}
+__global__ __launch_bounds__(1024) void k_bow_commit(const OrbKeyPoint* kf_keys, const OrbKeyPoint* f_keys, int fn,
+                                                     const int32_t* kf_mp, int checkOri, const int* out_src,
+                                                     int* out, int* result) {
+    __shared__ int s_hist[MT_HISTO];
+    __shared__ unsigned s_keep;
+    __shared__ int s_n;
+    if (threadIdx.x < MT_HISTO) s_hist[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_n = 0;
+    SYNC();
+    for (int i = threadIdx.x; i < fn; i += blockDim.x) {
+        const int s = out_src[i];
+        if (s >= 0 && checkOri) atomicAdd(&s_hist[mt_rot_bin(kf_keys[s].angle, f_keys[i].angle)], 1);
+    }
+    SYNC();
+    if (threadIdx.x == 0) s_keep = checkOri ? mt_three_maxima_keep(s_hist) : 0xFFFFFFFFu;
+    SYNC();
+    int cnt = 0;
+    for (int i = threadIdx.x; i < fn; i += blockDim.x) {
+        const int s = out_src[i];
+        int o = -1;
+        if (s >= 0 && (!checkOri || ((s_keep >> mt_rot_bin(kf_keys[s].angle, f_keys[i].angle)) & 1u))) o = kf_mp[s];
+        out[i] = o;
+        cnt += o >= 0 ? 1 : 0;
+    }
+    atomicAdd(&s_n, cnt);
+    SYNC();
+    if (threadIdx.x == 0) result[0] = s_n;
+}
+
+// ---- ComputeStereoFishEyeMatches' knnMatch(k=2) + ratio (Frame.cc:1144-1151) ----
+__global__ __launch_bounds__(MT_NT) void k_knn2(const uint32_t* L, int nl, const uint32_t* R, int nr, float ratio,
+                                                int* out_train, int* out_dist) {
+    __shared__ uint32_t s_r[MT_NT * 8];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t d[8];
+#pragma unroll
+    for (int w = 0; w < 8; w++) d[w] = i < nl ? L[8 * i + w] : 0u;
+    int d0 = MT_INF, d1 = MT_INF, t0 = -1;
+    for (int base = 0; base < nr; base += MT_NT) {
+        SYNC();
+        for (int k = threadIdx.x; k < MT_NT * 8; k += blockDim.x) s_r[k] = (base * 8 + k < nr * 8) ? R[base * 8 + k] : 0u;
+        SYNC();
+        const int lim = min(MT_NT, nr - base);
+        for (int jj = 0; jj < lim; jj++) {
+            int dist = 0;
+#pragma unroll
+            for (int w = 0; w < 8; w++) dist += __popc(d[w] ^ s_r[8 * jj + w]);
+            if (dist < d0) { d1 = d0; d0 = dist; t0 = base + jj; }
+            else if (dist < d1) d1 = dist;
+        }
+    }
+    if (i < nl) {
+        const bool ok = nr >= 2 && (float)d0 < (float)d1 * (double)ratio;
+        out_train[i] = ok ? t0 : -1;
+        out_dist[i] = ok ? d0 : -1;
+    }
+}
+
+// =============================================================================================
+// Host side (compiled in the engine TU after HIPCHK is defined).
+// Every call is synchronous from the caller's point of view (the reference methods return
+// nmatches), stateless and re-entrant: each calling thread owns a device arena, a pinned staging
+// buffer and a non-blocking stream (Tracking, LocalMapping and LoopClosing call the matcher
+// concurrently in the reference). All host inputs are packed into the pinned buffer and uploaded
+// with ONE copy; results come back with one copy per output array.
+// =============================================================================================
+namespace {
+
+struct MatchScratch {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    uint8_t* d = nullptr;
+    size_t dcap = 0;
+    uint8_t* h = nullptr;   // pinned
+    size_t hcap = 0;
+    // Deliberately never freed: thread_local destructors of the main thread can run after the HIP
+    // runtime has been torn down at exit; the arena is reused for the thread's lifetime.
+};
+thread_local MatchScratch t_ms;
+
+struct Plan {
+    struct Up { const void* src; size_t bytes; size_t off; };
+    std::vector<Up> ups;
+    size_t up_end = 0, end = 0;
+    static size_t a256(size_t b) { return (b + 255) & ~(size_t)255; }
+    size_t upload(const void* src, size_t bytes) {   // all uploads must be planned before scratch
+        const size_t o = end;
+        ups.push_back(Up{src, bytes, o});
+        end += a256(bytes);
+        up_end = end;
+        return o;
+    }
+    size_t scratch(size_t bytes) { const size_t o = end; end += a256(bytes); return o; }
+};
+
+int ms_prepare(const Plan& p) {
+    MatchScratch& m = t_ms;
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    if (m.device != dev) {   // new thread or device switch: fresh resources on this device
+        m = MatchScratch();
+        m.device = dev;
+        HIPCHK(hipStreamCreateWithFlags(&m.stream, hipStreamNonBlocking));
+    }
+    if (p.end > m.dcap) {
+        if (m.d) HIPCHK(hipFree(m.d));
+        m.d = nullptr;
+        const size_t cap = std::max<size_t>(p.end + p.end / 2, 1 << 20);
+        HIPCHK(hipMalloc(&m.d, cap));
+        m.dcap = cap;
+    }
+    if (p.up_end > m.hcap) {
+        if (m.h) HIPCHK(hipHostFree(m.h));
+        m.h = nullptr;
+        const size_t cap = std::max<size_t>(p.up_end + p.up_end / 2, 1 << 20);
+        HIPCHK(hipHostMalloc((void**)&m.h, cap, hipHostMallocDefault));
+        m.hcap = cap;
+    }
+    for (const auto& u : p.ups)
+        if (u.bytes) memcpy(m.h + u.off, u.src, u.bytes);
+    if (p.up_end) HIPCHK(hipMemcpyAsync(m.d, m.h, p.up_end, hipMemcpyHostToDevice, m.stream));
+    return ORBFE_OK;
+}
+
+template <typename T> T* ms_ptr(size_t off) { return reinterpret_cast<T*>(t_ms.d + off); }
+
+// Upload a frame and plan its grid; returns the device view after ms_prepare (fill_frame).
+struct FramePlan {
+    const orbfe_frame* F;
+    size_t keys, desc, uright, scale, cstart, cidx;
+    bool has_uright;
+    void plan(Plan& p, const orbfe_frame* f, bool want_grid, bool want_uright) {
+        F = f;
+        keys = p.upload(f->keys, (size_t)f->n * sizeof(orbfe_keypoint));
+        desc = p.upload(f->desc, (size_t)f->n * 32);
+        has_uright = want_uright && f->uright != nullptr;
+        uright = has_uright ? p.upload(f->uright, (size_t)f->n * 4) : 0;
+        scale = p.upload(f->scale_factors, (size_t)f->nlevels * 4);
+        (void)want_grid;
+    }
+    void plan_grid(Plan& p) {
+        cstart = p.scratch((MT_NCELL + 1) * 4);
+        cidx = p.scratch((size_t)std::max(F->n, 1) * 4);
+    }
+    FrameDev view() const {
+        FrameDev v;
+        v.n = F->n;
+        v.keys = ms_ptr<const OrbKeyPoint>(keys);
+        v.desc = ms_ptr<const uint32_t>(desc);
+        v.uright = has_uright ? ms_ptr<const float>(uright) : nullptr;
+        v.minx = F->min_x; v.maxx = F->max_x; v.miny = F->min_y; v.maxy = F->max_y;
+        // mfGridElementWidthInv / HeightInv (Frame.cc:163-164)
+        v.invw = static_cast<float>(ORBFE_GRID_COLS) / (F->max_x - F->min_x);
+        v.invh = static_cast<float>(ORBFE_GRID_ROWS) / (F->max_y - F->min_y);
+        v.mbf = F->mbf;
+        v.scale = ms_ptr<const float>(scale);
+        v.cstart = ms_ptr<const int>(cstart);
+        v.cidx = ms_ptr<const int>(cidx);
+        return v;
+    }
+    void launch_grid(const FrameDev& v) const {
+        hipLaunchKernelGGL(k_mt_grid, dim3(1), dim3(1024), 0, t_ms.stream, v.keys, v.n, v.minx, v.miny, v.invw,
+                           v.invh, (int*)v.cstart, (int*)v.cidx);
+    }
+};
+
+bool frame_ok(const orbfe_frame* f) {
+    return f && f->n >= 0 && f->n <= MT_GRID_MAXN && (f->n == 0 || (f->keys && f->desc)) && f->scale_factors &&
+           f->nlevels > 0;
+}
+
+inline void fill(int* p, int n, int v) {
+    if (n > 0) hipLaunchKernelGGL(k_mt_fill, dim3((n + 255) / 256), dim3(256), 0, t_ms.stream, p, n, v);
+}
+
+#define MT_MAX_PASSES 4096
+
+// Shared driver of the three slot-assigning SearchByProjection variants.
+// mode: 0 local map, 1 last frame, 2 keyframe.
+int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, const void* queries, int nq,
+            size_t qstride, size_t qobs_off, size_t qid_off, size_t qangle_off, size_t qlevel_off, float th, int a0, int a1, float thFar,
+            float nnratio, int maxDist, int checkOri) {
+    if (!frame_ok(F) || !mvp || nq < 0 || (nq > 0 && !queries)) return ORBFE_E_ARG;
+    if (mode != 2 && !mvp_obs) return ORBFE_E_ARG;
+    if (F->n == 0 || nq == 0) return 0;
+    if (nq > (1 << 24)) return ORBFE_E_CAPACITY;
+    const int n = F->n;
+    // level indices address mvScaleFactors: reject out-of-range ones instead of reading past it
+    for (int j = 0; j < nq; j++) {
+        const uint8_t* rec = (const uint8_t*)queries + (size_t)j * qstride;
+        const bool used = mode == 0 ? (((const orbfe_map_point*)rec)->flags & ORBFE_MP_IN_VIEW) != 0
+                                    : ((const orbfe_proj_point*)rec)->valid != 0;
+        const int lvl = *(const int32_t*)(rec + qlevel_off);
+        if (used && (lvl < 0 || lvl >= F->nlevels)) return ORBFE_E_ARG;
+    }
+    std::vector<int32_t> blocked0(n);
+    for (int k = 0; k < n; k++) blocked0[k] = mode == 2 ? (mvp[k] >= 0) : (mvp[k] >= 0 && mvp_obs[k] > 0);
+    Plan p;
+    FramePlan fp;
+    fp.plan(p, F, true, mode != 2);
+    const size_t o_q = p.upload(queries, (size_t)nq * qstride);
+    const size_t o_b0 = p.upload(blocked0.data(), (size_t)n * 4);
+    const size_t o_mvp = p.upload(mvp, (size_t)n * 4);
+    fp.plan_grid(p);
+    const size_t o_first = p.scratch((size_t)n * 4);
+    const size_t o_assign = p.scratch((size_t)nq * 4);
+    const size_t o_changed = p.scratch(MT_MAX_PASSES * 4);
+    const size_t o_result = p.scratch((size_t)(n + 2) * 4);
+    int rc = ms_prepare(p);
+    if (rc) return rc;
+    hipStream_t s = t_ms.stream;
+    const FrameDev fr = fp.view();
+    fp.launch_grid(fr);
+    int* first = ms_ptr<int>(o_first);
+    int* assign = ms_ptr<int>(o_assign);
+    int* changed = ms_ptr<int>(o_changed);
+    HIPCHK(hipMemsetAsync(changed, 0, MT_MAX_PASSES * 4, s));
+    fill(assign, nq, -1);
+    const uint8_t* q = ms_ptr<const uint8_t>(o_q);
+    const dim3 gq((nq + MT_NT - 1) / MT_NT);
+    int pass = 0;
+    const int chunk = 2;   // passes launched between host checks (most searches converge in 2-3)
+    while (true) {
+        for (int c = 0; c < chunk; c++, pass++) {
+            if (pass >= MT_MAX_PASSES) return ORBFE_E_CAPACITY;
+            fill(first, n, MT_INF);
+            hipLaunchKernelGGL(k_mt_first_strided, gq, dim3(MT_NT), 0, s, assign, q + qobs_off, (int)qstride, nq,
+                               mode == 2 ? 0 : 1, first);
+            if (mode == 0)
+                hipLaunchKernelGGL(k_sbp_local, gq, dim3(MT_NT), 0, s, fr, (const orbfe_map_point*)q, nq, th, a0, thFar,
+                                   nnratio, ms_ptr<const int>(o_b0), first, assign, changed + pass);
+            else
+                hipLaunchKernelGGL(k_sbp_proj, gq, dim3(MT_NT), 0, s, fr, (const orbfe_proj_point*)q, nq, th,
+                                   mode == 1 ? 0 : 1, a0, a1, maxDist, ms_ptr<const int>(o_b0), first, assign,
+                                   changed + pass);
+        }
+        int ch = 0;
+        HIPCHK(hipMemcpyAsync(&ch, changed + pass - 1, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (ch == 0) break;
+    }
+    int* result = ms_ptr<int>(o_result);
+    fill(result, n + 2, -1);
+    hipLaunchKernelGGL(k_mt_commit_slots, dim3(1), dim3(1024), 0, s, fr.keys, n, assign, (const int*)(q + qid_off),
+                       (const float*)(q + qangle_off), (int)qstride, nq, checkOri, ms_ptr<int>(o_mvp), result);
+    HIPCHK(hipGetLastError());
+    int nm = 0;
+    HIPCHK(hipMemcpyAsync(mvp, ms_ptr<int>(o_mvp), (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&nm, result, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return nm;
+}
+
+}  // namespace
+
+extern "C" {
+
+int orbfe_search_by_projection_local(const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs,
+                                     const orbfe_map_point* mps, int32_t n_mps, float th, int32_t bFarPoints,
+                                     float thFarPoints, float nnratio) {
+    return sbp_run(0, F, mvp, mvp_obs, mps, n_mps, sizeof(orbfe_map_point), offsetof(orbfe_map_point, observations),
+                   offsetof(orbfe_map_point, id), 0, offsetof(orbfe_map_point, scale_level), th, bFarPoints, 0, thFarPoints, nnratio, 0, 0);
+}
+
+int orbfe_search_by_projection_lastframe(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_obs,
+                                         const orbfe_proj_point* pts, int32_t n_pts, float th, int32_t bForward,
+                                         int32_t bBackward, int32_t checkOri) {
+    return sbp_run(1, cur, mvp, mvp_obs, pts, n_pts, sizeof(orbfe_proj_point),
+                   offsetof(orbfe_proj_point, observations), offsetof(orbfe_proj_point, id),
+                   offsetof(orbfe_proj_point, angle), offsetof(orbfe_proj_point, octave), th, bForward, bBackward, 0.f, 0.f, MT_TH_HIGH, checkOri);
+}
+
+int orbfe_search_by_projection_kf(const orbfe_frame* cur, int32_t* mvp, const orbfe_proj_point* pts, int32_t n_pts,
+                                  float th, int32_t ORBdist, int32_t checkOri) {
+    return sbp_run(2, cur, mvp, nullptr, pts, n_pts, sizeof(orbfe_proj_point),
+                   offsetof(orbfe_proj_point, observations), offsetof(orbfe_proj_point, id),
+                   offsetof(orbfe_proj_point, angle), offsetof(orbfe_proj_point, octave), th, 0, 0, 0.f, 0.f, ORBdist, checkOri);
+}
+
+int orbfe_search_for_initialization(const orbfe_frame* F1, const orbfe_frame* F2, float* prev_matched,
+                                    int32_t* matches12, int32_t windowSize, float nnratio, int32_t checkOri) {
+    if (!frame_ok(F1) || !frame_ok(F2) || !prev_matched || !matches12) return ORBFE_E_ARG;
+    const int n1 = F1->n;
+    if (n1 == 0) return 0;
+    if (F2->n == 0) {
+        for (int i = 0; i < n1; i++) matches12[i] = -1;
+        return 0;
+    }
+    Plan p;
+    FramePlan f1p, f2p;
+    f1p.plan(p, F1, false, false);
+    f2p.plan(p, F2, true, false);
+    const size_t o_prev = p.upload(prev_matched, (size_t)n1 * 8);
+    f1p.cstart = f1p.cidx = 0;
+    f2p.plan_grid(p);
+    const size_t o_assign = p.scratch((size_t)n1 * 4);
+    const size_t o_adist = p.scratch((size_t)n1 * 4);
+    const size_t o_skey = p.scratch((size_t)n1 * 4);
+    const size_t o_spmin = p.scratch((size_t)n1 * 4);
+    const size_t o_nsel = p.scratch(4);
+    const size_t o_changed = p.scratch(MT_MAX_PASSES * 4);
+    const size_t o_m12 = p.scratch((size_t)n1 * 4);
+    const size_t o_result = p.scratch(16);
+    int rc = ms_prepare(p);
+    if (rc) return rc;
+    hipStream_t s = t_ms.stream;
+    const FrameDev v1 = f1p.view(), v2 = f2p.view();
+    f2p.launch_grid(v2);
+    int* assign = ms_ptr<int>(o_assign);
+    int* adist = ms_ptr<int>(o_adist);
+    int* changed = ms_ptr<int>(o_changed);
+    HIPCHK(hipMemsetAsync(changed, 0, MT_MAX_PASSES * 4, s));
+    fill(assign, n1, -1);
+    fill(adist, n1, 0);
+    const dim3 gq((n1 + MT_NT - 1) / MT_NT);
+    int pass = 0;
+    while (true) {
+        for (int c = 0; c < 2; c++, pass++) {
+            if (pass >= MT_MAX_PASSES) return ORBFE_E_CAPACITY;
+            hipLaunchKernelGGL(k_init_state, dim3(1), dim3(1024), 0, s, assign, adist, n1, ms_ptr<uint32_t>(o_skey),
+                               ms_ptr<int>(o_spmin), ms_ptr<int>(o_nsel));
+            hipLaunchKernelGGL(k_init_eval, gq, dim3(MT_NT), 0, s, v1, v2, ms_ptr<const float>(o_prev), windowSize,
+                               nnratio, ms_ptr<const uint32_t>(o_skey), ms_ptr<const int>(o_spmin),
+                               ms_ptr<const int>(o_nsel), assign, adist, changed + pass);
+        }
+        int ch = 0;
+        HIPCHK(hipMemcpyAsync(&ch, changed + pass - 1, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (ch == 0) break;
+    }
+    hipLaunchKernelGGL(k_init_commit, dim3(1), dim3(1024), 0, s, v1, v2, assign, checkOri, ms_ptr<float>(o_prev),
+                       ms_ptr<int>(o_m12), ms_ptr<int>(o_result));
+    HIPCHK(hipGetLastError());
+    int nm = 0;
+    HIPCHK(hipMemcpyAsync(matches12, ms_ptr<int>(o_m12), (size_t)n1 * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(prev_matched, ms_ptr<float>(o_prev), (size_t)n1 * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&nm, ms_ptr<int>(o_result), 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return nm;
+}
+
+int orbfe_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, const int32_t* kf_mp, int32_t kf_n,
+                        const orbfe_feature_vector* kf_fv, const orbfe_frame* F, const orbfe_feature_vector* f_fv,
+                        int32_t* out, float nnratio, int32_t checkOri) {
+    if (!F || F->n < 0 || kf_n < 0 || !kf_fv || !f_fv || !out || (kf_n > 0 && (!kf_keys || !kf_desc || !kf_mp)))
+        return ORBFE_E_ARG;
+    const int fn = F->n;
+    for (int i = 0; i < fn; i++) out[i] = -1;
+    if (fn == 0 || kf_n == 0 || kf_fv->n_nodes <= 0 || f_fv->n_nodes <= 0) return 0;
+    // ordered merge-join of the two node lists (the reference's lower_bound walk, ORBmatcher.cc:244-371)
+    std::vector<int32_t> pairs;
+    int a = 0, b = 0;
+    while (a < kf_fv->n_nodes && b < f_fv->n_nodes) {
+        if (kf_fv->node_ids[a] == f_fv->node_ids[b]) { pairs.push_back(a); pairs.push_back(b); a++; b++; }
+        else if (kf_fv->node_ids[a] < f_fv->node_ids[b]) a++;
+        else b++;
+    }
+    if (pairs.empty()) return 0;
+    for (const orbfe_feature_vector* fv : {kf_fv, f_fv}) {
+        if (!fv->node_ids || !fv->offsets || fv->offsets[0] != 0) return ORBFE_E_ARG;
+        for (int i = 0; i < fv->n_nodes; i++)
+            if (fv->offsets[i + 1] < fv->offsets[i] || (i > 0 && fv->node_ids[i] <= fv->node_ids[i - 1]))
+                return ORBFE_E_ARG;
+    }
+    // each frame index must belong to one node only (DBoW2 transform); the per-node threads rely on it
+    std::vector<uint8_t> seen(fn, 0);
+    const int nfi = f_fv->offsets[f_fv->n_nodes];
+    for (int i = 0; i < nfi; i++) {
+        const uint32_t x = f_fv->indices[i];
+        if (x >= (uint32_t)fn || seen[x]) return ORBFE_E_ARG;
+        seen[x] = 1;
+    }
+    const int nki = kf_fv->offsets[kf_fv->n_nodes];
+    for (int i = 0; i < nki; i++)
+        if (kf_fv->indices[i] >= (uint32_t)kf_n) return ORBFE_E_ARG;
+    const int npairs = (int)pairs.size() / 2;
+    Plan p;
+    const size_t o_pairs = p.upload(pairs.data(), pairs.size() * 4);
+    const size_t o_kfoff = p.upload(kf_fv->offsets, (size_t)(kf_fv->n_nodes + 1) * 4);
+    const size_t o_kfidx = p.upload(kf_fv->indices, (size_t)nki * 4);
+    const size_t o_foff = p.upload(f_fv->offsets, (size_t)(f_fv->n_nodes + 1) * 4);
+    const size_t o_fidx = p.upload(f_fv->indices, (size_t)nfi * 4);
+    const size_t o_kfmp = p.upload(kf_mp, (size_t)kf_n * 4);
+    const size_t o_kfdesc = p.upload(kf_desc, (size_t)kf_n * 32);
+    const size_t o_kfkeys = p.upload(kf_keys, (size_t)kf_n * sizeof(orbfe_keypoint));
+    const size_t o_fdesc = p.upload(F->desc, (size_t)fn * 32);
+    const size_t o_fkeys = p.upload(F->keys, (size_t)fn * sizeof(orbfe_keypoint));
+    const size_t o_src = p.scratch((size_t)fn * 4);
+    const size_t o_out = p.scratch((size_t)fn * 4);
+    const size_t o_result = p.scratch(16);
+    int rc = ms_prepare(p);
+    if (rc) return rc;
+    hipStream_t s = t_ms.stream;
+    fill(ms_ptr<int>(o_src), fn, -1);
+    hipLaunchKernelGGL(k_bow_nodes, dim3((npairs + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, ms_ptr<const int>(o_pairs),
+                       npairs, ms_ptr<const int>(o_kfoff), ms_ptr<const uint32_t>(o_kfidx), ms_ptr<const int>(o_foff),
+                       ms_ptr<const uint32_t>(o_fidx), ms_ptr<const int32_t>(o_kfmp), ms_ptr<const uint32_t>(o_kfdesc),
+                       ms_ptr<const uint32_t>(o_fdesc), nnratio, ms_ptr<int>(o_src));
+    hipLaunchKernelGGL(k_bow_commit, dim3(1), dim3(1024), 0, s, ms_ptr<const OrbKeyPoint>(o_kfkeys),
+                       ms_ptr<const OrbKeyPoint>(o_fkeys), fn, ms_ptr<const int32_t>(o_kfmp), checkOri,
+                       ms_ptr<const int>(o_src), ms_ptr<int>(o_out), ms_ptr<int>(o_result));
+    HIPCHK(hipGetLastError());
+    int nm = 0;
+    HIPCHK(hipMemcpyAsync(out, ms_ptr<int>(o_out), (size_t)fn * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&nm, ms_ptr<int>(o_result), 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return nm;
+}
+
+int orbfe_stereo_knn_ratio(const uint8_t* left_desc, int32_t nl, const uint8_t* right_desc, int32_t nr, float ratio,
+                           int32_t* out_train, int32_t* out_dist) {
+    if (nl < 0 || nr < 0 || (nl > 0 && (!left_desc || !out_train || !out_dist)) || (nr > 0 && !right_desc))
+        return ORBFE_E_ARG;
+    if (nl == 0) return 0;
+    Plan p;
+    const size_t o_l = p.upload(left_desc, (size_t)nl * 32);
+    const size_t o_r = p.upload(right_desc, (size_t)nr * 32);
+    const size_t o_t = p.scratch((size_t)nl * 4);
+    const size_t o_d = p.scratch((size_t)nl * 4);
+    int rc = ms_prepare(p);
+    if (rc) return rc;
+    hipStream_t s = t_ms.stream;
+    hipLaunchKernelGGL(k_knn2, dim3((nl + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, ms_ptr<const uint32_t>(o_l), nl,
+                       ms_ptr<const uint32_t>(o_r), nr, ratio, ms_ptr<int>(o_t), ms_ptr<int>(o_d));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out_train, ms_ptr<int>(o_t), (size_t)nl * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out_dist, ms_ptr<int>(o_d), (size_t)nl * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    int good = 0;
+    for (int i = 0; i < nl; i++) good += out_train[i] >= 0;
+    return good;
+}
+
+}  // extern "C"

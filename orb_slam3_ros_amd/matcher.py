@@ -1,0 +1,194 @@
+"""ORBmatcher — host mirror of the Tracking-thread methods of ORB_SLAM3::ORBmatcher
+(include/ORBmatcher.h:38-109, src/ORBmatcher.cc) over the C-ABI of liborbfe.so.
+
+The reference methods take C++ objects (Frame&, KeyFrame*, MapPoint*); here they take flattened
+snapshots with the same fields (include/orbfe.h): `MatchFrame` (mvKeysUn, mDescriptors, mvuRight,
+image bounds, mvScaleFactors, mbf), MapPoint records (MAP_POINT_DTYPE / PROJ_POINT_DTYPE) and
+DBoW2 FeatureVectors (`FeatureVector`). MapPoint* values are int32 handles (-1 = NULL).
+Semantics — query order, "already matched" skips, ratio tests, rotation-consistency histogram
+and the returned nmatches — are those of the reference; all compute runs in liborbfe.so's HIP
+kernels (no CPU fallback).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .extractor import KEYPOINT_DTYPE
+
+# orbfe_map_point (80 B): MapPoint tracking snapshot (MapPoint.h:172-180)
+MAP_POINT_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"), ("view_cos", "<f4"),
+                            ("depth", "<f4"), ("scale_level", "<i4"), ("flags", "<i4"), ("observations", "<i4"),
+                            ("id", "<i4"), ("reserved", "<i4", (3,)), ("desc", "u1", (32,))])
+# orbfe_proj_point (64 B): a projected point of the last frame / a keyframe
+PROJ_POINT_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("invzc", "<f4"), ("octave", "<i4"), ("angle", "<f4"),
+                             ("valid", "<i4"), ("observations", "<i4"), ("id", "<i4"), ("desc", "u1", (32,))])
+assert MAP_POINT_DTYPE.itemsize == 80 and PROJ_POINT_DTYPE.itemsize == 64
+MP_IN_VIEW, MP_BAD = 1, 2
+TH_HIGH, TH_LOW, HISTO_LENGTH = 100, 50, 30   # ORBmatcher.cc:33-35
+
+
+class CFrame(ctypes.Structure):
+    """struct orbfe_frame"""
+    _fields_ = [("n", ctypes.c_int32), ("keys", ctypes.c_void_p), ("desc", ctypes.c_void_p),
+                ("uright", ctypes.c_void_p), ("min_x", ctypes.c_float), ("max_x", ctypes.c_float),
+                ("min_y", ctypes.c_float), ("max_y", ctypes.c_float), ("nlevels", ctypes.c_int32),
+                ("scale_factors", ctypes.c_void_p), ("mbf", ctypes.c_float)]
+
+
+class CFeatureVector(ctypes.Structure):
+    """struct orbfe_feature_vector"""
+    _fields_ = [("n_nodes", ctypes.c_int32), ("node_ids", ctypes.c_void_p), ("offsets", ctypes.c_void_p),
+                ("indices", ctypes.c_void_p)]
+
+
+class MatchFrame:
+    """The parts of a Frame the matchers read (Frame.h). keys: KEYPOINT_DTYPE [n] (mvKeysUn),
+    desc: uint8 [n, 32], bounds: (mnMinX, mnMaxX, mnMinY, mnMaxY), uright: float32 [n] or None."""
+
+    def __init__(self, keys, desc, bounds, scale_factors, uright=None, mbf: float = 0.0):
+        self.keys = np.ascontiguousarray(keys, KEYPOINT_DTYPE).reshape(-1)
+        self.desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        if len(self.keys) != len(self.desc):
+            raise ValueError("keys and descriptors differ in length")
+        self.uright = None if uright is None else np.ascontiguousarray(uright, np.float32).reshape(-1)
+        if self.uright is not None and len(self.uright) != len(self.keys):
+            raise ValueError("uright length")
+        self.scale_factors = np.ascontiguousarray(scale_factors, np.float32).reshape(-1)
+        self.bounds = tuple(float(np.float32(b)) for b in bounds)
+        self.mbf = float(mbf)
+        self.c = CFrame(len(self.keys), self.keys.ctypes.data, self.desc.ctypes.data,
+                        self.uright.ctypes.data if self.uright is not None else None, *self.bounds,
+                        len(self.scale_factors), self.scale_factors.ctypes.data, self.mbf)
+
+    @property
+    def N(self) -> int:
+        return len(self.keys)
+
+    def ref(self):
+        return ctypes.byref(self.c)
+
+
+class FeatureVector:
+    """DBoW2::FeatureVector (std::map<NodeId, std::vector<unsigned>>) flattened; node ids ascending."""
+
+    def __init__(self, mapping: dict):
+        ids = sorted(int(k) for k in mapping)
+        self.node_ids = np.asarray(ids, np.uint32)
+        lens = [len(mapping[k]) for k in ids]
+        self.offsets = np.zeros(len(ids) + 1, np.int32)
+        self.offsets[1:] = np.cumsum(lens, dtype=np.int64)
+        self.indices = np.asarray([int(i) for k in ids for i in mapping[k]], np.uint32)
+        if self.indices.size == 0:
+            self.indices = np.zeros(1, np.uint32)
+        self.c = CFeatureVector(len(ids), self.node_ids.ctypes.data, self.offsets.ctypes.data,
+                                self.indices.ctypes.data)
+
+    def ref(self):
+        return ctypes.byref(self.c)
+
+
+def _i32(a, n, what):
+    a = np.asarray(a)
+    if a.dtype != np.int32 or not a.flags.c_contiguous or a.size != n:
+        raise ValueError(f"{what} must be a contiguous int32 array of length {n}")
+    return a
+
+
+def _records(a, dtype, what):
+    a = np.asarray(a)
+    if a.dtype != dtype or not a.flags.c_contiguous:
+        raise ValueError(f"{what} must be a contiguous array of dtype {dtype}")
+    return a
+
+
+class ORBmatcher:
+    """ORBmatcher(nnratio=0.6, checkOri=true) (ORBmatcher.h:43)."""
+
+    def __init__(self, nnratio: float = 0.6, checkOri: bool = True):
+        self._lib = _lib.load()
+        self.mfNNratio = float(nnratio)
+        self.mbCheckOrientation = bool(checkOri)
+
+    @staticmethod
+    def DescriptorDistance(a, b) -> int:
+        a = np.ascontiguousarray(a, np.uint8)
+        b = np.ascontiguousarray(b, np.uint8)
+        return int(_lib.load().orbfe_descriptor_distance(a.ctypes.data, b.ctypes.data))
+
+    # SearchByProjection(Frame&, const vector<MapPoint*>&, th=3, bFarPoints=false, thFarPoints=50) (:43-213)
+    def SearchByProjectionLocalMap(self, F: MatchFrame, mvp, mvp_obs, map_points, th: float = 3.0,
+                                   bFarPoints: bool = False, thFarPoints: float = 50.0) -> int:
+        mvp = _i32(mvp, F.N, "mvp")
+        mvp_obs = _i32(mvp_obs, F.N, "mvp_obs")
+        mps = _records(map_points, MAP_POINT_DTYPE, "map_points")
+        return _lib.check(self._lib.orbfe_search_by_projection_local(
+            F.ref(), mvp.ctypes.data, mvp_obs.ctypes.data, mps.ctypes.data, len(mps), float(th), int(bFarPoints),
+            float(thFarPoints), self.mfNNratio), "SearchByProjection(local map)")
+
+    # SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono) (:1676-1887)
+    def SearchByProjectionLastFrame(self, cur: MatchFrame, mvp, mvp_obs, points, th: float, bForward: bool,
+                                    bBackward: bool) -> int:
+        mvp = _i32(mvp, cur.N, "mvp")
+        mvp_obs = _i32(mvp_obs, cur.N, "mvp_obs")
+        pts = _records(points, PROJ_POINT_DTYPE, "points")
+        return _lib.check(self._lib.orbfe_search_by_projection_lastframe(
+            cur.ref(), mvp.ctypes.data, mvp_obs.ctypes.data, pts.ctypes.data, len(pts), float(th), int(bForward),
+            int(bBackward), int(self.mbCheckOrientation)), "SearchByProjection(last frame)")
+
+    # SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist) (:1889-2010)
+    def SearchByProjectionKeyFrame(self, cur: MatchFrame, mvp, points, th: float, ORBdist: int) -> int:
+        mvp = _i32(mvp, cur.N, "mvp")
+        pts = _records(points, PROJ_POINT_DTYPE, "points")
+        return _lib.check(self._lib.orbfe_search_by_projection_kf(
+            cur.ref(), mvp.ctypes.data, pts.ctypes.data, len(pts), float(th), int(ORBdist),
+            int(self.mbCheckOrientation)), "SearchByProjection(keyframe)")
+
+    def SearchByProjection(self, *args, **kw) -> int:
+        """Overload dispatch like the C++ name: (F, mvp, mvp_obs, MAP_POINT records, ...) -> local map;
+        (F, mvp, mvp_obs, PROJ_POINT records, th, bForward, bBackward) -> last frame;
+        (F, mvp, PROJ_POINT records, th, ORBdist) -> keyframe."""
+        if len(args) >= 4 and isinstance(args[3], np.ndarray) and args[3].dtype == MAP_POINT_DTYPE:
+            return self.SearchByProjectionLocalMap(*args, **kw)
+        if len(args) >= 4 and isinstance(args[3], np.ndarray) and args[3].dtype == PROJ_POINT_DTYPE:
+            return self.SearchByProjectionLastFrame(*args, **kw)
+        return self.SearchByProjectionKeyFrame(*args, **kw)
+
+    # SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize=10) (:648-763)
+    def SearchForInitialization(self, F1: MatchFrame, F2: MatchFrame, vbPrevMatched, vnMatches12,
+                                windowSize: int = 10) -> int:
+        prev = np.asarray(vbPrevMatched)
+        if prev.dtype != np.float32 or not prev.flags.c_contiguous or prev.shape != (F1.N, 2):
+            raise ValueError("vbPrevMatched must be contiguous float32 [N1, 2]")
+        m12 = _i32(vnMatches12, F1.N, "vnMatches12")
+        return _lib.check(self._lib.orbfe_search_for_initialization(
+            F1.ref(), F2.ref(), prev.ctypes.data, m12.ctypes.data, int(windowSize), self.mfNNratio,
+            int(self.mbCheckOrientation)), "SearchForInitialization")
+
+    # SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPointMatches) (:223-425)
+    def SearchByBoW(self, kf_keys, kf_desc, kf_map_points, kf_featvec: FeatureVector, F: MatchFrame,
+                    f_featvec: FeatureVector):
+        """Returns (nmatches, vpMapPointMatches int32 [F.N])."""
+        kk = np.ascontiguousarray(kf_keys, KEYPOINT_DTYPE).reshape(-1)
+        kd = np.ascontiguousarray(kf_desc, np.uint8).reshape(-1, 32)
+        km = _i32(np.ascontiguousarray(kf_map_points, np.int32), len(kk), "kf_map_points")
+        out = np.full(F.N, -1, np.int32)
+        n = _lib.check(self._lib.orbfe_search_by_bow(
+            kk.ctypes.data, kd.ctypes.data, km.ctypes.data, len(kk), kf_featvec.ref(), F.ref(), f_featvec.ref(),
+            out.ctypes.data, self.mfNNratio, int(self.mbCheckOrientation)), "SearchByBoW")
+        return n, out
+
+
+def stereo_knn_ratio(left_desc, right_desc, ratio: float = 0.7):
+    """Descriptor stage of Frame::ComputeStereoFishEyeMatches (Frame.cc:1126-1151):
+    knnMatch(k=2) + Lowe ratio. Returns (good, train [nl], dist [nl])."""
+    lib = _lib.load()
+    L = np.ascontiguousarray(left_desc, np.uint8).reshape(-1, 32)
+    R = np.ascontiguousarray(right_desc, np.uint8).reshape(-1, 32)
+    t = np.full(len(L), -1, np.int32)
+    d = np.full(len(L), -1, np.int32)
+    g = _lib.check(lib.orbfe_stereo_knn_ratio(L.ctypes.data, len(L), R.ctypes.data, len(R), float(ratio),
+                                              t.ctypes.data, d.ctypes.data), "stereo_knn_ratio")
+    return g, t, d

@@ -1,0 +1,166 @@
+"""Seeded synthetic matcher workloads (no datasets offline), SURVEY.md §8c "Config 5".
+
+Frames get uniform keypoints with octaves in the extractor's per-level budget proportions, random
+angles and descriptors; map points / projected points are a mix of noisy COPIES of frame
+features (descriptor bits flipped with probability p, i.e. Binomial(256, p) flips, projected near
+the source keypoint so the ratio tests, "already matched" skips and rotation histogram all fire)
+and uniformly placed random ones. Used by the parity tests and bench.py's matcher line.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .extractor import KEYPOINT_DTYPE
+from .matcher import MAP_POINT_DTYPE, MP_BAD, MP_IN_VIEW, PROJ_POINT_DTYPE, FeatureVector, MatchFrame
+
+
+def scale_factors(nlevels: int = 8, scale_factor: float = 1.2) -> np.ndarray:
+    """mvScaleFactor (ORBextractor.cc:414-420): running float product."""
+    s = np.ones(nlevels, np.float32)
+    for i in range(1, nlevels):
+        s[i] = np.float32(s[i - 1] * np.float32(scale_factor))
+    return s
+
+
+def level_weights(nlevels: int = 8, scale_factor: float = 1.2) -> np.ndarray:
+    w = (1.0 / scale_factor) ** np.arange(nlevels)
+    return w / w.sum()
+
+
+def flip_bits(rng, desc: np.ndarray, p: float) -> np.ndarray:
+    bits = np.unpackbits(desc.reshape(-1, 32), axis=1)
+    bits ^= (rng.random(bits.shape) < p).astype(np.uint8)
+    return np.packbits(bits, axis=1)
+
+
+def synth_frame(rng, n: int, w: int = 752, h: int = 480, nlevels: int = 8, stereo: bool = True,
+                mbf: float = 0.110078 * 458.654) -> MatchFrame:
+    k = np.zeros(n, KEYPOINT_DTYPE)
+    k["x"] = rng.uniform(0, w - 1, n).astype(np.float32)
+    k["y"] = rng.uniform(0, h - 1, n).astype(np.float32)
+    k["octave"] = rng.choice(nlevels, n, p=level_weights(nlevels))
+    sf = scale_factors(nlevels)
+    k["size"] = (31.0 * sf[k["octave"]]).astype(np.float32)
+    k["angle"] = rng.uniform(0, 360, n).astype(np.float32)
+    k["response"] = rng.integers(7, 100, n).astype(np.float32)
+    k["class_id"] = -1
+    desc = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    ur = None
+    if stereo:
+        ur = np.where(rng.random(n) < 0.7, k["x"] - rng.uniform(0, 60, n), -1.0).astype(np.float32)
+    return MatchFrame(k, desc, (0.0, float(w), 0.0, float(h)), sf, ur, mbf)
+
+
+def perturbed_frame(rng, F: MatchFrame, shift=(4.0, -3.0), jitter: float = 1.0, rot: float = 10.0,
+                    flip_p: float = 0.05, drop: float = 0.1):
+    """Another view of F: keypoints shifted/jittered, angles rotated, descriptors noisy, some
+    replaced by new random features (the second frame of SearchForInitialization etc.).
+    Returns (frame, src): src[i] = index of the F feature that keypoint i copies, -1 if new."""
+    n = F.N
+    k = F.keys.copy()
+    k["x"] = np.clip(k["x"] + shift[0] + rng.normal(0, jitter, n), 0, F.bounds[1] - 1).astype(np.float32)
+    k["y"] = np.clip(k["y"] + shift[1] + rng.normal(0, jitter, n), 0, F.bounds[3] - 1).astype(np.float32)
+    k["angle"] = np.mod(k["angle"] + rot + rng.normal(0, 3.0, n), 360.0).astype(np.float32)
+    desc = flip_bits(rng, F.desc, flip_p)
+    new = rng.random(n) < drop
+    desc[new] = rng.integers(0, 256, (int(new.sum()), 32), dtype=np.uint8)
+    perm = rng.permutation(n)   # the other frame's keypoint order is unrelated
+    ur = None if F.uright is None else F.uright[perm] + np.float32(shift[0])
+    src = np.where(new, -1, np.arange(n))[perm]
+    return MatchFrame(k[perm], desc[perm], F.bounds, F.scale_factors, ur, F.mbf), src
+
+
+def synth_local_map(rng, F: MatchFrame, n_mps: int, copy_frac: float = 0.3, flip_p: float = 0.05,
+                    copy_near: bool = True, nlevels: int = 8) -> np.ndarray:
+    """Config 5 map points: mbTrackInView mostly set, projX/Y uniform (copies: near their source),
+    projXR = projX - U(0,60) (copies with a stereo source: that source's uR +- 1), level by budget,
+    viewCos in U(0.99, 1)."""
+    m = np.zeros(n_mps, MAP_POINT_DTYPE)
+    w, h = F.bounds[1], F.bounds[3]
+    m["proj_x"] = rng.uniform(0, w, n_mps)
+    m["proj_y"] = rng.uniform(0, h, n_mps)
+    m["proj_xr"] = m["proj_x"] - rng.uniform(0, 60, n_mps)
+    m["view_cos"] = rng.uniform(0.99, 1.0, n_mps)
+    m["depth"] = rng.uniform(0.5, 60.0, n_mps)
+    m["scale_level"] = rng.choice(nlevels, n_mps, p=level_weights(nlevels))
+    fl = np.full(n_mps, MP_IN_VIEW, np.int32)
+    fl[rng.random(n_mps) < 0.05] = 0
+    fl[rng.random(n_mps) < 0.02] |= MP_BAD
+    m["flags"] = fl
+    m["observations"] = np.where(rng.random(n_mps) < 0.1, 0, rng.integers(1, 20, n_mps))
+    m["id"] = np.arange(n_mps) + 1000
+    m["desc"] = rng.integers(0, 256, (n_mps, 32), dtype=np.uint8)
+    if F.N:
+        cp = np.nonzero(rng.random(n_mps) < copy_frac)[0]
+        src = rng.integers(0, F.N, len(cp))
+        m["desc"][cp] = flip_bits(rng, F.desc[src], flip_p)
+        if copy_near:
+            m["proj_x"][cp] = F.keys["x"][src] + rng.normal(0, 1.5, len(cp))
+            m["proj_y"][cp] = F.keys["y"][src] + rng.normal(0, 1.5, len(cp))
+            m["scale_level"][cp] = F.keys["octave"][src]
+            if F.uright is not None:
+                ur = F.uright[src]
+                m["proj_xr"][cp] = np.where(ur > 0, ur + rng.uniform(-1, 1, len(cp)), m["proj_xr"][cp])
+    return m
+
+
+def initial_slots(rng, n: int, frac: float = 0.1):
+    """Pre-existing F.mvpMapPoints handles and their Observations() (some zero)."""
+    mvp = np.full(n, -1, np.int32)
+    obs = np.zeros(n, np.int32)
+    sel = rng.random(n) < frac
+    mvp[sel] = rng.integers(1, 900, int(sel.sum()))
+    obs[sel] = np.where(rng.random(int(sel.sum())) < 0.4, 0, rng.integers(1, 10, int(sel.sum())))
+    return mvp, obs
+
+
+def synth_proj_points(rng, F: MatchFrame, n: int, copy_frac: float = 0.8, flip_p: float = 0.05, rot: float = 15.0,
+                      invalid: float = 0.1, behind: float = 0.02) -> np.ndarray:
+    """Projected last-frame / keyframe points: copies land near a current keypoint with its
+    octave (+-1) and angle + rot (+ noise, some outliers); the rest are random."""
+    p = np.zeros(n, PROJ_POINT_DTYPE)
+    w, h = F.bounds[1], F.bounds[3]
+    p["u"] = rng.uniform(-20, w + 20, n)
+    p["v"] = rng.uniform(-20, h + 20, n)
+    p["invzc"] = np.where(rng.random(n) < behind, -0.1, 1.0 / rng.uniform(1, 30, n))
+    p["octave"] = rng.integers(0, len(F.scale_factors), n)
+    p["angle"] = rng.uniform(0, 360, n)
+    p["valid"] = (rng.random(n) >= invalid).astype(np.int32)
+    p["observations"] = np.where(rng.random(n) < 0.1, 0, rng.integers(1, 20, n))
+    p["id"] = np.arange(n) + 5000
+    p["desc"] = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    if F.N:
+        cp = np.nonzero(rng.random(n) < copy_frac)[0]
+        src = rng.integers(0, F.N, len(cp))
+        p["desc"][cp] = flip_bits(rng, F.desc[src], flip_p)
+        p["u"][cp] = F.keys["x"][src] + rng.normal(0, 2.0, len(cp))
+        p["v"][cp] = F.keys["y"][src] + rng.normal(0, 2.0, len(cp))
+        p["octave"][cp] = np.clip(F.keys["octave"][src] + rng.integers(-1, 2, len(cp)), 0,
+                                  len(F.scale_factors) - 1)
+        outl = rng.random(len(cp)) < 0.15
+        p["angle"][cp] = np.mod(np.where(outl, rng.uniform(0, 360, len(cp)),
+                                         F.keys["angle"][src] + rot + rng.normal(0, 4, len(cp))), 360.0)
+        if F.uright is not None:   # keep invzc consistent with the stereo check for stereo sources
+            ur = F.uright[src]
+            iz = (p["u"][cp] - ur) / np.float32(F.mbf)
+            p["invzc"][cp] = np.where((ur > 0) & (iz > 0), iz, p["invzc"][cp])
+    return p
+
+
+def synth_bow(rng, n_words: int, kf: MatchFrame, F: MatchFrame, shared_src=None):
+    """Node assignment for both frames (a feature's node = the vocabulary node at the FeatureVector
+    level). Features of F that are noisy copies of KF features (shared_src[i] = KF index or -1)
+    share their source's node."""
+    wk = rng.integers(0, n_words, kf.N)
+    wf = rng.integers(0, n_words, F.N)
+    if shared_src is not None:
+        m = shared_src >= 0
+        wf[m] = wk[shared_src[m]]
+
+    def fv(words):
+        d = {}
+        for i, wd in enumerate(words.tolist()):
+            d.setdefault(int(wd) * 7 + 3, []).append(i)   # sparse node ids
+        return FeatureVector(d)
+
+    return fv(wk), fv(wf)

@@ -1,0 +1,185 @@
+"""GPU parity: the HIP ORBmatcher methods (through the C-ABI) against the CPU oracle's literal
+sequential restatement (oracle/orb_oracle_match.cpp), on seeded synthetic frames / map points.
+Match sets (every mvpMapPoints slot, vnMatches12, vbPrevMatched, SearchByBoW output) and
+nmatches must be identical. Includes the BASELINE config-5 stress: 100k map points against a
+1000- and a 5000-keypoint frame at th in {1, 3, 5, 15}, seed 12345.
+Parity is "unpinned" w.r.t. the real reference (no buildable reference, no matcher fixtures in
+it): the oracle is the restatement, see DESIGN.md.
+"""
+import numpy as np
+import pytest
+
+from orb_slam3_ros_amd import synth_match as sm
+from orb_slam3_ros_amd.matcher import ORBmatcher, stereo_knn_ratio
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def om(oracle_lib):
+    return oracle_lib
+
+
+def _local_case(seed, n_kp, n_mps, stereo=True, slots=0.1, copy_frac=0.3):
+    rng = np.random.default_rng(seed)
+    F = sm.synth_frame(rng, n_kp, stereo=stereo)
+    mps = sm.synth_local_map(rng, F, n_mps, copy_frac=copy_frac)
+    mvp, obs = sm.initial_slots(rng, n_kp, slots)
+    return F, mps, mvp, obs
+
+
+@pytest.mark.parametrize("th", [1, 3, 5, 15])
+@pytest.mark.parametrize("n_kp", [1000, 5000])
+def test_sbp_local_config5(gpu, om, th, n_kp):
+    F, mps, mvp0, obs = _local_case(12345, n_kp, 100_000)
+    m = ORBmatcher(0.8)
+    mvp_g = mvp0.copy()
+    ng = m.SearchByProjection(F, mvp_g, obs, mps, th)
+    mvp_o = mvp0.copy()
+    no = om.OracleMatcher(0.8).sbp_local(F, mvp_o, obs, mps, th)
+    assert ng == no
+    np.testing.assert_array_equal(mvp_g, mvp_o)
+    assert no > 0
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("stereo,bfar,ratio", [(True, False, 0.8), (False, False, 0.8), (True, True, 0.6)])
+def test_sbp_local_variants(gpu, om, seed, stereo, bfar, ratio):
+    F, mps, mvp0, obs = _local_case(seed, 1200, 8000, stereo=stereo, slots=0.3, copy_frac=0.6)
+    mvp_g, mvp_o = mvp0.copy(), mvp0.copy()
+    ng = ORBmatcher(ratio).SearchByProjectionLocalMap(F, mvp_g, obs, mps, 1.0, bfar, 20.0)
+    no = om.OracleMatcher(ratio).sbp_local(F, mvp_o, obs, mps, 1.0, bfar, 20.0)
+    assert ng == no
+    np.testing.assert_array_equal(mvp_g, mvp_o)
+
+
+def test_sbp_local_dense_conflicts(gpu, om):
+    """Many map points competing for few keypoints with Observations() == 0 slots: the ordered
+    'later points see earlier assignments' chain is long here."""
+    rng = np.random.default_rng(7)
+    F = sm.synth_frame(rng, 300, w=120, h=90)
+    mps = sm.synth_local_map(rng, F, 20000, copy_frac=0.9, flip_p=0.02)
+    mps["observations"] = np.where(rng.random(len(mps)) < 0.5, 0, mps["observations"])
+    mvp0 = np.full(F.N, -1, np.int32)
+    obs = np.zeros(F.N, np.int32)
+    for th in (1, 3, 15):
+        a, b = mvp0.copy(), mvp0.copy()
+        ng = ORBmatcher(0.8).SearchByProjectionLocalMap(F, a, obs, mps, th)
+        no = om.OracleMatcher(0.8).sbp_local(F, b, obs, mps, th)
+        assert ng == no
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13, 14])
+@pytest.mark.parametrize("mode", ["none", "forward", "backward"])
+@pytest.mark.parametrize("check_ori", [True, False])
+def test_sbp_lastframe(gpu, om, seed, mode, check_ori):
+    rng = np.random.default_rng(seed)
+    F = sm.synth_frame(rng, 1500, stereo=seed % 2 == 0)
+    pts = sm.synth_proj_points(rng, F, 1400)
+    mvp0, obs = sm.initial_slots(rng, F.N, 0.2)
+    for th in (7, 15):
+        a, b = mvp0.copy(), mvp0.copy()
+        fw, bw = mode == "forward", mode == "backward"
+        ng = ORBmatcher(0.9, check_ori).SearchByProjectionLastFrame(F, a, obs, pts, th, fw, bw)
+        no = om.OracleMatcher(0.9, check_ori).sbp_lastframe(F, b, obs, pts, th, fw, bw)
+        assert ng == no
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("seed", [21, 22, 23])
+@pytest.mark.parametrize("check_ori", [True, False])
+def test_sbp_keyframe(gpu, om, seed, check_ori):
+    rng = np.random.default_rng(seed)
+    F = sm.synth_frame(rng, 1000, stereo=False)
+    pts = sm.synth_proj_points(rng, F, 1200, copy_frac=0.7)
+    mvp0, _ = sm.initial_slots(rng, F.N, 0.25)
+    for th, orbdist in ((10, 100), (3, 64)):
+        a, b = mvp0.copy(), mvp0.copy()
+        ng = ORBmatcher(0.9, check_ori).SearchByProjectionKeyFrame(F, a, pts, th, orbdist)
+        no = om.OracleMatcher(0.9, check_ori).sbp_kf(F, b, pts, th, orbdist)
+        assert ng == no
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("seed", [31, 32, 33, 34])
+@pytest.mark.parametrize("window", [10, 100])
+def test_search_for_initialization(gpu, om, seed, window):
+    rng = np.random.default_rng(seed)
+    F1 = sm.synth_frame(rng, 2000, stereo=False)
+    F2, _ = sm.perturbed_frame(rng, F1, shift=(6.0, -4.0), jitter=2.0, rot=12.0, flip_p=0.06, drop=0.2)
+    prev0 = np.stack([F1.keys["x"], F1.keys["y"]], 1).astype(np.float32)
+    for check_ori in (True, False):
+        pa, pb = prev0.copy(), prev0.copy()
+        ma, mb = np.zeros(F1.N, np.int32), np.zeros(F1.N, np.int32)
+        ng = ORBmatcher(0.9, check_ori).SearchForInitialization(F1, F2, pa, ma, window)
+        no = om.OracleMatcher(0.9, check_ori).search_for_init(F1, F2, pb, mb, window)
+        assert ng == no
+        np.testing.assert_array_equal(ma, mb)
+        np.testing.assert_array_equal(pa, pb)
+
+
+def test_search_for_initialization_steals(gpu, om):
+    """Dense clone clusters: many F1 features select the same F2 feature, so vnMatches21
+    steals and vMatchedDistance updates chain through the query order."""
+    rng = np.random.default_rng(5)
+    F1 = sm.synth_frame(rng, 1500, w=160, h=120, stereo=False)
+    base = F1.desc[:20]
+    F1.desc[:] = sm.flip_bits(rng, base[rng.integers(0, 20, F1.N)], 0.03)
+    F1.keys["octave"][:] = 0
+    F2, _ = sm.perturbed_frame(rng, F1, shift=(1.0, 1.0), flip_p=0.03, drop=0.0)
+    prev0 = np.stack([F1.keys["x"], F1.keys["y"]], 1).astype(np.float32)
+    pa, pb = prev0.copy(), prev0.copy()
+    ma, mb = np.zeros(F1.N, np.int32), np.zeros(F1.N, np.int32)
+    ng = ORBmatcher(0.95, True).SearchForInitialization(F1, F2, pa, ma, 40)
+    no = om.OracleMatcher(0.95, True).search_for_init(F1, F2, pb, mb, 40)
+    assert ng == no
+    np.testing.assert_array_equal(ma, mb)
+    np.testing.assert_array_equal(pa, pb)
+
+
+@pytest.mark.parametrize("seed", [41, 42, 43])
+@pytest.mark.parametrize("check_ori", [True, False])
+def test_search_by_bow(gpu, om, seed, check_ori):
+    rng = np.random.default_rng(seed)
+    KF = sm.synth_frame(rng, 1000, stereo=False)
+    F, src = sm.perturbed_frame(rng, KF, rot=20.0, flip_p=0.05, drop=0.15)
+    kf_mp = np.where(rng.random(KF.N) < 0.25, -1, np.arange(KF.N) + 100).astype(np.int32)
+    for words in (50, 400):
+        fk, ff = sm.synth_bow(rng, words, KF, F, src)
+        ng, out_g = ORBmatcher(0.75, check_ori).SearchByBoW(KF.keys, KF.desc, kf_mp, fk, F, ff)
+        no, out_o = om.OracleMatcher(0.75, check_ori).search_by_bow(KF.keys, KF.desc, kf_mp, fk, F, ff)
+        assert ng == no
+        np.testing.assert_array_equal(out_g, out_o)
+        assert no > 0
+
+
+@pytest.mark.parametrize("nl,nr", [(1000, 1000), (1, 2), (333, 517), (700, 1)])
+def test_stereo_knn_ratio(gpu, om, nl, nr):
+    rng = np.random.default_rng(nl * 7 + nr)
+    R = rng.integers(0, 256, (nr, 32), dtype=np.uint8)
+    L = rng.integers(0, 256, (nl, 32), dtype=np.uint8)
+    k = min(nl, nr) // 2
+    if k:
+        L[:k] = sm.flip_bits(rng, R[rng.integers(0, nr, k)], 0.05)
+    if nr > 3:
+        R[nr // 2] = R[1]   # exact duplicate: tie order of knnMatch
+    g1, t1, d1 = stereo_knn_ratio(L, R)
+    g2, t2, d2 = om.stereo_knn_ratio(L, R)
+    assert g1 == g2
+    np.testing.assert_array_equal(t1, t2)
+    np.testing.assert_array_equal(d1, d2)
+
+
+def test_empty_inputs(gpu, om):
+    rng = np.random.default_rng(0)
+    F = sm.synth_frame(rng, 0)
+    m = ORBmatcher()
+    mvp = np.zeros(0, np.int32)
+    assert m.SearchByProjectionLocalMap(F, mvp, mvp, sm.synth_local_map(rng, F, 10)) == 0
+    F = sm.synth_frame(rng, 50)
+    mvp = np.full(50, -1, np.int32)
+    assert m.SearchByProjectionLocalMap(F, mvp, np.zeros(50, np.int32), np.zeros(0, sm.MAP_POINT_DTYPE)) == 0
+    assert (mvp == -1).all()
+    g, t, d = stereo_knn_ratio(np.zeros((0, 32), np.uint8), np.zeros((5, 32), np.uint8))
+    assert g == 0 and len(t) == 0

@@ -1,0 +1,217 @@
+"""CPU checks of the ORBmatcher oracle (oracle/orb_oracle_match.cpp) against an independent
+pure-Python literal restatement of the reference loops (float32 arithmetic via numpy scalars) on
+small seeded cases, plus properties of the synthetic workloads. No GPU needed."""
+import math
+
+import numpy as np
+import pytest
+
+from orb_slam3_ros_amd import synth_match as sm
+
+f32 = np.float32
+
+
+def _ham(a, b):
+    return int(np.unpackbits(np.bitwise_xor(a, b)).sum())
+
+
+class PyGrid:
+    """Frame::AssignFeaturesToGrid + GetFeaturesInArea (Frame.cc:385-416, 657-723)."""
+
+    def __init__(self, F):
+        self.F = F
+        self.invw = f32(64) / f32(f32(F.bounds[1]) - f32(F.bounds[0]))
+        self.invh = f32(48) / f32(f32(F.bounds[3]) - f32(F.bounds[2]))
+        self.cells = {}
+        for i, k in enumerate(F.keys):
+            px = int(round_half_away(f32(f32(k["x"] - f32(F.bounds[0])) * self.invw)))
+            py = int(round_half_away(f32(f32(k["y"] - f32(F.bounds[2])) * self.invh)))
+            if 0 <= px < 64 and 0 <= py < 48:
+                self.cells.setdefault((px, py), []).append(i)
+
+    def area(self, x, y, r, minL, maxL):
+        F, x, y, r = self.F, f32(x), f32(y), f32(r)
+        mnx, mny = f32(F.bounds[0]), f32(F.bounds[2])
+        c0 = max(0, math.floor(f32(f32(f32(x - mnx) - r) * self.invw)))
+        if c0 >= 64:
+            return []
+        c1 = min(63, math.ceil(f32(f32(f32(x - mnx) + r) * self.invw)))
+        if c1 < 0:
+            return []
+        r0 = max(0, math.floor(f32(f32(f32(y - mny) - r) * self.invh)))
+        if r0 >= 48:
+            return []
+        r1 = min(47, math.ceil(f32(f32(f32(y - mny) + r) * self.invh)))
+        if r1 < 0:
+            return []
+        check = minL > 0 or maxL >= 0
+        out = []
+        for ix in range(c0, c1 + 1):
+            for iy in range(r0, r1 + 1):
+                for i in self.cells.get((ix, iy), []):
+                    k = F.keys[i]
+                    if check and (k["octave"] < minL or (maxL >= 0 and k["octave"] > maxL)):
+                        continue
+                    if abs(f32(k["x"] - x)) < r and abs(f32(k["y"] - y)) < r:
+                        out.append(i)
+        return out
+
+
+def round_half_away(v):
+    return math.floor(v + 0.5) if v >= 0 else -math.floor(-v + 0.5)
+
+
+def py_sbp_local(F, mvp, obs, mps, th, nnratio):
+    """ORBmatcher.cc:43-213 (pinhole path)."""
+    g = PyGrid(F)
+    obs = obs.copy()
+    n = 0
+    for mp in mps:
+        if not (mp["flags"] & sm.MP_IN_VIEW) or (mp["flags"] & sm.MP_BAD):
+            continue
+        lvl = int(mp["scale_level"])
+        r = f32(2.5) if float(mp["view_cos"]) > 0.998 else f32(4.0)
+        if th != 1.0:
+            r = f32(r * f32(th))
+        R = f32(r * F.scale_factors[lvl])
+        bd, bl, bd2, bl2, bi = 256, -1, 256, -1, -1
+        for idx in g.area(mp["proj_x"], mp["proj_y"], R, lvl - 1, lvl):
+            if mvp[idx] >= 0 and obs[idx] > 0:
+                continue
+            if F.uright is not None and F.uright[idx] > 0 and abs(f32(mp["proj_xr"] - F.uright[idx])) > R:
+                continue
+            d = _ham(mp["desc"], F.desc[idx])
+            if d < bd:
+                bd2, bd, bl2, bl, bi = bd, d, bl, int(F.keys[idx]["octave"]), idx
+            elif d < bd2:
+                bl2, bd2 = int(F.keys[idx]["octave"]), d
+        if bd <= 100:
+            if bl == bl2 and bd > f32(nnratio) * f32(bd2):
+                continue
+            mvp[bi] = mp["id"]
+            obs[bi] = mp["observations"]
+            n += 1
+    return n
+
+
+def py_search_for_init(F1, F2, prev, nnratio, window, check_ori):
+    """ORBmatcher.cc:648-763."""
+    g = PyGrid(F2)
+    m12 = np.full(F1.N, -1, np.int32)
+    md = [2**31 - 1] * F2.N
+    m21 = [-1] * F2.N
+    hist = [[] for _ in range(30)]
+    n = 0
+    for i1 in range(F1.N):
+        if F1.keys[i1]["octave"] > 0:
+            continue
+        lvl = int(F1.keys[i1]["octave"])
+        bd = bd2 = 2**31 - 1
+        bi = -1
+        for i2 in g.area(prev[i1, 0], prev[i1, 1], window, lvl, lvl):
+            d = _ham(F1.desc[i1], F2.desc[i2])
+            if md[i2] <= d:
+                continue
+            if d < bd:
+                bd2, bd, bi = bd, d, i2
+            elif d < bd2:
+                bd2 = d
+        if bd <= 50 and bd < f32(bd2) * f32(nnratio):
+            if m21[bi] >= 0:
+                m12[m21[bi]] = -1
+                n -= 1
+            m12[i1], m21[bi], md[bi] = bi, i1, bd
+            n += 1
+            if check_ori:
+                rot = f32(F1.keys[i1]["angle"] - F2.keys[bi]["angle"])
+                if rot < 0:
+                    rot = f32(rot + f32(360))
+                b = int(round_half_away(f32(rot * f32(f32(1) / f32(30)))))
+                hist[0 if b == 30 else b].append(i1)
+    if check_ori:
+        sizes = [len(h) for h in hist]
+        m1 = m2 = m3 = 0
+        i1_ = i2_ = i3_ = -1
+        for i, s in enumerate(sizes):
+            if s > m1:
+                m3, m2, m1, i3_, i2_, i1_ = m2, m1, s, i2_, i1_, i
+            elif s > m2:
+                m3, m2, i3_, i2_ = m2, s, i2_, i
+            elif s > m3:
+                m3, i3_ = s, i
+        if m2 < 0.1 * m1:
+            i2_ = i3_ = -1
+        elif m3 < 0.1 * m1:
+            i3_ = -1
+        for i in range(30):
+            if i in (i1_, i2_, i3_):
+                continue
+            for j in hist[i]:
+                if m12[j] >= 0:
+                    m12[j] = -1
+                    n -= 1
+    for i in range(F1.N):
+        if m12[i] >= 0:
+            prev[i] = (F2.keys[m12[i]]["x"], F2.keys[m12[i]]["y"])
+    return n, m12
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_oracle_sbp_local_vs_python(oracle_lib, seed):
+    rng = np.random.default_rng(seed)
+    F = sm.synth_frame(rng, 150, w=200, h=150)
+    mps = sm.synth_local_map(rng, F, 600, copy_frac=0.7, flip_p=0.03)
+    mvp0, obs = sm.initial_slots(rng, F.N, 0.3)
+    for th in (1, 3):
+        a, b = mvp0.copy(), mvp0.copy()
+        na = oracle_lib.OracleMatcher(0.8).sbp_local(F, a, obs, mps, th)
+        nb = py_sbp_local(F, b, obs, mps, th, 0.8)
+        assert na == nb and na > 0
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_oracle_search_for_init_vs_python(oracle_lib, seed):
+    rng = np.random.default_rng(seed)
+    F1 = sm.synth_frame(rng, 300, w=200, h=150, stereo=False)
+    F1.keys["octave"][rng.random(F1.N) < 0.6] = 0
+    F2, _ = sm.perturbed_frame(rng, F1, shift=(2.0, 1.0), flip_p=0.04)
+    prev = np.stack([F1.keys["x"], F1.keys["y"]], 1).astype(np.float32)
+    pa, pb = prev.copy(), prev.copy()
+    ma = np.zeros(F1.N, np.int32)
+    na = oracle_lib.OracleMatcher(0.9, True).search_for_init(F1, F2, pa, ma, 20)
+    nb, mb = py_search_for_init(F1, F2, pb, 0.9, 20, True)
+    assert na == nb and na > 0
+    np.testing.assert_array_equal(ma, mb)
+    np.testing.assert_array_equal(pa, pb)
+
+
+def test_oracle_knn_vs_numpy(oracle_lib):
+    rng = np.random.default_rng(9)
+    L = rng.integers(0, 256, (60, 32), dtype=np.uint8)
+    R = rng.integers(0, 256, (80, 32), dtype=np.uint8)
+    L[:30] = sm.flip_bits(rng, R[:30], 0.05)
+    D = np.unpackbits(L[:, None, :] ^ R[None, :, :], axis=2).sum(2)
+    g, t, d = oracle_lib.stereo_knn_ratio(L, R)
+    for i in range(len(L)):
+        order = np.argsort(D[i], kind="stable")
+        d0, d1 = D[i, order[0]], D[i, order[1]]
+        ok = d0 < d1 * 0.7
+        assert t[i] == (order[0] if ok else -1)
+        assert d[i] == (d0 if ok else -1)
+    assert g == (t >= 0).sum() >= 25
+
+
+def test_feature_vector_layout():
+    fv = sm.FeatureVector({10: [3, 1], 2: [0], 7: []})
+    assert fv.node_ids.tolist() == [2, 7, 10]
+    assert fv.offsets.tolist() == [0, 1, 1, 3]
+    assert fv.indices.tolist() == [0, 3, 1]
+
+
+def test_record_layouts():
+    import ctypes
+    from orb_slam3_ros_amd.matcher import CFeatureVector, CFrame
+    assert sm.MAP_POINT_DTYPE.itemsize == 80 and sm.PROJ_POINT_DTYPE.itemsize == 64
+    assert ctypes.sizeof(CFrame) == 72 and CFrame.mbf.offset == 64
+    assert ctypes.sizeof(CFeatureVector) == 32
