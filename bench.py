@@ -43,14 +43,30 @@ def algorithmic_bytes(w, h):
     return sum(a * b for a, b in lv) + sum(a * b for a, b in lv[1:])
 
 
+def pmc_traffic(n_img, w, h):
+    """HBM bytes per pyramid+FAST pass from the newest committed PMC summary for this workload
+    (profiles/rNN_pmc_traffic.json, written by tools/pmc_summary.py from rocprofv3 FETCH_SIZE /
+    WRITE_SIZE passes of this same bench command); None when there is none."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if (d.get("images_per_step"), d.get("width"), d.get("height")) == (n_img, w, h):
+            best = (d["pyramid_fast_traffic_bytes_per_step"], os.path.basename(f))
+    return best
+
+
 def cpu_baseline(pairs_l, pairs_r, w, h, nfeatures, bf, fx):
     """Oracle CPU path (C++ restatement, kind='port') on a bounded sample, host cores."""
     from oracle import oracle
     oracle.build()
     L = oracle.lib()
     threads = max(1, min(16, os.cpu_count() or 1))
-    # bounded sample: ~10-30 s of CPU work (the oracle needs ~90 ms per stereo frame per core)
-    n = min(max(160, 8 * threads), 400)
+    # bounded sample: ~10-60 core-seconds of CPU work (the oracle needs ~40 ms per stereo frame per core)
+    n = min(max(400, 100 * threads), 1600)
     idx = [i % len(pairs_l) for i in range(n)]
     Ls = np.ascontiguousarray(np.stack([pairs_l[i] for i in idx]))
     Rs = np.ascontiguousarray(np.stack([pairs_r[i] for i in idx]))
@@ -71,6 +87,33 @@ def cpu_baseline(pairs_l, pairs_r, w, h, nfeatures, bf, fx):
             "seconds": round(dt, 3)}
 
 
+def matcher_config5(steps):
+    """BASELINE config 5: SearchByProjection(Frame&, local map) of 100k synthetic map points against
+    a 1000-keypoint stereo frame, seed 12345, th in {1, 3, 5, 15}, nnratio 0.8 (Tracking.cc:3429).
+    Timed through the host C-ABI call (records packed + uploaded every call, result copied back)."""
+    from orb_slam3_ros_amd import synth_match as sm
+    from orb_slam3_ros_amd.matcher import ORBmatcher
+    rng = np.random.default_rng(12345)
+    F = sm.synth_frame(rng, 1000)
+    mps = sm.synth_local_map(rng, F, 100_000)
+    mvp0, obs = sm.initial_slots(rng, F.N)
+    m = ORBmatcher(0.8)
+    out = {}
+    for th in (1, 3, 5, 15):
+        for _ in range(2):
+            m.SearchByProjectionLocalMap(F, mvp0.copy(), obs, mps, th)
+        bufs = [mvp0.copy() for _ in range(steps)]
+        t0 = time.perf_counter()
+        for b in bufs:
+            n = m.SearchByProjectionLocalMap(F, b, obs, mps, th)
+        dt = (time.perf_counter() - t0) / steps
+        out[f"th{th}"] = {"ms_per_call": round(dt * 1e3, 4), "calls_per_s": round(1.0 / dt, 2),
+                          "queries_per_s": round(len(mps) / dt, 1), "nmatches": int(n)}
+    return {"workload": "SearchByProjection local map: 100k map points (30% noisy copies, Binomial(256,0.05) "
+                        "flips) vs 1000-keypoint stereo frame, nnratio 0.8, seed 12345",
+            "timing": "host C-ABI call incl. 8 MB record upload and result download", "per_th": out}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -85,6 +128,7 @@ def main():
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stage-steps", type=int, default=10, help="extra steps with per-stage HIP events")
+    ap.add_argument("--matcher-steps", type=int, default=10, help="config-5 SearchByProjection calls per th (0: skip)")
     args = ap.parse_args()
 
     import torch
@@ -163,6 +207,7 @@ def main():
         bytes_img = algorithmic_bytes(W, H)
         achieved = n_img * bytes_img / (pyr_fast_ms * 1e-3) / 1e9
         dominant = max(stages, key=stages.get)
+        tr = pmc_traffic(n_img, W, H)
         result = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -193,7 +238,9 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": tr[0] if tr else None,
+                "traffic_unit": "bytes per launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                "traffic_source": tr[1] if tr else None,
                 "bytes_per_image": bytes_img,
                 "images_per_launch": n_img,
                 "kernel_ms_per_launch": round(pyr_fast_ms, 4),
@@ -203,6 +250,8 @@ def main():
             "keypoints_per_image_mean": float(counts[:, 0].mean()),
             "stereo_matches_per_frame_mean": float(nm.mean()),
         }
+        if args.matcher_steps > 0:
+            result["matcher_config5"] = matcher_config5(args.matcher_steps)
         if not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline([p[0] for p in pairs], [p[1] for p in pairs], W, H,
                                                   args.nfeatures, bf, fx)
