@@ -85,7 +85,8 @@ int ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoint
         r.id = H.of(p);
         if (r.flags == ORBFE_MP_IN_VIEW) copy_desc(p->GetDescriptor(), r.desc);
     }
-    const int n = orbfe_search_by_projection_local(&frame_view(F), mvp.data(), obs.data(), q.data(), (int)q.size(),
+    const orbfe_frame fr = frame_view(F);
+    const int n = orbfe_search_by_projection_local(&fr, mvp.data(), obs.data(), q.data(), (int)q.size(),
                                                    th, bFarPoints, thFarPoints, mfNNratio);
     for (int i = 0; i < F.N; i++) F.mvpMapPoints[i] = H.at(mvp[i]);
     return n;
@@ -120,7 +121,8 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, 
         r.id = H.of(p);
         copy_desc(p->GetDescriptor(), r.desc);
     }
-    const int n = orbfe_search_by_projection_lastframe(&frame_view(CurrentFrame), mvp.data(), obs.data(), q.data(),
+    const orbfe_frame fr = frame_view(CurrentFrame);
+    const int n = orbfe_search_by_projection_lastframe(&fr, mvp.data(), obs.data(), q.data(),
                                                        (int)q.size(), th, bForward, bBackward, mbCheckOrientation);
     for (int i = 0; i < CurrentFrame.N; i++) CurrentFrame.mvpMapPoints[i] = H.at(mvp[i]);
     return n;
@@ -155,7 +157,8 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set
         r.id = H.of(p);
         copy_desc(p->GetDescriptor(), r.desc);
     }
-    const int n = orbfe_search_by_projection_kf(&frame_view(CurrentFrame), mvp.data(), q.data(), (int)q.size(), th,
+    const orbfe_frame fr = frame_view(CurrentFrame);
+    const int n = orbfe_search_by_projection_kf(&fr, mvp.data(), q.data(), (int)q.size(), th,
                                                 ORBdist, mbCheckOrientation);
     for (int i = 0; i < CurrentFrame.N; i++) CurrentFrame.mvpMapPoints[i] = H.at(mvp[i]);
     return n;
@@ -166,7 +169,8 @@ int ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, vector<cv::Point2f
                                         vector<int>& vnMatches12, int windowSize) {
     vnMatches12.assign(F1.mvKeysUn.size(), -1);
     static_assert(sizeof(cv::Point2f) == 8, "Point2f layout");
-    return orbfe_search_for_initialization(&frame_view(F1), &frame_view(F2),
+    const orbfe_frame f1 = frame_view(F1), f2 = frame_view(F2);
+    return orbfe_search_for_initialization(&f1, &f2,
                                            reinterpret_cast<float*>(vbPrevMatched.data()), vnMatches12.data(),
                                            windowSize, mfNNratio, mbCheckOrientation);
 }
@@ -197,9 +201,10 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPoi
     const orbfe_feature_vector kfv{(int32_t)kid.size(), kid.data(), koff.data(), kidx.data()};
     const orbfe_feature_vector ffv{(int32_t)fid.size(), fid.data(), foff.data(), fidx.data()};
     vector<int32_t> out(F.N, -1);
+    const orbfe_frame fr = frame_view(F);
     const int n = orbfe_search_by_bow(reinterpret_cast<const orbfe_keypoint*>(pKF->mvKeysUn.data()),
                                       pKF->mDescriptors.data, kf_mp.data(), (int)kf_mp.size(), &kfv,
-                                      &frame_view(F), &ffv, out.data(), mfNNratio, mbCheckOrientation);
+                                      &fr, &ffv, out.data(), mfNNratio, mbCheckOrientation);
     vpMapPointMatches.assign(F.N, nullptr);
     for (int i = 0; i < F.N; i++) vpMapPointMatches[i] = H.at(out[i]);
     return n;
