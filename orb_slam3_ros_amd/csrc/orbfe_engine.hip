@@ -319,7 +319,7 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
     BlurKernel bk;
     memcpy(bk.k, h->blur_variant == 1 ? kBlurRound : kBlurED, sizeof(bk.k));
     if (tm) HIPCHK(hipEventRecord(ev[2], s));   // the blur is fused into k_describe (stage kept for the layout)
-    hipLaunchKernelGGL(k_fast, dim3((g.total_cells + 3) / 4, B), dim3(256), (size_t)4 * 4 * h->roi_max, s, P, pitch,
+    hipLaunchKernelGGL(k_fast, dim3((g.total_cells + 4 * FAST_CPW - 1) / (4 * FAST_CPW), B), dim3(256), (size_t)4 * 4 * h->roi_max, s, P, pitch,
                        h->d_pyr, g.pyr_bytes, g, h->roi_max, h->d_cellkeys, h->d_cellcnt, h->ablate_fast);
     if (tm) HIPCHK(hipEventRecord(ev[3], s));
     hipLaunchKernelGGL(k_octree, dim3(B, g.nlevels), dim3(OCT_NT), h->oct_lds, s, g, h->d_cellkeys, h->d_cellcnt,

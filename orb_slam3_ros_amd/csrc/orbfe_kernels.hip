@@ -314,6 +314,8 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* const* imgs, int in
 // (k, k+8), k = 0,2,4,6) on all pixels and compacts the candidates; pass 2 scores candidates only.
 // ---------------------------------------------------------------------------------------------
 typedef short orbfe_short2 __attribute__((ext_vector_type(2)));
+typedef unsigned short orbfe_ushort2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ orbfe_ushort2 as_us2(uint32_t w) { return __builtin_bit_cast(orbfe_ushort2, w); }
 // M = max over the 16 arcs of 9 contiguous ring pixels of max(min d, min -d), d_k = v - ring_k.
 // Both signs ride in one packed int16x2 lane so every min/max is one v_pk_{min,max}_i16.
 __device__ __forceinline__ int fast_M(const uint8_t* im, int stride, int x, int y) {
@@ -339,142 +341,257 @@ __device__ __forceinline__ int fast_M(const uint8_t* im, int stride, int x, int 
     return max((int)best.x, (int)best.y);
 }
 
+#define FAST_CPW 4    // cells per wave (the next cell's ROI is prefetched into registers)
+#define FAST_PF 16    // prefetch dwords per lane: ROI rows / rows-per-load (<= 48 / 4 = 12 at W = 35)
+struct FastCell {
+    int l, local, r0, c0, rows, cols, pitch;
+    gptr_u8 src;
+};
+__device__ __forceinline__ FastCell fast_cell(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
+                                              int pyr_stride, const OrbGeom& g, int b, int c) {
+    FastCell f;
+    int l = 0;
+    while (l + 1 < g.nlevels && c >= g.lv[l + 1].cell_base) l++;
+    const OrbLevel& L = g.lv[l];
+    f.l = l;
+    f.local = c - L.cell_base;
+    const int ci = f.local / L.n_cols, cj = f.local - ci * L.n_cols;
+    const int maxBX = L.w - ORBFE_MINB, maxBY = L.h - ORBFE_MINB;
+    f.r0 = ORBFE_MINB + ci * L.h_cell;
+    f.c0 = ORBFE_MINB + cj * L.w_cell;
+    const int r1 = min(f.r0 + L.h_cell + 6, maxBY), c1 = min(f.c0 + L.w_cell + 6, maxBX);
+    // the reference skips such cells (ORBextractor.cc:810,819); never true for its grid, kept for parity
+    const bool skip = (f.r0 >= maxBY - 3) || (f.c0 >= maxBX - 6);
+    f.rows = skip ? 0 : r1 - f.r0;
+    f.cols = skip ? 0 : c1 - f.c0;
+    f.src = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l, &f.pitch);
+    return f;
+}
+// LDS layout of a cell: rows of RS = 4*ng + 8 bytes (ng = ceil(dw/4) pixel groups), byte j of a
+// row = ROI column j - 1. Lanes load the aligned global dwords covering a row (nd + 1 lanes per
+// row, one dword each); the realigned dword comes from the next lane.
+__device__ __forceinline__ void fast_geom(const FastCell& f, int* ng, int* nd, int* lpr, int* rpl) {
+    const int dw = f.cols - 6, dh = f.rows - 6;
+    *ng = (dw > 0 && dh > 0) ? (dw + 3) >> 2 : 0;
+    *nd = *ng + 2;
+    *lpr = *nd + 1;
+    *rpl = 64 / *lpr;
+}
+__device__ __forceinline__ void fast_prefetch(const FastCell& f, int lane, uint32_t (&pf)[FAST_PF]) {
+    int ng, nd, lpr, rpl;
+    fast_geom(f, &ng, &nd, &lpr, &rpl);
+    if (!ng) return;
+    const int sy = lane / lpr, st = lane - sy * lpr;
+    if (sy >= rpl) return;
+    const int A0 = (f.c0 - 1) & ~3;
+    // reads stay inside the row: bytes [c0 - 4, c1 + 7) with c1 <= w - 16
+    const bool al = (f.pitch & 3) == 0 && ((((uintptr_t)f.src) & 3) == 0);
+    gptr_u8 base = f.src + (size_t)f.r0 * f.pitch + A0 + 4 * st;
+#pragma unroll
+    for (int u = 0; u < FAST_PF; u++) {
+        const int y = sy + u * rpl;
+        if (y < f.rows) {
+            gptr_u8 rp = base + (size_t)y * f.pitch;
+            if (al) {
+                pf[u] = *(gptr_u32)rp;
+            } else {
+                uint32_t a = 0;
+                for (int k = 0; k < 4; k++) a |= (uint32_t)rp[k] << (8 * k);
+                pf[u] = a;
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                               int pyr_stride, OrbGeom g, int roi_max, uint32_t* cellkeys,
                                               int* cellcnt, int ablate) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_fast[];
     const int wave = threadIdx.x >> 6, lane = lane_id();
-    const int c = blockIdx.x * 4 + wave;
     const int b = blockIdx.y;
     uint8_t* s_img = smem_fast + wave * 4 * roi_max;
     uint8_t* s_sc = s_img + roi_max;
     uint16_t* s_cand = (uint16_t*)(s_sc + roi_max);
-    const bool active = c < g.total_cells;
-    int l = 0;
-    if (active)
-        while (l + 1 < g.nlevels && c >= g.lv[l + 1].cell_base) l++;
-    const OrbLevel& L = g.lv[l];
-    const int local = c - L.cell_base;
-    const int ci = active ? local / L.n_cols : 0, cj = active ? local % L.n_cols : 0;
-    const int maxBX = L.w - ORBFE_MINB, maxBY = L.h - ORBFE_MINB;
-    const int r0 = ORBFE_MINB + ci * L.h_cell, c0 = ORBFE_MINB + cj * L.w_cell;
-    const int r1 = min(r0 + L.h_cell + 6, maxBY), c1 = min(c0 + L.w_cell + 6, maxBX);
-    // the reference skips such cells (ORBextractor.cc:810,819); never true for its grid, kept for parity
-    const bool skip = !active || (r0 >= maxBY - 3) || (c0 >= maxBX - 6);
-    const int rows = skip ? 0 : r1 - r0, cols = skip ? 0 : c1 - c0;
-    int pitch;
-    gptr_u8 src = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l, &pitch);
-    // LDS image rows have stride RS (dwords cover [c0 & ~3, c1)); pixel (y, x) of the ROI lives at
-    // s_img[y * RS + x] after shifting the base by (c0 & 3).
-    const int sh = c0 & 3;
-    const int RS = (cols + sh + 3) & ~3, nd = RS >> 2;
-    const bool al = (pitch & 3) == 0 && ((((uintptr_t)src) & 3) == 0);
-    {
-        const int total = rows * nd;
-        for (int base = lane; base < total; base += 64 * 8) {
-            uint32_t v[8];
-            if (al) {
-#pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const int i = min(base + 64 * u, total - 1);
-                    const int y = i / nd, cdw = i - y * nd;
-                    v[u] = *(gptr_u32)(src + (size_t)(r0 + y) * pitch + (c0 & ~3) + 4 * cdw);
-                }
-            } else {
-                for (int u = 0; u < 8; u++) {
-                    const int i = min(base + 64 * u, total - 1);
-                    const int y = i / nd, cdw = i - y * nd;
-                    const int gx = (c0 & ~3) + 4 * cdw;
-                    gptr_u8 sp = src + (size_t)(r0 + y) * pitch + gx;
-                    uint32_t a = 0;
-                    for (int k = 0; k < 4; k++)
-                        if (gx + k < L.w) a |= (uint32_t)sp[k] << (8 * k);
-                    v[u] = a;
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int i = base + 64 * u;
-                if (i < total) ((uint32_t*)s_img)[i] = v[u];
-            }
-        }
-        for (int i = lane; i < rows * nd; i += 64) ((uint32_t*)s_sc)[i] = 0u;
-    }
-    SYNC();
-    const uint8_t* s_px = s_img + sh;   // ROI pixel (y, x) = s_px[y * RS + x]
-    const int dw = cols - 6, dh = rows - 6;    const int ndet = (dw > 0 && dh > 0) ? dw * dh : 0;
+    const int cbeg = (blockIdx.x * 4 + wave) * FAST_CPW;
+    if (cbeg >= g.total_cells) return;
+    const int cend = min(cbeg + FAST_CPW, g.total_cells);
     const int th = g.min_th;
-    // p -> (dy, dx): floor((p + 0.5) * (1/dw)) is exact for p < 2^16 (error << 0.5/dw)
-    const float inv_dw = dw > 0 ? 1.0f / (float)dw : 0.f;
-    // timing-only ablation: stop after a phase, keep its results live, publish an empty cell
-    if (ablate == 1) { asm volatile("" ::"v"((int)s_px[lane])); if (active && lane == 0) cellcnt[(size_t)b * g.total_cells + c] = 0; return; }
-    // pass 1: necessary test on opposite pairs, compact candidates as (dy << 8 | dx)
-    int ncand = 0;
-    for (int p0 = 0; p0 < ndet; p0 += 64) {
-        const int p = p0 + lane;
-        bool cand = false;
-        int packed = 0;
-        if (p < ndet) {
-            const int dy = (int)(((float)p + 0.5f) * inv_dw), dx = p - dy * dw;
-            packed = (dy << 8) | dx;
-            const uint8_t* q = s_px + (dy + 3) * RS + dx + 3;
-            const int v = q[0];
-            const int lo = v - th, hi = v + th;
-            auto tb = [&](int k) -> int {
-                const int x = q[c_ring_dy[k] * RS + c_ring_dx[k]];
-                return x < lo ? 1 : (x > hi ? 2 : 0);
-            };
-            const int d = (tb(0) | tb(8)) & (tb(2) | tb(10)) & (tb(4) | tb(12)) & (tb(6) | tb(14));
-            cand = d != 0;
+    uint32_t pf[FAST_PF];
+    FastCell cur = fast_cell(imgs, in_pitch, pyr, pyr_stride, g, b, cbeg);
+    fast_prefetch(cur, lane, pf);
+    for (int c = cbeg; c < cend; c++) {
+        int ng, nd, lpr, rpl;
+        fast_geom(cur, &ng, &nd, &lpr, &rpl);
+        const int dw = cur.cols - 6, dh = cur.rows - 6;
+        const int RS = 4 * nd;
+        // stage: realign with the next lane's dword, zero the score map
+        if (ng) {
+            const int sy = lane / lpr, st = lane - sy * lpr, sal = (cur.c0 - 1) & 3;
+            uint32_t* s32w = (uint32_t*)s_img;
+            uint32_t* s32z = (uint32_t*)s_sc;
+#pragma unroll
+            for (int u = 0; u < FAST_PF; u++) {
+                const uint32_t lo = pf[u];
+                const uint32_t hi = __shfl_down(lo, 1, 64);
+                const int y = sy + u * rpl;
+                if (sy < rpl && st < nd && y < cur.rows) {
+                    s32w[y * nd + st] = __builtin_amdgcn_alignbyte(hi, lo, sal);
+                    s32z[y * nd + st] = 0u;
+                }
+            }
+            // rows beyond the prefetch window (only very wide / tall cells of tiny levels): direct
+            // loads; both lanes of a realignment pair share sy, hence the trip count
+            if (sy < rpl && sy + FAST_PF * rpl < cur.rows) {
+                const bool al = (cur.pitch & 3) == 0 && ((((uintptr_t)cur.src) & 3) == 0);
+                gptr_u8 base = cur.src + (size_t)cur.r0 * cur.pitch + ((cur.c0 - 1) & ~3) + 4 * st;
+                for (int y = sy + FAST_PF * rpl; y < cur.rows; y += rpl) {
+                    gptr_u8 rp = base + (size_t)y * cur.pitch;
+                    uint32_t lo = 0;
+                    if (al) lo = *(gptr_u32)rp;
+                    else
+                        for (int k = 0; k < 4; k++) lo |= (uint32_t)rp[k] << (8 * k);
+                    const uint32_t hi = __shfl_down(lo, 1, 64);
+                    if (st < nd) {
+                        s32w[y * nd + st] = __builtin_amdgcn_alignbyte(hi, lo, sal);
+                        s32z[y * nd + st] = 0u;
+                    }
+                }
+            }
         }
-        const unsigned long long m = __ballot(cand);
-        if (cand) s_cand[ncand + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)packed;
-        ncand += __popcll(m);
-    }
-    SYNC();
-    if (ablate == 2) { asm volatile("" ::"v"(ncand)); if (active && lane == 0) cellcnt[(size_t)b * g.total_cells + c] = 0; return; }
-    // pass 2: exact score for candidates only
-    for (int i = lane; i < ncand; i += 64) {
-        const int p = s_cand[i];
-        const int dy = p >> 8, dx = p & 255;
-        const int M = fast_M(s_px, RS, dx + 3, dy + 3);
-        s_sc[(dy + 3) * RS + dx + 3] = (uint8_t)(M > th ? M - 1 : 0);
-    }
-    SYNC();
-    if (ablate == 3) { asm volatile("" ::"v"((int)s_sc[lane])); if (active && lane == 0) cellcnt[(size_t)b * g.total_cells + c] = 0; return; }
-    // NMS (candidates only: every other pixel has score 0); survivors marked in s_img
-    int nhi = 0;
-    for (int i = lane; i < ncand; i += 64) {
-        const int p = s_cand[i];
-        const int dy = p >> 8, dx = p & 255;
-        const uint8_t* q = s_sc + (dy + 3) * RS + dx + 3;
-        const int s = q[0];
-        const bool surv = s > 0 && s > q[-1] && s > q[1] && s > q[-RS - 1] && s > q[-RS] && s > q[-RS + 1] &&
-                          s > q[RS - 1] && s > q[RS] && s > q[RS + 1];
-        nhi += (surv && s >= g.ini_th) ? 1 : 0;
-        s_cand[i] = surv ? (uint16_t)p : (uint16_t)0xFFFF;
-    }
-    nhi = wave_sum(nhi);
-    SYNC();
-    // emission in row-major order == candidate order (candidates were compacted in pixel order)
-    const int thr = nhi > 0 ? g.ini_th : 1;
-    int base = 0;
-    uint32_t* out = cellkeys + (size_t)b * g.cellkeys_per_img + L.cellkey_off + (size_t)local * L.cell_cap;
-    const int xr0 = c0 - ORBFE_MINB + 3, yr0 = r0 - ORBFE_MINB + 3;
-    for (int i0 = 0; i0 < ncand; i0 += 64) {
-        const int i = i0 + lane;
-        int s = 0, p = 0;
-        if (i < ncand) {
-            p = s_cand[i];
-            if (p != 0xFFFF) s = s_sc[((p >> 8) + 3) * RS + (p & 255) + 3];
+        WAVE_SYNC();
+        const FastCell me = cur;
+        if (c + 1 < cend) {   // prefetch the next cell while this one is processed
+            cur = fast_cell(imgs, in_pitch, pyr, pyr_stride, g, b, c + 1);
+            fast_prefetch(cur, lane, pf);
         }
-        const bool f = s >= thr && s > 0;
-        const unsigned long long m = __ballot(f);
-        const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
-        if (f) out[pos] = (uint32_t)(xr0 + (p & 255)) | ((uint32_t)(yr0 + (p >> 8)) << 12) | ((uint32_t)s << 24);
-        base += __popcll(m);
+        const OrbLevel& L = g.lv[me.l];
+        if (ablate == 1) {
+            asm volatile("" ::"v"((int)s_img[lane]));
+            if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = 0;
+            WAVE_SYNC();
+            continue;
+        }
+        const uint8_t* s_px = s_img + 1;   // ROI pixel (y, x) = s_px[y * RS + x]
+        // pass 1: FAST's exact necessary test (each 9-arc contains one pixel of every opposite
+        // pair (k, k+8), k = 0, 2, 4, 6, all of one sign) for 4 pixels per lane in packed u16x2
+        // arithmetic (even bytes / odd bytes); candidates compacted row-major as (dy << 8 | dx).
+        int ncand = 0;
+        if (ng) {
+            const int rpi = 64 / ng;
+            const int ly = lane / ng, lg = lane - ly * ng;
+            const uint32_t* s32 = (const uint32_t*)s_img;
+            const orbfe_ushort2 tv = {(unsigned short)th, (unsigned short)th};
+            const int valid4 = min(4, dw - 4 * lg);
+            const uint32_t vmask = ly < rpi && valid4 > 0 ? (1u << valid4) - 1u : 0u;
+            for (int y0 = 0; y0 < dh; y0 += rpi) {
+                const int y = y0 + ly;
+                uint32_t bits = 0;
+                if (vmask && y < dh) {
+                    const uint32_t* r0p = s32 + (y + 3) * nd + lg;   // dword q of the centre row
+                    const uint32_t c0w = r0p[0], c1w = r0p[1], c2w = r0p[2];
+                    const uint32_t pp[8] = {
+                        r0p[3 * nd + 1],                                                    // 0: (0, 3)
+                        r0p[-3 * nd + 1],                                                   // 8: (0,-3)
+                        __builtin_amdgcn_alignbyte(c2w, c1w, 3),                            // 4: (3, 0)
+                        __builtin_amdgcn_alignbyte(c1w, c0w, 1),                            // 12: (-3, 0)
+                        __builtin_amdgcn_alignbyte(r0p[2 * nd + 2], r0p[2 * nd + 1], 2),    // 2: (2, 2)
+                        __builtin_amdgcn_alignbyte(r0p[-2 * nd + 1], r0p[-2 * nd], 2),      // 10: (-2,-2)
+                        __builtin_amdgcn_alignbyte(r0p[-2 * nd + 2], r0p[-2 * nd + 1], 2),  // 6: (2,-2)
+                        __builtin_amdgcn_alignbyte(r0p[2 * nd + 1], r0p[2 * nd], 2)};       // 14: (-2, 2)
+#pragma unroll
+                    for (int par = 0; par < 2; par++) {
+                        const uint32_t sel = par ? 0x0c030c01u : 0x0c020c00u;
+                        const orbfe_ushort2 v = as_us2(__builtin_amdgcn_perm(0u, c1w, sel));
+                        const orbfe_ushort2 lo = __builtin_elementwise_sub_sat(v, tv), hi = v + tv;
+                        orbfe_ushort2 sd = {0xffff, 0xffff}, sb = {0xffff, 0xffff};
+#pragma unroll
+                        for (int k = 0; k < 4; k++) {
+                            const orbfe_ushort2 xa = as_us2(__builtin_amdgcn_perm(0u, pp[2 * k], sel));
+                            const orbfe_ushort2 xb = as_us2(__builtin_amdgcn_perm(0u, pp[2 * k + 1], sel));
+                            sd = __builtin_elementwise_min(sd, __builtin_elementwise_max(__builtin_elementwise_sub_sat(lo, xa),
+                                                                                          __builtin_elementwise_sub_sat(lo, xb)));
+                            sb = __builtin_elementwise_min(sb, __builtin_elementwise_max(__builtin_elementwise_sub_sat(xa, hi),
+                                                                                          __builtin_elementwise_sub_sat(xb, hi)));
+                        }
+                        const orbfe_ushort2 any = sd | sb;
+                        bits |= (any.x ? 1u : 0u) << par;
+                        bits |= (any.y ? 1u : 0u) << (2 + par);
+                    }
+                    bits &= vmask;
+                }
+                const int cnt = __popc(bits);
+                const int incl = wave_incl_scan(cnt);
+                int pos = ncand + incl - cnt;
+                const int packed = (y << 8) | (4 * lg);
+                for (int i = 0; i < 4; i++)
+                    if ((bits >> i) & 1u) s_cand[pos++] = (uint16_t)(packed + i);
+                ncand += __shfl(incl, 63, 64);
+            }
+        }
+        WAVE_SYNC();
+        if (ablate == 2) {
+            asm volatile("" ::"v"(ncand));
+            if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = 0;
+            WAVE_SYNC();
+            continue;
+        }
+        // pass 2: exact score for candidates only
+        for (int i = lane; i < ncand; i += 64) {
+            const int p = s_cand[i];
+            const int dy = p >> 8, dx = p & 255;
+            const int M = fast_M(s_px, RS, dx + 3, dy + 3);
+            s_sc[(dy + 3) * RS + dx + 3] = (uint8_t)(M > th ? M - 1 : 0);
+        }
+        WAVE_SYNC();
+        if (ablate == 3) {
+            asm volatile("" ::"v"((int)s_sc[lane]));
+            if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = 0;
+            WAVE_SYNC();
+            continue;
+        }
+        // NMS over candidates (every other pixel has score 0); survivors compacted in place,
+        // order preserved (a wave reads its 64 entries before writing positions <= them)
+        int nsurv = 0, nhi = 0;
+        for (int i0 = 0; i0 < ncand; i0 += 64) {
+            const int i = i0 + lane;
+            bool surv = false, hi = false;
+            int p = 0;
+            if (i < ncand) {
+                p = s_cand[i];
+                const uint8_t* q = s_sc + ((p >> 8) + 3) * RS + (p & 255) + 3;
+                const int sc = q[0];
+                surv = sc > 0 && sc > q[-1] && sc > q[1] && sc > q[-RS - 1] && sc > q[-RS] && sc > q[-RS + 1] &&
+                       sc > q[RS - 1] && sc > q[RS] && sc > q[RS + 1];
+                hi = surv && sc >= g.ini_th;
+            }
+            const unsigned long long m = __ballot(surv);
+            if (surv) s_cand[nsurv + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)p;
+            nsurv += __popcll(m);
+            nhi += __popcll(__ballot(hi));
+        }
+        WAVE_SYNC();
+        // emission in row-major order: survivors with score >= iniTh, or all of them when none
+        // reaches it (the reference's FAST(iniTh) -> FAST(minTh) fallback)
+        const int thr = nhi > 0 ? g.ini_th : 1;
+        int base = 0;
+        uint32_t* out = cellkeys + (size_t)b * g.cellkeys_per_img + L.cellkey_off + (size_t)me.local * L.cell_cap;
+        const int xr0 = me.c0 - ORBFE_MINB + 3, yr0 = me.r0 - ORBFE_MINB + 3;
+        for (int i0 = 0; i0 < nsurv; i0 += 64) {
+            const int i = i0 + lane;
+            int sc = 0, p = 0;
+            if (i < nsurv) {
+                p = s_cand[i];
+                sc = s_sc[((p >> 8) + 3) * RS + (p & 255) + 3];
+            }
+            const bool f = i < nsurv && sc >= thr;
+            const unsigned long long m = __ballot(f);
+            const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
+            if (f) out[pos] = (uint32_t)(xr0 + (p & 255)) | ((uint32_t)(yr0 + (p >> 8)) << 12) | ((uint32_t)sc << 24);
+            base += __popcll(m);
+        }
+        if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = base;
+        WAVE_SYNC();   // LDS is restaged for the next cell
     }
-    if (active && lane == 0) cellcnt[(size_t)b * g.total_cells + c] = base;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -124,6 +124,13 @@ def test_small_image(gpu, oracle_lib):
     _compare_extract(img, 500, (0, 0), oracle_lib)
 
 
+def test_large_cells(gpu, oracle_lib):
+    # 362x362: the top levels have a single 69x69 FAST cell (W/35 just below 2), which exceeds
+    # the kernel's register prefetch window and exercises its direct-load path
+    img = synth_image(12, 362, 362)
+    _compare_extract(img, 1000, (0, 0), oracle_lib)
+
+
 def test_mono_init_5000(gpu, oracle_lib):
     # Tracking's mpIniORBextractor uses 5*nFeatures while uninitialised (Tracking.cc:637,1622)
     img = synth_image(21, 752, 480)
