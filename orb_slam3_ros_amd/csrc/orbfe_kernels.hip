@@ -35,6 +35,8 @@ namespace orbfe {
 
 __constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
 __constant__ signed char c_pattern[ORBFE_PATTERN_PAIRS * 4] = ORBFE_BRIEF_PATTERN_INIT;
+constexpr int kRingDx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+constexpr int kRingDy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
 __constant__ int c_ring_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
 __constant__ int c_ring_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
 
@@ -404,12 +406,13 @@ __device__ __forceinline__ void fast_prefetch(const FastCell& f, int lane, uint3
 }
 
 __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
-                                              int pyr_stride, OrbGeom g, int roi_max, uint32_t* cellkeys,
-                                              int* cellcnt, int ablate) {
+                                              int pyr_stride, OrbGeom g, int roi_max, int cand_bytes,
+                                              uint32_t* cellkeys, int* cellcnt, int ablate) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_fast[];
     const int wave = threadIdx.x >> 6, lane = lane_id();
     const int b = blockIdx.y;
-    uint8_t* s_img = smem_fast + wave * 4 * roi_max;
+    // per wave: ROI image | score map | entry list (<= 2 entries per detection pixel)
+    uint8_t* s_img = smem_fast + wave * (2 * roi_max + cand_bytes);
     uint8_t* s_sc = s_img + roi_max;
     uint16_t* s_cand = (uint16_t*)(s_sc + roi_max);
     const int cbeg = (blockIdx.x * 4 + wave) * FAST_CPW;
@@ -485,7 +488,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
             const uint32_t vmask = ly < rpi && valid4 > 0 ? (1u << valid4) - 1u : 0u;
             for (int y0 = 0; y0 < dh; y0 += rpi) {
                 const int y = y0 + ly;
-                uint32_t bits = 0;
+                uint32_t dbits = 0, bbits = 0;
                 if (vmask && y < dh) {
                     const uint32_t* r0p = s32 + (y + 3) * nd + lg;   // dword q of the centre row
                     const uint32_t c0w = r0p[0], c1w = r0p[1], c2w = r0p[2];
@@ -513,19 +516,29 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
                             sb = __builtin_elementwise_min(sb, __builtin_elementwise_max(__builtin_elementwise_sub_sat(xa, hi),
                                                                                           __builtin_elementwise_sub_sat(xb, hi)));
                         }
-                        const orbfe_ushort2 any = sd | sb;
-                        bits |= (any.x ? 1u : 0u) << par;
-                        bits |= (any.y ? 1u : 0u) << (2 + par);
+                        dbits |= (sd.x ? 1u : 0u) << par;
+                        dbits |= (sd.y ? 1u : 0u) << (2 + par);
+                        bbits |= (sb.x ? 1u : 0u) << par;
+                        bbits |= (sb.y ? 1u : 0u) << (2 + par);
                     }
-                    bits &= vmask;
+                    dbits &= vmask;
+                    bbits &= vmask;
                 }
-                const int cnt = __popc(bits);
-                const int incl = wave_incl_scan(cnt);
-                int pos = ncand + incl - cnt;
-                const int packed = (y << 8) | (4 * lg);
-                for (int i = 0; i < 4; i++)
-                    if ((bits >> i) & 1u) s_cand[pos++] = (uint16_t)(packed + i);
-                ncand += __shfl(incl, 63, 64);
+                // one entry per (pixel, possible sign): dy << 7 | dx, bit 14 = bright, bit 15 =
+                // second entry of a pixel (both signs passed); at most one sign can be a corner
+                const int cnt = __popc(dbits) + __popc(bbits);   // <= 8: scan by bit planes
+                const unsigned long long lt = (1ull << lane) - 1ull;
+                const unsigned long long m0 = __ballot(cnt & 1), m1 = __ballot(cnt & 2), m2 = __ballot(cnt & 4),
+                                         m3 = __ballot(cnt & 8);
+                int pos = ncand + __popcll(m0 & lt) + 2 * __popcll(m1 & lt) + 4 * __popcll(m2 & lt) +
+                          8 * __popcll(m3 & lt);
+                const int packed = (y << 7) | (4 * lg);
+                for (int i = 0; i < 4; i++) {
+                    const uint32_t di = (dbits >> i) & 1u, bi = (bbits >> i) & 1u;
+                    if (di) s_cand[pos++] = (uint16_t)(packed + i);
+                    if (bi) s_cand[pos++] = (uint16_t)((packed + i) | 0x4000 | (di << 15));
+                }
+                ncand += __popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2) + 8 * __popcll(m3);
             }
         }
         WAVE_SYNC();
@@ -535,12 +548,48 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
             WAVE_SYNC();
             continue;
         }
-        // pass 2: exact score for candidates only
-        for (int i = lane; i < ncand; i += 64) {
-            const int p = s_cand[i];
-            const int dy = p >> 8, dx = p & 255;
-            const int M = fast_M(s_px, RS, dx + 3, dy + 3);
-            s_sc[(dy + 3) * RS + dx + 3] = (uint8_t)(M > th ? M - 1 : 0);
+        // pass 2: exact score M - 1 (corner iff M > th) of each entry for its sign only, two
+        // entries per lane in packed u16x2 (saturated differences: an arc with a negative minimum
+        // never decides a corner); corners are compacted in place, in pixel order, as dy << 7 | dx
+        int ncorner = 0;
+        for (int j0 = 0; j0 < ncand; j0 += 128) {
+            const int j = j0 + 2 * lane;
+            const uint32_t e2 = j < ncand ? ((const uint32_t*)s_cand)[j >> 1] : 0u;
+            const bool ok0 = j < ncand, ok1 = j + 1 < ncand;
+            const uint32_t e0 = e2 & 0xFFFFu, e1 = ok1 ? e2 >> 16 : e0;
+            const uint8_t* q0 = s_px + (((e0 >> 7) & 127) + 3) * RS + (e0 & 127) + 3;
+            const uint8_t* q1 = s_px + (((e1 >> 7) & 127) + 3) * RS + (e1 & 127) + 3;
+            const uint32_t v2 = (uint32_t)q0[0] | ((uint32_t)q1[0] << 16);
+            const uint32_t bmask = ((e0 & 0x4000u) ? 0x0000FFFFu : 0u) | ((e1 & 0x4000u) ? 0xFFFF0000u : 0u);
+            orbfe_ushort2 P[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const int o = kRingDy[k] * RS + kRingDx[k];
+                const orbfe_ushort2 x2 = as_us2((uint32_t)q0[o] | ((uint32_t)q1[o] << 16));
+                const uint32_t dk = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(as_us2(v2), x2));
+                const uint32_t bk = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(x2, as_us2(v2)));
+                P[k] = as_us2((bk & bmask) | (dk & ~bmask));
+            }
+            orbfe_ushort2 m2[16], m4[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(P[k], P[(k + 1) & 15]);
+#pragma unroll
+            for (int k = 0; k < 16; k++) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
+            orbfe_ushort2 best = {0, 0};
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+                best = __builtin_elementwise_max(
+                    best, __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]), P[(k + 8) & 15]));
+            const bool c0 = ok0 && (int)best.x > th, c1 = ok1 && (int)best.y > th;
+            if (c0) s_sc[(((e0 >> 7) & 127) + 3) * RS + (e0 & 127) + 3] = (uint8_t)(best.x - 1);
+            if (c1) s_sc[(((e1 >> 7) & 127) + 3) * RS + (e1 & 127) + 3] = (uint8_t)(best.y - 1);
+            const int cc = (int)c0 + (int)c1;
+            const unsigned long long lt = (1ull << lane) - 1ull;
+            const unsigned long long b0 = __ballot(cc & 1), b1 = __ballot(cc & 2);
+            int pos = ncorner + __popcll(b0 & lt) + 2 * __popcll(b1 & lt);
+            if (c0) s_cand[pos++] = (uint16_t)(e0 & 0x3FFFu);
+            if (c1) s_cand[pos] = (uint16_t)(e1 & 0x3FFFu);
+            ncorner += __popcll(b0) + 2 * __popcll(b1);
         }
         WAVE_SYNC();
         if (ablate == 3) {
@@ -549,18 +598,17 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
             WAVE_SYNC();
             continue;
         }
-        // NMS over candidates (every other pixel has score 0); survivors compacted in place,
-        // order preserved (a wave reads its 64 entries before writing positions <= them)
+        // NMS over corners (every other pixel has score 0); survivors compacted in place
         int nsurv = 0, nhi = 0;
-        for (int i0 = 0; i0 < ncand; i0 += 64) {
+        for (int i0 = 0; i0 < ncorner; i0 += 64) {
             const int i = i0 + lane;
             bool surv = false, hi = false;
             int p = 0;
-            if (i < ncand) {
+            if (i < ncorner) {
                 p = s_cand[i];
-                const uint8_t* q = s_sc + ((p >> 8) + 3) * RS + (p & 255) + 3;
+                const uint8_t* q = s_sc + ((p >> 7) + 3) * RS + (p & 127) + 3;
                 const int sc = q[0];
-                surv = sc > 0 && sc > q[-1] && sc > q[1] && sc > q[-RS - 1] && sc > q[-RS] && sc > q[-RS + 1] &&
+                surv = sc > q[-1] && sc > q[1] && sc > q[-RS - 1] && sc > q[-RS] && sc > q[-RS + 1] &&
                        sc > q[RS - 1] && sc > q[RS] && sc > q[RS + 1];
                 hi = surv && sc >= g.ini_th;
             }
@@ -581,12 +629,12 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
             int sc = 0, p = 0;
             if (i < nsurv) {
                 p = s_cand[i];
-                sc = s_sc[((p >> 8) + 3) * RS + (p & 255) + 3];
+                sc = s_sc[((p >> 7) + 3) * RS + (p & 127) + 3];
             }
             const bool f = i < nsurv && sc >= thr;
             const unsigned long long m = __ballot(f);
             const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
-            if (f) out[pos] = (uint32_t)(xr0 + (p & 255)) | ((uint32_t)(yr0 + (p >> 8)) << 12) | ((uint32_t)sc << 24);
+            if (f) out[pos] = (uint32_t)(xr0 + (p & 127)) | ((uint32_t)(yr0 + (p >> 7)) << 12) | ((uint32_t)sc << 24);
             base += __popcll(m);
         }
         if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = base;
