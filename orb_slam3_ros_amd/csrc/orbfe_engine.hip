@@ -227,9 +227,33 @@ static int build_geom(orbfe_extractor* h, int W, int H) {
                 for (; x < L.w - lanes / 2; x += lanes / 2) {}
             }
             L.simd_end = x;
-            // block geometry so the staged source window fits s_src[RZ_SROWS][RZ_SCOLS]
-            L.rz_rows = std::max(1, std::min(RZ_ROWS, (int)((RZ_SROWS - 3) / scale_y) + 1));
-            L.rz_cols = std::max(4, std::min(RZ_COLS, ((int)((RZ_SCOLS - 12) / scale_x)) & ~3));
+            // tile geometry: the largest tile whose source window fits s_src[RZ_SR][RZ_SCB] for
+            // every tile of the level (checked exactly on the coefficient tables)
+            (void)scale_x;
+            (void)scale_y;
+            const int16_t* tx = h->tab.data() + L.tab_x;
+            const int16_t* ty = h->tab.data() + L.tab_y;
+            auto rows_fit = [&](int tr) {
+                for (int y0 = 0; y0 < L.h; y0 += tr) {
+                    const int y1 = std::min(y0 + tr, L.h);
+                    if (ty[4 * (y1 - 1) + 1] - ty[4 * y0] + 1 > RZ_SR) return false;
+                }
+                return true;
+            };
+            auto cols_fit = [&](int tc) {
+                for (int x0 = 0; x0 < L.w; x0 += tc) {
+                    const int x1 = std::min(x0 + tc, L.w);
+                    const int sc0 = tx[3 * x0] & ~3, sc1 = std::min((int)tx[3 * (x1 - 1)] + 2, pw);
+                    if (round_up(sc1 - sc0, 4) > RZ_SCB) return false;
+                }
+                return true;
+            };
+            int tr = RZ_TR, tc = RZ_TC;
+            while (tr > 1 && !rows_fit(tr)) tr--;
+            while (tc > 4 && !cols_fit(tc)) tc -= 4;
+            if (!rows_fit(tr) || !cols_fit(tc)) return ORBFE_E_ARG;
+            L.rz_rows = tr;
+            L.rz_cols = tc;
         }
         L.blur_tiles_x = (L.w + BL_TW - 1) / BL_TW;
         L.blur_tiles_y = (L.h + BL_TH - 1) / BL_TH;

@@ -104,97 +104,99 @@ __device__ __forceinline__ uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : 
 // One block = RZ_ROWS output rows x RZ_COLS output columns; the source rows it needs are staged
 // in LDS with dword loads; each thread produces 4 adjacent output pixels (one dword store).
 // ---------------------------------------------------------------------------------------------
-#define RZ_ROWS 8
-#define RZ_COLS 1024
-#define RZ_SROWS 14           // >= ceil(RZ_ROWS * scale_y) + 2 source rows (host clamps rz_rows)
-#define RZ_SCOLS (RZ_COLS * 3 / 2 + 16)
+// Tile = up to RZ_TR output rows x RZ_TC output columns (the host shrinks both per level so the
+// source window fits): (A) the source window is loaded with one batch of aligned dword loads,
+// (B) the horizontal pass H = S[sx]*a0 + S[sx+1]*a1 (exact int) runs once per (source row,
+// output column) into LDS, (C) every thread finishes 4 adjacent output pixels of a row from two
+// 16-byte H reads and stores them with one dword store.
+#define RZ_TR 32
+#define RZ_TC 128
+#define RZ_SR 42              // source rows of a tile window (host-checked)
+#define RZ_SCB 176            // source bytes of a tile window row (host-checked)
+#define RZ_LD 8               // window dwords per thread: RZ_SR * RZ_SCB / 4 / 256 rounded up
 __global__ __launch_bounds__(256) void k_resize(const uint8_t* const* imgs, int in_pitch, uint8_t* pyr, int pyr_stride,
                                                 const int16_t* __restrict__ tab, OrbGeom g, int l) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_src[RZ_SROWS][RZ_SCOLS];
-    __shared__ int s_ty[RZ_ROWS][4];
+    __shared__ __attribute__((aligned(16))) uint8_t s_src[RZ_SR][RZ_SCB];
+    __shared__ __attribute__((aligned(16))) int s_h[RZ_SR][RZ_TC];
+    __shared__ int s_ty[RZ_TR][4];
     const OrbLevel& L = g.lv[l];
     const OrbLevel& Ps = g.lv[l - 1];
-    const int b = blockIdx.z;
-    const int y0 = blockIdx.y * L.rz_rows, x0 = blockIdx.x * L.rz_cols;
+    const int b = blockIdx.z, t = threadIdx.x;
+    const int TR = L.rz_rows, TC = L.rz_cols;
+    const int y0 = blockIdx.y * TR, x0 = blockIdx.x * TC;
+    const int y1 = min(y0 + TR, L.h), x1 = min(x0 + TC, L.w);
     int spitch;
     gptr_u8 src = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l - 1, &spitch);
     uint8_t* dst = pyr + (size_t)b * pyr_stride + L.pyr_off;
     const int16_t* tx = tab + L.tab_x;
     const int16_t* ty = tab + L.tab_y;
-    const int y1 = min(y0 + L.rz_rows, L.h), x1 = min(x0 + L.rz_cols, L.w);
-    const int sr0 = ty[4 * y0], sr1 = ty[4 * (y1 - 1) + 1];              // source rows [sr0, sr1]
+    const int sr0 = ty[4 * y0], sr1 = ty[4 * (y1 - 1) + 1];           // source rows [sr0, sr1]
     const int sc0 = tx[3 * x0] & ~3;
-    const int sc1 = min((int)tx[3 * (x1 - 1)] + 2, Ps.w);                 // source cols [sc0, sc1)
+    const int sc1 = min((int)tx[3 * (x1 - 1)] + 2, Ps.w);              // source cols [sc0, sc1)
     const int nsr = sr1 - sr0 + 1, nsc4 = (sc1 - sc0 + 3) >> 2;
+    const int nitems = nsr * nsc4;
     const bool aligned = ((spitch & 3) == 0) && ((((uintptr_t)src) & 3) == 0);
-    // every global load of the block is issued up front: source window, row and column coefficients
-    const int xq = x0 + 4 * threadIdx.x;     // first of this thread's 4 output columns
-    int sx[4], a0[4], a1[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int dx = min(xq + q, x1 - 1);
-        sx[q] = tx[3 * dx];
-        a0[q] = tx[3 * dx + 1];
-        a1[q] = tx[3 * dx + 2];
-    }
+    // this thread's output column for the horizontal pass and the row coefficients
+    const int hx = t % TC, hr0 = t / TC, hstep = 256 / TC;
+    const int hdx = min(x0 + hx, x1 - 1);
+    const int hsx = tx[3 * hdx] - sc0, ha0 = tx[3 * hdx + 1], ha1 = tx[3 * hdx + 2];
+    const bool hlin = hdx < L.xmax;
     int tyv = 0;
-    if (threadIdx.x < 4 * (y1 - y0)) tyv = ty[4 * y0 + threadIdx.x];
-    uint32_t v[RZ_SROWS][2];
-    if (aligned) {
-        // clamped addresses: every load is issued unconditionally, out-of-window lanes are dropped at the store
+    if (t < 4 * (y1 - y0)) tyv = ty[4 * y0 + t];
+    // (A) window: item i = (r, c) with r = i / nsc4 (float reciprocal is exact for i < 2^16)
+    const float inv_n = 1.0f / (float)nsc4;
+    uint32_t v[RZ_LD];
 #pragma unroll
-        for (int r = 0; r < RZ_SROWS; r++)
-#pragma unroll
-            for (int cc = 0; cc < 2; cc++) {
-                const int rr = min(r, nsr - 1), c = min((int)threadIdx.x + 256 * cc, nsc4 - 1);
-                v[r][cc] = *(gptr_u32)(src + (size_t)(sr0 + rr) * spitch + sc0 + 4 * c);
-            }
-    } else {
-        for (int r = 0; r < RZ_SROWS; r++)
-            for (int cc = 0; cc < 2; cc++) {
-                const int rr = min(r, nsr - 1), c = min((int)threadIdx.x + 256 * cc, nsc4 - 1);
-                gptr_u8 sp = src + (size_t)(sr0 + rr) * spitch + sc0 + 4 * c;
-                uint32_t x = 0;
-                for (int k = 0; k < 4; k++)
-                    if (sc0 + 4 * c + k < Ps.w) x |= (uint32_t)sp[k] << (8 * k);
-                v[r][cc] = x;
-            }
-    }
-#pragma unroll
-    for (int r = 0; r < RZ_SROWS; r++)
-#pragma unroll
-        for (int cc = 0; cc < 2; cc++) {
-            const int c = threadIdx.x + 256 * cc;
-            if (r < nsr && c < nsc4) *(uint32_t*)&s_src[r][4 * c] = v[r][cc];
+    for (int u = 0; u < RZ_LD; u++) {
+        const int i = min(t + 256 * u, nitems - 1);
+        const int r = (int)(((float)i + 0.5f) * inv_n), c = i - r * nsc4;
+        gptr_u8 sp = src + (size_t)(sr0 + r) * spitch + sc0 + 4 * c;
+        if (aligned) {
+            v[u] = *(gptr_u32)sp;
+        } else {
+            uint32_t x = 0;
+            for (int k = 0; k < 4; k++)
+                if (sc0 + 4 * c + k < Ps.w) x |= (uint32_t)sp[k] << (8 * k);
+            v[u] = x;
         }
-    if (threadIdx.x < 4 * (y1 - y0)) (&s_ty[0][0])[threadIdx.x] = tyv;
-    SYNC();
-    if (xq >= x1) return;
-    bool lin[4], vec[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int dx = min(xq + q, x1 - 1);
-        sx[q] -= sc0;
-        lin[q] = dx < L.xmax;
-        vec[q] = dx < L.simd_end;
     }
-    for (int dy = y0; dy < y1; dy++) {
-        const int r0 = s_ty[dy - y0][0] - sr0, r1 = s_ty[dy - y0][1] - sr0;
-        const int b0 = s_ty[dy - y0][2], b1 = s_ty[dy - y0][3];
+#pragma unroll
+    for (int u = 0; u < RZ_LD; u++) {
+        const int i = t + 256 * u;
+        if (i < nitems) {
+            const int r = (int)(((float)i + 0.5f) * inv_n), c = i - r * nsc4;
+            *(uint32_t*)&s_src[r][4 * c] = v[u];
+        }
+    }
+    if (t < 4 * (y1 - y0)) (&s_ty[0][0])[t] = tyv;
+    SYNC();
+    // (B) horizontal pass
+    if (hr0 < hstep) {
+        for (int r = hr0; r < nsr; r += hstep) {
+            const int p0 = s_src[r][hsx];
+            s_h[r][hx] = hlin ? p0 * ha0 + s_src[r][hsx + 1] * ha1 : p0 * 2048;
+        }
+    }
+    SYNC();
+    // (C) vertical pass: thread -> (row lane, 4-column group)
+    const int ng = TC >> 2, cg = t % ng, rl = t / ng, rstep = 256 / ng;
+    const int xq = x0 + 4 * cg;
+    if (rl >= rstep || xq >= x1) return;
+    bool vec[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) vec[q] = xq + q < L.simd_end;
+    for (int dy = y0 + rl; dy < y1; dy += rstep) {
+        const int* tyr = s_ty[dy - y0];
+        const int r0 = tyr[0] - sr0, r1 = tyr[1] - sr0, b0 = tyr[2], b1 = tyr[3];
+        const int4 H0 = *(const int4*)&s_h[r0][4 * cg];
+        const int4 H1 = *(const int4*)&s_h[r1][4 * cg];
+        const int h0[4] = {H0.x, H0.y, H0.z, H0.w}, h1[4] = {H1.x, H1.y, H1.z, H1.w};
         uint32_t packed = 0;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            int h0, h1;
-            if (lin[q]) {
-                h0 = s_src[r0][sx[q]] * a0[q] + s_src[r0][sx[q] + 1] * a1[q];
-                h1 = s_src[r1][sx[q]] * a0[q] + s_src[r1][sx[q] + 1] * a1[q];
-            } else {
-                h0 = s_src[r0][sx[q]] * 2048;
-                h1 = s_src[r1][sx[q]] * 2048;
-            }
             int vv;
-            if (vec[q]) vv = ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2) >> 2;
-            else vv = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+            if (vec[q]) vv = ((((h0[q] >> 4) * b0) >> 16) + (((h1[q] >> 4) * b1) >> 16) + 2) >> 2;
+            else vv = (h0[q] * b0 + h1[q] * b1 + (1 << 21)) >> 22;
             packed |= (uint32_t)sat_u8(vv) << (8 * q);
         }
         uint8_t* dp = dst + (size_t)dy * L.pitch + xq;
