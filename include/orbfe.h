@@ -217,6 +217,12 @@ int orbfe_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, c
 int orbfe_stereo_knn_ratio(const uint8_t* left_desc, int32_t nl, const uint8_t* right_desc, int32_t nr,
                            float ratio, int32_t* out_train, int32_t* out_dist);
 
+/* Per calling thread: when enabled, every matcher call above records HIP events around its
+ * kernels (after the input upload, before the result copy); orbfe_matcher_last_ms returns that
+ * device time of the thread's last call in ms (-1 when not timed). For bench.py. */
+int orbfe_matcher_set_timing(int enable);
+float orbfe_matcher_last_ms(void);
+
 /* Debug/inspection (tests only): copy an intermediate of image `image`, level `level` of the last
  * batch to host memory. what: 0 = per-cell FAST key counts (int32[n_cells]),
  * 1 = per-cell FAST key slots (uint32[n_cells * cell_cap], x_rel | y_rel << 12 | score << 24),

@@ -1196,9 +1196,7 @@ __device__ __forceinline__ float fast_atan2_dev(float y, float x) {
 #define DP_N (2 * DP_R + 1)          // 43
 #define DP_RAW_S 48                  // raw row stride (bytes)
 #define DP_Q_S 40                    // Q8 row-pass stride (u16 elements)
-#define DP_B_S 40                    // blurred row stride (bytes)
-#define DP_B 37                      // blurred window (2*18+1)
-#define DP_WAVE_LDS 7056   // >= 43*48 + 43*40*2 + 37*40, multiple of 16
+#define DP_WAVE_LDS 5504   // >= 43*48 + 43*40*2, multiple of 16
 __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                                   int pyr_stride, OrbGeom g, const uint32_t* __restrict__ outkeys,
                                                   const int* __restrict__ lvinfo, const int* __restrict__ ranks,
@@ -1225,7 +1223,6 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
     const int x = key & 0xfff, y = (key >> 12) & 0xfff;
     uint8_t* raw = s_dp[wave];
     uint16_t* rowq = (uint16_t*)(raw + DP_N * DP_RAW_S);
-    uint8_t* blr = raw + DP_N * DP_RAW_S + DP_N * DP_Q_S * 2;
     int pitch;
     gptr_u8 im = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l, &pitch);
     // ---- stage the raw patch: raw[r][c] = level(y - 21 + r, x - 21 + c), reflect-101 outside ----
@@ -1274,60 +1271,55 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
     m10 = wave_sum(m10);
     m01 = wave_sum(m01);
     const float angle = fast_atan2_dev((float)m01, (float)m10);
-    // ---- 7x7 Gaussian on the 37x37 window: row pass (Q8, exact) then column pass ----
+    // ---- 7x7 Gaussian: row pass (Q8, exact) over the 43x37 region in packed u16x2 (every
+    // partial sum fits 16 bits: sum(k) * 255 <= 65535); the column pass (Q16, rounded) runs only
+    // at the 512 points rBRIEF samples. Both passes are exact integer sums before the final
+    // rounding, so this equals blurring the whole level. ----
     const uint32_t k0 = bk.k[0], k1 = bk.k[1], k2 = bk.k[2], k3 = bk.k[3];
-    for (int it = lane; it < DP_N * 10; it += 64) {   // 43 rows x 10 groups of 4 output columns
-        const int r = it / 10, gq = it - r * 10;
-        const uint32_t* rp = (const uint32_t*)(raw + r * DP_RAW_S) + gq;
-        const uint32_t w0 = rp[0], w1 = rp[1], w2 = rp[2];
-        uint32_t by[12];
+    {
+        const orbfe_ushort2 K0 = {(unsigned short)k0, (unsigned short)k0}, K1 = {(unsigned short)k1, (unsigned short)k1};
+        const orbfe_ushort2 K2 = {(unsigned short)k2, (unsigned short)k2}, K3 = {(unsigned short)k3, (unsigned short)k3};
+        for (int it = lane; it < DP_N * 10; it += 64) {   // 43 rows x 10 groups of 4 output columns
+            const int r = it / 10, gq = it - r * 10;
+            const uint32_t* rp = (const uint32_t*)(raw + r * DP_RAW_S) + gq;
+            const uint32_t w0 = rp[0], w1 = rp[1], w2 = rp[2];
+            // P[j] = (byte j, byte j + 1) of the 12-byte run w0 w1 w2, as u16x2
+            orbfe_ushort2 P[10];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            by[k] = (w0 >> (8 * k)) & 255u;
-            by[4 + k] = (w1 >> (8 * k)) & 255u;
-            by[8 + k] = (w2 >> (8 * k)) & 255u;
+            for (int j = 0; j < 10; j++) {
+                const uint32_t sel = j < 4 ? (0x0c000c00u | ((uint32_t)(j + 1) << 16) | (uint32_t)j)
+                                           : (0x0c000c00u | ((uint32_t)(j - 3) << 16) | (uint32_t)(j - 4));
+                P[j] = as_us2(j < 4 ? __builtin_amdgcn_perm(w1, w0, sel) : __builtin_amdgcn_perm(w2, w1, sel));
+            }
+            const orbfe_ushort2 h01 = K0 * (P[0] + P[6]) + K1 * (P[1] + P[5]) + K2 * (P[2] + P[4]) + K3 * P[3];
+            const orbfe_ushort2 h23 = K0 * (P[2] + P[8]) + K1 * (P[3] + P[7]) + K2 * (P[4] + P[6]) + K3 * P[5];
+            uint2 pk;
+            pk.x = __builtin_bit_cast(uint32_t, h01);
+            pk.y = __builtin_bit_cast(uint32_t, h23);
+            *(uint2*)(rowq + r * DP_Q_S + 4 * gq) = pk;
         }
-        uint32_t h[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            h[q] = k0 * (by[q] + by[q + 6]) + k1 * (by[q + 1] + by[q + 5]) + k2 * (by[q + 2] + by[q + 4]) + k3 * by[q + 3];
-        uint2 pk;
-        pk.x = h[0] | (h[1] << 16);
-        pk.y = h[2] | (h[3] << 16);
-        *(uint2*)(rowq + r * DP_Q_S + 4 * gq) = pk;
     }
     WAVE_SYNC();
-    for (int it = lane; it < DP_B * 10; it += 64) {   // 37 rows x 10 groups of 4 columns
-        const int r = it / 10, gq = it - r * 10;
-        uint32_t a[7][4];
-#pragma unroll
-        for (int j = 0; j < 7; j++) {
-            const uint2 pk = *(const uint2*)(rowq + (r + j) * DP_Q_S + 4 * gq);
-            a[j][0] = pk.x & 0xffffu; a[j][1] = pk.x >> 16; a[j][2] = pk.y & 0xffffu; a[j][3] = pk.y >> 16;
-        }
-        uint32_t packed = 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint32_t sum = k0 * (a[0][q] + a[6][q]) + k1 * (a[1][q] + a[5][q]) + k2 * (a[2][q] + a[4][q]) + k3 * a[3][q];
-            const uint32_t v = (sum + 32768u) >> 16;
-            packed |= (v > 255u ? 255u : v) << (8 * q);
-        }
-        *(uint32_t*)(blr + r * DP_B_S + 4 * gq) = packed;
-    }
-    WAVE_SYNC();
-    // ---- rBRIEF on the blurred window, centre (18, 18) ----
+    // blurred(18 + dy, 18 + dx): column pass over rowq rows 18 + dy .. 24 + dy
+    auto blurred = [&](int dy, int dx) -> int {
+        const uint16_t* col = rowq + (18 + dy) * DP_Q_S + 18 + dx;
+        const uint32_t sum = k0 * ((uint32_t)col[0] + col[6 * DP_Q_S]) + k1 * ((uint32_t)col[DP_Q_S] + col[5 * DP_Q_S]) +
+                             k2 * ((uint32_t)col[2 * DP_Q_S] + col[4 * DP_Q_S]) + k3 * (uint32_t)col[3 * DP_Q_S];
+        const uint32_t v = (sum + 32768u) >> 16;
+        return (int)(v > 255u ? 255u : v);
+    };
+    // ---- rBRIEF, centre (18, 18) of the blurred window ----
     const float factorPI = (float)(M_PI / 180.f);
     const float ang = angle * factorPI;
     const float a = glibc_cosf(ang), bs = glibc_sinf(ang);
-    const uint8_t* bc = blr + 18 * DP_B_S + 18;
     unsigned long long masks[4];
 #pragma unroll
     for (int mm = 0; mm < 4; mm++) {
         const int pr = 64 * mm + lane;
         const float px0f = (float)c_pattern[4 * pr], py0f = (float)c_pattern[4 * pr + 1];
         const float px1f = (float)c_pattern[4 * pr + 2], py1f = (float)c_pattern[4 * pr + 3];
-        const int t0 = bc[(int)rintf(px0f * bs + py0f * a) * DP_B_S + (int)rintf(px0f * a - py0f * bs)];
-        const int t1 = bc[(int)rintf(px1f * bs + py1f * a) * DP_B_S + (int)rintf(px1f * a - py1f * bs)];
+        const int t0 = blurred((int)rintf(px0f * bs + py0f * a), (int)rintf(px0f * a - py0f * bs));
+        const int t1 = blurred((int)rintf(px1f * bs + py1f * a), (int)rintf(px1f * a - py1f * bs));
         masks[mm] = __ballot(t0 < t1);
     }
     const int rk = ranks[(size_t)b * g.out_per_img + flat];

@@ -523,6 +523,29 @@ struct MatchScratch {
 };
 thread_local MatchScratch t_ms;
 
+// Optional per-thread device timing of matcher calls (orbfe_matcher_set_timing): events bracket
+// the kernels of a call on the thread's stream (after the input upload, before the result copy).
+thread_local bool t_timing = false;
+thread_local float t_last_ms = -1.f;
+thread_local hipEvent_t t_ev[2] = {nullptr, nullptr};
+struct MsTimer {
+    bool on = false, ended = false;
+    MsTimer() {
+        t_last_ms = -1.f;
+        if (!t_timing) return;
+        if (!t_ev[0] && (hipEventCreate(&t_ev[0]) != hipSuccess || hipEventCreate(&t_ev[1]) != hipSuccess)) return;
+        on = hipEventRecord(t_ev[0], t_ms.stream) == hipSuccess;
+    }
+    void end() {
+        if (on) ended = hipEventRecord(t_ev[1], t_ms.stream) == hipSuccess;
+    }
+    ~MsTimer() {
+        float ms = 0.f;
+        if (ended && hipEventSynchronize(t_ev[1]) == hipSuccess && hipEventElapsedTime(&ms, t_ev[0], t_ev[1]) == hipSuccess)
+            t_last_ms = ms;
+    }
+};
+
 struct Plan {
     struct Up { const void* src; size_t bytes; size_t off; };
     std::vector<Up> ups;
@@ -653,6 +676,7 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     const size_t o_result = p.scratch((size_t)(n + 2) * 4);
     int rc = ms_prepare(p);
     if (rc) return rc;
+    MsTimer timer;
     hipStream_t s = t_ms.stream;
     const FrameDev fr = fp.view();
     fp.launch_grid(fr);
@@ -689,6 +713,7 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     hipLaunchKernelGGL(k_mt_commit_slots, dim3(1), dim3(1024), 0, s, fr.keys, n, assign, (const int*)(q + qid_off),
                        (const float*)(q + qangle_off), (int)qstride, nq, checkOri, ms_ptr<int>(o_mvp), result);
     HIPCHK(hipGetLastError());
+    timer.end();
     int nm = 0;
     HIPCHK(hipMemcpyAsync(mvp, ms_ptr<int>(o_mvp), (size_t)n * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(&nm, result, 4, hipMemcpyDeviceToHost, s));
@@ -748,6 +773,7 @@ int orbfe_search_for_initialization(const orbfe_frame* F1, const orbfe_frame* F2
     const size_t o_result = p.scratch(16);
     int rc = ms_prepare(p);
     if (rc) return rc;
+    MsTimer timer;
     hipStream_t s = t_ms.stream;
     const FrameDev v1 = f1p.view(), v2 = f2p.view();
     f2p.launch_grid(v2);
@@ -776,6 +802,7 @@ int orbfe_search_for_initialization(const orbfe_frame* F1, const orbfe_frame* F2
     hipLaunchKernelGGL(k_init_commit, dim3(1), dim3(1024), 0, s, v1, v2, assign, checkOri, ms_ptr<float>(o_prev),
                        ms_ptr<int>(o_m12), ms_ptr<int>(o_result));
     HIPCHK(hipGetLastError());
+    timer.end();
     int nm = 0;
     HIPCHK(hipMemcpyAsync(matches12, ms_ptr<int>(o_m12), (size_t)n1 * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(prev_matched, ms_ptr<float>(o_prev), (size_t)n1 * 8, hipMemcpyDeviceToHost, s));
@@ -835,6 +862,7 @@ int orbfe_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, c
     const size_t o_result = p.scratch(16);
     int rc = ms_prepare(p);
     if (rc) return rc;
+    MsTimer timer;
     hipStream_t s = t_ms.stream;
     fill(ms_ptr<int>(o_src), fn, -1);
     hipLaunchKernelGGL(k_bow_nodes, dim3((npairs + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, ms_ptr<const int>(o_pairs),
@@ -845,6 +873,7 @@ int orbfe_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, c
                        ms_ptr<const OrbKeyPoint>(o_fkeys), fn, ms_ptr<const int32_t>(o_kfmp), checkOri,
                        ms_ptr<const int>(o_src), ms_ptr<int>(o_out), ms_ptr<int>(o_result));
     HIPCHK(hipGetLastError());
+    timer.end();
     int nm = 0;
     HIPCHK(hipMemcpyAsync(out, ms_ptr<int>(o_out), (size_t)fn * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(&nm, ms_ptr<int>(o_result), 4, hipMemcpyDeviceToHost, s));
@@ -864,10 +893,12 @@ int orbfe_stereo_knn_ratio(const uint8_t* left_desc, int32_t nl, const uint8_t* 
     const size_t o_d = p.scratch((size_t)nl * 4);
     int rc = ms_prepare(p);
     if (rc) return rc;
+    MsTimer timer;
     hipStream_t s = t_ms.stream;
     hipLaunchKernelGGL(k_knn2, dim3((nl + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, ms_ptr<const uint32_t>(o_l), nl,
                        ms_ptr<const uint32_t>(o_r), nr, ratio, ms_ptr<int>(o_t), ms_ptr<int>(o_d));
     HIPCHK(hipGetLastError());
+    timer.end();
     HIPCHK(hipMemcpyAsync(out_train, ms_ptr<int>(o_t), (size_t)nl * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(out_dist, ms_ptr<int>(o_d), (size_t)nl * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -875,5 +906,12 @@ int orbfe_stereo_knn_ratio(const uint8_t* left_desc, int32_t nl, const uint8_t* 
     for (int i = 0; i < nl; i++) good += out_train[i] >= 0;
     return good;
 }
+
+int orbfe_matcher_set_timing(int enable) {
+    t_timing = enable != 0;
+    return ORBFE_OK;
+}
+
+float orbfe_matcher_last_ms(void) { return t_last_ms; }
 
 }  // extern "C"
