@@ -30,6 +30,11 @@ struct FrameDev {
     const float* scale;
     const int* cstart;      // MT_NCELL + 1 offsets, cell = ix * ORBFE_GRID_ROWS + iy
     const int* cidx;        // keypoint indices sorted by (cell, index)
+    // level-restricted grids (same layout): grid l holds the keypoints with octave in [l-1, l],
+    // the candidate set of a level-l SearchByProjection query (grid 0 = octave 0 only)
+    const int* pcstart;
+    const int* pcidx;
+    int gstride_c, gstride_i;
 };
 
 __device__ __forceinline__ int mt_hamming(const uint8_t* a, const uint32_t* b) {
@@ -43,8 +48,8 @@ __device__ __forceinline__ int mt_hamming(const uint8_t* a, const uint32_t* b) {
 
 // Frame::GetFeaturesInArea (Frame.cc:657-723), calling f(idx) in the reference's order.
 template <typename Fn>
-__device__ __forceinline__ void mt_for_area(const FrameDev& fr, float x, float y, float r, int minLevel, int maxLevel,
-                                            Fn&& f) {
+__device__ __forceinline__ void mt_for_area(const FrameDev& fr, const int* cs, const int* ci, float x, float y, float r,
+                                            int minLevel, int maxLevel, Fn&& f) {
     const int nMinCellX = max(0, (int)floorf((x - fr.minx - r) * fr.invw));
     if (nMinCellX >= ORBFE_GRID_COLS) return;
     const int nMaxCellX = min(ORBFE_GRID_COLS - 1, (int)ceilf((x - fr.minx + r) * fr.invw));
@@ -54,27 +59,33 @@ __device__ __forceinline__ void mt_for_area(const FrameDev& fr, float x, float y
     const int nMaxCellY = min(ORBFE_GRID_ROWS - 1, (int)ceilf((y - fr.miny + r) * fr.invh));
     if (nMaxCellY < 0) return;
     const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
-    for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
-        for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
-            const int c = ix * ORBFE_GRID_ROWS + iy;
-            for (int j = fr.cstart[c]; j < fr.cstart[c + 1]; j++) {
-                const int idx = fr.cidx[j];
-                const OrbKeyPoint kp = fr.keys[idx];
-                if (bCheckLevels) {
-                    if (kp.octave < minLevel) continue;
-                    if (maxLevel >= 0 && kp.octave > maxLevel) continue;
-                }
-                if (fabsf(kp.x - x) < r && fabsf(kp.y - y) < r) f(idx, kp);
+    // cells (ix, nMinCellY..nMaxCellY) are consecutive in the (cell, index)-sorted CSR, so each
+    // grid column of the window is ONE contiguous run already in the reference's iy-inner order
+    for (int ix = nMinCellX; ix <= nMaxCellX; ix++) {
+        const int j1 = cs[ix * ORBFE_GRID_ROWS + nMaxCellY + 1];
+        for (int j = cs[ix * ORBFE_GRID_ROWS + nMinCellY]; j < j1; j++) {
+            const int idx = ci[j];
+            const OrbKeyPoint kp = fr.keys[idx];
+            if (bCheckLevels) {
+                if (kp.octave < minLevel) continue;
+                if (maxLevel >= 0 && kp.octave > maxLevel) continue;
             }
+            if (fabsf(kp.x - x) < r && fabsf(kp.y - y) < r) f(idx, kp);
         }
+    }
 }
 
 // AssignFeaturesToGrid (Frame.cc:385-416): stable (cell, index) order via a bitonic sort of
 // (cell << 16 | index) keys in LDS. One block per frame, n <= MT_GRID_MAXN.
 #define MT_GRID_MAXN 8192
 __global__ __launch_bounds__(1024) void k_mt_grid(const OrbKeyPoint* keys, int n, float minx, float miny, float invw,
-                                                  float invh, int* cstart, int* cidx) {
+                                                  float invh, int* cstart, int* cidx, int gstride_c, int gstride_i) {
     __shared__ uint32_t s_k[MT_GRID_MAXN];
+    // block 0: full grid; block g >= 1: keypoints with octave in [g-2, g-1] (level-(g-1) candidates)
+    const int gi = blockIdx.x;
+    const int lvlo = gi == 0 ? INT_MIN : gi - 2, lvhi = gi == 0 ? INT_MAX : gi - 1;
+    cstart += (size_t)gi * gstride_c;
+    cidx += (size_t)gi * gstride_i;
     int P = 1;
     while (P < n) P <<= 1;
     for (int i = threadIdx.x; i < P; i += blockDim.x) {
@@ -84,7 +95,8 @@ __global__ __launch_bounds__(1024) void k_mt_grid(const OrbKeyPoint* keys, int n
             const int px = (int)roundf((kp.x - minx) * invw);
             const int py = (int)roundf((kp.y - miny) * invh);
             uint32_t cell = MT_NCELL;   // outside the grid: never a candidate (PosInGrid false)
-            if (!(px < 0 || px >= ORBFE_GRID_COLS || py < 0 || py >= ORBFE_GRID_ROWS))
+            if (!(px < 0 || px >= ORBFE_GRID_COLS || py < 0 || py >= ORBFE_GRID_ROWS) && kp.octave >= lvlo &&
+                kp.octave <= lvhi)
                 cell = (uint32_t)(px * ORBFE_GRID_ROWS + py);
             key = (cell << 16) | (uint32_t)i;
         }
@@ -142,7 +154,8 @@ __global__ __launch_bounds__(MT_NT) void k_sbp_local(FrameDev fr, const orbfe_ma
         if (bFactor) r *= th;
         const float R = r * fr.scale[lvl];
         int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
-        mt_for_area(fr, mp.proj_x, mp.proj_y, R, lvl - 1, lvl, [&](int idx, const OrbKeyPoint& kp) {
+        mt_for_area(fr, fr.pcstart + lvl * fr.gstride_c, fr.pcidx + lvl * fr.gstride_i, mp.proj_x, mp.proj_y, R,
+                    lvl - 1, lvl, [&](int idx, const OrbKeyPoint& kp) {
             if (blocked0[idx] || first[idx] < q) return;
             if (fr.uright && fr.uright[idx] > 0) {
                 const float er = fabsf(mp.proj_xr - fr.uright[idx]);
@@ -165,6 +178,154 @@ __global__ __launch_bounds__(MT_NT) void k_sbp_local(FrameDev fr, const orbfe_ma
     if (result != assign[q]) {
         assign[q] = result;
         atomicAdd(changed, 1);
+    }
+}
+
+// Wave-per-query form of k_sbp_local for wide search windows (th >= MT_WAVE_TH): the 64 lanes of
+// a wave enumerate the query's candidates in GetFeaturesInArea order (cells ix-outer / iy-inner,
+// flattened with a wave prefix sum) and keep the two smallest (dist, enumeration index) keys —
+// exactly the reference's sequential best / second-best (a later equal distance never displaces
+// an earlier one). Persistent blocks stage the frame's keypoints and descriptors in LDS.
+#define MT_WAVE_TH 6.0f
+#define MT_STAGE_MAX 1536
+__device__ __forceinline__ unsigned long long mt_wave_min64(unsigned long long v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const unsigned long long o = ((unsigned long long)(unsigned)__shfl_xor((int)(v >> 32), d, 64) << 32) |
+                                     (unsigned)__shfl_xor((int)(v & 0xffffffffu), d, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+#define MT_WNT 1024   // 16 waves per block share one staged copy of the frame
+template <bool STAGED>
+__global__ __launch_bounds__(MT_WNT) void k_sbp_local_wave(FrameDev fr, const orbfe_map_point* mps, int nq, float th,
+                                                        int bFar, float thFar, float nnratio, const int* blocked0,
+                                                        const int* first, int* assign, int* changed) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t mt_sm[];
+    int2* s_cell = (int2*)mt_sm;                                          // [16][64] (start, exclusive prefix)
+    float4* s_key = (float4*)(mt_sm + (MT_WNT / 64) * 64 * sizeof(int2));  // x, y, octave bits, uR
+    uint4* s_desc = (uint4*)(s_key + (STAGED ? fr.n : 0));         // 2 x uint4 per keypoint
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    if (STAGED) {
+        for (int i = tid; i < fr.n; i += MT_WNT) {
+            const OrbKeyPoint kp = fr.keys[i];
+            s_key[i] = make_float4(kp.x, kp.y, __int_as_float(kp.octave), fr.uright ? fr.uright[i] : -1.f);
+            const uint4* d = (const uint4*)(fr.desc + 8 * i);
+            s_desc[2 * i] = d[0];
+            s_desc[2 * i + 1] = d[1];
+        }
+        SYNC();
+    }
+    int2* my_cells = s_cell + 64 * wave;
+    constexpr int WPB = MT_WNT / 64;
+    for (int q = blockIdx.x * WPB + wave; q < nq; q += gridDim.x * WPB) {
+        const orbfe_map_point& mp = mps[q];
+        int result = -1;
+        if ((mp.flags & ORBFE_MP_IN_VIEW) && !(bFar && mp.depth > thFar) && !(mp.flags & ORBFE_MP_BAD)) {
+            const int lvl = mp.scale_level;
+            float r = mp.view_cos > 0.998 ? 2.5f : 4.0f;
+            if (th != 1.0f) r *= th;
+            const float R = r * fr.scale[lvl];
+            const float x = mp.proj_x, y = mp.proj_y, xr = mp.proj_xr;
+            uint32_t qd[8];
+#pragma unroll
+            for (int w = 0; w < 8; w++) {
+                uint32_t t;
+                memcpy(&t, mp.desc + 4 * w, 4);
+                qd[w] = __builtin_amdgcn_readfirstlane(t);
+            }
+            const int minLevel = lvl - 1, maxLevel = lvl;
+            const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+            const int* pcs = fr.pcstart + lvl * fr.gstride_c;
+            const int* pci = fr.pcidx + lvl * fr.gstride_i;
+            const int cx0 = max(0, (int)floorf((x - fr.minx - R) * fr.invw));
+            const int cx1 = min(ORBFE_GRID_COLS - 1, (int)ceilf((x - fr.minx + R) * fr.invw));
+            const int cy0 = max(0, (int)floorf((y - fr.miny - R) * fr.invh));
+            const int cy1 = min(ORBFE_GRID_ROWS - 1, (int)ceilf((y - fr.miny + R) * fr.invh));
+            unsigned long long b1 = ~0ull, b2 = ~0ull;
+            int b1idx = -1;
+            if (cx0 < ORBFE_GRID_COLS && cx1 >= 0 && cy0 < ORBFE_GRID_ROWS && cy1 >= 0 && cx0 <= cx1 && cy0 <= cy1) {
+                // one contiguous CSR run per grid column of the window (<= 64 columns)
+                const int ncell = cx1 - cx0 + 1;
+                int obase = 0;
+                for (int cb = 0; cb < ncell; cb += 64) {
+                    const int c = cb + lane;
+                    int st = 0, cnt = 0;
+                    if (c < ncell) {
+                        const int ix = cx0 + c;
+                        st = pcs[ix * ORBFE_GRID_ROWS + cy0];
+                        cnt = pcs[ix * ORBFE_GRID_ROWS + cy1 + 1] - st;
+                    }
+                    const int incl = wave_incl_scan(cnt);
+                    const int tot = __shfl(incl, 63, 64);
+                    my_cells[lane] = make_int2(st, incl - cnt);
+                    WAVE_SYNC();
+                    for (int j0 = 0; j0 < tot; j0 += 64) {
+                        const int j = j0 + lane;
+                        if (j < tot) {
+                            int lo = 0, hi = 64;   // last cell with prefix <= j
+                            while (hi - lo > 1) {
+                                const int mid = (lo + hi) >> 1;
+                                if (my_cells[mid].y <= j) lo = mid; else hi = mid;
+                            }
+                            const int2 ce = my_cells[lo];
+                            const int idx = pci[ce.x + (j - ce.y)];
+                            float kx, ky, ur;
+                            int oct;
+                            if (STAGED) {
+                                const float4 k4 = s_key[idx];
+                                kx = k4.x; ky = k4.y; oct = __float_as_int(k4.z); ur = k4.w;
+                            } else {
+                                const OrbKeyPoint kp = fr.keys[idx];
+                                kx = kp.x; ky = kp.y; oct = kp.octave; ur = fr.uright ? fr.uright[idx] : -1.f;
+                            }
+                            bool ok = true;
+                            if (bCheckLevels) {
+                                if (oct < minLevel) ok = false;
+                                if (maxLevel >= 0 && oct > maxLevel) ok = false;
+                            }
+                            ok = ok && fabsf(kx - x) < R && fabsf(ky - y) < R;
+                            ok = ok && !(blocked0[idx] || first[idx] < q);
+                            if (ok && ur > 0) ok = !(fabsf(xr - ur) > R);
+                            if (ok) {
+                                uint4 d0, d1;
+                                if (STAGED) { d0 = s_desc[2 * idx]; d1 = s_desc[2 * idx + 1]; }
+                                else { d0 = ((const uint4*)(fr.desc + 8 * idx))[0]; d1 = ((const uint4*)(fr.desc + 8 * idx))[1]; }
+                                const int dist = __popc(qd[0] ^ d0.x) + __popc(qd[1] ^ d0.y) + __popc(qd[2] ^ d0.z) +
+                                                 __popc(qd[3] ^ d0.w) + __popc(qd[4] ^ d1.x) + __popc(qd[5] ^ d1.y) +
+                                                 __popc(qd[6] ^ d1.z) + __popc(qd[7] ^ d1.w);
+                                if (dist < 256) {
+                                    const unsigned long long k = ((unsigned long long)dist << 32) |
+                                                                 ((unsigned long long)(obase + j) << 4) | (unsigned)oct;
+                                    if (k < b1) { b2 = b1; b1 = k; b1idx = idx; }
+                                    else if (k < b2) b2 = k;
+                                }
+                            }
+                        }
+                    }
+                    obase += tot;
+                    WAVE_SYNC();
+                }
+            }
+            const unsigned long long m1 = mt_wave_min64(b1);
+            const unsigned long long win = __ballot(b1 == m1 && m1 != ~0ull);
+            const unsigned long long m2 = mt_wave_min64(b1 == m1 ? b2 : b1);
+            if (m1 != ~0ull) {
+                const int wl = __ffsll((long long)win) - 1;
+                const int bestIdx = __shfl(b1idx, wl, 64);
+                const int bestDist = (int)(m1 >> 32), bestLevel = (int)(m1 & 15);
+                const int bestDist2 = m2 != ~0ull ? (int)(m2 >> 32) : 256;
+                const int bestLevel2 = m2 != ~0ull ? (int)(m2 & 15) : -1;
+                if (bestDist <= MT_TH_HIGH) {
+                    if (!(bestLevel == bestLevel2 && bestDist > nnratio * bestDist2)) result = bestIdx;
+                }
+            }
+        }
+        if (lane == 0 && result != assign[q]) {
+            assign[q] = result;
+            atomicAdd(changed, 1);
+        }
     }
 }
 
@@ -193,7 +354,7 @@ __global__ __launch_bounds__(MT_NT) void k_sbp_proj(FrameDev fr, const orbfe_pro
         else if (bBackward) { minL = 0; maxL = oct; }
         else { minL = oct - 1; maxL = oct + 1; }
         int bestDist = 256, bestIdx2 = -1;
-        mt_for_area(fr, p.u, p.v, radius, minL, maxL, [&](int i2, const OrbKeyPoint&) {
+        mt_for_area(fr, fr.cstart, fr.cidx, p.u, p.v, radius, minL, maxL, [&](int i2, const OrbKeyPoint&) {
             if (blocked0[i2] || first[i2] < q) return;
             if (mode == 0 && fr.uright && fr.uright[i2] > 0) {
                 const float ur = p.u - fr.mbf * p.invzc;
@@ -350,7 +511,9 @@ __global__ __launch_bounds__(MT_NT) void k_init_eval(FrameDev f1, FrameDev f2, c
         uint8_t d1[32];
         memcpy(d1, f1.desc + 8 * q, 32);
         int bestDist = MT_INF, bestDist2 = MT_INF, bestIdx2 = -1;
-        mt_for_area(f2, prev[2 * q], prev[2 * q + 1], (float)windowSize, level1, level1, [&](int i2, const OrbKeyPoint&) {
+        // only level-0 queries reach here: the octave-0 grid holds exactly the level-0 candidates
+        mt_for_area(f2, f2.pcstart, f2.pcidx, prev[2 * q], prev[2 * q + 1], (float)windowSize, level1, level1,
+                    [&](int i2, const OrbKeyPoint&) {
             const int dist = mt_hamming(d1, f2.desc + 8 * i2);
             // vMatchedDistance[i2] as seen by query q: last selector j < q of i2
             int lo = 0, hi = m;   // first key >= (i2 << 16 | q)
@@ -606,9 +769,11 @@ struct FramePlan {
         scale = p.upload(f->scale_factors, (size_t)f->nlevels * 4);
         (void)want_grid;
     }
-    void plan_grid(Plan& p) {
-        cstart = p.scratch((MT_NCELL + 1) * 4);
-        cidx = p.scratch((size_t)std::max(F->n, 1) * 4);
+    int ngrids = 1;
+    void plan_grid(Plan& p, int grids) {   // grids = 1 (full) + level-restricted grids
+        ngrids = grids;
+        cstart = p.scratch((size_t)grids * (MT_NCELL + 1) * 4);
+        cidx = p.scratch((size_t)grids * std::max(F->n, 1) * 4);
     }
     FrameDev view() const {
         FrameDev v;
@@ -624,11 +789,15 @@ struct FramePlan {
         v.scale = ms_ptr<const float>(scale);
         v.cstart = ms_ptr<const int>(cstart);
         v.cidx = ms_ptr<const int>(cidx);
+        v.gstride_c = MT_NCELL + 1;
+        v.gstride_i = std::max(F->n, 1);
+        v.pcstart = v.cstart + v.gstride_c;
+        v.pcidx = v.cidx + v.gstride_i;
         return v;
     }
     void launch_grid(const FrameDev& v) const {
-        hipLaunchKernelGGL(k_mt_grid, dim3(1), dim3(1024), 0, t_ms.stream, v.keys, v.n, v.minx, v.miny, v.invw,
-                           v.invh, (int*)v.cstart, (int*)v.cidx);
+        hipLaunchKernelGGL(k_mt_grid, dim3(ngrids), dim3(1024), 0, t_ms.stream, v.keys, v.n, v.minx, v.miny, v.invw,
+                           v.invh, (int*)v.cstart, (int*)v.cidx, v.gstride_c, v.gstride_i);
     }
 };
 
@@ -669,7 +838,7 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     const size_t o_q = p.upload(queries, (size_t)nq * qstride);
     const size_t o_b0 = p.upload(blocked0.data(), (size_t)n * 4);
     const size_t o_mvp = p.upload(mvp, (size_t)n * 4);
-    fp.plan_grid(p);
+    fp.plan_grid(p, mode == 0 ? F->nlevels + 1 : 1);
     const size_t o_first = p.scratch((size_t)n * 4);
     const size_t o_assign = p.scratch((size_t)nq * 4);
     const size_t o_changed = p.scratch(MT_MAX_PASSES * 4);
@@ -687,6 +856,7 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     fill(assign, nq, -1);
     const uint8_t* q = ms_ptr<const uint8_t>(o_q);
     const dim3 gq((nq + MT_NT - 1) / MT_NT);
+    const bool staged = n <= MT_STAGE_MAX;
     int pass = 0;
     const int chunk = 2;   // passes launched between host checks (most searches converge in 2-3)
     while (true) {
@@ -695,7 +865,16 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
             fill(first, n, MT_INF);
             hipLaunchKernelGGL(k_mt_first_strided, gq, dim3(MT_NT), 0, s, assign, q + qobs_off, (int)qstride, nq,
                                mode == 2 ? 0 : 1, first);
-            if (mode == 0)
+            if (mode == 0 && th >= MT_WAVE_TH) {
+                const int nb = std::min((nq + MT_WNT / 64 - 1) / (MT_WNT / 64), 512);
+                const size_t lds = (MT_WNT / 64) * 64 * sizeof(int2) + (staged ? (size_t)n * 48 : 0);
+                if (staged)
+                    hipLaunchKernelGGL(k_sbp_local_wave<true>, dim3(nb), dim3(MT_WNT), lds, s, fr, (const orbfe_map_point*)q,
+                                       nq, th, a0, thFar, nnratio, ms_ptr<const int>(o_b0), first, assign, changed + pass);
+                else
+                    hipLaunchKernelGGL(k_sbp_local_wave<false>, dim3(nb), dim3(MT_WNT), lds, s, fr, (const orbfe_map_point*)q,
+                                       nq, th, a0, thFar, nnratio, ms_ptr<const int>(o_b0), first, assign, changed + pass);
+            } else if (mode == 0)
                 hipLaunchKernelGGL(k_sbp_local, gq, dim3(MT_NT), 0, s, fr, (const orbfe_map_point*)q, nq, th, a0, thFar,
                                    nnratio, ms_ptr<const int>(o_b0), first, assign, changed + pass);
             else
@@ -762,7 +941,7 @@ int orbfe_search_for_initialization(const orbfe_frame* F1, const orbfe_frame* F2
     f2p.plan(p, F2, true, false);
     const size_t o_prev = p.upload(prev_matched, (size_t)n1 * 8);
     f1p.cstart = f1p.cidx = 0;
-    f2p.plan_grid(p);
+    f2p.plan_grid(p, 2);
     const size_t o_assign = p.scratch((size_t)n1 * 4);
     const size_t o_adist = p.scratch((size_t)n1 * 4);
     const size_t o_skey = p.scratch((size_t)n1 * 4);
