@@ -508,16 +508,18 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
                         const uint32_t sel = par ? 0x0c030c01u : 0x0c020c00u;
                         const orbfe_ushort2 v = as_us2(__builtin_amdgcn_perm(0u, c1w, sel));
                         const orbfe_ushort2 lo = __builtin_elementwise_sub_sat(v, tv), hi = v + tv;
-                        orbfe_ushort2 sd = {0xffff, 0xffff}, sb = {0xffff, 0xffff};
+                        // dark possible  <=> every pair has a member < v - t <=> max_k min(pair k) < v - t
+                        // bright possible <=> every pair has a member > v + t <=> min_k max(pair k) > v + t
+                        orbfe_ushort2 D = {0, 0}, B = {0xffff, 0xffff};
 #pragma unroll
                         for (int k = 0; k < 4; k++) {
                             const orbfe_ushort2 xa = as_us2(__builtin_amdgcn_perm(0u, pp[2 * k], sel));
                             const orbfe_ushort2 xb = as_us2(__builtin_amdgcn_perm(0u, pp[2 * k + 1], sel));
-                            sd = __builtin_elementwise_min(sd, __builtin_elementwise_max(__builtin_elementwise_sub_sat(lo, xa),
-                                                                                          __builtin_elementwise_sub_sat(lo, xb)));
-                            sb = __builtin_elementwise_min(sb, __builtin_elementwise_max(__builtin_elementwise_sub_sat(xa, hi),
-                                                                                          __builtin_elementwise_sub_sat(xb, hi)));
+                            D = __builtin_elementwise_max(D, __builtin_elementwise_min(xa, xb));
+                            B = __builtin_elementwise_min(B, __builtin_elementwise_max(xa, xb));
                         }
+                        const orbfe_ushort2 sd = __builtin_elementwise_sub_sat(lo, D);
+                        const orbfe_ushort2 sb = __builtin_elementwise_sub_sat(B, hi);
                         dbits |= (sd.x ? 1u : 0u) << par;
                         dbits |= (sd.y ? 1u : 0u) << (2 + par);
                         bbits |= (sb.x ? 1u : 0u) << par;
