@@ -583,9 +583,11 @@ int orbfe_stereo_match_batch(orbfe_extractor* left, int lbase, int lstep, orbfe_
                   left->last_counts, lbase, lstep};
     StereoSide SR{right->d_ptrs, right->last_pitch, right->d_pyr, right->g.pyr_bytes, right->last_kps,
                   right->last_desc, right->last_counts, rbase, rstep};
-    StereoArgs sa{bf, fx, g.kp_cap};
-    const size_t lds = (size_t)g.kp_cap * (32 + sizeof(RightRec)) + 4 * 512 + 4 * 128 * 4;
-    if (lds > 160 * 1024 || g.kp_cap > ST_SORT || g.kp_cap > 65535) return ORBFE_E_ARG;
+    int sort_cap = 1;
+    while (sort_cap < g.kp_cap) sort_cap <<= 1;
+    StereoArgs sa{bf, fx, g.kp_cap, sort_cap};
+    const size_t lds = (size_t)g.kp_cap * (32 + sizeof(RightRec)) + (size_t)sort_cap * 4 + (ST_NT / 64) * (512 + 128 * 4);
+    if (lds > 160 * 1024 - 64 || g.kp_cap > ST_SORT || g.kp_cap > 65535) return ORBFE_E_ARG;
     hipStream_t s = pick_stream(left, stream);
     std::lock_guard<std::mutex> lk(left->mu_stereo);
     if (left->sdist_frames < nframes) {
@@ -593,7 +595,7 @@ int orbfe_stereo_match_batch(orbfe_extractor* left, int lbase, int lstep, orbfe_
         HIPCHK(hipMalloc(&left->d_sdist, (size_t)nframes * g.kp_cap * 4));
         left->sdist_frames = nframes;
     }
-    hipLaunchKernelGGL(k_stereo, dim3((g.kp_cap + ST_LK - 1) / ST_LK, nframes), dim3(256), lds, s, g, SL, SR, sa,
+    hipLaunchKernelGGL(k_stereo, dim3((g.kp_cap + ST_LK - 1) / ST_LK, nframes), dim3(ST_NT), lds, s, g, SL, SR, sa,
                        d_uright, d_depth, left->d_sdist);
     hipLaunchKernelGGL(k_stereo_cut, dim3(nframes), dim3(256), 0, s, g, SL, sa, d_uright, d_depth, left->d_sdist,
                        d_nmatch);

@@ -1356,6 +1356,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
 struct StereoArgs {
     float bf, fx;
     int max_kp;
+    int sort_cap;   // power of two >= max_kp (LDS sort keys)
 };
 // One side (left or right camera) of a batch of frames: image f of this side is image
 // (base + f*step) of the extractor batch whose buffers are given here.
@@ -1375,47 +1376,77 @@ __device__ __forceinline__ int hamming32(const uint32_t* a, const uint32_t* b) {
     for (int i = 0; i < 8; i++) d += __popc(a[i] ^ b[i]);
     return d;
 }
-// Stage 1: one wave per left keypoint (4 per block), ST_LK left keypoints per block; the right
-// keypoints (x, row band, octave) and descriptors of the frame are staged in LDS once per block.
+// Stage 1: one wave per left keypoint (16 per block), ST_LK left keypoints per block; the right
+// keypoints (x, row band, octave) and descriptors of the frame are staged in LDS once per block
+// and the records are sorted by the first row of their band, so a left keypoint on row v scans
+// only the records with minr in [v - maxspan, v] (the reference's vRowIndices[v] superset; the
+// first-best-in-iR-order rule is kept by the (dist, iR) key).
 // Writes per left kp: uRight, depth (-1 = none) and the SAD distance of an accepted match (-1).
-#define ST_LK 64
+#define ST_LK 256
+#define ST_NT 1024
 struct RightRec { float x; int minr, maxr, oct; };
-__global__ __launch_bounds__(256) void k_stereo(OrbGeom g, StereoSide SL, StereoSide SR, StereoArgs sa,
-                                                float* uright, float* depth, int* sdist) {
+__global__ __launch_bounds__(ST_NT) void k_stereo(OrbGeom g, StereoSide SL, StereoSide SR, StereoArgs sa,
+                                                  float* uright, float* depth, int* sdist) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_st[];
+    __shared__ int s_maxspan;
     const int f = blockIdx.y;
     const int bL = SL.base + f * SL.step, bR = SR.base + f * SR.step;
     const int wave = threadIdx.x >> 6, lane = lane_id();
     const int N = SL.counts[2 * bL], Nr = SR.counts[2 * bR];
     const int i0 = blockIdx.x * ST_LK;
     if (i0 >= N) return;
+    int P = 1;
+    while (P < Nr) P <<= 1;
     uint32_t* s_descR = (uint32_t*)smem_st;                        // sa.max_kp * 8 words
     RightRec* s_rec = (RightRec*)(s_descR + 8 * sa.max_kp);        // sa.max_kp records
-    uint8_t* s_win = (uint8_t*)(s_rec + sa.max_kp) + wave * 512;   // per wave: IL 11x11 @0, IR 11x21 @128
-    int* s_part = (int*)((uint8_t*)(s_rec + sa.max_kp) + 4 * 512) + wave * 128;
+    uint32_t* s_key = (uint32_t*)(s_rec + sa.max_kp);              // sort keys, sa.sort_cap entries
+    uint8_t* s_win = (uint8_t*)(s_key + sa.sort_cap) + wave * 512; // per wave: IL 11x11 @0, IR 11x21 @128
+    int* s_part = (int*)((uint8_t*)(s_key + sa.sort_cap) + (ST_NT / 64) * 512) + wave * 128;
     const OrbKeyPoint* kR = SR.kps + (size_t)bR * g.kp_cap;
     const OrbKeyPoint* kL = SL.kps + (size_t)bL * g.kp_cap;
     const uint4* dR = (const uint4*)(SR.desc + (size_t)bR * g.kp_cap * 32);
     const uint32_t* dL = (const uint32_t*)(SL.desc + (size_t)bL * g.kp_cap * 32);
-    for (int i = threadIdx.x; i < Nr * 2; i += blockDim.x) ((uint4*)s_descR)[i] = dR[i];
-    for (int i = threadIdx.x; i < Nr; i += blockDim.x) {
-        const OrbKeyPoint kp = kR[i];
-        const float r = 2.0f * g.lv[kp.octave].scale;
-        RightRec rr;
-        rr.x = kp.x;
-        rr.oct = kp.octave;
-        rr.maxr = (int)ceilf(kp.y + r);
-        rr.minr = (int)floorf(kp.y - r);
-        s_rec[i] = rr;
-    }
+    if (threadIdx.x == 0) s_maxspan = 0;
     SYNC();
+    for (int i = threadIdx.x; i < Nr * 2; i += blockDim.x) ((uint4*)s_descR)[i] = dR[i];
+    int span = 0;
+    for (int i = threadIdx.x; i < P; i += blockDim.x) {
+        uint32_t key = 0xFFFFFFFFu;
+        if (i < Nr) {
+            const OrbKeyPoint kp = kR[i];
+            const float r = 2.0f * g.lv[kp.octave].scale;
+            RightRec rr;
+            rr.x = kp.x;
+            rr.oct = kp.octave;
+            rr.maxr = (int)ceilf(kp.y + r);
+            rr.minr = (int)floorf(kp.y - r);
+            s_rec[i] = rr;
+            span = max(span, rr.maxr - rr.minr);
+            key = ((uint32_t)(rr.minr + 1024) << 16) | (uint32_t)i;
+        }
+        s_key[i] = key;
+    }
+    atomicMax(&s_maxspan, span);
+    SYNC();
+    for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < P; i += blockDim.x) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const uint32_t a = s_key[i], c = s_key[ixj];
+                    if ((a > c) == ((i & k) == 0)) { s_key[i] = c; s_key[ixj] = a; }
+                }
+            }
+            SYNC();
+        }
+    const int maxspan = s_maxspan;
     float* uR_out = uright + (size_t)f * g.kp_cap;
     float* dp_out = depth + (size_t)f * g.kp_cap;
     int* sd_out = sdist + (size_t)f * g.kp_cap;
     const float mb = sa.bf / sa.fx;   // intended mb = mbf/fx (the reference reads it uninitialised)
     const float minZ = mb, minD = 0.f, maxD = sa.bf / minZ;
     const int iend = min(N, i0 + ST_LK);
-    for (int iL = i0 + wave; iL < iend; iL += 4) {
+    for (int iL = i0 + wave; iL < iend; iL += ST_NT / 64) {
         float outU = -1.0f, outD = -1.0f;
         int outS = -1;
         const OrbKeyPoint kpL = kL[iL];
@@ -1428,7 +1459,19 @@ __global__ __launch_bounds__(256) void k_stereo(OrbGeom g, StereoSide SL, Stereo
         for (int k = 0; k < 8; k++) dl[k] = dL[(size_t)iL * 8 + k];
         int bestKey = 0x7fffffff;   // (dist << 16) | iR: the first best in iR order
         bool anyCand = false;
-        for (int iR = lane; iR < Nr; iR += 64) {
+        // records whose band can contain `row`: minr in [row - maxspan, row]
+        auto lower = [&](uint32_t t) {
+            int lo = 0, hi = Nr;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (s_key[mid] < t) lo = mid + 1; else hi = mid;
+            }
+            return lo;
+        };
+        const int jlo = lower((uint32_t)max(row - maxspan + 1024, 0) << 16);
+        const int jhi = lower((uint32_t)max(row + 1 + 1024, 0) << 16);
+        for (int j = jlo + lane; j < jhi; j += 64) {
+            const int iR = (int)(s_key[j] & 0xFFFFu);
             const RightRec rr = s_rec[iR];
             if (rr.minr <= row && row <= rr.maxr) {
                 anyCand = true;
