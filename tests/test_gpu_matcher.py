@@ -183,3 +183,46 @@ def test_empty_inputs(gpu, om):
     assert (mvp == -1).all()
     g, t, d = stereo_knn_ratio(np.zeros((0, 32), np.uint8), np.zeros((5, 32), np.uint8))
     assert g == 0 and len(t) == 0
+
+
+class _GpuAsOracle:
+    """The product ORBmatcher behind the oracle-style call names used by the fixture runner."""
+
+    def __init__(self, nnratio, checkOri):
+        self.m = ORBmatcher(nnratio, checkOri)
+
+    def sbp_local(self, F, mvp, obs, mps, th, bFar=False, thFar=50.0):
+        return self.m.SearchByProjectionLocalMap(F, mvp, obs, mps, th, bFar, thFar)
+
+    def sbp_lastframe(self, F, mvp, obs, pts, th, fw, bw):
+        return self.m.SearchByProjectionLastFrame(F, mvp, obs, pts, th, fw, bw)
+
+    def sbp_kf(self, F, mvp, pts, th, orbdist):
+        return self.m.SearchByProjectionKeyFrame(F, mvp, pts, th, orbdist)
+
+    def search_for_init(self, F1, F2, prev, m12, window):
+        return self.m.SearchForInitialization(F1, F2, prev, m12, window)
+
+    def search_by_bow(self, kk, kd, kmp, fk, F, ff):
+        return self.m.SearchByBoW(kk, kd, kmp, fk, F, ff)
+
+
+def test_gpu_matcher_golden(gpu):
+    """The HIP matchers reproduce the committed per-query fixtures (tests/golden/matcher_golden.npz)."""
+    import importlib.util
+    import os
+    here = os.path.dirname(os.path.abspath(__file__))
+    spec = importlib.util.spec_from_file_location("make_matcher_golden",
+                                                  os.path.join(here, "golden", "make_matcher_golden.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    gold = np.load(os.path.join(here, "golden", "matcher_golden.npz"), allow_pickle=False)
+    for name, kind, d in mod.cases():
+        assert np.array_equal(mod.input_digest(kind, d), gold[name + "_in"]), f"{name}: generator drifted"
+        if kind == "knn":
+            res = stereo_knn_ratio(d["L"], d["R"])
+        else:
+            res = mod.run(_GpuAsOracle, kind, d)
+        assert res[0] == int(gold[name + "_n"][0]), name
+        for i, a in enumerate(res[1:]):
+            assert np.array_equal(np.asarray(a), gold[f"{name}_out{i}"]), f"{name} output {i}"

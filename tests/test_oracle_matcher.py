@@ -215,3 +215,26 @@ def test_record_layouts():
     assert sm.MAP_POINT_DTYPE.itemsize == 80 and sm.PROJ_POINT_DTYPE.itemsize == 64
     assert ctypes.sizeof(CFrame) == 72 and CFrame.mbf.offset == 64
     assert ctypes.sizeof(CFeatureVector) == 32
+
+
+def _golden_cases():
+    import importlib.util
+    import os
+    here = os.path.dirname(os.path.abspath(__file__))
+    spec = importlib.util.spec_from_file_location("make_matcher_golden",
+                                                  os.path.join(here, "golden", "make_matcher_golden.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    gold = np.load(os.path.join(here, "golden", "matcher_golden.npz"), allow_pickle=False)
+    return mod, gold
+
+
+def test_oracle_matcher_golden(oracle_lib):
+    """The oracle reproduces the committed per-query fixtures (regression pin)."""
+    mod, gold = _golden_cases()
+    for name, kind, d in mod.cases():
+        assert np.array_equal(mod.input_digest(kind, d), gold[name + "_in"]), f"{name}: generator drifted"
+        res = mod.run(oracle_lib.OracleMatcher, kind, d)
+        assert res[0] == int(gold[name + "_n"][0]), name
+        for i, a in enumerate(res[1:]):
+            assert np.array_equal(np.asarray(a), gold[f"{name}_out{i}"]), f"{name} output {i}"
