@@ -42,6 +42,18 @@ __constant__ int c_ring_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// Workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share one, each XCD has its
+// own L2): remap the linear block id so every XCD walks one contiguous range of logical blocks and
+// neighbouring tiles / cells / keypoints (which share halo rows and cache lines) share an L2.
+__device__ __forceinline__ int xcd_logical(int bid, int total) {
+    const int q = total >> 3, r = total & 7;
+    const int x = bid & 7, sl = bid >> 3;
+    return x * q + min(x, r) + sl;
+}
+__device__ __forceinline__ int block_linear() {
+    return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+}
+
 __device__ __forceinline__ int wave_incl_scan(int v) {
     const int lane = lane_id();
 #pragma unroll
@@ -121,9 +133,11 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t* const* imgs, int 
     __shared__ int s_ty[RZ_TR][4];
     const OrbLevel& L = g.lv[l];
     const OrbLevel& Ps = g.lv[l - 1];
-    const int b = blockIdx.z, t = threadIdx.x;
+    const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y * gridDim.z);
+    const int bx = lb % gridDim.x, by = (lb / gridDim.x) % gridDim.y;
+    const int b = lb / (gridDim.x * gridDim.y), t = threadIdx.x;
     const int TR = L.rz_rows, TC = L.rz_cols;
-    const int y0 = blockIdx.y * TR, x0 = blockIdx.x * TC;
+    const int y0 = by * TR, x0 = bx * TC;
     const int y1 = min(y0 + TR, L.h), x1 = min(x0 + TC, L.w);
     int spitch;
     gptr_u8 src = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l - 1, &spitch);
@@ -412,12 +426,13 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
                                               uint32_t* cellkeys, int* cellcnt, int ablate) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_fast[];
     const int wave = threadIdx.x >> 6, lane = lane_id();
-    const int b = blockIdx.y;
+    const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
+    const int bx = lb % gridDim.x, b = lb / gridDim.x;
     // per wave: ROI image | score map | entry list (<= 2 entries per detection pixel)
     uint8_t* s_img = smem_fast + wave * (2 * roi_max + cand_bytes);
     uint8_t* s_sc = s_img + roi_max;
     uint16_t* s_cand = (uint16_t*)(s_sc + roi_max);
-    const int cbeg = (blockIdx.x * 4 + wave) * FAST_CPW;
+    const int cbeg = (bx * 4 + wave) * FAST_CPW;
     if (cbeg >= g.total_cells) return;
     const int cend = min(cbeg + FAST_CPW, g.total_cells);
     const int th = g.min_th;
@@ -1205,8 +1220,9 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
                                                   OrbKeyPoint* kps, uint8_t* desc, int* counts, BlurKernel bk) {
     __shared__ __attribute__((aligned(16))) uint8_t s_dp[4][DP_WAVE_LDS];
     const int wave = threadIdx.x >> 6, lane = lane_id();
-    const int b = blockIdx.y;
-    const int flat = blockIdx.x * 4 + wave;   // index over all levels' output slots
+    const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
+    const int b = lb / gridDim.x;
+    const int flat = (lb % gridDim.x) * 4 + wave;   // index over all levels' output slots
     if (flat >= g.out_per_img) return;
     int l = 0;
     while (l + 1 < g.nlevels && flat >= g.lv[l + 1].out_off) l++;
@@ -1389,11 +1405,12 @@ __global__ __launch_bounds__(ST_NT) void k_stereo(OrbGeom g, StereoSide SL, Ster
                                                   float* uright, float* depth, int* sdist) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_st[];
     __shared__ int s_maxspan;
-    const int f = blockIdx.y;
+    const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
+    const int f = lb / gridDim.x;
     const int bL = SL.base + f * SL.step, bR = SR.base + f * SR.step;
     const int wave = threadIdx.x >> 6, lane = lane_id();
     const int N = SL.counts[2 * bL], Nr = SR.counts[2 * bR];
-    const int i0 = blockIdx.x * ST_LK;
+    const int i0 = (lb % gridDim.x) * ST_LK;
     if (i0 >= N) return;
     int P = 1;
     while (P < Nr) P <<= 1;
