@@ -141,6 +141,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stage-steps", type=int, default=10, help="extra steps with per-stage HIP events")
     ap.add_argument("--matcher-steps", type=int, default=10, help="config-5 SearchByProjection calls per th (0: skip)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (the measured path); gloo = CPU rehearsal of the multi-rank path")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank uses cuda:0 (rehearse N ranks on a 1-GPU box with --dist-backend gloo)")
     args = ap.parse_args()
 
     import torch
@@ -151,12 +155,16 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_rank = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    gloo = args.dist_backend == "gloo"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     W, H, F = args.width, args.height, args.frames
     bf, fx = 0.110078 * 458.654, 458.654   # EuRoC stereo baseline x fx
@@ -172,12 +180,16 @@ def main():
         sb = odist.slot_bytes(fe.cap)
         local_slots = torch.empty((2 * F, sb), dtype=torch.uint8, device=dev)
         all_slots = torch.empty((world * 2 * F, sb), dtype=torch.uint8, device=dev)
+        all_slots_host = torch.empty((world * 2 * F, sb), dtype=torch.uint8) if gloo else None
 
     def step():
         fe.run(images)
         if gather:
             odist.pack_slots(fe.counts, fe.kps, fe.desc, local_slots)
-            odist.allgather_slots(local_slots, all_slots)
+            if gloo:   # gloo gathers host tensors
+                odist.allgather_slots(local_slots.cpu(), all_slots_host)
+            else:
+                odist.allgather_slots(local_slots, all_slots)
 
     for _ in range(args.warmup):
         step()
@@ -192,7 +204,7 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device="cpu" if gloo else dev)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
@@ -240,6 +252,7 @@ def main():
                 "images_per_gpu_per_step": 2 * F,
                 "width": W, "height": H,
                 "allgather": gather,
+                "allgather_backend": (args.dist_backend if gather else None),
                 "pipelines": args.pipelines,
                 "parallelism": f"frame-sharded x{world}",
             },
