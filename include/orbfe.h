@@ -217,6 +217,47 @@ int orbfe_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, c
 int orbfe_stereo_knn_ratio(const uint8_t* left_desc, int32_t nl, const uint8_t* right_desc, int32_t nr,
                            float ratio, int32_t* out_train, int32_t* out_dist);
 
+/* ---------------------------------------------------------------------------------------------
+ * Local-map projection (the step before SearchByProjection in Tracking::SearchLocalPoints,
+ * Tracking.cc:3407-3452): Frame::isInFrustum (pinhole branch, Frame.cc:512-570) and
+ * MapPoint::PredictScale (MapPoint.cc:531-546) for every local map point, on the device.
+ * ------------------------------------------------------------------------------------------- */
+#define ORBFE_MP_SKIP 4              /* mnLastFrameSeen == current frame id: not projected */
+typedef struct orbfe_map_point_3d {
+    float pos[3];                    /* GetWorldPos() */
+    float normal[3];                 /* GetNormal() */
+    float min_dist, max_dist;        /* mfMinDistance, mfMaxDistance (GetMin/MaxDistanceInvariance scale them) */
+    int32_t flags;                   /* ORBFE_MP_BAD (isBad()), ORBFE_MP_SKIP */
+    int32_t observations;            /* Observations() */
+    int32_t id;                      /* handle stored into mvpMapPoints */
+    int32_t reserved;
+    uint8_t desc[32];                /* GetDescriptor() */
+} orbfe_map_point_3d;                /* 80 bytes */
+
+typedef struct orbfe_camera {
+    float Rcw[9];                    /* Frame::mRcw, row-major */
+    float tcw[3];                    /* Frame::mtcw */
+    float Ow[3];                     /* Frame::mOw (camera centre in the world) */
+    float fx, fy, cx, cy;            /* Pinhole mvParameters (Pinhole.cpp:43-49) */
+    float log_scale_factor;          /* Frame::mfLogScaleFactor */
+    float view_cos_limit;            /* 0.5 in SearchLocalPoints */
+} orbfe_camera;
+
+/* isInFrustum + PredictScale for n points: writes the tracking snapshot of each point to
+ * track[i] (mbTrackInView -> ORBFE_MP_IN_VIEW, mTrackProjX/Y/XR, mTrackDepth, mTrackViewCos,
+ * mnTrackScaleLevel; ORBFE_MP_BAD kept; desc / observations / id copied) and returns the number in
+ * view (nToMatch). Arithmetic: float, no FMA contraction, Eigen's left-to-right sums, glibc logf. */
+int orbfe_is_in_frustum(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* pts, int32_t n,
+                        orbfe_map_point* track);
+
+/* Tracking::SearchLocalPoints' projection + matching in one device pass: isInFrustum over pts,
+ * then (if any point is in view) SearchByProjection(F, points, th, bFarPoints, thFarPoints) with
+ * ratio nnratio. mvp / mvp_obs as orbfe_search_by_projection_local. *n_to_match (may be NULL)
+ * receives nToMatch. Returns nmatches. */
+int orbfe_search_local_points(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* pts,
+                              int32_t n, int32_t* mvp, const int32_t* mvp_obs, float th, int32_t bFarPoints,
+                              float thFarPoints, float nnratio, int32_t* n_to_match);
+
 /* Per calling thread: when enabled, every matcher call above records HIP events around its
  * kernels (after the input upload, before the result copy); orbfe_matcher_last_ms returns that
  * device time of the thread's last call in ms (-1 when not timed). For bench.py. */

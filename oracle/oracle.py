@@ -135,6 +135,8 @@ def _match_sigs(L):
     L.oro_search_for_init.argtypes = [vp, vp, vp, vp, ci, cf, ci]
     L.oro_search_by_bow.argtypes = [vp, vp, vp, ci, vp, vp, vp, vp, cf, ci]
     L.oro_stereo_knn_ratio.argtypes = [vp, ci, vp, ci, cf, vp, vp]
+    L.oro_is_in_frustum.argtypes = [vp, vp, vp, ci, vp]
+    L.oro_search_local_points.argtypes = [vp, vp, vp, ci, vp, vp, cf, ci, cf, cf, vp]
     return L
 
 
@@ -171,6 +173,26 @@ class OracleMatcher:
         n = self.L.oro_search_by_bow(kk.ctypes.data, kd.ctypes.data, km.ctypes.data, len(km), kf_fv.ref(), F.ref(),
                                      f_fv.ref(), out.ctypes.data, self.nnratio, self.checkOri)
         return n, out
+
+
+def is_in_frustum(F, cam, pts3d):
+    """(nToMatch, tracking records) — the caller passes MAP_POINT_DTYPE / MAP_POINT_3D_DTYPE arrays."""
+    from orb_slam3_ros_amd.matcher import MAP_POINT_DTYPE
+    L = _match_sigs(lib())
+    pts = np.ascontiguousarray(pts3d)
+    track = np.zeros(len(pts), MAP_POINT_DTYPE)
+    n = L.oro_is_in_frustum(F.ref(), ctypes.byref(cam), pts.ctypes.data, len(pts), track.ctypes.data)
+    return n, track
+
+
+def search_local_points(F, cam, pts3d, mvp, mvp_obs, th=1.0, bFar=False, thFar=50.0, nnratio=0.8):
+    L = _match_sigs(lib())
+    pts = np.ascontiguousarray(pts3d)
+    ntm = ctypes.c_int32(0)
+    n = L.oro_search_local_points(F.ref(), ctypes.byref(cam), pts.ctypes.data, len(pts), mvp.ctypes.data,
+                                  mvp_obs.ctypes.data, float(th), int(bFar), float(thFar), float(nnratio),
+                                  ctypes.byref(ntm))
+    return n, int(ntm.value)
 
 
 def stereo_knn_ratio(left_desc, right_desc, ratio=0.7):

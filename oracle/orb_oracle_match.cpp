@@ -12,6 +12,10 @@
 //   ORBmatcher::SearchByProjection (KF)      ORBmatcher.cc:1889-2010     -> oro_sbp_kf()
 //   ORBmatcher::ComputeThreeMaxima           ORBmatcher.cc:2012-2053     -> three_maxima()
 //   Frame::ComputeStereoFishEyeMatches kNN   Frame.cc:1126-1151          -> oro_stereo_knn_ratio()
+//   Frame::isInFrustum (pinhole)             Frame.cc:512-570            -> oro_is_in_frustum()
+//   MapPoint::PredictScale                   MapPoint.cc:531-546
+//   Tracking::SearchLocalPoints (projection + SearchByProjection)  Tracking.cc:3404-3453
+//                                                                        -> oro_search_local_points()
 // Only the pinhole / rectified branches (F.Nleft == -1) are restated; the KannalaBrandt8
 // right-camera branches are out of scope.
 // ============================================================================================
@@ -349,6 +353,79 @@ int oro_stereo_knn_ratio(const uint8_t* L, int32_t nl, const uint8_t* R, int32_t
         if (nr >= 2 && (float)d0 < (float)d1 * (double)ratio) { out_train[i] = t0; out_dist[i] = d0; good++; }
     }
     return good;
+}
+
+// Frame::isInFrustum, pinhole branch (Frame.cc:512-570), with Eigen's evaluation order spelled
+// out: (R*P)(i) = (R(i,0)*P0 + R(i,1)*P1) + R(i,2)*P2, norm = sqrt((x*x + y*y) + z*z), dot left to
+// right; Pinhole::project = fx * x / z + cx (Pinhole.cpp:43-49). PredictScale with the C library
+// logf (log(float) resolves to it through OpenCV's <math.h>).
+static bool is_in_frustum(const orbfe_frame* F, const orbfe_camera* c, const orbfe_map_point_3d& p,
+                          orbfe_map_point& t) {
+    t.flags &= ~ORBFE_MP_IN_VIEW;
+    t.proj_x = -1;
+    t.proj_y = -1;
+    const float P0 = p.pos[0], P1 = p.pos[1], P2 = p.pos[2];
+    float Pc[3];
+    for (int i = 0; i < 3; i++) {
+        const float* R = c->Rcw + 3 * i;
+        Pc[i] = ((R[0] * P0 + R[1] * P1) + R[2] * P2) + c->tcw[i];
+    }
+    const float Pc_dist = std::sqrt((Pc[0] * Pc[0] + Pc[1] * Pc[1]) + Pc[2] * Pc[2]);
+    const float PcZ = Pc[2];
+    const float invz = 1.0f / PcZ;
+    if (PcZ < 0.0f) return false;
+    const float u = c->fx * Pc[0] / Pc[2] + c->cx;
+    const float v = c->fy * Pc[1] / Pc[2] + c->cy;
+    if (u < F->min_x || u > F->max_x) return false;
+    if (v < F->min_y || v > F->max_y) return false;
+    t.proj_x = u;
+    t.proj_y = v;
+    const float maxDistance = 1.2f * p.max_dist, minDistance = 0.8f * p.min_dist;
+    const float PO0 = P0 - c->Ow[0], PO1 = P1 - c->Ow[1], PO2 = P2 - c->Ow[2];
+    const float dist = std::sqrt((PO0 * PO0 + PO1 * PO1) + PO2 * PO2);
+    if (dist < minDistance || dist > maxDistance) return false;
+    const float viewCos = ((PO0 * p.normal[0] + PO1 * p.normal[1]) + PO2 * p.normal[2]) / dist;
+    if (viewCos < c->view_cos_limit) return false;
+    const float ratio = p.max_dist / dist;
+    int nScale = (int)std::ceil(logf(ratio) / c->log_scale_factor);
+    if (nScale < 0) nScale = 0;
+    else if (nScale >= F->nlevels) nScale = F->nlevels - 1;
+    t.flags |= ORBFE_MP_IN_VIEW;
+    t.proj_x = u;
+    t.proj_xr = u - F->mbf * invz;
+    t.depth = Pc_dist;
+    t.proj_y = v;
+    t.scale_level = nScale;
+    t.view_cos = viewCos;
+    return true;
+}
+
+int oro_is_in_frustum(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* pts, int32_t n,
+                      orbfe_map_point* track) {
+    int nToMatch = 0;
+    for (int i = 0; i < n; i++) {
+        const orbfe_map_point_3d& p = pts[i];
+        orbfe_map_point& t = track[i];
+        memset(&t, 0, sizeof(t));
+        t.flags = p.flags & ORBFE_MP_BAD;
+        t.observations = p.observations;
+        t.id = p.id;
+        memcpy(t.desc, p.desc, 32);
+        if (p.flags & ORBFE_MP_SKIP) continue;   // mnLastFrameSeen == current: mbTrackInView = false
+        if (p.flags & ORBFE_MP_BAD) continue;
+        if (is_in_frustum(F, cam, p, t)) nToMatch++;
+    }
+    return nToMatch;
+}
+
+int oro_search_local_points(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* pts, int32_t n,
+                            int32_t* mvp, const int32_t* mvp_obs, float th, int32_t bFarPoints, float thFarPoints,
+                            float nnratio, int32_t* n_to_match) {
+    std::vector<orbfe_map_point> track(n > 0 ? n : 1);
+    const int nToMatch = oro_is_in_frustum(F, cam, pts, n, track.data());
+    if (n_to_match) *n_to_match = nToMatch;
+    if (nToMatch <= 0) return 0;
+    return oro_sbp_local(F, mvp, mvp_obs, track.data(), n, th, bFarPoints, thFarPoints, nnratio);
 }
 
 }  // extern "C"

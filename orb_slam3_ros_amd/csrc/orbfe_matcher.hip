@@ -13,6 +13,7 @@
 // keypoint index inside a cell: the grid is rebuilt with a stable (cell, index) sort), so the
 // reference's strict-< "first best wins" and best/second-best bookkeeping are reproduced verbatim.
 #pragma once
+#include "glibc_logf.h"
 
 #define MT_NT 256
 #define MT_TH_HIGH 100
@@ -370,6 +371,69 @@ __global__ __launch_bounds__(MT_NT) void k_sbp_proj(FrameDev fr, const orbfe_pro
         assign[q] = result;
         atomicAdd(changed, 1);
     }
+}
+
+// ---- Frame::isInFrustum (pinhole, Frame.cc:512-570) + MapPoint::PredictScale (MapPoint.cc:531-546)
+// for every local map point (Tracking.cc:3407-3425): one thread per point, float arithmetic in the
+// reference's (Eigen's) order, no contraction, glibc logf port. Writes the tracking snapshot the
+// SearchByProjection kernels read and counts nToMatch.
+struct CamDev {
+    float R[9], t[3], Ow[3], fx, fy, cx, cy, logsf, cos_limit;
+    float minx, maxx, miny, maxy, mbf;
+    int nlevels;
+};
+__global__ __launch_bounds__(MT_NT) void k_frustum(CamDev c, const orbfe_map_point_3d* pts, int n,
+                                                   orbfe_map_point* track, int* n_to_match) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const orbfe_map_point_3d p = pts[i];
+    orbfe_map_point t;
+    t.proj_x = -1.f; t.proj_y = -1.f; t.proj_xr = 0.f; t.view_cos = 0.f; t.depth = 0.f;
+    t.scale_level = 0;
+    t.flags = p.flags & ORBFE_MP_BAD;
+    t.observations = p.observations;
+    t.id = p.id;
+    t.reserved[0] = t.reserved[1] = t.reserved[2] = 0;
+    memcpy(t.desc, p.desc, 32);
+    bool in = false;
+    if (!(p.flags & (ORBFE_MP_SKIP | ORBFE_MP_BAD))) {
+        const float P0 = p.pos[0], P1 = p.pos[1], P2 = p.pos[2];
+        float Pc[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) Pc[k] = ((c.R[3 * k] * P0 + c.R[3 * k + 1] * P1) + c.R[3 * k + 2] * P2) + c.t[k];
+        const float Pc_dist = sqrtf((Pc[0] * Pc[0] + Pc[1] * Pc[1]) + Pc[2] * Pc[2]);
+        const float PcZ = Pc[2];
+        const float invz = 1.0f / PcZ;
+        if (!(PcZ < 0.0f)) {
+            const float u = c.fx * Pc[0] / Pc[2] + c.cx;
+            const float v = c.fy * Pc[1] / Pc[2] + c.cy;
+            if (!(u < c.minx || u > c.maxx) && !(v < c.miny || v > c.maxy)) {
+                t.proj_x = u;
+                t.proj_y = v;
+                const float maxDistance = 1.2f * p.max_dist, minDistance = 0.8f * p.min_dist;
+                const float PO0 = P0 - c.Ow[0], PO1 = P1 - c.Ow[1], PO2 = P2 - c.Ow[2];
+                const float dist = sqrtf((PO0 * PO0 + PO1 * PO1) + PO2 * PO2);
+                if (!(dist < minDistance || dist > maxDistance)) {
+                    const float viewCos = ((PO0 * p.normal[0] + PO1 * p.normal[1]) + PO2 * p.normal[2]) / dist;
+                    if (!(viewCos < c.cos_limit)) {
+                        const float ratio = p.max_dist / dist;
+                        int nScale = (int)ceilf(glibc_logf(ratio) / c.logsf);
+                        if (nScale < 0) nScale = 0;
+                        else if (nScale >= c.nlevels) nScale = c.nlevels - 1;
+                        t.flags |= ORBFE_MP_IN_VIEW;
+                        t.proj_xr = u - c.mbf * invz;
+                        t.depth = Pc_dist;
+                        t.scale_level = nScale;
+                        t.view_cos = viewCos;
+                        in = true;
+                    }
+                }
+            }
+        }
+    }
+    track[i] = t;
+    const unsigned long long m = __ballot(in);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(n_to_match, __popcll(m));
 }
 
 // rotation-histogram bin of an accepted match (ORBmatcher.cc:1775-1792): round(rot * (1/30)).
@@ -814,16 +878,27 @@ inline void fill(int* p, int n, int v) {
 
 // Shared driver of the three slot-assigning SearchByProjection variants.
 // mode: 0 local map, 1 last frame, 2 keyframe.
+// Local-map projection feeding sbp_run (mode 0): the query records are produced on the device by
+// k_frustum from map point geometry instead of being uploaded.
+struct FrustumIn {
+    const orbfe_camera* cam;
+    const orbfe_map_point_3d* pts;
+    int32_t* n_to_match;
+};
+
 int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, const void* queries, int nq,
             size_t qstride, size_t qobs_off, size_t qid_off, size_t qangle_off, size_t qlevel_off, float th, int a0, int a1, float thFar,
-            float nnratio, int maxDist, int checkOri) {
-    if (!frame_ok(F) || !mvp || nq < 0 || (nq > 0 && !queries)) return ORBFE_E_ARG;
+            float nnratio, int maxDist, int checkOri, const FrustumIn* fin = nullptr) {
+    if (!frame_ok(F) || !mvp || nq < 0 || (nq > 0 && !queries && !fin)) return ORBFE_E_ARG;
+    if (fin && (!fin->cam || (nq > 0 && !fin->pts) || mode != 0)) return ORBFE_E_ARG;
     if (mode != 2 && !mvp_obs) return ORBFE_E_ARG;
+    if (fin && fin->n_to_match) *fin->n_to_match = 0;
     if (F->n == 0 || nq == 0) return 0;
     if (nq > (1 << 24)) return ORBFE_E_CAPACITY;
     const int n = F->n;
     // level indices address mvScaleFactors: reject out-of-range ones instead of reading past it
-    for (int j = 0; j < nq; j++) {
+    // (frustum-produced levels are clamped to [0, nlevels) by PredictScale)
+    for (int j = 0; !fin && j < nq; j++) {
         const uint8_t* rec = (const uint8_t*)queries + (size_t)j * qstride;
         const bool used = mode == 0 ? (((const orbfe_map_point*)rec)->flags & ORBFE_MP_IN_VIEW) != 0
                                     : ((const orbfe_proj_point*)rec)->valid != 0;
@@ -835,10 +910,13 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     Plan p;
     FramePlan fp;
     fp.plan(p, F, true, mode != 2);
-    const size_t o_q = p.upload(queries, (size_t)nq * qstride);
+    const size_t o_q = fin ? p.upload(fin->pts, (size_t)nq * sizeof(orbfe_map_point_3d))
+                           : p.upload(queries, (size_t)nq * qstride);
     const size_t o_b0 = p.upload(blocked0.data(), (size_t)n * 4);
     const size_t o_mvp = p.upload(mvp, (size_t)n * 4);
     fp.plan_grid(p, mode == 0 ? F->nlevels + 1 : 1);
+    const size_t o_track = fin ? p.scratch((size_t)nq * sizeof(orbfe_map_point)) : 0;
+    const size_t o_ntm = fin ? p.scratch(16) : 0;
     const size_t o_first = p.scratch((size_t)n * 4);
     const size_t o_assign = p.scratch((size_t)nq * 4);
     const size_t o_changed = p.scratch(MT_MAX_PASSES * 4);
@@ -855,6 +933,29 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     HIPCHK(hipMemsetAsync(changed, 0, MT_MAX_PASSES * 4, s));
     fill(assign, nq, -1);
     const uint8_t* q = ms_ptr<const uint8_t>(o_q);
+    if (fin) {   // Tracking::SearchLocalPoints: project, count nToMatch, match only if > 0
+        const orbfe_camera& c = *fin->cam;
+        CamDev cd;
+        memcpy(cd.R, c.Rcw, sizeof(cd.R));
+        memcpy(cd.t, c.tcw, sizeof(cd.t));
+        memcpy(cd.Ow, c.Ow, sizeof(cd.Ow));
+        cd.fx = c.fx; cd.fy = c.fy; cd.cx = c.cx; cd.cy = c.cy;
+        cd.logsf = c.log_scale_factor;
+        cd.cos_limit = c.view_cos_limit;
+        cd.minx = F->min_x; cd.maxx = F->max_x; cd.miny = F->min_y; cd.maxy = F->max_y;
+        cd.mbf = F->mbf;
+        cd.nlevels = F->nlevels;
+        int* ntm = ms_ptr<int>(o_ntm);
+        HIPCHK(hipMemsetAsync(ntm, 0, 4, s));
+        hipLaunchKernelGGL(k_frustum, dim3((nq + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, cd,
+                           ms_ptr<const orbfe_map_point_3d>(o_q), nq, ms_ptr<orbfe_map_point>(o_track), ntm);
+        int h_ntm = 0;
+        HIPCHK(hipMemcpyAsync(&h_ntm, ntm, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (fin->n_to_match) *fin->n_to_match = h_ntm;
+        if (h_ntm <= 0) return 0;
+        q = ms_ptr<const uint8_t>(o_track);
+    }
     const dim3 gq((nq + MT_NT - 1) / MT_NT);
     const bool staged = n <= MT_STAGE_MAX;
     int pass = 0;
@@ -1084,6 +1185,51 @@ int orbfe_stereo_knn_ratio(const uint8_t* left_desc, int32_t nl, const uint8_t* 
     int good = 0;
     for (int i = 0; i < nl; i++) good += out_train[i] >= 0;
     return good;
+}
+
+int orbfe_search_local_points(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* pts,
+                              int32_t n, int32_t* mvp, const int32_t* mvp_obs, float th, int32_t bFarPoints,
+                              float thFarPoints, float nnratio, int32_t* n_to_match) {
+    const FrustumIn fin{cam, pts, n_to_match};
+    return sbp_run(0, F, mvp, mvp_obs, nullptr, n, sizeof(orbfe_map_point), offsetof(orbfe_map_point, observations),
+                   offsetof(orbfe_map_point, id), 0, offsetof(orbfe_map_point, scale_level), th, bFarPoints, 0,
+                   thFarPoints, nnratio, 0, 0, &fin);
+}
+
+int orbfe_is_in_frustum(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* pts, int32_t n,
+                        orbfe_map_point* track) {
+    if (!F || !cam || n < 0 || (n > 0 && (!pts || !track)) || F->nlevels <= 0) return ORBFE_E_ARG;
+    if (n == 0) return 0;
+    Plan p;
+    const size_t o_pts = p.upload(pts, (size_t)n * sizeof(orbfe_map_point_3d));
+    const size_t o_track = p.scratch((size_t)n * sizeof(orbfe_map_point));
+    const size_t o_ntm = p.scratch(16);
+    int rc = ms_prepare(p);
+    if (rc) return rc;
+    MsTimer timer;
+    hipStream_t s = t_ms.stream;
+    CamDev cd;
+    memcpy(cd.R, cam->Rcw, sizeof(cd.R));
+    memcpy(cd.t, cam->tcw, sizeof(cd.t));
+    memcpy(cd.Ow, cam->Ow, sizeof(cd.Ow));
+    cd.fx = cam->fx; cd.fy = cam->fy; cd.cx = cam->cx; cd.cy = cam->cy;
+    cd.logsf = cam->log_scale_factor;
+    cd.cos_limit = cam->view_cos_limit;
+    cd.minx = F->min_x; cd.maxx = F->max_x; cd.miny = F->min_y; cd.maxy = F->max_y;
+    cd.mbf = F->mbf;
+    cd.nlevels = F->nlevels;
+    int* ntm = ms_ptr<int>(o_ntm);
+    HIPCHK(hipMemsetAsync(ntm, 0, 4, s));
+    hipLaunchKernelGGL(k_frustum, dim3((n + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, cd,
+                       ms_ptr<const orbfe_map_point_3d>(o_pts), n, ms_ptr<orbfe_map_point>(o_track), ntm);
+    HIPCHK(hipGetLastError());
+    timer.end();
+    int h_ntm = 0;
+    HIPCHK(hipMemcpyAsync(track, ms_ptr<orbfe_map_point>(o_track), (size_t)n * sizeof(orbfe_map_point),
+                          hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&h_ntm, ntm, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return h_ntm;
 }
 
 int orbfe_matcher_set_timing(int enable) {

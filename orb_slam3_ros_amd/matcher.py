@@ -25,8 +25,12 @@ MAP_POINT_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<
 # orbfe_proj_point (64 B): a projected point of the last frame / a keyframe
 PROJ_POINT_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("invzc", "<f4"), ("octave", "<i4"), ("angle", "<f4"),
                              ("valid", "<i4"), ("observations", "<i4"), ("id", "<i4"), ("desc", "u1", (32,))])
-assert MAP_POINT_DTYPE.itemsize == 80 and PROJ_POINT_DTYPE.itemsize == 64
-MP_IN_VIEW, MP_BAD = 1, 2
+# orbfe_map_point_3d (80 B): MapPoint geometry for the local-map projection (Frame::isInFrustum)
+MAP_POINT_3D_DTYPE = np.dtype([("pos", "<f4", (3,)), ("normal", "<f4", (3,)), ("min_dist", "<f4"), ("max_dist", "<f4"),
+                               ("flags", "<i4"), ("observations", "<i4"), ("id", "<i4"), ("reserved", "<i4"),
+                               ("desc", "u1", (32,))])
+assert MAP_POINT_DTYPE.itemsize == 80 and PROJ_POINT_DTYPE.itemsize == 64 and MAP_POINT_3D_DTYPE.itemsize == 80
+MP_IN_VIEW, MP_BAD, MP_SKIP = 1, 2, 4
 TH_HIGH, TH_LOW, HISTO_LENGTH = 100, 50, 30   # ORBmatcher.cc:33-35
 
 
@@ -42,6 +46,32 @@ class CFeatureVector(ctypes.Structure):
     """struct orbfe_feature_vector"""
     _fields_ = [("n_nodes", ctypes.c_int32), ("node_ids", ctypes.c_void_p), ("offsets", ctypes.c_void_p),
                 ("indices", ctypes.c_void_p)]
+
+
+class Camera(ctypes.Structure):
+    """struct orbfe_camera: Frame::mRcw (row-major), mtcw, mOw, pinhole fx fy cx cy,
+    mfLogScaleFactor and the viewing-cosine limit (0.5 in Tracking::SearchLocalPoints)."""
+    _fields_ = [("Rcw", ctypes.c_float * 9), ("tcw", ctypes.c_float * 3), ("Ow", ctypes.c_float * 3),
+                ("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
+                ("log_scale_factor", ctypes.c_float), ("view_cos_limit", ctypes.c_float)]
+
+    @staticmethod
+    def make(Rcw, tcw, fx, fy, cx, cy, scale_factor=1.2, view_cos_limit=0.5):
+        R = np.asarray(Rcw, np.float32).reshape(3, 3)
+        t = np.asarray(tcw, np.float32).reshape(3)
+        Ow = (-(R.astype(np.float64).T @ t.astype(np.float64))).astype(np.float32)   # mOw = -Rcw^T tcw
+        c = Camera()
+        c.Rcw[:] = [float(v) for v in R.reshape(-1)]
+        c.tcw[:] = [float(v) for v in t]
+        c.Ow[:] = [float(v) for v in Ow]
+        c.fx, c.fy, c.cx, c.cy = float(fx), float(fy), float(cx), float(cy)
+        # Frame::mfLogScaleFactor = log(mfScaleFactor) on the float factor: the C library logf
+        libm = ctypes.CDLL("libm.so.6")
+        libm.logf.restype = ctypes.c_float
+        libm.logf.argtypes = [ctypes.c_float]
+        c.log_scale_factor = float(libm.logf(float(np.float32(scale_factor))))
+        c.view_cos_limit = float(view_cos_limit)
+        return c
 
 
 class MatchFrame:
@@ -179,6 +209,33 @@ class ORBmatcher:
             kk.ctypes.data, kd.ctypes.data, km.ctypes.data, len(kk), kf_featvec.ref(), F.ref(), f_featvec.ref(),
             out.ctypes.data, self.mfNNratio, int(self.mbCheckOrientation)), "SearchByBoW")
         return n, out
+
+
+def is_in_frustum(F: MatchFrame, cam: Camera, points3d):
+    """Frame::isInFrustum + MapPoint::PredictScale over points3d (MAP_POINT_3D_DTYPE) on the GPU.
+    Returns (nToMatch, tracking snapshots as MAP_POINT_DTYPE records)."""
+    lib = _lib.load()
+    pts = _records(points3d, MAP_POINT_3D_DTYPE, "points3d")
+    track = np.zeros(len(pts), MAP_POINT_DTYPE)
+    n = _lib.check(lib.orbfe_is_in_frustum(F.ref(), ctypes.byref(cam), pts.ctypes.data, len(pts), track.ctypes.data),
+                   "is_in_frustum")
+    return n, track
+
+
+def search_local_points(F: MatchFrame, cam: Camera, points3d, mvp, mvp_obs, th: float = 1.0, bFarPoints: bool = False,
+                        thFarPoints: float = 50.0, nnratio: float = 0.8):
+    """Tracking::SearchLocalPoints' projection + SearchByProjection (Tracking.cc:3404-3453) in one
+    device pass. mvp is updated in place. Returns (nmatches, nToMatch)."""
+    lib = _lib.load()
+    pts = _records(points3d, MAP_POINT_3D_DTYPE, "points3d")
+    mvp = _i32(mvp, F.N, "mvp")
+    mvp_obs = _i32(mvp_obs, F.N, "mvp_obs")
+    ntm = ctypes.c_int32(0)
+    n = _lib.check(lib.orbfe_search_local_points(F.ref(), ctypes.byref(cam), pts.ctypes.data, len(pts),
+                                                 mvp.ctypes.data, mvp_obs.ctypes.data, float(th), int(bFarPoints),
+                                                 float(thFarPoints), float(nnratio), ctypes.byref(ntm)),
+                   "search_local_points")
+    return n, int(ntm.value)
 
 
 def stereo_knn_ratio(left_desc, right_desc, ratio: float = 0.7):

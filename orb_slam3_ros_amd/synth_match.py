@@ -11,7 +11,8 @@ from __future__ import annotations
 import numpy as np
 
 from .extractor import KEYPOINT_DTYPE
-from .matcher import MAP_POINT_DTYPE, MP_BAD, MP_IN_VIEW, PROJ_POINT_DTYPE, FeatureVector, MatchFrame
+from .matcher import (MAP_POINT_3D_DTYPE, MAP_POINT_DTYPE, MP_BAD, MP_IN_VIEW, MP_SKIP, PROJ_POINT_DTYPE, Camera,
+                      FeatureVector, MatchFrame)
 
 
 def scale_factors(nlevels: int = 8, scale_factor: float = 1.2) -> np.ndarray:
@@ -164,3 +165,64 @@ def synth_bow(rng, n_words: int, kf: MatchFrame, F: MatchFrame, shared_src=None)
         return FeatureVector(d)
 
     return fv(wk), fv(wf)
+
+
+def synth_camera(rng, fx=458.654, fy=457.296, cx=367.215, cy=248.375, rot_deg=10.0):
+    """A random pose (rotation of up to rot_deg about a random axis, translation ~1 m)."""
+    axis = rng.normal(size=3)
+    axis /= np.linalg.norm(axis)
+    ang = np.deg2rad(rng.uniform(-rot_deg, rot_deg))
+    K = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    R = np.eye(3) + np.sin(ang) * K + (1 - np.cos(ang)) * K @ K
+    t = rng.normal(scale=1.0, size=3)
+    return Camera.make(R, t, fx, fy, cx, cy)
+
+
+def synth_local_map_3d(rng, F: MatchFrame, cam: Camera, n: int, copy_frac: float = 0.5, flip_p: float = 0.05,
+                       nlevels: int = 8, scale_factor: float = 1.2) -> np.ndarray:
+    """Local map points in the world: they project near frame keypoints (copies, predicted level =
+    the keypoint's octave) or anywhere around the image; a few are behind the camera, outside the
+    scale-invariance distance range, seen at a grazing angle, bad, or already seen this frame."""
+    R = np.array(cam.Rcw[:], np.float64).reshape(3, 3)
+    t = np.array(cam.tcw[:], np.float64)
+    w, h = F.bounds[1], F.bounds[3]
+    u = rng.uniform(-60, w + 60, n)
+    v = rng.uniform(-60, h + 60, n)
+    lvl = rng.choice(nlevels, n, p=level_weights(nlevels))
+    desc = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    if F.N:
+        cp = np.nonzero(rng.random(n) < copy_frac)[0]
+        src = rng.integers(0, F.N, len(cp))
+        u[cp] = F.keys["x"][src] + rng.normal(0, 1.0, len(cp))
+        v[cp] = F.keys["y"][src] + rng.normal(0, 1.0, len(cp))
+        lvl[cp] = F.keys["octave"][src]
+        desc[cp] = flip_bits(rng, F.desc[src], flip_p)
+    z = rng.uniform(0.5, 40.0, n)
+    z[rng.random(n) < 0.02] *= -1.0
+    Pc = np.stack([(u - cam.cx) * z / cam.fx, (v - cam.cy) * z / cam.fy, z], 1)
+    P = (Pc - t) @ R                       # R^T (Pc - t), row-vector form
+    dist = np.linalg.norm(Pc, axis=1)
+    # PredictScale(dist) = ceil(log(max/dist) / log(sf)) = lvl  <=>  max = dist * sf^(lvl - frac)
+    max_d = dist * scale_factor ** (lvl - rng.uniform(0.1, 0.9, n))
+    out = rng.random(n) < 0.08
+    max_d[out] *= rng.choice([0.5, 2.5], int(out.sum()))
+    min_d = max_d / scale_factor ** (nlevels - 1)
+    view = P - np.array(cam.Ow[:], np.float64)
+    view /= np.maximum(np.linalg.norm(view, axis=1, keepdims=True), 1e-9)
+    nrm = view + rng.normal(0, 0.3, (n, 3))
+    graze = rng.random(n) < 0.05
+    nrm[graze] = -nrm[graze]
+    nrm /= np.maximum(np.linalg.norm(nrm, axis=1, keepdims=True), 1e-9)
+    m = np.zeros(n, MAP_POINT_3D_DTYPE)
+    m["pos"] = P.astype(np.float32)
+    m["normal"] = nrm.astype(np.float32)
+    m["min_dist"] = min_d.astype(np.float32)
+    m["max_dist"] = max_d.astype(np.float32)
+    fl = np.zeros(n, np.int32)
+    fl[rng.random(n) < 0.03] |= MP_BAD
+    fl[rng.random(n) < 0.03] |= MP_SKIP
+    m["flags"] = fl
+    m["observations"] = np.where(rng.random(n) < 0.1, 0, rng.integers(1, 20, n))
+    m["id"] = np.arange(n) + 20000
+    m["desc"] = desc
+    return m

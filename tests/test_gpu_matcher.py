@@ -226,3 +226,39 @@ def test_gpu_matcher_golden(gpu):
         assert res[0] == int(gold[name + "_n"][0]), name
         for i, a in enumerate(res[1:]):
             assert np.array_equal(np.asarray(a), gold[f"{name}_out{i}"]), f"{name} output {i}"
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_is_in_frustum(gpu, om, seed):
+    """Frame::isInFrustum + PredictScale on the device: every tracking field bit-exact."""
+    from orb_slam3_ros_amd.matcher import is_in_frustum
+    rng = np.random.default_rng(seed)
+    F = sm.synth_frame(rng, 1000)
+    cam = sm.synth_camera(rng)
+    pts = sm.synth_local_map_3d(rng, F, cam, 50_000)
+    ng, tg = is_in_frustum(F, cam, pts)
+    no, to = om.is_in_frustum(F, cam, pts)
+    assert ng == no and no > 1000
+    inv = (to["flags"] & sm.MP_IN_VIEW) != 0
+    np.testing.assert_array_equal(tg["flags"], to["flags"])
+    for f in ("proj_x", "proj_y", "proj_xr", "depth", "view_cos"):
+        np.testing.assert_array_equal(tg[f][inv].view(np.uint32), to[f][inv].view(np.uint32), err_msg=f)
+    np.testing.assert_array_equal(tg["scale_level"][inv], to["scale_level"][inv])
+    np.testing.assert_array_equal(tg["desc"], to["desc"])
+
+
+@pytest.mark.parametrize("th", [1, 3, 15])
+@pytest.mark.parametrize("seed", [4, 5])
+def test_search_local_points(gpu, om, th, seed):
+    """Tracking::SearchLocalPoints' projection + SearchByProjection fused on the device."""
+    from orb_slam3_ros_amd.matcher import search_local_points
+    rng = np.random.default_rng(seed)
+    F = sm.synth_frame(rng, 1000)
+    cam = sm.synth_camera(rng)
+    pts = sm.synth_local_map_3d(rng, F, cam, 100_000)
+    mvp0, obs = sm.initial_slots(rng, F.N)
+    a, b = mvp0.copy(), mvp0.copy()
+    ng, tg = search_local_points(F, cam, pts, a, obs, th)
+    no, to = om.search_local_points(F, cam, pts, b, obs, th)
+    assert (ng, tg) == (no, to) and no > 0
+    np.testing.assert_array_equal(a, b)

@@ -238,3 +238,66 @@ def test_oracle_matcher_golden(oracle_lib):
         assert res[0] == int(gold[name + "_n"][0]), name
         for i, a in enumerate(res[1:]):
             assert np.array_equal(np.asarray(a), gold[f"{name}_out{i}"]), f"{name} output {i}"
+
+
+def py_is_in_frustum(F, cam, pts):
+    """Frame::isInFrustum (Frame.cc:512-570) + PredictScale (MapPoint.cc:531-546), float32 scalars."""
+    import ctypes
+    libm = ctypes.CDLL("libm.so.6")
+    libm.logf.restype = ctypes.c_float
+    libm.logf.argtypes = [ctypes.c_float]
+    R = np.array(cam.Rcw[:], np.float32).reshape(3, 3)
+    t = np.array(cam.tcw[:], np.float32)
+    Ow = np.array(cam.Ow[:], np.float32)
+    res = []
+    for p in pts:
+        if p["flags"] & (sm.MP_SKIP | sm.MP_BAD):
+            res.append(None)
+            continue
+        P = p["pos"].astype(np.float32)
+        Pc = [f32(f32(f32(R[i, 0] * P[0]) + f32(R[i, 1] * P[1])) + f32(R[i, 2] * P[2])) + t[i] for i in range(3)]
+        Pc = [f32(x) for x in Pc]
+        Pc_dist = f32(np.sqrt(f32(f32(f32(Pc[0] * Pc[0]) + f32(Pc[1] * Pc[1])) + f32(Pc[2] * Pc[2]))))
+        if Pc[2] < 0:
+            res.append(None)
+            continue
+        invz = f32(f32(1) / Pc[2])
+        u = f32(f32(f32(f32(cam.fx) * Pc[0]) / Pc[2]) + f32(cam.cx))
+        v = f32(f32(f32(f32(cam.fy) * Pc[1]) / Pc[2]) + f32(cam.cy))
+        if u < F.bounds[0] or u > F.bounds[1] or v < F.bounds[2] or v > F.bounds[3]:
+            res.append(None)
+            continue
+        PO = [f32(P[i] - Ow[i]) for i in range(3)]
+        dist = f32(np.sqrt(f32(f32(f32(PO[0] * PO[0]) + f32(PO[1] * PO[1])) + f32(PO[2] * PO[2]))))
+        if dist < f32(f32(0.8) * p["min_dist"]) or dist > f32(f32(1.2) * p["max_dist"]):
+            res.append(None)
+            continue
+        nrm = p["normal"]
+        vc = f32(f32(f32(f32(PO[0] * nrm[0]) + f32(PO[1] * nrm[1])) + f32(PO[2] * nrm[2])) / dist)
+        if vc < f32(cam.view_cos_limit):
+            res.append(None)
+            continue
+        ratio = f32(p["max_dist"] / dist)
+        lv = int(math.ceil(f32(f32(libm.logf(float(ratio))) / f32(cam.log_scale_factor))))
+        lv = min(max(lv, 0), len(F.scale_factors) - 1)
+        res.append((u, v, f32(u - f32(f32(F.mbf) * invz)), Pc_dist, vc, lv))
+    return res
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_oracle_frustum_vs_python(oracle_lib, seed):
+    rng = np.random.default_rng(seed)
+    F = sm.synth_frame(rng, 300)
+    cam = sm.synth_camera(rng)
+    pts = sm.synth_local_map_3d(rng, F, cam, 400)
+    n, tr = oracle_lib.is_in_frustum(F, cam, pts)
+    ref = py_is_in_frustum(F, cam, pts)
+    assert n == sum(r is not None for r in ref) and n > 100
+    for i, r in enumerate(ref):
+        inv = bool(tr["flags"][i] & sm.MP_IN_VIEW)
+        assert inv == (r is not None), i
+        if r is not None:
+            got = (tr["proj_x"][i], tr["proj_y"][i], tr["proj_xr"][i], tr["depth"][i], tr["view_cos"][i],
+                   int(tr["scale_level"][i]))
+            assert [np.float32(a).tobytes() for a in got[:5]] == [np.float32(b).tobytes() for b in r[:5]], i
+            assert got[5] == r[5], i
