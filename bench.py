@@ -119,6 +119,20 @@ def matcher_config5(steps):
         out[f"th{th}"] = {"ms_per_call": round(dt * 1e3, 4), "calls_per_s": round(1.0 / dt, 2),
                           "queries_per_s": round(len(mps) / dt, 1), "device_ms_per_call": round(dms, 4),
                           "device_queries_per_s": round(len(mps) / (dms * 1e-3), 1), "nmatches": int(n)}
+    # Tracking::SearchLocalPoints' projection (isInFrustum + PredictScale) fused with the
+    # th=1 search, 100k world points, device time (HIP events)
+    from orb_slam3_ros_amd.matcher import search_local_points
+    cam = sm.synth_camera(rng)
+    pts = sm.synth_local_map_3d(rng, F, cam, 100_000)
+    lib.orbfe_matcher_set_timing(1)
+    dev = []
+    for _ in range(steps + 2):
+        nm, ntm = search_local_points(F, cam, pts, mvp0.copy(), obs, 1.0)
+        dev.append(lib.orbfe_matcher_last_ms())
+    lib.orbfe_matcher_set_timing(0)
+    dms = float(np.mean(dev[2:]))
+    out["search_local_points_th1"] = {"device_ms_per_call": round(dms, 4), "points": len(pts), "n_to_match": ntm,
+                                      "nmatches": int(nm), "device_points_per_s": round(len(pts) / (dms * 1e-3), 1)}
     return {"workload": "SearchByProjection local map: 100k map points (30% noisy copies, Binomial(256,0.05) "
                         "flips) vs 1000-keypoint stereo frame, nnratio 0.8, seed 12345",
             "timing": "ms_per_call: host C-ABI call incl. 8 MB record upload and result download; "

@@ -258,6 +258,42 @@ int orbfe_search_local_points(const orbfe_frame* F, const orbfe_camera* cam, con
                               int32_t n, int32_t* mvp, const int32_t* mvp_obs, float th, int32_t bFarPoints,
                               float thFarPoints, float nnratio, int32_t* n_to_match);
 
+/* ---------------------------------------------------------------------------------------------
+ * Bag of words: DBoW2::TemplatedVocabulary<FORB> (Thirdparty/DBoW2/DBoW2/
+ * TemplatedVocabulary.h) — the loader of ORB-SLAM3's binary vocabulary format and transform(),
+ * called by Frame::ComputeBoW (Frame.cc) with levelsup = 4. The vocabulary tree lives in HBM.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct orbfe_vocabulary orbfe_vocabulary;
+#define ORBFE_TF_IDF 0               /* DBoW2::WeightingType */
+#define ORBFE_TF 1
+#define ORBFE_IDF 2
+#define ORBFE_BINARY 3
+#define ORBFE_L1_NORM 0              /* DBoW2::ScoringType */
+#define ORBFE_L2_NORM 1
+#define ORBFE_CHI_SQUARE 2
+#define ORBFE_KL 3
+#define ORBFE_BHATTACHARYYA 4
+#define ORBFE_DOT_PRODUCT 5
+
+/* TemplatedVocabulary::loadFromBinFile (TemplatedVocabulary.h:1478-1540) from an in-memory copy of
+ * the file: int k, int L, int scoring, int weighting, then per node 1..: int parent, uchar isLeaf,
+ * uchar desc[32], double weight. */
+int orbfe_vocabulary_load_bin(const uint8_t* data, size_t size, orbfe_vocabulary** out);
+/* The same tree from arrays (node 0 = root; parents[i] < i for i >= 1; children keep node order). */
+int orbfe_vocabulary_create(int32_t k, int32_t L, int32_t scoring, int32_t weighting, int32_t n_nodes,
+                            const int32_t* parents, const uint8_t* is_leaf, const uint8_t* desc,
+                            const double* weights, orbfe_vocabulary** out);
+void orbfe_vocabulary_destroy(orbfe_vocabulary* voc);
+int orbfe_vocabulary_info(const orbfe_vocabulary* voc, int32_t* k, int32_t* L, int32_t* n_nodes, int32_t* n_words);
+
+/* transform(features, BowVector& v, FeatureVector& fv, levelsup) (TemplatedVocabulary.h:1139-1198,
+ * :1218-1262) for n descriptors (n x 32 bytes). Outputs (capacity n each, fv_offsets n + 1):
+ * BowVector as ascending word ids + weights (*bow_n entries), FeatureVector as ascending node ids
+ * with offsets into fv_indices (*fv_n nodes). Returns 0. */
+int orbfe_vocabulary_transform(const orbfe_vocabulary* voc, const uint8_t* desc, int32_t n, int32_t levelsup,
+                               uint32_t* bow_word_ids, double* bow_weights, int32_t* bow_n,
+                               uint32_t* fv_node_ids, int32_t* fv_offsets, uint32_t* fv_indices, int32_t* fv_n);
+
 /* Per calling thread: when enabled, every matcher call above records HIP events around its
  * kernels (after the input upload, before the result copy); orbfe_matcher_last_ms returns that
  * device time of the thread's last call in ms (-1 when not timed). For bench.py. */

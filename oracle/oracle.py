@@ -19,7 +19,7 @@ KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle"
 
 
 def build(force: bool = False) -> str:
-    srcs = [os.path.join(_HERE, f) for f in ("orb_oracle.cpp", "orb_oracle_match.cpp", "Makefile")]
+    srcs = [os.path.join(_HERE, f) for f in ("orb_oracle.cpp", "orb_oracle_match.cpp", "orb_oracle_bow.cpp", "Makefile")]
     if force or not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in srcs):
         subprocess.run(["make", "-C", _HERE, "-B" if force else "-s"], check=True)
     return LIB
@@ -204,3 +204,63 @@ def stereo_knn_ratio(left_desc, right_desc, ratio=0.7):
     g = L.oro_stereo_knn_ratio(a.ctypes.data, len(a), b.ctypes.data, len(b), float(ratio), t.ctypes.data,
                                d.ctypes.data)
     return g, t, d
+
+
+# ---- DBoW2 vocabulary oracle (oracle/orb_oracle_bow.cpp) ----
+class OracleVocabulary:
+    def __init__(self, handle):
+        self.L_ = lib()
+        self.h = handle
+
+    @staticmethod
+    def _lib():
+        L = lib()
+        vp, ci = ctypes.c_void_p, ctypes.c_int
+        L.oro_voc_create.restype = vp
+        L.oro_voc_create.argtypes = [ci, ci, ci, ci, ci, vp, vp, vp, vp]
+        L.oro_voc_load_bin.restype = vp
+        L.oro_voc_load_bin.argtypes = [vp, ctypes.c_size_t]
+        L.oro_voc_destroy.argtypes = [vp]
+        L.oro_voc_transform.argtypes = [vp, vp, ci, ci, vp, vp, vp, vp, vp, vp, vp]
+        return L
+
+    @classmethod
+    def from_arrays(cls, k, Lv, scoring, weighting, parents, is_leaf, desc, weights):
+        L = cls._lib()
+        par = np.ascontiguousarray(parents, np.int32)
+        leaf = np.ascontiguousarray(is_leaf, np.uint8)
+        d = np.ascontiguousarray(desc, np.uint8)
+        w = np.ascontiguousarray(weights, np.float64)
+        o = cls(L.oro_voc_create(k, Lv, scoring, weighting, len(par), par.ctypes.data, leaf.ctypes.data,
+                                 d.ctypes.data, w.ctypes.data))
+        o._keep = (par, leaf, d, w)
+        return o
+
+    @classmethod
+    def from_bin(cls, data):
+        L = cls._lib()
+        buf = np.frombuffer(data, np.uint8)
+        h = L.oro_voc_load_bin(buf.ctypes.data, len(buf))
+        return cls(h) if h else None
+
+    def transform(self, desc, levelsup=4):
+        L = self._lib()
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(d)
+        bid = np.zeros(max(n, 1), np.uint32)
+        bw = np.zeros(max(n, 1), np.float64)
+        fid = np.zeros(max(n, 1), np.uint32)
+        foff = np.zeros(n + 1, np.int32)
+        fidx = np.zeros(max(n, 1), np.uint32)
+        nb, nf = ctypes.c_int(), ctypes.c_int()
+        L.oro_voc_transform(self.h, d.ctypes.data, n, levelsup, bid.ctypes.data, bw.ctypes.data, ctypes.byref(nb),
+                            fid.ctypes.data, foff.ctypes.data, fidx.ctypes.data, ctypes.byref(nf))
+        return (bid[:nb.value].copy(), bw[:nb.value].copy()), (fid[:nf.value].copy(), foff[:nf.value + 1].copy(),
+                                                               fidx[:foff[nf.value]].copy())
+
+    def __del__(self):
+        try:
+            if self.h:
+                self._lib().oro_voc_destroy(self.h)
+        except Exception:
+            pass

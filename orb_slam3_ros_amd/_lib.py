@@ -58,6 +58,11 @@ _SIGS = {
     "orbfe_search_by_bow": (_c_int, [_vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_float, _c_int]),
     "orbfe_stereo_knn_ratio": (_c_int, [_vp, _c_int, _vp, _c_int, _c_float, _vp, _vp]),
     "orbfe_matcher_set_timing": (_c_int, [_c_int]),
+    "orbfe_vocabulary_load_bin": (_c_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
+    "orbfe_vocabulary_create": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, ctypes.POINTER(_vp)]),
+    "orbfe_vocabulary_destroy": (None, [_vp]),
+    "orbfe_vocabulary_info": (_c_int, [_vp, _vp, _vp, _vp, _vp]),
+    "orbfe_vocabulary_transform": (_c_int, [_vp, _vp, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "orbfe_is_in_frustum": (_c_int, [_vp, _vp, _vp, _c_int, _vp]),
     "orbfe_search_local_points": (_c_int, [_vp, _vp, _vp, _c_int, _vp, _vp, _c_float, _c_int, _c_float, _c_float, _vp]),
     "orbfe_matcher_last_ms": (_c_float, []),
