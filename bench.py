@@ -155,6 +155,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stage-steps", type=int, default=10, help="extra steps with per-stage HIP events")
     ap.add_argument("--matcher-steps", type=int, default=10, help="config-5 SearchByProjection calls per th (0: skip)")
+    ap.add_argument("--rectify-steps", type=int, default=5,
+                    help="time cv::remap rectification of the step's images (reported separately; 0: skip)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (the measured path); gloo = CPU rehearsal of the multi-rank path")
     ap.add_argument("--same-device", action="store_true",
@@ -236,6 +238,26 @@ def main():
     fe_t.set_stage_timing(False)
     if fe_t is not fe:
         fe_t.close()
+    rect = None
+    if args.rectify_steps > 0 and rank == 0:
+        # System::TrackStereo's cv::remap of every image before extraction (not part of
+        # `value`: the reference's metric starts at the rectified images)
+        from orb_slam3_ros_amd.rectify import rectify_maps, remap_linear_batch
+        mx, my = rectify_maps(W, H, fx, 457.296, W / 2 - 8.6, H / 2 + 8.4, (-0.28340811, 0.07395907, 0.00019359, 1.76e-05))
+        dmx, dmy = torch.from_numpy(mx).to(dev), torch.from_numpy(my).to(dev)
+        rout = torch.empty_like(images)
+        remap_linear_batch(images, dmx, dmy, rout)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.rectify_steps):
+            remap_linear_batch(images, dmx, dmy, rout)
+        e1.record()
+        torch.cuda.synchronize()
+        rms = e0.elapsed_time(e1) / args.rectify_steps
+        rbytes = images.numel() * (1 + 1) + 2 * 4 * W * H   # read + write per image, maps once (L2 / IC)
+        rect = {"ms_per_step": round(rms, 4), "images": int(images.shape[0]),
+                "achieved_GBps": round(rbytes / (rms * 1e-3) / 1e9, 1)}
+        del rout
     counts = fe.counts.cpu().numpy()
     nm = fe.nmatch.cpu().numpy()
 
@@ -289,6 +311,8 @@ def main():
             "keypoints_per_image_mean": float(counts[:, 0].mean()),
             "stereo_matches_per_frame_mean": float(nm.mean()),
         }
+        if rect is not None:
+            result["rectify_remap"] = rect
         if args.matcher_steps > 0:
             result["matcher_config5"] = matcher_config5(args.matcher_steps)
         if not args.no_cpu_baseline:

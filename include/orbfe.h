@@ -294,6 +294,19 @@ int orbfe_vocabulary_transform(const orbfe_vocabulary* voc, const uint8_t* desc,
                                uint32_t* bow_word_ids, double* bow_weights, int32_t* bow_n,
                                uint32_t* fv_node_ids, int32_t* fv_offsets, uint32_t* fv_indices, int32_t* fv_n);
 
+/* ---------------------------------------------------------------------------------------------
+ * Stereo rectification: cv::remap(im, out, M1, M2, cv::INTER_LINEAR) with CV_32F
+ * maps from initUndistortRectifyMap (System.cc:233-240, Settings.cc:506-509), BORDER_CONSTANT 0.
+ * ------------------------------------------------------------------------------------------- */
+/* Batched, device-resident: n images (device pointer tables in host memory), one map pair
+ * (dw x dh floats each, row-major) shared by all; stream = hipStream_t or NULL. */
+int orbfe_remap_linear_batch(const uint8_t* const* d_src, int sw, int sh, int sstride, const float* d_mapx,
+                             const float* d_mapy, int dw, int dh, uint8_t* const* d_dst, int dstride, int n,
+                             void* stream);
+/* Host convenience for one image. */
+int orbfe_remap_linear(const uint8_t* src, int sw, int sh, int sstride, const float* mapx, const float* mapy, int dw,
+                       int dh, uint8_t* dst, int dstride);
+
 /* Per calling thread: when enabled, every matcher call above records HIP events around its
  * kernels (after the input upload, before the result copy); orbfe_matcher_last_ms returns that
  * device time of the thread's last call in ms (-1 when not timed). For bench.py. */

@@ -19,7 +19,7 @@ KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle"
 
 
 def build(force: bool = False) -> str:
-    srcs = [os.path.join(_HERE, f) for f in ("orb_oracle.cpp", "orb_oracle_match.cpp", "orb_oracle_bow.cpp", "Makefile")]
+    srcs = [os.path.join(_HERE, f) for f in ("orb_oracle.cpp", "orb_oracle_match.cpp", "orb_oracle_bow.cpp", "orb_oracle_remap.cpp", "Makefile")]
     if force or not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in srcs):
         subprocess.run(["make", "-C", _HERE, "-B" if force else "-s"], check=True)
     return LIB
@@ -264,3 +264,25 @@ class OracleVocabulary:
                 self._lib().oro_voc_destroy(self.h)
         except Exception:
             pass
+
+
+def remap_linear(src, mapx, mapy):
+    L = lib()
+    L.oro_remap_linear.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                   ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    src = np.ascontiguousarray(src, np.uint8)
+    mapx = np.ascontiguousarray(mapx, np.float32)
+    mapy = np.ascontiguousarray(mapy, np.float32)
+    dh, dw = mapx.shape
+    out = np.zeros((dh, dw), np.uint8)
+    L.oro_remap_linear(src.ctypes.data, src.shape[1], src.shape[0], src.strides[0], mapx.ctypes.data,
+                       mapy.ctypes.data, dw, dh, out.ctypes.data, dw)
+    return out
+
+
+def remap_bilinear_tab():
+    L = lib()
+    L.oro_remap_bilinear_tab.argtypes = [ctypes.c_void_p]
+    t = np.zeros((32 * 32, 4), np.int16)
+    L.oro_remap_bilinear_tab(t.ctypes.data)
+    return t

@@ -688,3 +688,6 @@ int orbfe_descriptor_distance(const uint8_t* a, const uint8_t* b) {
 
 // DBoW2 vocabulary transform (uses the matcher's per-thread arena).
 #include "orbfe_bow.hip"
+
+// cv::remap INTER_LINEAR (stereo rectification before extraction).
+#include "orbfe_remap.hip"

@@ -1,0 +1,131 @@
+// cv::remap(src, dst, map1, map2, INTER_LINEAR) for 8UC1 images and CV_32FC1 map pairs, the stereo
+// rectification of System::TrackStereo (System.cc:233-240, maps from initUndistortRectifyMap(...,
+// CV_32F, ...), Settings.cc:506-509), restated from OpenCV 4.2 imgwarp.cpp:
+//  * map -> fixed point: X = cvRound(mapx * 32), sx = X >> 5, fx = X & 31 (same for y);
+//  * BilinearTab_i[fy][fx] = ((32 - fy)(32 - fx), (32 - fy) fx, fy (32 - fx), fy fx) * 32 — exact
+//    integers summing to 32768 — except cell (0, 0), whose 32768 saturates to 32767 and whose
+//    deficit initInterTab2D adds to the (1, 1) weight: (32767, 0, 0, 1);
+//  * D = (w0 S00 + w1 S01 + w2 S10 + w3 S11 + 2^14) >> 15 (FixedPtCast, INTER_REMAP_COEF_BITS = 15);
+//  * BORDER_CONSTANT (value 0): a sample outside the source reads 0; a pixel whose 2x2 footprint
+//    is entirely outside is 0.
+// One thread per 4 adjacent output pixels (one dword store); maps are read as float4.
+#pragma once
+
+__device__ __forceinline__ uint8_t remap_px(gptr_u8 src, int sw, int sh, int sstride, float mx, float my) {
+    const float fxs = mx * 32.f, fys = my * 32.f;
+    // saturate_cast<int>(float): round half to even, saturating
+    const int X = fxs >= 2147483520.f ? INT_MAX : (fxs <= -2147483648.f ? INT_MIN : __float2int_rn(fxs));
+    const int Y = fys >= 2147483520.f ? INT_MAX : (fys <= -2147483648.f ? INT_MIN : __float2int_rn(fys));
+    const int sx = min(max(X >> 5, -32768), 32767), sy = min(max(Y >> 5, -32768), 32767);
+    const int ax = X & 31, ay = Y & 31;
+    int w0, w1, w2, w3;
+    if (ax == 0 && ay == 0) {
+        w0 = 32767; w1 = 0; w2 = 0; w3 = 1;
+    } else {
+        w0 = (32 - ay) * (32 - ax) * 32;
+        w1 = (32 - ay) * ax * 32;
+        w2 = ay * (32 - ax) * 32;
+        w3 = ay * ax * 32;
+    }
+    int v0, v1, v2, v3;
+    if ((unsigned)sx < (unsigned)max(sw - 1, 0) && (unsigned)sy < (unsigned)max(sh - 1, 0)) {
+        gptr_u8 p = src + (size_t)sy * sstride + sx;
+        v0 = p[0]; v1 = p[1]; v2 = p[sstride]; v3 = p[sstride + 1];
+    } else {
+        if (sx >= sw || sx + 1 < 0 || sy >= sh || sy + 1 < 0) return 0;
+        v0 = (sx >= 0 && sy >= 0) ? src[(size_t)sy * sstride + sx] : 0;
+        v1 = (sx + 1 < sw && sy >= 0) ? src[(size_t)sy * sstride + sx + 1] : 0;
+        v2 = (sx >= 0 && sy + 1 < sh) ? src[(size_t)(sy + 1) * sstride + sx] : 0;
+        v3 = (sx + 1 < sw && sy + 1 < sh) ? src[(size_t)(sy + 1) * sstride + sx + 1] : 0;
+    }
+    const int v = (v0 * w0 + v1 * w1 + v2 * w2 + v3 * w3 + (1 << 14)) >> 15;
+    return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
+
+__global__ __launch_bounds__(256) void k_remap(const uint8_t* const* srcs, int sw, int sh, int sstride,
+                                               const float* __restrict__ mapx, const float* __restrict__ mapy,
+                                               int dw, int dh, uint8_t* const* dsts, int dstride) {
+    const int img = blockIdx.y;
+    const int ng = (dw + 3) >> 2;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ng * dh) return;
+    const int y = t / ng, x0 = 4 * (t - y * ng);
+    gptr_u8 src = as_global(srcs[img]);
+    uint8_t* dst = dsts[img] + (size_t)y * dstride;
+    const float* mxr = mapx + (size_t)y * dw;
+    const float* myr = mapy + (size_t)y * dw;
+    uint32_t packed = 0;
+    const bool full = x0 + 4 <= dw;
+    float mx[4], my[4];
+    if (full && ((dw & 3) == 0)) {
+        const float4 a = *(const float4*)(mxr + x0), c = *(const float4*)(myr + x0);
+        mx[0] = a.x; mx[1] = a.y; mx[2] = a.z; mx[3] = a.w;
+        my[0] = c.x; my[1] = c.y; my[2] = c.z; my[3] = c.w;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            mx[q] = x0 + q < dw ? mxr[x0 + q] : 0.f;
+            my[q] = x0 + q < dw ? myr[x0 + q] : 0.f;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) packed |= (uint32_t)remap_px(src, sw, sh, sstride, mx[q], my[q]) << (8 * q);
+    if (full && ((((uintptr_t)(dst + x0)) & 3) == 0)) {
+        *(uint32_t*)(dst + x0) = packed;
+    } else {
+        for (int q = 0; q < 4 && x0 + q < dw; q++) dst[x0 + q] = (uint8_t)(packed >> (8 * q));
+    }
+}
+
+extern "C" {
+
+int orbfe_remap_linear_batch(const uint8_t* const* d_src, int sw, int sh, int sstride, const float* d_mapx,
+                             const float* d_mapy, int dw, int dh, uint8_t* const* d_dst, int dstride, int n,
+                             void* stream) {
+    if (n <= 0 || sw < 0 || sh < 0 || dw <= 0 || dh <= 0 || !d_src || !d_dst || !d_mapx || !d_mapy ||
+        sstride < sw || dstride < dw)
+        return n == 0 ? ORBFE_OK : ORBFE_E_ARG;
+    if ((size_t)sw * sh == 0) return ORBFE_E_EMPTY;
+    // the pointer tables travel with the launch (kernel arguments are copied at launch time)
+    hipStream_t s = (hipStream_t)stream;
+    const uint8_t** dsrc = nullptr;
+    uint8_t** ddst = nullptr;
+    HIPCHK(hipMallocAsync((void**)&dsrc, (size_t)n * sizeof(void*), s));
+    HIPCHK(hipMallocAsync((void**)&ddst, (size_t)n * sizeof(void*), s));
+    HIPCHK(hipMemcpyAsync(dsrc, d_src, (size_t)n * sizeof(void*), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(ddst, d_dst, (size_t)n * sizeof(void*), hipMemcpyHostToDevice, s));
+    const int ng = (dw + 3) >> 2;
+    hipLaunchKernelGGL(k_remap, dim3((ng * dh + 255) / 256, n), dim3(256), 0, s, dsrc, sw, sh, sstride, d_mapx, d_mapy,
+                       dw, dh, ddst, dstride);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipFreeAsync(dsrc, s));
+    HIPCHK(hipFreeAsync(ddst, s));
+    return ORBFE_OK;
+}
+
+int orbfe_remap_linear(const uint8_t* src, int sw, int sh, int sstride, const float* mapx, const float* mapy, int dw,
+                       int dh, uint8_t* dst, int dstride) {
+    if (!src || !mapx || !mapy || !dst || sw <= 0 || sh <= 0 || dw <= 0 || dh <= 0 || sstride < sw || dstride < dw)
+        return ORBFE_E_ARG;
+    Plan p;
+    const size_t o_mx = p.upload(mapx, (size_t)dw * dh * 4), o_my = p.upload(mapy, (size_t)dw * dh * 4);
+    const size_t o_src = p.upload(src, (size_t)sstride * (sh - 1) + sw);
+    const size_t o_dst = p.scratch((size_t)dw * dh);
+    const size_t o_ptr = p.scratch(16);
+    int rc = ms_prepare(p);
+    if (rc) return rc;
+    MsTimer timer;
+    hipStream_t s = t_ms.stream;
+    const uint8_t* ptrs[2] = {ms_ptr<const uint8_t>(o_src), ms_ptr<uint8_t>(o_dst)};
+    HIPCHK(hipMemcpyAsync(ms_ptr<uint8_t>(o_ptr), ptrs, 16, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_remap, dim3((((dw + 3) >> 2) * dh + 255) / 256, 1), dim3(256), 0, s,
+                       (const uint8_t* const*)ms_ptr<uint8_t>(o_ptr), sw, sh, sstride, ms_ptr<const float>(o_mx),
+                       ms_ptr<const float>(o_my), dw, dh, (uint8_t* const*)(ms_ptr<uint8_t>(o_ptr) + 8), dw);
+    HIPCHK(hipGetLastError());
+    timer.end();
+    HIPCHK(hipMemcpy2DAsync(dst, dstride, ms_ptr<uint8_t>(o_dst), dw, dw, dh, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return ORBFE_OK;
+}
+
+}  // extern "C"

@@ -55,7 +55,7 @@ def synth_image(seed: int, w: int = 752, h: int = 480, noise: float = 3.0) -> np
     """One seeded u8 image of shape (h, w)."""
     rng = np.random.default_rng(seed)
     img = _scene(rng, h, w) + rng.normal(0.0, noise, (h, w))
-    return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+    return np.ascontiguousarray(np.clip(np.rint(img), 0, 255).astype(np.uint8))
 
 
 def synth_stereo(seed: int, w: int = 752, h: int = 480, max_disp: float = 48.0,
