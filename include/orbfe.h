@@ -307,6 +307,13 @@ int orbfe_remap_linear_batch(const uint8_t* const* d_src, int sw, int sh, int ss
 int orbfe_remap_linear(const uint8_t* src, int sw, int sh, int sstride, const float* mapx, const float* mapy, int dw,
                        int dh, uint8_t* dst, int dstride);
 
+/* cv::undistortPoints(mat, mat, K, DistCoef, cv::Mat(), K) of Frame::UndistortKeyPoints
+ * (Frame.cc:747-780) for n points (x, y float pairs): K4 = {fx, fy, cx, cy} (float, as mK),
+ * dist = ndist (4, 5, 8 or 12) OpenCV coefficients k1 k2 p1 p2 [k3 [k4 k5 k6 [s1..s4]]]. OpenCV 4.2
+ * semantics: double arithmetic, 5 fixed-point iterations. Returns n. (The reference skips the call
+ * when k1 == 0; the caller keeps that test.) */
+int orbfe_undistort_points(const float* pts, int n, const float* K4, const float* dist, int ndist, float* out);
+
 /* Per calling thread: when enabled, every matcher call above records HIP events around its
  * kernels (after the input upload, before the result copy); orbfe_matcher_last_ms returns that
  * device time of the thread's last call in ms (-1 when not timed). For bench.py. */

@@ -286,3 +286,15 @@ def remap_bilinear_tab():
     t = np.zeros((32 * 32, 4), np.int16)
     L.oro_remap_bilinear_tab(t.ctypes.data)
     return t
+
+
+def undistort_points(pts, K4, dist):
+    L = lib()
+    L.oro_undistort_points.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                       ctypes.c_void_p]
+    p = np.ascontiguousarray(pts, np.float32).reshape(-1, 2)
+    k = np.ascontiguousarray(K4, np.float32).reshape(4)
+    d = np.ascontiguousarray(dist, np.float32).reshape(-1)
+    out = np.zeros_like(p)
+    L.oro_undistort_points(p.ctypes.data, len(p), k.ctypes.data, d.ctypes.data, len(d), out.ctypes.data)
+    return out

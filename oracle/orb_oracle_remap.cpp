@@ -101,6 +101,50 @@ int oro_remap_linear(const uint8_t* src, int sw, int sh, int sstride, const floa
     return 0;
 }
 
+// cv::undistortPoints for CV_32FC2 points, K = P = {fx, fy, cx, cy} (float), identity R and tilt,
+// default criteria (COUNT, 5): OpenCV 4.2 cvUndistortPointsInternal restated (Frame.cc:747-780).
+int oro_undistort_points(const float* pts, int n, const float* K4, const float* dist, int ndist, float* out) {
+    double k[14] = {0};
+    for (int i = 0; i < ndist && i < 14; i++) k[i] = (double)dist[i];
+    const double fx = K4[0], fy = K4[1], cx = K4[2], cy = K4[3];
+    const double ifx = 1. / fx, ify = 1. / fy;
+    const double RR[3][3] = {{fx, 0, cx}, {0, fy, cy}, {0, 0, 1}};   // P * R with R = I (exact)
+    const double T[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};        // invMatTilt
+    for (int i = 0; i < n; i++) {
+        double x = pts[2 * i], y = pts[2 * i + 1];
+        const double u = x, v = y;
+        x = (x - cx) * ifx;
+        y = (y - cy) * ify;
+        // Matx33d * Vec3d: each component summed left to right
+        const double v0 = T[0][0] * x + T[0][1] * y + T[0][2] * 1;
+        const double v1 = T[1][0] * x + T[1][1] * y + T[1][2] * 1;
+        const double v2 = T[2][0] * x + T[2][1] * y + T[2][2] * 1;
+        const double invProj = v2 ? 1. / v2 : 1;
+        double x0 = x = invProj * v0;
+        double y0 = y = invProj * v1;
+        for (int j = 0;; j++) {
+            if (j >= 5) break;   // TermCriteria(COUNT, 5, 0.01)
+            const double r2 = x * x + y * y;
+            const double icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+            if (icdist < 0) {
+                x = (u - cx) * ifx;
+                y = (v - cy) * ify;
+                break;
+            }
+            const double deltaX = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x) + k[8] * r2 + k[9] * r2 * r2;
+            const double deltaY = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y + k[10] * r2 + k[11] * r2 * r2;
+            x = (x0 - deltaX) * icdist;
+            y = (y0 - deltaY) * icdist;
+        }
+        const double xx = RR[0][0] * x + RR[0][1] * y + RR[0][2];
+        const double yy = RR[1][0] * x + RR[1][1] * y + RR[1][2];
+        const double ww = 1. / (RR[2][0] * x + RR[2][1] * y + RR[2][2]);
+        out[2 * i] = (float)(xx * ww);
+        out[2 * i + 1] = (float)(yy * ww);
+    }
+    return n;
+}
+
 // the fixed-point table itself (tests: it must equal the closed form the HIP kernel uses)
 void oro_remap_bilinear_tab(int16_t* out) {
     init_tab();

@@ -58,6 +58,7 @@ _SIGS = {
     "orbfe_search_by_bow": (_c_int, [_vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_float, _c_int]),
     "orbfe_stereo_knn_ratio": (_c_int, [_vp, _c_int, _vp, _c_int, _c_float, _vp, _vp]),
     "orbfe_matcher_set_timing": (_c_int, [_c_int]),
+    "orbfe_undistort_points": (_c_int, [_vp, _c_int, _vp, _vp, _c_int, _vp]),
     "orbfe_remap_linear": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _c_int, _vp, _c_int]),
     "orbfe_remap_linear_batch": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _c_int, _vp, _c_int, _c_int, _vp]),
     "orbfe_vocabulary_load_bin": (_c_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),

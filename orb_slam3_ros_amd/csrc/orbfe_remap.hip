@@ -77,7 +77,75 @@ __global__ __launch_bounds__(256) void k_remap(const uint8_t* const* srcs, int s
     }
 }
 
+// cv::undistortPoints(pts, pts, K, D, noArray(), K) for CV_32FC2 points (Frame::UndistortKeyPoints,
+// Frame.cc:747-780), restated from OpenCV 4.2 cvUndistortPointsInternal: double arithmetic, the
+// default criteria (COUNT, 5 iterations), identity tilt and rectification, P = K. One thread per
+// point; the expression order follows the OpenCV source (no contraction).
+struct UndistArgs {
+    double fx, fy, cx, cy, ifx, ify;
+    double k[12];
+};
+__global__ __launch_bounds__(256) void k_undistort(const float* __restrict__ in, int n, UndistArgs a, float* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double* k = a.k;
+    double x = in[2 * i], y = in[2 * i + 1];
+    const double u = x, v = y;
+    x = (x - a.cx) * a.ifx;
+    y = (y - a.cy) * a.ify;
+    // invMatTilt = identity: vecUntilt = (1*x + 0*y + 0*1, 0*x + 1*y + 0*1, 0*x + 0*y + 1*1)
+    const double ux = (1.0 * x + 0.0 * y) + 0.0 * 1.0, uy = (0.0 * x + 1.0 * y) + 0.0 * 1.0;
+    const double uz = (0.0 * x + 0.0 * y) + 1.0 * 1.0;
+    const double invProj = uz != 0.0 ? 1. / uz : 1;
+    double x0 = x = invProj * ux;
+    double y0 = y = invProj * uy;
+    for (int j = 0; j < 5; j++) {
+        const double r2 = x * x + y * y;
+        const double icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+        if (icdist < 0) {
+            x = (u - a.cx) * a.ifx;
+            y = (v - a.cy) * a.ify;
+            break;
+        }
+        const double deltaX = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x) + k[8] * r2 + k[9] * r2 * r2;
+        const double deltaY = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y + k[10] * r2 + k[11] * r2 * r2;
+        x = (x0 - deltaX) * icdist;
+        y = (y0 - deltaY) * icdist;
+    }
+    // RR = P * I = K
+    const double xx = a.fx * x + 0.0 * y + a.cx;
+    const double yy = 0.0 * x + a.fy * y + a.cy;
+    const double ww = 1. / (0.0 * x + 0.0 * y + 1.0);
+    out[2 * i] = (float)(xx * ww);
+    out[2 * i + 1] = (float)(yy * ww);
+}
+
 extern "C" {
+
+int orbfe_undistort_points(const float* pts, int n, const float* K4, const float* dist, int ndist, float* out) {
+    if (n < 0 || (n > 0 && (!pts || !out)) || !K4 || (ndist > 0 && !dist) || ndist < 0 || ndist > 12) return ORBFE_E_ARG;
+    if (n == 0) return 0;
+    UndistArgs a;
+    memset(&a, 0, sizeof(a));
+    a.fx = (double)K4[0]; a.fy = (double)K4[1]; a.cx = (double)K4[2]; a.cy = (double)K4[3];
+    a.ifx = 1. / a.fx;
+    a.ify = 1. / a.fy;
+    for (int i = 0; i < ndist; i++) a.k[i] = (double)dist[i];
+    Plan p;
+    const size_t o_in = p.upload(pts, (size_t)n * 8);
+    const size_t o_out = p.scratch((size_t)n * 8);
+    int rc = ms_prepare(p);
+    if (rc) return rc;
+    MsTimer timer;
+    hipStream_t s = t_ms.stream;
+    hipLaunchKernelGGL(k_undistort, dim3((n + 255) / 256), dim3(256), 0, s, ms_ptr<const float>(o_in), n, a,
+                       ms_ptr<float>(o_out));
+    HIPCHK(hipGetLastError());
+    timer.end();
+    HIPCHK(hipMemcpyAsync(out, ms_ptr<float>(o_out), (size_t)n * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return n;
+}
 
 int orbfe_remap_linear_batch(const uint8_t* const* d_src, int sw, int sh, int sstride, const float* d_mapx,
                              const float* d_mapy, int dw, int dh, uint8_t* const* d_dst, int dstride, int n,

@@ -61,3 +61,16 @@ def rectify_maps(w: int, h: int, fx: float, fy: float, cx: float, cy: float, dis
     xd = x * kr + 2 * p1 * x * y + p2 * (r2 + 2 * x * x)
     yd = y * kr + p1 * (r2 + 2 * y * y) + 2 * p2 * x * y
     return (fx * xd + cx).astype(np.float32), (fy * yd + cy).astype(np.float32)
+
+
+def undistort_points(pts, K4, dist):
+    """cv::undistortPoints(pts, pts, K, D, noArray(), K) of Frame::UndistortKeyPoints on the GPU:
+    pts float32 [n, 2], K4 = (fx, fy, cx, cy), dist = 4 / 5 / 8 / 12 OpenCV coefficients."""
+    lib = _lib.load()
+    p = np.ascontiguousarray(pts, np.float32).reshape(-1, 2)
+    k = np.ascontiguousarray(K4, np.float32).reshape(4)
+    d = np.ascontiguousarray(dist, np.float32).reshape(-1)
+    out = np.zeros_like(p)
+    _lib.check(lib.orbfe_undistort_points(p.ctypes.data, len(p), k.ctypes.data, d.ctypes.data, len(d), out.ctypes.data),
+               "undistort_points")
+    return out

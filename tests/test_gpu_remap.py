@@ -49,3 +49,20 @@ def test_remap_batch_device(gpu, oracle_lib):
     got = out.cpu().numpy()
     for i in range(4):
         np.testing.assert_array_equal(got[i], oracle_lib.remap_linear(imgs[i], mx, my))
+
+
+@pytest.mark.parametrize("dist", [
+    (-0.28340811, 0.07395907, 0.00019359, 1.76187114e-05),            # EuRoC cam0 (radial-tangential)
+    (-0.28, 0.07, 2e-4, 1.8e-5, 0.01),                                 # + k3
+    (0.5, -0.3, 1e-3, -2e-3, 0.1, 0.4, -0.2, 0.05),                    # rational model
+    (-1.5, 0.9, 0.01, 0.01),                                           # strong: icdist < 0 near corners
+])
+def test_undistort_points(gpu, oracle_lib, dist):
+    from orb_slam3_ros_amd.rectify import undistort_points
+    rng = np.random.default_rng(len(dist))
+    K = (458.654, 457.296, 367.215, 248.375)
+    pts = np.stack([rng.uniform(-20, 772, 5000), rng.uniform(-20, 500, 5000)], 1).astype(np.float32)
+    pts[:4] = [[0, 0], [751, 479], [K[2], K[3]], [367.2151, 248.3749]]
+    g = undistort_points(pts, K, np.array(dist, np.float32))
+    o = oracle_lib.undistort_points(pts, K, np.array(dist, np.float32))
+    np.testing.assert_array_equal(g.view(np.uint32), o.view(np.uint32))
