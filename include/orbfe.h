@@ -259,6 +259,23 @@ int orbfe_search_local_points(const orbfe_frame* F, const orbfe_camera* cam, con
                               float thFarPoints, float nnratio, int32_t* n_to_match);
 
 /* ---------------------------------------------------------------------------------------------
+ * Back-end matcher pieces (LocalMapping / LoopClosing threads)
+ * ------------------------------------------------------------------------------------------- */
+/* SearchByBoW(pKF1, pKF2, vpMatches12) (ORBmatcher.cc:765-903, pinhole path): mp1 / mp2 =
+ * GetMapPointMatches() handles with NULL and bad points as -1; out12[n1] = the handle of the KF2
+ * point matched to each KF1 keypoint, or -1. Returns nmatches. */
+int orbfe_search_by_bow_kf(const orbfe_keypoint* keys1, const uint8_t* desc1, const int32_t* mp1, int32_t n1,
+                           const orbfe_feature_vector* fv1, const orbfe_keypoint* keys2, const uint8_t* desc2,
+                           const int32_t* mp2, int32_t n2, const orbfe_feature_vector* fv2, int32_t* out12,
+                           float nnratio, int32_t checkOri);
+
+/* MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:329-403) for n_points points at once: the
+ * observed descriptors of point p are rows [offsets[p], offsets[p+1]) of desc (<= 2048 per point).
+ * best[p] = the row (relative to offsets[p]) with the least median Hamming distance to the others
+ * (median = sorted row [(N-1)/2], first on ties), -1 for a point without descriptors. */
+int orbfe_distinctive_descriptors(const uint8_t* desc, const int32_t* offsets, int32_t n_points, int32_t* best);
+
+/* ---------------------------------------------------------------------------------------------
  * Bag of words: DBoW2::TemplatedVocabulary<FORB> (Thirdparty/DBoW2/DBoW2/
  * TemplatedVocabulary.h) — the loader of ORB-SLAM3's binary vocabulary format and transform(),
  * called by Frame::ComputeBoW (Frame.cc) with levelsup = 4. The vocabulary tree lives in HBM.

@@ -135,6 +135,8 @@ def _match_sigs(L):
     L.oro_search_for_init.argtypes = [vp, vp, vp, vp, ci, cf, ci]
     L.oro_search_by_bow.argtypes = [vp, vp, vp, ci, vp, vp, vp, vp, cf, ci]
     L.oro_stereo_knn_ratio.argtypes = [vp, ci, vp, ci, cf, vp, vp]
+    L.oro_search_by_bow_kf.argtypes = [vp, vp, vp, ci, vp, vp, vp, vp, ci, vp, vp, cf, ci]
+    L.oro_distinctive_descriptors.argtypes = [vp, vp, ci, vp]
     L.oro_is_in_frustum.argtypes = [vp, vp, vp, ci, vp]
     L.oro_search_local_points.argtypes = [vp, vp, vp, ci, vp, vp, cf, ci, cf, cf, vp]
     return L
@@ -173,6 +175,27 @@ class OracleMatcher:
         n = self.L.oro_search_by_bow(kk.ctypes.data, kd.ctypes.data, km.ctypes.data, len(km), kf_fv.ref(), F.ref(),
                                      f_fv.ref(), out.ctypes.data, self.nnratio, self.checkOri)
         return n, out
+
+    def search_by_bow_kf(self, keys1, desc1, mp1, fv1, keys2, desc2, mp2, fv2):
+        k1, k2 = np.ascontiguousarray(keys1), np.ascontiguousarray(keys2)
+        d1 = np.ascontiguousarray(desc1, np.uint8)
+        d2 = np.ascontiguousarray(desc2, np.uint8)
+        m1 = np.ascontiguousarray(mp1, np.int32)
+        m2 = np.ascontiguousarray(mp2, np.int32)
+        out = np.full(len(k1), -1, np.int32)
+        n = self.L.oro_search_by_bow_kf(k1.ctypes.data, d1.ctypes.data, m1.ctypes.data, len(k1), fv1.ref(),
+                                        k2.ctypes.data, d2.ctypes.data, m2.ctypes.data, len(k2), fv2.ref(),
+                                        out.ctypes.data, self.nnratio, self.checkOri)
+        return n, out
+
+
+def distinctive_descriptors(desc, offsets):
+    L = _match_sigs(lib())
+    d = np.ascontiguousarray(desc, np.uint8)
+    o = np.ascontiguousarray(offsets, np.int32)
+    best = np.full(len(o) - 1, -1, np.int32)
+    L.oro_distinctive_descriptors(d.ctypes.data, o.ctypes.data, len(o) - 1, best.ctypes.data)
+    return best
 
 
 def is_in_frustum(F, cam, pts3d):

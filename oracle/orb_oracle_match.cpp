@@ -8,6 +8,8 @@
 //   ORBmatcher::RadiusByViewingCos           ORBmatcher.cc:215-221
 //   ORBmatcher::SearchByBoW(KF, F)           ORBmatcher.cc:223-425       -> oro_search_by_bow()
 //   ORBmatcher::SearchForInitialization      ORBmatcher.cc:648-763       -> oro_search_for_init()
+//   ORBmatcher::SearchByBoW(KF, KF)          ORBmatcher.cc:765-903       -> oro_search_by_bow_kf()
+//   MapPoint::ComputeDistinctiveDescriptors  MapPoint.cc:329-403         -> oro_distinctive_descriptors()
 //   ORBmatcher::SearchByProjection (frame)   ORBmatcher.cc:1676-1887     -> oro_sbp_lastframe()
 //   ORBmatcher::SearchByProjection (KF)      ORBmatcher.cc:1889-2010     -> oro_sbp_kf()
 //   ORBmatcher::ComputeThreeMaxima           ORBmatcher.cc:2012-2053     -> three_maxima()
@@ -19,6 +21,7 @@
 // Only the pinhole / rectified branches (F.Nleft == -1) are restated; the KannalaBrandt8
 // right-camera branches are out of scope.
 // ============================================================================================
+#include <algorithm>
 #include <climits>
 #include <cmath>
 #include <cstdint>
@@ -334,6 +337,87 @@ int oro_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, con
         }
     }
     return nmatches;
+}
+
+// vbMatched2 / vpMatches12 are indexed by keypoint; the std::map walk is the same merge-join as
+// the KF-F variant. Note the strict bestDist1 < TH_LOW here (<= in the KF-F variant).
+int oro_search_by_bow_kf(const orbfe_keypoint* keys1, const uint8_t* desc1, const int32_t* mp1, int32_t n1,
+                         const orbfe_feature_vector* fv1, const orbfe_keypoint* keys2, const uint8_t* desc2,
+                         const int32_t* mp2, int32_t n2, const orbfe_feature_vector* fv2, int32_t* out12,
+                         float nnratio, int32_t checkOri) {
+    std::vector<int> rotHist[HISTO_LENGTH];
+    std::vector<char> vbMatched2(n2 > 0 ? n2 : 1, 0);
+    for (int i = 0; i < n1; i++) out12[i] = -1;
+    int nmatches = 0;
+    int a = 0, b = 0;
+    while (a < fv1->n_nodes && b < fv2->n_nodes) {
+        if (fv1->node_ids[a] == fv2->node_ids[b]) {
+            for (int ia = fv1->offsets[a]; ia < fv1->offsets[a + 1]; ia++) {
+                const unsigned idx1 = fv1->indices[ia];
+                if (mp1[idx1] < 0) continue;   // !pMP1 || pMP1->isBad()
+                const uint8_t* d1 = desc1 + (size_t)idx1 * 32;
+                int bestDist1 = 256, bestIdx2 = -1, bestDist2 = 256;
+                for (int ib = fv2->offsets[b]; ib < fv2->offsets[b + 1]; ib++) {
+                    const unsigned idx2 = fv2->indices[ib];
+                    if (vbMatched2[idx2] || mp2[idx2] < 0) continue;
+                    const int dist = oracle::hamming(d1, desc2 + (size_t)idx2 * 32);
+                    if (dist < bestDist1) { bestDist2 = bestDist1; bestDist1 = dist; bestIdx2 = (int)idx2; }
+                    else if (dist < bestDist2) bestDist2 = dist;
+                }
+                if (bestDist1 < TH_LOW) {
+                    if (static_cast<float>(bestDist1) < nnratio * static_cast<float>(bestDist2)) {
+                        out12[idx1] = mp2[bestIdx2];
+                        vbMatched2[bestIdx2] = 1;
+                        if (checkOri) rotHist[rot_bin(keys1[idx1].angle, keys2[bestIdx2].angle)].push_back((int)idx1);
+                        nmatches++;
+                    }
+                }
+            }
+            a++;
+            b++;
+        } else if (fv1->node_ids[a] < fv2->node_ids[b]) {
+            while (a < fv1->n_nodes && fv1->node_ids[a] < fv2->node_ids[b]) a++;
+        } else {
+            while (b < fv2->n_nodes && fv2->node_ids[b] < fv1->node_ids[a]) b++;
+        }
+    }
+    if (checkOri) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        three_maxima(rotHist, HISTO_LENGTH, ind1, ind2, ind3);
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            if (i == ind1 || i == ind2 || i == ind3) continue;
+            for (int k : rotHist[i]) { out12[k] = -1; nmatches--; }
+        }
+    }
+    return nmatches;
+}
+
+// Distances[N][N] (symmetric, zero diagonal), each row sorted, median = row[0.5 * (N - 1)] with the
+// index truncated, first row with the strictly smallest median wins.
+int oro_distinctive_descriptors(const uint8_t* desc, const int32_t* offsets, int32_t n_points, int32_t* best) {
+    for (int p = 0; p < n_points; p++) {
+        const int N = offsets[p + 1] - offsets[p];
+        if (N == 0) { best[p] = -1; continue; }
+        const uint8_t* d = desc + (size_t)offsets[p] * 32;
+        std::vector<std::vector<float>> Distances(N, std::vector<float>(N));
+        for (int i = 0; i < N; i++) {
+            Distances[i][i] = 0;
+            for (int j = i + 1; j < N; j++) {
+                const int distij = oracle::hamming(d + (size_t)i * 32, d + (size_t)j * 32);
+                Distances[i][j] = distij;
+                Distances[j][i] = distij;
+            }
+        }
+        int BestMedian = INT_MAX, BestIdx = 0;
+        for (int i = 0; i < N; i++) {
+            std::vector<int> vDists(Distances[i].begin(), Distances[i].end());
+            std::sort(vDists.begin(), vDists.end());
+            const int median = vDists[(size_t)(0.5 * (N - 1))];
+            if (median < BestMedian) { BestMedian = median; BestIdx = i; }
+        }
+        best[p] = BestIdx;
+    }
+    return n_points;
 }
 
 // BFMatcher(NORM_HAMMING).knnMatch(k=2): per query the two smallest distances, earlier train index

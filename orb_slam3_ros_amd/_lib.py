@@ -56,6 +56,9 @@ _SIGS = {
     "orbfe_search_by_projection_kf": (_c_int, [_vp, _vp, _vp, _c_int, _c_float, _c_int, _c_int]),
     "orbfe_search_for_initialization": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _c_float, _c_int]),
     "orbfe_search_by_bow": (_c_int, [_vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_float, _c_int]),
+    "orbfe_search_by_bow_kf": (_c_int, [_vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _c_float,
+                                        _c_int]),
+    "orbfe_distinctive_descriptors": (_c_int, [_vp, _vp, _c_int, _vp]),
     "orbfe_stereo_knn_ratio": (_c_int, [_vp, _c_int, _vp, _c_int, _c_float, _vp, _vp]),
     "orbfe_matcher_set_timing": (_c_int, [_c_int]),
     "orbfe_undistort_points": (_c_int, [_vp, _c_int, _vp, _vp, _c_int, _vp]),

@@ -686,6 +686,9 @@ int orbfe_descriptor_distance(const uint8_t* a, const uint8_t* b) {
 // ORBmatcher methods (kernels + host wrappers; uses HIPCHK above).
 #include "orbfe_matcher.hip"
 
+// Back-end matcher pieces (SearchByBoW(KF, KF), ComputeDistinctiveDescriptors).
+#include "orbfe_backend.hip"
+
 // DBoW2 vocabulary transform (uses the matcher's per-thread arena).
 #include "orbfe_bow.hip"
 

@@ -210,6 +210,50 @@ class ORBmatcher:
             out.ctypes.data, self.mfNNratio, int(self.mbCheckOrientation)), "SearchByBoW")
         return n, out
 
+    # SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12) (:765-903)
+    def SearchByBoWKF(self, keys1, desc1, map_points1, featvec1: FeatureVector, keys2, desc2, map_points2,
+                      featvec2: FeatureVector):
+        """LocalMapping / LoopClosing variant. map_points* = GetMapPointMatches() handles, -1 for
+        NULL or bad points. Returns (nmatches, vpMatches12 int32 [len(keys1)]: KF2 handles or -1)."""
+        k1 = np.ascontiguousarray(keys1, KEYPOINT_DTYPE).reshape(-1)
+        k2 = np.ascontiguousarray(keys2, KEYPOINT_DTYPE).reshape(-1)
+        d1 = np.ascontiguousarray(desc1, np.uint8).reshape(-1, 32)
+        d2 = np.ascontiguousarray(desc2, np.uint8).reshape(-1, 32)
+        if len(d1) != len(k1) or len(d2) != len(k2):
+            raise ValueError("descriptor rows must match the keypoints")
+        m1 = _i32(np.ascontiguousarray(map_points1, np.int32), len(k1), "map_points1")
+        m2 = _i32(np.ascontiguousarray(map_points2, np.int32), len(k2), "map_points2")
+        out = np.full(len(k1), -1, np.int32)
+        n = _lib.check(self._lib.orbfe_search_by_bow_kf(
+            k1.ctypes.data, d1.ctypes.data, m1.ctypes.data, len(k1), featvec1.ref(), k2.ctypes.data, d2.ctypes.data,
+            m2.ctypes.data, len(k2), featvec2.ref(), out.ctypes.data, self.mfNNratio,
+            int(self.mbCheckOrientation)), "SearchByBoW(KF, KF)")
+        return n, out
+
+
+def compute_distinctive_descriptors(descriptor_sets):
+    """MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:329-403) for many points at once on the
+    GPU. descriptor_sets: a list of (N_i, 32) uint8 arrays (the descriptors of each point's
+    non-bad observations), or a (desc, offsets) pair of the concatenated rows and N+1 offsets.
+    Returns int32 [n_points]: the chosen row of each set, -1 for an empty set."""
+    if isinstance(descriptor_sets, tuple):
+        desc, offsets = descriptor_sets
+        desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        offsets = np.ascontiguousarray(offsets, np.int32)
+    else:
+        sets = [np.asarray(d, np.uint8).reshape(-1, 32) for d in descriptor_sets]
+        offsets = np.zeros(len(sets) + 1, np.int32)
+        offsets[1:] = np.cumsum([len(d) for d in sets])
+        desc = np.ascontiguousarray(np.concatenate(sets) if sets else np.zeros((0, 32), np.uint8))
+    n = len(offsets) - 1
+    if n < 0 or (n >= 0 and offsets[-1] != len(desc)):
+        raise ValueError("offsets must end at the number of descriptor rows")
+    best = np.full(max(n, 0), -1, np.int32)
+    lib = _lib.load()
+    _lib.check(lib.orbfe_distinctive_descriptors(desc.ctypes.data, offsets.ctypes.data, n, best.ctypes.data),
+               "ComputeDistinctiveDescriptors")
+    return best
+
 
 def is_in_frustum(F: MatchFrame, cam: Camera, points3d):
     """Frame::isInFrustum + MapPoint::PredictScale over points3d (MAP_POINT_3D_DTYPE) on the GPU.

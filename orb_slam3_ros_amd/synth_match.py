@@ -167,6 +167,33 @@ def synth_bow(rng, n_words: int, kf: MatchFrame, F: MatchFrame, shared_src=None)
     return fv(wk), fv(wf)
 
 
+def synth_kf_pair(rng, n1, words, rot=20.0, drop=0.15):
+    """Two keyframes sharing a scene: KF2 = perturbed copy of KF1 (dropped / extra points,
+    rotated angles), map-point handles with NULL / bad (-1) slots on both sides."""
+    K1 = synth_frame(rng, n1, stereo=False)
+    K2, src = perturbed_frame(rng, K1, rot=rot, flip_p=0.05, drop=drop)
+    mp1 = np.where(rng.random(K1.N) < 0.2, -1, np.arange(K1.N) + 10).astype(np.int32)
+    mp2 = np.where(rng.random(K2.N) < 0.2, -1, np.arange(K2.N) + 5000).astype(np.int32)
+    fv1, fv2 = synth_bow(rng, words, K1, K2, src)
+    return K1, K2, mp1, mp2, fv1, fv2
+
+
+def synth_distinctive_sets(rng, sizes, flip_p=0.2):
+    """Per-map-point observation descriptor sets (noisy copies of one descriptor) with duplicate
+    rows (equal medians: the first row must win)."""
+    sets = []
+    for N in sizes:
+        if N == 0:
+            sets.append(np.zeros((0, 32), np.uint8))
+            continue
+        base = rng.integers(0, 256, 32, dtype=np.uint8)
+        d = flip_bits(rng, np.repeat(base[None], N, 0), flip_p)
+        if N >= 4:
+            d[1] = d[3]
+        sets.append(d)
+    return sets
+
+
 def synth_camera(rng, fx=458.654, fy=457.296, cx=367.215, cy=248.375, rot_deg=10.0):
     """A random pose (rotation of up to rot_deg about a random axis, translation ~1 m)."""
     axis = rng.normal(size=3)

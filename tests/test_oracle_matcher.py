@@ -301,3 +301,102 @@ def test_oracle_frustum_vs_python(oracle_lib, seed):
                    int(tr["scale_level"][i]))
             assert [np.float32(a).tobytes() for a in got[:5]] == [np.float32(b).tobytes() for b in r[:5]], i
             assert got[5] == r[5], i
+
+
+def _py_three_maxima(hist):
+    max1 = max2 = max3 = 0
+    i1 = i2 = i3 = -1
+    for i, c in enumerate(hist):
+        if c > max1:
+            max3, max2, max1, i3, i2, i1 = max2, max1, c, i2, i1, i
+        elif c > max2:
+            max3, max2, i3, i2 = max2, c, i2, i
+        elif c > max3:
+            max3, i3 = c, i
+    if max2 < f32(0.1) * f32(max1):
+        i2 = i3 = -1
+    elif max3 < f32(0.1) * f32(max1):
+        i3 = -1
+    return {i1, i2, i3}
+
+
+def _py_rot_bin(a1, a2):
+    rot = f32(f32(a1) - f32(a2))
+    if rot < 0.0:
+        rot = f32(rot + f32(360.0))
+    b = int(round_half_away(f32(rot * f32(f32(1.0) / f32(30)))))
+    return 0 if b == 30 else b
+
+
+def py_search_by_bow_kf(k1, d1, mp1, fv1, k2, d2, mp2, fv2, nnratio, check_ori):
+    """ORBmatcher::SearchByBoW(KF, KF) (ORBmatcher.cc:765-903), literal."""
+    out = np.full(len(k1), -1, np.int32)
+    matched2 = np.zeros(len(k2), bool)
+    nodes2 = {int(n): fv2.indices[fv2.offsets[j]:fv2.offsets[j + 1]] for j, n in enumerate(fv2.node_ids)}
+    hist = [[] for _ in range(30)]
+    n = 0
+    for a, node in enumerate(fv1.node_ids):
+        if int(node) not in nodes2:
+            continue
+        for i1 in fv1.indices[fv1.offsets[a]:fv1.offsets[a + 1]]:
+            if mp1[i1] < 0:
+                continue
+            b1, bi, b2 = 256, -1, 256
+            for i2 in nodes2[int(node)]:
+                if matched2[i2] or mp2[i2] < 0:
+                    continue
+                d = _ham(d1[i1], d2[i2])
+                if d < b1:
+                    b2, b1, bi = b1, d, int(i2)
+                elif d < b2:
+                    b2 = d
+            if b1 < 50 and f32(b1) < f32(f32(nnratio) * f32(b2)):
+                out[i1] = mp2[bi]
+                matched2[bi] = True
+                if check_ori:
+                    hist[_py_rot_bin(k1[i1]["angle"], k2[bi]["angle"])].append(int(i1))
+                n += 1
+    if check_ori:
+        keep = _py_three_maxima([len(h) for h in hist])
+        for i, h in enumerate(hist):
+            if i not in keep:
+                for j in h:
+                    out[j] = -1
+                    n -= 1
+    return n, out
+
+
+def py_distinctive(sets):
+    """MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:329-403)."""
+    best = []
+    for d in sets:
+        N = len(d)
+        if N == 0:
+            best.append(-1)
+            continue
+        D = np.unpackbits(d[:, None, :] ^ d[None, :, :], axis=2).sum(2)
+        med = [int(np.sort(D[i])[int(0.5 * (N - 1))]) for i in range(N)]
+        best.append(int(np.argmin(med)))   # argmin = first minimum
+    return np.array(best, np.int32)
+
+
+@pytest.mark.parametrize("seed,check_ori", [(0, True), (1, False), (2, True)])
+def test_oracle_bow_kf_vs_python(oracle_lib, seed, check_ori):
+    rng = np.random.default_rng(seed)
+    K1, K2, mp1, mp2, fv1, fv2 = sm.synth_kf_pair(rng, 250, 40)
+    no, oo = oracle_lib.OracleMatcher(0.75, check_ori).search_by_bow_kf(K1.keys, K1.desc, mp1, fv1, K2.keys,
+                                                                          K2.desc, mp2, fv2)
+    np_, op = py_search_by_bow_kf(K1.keys, K1.desc, mp1, fv1, K2.keys, K2.desc, mp2, fv2, 0.75, check_ori)
+    assert no == np_ and no > 0
+    np.testing.assert_array_equal(oo, op)
+    assert no == (oo >= 0).sum()
+
+
+def test_oracle_distinctive_vs_python(oracle_lib):
+    rng = np.random.default_rng(5)
+    sets = sm.synth_distinctive_sets(rng, [0, 1, 2, 3, 4, 7, 30, 64, 65, 130])
+    offs = np.zeros(len(sets) + 1, np.int32)
+    offs[1:] = np.cumsum([len(d) for d in sets])
+    got = oracle_lib.distinctive_descriptors(np.concatenate(sets), offs)
+    np.testing.assert_array_equal(got, py_distinctive(sets))
+    assert got[0] == -1 and got[1] == 0
