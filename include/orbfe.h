@@ -275,6 +275,73 @@ int orbfe_search_by_bow_kf(const orbfe_keypoint* keys1, const uint8_t* desc1, co
  * (median = sorted row [(N-1)/2], first on ties), -1 for a point without descriptors. */
 int orbfe_distinctive_descriptors(const uint8_t* desc, const int32_t* offsets, int32_t n_points, int32_t* best);
 
+/* SearchForTriangulation(pKF1, pKF2, vMatchedPairs, bOnlyStereo, bCoarse) (ORBmatcher.cc:907-1146,
+ * pinhole keyframes without a second camera). mp1 / mp2: GetMapPoint(idx) presence (any MapPoint,
+ * bad or not, -> handle >= 0; NULL -> -1); keyframe uright = mvuRight (NULL = all monocular).
+ * F12 (row-major) and ep are the values the reference derives once per call:
+ * F12 = K1^-T [t12]x R12 K2^-1 (Pinhole::epipolarConstrain, Pinhole.cpp:107-129) and
+ * ep = pKF2->mpCamera->project(T2w * Cw1). level_sigma2_2 = pKF2->mvLevelSigma2.
+ * matches12[KF1->n] = the KF2 index matched to each KF1 keypoint or -1 (vMatchedPairs in
+ * ascending idx1 order). Returns nmatches. */
+int orbfe_search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, const orbfe_feature_vector* fv1,
+                                   const orbfe_frame* KF2, const int32_t* mp2, const orbfe_feature_vector* fv2,
+                                   const float* F12, const float* ep, const float* level_sigma2_2,
+                                   int32_t bOnlyStereo, int32_t bCoarse, int32_t checkOri, int32_t* matches12);
+
+/* A Sophus pose as the reference stores it: quaternion (x, y, z, w) + translation.
+ * kind ORBFE_SE3: Sophus::SE3f, unit quaternion, p' = (p + w*uv + v x uv) + t with uv = 2 (v x p)
+ *                 (sophus/so3.hpp:358-367, se3.hpp:321-324);
+ * kind ORBFE_SIM3: Sophus::Sim3f, RxSO3 quaternion with scale |q|^2,
+ *                 p' = (s*p + (w*uv + v x uv)) + t (rxso3.hpp:265-273, sim3.hpp:226-229). */
+#define ORBFE_SE3 0
+#define ORBFE_SIM3 1
+typedef struct orbfe_pose {
+    float q[4];
+    float t[3];
+    int32_t kind;
+} orbfe_pose;                        /* 32 bytes */
+
+/* What the back-end projections read of a keyframe besides orbfe_frame. */
+typedef struct orbfe_kf_camera {
+    orbfe_pose Tcw;                  /* world -> camera (GetPose(), or the SE3 made from Scw) */
+    float Ow[3];                     /* camera centre for the distance / viewing checks */
+    float fx, fy, cx, cy;
+    float log_scale_factor;          /* mfLogScaleFactor */
+} orbfe_kf_camera;
+
+/* The matching half of Fuse (ORBmatcher.cc:1148-1337 with sim3 = 0; :1339-1455, Fuse(pKF, Scw, ...)
+ * with sim3 = 1; pinhole, bRight = false): for every point with id >= 0 not flagged BAD / SKIP (SKIP =
+ * IsInKeyFrame(pKF), resp. already in pKF->GetMapPoints()), project, check and search the keyframe
+ * exactly as the reference loop does, and report best_idx[i] (-1 unless bestDist <= TH_LOW) and
+ * best_dist[i]. The map mutation that follows (Replace / AddObservation / vpReplacePoint) stays
+ * with the caller, in point order: a point's search reads nothing an earlier commit changes, only
+ * its isBad / IsInKeyFrame gate has to be re-read at commit time.
+ * inv_level_sigma2 = pKF->mvInvLevelSigma2. Returns the number of points with best_idx >= 0. */
+int orbfe_fuse(const orbfe_frame* KF, const orbfe_kf_camera* cam, const float* inv_level_sigma2,
+               const orbfe_map_point_3d* pts, int32_t n, float th, int32_t sim3, int32_t* best_idx,
+               int32_t* best_dist);
+
+/* SearchByProjection(pKF, Scw, vpPoints, vpMatched, th, ratioHamming) (ORBmatcher.cc:427-523) and,
+ * with point_kfs != NULL, the vpPointsKFs / vpMatchedKF overload (:525-646). cam->Tcw is the SE3
+ * the reference builds from Scw; matched = vpMatched handles [KF->n] (in/out), matched_kf =
+ * vpMatchedKF handles (in/out, with point_kfs). Points whose handle is already in matched, or
+ * flagged BAD, are skipped (so are id < 0 entries, which the reference cannot hold); a keypoint taken by an earlier point is not a candidate for later
+ * ones (sequential semantics preserved). Returns nmatches. */
+int orbfe_search_by_projection_sim3(const orbfe_frame* KF, const orbfe_kf_camera* cam, const orbfe_map_point_3d* pts,
+                                    int32_t n, const int32_t* point_kfs, int32_t th, float ratioHamming,
+                                    int32_t* matched, int32_t* matched_kf);
+
+/* SearchBySim3(pKF1, pKF2, vpMatches12, S12, th) (ORBmatcher.cc:1457-1674). pts1[KF1->n] /
+ * pts2[KF2->n]: the keyframes' GetMapPointMatches() (id < 0 = NULL, flags BAD = isBad()).
+ * cam1 = {T1w, pKF1 intrinsics (used for both projections), pKF1->mfLogScaleFactor};
+ * cam2 = {T2w, log scale factor of pKF2}; S12 / S21 Sim3 poses. matches12 = vpMatches12 handles
+ * (in/out); matched_idx2[i] = get<0>(vpMatches12[i]->GetIndexInKeyFrame(pKF2)) for the initial
+ * matches (-1 otherwise). Returns nFound. */
+int orbfe_search_by_sim3(const orbfe_frame* KF1, const orbfe_frame* KF2, const orbfe_map_point_3d* pts1,
+                         const orbfe_map_point_3d* pts2, const orbfe_kf_camera* cam1, const orbfe_kf_camera* cam2,
+                         const orbfe_pose* S12, const orbfe_pose* S21, float th, int32_t* matches12,
+                         const int32_t* matched_idx2);
+
 /* ---------------------------------------------------------------------------------------------
  * Bag of words: DBoW2::TemplatedVocabulary<FORB> (Thirdparty/DBoW2/DBoW2/
  * TemplatedVocabulary.h) — the loader of ORB-SLAM3's binary vocabulary format and transform(),

@@ -137,6 +137,10 @@ def _match_sigs(L):
     L.oro_stereo_knn_ratio.argtypes = [vp, ci, vp, ci, cf, vp, vp]
     L.oro_search_by_bow_kf.argtypes = [vp, vp, vp, ci, vp, vp, vp, vp, ci, vp, vp, cf, ci]
     L.oro_distinctive_descriptors.argtypes = [vp, vp, ci, vp]
+    L.oro_search_for_triangulation.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, vp]
+    L.oro_fuse.argtypes = [vp, vp, vp, vp, ci, cf, ci, vp, vp]
+    L.oro_sbp_sim3.argtypes = [vp, vp, vp, ci, vp, ci, cf, vp, vp]
+    L.oro_search_by_sim3.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, cf, vp, vp]
     L.oro_is_in_frustum.argtypes = [vp, vp, vp, ci, vp]
     L.oro_search_local_points.argtypes = [vp, vp, vp, ci, vp, vp, cf, ci, cf, cf, vp]
     return L
@@ -187,6 +191,46 @@ class OracleMatcher:
                                         k2.ctypes.data, d2.ctypes.data, m2.ctypes.data, len(k2), fv2.ref(),
                                         out.ctypes.data, self.nnratio, self.checkOri)
         return n, out
+
+
+    def search_for_triangulation(self, KF1, mp1, fv1, KF2, mp2, fv2, F12, ep, level_sigma2_2, bOnlyStereo=False,
+                                 bCoarse=False):
+        m1 = np.ascontiguousarray(mp1, np.int32)
+        m2 = np.ascontiguousarray(mp2, np.int32)
+        F = np.ascontiguousarray(F12, np.float32).reshape(9)
+        e = np.ascontiguousarray(ep, np.float32).reshape(2)
+        sg = np.ascontiguousarray(level_sigma2_2, np.float32)
+        out = np.full(KF1.N, -1, np.int32)
+        n = self.L.oro_search_for_triangulation(KF1.ref(), m1.ctypes.data, fv1.ref(), KF2.ref(), m2.ctypes.data,
+                                                fv2.ref(), F.ctypes.data, e.ctypes.data, sg.ctypes.data,
+                                                int(bOnlyStereo), int(bCoarse), self.checkOri, out.ctypes.data)
+        return n, out
+
+    def fuse(self, KF, cam, pts, th=3.0, inv_level_sigma2=None, sim3=False):
+        if inv_level_sigma2 is None:
+            sf = KF.scale_factors
+            inv_level_sigma2 = (np.float32(1.0) / (sf * sf)).astype(np.float32)
+        sig = np.ascontiguousarray(inv_level_sigma2, np.float32)
+        p = np.ascontiguousarray(pts)
+        bi = np.full(len(p), -1, np.int32)
+        bd = np.full(len(p), -1, np.int32)
+        n = self.L.oro_fuse(KF.ref(), ctypes.byref(cam), sig.ctypes.data, p.ctypes.data, len(p), float(th),
+                            int(bool(sim3)), bi.ctypes.data, bd.ctypes.data)
+        return n, bi, bd
+
+    def sbp_sim3(self, KF, cam, pts, matched, th=10, ratioHamming=1.0, point_kfs=None, matched_kf=None):
+        p = np.ascontiguousarray(pts)
+        pk = None if point_kfs is None else np.ascontiguousarray(point_kfs, np.int32)
+        return self.L.oro_sbp_sim3(KF.ref(), ctypes.byref(cam), p.ctypes.data, len(p),
+                                   None if pk is None else pk.ctypes.data, int(th), float(ratioHamming),
+                                   matched.ctypes.data, None if matched_kf is None else matched_kf.ctypes.data)
+
+    def search_by_sim3(self, KF1, KF2, pts1, pts2, cam1, cam2, S12, S21, th, matches12, matched_idx2=None):
+        p1, p2 = np.ascontiguousarray(pts1), np.ascontiguousarray(pts2)
+        mi = None if matched_idx2 is None else np.ascontiguousarray(matched_idx2, np.int32)
+        return self.L.oro_search_by_sim3(KF1.ref(), KF2.ref(), p1.ctypes.data, p2.ctypes.data, ctypes.byref(cam1),
+                                         ctypes.byref(cam2), ctypes.byref(S12), ctypes.byref(S21), float(th),
+                                         matches12.ctypes.data, None if mi is None else mi.ctypes.data)
 
 
 def distinctive_descriptors(desc, offsets):

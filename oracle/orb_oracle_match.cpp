@@ -10,6 +10,13 @@
 //   ORBmatcher::SearchForInitialization      ORBmatcher.cc:648-763       -> oro_search_for_init()
 //   ORBmatcher::SearchByBoW(KF, KF)          ORBmatcher.cc:765-903       -> oro_search_by_bow_kf()
 //   MapPoint::ComputeDistinctiveDescriptors  MapPoint.cc:329-403         -> oro_distinctive_descriptors()
+//   ORBmatcher::SearchForTriangulation       ORBmatcher.cc:907-1146      -> oro_search_for_triangulation()
+//   Pinhole::epipolarConstrain               Pinhole.cpp:107-129
+//   ORBmatcher::Fuse(KF, vpMapPoints)        ORBmatcher.cc:1148-1337     -> oro_fuse(sim3 = 0)
+//   ORBmatcher::Fuse(KF, Scw, ...)           ORBmatcher.cc:1339-1455     -> oro_fuse(sim3 = 1)
+//   ORBmatcher::SearchByProjection (Sim3)    ORBmatcher.cc:427-646       -> oro_sbp_sim3()
+//   ORBmatcher::SearchBySim3                 ORBmatcher.cc:1457-1674     -> oro_search_by_sim3()
+//   Sophus SO3/RxSO3 point action            so3.hpp:358-367, rxso3.hpp:265-273
 //   ORBmatcher::SearchByProjection (frame)   ORBmatcher.cc:1676-1887     -> oro_sbp_lastframe()
 //   ORBmatcher::SearchByProjection (KF)      ORBmatcher.cc:1889-2010     -> oro_sbp_kf()
 //   ORBmatcher::ComputeThreeMaxima           ORBmatcher.cc:2012-2053     -> three_maxima()
@@ -418,6 +425,279 @@ int oro_distinctive_descriptors(const uint8_t* desc, const int32_t* offsets, int
         best[p] = BestIdx;
     }
     return n_points;
+}
+
+// ---- back-end projections ----
+// Sophus point action in Eigen's evaluation order (no contraction). RxSO3's scale is
+// quaternion().squaredNorm(), which Eigen reduces as one SSE packet: (x*x + z*z) + (y*y + w*w).
+static void pose_apply(const orbfe_pose& P, const float p[3], float o[3]) {
+    const float vx = P.q[0], vy = P.q[1], vz = P.q[2], w = P.q[3];
+    float uv[3] = {vy * p[2] - vz * p[1], vz * p[0] - vx * p[2], vx * p[1] - vy * p[0]};
+    for (int k = 0; k < 3; k++) uv[k] += uv[k];
+    const float c[3] = {vy * uv[2] - vz * uv[1], vz * uv[0] - vx * uv[2], vx * uv[1] - vy * uv[0]};
+    if (P.kind == ORBFE_SIM3) {
+        const float sc = (vx * vx + vz * vz) + (vy * vy + w * w);
+        for (int k = 0; k < 3; k++) o[k] = (sc * p[k] + (w * uv[k] + c[k])) + P.t[k];
+    } else {
+        for (int k = 0; k < 3; k++) o[k] = ((p[k] + w * uv[k]) + c[k]) + P.t[k];
+    }
+}
+
+static bool kf_in_image(const orbfe_frame* F, float x, float y) {   // KeyFrame::IsInImage (KeyFrame.cc:753-756)
+    return x >= F->min_x && x < F->max_x && y >= F->min_y && y < F->max_y;
+}
+
+static int predict_scale(float max_dist, float dist, float logsf, int nlevels) {   // MapPoint.cc:514-529
+    const float ratio = max_dist / dist;
+    int nScale = (int)std::ceil(logf(ratio) / logsf);
+    if (nScale < 0) nScale = 0;
+    else if (nScale >= nlevels) nScale = nlevels - 1;
+    return nScale;
+}
+
+// Pinhole::epipolarConstrain with F12 precomputed (the value is the same on every call).
+static bool epipolar(const orbfe_keypoint& kp1, const orbfe_keypoint& kp2, const float* F, float unc) {
+    const float a = kp1.x * F[0] + kp1.y * F[3] + F[6];
+    const float b = kp1.x * F[1] + kp1.y * F[4] + F[7];
+    const float c = kp1.x * F[2] + kp1.y * F[5] + F[8];
+    const float num = a * kp2.x + b * kp2.y + c;
+    const float den = a * a + b * b;
+    if (den == 0) return false;
+    const float dsqr = num * num / den;
+    return dsqr < 3.84 * unc;
+}
+
+int oro_search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, const orbfe_feature_vector* fv1,
+                                 const orbfe_frame* KF2, const int32_t* mp2, const orbfe_feature_vector* fv2,
+                                 const float* F12, const float* ep, const float* level_sigma2_2, int32_t bOnlyStereo,
+                                 int32_t bCoarse, int32_t checkOri, int32_t* matches12) {
+    std::vector<int> rotHist[HISTO_LENGTH];
+    for (int i = 0; i < KF1->n; i++) matches12[i] = -1;
+    int nmatches = 0;
+    int a = 0, b = 0;
+    while (a < fv1->n_nodes && b < fv2->n_nodes) {
+        if (fv1->node_ids[a] == fv2->node_ids[b]) {
+            for (int ia = fv1->offsets[a]; ia < fv1->offsets[a + 1]; ia++) {
+                const unsigned idx1 = fv1->indices[ia];
+                if (mp1[idx1] >= 0) continue;   // a MapPoint is already there
+                const bool bStereo1 = KF1->uright && KF1->uright[idx1] >= 0;
+                if (bOnlyStereo && !bStereo1) continue;
+                const orbfe_keypoint& kp1 = KF1->keys[idx1];
+                const uint8_t* d1 = KF1->desc + (size_t)idx1 * 32;
+                int bestDist = TH_LOW, bestIdx2 = -1;
+                for (int ib = fv2->offsets[b]; ib < fv2->offsets[b + 1]; ib++) {
+                    const unsigned idx2 = fv2->indices[ib];
+                    if (mp2[idx2] >= 0) continue;   // vbMatched2 is never set by the reference
+                    const bool bStereo2 = KF2->uright && KF2->uright[idx2] >= 0;
+                    if (bOnlyStereo && !bStereo2) continue;
+                    const int dist = oracle::hamming(d1, KF2->desc + (size_t)idx2 * 32);
+                    if (dist > TH_LOW || dist > bestDist) continue;
+                    const orbfe_keypoint& kp2 = KF2->keys[idx2];
+                    if (!bStereo1 && !bStereo2) {
+                        const float distex = ep[0] - kp2.x;
+                        const float distey = ep[1] - kp2.y;
+                        if (distex * distex + distey * distey < 100 * KF2->scale_factors[kp2.octave]) continue;
+                    }
+                    if (bCoarse || epipolar(kp1, kp2, F12, level_sigma2_2[kp2.octave])) {
+                        bestIdx2 = (int)idx2;
+                        bestDist = dist;
+                    }
+                }
+                if (bestIdx2 >= 0) {
+                    matches12[idx1] = bestIdx2;
+                    nmatches++;
+                    if (checkOri) rotHist[rot_bin(kp1.angle, KF2->keys[bestIdx2].angle)].push_back((int)idx1);
+                }
+            }
+            a++;
+            b++;
+        } else if (fv1->node_ids[a] < fv2->node_ids[b]) {
+            while (a < fv1->n_nodes && fv1->node_ids[a] < fv2->node_ids[b]) a++;
+        } else {
+            while (b < fv2->n_nodes && fv2->node_ids[b] < fv1->node_ids[a]) b++;
+        }
+    }
+    if (checkOri) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        three_maxima(rotHist, HISTO_LENGTH, ind1, ind2, ind3);
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            if (i == ind1 || i == ind2 || i == ind3) continue;
+            for (int k : rotHist[i]) { matches12[k] = -1; nmatches--; }
+        }
+    }
+    return nmatches;
+}
+
+// The search half of both Fuse overloads; best_dist = -1 when no candidate survived the checks.
+int oro_fuse(const orbfe_frame* KF, const orbfe_kf_camera* cam, const float* inv_level_sigma2,
+             const orbfe_map_point_3d* pts, int32_t n, float th, int32_t sim3, int32_t* best_idx, int32_t* best_dist) {
+    const Grid grid(KF);
+    int nFused = 0;
+    for (int i = 0; i < n; i++) {
+        best_idx[i] = -1;
+        best_dist[i] = -1;
+        const orbfe_map_point_3d& mp = pts[i];
+        if (mp.id < 0) continue;   // !pMP
+        if (mp.flags & (ORBFE_MP_BAD | ORBFE_MP_SKIP)) continue;
+        float p3Dc[3];
+        pose_apply(cam->Tcw, mp.pos, p3Dc);
+        if (p3Dc[2] < 0.0f) continue;
+        const float invz = 1 / p3Dc[2];
+        const float u = cam->fx * p3Dc[0] / p3Dc[2] + cam->cx;   // Pinhole::project
+        const float v = cam->fy * p3Dc[1] / p3Dc[2] + cam->cy;
+        if (!kf_in_image(KF, u, v)) continue;
+        const float ur = u - KF->mbf * invz;
+        const float maxDistance = 1.2f * mp.max_dist, minDistance = 0.8f * mp.min_dist;
+        const float PO[3] = {mp.pos[0] - cam->Ow[0], mp.pos[1] - cam->Ow[1], mp.pos[2] - cam->Ow[2]};
+        const float dist3D = std::sqrt((PO[0] * PO[0] + PO[1] * PO[1]) + PO[2] * PO[2]);
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const float dotn = (PO[0] * mp.normal[0] + PO[1] * mp.normal[1]) + PO[2] * mp.normal[2];
+        if (dotn < 0.5 * dist3D) continue;
+        const int nPredictedLevel = predict_scale(mp.max_dist, dist3D, cam->log_scale_factor, KF->nlevels);
+        const float radius = th * KF->scale_factors[nPredictedLevel];
+        const std::vector<size_t> vIndices = grid.area(u, v, radius, -1, -1);
+        if (vIndices.empty()) continue;
+        int bestDist = sim3 ? INT_MAX : 256, bestIdx = -1;
+        for (size_t idx : vIndices) {
+            const orbfe_keypoint& kp = KF->keys[idx];
+            const int kpLevel = kp.octave;
+            if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+            if (!sim3) {
+                if (KF->uright && KF->uright[idx] >= 0) {
+                    const float ex = u - kp.x, ey = v - kp.y, er = ur - KF->uright[idx];
+                    const float e2 = ex * ex + ey * ey + er * er;
+                    if (e2 * inv_level_sigma2[kpLevel] > 7.8) continue;
+                } else {
+                    const float ex = u - kp.x, ey = v - kp.y;
+                    const float e2 = ex * ex + ey * ey;
+                    if (e2 * inv_level_sigma2[kpLevel] > 5.99) continue;
+                }
+            }
+            const int dist = oracle::hamming(mp.desc, KF->desc + idx * 32);
+            if (dist < bestDist) { bestDist = dist; bestIdx = (int)idx; }
+        }
+        if (bestIdx >= 0) best_dist[i] = bestDist;
+        if (bestDist <= TH_LOW) {
+            best_idx[i] = bestIdx;
+            nFused++;
+        }
+    }
+    return nFused;
+}
+
+int oro_sbp_sim3(const orbfe_frame* KF, const orbfe_kf_camera* cam, const orbfe_map_point_3d* pts, int32_t n,
+                 const int32_t* point_kfs, int32_t th, float ratioHamming, int32_t* matched, int32_t* matched_kf) {
+    const Grid grid(KF);
+    std::vector<int32_t> found;
+    for (int k = 0; k < KF->n; k++)
+        if (matched[k] >= 0) found.push_back(matched[k]);
+    std::sort(found.begin(), found.end());
+    int nmatches = 0;
+    for (int iMP = 0; iMP < n; iMP++) {
+        const orbfe_map_point_3d& mp = pts[iMP];
+        if (mp.id < 0) continue;   // NULL entry (the reference dereferences it; the API skips it)
+        if ((mp.flags & ORBFE_MP_BAD) || std::binary_search(found.begin(), found.end(), mp.id)) continue;
+        float p3Dc[3];
+        pose_apply(cam->Tcw, mp.pos, p3Dc);
+        if (p3Dc[2] < 0.0) continue;
+        float u, v;
+        if (!point_kfs) {
+            u = cam->fx * p3Dc[0] / p3Dc[2] + cam->cx;
+            v = cam->fy * p3Dc[1] / p3Dc[2] + cam->cy;
+        } else {
+            const float invz = 1 / p3Dc[2];
+            const float x = p3Dc[0] * invz, y = p3Dc[1] * invz;
+            u = cam->fx * x + cam->cx;
+            v = cam->fy * y + cam->cy;
+        }
+        if (!kf_in_image(KF, u, v)) continue;
+        const float maxDistance = 1.2f * mp.max_dist, minDistance = 0.8f * mp.min_dist;
+        const float PO[3] = {mp.pos[0] - cam->Ow[0], mp.pos[1] - cam->Ow[1], mp.pos[2] - cam->Ow[2]};
+        const float dist = std::sqrt((PO[0] * PO[0] + PO[1] * PO[1]) + PO[2] * PO[2]);
+        if (dist < minDistance || dist > maxDistance) continue;
+        const float dotn = (PO[0] * mp.normal[0] + PO[1] * mp.normal[1]) + PO[2] * mp.normal[2];
+        if (dotn < 0.5 * dist) continue;
+        const int nPredictedLevel = predict_scale(mp.max_dist, dist, cam->log_scale_factor, KF->nlevels);
+        const float radius = th * KF->scale_factors[nPredictedLevel];
+        const std::vector<size_t> vIndices = grid.area(u, v, radius, -1, -1);
+        if (vIndices.empty()) continue;
+        int bestDist = 256, bestIdx = -1;
+        for (size_t idx : vIndices) {
+            if (matched[idx] >= 0) continue;
+            const int kpLevel = KF->keys[idx].octave;
+            if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+            const int d = oracle::hamming(mp.desc, KF->desc + idx * 32);
+            if (d < bestDist) { bestDist = d; bestIdx = (int)idx; }
+        }
+        if (bestDist <= TH_LOW * ratioHamming) {
+            matched[bestIdx] = mp.id;
+            if (point_kfs && matched_kf) matched_kf[bestIdx] = point_kfs[iMP];
+            nmatches++;
+        }
+    }
+    return nmatches;
+}
+
+// One direction of SearchBySim3: points of A transformed by TAw then SBA, searched in B.
+static void sim3_side(const orbfe_frame* B, const Grid& gridB, const orbfe_map_point_3d* ptsA, int nA,
+                      const std::vector<char>& already, const orbfe_pose& TAw, const orbfe_pose& SBA,
+                      const orbfe_kf_camera* cam1, float logsfB, float th, std::vector<int>& vnMatch) {
+    vnMatch.assign(nA, -1);
+    for (int i = 0; i < nA; i++) {
+        const orbfe_map_point_3d& mp = ptsA[i];
+        if (mp.id < 0 || already[i]) continue;
+        if (mp.flags & ORBFE_MP_BAD) continue;
+        float pA[3], pB[3];
+        pose_apply(TAw, mp.pos, pA);
+        pose_apply(SBA, pA, pB);
+        if (pB[2] < 0.0) continue;
+        const float invz = (float)(1.0 / (double)pB[2]);
+        const float x = pB[0] * invz, y = pB[1] * invz;
+        const float u = cam1->fx * x + cam1->cx, v = cam1->fy * y + cam1->cy;
+        if (!kf_in_image(B, u, v)) continue;
+        const float maxDistance = 1.2f * mp.max_dist, minDistance = 0.8f * mp.min_dist;
+        const float dist3D = std::sqrt((pB[0] * pB[0] + pB[1] * pB[1]) + pB[2] * pB[2]);
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const int nPredictedLevel = predict_scale(mp.max_dist, dist3D, logsfB, B->nlevels);
+        const float radius = th * B->scale_factors[nPredictedLevel];
+        const std::vector<size_t> vIndices = gridB.area(u, v, radius, -1, -1);
+        if (vIndices.empty()) continue;
+        int bestDist = INT_MAX, bestIdx = -1;
+        for (size_t idx : vIndices) {
+            const int oct = B->keys[idx].octave;
+            if (oct < nPredictedLevel - 1 || oct > nPredictedLevel) continue;
+            const int d = oracle::hamming(mp.desc, B->desc + idx * 32);
+            if (d < bestDist) { bestDist = d; bestIdx = (int)idx; }
+        }
+        if (bestDist <= TH_HIGH) vnMatch[i] = bestIdx;
+    }
+}
+
+int oro_search_by_sim3(const orbfe_frame* KF1, const orbfe_frame* KF2, const orbfe_map_point_3d* pts1,
+                       const orbfe_map_point_3d* pts2, const orbfe_kf_camera* cam1, const orbfe_kf_camera* cam2,
+                       const orbfe_pose* S12, const orbfe_pose* S21, float th, int32_t* matches12,
+                       const int32_t* matched_idx2) {
+    const int N1 = KF1->n, N2 = KF2->n;
+    std::vector<char> already1(N1, 0), already2(N2, 0);
+    for (int i = 0; i < N1; i++)
+        if (matches12[i] >= 0) {
+            already1[i] = 1;
+            const int idx2 = matched_idx2 ? matched_idx2[i] : -1;
+            if (idx2 >= 0 && idx2 < N2) already2[idx2] = 1;
+        }
+    const Grid g1(KF1), g2(KF2);
+    std::vector<int> vnMatch1, vnMatch2;
+    sim3_side(KF2, g2, pts1, N1, already1, cam1->Tcw, *S21, cam1, cam2->log_scale_factor, th, vnMatch1);
+    sim3_side(KF1, g1, pts2, N2, already2, cam2->Tcw, *S12, cam1, cam1->log_scale_factor, th, vnMatch2);
+    int nFound = 0;
+    for (int i1 = 0; i1 < N1; i1++) {
+        const int idx2 = vnMatch1[i1];
+        if (idx2 >= 0 && vnMatch2[idx2] == i1) {
+            matches12[i1] = pts2[idx2].id;
+            nFound++;
+        }
+    }
+    return nFound;
 }
 
 // BFMatcher(NORM_HAMMING).knnMatch(k=2): per query the two smallest distances, earlier train index

@@ -59,6 +59,11 @@ _SIGS = {
     "orbfe_search_by_bow_kf": (_c_int, [_vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _c_float,
                                         _c_int]),
     "orbfe_distinctive_descriptors": (_c_int, [_vp, _vp, _c_int, _vp]),
+    "orbfe_search_for_triangulation": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int,
+                                                _vp]),
+    "orbfe_fuse": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _c_float, _c_int, _vp, _vp]),
+    "orbfe_search_by_projection_sim3": (_c_int, [_vp, _vp, _vp, _c_int, _vp, _c_int, _c_float, _vp, _vp]),
+    "orbfe_search_by_sim3": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_float, _vp, _vp]),
     "orbfe_stereo_knn_ratio": (_c_int, [_vp, _c_int, _vp, _c_int, _c_float, _vp, _vp]),
     "orbfe_matcher_set_timing": (_c_int, [_c_int]),
     "orbfe_undistort_points": (_c_int, [_vp, _c_int, _vp, _vp, _c_int, _vp]),

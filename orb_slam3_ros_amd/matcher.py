@@ -74,6 +74,96 @@ class Camera(ctypes.Structure):
         return c
 
 
+SE3, SIM3 = 0, 1
+
+
+def _logf(x: float) -> float:
+    libm = ctypes.CDLL("libm.so.6")
+    libm.logf.restype = ctypes.c_float
+    libm.logf.argtypes = [ctypes.c_float]
+    return float(libm.logf(float(np.float32(x))))
+
+
+def rotation_to_quaternion(R) -> np.ndarray:
+    """Unit quaternion (x, y, z, w) of a rotation matrix (Eigen's Quaternion(Matrix3) branch
+    structure, evaluated in double and rounded to float)."""
+    m = np.asarray(R, np.float64).reshape(3, 3)
+    tr = m[0, 0] + m[1, 1] + m[2, 2]
+    if tr > 0:
+        t = np.sqrt(tr + 1.0)
+        w = 0.5 * t
+        t = 0.5 / t
+        q = [(m[2, 1] - m[1, 2]) * t, (m[0, 2] - m[2, 0]) * t, (m[1, 0] - m[0, 1]) * t, w]
+    else:
+        i = 0
+        if m[1, 1] > m[0, 0]:
+            i = 1
+        if m[2, 2] > m[i, i]:
+            i = 2
+        j, k = (i + 1) % 3, (i + 2) % 3
+        t = np.sqrt(m[i, i] - m[j, j] - m[k, k] + 1.0)
+        q = [0.0, 0.0, 0.0, 0.0]
+        q[i] = 0.5 * t
+        t = 0.5 / t
+        q[3] = (m[k, j] - m[j, k]) * t
+        q[j] = (m[j, i] + m[i, j]) * t
+        q[k] = (m[k, i] + m[i, k]) * t
+    q = np.array(q, np.float64)
+    return (q / np.linalg.norm(q)).astype(np.float32)
+
+
+class Pose(ctypes.Structure):
+    """struct orbfe_pose: a Sophus SE3f (unit quaternion) or Sim3f (RxSO3 quaternion, scale |q|^2)."""
+    _fields_ = [("q", ctypes.c_float * 4), ("t", ctypes.c_float * 3), ("kind", ctypes.c_int32)]
+
+    @staticmethod
+    def se3(R, t):
+        p = Pose()
+        p.q[:] = [float(v) for v in rotation_to_quaternion(R)]
+        p.t[:] = [float(v) for v in np.asarray(t, np.float32).reshape(3)]
+        p.kind = SE3
+        return p
+
+    @staticmethod
+    def sim3(R, t, s):
+        p = Pose()
+        q = rotation_to_quaternion(R).astype(np.float64) * np.sqrt(float(s))
+        p.q[:] = [float(v) for v in q.astype(np.float32)]
+        p.t[:] = [float(v) for v in np.asarray(t, np.float32).reshape(3)]
+        p.kind = SIM3
+        return p
+
+    def rotation(self) -> np.ndarray:
+        x, y, z, w = [float(v) for v in self.q]
+        n = x * x + y * y + z * z + w * w
+        x, y, z, w = (v / np.sqrt(n) for v in (x, y, z, w))
+        return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                         [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                         [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+    def scale(self) -> float:
+        return float(sum(float(v) ** 2 for v in self.q)) if self.kind == SIM3 else 1.0
+
+
+class KFCamera(ctypes.Structure):
+    """struct orbfe_kf_camera: the keyframe pose (Sophus), camera centre, pinhole intrinsics and
+    mfLogScaleFactor read by the back-end projections."""
+    _fields_ = [("Tcw", Pose), ("Ow", ctypes.c_float * 3), ("fx", ctypes.c_float), ("fy", ctypes.c_float),
+                ("cx", ctypes.c_float), ("cy", ctypes.c_float), ("log_scale_factor", ctypes.c_float)]
+
+    @staticmethod
+    def make(Tcw: Pose, fx, fy, cx, cy, scale_factor=1.2, Ow=None):
+        c = KFCamera()
+        c.Tcw = Tcw
+        if Ow is None:
+            R, t = Tcw.rotation(), np.array(Tcw.t[:], np.float64)
+            Ow = -(R.T @ t)
+        c.Ow[:] = [float(v) for v in np.asarray(Ow, np.float32).reshape(3)]
+        c.fx, c.fy, c.cx, c.cy = float(fx), float(fy), float(cx), float(cy)
+        c.log_scale_factor = _logf(scale_factor)
+        return c
+
+
 class MatchFrame:
     """The parts of a Frame the matchers read (Frame.h). keys: KEYPOINT_DTYPE [n] (mvKeysUn),
     desc: uint8 [n, 32], bounds: (mnMinX, mnMaxX, mnMinY, mnMaxY), uright: float32 [n] or None."""
@@ -229,6 +319,77 @@ class ORBmatcher:
             m2.ctypes.data, len(k2), featvec2.ref(), out.ctypes.data, self.mfNNratio,
             int(self.mbCheckOrientation)), "SearchByBoW(KF, KF)")
         return n, out
+
+
+    # SearchForTriangulation(pKF1, pKF2, vMatchedPairs, bOnlyStereo, bCoarse) (:907-1146)
+    def SearchForTriangulation(self, KF1: MatchFrame, mp1, fv1: FeatureVector, KF2: MatchFrame, mp2,
+                               fv2: FeatureVector, F12, ep, level_sigma2_2, bOnlyStereo=False, bCoarse=False):
+        """mp1 / mp2: GetMapPoint presence per keypoint (handle or -1). F12 (3x3) and ep (2,) as the
+        reference computes them. Returns (nmatches, matches12 int32 [KF1.N]: KF2 index or -1);
+        vMatchedPairs = [(i, matches12[i]) for i with matches12[i] >= 0]."""
+        m1 = _i32(np.ascontiguousarray(mp1, np.int32), KF1.N, "mp1")
+        m2 = _i32(np.ascontiguousarray(mp2, np.int32), KF2.N, "mp2")
+        F = np.ascontiguousarray(F12, np.float32).reshape(9)
+        e = np.ascontiguousarray(ep, np.float32).reshape(2)
+        sg = np.ascontiguousarray(level_sigma2_2, np.float32).reshape(-1)
+        if len(sg) < len(KF2.scale_factors):
+            raise ValueError("level_sigma2_2 needs one entry per level")
+        out = np.full(KF1.N, -1, np.int32)
+        n = _lib.check(self._lib.orbfe_search_for_triangulation(
+            KF1.ref(), m1.ctypes.data, fv1.ref(), KF2.ref(), m2.ctypes.data, fv2.ref(), F.ctypes.data, e.ctypes.data,
+            sg.ctypes.data, int(bOnlyStereo), int(bCoarse), int(self.mbCheckOrientation), out.ctypes.data),
+            "SearchForTriangulation")
+        return n, out
+
+    # Fuse(pKF, vpMapPoints, th) (:1148-1337) / Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (:1339-1455)
+    def Fuse(self, KF: MatchFrame, cam: KFCamera, points3d, th=3.0, inv_level_sigma2=None, sim3=False):
+        """The search half of Fuse: (n_candidates, best_idx, best_dist) per point; the map mutation
+        (Replace / AddObservation / vpReplacePoint) is the caller's, in point order."""
+        pts = _records(points3d, MAP_POINT_3D_DTYPE, "points3d")
+        if inv_level_sigma2 is None:
+            sf = KF.scale_factors
+            inv_level_sigma2 = (np.float32(1.0) / (sf * sf)).astype(np.float32)
+        sig = np.ascontiguousarray(inv_level_sigma2, np.float32).reshape(-1)
+        if len(sig) < len(KF.scale_factors):
+            raise ValueError("inv_level_sigma2 needs one entry per level")
+        bi = np.full(len(pts), -1, np.int32)
+        bd = np.full(len(pts), -1, np.int32)
+        n = _lib.check(self._lib.orbfe_fuse(KF.ref(), ctypes.byref(cam), sig.ctypes.data, pts.ctypes.data, len(pts),
+                                            float(th), int(bool(sim3)), bi.ctypes.data, bd.ctypes.data), "Fuse")
+        return n, bi, bd
+
+    # SearchByProjection(pKF, Scw, vpPoints, vpMatched, th, ratioHamming) (:427-523) and the
+    # vpPointsKFs / vpMatchedKF overload (:525-646)
+    def SearchByProjectionSim3(self, KF: MatchFrame, cam: KFCamera, points3d, vpMatched, th=10, ratioHamming=1.0,
+                               point_kfs=None, vpMatchedKF=None):
+        """vpMatched (and vpMatchedKF with point_kfs) int32 [KF.N] updated in place. Returns nmatches."""
+        pts = _records(points3d, MAP_POINT_3D_DTYPE, "points3d")
+        m = _i32(vpMatched, KF.N, "vpMatched")
+        pk = mk = None
+        if point_kfs is not None:
+            pk = _i32(np.ascontiguousarray(point_kfs, np.int32), len(pts), "point_kfs")
+            mk = _i32(vpMatchedKF, KF.N, "vpMatchedKF")
+        return _lib.check(self._lib.orbfe_search_by_projection_sim3(
+            KF.ref(), ctypes.byref(cam), pts.ctypes.data, len(pts), None if pk is None else pk.ctypes.data, int(th),
+            float(ratioHamming), m.ctypes.data, None if mk is None else mk.ctypes.data), "SearchByProjection(Sim3)")
+
+    # SearchBySim3(pKF1, pKF2, vpMatches12, S12, th) (:1457-1674)
+    def SearchBySim3(self, KF1: MatchFrame, KF2: MatchFrame, points1, points2, cam1: KFCamera, cam2: KFCamera,
+                     S12: Pose, S21: Pose, th, vpMatches12, matched_idx2=None):
+        """points1 / points2: GetMapPointMatches() of each keyframe as MAP_POINT_3D_DTYPE (id -1 = NULL).
+        vpMatches12 int32 [KF1.N] updated in place; matched_idx2[i] = KF2 index of the initial match i.
+        Returns nFound."""
+        p1 = _records(points1, MAP_POINT_3D_DTYPE, "points1")
+        p2 = _records(points2, MAP_POINT_3D_DTYPE, "points2")
+        if len(p1) != KF1.N or len(p2) != KF2.N:
+            raise ValueError("one map-point record per keyframe keypoint")
+        m = _i32(vpMatches12, KF1.N, "vpMatches12")
+        mi = None if matched_idx2 is None else _i32(np.ascontiguousarray(matched_idx2, np.int32), KF1.N,
+                                                    "matched_idx2")
+        return _lib.check(self._lib.orbfe_search_by_sim3(
+            KF1.ref(), KF2.ref(), p1.ctypes.data, p2.ctypes.data, ctypes.byref(cam1), ctypes.byref(cam2),
+            ctypes.byref(S12), ctypes.byref(S21), float(th), m.ctypes.data, None if mi is None else mi.ctypes.data),
+            "SearchBySim3")
 
 
 def compute_distinctive_descriptors(descriptor_sets):

@@ -12,7 +12,7 @@ import numpy as np
 
 from .extractor import KEYPOINT_DTYPE
 from .matcher import (MAP_POINT_3D_DTYPE, MAP_POINT_DTYPE, MP_BAD, MP_IN_VIEW, MP_SKIP, PROJ_POINT_DTYPE, Camera,
-                      FeatureVector, MatchFrame)
+                      FeatureVector, KFCamera, MatchFrame, Pose)
 
 
 def scale_factors(nlevels: int = 8, scale_factor: float = 1.2) -> np.ndarray:
@@ -253,3 +253,135 @@ def synth_local_map_3d(rng, F: MatchFrame, cam: Camera, n: int, copy_frac: float
     m["id"] = np.arange(n) + 20000
     m["desc"] = desc
     return m
+
+
+# ---- back-end scenes ----
+def _rand_rotation(rng, rot_deg):
+    axis = rng.normal(size=3)
+    axis /= np.linalg.norm(axis)
+    ang = np.deg2rad(rng.uniform(-rot_deg, rot_deg))
+    K = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    return np.eye(3) + np.sin(ang) * K + (1 - np.cos(ang)) * K @ K
+
+
+def synth_kf_camera(rng, fx=458.654, fy=457.296, cx=367.215, cy=248.375, rot_deg=10.0) -> KFCamera:
+    R = _rand_rotation(rng, rot_deg)
+    t = rng.normal(scale=1.0, size=3)
+    return KFCamera.make(Pose.se3(R, t), fx, fy, cx, cy)
+
+
+def synth_fuse_scene(rng, n_kp: int, n_pts: int, dup: int = 1, copy_frac: float = 0.6):
+    """A keyframe, its camera and map points that project near its keypoints (for Fuse and
+    SearchByProjection(Sim3)). dup > 1 makes several points compete for the same keypoints.
+    The stereo keypoints that points were copied from get a consistent mvuRight."""
+    KF = synth_frame(rng, n_kp, stereo=True)
+    cam = synth_kf_camera(rng)
+    R = cam.Tcw.rotation()
+    c = Camera.make(R, np.array(cam.Tcw.t[:], np.float64), cam.fx, cam.fy, cam.cx, cam.cy)
+    base = synth_local_map_3d(rng, KF, c, max(n_pts // dup, 1), copy_frac=copy_frac)
+    pts = np.concatenate([base] * dup)[:n_pts].copy()
+    if dup > 1:   # jitter the duplicates so they are distinct points with the same neighbourhood
+        pts["pos"] += rng.normal(0, 1e-3, pts["pos"].shape).astype(np.float32)
+        pts["desc"] = flip_bits(rng, pts["desc"], 0.03)
+    pts["id"] = np.arange(len(pts)) + 20000
+    # consistent right coordinates for the keypoints nearest to a projected point
+    P = pts["pos"].astype(np.float64)
+    t = np.array(cam.Tcw.t[:], np.float64)
+    Pc = P @ R.T + t
+    ok = Pc[:, 2] > 0.1
+    u = cam.fx * Pc[ok, 0] / Pc[ok, 2] + cam.cx
+    v = cam.fy * Pc[ok, 1] / Pc[ok, 2] + cam.cy
+    ur_pt = u - KF.mbf / Pc[ok, 2]
+    if KF.uright is not None and ok.any():
+        d2 = (KF.keys["x"][:, None] - u[None, :]) ** 2 + (KF.keys["y"][:, None] - v[None, :]) ** 2
+        j = d2.argmin(1)
+        near = (d2[np.arange(KF.N), j] < 4.0) & (KF.uright >= 0)
+        KF.uright[near] = (ur_pt[j[near]] + rng.normal(0, 0.5, int(near.sum()))).astype(np.float32)
+    return KF, cam, pts
+
+
+def synth_sim3_pair(rng, n1: int, extra2: float = 0.2, scale: float = 1.0, nlevels: int = 8, sf: float = 1.2):
+    """Two keyframes looking at the same points (SearchBySim3 / SearchForTriangulation). Returns
+    (KF1, KF2, pts1, pts2, cam1, cam2, S12, S21, src) with src[j] = the KF1 keypoint KF2 keypoint j
+    observes (-1 if new). S12 maps camera-2 coordinates to camera 1 (scaled by `scale`)."""
+    fx, fy, cx, cy, w, h = 458.654, 457.296, 367.215, 248.375, 752, 480
+    R1 = _rand_rotation(rng, 5.0)
+    t1 = rng.normal(scale=0.5, size=3)
+    dR = _rand_rotation(rng, 8.0)
+    R2 = dR @ R1
+    t2 = t1 + rng.normal(scale=0.3, size=3)
+    cam1 = KFCamera.make(Pose.se3(R1, t1), fx, fy, cx, cy)
+    cam2 = KFCamera.make(Pose.se3(R2, t2), fx, fy, cx, cy)
+    KF1 = synth_frame(rng, n1, stereo=False)
+    u1, v1 = KF1.keys["x"].astype(np.float64), KF1.keys["y"].astype(np.float64)
+    z1 = rng.uniform(1.0, 12.0, n1)
+    Pc1 = np.stack([(u1 - cx) * z1 / fx, (v1 - cy) * z1 / fy, z1], 1)
+    Pw = (Pc1 - t1) @ R1
+    Pc2 = Pw @ R2.T + t2
+    o1 = KF1.keys["octave"].astype(np.float64)
+    max_d = z1 * np.sqrt(1 + ((u1 - cx) / fx) ** 2 + ((v1 - cy) / fy) ** 2) * sf ** (o1 - 0.5)
+    d2 = np.linalg.norm(Pc2, axis=1)
+    pred2 = np.clip(np.ceil(np.log(max_d / d2) / np.log(sf)), 0, nlevels - 1).astype(np.int32)
+    u2 = fx * Pc2[:, 0] / Pc2[:, 2] + cx + rng.normal(0, 0.7, n1)
+    v2 = fy * Pc2[:, 1] / Pc2[:, 2] + cy + rng.normal(0, 0.7, n1)
+    vis = (Pc2[:, 2] > 0) & (u2 >= 0) & (u2 < w) & (v2 >= 0) & (v2 < h) & (rng.random(n1) < 0.85)
+    idx = np.nonzero(vis)[0]
+    n_new = int(len(idx) * extra2)
+    n2 = len(idx) + n_new
+    k2 = np.zeros(n2, KEYPOINT_DTYPE)
+    k2["x"][:len(idx)] = u2[idx]
+    k2["y"][:len(idx)] = v2[idx]
+    k2["octave"][:len(idx)] = np.maximum(pred2[idx] - (rng.random(len(idx)) < 0.3), 0)
+    k2["x"][len(idx):] = rng.uniform(0, w - 1, n_new)
+    k2["y"][len(idx):] = rng.uniform(0, h - 1, n_new)
+    k2["octave"][len(idx):] = rng.choice(nlevels, n_new, p=level_weights(nlevels))
+    sfs = scale_factors(nlevels)
+    k2["size"] = (31.0 * sfs[k2["octave"]]).astype(np.float32)
+    k2["angle"] = np.mod(np.concatenate([KF1.keys["angle"][idx], rng.uniform(0, 360, n_new)]) + 15.0, 360.0)
+    k2["response"] = 20.0
+    k2["class_id"] = -1
+    d2desc = np.concatenate([flip_bits(rng, KF1.desc[idx], 0.06),
+                             rng.integers(0, 256, (n_new, 32), dtype=np.uint8)])
+    perm = rng.permutation(n2)
+    src = np.concatenate([idx, np.full(n_new, -1)])[perm]
+    KF2 = MatchFrame(k2[perm], d2desc[perm], (0.0, float(w), 0.0, float(h)), sfs, None, KF1.mbf)
+    # map points: KF1's (some NULL / bad) and KF2's (the same point for observed ones)
+    normal = Pw - np.array(cam1.Ow[:], np.float64)
+    normal /= np.linalg.norm(normal, axis=1, keepdims=True)
+    pts1 = np.zeros(n1, MAP_POINT_3D_DTYPE)
+    pts1["pos"] = Pw.astype(np.float32)
+    pts1["normal"] = normal.astype(np.float32)
+    pts1["max_dist"] = max_d.astype(np.float32)
+    pts1["min_dist"] = (max_d / sf ** (nlevels - 1)).astype(np.float32)
+    pts1["desc"] = KF1.desc
+    pts1["observations"] = 2
+    pts1["id"] = np.where(rng.random(n1) < 0.15, -1, np.arange(n1) + 1000)
+    pts1["flags"] = np.where(rng.random(n1) < 0.03, MP_BAD, 0)
+    pts2 = np.zeros(n2, MAP_POINT_3D_DTYPE)
+    has = src >= 0
+    pts2[has] = pts1[src[has]]
+    pts2["id"][has] = np.where(rng.random(int(has.sum())) < 0.1, -1, pts1["id"][src[has]] + 500000)
+    pts2["id"][~has] = -1
+    pts2["desc"] = KF2.desc
+    R12 = R1 @ R2.T
+    t12 = t1 - R12 @ t2
+    S12 = Pose.sim3(R12, t12 * scale, scale)
+    S21 = Pose.sim3(R12.T, -(R12.T @ (t12 * scale)) / scale, 1.0 / scale)
+    return KF1, KF2, pts1, pts2, cam1, cam2, S12, S21, src
+
+
+def fundamental_12(cam1: KFCamera, cam2: KFCamera):
+    """F12 = K1^-T [t12]x R12 K2^-1 and the epipole ep = project2(T2w * Cw1) (ORBmatcher.cc:914-920,
+    Pinhole.cpp:107-112), computed in float64 and rounded to float."""
+    R1, R2 = cam1.Tcw.rotation(), cam2.Tcw.rotation()
+    t1, t2 = np.array(cam1.Tcw.t[:], np.float64), np.array(cam2.Tcw.t[:], np.float64)
+    R12 = R1 @ R2.T
+    t12 = t1 - R12 @ t2
+    tx = np.array([[0, -t12[2], t12[1]], [t12[2], 0, -t12[0]], [-t12[1], t12[0], 0]])
+    K1 = np.array([[cam1.fx, 0, cam1.cx], [0, cam1.fy, cam1.cy], [0, 0, 1]])
+    K2 = np.array([[cam2.fx, 0, cam2.cx], [0, cam2.fy, cam2.cy], [0, 0, 1]])
+    F12 = np.linalg.inv(K1.T) @ tx @ R12 @ np.linalg.inv(K2)
+    Cw = -(R1.T @ t1)
+    C2 = R2 @ Cw + t2
+    ep = np.array([cam2.fx * C2[0] / C2[2] + cam2.cx, cam2.fy * C2[1] / C2[2] + cam2.cy])
+    return F12.astype(np.float32), ep.astype(np.float32)

@@ -11,7 +11,7 @@ import pytest
 
 from orb_slam3_ros_amd import synth_match as sm
 from orb_slam3_ros_amd._lib import OrbfeError
-from orb_slam3_ros_amd.matcher import FeatureVector, ORBmatcher, compute_distinctive_descriptors
+from orb_slam3_ros_amd.matcher import FeatureVector, MatchFrame, ORBmatcher, compute_distinctive_descriptors
 
 pytestmark = pytest.mark.gpu
 
@@ -68,3 +68,98 @@ def test_distinctive_descriptors_limits(gpu):
         compute_distinctive_descriptors([big])
     # all-identical rows: every median is 0, the first row wins
     np.testing.assert_array_equal(compute_distinctive_descriptors([np.ones((9, 32), np.uint8)]), [0])
+
+
+# ---- SearchForTriangulation / Fuse / SearchByProjection(Sim3) / SearchBySim3 ----
+@pytest.mark.parametrize("seed,coarse,only_stereo,check_ori", [(0, False, False, True), (1, True, False, True),
+                                                                (2, False, False, False), (3, False, True, True)])
+def test_search_for_triangulation(gpu, oracle_lib, seed, coarse, only_stereo, check_ori):
+    rng = np.random.default_rng(seed)
+    K1, K2, *_, c1, c2, S12, S21, src = sm.synth_sim3_pair(rng, 1500)
+    if only_stereo:   # stereo keypoints on both sides (mvuRight >= 0)
+        def stereo(K):
+            ur = np.where(rng.random(K.N) < 0.6, K.keys["x"] - 10, -1).astype(np.float32)
+            return MatchFrame(K.keys, K.desc, K.bounds, K.scale_factors, ur, K.mbf)
+        K1, K2 = stereo(K1), stereo(K2)
+    for words in (300, 20):
+        fv1, fv2 = sm.synth_bow(rng, words, K1, K2, src)
+        F12, ep = sm.fundamental_12(c1, c2)
+        sg = (K2.scale_factors * K2.scale_factors).astype(np.float32)
+        mp1 = np.where(rng.random(K1.N) < 0.4, 5, -1).astype(np.int32)
+        mp2 = np.where(rng.random(K2.N) < 0.4, 5, -1).astype(np.int32)
+        m = ORBmatcher(0.6, check_ori)
+        ng, og = m.SearchForTriangulation(K1, mp1, fv1, K2, mp2, fv2, F12, ep, sg, only_stereo, coarse)
+        no, oo = oracle_lib.OracleMatcher(0.6, check_ori).search_for_triangulation(K1, mp1, fv1, K2, mp2, fv2, F12,
+                                                                                    ep, sg, only_stereo, coarse)
+        assert ng == no
+        np.testing.assert_array_equal(og, oo)
+        assert no > 20
+
+
+@pytest.mark.parametrize("sim3", [0, 1])
+@pytest.mark.parametrize("seed,n_kp,n_pts,dup,th", [(0, 1000, 4000, 2, 3.0), (1, 2000, 20000, 3, 5.0),
+                                                    (2, 500, 800, 1, 1.0)])
+def test_fuse(gpu, oracle_lib, sim3, seed, n_kp, n_pts, dup, th):
+    rng = np.random.default_rng(seed)
+    KF, cam, pts = sm.synth_fuse_scene(rng, n_kp, n_pts, dup=dup)
+    ng, big, bdg = ORBmatcher().Fuse(KF, cam, pts, th, sim3=bool(sim3))
+    no, bio, bdo = oracle_lib.OracleMatcher().fuse(KF, cam, pts, th, sim3=sim3)
+    assert ng == no and no > 0
+    np.testing.assert_array_equal(big, bio)
+    np.testing.assert_array_equal(bdg, bdo)
+
+
+@pytest.mark.parametrize("with_kfs", [False, True])
+@pytest.mark.parametrize("seed,dup,ratio,th", [(0, 3, 1.0, 10), (1, 2, 0.5, 10), (2, 4, 1.0, 20)])
+def test_search_by_projection_sim3(gpu, oracle_lib, with_kfs, seed, dup, ratio, th):
+    rng = np.random.default_rng(seed)
+    KF, cam, pts = sm.synth_fuse_scene(rng, 1000, 3000, dup=dup)
+    matched0 = np.full(KF.N, -1, np.int32)
+    pre = rng.random(KF.N) < 0.1
+    matched0[pre] = rng.choice(pts["id"], int(pre.sum()))   # spAlreadyFound: those points are skipped
+    kfs = rng.integers(0, 50, len(pts)).astype(np.int32) if with_kfs else None
+    mk0 = np.where(pre, 99, -1).astype(np.int32)
+    mg, mkg = matched0.copy(), mk0.copy()
+    ng = ORBmatcher().SearchByProjectionSim3(KF, cam, pts, mg, th, ratio, kfs, mkg if with_kfs else None)
+    mo, mko = matched0.copy(), mk0.copy()
+    no = oracle_lib.OracleMatcher().sbp_sim3(KF, cam, pts, mo, th, ratio, kfs, mko if with_kfs else None)
+    assert ng == no and no > 0
+    np.testing.assert_array_equal(mg, mo)
+    if with_kfs:
+        np.testing.assert_array_equal(mkg, mko)
+
+
+@pytest.mark.parametrize("seed,scale,th", [(0, 1.0, 7.5), (1, 1.0, 15.0), (2, 1.3, 7.5), (3, 0.8, 10.0)])
+def test_search_by_sim3(gpu, oracle_lib, seed, scale, th):
+    rng = np.random.default_rng(seed)
+    K1, K2, p1, p2, c1, c2, S12, S21, src = sm.synth_sim3_pair(rng, 2000, scale=scale)
+    m0 = np.full(K1.N, -1, np.int32)
+    pre = np.nonzero(rng.random(K1.N) < 0.05)[0]
+    m0[pre] = 123
+    inv = np.full(K1.N, -1, np.int64)   # KF1 index -> the KF2 keypoint observing the same point
+    inv[src[src >= 0]] = np.nonzero(src >= 0)[0]
+    idx2 = np.full(K1.N, -1, np.int32)
+    idx2[pre] = inv[pre]
+    mg, mo = m0.copy(), m0.copy()
+    ng = ORBmatcher().SearchBySim3(K1, K2, p1, p2, c1, c2, S12, S21, th, mg, idx2)
+    no = oracle_lib.OracleMatcher().search_by_sim3(K1, K2, p1, p2, c1, c2, S12, S21, th, mo, idx2)
+    assert ng == no
+    np.testing.assert_array_equal(mg, mo)
+    if scale == 1.0:
+        assert no > 100
+
+
+def test_backend_edges(gpu):
+    rng = np.random.default_rng(9)
+    KF, cam, pts = sm.synth_fuse_scene(rng, 200, 300)
+    m = ORBmatcher()
+    n, bi, bd = m.Fuse(KF, cam, pts[:0], 3.0)
+    assert n == 0 and len(bi) == 0
+    bad = pts.copy()
+    bad["flags"] |= 2
+    n, bi, bd = m.Fuse(KF, cam, bad, 3.0)
+    assert n == 0 and (bi == -1).all() and (bd == -1).all()
+    cam2 = sm.synth_kf_camera(rng)
+    cam2.Tcw.kind = 7
+    with pytest.raises(OrbfeError):
+        m.Fuse(KF, cam2, pts, 3.0)

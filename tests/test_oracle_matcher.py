@@ -400,3 +400,149 @@ def test_oracle_distinctive_vs_python(oracle_lib):
     got = oracle_lib.distinctive_descriptors(np.concatenate(sets), offs)
     np.testing.assert_array_equal(got, py_distinctive(sets))
     assert got[0] == -1 and got[1] == 0
+
+
+# ---- back-end projections: literal float32 restatements ----
+def _py_pose_apply(P, p):
+    vx, vy, vz, w = (f32(v) for v in P.q)
+    t = [f32(v) for v in P.t]
+    p = [f32(v) for v in p]
+    uv = [f32(vy * p[2] - vz * p[1]), f32(vz * p[0] - vx * p[2]), f32(vx * p[1] - vy * p[0])]
+    uv = [f32(u + u) for u in uv]
+    c = [f32(vy * uv[2] - vz * uv[1]), f32(vz * uv[0] - vx * uv[2]), f32(vx * uv[1] - vy * uv[0])]
+    if P.kind == 1:
+        sc = f32(f32(vx * vx + vz * vz) + f32(vy * vy + w * w))
+        return [f32(f32(sc * p[k] + f32(w * uv[k] + c[k])) + t[k]) for k in range(3)]
+    return [f32(f32(f32(p[k] + w * uv[k]) + c[k]) + t[k]) for k in range(3)]
+
+
+def _py_predict(max_dist, dist, logsf, nlevels):
+    ratio = f32(f32(max_dist) / f32(dist))
+    n = int(math.ceil(f32(f32(np.log(ratio)) / f32(logsf))))   # numpy float32 log (parity of logf is tested natively)
+    return min(max(n, 0), nlevels - 1)
+
+
+def _py_in_image(F, x, y):
+    return F.bounds[0] <= x < F.bounds[1] and F.bounds[2] <= y < F.bounds[3]
+
+
+def py_fuse(KF, cam, pts, th, sim3):
+    g = PyGrid(KF)
+    inv = (f32(1.0) / (KF.scale_factors * KF.scale_factors)).astype(np.float32)
+    bi = np.full(len(pts), -1, np.int32)
+    bd = np.full(len(pts), -1, np.int32)
+    for i, mp in enumerate(pts):
+        if mp["flags"] & 6 or mp["id"] < 0:
+            continue
+        pc = _py_pose_apply(cam.Tcw, mp["pos"])
+        if pc[2] < 0:
+            continue
+        invz = f32(f32(1) / pc[2])
+        u = f32(f32(f32(cam.fx) * pc[0]) / pc[2] + f32(cam.cx))
+        v = f32(f32(f32(cam.fy) * pc[1]) / pc[2] + f32(cam.cy))
+        if not _py_in_image(KF, u, v):
+            continue
+        ur = f32(u - f32(KF.mbf) * invz)
+        PO = [f32(mp["pos"][k] - f32(cam.Ow[k])) for k in range(3)]
+        d = f32(np.sqrt(f32(f32(PO[0] * PO[0] + PO[1] * PO[1]) + PO[2] * PO[2])))
+        if d < f32(f32(0.8) * mp["min_dist"]) or d > f32(f32(1.2) * mp["max_dist"]):
+            continue
+        dot = f32(f32(PO[0] * mp["normal"][0] + PO[1] * mp["normal"][1]) + PO[2] * mp["normal"][2])
+        if float(dot) < 0.5 * float(d):
+            continue
+        lvl = _py_predict(mp["max_dist"], d, cam.log_scale_factor, len(KF.scale_factors))
+        r = f32(f32(th) * KF.scale_factors[lvl])
+        best, bidx = (2 ** 31 - 1 if sim3 else 256), -1
+        for idx in g.area(u, v, r, -1, -1):
+            kp = KF.keys[idx]
+            if kp["octave"] < lvl - 1 or kp["octave"] > lvl:
+                continue
+            if not sim3:
+                ex, ey = f32(u - kp["x"]), f32(v - kp["y"])
+                if KF.uright is not None and KF.uright[idx] >= 0:
+                    er = f32(ur - KF.uright[idx])
+                    e2 = f32(f32(ex * ex + ey * ey) + er * er)
+                    if float(f32(e2 * inv[kp["octave"]])) > 7.8:
+                        continue
+                else:
+                    e2 = f32(ex * ex + ey * ey)
+                    if float(f32(e2 * inv[kp["octave"]])) > 5.99:
+                        continue
+            dd = _ham(mp["desc"], KF.desc[idx])
+            if dd < best:
+                best, bidx = dd, idx
+        if bidx >= 0:
+            bd[i] = best
+        if best <= 50:
+            bi[i] = bidx
+    return int((bi >= 0).sum()), bi, bd
+
+
+@pytest.mark.parametrize("sim3", [0, 1])
+def test_oracle_fuse_vs_python(oracle_lib, sim3):
+    rng = np.random.default_rng(31 + sim3)
+    KF, cam, pts = sm.synth_fuse_scene(rng, 300, 500, dup=2)
+    n, bi, bd = oracle_lib.OracleMatcher().fuse(KF, cam, pts, 3.0, sim3=sim3)
+    n2, bi2, bd2 = py_fuse(KF, cam, pts, 3.0, sim3)
+    assert n == n2 and n > 20
+    np.testing.assert_array_equal(bi, bi2)
+    np.testing.assert_array_equal(bd, bd2)
+
+
+def py_search_by_sim3(K1, K2, p1, p2, c1, c2, S12, S21, th, m12):
+    def side(B, ptsA, already, TAw, SBA, logsfB):
+        g = PyGrid(B)
+        vn = np.full(len(ptsA), -1, np.int64)
+        for i, mp in enumerate(ptsA):
+            if mp["id"] < 0 or already[i] or mp["flags"] & 2:
+                continue
+            pB = _py_pose_apply(SBA, _py_pose_apply(TAw, mp["pos"]))
+            if pB[2] < 0:
+                continue
+            invz = f32(1.0 / float(pB[2]))
+            u = f32(f32(c1.fx) * f32(pB[0] * invz) + f32(c1.cx))
+            v = f32(f32(c1.fy) * f32(pB[1] * invz) + f32(c1.cy))
+            if not _py_in_image(B, u, v):
+                continue
+            d = f32(np.sqrt(f32(f32(pB[0] * pB[0] + pB[1] * pB[1]) + pB[2] * pB[2])))
+            if d < f32(f32(0.8) * mp["min_dist"]) or d > f32(f32(1.2) * mp["max_dist"]):
+                continue
+            lvl = _py_predict(mp["max_dist"], d, logsfB, len(B.scale_factors))
+            r = f32(f32(th) * B.scale_factors[lvl])
+            best, bidx = 2 ** 31 - 1, -1
+            for idx in g.area(u, v, r, -1, -1):
+                o = B.keys[idx]["octave"]
+                if o < lvl - 1 or o > lvl:
+                    continue
+                dd = _ham(mp["desc"], B.desc[idx])
+                if dd < best:
+                    best, bidx = dd, idx
+            if best <= 100:
+                vn[i] = bidx
+        return vn
+    a1 = m12 >= 0
+    vn1 = side(K2, p1, a1, c1.Tcw, S21, c2.log_scale_factor)
+    vn2 = side(K1, p2, np.zeros(K2.N, bool), c2.Tcw, S12, c1.log_scale_factor)
+    out = m12.copy()
+    n = 0
+    for i1 in range(K1.N):
+        j = vn1[i1]
+        if j >= 0 and vn2[j] == i1:
+            out[i1] = p2[j]["id"]
+            n += 1
+    return n, out
+
+
+@pytest.mark.parametrize("scale", [1.0, 1.3])
+def test_oracle_search_by_sim3_vs_python(oracle_lib, scale):
+    rng = np.random.default_rng(40)
+    K1, K2, p1, p2, c1, c2, S12, S21, _ = sm.synth_sim3_pair(rng, 250, scale=scale)
+    m = np.full(K1.N, -1, np.int32)
+    m[:10] = 7   # initial matches (no KF2 index given)
+    mo = m.copy()
+    n = oracle_lib.OracleMatcher().search_by_sim3(K1, K2, p1, p2, c1, c2, S12, S21, 7.5, mo)
+    n2, mp = py_search_by_sim3(K1, K2, p1, p2, c1, c2, S12, S21, 7.5, m)
+    assert n == n2
+    np.testing.assert_array_equal(mo, mp)
+    if scale == 1.0:
+        assert n > 50
