@@ -1,0 +1,295 @@
+// Replacement bodies for the LocalMapping / LoopClosing ORBmatcher methods
+// (orb_slam3/src/ORBmatcher.cc:427-646, 765-1674) and MapPoint::ComputeDistinctiveDescriptors
+// (MapPoint.cc:329-403) on top of liborbfe.so. Pinhole keyframes only: a keyframe
+// with a second camera (mpCamera2) keeps the original body, renamed *_cpu.
+// Built inside the ORB-SLAM3 tree; NOT compiled in this repository's container (no OpenCV /
+// Eigen / Sophus here). See INTEGRATION.md §4.
+#include "ORBmatcher.h"
+
+#include <cstring>
+#include <unordered_map>
+
+#include <orbfe.h>
+
+#include "KeyFrame.h"
+#include "MapPoint.h"
+
+using namespace std;
+
+namespace ORB_SLAM3 {
+
+namespace {
+
+struct Handles {   // MapPoint* <-> int32 (see ORBmatcher_orbfe.cc)
+    vector<MapPoint*> table;
+    unordered_map<MapPoint*, int32_t> id;
+    int32_t of(MapPoint* p) {
+        if (!p) return -1;
+        auto it = id.find(p);
+        if (it != id.end()) return it->second;
+        const int32_t h = (int32_t)table.size();
+        table.push_back(p);
+        id.emplace(p, h);
+        return h;
+    }
+    MapPoint* at(int32_t h) const { return h < 0 ? nullptr : table[h]; }
+};
+
+orbfe_frame kf_view(KeyFrame* K) {
+    orbfe_frame f;
+    f.n = K->N;
+    f.keys = reinterpret_cast<const orbfe_keypoint*>(K->mvKeysUn.data());
+    f.desc = K->mDescriptors.data;
+    f.uright = K->mvuRight.empty() ? nullptr : K->mvuRight.data();
+    f.min_x = K->mnMinX; f.max_x = K->mnMaxX; f.min_y = K->mnMinY; f.max_y = K->mnMaxY;
+    f.nlevels = K->mnScaleLevels;
+    f.scale_factors = K->mvScaleFactors.data();
+    f.mbf = K->mbf;
+    return f;
+}
+
+orbfe_pose pose_of(const Sophus::SE3f& T) {
+    orbfe_pose p;
+    const Eigen::Quaternionf& q = T.unit_quaternion();
+    p.q[0] = q.x(); p.q[1] = q.y(); p.q[2] = q.z(); p.q[3] = q.w();
+    const Eigen::Vector3f t = T.translation();
+    p.t[0] = t(0); p.t[1] = t(1); p.t[2] = t(2);
+    p.kind = ORBFE_SE3;
+    return p;
+}
+
+orbfe_pose pose_of(const Sophus::Sim3f& S) {
+    orbfe_pose p;
+    const Eigen::Quaternionf& q = S.quaternion();   // RxSO3: non-unit, |q|^2 = scale
+    p.q[0] = q.x(); p.q[1] = q.y(); p.q[2] = q.z(); p.q[3] = q.w();
+    const Eigen::Vector3f t = S.translation();
+    p.t[0] = t(0); p.t[1] = t(1); p.t[2] = t(2);
+    p.kind = ORBFE_SIM3;
+    return p;
+}
+
+orbfe_kf_camera kf_camera(KeyFrame* K, const Sophus::SE3f& Tcw, const Eigen::Vector3f& Ow) {
+    orbfe_kf_camera c;
+    c.Tcw = pose_of(Tcw);
+    c.Ow[0] = Ow(0); c.Ow[1] = Ow(1); c.Ow[2] = Ow(2);
+    c.fx = K->fx; c.fy = K->fy; c.cx = K->cx; c.cy = K->cy;
+    c.log_scale_factor = K->mfLogScaleFactor;
+    return c;
+}
+
+// GetMinDistance / GetMaxDistance: two accessors added to MapPoint.h.
+orbfe_map_point_3d point_3d(MapPoint* p, int32_t id, int32_t flags) {
+    orbfe_map_point_3d m;
+    memset(&m, 0, sizeof(m));
+    m.id = id;
+    if (!p) return m;
+    const Eigen::Vector3f X = p->GetWorldPos(), n = p->GetNormal();
+    for (int k = 0; k < 3; k++) { m.pos[k] = X(k); m.normal[k] = n(k); }
+    m.min_dist = p->GetMinDistance();
+    m.max_dist = p->GetMaxDistance();
+    m.flags = flags | (p->isBad() ? ORBFE_MP_BAD : 0);
+    m.observations = p->Observations();
+    memcpy(m.desc, p->GetDescriptor().data, 32);
+    return m;
+}
+
+struct FlatFV {   // DBoW2::FeatureVector flattened (ORBmatcher_orbfe.cc has the same helper)
+    vector<uint32_t> ids, idx;
+    vector<int32_t> off;
+    orbfe_feature_vector v;
+    explicit FlatFV(const DBoW2::FeatureVector& fv) {
+        off.push_back(0);
+        for (const auto& kv : fv) {
+            ids.push_back(kv.first);
+            idx.insert(idx.end(), kv.second.begin(), kv.second.end());
+            off.push_back((int32_t)idx.size());
+        }
+        v.n_nodes = (int32_t)ids.size();
+        v.node_ids = ids.data();
+        v.offsets = off.data();
+        v.indices = idx.data();
+    }
+};
+
+}  // namespace
+
+int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12) {
+    if (pKF1->mpCamera2 || pKF2->mpCamera2) return SearchByBoW_cpu(pKF1, pKF2, vpMatches12);
+    Handles H;
+    const vector<MapPoint*> v1 = pKF1->GetMapPointMatches(), v2 = pKF2->GetMapPointMatches();
+    vector<int32_t> m1(v1.size()), m2(v2.size()), out(v1.size());
+    for (size_t i = 0; i < v1.size(); i++) m1[i] = (v1[i] && !v1[i]->isBad()) ? H.of(v1[i]) : -1;
+    for (size_t i = 0; i < v2.size(); i++) m2[i] = (v2[i] && !v2[i]->isBad()) ? H.of(v2[i]) : -1;
+    FlatFV f1(pKF1->mFeatVec), f2(pKF2->mFeatVec);
+    const int n = orbfe_search_by_bow_kf(reinterpret_cast<const orbfe_keypoint*>(pKF1->mvKeysUn.data()),
+                                         pKF1->mDescriptors.data, m1.data(), pKF1->N, &f1.v,
+                                         reinterpret_cast<const orbfe_keypoint*>(pKF2->mvKeysUn.data()),
+                                         pKF2->mDescriptors.data, m2.data(), pKF2->N, &f2.v, out.data(), mfNNratio,
+                                         mbCheckOrientation);
+    vpMatches12.assign(v1.size(), static_cast<MapPoint*>(nullptr));
+    for (size_t i = 0; i < v1.size(); i++) vpMatches12[i] = H.at(out[i]);
+    return n;
+}
+
+int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, vector<pair<size_t, size_t>>& vMatchedPairs,
+                                       const bool bOnlyStereo, const bool bCoarse) {
+    if (pKF1->mpCamera2 || pKF2->mpCamera2)
+        return SearchForTriangulation_cpu(pKF1, pKF2, vMatchedPairs, bOnlyStereo, bCoarse);
+    // the per-call constants, computed exactly as the reference does (ORBmatcher.cc:913-927,
+    // Pinhole.cpp:109-112)
+    const Sophus::SE3f T1w = pKF1->GetPose(), T2w = pKF2->GetPose(), Tw2 = pKF2->GetPoseInverse();
+    const Eigen::Vector3f C2 = T2w * pKF1->GetCameraCenter();
+    const Eigen::Vector2f ep = pKF2->mpCamera->project(C2);
+    const Sophus::SE3f T12 = T1w * Tw2;
+    const Eigen::Matrix3f R12 = T12.rotationMatrix();
+    const Eigen::Vector3f t12 = T12.translation();
+    const Eigen::Matrix3f K1 = pKF1->mpCamera->toK_(), K2 = pKF2->mpCamera->toK_();
+    const Eigen::Matrix3f F = K1.transpose().inverse() * Sophus::SO3f::hat(t12) * R12 * K2.inverse();
+    float F12[9], epv[2] = {ep(0), ep(1)};
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) F12[3 * r + c] = F(r, c);
+    vector<int32_t> m1(pKF1->N), m2(pKF2->N), out(pKF1->N);
+    for (int i = 0; i < pKF1->N; i++) m1[i] = pKF1->GetMapPoint(i) ? 1 : -1;
+    for (int i = 0; i < pKF2->N; i++) m2[i] = pKF2->GetMapPoint(i) ? 1 : -1;
+    FlatFV f1(pKF1->mFeatVec), f2(pKF2->mFeatVec);
+    const orbfe_frame k1 = kf_view(pKF1), k2 = kf_view(pKF2);
+    const int n = orbfe_search_for_triangulation(&k1, m1.data(), &f1.v, &k2, m2.data(), &f2.v, F12, epv,
+                                                 pKF2->mvLevelSigma2.data(), bOnlyStereo, bCoarse,
+                                                 mbCheckOrientation, out.data());
+    vMatchedPairs.clear();
+    vMatchedPairs.reserve(n);
+    for (int i = 0; i < pKF1->N; i++)
+        if (out[i] >= 0) vMatchedPairs.push_back(make_pair((size_t)i, (size_t)out[i]));
+    return n;
+}
+
+int ORBmatcher::Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, const float th, const bool bRight) {
+    if (bRight || pKF->mpCamera2) return Fuse_cpu(pKF, vpMapPoints, th, bRight);
+    const orbfe_kf_camera cam = kf_camera(pKF, pKF->GetPose(), pKF->GetCameraCenter());
+    vector<orbfe_map_point_3d> q(vpMapPoints.size());
+    for (size_t i = 0; i < vpMapPoints.size(); i++) {
+        MapPoint* p = vpMapPoints[i];
+        q[i] = point_3d(p, p ? 0 : -1, (p && p->IsInKeyFrame(pKF)) ? ORBFE_MP_SKIP : 0);
+    }
+    vector<int32_t> best(q.size()), dist(q.size());
+    const orbfe_frame kf = kf_view(pKF);
+    if (orbfe_fuse(&kf, &cam, pKF->mvInvLevelSigma2.data(), q.data(), (int)q.size(), th, 0, best.data(),
+                   dist.data()) < 0)
+        return Fuse_cpu(pKF, vpMapPoints, th, bRight);
+    // the reference's commit, in point order; the isBad / IsInKeyFrame gate is re-read because an
+    // earlier commit (Replace / AddObservation) may have changed it
+    int nFused = 0;
+    for (size_t i = 0; i < vpMapPoints.size(); i++) {
+        MapPoint* pMP = vpMapPoints[i];
+        if (best[i] < 0 || !pMP || pMP->isBad() || pMP->IsInKeyFrame(pKF)) continue;
+        MapPoint* pMPinKF = pKF->GetMapPoint(best[i]);
+        if (pMPinKF) {
+            if (!pMPinKF->isBad()) {
+                if (pMPinKF->Observations() > pMP->Observations()) pMP->Replace(pMPinKF);
+                else pMPinKF->Replace(pMP);
+            }
+        } else {
+            pMP->AddObservation(pKF, best[i]);
+            pKF->AddMapPoint(pMP, best[i]);
+        }
+        nFused++;
+    }
+    return nFused;
+}
+
+int ORBmatcher::Fuse(KeyFrame* pKF, Sophus::Sim3f& Scw, const vector<MapPoint*>& vpPoints, float th,
+                     vector<MapPoint*>& vpReplacePoint) {
+    const Sophus::SE3f Tcw = Sophus::SE3f(Scw.rotationMatrix(), Scw.translation() / Scw.scale());
+    const orbfe_kf_camera cam = kf_camera(pKF, Tcw, Tcw.inverse().translation());
+    const set<MapPoint*> spAlreadyFound = pKF->GetMapPoints();
+    vector<orbfe_map_point_3d> q(vpPoints.size());
+    for (size_t i = 0; i < vpPoints.size(); i++)
+        q[i] = point_3d(vpPoints[i], 0, spAlreadyFound.count(vpPoints[i]) ? ORBFE_MP_SKIP : 0);
+    vector<int32_t> best(q.size()), dist(q.size());
+    const orbfe_frame kf = kf_view(pKF);
+    if (orbfe_fuse(&kf, &cam, nullptr, q.data(), (int)q.size(), th, 1, best.data(), dist.data()) < 0)
+        return Fuse_cpu(pKF, Scw, vpPoints, th, vpReplacePoint);
+    int nFused = 0;
+    for (size_t i = 0; i < vpPoints.size(); i++) {
+        if (best[i] < 0) continue;
+        MapPoint* pMP = vpPoints[i];
+        MapPoint* pMPinKF = pKF->GetMapPoint(best[i]);
+        if (pMPinKF) {
+            if (!pMPinKF->isBad()) vpReplacePoint[i] = pMPinKF;
+        } else {
+            pMP->AddObservation(pKF, best[i]);
+            pKF->AddMapPoint(pMP, best[i]);
+        }
+        nFused++;
+    }
+    return nFused;
+}
+
+int ORBmatcher::SearchByProjection(KeyFrame* pKF, Sophus::Sim3f& Scw, const vector<MapPoint*>& vpPoints,
+                                   vector<MapPoint*>& vpMatched, int th, float ratioHamming) {
+    const Sophus::SE3f Tcw = Sophus::SE3f(Scw.rotationMatrix(), Scw.translation() / Scw.scale());
+    const orbfe_kf_camera cam = kf_camera(pKF, Tcw, Tcw.inverse().translation());
+    Handles H;
+    vector<orbfe_map_point_3d> q(vpPoints.size());
+    for (size_t i = 0; i < vpPoints.size(); i++) q[i] = point_3d(vpPoints[i], H.of(vpPoints[i]), 0);
+    vector<int32_t> m(vpMatched.size());
+    for (size_t k = 0; k < vpMatched.size(); k++) m[k] = H.of(vpMatched[k]);
+    const orbfe_frame kf = kf_view(pKF);
+    const int n = orbfe_search_by_projection_sim3(&kf, &cam, q.data(), (int)q.size(), nullptr, th, ratioHamming,
+                                                  m.data(), nullptr);
+    for (size_t k = 0; k < vpMatched.size(); k++) vpMatched[k] = H.at(m[k]);
+    return n;
+}
+
+int ORBmatcher::SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12, const Sophus::Sim3f& S12,
+                             const float th) {
+    if (pKF1->mpCamera2 || pKF2->mpCamera2) return SearchBySim3_cpu(pKF1, pKF2, vpMatches12, S12, th);
+    Handles H;
+    const vector<MapPoint*> v1 = pKF1->GetMapPointMatches(), v2 = pKF2->GetMapPointMatches();
+    vector<orbfe_map_point_3d> p1(v1.size()), p2(v2.size());
+    for (size_t i = 0; i < v1.size(); i++) p1[i] = point_3d(v1[i], H.of(v1[i]), 0);
+    for (size_t i = 0; i < v2.size(); i++) p2[i] = point_3d(v2[i], H.of(v2[i]), 0);
+    vector<int32_t> m12(v1.size()), idx2(v1.size(), -1);
+    for (size_t i = 0; i < v1.size(); i++) {
+        m12[i] = H.of(vpMatches12[i]);
+        if (vpMatches12[i]) idx2[i] = get<0>(vpMatches12[i]->GetIndexInKeyFrame(pKF2));
+    }
+    orbfe_kf_camera c1 = kf_camera(pKF1, pKF1->GetPose(), pKF1->GetCameraCenter());
+    orbfe_kf_camera c2 = kf_camera(pKF2, pKF2->GetPose(), pKF2->GetCameraCenter());
+    const orbfe_pose s12 = pose_of(S12), s21 = pose_of(S12.inverse());
+    const orbfe_frame k1 = kf_view(pKF1), k2 = kf_view(pKF2);
+    const int n = orbfe_search_by_sim3(&k1, &k2, p1.data(), p2.data(), &c1, &c2, &s12, &s21, th, m12.data(),
+                                       idx2.data());
+    for (size_t i = 0; i < v1.size(); i++) vpMatches12[i] = H.at(m12[i]);
+    return n;
+}
+
+// MapPoint::ComputeDistinctiveDescriptors for the points LocalMapping updates in one step
+// (MapPointCulling / SearchInNeighbors call it per point; batching them is the caller's choice).
+void ComputeDistinctiveDescriptorsBatch(const vector<MapPoint*>& points) {
+    vector<uint8_t> desc;
+    vector<int32_t> off(1, 0);
+    for (size_t p = 0; p < points.size(); p++) {
+        if (points[p]->isBad()) {   // mbBad: the reference returns without touching the descriptor
+            off.push_back((int32_t)(desc.size() / 32));
+            continue;
+        }
+        for (const auto& obs : points[p]->GetObservations()) {
+            KeyFrame* pKF = obs.first;
+            if (pKF->isBad()) continue;
+            const int left = get<0>(obs.second), right = get<1>(obs.second);
+            for (int idx : {left, right}) {
+                if (idx < 0) continue;
+                const uint8_t* row = pKF->mDescriptors.ptr<uint8_t>(idx);
+                desc.insert(desc.end(), row, row + 32);
+            }
+        }
+        off.push_back((int32_t)(desc.size() / 32));
+    }
+    vector<int32_t> best(points.size());
+    orbfe_distinctive_descriptors(desc.data(), off.data(), (int)points.size(), best.data());
+    for (size_t p = 0; p < points.size(); p++)
+        if (best[p] >= 0) points[p]->SetDescriptor(&desc[32 * ((size_t)off[p] + best[p])]);   // under mMutexFeatures
+}
+
+}  // namespace ORB_SLAM3
