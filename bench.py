@@ -59,6 +59,46 @@ def pmc_traffic(n_img, w, h):
     return best
 
 
+def pmc_cache(n_img, w, h):
+    """Descriptor-pass L2 hit rate and LDS bank-conflict share from the newest committed cache PMC
+    summary for this workload (profiles/rNN_pmc_cache.json, tools/pmc_cache_summary.py)."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_cache.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if (d.get("images_per_step"), d.get("width"), d.get("height")) == (n_img, w, h):
+            best = (d["kernels"], os.path.basename(f))
+    return best
+
+
+def copy_peak_gbps(torch, dev, nbytes=1 << 30, reps=10):
+    """Measured device-to-device copy rate (read + write bytes / time) of a 1 GiB buffer with the
+    library's 16-byte-per-lane streaming copy kernel: the practical HBM ceiling the roofline is
+    also quoted against."""
+    from orb_slam3_ros_amd import _lib
+    lib = _lib.load()
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    s = torch.cuda.current_stream(dev)
+
+    def cp():
+        _lib.check(lib.orbfe_copy_stream(a.data_ptr(), b.data_ptr(), nbytes, s.cuda_stream), "copy_stream")
+
+    cp()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        cp()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    return 2 * nbytes / (ms * 1e-3) / 1e9
+
+
 def cpu_baseline(pairs_l, pairs_r, w, h, nfeatures, bf, fx):
     """Oracle CPU path (C++ restatement, kind='port') on a bounded sample, host cores."""
     from oracle import oracle
@@ -268,6 +308,8 @@ def main():
         achieved = n_img * bytes_img / (pyr_fast_ms * 1e-3) / 1e9
         dominant = max(stages, key=stages.get)
         tr = pmc_traffic(n_img, W, H)
+        cache = pmc_cache(n_img, W, H)
+        copy_peak = copy_peak_gbps(torch, dev)
         result = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -305,12 +347,18 @@ def main():
                 "bytes_per_image": bytes_img,
                 "images_per_launch": n_img,
                 "kernel_ms_per_launch": round(pyr_fast_ms, 4),
+                "copy_peak_measured": round(copy_peak, 1),
+                "frac_vs_copy_peak": round(achieved / copy_peak, 4),
             },
             "stage_ms": {k: round(v, 4) for k, v in stages.items()},
             "dominant_stage": dominant,
             "keypoints_per_image_mean": float(counts[:, 0].mean()),
             "stereo_matches_per_frame_mean": float(nm.mean()),
         }
+        if cache is not None and "k_describe" in cache[0]:
+            kd = cache[0]["k_describe"]
+            result["describe_pass"] = {"kernel": "k_describe", "l2_hit_rate": kd["l2_hit_rate"],
+                                       "lds_bank_conflict_share": kd["lds_conflict_share"], "source": cache[1]}
         if rect is not None:
             result["rectify_remap"] = rect
         if args.matcher_steps > 0:

@@ -420,6 +420,11 @@ int orbfe_debug_block_sort(uint64_t* data, int n);
 /* Library identification (build string). */
 const char* orbfe_version(void);
 
+/* Measurement helper (bench.py): streaming device-to-device copy of `bytes` (multiple of 16, both
+ * pointers 16-byte aligned) with 16-byte loads / stores per lane, on `stream` (NULL = legacy
+ * default). Its rate is the measured HBM copy ceiling the roofline is also quoted against. */
+int orbfe_copy_stream(const void* d_src, void* d_dst, size_t bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

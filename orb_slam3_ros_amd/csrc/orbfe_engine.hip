@@ -368,9 +368,27 @@ static hipStream_t pick_stream(orbfe_extractor* h, void* stream) {
     return stream ? (hipStream_t)stream : h->own_stream;
 }
 
+typedef unsigned int orbfe_u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_copy16(const orbfe_u32x4* __restrict__ src, orbfe_u32x4* __restrict__ dst,
+                                                size_t n) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
 extern "C" {
 
 const char* orbfe_version(void) { return "orbfe 0.1 (gfx950, HIP)"; }
+
+int orbfe_copy_stream(const void* d_src, void* d_dst, size_t bytes, void* stream) {
+    if (!d_src || !d_dst || (bytes & 15) || (((uintptr_t)d_src | (uintptr_t)d_dst) & 15)) return ORBFE_E_ARG;
+    const size_t n = bytes / 16;
+    if (!n) return ORBFE_OK;
+    const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 256 * 16);
+    hipLaunchKernelGGL(k_copy16, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const orbfe_u32x4*)d_src, (orbfe_u32x4*)d_dst, n);
+    HIPCHK(hipGetLastError());
+    return ORBFE_OK;
+}
 
 int orbfe_extractor_create(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST,
                            orbfe_extractor** out) {

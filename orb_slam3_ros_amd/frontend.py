@@ -42,7 +42,9 @@ class StereoFrontEnd:
             _lib.check(self.lib.orbfe_extractor_create(nfeatures, scale_factor, nlevels, ini_th, min_th,
                                                        ctypes.byref(h)), "create")
             self.handles.append(h)
-            self.streams.append(torch.cuda.Stream(self.device) if len(self.parts) > 1 else None)
+            # an explicit stream per pipeline: the library's NULL-stream default is its own
+            # non-blocking stream, which torch's default stream would not be ordered against
+            self.streams.append(torch.cuda.Stream(self.device))
         self.h = self.handles[0]
         self.cap = _lib.check(self.lib.orbfe_extractor_capacity(self.h, self.W, self.H), "capacity")
         for h in self.handles[1:]:
@@ -61,6 +63,8 @@ class StereoFrontEnd:
                        "set_batch_outputs")
         self._ptrs = None
         self._ptr_key = None
+        self._stage_on = False
+        self._stereo_ev = []
 
     def _pointer_arrays(self, images):
         key = (images.data_ptr(), tuple(images.shape), tuple(images.stride()))
@@ -72,45 +76,59 @@ class StereoFrontEnd:
         return self._ptrs
 
     def run(self, images, stream=None):
-        """images: [2F, H, W] uint8 CUDA tensor, contiguous rows (left = even, right = odd)."""
+        """images: [2F, H, W] uint8 CUDA tensor, contiguous rows (left = even, right = odd).
+        stream=None: the work runs on the front end's own torch streams, ordered after and before
+        the caller's current stream; otherwise everything is enqueued on `stream` (a hipStream_t)."""
         torch = self.torch
         assert images.dtype == torch.uint8 and images.dim() == 3 and images.is_cuda
         n = images.shape[0]
         assert n == 2 * self.F and images.shape[1] == self.H and images.shape[2] == self.W
         assert images.stride(2) == 1 and images.stride(1) >= self.W
         main = torch.cuda.current_stream(self.device)
-        s_main = stream if stream is not None else main.cuda_stream
         ptrs = self._pointer_arrays(images)
-        multi = len(self.parts) > 1
-        if multi:
+        if stream is None:   # ordered after / before the caller's current torch stream
             ev0 = torch.cuda.Event()
             ev0.record(main)
-        for h, st, p, (a, b) in zip(self.handles, self.streams, ptrs, self.parts):
-            if multi:
+        for i, (h, st, p, (a, b)) in enumerate(zip(self.handles, self.streams, ptrs, self.parts)):
+            if stream is None:
                 st.wait_event(ev0)
                 s = st.cuda_stream
             else:
-                s = s_main
+                s = stream
             _lib.check(self.lib.orbfe_extract_batch(h, 2 * (b - a), p, self.W, self.H, images.stride(1), 0, 0, s),
                        "extract_batch")
+            timed = self._stage_on and i == 0 and stream is None
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
             _lib.check(self.lib.orbfe_stereo_match_batch(h, 0, 2, h, 1, 2, b - a, self.bf, self.fx,
                                                          self.uright[a].data_ptr(), self.depth[a].data_ptr(),
                                                          self.nmatch[a:].data_ptr(), s), "stereo_match_batch")
-        if multi:
+            if timed:
+                e1.record(st)
+                self._stereo_ev.append((e0, e1))
+        if stream is None:
             for st in self.streams:
                 main.wait_stream(st)
 
     def set_stage_timing(self, on: bool):
         for h in self.handles:
             self.lib.orbfe_set_stage_timing(h, 1 if on else 0)
+        self._stage_on = bool(on)
+        self._stereo_ev = []
 
     def stage_timing(self):
-        """Mean per-batch stage times of the first pipeline (its own stream)."""
+        """Mean per-batch stage times of the first pipeline (its own stream); "stereo" =
+        ComputeStereoMatches (k_stereo + k_stereo_cut), HIP events on the launch stream."""
         ms = np.zeros(_lib.ORBFE_NUM_STAGES, np.float32)
         n = self.lib.orbfe_get_stage_timing(self.handles[0], ms.ctypes.data)
         for h in self.handles[1:]:
             self.lib.orbfe_get_stage_timing(h, np.zeros(_lib.ORBFE_NUM_STAGES, np.float32).ctypes.data)
-        return dict(zip(_lib.STAGE_NAMES, ms.tolist())), n
+        out = dict(zip(_lib.STAGE_NAMES, ms.tolist()))
+        if self._stereo_ev:
+            self.torch.cuda.synchronize(self.device)
+            out["stereo"] = float(np.mean([a.elapsed_time(b) for a, b in self._stereo_ev]))
+        return out, n
 
     def host_frame(self, f: int):
         """(kps_left structured, desc_left, uright, depth) of frame f, copied to the host."""

@@ -29,9 +29,12 @@ def remap_linear(src: np.ndarray, mapx: np.ndarray, mapy: np.ndarray) -> np.ndar
 
 def remap_linear_batch(src, mapx, mapy, out, stream=None):
     """Device path: src [n, sh, sw] u8 and out [n, dh, dw] u8 CUDA tensors, maps [dh, dw] float32
-    CUDA tensors shared by all images."""
+    CUDA tensors shared by all images. stream: hipStream_t (default: torch's current stream)."""
+    import torch
     lib = _lib.load()
     n = src.shape[0]
+    if stream is None:   # enqueue on the caller's current torch stream
+        stream = torch.cuda.current_stream(src.device).cuda_stream
     if src.stride(2) != 1 or out.stride(2) != 1 or not mapx.is_contiguous() or not mapy.is_contiguous():
         raise ValueError("remap_linear_batch needs row-contiguous images and contiguous maps")
     ps = (ctypes.c_void_p * n)(*[src[i].data_ptr() for i in range(n)])
