@@ -92,7 +92,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    # ORBFE_LIB: an alternative build of the same library (kernel A/B experiments, tools/)
+    p = path or os.environ.get("ORBFE_LIB") or LIB_PATH
     # One HIP runtime per process: torch ships its own libamdhip64.so with the same soname as
     # /opt/rocm's. Import torch first (when present) so liborbfe.so binds to that runtime too;
     # loading ours first would put two runtimes in the process and break device calls.
