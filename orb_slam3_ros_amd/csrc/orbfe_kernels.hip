@@ -435,7 +435,6 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
     const int cbeg = (bx * 4 + wave) * FAST_CPW;
     if (cbeg >= g.total_cells) return;
     const int cend = min(cbeg + FAST_CPW, g.total_cells);
-    const int th = g.min_th;
     uint32_t pf[FAST_PF];
     FastCell cur = fast_cell(imgs, in_pitch, pyr, pyr_stride, g, b, cbeg);
     fast_prefetch(cur, lane, pf);
@@ -492,154 +491,168 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
             continue;
         }
         const uint8_t* s_px = s_img + 1;   // ROI pixel (y, x) = s_px[y * RS + x]
-        // pass 1: FAST's exact necessary test (each 9-arc contains one pixel of every opposite
-        // pair (k, k+8), k = 0, 2, 4, 6, all of one sign) for 4 pixels per lane in packed u16x2
-        // arithmetic (even bytes / odd bytes); candidates compacted row-major as (dy << 8 | dx).
-        int ncand = 0;
-        if (ng) {
-            const int rpi = 64 / ng;
-            const int ly = lane / ng, lg = lane - ly * ng;
-            const uint32_t* s32 = (const uint32_t*)s_img;
-            const orbfe_ushort2 tv = {(unsigned short)th, (unsigned short)th};
-            const int valid4 = min(4, dw - 4 * lg);
-            const uint32_t vmask = ly < rpi && valid4 > 0 ? (1u << valid4) - 1u : 0u;
-            for (int y0 = 0; y0 < dh; y0 += rpi) {
-                const int y = y0 + ly;
-                uint32_t dbits = 0, bbits = 0;
-                if (vmask && y < dh) {
-                    const uint32_t* r0p = s32 + (y + 3) * nd + lg;   // dword q of the centre row
-                    const uint32_t c0w = r0p[0], c1w = r0p[1], c2w = r0p[2];
-                    const uint32_t pp[8] = {
-                        r0p[3 * nd + 1],                                                    // 0: (0, 3)
-                        r0p[-3 * nd + 1],                                                   // 8: (0,-3)
-                        __builtin_amdgcn_alignbyte(c2w, c1w, 3),                            // 4: (3, 0)
-                        __builtin_amdgcn_alignbyte(c1w, c0w, 1),                            // 12: (-3, 0)
-                        __builtin_amdgcn_alignbyte(r0p[2 * nd + 2], r0p[2 * nd + 1], 2),    // 2: (2, 2)
-                        __builtin_amdgcn_alignbyte(r0p[-2 * nd + 1], r0p[-2 * nd], 2),      // 10: (-2,-2)
-                        __builtin_amdgcn_alignbyte(r0p[-2 * nd + 2], r0p[-2 * nd + 1], 2),  // 6: (2,-2)
-                        __builtin_amdgcn_alignbyte(r0p[2 * nd + 1], r0p[2 * nd], 2)};       // 14: (-2, 2)
+        // attempt 0 = FAST at iniThFAST; attempt 1 (only when attempt 0 leaves no NMS survivor) =
+        // FAST at minThFAST over a cleared score map: the reference's per-cell fallback
+        // (ORBextractor.cc:826-846). Most cells stop after attempt 0, whose candidate set is a
+        // fraction of minThFAST's.
+        int nsurv = 0;
+        bool stop = false;
+        for (int attempt = 0; attempt < 2; attempt++) {
+            const int th = attempt == 0 ? g.ini_th : g.min_th;
+            if (attempt) {
+                uint32_t* s32z = (uint32_t*)s_sc;
+                for (int i = lane; i < me.rows * nd; i += 64) s32z[i] = 0u;
+                WAVE_SYNC();
+            }
+            // pass 1: FAST's exact necessary test (each 9-arc contains one pixel of every opposite
+            // pair (k, k+8), k = 0, 2, 4, 6, all of one sign) for 4 pixels per lane in packed u16x2
+            // arithmetic (even bytes / odd bytes); candidates compacted row-major as (dy << 8 | dx).
+            int ncand = 0;
+            if (ng) {
+                const int rpi = 64 / ng;
+                const int ly = lane / ng, lg = lane - ly * ng;
+                const uint32_t* s32 = (const uint32_t*)s_img;
+                const orbfe_ushort2 tv = {(unsigned short)th, (unsigned short)th};
+                const int valid4 = min(4, dw - 4 * lg);
+                const uint32_t vmask = ly < rpi && valid4 > 0 ? (1u << valid4) - 1u : 0u;
+                for (int y0 = 0; y0 < dh; y0 += rpi) {
+                    const int y = y0 + ly;
+                    uint32_t dbits = 0, bbits = 0;
+                    if (vmask && y < dh) {
+                        const uint32_t* r0p = s32 + (y + 3) * nd + lg;   // dword q of the centre row
+                        const uint32_t c0w = r0p[0], c1w = r0p[1], c2w = r0p[2];
+                        const uint32_t pp[8] = {
+                            r0p[3 * nd + 1],                                                    // 0: (0, 3)
+                            r0p[-3 * nd + 1],                                                   // 8: (0,-3)
+                            __builtin_amdgcn_alignbyte(c2w, c1w, 3),                            // 4: (3, 0)
+                            __builtin_amdgcn_alignbyte(c1w, c0w, 1),                            // 12: (-3, 0)
+                            __builtin_amdgcn_alignbyte(r0p[2 * nd + 2], r0p[2 * nd + 1], 2),    // 2: (2, 2)
+                            __builtin_amdgcn_alignbyte(r0p[-2 * nd + 1], r0p[-2 * nd], 2),      // 10: (-2,-2)
+                            __builtin_amdgcn_alignbyte(r0p[-2 * nd + 2], r0p[-2 * nd + 1], 2),  // 6: (2,-2)
+                            __builtin_amdgcn_alignbyte(r0p[2 * nd + 1], r0p[2 * nd], 2)};       // 14: (-2, 2)
 #pragma unroll
-                    for (int par = 0; par < 2; par++) {
-                        const uint32_t sel = par ? 0x0c030c01u : 0x0c020c00u;
-                        const orbfe_ushort2 v = as_us2(__builtin_amdgcn_perm(0u, c1w, sel));
-                        const orbfe_ushort2 lo = __builtin_elementwise_sub_sat(v, tv), hi = v + tv;
-                        // dark possible  <=> every pair has a member < v - t <=> max_k min(pair k) < v - t
-                        // bright possible <=> every pair has a member > v + t <=> min_k max(pair k) > v + t
-                        orbfe_ushort2 D = {0, 0}, B = {0xffff, 0xffff};
+                        for (int par = 0; par < 2; par++) {
+                            const uint32_t sel = par ? 0x0c030c01u : 0x0c020c00u;
+                            const orbfe_ushort2 v = as_us2(__builtin_amdgcn_perm(0u, c1w, sel));
+                            const orbfe_ushort2 lo = __builtin_elementwise_sub_sat(v, tv), hi = v + tv;
+                            // dark possible  <=> every pair has a member < v - t <=> max_k min(pair k) < v - t
+                            // bright possible <=> every pair has a member > v + t <=> min_k max(pair k) > v + t
+                            orbfe_ushort2 D = {0, 0}, B = {0xffff, 0xffff};
 #pragma unroll
-                        for (int k = 0; k < 4; k++) {
-                            const orbfe_ushort2 xa = as_us2(__builtin_amdgcn_perm(0u, pp[2 * k], sel));
-                            const orbfe_ushort2 xb = as_us2(__builtin_amdgcn_perm(0u, pp[2 * k + 1], sel));
-                            D = __builtin_elementwise_max(D, __builtin_elementwise_min(xa, xb));
-                            B = __builtin_elementwise_min(B, __builtin_elementwise_max(xa, xb));
+                            for (int k = 0; k < 4; k++) {
+                                const orbfe_ushort2 xa = as_us2(__builtin_amdgcn_perm(0u, pp[2 * k], sel));
+                                const orbfe_ushort2 xb = as_us2(__builtin_amdgcn_perm(0u, pp[2 * k + 1], sel));
+                                D = __builtin_elementwise_max(D, __builtin_elementwise_min(xa, xb));
+                                B = __builtin_elementwise_min(B, __builtin_elementwise_max(xa, xb));
+                            }
+                            const orbfe_ushort2 sd = __builtin_elementwise_sub_sat(lo, D);
+                            const orbfe_ushort2 sb = __builtin_elementwise_sub_sat(B, hi);
+                            dbits |= (sd.x ? 1u : 0u) << par;
+                            dbits |= (sd.y ? 1u : 0u) << (2 + par);
+                            bbits |= (sb.x ? 1u : 0u) << par;
+                            bbits |= (sb.y ? 1u : 0u) << (2 + par);
                         }
-                        const orbfe_ushort2 sd = __builtin_elementwise_sub_sat(lo, D);
-                        const orbfe_ushort2 sb = __builtin_elementwise_sub_sat(B, hi);
-                        dbits |= (sd.x ? 1u : 0u) << par;
-                        dbits |= (sd.y ? 1u : 0u) << (2 + par);
-                        bbits |= (sb.x ? 1u : 0u) << par;
-                        bbits |= (sb.y ? 1u : 0u) << (2 + par);
+                        dbits &= vmask;
+                        bbits &= vmask;
                     }
-                    dbits &= vmask;
-                    bbits &= vmask;
+                    // one entry per (pixel, possible sign): dy << 7 | dx, bit 14 = bright, bit 15 =
+                    // second entry of a pixel (both signs passed); at most one sign can be a corner
+                    const int cnt = __popc(dbits) + __popc(bbits);   // <= 8: scan by bit planes
+                    const unsigned long long lt = (1ull << lane) - 1ull;
+                    const unsigned long long m0 = __ballot(cnt & 1), m1 = __ballot(cnt & 2), m2 = __ballot(cnt & 4),
+                                             m3 = __ballot(cnt & 8);
+                    int pos = ncand + __popcll(m0 & lt) + 2 * __popcll(m1 & lt) + 4 * __popcll(m2 & lt) +
+                              8 * __popcll(m3 & lt);
+                    const int packed = (y << 7) | (4 * lg);
+                    for (int i = 0; i < 4; i++) {
+                        const uint32_t di = (dbits >> i) & 1u, bi = (bbits >> i) & 1u;
+                        if (di) s_cand[pos++] = (uint16_t)(packed + i);
+                        if (bi) s_cand[pos++] = (uint16_t)((packed + i) | 0x4000 | (di << 15));
+                    }
+                    ncand += __popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2) + 8 * __popcll(m3);
                 }
-                // one entry per (pixel, possible sign): dy << 7 | dx, bit 14 = bright, bit 15 =
-                // second entry of a pixel (both signs passed); at most one sign can be a corner
-                const int cnt = __popc(dbits) + __popc(bbits);   // <= 8: scan by bit planes
+            }
+            WAVE_SYNC();
+            if (ablate == 2) {
+                asm volatile("" ::"v"(ncand));
+                stop = true;
+                break;
+            }
+            // pass 2: exact score M - 1 (corner iff M > th) of each entry for its sign only, two
+            // entries per lane in packed u16x2 (saturated differences: an arc with a negative minimum
+            // never decides a corner); corners are compacted in place, in pixel order, as dy << 7 | dx
+            int ncorner = 0;
+            for (int j0 = 0; j0 < ncand; j0 += 128) {
+                const int j = j0 + 2 * lane;
+                const uint32_t e2 = j < ncand ? ((const uint32_t*)s_cand)[j >> 1] : 0u;
+                const bool ok0 = j < ncand, ok1 = j + 1 < ncand;
+                const uint32_t e0 = e2 & 0xFFFFu, e1 = ok1 ? e2 >> 16 : e0;
+                const uint8_t* q0 = s_px + (((e0 >> 7) & 127) + 3) * RS + (e0 & 127) + 3;
+                const uint8_t* q1 = s_px + (((e1 >> 7) & 127) + 3) * RS + (e1 & 127) + 3;
+                const uint32_t v2 = (uint32_t)q0[0] | ((uint32_t)q1[0] << 16);
+                const uint32_t bmask = ((e0 & 0x4000u) ? 0x0000FFFFu : 0u) | ((e1 & 0x4000u) ? 0xFFFF0000u : 0u);
+                orbfe_ushort2 P[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const int o = kRingDy[k] * RS + kRingDx[k];
+                    const orbfe_ushort2 x2 = as_us2((uint32_t)q0[o] | ((uint32_t)q1[o] << 16));
+                    const uint32_t dk = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(as_us2(v2), x2));
+                    const uint32_t bk = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(x2, as_us2(v2)));
+                    P[k] = as_us2((bk & bmask) | (dk & ~bmask));
+                }
+                orbfe_ushort2 m2[16], m4[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(P[k], P[(k + 1) & 15]);
+#pragma unroll
+                for (int k = 0; k < 16; k++) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
+                orbfe_ushort2 best = {0, 0};
+#pragma unroll
+                for (int k = 0; k < 16; k++)
+                    best = __builtin_elementwise_max(
+                        best, __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]), P[(k + 8) & 15]));
+                const bool c0 = ok0 && (int)best.x > th, c1 = ok1 && (int)best.y > th;
+                if (c0) s_sc[(((e0 >> 7) & 127) + 3) * RS + (e0 & 127) + 3] = (uint8_t)(best.x - 1);
+                if (c1) s_sc[(((e1 >> 7) & 127) + 3) * RS + (e1 & 127) + 3] = (uint8_t)(best.y - 1);
+                const int cc = (int)c0 + (int)c1;
                 const unsigned long long lt = (1ull << lane) - 1ull;
-                const unsigned long long m0 = __ballot(cnt & 1), m1 = __ballot(cnt & 2), m2 = __ballot(cnt & 4),
-                                         m3 = __ballot(cnt & 8);
-                int pos = ncand + __popcll(m0 & lt) + 2 * __popcll(m1 & lt) + 4 * __popcll(m2 & lt) +
-                          8 * __popcll(m3 & lt);
-                const int packed = (y << 7) | (4 * lg);
-                for (int i = 0; i < 4; i++) {
-                    const uint32_t di = (dbits >> i) & 1u, bi = (bbits >> i) & 1u;
-                    if (di) s_cand[pos++] = (uint16_t)(packed + i);
-                    if (bi) s_cand[pos++] = (uint16_t)((packed + i) | 0x4000 | (di << 15));
+                const unsigned long long b0 = __ballot(cc & 1), b1 = __ballot(cc & 2);
+                int pos = ncorner + __popcll(b0 & lt) + 2 * __popcll(b1 & lt);
+                if (c0) s_cand[pos++] = (uint16_t)(e0 & 0x3FFFu);
+                if (c1) s_cand[pos] = (uint16_t)(e1 & 0x3FFFu);
+                ncorner += __popcll(b0) + 2 * __popcll(b1);
+            }
+            WAVE_SYNC();
+            if (ablate == 3) {
+                asm volatile("" ::"v"((int)s_sc[lane]));
+                stop = true;
+                break;
+            }
+            // NMS over corners (every other pixel has score 0); survivors compacted in place
+            nsurv = 0;
+            for (int i0 = 0; i0 < ncorner; i0 += 64) {
+                const int i = i0 + lane;
+                bool surv = false;
+                int p = 0;
+                if (i < ncorner) {
+                    p = s_cand[i];
+                    const uint8_t* q = s_sc + ((p >> 7) + 3) * RS + (p & 127) + 3;
+                    const int sc = q[0];
+                    surv = sc > q[-1] && sc > q[1] && sc > q[-RS - 1] && sc > q[-RS] && sc > q[-RS + 1] &&
+                           sc > q[RS - 1] && sc > q[RS] && sc > q[RS + 1];
                 }
-                ncand += __popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2) + 8 * __popcll(m3);
+                const unsigned long long m = __ballot(surv);
+                if (surv) s_cand[nsurv + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)p;
+                nsurv += __popcll(m);
             }
-        }
-        WAVE_SYNC();
-        if (ablate == 2) {
-            asm volatile("" ::"v"(ncand));
+            WAVE_SYNC();
+            if (nsurv > 0) break;
+        }   // attempt
+        if (stop) {
             if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = 0;
             WAVE_SYNC();
             continue;
         }
-        // pass 2: exact score M - 1 (corner iff M > th) of each entry for its sign only, two
-        // entries per lane in packed u16x2 (saturated differences: an arc with a negative minimum
-        // never decides a corner); corners are compacted in place, in pixel order, as dy << 7 | dx
-        int ncorner = 0;
-        for (int j0 = 0; j0 < ncand; j0 += 128) {
-            const int j = j0 + 2 * lane;
-            const uint32_t e2 = j < ncand ? ((const uint32_t*)s_cand)[j >> 1] : 0u;
-            const bool ok0 = j < ncand, ok1 = j + 1 < ncand;
-            const uint32_t e0 = e2 & 0xFFFFu, e1 = ok1 ? e2 >> 16 : e0;
-            const uint8_t* q0 = s_px + (((e0 >> 7) & 127) + 3) * RS + (e0 & 127) + 3;
-            const uint8_t* q1 = s_px + (((e1 >> 7) & 127) + 3) * RS + (e1 & 127) + 3;
-            const uint32_t v2 = (uint32_t)q0[0] | ((uint32_t)q1[0] << 16);
-            const uint32_t bmask = ((e0 & 0x4000u) ? 0x0000FFFFu : 0u) | ((e1 & 0x4000u) ? 0xFFFF0000u : 0u);
-            orbfe_ushort2 P[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const int o = kRingDy[k] * RS + kRingDx[k];
-                const orbfe_ushort2 x2 = as_us2((uint32_t)q0[o] | ((uint32_t)q1[o] << 16));
-                const uint32_t dk = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(as_us2(v2), x2));
-                const uint32_t bk = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(x2, as_us2(v2)));
-                P[k] = as_us2((bk & bmask) | (dk & ~bmask));
-            }
-            orbfe_ushort2 m2[16], m4[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(P[k], P[(k + 1) & 15]);
-#pragma unroll
-            for (int k = 0; k < 16; k++) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
-            orbfe_ushort2 best = {0, 0};
-#pragma unroll
-            for (int k = 0; k < 16; k++)
-                best = __builtin_elementwise_max(
-                    best, __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]), P[(k + 8) & 15]));
-            const bool c0 = ok0 && (int)best.x > th, c1 = ok1 && (int)best.y > th;
-            if (c0) s_sc[(((e0 >> 7) & 127) + 3) * RS + (e0 & 127) + 3] = (uint8_t)(best.x - 1);
-            if (c1) s_sc[(((e1 >> 7) & 127) + 3) * RS + (e1 & 127) + 3] = (uint8_t)(best.y - 1);
-            const int cc = (int)c0 + (int)c1;
-            const unsigned long long lt = (1ull << lane) - 1ull;
-            const unsigned long long b0 = __ballot(cc & 1), b1 = __ballot(cc & 2);
-            int pos = ncorner + __popcll(b0 & lt) + 2 * __popcll(b1 & lt);
-            if (c0) s_cand[pos++] = (uint16_t)(e0 & 0x3FFFu);
-            if (c1) s_cand[pos] = (uint16_t)(e1 & 0x3FFFu);
-            ncorner += __popcll(b0) + 2 * __popcll(b1);
-        }
-        WAVE_SYNC();
-        if (ablate == 3) {
-            asm volatile("" ::"v"((int)s_sc[lane]));
-            if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = 0;
-            WAVE_SYNC();
-            continue;
-        }
-        // NMS over corners (every other pixel has score 0); survivors compacted in place
-        int nsurv = 0, nhi = 0;
-        for (int i0 = 0; i0 < ncorner; i0 += 64) {
-            const int i = i0 + lane;
-            bool surv = false, hi = false;
-            int p = 0;
-            if (i < ncorner) {
-                p = s_cand[i];
-                const uint8_t* q = s_sc + ((p >> 7) + 3) * RS + (p & 127) + 3;
-                const int sc = q[0];
-                surv = sc > q[-1] && sc > q[1] && sc > q[-RS - 1] && sc > q[-RS] && sc > q[-RS + 1] &&
-                       sc > q[RS - 1] && sc > q[RS] && sc > q[RS + 1];
-                hi = surv && sc >= g.ini_th;
-            }
-            const unsigned long long m = __ballot(surv);
-            if (surv) s_cand[nsurv + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)p;
-            nsurv += __popcll(m);
-            nhi += __popcll(__ballot(hi));
-        }
-        WAVE_SYNC();
-        // emission in row-major order: survivors with score >= iniTh, or all of them when none
-        // reaches it (the reference's FAST(iniTh) -> FAST(minTh) fallback)
-        const int thr = nhi > 0 ? g.ini_th : 1;
+        // emission of the survivors in row-major order (FAST's emission order)
         int base = 0;
         uint32_t* out = cellkeys + (size_t)b * g.cellkeys_per_img + L.cellkey_off + (size_t)me.local * L.cell_cap;
         const int xr0 = me.c0 - ORBFE_MINB + 3, yr0 = me.r0 - ORBFE_MINB + 3;
@@ -650,7 +663,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
                 p = s_cand[i];
                 sc = s_sc[((p >> 7) + 3) * RS + (p & 127) + 3];
             }
-            const bool f = i < nsurv && sc >= thr;
+            const bool f = i < nsurv;
             const unsigned long long m = __ballot(f);
             const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
             if (f) out[pos] = (uint32_t)(xr0 + (p & 127)) | ((uint32_t)(yr0 + (p >> 7)) << 12) | ((uint32_t)sc << 24);
