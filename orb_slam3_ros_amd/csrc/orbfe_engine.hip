@@ -290,6 +290,7 @@ static int ensure(orbfe_extractor* h, int W, int H, int B) {
         free_buffers(h);
     }
     if (h->oct_lds > 160 * 1024) return ORBFE_E_ARG;
+    if ((size_t)4 * (2 * h->roi_max + h->cand_bytes) > 160 * 1024) return ORBFE_E_ARG;   // k_fast: 4 waves
     B = std::max(B, 1);
     const OrbGeom& g = h->g;
     HIPCHK(hipMalloc(&h->d_tab, std::max<size_t>(2, h->tab.size() * 2)));

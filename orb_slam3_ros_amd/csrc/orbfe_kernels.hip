@@ -432,6 +432,9 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
     uint8_t* s_img = smem_fast + wave * (2 * roi_max + cand_bytes);
     uint8_t* s_sc = s_img + roi_max;
     uint16_t* s_cand = (uint16_t*)(s_sc + roi_max);
+    // pass-1 group records live in the (all-zero) score map until they are expanded, then those
+    // dwords are zeroed again: 4 * groups <= 4 * ng * dh < the cell's score-map bytes
+    uint32_t* s_grp = (uint32_t*)s_sc;
     const int cbeg = (bx * 4 + wave) * FAST_CPW;
     if (cbeg >= g.total_cells) return;
     const int cend = min(cbeg + FAST_CPW, g.total_cells);
@@ -507,7 +510,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
             // pass 1: FAST's exact necessary test (each 9-arc contains one pixel of every opposite
             // pair (k, k+8), k = 0, 2, 4, 6, all of one sign) for 4 pixels per lane in packed u16x2
             // arithmetic (even bytes / odd bytes); candidates compacted row-major as (dy << 8 | dx).
-            int ncand = 0;
+            int ncand = 0, ngrp = 0;
             if (ng) {
                 const int rpi = 64 / ng;
                 const int ly = lane / ng, lg = lane - ly * ng;
@@ -555,23 +558,39 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
                         dbits &= vmask;
                         bbits &= vmask;
                     }
-                    // one entry per (pixel, possible sign): dy << 7 | dx, bit 14 = bright, bit 15 =
-                    // second entry of a pixel (both signs passed); at most one sign can be a corner
-                    const int cnt = __popc(dbits) + __popc(bbits);   // <= 8: scan by bit planes
-                    const unsigned long long lt = (1ull << lane) - 1ull;
-                    const unsigned long long m0 = __ballot(cnt & 1), m1 = __ballot(cnt & 2), m2 = __ballot(cnt & 4),
-                                             m3 = __ballot(cnt & 8);
-                    int pos = ncand + __popcll(m0 & lt) + 2 * __popcll(m1 & lt) + 4 * __popcll(m2 & lt) +
-                              8 * __popcll(m3 & lt);
-                    const int packed = (y << 7) | (4 * lg);
-                    for (int i = 0; i < 4; i++) {
-                        const uint32_t di = (dbits >> i) & 1u, bi = (bbits >> i) & 1u;
-                        if (di) s_cand[pos++] = (uint16_t)(packed + i);
-                        if (bi) s_cand[pos++] = (uint16_t)((packed + i) | 0x4000 | (di << 15));
-                    }
-                    ncand += __popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2) + 8 * __popcll(m3);
+                    // 4-pixel groups with any candidate, compacted row-major (iteration-major,
+                    // then lane order): dy << 7 | dx0 in bits 0-13, dark bits 16-19, bright 20-23
+                    const uint32_t m8 = dbits | (bbits << 4);
+                    const unsigned long long gm = __ballot(m8 != 0u);
+                    if (m8)
+                        s_grp[ngrp + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(gm >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)gm, 0u))] =
+                            (uint32_t)((y << 7) | (4 * lg)) | (m8 << 16);
+                    ngrp += __popcll(gm);
                 }
             }
+            WAVE_SYNC();
+            // expand the groups into entries, one per (pixel, possible sign): dy << 7 | dx, bit 14 =
+            // bright, bit 15 = second entry of a pixel (both signs passed; at most one can be a corner)
+            for (int g0 = 0; g0 < ngrp; g0 += 64) {
+                const int gi = g0 + lane;
+                const uint32_t rec = gi < ngrp ? s_grp[gi] : 0u;
+                const uint32_t dbits = (rec >> 16) & 15u, bbits = rec >> 20;
+                const int cnt = __popc(rec >> 16);   // <= 8: scan by bit planes
+                const unsigned long long lt = (1ull << lane) - 1ull;
+                const unsigned long long m0 = __ballot(cnt & 1), m1 = __ballot(cnt & 2), m2 = __ballot(cnt & 4),
+                                         m3 = __ballot(cnt & 8);
+                int pos = ncand + __popcll(m0 & lt) + 2 * __popcll(m1 & lt) + 4 * __popcll(m2 & lt) +
+                          8 * __popcll(m3 & lt);
+                const int packed = (int)(rec & 0x3FFFu);
+                for (int i = 0; i < 4; i++) {
+                    const uint32_t di = (dbits >> i) & 1u, bi = (bbits >> i) & 1u;
+                    if (di) s_cand[pos++] = (uint16_t)(packed + i);
+                    if (bi) s_cand[pos++] = (uint16_t)((packed + i) | 0x4000 | (di << 15));
+                }
+                ncand += __popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2) + 8 * __popcll(m3);
+            }
+            for (int i = lane; i < ngrp; i += 64) s_grp[i] = 0u;
             WAVE_SYNC();
             if (ablate == 2) {
                 asm volatile("" ::"v"(ncand));
