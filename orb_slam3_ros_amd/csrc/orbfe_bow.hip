@@ -88,14 +88,7 @@ __global__ __launch_bounds__(1024) void k_bow_assemble(const int* o_word, const 
     SYNC();
     const int m = s_cnt;
     bow_sort_u64(s_a, m);
-    // segment heads: one thread per word sums its features in feature order
-    int nb_local = 0;
-    for (int j = threadIdx.x; j < m; j += blockDim.x) {
-        const uint32_t w = (uint32_t)(s_a[j] >> 32);
-        if (j == 0 || (uint32_t)(s_a[j - 1] >> 32) != w) nb_local++;
-    }
-    SYNC();
-    // ordered compaction of the heads (a simple serial pass: m <= BOW_MAXN)
+    // one entry per word, weights summed in feature order (a serial pass: m <= BOW_MAXN)
     if (threadIdx.x == 0) {
         int nb = 0;
         for (int j = 0; j < m; j++) {
@@ -128,7 +121,6 @@ __global__ __launch_bounds__(1024) void k_bow_assemble(const int* o_word, const 
         }
         counts[0] = nb;
     }
-    (void)nb_local;
     SYNC();
     // FeatureVector: (node, feature) keys of the same features
     if (threadIdx.x == 0) s_cnt = 0;
