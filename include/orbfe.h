@@ -163,6 +163,15 @@ int orbfe_search_by_projection_local(const orbfe_frame* F, int32_t* mvp, const i
                                      const orbfe_map_point* mps, int32_t n_mps, float th, int32_t bFarPoints,
                                      float thFarPoints, float nnratio);
 
+/* Device-resident forms for pipelines that keep frames and map points in HBM: F's keys / desc /
+ * uright / scale_factors, d_mvp, d_mvp_obs and the records are DEVICE pointers written on `stream`
+ * (hipStream_t, NULL = legacy default); the matcher waits for that stream, writes d_mvp in place
+ * and returns nmatches once the results are complete. Semantics are those of the host forms;
+ * records with a scale level outside [0, nlevels) are skipped (the host forms reject them). */
+int orbfe_search_by_projection_local_device(const orbfe_frame* F, int32_t* d_mvp, const int32_t* d_mvp_obs,
+                                            const orbfe_map_point* d_mps, int32_t n_mps, float th,
+                                            int32_t bFarPoints, float thFarPoints, float nnratio, void* stream);
+
 /* One projected point of the last frame for SearchByProjection(CurrentFrame, LastFrame, th, bMono)
  * (ORBmatcher.cc:1676-1887): the caller projects LastFrame.mvpMapPoints[i] with Tcw
  * (x3Dc = Tcw * X, invzc = 1/z, uv = K * x3Dc) and skips outliers / empty slots (valid = 0). */
@@ -257,6 +266,12 @@ int orbfe_is_in_frustum(const orbfe_frame* F, const orbfe_camera* cam, const orb
 int orbfe_search_local_points(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* pts,
                               int32_t n, int32_t* mvp, const int32_t* mvp_obs, float th, int32_t bFarPoints,
                               float thFarPoints, float nnratio, int32_t* n_to_match);
+/* Device-resident Tracking::SearchLocalPoints (see orbfe_search_by_projection_local_device):
+ * d_pts, d_mvp, d_mvp_obs and F's arrays are device pointers; *n_to_match (host) as above. */
+int orbfe_search_local_points_device(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* d_pts,
+                                     int32_t n, int32_t* d_mvp, const int32_t* d_mvp_obs, float th,
+                                     int32_t bFarPoints, float thFarPoints, float nnratio, int32_t* n_to_match,
+                                     void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Back-end matcher pieces (LocalMapping / LoopClosing threads)

@@ -57,6 +57,10 @@ _SIGS = {
     "orbfe_search_for_initialization": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _c_float, _c_int]),
     "orbfe_search_by_bow": (_c_int, [_vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_float, _c_int]),
     "orbfe_copy_stream": (_c_int, [_vp, _vp, ctypes.c_size_t, _vp]),
+    "orbfe_search_by_projection_local_device": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _c_float, _c_int, _c_float,
+                                                         _c_float, _vp]),
+    "orbfe_search_local_points_device": (_c_int, [_vp, _vp, _vp, _c_int, _vp, _vp, _c_float, _c_int, _c_float,
+                                                  _c_float, _vp, _vp]),
     "orbfe_search_by_bow_kf": (_c_int, [_vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _c_float,
                                         _c_int]),
     "orbfe_distinctive_descriptors": (_c_int, [_vp, _vp, _c_int, _vp]),

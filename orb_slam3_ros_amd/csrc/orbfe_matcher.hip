@@ -36,6 +36,7 @@ struct FrameDev {
     const int* pcstart;
     const int* pcidx;
     int gstride_c, gstride_i;
+    int nlevels;            // scale_level / octave of a query must lie in [0, nlevels)
 };
 
 __device__ __forceinline__ int mt_hamming(const uint8_t* a, const uint32_t* b) {
@@ -149,7 +150,8 @@ __global__ __launch_bounds__(MT_NT) void k_sbp_local(FrameDev fr, const orbfe_ma
     const orbfe_map_point& mp = mps[q];
     int result = -1;
     const bool bFactor = th != 1.0f;
-    if ((mp.flags & ORBFE_MP_IN_VIEW) && !(bFar && mp.depth > thFar) && !(mp.flags & ORBFE_MP_BAD)) {
+    if ((mp.flags & ORBFE_MP_IN_VIEW) && !(bFar && mp.depth > thFar) && !(mp.flags & ORBFE_MP_BAD) &&
+        mp.scale_level >= 0 && mp.scale_level < fr.nlevels) {   // level range: host-checked, device-guarded
         const int lvl = mp.scale_level;
         float r = mp.view_cos > 0.998 ? 2.5f : 4.0f;   // RadiusByViewingCos (ORBmatcher.cc:215-221)
         if (bFactor) r *= th;
@@ -223,7 +225,8 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wave(FrameDev fr, const or
     for (int q = blockIdx.x * WPB + wave; q < nq; q += gridDim.x * WPB) {
         const orbfe_map_point& mp = mps[q];
         int result = -1;
-        if ((mp.flags & ORBFE_MP_IN_VIEW) && !(bFar && mp.depth > thFar) && !(mp.flags & ORBFE_MP_BAD)) {
+        if ((mp.flags & ORBFE_MP_IN_VIEW) && !(bFar && mp.depth > thFar) && !(mp.flags & ORBFE_MP_BAD) &&
+            mp.scale_level >= 0 && mp.scale_level < fr.nlevels) {
             const int lvl = mp.scale_level;
             float r = mp.view_cos > 0.998 ? 2.5f : 4.0f;
             if (th != 1.0f) r *= th;
@@ -340,7 +343,7 @@ __global__ __launch_bounds__(MT_NT) void k_sbp_proj(FrameDev fr, const orbfe_pro
     if (q >= nq) return;
     const orbfe_proj_point& p = pts[q];
     int result = -1;
-    bool ok = p.valid != 0;
+    bool ok = p.valid != 0 && p.octave >= 0 && p.octave < fr.nlevels;
     if (ok && mode == 0) {
         if (p.invzc < 0) ok = false;
         else if (p.u < fr.minx || p.u > fr.maxx) ok = false;
@@ -839,18 +842,26 @@ struct FramePlan {
         cstart = p.scratch((size_t)grids * (MT_NCELL + 1) * 4);
         cidx = p.scratch((size_t)grids * std::max(F->n, 1) * 4);
     }
+    // device-resident frame: F's arrays are already device pointers (no upload)
+    bool dev = false;
+    void plan_dev(const orbfe_frame* f, bool want_uright) {
+        F = f;
+        dev = true;
+        has_uright = want_uright && f->uright != nullptr;
+    }
     FrameDev view() const {
         FrameDev v;
         v.n = F->n;
-        v.keys = ms_ptr<const OrbKeyPoint>(keys);
-        v.desc = ms_ptr<const uint32_t>(desc);
-        v.uright = has_uright ? ms_ptr<const float>(uright) : nullptr;
+        v.keys = dev ? (const OrbKeyPoint*)F->keys : ms_ptr<const OrbKeyPoint>(keys);
+        v.desc = dev ? (const uint32_t*)F->desc : ms_ptr<const uint32_t>(desc);
+        v.uright = has_uright ? (dev ? F->uright : ms_ptr<const float>(uright)) : nullptr;
         v.minx = F->min_x; v.maxx = F->max_x; v.miny = F->min_y; v.maxy = F->max_y;
         // mfGridElementWidthInv / HeightInv (Frame.cc:163-164)
         v.invw = static_cast<float>(ORBFE_GRID_COLS) / (F->max_x - F->min_x);
         v.invh = static_cast<float>(ORBFE_GRID_ROWS) / (F->max_y - F->min_y);
         v.mbf = F->mbf;
-        v.scale = ms_ptr<const float>(scale);
+        v.nlevels = F->nlevels;
+        v.scale = dev ? F->scale_factors : ms_ptr<const float>(scale);
         v.cstart = ms_ptr<const int>(cstart);
         v.cidx = ms_ptr<const int>(cidx);
         v.gstride_c = MT_NCELL + 1;
@@ -886,9 +897,21 @@ struct FrustumIn {
     int32_t* n_to_match;
 };
 
+// Device-resident call (the *_device entry points): F's arrays, mvp, mvp_obs and the query
+// records are device pointers produced on `caller`; the matcher's stream waits for it, results
+// are written in place and the call returns after they are complete.
+struct DevIn {
+    hipStream_t caller;
+};
+
+__global__ void k_blocked0(const int32_t* mvp, const int32_t* obs, int n, int any_slot, int* out) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) out[k] = any_slot ? (mvp[k] >= 0) : (mvp[k] >= 0 && obs[k] > 0);
+}
+
 int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, const void* queries, int nq,
             size_t qstride, size_t qobs_off, size_t qid_off, size_t qangle_off, size_t qlevel_off, float th, int a0, int a1, float thFar,
-            float nnratio, int maxDist, int checkOri, const FrustumIn* fin = nullptr) {
+            float nnratio, int maxDist, int checkOri, const FrustumIn* fin = nullptr, const DevIn* dev = nullptr) {
     if (!frame_ok(F) || !mvp || nq < 0 || (nq > 0 && !queries && !fin)) return ORBFE_E_ARG;
     if (fin && (!fin->cam || (nq > 0 && !fin->pts) || mode != 0)) return ORBFE_E_ARG;
     if (mode != 2 && !mvp_obs) return ORBFE_E_ARG;
@@ -897,23 +920,26 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     if (nq > (1 << 24)) return ORBFE_E_CAPACITY;
     const int n = F->n;
     // level indices address mvScaleFactors: reject out-of-range ones instead of reading past it
-    // (frustum-produced levels are clamped to [0, nlevels) by PredictScale)
-    for (int j = 0; !fin && j < nq; j++) {
+    // (frustum-produced levels are clamped to [0, nlevels) by PredictScale; device-resident
+    // records are not visible to the host: the kernels skip out-of-range levels instead)
+    for (int j = 0; !fin && !dev && j < nq; j++) {
         const uint8_t* rec = (const uint8_t*)queries + (size_t)j * qstride;
         const bool used = mode == 0 ? (((const orbfe_map_point*)rec)->flags & ORBFE_MP_IN_VIEW) != 0
                                     : ((const orbfe_proj_point*)rec)->valid != 0;
         const int lvl = *(const int32_t*)(rec + qlevel_off);
         if (used && (lvl < 0 || lvl >= F->nlevels)) return ORBFE_E_ARG;
     }
-    std::vector<int32_t> blocked0(n);
-    for (int k = 0; k < n; k++) blocked0[k] = mode == 2 ? (mvp[k] >= 0) : (mvp[k] >= 0 && mvp_obs[k] > 0);
+    std::vector<int32_t> blocked0(dev ? 0 : n);
+    for (int k = 0; !dev && k < n; k++) blocked0[k] = mode == 2 ? (mvp[k] >= 0) : (mvp[k] >= 0 && mvp_obs[k] > 0);
     Plan p;
     FramePlan fp;
-    fp.plan(p, F, true, mode != 2);
-    const size_t o_q = fin ? p.upload(fin->pts, (size_t)nq * sizeof(orbfe_map_point_3d))
-                           : p.upload(queries, (size_t)nq * qstride);
-    const size_t o_b0 = p.upload(blocked0.data(), (size_t)n * 4);
-    const size_t o_mvp = p.upload(mvp, (size_t)n * 4);
+    if (dev) fp.plan_dev(F, mode != 2);
+    else fp.plan(p, F, true, mode != 2);
+    const size_t o_q = dev ? 0 : fin ? p.upload(fin->pts, (size_t)nq * sizeof(orbfe_map_point_3d))
+                                     : p.upload(queries, (size_t)nq * qstride);
+    const size_t o_b0 = dev ? 0 : p.upload(blocked0.data(), (size_t)n * 4);
+    const size_t o_mvp = dev ? 0 : p.upload(mvp, (size_t)n * 4);
+    const size_t o_b0d = dev ? p.scratch((size_t)n * 4) : 0;
     fp.plan_grid(p, mode == 0 ? F->nlevels + 1 : 1);
     const size_t o_track = fin ? p.scratch((size_t)nq * sizeof(orbfe_map_point)) : 0;
     const size_t o_ntm = fin ? p.scratch(16) : 0;
@@ -923,16 +949,27 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     const size_t o_result = p.scratch((size_t)(n + 2) * 4);
     int rc = ms_prepare(p);
     if (rc) return rc;
-    MsTimer timer;
     hipStream_t s = t_ms.stream;
+    if (dev) {   // order after the producer of the device inputs
+        static thread_local hipEvent_t ev = nullptr;
+        if (!ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(ev, dev->caller));
+        HIPCHK(hipStreamWaitEvent(s, ev, 0));
+    }
+    MsTimer timer;
     const FrameDev fr = fp.view();
     fp.launch_grid(fr);
+    const int* b0 = dev ? ms_ptr<const int>(o_b0d) : ms_ptr<const int>(o_b0);
+    if (dev)
+        hipLaunchKernelGGL(k_blocked0, dim3((n + 255) / 256), dim3(256), 0, s, mvp, mvp_obs, n, mode == 2 ? 1 : 0,
+                           ms_ptr<int>(o_b0d));
+    int32_t* mvp_d = dev ? mvp : ms_ptr<int32_t>(o_mvp);
     int* first = ms_ptr<int>(o_first);
     int* assign = ms_ptr<int>(o_assign);
     int* changed = ms_ptr<int>(o_changed);
     HIPCHK(hipMemsetAsync(changed, 0, MT_MAX_PASSES * 4, s));
     fill(assign, nq, -1);
-    const uint8_t* q = ms_ptr<const uint8_t>(o_q);
+    const uint8_t* q = dev ? (const uint8_t*)(fin ? (const void*)fin->pts : queries) : ms_ptr<const uint8_t>(o_q);
     if (fin) {   // Tracking::SearchLocalPoints: project, count nToMatch, match only if > 0
         const orbfe_camera& c = *fin->cam;
         CamDev cd;
@@ -948,7 +985,7 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
         int* ntm = ms_ptr<int>(o_ntm);
         HIPCHK(hipMemsetAsync(ntm, 0, 4, s));
         hipLaunchKernelGGL(k_frustum, dim3((nq + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, cd,
-                           ms_ptr<const orbfe_map_point_3d>(o_q), nq, ms_ptr<orbfe_map_point>(o_track), ntm);
+                           (const orbfe_map_point_3d*)q, nq, ms_ptr<orbfe_map_point>(o_track), ntm);
         int h_ntm = 0;
         HIPCHK(hipMemcpyAsync(&h_ntm, ntm, 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
@@ -971,17 +1008,16 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
                 const size_t lds = (MT_WNT / 64) * 64 * sizeof(int2) + (staged ? (size_t)n * 48 : 0);
                 if (staged)
                     hipLaunchKernelGGL(k_sbp_local_wave<true>, dim3(nb), dim3(MT_WNT), lds, s, fr, (const orbfe_map_point*)q,
-                                       nq, th, a0, thFar, nnratio, ms_ptr<const int>(o_b0), first, assign, changed + pass);
+                                       nq, th, a0, thFar, nnratio, b0, first, assign, changed + pass);
                 else
                     hipLaunchKernelGGL(k_sbp_local_wave<false>, dim3(nb), dim3(MT_WNT), lds, s, fr, (const orbfe_map_point*)q,
-                                       nq, th, a0, thFar, nnratio, ms_ptr<const int>(o_b0), first, assign, changed + pass);
+                                       nq, th, a0, thFar, nnratio, b0, first, assign, changed + pass);
             } else if (mode == 0)
                 hipLaunchKernelGGL(k_sbp_local, gq, dim3(MT_NT), 0, s, fr, (const orbfe_map_point*)q, nq, th, a0, thFar,
-                                   nnratio, ms_ptr<const int>(o_b0), first, assign, changed + pass);
+                                   nnratio, b0, first, assign, changed + pass);
             else
                 hipLaunchKernelGGL(k_sbp_proj, gq, dim3(MT_NT), 0, s, fr, (const orbfe_proj_point*)q, nq, th,
-                                   mode == 1 ? 0 : 1, a0, a1, maxDist, ms_ptr<const int>(o_b0), first, assign,
-                                   changed + pass);
+                                   mode == 1 ? 0 : 1, a0, a1, maxDist, b0, first, assign, changed + pass);
         }
         int ch = 0;
         HIPCHK(hipMemcpyAsync(&ch, changed + pass - 1, 4, hipMemcpyDeviceToHost, s));
@@ -991,11 +1027,11 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     int* result = ms_ptr<int>(o_result);
     fill(result, n + 2, -1);
     hipLaunchKernelGGL(k_mt_commit_slots, dim3(1), dim3(1024), 0, s, fr.keys, n, assign, (const int*)(q + qid_off),
-                       (const float*)(q + qangle_off), (int)qstride, nq, checkOri, ms_ptr<int>(o_mvp), result);
+                       (const float*)(q + qangle_off), (int)qstride, nq, checkOri, mvp_d, result);
     HIPCHK(hipGetLastError());
     timer.end();
     int nm = 0;
-    HIPCHK(hipMemcpyAsync(mvp, ms_ptr<int>(o_mvp), (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    if (!dev) HIPCHK(hipMemcpyAsync(mvp, mvp_d, (size_t)n * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(&nm, result, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     return nm;
@@ -1194,6 +1230,26 @@ int orbfe_search_local_points(const orbfe_frame* F, const orbfe_camera* cam, con
     return sbp_run(0, F, mvp, mvp_obs, nullptr, n, sizeof(orbfe_map_point), offsetof(orbfe_map_point, observations),
                    offsetof(orbfe_map_point, id), 0, offsetof(orbfe_map_point, scale_level), th, bFarPoints, 0,
                    thFarPoints, nnratio, 0, 0, &fin);
+}
+
+int orbfe_search_by_projection_local_device(const orbfe_frame* F, int32_t* d_mvp, const int32_t* d_mvp_obs,
+                                            const orbfe_map_point* d_mps, int32_t n_mps, float th,
+                                            int32_t bFarPoints, float thFarPoints, float nnratio, void* stream) {
+    const DevIn dv{(hipStream_t)stream};
+    return sbp_run(0, F, d_mvp, d_mvp_obs, d_mps, n_mps, sizeof(orbfe_map_point), offsetof(orbfe_map_point, observations),
+                   offsetof(orbfe_map_point, id), 0, offsetof(orbfe_map_point, scale_level), th, bFarPoints, 0,
+                   thFarPoints, nnratio, 0, 0, nullptr, &dv);
+}
+
+int orbfe_search_local_points_device(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* d_pts,
+                                     int32_t n, int32_t* d_mvp, const int32_t* d_mvp_obs, float th,
+                                     int32_t bFarPoints, float thFarPoints, float nnratio, int32_t* n_to_match,
+                                     void* stream) {
+    const FrustumIn fin{cam, d_pts, n_to_match};
+    const DevIn dv{(hipStream_t)stream};
+    return sbp_run(0, F, d_mvp, d_mvp_obs, nullptr, n, sizeof(orbfe_map_point), offsetof(orbfe_map_point, observations),
+                   offsetof(orbfe_map_point, id), 0, offsetof(orbfe_map_point, scale_level), th, bFarPoints, 0,
+                   thFarPoints, nnratio, 0, 0, &fin, &dv);
 }
 
 int orbfe_is_in_frustum(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* pts, int32_t n,

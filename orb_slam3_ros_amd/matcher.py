@@ -392,6 +392,75 @@ class ORBmatcher:
             "SearchBySim3")
 
 
+class DeviceMatchFrame:
+    """A MatchFrame whose arrays live in HBM (torch CUDA tensors): the frame argument of the
+    *_device entry points. The host struct carries the device pointers."""
+
+    def __init__(self, F: MatchFrame, device):
+        import torch
+        self.N = F.N
+        self.bounds = F.bounds
+        self.keys = torch.from_numpy(np.ascontiguousarray(F.keys).view(np.uint8).reshape(-1).copy()).to(device)
+        self.desc = torch.from_numpy(F.desc.copy()).to(device)
+        self.uright = None if F.uright is None else torch.from_numpy(F.uright.copy()).to(device)
+        self.scale_factors = torch.from_numpy(F.scale_factors.copy()).to(device)
+        self.c = CFrame(F.N, self.keys.data_ptr(), self.desc.data_ptr(),
+                        self.uright.data_ptr() if self.uright is not None else None, *F.bounds,
+                        len(F.scale_factors), self.scale_factors.data_ptr(), F.mbf)
+
+    def ref(self):
+        return ctypes.byref(self.c)
+
+
+def _dev_i32(t, n, what):
+    import torch
+    if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.int32 and t.is_contiguous() and
+            t.numel() == n):
+        raise ValueError(f"{what} must be a contiguous CUDA int32 tensor of length {n}")
+    return t
+
+
+def _dev_records(t, itemsize, what):
+    import torch
+    if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.uint8 and t.is_contiguous() and
+            t.numel() % itemsize == 0):
+        raise ValueError(f"{what} must be a contiguous CUDA uint8 tensor of {itemsize}-byte records")
+    return t.numel() // itemsize
+
+
+def search_by_projection_local_device(F: DeviceMatchFrame, mvp, mvp_obs, mps, th=3.0, bFarPoints=False,
+                                      thFarPoints=50.0, nnratio=0.8):
+    """SearchByProjection(F, vpMapPoints, th, bFar, thFar) on device-resident data: mvp / mvp_obs
+    CUDA int32 [F.N] (mvp updated in place), mps a CUDA uint8 tensor of MAP_POINT_DTYPE records.
+    Enqueued after the current torch stream's work. Returns nmatches."""
+    import torch
+    lib = _lib.load()
+    n = _dev_records(mps, MAP_POINT_DTYPE.itemsize, "mps")
+    _dev_i32(mvp, F.N, "mvp")
+    _dev_i32(mvp_obs, F.N, "mvp_obs")
+    st = torch.cuda.current_stream(mvp.device).cuda_stream
+    return _lib.check(lib.orbfe_search_by_projection_local_device(
+        F.ref(), mvp.data_ptr(), mvp_obs.data_ptr(), mps.data_ptr(), n, float(th), int(bFarPoints),
+        float(thFarPoints), float(nnratio), st), "search_by_projection_local_device")
+
+
+def search_local_points_device(F: DeviceMatchFrame, cam: Camera, points3d, mvp, mvp_obs, th=1.0, bFarPoints=False,
+                               thFarPoints=50.0, nnratio=0.8):
+    """Tracking::SearchLocalPoints on device-resident data (points3d: CUDA uint8 tensor of
+    MAP_POINT_3D_DTYPE records). Returns (nmatches, nToMatch)."""
+    import torch
+    lib = _lib.load()
+    n = _dev_records(points3d, MAP_POINT_3D_DTYPE.itemsize, "points3d")
+    _dev_i32(mvp, F.N, "mvp")
+    _dev_i32(mvp_obs, F.N, "mvp_obs")
+    ntm = ctypes.c_int32(0)
+    st = torch.cuda.current_stream(mvp.device).cuda_stream
+    nm = _lib.check(lib.orbfe_search_local_points_device(
+        F.ref(), ctypes.byref(cam), points3d.data_ptr(), n, mvp.data_ptr(), mvp_obs.data_ptr(), float(th),
+        int(bFarPoints), float(thFarPoints), float(nnratio), ctypes.byref(ntm), st), "search_local_points_device")
+    return nm, int(ntm.value)
+
+
 def compute_distinctive_descriptors(descriptor_sets):
     """MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:329-403) for many points at once on the
     GPU. descriptor_sets: a list of (N_i, 32) uint8 arrays (the descriptors of each point's

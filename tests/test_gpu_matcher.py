@@ -262,3 +262,39 @@ def test_search_local_points(gpu, om, th, seed):
     no, to = om.search_local_points(F, cam, pts, b, obs, th)
     assert (ng, tg) == (no, to) and no > 0
     np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("th", [1, 3, 15])
+def test_sbp_local_device_resident(gpu, om, th):
+    """orbfe_search_by_projection_local_device (records, slots and frame in HBM) == the oracle."""
+    import torch
+    from orb_slam3_ros_amd.matcher import DeviceMatchFrame, search_by_projection_local_device
+    F, mps, mvp0, obs = _local_case(777, 1000, 50_000)
+    Fd = DeviceMatchFrame(F, gpu)
+    mvp_t = torch.from_numpy(mvp0.copy()).to(gpu)
+    obs_t = torch.from_numpy(obs.copy()).to(gpu)
+    mps_t = torch.from_numpy(mps.view(np.uint8).reshape(-1).copy()).to(gpu)
+    ng = search_by_projection_local_device(Fd, mvp_t, obs_t, mps_t, th)
+    mvp_o = mvp0.copy()
+    no = om.OracleMatcher(0.8).sbp_local(F, mvp_o, obs, mps, th)
+    assert ng == no and no > 0
+    np.testing.assert_array_equal(mvp_t.cpu().numpy(), mvp_o)
+
+
+def test_search_local_points_device_resident(gpu, om):
+    import torch
+    from orb_slam3_ros_amd.matcher import DeviceMatchFrame, search_local_points_device
+    rng = np.random.default_rng(31)
+    F = sm.synth_frame(rng, 1000)
+    cam = sm.synth_camera(rng)
+    pts = sm.synth_local_map_3d(rng, F, cam, 20000)
+    mvp0, obs = sm.initial_slots(rng, F.N, 0.1)
+    Fd = DeviceMatchFrame(F, gpu)
+    mvp_t = torch.from_numpy(mvp0.copy()).to(gpu)
+    obs_t = torch.from_numpy(obs.copy()).to(gpu)
+    pts_t = torch.from_numpy(pts.view(np.uint8).reshape(-1).copy()).to(gpu)
+    ng, ntm_g = search_local_points_device(Fd, cam, pts_t, mvp_t, obs_t, 1.0)
+    mvp_o = mvp0.copy()
+    no, ntm_o = om.search_local_points(F, cam, pts, mvp_o, obs, 1.0)
+    assert (ng, ntm_g) == (no, ntm_o) and no > 0
+    np.testing.assert_array_equal(mvp_t.cpu().numpy(), mvp_o)
