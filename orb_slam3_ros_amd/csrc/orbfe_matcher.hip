@@ -470,54 +470,55 @@ __device__ __forceinline__ unsigned mt_three_maxima_keep(const int* hist) {
 // Final write-back for slot-assigning searches: slot k gets the LAST query that chose it; with
 // checkOri, every entry of a dropped bin clears its slot and decrements nmatches
 // (ORBmatcher.cc:1860-1884). q_angle: the query-side angle per query; frame angle from keys.
-__global__ __launch_bounds__(1024) void k_mt_commit_slots(const OrbKeyPoint* keys, int n, const int* assign,
-                                                          const int* qid, const float* q_angle, int q_stride_bytes,
-                                                          int nq, int checkOri, int* mvp, int* result) {
+// Three grid-wide steps over the queries / slots (result[0] = assigned count, result[1] = dropped
+// count, result[2 + k] = last assigner of slot k or -2 when cleared, hist[30] = rotation bins):
+// K1 counts, bins and takes the last assigner; K2 (checkOri only) clears the slots of entries in
+// dropped bins; K3 writes the slots.
+__global__ __launch_bounds__(MT_NT) void k_mt_commit_count(const OrbKeyPoint* keys, const int* assign,
+                                                           const float* q_angle, int q_stride_bytes, int nq,
+                                                           int checkOri, int* result, int* hist) {
     __shared__ int s_hist[MT_HISTO];
-    __shared__ unsigned s_keep;
-    __shared__ int s_n;
     if (threadIdx.x < MT_HISTO) s_hist[threadIdx.x] = 0;
-    if (threadIdx.x == 0) s_n = 0;
     SYNC();
-    int cnt = 0;
-    for (int j = threadIdx.x; j < nq; j += blockDim.x) {
-        const int a = assign[j];
-        if (a < 0) continue;
-        cnt++;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int a = j < nq ? assign[j] : -1;
+    if (a >= 0) {
+        atomicMax(&result[2 + a], j);
         if (checkOri) {
             const float qa = *(const float*)((const uint8_t*)q_angle + (size_t)j * q_stride_bytes);
             atomicAdd(&s_hist[mt_rot_bin(qa, keys[a].angle)], 1);
         }
     }
-    atomicAdd(&s_n, cnt);
+    const unsigned long long m = __ballot(a >= 0);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&result[0], __popcll(m));
     SYNC();
-    if (threadIdx.x == 0) s_keep = checkOri ? mt_three_maxima_keep(s_hist) : 0xFFFFFFFFu;
+    if (checkOri && threadIdx.x < MT_HISTO && s_hist[threadIdx.x]) atomicAdd(&hist[threadIdx.x], s_hist[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(MT_NT) void k_mt_commit_drop(const OrbKeyPoint* keys, const int* assign,
+                                                          const float* q_angle, int q_stride_bytes, int nq,
+                                                          const int* hist, int* result) {
+    __shared__ unsigned s_keep;
+    if (threadIdx.x == 0) s_keep = mt_three_maxima_keep(hist);
     SYNC();
-    // last assigner per slot: sequential order = query index; the largest j wins
-    for (int j = threadIdx.x; j < nq; j += blockDim.x) {
-        const int a = assign[j];
-        if (a >= 0) atomicMax(&result[2 + a], j);
-    }
-    SYNC();
-    int dropped = 0;
-    for (int j = threadIdx.x; j < nq; j += blockDim.x) {
-        const int a = assign[j];
-        if (a < 0 || !checkOri) continue;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int a = j < nq ? assign[j] : -1;
+    bool drop = false;
+    if (a >= 0) {
         const float qa = *(const float*)((const uint8_t*)q_angle + (size_t)j * q_stride_bytes);
-        if (!((s_keep >> mt_rot_bin(qa, keys[a].angle)) & 1u)) {
-            dropped++;
-            result[2 + a] = -2;   // cleared slot marker (cannot race with a winner write: written after SYNC)
-        }
+        drop = !((s_keep >> mt_rot_bin(qa, keys[a].angle)) & 1u);
+        if (drop) result[2 + a] = -2;   // K1 finished before this kernel: no race with the winner write
     }
-    SYNC();
-    atomicAdd(&s_n, -dropped);
-    SYNC();
-    for (int k = threadIdx.x; k < n; k += blockDim.x) {
-        const int w = result[2 + k];
-        if (w == -2) mvp[k] = -1;
-        else if (w >= 0) mvp[k] = *(const int*)((const uint8_t*)qid + (size_t)w * q_stride_bytes);
-    }
-    if (threadIdx.x == 0) result[0] = s_n;
+    const unsigned long long m = __ballot(drop);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&result[1], __popcll(m));
+}
+
+__global__ void k_mt_commit_write(int n, const int* qid, int q_stride_bytes, const int* result, int* mvp) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const int w = result[2 + k];
+    if (w == -2) mvp[k] = -1;
+    else if (w >= 0) mvp[k] = *(const int*)((const uint8_t*)qid + (size_t)w * q_stride_bytes);
 }
 
 // ---- SearchForInitialization (ORBmatcher.cc:648-763) ----
@@ -947,6 +948,7 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     const size_t o_assign = p.scratch((size_t)nq * 4);
     const size_t o_changed = p.scratch(MT_MAX_PASSES * 4);
     const size_t o_result = p.scratch((size_t)(n + 2) * 4);
+    const size_t o_hist = p.scratch(MT_HISTO * 4);
     int rc = ms_prepare(p);
     if (rc) return rc;
     hipStream_t s = t_ms.stream;
@@ -1026,15 +1028,23 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     }
     int* result = ms_ptr<int>(o_result);
     fill(result, n + 2, -1);
-    hipLaunchKernelGGL(k_mt_commit_slots, dim3(1), dim3(1024), 0, s, fr.keys, n, assign, (const int*)(q + qid_off),
-                       (const float*)(q + qangle_off), (int)qstride, nq, checkOri, mvp_d, result);
+    int* hist = ms_ptr<int>(o_hist);
+    HIPCHK(hipMemsetAsync(hist, 0, MT_HISTO * 4, s));
+    HIPCHK(hipMemsetAsync(result, 0, 8, s));
+    hipLaunchKernelGGL(k_mt_commit_count, gq, dim3(MT_NT), 0, s, fr.keys, assign, (const float*)(q + qangle_off),
+                       (int)qstride, nq, checkOri, result, hist);
+    if (checkOri)
+        hipLaunchKernelGGL(k_mt_commit_drop, gq, dim3(MT_NT), 0, s, fr.keys, assign, (const float*)(q + qangle_off),
+                           (int)qstride, nq, hist, result);
+    hipLaunchKernelGGL(k_mt_commit_write, dim3((n + 255) / 256), dim3(256), 0, s, n, (const int*)(q + qid_off),
+                       (int)qstride, result, mvp_d);
     HIPCHK(hipGetLastError());
     timer.end();
-    int nm = 0;
+    int cnt[2] = {0, 0};
     if (!dev) HIPCHK(hipMemcpyAsync(mvp, mvp_d, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&nm, result, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(cnt, result, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    return nm;
+    return cnt[0] - cnt[1];
 }
 
 }  // namespace
