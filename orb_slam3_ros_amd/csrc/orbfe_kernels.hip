@@ -1327,25 +1327,23 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
     // rounding, so this equals blurring the whole level. ----
     const uint32_t k0 = bk.k[0], k1 = bk.k[1], k2 = bk.k[2], k3 = bk.k[3];
     {
-        const orbfe_ushort2 K0 = {(unsigned short)k0, (unsigned short)k0}, K1 = {(unsigned short)k1, (unsigned short)k1};
-        const orbfe_ushort2 K2 = {(unsigned short)k2, (unsigned short)k2}, K3 = {(unsigned short)k3, (unsigned short)k3};
+        // output j of a 4-column group = taps 0-3 . (k0 k1 k2 k3) + taps 4-6 . (k2 k1 k0 0), each a
+        // v_dot4_u32_u8 over a byte-aligned window of the 12-byte run w0 w1 w2 (exact: <= 65280)
+        const uint32_t KLO = k0 | (k1 << 8) | (k2 << 16) | (k3 << 24), KHI = k2 | (k1 << 8) | (k0 << 16);
         for (int it = lane; it < DP_N * 10; it += 64) {   // 43 rows x 10 groups of 4 output columns
             const int r = it / 10, gq = it - r * 10;
             const uint32_t* rp = (const uint32_t*)(raw + r * DP_RAW_S) + gq;
             const uint32_t w0 = rp[0], w1 = rp[1], w2 = rp[2];
-            // P[j] = (byte j, byte j + 1) of the 12-byte run w0 w1 w2, as u16x2
-            orbfe_ushort2 P[10];
+            uint32_t h[4];
 #pragma unroll
-            for (int j = 0; j < 10; j++) {
-                const uint32_t sel = j < 4 ? (0x0c000c00u | ((uint32_t)(j + 1) << 16) | (uint32_t)j)
-                                           : (0x0c000c00u | ((uint32_t)(j - 3) << 16) | (uint32_t)(j - 4));
-                P[j] = as_us2(j < 4 ? __builtin_amdgcn_perm(w1, w0, sel) : __builtin_amdgcn_perm(w2, w1, sel));
+            for (int j = 0; j < 4; j++) {
+                const uint32_t lo = j ? __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)j) : w0;
+                const uint32_t hi = j ? __builtin_amdgcn_alignbyte(w2, w1, (uint32_t)j) : w1;
+                h[j] = __builtin_amdgcn_udot4(hi, KHI, __builtin_amdgcn_udot4(lo, KLO, 0u, false), false);
             }
-            const orbfe_ushort2 h01 = K0 * (P[0] + P[6]) + K1 * (P[1] + P[5]) + K2 * (P[2] + P[4]) + K3 * P[3];
-            const orbfe_ushort2 h23 = K0 * (P[2] + P[8]) + K1 * (P[3] + P[7]) + K2 * (P[4] + P[6]) + K3 * P[5];
             uint2 pk;
-            pk.x = __builtin_bit_cast(uint32_t, h01);
-            pk.y = __builtin_bit_cast(uint32_t, h23);
+            pk.x = h[0] | (h[1] << 16);
+            pk.y = h[2] | (h[3] << 16);
             *(uint2*)(rowq + r * DP_Q_S + 4 * gq) = pk;
         }
     }
