@@ -1349,10 +1349,13 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
     }
     WAVE_SYNC();
     // blurred(18 + dy, 18 + dx): column pass over rowq rows 18 + dy .. 24 + dy
+    // (24-bit multiplies are exact here: pair sums <= 2 * 65280, taps <= 256)
     auto blurred = [&](int dy, int dx) -> int {
-        const uint16_t* col = rowq + (18 + dy) * DP_Q_S + 18 + dx;
-        const uint32_t sum = k0 * ((uint32_t)col[0] + col[6 * DP_Q_S]) + k1 * ((uint32_t)col[DP_Q_S] + col[5 * DP_Q_S]) +
-                             k2 * ((uint32_t)col[2 * DP_Q_S] + col[4 * DP_Q_S]) + k3 * (uint32_t)col[3 * DP_Q_S];
+        const uint16_t* col = rowq + __mul24(18 + dy, DP_Q_S) + 18 + dx;
+        const uint32_t sum = __umul24(k0, (uint32_t)col[0] + col[6 * DP_Q_S]) +
+                             __umul24(k1, (uint32_t)col[DP_Q_S] + col[5 * DP_Q_S]) +
+                             __umul24(k2, (uint32_t)col[2 * DP_Q_S] + col[4 * DP_Q_S]) +
+                             __umul24(k3, (uint32_t)col[3 * DP_Q_S]);
         const uint32_t v = (sum + 32768u) >> 16;
         return (int)(v > 255u ? 255u : v);
     };
