@@ -186,9 +186,13 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t* const* imgs, int 
     SYNC();
     // (B) horizontal pass
     if (hr0 < hstep) {
+        // beyond xmax the reference takes S[sx] * 2048: a0 = 2048, a1 = 0 gives it branch-free (the
+        // byte at sx + 1 is inside the LDS window and multiplied by 0); 24-bit multiplies are exact
+        // (coefficients <= 2048). A plain loop: unrolling it measured slower.
+        const uint32_t a0 = hlin ? (uint32_t)ha0 : 2048u, a1 = hlin ? (uint32_t)ha1 : 0u;
         for (int r = hr0; r < nsr; r += hstep) {
-            const int p0 = s_src[r][hsx];
-            s_h[r][hx] = hlin ? p0 * ha0 + s_src[r][hsx + 1] * ha1 : p0 * 2048;
+            const uint32_t p0 = s_src[r][hsx], p1 = s_src[r][hsx + 1];
+            s_h[r][hx] = (int)(__umul24(p0, a0) + __umul24(p1, a1));
         }
     }
     SYNC();
