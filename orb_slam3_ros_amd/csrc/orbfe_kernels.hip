@@ -1555,24 +1555,44 @@ __global__ __launch_bounds__(ST_NT) void k_stereo(OrbGeom g, StereoSide SL, Ster
                 gptr_u8 IL = level_base(SL.imgs, SL.in_pitch, SL.pyr, SL.pyr_stride, g, bL, levelL, &pL);
                 gptr_u8 IR = level_base(SR.imgs, SR.in_pitch, SR.pyr, SR.pyr_stride, g, bR, levelL, &pR);
                 const int r0 = (int)(scaledvL - w), c0L = (int)(scaleduL - w), c0R = (int)(scaleduR0 - Lr - w);
-                // stage IL 11x11 and IR 11x21 windows
-                for (int i = lane; i < 121 + 231; i += 64) {
-                    if (i < 121) {
-                        const int yy = i / 11, xx = i - yy * 11;
-                        s_win[i] = IL[(size_t)(r0 + yy) * pL + c0L + xx];
+                // stage the IL 11x11 and IR 11x21 windows as dword rows (IL: 3 dwords, byte 11
+                // zeroed; IR: 6 dwords): lanes 0-10 load a left row, 11-21 a right row with aligned
+                // dword loads (the windows lie >= 6 px inside the level, so the <= 3-byte over-reads
+                // stay inside the image) realigned by v_alignbyte
+                uint32_t* s_wl = (uint32_t*)s_win;          // [11][3]
+                uint32_t* s_wr = (uint32_t*)s_win + 33;     // [11][6]
+                if (lane < 22) {
+                    const bool left = lane < 11;
+                    const int yy = left ? lane : lane - 11;
+                    gptr_u8 rp = left ? IL + (size_t)(r0 + yy) * pL + c0L : IR + (size_t)(r0 + yy) * pR + c0R;
+                    const uint32_t sh = (uint32_t)((uintptr_t)rp & 3);
+                    gptr_u32 ap = (gptr_u32)(rp - sh);
+                    uint32_t w[7];
+#pragma unroll
+                    for (int k = 0; k < 7; k++) w[k] = (left && k >= 4) ? 0u : ap[k];
+                    if (left) {
+#pragma unroll
+                        for (int k = 0; k < 3; k++) {
+                            uint32_t o = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+                            if (k == 2) o &= 0x00FFFFFFu;
+                            s_wl[yy * 3 + k] = o;
+                        }
                     } else {
-                        const int j = i - 121, yy = j / 21, xx = j - yy * 21;
-                        s_win[128 + j] = IR[(size_t)(r0 + yy) * pR + c0R + xx];
+#pragma unroll
+                        for (int k = 0; k < 6; k++) s_wr[yy * 6 + k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
                     }
                 }
-                // lanes: (shift inc, window row) pairs -> row SAD over 11 columns
+                // lanes: (shift inc, window row) pairs -> row SAD over 11 columns, 3 v_sad_u8
                 for (int pidx = lane; pidx < 121; pidx += 64) {
                     const int inc = pidx / 11, yy = pidx - inc * 11;
-                    int sad = 0;
-#pragma unroll
-                    for (int xx = 0; xx < 11; xx++)
-                        sad += abs((int)s_win[yy * 11 + xx] - (int)s_win[128 + yy * 21 + inc + xx]);
-                    s_part[pidx] = sad;
+                    const uint32_t* rr = s_wr + yy * 6 + (inc >> 2);
+                    const uint32_t ish = (uint32_t)(inc & 3);
+                    const uint32_t r0w = __builtin_amdgcn_alignbyte(rr[1], rr[0], ish);
+                    const uint32_t r1w = __builtin_amdgcn_alignbyte(rr[2], rr[1], ish);
+                    const uint32_t r2w = __builtin_amdgcn_alignbyte(rr[3], rr[2], ish) & 0x00FFFFFFu;
+                    const uint32_t* ll = s_wl + yy * 3;
+                    s_part[pidx] = (int)__builtin_amdgcn_sad_u8(
+                        ll[2], r2w, __builtin_amdgcn_sad_u8(ll[1], r1w, __builtin_amdgcn_sad_u8(ll[0], r0w, 0u)));
                 }
                 int dsum = 0;
                 if (lane < 11)
