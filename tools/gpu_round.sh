@@ -15,3 +15,9 @@ for grp in "FETCH_SIZE" "WRITE_SIZE"; do
   timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d gpurun_out/pmc/p$i -o run -- $CMD > gpurun_out/pmc/p$i.log 2>&1 || { tail -20 gpurun_out/pmc/p$i.log; exit 1; }
 done
 find gpurun_out/prof gpurun_out/pmc -name "*.csv" | head -20
+mkdir -p gpurun_out/pmcc
+i=0
+for grp in "TCC_HIT_sum TCC_MISS_sum" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d gpurun_out/pmcc/c$i -o run -- $CMD > gpurun_out/pmcc/c$i.log 2>&1 || { tail -20 gpurun_out/pmcc/c$i.log; exit 1; }
+done
