@@ -73,8 +73,7 @@ struct orbfe_extractor {
     int W = 0, H = 0, cap_b = 0;
     OrbGeom g{};
     std::vector<int16_t> tab;
-    int roi_max = 0;
-    int cand_bytes = 0;   // k_fast entry list per wave: 2 u16 entries per detection pixel
+    FastLds fast_lds{};   // k_fast per-wave LDS layout (max over levels)
     size_t oct_lds = 0;
     // device buffers
     int16_t* d_tab = nullptr;
@@ -145,7 +144,8 @@ static int build_geom(orbfe_extractor* h, int W, int H) {
     g.min_th = std::min(std::max(h->min_th, 0), 255);
     h->tab.clear();
     int cell_base = 0, cellkey_off = 0, out_off = 0, pyr_off = 0, blur_off = 0, tile_base = 0;
-    int max_cells = 0, node_cap = 0, roi_max = 0, cand_bytes = 0;
+    int max_cells = 0, node_cap = 0;
+    FastLds fl{0, 0, 0, 0};
     int pw = W, ph = H;
     for (int l = 0; l < h->nlevels; l++) {
         OrbLevel& L = g.lv[l];
@@ -177,8 +177,13 @@ static int build_geom(orbfe_extractor* h, int W, int H) {
         L.cell_cap = ((L.w_cell + 1) / 2) * ((L.h_cell + 1) / 2);
         L.cellkey_off = cellkey_off;
         cellkey_off += ncell * L.cell_cap;
-        roi_max = std::max(roi_max, round_up((L.w_cell + 12) * (L.h_cell + 6), 16));   // RS <= cols + 6
-        cand_bytes = std::max(cand_bytes, round_up(4 * L.w_cell * L.h_cell, 16));
+        {   // k_fast: RS = 4 * (ceil(dw / 4) + 2) with dw <= w_cell; ROI rows <= h_cell + 6, score
+            // map rows <= h_cell + 2; corner list 2 B per pixel and >= 8 B per 4-pixel group + 256
+            const int rs = 4 * ((L.w_cell + 3) / 4 + 2), grp = ((L.w_cell + 3) / 4) * L.h_cell;
+            fl.roi = std::max(fl.roi, round_up(rs * (L.h_cell + 6), 16));
+            fl.sc = std::max(fl.sc, round_up(rs * (L.h_cell + 2), 16));
+            fl.cor = std::max(fl.cor, round_up(std::max(2 * L.w_cell * L.h_cell, 8 * grp + 256), 16));
+        }
         if (L.w_cell > 127 || L.h_cell > 127) return ORBFE_E_ARG;   // k_fast packs dx, dy in 7 bits
         // octree
         L.budget = h->per_level[l];
@@ -271,8 +276,8 @@ static int build_geom(orbfe_extractor* h, int W, int H) {
     g.blur_tiles = tile_base;
     g.max_cells_level = max_cells;
     g.node_cap = node_cap;
-    h->roi_max = roi_max;
-    h->cand_bytes = cand_bytes;
+    fl.wave_bytes = fl.roi + fl.sc + fl.cor + FAST_ENT_BYTES;
+    h->fast_lds = fl;
     h->oct_lds = octree_lds_bytes(g);
     return ORBFE_OK;
 }
@@ -290,7 +295,7 @@ static int ensure(orbfe_extractor* h, int W, int H, int B) {
         free_buffers(h);
     }
     if (h->oct_lds > 160 * 1024) return ORBFE_E_ARG;
-    if ((size_t)4 * (2 * h->roi_max + h->cand_bytes) > 160 * 1024) return ORBFE_E_ARG;   // k_fast: 4 waves
+    if ((size_t)4 * h->fast_lds.wave_bytes > 160 * 1024) return ORBFE_E_ARG;   // k_fast: 4 waves per block
     B = std::max(B, 1);
     const OrbGeom& g = h->g;
     HIPCHK(hipMalloc(&h->d_tab, std::max<size_t>(2, h->tab.size() * 2)));
@@ -349,8 +354,8 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
     memcpy(bk.k, h->blur_variant == 1 ? kBlurRound : kBlurED, sizeof(bk.k));
     if (tm) HIPCHK(hipEventRecord(ev[2], s));   // the blur is fused into k_describe (stage kept for the layout)
     hipLaunchKernelGGL(k_fast, dim3((g.total_cells + 4 * FAST_CPW - 1) / (4 * FAST_CPW), B), dim3(256),
-                       (size_t)4 * (2 * h->roi_max + h->cand_bytes), s, P, pitch, h->d_pyr, g.pyr_bytes, g, h->roi_max,
-                       h->cand_bytes, h->d_cellkeys, h->d_cellcnt, h->ablate_fast);
+                       (size_t)4 * h->fast_lds.wave_bytes, s, P, pitch, h->d_pyr, g.pyr_bytes, g, h->fast_lds,
+                       h->d_cellkeys, h->d_cellcnt, h->ablate_fast);
     if (tm) HIPCHK(hipEventRecord(ev[3], s));
     hipLaunchKernelGGL(k_octree, dim3(B, g.nlevels), dim3(OCT_NT), h->oct_lds, s, g, h->d_cellkeys, h->d_cellcnt,
                        h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, lap0, lap1, h->d_oct_ts);

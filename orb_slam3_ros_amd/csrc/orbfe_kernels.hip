@@ -425,20 +425,25 @@ __device__ __forceinline__ void fast_prefetch(const FastCell& f, int lane, uint3
     }
 }
 
+struct FastLds {
+    int roi, sc, cor, wave_bytes;   // bytes per wave: ROI image, score map, corner list (+ entries)
+};
+#define FAST_ENT_BYTES 1024     // entry chunk: 64 groups x <= 8 entries x 2 B
+
 __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
-                                              int pyr_stride, OrbGeom g, int roi_max, int cand_bytes,
-                                              uint32_t* cellkeys, int* cellcnt, int ablate) {
+                                              int pyr_stride, OrbGeom g, FastLds fl, uint32_t* cellkeys,
+                                              int* cellcnt, int ablate) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_fast[];
     const int wave = threadIdx.x >> 6, lane = lane_id();
     const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
     const int bx = lb % gridDim.x, b = lb / gridDim.x;
-    // per wave: ROI image | score map | entry list (<= 2 entries per detection pixel)
-    uint8_t* s_img = smem_fast + wave * (2 * roi_max + cand_bytes);
-    uint8_t* s_sc = s_img + roi_max;
-    uint16_t* s_cand = (uint16_t*)(s_sc + roi_max);
-    // pass-1 group records live in the (all-zero) score map until they are expanded, then those
-    // dwords are zeroed again: 4 * groups <= 4 * ng * dh < the cell's score-map bytes
-    uint32_t* s_grp = (uint32_t*)s_sc;
+    // per wave: ROI image (rows of RS bytes) | score map of the detection rect + 1-pixel ring
+    // (same RS, origin at ROI (2, 2)) | corner list (2 B per pixel; its tail holds the pass-1
+    // group records) | entry chunk (<= 8 entries for each of 64 groups)
+    uint8_t* s_img = smem_fast + wave * fl.wave_bytes;
+    uint8_t* s_sc = s_img + fl.roi;
+    uint16_t* s_cor = (uint16_t*)(s_sc + fl.sc);
+    uint16_t* s_ent = (uint16_t*)((uint8_t*)s_cor + fl.cor);
     const int cbeg = (bx * 4 + wave) * FAST_CPW;
     if (cbeg >= g.total_cells) return;
     const int cend = min(cbeg + FAST_CPW, g.total_cells);
@@ -462,7 +467,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
                 const int y = sy + u * rpl;
                 if (sy < rpl && st < nd && y < cur.rows) {
                     s32w[y * nd + st] = __builtin_amdgcn_alignbyte(hi, lo, sal);
-                    s32z[y * nd + st] = 0u;
+                    if (y < dh + 2) s32z[y * nd + st] = 0u;
                 }
             }
             // rows beyond the prefetch window (only very wide / tall cells of tiny levels): direct
@@ -479,7 +484,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
                     const uint32_t hi = __shfl_down(lo, 1, 64);
                     if (st < nd) {
                         s32w[y * nd + st] = __builtin_amdgcn_alignbyte(hi, lo, sal);
-                        s32z[y * nd + st] = 0u;
+                        if (y < dh + 2) s32z[y * nd + st] = 0u;
                     }
                 }
             }
@@ -508,13 +513,15 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
             const int th = attempt == 0 ? g.ini_th : g.min_th;
             if (attempt) {
                 uint32_t* s32z = (uint32_t*)s_sc;
-                for (int i = lane; i < me.rows * nd; i += 64) s32z[i] = 0u;
+                for (int i = lane; i < (dh + 2) * nd; i += 64) s32z[i] = 0u;
                 WAVE_SYNC();
             }
             // pass 1: FAST's exact necessary test (each 9-arc contains one pixel of every opposite
             // pair (k, k+8), k = 0, 2, 4, 6, all of one sign) for 4 pixels per lane in packed u16x2
             // arithmetic (even bytes / odd bytes); candidates compacted row-major as (dy << 8 | dx).
-            int ncand = 0, ngrp = 0;
+            int ngrp = 0;
+            // group records at the tail of the corner list: <= ng * dh of them
+            uint32_t* s_grp = (uint32_t*)((uint8_t*)s_cor + fl.cor) - ng * dh;
             if (ng) {
                 const int rpi = 64 / ng;
                 const int ly = lane / ng, lg = lane - ly * ng;
@@ -576,75 +583,81 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
             WAVE_SYNC();
             // expand the groups into entries, one per (pixel, possible sign): dy << 7 | dx, bit 14 =
             // bright, bit 15 = second entry of a pixel (both signs passed; at most one can be a corner)
-            for (int g0 = 0; g0 < ngrp; g0 += 64) {
-                const int gi = g0 + lane;
-                const uint32_t rec = gi < ngrp ? s_grp[gi] : 0u;
-                const uint32_t dbits = (rec >> 16) & 15u, bbits = rec >> 20;
-                const int cnt = __popc(rec >> 16);   // <= 8: scan by bit planes
-                const unsigned long long lt = (1ull << lane) - 1ull;
-                const unsigned long long m0 = __ballot(cnt & 1), m1 = __ballot(cnt & 2), m2 = __ballot(cnt & 4),
-                                         m3 = __ballot(cnt & 8);
-                int pos = ncand + __popcll(m0 & lt) + 2 * __popcll(m1 & lt) + 4 * __popcll(m2 & lt) +
-                          8 * __popcll(m3 & lt);
-                const int packed = (int)(rec & 0x3FFFu);
-                for (int i = 0; i < 4; i++) {
-                    const uint32_t di = (dbits >> i) & 1u, bi = (bbits >> i) & 1u;
-                    if (di) s_cand[pos++] = (uint16_t)(packed + i);
-                    if (bi) s_cand[pos++] = (uint16_t)((packed + i) | 0x4000 | (di << 15));
-                }
-                ncand += __popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2) + 8 * __popcll(m3);
-            }
-            for (int i = lane; i < ngrp; i += 64) s_grp[i] = 0u;
-            WAVE_SYNC();
             if (ablate == 2) {
-                asm volatile("" ::"v"(ncand));
+                asm volatile("" ::"v"(ngrp));
                 stop = true;
                 break;
             }
-            // pass 2: exact score M - 1 (corner iff M > th) of each entry for its sign only, two
-            // entries per lane in packed u16x2 (saturated differences: an arc with a negative minimum
-            // never decides a corner); corners are compacted in place, in pixel order, as dy << 7 | dx
+            // per chunk of 64 groups: expand into entries, one per (pixel, possible sign): dy << 7 |
+            // dx, bit 14 = bright, bit 15 = second entry of a pixel (both signs passed; at most one
+            // can be a corner); then the exact score of the chunk's entries. Corners are appended in
+            // pixel order to the corner list, whose tail holds the group records still to come
+            // (cor_bytes >= 8 * groups + 256 keeps the two apart).
             int ncorner = 0;
-            for (int j0 = 0; j0 < ncand; j0 += 128) {
-                const int j = j0 + 2 * lane;
-                const uint32_t e2 = j < ncand ? ((const uint32_t*)s_cand)[j >> 1] : 0u;
-                const bool ok0 = j < ncand, ok1 = j + 1 < ncand;
-                const uint32_t e0 = e2 & 0xFFFFu, e1 = ok1 ? e2 >> 16 : e0;
-                const uint8_t* q0 = s_px + (((e0 >> 7) & 127) + 3) * RS + (e0 & 127) + 3;
-                const uint8_t* q1 = s_px + (((e1 >> 7) & 127) + 3) * RS + (e1 & 127) + 3;
-                const uint32_t v2 = (uint32_t)q0[0] | ((uint32_t)q1[0] << 16);
-                const uint32_t bmask = ((e0 & 0x4000u) ? 0x0000FFFFu : 0u) | ((e1 & 0x4000u) ? 0xFFFF0000u : 0u);
-                orbfe_ushort2 P[16];
-#pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    const int o = kRingDy[k] * RS + kRingDx[k];
-                    const orbfe_ushort2 x2 = as_us2((uint32_t)q0[o] | ((uint32_t)q1[o] << 16));
-                    const uint32_t dk = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(as_us2(v2), x2));
-                    const uint32_t bk = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(x2, as_us2(v2)));
-                    P[k] = as_us2((bk & bmask) | (dk & ~bmask));
+            for (int g0 = 0; g0 < ngrp; g0 += 64) {
+                int nent = 0;
+                {
+                    const int gi = g0 + lane;
+                    const uint32_t rec = gi < ngrp ? s_grp[gi] : 0u;
+                    const uint32_t dbits = (rec >> 16) & 15u, bbits = rec >> 20;
+                    const int cnt = __popc(rec >> 16);   // <= 8: scan by bit planes
+                    const unsigned long long lt = (1ull << lane) - 1ull;
+                    const unsigned long long m0 = __ballot(cnt & 1), m1 = __ballot(cnt & 2), m2 = __ballot(cnt & 4),
+                                             m3 = __ballot(cnt & 8);
+                    int pos = __popcll(m0 & lt) + 2 * __popcll(m1 & lt) + 4 * __popcll(m2 & lt) + 8 * __popcll(m3 & lt);
+                    const int packed = (int)(rec & 0x3FFFu);
+                    for (int i = 0; i < 4; i++) {
+                        const uint32_t di = (dbits >> i) & 1u, bi = (bbits >> i) & 1u;
+                        if (di) s_ent[pos++] = (uint16_t)(packed + i);
+                        if (bi) s_ent[pos++] = (uint16_t)((packed + i) | 0x4000 | (di << 15));
+                    }
+                    nent = __popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2) + 8 * __popcll(m3);
                 }
-                orbfe_ushort2 m2[16], m4[16];
+                WAVE_SYNC();
+                // pass 2: exact score M - 1 (corner iff M > th) of each entry for its sign only, two
+                // entries per lane in packed u16x2 (saturated differences: an arc with a negative
+                // minimum never decides a corner)
+                for (int j0 = 0; j0 < nent; j0 += 128) {
+                    const int j = j0 + 2 * lane;
+                    const uint32_t e2 = j < nent ? ((const uint32_t*)s_ent)[j >> 1] : 0u;
+                    const bool ok0 = j < nent, ok1 = j + 1 < nent;
+                    const uint32_t e0 = e2 & 0xFFFFu, e1 = ok1 ? e2 >> 16 : e0;
+                    const uint8_t* q0 = s_px + (((e0 >> 7) & 127) + 3) * RS + (e0 & 127) + 3;
+                    const uint8_t* q1 = s_px + (((e1 >> 7) & 127) + 3) * RS + (e1 & 127) + 3;
+                    const uint32_t v2 = (uint32_t)q0[0] | ((uint32_t)q1[0] << 16);
+                    const uint32_t bmask = ((e0 & 0x4000u) ? 0x0000FFFFu : 0u) | ((e1 & 0x4000u) ? 0xFFFF0000u : 0u);
+                    orbfe_ushort2 P[16];
 #pragma unroll
-                for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(P[k], P[(k + 1) & 15]);
+                    for (int k = 0; k < 16; k++) {
+                        const int o = kRingDy[k] * RS + kRingDx[k];
+                        const orbfe_ushort2 x2 = as_us2((uint32_t)q0[o] | ((uint32_t)q1[o] << 16));
+                        const uint32_t dk = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(as_us2(v2), x2));
+                        const uint32_t bk = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(x2, as_us2(v2)));
+                        P[k] = as_us2((bk & bmask) | (dk & ~bmask));
+                    }
+                    orbfe_ushort2 m2[16], m4[16];
 #pragma unroll
-                for (int k = 0; k < 16; k++) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
-                orbfe_ushort2 best = {0, 0};
+                    for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(P[k], P[(k + 1) & 15]);
 #pragma unroll
-                for (int k = 0; k < 16; k++)
-                    best = __builtin_elementwise_max(
-                        best, __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]), P[(k + 8) & 15]));
-                const bool c0 = ok0 && (int)best.x > th, c1 = ok1 && (int)best.y > th;
-                if (c0) s_sc[(((e0 >> 7) & 127) + 3) * RS + (e0 & 127) + 3] = (uint8_t)(best.x - 1);
-                if (c1) s_sc[(((e1 >> 7) & 127) + 3) * RS + (e1 & 127) + 3] = (uint8_t)(best.y - 1);
-                const int cc = (int)c0 + (int)c1;
-                const unsigned long long lt = (1ull << lane) - 1ull;
-                const unsigned long long b0 = __ballot(cc & 1), b1 = __ballot(cc & 2);
-                int pos = ncorner + __popcll(b0 & lt) + 2 * __popcll(b1 & lt);
-                if (c0) s_cand[pos++] = (uint16_t)(e0 & 0x3FFFu);
-                if (c1) s_cand[pos] = (uint16_t)(e1 & 0x3FFFu);
-                ncorner += __popcll(b0) + 2 * __popcll(b1);
+                    for (int k = 0; k < 16; k++) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
+                    orbfe_ushort2 best = {0, 0};
+#pragma unroll
+                    for (int k = 0; k < 16; k++)
+                        best = __builtin_elementwise_max(
+                            best, __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]), P[(k + 8) & 15]));
+                    const bool c0 = ok0 && (int)best.x > th, c1 = ok1 && (int)best.y > th;
+                    if (c0) s_sc[(((e0 >> 7) & 127) + 1) * RS + (e0 & 127) + 1] = (uint8_t)(best.x - 1);
+                    if (c1) s_sc[(((e1 >> 7) & 127) + 1) * RS + (e1 & 127) + 1] = (uint8_t)(best.y - 1);
+                    const int cc = (int)c0 + (int)c1;
+                    const unsigned long long lt = (1ull << lane) - 1ull;
+                    const unsigned long long b0 = __ballot(cc & 1), b1 = __ballot(cc & 2);
+                    int pos = ncorner + __popcll(b0 & lt) + 2 * __popcll(b1 & lt);
+                    if (c0) s_cor[pos++] = (uint16_t)(e0 & 0x3FFFu);
+                    if (c1) s_cor[pos] = (uint16_t)(e1 & 0x3FFFu);
+                    ncorner += __popcll(b0) + 2 * __popcll(b1);
+                }
+                WAVE_SYNC();   // s_ent is refilled by the next chunk
             }
-            WAVE_SYNC();
             if (ablate == 3) {
                 asm volatile("" ::"v"((int)s_sc[lane]));
                 stop = true;
@@ -657,14 +670,14 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
                 bool surv = false;
                 int p = 0;
                 if (i < ncorner) {
-                    p = s_cand[i];
-                    const uint8_t* q = s_sc + ((p >> 7) + 3) * RS + (p & 127) + 3;
+                    p = s_cor[i];
+                    const uint8_t* q = s_sc + ((p >> 7) + 1) * RS + (p & 127) + 1;
                     const int sc = q[0];
                     surv = sc > q[-1] && sc > q[1] && sc > q[-RS - 1] && sc > q[-RS] && sc > q[-RS + 1] &&
                            sc > q[RS - 1] && sc > q[RS] && sc > q[RS + 1];
                 }
                 const unsigned long long m = __ballot(surv);
-                if (surv) s_cand[nsurv + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)p;
+                if (surv) s_cor[nsurv + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)p;
                 nsurv += __popcll(m);
             }
             WAVE_SYNC();
@@ -683,8 +696,8 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
             const int i = i0 + lane;
             int sc = 0, p = 0;
             if (i < nsurv) {
-                p = s_cand[i];
-                sc = s_sc[((p >> 7) + 3) * RS + (p & 127) + 3];
+                p = s_cor[i];
+                sc = s_sc[((p >> 7) + 1) * RS + (p & 127) + 1];
             }
             const bool f = i < nsurv;
             const unsigned long long m = __ballot(f);
