@@ -118,6 +118,7 @@ struct orbfe_extractor {
     int* last_counts = nullptr;
     std::mutex mu;
     int ablate_fast = 0;   // ORBFE_ABLATE_FAST: timing-only builds of k_fast (outputs invalid when != 0)
+    int ablate_desc = 0;   // ORBFE_ABLATE_DESC: the same for k_describe
     unsigned long long* d_oct_ts = nullptr;   // ORBFE_OCT_STAMPS: per-phase s_memtime of the octree (image 0)
 };
 
@@ -361,7 +362,8 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
                        h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, lap0, lap1, h->d_oct_ts);
     if (tm) HIPCHK(hipEventRecord(ev[4], s));
     hipLaunchKernelGGL(k_describe, dim3((g.out_per_img + 3) / 4, B), dim3(256), 0, s, P, pitch, h->d_pyr,
-                       g.pyr_bytes, g, h->d_outkeys, h->d_lvinfo, h->d_ranks, o_kps, o_desc, o_counts, bk);
+                       g.pyr_bytes, g, h->d_outkeys, h->d_lvinfo, h->d_ranks, o_kps, o_desc, o_counts, bk,
+                       h->ablate_desc);
     if (tm) HIPCHK(hipEventRecord(ev[5], s));
     HIPCHK(hipGetLastError());
     h->last_kps = o_kps;
@@ -408,6 +410,7 @@ int orbfe_extractor_create(int nfeatures, float scaleFactor, int nlevels, int in
     h->scale_factor_f = scaleFactor;
     h->scale_factor = scaleFactor;   // double member initialised from the float argument (ORBextractor.h:96)
     if (const char* ab = getenv("ORBFE_ABLATE_FAST")) h->ablate_fast = atoi(ab);
+    if (const char* ab = getenv("ORBFE_ABLATE_DESC")) h->ablate_desc = atoi(ab);
     if (getenv("ORBFE_OCT_STAMPS")) {
         if (hipMalloc(&h->d_oct_ts, 64 * 8 * ORBFE_MAX_LEVELS) != hipSuccess) { delete h; return ORBFE_E_DEVICE; }
         (void)hipMemset(h->d_oct_ts, 0, 64 * 8 * ORBFE_MAX_LEVELS);

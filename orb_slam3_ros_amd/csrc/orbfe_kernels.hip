@@ -1266,7 +1266,8 @@ __device__ __forceinline__ float fast_atan2_dev(float y, float x) {
 __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                                   int pyr_stride, OrbGeom g, const uint32_t* __restrict__ outkeys,
                                                   const int* __restrict__ lvinfo, const int* __restrict__ ranks,
-                                                  OrbKeyPoint* kps, uint8_t* desc, int* counts, BlurKernel bk) {
+                                                  OrbKeyPoint* kps, uint8_t* desc, int* counts, BlurKernel bk,
+                                                  int ablate) {
     __shared__ __attribute__((aligned(16))) uint8_t s_dp[4][DP_WAVE_LDS];
     const int wave = threadIdx.x >> 6, lane = lane_id();
     const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
@@ -1288,6 +1289,25 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
     if (i >= inf[4 * l]) return;
     const uint32_t key = outkeys[(size_t)b * g.out_per_img + flat];
     const int x = key & 0xfff, y = (key >> 12) & 0xfff;
+    // output slot: lapping reorder (ORBextractor.cc:1153-1162)
+    const int rk = ranks[(size_t)b * g.out_per_img + flat];
+    int slot;
+    if (rk & 0x40000000) slot = ntot - 1 - (lap_before + (rk & 0x3fffffff));
+    else slot = mono_before + rk;
+    const size_t o = (size_t)b * g.kp_cap + slot;
+    auto emit_kp = [&](float angle) {
+        if (lane == 0) {
+            OrbKeyPoint kp;
+            kp.x = (l == 0) ? (float)x : (float)x * L.scale;
+            kp.y = (l == 0) ? (float)y : (float)y * L.scale;
+            kp.size = (float)L.patch_size;
+            kp.angle = angle;
+            kp.response = (float)(key >> 24);
+            kp.octave = l;
+            kp.class_id = -1;
+            kps[o] = kp;
+        }
+    };
     uint8_t* raw = s_dp[wave];
     uint16_t* rowq = (uint16_t*)(raw + DP_N * DP_RAW_S);
     int pitch;
@@ -1320,6 +1340,11 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
         }
     }
     WAVE_SYNC();
+    if (ablate == 1) {   // timing-only (descriptors invalid, keypoint records valid): staging
+        asm volatile("" ::"v"((int)raw[lane]));
+        emit_kp(0.f);
+        return;
+    }
     // ---- IC_Angle on the unblurred patch, centre (21, 21) ----
     const uint8_t* center = raw + DP_R * DP_RAW_S + DP_R;
     const int u = (lane & 31) - 15;
@@ -1338,6 +1363,11 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
     m10 = wave_sum(m10);
     m01 = wave_sum(m01);
     const float angle = fast_atan2_dev((float)m01, (float)m10);
+    if (ablate == 2) {   // + IC_Angle
+        asm volatile("" ::"v"(angle));
+        emit_kp(angle);
+        return;
+    }
     // ---- 7x7 Gaussian: row pass (Q8, exact) over the 43x37 region in packed u16x2 (every
     // partial sum fits 16 bits: sum(k) * 255 <= 65535); the column pass (Q16, rounded) runs only
     // at the 512 points rBRIEF samples. Both passes are exact integer sums before the final
@@ -1365,6 +1395,11 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
         }
     }
     WAVE_SYNC();
+    if (ablate == 3) {   // + Gaussian row pass
+        asm volatile("" ::"v"((int)rowq[lane]), "v"(angle));
+        emit_kp(angle);
+        return;
+    }
     // blurred(18 + dy, 18 + dx): column pass over rowq rows 18 + dy .. 24 + dy
     // (24-bit multiplies are exact here: pair sums <= 2 * 65280, taps <= 256)
     auto blurred = [&](int dy, int dx) -> int {
@@ -1390,26 +1425,11 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
         const int t1 = blurred((int)rintf(px1f * bs + py1f * a), (int)rintf(px1f * a - py1f * bs));
         masks[mm] = __ballot(t0 < t1);
     }
-    const int rk = ranks[(size_t)b * g.out_per_img + flat];
-    int slot;
-    if (rk & 0x40000000) slot = ntot - 1 - (lap_before + (rk & 0x3fffffff));
-    else slot = mono_before + rk;
-    const size_t o = (size_t)b * g.kp_cap + slot;
     if (lane < 4) {
         unsigned long long mv = lane == 0 ? masks[0] : lane == 1 ? masks[1] : lane == 2 ? masks[2] : masks[3];
         ((unsigned long long*)(desc + o * 32))[lane] = mv;
     }
-    if (lane == 0) {
-        OrbKeyPoint kp;
-        kp.x = (l == 0) ? (float)x : (float)x * L.scale;
-        kp.y = (l == 0) ? (float)y : (float)y * L.scale;
-        kp.size = (float)L.patch_size;
-        kp.angle = angle;
-        kp.response = (float)(key >> 24);
-        kp.octave = l;
-        kp.class_id = -1;
-        kps[o] = kp;
-    }
+    emit_kp(angle);
 }
 
 // ---------------------------------------------------------------------------------------------
