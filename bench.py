@@ -5,7 +5,9 @@ A step = one pass of the hot path over one batch of synthetic stereo frames resi
 ORBextractor::operator() on every left and right image (pyramid, FAST cells, octree,
 orientation, blur, rBRIEF) + Frame::ComputeStereoMatches per frame, all on the GPU (liborbfe.so).
 With N > 1 GPUs (torchrun, one process per GPU) every rank processes its own shard of frames
-(weak scaling) and the per-image feature slots are all-gathered over RCCL at the end of the step.
+(weak scaling) and each step's keypoint + descriptor slab is all-gathered over RCCL, overlapped
+with the next step's kernels (distributed.SlabExchange); the timed region ends after the last
+step's gather.
 
 Prints ONE JSON line (rank 0). See DESIGN.md §Measurement for the roofline bytes.
 """
@@ -255,22 +257,28 @@ def main():
     fe = StereoFrontEnd(F, W, H, nfeatures=args.nfeatures, bf=bf, fx=fx, device=dev, pipelines=args.pipelines)
     gather = world > 1 and not args.no_allgather
     if gather:
-        sb = odist.slot_bytes(fe.cap)
-        local_slots = torch.empty((2 * F, sb), dtype=torch.uint8, device=dev)
-        all_slots = torch.empty((world * 2 * F, sb), dtype=torch.uint8, device=dev)
-        all_slots_host = torch.empty((world * 2 * F, sb), dtype=torch.uint8) if gloo else None
+        # zero-copy, double-buffered slab exchange: the extractor writes step k's outputs into slab
+        # k % 2 and its all-gather runs asynchronously under step k + 1's kernels
+        xchg = odist.SlabExchange(2 * F, fe.cap, dev)
+    it = [0]
 
     def step():
+        k = it[0]
+        it[0] += 1
+        if gather:
+            xchg.acquire(k)             # the gather that last read slab k % 2 has finished
+            fe.bind_outputs(*xchg.views(k))
         fe.run(images)
         if gather:
-            odist.pack_slots(fe.counts, fe.kps, fe.desc, local_slots)
-            if gloo:   # gloo gathers host tensors
-                odist.allgather_slots(local_slots.cpu(), all_slots_host)
-            else:
-                odist.allgather_slots(local_slots, all_slots)
+            xchg.post(k)
+
+    def drain():
+        if gather:
+            xchg.drain()
 
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -278,6 +286,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()                             # every step's exchange is inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -353,6 +362,9 @@ def main():
                 "width": W, "height": H,
                 "allgather": gather,
                 "allgather_backend": (args.dist_backend if gather else None),
+                "allgather_bytes_per_rank_per_step": (odist.slab_bytes(2 * F, fe.cap) if gather else 0),
+                "allgather_overlap": (None if not gather else "synchronous host copies (gloo rehearsal)" if gloo else
+                                      "async, double-buffered: step k's gather runs under step k+1's kernels"),
                 "pipelines": args.pipelines,
                 "parallelism": f"frame-sharded x{world}",
             },

@@ -1252,7 +1252,9 @@ __device__ __forceinline__ float fast_atan2_dev(float y, float x) {
     return a;
 }
 
-// Fused per-keypoint pipeline, one wave per keypoint: the 43x43 patch of the UNBLURRED level
+// Fused per-keypoint pipeline, one wave per keypoint (several keypoints per wave with the next
+// patch prefetched into registers measured slower: the loop raised the kernel to 123-129 VGPRs,
+// 3-4 waves per SIMD, against 7 with one keypoint): the 43x43 patch of the UNBLURRED level
 // around the keypoint (reflect-101 outside the level) is staged in LDS once; IC_Angle reads it
 // directly; the 7x7 Gaussian of the level is evaluated on the 37x37 window the descriptor can
 // sample (|offset| <= 18) with the exact separable fixed-point arithmetic of k_blur's reference
@@ -1263,38 +1265,65 @@ __device__ __forceinline__ float fast_atan2_dev(float y, float x) {
 #define DP_RAW_S 48                  // raw row stride (bytes)
 #define DP_Q_S 40                    // Q8 row-pass stride (u16 elements)
 #define DP_WAVE_LDS 5504   // >= 43*48 + 43*40*2, multiple of 16
-__global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
-                                                  int pyr_stride, OrbGeom g, const uint32_t* __restrict__ outkeys,
-                                                  const int* __restrict__ lvinfo, const int* __restrict__ ranks,
-                                                  OrbKeyPoint* kps, uint8_t* desc, int* counts, BlurKernel bk,
-                                                  int ablate) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_dp[4][DP_WAVE_LDS];
-    const int wave = threadIdx.x >> 6, lane = lane_id();
-    const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
-    const int b = lb / gridDim.x;
-    const int flat = (lb % gridDim.x) * 4 + wave;   // index over all levels' output slots
-    if (flat >= g.out_per_img) return;
+#define DP_ND (DP_N * (DP_RAW_S / 4))   // 516 patch dwords
+// One output slot of an image (wave-uniform): level, key, output index and the patch geometry.
+struct DescSlot {
+    int valid, l, x, y, interior, pitch, gx0, sh;
+    uint32_t key;
+    size_t o;
+    gptr_u8 im;
+};
+__device__ __forceinline__ DescSlot desc_slot(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
+                                              int pyr_stride, const OrbGeom& g, const uint32_t* __restrict__ outkeys,
+                                              const int* __restrict__ inf, const int* __restrict__ ranks, int b,
+                                              int flat, int ntot) {
+    DescSlot d;
+    d.valid = 0;
+    if (flat >= g.out_per_img) return d;
     int l = 0;
     while (l + 1 < g.nlevels && flat >= g.lv[l + 1].out_off) l++;
     const OrbLevel& L = g.lv[l];
-    const int i = flat - L.out_off;
-    const int* inf = lvinfo + (size_t)b * g.nlevels * 4;
-    int ntot = 0, lap_before = 0, mono_before = 0, mono_tot = 0;
-    for (int k = 0; k < g.nlevels; k++) {
-        ntot += inf[4 * k];
-        mono_tot += inf[4 * k + 2];
-        if (k < l) { lap_before += inf[4 * k + 1]; mono_before += inf[4 * k + 2]; }
-    }
-    if (flat == 0 && lane == 0) { counts[2 * b] = ntot; counts[2 * b + 1] = mono_tot; }
-    if (i >= inf[4 * l]) return;
-    const uint32_t key = outkeys[(size_t)b * g.out_per_img + flat];
-    const int x = key & 0xfff, y = (key >> 12) & 0xfff;
+    if (flat - L.out_off >= inf[4 * l]) return d;
+    int lap_before = 0, mono_before = 0;
+    for (int k = 0; k < l; k++) { lap_before += inf[4 * k + 1]; mono_before += inf[4 * k + 2]; }
+    d.valid = 1;
+    d.l = l;
+    d.key = (uint32_t)__builtin_amdgcn_readfirstlane((int)outkeys[(size_t)b * g.out_per_img + flat]);
+    d.x = d.key & 0xfff;
+    d.y = (d.key >> 12) & 0xfff;
     // output slot: lapping reorder (ORBextractor.cc:1153-1162)
-    const int rk = ranks[(size_t)b * g.out_per_img + flat];
-    int slot;
-    if (rk & 0x40000000) slot = ntot - 1 - (lap_before + (rk & 0x3fffffff));
-    else slot = mono_before + rk;
-    const size_t o = (size_t)b * g.kp_cap + slot;
+    const int rk = __builtin_amdgcn_readfirstlane(ranks[(size_t)b * g.out_per_img + flat]);
+    const int slot = (rk & 0x40000000) ? ntot - 1 - (lap_before + (rk & 0x3fffffff)) : mono_before + rk;
+    d.o = (size_t)b * g.kp_cap + slot;
+    d.im = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l, &d.pitch);
+    const int px0 = d.x - DP_R, py0 = d.y - DP_R;
+    d.gx0 = px0 & ~3;
+    d.sh = px0 - d.gx0;
+    d.interior = px0 >= 0 && py0 >= 0 && py0 + DP_N <= L.h && d.gx0 + DP_RAW_S + 4 <= L.w && (d.pitch & 3) == 0 &&
+                 ((((uintptr_t)d.im) & 3) == 0);
+    return d;
+}
+// Patch dwords of an interior slot (dword it = row it / 12, column group it % 12; lo | hi realign)
+__device__ __forceinline__ void desc_load(const DescSlot& d, int lane, uint32_t (&lo)[9], uint32_t (&hi)[9]) {
+    const int py0 = d.y - DP_R;
+#pragma unroll
+    for (int u = 0; u < 9; u++) {
+        const int it = min(lane + 64 * u, DP_ND - 1);
+        const int r = it / (DP_RAW_S / 4), k = it - r * (DP_RAW_S / 4);
+        gptr_u32 rp = (gptr_u32)(d.im + (size_t)(py0 + r) * d.pitch + d.gx0) + k;
+        lo[u] = rp[0];
+        hi[u] = rp[1];
+    }
+}
+// IC_Angle + Gaussian + rBRIEF of one slot whose raw patch is staged in `raw`; writes the
+// keypoint record and the descriptor row.
+__device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g, const uint8_t* raw, uint16_t* rowq,
+                                             const uint32_t (&pat)[4], int lane, OrbKeyPoint* kps, uint8_t* desc,
+                                             const BlurKernel& bk, int ablate) {
+    const OrbLevel& L = g.lv[d.l];
+    const int l = d.l, x = d.x, y = d.y;
+    const uint32_t key = d.key;
+    const size_t o = d.o;
     auto emit_kp = [&](float angle) {
         if (lane == 0) {
             OrbKeyPoint kp;
@@ -1308,38 +1337,6 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
             kps[o] = kp;
         }
     };
-    uint8_t* raw = s_dp[wave];
-    uint16_t* rowq = (uint16_t*)(raw + DP_N * DP_RAW_S);
-    int pitch;
-    gptr_u8 im = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l, &pitch);
-    // ---- stage the raw patch: raw[r][c] = level(y - 21 + r, x - 21 + c), reflect-101 outside ----
-    const int px0 = x - DP_R, py0 = y - DP_R;
-    const int gx0 = px0 & ~3, sh = px0 - gx0;
-    const bool interior = px0 >= 0 && py0 >= 0 && py0 + DP_N <= L.h && gx0 + DP_RAW_S + 4 <= L.w &&
-                          (pitch & 3) == 0 && ((((uintptr_t)im) & 3) == 0);
-    if (interior) {
-        constexpr int ND = DP_N * (DP_RAW_S / 4);   // 516 dwords
-        uint32_t lo[9], hi[9];
-#pragma unroll
-        for (int u = 0; u < 9; u++) {
-            const int it = min(lane + 64 * u, ND - 1);
-            const int r = it / (DP_RAW_S / 4), k = it - r * (DP_RAW_S / 4);
-            gptr_u32 rp = (gptr_u32)(im + (size_t)(py0 + r) * pitch + gx0) + k;
-            lo[u] = rp[0];
-            hi[u] = rp[1];
-        }
-#pragma unroll
-        for (int u = 0; u < 9; u++) {
-            const int it = lane + 64 * u;
-            if (it < ND) ((uint32_t*)raw)[it] = __builtin_amdgcn_alignbyte(hi[u], lo[u], (unsigned)sh);
-        }
-    } else {
-        for (int it = lane; it < DP_N * DP_N; it += 64) {
-            const int r = it / DP_N, c = it - r * DP_N;
-            raw[r * DP_RAW_S + c] = im[(size_t)reflect101(py0 + r, L.h) * pitch + reflect101(px0 + c, L.w)];
-        }
-    }
-    WAVE_SYNC();
     if (ablate == 1) {   // timing-only (descriptors invalid, keypoint records valid): staging
         asm volatile("" ::"v"((int)raw[lane]));
         emit_kp(0.f);
@@ -1418,9 +1415,9 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
     unsigned long long masks[4];
 #pragma unroll
     for (int mm = 0; mm < 4; mm++) {
-        const int pr = 64 * mm + lane;
-        const float px0f = (float)c_pattern[4 * pr], py0f = (float)c_pattern[4 * pr + 1];
-        const float px1f = (float)c_pattern[4 * pr + 2], py1f = (float)c_pattern[4 * pr + 3];
+        const uint32_t pw = pat[mm];   // pair 64 * mm + lane
+        const float px0f = (float)(int8_t)(pw & 255u), py0f = (float)(int8_t)((pw >> 8) & 255u);
+        const float px1f = (float)(int8_t)((pw >> 16) & 255u), py1f = (float)(int8_t)(pw >> 24);
         const int t0 = blurred((int)rintf(px0f * bs + py0f * a), (int)rintf(px0f * a - py0f * bs));
         const int t1 = blurred((int)rintf(px1f * bs + py1f * a), (int)rintf(px1f * a - py1f * bs));
         masks[mm] = __ballot(t0 < t1);
@@ -1431,6 +1428,55 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
     }
     emit_kp(angle);
 }
+
+__global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
+                                                  int pyr_stride, OrbGeom g, const uint32_t* __restrict__ outkeys,
+                                                  const int* __restrict__ lvinfo, const int* __restrict__ ranks,
+                                                  OrbKeyPoint* kps, uint8_t* desc, int* counts, BlurKernel bk,
+                                                  int ablate) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_dp[4][DP_WAVE_LDS];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
+    const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
+    const int b = lb / gridDim.x;
+    const int flat = (lb % gridDim.x) * 4 + wave;   // index over all levels' output slots
+    if (flat >= g.out_per_img) return;
+    // the rBRIEF pairs of this lane (pair 64 * mm + lane: x0, y0, x1, y1 as signed bytes), issued
+    // first so they land while the slot is resolved and its patch loads
+    uint32_t pat[4];
+#pragma unroll
+    for (int mm = 0; mm < 4; mm++) pat[mm] = ((const uint32_t*)c_pattern)[64 * mm + lane];
+    const int* inf = lvinfo + (size_t)b * g.nlevels * 4;
+    int ntot = 0, mono_tot = 0;
+    for (int k = 0; k < g.nlevels; k++) {
+        ntot += inf[4 * k];
+        mono_tot += inf[4 * k + 2];
+    }
+    if (flat == 0 && lane == 0) { counts[2 * b] = ntot; counts[2 * b + 1] = mono_tot; }
+    const DescSlot d = desc_slot(imgs, in_pitch, pyr, pyr_stride, g, outkeys, inf, ranks, b, flat, ntot);
+    if (!d.valid) return;
+    uint8_t* raw = s_dp[wave];
+    uint16_t* rowq = (uint16_t*)(raw + DP_N * DP_RAW_S);
+    // ---- stage the raw patch: raw[r][c] = level(y - 21 + r, x - 21 + c), reflect-101 outside ----
+    if (d.interior) {
+        uint32_t lo[9], hi[9];
+        desc_load(d, lane, lo, hi);
+#pragma unroll
+        for (int u = 0; u < 9; u++) {
+            const int it = lane + 64 * u;
+            if (it < DP_ND) ((uint32_t*)raw)[it] = __builtin_amdgcn_alignbyte(hi[u], lo[u], (unsigned)d.sh);
+        }
+    } else {
+        const OrbLevel& L = g.lv[d.l];
+        const int px0 = d.x - DP_R, py0 = d.y - DP_R;
+        for (int it = lane; it < DP_N * DP_N; it += 64) {
+            const int r = it / DP_N, c = it - r * DP_N;
+            raw[r * DP_RAW_S + c] = d.im[(size_t)reflect101(py0 + r, L.h) * d.pitch + reflect101(px0 + c, L.w)];
+        }
+    }
+    WAVE_SYNC();
+    describe_one(d, g, raw, rowq, pat, lane, kps, desc, bk, ablate);
+}
+#undef DP_ND
 
 // ---------------------------------------------------------------------------------------------
 // K6: Frame::ComputeStereoMatches for a batch of rectified frames. One block (4 waves) per frame;

@@ -57,14 +57,25 @@ class StereoFrontEnd:
         self.uright = t.zeros((self.F, self.cap), dtype=t.float32, device=self.device)
         self.depth = t.zeros((self.F, self.cap), dtype=t.float32, device=self.device)
         self.nmatch = t.zeros((self.F,), dtype=t.int32, device=self.device)
-        for h, (a, b) in zip(self.handles, self.parts):
-            _lib.check(self.lib.orbfe_set_batch_outputs(h, self.kps[2 * a].data_ptr(), self.desc[2 * a].data_ptr(),
-                                                        self.counts[2 * a].data_ptr(), 2 * (b - a)),
-                       "set_batch_outputs")
+        self.bind_outputs(self.counts, self.kps, self.desc)
         self._ptrs = None
         self._ptr_key = None
         self._stage_on = False
         self._stereo_ev = []
+
+    def bind_outputs(self, counts, kps, desc):
+        """Direct the batch outputs (counts [2F,2] i32, keypoints [2F,cap,7] i32, descriptors
+        [2F,cap,32] u8, contiguous device tensors) into caller-owned buffers, e.g. the views of a
+        distributed.SlabExchange slab; takes effect from the next run()."""
+        n, t = 2 * self.F, self.torch
+        assert counts.shape == (n, 2) and counts.dtype == t.int32 and counts.is_contiguous()
+        assert kps.shape == (n, self.cap, 7) and kps.dtype == t.int32 and kps.is_contiguous()
+        assert desc.shape == (n, self.cap, 32) and desc.dtype == t.uint8 and desc.is_contiguous()
+        self.counts, self.kps, self.desc = counts, kps, desc
+        for h, (a, b) in zip(self.handles, self.parts):
+            _lib.check(self.lib.orbfe_set_batch_outputs(h, kps[2 * a].data_ptr(), desc[2 * a].data_ptr(),
+                                                        counts[2 * a].data_ptr(), 2 * (b - a)),
+                       "set_batch_outputs")
 
     def _pointer_arrays(self, images):
         key = (images.data_ptr(), tuple(images.shape), tuple(images.stride()))
