@@ -106,6 +106,12 @@ __device__ __forceinline__ int reflect101(int p, int n) {
     return p;
 }
 
+// a / d for 0 <= a < 2^16 and 1 <= d <= 2^16 (d typically wave-uniform): (a + 0.5) / d is at least
+// 1 / (2d) away from an integer, far above the error of v_rcp_f32, so the truncation is exact
+__device__ __forceinline__ int small_div(int a, int d) {
+    return (int)(((float)a + 0.5f) * __builtin_amdgcn_rcpf((float)d));
+}
+
 __device__ __forceinline__ uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
 
 // ---------------------------------------------------------------------------------------------
@@ -403,7 +409,7 @@ __device__ __forceinline__ void fast_prefetch(const FastCell& f, int lane, uint3
     int ng, nd, lpr, rpl;
     fast_geom(f, &ng, &nd, &lpr, &rpl);
     if (!ng) return;
-    const int sy = lane / lpr, st = lane - sy * lpr;
+    const int sy = small_div(lane, lpr), st = lane - sy * lpr;
     if (sy >= rpl) return;
     const int A0 = (f.c0 - 1) & ~3;
     // reads stay inside the row: bytes [c0 - 4, c1 + 7) with c1 <= w - 16
@@ -434,7 +440,9 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
                                               int pyr_stride, OrbGeom g, FastLds fl, uint32_t* cellkeys,
                                               int* cellcnt, int ablate) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_fast[];
-    const int wave = threadIdx.x >> 6, lane = lane_id();
+    // wave-uniform in an SGPR: the cell geometry (level search, cell row / column division, ROI
+    // bounds, row bases) is then scalar code instead of per-lane VALU divisions
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
     const int bx = lb % gridDim.x, b = lb / gridDim.x;
     // per wave: ROI image (rows of RS bytes) | score map of the detection rect + 1-pixel ring
@@ -457,7 +465,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
         const int RS = 4 * nd;
         // stage: realign with the next lane's dword, zero the score map
         if (ng) {
-            const int sy = lane / lpr, st = lane - sy * lpr, sal = (cur.c0 - 1) & 3;
+            const int sy = small_div(lane, lpr), st = lane - sy * lpr, sal = (cur.c0 - 1) & 3;
             uint32_t* s32w = (uint32_t*)s_img;
             uint32_t* s32z = (uint32_t*)s_sc;
 #pragma unroll
@@ -524,7 +532,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
             uint32_t* s_grp = (uint32_t*)((uint8_t*)s_cor + fl.cor) - ng * dh;
             if (ng) {
                 const int rpi = 64 / ng;
-                const int ly = lane / ng, lg = lane - ly * ng;
+                const int ly = small_div(lane, ng), lg = lane - ly * ng;
                 const uint32_t* s32 = (const uint32_t*)s_img;
                 const orbfe_ushort2 tv = {(unsigned short)th, (unsigned short)th};
                 const int valid4 = min(4, dw - 4 * lg);
@@ -1524,7 +1532,7 @@ __global__ __launch_bounds__(ST_NT) void k_stereo(OrbGeom g, StereoSide SL, Ster
     const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
     const int f = lb / gridDim.x;
     const int bL = SL.base + f * SL.step, bR = SR.base + f * SR.step;
-    const int wave = threadIdx.x >> 6, lane = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     const int N = SL.counts[2 * bL], Nr = SR.counts[2 * bR];
     const int i0 = (lb % gridDim.x) * ST_LK;
     if (i0 >= N) return;
