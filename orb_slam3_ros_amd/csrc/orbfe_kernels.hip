@@ -342,6 +342,19 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* const* imgs, int in
 // (k, k+8), k = 0,2,4,6) on all pixels and compacts the candidates; pass 2 scores candidates only.
 // ---------------------------------------------------------------------------------------------
 typedef short orbfe_short2 __attribute__((ext_vector_type(2)));
+// Pixels as f16 1024 + v (bit pattern 0x64XX: byte v under the exponent byte 0x64): every value,
+// threshold offset and difference FAST forms is an integer of magnitude < 2048, exact in f16, and
+// gfx950's 3-input v_pk_minimum3_f16 / v_pk_maximum3_f16 halve the min/max networks.
+typedef _Float16 orbfe_half2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ orbfe_half2 as_h2(uint32_t w) { return __builtin_bit_cast(orbfe_half2, w); }
+__device__ __forceinline__ uint32_t h2_bits(orbfe_half2 h) { return __builtin_bit_cast(uint32_t, h); }
+__device__ __forceinline__ orbfe_half2 hmin(orbfe_half2 a, orbfe_half2 b) { return __builtin_elementwise_minimum(a, b); }
+__device__ __forceinline__ orbfe_half2 hmax(orbfe_half2 a, orbfe_half2 b) { return __builtin_elementwise_maximum(a, b); }
+// bytes 0 and 2 (sel 0x04020400) or 1 and 3 (sel 0x04030401) of w as f16 1024 + byte
+__device__ __forceinline__ orbfe_half2 px_h2(uint32_t w, uint32_t sel) {
+    return as_h2(__builtin_amdgcn_perm(0x64646464u, w, sel));
+}
+
 typedef unsigned short orbfe_ushort2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ orbfe_ushort2 as_us2(uint32_t w) { return __builtin_bit_cast(orbfe_ushort2, w); }
 // M = max over the 16 arcs of 9 contiguous ring pixels of max(min d, min -d), d_k = v - ring_k.
@@ -533,53 +546,58 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
             if (ng) {
                 const int rpi = 64 / ng;
                 const int ly = small_div(lane, ng), lg = lane - ly * ng;
-                const uint32_t* s32 = (const uint32_t*)s_img;
-                const orbfe_ushort2 tv = {(unsigned short)th, (unsigned short)th};
+                const _Float16 tf = (_Float16)th;
+                const orbfe_half2 tv = {tf, tf};
                 const int valid4 = min(4, dw - 4 * lg);
-                const uint32_t vmask = ly < rpi && valid4 > 0 ? (1u << valid4) - 1u : 0u;
+                // flag bits of pixel k: 2k + 1 = dark possible, 2k = bright possible
+                const uint32_t vmask = ly < rpi && valid4 > 0 ? (1u << (2 * valid4)) - 1u : 0u;
                 for (int y0 = 0; y0 < dh; y0 += rpi) {
                     const int y = y0 + ly;
-                    uint32_t dbits = 0, bbits = 0;
+                    uint32_t m8 = 0;
                     if (vmask && y < dh) {
-                        const uint32_t* r0p = s32 + (y + 3) * nd + lg;   // dword q of the centre row
-                        const uint32_t c0w = r0p[0], c1w = r0p[1], c2w = r0p[2];
+                        // centre pixels k = 0..3 at ROI (y + 3, 4 lg + 3 + k) = byte 4 lg + 4 + k of the row
+                        const uint8_t* cp = s_img + (y + 3) * RS + 4 * lg + 4;
+                        const uint32_t cw = *(const uint32_t*)cp;
+                        // aligned dwords + v_alignbyte: unaligned ds_read_b32 measured 40 % slower for the kernel
+                        const uint32_t* r0p = (const uint32_t*)cp - 1;   // dword of ROI columns 4 lg - 1 ..
+                        const uint32_t c0w = r0p[0], c2w = r0p[2];
                         const uint32_t pp[8] = {
-                            r0p[3 * nd + 1],                                                    // 0: (0, 3)
-                            r0p[-3 * nd + 1],                                                   // 8: (0,-3)
-                            __builtin_amdgcn_alignbyte(c2w, c1w, 3),                            // 4: (3, 0)
-                            __builtin_amdgcn_alignbyte(c1w, c0w, 1),                            // 12: (-3, 0)
-                            __builtin_amdgcn_alignbyte(r0p[2 * nd + 2], r0p[2 * nd + 1], 2),    // 2: (2, 2)
-                            __builtin_amdgcn_alignbyte(r0p[-2 * nd + 1], r0p[-2 * nd], 2),      // 10: (-2,-2)
-                            __builtin_amdgcn_alignbyte(r0p[-2 * nd + 2], r0p[-2 * nd + 1], 2),  // 6: (2,-2)
-                            __builtin_amdgcn_alignbyte(r0p[2 * nd + 1], r0p[2 * nd], 2)};       // 14: (-2, 2)
+                            r0p[3 * nd + 1], r0p[-3 * nd + 1],                                            // (0, 3), (0, -3)
+                            __builtin_amdgcn_alignbyte(c2w, cw, 3), __builtin_amdgcn_alignbyte(cw, c0w, 1),  // (3, 0), (-3, 0)
+                            __builtin_amdgcn_alignbyte(r0p[2 * nd + 2], r0p[2 * nd + 1], 2),               // (2, 2)
+                            __builtin_amdgcn_alignbyte(r0p[-2 * nd + 1], r0p[-2 * nd], 2),                 // (-2, -2)
+                            __builtin_amdgcn_alignbyte(r0p[-2 * nd + 2], r0p[-2 * nd + 1], 2),             // (2, -2)
+                            __builtin_amdgcn_alignbyte(r0p[2 * nd + 1], r0p[2 * nd], 2)};                  // (-2, 2)
+                        uint32_t sd[2], sb[2];
 #pragma unroll
                         for (int par = 0; par < 2; par++) {
-                            const uint32_t sel = par ? 0x0c030c01u : 0x0c020c00u;
-                            const orbfe_ushort2 v = as_us2(__builtin_amdgcn_perm(0u, c1w, sel));
-                            const orbfe_ushort2 lo = __builtin_elementwise_sub_sat(v, tv), hi = v + tv;
+                            const uint32_t sel = par ? 0x04030401u : 0x04020400u;
+                            const orbfe_half2 v = px_h2(cw, sel);
                             // dark possible  <=> every pair has a member < v - t <=> max_k min(pair k) < v - t
                             // bright possible <=> every pair has a member > v + t <=> min_k max(pair k) > v + t
-                            orbfe_ushort2 D = {0, 0}, B = {0xffff, 0xffff};
+                            orbfe_half2 mn[4], mx[4];
 #pragma unroll
                             for (int k = 0; k < 4; k++) {
-                                const orbfe_ushort2 xa = as_us2(__builtin_amdgcn_perm(0u, pp[2 * k], sel));
-                                const orbfe_ushort2 xb = as_us2(__builtin_amdgcn_perm(0u, pp[2 * k + 1], sel));
-                                D = __builtin_elementwise_max(D, __builtin_elementwise_min(xa, xb));
-                                B = __builtin_elementwise_min(B, __builtin_elementwise_max(xa, xb));
+                                const orbfe_half2 xa = px_h2(pp[2 * k], sel), xb = px_h2(pp[2 * k + 1], sel);
+                                mn[k] = hmin(xa, xb);
+                                mx[k] = hmax(xa, xb);
                             }
-                            const orbfe_ushort2 sd = __builtin_elementwise_sub_sat(lo, D);
-                            const orbfe_ushort2 sb = __builtin_elementwise_sub_sat(B, hi);
-                            dbits |= (sd.x ? 1u : 0u) << par;
-                            dbits |= (sd.y ? 1u : 0u) << (2 + par);
-                            bbits |= (sb.x ? 1u : 0u) << par;
-                            bbits |= (sb.y ? 1u : 0u) << (2 + par);
+                            const orbfe_half2 D = hmax(hmax(hmax(mn[0], mn[1]), mn[2]), mn[3]);
+                            const orbfe_half2 B = hmin(hmin(hmin(mx[0], mx[1]), mx[2]), mx[3]);
+                            // exact differences: the sign bit of each half is the flag
+                            sd[par] = h2_bits(D - (v - tv));
+                            sb[par] = h2_bits((v + tv) - B);
                         }
-                        dbits &= vmask;
-                        bbits &= vmask;
+                        // sign bytes -> pixel order (byte k = pixel k), dark at bit 7, bright at bit 6,
+                        // then gathered into bits 2k + 1 / 2k by one dot product
+                        const uint32_t A = __builtin_amdgcn_perm(sd[1], sd[0], 0x07030501u);
+                        const uint32_t Bq = __builtin_amdgcn_perm(sb[1], sb[0], 0x07030501u);
+                        const uint32_t F = (A & 0x80808080u) | ((Bq >> 1) & 0x40404040u);
+                        m8 = __builtin_amdgcn_udot4(F >> 6, 0x40100401u, 0u, false) & vmask;
                     }
                     // 4-pixel groups with any candidate, compacted row-major (iteration-major,
-                    // then lane order): dy << 7 | dx0 in bits 0-13, dark bits 16-19, bright 20-23
-                    const uint32_t m8 = dbits | (bbits << 4);
+                    // then lane order): dy << 7 | dx0 in bits 0-13, flags in bits 16-23 (pixel k:
+                    // bit 17 + 2k dark, 16 + 2k bright)
                     const unsigned long long gm = __ballot(m8 != 0u);
                     if (m8)
                         s_grp[ngrp + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(gm >> 32),
@@ -607,7 +625,6 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
                 {
                     const int gi = g0 + lane;
                     const uint32_t rec = gi < ngrp ? s_grp[gi] : 0u;
-                    const uint32_t dbits = (rec >> 16) & 15u, bbits = rec >> 20;
                     const int cnt = __popc(rec >> 16);   // <= 8: scan by bit planes
                     const unsigned long long lt = (1ull << lane) - 1ull;
                     const unsigned long long m0 = __ballot(cnt & 1), m1 = __ballot(cnt & 2), m2 = __ballot(cnt & 4),
@@ -615,7 +632,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
                     int pos = __popcll(m0 & lt) + 2 * __popcll(m1 & lt) + 4 * __popcll(m2 & lt) + 8 * __popcll(m3 & lt);
                     const int packed = (int)(rec & 0x3FFFu);
                     for (int i = 0; i < 4; i++) {
-                        const uint32_t di = (dbits >> i) & 1u, bi = (bbits >> i) & 1u;
+                        const uint32_t di = (rec >> (17 + 2 * i)) & 1u, bi = (rec >> (16 + 2 * i)) & 1u;
                         if (di) s_ent[pos++] = (uint16_t)(packed + i);
                         if (bi) s_ent[pos++] = (uint16_t)((packed + i) | 0x4000 | (di << 15));
                     }
@@ -623,8 +640,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
                 }
                 WAVE_SYNC();
                 // pass 2: exact score M - 1 (corner iff M > th) of each entry for its sign only, two
-                // entries per lane in packed u16x2 (saturated differences: an arc with a negative
-                // minimum never decides a corner)
+                // entries per lane in packed f16 (pixels as 1024 + v, exact signed differences)
                 for (int j0 = 0; j0 < nent; j0 += 128) {
                     const int j = j0 + 2 * lane;
                     const uint32_t e2 = j < nent ? ((const uint32_t*)s_ent)[j >> 1] : 0u;
@@ -632,30 +648,33 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
                     const uint32_t e0 = e2 & 0xFFFFu, e1 = ok1 ? e2 >> 16 : e0;
                     const uint8_t* q0 = s_px + (((e0 >> 7) & 127) + 3) * RS + (e0 & 127) + 3;
                     const uint8_t* q1 = s_px + (((e1 >> 7) & 127) + 3) * RS + (e1 & 127) + 3;
-                    const uint32_t v2 = (uint32_t)q0[0] | ((uint32_t)q1[0] << 16);
-                    const uint32_t bmask = ((e0 & 0x4000u) ? 0x0000FFFFu : 0u) | ((e1 & 0x4000u) ? 0xFFFF0000u : 0u);
-                    orbfe_ushort2 P[16];
+                    const uint32_t v2 = (uint32_t)q0[0] | ((uint32_t)q1[0] << 16) | 0x64006400u;
+                    // f16 sign flip of the bright halves: x - v = -(v - x)
+                    const uint32_t bmask = ((e0 & 0x4000u) ? 0x00008000u : 0u) | ((e1 & 0x4000u) ? 0x80000000u : 0u);
+                    orbfe_half2 P[16];
 #pragma unroll
                     for (int k = 0; k < 16; k++) {
                         const int o = kRingDy[k] * RS + kRingDx[k];
-                        const orbfe_ushort2 x2 = as_us2((uint32_t)q0[o] | ((uint32_t)q1[o] << 16));
-                        const uint32_t dk = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(as_us2(v2), x2));
-                        const uint32_t bk = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(x2, as_us2(v2)));
-                        P[k] = as_us2((bk & bmask) | (dk & ~bmask));
+                        const uint32_t x2 = (uint32_t)q0[o] | ((uint32_t)q1[o] << 16) | 0x64006400u;
+                        P[k] = as_h2(h2_bits(as_h2(v2) - as_h2(x2)) ^ bmask);
                     }
-                    orbfe_ushort2 m2[16], m4[16];
+                    // M = max over the 16 arcs of the arc minimum (signed: an arc with a minimum <= 0
+                    // never makes a corner, th >= 0)
+                    orbfe_half2 m2[16], m4[16], m9[16];
 #pragma unroll
-                    for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(P[k], P[(k + 1) & 15]);
+                    for (int k = 0; k < 16; k++) m2[k] = hmin(P[k], P[(k + 1) & 15]);
 #pragma unroll
-                    for (int k = 0; k < 16; k++) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
-                    orbfe_ushort2 best = {0, 0};
+                    for (int k = 0; k < 16; k++) m4[k] = hmin(m2[k], m2[(k + 2) & 15]);
 #pragma unroll
-                    for (int k = 0; k < 16; k++)
-                        best = __builtin_elementwise_max(
-                            best, __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]), P[(k + 8) & 15]));
-                    const bool c0 = ok0 && (int)best.x > th, c1 = ok1 && (int)best.y > th;
-                    if (c0) s_sc[(((e0 >> 7) & 127) + 1) * RS + (e0 & 127) + 1] = (uint8_t)(best.x - 1);
-                    if (c1) s_sc[(((e1 >> 7) & 127) + 1) * RS + (e1 & 127) + 1] = (uint8_t)(best.y - 1);
+                    for (int k = 0; k < 16; k++) m9[k] = hmin(hmin(m4[k], m4[(k + 4) & 15]), P[(k + 8) & 15]);
+#pragma unroll
+                    for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+                        for (int k = 0; k < w; k++) m9[k] = hmax(m9[k], m9[k + w]);
+                    const int bx = (int)(float)m9[0].x, by = (int)(float)m9[0].y;
+                    const bool c0 = ok0 && bx > th, c1 = ok1 && by > th;
+                    if (c0) s_sc[(((e0 >> 7) & 127) + 1) * RS + (e0 & 127) + 1] = (uint8_t)(bx - 1);
+                    if (c1) s_sc[(((e1 >> 7) & 127) + 1) * RS + (e1 & 127) + 1] = (uint8_t)(by - 1);
                     const int cc = (int)c0 + (int)c1;
                     const unsigned long long lt = (1ull << lane) - 1ull;
                     const unsigned long long b0 = __ballot(cc & 1), b1 = __ballot(cc & 2);
