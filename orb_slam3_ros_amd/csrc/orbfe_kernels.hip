@@ -342,17 +342,18 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* const* imgs, int in
 // (k, k+8), k = 0,2,4,6) on all pixels and compacts the candidates; pass 2 scores candidates only.
 // ---------------------------------------------------------------------------------------------
 typedef short orbfe_short2 __attribute__((ext_vector_type(2)));
-// Pixels as f16 1024 + v (bit pattern 0x64XX: byte v under the exponent byte 0x64): every value,
-// threshold offset and difference FAST forms is an integer of magnitude < 2048, exact in f16, and
-// gfx950's 3-input v_pk_minimum3_f16 / v_pk_maximum3_f16 halve the min/max networks.
+// Pixels as f16 denormals v * 2^-24 (the u16 bit pattern of the byte; the kernels keep f16
+// denormals, float_denorm_mode_16_64 = 3): every value, threshold offset and difference FAST forms
+// is an integer multiple of 2^-24 below 2048 * 2^-24, exact in f16, and gfx950's 3-input
+// v_pk_minimum3_f16 / v_pk_maximum3_f16 halve the min/max networks.
 typedef _Float16 orbfe_half2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ orbfe_half2 as_h2(uint32_t w) { return __builtin_bit_cast(orbfe_half2, w); }
 __device__ __forceinline__ uint32_t h2_bits(orbfe_half2 h) { return __builtin_bit_cast(uint32_t, h); }
 __device__ __forceinline__ orbfe_half2 hmin(orbfe_half2 a, orbfe_half2 b) { return __builtin_elementwise_minimum(a, b); }
 __device__ __forceinline__ orbfe_half2 hmax(orbfe_half2 a, orbfe_half2 b) { return __builtin_elementwise_maximum(a, b); }
-// bytes 0 and 2 (sel 0x04020400) or 1 and 3 (sel 0x04030401) of w as f16 1024 + byte
+// bytes 0 and 2 (sel 0x0c020c00) or 1 and 3 (sel 0x0c030c01) of w as f16 byte * 2^-24
 __device__ __forceinline__ orbfe_half2 px_h2(uint32_t w, uint32_t sel) {
-    return as_h2(__builtin_amdgcn_perm(0x64646464u, w, sel));
+    return as_h2(__builtin_amdgcn_perm(0u, w, sel));
 }
 
 typedef unsigned short orbfe_ushort2 __attribute__((ext_vector_type(2)));
@@ -546,7 +547,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
             if (ng) {
                 const int rpi = 64 / ng;
                 const int ly = small_div(lane, ng), lg = lane - ly * ng;
-                const _Float16 tf = (_Float16)th;
+                const _Float16 tf = __builtin_bit_cast(_Float16, (unsigned short)th);   // th * 2^-24
                 const orbfe_half2 tv = {tf, tf};
                 const int valid4 = min(4, dw - 4 * lg);
                 // flag bits of pixel k: 2k + 1 = dark possible, 2k = bright possible
@@ -571,7 +572,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
                         uint32_t sd[2], sb[2];
 #pragma unroll
                         for (int par = 0; par < 2; par++) {
-                            const uint32_t sel = par ? 0x04030401u : 0x04020400u;
+                            const uint32_t sel = par ? 0x0c030c01u : 0x0c020c00u;
                             const orbfe_half2 v = px_h2(cw, sel);
                             // dark possible  <=> every pair has a member < v - t <=> max_k min(pair k) < v - t
                             // bright possible <=> every pair has a member > v + t <=> min_k max(pair k) > v + t
@@ -648,15 +649,22 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
                     const uint32_t e0 = e2 & 0xFFFFu, e1 = ok1 ? e2 >> 16 : e0;
                     const uint8_t* q0 = s_px + (((e0 >> 7) & 127) + 3) * RS + (e0 & 127) + 3;
                     const uint8_t* q1 = s_px + (((e1 >> 7) & 127) + 3) * RS + (e1 & 127) + 3;
-                    const uint32_t v2 = (uint32_t)q0[0] | ((uint32_t)q1[0] << 16) | 0x64006400u;
-                    // f16 sign flip of the bright halves: x - v = -(v - x)
+                    // the two entries' pixels as one u16x2 = f16 denormals v * 2^-24 (f16 denormals are
+                    // kept, float_denorm_mode_16_64 = 3; every sum / difference here is exact)
+                    const orbfe_half2 v2 = as_h2(__builtin_bit_cast(uint32_t, orbfe_ushort2{q0[0], q1[0]}));
+                    // d = s (v - x) with s = +1 (dark) / -1 (bright) per half, one exact fma per ring pixel
                     const uint32_t bmask = ((e0 & 0x4000u) ? 0x00008000u : 0u) | ((e1 & 0x4000u) ? 0x80000000u : 0u);
+                    const orbfe_half2 ns = as_h2(0xBC00BC00u ^ bmask);   // -s
+                    const orbfe_half2 sv = as_h2(h2_bits(v2) ^ bmask);   // s v
+                    // ring reads from the top-left corner of the 7x7 box: non-negative immediate offsets
+                    const uint8_t* t0 = q0 - 3 * RS - 3;
+                    const uint8_t* t1 = q1 - 3 * RS - 3;
                     orbfe_half2 P[16];
 #pragma unroll
                     for (int k = 0; k < 16; k++) {
-                        const int o = kRingDy[k] * RS + kRingDx[k];
-                        const uint32_t x2 = (uint32_t)q0[o] | ((uint32_t)q1[o] << 16) | 0x64006400u;
-                        P[k] = as_h2(h2_bits(as_h2(v2) - as_h2(x2)) ^ bmask);
+                        const int o = (kRingDy[k] + 3) * RS + kRingDx[k] + 3;
+                        const orbfe_half2 x2 = as_h2(__builtin_bit_cast(uint32_t, orbfe_ushort2{t0[o], t1[o]}));
+                        P[k] = __builtin_elementwise_fma(x2, ns, sv);
                     }
                     // M = max over the 16 arcs of the arc minimum (signed: an arc with a minimum <= 0
                     // never makes a corner, th >= 0)
@@ -671,7 +679,10 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
                     for (int w = 8; w >= 1; w >>= 1)
 #pragma unroll
                         for (int k = 0; k < w; k++) m9[k] = hmax(m9[k], m9[k + w]);
-                    const int bx = (int)(float)m9[0].x, by = (int)(float)m9[0].y;
+                    // M as an integer: the bits of a non-negative denormal; negative -> no corner
+                    const uint32_t mb = h2_bits(m9[0]);
+                    const int bx = (mb & 0x8000u) ? -1 : (int)(mb & 0x7fffu);
+                    const int by = (mb & 0x80000000u) ? -1 : (int)((mb >> 16) & 0x7fffu);
                     const bool c0 = ok0 && bx > th, c1 = ok1 && by > th;
                     if (c0) s_sc[(((e0 >> 7) & 127) + 1) * RS + (e0 & 127) + 1] = (uint8_t)(bx - 1);
                     if (c1) s_sc[(((e1 >> 7) & 127) + 1) * RS + (e1 & 127) + 1] = (uint8_t)(by - 1);
