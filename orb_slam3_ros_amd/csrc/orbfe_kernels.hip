@@ -157,20 +157,22 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t* const* imgs, int 
     const int nitems = nsr * nsc4;
     const bool aligned = ((spitch & 3) == 0) && ((((uintptr_t)src) & 3) == 0);
     // this thread's output column for the horizontal pass and the row coefficients
-    const int hx = t % TC, hr0 = t / TC, hstep = 256 / TC;
+    const int hr0 = small_div(t, TC), hx = t - hr0 * TC, hstep = small_div(256, TC);
     const int hdx = min(x0 + hx, x1 - 1);
     const int hsx = tx[3 * hdx] - sc0, ha0 = tx[3 * hdx + 1], ha1 = tx[3 * hdx + 2];
     const bool hlin = hdx < L.xmax;
     int tyv = 0;
     if (t < 4 * (y1 - y0)) tyv = ty[4 * y0 + t];
-    // (A) window: item i = (r, c) with r = i / nsc4 (float reciprocal is exact for i < 2^16)
-    const float inv_n = 1.0f / (float)nsc4;
+    // (A) window: item i = (r, c) with r = i / nsc4 (reciprocal-exact for i < 2^16); rows < 2^12 and
+    // pitches < 2^13, so the offsets are 24-bit products
     uint32_t v[RZ_LD];
+    int lds_off[RZ_LD];
 #pragma unroll
     for (int u = 0; u < RZ_LD; u++) {
         const int i = min(t + 256 * u, nitems - 1);
-        const int r = (int)(((float)i + 0.5f) * inv_n), c = i - r * nsc4;
-        gptr_u8 sp = src + (size_t)(sr0 + r) * spitch + sc0 + 4 * c;
+        const int r = small_div(i, nsc4), c = i - (int)__umul24((uint32_t)r, (uint32_t)nsc4);
+        lds_off[u] = (int)__umul24((uint32_t)r, RZ_SCB) + 4 * c;
+        gptr_u8 sp = src + __umul24((uint32_t)(sr0 + r), (uint32_t)spitch) + sc0 + 4 * c;
         if (aligned) {
             v[u] = *(gptr_u32)sp;
         } else {
@@ -181,13 +183,8 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t* const* imgs, int 
         }
     }
 #pragma unroll
-    for (int u = 0; u < RZ_LD; u++) {
-        const int i = t + 256 * u;
-        if (i < nitems) {
-            const int r = (int)(((float)i + 0.5f) * inv_n), c = i - r * nsc4;
-            *(uint32_t*)&s_src[r][4 * c] = v[u];
-        }
-    }
+    for (int u = 0; u < RZ_LD; u++)
+        if (t + 256 * u < nitems) *(uint32_t*)(&s_src[0][0] + lds_off[u]) = v[u];
     if (t < 4 * (y1 - y0)) (&s_ty[0][0])[t] = tyv;
     SYNC();
     // (B) horizontal pass
@@ -203,25 +200,38 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t* const* imgs, int 
     }
     SYNC();
     // (C) vertical pass: thread -> (row lane, 4-column group)
-    const int ng = TC >> 2, cg = t % ng, rl = t / ng, rstep = 256 / ng;
+    const int ng = TC >> 2, rl = small_div(t, ng), cg = t - rl * ng, rstep = small_div(256, ng);
     const int xq = x0 + 4 * cg;
     if (rl >= rstep || xq >= x1) return;
+    // columns < simd_end take the universal-intrinsic rounding; a 4-column group is almost always
+    // entirely on one side (one wave-uniform branch, no per-column divergence)
+    const bool all_vec = xq + 3 < L.simd_end;
     bool vec[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) vec[q] = xq + q < L.simd_end;
     for (int dy = y0 + rl; dy < y1; dy += rstep) {
         const int* tyr = s_ty[dy - y0];
-        const int r0 = tyr[0] - sr0, r1 = tyr[1] - sr0, b0 = tyr[2], b1 = tyr[3];
+        const int r0 = tyr[0] - sr0, r1 = tyr[1] - sr0;
+        const uint32_t b0 = (uint32_t)tyr[2], b1 = (uint32_t)tyr[3];   // coefficients in [0, 2048]
         const int4 H0 = *(const int4*)&s_h[r0][4 * cg];
         const int4 H1 = *(const int4*)&s_h[r1][4 * cg];
-        const int h0[4] = {H0.x, H0.y, H0.z, H0.w}, h1[4] = {H1.x, H1.y, H1.z, H1.w};
+        const uint32_t h0[4] = {(uint32_t)H0.x, (uint32_t)H0.y, (uint32_t)H0.z, (uint32_t)H0.w};
+        const uint32_t h1[4] = {(uint32_t)H1.x, (uint32_t)H1.y, (uint32_t)H1.z, (uint32_t)H1.w};
+        // H <= 255 * 2048 < 2^20 and b <= 2^11: 24-bit multiplies are exact, every sum < 2^31
         uint32_t packed = 0;
+        if (all_vec) {
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            int vv;
-            if (vec[q]) vv = ((((h0[q] >> 4) * b0) >> 16) + (((h1[q] >> 4) * b1) >> 16) + 2) >> 2;
-            else vv = (h0[q] * b0 + h1[q] * b1 + (1 << 21)) >> 22;
-            packed |= (uint32_t)sat_u8(vv) << (8 * q);
+            for (int q = 0; q < 4; q++) {
+                const uint32_t vv = ((__umul24(h0[q] >> 4, b0) >> 16) + (__umul24(h1[q] >> 4, b1) >> 16) + 2) >> 2;
+                packed |= min(vv, 255u) << (8 * q);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t vs = ((__umul24(h0[q] >> 4, b0) >> 16) + (__umul24(h1[q] >> 4, b1) >> 16) + 2) >> 2;
+                const uint32_t vl = (__umul24(h0[q], b0) + __umul24(h1[q], b1) + (1u << 21)) >> 22;
+                packed |= min(vec[q] ? vs : vl, 255u) << (8 * q);
+            }
         }
         uint8_t* dp = dst + (size_t)dy * L.pitch + xq;
         if (xq + 4 <= x1) {

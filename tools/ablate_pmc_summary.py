@@ -21,7 +21,7 @@ def main(d):
         seen = set()
         for r in csv.DictReader(open(f[0])):
             k = r["Kernel_Name"].split("(")[0].replace("orbfe::", "")
-            if k not in ("k_fast", "k_describe"):
+            if not k.startswith("k_"):
                 continue
             acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
             key = (k, r["Dispatch_Id"])
@@ -29,7 +29,7 @@ def main(d):
                 seen.add(key)
                 n[k] += 1
         rows[os.path.basename(m)] = {k: {c: v / n[k] for c, v in acc[k].items()} for k in acc}
-    for k in ("k_fast", "k_describe"):
+    for k in sorted({k for r in rows.values() for k in r}):
         print(k)
         prev = None
         for mode in sorted(rows):
