@@ -127,11 +127,15 @@ __device__ __forceinline__ uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : 
 // (B) the horizontal pass H = S[sx]*a0 + S[sx+1]*a1 (exact int) runs once per (source row,
 // output column) into LDS, (C) every thread finishes 4 adjacent output pixels of a row from two
 // 16-byte H reads and stores them with one dword store.
-#define RZ_TR 32
+#ifndef RZ_TR
+#define RZ_TR 24
+#define RZ_SR 32              // source rows of a tile window (host-checked)
+#endif
+#ifndef RZ_TC
 #define RZ_TC 128
-#define RZ_SR 42              // source rows of a tile window (host-checked)
 #define RZ_SCB 176            // source bytes of a tile window row (host-checked)
-#define RZ_LD 8               // window dwords per thread: RZ_SR * RZ_SCB / 4 / 256 rounded up
+#endif
+#define RZ_LD ((RZ_SR * RZ_SCB / 4 + 255) / 256)   // window dwords per thread
 __global__ __launch_bounds__(256) void k_resize(const uint8_t* const* imgs, int in_pitch, uint8_t* pyr, int pyr_stride,
                                                 const int16_t* __restrict__ tab, OrbGeom g, int l) {
     __shared__ __attribute__((aligned(16))) uint8_t s_src[RZ_SR][RZ_SCB];
