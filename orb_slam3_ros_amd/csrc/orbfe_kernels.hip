@@ -34,6 +34,27 @@ namespace orbfe {
     } while (0)
 
 __constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+// IC_Angle disc as byte masks: row v = -15..15 of the 43x43 describe patch (centre column 21),
+// dwords 1..9 of the 48-byte row (columns 4..39); byte = 0xFF iff |column - 21| <= umax[|v|]
+// (ORBextractor.cc:451-468 umax, :76-103 disc). 12 dwords per row (16-byte aligned rows).
+struct IcMaskTab { uint32_t m[31][12]; };
+constexpr IcMaskTab make_ic_mask() {
+    IcMaskTab t{};
+    constexpr int um[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+    for (int vi = 0; vi < 31; vi++) {
+        const int d = um[vi < 15 ? 15 - vi : vi - 15];
+        for (int j = 0; j < 9; j++) {
+            uint32_t w = 0;
+            for (int b = 0; b < 4; b++) {
+                const int u = 4 * (j + 1) + b - 21;
+                if (u >= -d && u <= d) w |= 0xFFu << (8 * b);
+            }
+            t.m[vi][j] = w;
+        }
+    }
+    return t;
+}
+__constant__ IcMaskTab c_ic_mask = make_ic_mask();
 __constant__ signed char c_pattern[ORBFE_PATTERN_PAIRS * 4] = ORBFE_BRIEF_PATTERN_INIT;
 constexpr int kRingDx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
 constexpr int kRingDy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
@@ -1356,15 +1377,17 @@ __device__ __forceinline__ DescSlot desc_slot(const uint8_t* const* imgs, int in
     return d;
 }
 // Patch dwords of an interior slot (dword it = row it / 12, column group it % 12; lo | hi realign)
+// Patch dwords of an interior slot: lanes 0..59 = 5 rows x 12 dwords, iteration u covers rows
+// 5u .. 5u + 4 (lo | hi realign to the patch origin); rows past 42 re-read row 42 (not stored)
 __device__ __forceinline__ void desc_load(const DescSlot& d, int lane, uint32_t (&lo)[9], uint32_t (&hi)[9]) {
-    const int py0 = d.y - DP_R;
+    const int r0 = min(small_div(lane, 12), 4), k = lane - 12 * small_div(lane, 12);
+    gptr_u8 b0 = d.im + (size_t)(d.y - DP_R) * d.pitch + d.gx0 + 4 * k;
 #pragma unroll
     for (int u = 0; u < 9; u++) {
-        const int it = min(lane + 64 * u, DP_ND - 1);
-        const int r = it / (DP_RAW_S / 4), k = it - r * (DP_RAW_S / 4);
-        gptr_u32 rp = (gptr_u32)(d.im + (size_t)(py0 + r) * d.pitch + d.gx0) + k;
-        lo[u] = rp[0];
-        hi[u] = rp[1];
+        const uint32_t row = (uint32_t)min(r0 + 5 * u, DP_N - 1);
+        gptr_u32 q = (gptr_u32)(b0 + __umul24(row, (uint32_t)d.pitch));
+        lo[u] = q[0];
+        hi[u] = q[1];
     }
 }
 // IC_Angle + Gaussian + rBRIEF of one slot whose raw patch is staged in `raw`; writes the
@@ -1394,20 +1417,29 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
         emit_kp(0.f);
         return;
     }
-    // ---- IC_Angle on the unblurred patch, centre (21, 21) ----
-    const uint8_t* center = raw + DP_R * DP_RAW_S + DP_R;
-    const int u = (lane & 31) - 15;
+    // ---- IC_Angle on the unblurred patch, centre (21, 21): lane v + 15 sums disc row v with
+    // two v_dot4 per dword: m10 = sum (u + 16) I - 16 sum I, m01 = sum v * sum I (exact integers,
+    // the reference's sums in another order) ----
     int m10 = 0, m01 = 0;
-    if ((lane & 31) < 31) {
-        const int v0 = lane < 32 ? 1 : 9, v1 = lane < 32 ? 8 : 15;
-        if (lane < 32) m10 += u * (int)center[u];
-        for (int v = v0; v <= v1; v++) {
-            if (u >= -c_umax[v] && u <= c_umax[v]) {
-                const int vp = center[u + v * DP_RAW_S], vm = center[u - v * DP_RAW_S];
-                m10 += u * (vp + vm);
-                m01 += v * (vp - vm);
-            }
+    if (lane < 31) {
+        const uint4* rowp = (const uint4*)(raw + (lane + DP_R - 15) * DP_RAW_S);
+        const uint4* mk = (const uint4*)c_ic_mask.m[lane];
+        const uint4 q0 = rowp[0], q1 = rowp[1], q2 = rowp[2];
+        const uint4 k0 = mk[0], k1 = mk[1], k2 = mk[2];
+        const uint32_t I[9] = {q0.y & k0.x, q0.z & k0.y, q0.w & k0.z, q1.x & k0.w, q1.y & k1.x,
+                               q1.z & k1.y, q1.w & k1.z, q2.x & k1.w, q2.y & k2.x};
+        uint32_t s1 = 0, su = 0;
+#pragma unroll
+        for (int j = 0; j < 9; j++) {
+            // byte b of dword j is column 4 (j + 1) + b: weight u + 16 = 4 j + b - 1 (0 for the
+            // never-in-disc column 4)
+            const uint32_t w = (j == 0 ? 0u : (uint32_t)(4 * j - 1)) | ((uint32_t)(4 * j) << 8) |
+                               ((uint32_t)(4 * j + 1) << 16) | ((uint32_t)(4 * j + 2) << 24);
+            s1 = __builtin_amdgcn_udot4(I[j], 0x01010101u, s1, false);
+            su = __builtin_amdgcn_udot4(I[j], w, su, false);
         }
+        m10 = (int)su - 16 * (int)s1;
+        m01 = (lane - 15) * (int)s1;
     }
     m10 = wave_sum(m10);
     m01 = wave_sum(m01);
@@ -1426,8 +1458,12 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
         // output j of a 4-column group = taps 0-3 . (k0 k1 k2 k3) + taps 4-6 . (k2 k1 k0 0), each a
         // v_dot4_u32_u8 over a byte-aligned window of the 12-byte run w0 w1 w2 (exact: <= 65280)
         const uint32_t KLO = k0 | (k1 << 8) | (k2 << 16) | (k3 << 24), KHI = k2 | (k1 << 8) | (k0 << 16);
-        for (int it = lane; it < DP_N * 10; it += 64) {   // 43 rows x 10 groups of 4 output columns
-            const int r = it / 10, gq = it - r * 10;
+        // 43 rows x 10 groups of 4 output columns: lanes 0..59 = 6 rows x 10 groups, rows r0 + 6 i
+        const int r0 = small_div(lane, 10), gq = lane - 10 * r0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int r = r0 + 6 * i;
+            if (lane >= 60 || r >= DP_N) break;
             const uint32_t* rp = (const uint32_t*)(raw + r * DP_RAW_S) + gq;
             const uint32_t w0 = rp[0], w1 = rp[1], w2 = rp[2];
             uint32_t h[4];
@@ -1512,11 +1548,11 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
     if (d.interior) {
         uint32_t lo[9], hi[9];
         desc_load(d, lane, lo, hi);
+        const int r0 = small_div(lane, 12), k = lane - 12 * r0;
+        uint32_t* wp = (uint32_t*)raw + r0 * (DP_RAW_S / 4) + k;
 #pragma unroll
-        for (int u = 0; u < 9; u++) {
-            const int it = lane + 64 * u;
-            if (it < DP_ND) ((uint32_t*)raw)[it] = __builtin_amdgcn_alignbyte(hi[u], lo[u], (unsigned)d.sh);
-        }
+        for (int u = 0; u < 9; u++)
+            if (lane < 60 && r0 + 5 * u < DP_N) wp[u * 5 * (DP_RAW_S / 4)] = __builtin_amdgcn_alignbyte(hi[u], lo[u], (unsigned)d.sh);
     } else {
         const OrbLevel& L = g.lv[d.l];
         const int px0 = d.x - DP_R, py0 = d.y - DP_R;
