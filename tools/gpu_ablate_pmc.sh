@@ -7,6 +7,7 @@ export TMPDIR=/tmp
 CMD="python bench.py --steps 2 --warmup 1 --stage-steps 1 --no-cpu-baseline --matcher-steps 0 --rectify-steps 0"
 CNT="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_LDS"
 for m in 0 1 2 3; do
-  ORBFE_ABLATE_FAST=$m ORBFE_ABLATE_DESC=$m timeout -k 10 120 rocprofv3 --pmc $CNT --kernel-trace --output-format csv -d gpurun_out/abpmc/m$m -o run -- $CMD > gpurun_out/abpmc/m$m.log 2>&1 || { tail -20 gpurun_out/abpmc/m$m.log; exit 1; }
+  env_fast=$m; env_desc=$m; [ "$ONLY" = desc ] && env_fast=0; [ "$ONLY" = fast ] && env_desc=0
+  ORBFE_ABLATE_FAST=$env_fast ORBFE_ABLATE_DESC=$env_desc timeout -k 10 120 rocprofv3 --pmc $CNT --kernel-trace --output-format csv -d gpurun_out/abpmc/m$m -o run -- $CMD > gpurun_out/abpmc/m$m.log 2>&1 || { tail -20 gpurun_out/abpmc/m$m.log; exit 1; }
 done
 python tools/ablate_pmc_summary.py gpurun_out/abpmc
