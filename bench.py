@@ -107,8 +107,8 @@ def cpu_baseline(pairs_l, pairs_r, w, h, nfeatures, bf, fx):
     oracle.build()
     L = oracle.lib()
     threads = max(1, min(16, os.cpu_count() or 1))
-    # bounded sample: ~10-60 core-seconds of CPU work (the oracle needs ~40 ms per stereo frame per core)
-    n = min(max(400, 100 * threads), 1600)
+    # bounded sample: about 10 s wall on 16 threads (the oracle needs ~40 ms per stereo frame per core)
+    n = min(max(400, 250 * threads), 4000)
     idx = [i % len(pairs_l) for i in range(n)]
     Ls = np.ascontiguousarray(np.stack([pairs_l[i] for i in idx]))
     Rs = np.ascontiguousarray(np.stack([pairs_r[i] for i in idx]))
