@@ -56,6 +56,15 @@ constexpr IcMaskTab make_ic_mask() {
 }
 __constant__ IcMaskTab c_ic_mask = make_ic_mask();
 __constant__ signed char c_pattern[ORBFE_PATTERN_PAIRS * 4] = ORBFE_BRIEF_PATTERN_INIT;
+// the same pattern as floats (pair i = x0, y0, x1, y1 at 4 i): no per-sample int -> float conversion
+struct PatternF { float v[ORBFE_PATTERN_PAIRS * 4]; };
+constexpr PatternF make_pattern_f() {
+    constexpr signed char p[ORBFE_PATTERN_PAIRS * 4] = ORBFE_BRIEF_PATTERN_INIT;
+    PatternF t{};
+    for (int i = 0; i < ORBFE_PATTERN_PAIRS * 4; i++) t.v[i] = (float)p[i];
+    return t;
+}
+__constant__ PatternF c_pattern_f = make_pattern_f();
 constexpr int kRingDx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
 constexpr int kRingDy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
 __constant__ int c_ring_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
@@ -89,6 +98,18 @@ __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
     return v;
+}
+
+// Wave-uniform sum with four DPP steps (row_shr 1, 2, 4, 8 leave each 16-lane row's sum in its
+// lane 15) and four readlanes: 8 VALU instead of the bpermute butterfly's ~18. Every lane must be
+// active.
+__device__ __forceinline__ int wave_sum_dpp(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+    return __builtin_amdgcn_readlane(v, 15) + __builtin_amdgcn_readlane(v, 31) + __builtin_amdgcn_readlane(v, 47) +
+           __builtin_amdgcn_readlane(v, 63);
 }
 
 // In-place exclusive scan of arr[0..n) by ONE wave (the caller's block is that wave). Returns total.
@@ -1393,7 +1414,7 @@ __device__ __forceinline__ void desc_load(const DescSlot& d, int lane, uint32_t 
 // IC_Angle + Gaussian + rBRIEF of one slot whose raw patch is staged in `raw`; writes the
 // keypoint record and the descriptor row.
 __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g, const uint8_t* raw, uint16_t* rowq,
-                                             const uint32_t (&pat)[4], int lane, OrbKeyPoint* kps, uint8_t* desc,
+                                             const float4 (&pat)[4], int lane, OrbKeyPoint* kps, uint8_t* desc,
                                              const BlurKernel& bk, int ablate) {
     const OrbLevel& L = g.lv[d.l];
     const int l = d.l, x = d.x, y = d.y;
@@ -1441,8 +1462,8 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
         m10 = (int)su - 16 * (int)s1;
         m01 = (lane - 15) * (int)s1;
     }
-    m10 = wave_sum(m10);
-    m01 = wave_sum(m01);
+    m10 = wave_sum_dpp(m10);
+    m01 = wave_sum_dpp(m01);
     const float angle = fast_atan2_dev((float)m01, (float)m10);
     if (ablate == 2) {   // + IC_Angle
         asm volatile("" ::"v"(angle));
@@ -1485,10 +1506,34 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
         emit_kp(angle);
         return;
     }
-    // blurred(18 + dy, 18 + dx): column pass over rowq rows 18 + dy .. 24 + dy
-    // (24-bit multiplies are exact here: pair sums <= 2 * 65280, taps <= 256)
-    auto blurred = [&](int dy, int dx) -> int {
-        const uint16_t* col = rowq + __mul24(18 + dy, DP_Q_S) + 18 + dx;
+    // ---- rBRIEF, centre (18, 18) of the blurred window ----
+    const float factorPI = (float)(M_PI / 180.f);
+    const float ang = angle * factorPI;
+    const float a = glibc_cosf(ang), bs = glibc_sinf(ang);
+    // sample (px, py) -> row cvRound(px b + py a), column cvRound(px a - py b) (ORBextractor.cc:117-119):
+    // products in packed f32, then (px b, px a) + (py a, py b) * (1, -1) as one packed fma (the
+    // product with +-1 is exact, so this rounds like the reference's separate add / subtract), then
+    // + 1.5 * 2^23 rounds each sum half-even to an integer (|sum| < 2^22) in the low mantissa bits.
+    // The low 24 bits of the row bits are 2^22 + row, the column bits 0x4B400000 + column: the LDS
+    // byte address of rowq(18 + row, 18 + column), the top tap of the column pass, is one 24-bit
+    // multiply-add and one shift-add, the constant offsets folded into K (mod 2^32).
+    // (__float_as_uint, not __builtin_bit_cast, on the vector elements: this clang folds a bit_cast
+    // of rc.y to rc.x.)
+    typedef float orbfe_f2 __attribute__((ext_vector_type(2)));
+    typedef const __attribute__((address_space(3))) uint16_t* lds_u16p;
+    const orbfe_f2 cs = {bs, a}, sn = {a, bs}, sg = {1.0f, -1.0f}, mag = {12582912.0f, 12582912.0f};
+    const uint32_t S = 2 * DP_Q_S;
+    const uint32_t K = (uint32_t)(uintptr_t)(lds_u16p)rowq + 18u * S + 36u - (1u << 22) * S - 2u * 0x4B400000u;
+    auto sample_addr = [&](float px, float py) -> uint32_t {
+        const orbfe_f2 u = orbfe_f2{px, px} * cs;   // (px b, px a)
+        const orbfe_f2 v = orbfe_f2{py, py} * sn;   // (py a, py b)
+        const orbfe_f2 rc = __builtin_elementwise_fma(v, sg, u) + mag;
+        return __umul24(__float_as_uint(rc.x), S) + 2u * __float_as_uint(rc.y) + K;
+    };
+    // blurred value at a sample: the column pass over rowq rows 18 + row .. 24 + row (24-bit multiplies are
+    // exact here: pair sums <= 2 * 65280, taps <= 256)
+    auto blurred_at = [&](uint32_t ad) -> int {
+        const lds_u16p col = (lds_u16p)(size_t)ad;
         const uint32_t sum = __umul24(k0, (uint32_t)col[0] + col[6 * DP_Q_S]) +
                              __umul24(k1, (uint32_t)col[DP_Q_S] + col[5 * DP_Q_S]) +
                              __umul24(k2, (uint32_t)col[2 * DP_Q_S] + col[4 * DP_Q_S]) +
@@ -1496,18 +1541,12 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
         const uint32_t v = (sum + 32768u) >> 16;
         return (int)(v > 255u ? 255u : v);
     };
-    // ---- rBRIEF, centre (18, 18) of the blurred window ----
-    const float factorPI = (float)(M_PI / 180.f);
-    const float ang = angle * factorPI;
-    const float a = glibc_cosf(ang), bs = glibc_sinf(ang);
     unsigned long long masks[4];
 #pragma unroll
     for (int mm = 0; mm < 4; mm++) {
-        const uint32_t pw = pat[mm];   // pair 64 * mm + lane
-        const float px0f = (float)(int8_t)(pw & 255u), py0f = (float)(int8_t)((pw >> 8) & 255u);
-        const float px1f = (float)(int8_t)((pw >> 16) & 255u), py1f = (float)(int8_t)(pw >> 24);
-        const int t0 = blurred((int)rintf(px0f * bs + py0f * a), (int)rintf(px0f * a - py0f * bs));
-        const int t1 = blurred((int)rintf(px1f * bs + py1f * a), (int)rintf(px1f * a - py1f * bs));
+        const float4 pw = pat[mm];   // pair 64 * mm + lane
+        const int t0 = blurred_at(sample_addr(pw.x, pw.y));
+        const int t1 = blurred_at(sample_addr(pw.z, pw.w));
         masks[mm] = __ballot(t0 < t1);
     }
     if (lane < 4) {
@@ -1530,9 +1569,9 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
     if (flat >= g.out_per_img) return;
     // the rBRIEF pairs of this lane (pair 64 * mm + lane: x0, y0, x1, y1 as signed bytes), issued
     // first so they land while the slot is resolved and its patch loads
-    uint32_t pat[4];
+    float4 pat[4];
 #pragma unroll
-    for (int mm = 0; mm < 4; mm++) pat[mm] = ((const uint32_t*)c_pattern)[64 * mm + lane];
+    for (int mm = 0; mm < 4; mm++) pat[mm] = ((const float4*)c_pattern_f.v)[64 * mm + lane];
     const int* inf = lvinfo + (size_t)b * g.nlevels * 4;
     int ntot = 0, mono_tot = 0;
     for (int k = 0; k < g.nlevels; k++) {
