@@ -1357,8 +1357,9 @@ __device__ __forceinline__ float fast_atan2_dev(float y, float x) {
 #define DP_R 21                      // patch radius: 18 (pattern) + 3 (blur)
 #define DP_N (2 * DP_R + 1)          // 43
 #define DP_RAW_S 48                  // raw row stride (bytes)
-#define DP_Q_S 40                    // Q8 row-pass stride (u16 elements)
-#define DP_WAVE_LDS 5504   // >= 43*48 + 43*40*2, multiple of 16
+#define DP_NP 22                     // row pairs of the Q8 row pass (row 43 is padding)
+#define DP_P_S 40                    // row-pair stride (dwords: one (row 2p, row 2p+1) u16 pair per column)
+#define DP_WAVE_LDS 5600   // >= 43*48 + 22*40*4, multiple of 16
 #define DP_ND (DP_N * (DP_RAW_S / 4))   // 516 patch dwords
 // One output slot of an image (wave-uniform): level, key, output index and the patch geometry.
 struct DescSlot {
@@ -1413,7 +1414,7 @@ __device__ __forceinline__ void desc_load(const DescSlot& d, int lane, uint32_t 
 }
 // IC_Angle + Gaussian + rBRIEF of one slot whose raw patch is staged in `raw`; writes the
 // keypoint record and the descriptor row.
-__device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g, const uint8_t* raw, uint16_t* rowq,
+__device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g, const uint8_t* raw, uint32_t* rowp,
                                              const float4 (&pat)[4], int lane, OrbKeyPoint* kps, uint8_t* desc,
                                              const BlurKernel& bk, int ablate) {
     const OrbLevel& L = g.lv[d.l];
@@ -1479,30 +1480,38 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
         // output j of a 4-column group = taps 0-3 . (k0 k1 k2 k3) + taps 4-6 . (k2 k1 k0 0), each a
         // v_dot4_u32_u8 over a byte-aligned window of the 12-byte run w0 w1 w2 (exact: <= 65280)
         const uint32_t KLO = k0 | (k1 << 8) | (k2 << 16) | (k3 << 24), KHI = k2 | (k1 << 8) | (k0 << 16);
-        // 43 rows x 10 groups of 4 output columns: lanes 0..59 = 6 rows x 10 groups, rows r0 + 6 i
-        const int r0 = small_div(lane, 10), gq = lane - 10 * r0;
+        // row pairs (2 p, 2 p + 1) x 10 groups of 4 output columns: lanes 0..59 = 6 pairs x 10 groups,
+        // pairs p0 + 6 i; the pair is stored as one dword per column (row 2 p low, 2 p + 1 high), one
+        // 16-byte store per group. Row 43 does not exist: its half is 0 (never weighted).
+        const int p0 = small_div(lane, 10), gq = lane - 10 * p0;
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const int r = r0 + 6 * i;
-            if (lane >= 60 || r >= DP_N) break;
-            const uint32_t* rp = (const uint32_t*)(raw + r * DP_RAW_S) + gq;
-            const uint32_t w0 = rp[0], w1 = rp[1], w2 = rp[2];
-            uint32_t h[4];
+        for (int i = 0; i < 4; i++) {
+            const int pr = p0 + 6 * i;
+            if (lane >= 60 || pr >= DP_NP) break;
+            uint32_t h[2][4];
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t lo = j ? __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)j) : w0;
-                const uint32_t hi = j ? __builtin_amdgcn_alignbyte(w2, w1, (uint32_t)j) : w1;
-                h[j] = __builtin_amdgcn_udot4(hi, KHI, __builtin_amdgcn_udot4(lo, KLO, 0u, false), false);
+            for (int e = 0; e < 2; e++) {
+                const uint32_t* rp = (const uint32_t*)(raw + (2 * pr + e) * DP_RAW_S) + gq;
+                const uint32_t w0 = rp[0], w1 = rp[1], w2 = rp[2];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t lo = j ? __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)j) : w0;
+                    const uint32_t hi = j ? __builtin_amdgcn_alignbyte(w2, w1, (uint32_t)j) : w1;
+                    h[e][j] = __builtin_amdgcn_udot4(hi, KHI, __builtin_amdgcn_udot4(lo, KLO, 0u, false), false);
+                }
             }
-            uint2 pk;
-            pk.x = h[0] | (h[1] << 16);
-            pk.y = h[2] | (h[3] << 16);
-            *(uint2*)(rowq + r * DP_Q_S + 4 * gq) = pk;
+            const bool last = 2 * pr + 1 >= DP_N;
+            uint4 pk;
+            pk.x = h[0][0] | (last ? 0u : h[1][0] << 16);
+            pk.y = h[0][1] | (last ? 0u : h[1][1] << 16);
+            pk.z = h[0][2] | (last ? 0u : h[1][2] << 16);
+            pk.w = h[0][3] | (last ? 0u : h[1][3] << 16);
+            *(uint4*)(rowp + pr * DP_P_S + 4 * gq) = pk;
         }
     }
     WAVE_SYNC();
     if (ablate == 3) {   // + Gaussian row pass
-        asm volatile("" ::"v"((int)rowq[lane]), "v"(angle));
+        asm volatile("" ::"v"(rowp[lane]), "v"(angle));
         emit_kp(angle);
         return;
     }
@@ -1513,40 +1522,50 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
     // sample (px, py) -> row cvRound(px b + py a), column cvRound(px a - py b) (ORBextractor.cc:117-119):
     // products in packed f32, then (px b, px a) + (py a, py b) * (1, -1) as one packed fma (the
     // product with +-1 is exact, so this rounds like the reference's separate add / subtract), then
-    // + 1.5 * 2^23 rounds each sum half-even to an integer (|sum| < 2^22) in the low mantissa bits.
-    // The low 24 bits of the row bits are 2^22 + row, the column bits 0x4B400000 + column: the LDS
-    // byte address of rowq(18 + row, 18 + column), the top tap of the column pass, is one 24-bit
-    // multiply-add and one shift-add, the constant offsets folded into K (mod 2^32).
+    // + (1.5 * 2^23 + 18) rounds each sum half-even to an integer (|sum| < 2^22) in the low mantissa
+    // bits: the row bits are 0x4B400000 + R, R = 18 + row the top tap of the column pass, the column
+    // bits 0x4B400000 + C, C = 18 + column. Pair row R >> 1 of rowp holds rows (R & ~1, R | 1), so
+    // pair rows R >> 1 .. (R >> 1) + 3 hold every tap; a byte shift of 2 (R odd) or 0 realigns them
+    // to (R, R+1), (R+2, R+3), (R+4, R+5), (R+6, -) and one v_dot2_u32_u16 per dword sums the taps
+    // with (k0, k1), (k2, k3), (k2, k1), (k0, 0). The LDS byte address (R >> 1) * S + 4 C is one
+    // shift, one 24-bit multiply-add and one shift-add: the 24-bit multiply sees
+    // (0x4B400000 + R) >> 1 as 0xA00000 + (R >> 1), and the constant offsets fold into KC (mod 2^32).
     // (__float_as_uint, not __builtin_bit_cast, on the vector elements: this clang folds a bit_cast
     // of rc.y to rc.x.)
     typedef float orbfe_f2 __attribute__((ext_vector_type(2)));
-    typedef const __attribute__((address_space(3))) uint16_t* lds_u16p;
-    const orbfe_f2 cs = {bs, a}, sn = {a, bs}, sg = {1.0f, -1.0f}, mag = {12582912.0f, 12582912.0f};
-    const uint32_t S = 2 * DP_Q_S;
-    const uint32_t K = (uint32_t)(uintptr_t)(lds_u16p)rowq + 18u * S + 36u - (1u << 22) * S - 2u * 0x4B400000u;
-    auto sample_addr = [&](float px, float py) -> uint32_t {
+    typedef const __attribute__((address_space(3))) uint32_t* lds_u32p;
+    const orbfe_f2 cs = {bs, a}, sn = {a, bs}, sg = {1.0f, -1.0f}, mag = {12582930.0f, 12582930.0f};
+    const uint32_t S = 4 * DP_P_S;
+    const uint32_t KC = (uint32_t)(uintptr_t)(lds_u32p)rowp - 0xA00000u * S - 4u * 0x4B400000u;
+    struct Samp { uint32_t ad, sh; };
+    auto sample_at = [&](float px, float py) -> Samp {
         const orbfe_f2 u = orbfe_f2{px, px} * cs;   // (px b, px a)
         const orbfe_f2 v = orbfe_f2{py, py} * sn;   // (py a, py b)
         const orbfe_f2 rc = __builtin_elementwise_fma(v, sg, u) + mag;
-        return __umul24(__float_as_uint(rc.x), S) + 2u * __float_as_uint(rc.y) + K;
+        const uint32_t rb = __float_as_uint(rc.x), cb = __float_as_uint(rc.y);
+        return Samp{__umul24(rb >> 1, S) + 4u * cb + KC, rb << 1};
     };
-    // blurred value at a sample: the column pass over rowq rows 18 + row .. 24 + row (24-bit multiplies are
-    // exact here: pair sums <= 2 * 65280, taps <= 256)
-    auto blurred_at = [&](uint32_t ad) -> int {
-        const lds_u16p col = (lds_u16p)(size_t)ad;
-        const uint32_t sum = __umul24(k0, (uint32_t)col[0] + col[6 * DP_Q_S]) +
-                             __umul24(k1, (uint32_t)col[DP_Q_S] + col[5 * DP_Q_S]) +
-                             __umul24(k2, (uint32_t)col[2 * DP_Q_S] + col[4 * DP_Q_S]) +
-                             __umul24(k3, (uint32_t)col[3 * DP_Q_S]);
-        const uint32_t v = (sum + 32768u) >> 16;
-        return (int)(v > 255u ? 255u : v);
+    const uint32_t C01 = k0 | (k1 << 16), C23 = k2 | (k3 << 16), C21 = k2 | (k1 << 16), C0 = k0;
+    // blurred value at a sample (exact: every partial sum < 2^32)
+    auto blurred_at = [&](Samp sp) -> uint32_t {
+        const lds_u32p q = (lds_u32p)(size_t)sp.ad;
+        const uint32_t d0 = q[0], d1 = q[DP_P_S], d2 = q[2 * DP_P_S], d3 = q[3 * DP_P_S];
+        // v_alignbyte uses the low 2 bits of the shift: rb << 1 is 2 for odd R, 0 for even
+        const uint32_t a0 = __builtin_amdgcn_alignbyte(d1, d0, sp.sh), a1 = __builtin_amdgcn_alignbyte(d2, d1, sp.sh);
+        const uint32_t a2 = __builtin_amdgcn_alignbyte(d3, d2, sp.sh), a3 = __builtin_amdgcn_alignbyte(0u, d3, sp.sh);
+        uint32_t sum = __builtin_amdgcn_udot2(__builtin_bit_cast(orbfe_ushort2, a0), __builtin_bit_cast(orbfe_ushort2, C01), 32768u, false);
+        sum = __builtin_amdgcn_udot2(__builtin_bit_cast(orbfe_ushort2, a1), __builtin_bit_cast(orbfe_ushort2, C23), sum, false);
+        sum = __builtin_amdgcn_udot2(__builtin_bit_cast(orbfe_ushort2, a2), __builtin_bit_cast(orbfe_ushort2, C21), sum, false);
+        sum = __builtin_amdgcn_udot2(__builtin_bit_cast(orbfe_ushort2, a3), __builtin_bit_cast(orbfe_ushort2, C0), sum, false);
+        const uint32_t v = sum >> 16;
+        return v > 255u ? 255u : v;
     };
     unsigned long long masks[4];
 #pragma unroll
     for (int mm = 0; mm < 4; mm++) {
         const float4 pw = pat[mm];   // pair 64 * mm + lane
-        const int t0 = blurred_at(sample_addr(pw.x, pw.y));
-        const int t1 = blurred_at(sample_addr(pw.z, pw.w));
+        const uint32_t t0 = blurred_at(sample_at(pw.x, pw.y));
+        const uint32_t t1 = blurred_at(sample_at(pw.z, pw.w));
         masks[mm] = __ballot(t0 < t1);
     }
     if (lane < 4) {
@@ -1582,7 +1601,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
     const DescSlot d = desc_slot(imgs, in_pitch, pyr, pyr_stride, g, outkeys, inf, ranks, b, flat, ntot);
     if (!d.valid) return;
     uint8_t* raw = s_dp[wave];
-    uint16_t* rowq = (uint16_t*)(raw + DP_N * DP_RAW_S);
+    uint32_t* rowp = (uint32_t*)(raw + DP_N * DP_RAW_S);
     // ---- stage the raw patch: raw[r][c] = level(y - 21 + r, x - 21 + c), reflect-101 outside ----
     if (d.interior) {
         uint32_t lo[9], hi[9];
@@ -1601,7 +1620,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
         }
     }
     WAVE_SYNC();
-    describe_one(d, g, raw, rowq, pat, lane, kps, desc, bk, ablate);
+    describe_one(d, g, raw, rowp, pat, lane, kps, desc, bk, ablate);
 }
 #undef DP_ND
 
