@@ -1368,27 +1368,54 @@ struct DescSlot {
     size_t o;
     gptr_u8 im;
 };
+// Per-image level table of one wave (k_octree's lvinfo): lane l < nlevels holds level l's
+// (n, nlap, nmono, K); the lapping / non-lapping keys of the levels before l (exclusive prefixes)
+// and the image totals come from DPP scans over the first 16 lanes (nlevels <= 12), no scalar loops.
+struct DescImg {
+    int n, lap_before, mono_before;   // per lane (level = lane)
+    int ntot, mono_tot;               // wave-uniform
+};
+__device__ __forceinline__ int row_incl_scan_dpp(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+    return v;
+}
+__device__ __forceinline__ DescImg desc_img(const OrbGeom& g, const int* __restrict__ inf, int lane) {
+    int4 li = make_int4(0, 0, 0, 0);
+    if (lane < g.nlevels) li = ((const int4*)inf)[lane];
+    DescImg di;
+    di.n = li.x;
+    const int lapi = row_incl_scan_dpp(li.y), monoi = row_incl_scan_dpp(li.z), ni = row_incl_scan_dpp(li.x);
+    di.lap_before = lapi - li.y;
+    di.mono_before = monoi - li.z;
+    di.ntot = __builtin_amdgcn_readlane(ni, 15);
+    di.mono_tot = __builtin_amdgcn_readlane(monoi, 15);
+    return di;
+}
+// Slot `flat` of an image: its level (searched upwards from *lvl: a wave's slots ascend), key and
+// rank (lane j of kv / rv holds those of the wave's slot j).
 __device__ __forceinline__ DescSlot desc_slot(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
-                                              int pyr_stride, const OrbGeom& g, const uint32_t* __restrict__ outkeys,
-                                              const int* __restrict__ inf, const int* __restrict__ ranks, int b,
-                                              int flat, int ntot) {
+                                              int pyr_stride, const OrbGeom& g, const DescImg& di, uint32_t kv,
+                                              int rv, int j, int* lvl, int b, int flat) {
     DescSlot d;
     d.valid = 0;
     if (flat >= g.out_per_img) return d;
-    int l = 0;
+    int l = *lvl;
     while (l + 1 < g.nlevels && flat >= g.lv[l + 1].out_off) l++;
+    *lvl = l;
     const OrbLevel& L = g.lv[l];
-    if (flat - L.out_off >= inf[4 * l]) return d;
-    int lap_before = 0, mono_before = 0;
-    for (int k = 0; k < l; k++) { lap_before += inf[4 * k + 1]; mono_before += inf[4 * k + 2]; }
+    if (flat - L.out_off >= __builtin_amdgcn_readlane(di.n, l)) return d;
     d.valid = 1;
     d.l = l;
-    d.key = (uint32_t)__builtin_amdgcn_readfirstlane((int)outkeys[(size_t)b * g.out_per_img + flat]);
+    d.key = (uint32_t)__builtin_amdgcn_readlane((int)kv, j);
     d.x = d.key & 0xfff;
     d.y = (d.key >> 12) & 0xfff;
     // output slot: lapping reorder (ORBextractor.cc:1153-1162)
-    const int rk = __builtin_amdgcn_readfirstlane(ranks[(size_t)b * g.out_per_img + flat]);
-    const int slot = (rk & 0x40000000) ? ntot - 1 - (lap_before + (rk & 0x3fffffff)) : mono_before + rk;
+    const int rk = __builtin_amdgcn_readlane(rv, j);
+    const int slot = (rk & 0x40000000) ? di.ntot - 1 - (__builtin_amdgcn_readlane(di.lap_before, l) + (rk & 0x3fffffff))
+                                       : __builtin_amdgcn_readlane(di.mono_before, l) + rk;
     d.o = (size_t)b * g.kp_cap + slot;
     d.im = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l, &d.pitch);
     const int px0 = d.x - DP_R, py0 = d.y - DP_R;
@@ -1398,18 +1425,33 @@ __device__ __forceinline__ DescSlot desc_slot(const uint8_t* const* imgs, int in
                  ((((uintptr_t)d.im) & 3) == 0);
     return d;
 }
-// Patch dwords of an interior slot (dword it = row it / 12, column group it % 12; lo | hi realign)
-// Patch dwords of an interior slot: lanes 0..59 = 5 rows x 12 dwords, iteration u covers rows
-// 5u .. 5u + 4 (lo | hi realign to the patch origin); rows past 42 re-read row 42 (not stored)
-__device__ __forceinline__ void desc_load(const DescSlot& d, int lane, uint32_t (&lo)[9], uint32_t (&hi)[9]) {
-    const int r0 = min(small_div(lane, 12), 4), k = lane - 12 * small_div(lane, 12);
-    gptr_u8 b0 = d.im + (size_t)(d.y - DP_R) * d.pitch + d.gx0 + 4 * k;
+// Patch of an interior slot as 16-byte chunks of the 48-byte rows from gx0: lane = 3 r + k (k =
+// chunk of the row), load u covers rows 21 u .. 21 u + 20 (lane 63 idle; rows past 42 re-read row
+// 42, not stored). Three dwordx4 loads per lane instead of 18 dword loads.
+typedef uint32_t orbfe_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void desc_load(const DescSlot& d, int lane, orbfe_u32x4 (&q)[3]) {
+    const int r0 = small_div(lane, 3), k = lane - 3 * r0;
+    gptr_u8 b0 = d.im + (size_t)(d.y - DP_R) * d.pitch + d.gx0 + 16 * k;
 #pragma unroll
-    for (int u = 0; u < 9; u++) {
-        const uint32_t row = (uint32_t)min(r0 + 5 * u, DP_N - 1);
-        gptr_u32 q = (gptr_u32)(b0 + __umul24(row, (uint32_t)d.pitch));
-        lo[u] = q[0];
-        hi[u] = q[1];
+    for (int u = 0; u < 3; u++) {
+        const uint32_t row = (uint32_t)min(r0 + 21 * u, DP_N - 1);
+        q[u] = *(const ORBFE_GLOBAL orbfe_u32x4*)(b0 + __umul24(row, (uint32_t)d.pitch));
+    }
+}
+// Realign the chunks to the patch origin (byte shift sh; the fourth dword takes the next lane's
+// first, a DPP wave_shl) and store them as 16-byte rows pieces. The last chunk of a row only needs
+// bytes up to column 42 < 48 - 3, so its neighbour (the next row's chunk) is never used.
+__device__ __forceinline__ void desc_stage(uint8_t* raw, int lane, const orbfe_u32x4 (&q)[3], int sh) {
+    const int r0 = small_div(lane, 3), k = lane - 3 * r0;
+#pragma unroll
+    for (int u = 0; u < 3; u++) {
+        const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q[u].x, 0x130, 0xf, 0xf, false);
+        uint4 w;
+        w.x = __builtin_amdgcn_alignbyte(q[u].y, q[u].x, (uint32_t)sh);
+        w.y = __builtin_amdgcn_alignbyte(q[u].z, q[u].y, (uint32_t)sh);
+        w.z = __builtin_amdgcn_alignbyte(q[u].w, q[u].z, (uint32_t)sh);
+        w.w = __builtin_amdgcn_alignbyte(nx, q[u].w, (uint32_t)sh);
+        if (lane < 63 && r0 + 21 * u < DP_N) *(uint4*)(raw + (r0 + 21 * u) * DP_RAW_S + 16 * k) = w;
     }
 }
 // IC_Angle + Gaussian + rBRIEF of one slot whose raw patch is staged in `raw`; writes the
@@ -1575,6 +1617,10 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
     emit_kp(angle);
 }
 
+#ifndef DP_KPW
+#define DP_KPW 1   // slots per wave (> 1: the next slot's patch loads overlap this slot's compute;
+                   // measured slower at 2, the extra registers cost occupancy)
+#endif
 __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                                   int pyr_stride, OrbGeom g, const uint32_t* __restrict__ outkeys,
                                                   const int* __restrict__ lvinfo, const int* __restrict__ ranks,
@@ -1584,43 +1630,54 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, in
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
     const int b = lb / gridDim.x;
-    const int flat = (lb % gridDim.x) * 4 + wave;   // index over all levels' output slots
-    if (flat >= g.out_per_img) return;
-    // the rBRIEF pairs of this lane (pair 64 * mm + lane: x0, y0, x1, y1 as signed bytes), issued
-    // first so they land while the slot is resolved and its patch loads
+    const int flat0 = ((lb % gridDim.x) * 4 + wave) * DP_KPW;   // first of this wave's output slots
+    if (flat0 >= g.out_per_img) return;
+    // the rBRIEF pairs of this lane (pair 64 * mm + lane: x0, y0, x1, y1), issued first
     float4 pat[4];
 #pragma unroll
     for (int mm = 0; mm < 4; mm++) pat[mm] = ((const float4*)c_pattern_f.v)[64 * mm + lane];
-    const int* inf = lvinfo + (size_t)b * g.nlevels * 4;
-    int ntot = 0, mono_tot = 0;
-    for (int k = 0; k < g.nlevels; k++) {
-        ntot += inf[4 * k];
-        mono_tot += inf[4 * k + 2];
+    // keys and ranks of the wave's slots (lane j: slot flat0 + j), one load each
+    uint32_t kv = 0;
+    int rv = 0;
+    if (lane < DP_KPW && flat0 + lane < g.out_per_img) {
+        kv = outkeys[(size_t)b * g.out_per_img + flat0 + lane];
+        rv = ranks[(size_t)b * g.out_per_img + flat0 + lane];
     }
-    if (flat == 0 && lane == 0) { counts[2 * b] = ntot; counts[2 * b + 1] = mono_tot; }
-    const DescSlot d = desc_slot(imgs, in_pitch, pyr, pyr_stride, g, outkeys, inf, ranks, b, flat, ntot);
-    if (!d.valid) return;
+    const DescImg di = desc_img(g, lvinfo + (size_t)b * g.nlevels * 4, lane);
+    if (flat0 == 0 && lane == 0) { counts[2 * b] = di.ntot; counts[2 * b + 1] = di.mono_tot; }
     uint8_t* raw = s_dp[wave];
     uint32_t* rowp = (uint32_t*)(raw + DP_N * DP_RAW_S);
-    // ---- stage the raw patch: raw[r][c] = level(y - 21 + r, x - 21 + c), reflect-101 outside ----
-    if (d.interior) {
-        uint32_t lo[9], hi[9];
-        desc_load(d, lane, lo, hi);
-        const int r0 = small_div(lane, 12), k = lane - 12 * r0;
-        uint32_t* wp = (uint32_t*)raw + r0 * (DP_RAW_S / 4) + k;
+    int lvl = 0;
+    DescSlot cur = desc_slot(imgs, in_pitch, pyr, pyr_stride, g, di, kv, rv, 0, &lvl, b, flat0);
+    orbfe_u32x4 pq[3];
+    if (cur.valid && cur.interior) desc_load(cur, lane, pq);
 #pragma unroll
-        for (int u = 0; u < 9; u++)
-            if (lane < 60 && r0 + 5 * u < DP_N) wp[u * 5 * (DP_RAW_S / 4)] = __builtin_amdgcn_alignbyte(hi[u], lo[u], (unsigned)d.sh);
-    } else {
-        const OrbLevel& L = g.lv[d.l];
-        const int px0 = d.x - DP_R, py0 = d.y - DP_R;
-        for (int it = lane; it < DP_N * DP_N; it += 64) {
-            const int r = it / DP_N, c = it - r * DP_N;
-            raw[r * DP_RAW_S + c] = d.im[(size_t)reflect101(py0 + r, L.h) * d.pitch + reflect101(px0 + c, L.w)];
+    for (int j = 0; j < DP_KPW; j++) {
+        // ---- stage the raw patch: raw[r][c] = level(y - 21 + r, x - 21 + c), reflect-101 outside ----
+        if (cur.valid) {
+            if (cur.interior) {
+                desc_stage(raw, lane, pq, cur.sh);
+            } else {
+                const OrbLevel& L = g.lv[cur.l];
+                const int px0 = cur.x - DP_R, py0 = cur.y - DP_R;
+                for (int it = lane; it < DP_N * DP_N; it += 64) {
+                    const int r = it / DP_N, c = it - r * DP_N;
+                    raw[r * DP_RAW_S + c] = cur.im[(size_t)reflect101(py0 + r, L.h) * cur.pitch + reflect101(px0 + c, L.w)];
+                }
+            }
         }
+        WAVE_SYNC();
+        // the next slot's patch loads fly while this one is described
+        DescSlot nxt;
+        nxt.valid = 0;
+        if (j + 1 < DP_KPW) {
+            nxt = desc_slot(imgs, in_pitch, pyr, pyr_stride, g, di, kv, rv, j + 1, &lvl, b, flat0 + j + 1);
+            if (nxt.valid && nxt.interior) desc_load(nxt, lane, pq);
+        }
+        if (cur.valid && ablate != 7) describe_one(cur, g, raw, rowp, pat, lane, kps, desc, bk, ablate);
+        WAVE_SYNC();   // the patch area is restaged for the next slot
+        cur = nxt;
     }
-    WAVE_SYNC();
-    describe_one(d, g, raw, rowp, pat, lane, kps, desc, bk, ablate);
 }
 #undef DP_ND
 
