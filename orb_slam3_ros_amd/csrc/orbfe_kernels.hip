@@ -134,6 +134,7 @@ __device__ int wave_excl_scan_lds(int* arr, int n) {
 typedef const ORBFE_GLOBAL uint8_t* gptr_u8;
 typedef const ORBFE_GLOBAL uint32_t* gptr_u32;
 __device__ __forceinline__ gptr_u8 as_global(const uint8_t* p) { return (gptr_u8)p; }
+typedef uint32_t orbfe_u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ gptr_u8 level_base(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                               int pyr_stride, const OrbGeom& g, int b, int l, int* pitch) {
@@ -440,7 +441,7 @@ __device__ __forceinline__ int fast_M(const uint8_t* im, int stride, int x, int 
 }
 
 #define FAST_CPW 4    // cells per wave (the next cell's ROI is prefetched into registers)
-#define FAST_PF 16    // prefetch dwords per lane: ROI rows / rows-per-load (<= 48 / 4 = 12 at W = 35)
+#define FAST_PF 4     // prefetched 16-byte chunks per lane (rows / rows-per-load: 2 at W = 35)
 struct FastCell {
     int l, local, r0, c0, rows, cols, pitch;
     gptr_u8 src;
@@ -466,36 +467,53 @@ __device__ __forceinline__ FastCell fast_cell(const uint8_t* const* imgs, int in
     return f;
 }
 // LDS layout of a cell: rows of RS = 4*ng + 8 bytes (ng = ceil(dw/4) pixel groups), byte j of a
-// row = ROI column j - 1. Lanes load the aligned global dwords covering a row (nd + 1 lanes per
-// row, one dword each); the realigned dword comes from the next lane.
-__device__ __forceinline__ void fast_geom(const FastCell& f, int* ng, int* nd, int* lpr, int* rpl) {
+// row = ROI column j - 1. A row is loaded as cpr 16-byte chunks from the aligned dword A0 =
+// (c0 - 1) & ~3 (cpr = ceil((nd + 1) / 4): the nd LDS dwords plus one for the realignment), one
+// chunk per lane, rpl rows per load; the realigned fourth dword of a chunk takes the next lane's
+// first dword (a DPP wave_shl). Reads end at most 20 bytes past c1 <= w - 16, inside the next row
+// (ROI rows end 17 rows above the last image row).
+__device__ __forceinline__ void fast_geom(const FastCell& f, int* ng, int* nd, int* cpr, int* rpl) {
     const int dw = f.cols - 6, dh = f.rows - 6;
     *ng = (dw > 0 && dh > 0) ? (dw + 3) >> 2 : 0;
     *nd = *ng + 2;
-    *lpr = *nd + 1;
-    *rpl = 64 / *lpr;
+    *cpr = (*nd + 4) >> 2;
+    *rpl = small_div(64, *cpr);
 }
-__device__ __forceinline__ void fast_prefetch(const FastCell& f, int lane, uint32_t (&pf)[FAST_PF]) {
-    int ng, nd, lpr, rpl;
-    fast_geom(f, &ng, &nd, &lpr, &rpl);
+__device__ __forceinline__ orbfe_u32x4 fast_chunk(gptr_u8 rp, bool al) {
+    if (al) return *(const ORBFE_GLOBAL orbfe_u32x4*)rp;
+    orbfe_u32x4 q = {0u, 0u, 0u, 0u};
+    for (int k = 0; k < 16; k++) q[k >> 2] |= (uint32_t)rp[k] << (8 * (k & 3));
+    return q;
+}
+__device__ __forceinline__ void fast_prefetch(const FastCell& f, int lane, orbfe_u32x4 (&pf)[FAST_PF]) {
+    int ng, nd, cpr, rpl;
+    fast_geom(f, &ng, &nd, &cpr, &rpl);
     if (!ng) return;
-    const int sy = small_div(lane, lpr), st = lane - sy * lpr;
+    const int sy = small_div(lane, cpr), st = lane - sy * cpr;
     if (sy >= rpl) return;
     const int A0 = (f.c0 - 1) & ~3;
-    // reads stay inside the row: bytes [c0 - 4, c1 + 7) with c1 <= w - 16
     const bool al = (f.pitch & 3) == 0 && ((((uintptr_t)f.src) & 3) == 0);
-    gptr_u8 base = f.src + (size_t)f.r0 * f.pitch + A0 + 4 * st;
+    gptr_u8 base = f.src + (size_t)f.r0 * f.pitch + A0 + 16 * st;
 #pragma unroll
     for (int u = 0; u < FAST_PF; u++) {
         const int y = sy + u * rpl;
-        if (y < f.rows) {
-            gptr_u8 rp = base + (size_t)y * f.pitch;
-            if (al) {
-                pf[u] = *(gptr_u32)rp;
-            } else {
-                uint32_t a = 0;
-                for (int k = 0; k < 4; k++) a |= (uint32_t)rp[k] << (8 * k);
-                pf[u] = a;
+        if (y < f.rows) pf[u] = fast_chunk(base + (size_t)y * f.pitch, al);
+    }
+}
+// realign a chunk by sal bytes and store its dwords (< nd) to row y of the ROI image; rows of the
+// score map (y < dh + 2) are zeroed alongside
+__device__ __forceinline__ void fast_stage_chunk(uint32_t* s32w, uint32_t* s32z, const orbfe_u32x4& q, int sal,
+                                                 int y, int st, int nd, int dh, bool ok) {
+    const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q.x, 0x130, 0xf, 0xf, false);
+    const uint32_t w[4] = {__builtin_amdgcn_alignbyte(q.y, q.x, (uint32_t)sal), __builtin_amdgcn_alignbyte(q.z, q.y, (uint32_t)sal),
+                           __builtin_amdgcn_alignbyte(q.w, q.z, (uint32_t)sal), __builtin_amdgcn_alignbyte(nx, q.w, (uint32_t)sal)};
+    if (ok) {
+        const int d0 = 4 * st;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            if (d0 + i < nd) {
+                s32w[y * nd + d0 + i] = w[i];
+                if (y < dh + 2) s32z[y * nd + d0 + i] = 0u;
             }
         }
     }
@@ -525,45 +543,35 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
     const int cbeg = (bx * 4 + wave) * FAST_CPW;
     if (cbeg >= g.total_cells) return;
     const int cend = min(cbeg + FAST_CPW, g.total_cells);
-    uint32_t pf[FAST_PF];
+    orbfe_u32x4 pf[FAST_PF];
     FastCell cur = fast_cell(imgs, in_pitch, pyr, pyr_stride, g, b, cbeg);
     fast_prefetch(cur, lane, pf);
     for (int c = cbeg; c < cend; c++) {
-        int ng, nd, lpr, rpl;
-        fast_geom(cur, &ng, &nd, &lpr, &rpl);
+        int ng, nd, cpr, rpl;
+        fast_geom(cur, &ng, &nd, &cpr, &rpl);
         const int dw = cur.cols - 6, dh = cur.rows - 6;
         const int RS = 4 * nd;
-        // stage: realign with the next lane's dword, zero the score map
+        // stage: realign, zero the score map
         if (ng) {
-            const int sy = small_div(lane, lpr), st = lane - sy * lpr, sal = (cur.c0 - 1) & 3;
+            const int sy = small_div(lane, cpr), st = lane - sy * cpr, sal = (cur.c0 - 1) & 3;
             uint32_t* s32w = (uint32_t*)s_img;
             uint32_t* s32z = (uint32_t*)s_sc;
 #pragma unroll
             for (int u = 0; u < FAST_PF; u++) {
-                const uint32_t lo = pf[u];
-                const uint32_t hi = __shfl_down(lo, 1, 64);
                 const int y = sy + u * rpl;
-                if (sy < rpl && st < nd && y < cur.rows) {
-                    s32w[y * nd + st] = __builtin_amdgcn_alignbyte(hi, lo, sal);
-                    if (y < dh + 2) s32z[y * nd + st] = 0u;
-                }
+                fast_stage_chunk(s32w, s32z, pf[u], sal, y, st, nd, dh, sy < rpl && y < cur.rows);
             }
-            // rows beyond the prefetch window (only very wide / tall cells of tiny levels): direct
-            // loads; both lanes of a realignment pair share sy, hence the trip count
-            if (sy < rpl && sy + FAST_PF * rpl < cur.rows) {
+            // rows beyond the prefetch window (only very tall cells of tiny levels): direct loads with a
+            // wave-uniform trip count (the DPP needs every lane)
+            if (FAST_PF * rpl < cur.rows) {
                 const bool al = (cur.pitch & 3) == 0 && ((((uintptr_t)cur.src) & 3) == 0);
-                gptr_u8 base = cur.src + (size_t)cur.r0 * cur.pitch + ((cur.c0 - 1) & ~3) + 4 * st;
-                for (int y = sy + FAST_PF * rpl; y < cur.rows; y += rpl) {
-                    gptr_u8 rp = base + (size_t)y * cur.pitch;
-                    uint32_t lo = 0;
-                    if (al) lo = *(gptr_u32)rp;
-                    else
-                        for (int k = 0; k < 4; k++) lo |= (uint32_t)rp[k] << (8 * k);
-                    const uint32_t hi = __shfl_down(lo, 1, 64);
-                    if (st < nd) {
-                        s32w[y * nd + st] = __builtin_amdgcn_alignbyte(hi, lo, sal);
-                        if (y < dh + 2) s32z[y * nd + st] = 0u;
-                    }
+                gptr_u8 base = cur.src + (size_t)cur.r0 * cur.pitch + ((cur.c0 - 1) & ~3) + 16 * st;
+                for (int y0 = FAST_PF * rpl; y0 < cur.rows; y0 += rpl) {
+                    const int y = y0 + sy;
+                    const bool ok = sy < rpl && y < cur.rows;
+                    orbfe_u32x4 q = {0u, 0u, 0u, 0u};
+                    if (ok) q = fast_chunk(base + (size_t)y * cur.pitch, al);
+                    fast_stage_chunk(s32w, s32z, q, sal, y, st, nd, dh, ok);
                 }
             }
         }
@@ -1428,7 +1436,6 @@ __device__ __forceinline__ DescSlot desc_slot(const uint8_t* const* imgs, int in
 // Patch of an interior slot as 16-byte chunks of the 48-byte rows from gx0: lane = 3 r + k (k =
 // chunk of the row), load u covers rows 21 u .. 21 u + 20 (lane 63 idle; rows past 42 re-read row
 // 42, not stored). Three dwordx4 loads per lane instead of 18 dword loads.
-typedef uint32_t orbfe_u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void desc_load(const DescSlot& d, int lane, orbfe_u32x4 (&q)[3]) {
     const int r0 = small_div(lane, 3), k = lane - 3 * r0;
     gptr_u8 b0 = d.im + (size_t)(d.y - DP_R) * d.pitch + d.gx0 + 16 * k;
