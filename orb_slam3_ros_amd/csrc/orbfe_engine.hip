@@ -250,7 +250,7 @@ static int build_geom(orbfe_extractor* h, int W, int H) {
                 for (int x0 = 0; x0 < L.w; x0 += tc) {
                     const int x1 = std::min(x0 + tc, L.w);
                     const int sc0 = tx[3 * x0] & ~3, sc1 = std::min((int)tx[3 * (x1 - 1)] + 2, pw);
-                    if (round_up(sc1 - sc0, 4) > RZ_SCB) return false;
+                    if (round_up(sc1 - sc0, 16) > RZ_SCB) return false;   // k_resize stores 16-byte chunks
                 }
                 return true;
             };

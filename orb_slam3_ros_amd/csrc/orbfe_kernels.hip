@@ -178,7 +178,7 @@ __device__ __forceinline__ uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : 
 #define RZ_TC 128
 #define RZ_SCB 176            // source bytes of a tile window row (host-checked)
 #endif
-#define RZ_LD ((RZ_SR * RZ_SCB / 4 + 255) / 256)   // window dwords per thread
+#define RZ_LD ((RZ_SR * RZ_SCB / 16 + 255) / 256)  // window 16-byte chunks per thread
 __global__ __launch_bounds__(256) void k_resize(const uint8_t* const* imgs, int in_pitch, uint8_t* pyr, int pyr_stride,
                                                 const int16_t* __restrict__ tab, OrbGeom g, int l) {
     __shared__ __attribute__((aligned(16))) uint8_t s_src[RZ_SR][RZ_SCB];
@@ -200,8 +200,8 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t* const* imgs, int 
     const int sr0 = ty[4 * y0], sr1 = ty[4 * (y1 - 1) + 1];           // source rows [sr0, sr1]
     const int sc0 = tx[3 * x0] & ~3;
     const int sc1 = min((int)tx[3 * (x1 - 1)] + 2, Ps.w);              // source cols [sc0, sc1)
-    const int nsr = sr1 - sr0 + 1, nsc4 = (sc1 - sc0 + 3) >> 2;
-    const int nitems = nsr * nsc4;
+    const int nsr = sr1 - sr0 + 1, nsc16 = (sc1 - sc0 + 15) >> 4;
+    const int nitems = nsr * nsc16;
     const bool aligned = ((spitch & 3) == 0) && ((((uintptr_t)src) & 3) == 0);
     // this thread's output column for the horizontal pass and the row coefficients
     const int hr0 = small_div(t, TC), hx = t - hr0 * TC, hstep = small_div(256, TC);
@@ -210,28 +210,31 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t* const* imgs, int 
     const bool hlin = hdx < L.xmax;
     int tyv = 0;
     if (t < 4 * (y1 - y0)) tyv = ty[4 * y0 + t];
-    // (A) window: item i = (r, c) with r = i / nsc4 (reciprocal-exact for i < 2^16); rows < 2^12 and
-    // pitches < 2^13, so the offsets are 24-bit products
-    uint32_t v[RZ_LD];
+    // (A) window as 16-byte chunks: item i = (r, c) with r = i / nsc16 (reciprocal-exact for
+    // i < 2^16); rows < 2^12 and pitches < 2^13, so the offsets are 24-bit products. A chunk that
+    // would cross the row's pitch (the last one of a row, the source may be the caller's image) is
+    // read as guarded dwords.
+    orbfe_u32x4 v[RZ_LD];
     int lds_off[RZ_LD];
 #pragma unroll
     for (int u = 0; u < RZ_LD; u++) {
         const int i = min(t + 256 * u, nitems - 1);
-        const int r = small_div(i, nsc4), c = i - (int)__umul24((uint32_t)r, (uint32_t)nsc4);
-        lds_off[u] = (int)__umul24((uint32_t)r, RZ_SCB) + 4 * c;
-        gptr_u8 sp = src + __umul24((uint32_t)(sr0 + r), (uint32_t)spitch) + sc0 + 4 * c;
-        if (aligned) {
-            v[u] = *(gptr_u32)sp;
+        const int r = small_div(i, nsc16), c = i - (int)__umul24((uint32_t)r, (uint32_t)nsc16);
+        lds_off[u] = (int)__umul24((uint32_t)r, RZ_SCB) + 16 * c;
+        const int col = sc0 + 16 * c;
+        gptr_u8 sp = src + __umul24((uint32_t)(sr0 + r), (uint32_t)spitch) + col;
+        if (aligned && col + 16 <= spitch) {
+            v[u] = *(const ORBFE_GLOBAL orbfe_u32x4*)sp;
         } else {
-            uint32_t x = 0;
-            for (int k = 0; k < 4; k++)
-                if (sc0 + 4 * c + k < Ps.w) x |= (uint32_t)sp[k] << (8 * k);
+            orbfe_u32x4 x = {0u, 0u, 0u, 0u};
+            for (int k = 0; k < 16; k++)
+                if (col + k < Ps.w) x[k >> 2] |= (uint32_t)sp[k] << (8 * (k & 3));
             v[u] = x;
         }
     }
 #pragma unroll
     for (int u = 0; u < RZ_LD; u++)
-        if (t + 256 * u < nitems) *(uint32_t*)(&s_src[0][0] + lds_off[u]) = v[u];
+        if (t + 256 * u < nitems) *(orbfe_u32x4*)(&s_src[0][0] + lds_off[u]) = v[u];
     if (t < 4 * (y1 - y0)) (&s_ty[0][0])[t] = tyv;
     SYNC();
     // (B) horizontal pass
