@@ -347,7 +347,8 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
     uint8_t* o_desc = ext ? h->ext_desc : h->d_desc;
     int* o_counts = ext ? h->ext_counts : h->d_counts;
     for (int l = 1; l < g.nlevels; l++) {
-        dim3 grid((g.lv[l].w + g.lv[l].rz_cols - 1) / g.lv[l].rz_cols, (g.lv[l].h + g.lv[l].rz_rows - 1) / g.lv[l].rz_rows, B);
+        const int tiles_y = (g.lv[l].h + g.lv[l].rz_rows - 1) / g.lv[l].rz_rows;
+        dim3 grid((g.lv[l].w + g.lv[l].rz_cols - 1) / g.lv[l].rz_cols, (tiles_y + RZ_TPB - 1) / RZ_TPB, B);
         hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, s, P, pitch, h->d_pyr, g.pyr_bytes, h->d_tab, g, l);
     }
     if (tm) HIPCHK(hipEventRecord(ev[1], s));

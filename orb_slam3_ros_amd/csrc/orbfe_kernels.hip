@@ -155,6 +155,11 @@ __device__ __forceinline__ int small_div(int a, int d) {
     return (int)(((float)a + 0.5f) * __builtin_amdgcn_rcpf((float)d));
 }
 
+// bits 32..47 of the product of two 24-bit operands (v_mul_hi_u32_u24)
+__device__ __forceinline__ uint32_t mulhi_u24(uint32_t a, uint32_t b) {
+    return (uint32_t)(((uint64_t)(a & 0xFFFFFFu) * (uint64_t)(b & 0xFFFFFFu)) >> 32);
+}
+
 __device__ __forceinline__ uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
 
 // ---------------------------------------------------------------------------------------------
@@ -166,7 +171,7 @@ __device__ __forceinline__ uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : 
 // in LDS with dword loads; each thread produces 4 adjacent output pixels (one dword store).
 // ---------------------------------------------------------------------------------------------
 // Tile = up to RZ_TR output rows x RZ_TC output columns (the host shrinks both per level so the
-// source window fits): (A) the source window is loaded with one batch of aligned dword loads,
+// source window fits): (A) the source window is loaded with one batch of 16-byte chunk loads,
 // (B) the horizontal pass H = S[sx]*a0 + S[sx+1]*a1 (exact int) runs once per (source row,
 // output column) into LDS, (C) every thread finishes 4 adjacent output pixels of a row from two
 // 16-byte H reads and stores them with one dword store.
@@ -179,7 +184,11 @@ __device__ __forceinline__ uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : 
 #define RZ_SCB 176            // source bytes of a tile window row (host-checked)
 #endif
 #define RZ_LD ((RZ_SR * RZ_SCB / 16 + 255) / 256)  // window 16-byte chunks per thread
-__global__ __launch_bounds__(256) void k_resize(const uint8_t* const* imgs, int in_pitch, uint8_t* pyr, int pyr_stride,
+#ifndef RZ_TPB
+#define RZ_TPB 4              // vertically adjacent tiles per block: the next tile's window loads fly
+                              // while this tile's passes run
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k_resize(const uint8_t* const* imgs, int in_pitch, uint8_t* pyr, int pyr_stride,
                                                 const int16_t* __restrict__ tab, OrbGeom g, int l) {
     __shared__ __attribute__((aligned(16))) uint8_t s_src[RZ_SR][RZ_SCB];
     __shared__ __attribute__((aligned(16))) int s_h[RZ_SR][RZ_TC];
@@ -190,105 +199,140 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t* const* imgs, int 
     const int bx = lb % gridDim.x, by = (lb / gridDim.x) % gridDim.y;
     const int b = lb / (gridDim.x * gridDim.y), t = threadIdx.x;
     const int TR = L.rz_rows, TC = L.rz_cols;
-    const int y0 = by * TR, x0 = bx * TC;
-    const int y1 = min(y0 + TR, L.h), x1 = min(x0 + TC, L.w);
+    const int x0 = bx * TC, x1 = min(x0 + TC, L.w);
+    const int tile0 = by * RZ_TPB, tile1 = min(tile0 + RZ_TPB, (L.h + TR - 1) / TR);
     int spitch;
     gptr_u8 src = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l - 1, &spitch);
     uint8_t* dst = pyr + (size_t)b * pyr_stride + L.pyr_off;
     const int16_t* tx = tab + L.tab_x;
     const int16_t* ty = tab + L.tab_y;
-    const int sr0 = ty[4 * y0], sr1 = ty[4 * (y1 - 1) + 1];           // source rows [sr0, sr1]
+    // source columns [sc0, sc1) of the column tile (the same for all of the block's tiles)
     const int sc0 = tx[3 * x0] & ~3;
-    const int sc1 = min((int)tx[3 * (x1 - 1)] + 2, Ps.w);              // source cols [sc0, sc1)
-    const int nsr = sr1 - sr0 + 1, nsc16 = (sc1 - sc0 + 15) >> 4;
-    const int nitems = nsr * nsc16;
+    const int sc1 = min((int)tx[3 * (x1 - 1)] + 2, Ps.w);
+    const int nsc16 = (sc1 - sc0 + 15) >> 4;
     const bool aligned = ((spitch & 3) == 0) && ((((uintptr_t)src) & 3) == 0);
-    // this thread's output column for the horizontal pass and the row coefficients
+    // this thread's output column for the horizontal pass and its coefficients
     const int hr0 = small_div(t, TC), hx = t - hr0 * TC, hstep = small_div(256, TC);
     const int hdx = min(x0 + hx, x1 - 1);
     const int hsx = tx[3 * hdx] - sc0, ha0 = tx[3 * hdx + 1], ha1 = tx[3 * hdx + 2];
     const bool hlin = hdx < L.xmax;
-    int tyv = 0;
-    if (t < 4 * (y1 - y0)) tyv = ty[4 * y0 + t];
-    // (A) window as 16-byte chunks: item i = (r, c) with r = i / nsc16 (reciprocal-exact for
+    // stored horizontal sums: Hs = H << 4 (exact: H < 2^20), for the universal-intrinsic columns
+    // masked to (H >> 4) << 8, the operand the vertical pass feeds to v_mul_hi_u32_u24
+    const uint32_t hmask = hdx < L.simd_end ? 0xFFFF00u : 0xFFFFFFFFu;
+    // window items of this thread: 16-byte chunk i = (r, c) with r = i / nsc16 (reciprocal-exact for
     // i < 2^16); rows < 2^12 and pitches < 2^13, so the offsets are 24-bit products. A chunk that
     // would cross the row's pitch (the last one of a row, the source may be the caller's image) is
-    // read as guarded dwords.
-    orbfe_u32x4 v[RZ_LD];
-    int lds_off[RZ_LD];
+    // read as guarded bytes.
+    int it_r[RZ_LD], it_off[RZ_LD], it_g[RZ_LD];
+    bool it_al[RZ_LD];
 #pragma unroll
     for (int u = 0; u < RZ_LD; u++) {
-        const int i = min(t + 256 * u, nitems - 1);
+        const int i = t + 256 * u;
         const int r = small_div(i, nsc16), c = i - (int)__umul24((uint32_t)r, (uint32_t)nsc16);
-        lds_off[u] = (int)__umul24((uint32_t)r, RZ_SCB) + 16 * c;
-        const int col = sc0 + 16 * c;
-        gptr_u8 sp = src + __umul24((uint32_t)(sr0 + r), (uint32_t)spitch) + col;
-        if (aligned && col + 16 <= spitch) {
-            v[u] = *(const ORBFE_GLOBAL orbfe_u32x4*)sp;
-        } else {
-            orbfe_u32x4 x = {0u, 0u, 0u, 0u};
-            for (int k = 0; k < 16; k++)
-                if (col + k < Ps.w) x[k >> 2] |= (uint32_t)sp[k] << (8 * (k & 3));
-            v[u] = x;
-        }
+        it_r[u] = r;
+        it_off[u] = (int)__umul24((uint32_t)r, RZ_SCB) + 16 * c;
+        it_g[u] = sc0 + 16 * c;
+        it_al[u] = aligned && sc0 + 16 * c + 16 <= spitch;
     }
+    // (A) window of the tile at output rows [y0, y1): source rows [sr0, sr0 + nsr)
+    orbfe_u32x4 v[RZ_LD];
+    int tyv = 0;
+    auto fetch = [&](int y0, int y1, int sr0, int nsr) {
 #pragma unroll
-    for (int u = 0; u < RZ_LD; u++)
-        if (t + 256 * u < nitems) *(orbfe_u32x4*)(&s_src[0][0] + lds_off[u]) = v[u];
-    if (t < 4 * (y1 - y0)) (&s_ty[0][0])[t] = tyv;
-    SYNC();
-    // (B) horizontal pass
-    if (hr0 < hstep) {
-        // beyond xmax the reference takes S[sx] * 2048: a0 = 2048, a1 = 0 gives it branch-free (the
-        // byte at sx + 1 is inside the LDS window and multiplied by 0); 24-bit multiplies are exact
-        // (coefficients <= 2048). A plain loop: unrolling it measured slower.
-        const uint32_t a0 = hlin ? (uint32_t)ha0 : 2048u, a1 = hlin ? (uint32_t)ha1 : 0u;
-        for (int r = hr0; r < nsr; r += hstep) {
-            const uint32_t p0 = s_src[r][hsx], p1 = s_src[r][hsx + 1];
-            s_h[r][hx] = (int)(__umul24(p0, a0) + __umul24(p1, a1));
+        for (int u = 0; u < RZ_LD; u++) {
+            if (it_r[u] < nsr) {
+                gptr_u8 sp = src + __umul24((uint32_t)(sr0 + it_r[u]), (uint32_t)spitch) + it_g[u];
+                if (it_al[u]) {
+                    v[u] = *(const ORBFE_GLOBAL orbfe_u32x4*)sp;
+                } else {
+                    orbfe_u32x4 x = {0u, 0u, 0u, 0u};
+                    for (int k = 0; k < 16; k++)
+                        if (it_g[u] + k < Ps.w) x[k >> 2] |= (uint32_t)sp[k] << (8 * (k & 3));
+                    v[u] = x;
+                }
+            }
         }
-    }
-    SYNC();
-    // (C) vertical pass: thread -> (row lane, 4-column group)
+        // (sy, sy + 1, b0 << 8, b1 << 8): the vertical pass multiplies the b's with v_mul_hi_u32_u24
+        if (t < 4 * (y1 - y0)) tyv = (int)ty[4 * y0 + t] << ((t & 2) ? 8 : 0);
+    };
+    int y0 = tile0 * TR, y1 = min(y0 + TR, L.h);
+    int sr0 = ty[4 * y0], nsr = ty[4 * (y1 - 1) + 1] - sr0 + 1;
+    fetch(y0, y1, sr0, nsr);
+    // (C) vertical pass mapping: thread -> (row lane, 4-column group)
     const int ng = TC >> 2, rl = small_div(t, ng), cg = t - rl * ng, rstep = small_div(256, ng);
     const int xq = x0 + 4 * cg;
-    if (rl >= rstep || xq >= x1) return;
+    const bool vact = rl < rstep && xq < x1;
     // columns < simd_end take the universal-intrinsic rounding; a 4-column group is almost always
     // entirely on one side (one wave-uniform branch, no per-column divergence)
     const bool all_vec = xq + 3 < L.simd_end;
     bool vec[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) vec[q] = xq + q < L.simd_end;
-    for (int dy = y0 + rl; dy < y1; dy += rstep) {
-        const int* tyr = s_ty[dy - y0];
-        const int r0 = tyr[0] - sr0, r1 = tyr[1] - sr0;
-        const uint32_t b0 = (uint32_t)tyr[2], b1 = (uint32_t)tyr[3];   // coefficients in [0, 2048]
-        const int4 H0 = *(const int4*)&s_h[r0][4 * cg];
-        const int4 H1 = *(const int4*)&s_h[r1][4 * cg];
-        const uint32_t h0[4] = {(uint32_t)H0.x, (uint32_t)H0.y, (uint32_t)H0.z, (uint32_t)H0.w};
-        const uint32_t h1[4] = {(uint32_t)H1.x, (uint32_t)H1.y, (uint32_t)H1.z, (uint32_t)H1.w};
-        // H <= 255 * 2048 < 2^20 and b <= 2^11: 24-bit multiplies are exact, every sum < 2^31
-        uint32_t packed = 0;
-        if (all_vec) {
+    for (int tile = tile0; tile < tile1; tile++) {
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint32_t vv = ((__umul24(h0[q] >> 4, b0) >> 16) + (__umul24(h1[q] >> 4, b1) >> 16) + 2) >> 2;
-                packed |= min(vv, 255u) << (8 * q);
-            }
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint32_t vs = ((__umul24(h0[q] >> 4, b0) >> 16) + (__umul24(h1[q] >> 4, b1) >> 16) + 2) >> 2;
-                const uint32_t vl = (__umul24(h0[q], b0) + __umul24(h1[q], b1) + (1u << 21)) >> 22;
-                packed |= min(vec[q] ? vs : vl, 255u) << (8 * q);
+        for (int u = 0; u < RZ_LD; u++)
+            if (it_r[u] < nsr) *(orbfe_u32x4*)(&s_src[0][0] + it_off[u]) = v[u];
+        if (t < 4 * (y1 - y0)) (&s_ty[0][0])[t] = tyv;
+        SYNC();
+        const int cy0 = y0, cy1 = y1, csr0 = sr0, cnsr = nsr;
+        if (tile + 1 < tile1) {   // the next tile's window loads overlap this tile's passes
+            y0 = y1;
+            y1 = min(y0 + TR, L.h);
+            sr0 = ty[4 * y0];
+            nsr = ty[4 * (y1 - 1) + 1] - sr0 + 1;
+            fetch(y0, y1, sr0, nsr);
+        }
+        // (B) horizontal pass
+        if (hr0 < hstep) {
+            // beyond xmax the reference takes S[sx] * 2048: a0 = 2048, a1 = 0 gives it branch-free
+            // (the byte at sx + 1 is inside the LDS window and multiplied by 0); 24-bit multiplies
+            // are exact (coefficients <= 2048). A plain loop: unrolling it measured slower.
+            const uint32_t a0 = (hlin ? (uint32_t)ha0 : 2048u) << 4, a1 = (hlin ? (uint32_t)ha1 : 0u) << 4;
+            for (int r = hr0; r < cnsr; r += hstep) {
+                const uint32_t p0 = s_src[r][hsx], p1 = s_src[r][hsx + 1];
+                s_h[r][hx] = (int)((__umul24(p0, a0) + __umul24(p1, a1)) & hmask);
             }
         }
-        uint8_t* dp = dst + (size_t)dy * L.pitch + xq;
-        if (xq + 4 <= x1) {
-            *(uint32_t*)dp = packed;
-        } else {
-            for (int q = 0; q < 4 && xq + q < x1; q++) dp[q] = (uint8_t)(packed >> (8 * q));
+        SYNC();
+        // (C) vertical pass
+        if (vact) {
+            for (int dy = cy0 + rl; dy < cy1; dy += rstep) {
+                const int* tyr = s_ty[dy - cy0];
+                const int r0 = tyr[0] - csr0, r1 = tyr[1] - csr0;
+                const uint32_t b0s = (uint32_t)tyr[2], b1s = (uint32_t)tyr[3];   // coefficients in [0, 2048], << 8
+                const int4 H0 = *(const int4*)&s_h[r0][4 * cg];
+                const int4 H1 = *(const int4*)&s_h[r1][4 * cg];
+                const uint32_t h0[4] = {(uint32_t)H0.x, (uint32_t)H0.y, (uint32_t)H0.z, (uint32_t)H0.w};
+                const uint32_t h1[4] = {(uint32_t)H1.x, (uint32_t)H1.y, (uint32_t)H1.z, (uint32_t)H1.w};
+                // universal-intrinsic columns: ((H >> 4) * b) >> 16 = mul_hi_u24((H >> 4) << 8, b << 8).
+                // No saturation is needed: a0 + a1 and b0 + b1 are at most 2049 (independently rounded
+                // coefficients), so H >> 4 <= 32655 and both forms are <= 255 (1020 + 2 >> 2; and
+                // (522495 * 2049 + 2^21) >> 22).
+                uint32_t packed = 0;
+                if (all_vec) {
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const uint32_t vv = (mulhi_u24(h0[q], b0s) + mulhi_u24(h1[q], b1s) + 2) >> 2;
+                        packed |= vv << (8 * q);
+                    }
+                } else {
+                    const uint32_t b0 = b0s >> 8, b1 = b1s >> 8;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const uint32_t vs = (mulhi_u24(h0[q], b0s) + mulhi_u24(h1[q], b1s) + 2) >> 2;
+                        const uint32_t vl = (__umul24(h0[q] >> 4, b0) + __umul24(h1[q] >> 4, b1) + (1u << 21)) >> 22;
+                        packed |= (vec[q] ? vs : vl) << (8 * q);
+                    }
+                }
+                uint8_t* dp = dst + (size_t)dy * L.pitch + xq;
+                if (xq + 4 <= x1) {
+                    *(uint32_t*)dp = packed;
+                } else {
+                    for (int q = 0; q < 4 && xq + q < x1; q++) dp[q] = (uint8_t)(packed >> (8 * q));
+                }
+            }
         }
+        SYNC();   // s_src / s_h / s_ty are refilled for the next tile
     }
 }
 
