@@ -336,7 +336,7 @@ def main():
         n_img = 2 * F
         pyr_fast_ms = stages["resize"] + stages["fast"]
         bytes_img = algorithmic_bytes(W, H)
-        achieved = n_img * bytes_img / (pyr_fast_ms * 1e-3) / 1e9
+        achieved = n_img * bytes_img / (pyr_fast_ms * 1e-3) / 1e9 if pyr_fast_ms > 0 else 0.0
         dominant = max(stages, key=stages.get)
         tr = pmc_traffic(n_img, W, H)
         cache = pmc_cache(n_img, W, H)

@@ -571,6 +571,248 @@ struct FastLds {
 };
 #define FAST_ENT_BYTES 1024     // entry chunk: 64 groups x <= 8 entries x 2 B
 
+// Detection of one staged cell (both attempts, NMS, emission). NDC = the LDS row length in dwords
+// when known at compile time (0: runtime nd): every LDS offset of the ring / neighbour reads is then
+// an immediate instead of a per-read VALU add.
+template <int NDC>
+__device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds& fl, const FastCell& me, int ng,
+                                                 int nd_rt, int dw, int dh, uint8_t* s_img, uint8_t* s_sc,
+                                                 uint16_t* s_cor, uint16_t* s_ent, uint32_t* cellkeys, int* cellcnt,
+                                                 int b, int c, int lane, int ablate) {
+    const int nd = NDC ? NDC : nd_rt;
+    const int RS = 4 * nd;
+    const OrbLevel& L = g.lv[me.l];
+    if (ablate == 1) {
+        asm volatile("" ::"v"((int)s_img[lane]));
+        if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = 0;
+        WAVE_SYNC();
+        return;
+    }
+    const uint8_t* s_px = s_img + 1;   // ROI pixel (y, x) = s_px[y * RS + x]
+    // attempt 0 = FAST at iniThFAST; attempt 1 (only when attempt 0 leaves no NMS survivor) =
+    // FAST at minThFAST over a cleared score map: the reference's per-cell fallback
+    // (ORBextractor.cc:826-846). Most cells stop after attempt 0, whose candidate set is a
+    // fraction of minThFAST's.
+    int nsurv = 0;
+    bool stop = false;
+    for (int attempt = 0; attempt < 2; attempt++) {
+        const int th = attempt == 0 ? g.ini_th : g.min_th;
+        if (attempt) {
+            uint32_t* s32z = (uint32_t*)s_sc;
+            for (int i = lane; i < (dh + 2) * nd; i += 64) s32z[i] = 0u;
+            WAVE_SYNC();
+        }
+        // pass 1: FAST's exact necessary test (each 9-arc contains one pixel of every opposite
+        // pair (k, k+8), k = 0, 2, 4, 6, all of one sign) for 4 pixels per lane in packed u16x2
+        // arithmetic (even bytes / odd bytes); candidates compacted row-major as (dy << 8 | dx).
+        int ngrp = 0;
+        // group records at the tail of the corner list: <= ng * dh of them
+        uint32_t* s_grp = (uint32_t*)((uint8_t*)s_cor + fl.cor) - ng * dh;
+        if (ng) {
+            const int rpi = 64 / ng;
+            const int ly = small_div(lane, ng), lg = lane - ly * ng;
+            const _Float16 tf = __builtin_bit_cast(_Float16, (unsigned short)th);   // th * 2^-24
+            const orbfe_half2 tv = {tf, tf};
+            const int valid4 = min(4, dw - 4 * lg);
+            // flag bits of pixel k: 2k + 1 = dark possible, 2k = bright possible
+            const uint32_t vmask = ly < rpi && valid4 > 0 ? (1u << (2 * valid4)) - 1u : 0u;
+            for (int y0 = 0; y0 < dh; y0 += rpi) {
+                const int y = y0 + ly;
+                uint32_t m8 = 0;
+                if (vmask && y < dh) {
+                    // centre pixels k = 0..3 at ROI (y + 3, 4 lg + 3 + k) = byte 4 lg + 4 + k of the row
+                    const uint8_t* cp = s_img + (y + 3) * RS + 4 * lg + 4;
+                    const uint32_t cw = *(const uint32_t*)cp;
+                    // aligned dwords + v_alignbyte: unaligned ds_read_b32 measured 40 % slower for the kernel
+                    const uint32_t* r0p = (const uint32_t*)cp - 1;   // dword of ROI columns 4 lg - 1 ..
+                    const uint32_t c0w = r0p[0], c2w = r0p[2];
+                    // ring samples as (hi, lo, byte shift): the 4 bytes of sample k are bytes s .. s + 3 of
+                    // hi:lo, so one v_perm per parity picks its even / odd pixels as f16 halves directly
+                    const uint32_t ph[8] = {0u, 0u, c2w, cw, r0p[2 * nd + 2], r0p[-2 * nd + 1], r0p[-2 * nd + 2], r0p[2 * nd + 1]};
+                    const uint32_t pl[8] = {r0p[3 * nd + 1], r0p[-3 * nd + 1], cw, c0w,          // (0, 3), (0, -3), (3, 0), (-3, 0)
+                                            r0p[2 * nd + 1], r0p[-2 * nd], r0p[-2 * nd + 1], r0p[2 * nd]};   // (2, 2), (-2, -2), (2, -2), (-2, 2)
+                    constexpr uint32_t psh[8] = {0, 0, 3, 1, 2, 2, 2, 2};
+                    uint32_t sd[2], sb[2];
+#pragma unroll
+                    for (int par = 0; par < 2; par++) {
+                        const uint32_t sel = par ? 0x0c030c01u : 0x0c020c00u;
+                        const orbfe_half2 v = px_h2(cw, sel);
+                        // dark possible  <=> every pair has a member < v - t <=> max_k min(pair k) < v - t
+                        // bright possible <=> every pair has a member > v + t <=> min_k max(pair k) > v + t
+                        orbfe_half2 mn[4], mx[4];
+#pragma unroll
+                        for (int k = 0; k < 4; k++) {
+                            const uint32_t sa = 0x0c000c00u | (psh[2 * k] + par) | ((psh[2 * k] + par + 2) << 16);
+                            const uint32_t sb2 = 0x0c000c00u | (psh[2 * k + 1] + par) | ((psh[2 * k + 1] + par + 2) << 16);
+                            const orbfe_half2 xa = as_h2(__builtin_amdgcn_perm(ph[2 * k], pl[2 * k], sa));
+                            const orbfe_half2 xb = as_h2(__builtin_amdgcn_perm(ph[2 * k + 1], pl[2 * k + 1], sb2));
+                            mn[k] = hmin(xa, xb);
+                            mx[k] = hmax(xa, xb);
+                        }
+                        const orbfe_half2 D = hmax(hmax(hmax(mn[0], mn[1]), mn[2]), mn[3]);
+                        const orbfe_half2 B = hmin(hmin(hmin(mx[0], mx[1]), mx[2]), mx[3]);
+                        // exact differences: the sign bit of each half is the flag
+                        sd[par] = h2_bits(D - (v - tv));
+                        sb[par] = h2_bits((v + tv) - B);
+                    }
+                    // sign bytes -> pixel order (byte k = pixel k), dark at bit 7, bright at bit 6,
+                    // then gathered into bits 2k + 1 / 2k by one dot product
+                    const uint32_t A = __builtin_amdgcn_perm(sd[1], sd[0], 0x07030501u);
+                    const uint32_t Bq = __builtin_amdgcn_perm(sb[1], sb[0], 0x07030501u);
+                    const uint32_t F = (A & 0x80808080u) | ((Bq >> 1) & 0x40404040u);
+                    m8 = __builtin_amdgcn_udot4(F >> 6, 0x40100401u, 0u, false) & vmask;
+                }
+                // 4-pixel groups with any candidate, compacted row-major (iteration-major,
+                // then lane order): dy << 7 | dx0 in bits 0-13, flags in bits 16-23 (pixel k:
+                // bit 17 + 2k dark, 16 + 2k bright)
+                const unsigned long long gm = __ballot(m8 != 0u);
+                if (m8)
+                    s_grp[ngrp + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(gm >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)gm, 0u))] =
+                        (uint32_t)((y << 7) | (4 * lg)) | (m8 << 16);
+                ngrp += __popcll(gm);
+            }
+        }
+        WAVE_SYNC();
+        // expand the groups into entries, one per (pixel, possible sign): dy << 7 | dx, bit 14 =
+        // bright, bit 15 = second entry of a pixel (both signs passed; at most one can be a corner)
+        if (ablate == 2) {
+            asm volatile("" ::"v"(ngrp));
+            stop = true;
+            break;
+        }
+        // per chunk of 64 groups: expand into entries, one per (pixel, possible sign): dy << 7 |
+        // dx, bit 14 = bright, bit 15 = second entry of a pixel (both signs passed; at most one
+        // can be a corner); then the exact score of the chunk's entries. Corners are appended in
+        // pixel order to the corner list, whose tail holds the group records still to come
+        // (cor_bytes >= 8 * groups + 256 keeps the two apart).
+        int ncorner = 0;
+        for (int g0 = 0; g0 < ngrp; g0 += 64) {
+            int nent = 0;
+            {
+                const int gi = g0 + lane;
+                const uint32_t rec = gi < ngrp ? s_grp[gi] : 0u;
+                const int cnt = __popc(rec >> 16);   // <= 8: scan by bit planes
+                const unsigned long long lt = (1ull << lane) - 1ull;
+                const unsigned long long m0 = __ballot(cnt & 1), m1 = __ballot(cnt & 2), m2 = __ballot(cnt & 4),
+                                         m3 = __ballot(cnt & 8);
+                int pos = __popcll(m0 & lt) + 2 * __popcll(m1 & lt) + 4 * __popcll(m2 & lt) + 8 * __popcll(m3 & lt);
+                const int packed = (int)(rec & 0x3FFFu);
+                for (int i = 0; i < 4; i++) {
+                    const uint32_t di = (rec >> (17 + 2 * i)) & 1u, bi = (rec >> (16 + 2 * i)) & 1u;
+                    if (di) s_ent[pos++] = (uint16_t)(packed + i);
+                    if (bi) s_ent[pos++] = (uint16_t)((packed + i) | 0x4000 | (di << 15));
+                }
+                nent = __popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2) + 8 * __popcll(m3);
+            }
+            WAVE_SYNC();
+            // pass 2: exact score M - 1 (corner iff M > th) of each entry for its sign only, two
+            // entries per lane in packed f16 (pixels as 1024 + v, exact signed differences)
+            for (int j0 = 0; j0 < nent; j0 += 128) {
+                const int j = j0 + 2 * lane;
+                const uint32_t e2 = j < nent ? ((const uint32_t*)s_ent)[j >> 1] : 0u;
+                const bool ok0 = j < nent, ok1 = j + 1 < nent;
+                const uint32_t e0 = e2 & 0xFFFFu, e1 = ok1 ? e2 >> 16 : e0;
+                const uint8_t* q0 = s_px + (((e0 >> 7) & 127) + 3) * RS + (e0 & 127) + 3;
+                const uint8_t* q1 = s_px + (((e1 >> 7) & 127) + 3) * RS + (e1 & 127) + 3;
+                // the two entries' pixels as one u16x2 = f16 denormals v * 2^-24 (f16 denormals are
+                // kept, float_denorm_mode_16_64 = 3; every sum / difference here is exact)
+                const orbfe_half2 v2 = as_h2(__builtin_bit_cast(uint32_t, orbfe_ushort2{q0[0], q1[0]}));
+                // d = s (v - x) with s = +1 (dark) / -1 (bright) per half, one exact fma per ring pixel
+                const uint32_t bmask = ((e0 & 0x4000u) ? 0x00008000u : 0u) | ((e1 & 0x4000u) ? 0x80000000u : 0u);
+                const orbfe_half2 ns = as_h2(0xBC00BC00u ^ bmask);   // -s
+                const orbfe_half2 sv = as_h2(h2_bits(v2) ^ bmask);   // s v
+                // ring reads from the top-left corner of the 7x7 box: non-negative immediate offsets
+                const uint8_t* t0 = q0 - 3 * RS - 3;
+                const uint8_t* t1 = q1 - 3 * RS - 3;
+                orbfe_half2 P[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const int o = (kRingDy[k] + 3) * RS + kRingDx[k] + 3;
+                    const orbfe_half2 x2 = as_h2(__builtin_bit_cast(uint32_t, orbfe_ushort2{t0[o], t1[o]}));
+                    P[k] = __builtin_elementwise_fma(x2, ns, sv);
+                }
+                // M = max over the 16 arcs of the arc minimum (signed: an arc with a minimum <= 0
+                // never makes a corner, th >= 0)
+                orbfe_half2 m2[16], m4[16], m9[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) m2[k] = hmin(P[k], P[(k + 1) & 15]);
+#pragma unroll
+                for (int k = 0; k < 16; k++) m4[k] = hmin(m2[k], m2[(k + 2) & 15]);
+#pragma unroll
+                for (int k = 0; k < 16; k++) m9[k] = hmin(hmin(m4[k], m4[(k + 4) & 15]), P[(k + 8) & 15]);
+#pragma unroll
+                for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+                    for (int k = 0; k < w; k++) m9[k] = hmax(m9[k], m9[k + w]);
+                // M as an integer: the bits of a non-negative denormal; negative -> no corner
+                const uint32_t mb = h2_bits(m9[0]);
+                const int bx = (mb & 0x8000u) ? -1 : (int)(mb & 0x7fffu);
+                const int by = (mb & 0x80000000u) ? -1 : (int)((mb >> 16) & 0x7fffu);
+                const bool c0 = ok0 && bx > th, c1 = ok1 && by > th;
+                if (c0) s_sc[(((e0 >> 7) & 127) + 1) * RS + (e0 & 127) + 1] = (uint8_t)(bx - 1);
+                if (c1) s_sc[(((e1 >> 7) & 127) + 1) * RS + (e1 & 127) + 1] = (uint8_t)(by - 1);
+                const int cc = (int)c0 + (int)c1;
+                const unsigned long long lt = (1ull << lane) - 1ull;
+                const unsigned long long b0 = __ballot(cc & 1), b1 = __ballot(cc & 2);
+                int pos = ncorner + __popcll(b0 & lt) + 2 * __popcll(b1 & lt);
+                if (c0) s_cor[pos++] = (uint16_t)(e0 & 0x3FFFu);
+                if (c1) s_cor[pos] = (uint16_t)(e1 & 0x3FFFu);
+                ncorner += __popcll(b0) + 2 * __popcll(b1);
+            }
+            WAVE_SYNC();   // s_ent is refilled by the next chunk
+        }
+        if (ablate == 3) {
+            asm volatile("" ::"v"((int)s_sc[lane]));
+            stop = true;
+            break;
+        }
+        // NMS over corners (every other pixel has score 0); survivors compacted in place
+        nsurv = 0;
+        for (int i0 = 0; i0 < ncorner; i0 += 64) {
+            const int i = i0 + lane;
+            bool surv = false;
+            int p = 0;
+            if (i < ncorner) {
+                p = s_cor[i];
+                const uint8_t* q = s_sc + ((p >> 7) + 1) * RS + (p & 127) + 1;
+                const int sc = q[0];
+                surv = sc > q[-1] && sc > q[1] && sc > q[-RS - 1] && sc > q[-RS] && sc > q[-RS + 1] &&
+                       sc > q[RS - 1] && sc > q[RS] && sc > q[RS + 1];
+            }
+            const unsigned long long m = __ballot(surv);
+            if (surv) s_cor[nsurv + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)p;
+            nsurv += __popcll(m);
+        }
+        WAVE_SYNC();
+        if (nsurv > 0) break;
+    }   // attempt
+    if (stop) {
+        if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = 0;
+        WAVE_SYNC();
+        return;
+    }
+    // emission of the survivors in row-major order (FAST's emission order)
+    int base = 0;
+    uint32_t* out = cellkeys + (size_t)b * g.cellkeys_per_img + L.cellkey_off + (size_t)me.local * L.cell_cap;
+    const int xr0 = me.c0 - ORBFE_MINB + 3, yr0 = me.r0 - ORBFE_MINB + 3;
+    for (int i0 = 0; i0 < nsurv; i0 += 64) {
+        const int i = i0 + lane;
+        int sc = 0, p = 0;
+        if (i < nsurv) {
+            p = s_cor[i];
+            sc = s_sc[((p >> 7) + 1) * RS + (p & 127) + 1];
+        }
+        const bool f = i < nsurv;
+        const unsigned long long m = __ballot(f);
+        const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
+        if (f) out[pos] = (uint32_t)(xr0 + (p & 127)) | ((uint32_t)(yr0 + (p >> 7)) << 12) | ((uint32_t)sc << 24);
+        base += __popcll(m);
+    }
+    if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = base;
+    WAVE_SYNC();   // LDS is restaged for the next cell
+}
+
 __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                               int pyr_stride, OrbGeom g, FastLds fl, uint32_t* cellkeys,
                                               int* cellcnt, int ablate) {
@@ -597,7 +839,6 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
         int ng, nd, cpr, rpl;
         fast_geom(cur, &ng, &nd, &cpr, &rpl);
         const int dw = cur.cols - 6, dh = cur.rows - 6;
-        const int RS = 4 * nd;
         // stage: realign, zero the score map
         if (ng) {
             const int sy = small_div(lane, cpr), st = lane - sy * cpr, sal = (cur.c0 - 1) & 3;
@@ -628,234 +869,12 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
             cur = fast_cell(imgs, in_pitch, pyr, pyr_stride, g, b, c + 1);
             fast_prefetch(cur, lane, pf);
         }
-        const OrbLevel& L = g.lv[me.l];
-        if (ablate == 1) {
-            asm volatile("" ::"v"((int)s_img[lane]));
-            if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = 0;
-            WAVE_SYNC();
-            continue;
-        }
-        const uint8_t* s_px = s_img + 1;   // ROI pixel (y, x) = s_px[y * RS + x]
-        // attempt 0 = FAST at iniThFAST; attempt 1 (only when attempt 0 leaves no NMS survivor) =
-        // FAST at minThFAST over a cleared score map: the reference's per-cell fallback
-        // (ORBextractor.cc:826-846). Most cells stop after attempt 0, whose candidate set is a
-        // fraction of minThFAST's.
-        int nsurv = 0;
-        bool stop = false;
-        for (int attempt = 0; attempt < 2; attempt++) {
-            const int th = attempt == 0 ? g.ini_th : g.min_th;
-            if (attempt) {
-                uint32_t* s32z = (uint32_t*)s_sc;
-                for (int i = lane; i < (dh + 2) * nd; i += 64) s32z[i] = 0u;
-                WAVE_SYNC();
-            }
-            // pass 1: FAST's exact necessary test (each 9-arc contains one pixel of every opposite
-            // pair (k, k+8), k = 0, 2, 4, 6, all of one sign) for 4 pixels per lane in packed u16x2
-            // arithmetic (even bytes / odd bytes); candidates compacted row-major as (dy << 8 | dx).
-            int ngrp = 0;
-            // group records at the tail of the corner list: <= ng * dh of them
-            uint32_t* s_grp = (uint32_t*)((uint8_t*)s_cor + fl.cor) - ng * dh;
-            if (ng) {
-                const int rpi = 64 / ng;
-                const int ly = small_div(lane, ng), lg = lane - ly * ng;
-                const _Float16 tf = __builtin_bit_cast(_Float16, (unsigned short)th);   // th * 2^-24
-                const orbfe_half2 tv = {tf, tf};
-                const int valid4 = min(4, dw - 4 * lg);
-                // flag bits of pixel k: 2k + 1 = dark possible, 2k = bright possible
-                const uint32_t vmask = ly < rpi && valid4 > 0 ? (1u << (2 * valid4)) - 1u : 0u;
-                for (int y0 = 0; y0 < dh; y0 += rpi) {
-                    const int y = y0 + ly;
-                    uint32_t m8 = 0;
-                    if (vmask && y < dh) {
-                        // centre pixels k = 0..3 at ROI (y + 3, 4 lg + 3 + k) = byte 4 lg + 4 + k of the row
-                        const uint8_t* cp = s_img + (y + 3) * RS + 4 * lg + 4;
-                        const uint32_t cw = *(const uint32_t*)cp;
-                        // aligned dwords + v_alignbyte: unaligned ds_read_b32 measured 40 % slower for the kernel
-                        const uint32_t* r0p = (const uint32_t*)cp - 1;   // dword of ROI columns 4 lg - 1 ..
-                        const uint32_t c0w = r0p[0], c2w = r0p[2];
-                        const uint32_t pp[8] = {
-                            r0p[3 * nd + 1], r0p[-3 * nd + 1],                                            // (0, 3), (0, -3)
-                            __builtin_amdgcn_alignbyte(c2w, cw, 3), __builtin_amdgcn_alignbyte(cw, c0w, 1),  // (3, 0), (-3, 0)
-                            __builtin_amdgcn_alignbyte(r0p[2 * nd + 2], r0p[2 * nd + 1], 2),               // (2, 2)
-                            __builtin_amdgcn_alignbyte(r0p[-2 * nd + 1], r0p[-2 * nd], 2),                 // (-2, -2)
-                            __builtin_amdgcn_alignbyte(r0p[-2 * nd + 2], r0p[-2 * nd + 1], 2),             // (2, -2)
-                            __builtin_amdgcn_alignbyte(r0p[2 * nd + 1], r0p[2 * nd], 2)};                  // (-2, 2)
-                        uint32_t sd[2], sb[2];
-#pragma unroll
-                        for (int par = 0; par < 2; par++) {
-                            const uint32_t sel = par ? 0x0c030c01u : 0x0c020c00u;
-                            const orbfe_half2 v = px_h2(cw, sel);
-                            // dark possible  <=> every pair has a member < v - t <=> max_k min(pair k) < v - t
-                            // bright possible <=> every pair has a member > v + t <=> min_k max(pair k) > v + t
-                            orbfe_half2 mn[4], mx[4];
-#pragma unroll
-                            for (int k = 0; k < 4; k++) {
-                                const orbfe_half2 xa = px_h2(pp[2 * k], sel), xb = px_h2(pp[2 * k + 1], sel);
-                                mn[k] = hmin(xa, xb);
-                                mx[k] = hmax(xa, xb);
-                            }
-                            const orbfe_half2 D = hmax(hmax(hmax(mn[0], mn[1]), mn[2]), mn[3]);
-                            const orbfe_half2 B = hmin(hmin(hmin(mx[0], mx[1]), mx[2]), mx[3]);
-                            // exact differences: the sign bit of each half is the flag
-                            sd[par] = h2_bits(D - (v - tv));
-                            sb[par] = h2_bits((v + tv) - B);
-                        }
-                        // sign bytes -> pixel order (byte k = pixel k), dark at bit 7, bright at bit 6,
-                        // then gathered into bits 2k + 1 / 2k by one dot product
-                        const uint32_t A = __builtin_amdgcn_perm(sd[1], sd[0], 0x07030501u);
-                        const uint32_t Bq = __builtin_amdgcn_perm(sb[1], sb[0], 0x07030501u);
-                        const uint32_t F = (A & 0x80808080u) | ((Bq >> 1) & 0x40404040u);
-                        m8 = __builtin_amdgcn_udot4(F >> 6, 0x40100401u, 0u, false) & vmask;
-                    }
-                    // 4-pixel groups with any candidate, compacted row-major (iteration-major,
-                    // then lane order): dy << 7 | dx0 in bits 0-13, flags in bits 16-23 (pixel k:
-                    // bit 17 + 2k dark, 16 + 2k bright)
-                    const unsigned long long gm = __ballot(m8 != 0u);
-                    if (m8)
-                        s_grp[ngrp + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(gm >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)gm, 0u))] =
-                            (uint32_t)((y << 7) | (4 * lg)) | (m8 << 16);
-                    ngrp += __popcll(gm);
-                }
-            }
-            WAVE_SYNC();
-            // expand the groups into entries, one per (pixel, possible sign): dy << 7 | dx, bit 14 =
-            // bright, bit 15 = second entry of a pixel (both signs passed; at most one can be a corner)
-            if (ablate == 2) {
-                asm volatile("" ::"v"(ngrp));
-                stop = true;
-                break;
-            }
-            // per chunk of 64 groups: expand into entries, one per (pixel, possible sign): dy << 7 |
-            // dx, bit 14 = bright, bit 15 = second entry of a pixel (both signs passed; at most one
-            // can be a corner); then the exact score of the chunk's entries. Corners are appended in
-            // pixel order to the corner list, whose tail holds the group records still to come
-            // (cor_bytes >= 8 * groups + 256 keeps the two apart).
-            int ncorner = 0;
-            for (int g0 = 0; g0 < ngrp; g0 += 64) {
-                int nent = 0;
-                {
-                    const int gi = g0 + lane;
-                    const uint32_t rec = gi < ngrp ? s_grp[gi] : 0u;
-                    const int cnt = __popc(rec >> 16);   // <= 8: scan by bit planes
-                    const unsigned long long lt = (1ull << lane) - 1ull;
-                    const unsigned long long m0 = __ballot(cnt & 1), m1 = __ballot(cnt & 2), m2 = __ballot(cnt & 4),
-                                             m3 = __ballot(cnt & 8);
-                    int pos = __popcll(m0 & lt) + 2 * __popcll(m1 & lt) + 4 * __popcll(m2 & lt) + 8 * __popcll(m3 & lt);
-                    const int packed = (int)(rec & 0x3FFFu);
-                    for (int i = 0; i < 4; i++) {
-                        const uint32_t di = (rec >> (17 + 2 * i)) & 1u, bi = (rec >> (16 + 2 * i)) & 1u;
-                        if (di) s_ent[pos++] = (uint16_t)(packed + i);
-                        if (bi) s_ent[pos++] = (uint16_t)((packed + i) | 0x4000 | (di << 15));
-                    }
-                    nent = __popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2) + 8 * __popcll(m3);
-                }
-                WAVE_SYNC();
-                // pass 2: exact score M - 1 (corner iff M > th) of each entry for its sign only, two
-                // entries per lane in packed f16 (pixels as 1024 + v, exact signed differences)
-                for (int j0 = 0; j0 < nent; j0 += 128) {
-                    const int j = j0 + 2 * lane;
-                    const uint32_t e2 = j < nent ? ((const uint32_t*)s_ent)[j >> 1] : 0u;
-                    const bool ok0 = j < nent, ok1 = j + 1 < nent;
-                    const uint32_t e0 = e2 & 0xFFFFu, e1 = ok1 ? e2 >> 16 : e0;
-                    const uint8_t* q0 = s_px + (((e0 >> 7) & 127) + 3) * RS + (e0 & 127) + 3;
-                    const uint8_t* q1 = s_px + (((e1 >> 7) & 127) + 3) * RS + (e1 & 127) + 3;
-                    // the two entries' pixels as one u16x2 = f16 denormals v * 2^-24 (f16 denormals are
-                    // kept, float_denorm_mode_16_64 = 3; every sum / difference here is exact)
-                    const orbfe_half2 v2 = as_h2(__builtin_bit_cast(uint32_t, orbfe_ushort2{q0[0], q1[0]}));
-                    // d = s (v - x) with s = +1 (dark) / -1 (bright) per half, one exact fma per ring pixel
-                    const uint32_t bmask = ((e0 & 0x4000u) ? 0x00008000u : 0u) | ((e1 & 0x4000u) ? 0x80000000u : 0u);
-                    const orbfe_half2 ns = as_h2(0xBC00BC00u ^ bmask);   // -s
-                    const orbfe_half2 sv = as_h2(h2_bits(v2) ^ bmask);   // s v
-                    // ring reads from the top-left corner of the 7x7 box: non-negative immediate offsets
-                    const uint8_t* t0 = q0 - 3 * RS - 3;
-                    const uint8_t* t1 = q1 - 3 * RS - 3;
-                    orbfe_half2 P[16];
-#pragma unroll
-                    for (int k = 0; k < 16; k++) {
-                        const int o = (kRingDy[k] + 3) * RS + kRingDx[k] + 3;
-                        const orbfe_half2 x2 = as_h2(__builtin_bit_cast(uint32_t, orbfe_ushort2{t0[o], t1[o]}));
-                        P[k] = __builtin_elementwise_fma(x2, ns, sv);
-                    }
-                    // M = max over the 16 arcs of the arc minimum (signed: an arc with a minimum <= 0
-                    // never makes a corner, th >= 0)
-                    orbfe_half2 m2[16], m4[16], m9[16];
-#pragma unroll
-                    for (int k = 0; k < 16; k++) m2[k] = hmin(P[k], P[(k + 1) & 15]);
-#pragma unroll
-                    for (int k = 0; k < 16; k++) m4[k] = hmin(m2[k], m2[(k + 2) & 15]);
-#pragma unroll
-                    for (int k = 0; k < 16; k++) m9[k] = hmin(hmin(m4[k], m4[(k + 4) & 15]), P[(k + 8) & 15]);
-#pragma unroll
-                    for (int w = 8; w >= 1; w >>= 1)
-#pragma unroll
-                        for (int k = 0; k < w; k++) m9[k] = hmax(m9[k], m9[k + w]);
-                    // M as an integer: the bits of a non-negative denormal; negative -> no corner
-                    const uint32_t mb = h2_bits(m9[0]);
-                    const int bx = (mb & 0x8000u) ? -1 : (int)(mb & 0x7fffu);
-                    const int by = (mb & 0x80000000u) ? -1 : (int)((mb >> 16) & 0x7fffu);
-                    const bool c0 = ok0 && bx > th, c1 = ok1 && by > th;
-                    if (c0) s_sc[(((e0 >> 7) & 127) + 1) * RS + (e0 & 127) + 1] = (uint8_t)(bx - 1);
-                    if (c1) s_sc[(((e1 >> 7) & 127) + 1) * RS + (e1 & 127) + 1] = (uint8_t)(by - 1);
-                    const int cc = (int)c0 + (int)c1;
-                    const unsigned long long lt = (1ull << lane) - 1ull;
-                    const unsigned long long b0 = __ballot(cc & 1), b1 = __ballot(cc & 2);
-                    int pos = ncorner + __popcll(b0 & lt) + 2 * __popcll(b1 & lt);
-                    if (c0) s_cor[pos++] = (uint16_t)(e0 & 0x3FFFu);
-                    if (c1) s_cor[pos] = (uint16_t)(e1 & 0x3FFFu);
-                    ncorner += __popcll(b0) + 2 * __popcll(b1);
-                }
-                WAVE_SYNC();   // s_ent is refilled by the next chunk
-            }
-            if (ablate == 3) {
-                asm volatile("" ::"v"((int)s_sc[lane]));
-                stop = true;
-                break;
-            }
-            // NMS over corners (every other pixel has score 0); survivors compacted in place
-            nsurv = 0;
-            for (int i0 = 0; i0 < ncorner; i0 += 64) {
-                const int i = i0 + lane;
-                bool surv = false;
-                int p = 0;
-                if (i < ncorner) {
-                    p = s_cor[i];
-                    const uint8_t* q = s_sc + ((p >> 7) + 1) * RS + (p & 127) + 1;
-                    const int sc = q[0];
-                    surv = sc > q[-1] && sc > q[1] && sc > q[-RS - 1] && sc > q[-RS] && sc > q[-RS + 1] &&
-                           sc > q[RS - 1] && sc > q[RS] && sc > q[RS + 1];
-                }
-                const unsigned long long m = __ballot(surv);
-                if (surv) s_cor[nsurv + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)p;
-                nsurv += __popcll(m);
-            }
-            WAVE_SYNC();
-            if (nsurv > 0) break;
-        }   // attempt
-        if (stop) {
-            if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = 0;
-            WAVE_SYNC();
-            continue;
-        }
-        // emission of the survivors in row-major order (FAST's emission order)
-        int base = 0;
-        uint32_t* out = cellkeys + (size_t)b * g.cellkeys_per_img + L.cellkey_off + (size_t)me.local * L.cell_cap;
-        const int xr0 = me.c0 - ORBFE_MINB + 3, yr0 = me.r0 - ORBFE_MINB + 3;
-        for (int i0 = 0; i0 < nsurv; i0 += 64) {
-            const int i = i0 + lane;
-            int sc = 0, p = 0;
-            if (i < nsurv) {
-                p = s_cor[i];
-                sc = s_sc[((p >> 7) + 1) * RS + (p & 127) + 1];
-            }
-            const bool f = i < nsurv;
-            const unsigned long long m = __ballot(f);
-            const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
-            if (f) out[pos] = (uint32_t)(xr0 + (p & 127)) | ((uint32_t)(yr0 + (p >> 7)) << 12) | ((uint32_t)sc << 24);
-            base += __popcll(m);
-        }
-        if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = base;
-        WAVE_SYNC();   // LDS is restaged for the next cell
+        if (nd == 11)
+            fast_cell_detect<11>(g, fl, me, ng, nd, dw, dh, s_img, s_sc, s_cor, s_ent, cellkeys, cellcnt, b, c, lane, ablate);
+        else if (nd == 12)
+            fast_cell_detect<12>(g, fl, me, ng, nd, dw, dh, s_img, s_sc, s_cor, s_ent, cellkeys, cellcnt, b, c, lane, ablate);
+        else
+            fast_cell_detect<0>(g, fl, me, ng, nd, dw, dh, s_img, s_sc, s_cor, s_ent, cellkeys, cellcnt, b, c, lane, ablate);
     }
 }
 
@@ -1771,7 +1790,9 @@ __device__ __forceinline__ int hamming32(const uint32_t* a, const uint32_t* b) {
 // only the records with minr in [v - maxspan, v] (the reference's vRowIndices[v] superset; the
 // first-best-in-iR-order rule is kept by the (dist, iR) key).
 // Writes per left kp: uRight, depth (-1 = none) and the SAD distance of an accepted match (-1).
+#ifndef ST_LK
 #define ST_LK 256
+#endif
 #define ST_NT 1024
 struct RightRec { float x; int minr, maxr, oct; };
 __global__ __launch_bounds__(ST_NT) void k_stereo(OrbGeom g, StereoSide SL, StereoSide SR, StereoArgs sa,
