@@ -495,7 +495,9 @@ __device__ __forceinline__ int fast_M(const uint8_t* im, int stride, int x, int 
     return max((int)best.x, (int)best.y);
 }
 
+#ifndef FAST_CPW
 #define FAST_CPW 4    // cells per wave (the next cell's ROI is prefetched into registers)
+#endif
 #define FAST_PF 4     // prefetched 16-byte chunks per lane (rows / rows-per-load: 2 at W = 35)
 struct FastCell {
     int l, local, r0, c0, rows, cols, pitch;
