@@ -16,8 +16,9 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import platform
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -30,6 +31,9 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # Algorithmic bytes of the pyramid+FAST pass per 752x480 image: every level read
 # once + levels 1..7 written once.
 PYR_FAST_BYTES = {(752, 480): 1873774, (1241, 376): 2421578, (512, 512): 1361776}
+EUROC_BF, EUROC_FX = 0.110078 * 458.654, 458.654   # EuRoC MH_01 stereo: baseline x fx
+KITTI_BF, KITTI_FX = 0.5327 * 721.5377, 721.5377   # KITTI 2011_09_26 stereo
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2   # wave64 VALU instr/s: 1024 SIMD-32s, 2 cycles each (MI355X_MICROARCH.md)
 
 
 def level_sizes(w, h, nlevels=8, sf=1.2):
@@ -58,6 +62,20 @@ def pmc_traffic(n_img, w, h):
             continue
         if (d.get("images_per_step"), d.get("width"), d.get("height")) == (n_img, w, h):
             best = (d["pyramid_fast_traffic_bytes_per_step"], os.path.basename(f))
+    return best
+
+
+def tr_kernels(n_img, w, h):
+    """Per-kernel entries of the newest committed PMC traffic summary of this workload ({} if none)."""
+    import glob
+    best = {}
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if (d.get("images_per_step"), d.get("width"), d.get("height")) == (n_img, w, h):
+            best = d["kernels"]
     return best
 
 
@@ -101,32 +119,194 @@ def copy_peak_gbps(torch, dev, nbytes=1 << 30, reps=10):
     return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
-def cpu_baseline(pairs_l, pairs_r, w, h, nfeatures, bf, fx):
-    """Oracle CPU path (C++ restatement, kind='port') on a bounded sample, host cores."""
+def _host_cpu():
+    """nproc, the job's usable CPUs (affinity mask, cgroup quota) and lscpu's model / sockets."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity"] = os.cpu_count()
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    info["cgroup_cpu_quota"] = quota
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core"):
+                info[k.strip()] = v.strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return info
+
+
+def start_native_oracle_build():
+    """The reference builds with -O3 -march=native (CMakeLists.txt:11-14): compile the oracle's
+    extractor + stereo restatement for THIS host in the background (a few seconds) while the GPU
+    legs run. Returns (process, path) or (None, None)."""
+    out = os.path.join(tempfile.gettempdir(), f"orbfe_oracle_native_{os.getpid()}.so")
+    src = os.path.join(ROOT, "oracle", "orb_oracle.cpp")
+    cmd = ["g++", "-O3", "-march=native", "-ffp-contract=off", "-fno-fast-math", "-std=c++17", "-fPIC", "-shared",
+           "-o", out, src, "-lpthread"]
+    try:
+        return subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE), out
+    except OSError:
+        return None, None
+
+
+def _oracle_cdll(native):
+    """The -march=native oracle if it built, else the portable (x86-64-v3) checker build."""
+    import ctypes
+    from oracle import oracle
+    proc, path = native
+    flags = "-O3 -march=x86-64-v3 (portable oracle build; the native build failed)"
+    L = None
+    if proc is not None:
+        proc.wait()
+        if proc.returncode == 0 and os.path.exists(path):
+            L = ctypes.CDLL(path)
+            flags = "-O3 -march=native -ffp-contract=off (built on this host at bench time)"
+    if L is None:
+        oracle.build()
+        L = ctypes.CDLL(oracle.LIB)
+    vp, ci, cf, cd = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.POINTER(ctypes.c_double)
+    L.oro_bench_stereo.restype = ctypes.c_long
+    L.oro_bench_stereo.argtypes = [vp, vp, ci, ci, ci, ci, cf, ci, ci, ci, cf, cf, ci]
+    L.oro_bench_stereo_latency.restype = ctypes.c_long
+    L.oro_bench_stereo_latency.argtypes = [vp, vp, ci, ci, ci, ci, cf, ci, ci, ci, cf, cf, ci, cd]
+    L.oro_bench_mono.restype = ctypes.c_long
+    L.oro_bench_mono.argtypes = [vp, ci, ci, ci, ci, cf, ci, ci, ci, ci, ci, ci, cd]
+    return L, flags
+
+
+def cpu_baseline(native, budget_s=4.0):
+    """SURVEY §8(d) CPU timing of the oracle (the C++ restatement, kind='port') on this host, in
+    the same run: per config, 1-thread frame-serial latency, the reference's 2-thread L/R split
+    latency (Frame.cc:122-125, stereo configs), and throughput with one frame per thread on every
+    CPU the job may use. Each mode runs a bounded sample of about `budget_s` seconds."""
+    import ctypes
+    from orb_slam3_ros_amd.synth import synth_image, synth_stereo
+    L, flags = _oracle_cdll(native)
+    cpu = _host_cpu()
+    threads = cpu["affinity"] or 1
+    if cpu["cgroup_cpu_quota"]:
+        threads = max(1, min(threads, int(np.ceil(cpu["cgroup_cpu_quota"]))))
+    ms = ctypes.c_double()
+    out = {}
+
+    def stereo_cfg(name, W, H, nf, bf, fx, seed):
+        U = 8
+        pairs = [synth_stereo(seed + i, W, H) for i in range(U)]
+        Ls = np.ascontiguousarray(np.stack([p[0] for p in pairs]))
+        Rs = np.ascontiguousarray(np.stack([p[1] for p in pairs]))
+        L.oro_bench_stereo_latency(Ls.ctypes.data, Rs.ctypes.data, 1, W, H, nf, 1.2, 8, 20, 7, bf, fx, 0, ctypes.byref(ms))
+        est = max(ms.value, 1.0)
+        n1 = int(min(400, max(8, budget_s * 1e3 / est)))
+        idx = [i % U for i in range(n1)]
+        Ln, Rn = np.ascontiguousarray(Ls[idx]), np.ascontiguousarray(Rs[idx])
+        L.oro_bench_stereo_latency(Ln.ctypes.data, Rn.ctypes.data, n1, W, H, nf, 1.2, 8, 20, 7, bf, fx, 0,
+                                   ctypes.byref(ms))
+        lat1 = ms.value
+        L.oro_bench_stereo_latency(Ln.ctypes.data, Rn.ctypes.data, n1, W, H, nf, 1.2, 8, 20, 7, bf, fx, 1,
+                                   ctypes.byref(ms))
+        lat2 = ms.value
+        nt = int(min(20000, max(2 * threads, budget_s * 1e3 * threads / est)))
+        idx = [i % U for i in range(nt)]
+        Ln, Rn = np.ascontiguousarray(Ls[idx]), np.ascontiguousarray(Rs[idx])
+        t0 = time.perf_counter()
+        L.oro_bench_stereo(Ln.ctypes.data, Rn.ctypes.data, nt, W, H, nf, 1.2, 8, 20, 7, bf, fx, threads)
+        dt = time.perf_counter() - t0
+        out[name] = {"latency_1t_ms": round(lat1, 3), "latency_lr2t_ms": round(lat2, 3),
+                     "throughput_frames_per_s": round(nt / dt, 2), "throughput_threads": threads,
+                     "sample": f"{n1} frames per latency mode, {nt} frames for throughput ({U} distinct "
+                               f"synthetic {W}x{H} pairs, nFeatures {nf}); extract L+R + ComputeStereoMatches"}
+
+    def mono_cfg(name, W, H, nf, seed):
+        U = 8
+        imgs = np.ascontiguousarray(np.stack([synth_image(seed + i, W, H) for i in range(U)]))
+        L.oro_bench_mono(imgs.ctypes.data, 1, W, H, nf, 1.2, 8, 20, 7, 0, 1000, 1, ctypes.byref(ms))
+        est = max(ms.value, 1.0)
+        n1 = int(min(800, max(8, budget_s * 1e3 / est)))
+        idx = [i % U for i in range(n1)]
+        In = np.ascontiguousarray(imgs[idx])
+        L.oro_bench_mono(In.ctypes.data, n1, W, H, nf, 1.2, 8, 20, 7, 0, 1000, 1, ctypes.byref(ms))
+        lat1 = ms.value / n1
+        nt = int(min(40000, max(2 * threads, budget_s * 1e3 * threads / est)))
+        idx = [i % U for i in range(nt)]
+        In = np.ascontiguousarray(imgs[idx])
+        L.oro_bench_mono(In.ctypes.data, nt, W, H, nf, 1.2, 8, 20, 7, 0, 1000, threads, ctypes.byref(ms))
+        out[name] = {"latency_1t_ms": round(lat1, 3), "throughput_frames_per_s": round(nt / (ms.value * 1e-3), 2),
+                     "throughput_threads": threads,
+                     "sample": f"{n1} frames latency, {nt} frames throughput ({U} distinct synthetic {W}x{H} "
+                               f"images, nFeatures {nf}, vLappingArea {{0, 1000}} as the mono Frame passes)"}
+
+    t0 = time.perf_counter()
+    stereo_cfg("config2_euroc_stereo_752x480", 752, 480, 1000, EUROC_BF, EUROC_FX, 9000)
+    mono_cfg("config1_euroc_mono_752x480", 752, 480, 1000, 9100)
+    stereo_cfg("config3_kitti_stereo_1241x376", 1241, 376, 2000, KITTI_BF, KITTI_FX, 9200)
+    total = time.perf_counter() - t0
+    c2 = out["config2_euroc_stereo_752x480"]
+    return {"value": c2["throughput_frames_per_s"], "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": "config 2 throughput, one stereo frame per thread on every usable CPU; " + c2["sample"],
+            "latency_1t": c2["latency_1t_ms"], "latency_lr2t": c2["latency_lr2t_ms"],
+            "throughput_nproc": c2["throughput_frames_per_s"], "configs": out, "host": cpu,
+            "build": f"oracle/orb_oracle.cpp {flags}", "seconds": round(total, 2),
+            "note": "oracle CPU path (faithful C++ restatement), not OpenCV's SIMD code; threads = min(affinity, "
+                    "cgroup quota) — nproc reports the whole machine"}
+
+
+def parity_check(fe, images_host_pairs, frame_pair, nframes, nfeat, bf, fx, stereo="rectified", lap=(0, 0)):
+    """CHECKER, outside every timed region: frames 0..nframes-1 of the last step against the CPU
+    oracle (keypoint records, descriptors, monoIndex, uRight / depth bits, nmatch or the kNN
+    candidates). Returns (ok, message)."""
+    import concurrent.futures as cf
     from oracle import oracle
     oracle.build()
-    L = oracle.lib()
-    threads = max(1, min(16, os.cpu_count() or 1))
-    # bounded sample: about 10 s wall on 16 threads (the oracle needs ~40 ms per stereo frame per core)
-    n = min(max(400, 250 * threads), 4000)
-    idx = [i % len(pairs_l) for i in range(n)]
-    Ls = np.ascontiguousarray(np.stack([pairs_l[i] for i in idx]))
-    Rs = np.ascontiguousarray(np.stack([pairs_r[i] for i in idx]))
-    t0 = time.perf_counter()
-    L.oro_bench_stereo(Ls.ctypes.data, Rs.ctypes.data, n, w, h, nfeatures, 1.2, 8, 20, 7, bf, fx, threads)
-    dt = time.perf_counter() - t0
-    cpu = "unknown"
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
-    return {"value": round(n / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n} stereo frames {w}x{h} (extract L+R + ComputeStereoMatches), {threads} threads, "
-                      f"frame-parallel, oracle/orb_oracle.cpp -O3 -march=x86-64-v3; host CPU: {cpu}",
-            "seconds": round(dt, 3)}
+
+    def ref(p):
+        left, right = images_host_pairs[p]
+        ol, orr = oracle.OracleExtractor(nfeat, 1.2, 8, 20, 7), oracle.OracleExtractor(nfeat, 1.2, 8, 20, 7)
+        r = (ol(left, lap), orr(right, lap))
+        if stereo == "rectified":
+            r = r + (oracle.stereo_match(ol, orr, r[0][1], r[0][2], r[1][1], r[1][2], bf, fx),)
+        else:
+            ml, mr = r[0][0], r[1][0]
+            r = r + (oracle.stereo_knn_ratio(r[0][2][ml:], r[1][2][mr:], 0.7),)
+        return r
+
+    uniq = sorted({int(frame_pair[f]) for f in range(nframes)})
+    with cf.ThreadPoolExecutor(8) as ex:
+        refs = dict(zip(uniq, ex.map(ref, uniq)))
+    nmatch = fe.nmatch.cpu().numpy()
+    for f in range(nframes):
+        r = refs[int(frame_pair[f])]
+        for side in (0, 1):
+            mono, kp, d = fe.host_image(2 * f + side)
+            om, ok_, od = r[side]
+            if mono != om or len(kp) != len(ok_) or not np.array_equal(kp.view(np.uint32), ok_.view(np.uint32)) \
+                    or not np.array_equal(d, od):
+                return False, f"frame {f} side {side}: keypoints / descriptors differ from the oracle"
+        n = len(r[0][1])
+        if stereo == "rectified":
+            ur, dp, nm = r[2]
+            if int(nmatch[f]) != nm or not np.array_equal(fe.uright[f, :n].cpu().numpy().view(np.uint32),
+                                                          ur.view(np.uint32)) \
+                    or not np.array_equal(fe.depth[f, :n].cpu().numpy().view(np.uint32), dp.view(np.uint32)):
+                return False, f"frame {f}: ComputeStereoMatches output differs from the oracle"
+        else:
+            good, t, _ = r[2]
+            ml, mr = r[0][0], r[1][0]
+            l2r = fe.l2r[f, :n].cpu().numpy()
+            exp = np.full(n, -1, np.int32)
+            exp[ml:][t >= 0] = t[t >= 0] + mr
+            if int(nmatch[f]) != good or not np.array_equal(l2r, exp):
+                return False, f"frame {f}: fisheye kNN candidates differ from the oracle"
+    return True, f"frames 0..{nframes - 1} bit-exact vs the CPU oracle ({len(uniq)} distinct pairs)"
 
 
 def matcher_config5(steps):
@@ -204,6 +384,79 @@ def matcher_config5(steps):
             "per_th": out}
 
 
+def make_images(rank, W, H, F, U, dev, seed0=0):
+    """Interleaved [2F, H, W] device tensor of U distinct synthetic stereo pairs tiled over F frames
+    (frame f = pair f % U); returns (images, host pairs, frame -> pair map)."""
+    import torch
+    from orb_slam3_ros_amd.synth import synth_stereo
+    U = min(U, F)
+    pairs = [synth_stereo(seed0 + 1000 * rank + i, W, H) for i in range(U)]
+    host = np.empty((2 * F, H, W), np.uint8)
+    for f in range(F):
+        host[2 * f], host[2 * f + 1] = pairs[f % U]
+    return torch.from_numpy(host).to(dev), pairs, np.arange(F) % U
+
+
+def time_steps(fe, images, steps, warmup):
+    import torch
+    for _ in range(warmup):
+        fe.run(images)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fe.run(images)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def stage_times(fe, images, n):
+    import torch
+    fe.set_stage_timing(True)
+    for _ in range(n):
+        fe.run(images)
+    torch.cuda.synchronize()
+    st, _ = fe.stage_timing()
+    fe.set_stage_timing(False)
+    return st
+
+
+def pmc_valu(n_img, w, h):
+    """Per-kernel VALU instruction counts and wave states from the newest committed PMC summary of
+    this workload (profiles/rNN_pmc_valu.json, tools/pmc_valu_summary.py)."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_valu.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if (d.get("images_per_step"), d.get("width"), d.get("height")) == (n_img, w, h):
+            best = (d["kernels"], os.path.basename(f))
+    return best
+
+
+def side_leg(dev, name, W, H, nf, F, steps, warmup, stereo, lap, bf, fx, check_frames, seed0):
+    """A secondary BASELINE config on this GPU (rank 0, not part of `value`): throughput, stage
+    times, the pyramid+FAST kernel roofline and a post-timing parity check."""
+    from orb_slam3_ros_amd.frontend import StereoFrontEnd
+    images, pairs, fmap = make_images(0, W, H, F, 8, dev, seed0)
+    fe = StereoFrontEnd(F, W, H, nfeatures=nf, bf=bf, fx=fx, device=dev, lap_left=lap, lap_right=lap, stereo=stereo)
+    sec = time_steps(fe, images, steps, warmup)
+    st = stage_times(fe, images, max(3, steps // 2))
+    pf = st["resize"] + st["fast"]
+    nb = algorithmic_bytes(W, H)
+    ok, msg = parity_check(fe, pairs, fmap, min(check_frames, F), nf, bf, fx, stereo=stereo, lap=lap)
+    out = {"workload": name, "frames_per_step": F, "images_per_step": 2 * F, "ms_per_step": round(sec * 1e3, 4),
+           "frames_per_s": round(F / sec, 2), "stage_ms": {k: round(v, 4) for k, v in st.items()},
+           "pyramid_fast_roofline": {"achieved_GBps": round(2 * F * nb / (pf * 1e-3) / 1e9, 1),
+                                     "frac": round(2 * F * nb / (pf * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                     "bytes_per_image": nb, "kernel_ms_per_launch": round(pf, 4)},
+           "stereo_matches_per_frame_mean": float(fe.nmatch.float().mean().item()),
+           "parity": {"ok": ok, "detail": msg}}
+    fe.close()
+    return out, ok
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -217,6 +470,9 @@ def main():
     ap.add_argument("--pipelines", type=int, default=1, help="sub-batches on separate HIP streams")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true", help="skip the post-timing oracle check (profiling runs)")
+    ap.add_argument("--parity-frames", type=int, default=16)
+    ap.add_argument("--no-side-configs", action="store_true", help="skip the config 3 / config 4 legs")
     ap.add_argument("--stage-steps", type=int, default=10, help="extra steps with per-stage HIP events")
     ap.add_argument("--matcher-steps", type=int, default=10, help="config-5 SearchByProjection calls per th (0: skip)")
     ap.add_argument("--rectify-steps", type=int, default=5,
@@ -227,14 +483,17 @@ def main():
                     help="every rank uses cuda:0 (rehearse N ranks on a 1-GPU box with --dist-backend gloo)")
     args = ap.parse_args()
 
+    native = (None, None)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        native = start_native_oracle_build()   # compiles while the GPU legs run
+
     import torch
     import torch.distributed as dist
     from orb_slam3_ros_amd.frontend import StereoFrontEnd
-    from orb_slam3_ros_amd.synth import synth_stereo
     from orb_slam3_ros_amd import distributed as odist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local_rank = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
@@ -247,13 +506,8 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
 
     W, H, F = args.width, args.height, args.frames
-    bf, fx = 0.110078 * 458.654, 458.654   # EuRoC stereo baseline x fx
-    U = min(args.unique, F)
-    pairs = [synth_stereo(1000 * rank + i, W, H) for i in range(U)]
-    host = np.empty((2 * F, H, W), np.uint8)
-    for f in range(F):
-        host[2 * f], host[2 * f + 1] = pairs[f % U]
-    images = torch.from_numpy(host).to(dev)
+    bf, fx = EUROC_BF, EUROC_FX
+    images, pairs, fmap = make_images(rank, W, H, F, args.unique, dev)
     fe = StereoFrontEnd(F, W, H, nfeatures=args.nfeatures, bf=bf, fx=fx, device=dev, pipelines=args.pipelines)
     gather = world > 1 and not args.no_allgather
     if gather:
@@ -298,15 +552,19 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
     value = world * F * args.steps / elapsed
 
+    # ---- checker: the last timed step's outputs against the CPU oracle (outside the timed region)
+    parity = None
+    if not args.no_parity:
+        ok, msg = parity_check(fe, pairs, fmap, min(args.parity_frames, F), args.nfeatures, bf, fx)
+        parity = {"ok": ok, "detail": msg, "rank": rank}
+        if not ok:
+            print(json.dumps({"parity": parity}), file=sys.stderr, flush=True)
+            sys.exit(3)
+
     # per-stage HIP-event timing on the launch stream (separate steps, same workload, one pipeline
     # so the events bracket kernels that run alone on the GPU)
     fe_t = fe if args.pipelines == 1 else StereoFrontEnd(F, W, H, nfeatures=args.nfeatures, bf=bf, fx=fx, device=dev)
-    fe_t.set_stage_timing(True)
-    for _ in range(args.stage_steps):
-        fe_t.run(images)
-    torch.cuda.synchronize()
-    stages, nrec = fe_t.stage_timing()
-    fe_t.set_stage_timing(False)
+    stages = stage_times(fe_t, images, args.stage_steps)
     if fe_t is not fe:
         fe_t.close()
     rect = None
@@ -325,9 +583,10 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         rms = e0.elapsed_time(e1) / args.rectify_steps
-        rbytes = images.numel() * (1 + 1) + 2 * 4 * W * H   # read + write per image, maps once (L2 / IC)
+        rbytes = images.numel() * (1 + 1) + 2 * 4 * W * H   # read + write per image, maps once
         rect = {"ms_per_step": round(rms, 4), "images": int(images.shape[0]),
-                "achieved_GBps": round(rbytes / (rms * 1e-3) / 1e9, 1)}
+                "achieved_GBps": round(rbytes / (rms * 1e-3) / 1e9, 1),
+                "algorithmic_bytes_per_step": int(rbytes)}
         del rout
     counts = fe.counts.cpu().numpy()
     nm = fe.nmatch.cpu().numpy()
@@ -340,6 +599,7 @@ def main():
         dominant = max(stages, key=stages.get)
         tr = pmc_traffic(n_img, W, H)
         cache = pmc_cache(n_img, W, H)
+        valu = pmc_valu(n_img, W, H)
         copy_peak = copy_peak_gbps(torch, dev)
         result = {
             "metric": METRIC,
@@ -388,18 +648,47 @@ def main():
             "dominant_stage": dominant,
             "keypoints_per_image_mean": float(counts[:, 0].mean()),
             "stereo_matches_per_frame_mean": float(nm.mean()),
+            "parity": parity,
         }
+        if valu is not None:
+            # VALU issue fraction per kernel: committed SQ_INSTS_VALU per launch over this run's kernel
+            # time x the wave64 issue peak (2 cycles per instruction on each of 1024 SIMD-32s)
+            kt = {"k_resize": stages["resize"], "k_fast": stages["fast"], "k_octree": stages["octree"],
+                  "k_describe": stages["describe"]}
+            result["roofline"]["valu_issue_frac"] = {
+                k: round(v["valu_per_step"] / (kt[k] * 1e-3) / VALU_ISSUE_PEAK, 4)
+                for k, v in valu[0].items() if k in kt and kt[k] > 0}
+            result["roofline"]["valu_source"] = valu[1]
         if cache is not None and "k_describe" in cache[0]:
             kd = cache[0]["k_describe"]
             result["describe_pass"] = {"kernel": "k_describe", "l2_hit_rate": kd["l2_hit_rate"],
                                        "lds_bank_conflict_share": kd["lds_conflict_share"], "source": cache[1]}
         if rect is not None:
+            if tr is not None and "k_remap" in tr_kernels(n_img, W, H):
+                rk = tr_kernels(n_img, W, H)["k_remap"]
+                rect["pmc_traffic_bytes_per_step"] = rk["read_bytes_per_step"] + rk["write_bytes_per_step"]
             result["rectify_remap"] = rect
+        if world == 1 and not args.no_side_configs:
+            legs, all_ok = {}, True
+            legs["config3"], ok3 = side_leg(dev, "KITTI-like stereo 1241x376, nFeatures 2000 (BASELINE config 3): "
+                                                 "extract L+R + ComputeStereoMatches", 1241, 376, 2000, 256,
+                                            max(3, args.steps // 2), 2, "rectified", (0, 0), KITTI_BF, KITTI_FX, 8,
+                                            20000)
+            legs["config4_step"], ok4 = side_leg(dev, "TUM-VI-like 512x512 KannalaBrandt8 stereo, per-GPU step of "
+                                                      "BASELINE config 4: 8 images (4 stereo frames), vLappingArea "
+                                                      "{0,511}, batched knnMatch(k=2)+ratio", 512, 512, 1000, 4,
+                                                 max(10, args.steps), 3, "fisheye", (0, 511), 0.0, 1.0, 4, 21000)
+            legs["config4_batch"], ok4b = side_leg(dev, "as config4_step at a 512-image batch (throughput)", 512, 512,
+                                                   1000, 256, max(3, args.steps // 2), 2, "fisheye", (0, 511), 0.0,
+                                                   1.0, 4, 22000)
+            result["side_configs"] = legs
+            if not (ok3 and ok4 and ok4b):
+                print(json.dumps(result), file=sys.stderr, flush=True)
+                sys.exit(3)
         if args.matcher_steps > 0:
             result["matcher_config5"] = matcher_config5(args.matcher_steps)
-        if not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline([p[0] for p in pairs], [p[1] for p in pairs], W, H,
-                                                  args.nfeatures, bf, fx)
+        if not args.no_cpu_baseline and world == 1:
+            result["cpu_baseline"] = cpu_baseline(native)
         print(json.dumps(result), flush=True)
     fe.close()
     if world > 1:

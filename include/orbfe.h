@@ -74,21 +74,27 @@ int orbfe_pyramid_level(orbfe_extractor* h, int image, int level, uint8_t* dst, 
  * (NULL = the handle's own stream). Outputs stay on the device: see orbfe_batch_outputs. */
 int orbfe_extract_batch(orbfe_extractor* h, int nimg, const uint8_t* const* d_imgs, int width, int height,
                         int pitch, int lap0, int lap1, void* stream);
+/* orbfe_extract_batch with a vLappingArea per image: laps[2*i], laps[2*i+1] (host array) for image i,
+ * e.g. the left and right KannalaBrandt8 cameras' own mvLappingArea (Frame.cc:1059-1060). */
+int orbfe_extract_batch_laps(orbfe_extractor* h, int nimg, const uint8_t* const* d_imgs, int width, int height,
+                             int pitch, const int32_t* laps, void* stream);
+
 /* Device pointers of the last batch: kps[nimg][cap], desc[nimg][cap][32], counts[nimg][2] =
  * {n, monoIndex}. Valid until the next call on this handle. */
 int orbfe_batch_outputs(orbfe_extractor* h, orbfe_keypoint** d_kps, uint8_t** d_desc, int** d_counts, int* cap);
 
 /* Make later orbfe_extract_batch calls write their outputs into caller-owned device buffers
  * (kps[cap_images][cap], desc[cap_images][cap][32], counts[cap_images][2]) instead of the
- * handle's own; cap = orbfe_extractor_capacity(). Pass NULLs to revert. */
+ * handle's own; cap = orbfe_extractor_capacity(). Pass NULLs to revert. While bound, a batch of more
+ * than cap_images images fails with ORBFE_E_CAPACITY. The host API (orbfe_extract) never uses them. */
 int orbfe_set_batch_outputs(orbfe_extractor* h, orbfe_keypoint* d_kps, uint8_t* d_desc, int* d_counts,
                             int cap_images);
 
 /* Per-kernel HIP-event timing (for bench.py's roofline). While enabled, every batch records
  * events around each stage on the stream it runs on (no host sync). orbfe_get_stage_timing waits
  * for the recorded batches, writes the MEAN ms per batch of each stage to ms[0..ORBFE_NUM_STAGES)
- * = {resize (all levels), blur, fast, octree, describe}, resets, and returns the batch count. */
-#define ORBFE_NUM_STAGES 5
+ * = {resize (all levels), fast, octree, describe}, resets, and returns the batch count. */
+#define ORBFE_NUM_STAGES 4
 int orbfe_set_stage_timing(orbfe_extractor* h, int enable);
 int orbfe_get_stage_timing(orbfe_extractor* h, float* ms);
 
@@ -225,6 +231,17 @@ int orbfe_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, c
  * TriangulateMatches post-filter stays with the camera model on the host. */
 int orbfe_stereo_knn_ratio(const uint8_t* left_desc, int32_t nl, const uint8_t* right_desc, int32_t nr,
                            float ratio, int32_t* out_train, int32_t* out_dist);
+
+/* Batched, device-resident form of the same stage for nframes KannalaBrandt8 stereo frames over
+ * the last batch outputs of the extractor handles (the lapping-area rows the reference slices out,
+ * Frame.cc:1129-1133): frame f's queries are rows [monoIndex, n) of left image (lbase + f*lstep),
+ * its train rows [monoIndex, n) of right image (rbase + f*rstep) (left == right allowed).
+ * Device outputs, [nframes][cap] in the frame's full keypoint numbering: d_l2r[i] = right keypoint
+ * index (trainIdx + monoRight) if Lowe's test passes (the mvLeftToRightMatch candidate before the
+ * host-side TriangulateMatches depth check) else -1; d_dist[i] its distance or -1;
+ * d_ngood[nframes] = passing queries per frame (descMatches). Enqueued on stream, no host sync. */
+int orbfe_stereo_knn_batch(orbfe_extractor* left, int lbase, int lstep, orbfe_extractor* right, int rbase, int rstep,
+                           int nframes, float ratio, int32_t* d_l2r, int32_t* d_dist, int32_t* d_ngood, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Local-map projection (the step before SearchByProjection in Tracking::SearchLocalPoints,

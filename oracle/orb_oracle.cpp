@@ -33,6 +33,7 @@
 // Built with -ffp-contract=off (see oracle/Makefile).
 // ============================================================================================
 #include <algorithm>
+#include <chrono>
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
@@ -836,6 +837,72 @@ long oro_bench_stereo(const uint8_t* L, const uint8_t* R, int nframes, int w, in
     long s = 0;
     for (long v : tot) s += v;
     return s;
+}
+
+// CPU latency modes of SURVEY §8(d), one frame at a time on the calling thread:
+//   lr_split = 0: extract(L), extract(R), ComputeStereoMatches, all on one thread (frame-serial);
+//   lr_split = 1: the reference's split (Frame.cc:122-125): two std::threads per frame run
+//                 ExtractORB(left) / ExtractORB(right) on separate extractor instances, joined, then
+//                 ComputeStereoMatches on the calling thread.
+// *ms_per_frame = mean wall time per frame. Returns the total stereo matches.
+long oro_bench_stereo_latency(const uint8_t* L, const uint8_t* R, int nframes, int w, int h, int nfeatures,
+                              float sf, int nlevels, int ini, int mn, float bf, float fx, int lr_split,
+                              double* ms_per_frame) {
+    Extractor el(nfeatures, sf, nlevels, ini, mn), er(nfeatures, sf, nlevels, ini, mn);
+    std::vector<KeyPoint> kl, kr;
+    std::vector<uint8_t> dl, dr;
+    std::vector<float> ur, dp;
+    long tot = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int f = 0; f < nframes; f++) {
+        Image a, b;
+        a.w = b.w = w; a.h = b.h = h;
+        a.px.assign(L + (size_t)f * w * h, L + (size_t)(f + 1) * w * h);
+        b.px.assign(R + (size_t)f * w * h, R + (size_t)(f + 1) * w * h);
+        if (lr_split) {
+            std::thread tl([&]() { el.extract(a, 0, 0, kl, dl); });
+            std::thread tr([&]() { er.extract(b, 0, 0, kr, dr); });
+            tl.join();
+            tr.join();
+        } else {
+            el.extract(a, 0, 0, kl, dl);
+            er.extract(b, 0, 0, kr, dr);
+        }
+        ur.resize(kl.size() + 1); dp.resize(kl.size() + 1);
+        tot += oro_stereo_match(&el, &er, kl.data(), dl.data(), (int)kl.size(), kr.data(), dr.data(), (int)kr.size(),
+                                bf, fx, ur.data(), dp.data());
+    }
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (ms_per_frame) *ms_per_frame = nframes > 0 ? ms / nframes : 0.0;
+    return tot;
+}
+
+// Monocular frames (config 1): ORBextractor::operator() with the mono Frame's vLappingArea
+// (Frame.cc:311 passes {0, 1000}), `nthreads` frames in flight (1 = frame-serial latency).
+// Returns the total keypoints; *ms_total = wall time.
+long oro_bench_mono(const uint8_t* imgs, int nimg, int w, int h, int nfeatures, float sf, int nlevels, int ini, int mn,
+                    int lap0, int lap1, int nthreads, double* ms_total) {
+    std::vector<std::thread> th;
+    std::vector<long> counts(nthreads, 0);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int t = 0; t < nthreads; t++) {
+        th.emplace_back([&, t]() {
+            Extractor e(nfeatures, sf, nlevels, ini, mn);
+            std::vector<KeyPoint> out;
+            std::vector<uint8_t> d;
+            for (int i = t; i < nimg; i += nthreads) {
+                Image im; im.w = w; im.h = h;
+                im.px.assign(imgs + (size_t)i * w * h, imgs + (size_t)(i + 1) * w * h);
+                e.extract(im, lap0, lap1, out, d);
+                counts[t] += (long)out.size();
+            }
+        });
+    }
+    for (auto& t : th) t.join();
+    if (ms_total) *ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    long tot = 0;
+    for (long c : counts) tot += c;
+    return tot;
 }
 
 }  // extern "C"

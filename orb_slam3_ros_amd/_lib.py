@@ -17,8 +17,8 @@ ORBFE_E_EMPTY = -1
 ORBFE_E_ARG = -2
 ORBFE_E_DEVICE = -3
 ORBFE_E_CAPACITY = -4
-ORBFE_NUM_STAGES = 5
-STAGE_NAMES = ("resize", "blur", "fast", "octree", "describe")
+ORBFE_NUM_STAGES = 4
+STAGE_NAMES = ("resize", "fast", "octree", "describe")
 
 
 class OrbKeyPoint(ctypes.Structure):
@@ -40,6 +40,7 @@ _SIGS = {
     "orbfe_extract": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _P_int]),
     "orbfe_pyramid_level": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _P_int, _P_int]),
     "orbfe_extract_batch": (_c_int, [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp]),
+    "orbfe_extract_batch_laps": (_c_int, [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp]),
     "orbfe_batch_outputs": (_c_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp), _P_int]),
     "orbfe_set_stage_timing": (_c_int, [_vp, _c_int]),
     "orbfe_set_batch_outputs": (_c_int, [_vp, _vp, _vp, _vp, _c_int]),
@@ -70,6 +71,8 @@ _SIGS = {
     "orbfe_search_by_projection_sim3": (_c_int, [_vp, _vp, _vp, _c_int, _vp, _c_int, _c_float, _vp, _vp]),
     "orbfe_search_by_sim3": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_float, _vp, _vp]),
     "orbfe_stereo_knn_ratio": (_c_int, [_vp, _c_int, _vp, _c_int, _c_float, _vp, _vp]),
+    "orbfe_stereo_knn_batch": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp,
+                                        _vp]),
     "orbfe_matcher_set_timing": (_c_int, [_c_int]),
     "orbfe_undistort_points": (_c_int, [_vp, _c_int, _vp, _vp, _c_int, _vp]),
     "orbfe_remap_linear": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _c_int, _vp, _c_int]),

@@ -78,7 +78,6 @@ struct orbfe_extractor {
     // device buffers
     int16_t* d_tab = nullptr;
     uint8_t* d_pyr = nullptr;
-    uint8_t* d_blur = nullptr;
     uint32_t* d_cellkeys = nullptr;
     int* d_cellcnt = nullptr;
     uint32_t* d_lkeys = nullptr;
@@ -95,13 +94,14 @@ struct orbfe_extractor {
     float* d_uright = nullptr;
     float* d_depth = nullptr;
     int* d_nmatch = nullptr;
-    int stereo_cap_frames = 0;
     int* d_sdist = nullptr;       // per left kp SAD distance of accepted stereo matches
-    int sdist_frames = 0;
+    int sdist_frames = 0, sdist_kp = 0;   // d_sdist holds sdist_frames x sdist_kp entries
+    int stereo_kp = 0;            // d_uright / d_depth (host-API stereo) hold stereo_kp entries
     std::mutex mu_stereo;
     // last batch description
     int last_nimg = 0, last_pitch = 0;
     std::vector<const uint8_t*> last_ptrs;
+    std::vector<int> last_laps;   // vLappingArea {lap0, lap1} per image of the last batch
     // stage timing
     bool timing = false;
     hipEvent_t ev[ORBFE_NUM_STAGES + 1] = {};   // spare set (host API)
@@ -117,13 +117,11 @@ struct orbfe_extractor {
     uint8_t* last_desc = nullptr;
     int* last_counts = nullptr;
     std::mutex mu;
-    int ablate_fast = 0;   // ORBFE_ABLATE_FAST: timing-only builds of k_fast (outputs invalid when != 0)
-    int ablate_desc = 0;   // ORBFE_ABLATE_DESC: the same for k_describe
-    unsigned long long* d_oct_ts = nullptr;   // ORBFE_OCT_STAMPS: per-phase s_memtime of the octree (image 0)
+    unsigned long long* d_oct_ts = nullptr;   // -DORBFE_OCT_STAMPS builds: per-phase s_memtime of the octree (image 0)
 };
 
 static void free_buffers(orbfe_extractor* h) {
-    void** bufs[] = {(void**)&h->d_tab, (void**)&h->d_pyr, (void**)&h->d_blur, (void**)&h->d_cellkeys,
+    void** bufs[] = {(void**)&h->d_tab, (void**)&h->d_pyr, (void**)&h->d_cellkeys,
                      (void**)&h->d_cellcnt, (void**)&h->d_lkeys, (void**)&h->d_nodeof, (void**)&h->d_outkeys,
                      (void**)&h->d_lvinfo, (void**)&h->d_ranks, (void**)&h->d_kps, (void**)&h->d_desc,
                      (void**)&h->d_counts, (void**)&h->d_ptrs};
@@ -132,19 +130,26 @@ static void free_buffers(orbfe_extractor* h) {
         *p = nullptr;
     }
     h->cap_b = 0;
+    h->last_nimg = 0;   // the previous batch's intermediates are gone
+    h->last_kps = nullptr;
+    h->last_desc = nullptr;
+    h->last_counts = nullptr;
+    h->last_ptrs.clear();
+    h->last_laps.clear();
 }
 
-// Per-level geometry with the reference's expressions (see orbfe_types.h).
-static int build_geom(orbfe_extractor* h, int W, int H) {
-    OrbGeom& g = h->g;
+// Per-level geometry with the reference's expressions (see orbfe_types.h), derived into the
+// caller's locals: the handle's current geometry stays untouched when the size is rejected.
+static int build_geom(const orbfe_extractor* h, int W, int H, OrbGeom& g, std::vector<int16_t>& tab,
+                      FastLds& fast_lds, size_t& oct_lds) {
     memset(&g, 0, sizeof(g));
     g.nlevels = h->nlevels;
     g.width = W;
     g.height = H;
     g.ini_th = std::min(std::max(h->ini_th, 0), 255);
     g.min_th = std::min(std::max(h->min_th, 0), 255);
-    h->tab.clear();
-    int cell_base = 0, cellkey_off = 0, out_off = 0, pyr_off = 0, blur_off = 0, tile_base = 0;
+    tab.clear();
+    int cell_base = 0, cellkey_off = 0, out_off = 0, pyr_off = 0;
     int max_cells = 0, node_cap = 0;
     FastLds fl{0, 0, 0, 0};
     int pw = W, ph = H;
@@ -161,8 +166,6 @@ static int build_geom(orbfe_extractor* h, int W, int H) {
         L.pitch = round_up(L.w, 16);
         L.pyr_off = l == 0 ? 0 : pyr_off;
         if (l > 0) pyr_off += round_up(L.pitch * L.h, 256);
-        L.blur_off = blur_off;
-        blur_off += round_up(L.pitch * L.h, 256);
         // FAST cell grid (ORBextractor.cc:789-803)
         const int minB = ORBFE_MINB, maxBX = L.w - ORBFE_MINB, maxBY = L.h - ORBFE_MINB;
         const float width = (float)(maxBX - minB), height = (float)(maxBY - minB);
@@ -199,7 +202,7 @@ static int build_geom(orbfe_extractor* h, int W, int H) {
         if (l > 0) {
             const double inv_x = (double)L.w / pw, inv_y = (double)L.h / ph;
             const double scale_x = 1. / inv_x, scale_y = 1. / inv_y;
-            L.tab_x = (int)h->tab.size();
+            L.tab_x = (int)tab.size();
             int xmax = L.w;
             for (int dx = 0; dx < L.w; dx++) {
                 float fx = (float)((dx + 0.5) * scale_x - 0.5);
@@ -210,21 +213,21 @@ static int build_geom(orbfe_extractor* h, int W, int H) {
                     xmax = std::min(xmax, dx);
                     if (sx >= pw - 1) { fx = 0; sx = pw - 1; }
                 }
-                h->tab.push_back((int16_t)sx);
-                h->tab.push_back(sat_s16((1.f - fx) * 2048));
-                h->tab.push_back(sat_s16(fx * 2048));
+                tab.push_back((int16_t)sx);
+                tab.push_back(sat_s16((1.f - fx) * 2048));
+                tab.push_back(sat_s16(fx * 2048));
             }
             L.xmax = xmax;
-            L.tab_y = (int)h->tab.size();
+            L.tab_y = (int)tab.size();
             for (int dy = 0; dy < L.h; dy++) {
                 float fy = (float)((dy + 0.5) * scale_y - 0.5);
                 int sy = cv_floor(fy);
                 fy -= sy;
                 auto clip = [&](int v) { return v < 0 ? 0 : (v >= ph ? ph - 1 : v); };
-                h->tab.push_back((int16_t)clip(sy));
-                h->tab.push_back((int16_t)clip(sy + 1));
-                h->tab.push_back(sat_s16((1.f - fy) * 2048));
-                h->tab.push_back(sat_s16(fy * 2048));
+                tab.push_back((int16_t)clip(sy));
+                tab.push_back((int16_t)clip(sy + 1));
+                tab.push_back(sat_s16((1.f - fy) * 2048));
+                tab.push_back(sat_s16(fy * 2048));
             }
             int x = 0;
             const int lanes = h->resize_simd_lanes;
@@ -237,8 +240,8 @@ static int build_geom(orbfe_extractor* h, int W, int H) {
             // every tile of the level (checked exactly on the coefficient tables)
             (void)scale_x;
             (void)scale_y;
-            const int16_t* tx = h->tab.data() + L.tab_x;
-            const int16_t* ty = h->tab.data() + L.tab_y;
+            const int16_t* tx = tab.data() + L.tab_x;
+            const int16_t* ty = tab.data() + L.tab_y;
             auto rows_fit = [&](int tr) {
                 for (int y0 = 0; y0 < L.h; y0 += tr) {
                     const int y1 = std::min(y0 + tr, L.h);
@@ -261,10 +264,6 @@ static int build_geom(orbfe_extractor* h, int W, int H) {
             L.rz_rows = tr;
             L.rz_cols = tc;
         }
-        L.blur_tiles_x = (L.w + BL_TW - 1) / BL_TW;
-        L.blur_tiles_y = (L.h + BL_TH - 1) / BL_TH;
-        L.blur_tile_base = tile_base;
-        tile_base += L.blur_tiles_x * L.blur_tiles_y;
         pw = L.w;
         ph = L.h;
     }
@@ -273,13 +272,13 @@ static int build_geom(orbfe_extractor* h, int W, int H) {
     g.out_per_img = out_off;
     g.kp_cap = out_off;
     g.pyr_bytes = round_up(std::max(pyr_off, 256), 256);
-    g.blur_bytes = round_up(blur_off, 256);
-    g.blur_tiles = tile_base;
     g.max_cells_level = max_cells;
     g.node_cap = node_cap;
     fl.wave_bytes = fl.roi + fl.sc + fl.cor + FAST_ENT_BYTES;
-    h->fast_lds = fl;
-    h->oct_lds = octree_lds_bytes(g);
+    fast_lds = fl;
+    oct_lds = octree_lds_bytes(g);
+    if (oct_lds > 160 * 1024) return ORBFE_E_ARG;
+    if ((size_t)4 * fast_lds.wave_bytes > 160 * 1024) return ORBFE_E_ARG;   // k_fast: 4 waves per block
     return ORBFE_OK;
 }
 
@@ -287,16 +286,23 @@ static int ensure(orbfe_extractor* h, int W, int H, int B) {
     if (W == h->W && H == h->H && B <= h->cap_b) return ORBFE_OK;
     HIPCHK(hipSetDevice(h->device));
     if (W != h->W || H != h->H) {
-        free_buffers(h);
-        int rc = build_geom(h, W, H);
+        // a rejected size leaves the handle exactly as it was (geometry, tables and buffers)
+        OrbGeom g;
+        std::vector<int16_t> tab;
+        FastLds fl{};
+        size_t oct = 0;
+        int rc = build_geom(h, W, H, g, tab, fl, oct);
         if (rc) return rc;
+        free_buffers(h);
+        h->g = g;
+        h->tab.swap(tab);
+        h->fast_lds = fl;
+        h->oct_lds = oct;
         h->W = W;
         h->H = H;
     } else {
         free_buffers(h);
     }
-    if (h->oct_lds > 160 * 1024) return ORBFE_E_ARG;
-    if ((size_t)4 * h->fast_lds.wave_bytes > 160 * 1024) return ORBFE_E_ARG;   // k_fast: 4 waves per block
     B = std::max(B, 1);
     const OrbGeom& g = h->g;
     HIPCHK(hipMalloc(&h->d_tab, std::max<size_t>(2, h->tab.size() * 2)));
@@ -312,20 +318,32 @@ static int ensure(orbfe_extractor* h, int W, int H, int B) {
     HIPCHK(hipMalloc(&h->d_kps, (size_t)B * g.kp_cap * sizeof(OrbKeyPoint)));
     HIPCHK(hipMalloc(&h->d_desc, (size_t)B * g.kp_cap * 32));
     HIPCHK(hipMalloc(&h->d_counts, (size_t)B * 2 * 4));
-    HIPCHK(hipMalloc(&h->d_ptrs, (size_t)B * sizeof(void*)));
+    HIPCHK(hipMalloc(&h->d_ptrs, (size_t)B * (sizeof(void*) + 2 * sizeof(int))));   // image pointers, then laps
     h->cap_b = B;
     h->last_ptrs.clear();
+    h->last_laps.clear();
     return ORBFE_OK;
 }
 
-static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs, int pitch, int lap0, int lap1,
-                     hipStream_t s) {
+static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs, int pitch, const int* laps,
+                     hipStream_t s, bool use_ext) {
     const OrbGeom& g = h->g;
+    // caller-owned outputs (orbfe_set_batch_outputs) too small for this batch: refuse rather than
+    // silently writing the handle's own buffers
+    if (use_ext && h->ext_kps && B > h->ext_cap_images) return ORBFE_E_CAPACITY;
     bool same = (int)h->last_ptrs.size() == B;
     for (int i = 0; same && i < B; i++) same = h->last_ptrs[i] == host_ptrs[i];
+    for (int i = 0; same && i < 2 * B; i++) same = h->last_laps[i] == laps[i];
+    int2* d_laps = (int2*)((uint8_t*)h->d_ptrs + (size_t)B * sizeof(void*));
     if (!same) {
         h->last_ptrs.assign(host_ptrs, host_ptrs + B);
-        HIPCHK(hipMemcpyAsync(h->d_ptrs, h->last_ptrs.data(), (size_t)B * sizeof(void*), hipMemcpyHostToDevice, s));
+        h->last_laps.assign(laps, laps + 2 * B);
+        std::vector<uint8_t> pk((size_t)B * (sizeof(void*) + 2 * sizeof(int)));
+        memcpy(pk.data(), h->last_ptrs.data(), (size_t)B * sizeof(void*));
+        memcpy(pk.data() + (size_t)B * sizeof(void*), h->last_laps.data(), (size_t)B * 2 * sizeof(int));
+        // synchronous w.r.t. the host buffer (pageable source), ordered on s for the device
+        HIPCHK(hipMemcpyAsync(h->d_ptrs, pk.data(), pk.size(), hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
     }
     h->last_nimg = B;
     h->last_pitch = pitch;
@@ -342,7 +360,7 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
         ev = h->ev_ring[h->ev_used++].data();
         HIPCHK(hipEventRecord(ev[0], s));
     }
-    const bool ext = h->ext_kps && B <= h->ext_cap_images;
+    const bool ext = use_ext && h->ext_kps;
     OrbKeyPoint* o_kps = ext ? h->ext_kps : h->d_kps;
     uint8_t* o_desc = ext ? h->ext_desc : h->d_desc;
     int* o_counts = ext ? h->ext_counts : h->d_counts;
@@ -352,20 +370,18 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
         hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, s, P, pitch, h->d_pyr, g.pyr_bytes, h->d_tab, g, l);
     }
     if (tm) HIPCHK(hipEventRecord(ev[1], s));
-    BlurKernel bk;
+    BlurKernel bk;   // the Gaussian blur is fused into k_describe
     memcpy(bk.k, h->blur_variant == 1 ? kBlurRound : kBlurED, sizeof(bk.k));
-    if (tm) HIPCHK(hipEventRecord(ev[2], s));   // the blur is fused into k_describe (stage kept for the layout)
     hipLaunchKernelGGL(k_fast, dim3((g.total_cells + 4 * FAST_CPW - 1) / (4 * FAST_CPW), B), dim3(256),
                        (size_t)4 * h->fast_lds.wave_bytes, s, P, pitch, h->d_pyr, g.pyr_bytes, g, h->fast_lds,
-                       h->d_cellkeys, h->d_cellcnt, h->ablate_fast);
-    if (tm) HIPCHK(hipEventRecord(ev[3], s));
+                       h->d_cellkeys, h->d_cellcnt);
+    if (tm) HIPCHK(hipEventRecord(ev[2], s));
     hipLaunchKernelGGL(k_octree, dim3(B, g.nlevels), dim3(OCT_NT), h->oct_lds, s, g, h->d_cellkeys, h->d_cellcnt,
-                       h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, lap0, lap1, h->d_oct_ts);
-    if (tm) HIPCHK(hipEventRecord(ev[4], s));
+                       h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, d_laps, h->d_oct_ts);
+    if (tm) HIPCHK(hipEventRecord(ev[3], s));
     hipLaunchKernelGGL(k_describe, dim3((g.out_per_img + 4 * DP_KPW - 1) / (4 * DP_KPW), B), dim3(256), 0, s, P, pitch, h->d_pyr,
-                       g.pyr_bytes, g, h->d_outkeys, h->d_lvinfo, h->d_ranks, o_kps, o_desc, o_counts, bk,
-                       h->ablate_desc);
-    if (tm) HIPCHK(hipEventRecord(ev[5], s));
+                       g.pyr_bytes, g, h->d_outkeys, h->d_lvinfo, h->d_ranks, o_kps, o_desc, o_counts, bk);
+    if (tm) HIPCHK(hipEventRecord(ev[4], s));
     HIPCHK(hipGetLastError());
     h->last_kps = o_kps;
     h->last_desc = o_desc;
@@ -410,12 +426,10 @@ int orbfe_extractor_create(int nfeatures, float scaleFactor, int nlevels, int in
     h->min_th = minThFAST;
     h->scale_factor_f = scaleFactor;
     h->scale_factor = scaleFactor;   // double member initialised from the float argument (ORBextractor.h:96)
-    if (const char* ab = getenv("ORBFE_ABLATE_FAST")) h->ablate_fast = atoi(ab);
-    if (const char* ab = getenv("ORBFE_ABLATE_DESC")) h->ablate_desc = atoi(ab);
-    if (getenv("ORBFE_OCT_STAMPS")) {
-        if (hipMalloc(&h->d_oct_ts, 64 * 8 * ORBFE_MAX_LEVELS) != hipSuccess) { delete h; return ORBFE_E_DEVICE; }
-        (void)hipMemset(h->d_oct_ts, 0, 64 * 8 * ORBFE_MAX_LEVELS);
-    }
+#if ORBFE_OCT_STAMPS
+    if (hipMalloc(&h->d_oct_ts, 64 * 8 * ORBFE_MAX_LEVELS) != hipSuccess) { delete h; return ORBFE_E_DEVICE; }
+    (void)hipMemset(h->d_oct_ts, 0, 64 * 8 * ORBFE_MAX_LEVELS);
+#endif
     // ORBextractor.cc:414-445
     h->scale.resize(nlevels);
     h->sigma2.resize(nlevels);
@@ -501,7 +515,19 @@ int orbfe_extract_batch(orbfe_extractor* h, int nimg, const uint8_t* const* d_im
     std::lock_guard<std::mutex> lk(h->mu);
     int rc = ensure(h, width, height, nimg);
     if (rc) return rc;
-    return run_batch(h, nimg, d_imgs, pitch, lap0, lap1, pick_stream(h, stream));
+    std::vector<int> laps(2 * (size_t)nimg);
+    for (int i = 0; i < nimg; i++) { laps[2 * i] = lap0; laps[2 * i + 1] = lap1; }
+    return run_batch(h, nimg, d_imgs, pitch, laps.data(), pick_stream(h, stream), true);
+}
+
+int orbfe_extract_batch_laps(orbfe_extractor* h, int nimg, const uint8_t* const* d_imgs, int width, int height,
+                             int pitch, const int32_t* laps, void* stream) {
+    if (!h || nimg <= 0 || !d_imgs || !laps || pitch < width) return ORBFE_E_ARG;
+    if (width <= 0 || height <= 0) return ORBFE_E_EMPTY;
+    std::lock_guard<std::mutex> lk(h->mu);
+    int rc = ensure(h, width, height, nimg);
+    if (rc) return rc;
+    return run_batch(h, nimg, d_imgs, pitch, laps, pick_stream(h, stream), true);
 }
 
 int orbfe_batch_outputs(orbfe_extractor* h, orbfe_keypoint** d_kps, uint8_t** d_desc, int** d_counts, int* cap) {
@@ -563,7 +589,8 @@ int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int width, int height,
     }
     HIPCHK(hipMemcpy2DAsync(h->d_stage, width, img, stride, width, height, hipMemcpyHostToDevice, s));
     const uint8_t* ptrs[1] = {h->d_stage};
-    rc = run_batch(h, 1, ptrs, width, lap0, lap1, s);
+    const int laps[2] = {lap0, lap1};
+    rc = run_batch(h, 1, ptrs, width, laps, s, false);
     if (rc) return rc;
     int cnt[2];
     HIPCHK(hipMemcpyAsync(cnt, h->last_counts, 8, hipMemcpyDeviceToHost, s));
@@ -619,10 +646,13 @@ int orbfe_stereo_match_batch(orbfe_extractor* left, int lbase, int lstep, orbfe_
     if (lds > 160 * 1024 - 64 || g.kp_cap > ST_SORT || g.kp_cap > 65535) return ORBFE_E_ARG;
     hipStream_t s = pick_stream(left, stream);
     std::lock_guard<std::mutex> lk(left->mu_stereo);
-    if (left->sdist_frames < nframes) {
+    if (left->sdist_frames < nframes || left->sdist_kp < g.kp_cap) {
         if (left->d_sdist) HIPCHK(hipFree(left->d_sdist));
+        left->d_sdist = nullptr;
+        left->sdist_frames = left->sdist_kp = 0;
         HIPCHK(hipMalloc(&left->d_sdist, (size_t)nframes * g.kp_cap * 4));
         left->sdist_frames = nframes;
+        left->sdist_kp = g.kp_cap;
     }
     hipLaunchKernelGGL(k_stereo, dim3((g.kp_cap + ST_LK - 1) / ST_LK, nframes), dim3(ST_NT), lds, s, g, SL, SR, sa,
                        d_uright, d_depth, left->d_sdist);
@@ -636,11 +666,15 @@ int orbfe_stereo_match(orbfe_extractor* left, orbfe_extractor* right, float bf, 
                        float* depth) {
     if (!left || !right) return ORBFE_E_ARG;
     std::lock_guard<std::mutex> lk(left->mu);
-    if (!left->d_uright || left->stereo_cap_frames < 1) {
+    if (!left->d_uright || left->stereo_kp < left->g.kp_cap) {   // (re)size for the current geometry
+        if (left->d_uright) HIPCHK(hipFree(left->d_uright));
+        if (left->d_depth) HIPCHK(hipFree(left->d_depth));
+        left->d_uright = left->d_depth = nullptr;
+        left->stereo_kp = 0;
         HIPCHK(hipMalloc(&left->d_uright, (size_t)left->g.kp_cap * 4));
         HIPCHK(hipMalloc(&left->d_depth, (size_t)left->g.kp_cap * 4));
-        HIPCHK(hipMalloc(&left->d_nmatch, 4));
-        left->stereo_cap_frames = 1;
+        if (!left->d_nmatch) HIPCHK(hipMalloc(&left->d_nmatch, 4));
+        left->stereo_kp = left->g.kp_cap;
     }
     HIPCHK(hipStreamSynchronize(right->own_stream));
     int rc = orbfe_stereo_match_batch(left, 0, 1, right, 0, 1, 1, bf, fx, left->d_uright, left->d_depth,

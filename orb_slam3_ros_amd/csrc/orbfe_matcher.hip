@@ -732,6 +732,73 @@ __global__ __launch_bounds__(MT_NT) void k_knn2(const uint32_t* L, int nl, const
     }
 }
 
+// Batched form of the same descriptor stage over the extractor's device outputs: frame f's queries
+// are rows [monoL, nL) of left image (lbase + f lstep), its train set rows [monoR, nR) of right
+// image (rbase + f rstep) (ComputeStereoFishEyeMatches' stereoDescLeft / stereoDescRight,
+// Frame.cc:1129-1133). One 256-thread block per (frame, 64 query slots): the frame's train rows
+// are staged in LDS once per block, each wave scans a quarter of them for the same 64 queries
+// (LDS broadcast reads), and the four partial top-2 lists are merged in train order so ties keep
+// the earlier train row (cv::BFMatcher's strict-less insertion). Outputs in the frame's full keypoint
+// numbering: l2r[f][i] = right keypoint index (trainIdx + monoRight) when Lowe's test passes, else -1;
+// dist[f][i] its Hamming distance or -1; ngood[f] += passed queries (zeroed by the launcher).
+#define KNN_Q 64
+__global__ __launch_bounds__(256) void k_knn2_batch(StereoSide SL, StereoSide SR, int cap, float ratio,
+                                                    int* __restrict__ l2r, int* __restrict__ dist, int* ngood) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_train[];   // [cap][8]
+    __shared__ int s_part[4][KNN_Q][3];
+    const int f = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int li = SL.base + f * SL.step, ri = SR.base + f * SR.step;
+    const int nL = SL.counts[2 * li], monoL = SL.counts[2 * li + 1];
+    const int nR = SR.counts[2 * ri], monoR = SR.counts[2 * ri + 1];
+    const int q = blockIdx.x * KNN_Q + lane;
+    int* o_t = l2r + (size_t)f * cap;
+    int* o_d = dist + (size_t)f * cap;
+    const int q0 = max(blockIdx.x * KNN_Q, monoL), q1 = min(blockIdx.x * KNN_Q + KNN_Q, nL);
+    if (q0 >= q1) {   // no query in this slot range: only the -1 fill
+        if (wave == 0 && q < cap) { o_t[q] = -1; o_d[q] = -1; }
+        return;
+    }
+    const int nt = max(nR - monoR, 0);
+    const uint32_t* rdesc = (const uint32_t*)(SR.desc + ((size_t)ri * cap + monoR) * 32);
+    for (int k = threadIdx.x; k < nt * 8; k += 256) s_train[k] = rdesc[k];
+    const bool valid = q >= monoL && q < nL;
+    uint32_t d[8];
+    const uint32_t* ld = (const uint32_t*)(SL.desc + ((size_t)li * cap + (valid ? q : q0)) * 32);
+#pragma unroll
+    for (int w = 0; w < 8; w++) d[w] = ld[w];
+    SYNC();
+    const int j0 = (int)(((long)nt * wave) >> 2), j1 = (int)(((long)nt * (wave + 1)) >> 2);
+    int d0 = MT_INF, d1 = MT_INF, t0 = -1;
+    for (int j = j0; j < j1; j++) {
+        const uint4 a = *(const uint4*)&s_train[8 * j];
+        const uint4 b = *(const uint4*)&s_train[8 * j + 4];
+        int dd = __popc(d[0] ^ a.x) + __popc(d[1] ^ a.y) + __popc(d[2] ^ a.z) + __popc(d[3] ^ a.w) +
+                 __popc(d[4] ^ b.x) + __popc(d[5] ^ b.y) + __popc(d[6] ^ b.z) + __popc(d[7] ^ b.w);
+        if (dd < d0) { d1 = d0; d0 = dd; t0 = j; }
+        else if (dd < d1) d1 = dd;
+    }
+    s_part[wave][lane][0] = d0;
+    s_part[wave][lane][1] = d1;
+    s_part[wave][lane][2] = t0;
+    SYNC();
+    if (wave == 0) {
+        // merge the later ranges into the running top-2: a later row wins only when strictly closer
+        for (int w = 1; w < 4; w++) {
+            const int b0 = s_part[w][lane][0], b1 = s_part[w][lane][1], bt = s_part[w][lane][2];
+            if (b0 < d0) { d1 = min(d0, b1); d0 = b0; t0 = bt; }
+            else d1 = min(d1, b0);
+        }
+        if (q < cap) {
+            // (*it).size() >= 2 && d0 < d1 * 0.7 (DMatch distances are float; the product in double, as k_knn2)
+            const bool ok = valid && nt >= 2 && (float)d0 < (float)d1 * (double)ratio;
+            o_t[q] = ok ? t0 + monoR : -1;
+            o_d[q] = ok ? d0 : -1;
+            const unsigned long long m = __ballot(ok);
+            if (lane == 0 && m) atomicAdd(ngood + f, (int)__popcll(m));
+        }
+    }
+}
+
 // =============================================================================================
 // Host side (compiled in the engine TU after HIPCHK is defined).
 // Every call is synchronous from the caller's point of view (the reference methods return
@@ -1231,6 +1298,29 @@ int orbfe_stereo_knn_ratio(const uint8_t* left_desc, int32_t nl, const uint8_t* 
     int good = 0;
     for (int i = 0; i < nl; i++) good += out_train[i] >= 0;
     return good;
+}
+
+int orbfe_stereo_knn_batch(orbfe_extractor* left, int lbase, int lstep, orbfe_extractor* right, int rbase, int rstep,
+                           int nframes, float ratio, int32_t* d_l2r, int32_t* d_dist, int32_t* d_ngood, void* stream) {
+    if (!left || !right || nframes <= 0 || !d_l2r || !d_dist || !d_ngood) return ORBFE_E_ARG;
+    std::lock_guard<std::mutex> lk(left->mu_stereo);
+    if (!left->cap_b || !right->cap_b || left->g.kp_cap != right->g.kp_cap) return ORBFE_E_ARG;
+    if (lbase < 0 || rbase < 0 || lbase + (nframes - 1) * lstep >= left->last_nimg ||
+        rbase + (nframes - 1) * rstep >= right->last_nimg)
+        return ORBFE_E_ARG;
+    const int cap = left->g.kp_cap;
+    const size_t lds = (size_t)cap * 32;
+    if (lds > 128 * 1024) return ORBFE_E_ARG;
+    StereoSide SL{left->d_ptrs, left->last_pitch, left->d_pyr, left->g.pyr_bytes, left->last_kps, left->last_desc,
+                  left->last_counts, lbase, lstep};
+    StereoSide SR{right->d_ptrs, right->last_pitch, right->d_pyr, right->g.pyr_bytes, right->last_kps,
+                  right->last_desc, right->last_counts, rbase, rstep};
+    hipStream_t s = pick_stream(left, stream);
+    HIPCHK(hipMemsetAsync(d_ngood, 0, (size_t)nframes * 4, s));
+    hipLaunchKernelGGL(k_knn2_batch, dim3((cap + KNN_Q - 1) / KNN_Q, nframes), dim3(256), lds, s, SL, SR, cap, ratio,
+                       (int*)d_l2r, (int*)d_dist, (int*)d_ngood);
+    HIPCHK(hipGetLastError());
+    return ORBFE_OK;
 }
 
 int orbfe_search_local_points(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* pts,

@@ -11,9 +11,8 @@
 
 struct OrbLevel {
     int w, h;                 // level size (cvRound((float)cols * invScale), ORBextractor.cc:1175)
-    int pitch;                // row pitch of this level in the pyramid / blur buffers
+    int pitch;                // row pitch of this level in the pyramid buffer
     int pyr_off;              // byte offset of the level inside one image's pyramid slab (levels >= 1)
-    int blur_off;             // byte offset inside one image's blurred slab (all levels)
     float scale, inv_scale;   // mvScaleFactor / mvInvScaleFactor
     int patch_size;           // (int)(PATCH_SIZE * scale) (ORBextractor.cc:880)
     // FAST cell grid (ORBextractor.cc:797-803)
@@ -32,8 +31,6 @@ struct OrbLevel {
     int tab_y;                // 4*h entries: sy0, sy1 (clipped), beta0, beta1
     int xmax;                 // first dx whose right neighbour leaves the source row
     int simd_end;             // first column handled by the scalar vertical tail
-    // blur tiling
-    int blur_tiles_x, blur_tiles_y, blur_tile_base;
     int rz_rows, rz_cols;     // output rows / cols per k_resize block (fit the LDS source window)
 };
 
@@ -46,8 +43,6 @@ struct OrbGeom {
     int out_per_img;          // octree output slots over all levels
     int kp_cap;               // final keypoints per image (= out_per_img)
     int pyr_bytes;            // bytes of levels >= 1 per image (padded)
-    int blur_bytes;           // bytes of blurred levels per image (padded)
-    int blur_tiles;           // total blur tiles
     int max_cells_level;      // max cells in one level
     int node_cap;             // octree node capacity (max over levels)
     OrbLevel lv[ORBFE_MAX_LEVELS];

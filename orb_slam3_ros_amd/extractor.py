@@ -41,7 +41,7 @@ class ORBextractor:
 
     # ---- getters (ORBextractor.h:61-81) ----
     def GetLevels(self) -> int:
-        return self.nlevels
+        return _lib.check(self._lib.orbfe_extractor_levels(self._h), "orbfe_extractor_levels")
 
     def GetScaleFactor(self) -> float:
         return self._scale_factor

@@ -1,4 +1,4 @@
-"""Batched device front-end: extract(L) + extract(R) + ComputeStereoMatches for many stereo frames
+"""Batched device front-end: extract(L) + extract(R) + the stereo matcher for many stereo frames
 per launch sequence (the multi-frame / multi-camera path of BASELINE config 2-4).
 
 Frame f of a batch is images (2f, 2f+1) of one interleaved [2F, H, W] u8 device tensor: this is
@@ -6,6 +6,11 @@ the batched form of Frame::Frame(stereo) (Frame.cc:101-197), which runs ORBextra
 on the left and right image on two threads (Frame.cc:122-125) and then ComputeStereoMatches
 (Frame.cc:141, :811-981). Outputs are device tensors in the reference's order (mvKeys,
 mDescriptors, mvuRight, mvDepth per frame, padded to `cap`).
+
+stereo="fisheye" is the KannalaBrandt8 constructor (Frame.cc:1007-1075): each side is extracted
+with its camera's vLappingArea (Frame.cc:1059-1060) and ComputeStereoFishEyeMatches' descriptor
+stage (knnMatch k=2 over the lapping rows + Lowe's 0.7, Frame.cc:1126-1151) runs batched on the
+device; `l2r` holds the mvLeftToRightMatch candidates the host-side TriangulateMatches filters.
 
 torch is used only for device memory and streams; all compute is in liborbfe.so.
 """
@@ -26,12 +31,18 @@ class StereoFrontEnd:
 
     def __init__(self, frames: int, width: int, height: int, nfeatures: int = 1000, scale_factor: float = 1.2,
                  nlevels: int = 8, ini_th: int = 20, min_th: int = 7, bf: float = 0.110078 * 458.654,
-                 fx: float = 458.654, device=None, pipelines: int = 1):
+                 fx: float = 458.654, device=None, pipelines: int = 1, lap_left=(0, 0), lap_right=(0, 0),
+                 stereo: str = "rectified", knn_ratio: float = 0.7):
         import torch
         self.torch = torch
         self.lib = _lib.load()
         self.F, self.W, self.H = int(frames), int(width), int(height)
         self.bf, self.fx = float(bf), float(fx)
+        if stereo not in ("rectified", "fisheye", "none"):
+            raise ValueError(f"stereo must be 'rectified', 'fisheye' or 'none', not {stereo!r}")
+        self.stereo, self.knn_ratio = stereo, float(knn_ratio)
+        self.lap_left = (int(lap_left[0]), int(lap_left[1]))
+        self.lap_right = (int(lap_right[0]), int(lap_right[1]))
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         P = max(1, min(int(pipelines), self.F))
         bounds = [self.F * i // P for i in range(P + 1)]
@@ -57,6 +68,9 @@ class StereoFrontEnd:
         self.uright = t.zeros((self.F, self.cap), dtype=t.float32, device=self.device)
         self.depth = t.zeros((self.F, self.cap), dtype=t.float32, device=self.device)
         self.nmatch = t.zeros((self.F,), dtype=t.int32, device=self.device)
+        if stereo == "fisheye":   # mvLeftToRightMatch candidates + their distances
+            self.l2r = t.full((self.F, self.cap), -1, dtype=t.int32, device=self.device)
+            self.l2r_dist = t.full((self.F, self.cap), -1, dtype=t.int32, device=self.device)
         self.bind_outputs(self.counts, self.kps, self.desc)
         self._ptrs = None
         self._ptr_key = None
@@ -106,21 +120,39 @@ class StereoFrontEnd:
                 s = st.cuda_stream
             else:
                 s = stream
-            _lib.check(self.lib.orbfe_extract_batch(h, 2 * (b - a), p, self.W, self.H, images.stride(1), 0, 0, s),
-                       "extract_batch")
+            if self.lap_left == self.lap_right:
+                _lib.check(self.lib.orbfe_extract_batch(h, 2 * (b - a), p, self.W, self.H, images.stride(1),
+                                                        self.lap_left[0], self.lap_left[1], s), "extract_batch")
+            else:
+                _lib.check(self.lib.orbfe_extract_batch_laps(h, 2 * (b - a), p, self.W, self.H, images.stride(1),
+                                                             self._laps(b - a).ctypes.data, s), "extract_batch_laps")
+            if self.stereo == "none":
+                continue
             timed = self._stage_on and i == 0 and stream is None
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(st)
-            _lib.check(self.lib.orbfe_stereo_match_batch(h, 0, 2, h, 1, 2, b - a, self.bf, self.fx,
-                                                         self.uright[a].data_ptr(), self.depth[a].data_ptr(),
-                                                         self.nmatch[a:].data_ptr(), s), "stereo_match_batch")
+            if self.stereo == "fisheye":
+                _lib.check(self.lib.orbfe_stereo_knn_batch(h, 0, 2, h, 1, 2, b - a, self.knn_ratio,
+                                                           self.l2r[a].data_ptr(), self.l2r_dist[a].data_ptr(),
+                                                           self.nmatch[a:].data_ptr(), s), "stereo_knn_batch")
+            else:
+                _lib.check(self.lib.orbfe_stereo_match_batch(h, 0, 2, h, 1, 2, b - a, self.bf, self.fx,
+                                                             self.uright[a].data_ptr(), self.depth[a].data_ptr(),
+                                                             self.nmatch[a:].data_ptr(), s), "stereo_match_batch")
             if timed:
                 e1.record(st)
                 self._stereo_ev.append((e0, e1))
         if stream is None:
             for st in self.streams:
                 main.wait_stream(st)
+
+    def _laps(self, nframes):
+        key = ("laps", nframes)
+        if getattr(self, "_lap_key", None) != key:
+            self._lap_arr = np.array([*self.lap_left, *self.lap_right] * nframes, np.int32)
+            self._lap_key = key
+        return self._lap_arr
 
     def set_stage_timing(self, on: bool):
         for h in self.handles:
@@ -141,12 +173,17 @@ class StereoFrontEnd:
             out["stereo"] = float(np.mean([a.elapsed_time(b) for a, b in self._stereo_ev]))
         return out, n
 
+    def host_image(self, i: int):
+        """(monoIndex, keypoints (structured), descriptors) of batch image i, copied to the host."""
+        n, mono = (int(v) for v in self.counts[i].cpu().numpy())
+        kp = self.kps[i, :n].cpu().numpy().view(KEYPOINT_DTYPE).reshape(n)
+        return mono, kp, self.desc[i, :n].cpu().numpy()
+
     def host_frame(self, f: int):
         """(kps_left structured, desc_left, uright, depth) of frame f, copied to the host."""
-        c = self.counts[2 * f].cpu().numpy()
-        n = int(c[0])
-        kp = self.kps[2 * f, :n].cpu().numpy().view(KEYPOINT_DTYPE).reshape(n)
-        return kp, self.desc[2 * f, :n].cpu().numpy(), self.uright[f, :n].cpu().numpy(), self.depth[f, :n].cpu().numpy()
+        _, kp, d = self.host_image(2 * f)
+        n = len(kp)
+        return kp, d, self.uright[f, :n].cpu().numpy(), self.depth[f, :n].cpu().numpy()
 
     def close(self):
         for h in self.handles:
