@@ -443,7 +443,7 @@ def side_leg(dev, name, W, H, nf, F, steps, warmup, stereo, lap, bf, fx, check_f
     fe = StereoFrontEnd(F, W, H, nfeatures=nf, bf=bf, fx=fx, device=dev, lap_left=lap, lap_right=lap, stereo=stereo)
     sec = time_steps(fe, images, steps, warmup)
     st = stage_times(fe, images, max(3, steps // 2))
-    pf = st["resize"] + st["fast"]
+    pf = st["pyramid_fast"]
     nb = algorithmic_bytes(W, H)
     ok, msg = parity_check(fe, pairs, fmap, min(check_frames, F), nf, bf, fx, stereo=stereo, lap=lap)
     out = {"workload": name, "frames_per_step": F, "images_per_step": 2 * F, "ms_per_step": round(sec * 1e3, 4),
@@ -467,6 +467,8 @@ def main():
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--nfeatures", type=int, default=1000)
     ap.add_argument("--unique", type=int, default=16, help="distinct synthetic frames (tiled over the batch)")
+    ap.add_argument("--path", choices=["default", "fused", "legacy"], default="default",
+                    help="pyramid+FAST implementation (default: the library's)")
     ap.add_argument("--pipelines", type=int, default=1, help="sub-batches on separate HIP streams")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -509,6 +511,8 @@ def main():
     bf, fx = EUROC_BF, EUROC_FX
     images, pairs, fmap = make_images(rank, W, H, F, args.unique, dev)
     fe = StereoFrontEnd(F, W, H, nfeatures=args.nfeatures, bf=bf, fx=fx, device=dev, pipelines=args.pipelines)
+    if args.path != "default":
+        fe.set_path(0 if args.path == "fused" else 1)
     gather = world > 1 and not args.no_allgather
     if gather:
         # zero-copy, double-buffered slab exchange: the extractor writes step k's outputs into slab
@@ -593,7 +597,9 @@ def main():
 
     if rank == 0:
         n_img = 2 * F
-        pyr_fast_ms = stages["resize"] + stages["fast"]
+        pyr_fast_ms = stages["pyramid_fast"]
+        pf_kernel = ("pyramid+FAST pass, fused: k_pyrfast x8 levels (FAST of level l + resize of level l+1)"
+                     if fe.path() == 0 else "pyramid+FAST pass: k_resize x7 + k_fast")
         bytes_img = algorithmic_bytes(W, H)
         achieved = n_img * bytes_img / (pyr_fast_ms * 1e-3) / 1e9 if pyr_fast_ms > 0 else 0.0
         dominant = max(stages, key=stages.get)
@@ -630,7 +636,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "pyramid+FAST pass (k_resize x7 + k_fast)",
+                "kernel": pf_kernel,
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -653,8 +659,7 @@ def main():
         if valu is not None:
             # VALU issue fraction per kernel: committed SQ_INSTS_VALU per launch over this run's kernel
             # time x the wave64 issue peak (2 cycles per instruction on each of 1024 SIMD-32s)
-            kt = {"k_resize": stages["resize"], "k_fast": stages["fast"], "k_octree": stages["octree"],
-                  "k_describe": stages["describe"]}
+            kt = {"k_pyrfast": stages["pyramid_fast"], "k_octree": stages["octree"], "k_describe": stages["describe"]}
             result["roofline"]["valu_issue_frac"] = {
                 k: round(v["valu_per_step"] / (kt[k] * 1e-3) / VALU_ISSUE_PEAK, 4)
                 for k, v in valu[0].items() if k in kt and kt[k] > 0}

@@ -90,11 +90,19 @@ int orbfe_batch_outputs(orbfe_extractor* h, orbfe_keypoint** d_kps, uint8_t** d_
 int orbfe_set_batch_outputs(orbfe_extractor* h, orbfe_keypoint* d_kps, uint8_t* d_desc, int* d_counts,
                             int cap_images);
 
+/* Pyramid + FAST implementation of this handle: path 0 (default) = the fused band pass (one
+ * launch per level: FAST cells of level l and the resize of level l+1 from the same staged rows),
+ * used whenever the level geometry allows it; path 1 = separate k_resize / k_fast launches (also
+ * the automatic choice for geometries the band pass does not cover). Both are bit-exact.
+ * orbfe_extractor_get_path returns the path a width x height batch will take (0 or 1). */
+int orbfe_extractor_set_path(orbfe_extractor* h, int path);
+int orbfe_extractor_get_path(orbfe_extractor* h, int width, int height);
+
 /* Per-kernel HIP-event timing (for bench.py's roofline). While enabled, every batch records
  * events around each stage on the stream it runs on (no host sync). orbfe_get_stage_timing waits
  * for the recorded batches, writes the MEAN ms per batch of each stage to ms[0..ORBFE_NUM_STAGES)
- * = {resize (all levels), fast, octree, describe}, resets, and returns the batch count. */
-#define ORBFE_NUM_STAGES 4
+ * = {pyramid + FAST (all levels), octree, describe}, resets, and returns the batch count. */
+#define ORBFE_NUM_STAGES 3
 int orbfe_set_stage_timing(orbfe_extractor* h, int enable);
 int orbfe_get_stage_timing(orbfe_extractor* h, float* ms);
 

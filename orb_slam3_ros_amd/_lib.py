@@ -17,8 +17,8 @@ ORBFE_E_EMPTY = -1
 ORBFE_E_ARG = -2
 ORBFE_E_DEVICE = -3
 ORBFE_E_CAPACITY = -4
-ORBFE_NUM_STAGES = 4
-STAGE_NAMES = ("resize", "fast", "octree", "describe")
+ORBFE_NUM_STAGES = 3
+STAGE_NAMES = ("pyramid_fast", "octree", "describe")
 
 
 class OrbKeyPoint(ctypes.Structure):
@@ -43,6 +43,8 @@ _SIGS = {
     "orbfe_extract_batch_laps": (_c_int, [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp]),
     "orbfe_batch_outputs": (_c_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp), _P_int]),
     "orbfe_set_stage_timing": (_c_int, [_vp, _c_int]),
+    "orbfe_extractor_set_path": (_c_int, [_vp, _c_int]),
+    "orbfe_extractor_get_path": (_c_int, [_vp, _c_int, _c_int]),
     "orbfe_set_batch_outputs": (_c_int, [_vp, _vp, _vp, _vp, _c_int]),
     "orbfe_get_stage_timing": (_c_int, [_vp, _vp]),
     "orbfe_stereo_match_batch": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_float, _c_float,

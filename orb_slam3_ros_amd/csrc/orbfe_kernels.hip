@@ -491,6 +491,39 @@ __device__ __forceinline__ void fast_stage_chunk(uint32_t* s32w, uint32_t* s32z,
     }
 }
 
+// Stage a prefetched cell ROI into the wave's LDS image (realigned rows of 4 * nd bytes) and zero
+// the score map rows (y < dh + 2) alongside; ends with WAVE_SYNC.
+__device__ __forceinline__ void fast_stage_cell(const FastCell& cur, const orbfe_u32x4 (&pf)[FAST_PF], uint8_t* s_img,
+                                                uint8_t* s_sc, int lane) {
+    int ng, nd, cpr, rpl;
+    fast_geom(cur, &ng, &nd, &cpr, &rpl);
+    const int dh = cur.rows - 6;
+    if (ng) {
+        const int sy = small_div(lane, cpr), st = lane - sy * cpr, sal = (cur.c0 - 1) & 3;
+        uint32_t* s32w = (uint32_t*)s_img;
+        uint32_t* s32z = (uint32_t*)s_sc;
+#pragma unroll
+        for (int u = 0; u < FAST_PF; u++) {
+            const int y = sy + u * rpl;
+            fast_stage_chunk(s32w, s32z, pf[u], sal, y, st, nd, dh, sy < rpl && y < cur.rows);
+        }
+        // rows beyond the prefetch window (only very tall cells of tiny levels): direct loads with a
+        // wave-uniform trip count (the DPP needs every lane)
+        if (FAST_PF * rpl < cur.rows) {
+            const bool al = (cur.pitch & 3) == 0 && ((((uintptr_t)cur.src) & 3) == 0);
+            gptr_u8 base = cur.src + (size_t)cur.r0 * cur.pitch + ((cur.c0 - 1) & ~3) + 16 * st;
+            for (int y0 = FAST_PF * rpl; y0 < cur.rows; y0 += rpl) {
+                const int y = y0 + sy;
+                const bool ok = sy < rpl && y < cur.rows;
+                orbfe_u32x4 q = {0u, 0u, 0u, 0u};
+                if (ok) q = fast_chunk(base + (size_t)y * cur.pitch, al);
+                fast_stage_chunk(s32w, s32z, q, sal, y, st, nd, dh, ok);
+            }
+        }
+    }
+    WAVE_SYNC();
+}
+
 struct FastLds {
     int roi, sc, cor, wave_bytes;   // bytes per wave: ROI image, score map, corner list (+ entries)
 };
@@ -503,7 +536,7 @@ template <int NDC>
 __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds& fl, const FastCell& me, int ng,
                                                  int nd_rt, int dw, int dh, uint8_t* s_img, uint8_t* s_sc,
                                                  uint16_t* s_cor, uint16_t* s_ent, uint32_t* cellkeys, int* cellcnt,
-                                                 int b, int c, int lane, int ablate) {
+                                                 int b, int c, int lane, int ablate, int first_attempt = 0) {
     const int nd = NDC ? NDC : nd_rt;
     const int RS = 4 * nd;
     const OrbLevel& L = g.lv[me.l];
@@ -520,7 +553,7 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
     // fraction of minThFAST's.
     int nsurv = 0;
     bool stop = false;
-    for (int attempt = 0; attempt < 2; attempt++) {
+    for (int attempt = first_attempt; attempt < 2; attempt++) {
         const int th = attempt == 0 ? g.ini_th : g.min_th;
         if (attempt) {
             uint32_t* s32z = (uint32_t*)s_sc;
@@ -740,7 +773,7 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
 
 __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                               int pyr_stride, OrbGeom g, FastLds fl, uint32_t* cellkeys,
-                                              int* cellcnt) {
+                                              int* cellcnt, int c_lo, int c_hi) {
     constexpr int ablate = ORBFE_ABLATE_FAST;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_fast[];
     // wave-uniform in an SGPR: the cell geometry (level search, cell row / column division, ROI
@@ -755,9 +788,9 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
     uint8_t* s_sc = s_img + fl.roi;
     uint16_t* s_cor = (uint16_t*)(s_sc + fl.sc);
     uint16_t* s_ent = (uint16_t*)((uint8_t*)s_cor + fl.cor);
-    const int cbeg = (bx * 4 + wave) * FAST_CPW;
-    if (cbeg >= g.total_cells) return;
-    const int cend = min(cbeg + FAST_CPW, g.total_cells);
+    const int cbeg = c_lo + (bx * 4 + wave) * FAST_CPW;   // the launch covers cells [c_lo, c_hi)
+    if (cbeg >= c_hi) return;
+    const int cend = min(cbeg + FAST_CPW, c_hi);
     orbfe_u32x4 pf[FAST_PF];
     FastCell cur = fast_cell(imgs, in_pitch, pyr, pyr_stride, g, b, cbeg);
     fast_prefetch(cur, lane, pf);
@@ -765,31 +798,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
         int ng, nd, cpr, rpl;
         fast_geom(cur, &ng, &nd, &cpr, &rpl);
         const int dw = cur.cols - 6, dh = cur.rows - 6;
-        // stage: realign, zero the score map
-        if (ng) {
-            const int sy = small_div(lane, cpr), st = lane - sy * cpr, sal = (cur.c0 - 1) & 3;
-            uint32_t* s32w = (uint32_t*)s_img;
-            uint32_t* s32z = (uint32_t*)s_sc;
-#pragma unroll
-            for (int u = 0; u < FAST_PF; u++) {
-                const int y = sy + u * rpl;
-                fast_stage_chunk(s32w, s32z, pf[u], sal, y, st, nd, dh, sy < rpl && y < cur.rows);
-            }
-            // rows beyond the prefetch window (only very tall cells of tiny levels): direct loads with a
-            // wave-uniform trip count (the DPP needs every lane)
-            if (FAST_PF * rpl < cur.rows) {
-                const bool al = (cur.pitch & 3) == 0 && ((((uintptr_t)cur.src) & 3) == 0);
-                gptr_u8 base = cur.src + (size_t)cur.r0 * cur.pitch + ((cur.c0 - 1) & ~3) + 16 * st;
-                for (int y0 = FAST_PF * rpl; y0 < cur.rows; y0 += rpl) {
-                    const int y = y0 + sy;
-                    const bool ok = sy < rpl && y < cur.rows;
-                    orbfe_u32x4 q = {0u, 0u, 0u, 0u};
-                    if (ok) q = fast_chunk(base + (size_t)y * cur.pitch, al);
-                    fast_stage_chunk(s32w, s32z, q, sal, y, st, nd, dh, ok);
-                }
-            }
-        }
-        WAVE_SYNC();
+        fast_stage_cell(cur, pf, s_img, s_sc, lane);
         const FastCell me = cur;
         if (c + 1 < cend) {   // prefetch the next cell while this one is processed
             cur = fast_cell(imgs, in_pitch, pyr, pyr_stride, g, b, c + 1);
