@@ -140,39 +140,56 @@ int orbfe_descriptor_distance(const uint8_t* a, const uint8_t* b);   /* Descript
 
 /* The parts of a Frame the matchers read (Frame.h). Keypoints are mvKeysUn (== mvKeys for the
  * rectified / undistorted case); the 64x48 grid (AssignFeaturesToGrid, Frame.cc:385-416) is
- * rebuilt from them with the reference's PosInGrid arithmetic. */
+ * rebuilt from them with the reference's PosInGrid arithmetic.
+ * Two-camera frames (Nleft != -1: the KannalaBrandt8 stereo constructor, Frame.cc:1000-1125):
+ * two_cams = 1, keys = mvKeys [0, nleft) followed by mvKeysRight [nleft, n) (the reference's
+ * AssignFeaturesToGrid reads exactly these, Frame.cc:401-403), desc / mvpMapPoints rows in the same
+ * numbering (mDescriptors = [left; right]), a left grid over [0, nleft) and a right grid (mGridRight)
+ * over [nleft, n); l2r / r2l = mvLeftToRightMatch / mvRightToLeftMatch. A zero-initialised tail
+ * (two_cams = 0) is the single-camera frame (Nleft == -1). */
 typedef struct orbfe_frame {
     int32_t n;                       /* N */
-    const orbfe_keypoint* keys;      /* mvKeysUn [n] */
+    const orbfe_keypoint* keys;      /* mvKeysUn [n] (two_cams: mvKeys ++ mvKeysRight) */
     const uint8_t* desc;             /* mDescriptors [n][32] */
-    const float* uright;             /* mvuRight [n] or NULL (monocular) */
+    const float* uright;             /* mvuRight [n] or NULL (monocular; not read for two_cams) */
     float min_x, max_x, min_y, max_y;   /* mnMinX, mnMaxX, mnMinY, mnMaxY (ComputeImageBounds) */
     int32_t nlevels;
     const float* scale_factors;      /* mvScaleFactors [nlevels] */
     float mbf;                       /* mbf (stereo baseline * fx) */
+    int32_t two_cams;                /* 1: Nleft != -1 (fields below valid) */
+    int32_t nleft;                   /* Nleft, 0 <= nleft <= n */
+    const int32_t* l2r;              /* mvLeftToRightMatch [nleft] (right index or -1) */
+    const int32_t* r2l;              /* mvRightToLeftMatch [n - nleft] (left index or -1) */
 } orbfe_frame;
 
 /* MapPoint tracking snapshot for SearchByProjection(Frame&, vector<MapPoint*>, ...)
  * (MapPoint.h:172-180; filled by Frame::isInFrustum, Tracking.cc:3407-3425). 80 bytes. */
 #define ORBFE_MP_IN_VIEW 1           /* mbTrackInView */
 #define ORBFE_MP_BAD 2               /* isBad() */
+#define ORBFE_MP_IN_VIEW_R 8         /* mbTrackInViewR (two-camera frames, Frame.cc:575-584) */
 typedef struct orbfe_map_point {
-    float proj_x, proj_y, proj_xr;   /* mTrackProjX, mTrackProjY, mTrackProjXR */
+    float proj_x, proj_y, proj_xr;   /* mTrackProjX, mTrackProjY, mTrackProjXR (two_cams: the right-camera x) */
     float view_cos;                  /* mTrackViewCos */
     float depth;                     /* mTrackDepth */
     int32_t scale_level;             /* mnTrackScaleLevel */
     int32_t flags;                   /* ORBFE_MP_* */
     int32_t observations;            /* Observations() */
     int32_t id;                      /* handle stored into mvpMapPoints */
-    int32_t reserved[3];
+    float proj_yr;                   /* mTrackProjYR (two-camera frames, Frame.cc:1227-1230) */
+    float view_cos_r;                /* mTrackViewCosR */
+    int32_t scale_level_r;           /* mnTrackScaleLevelR (-1: right branch skipped) */
     uint8_t desc[32];                /* GetDescriptor() */
 } orbfe_map_point;
 
 /* ORBmatcher(nnratio).SearchByProjection(F, vpMapPoints, th, bFarPoints, thFarPoints)
- * (ORBmatcher.cc:43-213, pinhole/rectified path). mvp: F.mvpMapPoints as handles [F.n], updated in
- * place; mvp_obs: Observations() of the MapPoint currently in each slot (0 when empty). Points are
- * processed in array order exactly as the reference loop (a keypoint already holding a point with
- * Observations() > 0 is skipped). Returns nmatches. */
+ * (ORBmatcher.cc:43-213). mvp: F.mvpMapPoints as handles [F.n], updated in place; mvp_obs:
+ * Observations() of the MapPoint currently in each slot (0 when empty). Points are processed in
+ * array order exactly as the reference loop (a keypoint already holding a point with
+ * Observations() > 0 is skipped). Two-camera frames (F->two_cams) take the reference's Nleft != -1
+ * branches: the left search without the mvuRight check, the stereo partner slot written through
+ * mvLeftToRightMatch (:124-128), and the right-camera search over the right grid with the
+ * ORBFE_MP_IN_VIEW_R fields (:138-209: radius NOT scaled by th, partner through
+ * mvRightToLeftMatch). Returns nmatches. */
 int orbfe_search_by_projection_local(const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs,
                                      const orbfe_map_point* mps, int32_t n_mps, float th, int32_t bFarPoints,
                                      float thFarPoints, float nnratio);
@@ -205,6 +222,16 @@ int orbfe_search_by_projection_lastframe(const orbfe_frame* cur, int32_t* mvp, c
                                          const orbfe_proj_point* pts, int32_t n_pts, float th, int32_t bForward,
                                          int32_t bBackward, int32_t checkOri);
 
+/* The same search for a two-camera CurrentFrame (CurrentFrame.Nleft != -1, ORBmatcher.cc:1794-1858):
+ * right_uv[2 i] / right_uv[2 i + 1] = mpCamera->project(GetRelativePoseTrl() * x3Dc) of point i (the
+ * caller's camera model); after the left search (left grid, no mvuRight check; a point whose left
+ * window is empty skips both, :1738-1739) the right grid is searched and the slot nleft + bestIdx2
+ * written; both enter the rotation histogram. pts[i].octave is nLastOctave (LastFrame.mvKeys /
+ * mvKeysRight). For a single-camera cur (two_cams = 0) right_uv is ignored (== the function above). */
+int orbfe_search_by_projection_lastframe_stereo(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_obs,
+                                                const orbfe_proj_point* pts, const float* right_uv, int32_t n_pts,
+                                                float th, int32_t bForward, int32_t bBackward, int32_t checkOri);
+
 /* Relocalisation refinement SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
  * (ORBmatcher.cc:1889-2010): one entry per KF map point that is not bad and not already found,
  * projected by the caller; octave = PredictScale(...) (MapPoint.cc:531-546), angle =
@@ -227,8 +254,12 @@ typedef struct orbfe_feature_vector {
     const uint32_t* indices;
 } orbfe_feature_vector;
 
-/* SearchByBoW(pKF, F, vpMapPointMatches) (ORBmatcher.cc:223-425, monocular/pinhole path).
- * kf_mp: pKF->GetMapPointMatches() handles with bad points already mapped to -1; out: [F.n]. */
+/* SearchByBoW(pKF, F, vpMapPointMatches) (ORBmatcher.cc:223-425).
+ * kf_mp: pKF->GetMapPointMatches() handles with bad points already mapped to -1; out: [F.n].
+ * kf_keys[i] is the keypoint the reference reads for KF index i (mvKeysUn, or for a two-camera KF
+ * mvKeys / mvKeysRight by side, :327-329). A two-camera F (F->two_cams) takes the Nleft != -1 walk:
+ * separate left / right best-and-second, the right match only inside the left's bestDist1 <= TH_LOW
+ * and its ratio test disabled (the reference's "|| true", :359). */
 int orbfe_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, const int32_t* kf_mp, int32_t kf_n,
                         const orbfe_feature_vector* kf_fv, const orbfe_frame* F, const orbfe_feature_vector* f_fv,
                         int32_t* out, float nnratio, int32_t checkOri);

@@ -131,6 +131,7 @@ def _match_sigs(L):
     vp, ci, cf = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
     L.oro_sbp_local.argtypes = [vp, vp, vp, vp, ci, cf, ci, cf, cf]
     L.oro_sbp_lastframe.argtypes = [vp, vp, vp, vp, ci, cf, ci, ci, ci]
+    L.oro_sbp_lastframe_stereo.argtypes = [vp, vp, vp, vp, vp, ci, cf, ci, ci, ci]
     L.oro_sbp_kf.argtypes = [vp, vp, vp, ci, cf, ci, ci]
     L.oro_search_for_init.argtypes = [vp, vp, vp, vp, ci, cf, ci]
     L.oro_search_by_bow.argtypes = [vp, vp, vp, ci, vp, vp, vp, vp, cf, ci]
@@ -162,6 +163,12 @@ class OracleMatcher:
     def sbp_lastframe(self, F, mvp, mvp_obs, pts, th, bForward, bBackward):
         return self.L.oro_sbp_lastframe(F.ref(), mvp.ctypes.data, mvp_obs.ctypes.data, pts.ctypes.data, len(pts),
                                         float(th), int(bForward), int(bBackward), self.checkOri)
+
+    def sbp_lastframe_stereo(self, F, mvp, mvp_obs, pts, right_uv, th, bForward, bBackward):
+        ruv = np.ascontiguousarray(right_uv, np.float32)
+        return self.L.oro_sbp_lastframe_stereo(F.ref(), mvp.ctypes.data, mvp_obs.ctypes.data, pts.ctypes.data,
+                                               ruv.ctypes.data, len(pts), float(th), int(bForward), int(bBackward),
+                                               self.checkOri)
 
     def sbp_kf(self, F, mvp, pts, th, ORBdist):
         return self.L.oro_sbp_kf(F.ref(), mvp.ctypes.data, pts.ctypes.data, len(pts), float(th), int(ORBdist),

@@ -25,8 +25,11 @@
 //   MapPoint::PredictScale                   MapPoint.cc:531-546
 //   Tracking::SearchLocalPoints (projection + SearchByProjection)  Tracking.cc:3404-3453
 //                                                                        -> oro_search_local_points()
-// Only the pinhole / rectified branches (F.Nleft == -1) are restated; the KannalaBrandt8
-// right-camera branches are out of scope.
+// Two-camera frames (F.Nleft != -1, orbfe_frame.two_cams) follow the reference's Nleft branches of
+// SearchByProjection (local map :95-209, last frame :1727-1858) and SearchByBoW(KF, F) (:270-386):
+// keys[0, nleft) = mvKeys with the left grid mGrid, keys[nleft, n) = mvKeysRight with mGridRight
+// (AssignFeaturesToGrid :399-413, GetFeaturesInArea(..., bRight) :657-723). Grid keeps GLOBAL row
+// indices (right row = nleft + the reference's right index).
 // ============================================================================================
 #include <algorithm>
 #include <climits>
@@ -50,10 +53,12 @@ struct Grid {
     const orbfe_frame* F;
     float invw, invh;
     std::vector<size_t> cell[ORBFE_GRID_COLS][ORBFE_GRID_ROWS];
-    explicit Grid(const orbfe_frame* f) : F(f) {
+    // side: -1 all rows (Nleft == -1), 0 the left rows [0, nleft) (mGrid), 1 the right rows (mGridRight)
+    explicit Grid(const orbfe_frame* f, int side = -1) : F(f) {
         invw = static_cast<float>(ORBFE_GRID_COLS) / (F->max_x - F->min_x);
         invh = static_cast<float>(ORBFE_GRID_ROWS) / (F->max_y - F->min_y);
-        for (int i = 0; i < F->n; i++) {
+        const int i0 = side == 1 ? F->nleft : 0, i1 = side == 0 ? F->nleft : F->n;
+        for (int i = i0; i < i1; i++) {
             const orbfe_keypoint& kp = F->keys[i];
             int px = (int)std::round((kp.x - F->min_x) * invw);
             int py = (int)std::round((kp.y - F->min_y) * invh);
@@ -125,53 +130,100 @@ extern "C" {
 
 int oro_sbp_local(const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs_in, const orbfe_map_point* mps,
                   int32_t n_mps, float th, int32_t bFarPoints, float thFarPoints, float nnratio) {
-    Grid grid(F);
+    const bool two = F->two_cams != 0;   // F.Nleft != -1
+    const int Nleft = F->nleft;
+    Grid grid(F, two ? 0 : -1);
+    Grid gridR(F, two ? 1 : -1);
     std::vector<int32_t> obs(mvp_obs_in, mvp_obs_in + F->n);
+    auto put = [&](int slot, const orbfe_map_point& mp) { mvp[slot] = mp.id; obs[slot] = mp.observations; };
     int nmatches = 0;
     const bool bFactor = th != 1.0;
     for (int iMP = 0; iMP < n_mps; iMP++) {
         const orbfe_map_point& mp = mps[iMP];
-        if (!(mp.flags & ORBFE_MP_IN_VIEW)) continue;
+        const bool inView = (mp.flags & ORBFE_MP_IN_VIEW) != 0, inViewR = two && (mp.flags & ORBFE_MP_IN_VIEW_R);
+        if (!inView && !inViewR) continue;
         if (bFarPoints && mp.depth > thFarPoints) continue;
         if (mp.flags & ORBFE_MP_BAD) continue;
-        const int nPredictedLevel = mp.scale_level;
-        float r = radius_by_viewing_cos(mp.view_cos);
-        if (bFactor) r *= th;
-        const std::vector<size_t> vIndices =
-            grid.area(mp.proj_x, mp.proj_y, r * F->scale_factors[nPredictedLevel], nPredictedLevel - 1, nPredictedLevel);
-        if (vIndices.empty()) continue;
-        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
-        for (size_t idx : vIndices) {
-            if (mvp[idx] >= 0 && obs[idx] > 0) continue;
-            if (F->uright && F->uright[idx] > 0) {
-                const float er = std::fabs(mp.proj_xr - F->uright[idx]);
-                if (er > r * F->scale_factors[nPredictedLevel]) continue;
-            }
-            const int dist = oracle::hamming(mp.desc, F->desc + idx * 32);
-            if (dist < bestDist) {
-                bestDist2 = bestDist; bestDist = dist;
-                bestLevel2 = bestLevel; bestLevel = F->keys[idx].octave;
-                bestIdx = (int)idx;
-            } else if (dist < bestDist2) {
-                bestLevel2 = F->keys[idx].octave;
-                bestDist2 = dist;
+        if (inView) {
+            const int nPredictedLevel = mp.scale_level;
+            float r = radius_by_viewing_cos(mp.view_cos);
+            if (bFactor) r *= th;
+            const std::vector<size_t> vIndices =
+                grid.area(mp.proj_x, mp.proj_y, r * F->scale_factors[nPredictedLevel], nPredictedLevel - 1, nPredictedLevel);
+            if (!vIndices.empty()) {
+                int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+                for (size_t idx : vIndices) {
+                    if (mvp[idx] >= 0 && obs[idx] > 0) continue;
+                    if (!two && F->uright && F->uright[idx] > 0) {
+                        const float er = std::fabs(mp.proj_xr - F->uright[idx]);
+                        if (er > r * F->scale_factors[nPredictedLevel]) continue;
+                    }
+                    const int dist = oracle::hamming(mp.desc, F->desc + idx * 32);
+                    // octave: mvKeysUn[idx] / mvKeys[idx] / mvKeysRight[idx - Nleft] == keys[idx]
+                    if (dist < bestDist) {
+                        bestDist2 = bestDist; bestDist = dist;
+                        bestLevel2 = bestLevel; bestLevel = F->keys[idx].octave;
+                        bestIdx = (int)idx;
+                    } else if (dist < bestDist2) {
+                        bestLevel2 = F->keys[idx].octave;
+                        bestDist2 = dist;
+                    }
+                }
+                if (bestDist <= TH_HIGH) {
+                    if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;   // skips the right search too
+                    if (bestLevel != bestLevel2 || bestDist <= nnratio * bestDist2) {
+                        put(bestIdx, mp);
+                        if (two && F->l2r[bestIdx] != -1) {   // the stereo partner in the right camera
+                            put(F->l2r[bestIdx] + Nleft, mp);
+                            nmatches++;
+                        }
+                        nmatches++;
+                    }
+                }
             }
         }
-        if (bestDist <= TH_HIGH) {
-            if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
-            if (bestLevel != bestLevel2 || bestDist <= nnratio * bestDist2) {
-                mvp[bestIdx] = mp.id;
-                obs[bestIdx] = mp.observations;
-                nmatches++;
+        if (two && inViewR) {
+            const int nPredictedLevel = mp.scale_level_r;
+            if (nPredictedLevel != -1) {
+                const float r = radius_by_viewing_cos(mp.view_cos_r);   // not scaled by th (:141)
+                const std::vector<size_t> vIndices = gridR.area(mp.proj_xr, mp.proj_yr,
+                                                                r * F->scale_factors[nPredictedLevel],
+                                                                nPredictedLevel - 1, nPredictedLevel);
+                if (vIndices.empty()) continue;
+                int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+                for (size_t idx : vIndices) {   // global rows: idx + Nleft in the reference's numbering
+                    if (mvp[idx] >= 0 && obs[idx] > 0) continue;
+                    const int dist = oracle::hamming(mp.desc, F->desc + idx * 32);
+                    if (dist < bestDist) {
+                        bestDist2 = bestDist; bestDist = dist;
+                        bestLevel2 = bestLevel; bestLevel = F->keys[idx].octave;
+                        bestIdx = (int)idx;
+                    } else if (dist < bestDist2) {
+                        bestLevel2 = F->keys[idx].octave;
+                        bestDist2 = dist;
+                    }
+                }
+                if (bestDist <= TH_HIGH) {
+                    if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
+                    if (F->r2l[bestIdx - Nleft] != -1) {
+                        put(F->r2l[bestIdx - Nleft], mp);
+                        nmatches++;
+                    }
+                    put(bestIdx, mp);
+                    nmatches++;
+                }
             }
         }
     }
     return nmatches;
 }
 
-int oro_sbp_lastframe(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_obs_in, const orbfe_proj_point* pts,
-                      int32_t n_pts, float th, int32_t bForward, int32_t bBackward, int32_t checkOri) {
-    Grid grid(cur);
+int oro_sbp_lastframe_stereo(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_obs_in,
+                             const orbfe_proj_point* pts, const float* right_uv, int32_t n_pts, float th,
+                             int32_t bForward, int32_t bBackward, int32_t checkOri) {
+    const bool two = cur->two_cams != 0;   // CurrentFrame.Nleft != -1
+    Grid grid(cur, two ? 0 : -1);
+    Grid gridR(cur, two ? 1 : -1);
     std::vector<int32_t> obs(mvp_obs_in, mvp_obs_in + cur->n);
     std::vector<int> rotHist[HISTO_LENGTH];
     int nmatches = 0;
@@ -187,11 +239,11 @@ int oro_sbp_lastframe(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_o
         if (bForward) v2 = grid.area(p.u, p.v, radius, nLastOctave, -1);
         else if (bBackward) v2 = grid.area(p.u, p.v, radius, 0, nLastOctave);
         else v2 = grid.area(p.u, p.v, radius, nLastOctave - 1, nLastOctave + 1);
-        if (v2.empty()) continue;
+        if (v2.empty()) continue;   // skips the right-camera search as well
         int bestDist = 256, bestIdx2 = -1;
         for (size_t i2 : v2) {
             if (mvp[i2] >= 0 && obs[i2] > 0) continue;
-            if (cur->uright && cur->uright[i2] > 0) {
+            if (!two && cur->uright && cur->uright[i2] > 0) {
                 const float ur = p.u - cur->mbf * p.invzc;
                 const float er = std::fabs(ur - cur->uright[i2]);
                 if (er > radius) continue;
@@ -205,6 +257,25 @@ int oro_sbp_lastframe(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_o
             nmatches++;
             if (checkOri) rotHist[rot_bin(p.angle, cur->keys[bestIdx2].angle)].push_back(bestIdx2);
         }
+        if (two) {   // :1794-1858, the projection into the right camera comes from the caller
+            const float ur = right_uv[2 * i], vr = right_uv[2 * i + 1];
+            std::vector<size_t> w2;
+            if (bForward) w2 = gridR.area(ur, vr, radius, nLastOctave, -1);
+            else if (bBackward) w2 = gridR.area(ur, vr, radius, 0, nLastOctave);
+            else w2 = gridR.area(ur, vr, radius, nLastOctave - 1, nLastOctave + 1);
+            int bestDistR = 256, bestIdxR = -1;
+            for (size_t i2 : w2) {   // global rows (i2 + Nleft in the reference)
+                if (mvp[i2] >= 0 && obs[i2] > 0) continue;
+                const int dist = oracle::hamming(p.desc, cur->desc + i2 * 32);
+                if (dist < bestDistR) { bestDistR = dist; bestIdxR = (int)i2; }
+            }
+            if (bestDistR <= TH_HIGH) {
+                mvp[bestIdxR] = p.id;
+                obs[bestIdxR] = p.observations;
+                nmatches++;
+                if (checkOri) rotHist[rot_bin(p.angle, cur->keys[bestIdxR].angle)].push_back(bestIdxR);
+            }
+        }
     }
     if (checkOri) {
         int ind1 = -1, ind2 = -1, ind3 = -1;
@@ -214,6 +285,12 @@ int oro_sbp_lastframe(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_o
                 for (int k : rotHist[i]) { mvp[k] = -1; nmatches--; }
     }
     return nmatches;
+}
+
+int oro_sbp_lastframe(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_obs_in, const orbfe_proj_point* pts,
+                      int32_t n_pts, float th, int32_t bForward, int32_t bBackward, int32_t checkOri) {
+    if (cur->two_cams) return -1;   // needs the right-camera projections (oro_sbp_lastframe_stereo)
+    return oro_sbp_lastframe_stereo(cur, mvp, mvp_obs_in, pts, nullptr, n_pts, th, bForward, bBackward, checkOri);
 }
 
 int oro_sbp_kf(const orbfe_frame* cur, int32_t* mvp, const orbfe_proj_point* pts, int32_t n_pts, float th,
@@ -312,17 +389,32 @@ int oro_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, con
                 if (mp < 0) continue;
                 const uint8_t* dKF = kf_desc + (size_t)realIdxKF * 32;
                 int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
+                int bestDist1R = 256, bestIdxFR = -1, bestDist2R = 256;
                 for (int ib = ffv->offsets[b]; ib < ffv->offsets[b + 1]; ib++) {
                     const unsigned realIdxF = ffv->indices[ib];
                     if (out[realIdxF] >= 0) continue;
                     const int dist = oracle::hamming(dKF, F->desc + (size_t)realIdxF * 32);
-                    if (dist < bestDist1) { bestDist2 = bestDist1; bestDist1 = dist; bestIdxF = (int)realIdxF; }
-                    else if (dist < bestDist2) bestDist2 = dist;
+                    if (!F->two_cams) {
+                        if (dist < bestDist1) { bestDist2 = bestDist1; bestDist1 = dist; bestIdxF = (int)realIdxF; }
+                        else if (dist < bestDist2) bestDist2 = dist;
+                    } else {   // :288-313
+                        const bool left = (int)realIdxF < F->nleft;
+                        if (left && dist < bestDist1) { bestDist2 = bestDist1; bestDist1 = dist; bestIdxF = (int)realIdxF; }
+                        else if (left && dist < bestDist2) bestDist2 = dist;
+                        if (!left && dist < bestDist1R) { bestDist2R = bestDist1R; bestDist1R = dist; bestIdxFR = (int)realIdxF; }
+                        else if (!left && dist < bestDist2R) bestDist2R = dist;
+                    }
                 }
                 if (bestDist1 <= TH_LOW) {
                     if (static_cast<float>(bestDist1) < nnratio * static_cast<float>(bestDist2)) {
                         out[bestIdxF] = mp;
                         if (checkOri) rotHist[rot_bin(kf_keys[realIdxKF].angle, F->keys[bestIdxF].angle)].push_back(bestIdxF);
+                        nmatches++;
+                    }
+                    if (bestDist1R <= TH_LOW) {
+                        // the reference's ratio test here ends in "|| true" (:359): always taken
+                        out[bestIdxFR] = mp;
+                        if (checkOri) rotHist[rot_bin(kf_keys[realIdxKF].angle, F->keys[bestIdxFR].angle)].push_back(bestIdxFR);
                         nmatches++;
                     }
                 }

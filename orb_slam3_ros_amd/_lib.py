@@ -56,6 +56,8 @@ _SIGS = {
     "orbfe_version": (ctypes.c_char_p, []),
     "orbfe_search_by_projection_local": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _c_float, _c_int, _c_float, _c_float]),
     "orbfe_search_by_projection_lastframe": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _c_float, _c_int, _c_int, _c_int]),
+    "orbfe_search_by_projection_lastframe_stereo": (_c_int, [_vp, _vp, _vp, _vp, _vp, _c_int, _c_float, _c_int, _c_int,
+                                                             _c_int]),
     "orbfe_search_by_projection_kf": (_c_int, [_vp, _vp, _vp, _c_int, _c_float, _c_int, _c_int]),
     "orbfe_search_for_initialization": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _c_float, _c_int]),
     "orbfe_search_by_bow": (_c_int, [_vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_float, _c_int]),

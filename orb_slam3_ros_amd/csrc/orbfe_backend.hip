@@ -494,7 +494,7 @@ int orbfe_search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, c
                                    const orbfe_frame* KF2, const int32_t* mp2, const orbfe_feature_vector* fv2,
                                    const float* F12, const float* ep, const float* level_sigma2_2,
                                    int32_t bOnlyStereo, int32_t bCoarse, int32_t checkOri, int32_t* matches12) {
-    if (!frame_ok(KF1) || !frame_ok(KF2) || !F12 || !ep || !level_sigma2_2 || (KF1->n > 0 && (!mp1 || !matches12)) ||
+    if (!frame1_ok(KF1) || !frame1_ok(KF2) || !F12 || !ep || !level_sigma2_2 || (KF1->n > 0 && (!mp1 || !matches12)) ||
         (KF2->n > 0 && !mp2))
         return ORBFE_E_ARG;
     const int n1 = KF1->n, n2 = KF2->n;
@@ -562,7 +562,7 @@ int orbfe_search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, c
 int orbfe_fuse(const orbfe_frame* KF, const orbfe_kf_camera* cam, const float* inv_level_sigma2,
                const orbfe_map_point_3d* pts, int32_t n, float th, int32_t sim3, int32_t* best_idx,
                int32_t* best_dist) {
-    if (!frame_ok(KF) || !cam || !pose_ok(&cam->Tcw) || n < 0 || (n > 0 && (!pts || !best_idx || !best_dist)) ||
+    if (!frame1_ok(KF) || !cam || !pose_ok(&cam->Tcw) || n < 0 || (n > 0 && (!pts || !best_idx || !best_dist)) ||
         (!sim3 && !inv_level_sigma2))
         return ORBFE_E_ARG;
     for (int i = 0; i < n; i++) best_idx[i] = best_dist[i] = -1;
@@ -607,7 +607,7 @@ int orbfe_fuse(const orbfe_frame* KF, const orbfe_kf_camera* cam, const float* i
 int orbfe_search_by_projection_sim3(const orbfe_frame* KF, const orbfe_kf_camera* cam, const orbfe_map_point_3d* pts,
                                     int32_t n, const int32_t* point_kfs, int32_t th, float ratioHamming,
                                     int32_t* matched, int32_t* matched_kf) {
-    if (!frame_ok(KF) || !cam || !pose_ok(&cam->Tcw) || n < 0 || (n > 0 && !pts) || (KF->n > 0 && !matched) ||
+    if (!frame1_ok(KF) || !cam || !pose_ok(&cam->Tcw) || n < 0 || (n > 0 && !pts) || (KF->n > 0 && !matched) ||
         (point_kfs && KF->n > 0 && !matched_kf))
         return ORBFE_E_ARG;
     if (n == 0 || KF->n == 0) return 0;
@@ -659,7 +659,7 @@ int orbfe_search_by_projection_sim3(const orbfe_frame* KF, const orbfe_kf_camera
             if (pass >= MT_MAX_PASSES) return ORBFE_E_CAPACITY;
             fill(first, nk, MT_INF);
             hipLaunchKernelGGL(k_mt_first_strided, gq, dim3(MT_NT), 0, s, assign, (const uint8_t*)assign, 4, n, 0,
-                               first);
+                               first, 1);
             hipLaunchKernelGGL(k_kf_search, gq, dim3(MT_NT), 0, s, fr, ms_ptr<const KfProj>(o_pj),
                                ms_ptr<const orbfe_map_point_3d>(o_pts), n, (float)th, 0, (const float*)nullptr, 256,
                                max_acc, ms_ptr<const int>(o_b0), first, assign, (int*)nullptr, changed + pass);
@@ -687,7 +687,7 @@ int orbfe_search_by_sim3(const orbfe_frame* KF1, const orbfe_frame* KF2, const o
                          const orbfe_map_point_3d* pts2, const orbfe_kf_camera* cam1, const orbfe_kf_camera* cam2,
                          const orbfe_pose* S12, const orbfe_pose* S21, float th, int32_t* matches12,
                          const int32_t* matched_idx2) {
-    if (!frame_ok(KF1) || !frame_ok(KF2) || !cam1 || !cam2 || !pose_ok(&cam1->Tcw) || !pose_ok(&cam2->Tcw) ||
+    if (!frame1_ok(KF1) || !frame1_ok(KF2) || !cam1 || !cam2 || !pose_ok(&cam1->Tcw) || !pose_ok(&cam2->Tcw) ||
         !pose_ok(S12) || !pose_ok(S21) || (KF1->n > 0 && (!pts1 || !matches12)) || (KF2->n > 0 && !pts2))
         return ORBFE_E_ARG;
     const int n1 = KF1->n, n2 = KF2->n;

@@ -37,6 +37,11 @@ struct FrameDev {
     const int* pcidx;
     int gstride_c, gstride_i;
     int nlevels;            // scale_level / octave of a query must lie in [0, nlevels)
+    // two-camera frame (Nleft != -1): rows [0, nleft) are mvKeys, [nleft, n) mvKeysRight; every
+    // grid holds the left cells first and the right cells (mGridRight) at cell + MT_NCELL
+    int nleft;              // -1: single camera
+    const int* l2r;         // mvLeftToRightMatch [nleft]
+    const int* r2l;         // mvRightToLeftMatch [n - nleft]
 };
 
 __device__ __forceinline__ int mt_hamming(const uint8_t* a, const uint32_t* b) {
@@ -78,10 +83,12 @@ __device__ __forceinline__ void mt_for_area(const FrameDev& fr, const int* cs, c
 }
 
 // AssignFeaturesToGrid (Frame.cc:385-416): stable (cell, index) order via a bitonic sort of
-// (cell << 16 | index) keys in LDS. One block per frame, n <= MT_GRID_MAXN.
+// (cell << 16 | index) keys in LDS. One block per frame, n <= MT_GRID_MAXN. Two-camera frames
+// (nleft >= 0): rows >= nleft go to the right grid, cells MT_NCELL.. (Frame.cc:408-411).
 #define MT_GRID_MAXN 8192
-__global__ __launch_bounds__(1024) void k_mt_grid(const OrbKeyPoint* keys, int n, float minx, float miny, float invw,
-                                                  float invh, int* cstart, int* cidx, int gstride_c, int gstride_i) {
+__global__ __launch_bounds__(1024) void k_mt_grid(const OrbKeyPoint* keys, int n, int nleft, float minx, float miny,
+                                                  float invw, float invh, int* cstart, int* cidx, int gstride_c,
+                                                  int gstride_i) {
     __shared__ uint32_t s_k[MT_GRID_MAXN];
     // block 0: full grid; block g >= 1: keypoints with octave in [g-2, g-1] (level-(g-1) candidates)
     const int gi = blockIdx.x;
@@ -90,16 +97,17 @@ __global__ __launch_bounds__(1024) void k_mt_grid(const OrbKeyPoint* keys, int n
     cidx += (size_t)gi * gstride_i;
     int P = 1;
     while (P < n) P <<= 1;
+    const int ncells = nleft >= 0 ? 2 * MT_NCELL : MT_NCELL;
     for (int i = threadIdx.x; i < P; i += blockDim.x) {
         uint32_t key = 0xFFFFFFFFu;
         if (i < n) {
             const OrbKeyPoint kp = keys[i];
             const int px = (int)roundf((kp.x - minx) * invw);
             const int py = (int)roundf((kp.y - miny) * invh);
-            uint32_t cell = MT_NCELL;   // outside the grid: never a candidate (PosInGrid false)
+            uint32_t cell = (uint32_t)ncells;   // outside the grid: never a candidate (PosInGrid false)
             if (!(px < 0 || px >= ORBFE_GRID_COLS || py < 0 || py >= ORBFE_GRID_ROWS) && kp.octave >= lvlo &&
                 kp.octave <= lvhi)
-                cell = (uint32_t)(px * ORBFE_GRID_ROWS + py);
+                cell = (uint32_t)(px * ORBFE_GRID_ROWS + py + (nleft >= 0 && i >= nleft ? MT_NCELL : 0));
             key = (cell << 16) | (uint32_t)i;
         }
         s_k[i] = key;
@@ -117,7 +125,7 @@ __global__ __launch_bounds__(1024) void k_mt_grid(const OrbKeyPoint* keys, int n
             SYNC();
         }
     for (int i = threadIdx.x; i < n; i += blockDim.x) cidx[i] = (int)(s_k[i] & 0xFFFFu);
-    for (int c = threadIdx.x; c <= MT_NCELL; c += blockDim.x) {
+    for (int c = threadIdx.x; c <= ncells; c += blockDim.x) {
         int lo = 0, hi = n;   // first position with cell >= c
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
@@ -127,14 +135,16 @@ __global__ __launch_bounds__(1024) void k_mt_grid(const OrbKeyPoint* keys, int n
     }
 }
 
-// first[k] = min query index j with assign[j] == k (and Observations_j > 0 when need_obs); the
-// observation count is read from the query records (byte stride) in place.
-__global__ void k_mt_first_strided(const int* assign, const uint8_t* qobs, int stride, int nq, int need_obs,
-                                   int* first) {
+// first[k] = min entry index j with assign[j] == k (and Observations > 0 of its query when
+// need_obs); the observation count is read from the query records (byte stride) in place. A query
+// writes W consecutive entries (its slot writes in the reference's order), so entry j belongs to
+// query j / W and entry order is the reference's write order.
+__global__ void k_mt_first_strided(const int* assign, const uint8_t* qobs, int stride, int nent, int need_obs,
+                                   int* first, int W) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= nq) return;
+    if (j >= nent) return;
     const int a = assign[j];
-    if (a >= 0 && (!need_obs || *(const int*)(qobs + (size_t)j * stride) > 0)) atomicMin(&first[a], j);
+    if (a >= 0 && (!need_obs || *(const int*)(qobs + (size_t)(j / W) * stride) > 0)) atomicMin(&first[a], j);
 }
 __global__ void k_mt_fill(int* p, int n, int v) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -376,6 +386,172 @@ __global__ __launch_bounds__(MT_NT) void k_sbp_proj(FrameDev fr, const orbfe_pro
     }
 }
 
+// ---- Two-camera frames (F.Nleft != -1). A query writes up to W slots in the reference's order; the
+// entry index 4 q + b (local map) / 2 q + b (last frame) is the write's position in the sequential
+// run, and a branch at entry e sees exactly the writes with a smaller entry index. The last-frame
+// writes are all guarded by the "already taken" check, so first[k] < e decides as in the
+// single-camera kernels. The local map's partner writes are NOT guarded (the reference overwrites
+// the partner slot unconditionally), so there the occupant at entry e is the slot's LAST writer
+// before e: every pass buckets the writes per slot (k_slot_count / k_slot_fill) and a candidate
+// scans its slot's bucket.
+// SearchByProjection(F, vpMapPoints, ...) Nleft != -1 (ORBmatcher.cc:62-209): entries
+//   b = 0 left best, 1 its right partner nleft + mvLeftToRightMatch[best] (:124-128),
+//   b = 2 mvRightToLeftMatch[right best] (:197-201), 3 the right best (nleft + bestIdx, :204).
+__device__ __forceinline__ void mt_best2_update(int dist, int oct, int idx, int& bestDist, int& bestLevel,
+                                                int& bestDist2, int& bestLevel2, int& bestIdx) {
+    if (dist < bestDist) {
+        bestDist2 = bestDist; bestDist = dist;
+        bestLevel2 = bestLevel; bestLevel = oct;
+        bestIdx = idx;
+    } else if (dist < bestDist2) {
+        bestLevel2 = oct;
+        bestDist2 = dist;
+    }
+}
+__global__ void k_slot_count(const int* assign, int nent, int* cnt) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < nent && assign[e] >= 0) atomicAdd(&cnt[assign[e]], 1);
+}
+// exclusive scan of cnt[0, n) into off[0, n] (one 1024-thread block, n <= MT_GRID_MAXN); cursor = off
+__global__ __launch_bounds__(1024) void k_slot_scan(const int* cnt, int n, int* off, int* cursor) {
+    __shared__ int s_part[1024];
+    const int t = threadIdx.x, per = (n + 1023) / 1024, i0 = t * per, i1 = min(i0 + per, n);
+    int sum = 0;
+    for (int i = i0; i < i1; i++) sum += cnt[i];
+    s_part[t] = sum;
+    SYNC();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int v = t >= d ? s_part[t - d] : 0;
+        SYNC();
+        s_part[t] += v;
+        SYNC();
+    }
+    int run = s_part[t] - sum;
+    for (int i = i0; i < i1; i++) { off[i] = run; cursor[i] = run; run += cnt[i]; }
+    if (t == 1023) off[n] = s_part[1023];
+}
+__global__ void k_slot_fill(const int* assign, int nent, int* cursor, int* lst) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < nent && assign[e] >= 0) lst[atomicAdd(&cursor[assign[e]], 1)] = e;
+}
+// occupant of slot k before entry e: blocked when it holds a point with Observations() > 0
+__device__ __forceinline__ bool mt_taken(const int* off, const int* lst, const orbfe_map_point* mps,
+                                         const int* blocked0, int k, int e) {
+    int last = -1;
+    for (int p = off[k]; p < off[k + 1]; p++) {
+        const int w = lst[p];
+        if (w < e && w > last) last = w;
+    }
+    return last < 0 ? blocked0[k] != 0 : mps[last >> 2].observations > 0;
+}
+__global__ __launch_bounds__(MT_NT) void k_sbp_local2(FrameDev fr, const orbfe_map_point* mps, int nq, float th,
+                                                      int bFar, float thFar, float nnratio, const int* blocked0,
+                                                      const int* off, const int* lst, int* assign, int* changed) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    const orbfe_map_point& mp = mps[q];
+    int res[4] = {-1, -1, -1, -1};
+    const bool inView = (mp.flags & ORBFE_MP_IN_VIEW) != 0, inViewR = (mp.flags & ORBFE_MP_IN_VIEW_R) != 0;
+    bool go = (inView || inViewR) && !(bFar && mp.depth > thFar) && !(mp.flags & ORBFE_MP_BAD);
+    const int e0 = 4 * q;
+    if (go && inView && mp.scale_level >= 0 && mp.scale_level < fr.nlevels) {
+        const int lvl = mp.scale_level;
+        float r = mp.view_cos > 0.998 ? 2.5f : 4.0f;
+        if (th != 1.0f) r *= th;
+        const float R = r * fr.scale[lvl];
+        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+        mt_for_area(fr, fr.pcstart + lvl * fr.gstride_c, fr.pcidx + lvl * fr.gstride_i, mp.proj_x, mp.proj_y, R,
+                    lvl - 1, lvl, [&](int idx, const OrbKeyPoint& kp) {
+            if (mt_taken(off, lst, mps, blocked0, idx, e0)) return;   // no mvuRight check when Nleft != -1
+            mt_best2_update(mt_hamming(mp.desc, fr.desc + 8 * idx), kp.octave, idx, bestDist, bestLevel, bestDist2,
+                            bestLevel2, bestIdx);
+        });
+        if (bestDist <= MT_TH_HIGH) {
+            if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) {
+                go = false;   // the reference's `continue` also skips the right-camera search
+            } else {
+                res[0] = bestIdx;
+                const int p = fr.l2r[bestIdx];
+                if (p >= 0 && fr.nleft + p < fr.n) res[1] = fr.nleft + p;   // != -1 (range-guarded)
+            }
+        }
+    }
+    if (go && inViewR && mp.scale_level_r != -1 && mp.scale_level_r >= 0 && mp.scale_level_r < fr.nlevels) {
+        const int lvl = mp.scale_level_r;
+        const float r = mp.view_cos_r > 0.998 ? 2.5f : 4.0f;   // RadiusByViewingCos, not scaled by th (:141)
+        const float R = r * fr.scale[lvl];
+        // this query's own partner write (entry 4 q + 1, this pass's value) is the slot's latest
+        // write when it exists; the other writes seen are those of earlier points (entries < 4 q)
+        const int own = res[1], own_obs = mp.observations;
+        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+        mt_for_area(fr, fr.pcstart + lvl * fr.gstride_c + MT_NCELL, fr.pcidx + lvl * fr.gstride_i, mp.proj_xr,
+                    mp.proj_yr, R, lvl - 1, lvl, [&](int idx, const OrbKeyPoint& kp) {
+            if (idx == own ? own_obs > 0 : mt_taken(off, lst, mps, blocked0, idx, e0)) return;
+            mt_best2_update(mt_hamming(mp.desc, fr.desc + 8 * idx), kp.octave, idx, bestDist, bestLevel, bestDist2,
+                            bestLevel2, bestIdx);
+        });
+        if (bestDist <= MT_TH_HIGH && !(bestLevel == bestLevel2 && bestDist > nnratio * bestDist2)) {
+            const int p = fr.r2l[bestIdx - fr.nleft];
+            if (p >= 0 && p < fr.nleft) res[2] = p;
+            res[3] = bestIdx;
+        }
+    }
+    int ch = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++)
+        if (res[b] != assign[e0 + b]) { assign[e0 + b] = res[b]; ch = 1; }
+    if (ch) atomicAdd(changed, 1);
+}
+
+// SearchByProjection(CurrentFrame, LastFrame, th, bMono) with CurrentFrame.Nleft != -1
+// (ORBmatcher.cc:1695-1858): entry 2 q = the left-grid best, 2 q + 1 = the right-grid best for the
+// caller's right-camera projection right_uv[q]; a point whose left window is empty skips both.
+__global__ __launch_bounds__(MT_NT) void k_sbp_proj2(FrameDev fr, const orbfe_proj_point* pts, const float2* right_uv,
+                                                     int nq, float th, int bForward, int bBackward,
+                                                     const int* blocked0, const int* first, int* assign,
+                                                     int* changed) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    const orbfe_proj_point& p = pts[q];
+    int res[2] = {-1, -1};
+    bool ok = p.valid != 0 && p.octave >= 0 && p.octave < fr.nlevels;
+    if (ok && p.invzc < 0) ok = false;
+    else if (ok && (p.u < fr.minx || p.u > fr.maxx)) ok = false;
+    else if (ok && (p.v < fr.miny || p.v > fr.maxy)) ok = false;
+    if (ok) {
+        const int oct = p.octave;
+        const float radius = th * fr.scale[oct];
+        int minL, maxL;
+        if (bForward) { minL = oct; maxL = -1; }
+        else if (bBackward) { minL = 0; maxL = oct; }
+        else { minL = oct - 1; maxL = oct + 1; }
+        int bestDist = 256, bestIdx2 = -1, ncand = 0;
+        mt_for_area(fr, fr.cstart, fr.cidx, p.u, p.v, radius, minL, maxL, [&](int i2, const OrbKeyPoint&) {
+            ncand++;   // vIndices2 non-empty (blocked candidates included)
+            if (blocked0[i2] || first[i2] < 2 * q) return;
+            const int dist = mt_hamming(p.desc, fr.desc + 8 * i2);
+            if (dist < bestDist) { bestDist = dist; bestIdx2 = i2; }
+        });
+        if (ncand > 0) {
+            if (bestDist <= MT_TH_HIGH) res[0] = bestIdx2;
+            const float2 uv = right_uv[q];
+            int bestDistR = 256, bestIdxR = -1;
+            mt_for_area(fr, fr.cstart + MT_NCELL, fr.cidx, uv.x, uv.y, radius, minL, maxL, [&](int i2, const OrbKeyPoint&) {
+                if (blocked0[i2] || first[i2] < 2 * q + 1) return;
+                const int dist = mt_hamming(p.desc, fr.desc + 8 * i2);
+                if (dist < bestDistR) { bestDistR = dist; bestIdxR = i2; }
+            });
+            if (bestDistR <= MT_TH_HIGH) res[1] = bestIdxR;
+        }
+    }
+    const bool ch = res[0] != assign[2 * q] || res[1] != assign[2 * q + 1];
+    if (ch) {
+        assign[2 * q] = res[0];
+        assign[2 * q + 1] = res[1];
+        atomicAdd(changed, 1);
+    }
+}
+
 // ---- Frame::isInFrustum (pinhole, Frame.cc:512-570) + MapPoint::PredictScale (MapPoint.cc:531-546)
 // for every local map point (Tracking.cc:3407-3425): one thread per point, float arithmetic in the
 // reference's (Eigen's) order, no contraction, glibc logf port. Writes the tracking snapshot the
@@ -396,7 +572,9 @@ __global__ __launch_bounds__(MT_NT) void k_frustum(CamDev c, const orbfe_map_poi
     t.flags = p.flags & ORBFE_MP_BAD;
     t.observations = p.observations;
     t.id = p.id;
-    t.reserved[0] = t.reserved[1] = t.reserved[2] = 0;
+    t.proj_yr = 0.f;
+    t.view_cos_r = 0.f;
+    t.scale_level_r = -1;
     memcpy(t.desc, p.desc, 32);
     bool in = false;
     if (!(p.flags & (ORBFE_MP_SKIP | ORBFE_MP_BAD))) {
@@ -476,7 +654,7 @@ __device__ __forceinline__ unsigned mt_three_maxima_keep(const int* hist) {
 // dropped bins; K3 writes the slots.
 __global__ __launch_bounds__(MT_NT) void k_mt_commit_count(const OrbKeyPoint* keys, const int* assign,
                                                            const float* q_angle, int q_stride_bytes, int nq,
-                                                           int checkOri, int* result, int* hist) {
+                                                           int checkOri, int* result, int* hist, int W) {
     __shared__ int s_hist[MT_HISTO];
     if (threadIdx.x < MT_HISTO) s_hist[threadIdx.x] = 0;
     SYNC();
@@ -485,7 +663,7 @@ __global__ __launch_bounds__(MT_NT) void k_mt_commit_count(const OrbKeyPoint* ke
     if (a >= 0) {
         atomicMax(&result[2 + a], j);
         if (checkOri) {
-            const float qa = *(const float*)((const uint8_t*)q_angle + (size_t)j * q_stride_bytes);
+            const float qa = *(const float*)((const uint8_t*)q_angle + (size_t)(j / W) * q_stride_bytes);
             atomicAdd(&s_hist[mt_rot_bin(qa, keys[a].angle)], 1);
         }
     }
@@ -497,7 +675,7 @@ __global__ __launch_bounds__(MT_NT) void k_mt_commit_count(const OrbKeyPoint* ke
 
 __global__ __launch_bounds__(MT_NT) void k_mt_commit_drop(const OrbKeyPoint* keys, const int* assign,
                                                           const float* q_angle, int q_stride_bytes, int nq,
-                                                          const int* hist, int* result) {
+                                                          const int* hist, int* result, int W) {
     __shared__ unsigned s_keep;
     if (threadIdx.x == 0) s_keep = mt_three_maxima_keep(hist);
     SYNC();
@@ -505,7 +683,7 @@ __global__ __launch_bounds__(MT_NT) void k_mt_commit_drop(const OrbKeyPoint* key
     const int a = j < nq ? assign[j] : -1;
     bool drop = false;
     if (a >= 0) {
-        const float qa = *(const float*)((const uint8_t*)q_angle + (size_t)j * q_stride_bytes);
+        const float qa = *(const float*)((const uint8_t*)q_angle + (size_t)(j / W) * q_stride_bytes);
         drop = !((s_keep >> mt_rot_bin(qa, keys[a].angle)) & 1u);
         if (drop) result[2 + a] = -2;   // K1 finished before this kernel: no race with the winner write
     }
@@ -513,12 +691,12 @@ __global__ __launch_bounds__(MT_NT) void k_mt_commit_drop(const OrbKeyPoint* key
     if ((threadIdx.x & 63) == 0 && m) atomicAdd(&result[1], __popcll(m));
 }
 
-__global__ void k_mt_commit_write(int n, const int* qid, int q_stride_bytes, const int* result, int* mvp) {
+__global__ void k_mt_commit_write(int n, const int* qid, int q_stride_bytes, const int* result, int* mvp, int W) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     const int w = result[2 + k];
     if (w == -2) mvp[k] = -1;
-    else if (w >= 0) mvp[k] = *(const int*)((const uint8_t*)qid + (size_t)w * q_stride_bytes);
+    else if (w >= 0) mvp[k] = *(const int*)((const uint8_t*)qid + (size_t)(w / W) * q_stride_bytes);
 }
 
 // ---- SearchForInitialization (ORBmatcher.cc:648-763) ----
@@ -647,10 +825,12 @@ __global__ __launch_bounds__(1024) void k_init_commit(FrameDev f1, FrameDev f2, 
 // ---- SearchByBoW(KF, F) (ORBmatcher.cc:223-425): one thread per node present in both vectors.
 // Every frame index belongs to exactly one vocabulary node, so the "already matched" skip is local
 // to the node and the node walks are independent (the reference's order inside a node is kept).
+// A two-camera F (nleft >= 0) keeps a left and a right best / second-best (:288-313); the right
+// match is taken inside the left's bestDist1 <= TH_LOW with its ratio test disabled ("|| true", :359).
 __global__ __launch_bounds__(MT_NT) void k_bow_nodes(const int* pairs, int npairs, const int* kf_off,
                                                      const uint32_t* kf_idx, const int* f_off, const uint32_t* f_idx,
                                                      const int32_t* kf_mp, const uint32_t* kf_desc,
-                                                     const uint32_t* f_desc, float nnratio, int* out_src) {
+                                                     const uint32_t* f_desc, float nnratio, int nleft, int* out_src) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= npairs) return;
     const int a = pairs[2 * t], b = pairs[2 * t + 1];
@@ -661,17 +841,26 @@ __global__ __launch_bounds__(MT_NT) void k_bow_nodes(const int* pairs, int npair
 #pragma unroll
         for (int w = 0; w < 8; w++) dk[w] = kf_desc[8 * realIdxKF + w];
         int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
+        int bestDist1R = 256, bestIdxFR = -1, bestDist2R = 256;
         for (int ib = f_off[b]; ib < f_off[b + 1]; ib++) {
             const unsigned realIdxF = f_idx[ib];
             if (out_src[realIdxF] >= 0) continue;
             int dist = 0;
 #pragma unroll
             for (int w = 0; w < 8; w++) dist += __popc(dk[w] ^ f_desc[8 * realIdxF + w]);
-            if (dist < bestDist1) { bestDist2 = bestDist1; bestDist1 = dist; bestIdxF = (int)realIdxF; }
-            else if (dist < bestDist2) bestDist2 = dist;
+            if (nleft < 0 || (int)realIdxF < nleft) {
+                if (dist < bestDist1) { bestDist2 = bestDist1; bestDist1 = dist; bestIdxF = (int)realIdxF; }
+                else if (dist < bestDist2) bestDist2 = dist;
+            } else {
+                if (dist < bestDist1R) { bestDist2R = bestDist1R; bestDist1R = dist; bestIdxFR = (int)realIdxF; }
+                else if (dist < bestDist2R) bestDist2R = dist;
+            }
         }
-        if (bestDist1 <= MT_TH_LOW && static_cast<float>(bestDist1) < nnratio * static_cast<float>(bestDist2))
-            out_src[bestIdxF] = (int)realIdxKF;
+        (void)bestDist2R;
+        if (bestDist1 <= MT_TH_LOW) {
+            if (static_cast<float>(bestDist1) < nnratio * static_cast<float>(bestDist2)) out_src[bestIdxF] = (int)realIdxKF;
+            if (bestDist1R <= MT_TH_LOW) out_src[bestIdxFR] = (int)realIdxKF;
+        }
     }
 }
 __global__ __launch_bounds__(1024) void k_bow_commit(const OrbKeyPoint* kf_keys, const OrbKeyPoint* f_keys, int fn,
@@ -893,21 +1082,28 @@ template <typename T> T* ms_ptr(size_t off) { return reinterpret_cast<T*>(t_ms.d
 // Upload a frame and plan its grid; returns the device view after ms_prepare (fill_frame).
 struct FramePlan {
     const orbfe_frame* F;
-    size_t keys, desc, uright, scale, cstart, cidx;
+    size_t keys, desc, uright, scale, cstart, cidx, l2r = 0, r2l = 0;
     bool has_uright;
+    bool two = false;   // Nleft != -1: left + right grids, l2r / r2l uploaded
     void plan(Plan& p, const orbfe_frame* f, bool want_grid, bool want_uright) {
         F = f;
+        two = f->two_cams != 0;
         keys = p.upload(f->keys, (size_t)f->n * sizeof(orbfe_keypoint));
         desc = p.upload(f->desc, (size_t)f->n * 32);
-        has_uright = want_uright && f->uright != nullptr;
+        has_uright = !two && want_uright && f->uright != nullptr;
         uright = has_uright ? p.upload(f->uright, (size_t)f->n * 4) : 0;
         scale = p.upload(f->scale_factors, (size_t)f->nlevels * 4);
+        if (two) {
+            l2r = p.upload(f->l2r, (size_t)f->nleft * 4);
+            r2l = p.upload(f->r2l, (size_t)(f->n - f->nleft) * 4);
+        }
         (void)want_grid;
     }
     int ngrids = 1;
+    int cells() const { return (two ? 2 : 1) * MT_NCELL; }
     void plan_grid(Plan& p, int grids) {   // grids = 1 (full) + level-restricted grids
         ngrids = grids;
-        cstart = p.scratch((size_t)grids * (MT_NCELL + 1) * 4);
+        cstart = p.scratch((size_t)grids * (cells() + 1) * 4);
         cidx = p.scratch((size_t)grids * std::max(F->n, 1) * 4);
     }
     // device-resident frame: F's arrays are already device pointers (no upload)
@@ -915,7 +1111,8 @@ struct FramePlan {
     void plan_dev(const orbfe_frame* f, bool want_uright) {
         F = f;
         dev = true;
-        has_uright = want_uright && f->uright != nullptr;
+        two = f->two_cams != 0;
+        has_uright = !two && want_uright && f->uright != nullptr;
     }
     FrameDev view() const {
         FrameDev v;
@@ -932,21 +1129,39 @@ struct FramePlan {
         v.scale = dev ? F->scale_factors : ms_ptr<const float>(scale);
         v.cstart = ms_ptr<const int>(cstart);
         v.cidx = ms_ptr<const int>(cidx);
-        v.gstride_c = MT_NCELL + 1;
+        v.gstride_c = cells() + 1;
         v.gstride_i = std::max(F->n, 1);
         v.pcstart = v.cstart + v.gstride_c;
         v.pcidx = v.cidx + v.gstride_i;
+        v.nleft = two ? F->nleft : -1;
+        v.l2r = two ? (dev ? F->l2r : ms_ptr<const int>(l2r)) : nullptr;
+        v.r2l = two ? (dev ? F->r2l : ms_ptr<const int>(r2l)) : nullptr;
         return v;
     }
     void launch_grid(const FrameDev& v) const {
-        hipLaunchKernelGGL(k_mt_grid, dim3(ngrids), dim3(1024), 0, t_ms.stream, v.keys, v.n, v.minx, v.miny, v.invw,
-                           v.invh, (int*)v.cstart, (int*)v.cidx, v.gstride_c, v.gstride_i);
+        hipLaunchKernelGGL(k_mt_grid, dim3(ngrids), dim3(1024), 0, t_ms.stream, v.keys, v.n, v.nleft, v.minx, v.miny,
+                           v.invw, v.invh, (int*)v.cstart, (int*)v.cidx, v.gstride_c, v.gstride_i);
     }
 };
 
 bool frame_ok(const orbfe_frame* f) {
     return f && f->n >= 0 && f->n <= MT_GRID_MAXN && (f->n == 0 || (f->keys && f->desc)) && f->scale_factors &&
-           f->nlevels > 0;
+           f->nlevels > 0 &&
+           (!f->two_cams || (f->nleft >= 0 && f->nleft <= f->n && (f->nleft == 0 || f->l2r) &&
+                             (f->nleft == f->n || f->r2l)));
+}
+// single-camera frames only: the back-end matchers and SearchForInitialization restate the
+// reference's Nleft == -1 branches
+bool frame1_ok(const orbfe_frame* f) { return frame_ok(f) && !f->two_cams; }
+// host check of a two-camera frame's stereo links (they index slots)
+bool links_ok(const orbfe_frame* f) {
+    if (!f->two_cams) return true;
+    const int nr = f->n - f->nleft;
+    for (int i = 0; i < f->nleft; i++)
+        if (f->l2r[i] < -1 || f->l2r[i] >= nr) return false;
+    for (int i = 0; i < nr; i++)
+        if (f->r2l[i] < -1 || f->r2l[i] >= f->nleft) return false;
+    return true;
 }
 
 inline void fill(int* p, int n, int v) {
@@ -979,10 +1194,18 @@ __global__ void k_blocked0(const int32_t* mvp, const int32_t* obs, int n, int an
 
 int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, const void* queries, int nq,
             size_t qstride, size_t qobs_off, size_t qid_off, size_t qangle_off, size_t qlevel_off, float th, int a0, int a1, float thFar,
-            float nnratio, int maxDist, int checkOri, const FrustumIn* fin = nullptr, const DevIn* dev = nullptr) {
+            float nnratio, int maxDist, int checkOri, const FrustumIn* fin = nullptr, const DevIn* dev = nullptr,
+            const float* right_uv = nullptr) {
     if (!frame_ok(F) || !mvp || nq < 0 || (nq > 0 && !queries && !fin)) return ORBFE_E_ARG;
     if (fin && (!fin->cam || (nq > 0 && !fin->pts) || mode != 0)) return ORBFE_E_ARG;
     if (mode != 2 && !mvp_obs) return ORBFE_E_ARG;
+    const bool two = F->two_cams != 0;
+    // two-camera frames: the local-map search takes the snapshot's right-view fields (no device
+    // isInFrustum for the fisheye model), the last-frame search needs the right projections
+    if (two && (fin || (mode == 1 && nq > 0 && !right_uv))) return ORBFE_E_ARG;
+    if (two && !dev && !links_ok(F)) return ORBFE_E_ARG;
+    // slot writes per query, in the reference's order (entry index = W q + b)
+    const int W = !two ? 1 : mode == 0 ? 4 : mode == 1 ? 2 : 1;
     if (fin && fin->n_to_match) *fin->n_to_match = 0;
     if (F->n == 0 || nq == 0) return 0;
     if (nq > (1 << 24)) return ORBFE_E_CAPACITY;
@@ -996,6 +1219,12 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
                                     : ((const orbfe_proj_point*)rec)->valid != 0;
         const int lvl = *(const int32_t*)(rec + qlevel_off);
         if (used && (lvl < 0 || lvl >= F->nlevels)) return ORBFE_E_ARG;
+        if (two && mode == 0) {
+            const orbfe_map_point* m = (const orbfe_map_point*)rec;
+            if ((m->flags & ORBFE_MP_IN_VIEW_R) && m->scale_level_r != -1 &&
+                (m->scale_level_r < 0 || m->scale_level_r >= F->nlevels))
+                return ORBFE_E_ARG;
+        }
     }
     std::vector<int32_t> blocked0(dev ? 0 : n);
     for (int k = 0; !dev && k < n; k++) blocked0[k] = mode == 2 ? (mvp[k] >= 0) : (mvp[k] >= 0 && mvp_obs[k] > 0);
@@ -1011,8 +1240,13 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     fp.plan_grid(p, mode == 0 ? F->nlevels + 1 : 1);
     const size_t o_track = fin ? p.scratch((size_t)nq * sizeof(orbfe_map_point)) : 0;
     const size_t o_ntm = fin ? p.scratch(16) : 0;
+    const size_t o_ruv = (two && mode == 1 && !dev) ? p.upload(right_uv, (size_t)nq * 8) : 0;
     const size_t o_first = p.scratch((size_t)n * 4);
-    const size_t o_assign = p.scratch((size_t)nq * 4);
+    const size_t o_assign = p.scratch((size_t)nq * W * 4);
+    const bool buckets = two && mode == 0;
+    const size_t o_soff = buckets ? p.scratch((size_t)(n + 1) * 4) : 0;
+    const size_t o_scur = buckets ? p.scratch((size_t)n * 4) : 0;
+    const size_t o_slst = buckets ? p.scratch((size_t)nq * W * 4) : 0;
     const size_t o_changed = p.scratch(MT_MAX_PASSES * 4);
     const size_t o_result = p.scratch((size_t)(n + 2) * 4);
     const size_t o_hist = p.scratch(MT_HISTO * 4);
@@ -1037,7 +1271,8 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     int* assign = ms_ptr<int>(o_assign);
     int* changed = ms_ptr<int>(o_changed);
     HIPCHK(hipMemsetAsync(changed, 0, MT_MAX_PASSES * 4, s));
-    fill(assign, nq, -1);
+    fill(assign, nq * W, -1);
+    const float2* ruv = (two && mode == 1) ? (dev ? (const float2*)right_uv : ms_ptr<const float2>(o_ruv)) : nullptr;
     const uint8_t* q = dev ? (const uint8_t*)(fin ? (const void*)fin->pts : queries) : ms_ptr<const uint8_t>(o_q);
     if (fin) {   // Tracking::SearchLocalPoints: project, count nToMatch, match only if > 0
         const orbfe_camera& c = *fin->cam;
@@ -1069,10 +1304,27 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     while (true) {
         for (int c = 0; c < chunk; c++, pass++) {
             if (pass >= MT_MAX_PASSES) return ORBFE_E_CAPACITY;
+            const dim3 gw((nq * W + MT_NT - 1) / MT_NT);
+            if (two && mode == 0) {   // per-slot write buckets (unguarded partner writes)
+                int* cnt = first;   // n + 1 counters, then the scan's offsets / cursors / lists
+                int* off = ms_ptr<int>(o_soff);
+                int* cur = ms_ptr<int>(o_scur);
+                int* lst = ms_ptr<int>(o_slst);
+                HIPCHK(hipMemsetAsync(cnt, 0, (size_t)n * 4, s));
+                hipLaunchKernelGGL(k_slot_count, gw, dim3(MT_NT), 0, s, assign, nq * W, cnt);
+                hipLaunchKernelGGL(k_slot_scan, dim3(1), dim3(1024), 0, s, cnt, n, off, cur);
+                hipLaunchKernelGGL(k_slot_fill, gw, dim3(MT_NT), 0, s, assign, nq * W, cur, lst);
+                hipLaunchKernelGGL(k_sbp_local2, gq, dim3(MT_NT), 0, s, fr, (const orbfe_map_point*)q, nq, th, a0, thFar,
+                                   nnratio, b0, (const int*)off, (const int*)lst, assign, changed + pass);
+                continue;
+            }
             fill(first, n, MT_INF);
-            hipLaunchKernelGGL(k_mt_first_strided, gq, dim3(MT_NT), 0, s, assign, q + qobs_off, (int)qstride, nq,
-                               mode == 2 ? 0 : 1, first);
-            if (mode == 0 && th >= MT_WAVE_TH) {
+            hipLaunchKernelGGL(k_mt_first_strided, gw, dim3(MT_NT), 0, s, assign, q + qobs_off, (int)qstride, nq * W,
+                               mode == 2 ? 0 : 1, first, W);
+            if (two && mode == 1) {
+                hipLaunchKernelGGL(k_sbp_proj2, gq, dim3(MT_NT), 0, s, fr, (const orbfe_proj_point*)q, ruv, nq, th, a0,
+                                   a1, b0, first, assign, changed + pass);
+            } else if (mode == 0 && th >= MT_WAVE_TH) {
                 const int nb = std::min((nq + MT_WNT / 64 - 1) / (MT_WNT / 64), 512);
                 const size_t lds = (MT_WNT / 64) * 64 * sizeof(int2) + (staged ? (size_t)n * 48 : 0);
                 if (staged)
@@ -1098,13 +1350,14 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     int* hist = ms_ptr<int>(o_hist);
     HIPCHK(hipMemsetAsync(hist, 0, MT_HISTO * 4, s));
     HIPCHK(hipMemsetAsync(result, 0, 8, s));
-    hipLaunchKernelGGL(k_mt_commit_count, gq, dim3(MT_NT), 0, s, fr.keys, assign, (const float*)(q + qangle_off),
-                       (int)qstride, nq, checkOri, result, hist);
+    const dim3 ge((nq * W + MT_NT - 1) / MT_NT);
+    hipLaunchKernelGGL(k_mt_commit_count, ge, dim3(MT_NT), 0, s, fr.keys, assign, (const float*)(q + qangle_off),
+                       (int)qstride, nq * W, checkOri, result, hist, W);
     if (checkOri)
-        hipLaunchKernelGGL(k_mt_commit_drop, gq, dim3(MT_NT), 0, s, fr.keys, assign, (const float*)(q + qangle_off),
-                           (int)qstride, nq, hist, result);
+        hipLaunchKernelGGL(k_mt_commit_drop, ge, dim3(MT_NT), 0, s, fr.keys, assign, (const float*)(q + qangle_off),
+                           (int)qstride, nq * W, hist, result, W);
     hipLaunchKernelGGL(k_mt_commit_write, dim3((n + 255) / 256), dim3(256), 0, s, n, (const int*)(q + qid_off),
-                       (int)qstride, result, mvp_d);
+                       (int)qstride, result, mvp_d, W);
     HIPCHK(hipGetLastError());
     timer.end();
     int cnt[2] = {0, 0};
@@ -1125,6 +1378,14 @@ int orbfe_search_by_projection_local(const orbfe_frame* F, int32_t* mvp, const i
                    offsetof(orbfe_map_point, id), 0, offsetof(orbfe_map_point, scale_level), th, bFarPoints, 0, thFarPoints, nnratio, 0, 0);
 }
 
+int orbfe_search_by_projection_lastframe_stereo(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_obs,
+                                                const orbfe_proj_point* pts, const float* right_uv, int32_t n_pts,
+                                                float th, int32_t bForward, int32_t bBackward, int32_t checkOri) {
+    return sbp_run(1, cur, mvp, mvp_obs, pts, n_pts, sizeof(orbfe_proj_point), offsetof(orbfe_proj_point, observations),
+                   offsetof(orbfe_proj_point, id), offsetof(orbfe_proj_point, angle), offsetof(orbfe_proj_point, octave),
+                   th, bForward, bBackward, 0.f, 0.f, MT_TH_HIGH, checkOri, nullptr, nullptr, right_uv);
+}
+
 int orbfe_search_by_projection_lastframe(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_obs,
                                          const orbfe_proj_point* pts, int32_t n_pts, float th, int32_t bForward,
                                          int32_t bBackward, int32_t checkOri) {
@@ -1142,7 +1403,7 @@ int orbfe_search_by_projection_kf(const orbfe_frame* cur, int32_t* mvp, const or
 
 int orbfe_search_for_initialization(const orbfe_frame* F1, const orbfe_frame* F2, float* prev_matched,
                                     int32_t* matches12, int32_t windowSize, float nnratio, int32_t checkOri) {
-    if (!frame_ok(F1) || !frame_ok(F2) || !prev_matched || !matches12) return ORBFE_E_ARG;
+    if (!frame1_ok(F1) || !frame1_ok(F2) || !prev_matched || !matches12) return ORBFE_E_ARG;
     const int n1 = F1->n;
     if (n1 == 0) return 0;
     if (F2->n == 0) {
@@ -1209,6 +1470,7 @@ int orbfe_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, c
                         int32_t* out, float nnratio, int32_t checkOri) {
     if (!F || F->n < 0 || kf_n < 0 || !kf_fv || !f_fv || !out || (kf_n > 0 && (!kf_keys || !kf_desc || !kf_mp)))
         return ORBFE_E_ARG;
+    if (F->two_cams && (F->nleft < 0 || F->nleft > F->n)) return ORBFE_E_ARG;
     const int fn = F->n;
     for (int i = 0; i < fn; i++) out[i] = -1;
     if (fn == 0 || kf_n == 0 || kf_fv->n_nodes <= 0 || f_fv->n_nodes <= 0) return 0;
@@ -1261,7 +1523,7 @@ int orbfe_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, c
     hipLaunchKernelGGL(k_bow_nodes, dim3((npairs + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, ms_ptr<const int>(o_pairs),
                        npairs, ms_ptr<const int>(o_kfoff), ms_ptr<const uint32_t>(o_kfidx), ms_ptr<const int>(o_foff),
                        ms_ptr<const uint32_t>(o_fidx), ms_ptr<const int32_t>(o_kfmp), ms_ptr<const uint32_t>(o_kfdesc),
-                       ms_ptr<const uint32_t>(o_fdesc), nnratio, ms_ptr<int>(o_src));
+                       ms_ptr<const uint32_t>(o_fdesc), nnratio, F->two_cams ? F->nleft : -1, ms_ptr<int>(o_src));
     hipLaunchKernelGGL(k_bow_commit, dim3(1), dim3(1024), 0, s, ms_ptr<const OrbKeyPoint>(o_kfkeys),
                        ms_ptr<const OrbKeyPoint>(o_fkeys), fn, ms_ptr<const int32_t>(o_kfmp), checkOri,
                        ms_ptr<const int>(o_src), ms_ptr<int>(o_out), ms_ptr<int>(o_result));

@@ -21,7 +21,8 @@ from .extractor import KEYPOINT_DTYPE
 # orbfe_map_point (80 B): MapPoint tracking snapshot (MapPoint.h:172-180)
 MAP_POINT_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"), ("view_cos", "<f4"),
                             ("depth", "<f4"), ("scale_level", "<i4"), ("flags", "<i4"), ("observations", "<i4"),
-                            ("id", "<i4"), ("reserved", "<i4", (3,)), ("desc", "u1", (32,))])
+                            ("id", "<i4"), ("proj_yr", "<f4"), ("view_cos_r", "<f4"), ("scale_level_r", "<i4"),
+                            ("desc", "u1", (32,))])
 # orbfe_proj_point (64 B): a projected point of the last frame / a keyframe
 PROJ_POINT_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("invzc", "<f4"), ("octave", "<i4"), ("angle", "<f4"),
                              ("valid", "<i4"), ("observations", "<i4"), ("id", "<i4"), ("desc", "u1", (32,))])
@@ -30,7 +31,7 @@ MAP_POINT_3D_DTYPE = np.dtype([("pos", "<f4", (3,)), ("normal", "<f4", (3,)), ("
                                ("flags", "<i4"), ("observations", "<i4"), ("id", "<i4"), ("reserved", "<i4"),
                                ("desc", "u1", (32,))])
 assert MAP_POINT_DTYPE.itemsize == 80 and PROJ_POINT_DTYPE.itemsize == 64 and MAP_POINT_3D_DTYPE.itemsize == 80
-MP_IN_VIEW, MP_BAD, MP_SKIP = 1, 2, 4
+MP_IN_VIEW, MP_BAD, MP_SKIP, MP_IN_VIEW_R = 1, 2, 4, 8
 TH_HIGH, TH_LOW, HISTO_LENGTH = 100, 50, 30   # ORBmatcher.cc:33-35
 
 
@@ -39,7 +40,8 @@ class CFrame(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int32), ("keys", ctypes.c_void_p), ("desc", ctypes.c_void_p),
                 ("uright", ctypes.c_void_p), ("min_x", ctypes.c_float), ("max_x", ctypes.c_float),
                 ("min_y", ctypes.c_float), ("max_y", ctypes.c_float), ("nlevels", ctypes.c_int32),
-                ("scale_factors", ctypes.c_void_p), ("mbf", ctypes.c_float)]
+                ("scale_factors", ctypes.c_void_p), ("mbf", ctypes.c_float), ("two_cams", ctypes.c_int32),
+                ("nleft", ctypes.c_int32), ("l2r", ctypes.c_void_p), ("r2l", ctypes.c_void_p)]
 
 
 class CFeatureVector(ctypes.Structure):
@@ -166,9 +168,12 @@ class KFCamera(ctypes.Structure):
 
 class MatchFrame:
     """The parts of a Frame the matchers read (Frame.h). keys: KEYPOINT_DTYPE [n] (mvKeysUn),
-    desc: uint8 [n, 32], bounds: (mnMinX, mnMaxX, mnMinY, mnMaxY), uright: float32 [n] or None."""
+    desc: uint8 [n, 32], bounds: (mnMinX, mnMaxX, mnMinY, mnMaxY), uright: float32 [n] or None.
+    Two-camera frame (Nleft != -1): nleft given, keys / desc = mvKeys ++ mvKeysRight, l2r / r2l =
+    mvLeftToRightMatch [nleft] / mvRightToLeftMatch [n - nleft] (int32, -1 = none)."""
 
-    def __init__(self, keys, desc, bounds, scale_factors, uright=None, mbf: float = 0.0):
+    def __init__(self, keys, desc, bounds, scale_factors, uright=None, mbf: float = 0.0, nleft=None, l2r=None,
+                 r2l=None):
         self.keys = np.ascontiguousarray(keys, KEYPOINT_DTYPE).reshape(-1)
         self.desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
         if len(self.keys) != len(self.desc):
@@ -179,9 +184,24 @@ class MatchFrame:
         self.scale_factors = np.ascontiguousarray(scale_factors, np.float32).reshape(-1)
         self.bounds = tuple(float(np.float32(b)) for b in bounds)
         self.mbf = float(mbf)
+        self.nleft = None if nleft is None else int(nleft)
+        if self.nleft is not None:
+            n = len(self.keys)
+            if not 0 <= self.nleft <= n:
+                raise ValueError("nleft out of range")
+            self.l2r = np.ascontiguousarray(np.full(self.nleft, -1) if l2r is None else l2r, np.int32).reshape(-1)
+            self.r2l = np.ascontiguousarray(np.full(n - self.nleft, -1) if r2l is None else r2l, np.int32).reshape(-1)
+            if len(self.l2r) != self.nleft or len(self.r2l) != n - self.nleft:
+                raise ValueError("l2r / r2l lengths must be nleft / n - nleft")
+            # an empty side still needs a valid pointer
+            self._l2r_buf = self.l2r if len(self.l2r) else np.zeros(1, np.int32)
+            self._r2l_buf = self.r2l if len(self.r2l) else np.zeros(1, np.int32)
         self.c = CFrame(len(self.keys), self.keys.ctypes.data, self.desc.ctypes.data,
                         self.uright.ctypes.data if self.uright is not None else None, *self.bounds,
-                        len(self.scale_factors), self.scale_factors.ctypes.data, self.mbf)
+                        len(self.scale_factors), self.scale_factors.ctypes.data, self.mbf,
+                        1 if self.nleft is not None else 0, self.nleft or 0,
+                        self._l2r_buf.ctypes.data if self.nleft is not None else None,
+                        self._r2l_buf.ctypes.data if self.nleft is not None else None)
 
     @property
     def N(self) -> int:
@@ -257,6 +277,20 @@ class ORBmatcher:
         return _lib.check(self._lib.orbfe_search_by_projection_lastframe(
             cur.ref(), mvp.ctypes.data, mvp_obs.ctypes.data, pts.ctypes.data, len(pts), float(th), int(bForward),
             int(bBackward), int(self.mbCheckOrientation)), "SearchByProjection(last frame)")
+
+    # the same for a two-camera CurrentFrame (:1794-1858): right_uv float32 [n, 2] = the points
+    # projected into the right camera by the caller's camera model
+    def SearchByProjectionLastFrameStereo(self, cur: MatchFrame, mvp, mvp_obs, points, right_uv, th: float,
+                                          bForward: bool, bBackward: bool) -> int:
+        mvp = _i32(mvp, cur.N, "mvp")
+        mvp_obs = _i32(mvp_obs, cur.N, "mvp_obs")
+        pts = _records(points, PROJ_POINT_DTYPE, "points")
+        ruv = np.asarray(right_uv)
+        if ruv.dtype != np.float32 or not ruv.flags.c_contiguous or ruv.shape != (len(pts), 2):
+            raise ValueError("right_uv must be contiguous float32 [n_points, 2]")
+        return _lib.check(self._lib.orbfe_search_by_projection_lastframe_stereo(
+            cur.ref(), mvp.ctypes.data, mvp_obs.ctypes.data, pts.ctypes.data, ruv.ctypes.data, len(pts), float(th),
+            int(bForward), int(bBackward), int(self.mbCheckOrientation)), "SearchByProjection(last frame, stereo)")
 
     # SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist) (:1889-2010)
     def SearchByProjectionKeyFrame(self, cur: MatchFrame, mvp, points, th: float, ORBdist: int) -> int:
@@ -404,9 +438,15 @@ class DeviceMatchFrame:
         self.desc = torch.from_numpy(F.desc.copy()).to(device)
         self.uright = None if F.uright is None else torch.from_numpy(F.uright.copy()).to(device)
         self.scale_factors = torch.from_numpy(F.scale_factors.copy()).to(device)
+        two = getattr(F, "nleft", None) is not None
+        if two:   # mvLeftToRightMatch / mvRightToLeftMatch in HBM as well
+            self.l2r = torch.from_numpy(F._l2r_buf.copy()).to(device)
+            self.r2l = torch.from_numpy(F._r2l_buf.copy()).to(device)
         self.c = CFrame(F.N, self.keys.data_ptr(), self.desc.data_ptr(),
                         self.uright.data_ptr() if self.uright is not None else None, *F.bounds,
-                        len(F.scale_factors), self.scale_factors.data_ptr(), F.mbf)
+                        len(F.scale_factors), self.scale_factors.data_ptr(), F.mbf, 1 if two else 0,
+                        F.nleft if two else 0, self.l2r.data_ptr() if two else None,
+                        self.r2l.data_ptr() if two else None)
 
     def ref(self):
         return ctypes.byref(self.c)

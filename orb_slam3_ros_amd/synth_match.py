@@ -11,7 +11,7 @@ from __future__ import annotations
 import numpy as np
 
 from .extractor import KEYPOINT_DTYPE
-from .matcher import (MAP_POINT_3D_DTYPE, MAP_POINT_DTYPE, MP_BAD, MP_IN_VIEW, MP_SKIP, PROJ_POINT_DTYPE, Camera,
+from .matcher import (MAP_POINT_3D_DTYPE, MAP_POINT_DTYPE, MP_BAD, MP_IN_VIEW, MP_IN_VIEW_R, MP_SKIP, PROJ_POINT_DTYPE, Camera,
                       FeatureVector, KFCamera, MatchFrame, Pose)
 
 
@@ -385,3 +385,113 @@ def fundamental_12(cam1: KFCamera, cam2: KFCamera):
     C2 = R2 @ Cw + t2
     ep = np.array([cam2.fx * C2[0] / C2[2] + cam2.cx, cam2.fy * C2[1] / C2[2] + cam2.cy])
     return F12.astype(np.float32), ep.astype(np.float32)
+
+
+# ---- two-camera (KannalaBrandt8 stereo, Frame.Nleft != -1) workloads, config 4's tracking path ----
+def synth_frame_two(rng, nl: int, nr: int, w: int = 512, h: int = 512, nlevels: int = 8, stereo_frac: float = 0.5,
+                    flip_p: float = 0.04) -> MatchFrame:
+    """mvKeys (nl) ++ mvKeysRight (nr) on a w x h fisheye pair. A stereo_frac share of the left
+    features has a right partner (a noisy copy a few pixels to the left, same octave):
+    mvLeftToRightMatch / mvRightToLeftMatch link them both ways."""
+    L = synth_frame(rng, nl, w, h, nlevels, stereo=False)
+    R = synth_frame(rng, nr, w, h, nlevels, stereo=False)
+    keys = np.concatenate([L.keys, R.keys])
+    desc = np.concatenate([L.desc, R.desc])
+    l2r = np.full(nl, -1, np.int32)
+    r2l = np.full(nr, -1, np.int32)
+    npair = int(min(nl, nr) * stereo_frac)
+    if npair:
+        li = rng.choice(nl, npair, replace=False)
+        ri = rng.choice(nr, npair, replace=False)
+        l2r[li] = ri
+        r2l[ri] = li
+        k = keys[nl + ri]
+        k["x"] = np.clip(keys["x"][li] - rng.uniform(2, 40, npair), 0, w - 1).astype(np.float32)
+        k["y"] = np.clip(keys["y"][li] + rng.normal(0, 1.0, npair), 0, h - 1).astype(np.float32)
+        k["octave"] = keys["octave"][li]
+        k["angle"] = np.mod(keys["angle"][li] + rng.normal(0, 2.0, npair), 360.0).astype(np.float32)
+        keys[nl + ri] = k
+        desc[nl + ri] = flip_bits(rng, desc[li], flip_p)
+    return MatchFrame(keys, desc, L.bounds, L.scale_factors, None, L.mbf, nleft=nl, l2r=l2r, r2l=r2l)
+
+
+def synth_local_map_two(rng, F: MatchFrame, n_mps: int, copy_frac: float = 0.5, flip_p: float = 0.05,
+                        nlevels: int = 8) -> np.ndarray:
+    """Map points seen by a two-camera frame: left view fields as synth_local_map, plus
+    mbTrackInViewR / mTrackProjXR, YR / mTrackViewCosR / mnTrackScaleLevelR. Copies of a right
+    feature project next to it in the right camera (and next to its left partner, if any)."""
+    nl = F.nleft
+    m = synth_local_map(rng, F, n_mps, copy_frac=0.0, flip_p=flip_p, nlevels=nlevels)
+    w, h = F.bounds[1], F.bounds[3]
+    m["proj_xr"] = rng.uniform(0, w, n_mps)
+    m["proj_yr"] = rng.uniform(0, h, n_mps)
+    m["view_cos_r"] = rng.uniform(0.99, 1.0, n_mps)
+    m["scale_level_r"] = np.where(rng.random(n_mps) < 0.05, -1, rng.choice(nlevels, n_mps, p=level_weights(nlevels)))
+    fl = m["flags"].copy()
+    inr = rng.random(n_mps) < 0.8
+    fl = np.where(inr, fl | MP_IN_VIEW_R, fl)
+    fl = np.where(rng.random(n_mps) < 0.15, fl & ~MP_IN_VIEW, fl)   # seen by the right camera only
+    m["flags"] = fl.astype(np.int32)
+    if F.N:
+        cp = np.nonzero(rng.random(n_mps) < copy_frac)[0]
+        src = rng.integers(0, F.N, len(cp))
+        m["desc"][cp] = flip_bits(rng, F.desc[src], flip_p)
+        left = src < nl
+        # left source: left view near it, right view near its partner (or random)
+        li = cp[left]
+        ls = src[left]
+        m["proj_x"][li] = F.keys["x"][ls] + rng.normal(0, 1.5, len(li))
+        m["proj_y"][li] = F.keys["y"][ls] + rng.normal(0, 1.5, len(li))
+        m["scale_level"][li] = F.keys["octave"][ls]
+        part = F.l2r[ls]
+        hp = part >= 0
+        m["proj_xr"][li[hp]] = F.keys["x"][nl + part[hp]] + rng.normal(0, 1.5, int(hp.sum()))
+        m["proj_yr"][li[hp]] = F.keys["y"][nl + part[hp]] + rng.normal(0, 1.5, int(hp.sum()))
+        m["scale_level_r"][li[hp]] = F.keys["octave"][nl + part[hp]]
+        # right source: right view near it, left view near its partner (or random)
+        ri = cp[~left]
+        rs = src[~left]
+        m["proj_xr"][ri] = F.keys["x"][rs] + rng.normal(0, 1.5, len(ri))
+        m["proj_yr"][ri] = F.keys["y"][rs] + rng.normal(0, 1.5, len(ri))
+        m["scale_level_r"][ri] = F.keys["octave"][rs]
+        part = F.r2l[rs - nl]
+        hp = part >= 0
+        m["proj_x"][ri[hp]] = F.keys["x"][part[hp]] + rng.normal(0, 1.5, int(hp.sum()))
+        m["proj_y"][ri[hp]] = F.keys["y"][part[hp]] + rng.normal(0, 1.5, int(hp.sum()))
+        m["scale_level"][ri[hp]] = F.keys["octave"][part[hp]]
+    return m
+
+
+def synth_proj_points_two(rng, F: MatchFrame, n: int, copy_frac: float = 0.8, flip_p: float = 0.05,
+                          rot: float = 15.0):
+    """Last-frame points for a two-camera current frame: (records, right_uv [n, 2]). Copies of a
+    left feature land near it (and near its right partner in right_uv); the rest are random."""
+    nl = F.nleft
+    left = MatchFrame(F.keys[:nl], F.desc[:nl], F.bounds, F.scale_factors)
+    p = synth_proj_points(rng, left, n, copy_frac=0.0, flip_p=flip_p, rot=rot)
+    w, h = F.bounds[1], F.bounds[3]
+    ruv = np.stack([rng.uniform(-20, w + 20, n), rng.uniform(-20, h + 20, n)], 1).astype(np.float32)
+    if F.N:
+        cp = np.nonzero(rng.random(n) < copy_frac)[0]
+        src = rng.integers(0, F.N, len(cp))
+        p["desc"][cp] = flip_bits(rng, F.desc[src], flip_p)
+        lft = src < nl
+        ls, rs = src[lft], src[~lft]
+        lc, rc = cp[lft], cp[~lft]
+        p["u"][lc] = F.keys["x"][ls] + rng.normal(0, 2.0, len(lc))
+        p["v"][lc] = F.keys["y"][ls] + rng.normal(0, 2.0, len(lc))
+        part = F.l2r[ls]
+        hp = part >= 0
+        ruv[lc[hp], 0] = F.keys["x"][nl + part[hp]] + rng.normal(0, 2.0, int(hp.sum()))
+        ruv[lc[hp], 1] = F.keys["y"][nl + part[hp]] + rng.normal(0, 2.0, int(hp.sum()))
+        ruv[rc, 0] = F.keys["x"][rs] + rng.normal(0, 2.0, len(rc))
+        ruv[rc, 1] = F.keys["y"][rs] + rng.normal(0, 2.0, len(rc))
+        part = F.r2l[rs - nl]
+        hp = part >= 0
+        p["u"][rc[hp]] = F.keys["x"][part[hp]] + rng.normal(0, 2.0, int(hp.sum()))
+        p["v"][rc[hp]] = F.keys["y"][part[hp]] + rng.normal(0, 2.0, int(hp.sum()))
+        p["octave"][cp] = np.clip(F.keys["octave"][src] + rng.integers(-1, 2, len(cp)), 0, len(F.scale_factors) - 1)
+        outl = rng.random(len(cp)) < 0.15
+        p["angle"][cp] = np.mod(np.where(outl, rng.uniform(0, 360, len(cp)),
+                                         F.keys["angle"][src] + rot + rng.normal(0, 4, len(cp))), 360.0)
+    return p, ruv

@@ -9,6 +9,7 @@
 #include <cassert>
 #include <cstring>
 #include <stdexcept>
+#include <string>
 
 #include <orbfe.h>
 
@@ -16,6 +17,11 @@ using namespace cv;
 using namespace std;
 
 namespace ORB_SLAM3 {
+
+// Defined by shim/ORBmatcher_orbfe.cc next to the ComputeStereoMatches replacement: the only
+// reader of mvImagePyramid in the reference (Frame.cc:818-923), which this file no longer fills.
+// Replacing ORBextractor.cc without that rerouting is a link error, not a silent wrong read.
+extern const int kOrbfeStereoRerouted;
 
 static_assert(sizeof(cv::KeyPoint) == sizeof(orbfe_keypoint), "cv::KeyPoint layout (28 B) expected");
 
@@ -28,6 +34,7 @@ ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int
     if (orbfe_extractor_create(nfeatures, _scaleFactor, nlevels, iniThFAST, minThFAST, &h) != ORBFE_OK)
         throw std::runtime_error("orbfe_extractor_create failed (no HIP device?)");
     mpOrbfe = h;
+    if (kOrbfeStereoRerouted != 1) throw std::logic_error("ComputeStereoMatches is not routed to orbfe_stereo_match");
     mvScaleFactor.resize(nlevels);
     mvInvScaleFactor.resize(nlevels);
     mvLevelSigma2.resize(nlevels);
@@ -56,7 +63,8 @@ int ORBextractor::operator()(InputArray _image, InputArray _mask, vector<KeyPoin
                                         vLappingArea[1], reinterpret_cast<orbfe_keypoint*>(_keypoints.data()),
                                         desc.data, cap, &n);
     if (monoIndex == ORBFE_E_EMPTY) { _keypoints.clear(); return -1; }
-    if (monoIndex < 0) throw std::runtime_error("orbfe_extract failed");
+    if (monoIndex < 0)   // device error or a capacity limit: no CPU extractor is linked to fall back to
+        throw std::runtime_error("orbfe_extract failed with code " + std::to_string(monoIndex));
     _keypoints.resize(n);
     if (n == 0) {
         _descriptors.release();
@@ -65,7 +73,8 @@ int ORBextractor::operator()(InputArray _image, InputArray _mask, vector<KeyPoin
         desc.rowRange(0, n).copyTo(_descriptors.getMat());
     }
     // mvImagePyramid is read only by Frame::ComputeStereoMatches, which the Frame shim routes to
-    // orbfe_stereo_match; call MaterialisePyramid() when host levels are needed elsewhere.
+    // orbfe_stereo_match (kOrbfeStereoRerouted above makes that a link-time requirement); call
+    // MaterialisePyramid() when host levels are needed elsewhere (the CPU stereo fallback does).
     mvImagePyramid.clear();
     return monoIndex;
 }

@@ -1,11 +1,14 @@
 // Replacement bodies for the LocalMapping / LoopClosing ORBmatcher methods
 // (orb_slam3/src/ORBmatcher.cc:427-646, 765-1674) and MapPoint::ComputeDistinctiveDescriptors
 // (MapPoint.cc:329-403) on top of liborbfe.so. Pinhole keyframes only: a keyframe
-// with a second camera (mpCamera2) keeps the original body, renamed *_cpu.
+// with a second camera (mpCamera2) keeps the original body, renamed *_cpu, which also runs (after
+// one logged line) whenever the library returns an error.
 // Built inside the ORB-SLAM3 tree; NOT compiled in this repository's container (no OpenCV /
 // Eigen / Sophus here). See INTEGRATION.md §4.
 #include "ORBmatcher.h"
 
+#include <atomic>
+#include <cstdio>
 #include <cstring>
 #include <unordered_map>
 
@@ -35,8 +38,17 @@ struct Handles {   // MapPoint* <-> int32 (see ORBmatcher_orbfe.cc)
     MapPoint* at(int32_t h) const { return h < 0 ? nullptr : table[h]; }
 };
 
+bool failed(int rc, const char* what) {   // see ORBmatcher_orbfe.cc
+    if (rc >= 0) return false;
+    static std::atomic<int> logged{0};
+    if (logged.fetch_add(1) < 16)
+        fprintf(stderr, "[orbfe] %s returned %d; running the CPU implementation\n", what, rc);
+    return true;
+}
+
 orbfe_frame kf_view(KeyFrame* K) {
     orbfe_frame f;
+    memset(&f, 0, sizeof(f));   // two_cams = 0: single-camera keyframe
     f.n = K->N;
     f.keys = reinterpret_cast<const orbfe_keypoint*>(K->mvKeysUn.data());
     f.desc = K->mDescriptors.data;
@@ -126,6 +138,7 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& v
                                          reinterpret_cast<const orbfe_keypoint*>(pKF2->mvKeysUn.data()),
                                          pKF2->mDescriptors.data, m2.data(), pKF2->N, &f2.v, out.data(), mfNNratio,
                                          mbCheckOrientation);
+    if (failed(n, "orbfe_search_by_bow_kf")) return SearchByBoW_cpu(pKF1, pKF2, vpMatches12);
     vpMatches12.assign(v1.size(), static_cast<MapPoint*>(nullptr));
     for (size_t i = 0; i < v1.size(); i++) vpMatches12[i] = H.at(out[i]);
     return n;
@@ -156,6 +169,8 @@ int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, vector<pa
     const int n = orbfe_search_for_triangulation(&k1, m1.data(), &f1.v, &k2, m2.data(), &f2.v, F12, epv,
                                                  pKF2->mvLevelSigma2.data(), bOnlyStereo, bCoarse,
                                                  mbCheckOrientation, out.data());
+    if (failed(n, "orbfe_search_for_triangulation"))
+        return SearchForTriangulation_cpu(pKF1, pKF2, vMatchedPairs, bOnlyStereo, bCoarse);
     vMatchedPairs.clear();
     vMatchedPairs.reserve(n);
     for (int i = 0; i < pKF1->N; i++)
@@ -237,6 +252,8 @@ int ORBmatcher::SearchByProjection(KeyFrame* pKF, Sophus::Sim3f& Scw, const vect
     const orbfe_frame kf = kf_view(pKF);
     const int n = orbfe_search_by_projection_sim3(&kf, &cam, q.data(), (int)q.size(), nullptr, th, ratioHamming,
                                                   m.data(), nullptr);
+    if (failed(n, "orbfe_search_by_projection_sim3"))
+        return SearchByProjection_cpu(pKF, Scw, vpPoints, vpMatched, th, ratioHamming);
     for (size_t k = 0; k < vpMatched.size(); k++) vpMatched[k] = H.at(m[k]);
     return n;
 }
@@ -260,6 +277,7 @@ int ORBmatcher::SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& 
     const orbfe_frame k1 = kf_view(pKF1), k2 = kf_view(pKF2);
     const int n = orbfe_search_by_sim3(&k1, &k2, p1.data(), p2.data(), &c1, &c2, &s12, &s21, th, m12.data(),
                                        idx2.data());
+    if (failed(n, "orbfe_search_by_sim3")) return SearchBySim3_cpu(pKF1, pKF2, vpMatches12, S12, th);
     for (size_t i = 0; i < v1.size(); i++) vpMatches12[i] = H.at(m12[i]);
     return n;
 }
@@ -287,7 +305,11 @@ void ComputeDistinctiveDescriptorsBatch(const vector<MapPoint*>& points) {
         off.push_back((int32_t)(desc.size() / 32));
     }
     vector<int32_t> best(points.size());
-    orbfe_distinctive_descriptors(desc.data(), off.data(), (int)points.size(), best.data());
+    if (failed(orbfe_distinctive_descriptors(desc.data(), off.data(), (int)points.size(), best.data()),
+               "orbfe_distinctive_descriptors")) {
+        for (MapPoint* p : points) p->ComputeDistinctiveDescriptors();
+        return;
+    }
     for (size_t p = 0; p < points.size(); p++)
         if (best[p] >= 0) points[p]->SetDescriptor(&desc[32 * ((size_t)off[p] + best[p])]);   // under mMutexFeatures
 }

@@ -1,12 +1,17 @@
 // Replacement bodies for the Tracking-thread ORBmatcher methods (orb_slam3/src/ORBmatcher.cc)
-// and Frame::ComputeStereoMatches (Frame.cc:811-981) on top of liborbfe.so. The original
-// bodies of these methods are removed from ORBmatcher.cc / Frame.cc; every other method
-// (SearchForTriangulation, Fuse, SearchBySim3, ...) keeps its CPU code. The KannalaBrandt8
-// branches (F.Nleft != -1) keep the original code, renamed *_cpu.
+// and Frame::ComputeStereoMatches (Frame.cc:811-981) on top of liborbfe.so. The original bodies
+// of the replaced methods stay in ORBmatcher.cc / Frame.cc renamed *_cpu: every replacement checks
+// the library's return code and, on an error (no device, a capacity or argument limit), logs the
+// reason once and runs the *_cpu body instead, so a failure never reaches Tracking as a negative
+// nmatches or a silently monocular frame. Both camera layouts are handled on the device: Nleft ==
+// -1 frames and the KannalaBrandt8 two-camera frames (Nleft != -1: keys mvKeys ++ mvKeysRight,
+// mvLeftToRightMatch / mvRightToLeftMatch).
 // Built inside the ORB-SLAM3 tree; NOT compiled in this repository's container (no OpenCV /
 // Eigen / Sophus here). See INTEGRATION.md.
 #include "ORBmatcher.h"
 
+#include <atomic>
+#include <cstdio>
 #include <cstring>
 #include <unordered_map>
 
@@ -19,6 +24,11 @@
 using namespace std;
 
 namespace ORB_SLAM3 {
+
+// Defined here, referenced by shim/ORBextractor_orbfe.cc: an ORBextractor.cc replaced without this
+// file (and the ComputeStereoMatches body below) fails to link instead of leaving Frame.cc reading
+// the mvImagePyramid the shim no longer fills.
+extern const int kOrbfeStereoRerouted = 1;
 
 namespace {
 
@@ -38,11 +48,35 @@ struct Handles {
     MapPoint* at(int32_t h) const { return h < 0 ? nullptr : table[h]; }
 };
 
-// Frame fields the matchers read (Frame.h); mvKeysUn and mDescriptors stay borrowed.
-orbfe_frame frame_view(const Frame& F) {
+// One log line per call site and error code; the caller then runs the CPU body.
+bool failed(int rc, const char* what) {
+    if (rc >= 0) return false;
+    static std::atomic<int> logged{0};
+    if (logged.fetch_add(1) < 16)
+        fprintf(stderr, "[orbfe] %s returned %d (%s); running the CPU implementation\n", what, rc,
+                rc == ORBFE_E_ARG ? "argument / capacity limit" : rc == ORBFE_E_DEVICE ? "HIP device error"
+                : rc == ORBFE_E_CAPACITY ? "capacity" : "error");
+    return true;
+}
+
+// Frame fields the matchers read (Frame.h). Single camera: mvKeysUn and mDescriptors borrowed.
+// Two cameras (Nleft != -1): keys = mvKeys ++ mvKeysRight (AssignFeaturesToGrid's keypoints,
+// Frame.cc:401-403) in `keys`, the stereo links borrowed.
+orbfe_frame frame_view(const Frame& F, vector<cv::KeyPoint>& keys) {
     orbfe_frame f;
+    memset(&f, 0, sizeof(f));
     f.n = F.N;
-    f.keys = reinterpret_cast<const orbfe_keypoint*>(F.mvKeysUn.data());
+    if (F.Nleft == -1) {
+        f.keys = reinterpret_cast<const orbfe_keypoint*>(F.mvKeysUn.data());
+    } else {
+        keys.assign(F.mvKeys.begin(), F.mvKeys.end());
+        keys.insert(keys.end(), F.mvKeysRight.begin(), F.mvKeysRight.end());
+        f.keys = reinterpret_cast<const orbfe_keypoint*>(keys.data());
+        f.two_cams = 1;
+        f.nleft = F.Nleft;
+        f.l2r = F.mvLeftToRightMatch.data();
+        f.r2l = F.mvRightToLeftMatch.data();
+    }
     f.desc = F.mDescriptors.data;   // N x 32, continuous
     f.uright = F.mvuRight.empty() ? nullptr : F.mvuRight.data();
     f.min_x = Frame::mnMinX; f.max_x = Frame::mnMaxX; f.min_y = Frame::mnMinY; f.max_y = Frame::mnMaxY;
@@ -64,12 +98,16 @@ void slots_of(const Frame& F, Handles& H, vector<int32_t>& mvp, vector<int32_t>*
 
 void copy_desc(const cv::Mat& d, uint8_t out[32]) { memcpy(out, d.ptr<uint8_t>(0), 32); }
 
+// keypoint i of a frame / keyframe in the reference's side-aware lookup
+const cv::KeyPoint& key_of(const Frame& F, int i) {
+    return F.Nleft == -1 ? F.mvKeysUn[i] : i < F.Nleft ? F.mvKeys[i] : F.mvKeysRight[i - F.Nleft];
+}
+
 }  // namespace
 
 // ORBmatcher.cc:43-213
 int ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoints, const float th,
                                    const bool bFarPoints, const float thFarPoints) {
-    if (F.Nleft != -1) return SearchByProjection_cpu(F, vpMapPoints, th, bFarPoints, thFarPoints);
     Handles H;
     vector<int32_t> mvp, obs;
     slots_of(F, H, mvp, &obs);
@@ -81,30 +119,40 @@ int ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoint
         r.proj_x = p->mTrackProjX; r.proj_y = p->mTrackProjY; r.proj_xr = p->mTrackProjXR;
         r.view_cos = p->mTrackViewCos; r.depth = p->mTrackDepth; r.scale_level = p->mnTrackScaleLevel;
         r.flags = (p->mbTrackInView ? ORBFE_MP_IN_VIEW : 0) | (p->isBad() ? ORBFE_MP_BAD : 0);
+        if (F.Nleft != -1) {
+            r.flags |= p->mbTrackInViewR ? ORBFE_MP_IN_VIEW_R : 0;
+            r.proj_yr = p->mTrackProjYR;
+            r.view_cos_r = p->mTrackViewCosR;
+            r.scale_level_r = p->mnTrackScaleLevelR;
+        }
         r.observations = p->Observations();
         r.id = H.of(p);
-        if (r.flags == ORBFE_MP_IN_VIEW) copy_desc(p->GetDescriptor(), r.desc);
+        if ((r.flags & (ORBFE_MP_IN_VIEW | ORBFE_MP_IN_VIEW_R)) && !(r.flags & ORBFE_MP_BAD))
+            copy_desc(p->GetDescriptor(), r.desc);
     }
-    const orbfe_frame fr = frame_view(F);
+    vector<cv::KeyPoint> keys;
+    const orbfe_frame fr = frame_view(F, keys);
     const int n = orbfe_search_by_projection_local(&fr, mvp.data(), obs.data(), q.data(), (int)q.size(),
                                                    th, bFarPoints, thFarPoints, mfNNratio);
+    if (failed(n, "orbfe_search_by_projection_local"))
+        return SearchByProjection_cpu(F, vpMapPoints, th, bFarPoints, thFarPoints);
     for (int i = 0; i < F.N; i++) F.mvpMapPoints[i] = H.at(mvp[i]);
     return n;
 }
 
 // ORBmatcher.cc:1676-1887 (projection with Tcw stays on the host, as in the reference)
 int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, const float th, const bool bMono) {
-    if (CurrentFrame.Nleft != -1 || LastFrame.Nleft != -1)
-        return SearchByProjection_cpu(CurrentFrame, LastFrame, th, bMono);
     const Sophus::SE3f Tcw = CurrentFrame.GetPose();
     const Eigen::Vector3f twc = Tcw.inverse().translation();
     const Eigen::Vector3f tlc = LastFrame.GetPose() * twc;
     const bool bForward = tlc(2) > CurrentFrame.mb && !bMono;
     const bool bBackward = -tlc(2) > CurrentFrame.mb && !bMono;
+    const bool two = CurrentFrame.Nleft != -1;
     Handles H;
     vector<int32_t> mvp, obs;
     slots_of(CurrentFrame, H, mvp, &obs);
     vector<orbfe_proj_point> q(LastFrame.N);
+    vector<float> ruv(two ? 2 * (size_t)LastFrame.N : 0, 0.f);
     for (int i = 0; i < LastFrame.N; i++) {
         orbfe_proj_point& r = q[i];
         memset(&r, 0, sizeof(r));
@@ -114,21 +162,33 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, 
         r.invzc = 1.0 / x3Dc(2);
         const Eigen::Vector2f uv = CurrentFrame.mpCamera->project(x3Dc);
         r.u = uv(0); r.v = uv(1);
-        r.octave = LastFrame.mvKeys[i].octave;
-        r.angle = LastFrame.mvKeysUn[i].angle;
+        // nLastOctave and kpLF (:1721-1722, :1765-1767)
+        r.octave = (LastFrame.Nleft == -1 || i < LastFrame.Nleft) ? LastFrame.mvKeys[i].octave
+                                                                   : LastFrame.mvKeysRight[i - LastFrame.Nleft].octave;
+        r.angle = key_of(LastFrame, i).angle;
         r.valid = 1;
         r.observations = p->Observations();
         r.id = H.of(p);
         copy_desc(p->GetDescriptor(), r.desc);
+        if (two && !(r.invzc < 0)) {   // :1795-1796: the reference projects with mpCamera here too
+            const Eigen::Vector3f x3Dr = CurrentFrame.GetRelativePoseTrl() * x3Dc;
+            const Eigen::Vector2f uvr = CurrentFrame.mpCamera->project(x3Dr);
+            ruv[2 * i] = uvr(0);
+            ruv[2 * i + 1] = uvr(1);
+        }
     }
-    const orbfe_frame fr = frame_view(CurrentFrame);
-    const int n = orbfe_search_by_projection_lastframe(&fr, mvp.data(), obs.data(), q.data(),
-                                                       (int)q.size(), th, bForward, bBackward, mbCheckOrientation);
+    vector<cv::KeyPoint> keys;
+    const orbfe_frame fr = frame_view(CurrentFrame, keys);
+    const int n = orbfe_search_by_projection_lastframe_stereo(&fr, mvp.data(), obs.data(), q.data(),
+                                                              two ? ruv.data() : nullptr, (int)q.size(), th,
+                                                              bForward, bBackward, mbCheckOrientation);
+    if (failed(n, "orbfe_search_by_projection_lastframe_stereo"))
+        return SearchByProjection_cpu(CurrentFrame, LastFrame, th, bMono);
     for (int i = 0; i < CurrentFrame.N; i++) CurrentFrame.mvpMapPoints[i] = H.at(mvp[i]);
     return n;
 }
 
-// ORBmatcher.cc:1889-2010
+// ORBmatcher.cc:1889-2010 (no right-camera branch: the left grid of a two-camera frame)
 int ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>& sAlreadyFound,
                                    const float th, const int ORBdist) {
     const Sophus::SE3f Tcw = CurrentFrame.GetPose();
@@ -157,33 +217,48 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set
         r.id = H.of(p);
         copy_desc(p->GetDescriptor(), r.desc);
     }
-    const orbfe_frame fr = frame_view(CurrentFrame);
+    vector<cv::KeyPoint> keys;
+    const orbfe_frame fr = frame_view(CurrentFrame, keys);
     const int n = orbfe_search_by_projection_kf(&fr, mvp.data(), q.data(), (int)q.size(), th,
                                                 ORBdist, mbCheckOrientation);
+    if (failed(n, "orbfe_search_by_projection_kf"))
+        return SearchByProjection_cpu(CurrentFrame, pKF, sAlreadyFound, th, ORBdist);
     for (int i = 0; i < CurrentFrame.N; i++) CurrentFrame.mvpMapPoints[i] = H.at(mvp[i]);
     return n;
 }
 
-// ORBmatcher.cc:648-763
+// ORBmatcher.cc:648-763 (monocular initialisation: single-camera frames)
 int ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, vector<cv::Point2f>& vbPrevMatched,
                                         vector<int>& vnMatches12, int windowSize) {
-    vnMatches12.assign(F1.mvKeysUn.size(), -1);
     static_assert(sizeof(cv::Point2f) == 8, "Point2f layout");
-    const orbfe_frame f1 = frame_view(F1), f2 = frame_view(F2);
-    return orbfe_search_for_initialization(&f1, &f2,
-                                           reinterpret_cast<float*>(vbPrevMatched.data()), vnMatches12.data(),
-                                           windowSize, mfNNratio, mbCheckOrientation);
+    vector<cv::KeyPoint> k1, k2;
+    const orbfe_frame f1 = frame_view(F1, k1), f2 = frame_view(F2, k2);
+    vector<cv::Point2f> prev(vbPrevMatched);
+    vector<int> m12(F1.mvKeysUn.size(), -1);
+    const int n = orbfe_search_for_initialization(&f1, &f2, reinterpret_cast<float*>(prev.data()), m12.data(),
+                                                  windowSize, mfNNratio, mbCheckOrientation);
+    if (failed(n, "orbfe_search_for_initialization"))
+        return SearchForInitialization_cpu(F1, F2, vbPrevMatched, vnMatches12, windowSize);
+    vbPrevMatched.swap(prev);
+    vnMatches12.swap(m12);
+    return n;
 }
 
-// ORBmatcher.cc:223-425 (pinhole path)
+// ORBmatcher.cc:223-425
 int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPointMatches) {
-    if (F.Nleft != -1) return SearchByBoW_cpu(pKF, F, vpMapPointMatches);
     const vector<MapPoint*> vpMapPointsKF = pKF->GetMapPointMatches();
     Handles H;
     vector<int32_t> kf_mp(vpMapPointsKF.size());
     for (size_t i = 0; i < vpMapPointsKF.size(); i++) {
         MapPoint* p = vpMapPointsKF[i];
         kf_mp[i] = (p && !p->isBad()) ? H.of(p) : -1;
+    }
+    // kp of the KF index (:327-329): mvKeysUn, or by side for a two-camera KF
+    vector<cv::KeyPoint> kf_keys;
+    if (pKF->mpCamera2) {
+        kf_keys.resize(vpMapPointsKF.size());
+        for (size_t i = 0; i < kf_keys.size(); i++)
+            kf_keys[i] = (int)i >= pKF->NLeft ? pKF->mvKeysRight[i - pKF->NLeft] : pKF->mvKeys[i];
     }
     auto flatten = [](const DBoW2::FeatureVector& fv, vector<uint32_t>& ids, vector<int32_t>& off,
                       vector<uint32_t>& idx) {
@@ -201,22 +276,32 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPoi
     const orbfe_feature_vector kfv{(int32_t)kid.size(), kid.data(), koff.data(), kidx.data()};
     const orbfe_feature_vector ffv{(int32_t)fid.size(), fid.data(), foff.data(), fidx.data()};
     vector<int32_t> out(F.N, -1);
-    const orbfe_frame fr = frame_view(F);
-    const int n = orbfe_search_by_bow(reinterpret_cast<const orbfe_keypoint*>(pKF->mvKeysUn.data()),
-                                      pKF->mDescriptors.data, kf_mp.data(), (int)kf_mp.size(), &kfv,
-                                      &fr, &ffv, out.data(), mfNNratio, mbCheckOrientation);
+    vector<cv::KeyPoint> keys;
+    const orbfe_frame fr = frame_view(F, keys);
+    const int n = orbfe_search_by_bow(
+        reinterpret_cast<const orbfe_keypoint*>(pKF->mpCamera2 ? kf_keys.data() : pKF->mvKeysUn.data()),
+        pKF->mDescriptors.data, kf_mp.data(), (int)kf_mp.size(), &kfv, &fr, &ffv, out.data(), mfNNratio,
+        mbCheckOrientation);
+    if (failed(n, "orbfe_search_by_bow")) return SearchByBoW_cpu(pKF, F, vpMapPointMatches);
     vpMapPointMatches.assign(F.N, nullptr);
     for (int i = 0; i < F.N; i++) vpMapPointMatches[i] = H.at(out[i]);
     return n;
 }
 
-// Frame.cc:811-981 (replaces the body of Frame::ComputeStereoMatches; lives in Frame.cc)
+// Frame.cc:811-981: the body of Frame::ComputeStereoMatches becomes (it lives in Frame.cc, with
+// the original body renamed ComputeStereoMatches_cpu):
 //   void Frame::ComputeStereoMatches() {
 //       mvuRight = vector<float>(N, -1.0f);
 //       mvDepth = vector<float>(N, -1.0f);
-//       orbfe_stereo_match(static_cast<orbfe_extractor*>(mpORBextractorLeft->mpOrbfe),
-//                          static_cast<orbfe_extractor*>(mpORBextractorRight->mpOrbfe),
-//                          mbf, fx, mvuRight.data(), mvDepth.data());
+//       const int rc = orbfe_stereo_match(static_cast<orbfe_extractor*>(mpORBextractorLeft->mpOrbfe),
+//                                         static_cast<orbfe_extractor*>(mpORBextractorRight->mpOrbfe),
+//                                         mbf, fx, mvuRight.data(), mvDepth.data());
+//       if (rc < 0) {   // e.g. ORBFE_E_ARG: more than 2048 keypoints per image (nFeatures > ~2000)
+//           fprintf(stderr, "[orbfe] orbfe_stereo_match returned %d; running the CPU implementation\n", rc);
+//           mpORBextractorLeft->MaterialisePyramid();
+//           mpORBextractorRight->MaterialisePyramid();
+//           ComputeStereoMatches_cpu();
+//       }
 //   }
 
 }  // namespace ORB_SLAM3

@@ -298,3 +298,128 @@ def test_search_local_points_device_resident(gpu, om):
     no, ntm_o = om.search_local_points(F, cam, pts, mvp_o, obs, 1.0)
     assert (ng, ntm_g) == (no, ntm_o) and no > 0
     np.testing.assert_array_equal(mvp_t.cpu().numpy(), mvp_o)
+
+
+# ---- two-camera frames (Frame.Nleft != -1, KannalaBrandt8 stereo: config 4's tracking path) ----
+def _two_case(seed, nl=1000, nr=950, n_mps=20000, slots=0.15):
+    rng = np.random.default_rng(seed)
+    F = sm.synth_frame_two(rng, nl, nr)
+    mps = sm.synth_local_map_two(rng, F, n_mps)
+    mvp, obs = sm.initial_slots(rng, F.N, slots)
+    return rng, F, mps, mvp, obs
+
+
+@pytest.mark.parametrize("seed", [61, 62])
+@pytest.mark.parametrize("th", [1, 3, 15])
+def test_sbp_local_two_cams(gpu, om, seed, th):
+    """SearchByProjection(F, vpMapPoints) with Nleft != -1 (ORBmatcher.cc:62-209): left search,
+    mvLeftToRightMatch partner, right-grid search, mvRightToLeftMatch partner."""
+    _, F, mps, mvp0, obs = _two_case(seed)
+    for ratio, bfar in ((0.8, False), (0.6, True)):
+        a, b = mvp0.copy(), mvp0.copy()
+        ng = ORBmatcher(ratio).SearchByProjectionLocalMap(F, a, obs, mps, th, bfar, 20.0)
+        no = om.OracleMatcher(ratio).sbp_local(F, b, obs, mps, th, bfar, 20.0)
+        assert ng == no and no > 0
+        np.testing.assert_array_equal(a, b)
+
+
+def test_sbp_local_two_cams_dense(gpu, om):
+    """Few keypoints, many competing points with Observations() == 0 and dense stereo links: long
+    ordered chains through both cameras' slots."""
+    rng = np.random.default_rng(65)
+    F = sm.synth_frame_two(rng, 150, 140, w=120, h=90, stereo_frac=0.9)
+    mps = sm.synth_local_map_two(rng, F, 8000, copy_frac=0.9, flip_p=0.02)
+    mps["observations"] = np.where(rng.random(len(mps)) < 0.5, 0, mps["observations"])
+    mvp0, obs = np.full(F.N, -1, np.int32), np.zeros(F.N, np.int32)
+    for th in (1, 3):
+        a, b = mvp0.copy(), mvp0.copy()
+        ng = ORBmatcher(0.8).SearchByProjectionLocalMap(F, a, obs, mps, th)
+        no = om.OracleMatcher(0.8).sbp_local(F, b, obs, mps, th)
+        assert ng == no
+        np.testing.assert_array_equal(a, b)
+
+
+def test_sbp_local_two_cams_device_resident(gpu, om):
+    import torch
+    from orb_slam3_ros_amd.matcher import DeviceMatchFrame, search_by_projection_local_device
+    _, F, mps, mvp0, obs = _two_case(66)
+    Fd = DeviceMatchFrame(F, gpu)
+    mvp_t = torch.from_numpy(mvp0.copy()).to(gpu)
+    obs_t = torch.from_numpy(obs.copy()).to(gpu)
+    mps_t = torch.from_numpy(mps.view(np.uint8).reshape(-1).copy()).to(gpu)
+    ng = search_by_projection_local_device(Fd, mvp_t, obs_t, mps_t, 3.0)
+    mvp_o = mvp0.copy()
+    no = om.OracleMatcher(0.8).sbp_local(F, mvp_o, obs, mps, 3.0)
+    assert ng == no and no > 0
+    np.testing.assert_array_equal(mvp_t.cpu().numpy(), mvp_o)
+
+
+@pytest.mark.parametrize("seed", [71, 72, 73])
+@pytest.mark.parametrize("mode", ["none", "forward", "backward"])
+@pytest.mark.parametrize("check_ori", [True, False])
+def test_sbp_lastframe_two_cams(gpu, om, seed, mode, check_ori):
+    """SearchByProjection(CurrentFrame, LastFrame) with CurrentFrame.Nleft != -1 (:1727-1858)."""
+    rng = np.random.default_rng(seed)
+    F = sm.synth_frame_two(rng, 1200, 1100)
+    pts, ruv = sm.synth_proj_points_two(rng, F, 1500)
+    mvp0, obs = sm.initial_slots(rng, F.N, 0.2)
+    fw, bw = mode == "forward", mode == "backward"
+    for th in (7, 15):
+        a, b = mvp0.copy(), mvp0.copy()
+        ng = ORBmatcher(0.9, check_ori).SearchByProjectionLastFrameStereo(F, a, obs, pts, ruv, th, fw, bw)
+        no = om.OracleMatcher(0.9, check_ori).sbp_lastframe_stereo(F, b, obs, pts, ruv, th, fw, bw)
+        assert ng == no and no > 0
+        np.testing.assert_array_equal(a, b)
+
+
+def test_sbp_two_cams_keyframe_left_grid(gpu, om):
+    """SearchByProjection(CurrentFrame, pKF) has no right-camera branch: a two-camera frame is
+    searched through its left grid only (GetFeaturesInArea's default bRight = false)."""
+    rng = np.random.default_rng(74)
+    F = sm.synth_frame_two(rng, 900, 900)
+    left = sm.MatchFrame(F.keys[:900], F.desc[:900], F.bounds, F.scale_factors)
+    pts = sm.synth_proj_points(rng, left, 1000, copy_frac=0.7)
+    mvp0, _ = sm.initial_slots(rng, F.N, 0.2)
+    a, b = mvp0.copy(), mvp0.copy()
+    ng = ORBmatcher(0.9, True).SearchByProjectionKeyFrame(F, a, pts, 10, 100)
+    # oracle: the same search over the left rows (the right rows are never candidates)
+    bl = b[:900].copy()
+    no = om.OracleMatcher(0.9, True).sbp_kf(left, bl, pts, 10, 100)
+    b[:900] = bl
+    assert ng == no and no > 0
+    np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("seed", [81, 82, 83])
+@pytest.mark.parametrize("check_ori", [True, False])
+def test_search_by_bow_two_cams(gpu, om, seed, check_ori):
+    """SearchByBoW(pKF, F) with F.Nleft != -1 (:288-386, the right match's "|| true")."""
+    rng = np.random.default_rng(seed)
+    KF = sm.synth_frame(rng, 1000, 512, 512, stereo=False)
+    F = sm.synth_frame_two(rng, 900, 900)
+    # F's features: noisy copies of KF features on both cameras
+    src = np.where(rng.random(F.N) < 0.7, rng.integers(0, KF.N, F.N), -1)
+    cp = src >= 0
+    F.desc[cp] = sm.flip_bits(rng, KF.desc[src[cp]], 0.05)
+    F.keys["angle"][cp] = np.mod(KF.keys["angle"][src[cp]] + 20 + rng.normal(0, 3, int(cp.sum())), 360)
+    kf_mp = np.where(rng.random(KF.N) < 0.25, -1, np.arange(KF.N) + 100).astype(np.int32)
+    for words in (50, 400):
+        fk, ff = sm.synth_bow(rng, words, KF, F, src)
+        ng, out_g = ORBmatcher(0.75, check_ori).SearchByBoW(KF.keys, KF.desc, kf_mp, fk, F, ff)
+        no, out_o = om.OracleMatcher(0.75, check_ori).search_by_bow(KF.keys, KF.desc, kf_mp, fk, F, ff)
+        assert ng == no and no > 0
+        np.testing.assert_array_equal(out_g, out_o)
+        assert (out_o[900:] >= 0).any()   # right-camera matches happened
+
+
+def test_two_cams_rejected_where_unsupported(gpu):
+    """The single-camera-only entries refuse a two-camera frame instead of mis-reading it."""
+    from orb_slam3_ros_amd._lib import OrbfeError
+    rng = np.random.default_rng(90)
+    F = sm.synth_frame_two(rng, 50, 40)
+    pts = sm.synth_proj_points(rng, sm.MatchFrame(F.keys[:50], F.desc[:50], F.bounds, F.scale_factors), 20)
+    mvp, obs = np.full(F.N, -1, np.int32), np.zeros(F.N, np.int32)
+    with pytest.raises(OrbfeError):   # last-frame search without the right projections
+        ORBmatcher(0.9).SearchByProjectionLastFrame(F, mvp, obs, pts, 7, False, False)
+    with pytest.raises(OrbfeError):
+        ORBmatcher(0.9).SearchForInitialization(F, F, np.zeros((F.N, 2), np.float32), np.zeros(F.N, np.int32))

@@ -213,7 +213,9 @@ def test_record_layouts():
     import ctypes
     from orb_slam3_ros_amd.matcher import CFeatureVector, CFrame
     assert sm.MAP_POINT_DTYPE.itemsize == 80 and sm.PROJ_POINT_DTYPE.itemsize == 64
-    assert ctypes.sizeof(CFrame) == 72 and CFrame.mbf.offset == 64
+    assert ctypes.sizeof(CFrame) == 96 and CFrame.mbf.offset == 64
+    assert CFrame.two_cams.offset == 68 and CFrame.nleft.offset == 72 and CFrame.l2r.offset == 80
+    assert sm.MAP_POINT_DTYPE.fields["proj_yr"][1] == 36 and sm.MAP_POINT_DTYPE.fields["scale_level_r"][1] == 44
     assert ctypes.sizeof(CFeatureVector) == 32
 
 
