@@ -345,7 +345,7 @@ def matcher_config5(steps):
         lib.orbfe_matcher_set_timing(0)
         dms = float(np.mean(dev))
         # device-resident call (records, slots and frame already in HBM): wall time per call, which
-        # includes the host-checked convergence of the ordered passes
+        # includes its single host round trip (the ordered passes converge on the device)
         mvp_t = [torch.from_numpy(mvp0.copy()).to(dev_t) for _ in range(steps + 2)]
         for b in mvp_t[:2]:
             search_by_projection_local_device(Fd, b, obs_t, mps_t, th)
@@ -360,7 +360,8 @@ def matcher_config5(steps):
                           "queries_per_s": round(len(mps) / dt, 1), "device_ms_per_call": round(dms, 4),
                           "device_queries_per_s": round(len(mps) / (dms * 1e-3), 1),
                           "resident_ms_per_call": round(rdt * 1e3, 4),
-                          "resident_queries_per_s": round(len(mps) / rdt, 1), "nmatches": int(n)}
+                          "resident_queries_per_s": round(len(mps) / rdt, 1),
+                          "resident_over_device": round(rdt * 1e3 / dms, 4), "nmatches": int(n)}
     # Tracking::SearchLocalPoints' projection (isInFrustum + PredictScale) fused with the
     # th=1 search, 100k world points, device time (HIP events)
     from orb_slam3_ros_amd.matcher import search_local_points

@@ -151,10 +151,33 @@ __global__ void k_mt_fill(int* p, int n, int v) {
     if (i < n) p[i] = v;
 }
 
+// Device-side convergence of the single-camera passes: ONE kernel per pass. Pass p reads the
+// state first_p (built during pass p - 1), adds its own assignments to first_{p+1} (atomicMin of
+// the query index; Observations() > 0 when need_obs) and clears first_{p+2} for the pass after
+// (three rotating buffers). A pass whose predecessor changed nothing returns at once (gate), so
+// the host enqueues a batch of passes plus the gated commit and synchronises once per call.
+struct PassIO {
+    const int* gate;     // changed count of the previous pass (nullptr: pass 0 always runs)
+    int* first_next;     // first_{p+1}
+    int* first_fill;     // first_{p+2}, cleared here
+    int n;               // slots
+    int need_obs;        // the slot blocks later queries only if the point has observations
+};
+__device__ __forceinline__ bool pass_gated(const PassIO& io) { return io.gate && *io.gate == 0; }
+__device__ __forceinline__ void pass_fill(const PassIO& io) {
+    const int nt = gridDim.x * blockDim.x;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < io.n; i += nt) io.first_fill[i] = MT_INF;
+}
+__device__ __forceinline__ void pass_publish(const PassIO& io, int q, int result, int obs) {
+    if (result >= 0 && (!io.need_obs || obs > 0)) atomicMin(&io.first_next[result], q);
+}
+
 // ---- SearchByProjection(Frame&, vector<MapPoint*>, th, bFarPoints, thFar) (ORBmatcher.cc:43-213) ----
 __global__ __launch_bounds__(MT_NT) void k_sbp_local(FrameDev fr, const orbfe_map_point* mps, int nq, float th,
                                                      int bFar, float thFar, float nnratio, const int* blocked0,
-                                                     const int* first, int* assign, int* changed) {
+                                                     const int* first, int* assign, int* changed, PassIO io) {
+    if (pass_gated(io)) return;
+    pass_fill(io);
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nq) return;
     const orbfe_map_point& mp = mps[q];
@@ -188,6 +211,7 @@ __global__ __launch_bounds__(MT_NT) void k_sbp_local(FrameDev fr, const orbfe_ma
             if (!(bestLevel == bestLevel2 && bestDist > nnratio * bestDist2)) result = bestIdx;
         }
     }
+    pass_publish(io, q, result, mp.observations);
     if (result != assign[q]) {
         assign[q] = result;
         atomicAdd(changed, 1);
@@ -214,8 +238,10 @@ __device__ __forceinline__ unsigned long long mt_wave_min64(unsigned long long v
 template <bool STAGED>
 __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wave(FrameDev fr, const orbfe_map_point* mps, int nq, float th,
                                                         int bFar, float thFar, float nnratio, const int* blocked0,
-                                                        const int* first, int* assign, int* changed) {
+                                                        const int* first, int* assign, int* changed, PassIO io) {
     extern __shared__ __attribute__((aligned(16))) uint8_t mt_sm[];
+    if (pass_gated(io)) return;
+    pass_fill(io);
     int2* s_cell = (int2*)mt_sm;                                          // [16][64] (start, exclusive prefix)
     float4* s_key = (float4*)(mt_sm + (MT_WNT / 64) * 64 * sizeof(int2));  // x, y, octave bits, uR
     uint4* s_desc = (uint4*)(s_key + (STAGED ? fr.n : 0));         // 2 x uint4 per keypoint
@@ -336,9 +362,12 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wave(FrameDev fr, const or
                 }
             }
         }
-        if (lane == 0 && result != assign[q]) {
-            assign[q] = result;
-            atomicAdd(changed, 1);
+        if (lane == 0) {
+            pass_publish(io, q, result, mp.observations);
+            if (result != assign[q]) {
+                assign[q] = result;
+                atomicAdd(changed, 1);
+            }
         }
     }
 }
@@ -348,7 +377,9 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wave(FrameDev fr, const or
 __global__ __launch_bounds__(MT_NT) void k_sbp_proj(FrameDev fr, const orbfe_proj_point* pts, int nq, float th,
                                                     int mode /*0 lastframe, 1 kf*/, int bForward, int bBackward,
                                                     int maxDist, const int* blocked0, const int* first, int* assign,
-                                                    int* changed) {
+                                                    int* changed, PassIO io) {
+    if (pass_gated(io)) return;
+    pass_fill(io);
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nq) return;
     const orbfe_proj_point& p = pts[q];
@@ -380,6 +411,7 @@ __global__ __launch_bounds__(MT_NT) void k_sbp_proj(FrameDev fr, const orbfe_pro
         });
         if (bestDist <= maxDist) result = bestIdx2;
     }
+    pass_publish(io, q, result, p.observations);
     if (result != assign[q]) {
         assign[q] = result;
         atomicAdd(changed, 1);
@@ -654,7 +686,9 @@ __device__ __forceinline__ unsigned mt_three_maxima_keep(const int* hist) {
 // dropped bins; K3 writes the slots.
 __global__ __launch_bounds__(MT_NT) void k_mt_commit_count(const OrbKeyPoint* keys, const int* assign,
                                                            const float* q_angle, int q_stride_bytes, int nq,
-                                                           int checkOri, int* result, int* hist, int W) {
+                                                           int checkOri, int* result, int* hist, int W,
+                                                           const int* gate = nullptr) {
+    if (gate && *gate != 0) return;   // passes not converged yet: the host launches more first
     __shared__ int s_hist[MT_HISTO];
     if (threadIdx.x < MT_HISTO) s_hist[threadIdx.x] = 0;
     SYNC();
@@ -675,7 +709,9 @@ __global__ __launch_bounds__(MT_NT) void k_mt_commit_count(const OrbKeyPoint* ke
 
 __global__ __launch_bounds__(MT_NT) void k_mt_commit_drop(const OrbKeyPoint* keys, const int* assign,
                                                           const float* q_angle, int q_stride_bytes, int nq,
-                                                          const int* hist, int* result, int W) {
+                                                          const int* hist, int* result, int W,
+                                                          const int* gate = nullptr) {
+    if (gate && *gate != 0) return;
     __shared__ unsigned s_keep;
     if (threadIdx.x == 0) s_keep = mt_three_maxima_keep(hist);
     SYNC();
@@ -691,7 +727,9 @@ __global__ __launch_bounds__(MT_NT) void k_mt_commit_drop(const OrbKeyPoint* key
     if ((threadIdx.x & 63) == 0 && m) atomicAdd(&result[1], __popcll(m));
 }
 
-__global__ void k_mt_commit_write(int n, const int* qid, int q_stride_bytes, const int* result, int* mvp, int W) {
+__global__ void k_mt_commit_write(int n, const int* qid, int q_stride_bytes, const int* result, int* mvp, int W,
+                                  const int* gate = nullptr) {
+    if (gate && *gate != 0) return;
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     const int w = result[2 + k];
@@ -1242,6 +1280,8 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     const size_t o_ntm = fin ? p.scratch(16) : 0;
     const size_t o_ruv = (two && mode == 1 && !dev) ? p.upload(right_uv, (size_t)nq * 8) : 0;
     const size_t o_first = p.scratch((size_t)n * 4);
+    const size_t o_first1 = p.scratch((size_t)n * 4);   // rotating pass states (W == 1)
+    const size_t o_first2 = p.scratch((size_t)n * 4);
     const size_t o_assign = p.scratch((size_t)nq * W * 4);
     const bool buckets = two && mode == 0;
     const size_t o_soff = buckets ? p.scratch((size_t)(n + 1) * 4) : 0;
@@ -1299,20 +1339,80 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     }
     const dim3 gq((nq + MT_NT - 1) / MT_NT);
     const bool staged = n <= MT_STAGE_MAX;
+    int* result = ms_ptr<int>(o_result);
+    int* hist = ms_ptr<int>(o_hist);
+    const dim3 ge((nq * W + MT_NT - 1) / MT_NT);
+    auto commit = [&](const int* gate) {
+        fill(result, n + 2, -1);
+        HIPCHK(hipMemsetAsync(hist, 0, MT_HISTO * 4, s));
+        HIPCHK(hipMemsetAsync(result, 0, 8, s));
+        hipLaunchKernelGGL(k_mt_commit_count, ge, dim3(MT_NT), 0, s, fr.keys, assign, (const float*)(q + qangle_off),
+                           (int)qstride, nq * W, checkOri, result, hist, W, gate);
+        if (checkOri)
+            hipLaunchKernelGGL(k_mt_commit_drop, ge, dim3(MT_NT), 0, s, fr.keys, assign,
+                               (const float*)(q + qangle_off), (int)qstride, nq * W, hist, result, W, gate);
+        hipLaunchKernelGGL(k_mt_commit_write, dim3((n + 255) / 256), dim3(256), 0, s, n, (const int*)(q + qid_off),
+                           (int)qstride, result, mvp_d, W, gate);
+        return ORBFE_OK;
+    };
     int pass = 0;
-    const int chunk = 2;   // passes launched between host checks (most searches converge in 2-3)
+    int cnt[2] = {0, 0};
+    if (W == 1) {
+        // single camera: one gated kernel per pass (PassIO), a batch of passes and the gated commit
+        // per host round trip; most searches converge within the first batch (2-4 passes)
+        int* fb[3] = {first, ms_ptr<int>(o_first1), ms_ptr<int>(o_first2)};
+        fill(fb[0], n, MT_INF);   // state of the all -1 assignment
+        fill(fb[1], n, MT_INF);
+        const int batch = 6;
+        while (true) {
+            for (int c = 0; c < batch; c++, pass++) {
+                if (pass >= MT_MAX_PASSES) return ORBFE_E_CAPACITY;
+                PassIO io{pass ? changed + pass - 1 : nullptr, fb[(pass + 1) % 3], fb[(pass + 2) % 3], n,
+                          mode == 2 ? 0 : 1};
+                const int* fcur = fb[pass % 3];
+                if (mode == 0 && th >= MT_WAVE_TH) {
+                    const int nb = std::min((nq + MT_WNT / 64 - 1) / (MT_WNT / 64), 512);
+                    const size_t lds = (MT_WNT / 64) * 64 * sizeof(int2) + (staged ? (size_t)n * 48 : 0);
+                    if (staged)
+                        hipLaunchKernelGGL(k_sbp_local_wave<true>, dim3(nb), dim3(MT_WNT), lds, s, fr,
+                                           (const orbfe_map_point*)q, nq, th, a0, thFar, nnratio, b0, fcur, assign,
+                                           changed + pass, io);
+                    else
+                        hipLaunchKernelGGL(k_sbp_local_wave<false>, dim3(nb), dim3(MT_WNT), lds, s, fr,
+                                           (const orbfe_map_point*)q, nq, th, a0, thFar, nnratio, b0, fcur, assign,
+                                           changed + pass, io);
+                } else if (mode == 0) {
+                    hipLaunchKernelGGL(k_sbp_local, gq, dim3(MT_NT), 0, s, fr, (const orbfe_map_point*)q, nq, th, a0,
+                                       thFar, nnratio, b0, fcur, assign, changed + pass, io);
+                } else {
+                    hipLaunchKernelGGL(k_sbp_proj, gq, dim3(MT_NT), 0, s, fr, (const orbfe_proj_point*)q, nq, th,
+                                       mode == 1 ? 0 : 1, a0, a1, maxDist, b0, fcur, assign, changed + pass, io);
+                }
+            }
+            commit(changed + pass - 1);   // runs only if the last pass changed nothing
+            HIPCHK(hipGetLastError());
+            timer.end();
+            int ch = 0;
+            if (!dev) HIPCHK(hipMemcpyAsync(mvp, mvp_d, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(cnt, result, 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(&ch, changed + pass - 1, 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            if (ch == 0) return cnt[0] - cnt[1];
+        }
+    }
+    const int chunk = 2;   // passes launched between host checks (two-camera frames)
     while (true) {
         for (int c = 0; c < chunk; c++, pass++) {
             if (pass >= MT_MAX_PASSES) return ORBFE_E_CAPACITY;
             const dim3 gw((nq * W + MT_NT - 1) / MT_NT);
             if (two && mode == 0) {   // per-slot write buckets (unguarded partner writes)
-                int* cnt = first;   // n + 1 counters, then the scan's offsets / cursors / lists
+                int* cntb = first;   // n counters, then the scan's offsets / cursors / lists
                 int* off = ms_ptr<int>(o_soff);
                 int* cur = ms_ptr<int>(o_scur);
                 int* lst = ms_ptr<int>(o_slst);
-                HIPCHK(hipMemsetAsync(cnt, 0, (size_t)n * 4, s));
-                hipLaunchKernelGGL(k_slot_count, gw, dim3(MT_NT), 0, s, assign, nq * W, cnt);
-                hipLaunchKernelGGL(k_slot_scan, dim3(1), dim3(1024), 0, s, cnt, n, off, cur);
+                HIPCHK(hipMemsetAsync(cntb, 0, (size_t)n * 4, s));
+                hipLaunchKernelGGL(k_slot_count, gw, dim3(MT_NT), 0, s, assign, nq * W, cntb);
+                hipLaunchKernelGGL(k_slot_scan, dim3(1), dim3(1024), 0, s, cntb, n, off, cur);
                 hipLaunchKernelGGL(k_slot_fill, gw, dim3(MT_NT), 0, s, assign, nq * W, cur, lst);
                 hipLaunchKernelGGL(k_sbp_local2, gq, dim3(MT_NT), 0, s, fr, (const orbfe_map_point*)q, nq, th, a0, thFar,
                                    nnratio, b0, (const int*)off, (const int*)lst, assign, changed + pass);
@@ -1321,46 +1421,17 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
             fill(first, n, MT_INF);
             hipLaunchKernelGGL(k_mt_first_strided, gw, dim3(MT_NT), 0, s, assign, q + qobs_off, (int)qstride, nq * W,
                                mode == 2 ? 0 : 1, first, W);
-            if (two && mode == 1) {
-                hipLaunchKernelGGL(k_sbp_proj2, gq, dim3(MT_NT), 0, s, fr, (const orbfe_proj_point*)q, ruv, nq, th, a0,
-                                   a1, b0, first, assign, changed + pass);
-            } else if (mode == 0 && th >= MT_WAVE_TH) {
-                const int nb = std::min((nq + MT_WNT / 64 - 1) / (MT_WNT / 64), 512);
-                const size_t lds = (MT_WNT / 64) * 64 * sizeof(int2) + (staged ? (size_t)n * 48 : 0);
-                if (staged)
-                    hipLaunchKernelGGL(k_sbp_local_wave<true>, dim3(nb), dim3(MT_WNT), lds, s, fr, (const orbfe_map_point*)q,
-                                       nq, th, a0, thFar, nnratio, b0, first, assign, changed + pass);
-                else
-                    hipLaunchKernelGGL(k_sbp_local_wave<false>, dim3(nb), dim3(MT_WNT), lds, s, fr, (const orbfe_map_point*)q,
-                                       nq, th, a0, thFar, nnratio, b0, first, assign, changed + pass);
-            } else if (mode == 0)
-                hipLaunchKernelGGL(k_sbp_local, gq, dim3(MT_NT), 0, s, fr, (const orbfe_map_point*)q, nq, th, a0, thFar,
-                                   nnratio, b0, first, assign, changed + pass);
-            else
-                hipLaunchKernelGGL(k_sbp_proj, gq, dim3(MT_NT), 0, s, fr, (const orbfe_proj_point*)q, nq, th,
-                                   mode == 1 ? 0 : 1, a0, a1, maxDist, b0, first, assign, changed + pass);
+            hipLaunchKernelGGL(k_sbp_proj2, gq, dim3(MT_NT), 0, s, fr, (const orbfe_proj_point*)q, ruv, nq, th, a0,
+                               a1, b0, first, assign, changed + pass);
         }
         int ch = 0;
         HIPCHK(hipMemcpyAsync(&ch, changed + pass - 1, 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         if (ch == 0) break;
     }
-    int* result = ms_ptr<int>(o_result);
-    fill(result, n + 2, -1);
-    int* hist = ms_ptr<int>(o_hist);
-    HIPCHK(hipMemsetAsync(hist, 0, MT_HISTO * 4, s));
-    HIPCHK(hipMemsetAsync(result, 0, 8, s));
-    const dim3 ge((nq * W + MT_NT - 1) / MT_NT);
-    hipLaunchKernelGGL(k_mt_commit_count, ge, dim3(MT_NT), 0, s, fr.keys, assign, (const float*)(q + qangle_off),
-                       (int)qstride, nq * W, checkOri, result, hist, W);
-    if (checkOri)
-        hipLaunchKernelGGL(k_mt_commit_drop, ge, dim3(MT_NT), 0, s, fr.keys, assign, (const float*)(q + qangle_off),
-                           (int)qstride, nq * W, hist, result, W);
-    hipLaunchKernelGGL(k_mt_commit_write, dim3((n + 255) / 256), dim3(256), 0, s, n, (const int*)(q + qid_off),
-                       (int)qstride, result, mvp_d, W);
+    commit(nullptr);
     HIPCHK(hipGetLastError());
     timer.end();
-    int cnt[2] = {0, 0};
     if (!dev) HIPCHK(hipMemcpyAsync(mvp, mvp_d, (size_t)n * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(cnt, result, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
