@@ -79,6 +79,7 @@ struct orbfe_extractor {
     OrbGeom g{};
     std::vector<int16_t> tab;
     FastLds fast_lds{};   // k_fast per-wave LDS layout (max over levels)
+    FastLds fast_lds_lv[ORBFE_MAX_LEVELS] = {};   // per level: a launch over levels [a, b] sizes its LDS by their max
     size_t oct_lds = 0;
     // device buffers
     int16_t* d_tab = nullptr;
@@ -244,7 +245,7 @@ static bool build_bands(OrbGeom& g, int l, std::vector<int16_t>& tab, const Fast
 // Per-level geometry with the reference's expressions (see orbfe_types.h), derived into the
 // caller's locals: the handle's current geometry stays untouched when the size is rejected.
 static int build_geom(const orbfe_extractor* h, int W, int H, OrbGeom& g, std::vector<int16_t>& tab,
-                      FastLds& fast_lds, size_t& oct_lds) {
+                      FastLds& fast_lds, FastLds* fast_lds_lv, size_t& oct_lds) {
     memset(&g, 0, sizeof(g));
     g.nlevels = h->nlevels;
     g.width = W;
@@ -284,12 +285,17 @@ static int build_geom(const orbfe_extractor* h, int W, int H, OrbGeom& g, std::v
         L.cell_cap = ((L.w_cell + 1) / 2) * ((L.h_cell + 1) / 2);
         L.cellkey_off = cellkey_off;
         cellkey_off += ncell * L.cell_cap;
-        {   // k_fast: RS = 4 * (ceil(dw / 4) + 2) with dw <= w_cell; ROI rows <= h_cell + 6, score
+        {   // k_fast: RS = 16 * ceil((ceil(dw / 4) + 2) / 4) with dw <= w_cell; ROI rows <= h_cell + 6, score
             // map rows <= h_cell + 2; corner list 2 B per pixel and >= 8 B per 4-pixel group + 256
-            const int rs = 4 * ((L.w_cell + 3) / 4 + 2), grp = ((L.w_cell + 3) / 4) * L.h_cell;
-            fl.roi = std::max(fl.roi, round_up(rs * (L.h_cell + 6), 16));
-            fl.sc = std::max(fl.sc, round_up(rs * (L.h_cell + 2), 16));
-            fl.cor = std::max(fl.cor, round_up(std::max(2 * L.w_cell * L.h_cell, 8 * grp + 256), 16));
+            const int rs = 16 * (((L.w_cell + 3) / 4 + 2 + 3) / 4), grp = ((L.w_cell + 3) / 4) * L.h_cell;
+            FastLds& f = fast_lds_lv[l];
+            f.roi = round_up(rs * (L.h_cell + 6), 16);
+            f.sc = round_up(rs * (L.h_cell + 2), 16);
+            f.cor = round_up(std::max(2 * L.w_cell * L.h_cell, 8 * grp + 256), 16);
+            f.wave_bytes = f.roi + f.sc + f.cor + FAST_ENT_BYTES;
+            fl.roi = std::max(fl.roi, f.roi);
+            fl.sc = std::max(fl.sc, f.sc);
+            fl.cor = std::max(fl.cor, f.cor);
         }
         if (L.w_cell > 127 || L.h_cell > 127) return ORBFE_E_ARG;   // k_fast packs dx, dy in 7 bits
         // octree
@@ -394,14 +400,15 @@ static int ensure(orbfe_extractor* h, int W, int H, int B) {
         // a rejected size leaves the handle exactly as it was (geometry, tables and buffers)
         OrbGeom g;
         std::vector<int16_t> tab;
-        FastLds fl{};
+        FastLds fl{}, fl_lv[ORBFE_MAX_LEVELS] = {};
         size_t oct = 0;
-        int rc = build_geom(h, W, H, g, tab, fl, oct);
+        int rc = build_geom(h, W, H, g, tab, fl, fl_lv, oct);
         if (rc) return rc;
         free_buffers(h);
         h->g = g;
         h->tab.swap(tab);
         h->fast_lds = fl;
+        memcpy(h->fast_lds_lv, fl_lv, sizeof(fl_lv));
         h->oct_lds = oct;
         h->W = W;
         h->H = H;
@@ -517,28 +524,54 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
                            (size_t)4 * h->fast_lds.wave_bytes, s, P0, pitch0, h->d_pyr, g.pyr_bytes, g, h->fast_lds,
                            h->d_cellkeys, h->d_cellcnt, h->d_fblist);
     } else {
-        // ComputePyramid's chain (level l from level l - 1) is a sequence of short, latency-bound
-        // launches on the batch stream; FAST of level 0 (the input images) runs beside it on the
-        // low-priority side stream, then one k_fast launch covers levels 1.. after the chain
-        // (level l's cells are [lv[l].cell_base, lv[l + 1].cell_base)). Per-level FAST launches
-        // overlapped with the chain measured slower: each is too small to fill the GPU.
+        // ComputePyramid's chain (level l from level l - 1) is a sequence of dependent k_resize
+        // launches on the batch stream; k_fast launches (level l's cells are [lv[l].cell_base,
+        // lv[l + 1].cell_base)) run beside it on the low-priority side stream as their levels
+        // become ready. Measured: the launches share one saturated machine, so the
+        // pass costs about the sum of the kernels' isolated times whatever the overlap; this
+        // order is marginally the best of those tried.
         hipStream_t s2 = h->side_stream;
-        auto fast_range = [&](hipStream_t st, int c0, int c1) {
+        // each launch sizes its per-wave LDS by the levels it covers (level 0's cells need less than
+        // the tall cells of the top levels: more resident waves per CU)
+        auto fast_range = [&](hipStream_t st, int l0, int l1) {
+            FastLds fl{0, 0, 0, 0};
+            for (int l = l0; l < l1; l++) {
+                fl.roi = std::max(fl.roi, h->fast_lds_lv[l].roi);
+                fl.sc = std::max(fl.sc, h->fast_lds_lv[l].sc);
+                fl.cor = std::max(fl.cor, h->fast_lds_lv[l].cor);
+            }
+            const int c0 = g.lv[l0].cell_base, c1 = l1 < g.nlevels ? g.lv[l1].cell_base : g.total_cells;
+            fl.wave_bytes = fl.roi + fl.sc + fl.cor + FAST_ENT_BYTES;
             hipLaunchKernelGGL(k_fast, dim3((c1 - c0 + 4 * FAST_CPW - 1) / (4 * FAST_CPW), B), dim3(256),
-                               (size_t)4 * h->fast_lds.wave_bytes, st, P, pitch, h->d_pyr, g.pyr_bytes, g,
-                               h->fast_lds, h->d_cellkeys, h->d_cellcnt, c0, c1);
+                               (size_t)4 * fl.wave_bytes, st, P, pitch, h->d_pyr, g.pyr_bytes, g, fl, h->d_cellkeys,
+                               h->d_cellcnt, c0, c1);
         };
-        const int c_l1 = g.nlevels > 1 ? g.lv[1].cell_base : g.total_cells;
+#ifdef FAST_NO_OVERLAP
+        s2 = s;   // profiling builds: every launch in stream order (isolated kernel times)
+#endif
+#ifndef FAST_MID
+#define FAST_MID 4   // FAST of levels [1, FAST_MID) runs on the side stream once resize has built them
+#endif
+        // side stream: FAST of level 0 at once, then of levels [1, lmid) when the chain has built
+        // them (beside the chain's short, latency-bound top-level launches); batch stream: the
+        // chain, then FAST of levels [lmid, nlevels)
+        const int lmid = std::min(std::max(FAST_MID, 1), g.nlevels);
         HIPCHK(hipEventRecord(h->ev_fork[0], s));
         HIPCHK(hipStreamWaitEvent(s2, h->ev_fork[0], 0));
-        fast_range(s2, 0, c_l1);
-        HIPCHK(hipEventRecord(h->ev_fork[1], s2));
+        fast_range(s2, 0, 1);
+        // ComputePyramid: one k_resize launch per level (level l from level l - 1)
         for (int l = 1; l < g.nlevels; l++) {
             const int tiles_y = (g.lv[l].h + g.lv[l].rz_rows - 1) / g.lv[l].rz_rows;
             dim3 grid((g.lv[l].w + g.lv[l].rz_cols - 1) / g.lv[l].rz_cols, (tiles_y + RZ_TPB - 1) / RZ_TPB, B);
             hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, s, P, pitch, h->d_pyr, g.pyr_bytes, h->d_tab, g, l);
+            if (l + 1 == lmid) {
+                HIPCHK(hipEventRecord(h->ev_fork[2], s));
+                HIPCHK(hipStreamWaitEvent(s2, h->ev_fork[2], 0));
+                fast_range(s2, 1, lmid);
+            }
         }
-        if (c_l1 < g.total_cells) fast_range(s, c_l1, g.total_cells);
+        HIPCHK(hipEventRecord(h->ev_fork[1], s2));
+        if (lmid < g.nlevels) fast_range(s, lmid, g.nlevels);
         HIPCHK(hipStreamWaitEvent(s, h->ev_fork[1], 0));
     }
     BlurKernel bk;   // the Gaussian blur is fused into k_describe

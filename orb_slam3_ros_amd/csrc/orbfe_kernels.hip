@@ -415,9 +415,19 @@ __device__ __forceinline__ int fast_M(const uint8_t* im, int stride, int x, int 
 #endif
 #define FAST_PF 4     // prefetched 16-byte chunks per lane (rows / rows-per-load: 2 at W = 35)
 struct FastCell {
-    int l, local, r0, c0, rows, cols, pitch;
+    int l, local, ci, cj, r0, c0, rows, cols, pitch;
     gptr_u8 src;
 };
+__device__ __forceinline__ void fast_cell_rect(FastCell& f, const OrbLevel& L) {
+    const int maxBX = L.w - ORBFE_MINB, maxBY = L.h - ORBFE_MINB;
+    f.r0 = ORBFE_MINB + f.ci * L.h_cell;
+    f.c0 = ORBFE_MINB + f.cj * L.w_cell;
+    const int r1 = min(f.r0 + L.h_cell + 6, maxBY), c1 = min(f.c0 + L.w_cell + 6, maxBX);
+    // the reference skips such cells (ORBextractor.cc:810,819); never true for its grid, kept for parity
+    const bool skip = (f.r0 >= maxBY - 3) || (f.c0 >= maxBX - 6);
+    f.rows = skip ? 0 : r1 - f.r0;
+    f.cols = skip ? 0 : c1 - f.c0;
+}
 __device__ __forceinline__ FastCell fast_cell(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                               int pyr_stride, const OrbGeom& g, int b, int c) {
     FastCell f;
@@ -426,24 +436,36 @@ __device__ __forceinline__ FastCell fast_cell(const uint8_t* const* imgs, int in
     const OrbLevel& L = g.lv[l];
     f.l = l;
     f.local = c - L.cell_base;
-    const int ci = f.local / L.n_cols, cj = f.local - ci * L.n_cols;
-    const int maxBX = L.w - ORBFE_MINB, maxBY = L.h - ORBFE_MINB;
-    f.r0 = ORBFE_MINB + ci * L.h_cell;
-    f.c0 = ORBFE_MINB + cj * L.w_cell;
-    const int r1 = min(f.r0 + L.h_cell + 6, maxBY), c1 = min(f.c0 + L.w_cell + 6, maxBX);
-    // the reference skips such cells (ORBextractor.cc:810,819); never true for its grid, kept for parity
-    const bool skip = (f.r0 >= maxBY - 3) || (f.c0 >= maxBX - 6);
-    f.rows = skip ? 0 : r1 - f.r0;
-    f.cols = skip ? 0 : c1 - f.c0;
+    f.ci = f.local / L.n_cols;
+    f.cj = f.local - f.ci * L.n_cols;
+    fast_cell_rect(f, L);
     f.src = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l, &f.pitch);
     return f;
 }
-// LDS layout of a cell: rows of RS = 4*ng + 8 bytes (ng = ceil(dw/4) pixel groups), byte j of a
-// row = ROI column j - 1. A row is loaded as cpr 16-byte chunks from the aligned dword A0 =
-// (c0 - 1) & ~3 (cpr = ceil((nd + 1) / 4): the nd LDS dwords plus one for the realignment), one
-// chunk per lane, rpl rows per load; the realigned fourth dword of a chunk takes the next lane's
-// first dword (a DPP wave_shl). Reads end at most 20 bytes past c1 <= w - 16, inside the next row
-// (ROI rows end 17 rows above the last image row).
+// the cell after f in cell order (no divisions: the wave walks consecutive cells)
+__device__ __forceinline__ FastCell fast_cell_next(const FastCell& f, const uint8_t* const* imgs, int in_pitch,
+                                                   const uint8_t* pyr, int pyr_stride, const OrbGeom& g, int b) {
+    FastCell n = f;
+    n.local++;
+    if (++n.cj == g.lv[n.l].n_cols) {
+        n.cj = 0;
+        if (++n.ci == g.lv[n.l].n_rows) {
+            n.l++;
+            n.local = n.ci = 0;
+            n.src = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, n.l, &n.pitch);
+        }
+    }
+    fast_cell_rect(n, g.lv[n.l]);
+    return n;
+}
+// LDS layout of a cell: rows of RS = 16 * ceil(nd / 4) bytes (nd = ng + 2 dwords are read, ng =
+// ceil(dw / 4) pixel groups; the rest of a row is padding), byte j of a row = ROI column j - 1, so
+// every row starts 16-byte aligned and a realigned chunk is one ds_write_b128. A row is loaded as
+// cpr 16-byte chunks from the aligned dword A0 = (c0 - 1) & ~3 (cpr = ceil((nd + 1) / 4): the
+// written chunks plus the dword the realignment takes from the next one), one chunk per lane, rpl
+// rows per load; the realigned fourth dword of a chunk takes the next lane's first dword (a DPP
+// wave_shl; for the last chunk of a row that is padding). Reads end at most 20 bytes past c1 <=
+// w - 16, inside the next row (ROI rows end 17 rows above the last image row).
 __device__ __forceinline__ void fast_geom(const FastCell& f, int* ng, int* nd, int* cpr, int* rpl) {
     const int dw = f.cols - 6, dh = f.rows - 6;
     *ng = (dw > 0 && dh > 0) ? (dw + 3) >> 2 : 0;
@@ -451,6 +473,8 @@ __device__ __forceinline__ void fast_geom(const FastCell& f, int* ng, int* nd, i
     *cpr = (*nd + 4) >> 2;
     *rpl = small_div(64, *cpr);
 }
+// row stride of the cell's LDS image and score map in dwords
+__device__ __forceinline__ int fast_rsd(int nd) { return 4 * ((nd + 3) >> 2); }
 __device__ __forceinline__ orbfe_u32x4 fast_chunk(gptr_u8 rp, bool al) {
     if (al) return *(const ORBFE_GLOBAL orbfe_u32x4*)rp;
     orbfe_u32x4 q = {0u, 0u, 0u, 0u};
@@ -472,27 +496,17 @@ __device__ __forceinline__ void fast_prefetch(const FastCell& f, int lane, orbfe
         if (y < f.rows) pf[u] = fast_chunk(base + (size_t)y * f.pitch, al);
     }
 }
-// realign a chunk by sal bytes and store its dwords (< nd) to row y of the ROI image; rows of the
-// score map (y < dh + 2) are zeroed alongside
-__device__ __forceinline__ void fast_stage_chunk(uint32_t* s32w, uint32_t* s32z, const orbfe_u32x4& q, int sal,
-                                                 int y, int st, int nd, int dh, bool ok) {
+// realign a chunk by sal bytes (the DPP needs every lane) and store it as row y's chunk st
+__device__ __forceinline__ void fast_stage_chunk(uint8_t* s_img, const orbfe_u32x4& q, int sal, int y, int st,
+                                                 int rs, bool ok) {
     const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q.x, 0x130, 0xf, 0xf, false);
-    const uint32_t w[4] = {__builtin_amdgcn_alignbyte(q.y, q.x, (uint32_t)sal), __builtin_amdgcn_alignbyte(q.z, q.y, (uint32_t)sal),
+    const orbfe_u32x4 w = {__builtin_amdgcn_alignbyte(q.y, q.x, (uint32_t)sal), __builtin_amdgcn_alignbyte(q.z, q.y, (uint32_t)sal),
                            __builtin_amdgcn_alignbyte(q.w, q.z, (uint32_t)sal), __builtin_amdgcn_alignbyte(nx, q.w, (uint32_t)sal)};
-    if (ok) {
-        const int d0 = 4 * st;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            if (d0 + i < nd) {
-                s32w[y * nd + d0 + i] = w[i];
-                if (y < dh + 2) s32z[y * nd + d0 + i] = 0u;
-            }
-        }
-    }
+    if (ok) *(orbfe_u32x4*)(s_img + y * rs + 16 * st) = w;
 }
 
-// Stage a prefetched cell ROI into the wave's LDS image (realigned rows of 4 * nd bytes) and zero
-// the score map rows (y < dh + 2) alongside; ends with WAVE_SYNC.
+// Stage a prefetched cell ROI into the wave's LDS image and zero the score map (rows < dh + 2);
+// ends with WAVE_SYNC.
 __device__ __forceinline__ void fast_stage_cell(const FastCell& cur, const orbfe_u32x4 (&pf)[FAST_PF], uint8_t* s_img,
                                                 uint8_t* s_sc, int lane) {
     int ng, nd, cpr, rpl;
@@ -500,12 +514,12 @@ __device__ __forceinline__ void fast_stage_cell(const FastCell& cur, const orbfe
     const int dh = cur.rows - 6;
     if (ng) {
         const int sy = small_div(lane, cpr), st = lane - sy * cpr, sal = (cur.c0 - 1) & 3;
-        uint32_t* s32w = (uint32_t*)s_img;
-        uint32_t* s32z = (uint32_t*)s_sc;
+        const int rs = 4 * fast_rsd(nd), nw = (nd + 3) >> 2;
+        const bool wr = sy < rpl && st < nw;
 #pragma unroll
         for (int u = 0; u < FAST_PF; u++) {
             const int y = sy + u * rpl;
-            fast_stage_chunk(s32w, s32z, pf[u], sal, y, st, nd, dh, sy < rpl && y < cur.rows);
+            fast_stage_chunk(s_img, pf[u], sal, y, st, rs, wr && y < cur.rows);
         }
         // rows beyond the prefetch window (only very tall cells of tiny levels): direct loads with a
         // wave-uniform trip count (the DPP needs every lane)
@@ -517,9 +531,12 @@ __device__ __forceinline__ void fast_stage_cell(const FastCell& cur, const orbfe
                 const bool ok = sy < rpl && y < cur.rows;
                 orbfe_u32x4 q = {0u, 0u, 0u, 0u};
                 if (ok) q = fast_chunk(base + (size_t)y * cur.pitch, al);
-                fast_stage_chunk(s32w, s32z, q, sal, y, st, nd, dh, ok);
+                fast_stage_chunk(s_img, q, sal, y, st, rs, ok && st < nw);
             }
         }
+        const orbfe_u32x4 z = {0u, 0u, 0u, 0u};
+        const int nz = (dh + 2) * (rs >> 4);
+        for (int i = lane; i < nz; i += 64) ((orbfe_u32x4*)s_sc)[i] = z;
     }
     WAVE_SYNC();
 }
@@ -529,15 +546,15 @@ struct FastLds {
 };
 #define FAST_ENT_BYTES 1024     // entry chunk: 64 groups x <= 8 entries x 2 B
 
-// Detection of one staged cell (both attempts, NMS, emission). NDC = the LDS row length in dwords
-// when known at compile time (0: runtime nd): every LDS offset of the ring / neighbour reads is then
+// Detection of one staged cell (both attempts, NMS, emission). NDC = the LDS row stride in dwords
+// when known at compile time (0: runtime): every LDS offset of the ring / neighbour reads is then
 // an immediate instead of a per-read VALU add.
 template <int NDC>
 __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds& fl, const FastCell& me, int ng,
                                                  int nd_rt, int dw, int dh, uint8_t* s_img, uint8_t* s_sc,
                                                  uint16_t* s_cor, uint16_t* s_ent, uint32_t* cellkeys, int* cellcnt,
                                                  int b, int c, int lane, int ablate, int first_attempt = 0) {
-    const int nd = NDC ? NDC : nd_rt;
+    const int nd = NDC ? NDC : fast_rsd(nd_rt);   // row stride in dwords (>= the nd_rt dwords read)
     const int RS = 4 * nd;
     const OrbLevel& L = g.lv[me.l];
     if (ablate == 1) {
@@ -801,12 +818,10 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
         fast_stage_cell(cur, pf, s_img, s_sc, lane);
         const FastCell me = cur;
         if (c + 1 < cend) {   // prefetch the next cell while this one is processed
-            cur = fast_cell(imgs, in_pitch, pyr, pyr_stride, g, b, c + 1);
+            cur = fast_cell_next(cur, imgs, in_pitch, pyr, pyr_stride, g, b);
             fast_prefetch(cur, lane, pf);
         }
-        if (nd == 11)
-            fast_cell_detect<11>(g, fl, me, ng, nd, dw, dh, s_img, s_sc, s_cor, s_ent, cellkeys, cellcnt, b, c, lane, ablate);
-        else if (nd == 12)
+        if (fast_rsd(nd) == 12)
             fast_cell_detect<12>(g, fl, me, ng, nd, dw, dh, s_img, s_sc, s_cor, s_ent, cellkeys, cellcnt, b, c, lane, ablate);
         else
             fast_cell_detect<0>(g, fl, me, ng, nd, dw, dh, s_img, s_sc, s_cor, s_ent, cellkeys, cellcnt, b, c, lane, ablate);

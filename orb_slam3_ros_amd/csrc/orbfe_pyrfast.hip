@@ -490,9 +490,7 @@ __global__ __launch_bounds__(256) void k_fallback(const uint8_t* const* imgs, in
         int ng, nd, cpr, rpl;
         fast_geom(me, &ng, &nd, &cpr, &rpl);
         const int dw = me.cols - 6, dh = me.rows - 6;
-        if (nd == 11)
-            fast_cell_detect<11>(g, fl, me, ng, nd, dw, dh, f_img, f_sc, f_cor, f_ent, cellkeys, cellcnt, b, c, lane, 0, 1);
-        else if (nd == 12)
+        if (fast_rsd(nd) == 12)
             fast_cell_detect<12>(g, fl, me, ng, nd, dw, dh, f_img, f_sc, f_cor, f_ent, cellkeys, cellcnt, b, c, lane, 0, 1);
         else
             fast_cell_detect<0>(g, fl, me, ng, nd, dw, dh, f_img, f_sc, f_cor, f_ent, cellkeys, cellcnt, b, c, lane, 0, 1);
