@@ -658,12 +658,19 @@ def main():
             "parity": parity,
         }
         if valu is not None:
-            # VALU issue fraction per kernel: committed SQ_INSTS_VALU per launch over this run's kernel
-            # time x the wave64 issue peak (2 cycles per instruction on each of 1024 SIMD-32s)
-            kt = {"k_pyrfast": stages["pyramid_fast"], "k_octree": stages["octree"], "k_describe": stages["describe"]}
-            result["roofline"]["valu_issue_frac"] = {
-                k: round(v["valu_per_step"] / (kt[k] * 1e-3) / VALU_ISSUE_PEAK, 4)
-                for k, v in valu[0].items() if k in kt and kt[k] > 0}
+            # VALU issue fraction per kernel (committed rocprofv3 counters of this workload on the
+            # isolated-timing build: SQ_INSTS_VALU per step over the kernel's own trace time x the
+            # wave64 issue peak, 1024 SIMD-32s x 2.4 GHz / 2 cycles), and for the pyramid+FAST pass as
+            # timed in this run
+            vk = valu[0]
+            result["roofline"]["valu_issue_frac"] = {k: v["valu_issue_frac"] for k, v in vk.items()
+                                                     if k in ("k_resize", "k_fast", "k_octree", "k_describe",
+                                                              "k_stereo")}
+            if "k_resize" in vk and "k_fast" in vk and pyr_fast_ms > 0:
+                result["roofline"]["valu_issue_frac_pass"] = round(
+                    (vk["k_resize"]["valu_per_step"] + vk["k_fast"]["valu_per_step"]) / (pyr_fast_ms * 1e-3)
+                    / VALU_ISSUE_PEAK, 4)
+            result["roofline"]["wave_states"] = {k: vk[k]["wave_state"] for k in ("k_resize", "k_fast") if k in vk}
             result["roofline"]["valu_source"] = valu[1]
         if cache is not None and "k_describe" in cache[0]:
             kd = cache[0]["k_describe"]

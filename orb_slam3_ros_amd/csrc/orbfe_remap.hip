@@ -8,53 +8,80 @@
 //  * D = (w0 S00 + w1 S01 + w2 S10 + w3 S11 + 2^14) >> 15 (FixedPtCast, INTER_REMAP_COEF_BITS = 15);
 //  * BORDER_CONSTANT (value 0): a sample outside the source reads 0; a pixel whose 2x2 footprint
 //    is entirely outside is 0.
-// One thread per 4 adjacent output pixels (one dword store); maps are read as float4.
 #pragma once
 
-__device__ __forceinline__ uint8_t remap_px(gptr_u8 src, int sw, int sh, int sstride, float mx, float my) {
+// The map-only part of one output pixel (identical for every image of a batch: one map pair
+// serves one camera): source offset of the 2x2 footprint, the BilinearTab_i weights packed as
+// u16 pairs, which footprint samples lie inside the source (bits 0-3: S00, S01, S10, S11) and
+// whether the whole footprint is outside (the pixel is 0).
+struct RemapPx {
+    int off;
+    uint32_t w01, w23;
+    uint32_t inside;   // bits 0-3 as above, bit 4 = at least one sample inside
+};
+__device__ __forceinline__ RemapPx remap_setup(int sw, int sh, int sstride, float mx, float my) {
     const float fxs = mx * 32.f, fys = my * 32.f;
     // saturate_cast<int>(float): round half to even, saturating
     const int X = fxs >= 2147483520.f ? INT_MAX : (fxs <= -2147483648.f ? INT_MIN : __float2int_rn(fxs));
     const int Y = fys >= 2147483520.f ? INT_MAX : (fys <= -2147483648.f ? INT_MIN : __float2int_rn(fys));
     const int sx = min(max(X >> 5, -32768), 32767), sy = min(max(Y >> 5, -32768), 32767);
     const int ax = X & 31, ay = Y & 31;
-    int w0, w1, w2, w3;
+    uint32_t w0, w1, w2, w3;
     if (ax == 0 && ay == 0) {
         w0 = 32767; w1 = 0; w2 = 0; w3 = 1;
     } else {
-        w0 = (32 - ay) * (32 - ax) * 32;
-        w1 = (32 - ay) * ax * 32;
-        w2 = ay * (32 - ax) * 32;
-        w3 = ay * ax * 32;
+        w0 = (uint32_t)((32 - ay) * (32 - ax) * 32);
+        w1 = (uint32_t)((32 - ay) * ax * 32);
+        w2 = (uint32_t)(ay * (32 - ax) * 32);
+        w3 = (uint32_t)(ay * ax * 32);
     }
+    RemapPx r;
+    r.w01 = w0 | (w1 << 16);
+    r.w23 = w2 | (w3 << 16);
+    if (sx >= sw || sx + 1 < 0 || sy >= sh || sy + 1 < 0) {
+        r.off = 0;
+        r.inside = 0;
+        return r;
+    }
+    r.off = sy * sstride + sx;   // sx, sy in [-1, sw - 1] x [-1, sh - 1] here
+    r.inside = 16u | (sx >= 0 && sy >= 0 ? 1u : 0u) | (sx + 1 < sw && sy >= 0 ? 2u : 0u) |
+               (sx >= 0 && sy + 1 < sh ? 4u : 0u) | (sx + 1 < sw && sy + 1 < sh ? 8u : 0u);
+    return r;
+}
+// D = (w0 S00 + w1 S01 + w2 S10 + w3 S11 + 2^14) >> 15 (FixedPtCast, INTER_REMAP_COEF_BITS = 15);
+// BORDER_CONSTANT: a sample outside the source reads 0
+__device__ __forceinline__ uint32_t remap_apply(gptr_u8 src, int sstride, const RemapPx& r) {
+    if (!(r.inside & 16u)) return 0u;
+    gptr_u8 p = src + r.off;
     int v0, v1, v2, v3;
-    if ((unsigned)sx < (unsigned)max(sw - 1, 0) && (unsigned)sy < (unsigned)max(sh - 1, 0)) {
-        gptr_u8 p = src + (size_t)sy * sstride + sx;
+    if ((r.inside & 15u) == 15u) {
         v0 = p[0]; v1 = p[1]; v2 = p[sstride]; v3 = p[sstride + 1];
     } else {
-        if (sx >= sw || sx + 1 < 0 || sy >= sh || sy + 1 < 0) return 0;
-        v0 = (sx >= 0 && sy >= 0) ? src[(size_t)sy * sstride + sx] : 0;
-        v1 = (sx + 1 < sw && sy >= 0) ? src[(size_t)sy * sstride + sx + 1] : 0;
-        v2 = (sx >= 0 && sy + 1 < sh) ? src[(size_t)(sy + 1) * sstride + sx] : 0;
-        v3 = (sx + 1 < sw && sy + 1 < sh) ? src[(size_t)(sy + 1) * sstride + sx + 1] : 0;
+        v0 = (r.inside & 1u) ? p[0] : 0;
+        v1 = (r.inside & 2u) ? p[1] : 0;
+        v2 = (r.inside & 4u) ? p[sstride] : 0;
+        v3 = (r.inside & 8u) ? p[sstride + 1] : 0;
     }
-    const int v = (v0 * w0 + v1 * w1 + v2 * w2 + v3 * w3 + (1 << 14)) >> 15;
-    return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+    const int v = (v0 * (int)(r.w01 & 0xFFFFu) + v1 * (int)(r.w01 >> 16) + v2 * (int)(r.w23 & 0xFFFFu) +
+                   v3 * (int)(r.w23 >> 16) + (1 << 14)) >> 15;
+    return (uint32_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
 }
 
+// One thread per 4 adjacent output pixels of one map tile, for RM_IPB images of the batch: the map
+// is read and converted once per tile and image group instead of once per image (the maps are
+// larger than the images: 8 B per pixel).
+#ifndef RM_IPB
+#define RM_IPB 4
+#endif
 __global__ __launch_bounds__(256) void k_remap(const uint8_t* const* srcs, int sw, int sh, int sstride,
                                                const float* __restrict__ mapx, const float* __restrict__ mapy,
-                                               int dw, int dh, uint8_t* const* dsts, int dstride) {
-    const int img = blockIdx.y;
+                                               int dw, int dh, uint8_t* const* dsts, int dstride, int n) {
     const int ng = (dw + 3) >> 2;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ng * dh) return;
     const int y = t / ng, x0 = 4 * (t - y * ng);
-    gptr_u8 src = as_global(srcs[img]);
-    uint8_t* dst = dsts[img] + (size_t)y * dstride;
     const float* mxr = mapx + (size_t)y * dw;
     const float* myr = mapy + (size_t)y * dw;
-    uint32_t packed = 0;
     const bool full = x0 + 4 <= dw;
     float mx[4], my[4];
     if (full && ((dw & 3) == 0)) {
@@ -68,12 +95,21 @@ __global__ __launch_bounds__(256) void k_remap(const uint8_t* const* srcs, int s
             my[q] = x0 + q < dw ? myr[x0 + q] : 0.f;
         }
     }
+    RemapPx r[4];
 #pragma unroll
-    for (int q = 0; q < 4; q++) packed |= (uint32_t)remap_px(src, sw, sh, sstride, mx[q], my[q]) << (8 * q);
-    if (full && ((((uintptr_t)(dst + x0)) & 3) == 0)) {
-        *(uint32_t*)(dst + x0) = packed;
-    } else {
-        for (int q = 0; q < 4 && x0 + q < dw; q++) dst[x0 + q] = (uint8_t)(packed >> (8 * q));
+    for (int q = 0; q < 4; q++) r[q] = remap_setup(sw, sh, sstride, mx[q], my[q]);
+    const int i0 = blockIdx.y * RM_IPB, i1 = min(i0 + RM_IPB, n);
+    for (int img = i0; img < i1; img++) {
+        gptr_u8 src = as_global(srcs[img]);
+        uint8_t* dst = dsts[img] + (size_t)y * dstride;
+        uint32_t packed = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) packed |= remap_apply(src, sstride, r[q]) << (8 * q);
+        if (full && ((((uintptr_t)(dst + x0)) & 3) == 0)) {
+            *(uint32_t*)(dst + x0) = packed;
+        } else {
+            for (int q = 0; q < 4 && x0 + q < dw; q++) dst[x0 + q] = (uint8_t)(packed >> (8 * q));
+        }
     }
 }
 
@@ -163,8 +199,8 @@ int orbfe_remap_linear_batch(const uint8_t* const* d_src, int sw, int sh, int ss
     HIPCHK(hipMemcpyAsync(dsrc, d_src, (size_t)n * sizeof(void*), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(ddst, d_dst, (size_t)n * sizeof(void*), hipMemcpyHostToDevice, s));
     const int ng = (dw + 3) >> 2;
-    hipLaunchKernelGGL(k_remap, dim3((ng * dh + 255) / 256, n), dim3(256), 0, s, dsrc, sw, sh, sstride, d_mapx, d_mapy,
-                       dw, dh, ddst, dstride);
+    hipLaunchKernelGGL(k_remap, dim3((ng * dh + 255) / 256, (n + RM_IPB - 1) / RM_IPB), dim3(256), 0, s, dsrc, sw, sh,
+                       sstride, d_mapx, d_mapy, dw, dh, ddst, dstride, n);
     HIPCHK(hipGetLastError());
     HIPCHK(hipFreeAsync(dsrc, s));
     HIPCHK(hipFreeAsync(ddst, s));
@@ -188,7 +224,7 @@ int orbfe_remap_linear(const uint8_t* src, int sw, int sh, int sstride, const fl
     HIPCHK(hipMemcpyAsync(ms_ptr<uint8_t>(o_ptr), ptrs, 16, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_remap, dim3((((dw + 3) >> 2) * dh + 255) / 256, 1), dim3(256), 0, s,
                        (const uint8_t* const*)ms_ptr<uint8_t>(o_ptr), sw, sh, sstride, ms_ptr<const float>(o_mx),
-                       ms_ptr<const float>(o_my), dw, dh, (uint8_t* const*)(ms_ptr<uint8_t>(o_ptr) + 8), dw);
+                       ms_ptr<const float>(o_my), dw, dh, (uint8_t* const*)(ms_ptr<uint8_t>(o_ptr) + 8), dw, 1);
     HIPCHK(hipGetLastError());
     timer.end();
     HIPCHK(hipMemcpy2DAsync(dst, dstride, ms_ptr<uint8_t>(o_dst), dw, dw, dh, hipMemcpyDeviceToHost, s));

@@ -11,6 +11,6 @@ for so in variants/liborbfe_*.so; do
   mkdir -p $D
   ORBFE_LIB=$PWD/$so timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $D -o run -- python bench.py --steps 5 --warmup 2 --stage-steps 1 --no-cpu-baseline --no-parity --matcher-steps 0 --rectify-steps 0 --no-side-configs ${BENCH_ARGS} > $D/log 2>&1 || { tail -20 $D/log; exit 1; }
   echo "=== $n $(grep -o '"value": [0-9.]*' $D/log | head -1)"
-  python tools/trace_grid_summary.py $D | grep -v "k_copy\|k_stereo\|k_describe\|k_octree"
+  python tools/trace_grid_summary.py $D | grep -v "k_copy"
 done
 done
