@@ -728,7 +728,9 @@ __global__ __launch_bounds__(MT_NT) void k_mt_commit_drop(const OrbKeyPoint* key
 }
 
 __global__ void k_mt_commit_write(int n, const int* qid, int q_stride_bytes, const int* result, int* mvp, int W,
-                                  const int* gate = nullptr) {
+                                  const int* gate = nullptr, int* ch_out = nullptr) {
+    // ch_out (result[-1]): the gate's value, so one host read brings the change flag and the counts
+    if (ch_out && blockIdx.x == 0 && threadIdx.x == 0) *ch_out = gate ? *gate : 0;
     if (gate && *gate != 0) return;
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
@@ -1043,6 +1045,7 @@ struct MatchScratch {
     size_t dcap = 0;
     uint8_t* h = nullptr;   // pinned
     size_t hcap = 0;
+    int* hs = nullptr;      // pinned status words read back at the end of a call
     // Deliberately never freed: thread_local destructors of the main thread can run after the HIP
     // runtime has been torn down at exit; the arena is reused for the thread's lifetime.
 };
@@ -1094,6 +1097,7 @@ int ms_prepare(const Plan& p) {
         m = MatchScratch();
         m.device = dev;
         HIPCHK(hipStreamCreateWithFlags(&m.stream, hipStreamNonBlocking));
+        HIPCHK(hipHostMalloc((void**)&m.hs, 64, hipHostMallocDefault));
     }
     if (p.end > m.dcap) {
         if (m.d) HIPCHK(hipFree(m.d));
@@ -1225,9 +1229,35 @@ struct DevIn {
     hipStream_t caller;
 };
 
-__global__ void k_blocked0(const int32_t* mvp, const int32_t* obs, int n, int any_slot, int* out) {
+// Every per-search initialisation of sbp_run in one launch (each used to be its own fill /
+// memset / kernel call): initial blocked flags of a device-resident search (b0d != nullptr), the
+// pass states of the all -1 assignment, the assignment, the change flags, the rotation histogram
+// and the commit result (resb[0] = change-flag copy, resb[1..2] = counts, resb[3 + k] = -1).
+struct SbpInit {
+    const int32_t* mvp;
+    const int32_t* obs;
+    int any_slot;
+    int* b0d;
+    int* fb0;
+    int* fb1;
+    int* assign;
+    int nassign;
+    int* changed;
+    int* hist;
+    int* resb;
+    int n;
+};
+__global__ void k_sbp_init(SbpInit a) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < n) out[k] = any_slot ? (mvp[k] >= 0) : (mvp[k] >= 0 && obs[k] > 0);
+    if (k < a.n) {
+        if (a.b0d) a.b0d[k] = a.any_slot ? (a.mvp[k] >= 0) : (a.mvp[k] >= 0 && a.obs[k] > 0);
+        a.fb0[k] = MT_INF;
+        a.fb1[k] = MT_INF;
+    }
+    if (k < a.nassign) a.assign[k] = -1;
+    if (k < MT_MAX_PASSES) a.changed[k] = 0;
+    if (k < MT_HISTO) a.hist[k] = 0;
+    if (k < a.n + 3) a.resb[k] = k < 3 ? 0 : -1;
 }
 
 int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, const void* queries, int nq,
@@ -1288,7 +1318,7 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     const size_t o_scur = buckets ? p.scratch((size_t)n * 4) : 0;
     const size_t o_slst = buckets ? p.scratch((size_t)nq * W * 4) : 0;
     const size_t o_changed = p.scratch(MT_MAX_PASSES * 4);
-    const size_t o_result = p.scratch((size_t)(n + 2) * 4);
+    const size_t o_result = p.scratch((size_t)(n + 3) * 4);   // [change flag copy | counts | slots]
     const size_t o_hist = p.scratch(MT_HISTO * 4);
     int rc = ms_prepare(p);
     if (rc) return rc;
@@ -1303,15 +1333,18 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     const FrameDev fr = fp.view();
     fp.launch_grid(fr);
     const int* b0 = dev ? ms_ptr<const int>(o_b0d) : ms_ptr<const int>(o_b0);
-    if (dev)
-        hipLaunchKernelGGL(k_blocked0, dim3((n + 255) / 256), dim3(256), 0, s, mvp, mvp_obs, n, mode == 2 ? 1 : 0,
-                           ms_ptr<int>(o_b0d));
     int32_t* mvp_d = dev ? mvp : ms_ptr<int32_t>(o_mvp);
     int* first = ms_ptr<int>(o_first);
     int* assign = ms_ptr<int>(o_assign);
     int* changed = ms_ptr<int>(o_changed);
-    HIPCHK(hipMemsetAsync(changed, 0, MT_MAX_PASSES * 4, s));
-    fill(assign, nq * W, -1);
+    int* resb = ms_ptr<int>(o_result);
+    int* hist = ms_ptr<int>(o_hist);
+    {
+        const SbpInit ia{mvp, mvp_obs, mode == 2 ? 1 : 0, dev ? ms_ptr<int>(o_b0d) : nullptr, first,
+                         ms_ptr<int>(o_first1), assign, nq * W, changed, hist, resb, n};
+        const int ni = std::max(std::max(n + 3, nq * W), MT_MAX_PASSES);
+        hipLaunchKernelGGL(k_sbp_init, dim3((ni + 255) / 256), dim3(256), 0, s, ia);
+    }
     const float2* ruv = (two && mode == 1) ? (dev ? (const float2*)right_uv : ms_ptr<const float2>(o_ruv)) : nullptr;
     const uint8_t* q = dev ? (const uint8_t*)(fin ? (const void*)fin->pts : queries) : ms_ptr<const uint8_t>(o_q);
     if (fin) {   // Tracking::SearchLocalPoints: project, count nToMatch, match only if > 0
@@ -1339,30 +1372,24 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     }
     const dim3 gq((nq + MT_NT - 1) / MT_NT);
     const bool staged = n <= MT_STAGE_MAX;
-    int* result = ms_ptr<int>(o_result);
-    int* hist = ms_ptr<int>(o_hist);
+    int* result = resb + 1;
     const dim3 ge((nq * W + MT_NT - 1) / MT_NT);
+    // the commit runs once (a gated commit that does not run leaves result / hist as k_sbp_init set them)
     auto commit = [&](const int* gate) {
-        fill(result, n + 2, -1);
-        HIPCHK(hipMemsetAsync(hist, 0, MT_HISTO * 4, s));
-        HIPCHK(hipMemsetAsync(result, 0, 8, s));
         hipLaunchKernelGGL(k_mt_commit_count, ge, dim3(MT_NT), 0, s, fr.keys, assign, (const float*)(q + qangle_off),
                            (int)qstride, nq * W, checkOri, result, hist, W, gate);
         if (checkOri)
             hipLaunchKernelGGL(k_mt_commit_drop, ge, dim3(MT_NT), 0, s, fr.keys, assign,
                                (const float*)(q + qangle_off), (int)qstride, nq * W, hist, result, W, gate);
         hipLaunchKernelGGL(k_mt_commit_write, dim3((n + 255) / 256), dim3(256), 0, s, n, (const int*)(q + qid_off),
-                           (int)qstride, result, mvp_d, W, gate);
+                           (int)qstride, result, mvp_d, W, gate, resb);
         return ORBFE_OK;
     };
     int pass = 0;
-    int cnt[2] = {0, 0};
     if (W == 1) {
         // single camera: one gated kernel per pass (PassIO), a batch of passes and the gated commit
         // per host round trip; most searches converge within the first batch (2-4 passes)
-        int* fb[3] = {first, ms_ptr<int>(o_first1), ms_ptr<int>(o_first2)};
-        fill(fb[0], n, MT_INF);   // state of the all -1 assignment
-        fill(fb[1], n, MT_INF);
+        int* fb[3] = {first, ms_ptr<int>(o_first1), ms_ptr<int>(o_first2)};   // fb[0], fb[1] = MT_INF (k_sbp_init)
         const int batch = 6;
         while (true) {
             for (int c = 0; c < batch; c++, pass++) {
@@ -1392,12 +1419,11 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
             commit(changed + pass - 1);   // runs only if the last pass changed nothing
             HIPCHK(hipGetLastError());
             timer.end();
-            int ch = 0;
+            int* st = t_ms.hs;   // change flag of the last pass, assigned count, dropped count
             if (!dev) HIPCHK(hipMemcpyAsync(mvp, mvp_d, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipMemcpyAsync(cnt, result, 8, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipMemcpyAsync(&ch, changed + pass - 1, 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(st, resb, 12, hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
-            if (ch == 0) return cnt[0] - cnt[1];
+            if (st[0] == 0) return st[1] - st[2];
         }
     }
     const int chunk = 2;   // passes launched between host checks (two-camera frames)
@@ -1424,14 +1450,15 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
             hipLaunchKernelGGL(k_sbp_proj2, gq, dim3(MT_NT), 0, s, fr, (const orbfe_proj_point*)q, ruv, nq, th, a0,
                                a1, b0, first, assign, changed + pass);
         }
-        int ch = 0;
-        HIPCHK(hipMemcpyAsync(&ch, changed + pass - 1, 4, hipMemcpyDeviceToHost, s));
+        int* ch = t_ms.hs;   // pinned: a pageable 4-byte read back costs more than the passes
+        HIPCHK(hipMemcpyAsync(ch, changed + pass - 1, 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        if (ch == 0) break;
+        if (*ch == 0) break;
     }
     commit(nullptr);
     HIPCHK(hipGetLastError());
     timer.end();
+    int* cnt = t_ms.hs;
     if (!dev) HIPCHK(hipMemcpyAsync(mvp, mvp_d, (size_t)n * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(cnt, result, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
