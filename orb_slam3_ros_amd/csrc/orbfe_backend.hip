@@ -411,8 +411,9 @@ int orbfe_search_by_bow_kf(const orbfe_keypoint* keys1, const uint8_t* desc1, co
     timer.end();
     int nm = 0;
     HIPCHK(hipMemcpyAsync(out12, ms_ptr<int>(o_out), (size_t)n1 * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&nm, ms_ptr<int>(o_res), 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(t_ms.hs, ms_ptr<int>(o_res), 4, hipMemcpyDeviceToHost, s));   // pinned
     HIPCHK(hipStreamSynchronize(s));
+    nm = t_ms.hs[0];
     return nm;
 }
 
@@ -554,8 +555,9 @@ int orbfe_search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, c
     timer.end();
     int nm = 0;
     HIPCHK(hipMemcpyAsync(matches12, ms_ptr<int>(o_out), (size_t)n1 * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&nm, ms_ptr<int>(o_res), 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(t_ms.hs, ms_ptr<int>(o_res), 4, hipMemcpyDeviceToHost, s));   // pinned
     HIPCHK(hipStreamSynchronize(s));
+    nm = t_ms.hs[0];
     return nm;
 }
 
@@ -599,8 +601,9 @@ int orbfe_fuse(const orbfe_frame* KF, const orbfe_kf_camera* cam, const float* i
     int nf = 0;
     HIPCHK(hipMemcpyAsync(best_idx, ms_ptr<int>(o_as), (size_t)n * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(best_dist, ms_ptr<int>(o_ds), (size_t)n * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&nf, ms_ptr<int>(o_cnt), 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(t_ms.hs, ms_ptr<int>(o_cnt), 4, hipMemcpyDeviceToHost, s));   // pinned
     HIPCHK(hipStreamSynchronize(s));
+    nf = t_ms.hs[0];
     return nf;
 }
 
@@ -665,8 +668,9 @@ int orbfe_search_by_projection_sim3(const orbfe_frame* KF, const orbfe_kf_camera
                                max_acc, ms_ptr<const int>(o_b0), first, assign, (int*)nullptr, changed + pass);
         }
         int ch = 0;
-        HIPCHK(hipMemcpyAsync(&ch, changed + pass - 1, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(t_ms.hs, changed + pass - 1, 4, hipMemcpyDeviceToHost, s));   // pinned
         HIPCHK(hipStreamSynchronize(s));
+        ch = t_ms.hs[0];
         if (ch == 0) break;
     }
     HIPCHK(hipMemsetAsync(ms_ptr<int>(o_cnt), 0, 4, s));
@@ -678,8 +682,9 @@ int orbfe_search_by_projection_sim3(const orbfe_frame* KF, const orbfe_kf_camera
     int nm = 0;
     HIPCHK(hipMemcpyAsync(matched, ms_ptr<int32_t>(o_m), (size_t)nk * 4, hipMemcpyDeviceToHost, s));
     if (point_kfs) HIPCHK(hipMemcpyAsync(matched_kf, ms_ptr<int32_t>(o_mk), (size_t)nk * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&nm, ms_ptr<int>(o_cnt), 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(t_ms.hs, ms_ptr<int>(o_cnt), 4, hipMemcpyDeviceToHost, s));   // pinned
     HIPCHK(hipStreamSynchronize(s));
+    nm = t_ms.hs[0];
     return nm;
 }
 
@@ -753,8 +758,9 @@ int orbfe_search_by_sim3(const orbfe_frame* KF1, const orbfe_frame* KF2, const o
     timer.end();
     int nf = 0;
     HIPCHK(hipMemcpyAsync(matches12, ms_ptr<int32_t>(o_m12), (size_t)n1 * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&nf, ms_ptr<int>(o_cnt), 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(t_ms.hs, ms_ptr<int>(o_cnt), 4, hipMemcpyDeviceToHost, s));   // pinned
     HIPCHK(hipStreamSynchronize(s));
+    nf = t_ms.hs[0];
     return nf;
 }
 

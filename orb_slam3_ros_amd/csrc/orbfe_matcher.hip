@@ -1364,8 +1364,9 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
         hipLaunchKernelGGL(k_frustum, dim3((nq + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, cd,
                            (const orbfe_map_point_3d*)q, nq, ms_ptr<orbfe_map_point>(o_track), ntm);
         int h_ntm = 0;
-        HIPCHK(hipMemcpyAsync(&h_ntm, ntm, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(t_ms.hs, ntm, 4, hipMemcpyDeviceToHost, s));   // pinned
         HIPCHK(hipStreamSynchronize(s));
+        h_ntm = t_ms.hs[0];
         if (fin->n_to_match) *fin->n_to_match = h_ntm;
         if (h_ntm <= 0) return 0;
         q = ms_ptr<const uint8_t>(o_track);
@@ -1547,8 +1548,9 @@ int orbfe_search_for_initialization(const orbfe_frame* F1, const orbfe_frame* F2
                                ms_ptr<const int>(o_nsel), assign, adist, changed + pass);
         }
         int ch = 0;
-        HIPCHK(hipMemcpyAsync(&ch, changed + pass - 1, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(t_ms.hs, changed + pass - 1, 4, hipMemcpyDeviceToHost, s));   // pinned
         HIPCHK(hipStreamSynchronize(s));
+        ch = t_ms.hs[0];
         if (ch == 0) break;
     }
     hipLaunchKernelGGL(k_init_commit, dim3(1), dim3(1024), 0, s, v1, v2, assign, checkOri, ms_ptr<float>(o_prev),
@@ -1558,8 +1560,9 @@ int orbfe_search_for_initialization(const orbfe_frame* F1, const orbfe_frame* F2
     int nm = 0;
     HIPCHK(hipMemcpyAsync(matches12, ms_ptr<int>(o_m12), (size_t)n1 * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(prev_matched, ms_ptr<float>(o_prev), (size_t)n1 * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&nm, ms_ptr<int>(o_result), 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(t_ms.hs, ms_ptr<int>(o_result), 4, hipMemcpyDeviceToHost, s));   // pinned
     HIPCHK(hipStreamSynchronize(s));
+    nm = t_ms.hs[0];
     return nm;
 }
 
@@ -1629,8 +1632,9 @@ int orbfe_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, c
     timer.end();
     int nm = 0;
     HIPCHK(hipMemcpyAsync(out, ms_ptr<int>(o_out), (size_t)fn * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&nm, ms_ptr<int>(o_result), 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(t_ms.hs, ms_ptr<int>(o_result), 4, hipMemcpyDeviceToHost, s));   // pinned
     HIPCHK(hipStreamSynchronize(s));
+    nm = t_ms.hs[0];
     return nm;
 }
 
@@ -1743,8 +1747,9 @@ int orbfe_is_in_frustum(const orbfe_frame* F, const orbfe_camera* cam, const orb
     int h_ntm = 0;
     HIPCHK(hipMemcpyAsync(track, ms_ptr<orbfe_map_point>(o_track), (size_t)n * sizeof(orbfe_map_point),
                           hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&h_ntm, ntm, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(t_ms.hs, ntm, 4, hipMemcpyDeviceToHost, s));   // pinned
     HIPCHK(hipStreamSynchronize(s));
+    h_ntm = t_ms.hs[0];
     return h_ntm;
 }
 
