@@ -413,6 +413,9 @@ __device__ __forceinline__ int fast_M(const uint8_t* im, int stride, int x, int 
 #ifndef FAST_CPW
 #define FAST_CPW 4    // cells per wave (the next cell's ROI is prefetched into registers)
 #endif
+#ifndef FAST_P1_PAIR
+#define FAST_P1_PAIR 1   // pass 1 evaluates two row blocks per loop iteration
+#endif
 #define FAST_PF 4     // prefetched 16-byte chunks per lane (rows / rows-per-load: 2 at W = 35)
 struct FastCell {
     int l, local, ci, cj, r0, c0, rows, cols, pitch;
@@ -591,62 +594,72 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
             const int valid4 = min(4, dw - 4 * lg);
             // flag bits of pixel k: 2k + 1 = dark possible, 2k = bright possible
             const uint32_t vmask = ly < rpi && valid4 > 0 ? (1u << (2 * valid4)) - 1u : 0u;
-            for (int y0 = 0; y0 < dh; y0 += rpi) {
-                const int y = y0 + ly;
-                uint32_t m8 = 0;
-                if (vmask && y < dh) {
-                    // centre pixels k = 0..3 at ROI (y + 3, 4 lg + 3 + k) = byte 4 lg + 4 + k of the row
-                    const uint8_t* cp = s_img + (y + 3) * RS + 4 * lg + 4;
-                    const uint32_t cw = *(const uint32_t*)cp;
-                    // aligned dwords + v_alignbyte: unaligned ds_read_b32 measured 40 % slower for the kernel
-                    const uint32_t* r0p = (const uint32_t*)cp - 1;   // dword of ROI columns 4 lg - 1 ..
-                    const uint32_t c0w = r0p[0], c2w = r0p[2];
-                    // ring samples as (hi, lo, byte shift): the 4 bytes of sample k are bytes s .. s + 3 of
-                    // hi:lo, so one v_perm per parity picks its even / odd pixels as f16 halves directly
-                    const uint32_t ph[8] = {0u, 0u, c2w, cw, r0p[2 * nd + 2], r0p[-2 * nd + 1], r0p[-2 * nd + 2], r0p[2 * nd + 1]};
-                    const uint32_t pl[8] = {r0p[3 * nd + 1], r0p[-3 * nd + 1], cw, c0w,          // (0, 3), (0, -3), (3, 0), (-3, 0)
-                                            r0p[2 * nd + 1], r0p[-2 * nd], r0p[-2 * nd + 1], r0p[2 * nd]};   // (2, 2), (-2, -2), (2, -2), (-2, 2)
-                    constexpr uint32_t psh[8] = {0, 0, 3, 1, 2, 2, 2, 2};
-                    uint32_t sd[2], sb[2];
+            // the test for the lane's 4 pixels of ROI row y + 3
+            auto pretest = [&](int y) -> uint32_t {
+                if (!(vmask && y < dh)) return 0u;
+                // centre pixels k = 0..3 at ROI (y + 3, 4 lg + 3 + k) = byte 4 lg + 4 + k of the row
+                const uint8_t* cp = s_img + (y + 3) * RS + 4 * lg + 4;
+                const uint32_t cw = *(const uint32_t*)cp;
+                // aligned dwords + v_alignbyte: unaligned ds_read_b32 measured 40 % slower for the kernel
+                const uint32_t* r0p = (const uint32_t*)cp - 1;   // dword of ROI columns 4 lg - 1 ..
+                const uint32_t c0w = r0p[0], c2w = r0p[2];
+                // ring samples as (hi, lo, byte shift): the 4 bytes of sample k are bytes s .. s + 3 of
+                // hi:lo, so one v_perm per parity picks its even / odd pixels as f16 halves directly
+                const uint32_t ph[8] = {0u, 0u, c2w, cw, r0p[2 * nd + 2], r0p[-2 * nd + 1], r0p[-2 * nd + 2], r0p[2 * nd + 1]};
+                const uint32_t pl[8] = {r0p[3 * nd + 1], r0p[-3 * nd + 1], cw, c0w,          // (0, 3), (0, -3), (3, 0), (-3, 0)
+                                        r0p[2 * nd + 1], r0p[-2 * nd], r0p[-2 * nd + 1], r0p[2 * nd]};   // (2, 2), (-2, -2), (2, -2), (-2, 2)
+                constexpr uint32_t psh[8] = {0, 0, 3, 1, 2, 2, 2, 2};
+                uint32_t sd[2], sb[2];
 #pragma unroll
-                    for (int par = 0; par < 2; par++) {
-                        const uint32_t sel = par ? 0x0c030c01u : 0x0c020c00u;
-                        const orbfe_half2 v = px_h2(cw, sel);
-                        // dark possible  <=> every pair has a member < v - t <=> max_k min(pair k) < v - t
-                        // bright possible <=> every pair has a member > v + t <=> min_k max(pair k) > v + t
-                        orbfe_half2 mn[4], mx[4];
+                for (int par = 0; par < 2; par++) {
+                    const uint32_t sel = par ? 0x0c030c01u : 0x0c020c00u;
+                    const orbfe_half2 v = px_h2(cw, sel);
+                    // dark possible  <=> every pair has a member < v - t <=> max_k min(pair k) < v - t
+                    // bright possible <=> every pair has a member > v + t <=> min_k max(pair k) > v + t
+                    orbfe_half2 mn[4], mx[4];
 #pragma unroll
-                        for (int k = 0; k < 4; k++) {
-                            const uint32_t sa = 0x0c000c00u | (psh[2 * k] + par) | ((psh[2 * k] + par + 2) << 16);
-                            const uint32_t sb2 = 0x0c000c00u | (psh[2 * k + 1] + par) | ((psh[2 * k + 1] + par + 2) << 16);
-                            const orbfe_half2 xa = as_h2(__builtin_amdgcn_perm(ph[2 * k], pl[2 * k], sa));
-                            const orbfe_half2 xb = as_h2(__builtin_amdgcn_perm(ph[2 * k + 1], pl[2 * k + 1], sb2));
-                            mn[k] = hmin(xa, xb);
-                            mx[k] = hmax(xa, xb);
-                        }
-                        const orbfe_half2 D = hmax(hmax(hmax(mn[0], mn[1]), mn[2]), mn[3]);
-                        const orbfe_half2 B = hmin(hmin(hmin(mx[0], mx[1]), mx[2]), mx[3]);
-                        // exact differences: the sign bit of each half is the flag
-                        sd[par] = h2_bits(D - (v - tv));
-                        sb[par] = h2_bits((v + tv) - B);
+                    for (int k = 0; k < 4; k++) {
+                        const uint32_t sa = 0x0c000c00u | (psh[2 * k] + par) | ((psh[2 * k] + par + 2) << 16);
+                        const uint32_t sb2 = 0x0c000c00u | (psh[2 * k + 1] + par) | ((psh[2 * k + 1] + par + 2) << 16);
+                        const orbfe_half2 xa = as_h2(__builtin_amdgcn_perm(ph[2 * k], pl[2 * k], sa));
+                        const orbfe_half2 xb = as_h2(__builtin_amdgcn_perm(ph[2 * k + 1], pl[2 * k + 1], sb2));
+                        mn[k] = hmin(xa, xb);
+                        mx[k] = hmax(xa, xb);
                     }
-                    // sign bytes -> pixel order (byte k = pixel k), dark at bit 7, bright at bit 6,
-                    // then gathered into bits 2k + 1 / 2k by one dot product
-                    const uint32_t A = __builtin_amdgcn_perm(sd[1], sd[0], 0x07030501u);
-                    const uint32_t Bq = __builtin_amdgcn_perm(sb[1], sb[0], 0x07030501u);
-                    const uint32_t F = (A & 0x80808080u) | ((Bq >> 1) & 0x40404040u);
-                    m8 = __builtin_amdgcn_udot4(F >> 6, 0x40100401u, 0u, false) & vmask;
+                    const orbfe_half2 D = hmax(hmax(hmax(mn[0], mn[1]), mn[2]), mn[3]);
+                    const orbfe_half2 B = hmin(hmin(hmin(mx[0], mx[1]), mx[2]), mx[3]);
+                    // exact differences: the sign bit of each half is the flag
+                    sd[par] = h2_bits(D - (v - tv));
+                    sb[par] = h2_bits((v + tv) - B);
                 }
-                // 4-pixel groups with any candidate, compacted row-major (iteration-major,
-                // then lane order): dy << 7 | dx0 in bits 0-13, flags in bits 16-23 (pixel k:
-                // bit 17 + 2k dark, 16 + 2k bright)
+                // sign bytes -> pixel order (byte k = pixel k), dark at bit 7, bright at bit 6,
+                // then gathered into bits 2k + 1 / 2k by one dot product
+                const uint32_t A = __builtin_amdgcn_perm(sd[1], sd[0], 0x07030501u);
+                const uint32_t Bq = __builtin_amdgcn_perm(sb[1], sb[0], 0x07030501u);
+                const uint32_t F = (A & 0x80808080u) | ((Bq >> 1) & 0x40404040u);
+                return __builtin_amdgcn_udot4(F >> 6, 0x40100401u, 0u, false) & vmask;
+            };
+            // 4-pixel groups with any candidate, compacted row-major (iteration-major, then lane
+            // order): dy << 7 | dx0 in bits 0-13, flags in bits 16-23 (pixel k: bit 17 + 2k dark,
+            // 16 + 2k bright)
+            auto compact = [&](int y, uint32_t m8) {
                 const unsigned long long gm = __ballot(m8 != 0u);
                 if (m8)
                     s_grp[ngrp + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(gm >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)gm, 0u))] =
                         (uint32_t)((y << 7) | (4 * lg)) | (m8 << 16);
                 ngrp += __popcll(gm);
+            };
+#if FAST_P1_PAIR
+            // two row blocks per iteration: both blocks' LDS reads issue before either's compute
+            for (int y0 = 0; y0 < dh; y0 += 2 * rpi) {
+                const uint32_t ma = pretest(y0 + ly), mb = pretest(y0 + rpi + ly);
+                compact(y0 + ly, ma);
+                if (y0 + rpi < dh) compact(y0 + rpi + ly, mb);
             }
+#else
+            for (int y0 = 0; y0 < dh; y0 += rpi) compact(y0 + ly, pretest(y0 + ly));
+#endif
         }
         WAVE_SYNC();
         // expand the groups into entries, one per (pixel, possible sign): dy << 7 | dx, bit 14 =
@@ -837,7 +850,9 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
 // winner is the first max-response key in key order, i.e. max(score) then min(index)
 // (ORBextractor.cc:757-776).
 // ---------------------------------------------------------------------------------------------
+#ifndef OCT_NT
 #define OCT_NT 256
+#endif
 #define OCT_U 4
 // expandable node: (size << 44) | (UL.x << 32) | list position; compareNodes orders by the high 32 bits
 struct ExpLess64 {
