@@ -372,6 +372,20 @@ static int build_geom(const orbfe_extractor* h, int W, int H, OrbGeom& g, std::v
             if (!rows_fit(tr) || !cols_fit(tc)) return ORBFE_E_ARG;
             L.rz_rows = tr;
             L.rz_cols = tc;
+            // k_resize_s rules: in every lane group of 4 output columns, columns 0, 1 take their
+            // byte pair at sx - (sx_0 & ~3) in [0, 6], columns 2, 3 at that offset - 2 in [0, 6];
+            // every output row reads rows (s - 1, s), the table never clipping, for distinct s
+            L.rs_ok = 1;
+            for (int xq = 0; xq < L.w && L.rs_ok; xq += 4) {
+                const int base = tx[3 * xq] & ~3;
+                for (int q = 0; q < 4 && xq + q < L.w; q++) {
+                    const int off = tx[3 * (xq + q)] - base - (q >= 2 ? 2 : 0);
+                    if (off < 0 || off > 6) L.rs_ok = 0;
+                }
+            }
+            for (int y = 0; y < L.h && L.rs_ok; y++)
+                if (ty[4 * y + 1] != ty[4 * y] + 1 || (y > 0 && ty[4 * y + 1] == ty[4 * (y - 1) + 1])) L.rs_ok = 0;
+            L.rs_rows = std::min(RS_ROWS, 64);
         }
         pw = L.w;
         ph = L.h;
@@ -380,7 +394,8 @@ static int build_geom(const orbfe_extractor* h, int W, int H, OrbGeom& g, std::v
     g.cellkeys_per_img = cellkey_off;
     g.out_per_img = out_off;
     g.kp_cap = out_off;
-    g.pyr_bytes = round_up(std::max(pyr_off, 256), 256);
+    g.pyr_slack = pyr_off;
+    g.pyr_bytes = round_up(pyr_off + 256, 256);
     g.max_cells_level = max_cells;
     g.node_cap = node_cap;
     fl.wave_bytes = fl.roi + fl.sc + fl.cor + FAST_ENT_BYTES;
@@ -552,6 +567,9 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
 #ifndef FAST_MID
 #define FAST_MID 4   // FAST of levels [1, FAST_MID) runs on the side stream once resize has built them
 #endif
+#ifndef RZ_STREAM
+#define RZ_STREAM 1  // 0: every level with the LDS-tiled k_resize (A/B builds)
+#endif
         // side stream: FAST of level 0 at once, then of levels [1, lmid) when the chain has built
         // them (beside the chain's short, latency-bound top-level launches); batch stream: the
         // chain, then FAST of levels [lmid, nlevels)
@@ -559,11 +577,22 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
         HIPCHK(hipEventRecord(h->ev_fork[0], s));
         HIPCHK(hipStreamWaitEvent(s2, h->ev_fork[0], 0));
         fast_range(s2, 0, 1);
-        // ComputePyramid: one k_resize launch per level (level l from level l - 1)
+        // k_resize_s reads dwords: level 0 must be 4-byte aligned (else k_resize builds level 1)
+        bool al0 = (pitch & 3) == 0;
+        for (int i = 0; al0 && i < B; i++) al0 = (((uintptr_t)host_ptrs[i]) & 3) == 0;
+        // ComputePyramid: one launch per level (level l from level l - 1); the row-streamed k_resize_s
+        // unless the level's column windows break its rules (then the LDS-tiled k_resize)
         for (int l = 1; l < g.nlevels; l++) {
-            const int tiles_y = (g.lv[l].h + g.lv[l].rz_rows - 1) / g.lv[l].rz_rows;
-            dim3 grid((g.lv[l].w + g.lv[l].rz_cols - 1) / g.lv[l].rz_cols, (tiles_y + RZ_TPB - 1) / RZ_TPB, B);
-            hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, s, P, pitch, h->d_pyr, g.pyr_bytes, h->d_tab, g, l);
+            const OrbLevel& L = g.lv[l];
+            if (RZ_STREAM && L.rs_ok && (l > 1 || al0)) {
+                const int nstrips = (L.w + RS_COLS - 1) / RS_COLS, nitems = nstrips * ((L.h + L.rs_rows - 1) / L.rs_rows);
+                hipLaunchKernelGGL(k_resize_s, dim3((nitems + 3) / 4, B), dim3(256), 0, s, P, pitch, h->d_pyr,
+                                   g.pyr_bytes, h->d_tab, g, l, nstrips, nitems);
+            } else {
+                const int tiles_y = (L.h + L.rz_rows - 1) / L.rz_rows;
+                dim3 grid((L.w + L.rz_cols - 1) / L.rz_cols, (tiles_y + RZ_TPB - 1) / RZ_TPB, B);
+                hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, s, P, pitch, h->d_pyr, g.pyr_bytes, h->d_tab, g, l);
+            }
             if (l + 1 == lmid) {
                 HIPCHK(hipEventRecord(h->ev_fork[2], s));
                 HIPCHK(hipStreamWaitEvent(s2, h->ev_fork[2], 0));

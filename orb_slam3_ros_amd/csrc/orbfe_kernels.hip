@@ -14,6 +14,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "brief_pattern.h"
 #include "glibc_sincosf.h"
 #include "orbfe_types.h"
@@ -351,6 +353,161 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
             }
         }
         SYNC();   // s_src / s_h / s_ty are refilled for the next tile
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1b: the same level build as k_resize (same tables, xmax and simd_end rules, bit-identical
+// output), streamed by rows with no LDS and no barrier. One wave owns a strip of 256 output
+// columns (4 adjacent ones per lane) and a chunk of rs_rows output rows, and walks the chunk's
+// source rows in order:
+//  - a source row is 3 aligned dwords per lane from (sx_0 & ~3), the window holding the byte pairs
+//    (S[sx_q], S[sx_q + 1]) of the lane's 4 columns; RS_D rows of loads are in flight;
+//  - the horizontal sum of a column is one v_perm (the byte pair as u16x2) and one
+//    v_dot2_u32_u16 with the packed coefficients (a0 << 4, a1 << 4): H << 4, as k_resize stores it;
+//  - an output row is finished when its second source row is in (rows s - 1, s);
+//  - every row step stores exactly one dword per lane, unconditionally (a step that finishes no
+//    output row, and a lane past the width, store to the image's slack area): with a static store
+//    count per step the compiler waits for a row's loads without draining later stores.
+// Host-checked per level (OrbLevel::rs_ok): columns 0, 1 take their pair from bytes 0..7 of the
+// window, columns 2, 3 from bytes 2..9; every output row reads rows (s - 1, s) for distinct s (the
+// table never clips). Bytes at or past the source width only ever meet a zero coefficient, so a
+// dword that would cross the row pitch is read from the row's last dword instead.
+// ---------------------------------------------------------------------------------------------
+#ifndef RS_D
+#define RS_D 2               // source rows of loads in flight per wave (the loop body's unroll;
+                             // measured: 1-6 within 3 %, deeper is slower)
+#endif
+#ifndef RS_ROWS
+#define RS_ROWS 16           // output rows per wave (<= 64: one table row per lane)
+#endif
+#define RS_COLS 256          // output columns per wave strip
+typedef unsigned short orbfe_ushort2_rs __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(256) void k_resize_s(const uint8_t* const* imgs, int in_pitch, uint8_t* pyr,
+                                                  int pyr_stride, const int16_t* __restrict__ tab, OrbGeom g, int l,
+                                                  int nstrips, int nitems) {
+    const OrbLevel& L = g.lv[l];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
+    const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
+    const int bx = lb % gridDim.x, b = lb / gridDim.x;
+    const int item = bx * 4 + wave;
+    if (item >= nitems) return;
+    const int chunk = item / nstrips, strip = item - chunk * nstrips;
+    const int y0 = chunk * L.rs_rows, y1 = min(y0 + L.rs_rows, L.h);
+    int spitch;
+    gptr_u8 src = level_base(imgs, in_pitch, pyr, pyr_stride, g, b, l - 1, &spitch);
+    uint8_t* dst = pyr + (size_t)b * pyr_stride + L.pyr_off;
+    const int16_t* tx = tab + L.tab_x;
+    const int16_t* ty = tab + L.tab_y;
+    const int xq = strip * RS_COLS + 4 * lane;
+    const bool act = xq < L.w;
+    // the lane's columns: v_perm selectors, packed coefficients, stored-sum masks
+    const int base = tx[3 * min(xq, L.w - 1)] & ~3;
+    uint32_t sel[4], coef[4], hmask[4];
+    bool vec[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int x = min(xq + q, L.w - 1);
+        const bool lin = x < L.xmax;
+        const uint32_t a0 = lin ? (uint32_t)tx[3 * x + 1] : 2048u, a1 = lin ? (uint32_t)tx[3 * x + 2] : 0u;
+        const uint32_t off = (uint32_t)(tx[3 * x] - base) - (q >= 2 ? 2u : 0u);
+        sel[q] = 0x0c000c00u | (off & 7u) | (((off + 1u) & 7u) << 16);
+        coef[q] = (a0 << 4) | (a1 << 20);
+        vec[q] = x < L.simd_end;
+        hmask[q] = vec[q] ? 0xFFFF00u : 0xFFFFFFFFu;
+    }
+    const bool lv_all = !act || (vec[0] && vec[1] && vec[2] && vec[3]);
+    // the chunk's vertical table rows, one per lane: (sy + 1, b0 << 8, b1 << 8) of row y0 + lane
+    int t_s0 = 0, t_r1 = 0, t_b0 = 0, t_b1 = 0;
+    if (y0 + lane < y1) {
+        const int16_t* tr = ty + 4 * (y0 + lane);
+        t_s0 = tr[0];
+        t_r1 = tr[1];
+        t_b0 = (int)tr[2] << 8;
+        t_b1 = (int)tr[3] << 8;
+    }
+    const int s_lo = __builtin_amdgcn_readfirstlane(t_s0);
+    const int s_hi = ty[4 * (y1 - 1) + 1];
+    int y = y0;
+    int r1 = __builtin_amdgcn_readfirstlane(t_r1);
+    uint32_t b0s = (uint32_t)__builtin_amdgcn_readfirstlane(t_b0), b1s = (uint32_t)__builtin_amdgcn_readfirstlane(t_b1);
+    uint8_t* drow = dst + (size_t)y0 * L.pitch + xq;
+    uint32_t* slack = (uint32_t*)(pyr + (size_t)b * pyr_stride + g.pyr_slack) + lane;
+    uint32_t Hp[4] = {0u, 0u, 0u, 0u};
+    // one source row s (window dwords w0..w2): its horizontal sums, then the output row whose
+    // second source row is s, if any
+    auto step = [&](int s, uint32_t w0, uint32_t w1, uint32_t w2) {
+        // bytes 2..9 of the window for columns 2, 3
+        const uint32_t c0 = __builtin_amdgcn_alignbyte(w1, w0, 2u), c1 = __builtin_amdgcn_alignbyte(w2, w1, 2u);
+        uint32_t Hc[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t pr = q < 2 ? __builtin_amdgcn_perm(w1, w0, sel[q]) : __builtin_amdgcn_perm(c1, c0, sel[q]);
+            Hc[q] = __builtin_amdgcn_udot2(__builtin_bit_cast(orbfe_ushort2_rs, pr),
+                                           __builtin_bit_cast(orbfe_ushort2_rs, coef[q]), 0u, false) &
+                    hmask[q];
+        }
+        const bool fin = r1 == s;
+        uint32_t packed = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            packed |= ((mulhi_u24(Hp[q], b0s) + mulhi_u24(Hc[q], b1s) + 2u) >> 2) << (8 * q);
+        if (!lv_all) {   // the lane holding the level's scalar-tail columns (>= simd_end)
+            const uint32_t b0 = b0s >> 8, b1 = b1s >> 8;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t vl = (__umul24(Hp[q] >> 4, b0) + __umul24(Hc[q] >> 4, b1) + (1u << 21)) >> 22;
+                const uint32_t m = vec[q] ? 0u : 0xFFu << (8 * q);
+                packed = (packed & ~m) | ((vl << (8 * q)) & m);
+            }
+        }
+        // a whole dword even for the level's last, partial group: the bytes past the width land
+        // in the row's pitch padding, which nothing reads as pixels
+        *(uint32_t*)(fin && act ? (uint32_t*)drow : slack) = packed;
+        if (fin) {
+            drow += L.pitch;
+            if (++y == y1) {
+                r1 = -1;
+            } else {
+                const int k = y - y0;
+                r1 = __builtin_amdgcn_readlane(t_r1, k);
+                b0s = (uint32_t)__builtin_amdgcn_readlane(t_b0, k);
+                b1s = (uint32_t)__builtin_amdgcn_readlane(t_b1, k);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) Hp[q] = Hc[q];
+    };
+    // dword loads: the host launches this kernel only on 4-byte aligned rows (the pyramid always;
+    // level 0 when the caller's images are, else k_resize builds level 1). A loop over blocks of
+    // RS_D rows, each unrolled (static buffer indices, small code). Loads run RS_D rows ahead,
+    // unconditionally (clamped to the last row); the steps past the last row finish no output row.
+    // The prologue issues the loop's (loads, store) pattern per row, in order, so the loop entry
+    // and its back edge present the same outstanding counts.
+    int doff[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) doff[k] = min(base + 4 * k, spitch - 4);
+    auto ld = [&](int s, uint32_t (&w)[3]) {
+        gptr_u8 rp = src + (size_t)s * spitch;
+#pragma unroll
+        for (int k = 0; k < 3; k++) w[k] = *(const ORBFE_GLOBAL uint32_t*)(rp + doff[k]);
+    };
+    uint32_t buf[RS_D][3];
+#pragma unroll
+    for (int d = 0; d < RS_D; d++) {
+        ld(min(s_lo + d, s_hi), buf[d]);
+        *slack = 0u;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    for (int sb = s_lo; sb <= s_hi; sb += RS_D) {
+#pragma unroll
+        for (int d = 0; d < RS_D; d++) {
+            const uint32_t w0 = buf[d][0], w1 = buf[d][1], w2 = buf[d][2];
+            ld(min(sb + RS_D + d, s_hi), buf[d]);
+            // keep the loads here: the scheduler would otherwise sink them next to their use
+            __builtin_amdgcn_sched_barrier(0);
+            step(sb + d, w0, w1, w2);
+        }
     }
 }
 
