@@ -37,8 +37,12 @@ def remap_linear_batch(src, mapx, mapy, out, stream=None):
         stream = torch.cuda.current_stream(src.device).cuda_stream
     if src.stride(2) != 1 or out.stride(2) != 1 or not mapx.is_contiguous() or not mapy.is_contiguous():
         raise ValueError("remap_linear_batch needs row-contiguous images and contiguous maps")
-    ps = (ctypes.c_void_p * n)(*[src[i].data_ptr() for i in range(n)])
-    pd = (ctypes.c_void_p * n)(*[out[i].data_ptr() for i in range(n)])
+    # per-image base pointers by arithmetic (one data_ptr() per tensor, not per image)
+    idx = np.arange(n, dtype=np.uint64)
+    src_ptrs = np.uint64(src.data_ptr()) + idx * np.uint64(src.stride(0) * src.element_size())
+    dst_ptrs = np.uint64(out.data_ptr()) + idx * np.uint64(out.stride(0) * out.element_size())
+    ps = src_ptrs.ctypes.data_as(ctypes.POINTER(ctypes.c_void_p))
+    pd = dst_ptrs.ctypes.data_as(ctypes.POINTER(ctypes.c_void_p))
     _lib.check(lib.orbfe_remap_linear_batch(ps, src.shape[2], src.shape[1], src.stride(1), mapx.data_ptr(),
                                             mapy.data_ptr(), out.shape[2], out.shape[1], pd, out.stride(1), n,
                                             stream), "remap_linear_batch")
