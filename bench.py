@@ -600,7 +600,7 @@ def main():
         n_img = 2 * F
         pyr_fast_ms = stages["pyramid_fast"]
         pf_kernel = ("pyramid+FAST pass, fused: k_pyrfast x8 levels (FAST of level l + resize of level l+1)"
-                     if fe.path() == 0 else "pyramid+FAST pass: k_resize x7 + k_fast")
+                     if fe.path() == 0 else "pyramid+FAST pass: k_resize_s x7 + k_fast")
         bytes_img = algorithmic_bytes(W, H)
         achieved = n_img * bytes_img / (pyr_fast_ms * 1e-3) / 1e9 if pyr_fast_ms > 0 else 0.0
         dominant = max(stages, key=stages.get)
@@ -663,14 +663,16 @@ def main():
             # wave64 issue peak, 1024 SIMD-32s x 2.4 GHz / 2 cycles), and for the pyramid+FAST pass as
             # timed in this run
             vk = valu[0]
+            # the pyramid kernels: k_resize_s (row-streamed, the default) and / or k_resize (LDS-tiled)
+            pyr_k = [k for k in vk if k.startswith("k_resize")]
             result["roofline"]["valu_issue_frac"] = {k: v["valu_issue_frac"] for k, v in vk.items()
-                                                     if k in ("k_resize", "k_fast", "k_octree", "k_describe",
-                                                              "k_stereo")}
-            if "k_resize" in vk and "k_fast" in vk and pyr_fast_ms > 0:
+                                                     if k in pyr_k or k in ("k_fast", "k_octree", "k_describe",
+                                                                            "k_stereo")}
+            if pyr_k and "k_fast" in vk and pyr_fast_ms > 0:
                 result["roofline"]["valu_issue_frac_pass"] = round(
-                    (vk["k_resize"]["valu_per_step"] + vk["k_fast"]["valu_per_step"]) / (pyr_fast_ms * 1e-3)
-                    / VALU_ISSUE_PEAK, 4)
-            result["roofline"]["wave_states"] = {k: vk[k]["wave_state"] for k in ("k_resize", "k_fast") if k in vk}
+                    (sum(vk[k]["valu_per_step"] for k in pyr_k) + vk["k_fast"]["valu_per_step"])
+                    / (pyr_fast_ms * 1e-3) / VALU_ISSUE_PEAK, 4)
+            result["roofline"]["wave_states"] = {k: vk[k]["wave_state"] for k in pyr_k + ["k_fast"] if k in vk}
             result["roofline"]["valu_source"] = valu[1]
         if cache is not None and "k_describe" in cache[0]:
             kd = cache[0]["k_describe"]

@@ -74,7 +74,7 @@ def main():
                       "fetch_kb_raw_per_step": round(v.get("FETCH_SIZE", 0.0) / runs, 1),
                       "read_bytes_per_step": int(2 * 1024 * v.get("FETCH_SIZE", 0.0) / runs),
                       "write_bytes_per_step": int(1024 * v.get("WRITE_SIZE", 0.0) / runs)}
-    pf = [traffic[k] for k in ("k_resize", "k_fast") if k in traffic]
+    pf = [traffic[k] for k in traffic if k.startswith("k_resize") or k == "k_fast"]
     t = dict(hdr, source="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE --kernel-trace (separate passes)",
              correction="read = 2 x FETCH_SIZE(KB) x 1024 (gfx950 streaming-read factor); write = WRITE_SIZE x 1024",
              kernels=traffic,
