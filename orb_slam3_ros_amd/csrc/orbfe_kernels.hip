@@ -375,8 +375,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
 // dword that would cross the row pitch is read from the row's last dword instead.
 // ---------------------------------------------------------------------------------------------
 #ifndef RS_D
-#define RS_D 2               // source rows of loads in flight per wave (the loop body's unroll;
-                             // measured: 1-6 within 3 %, deeper is slower)
+#define RS_D 3               // rows of loads in flight per wave = RS_D - 1 (the loop body's unroll;
+                             // measured: 1-6 rows within 3 %, deeper is slower)
 #endif
 #ifndef RS_ROWS
 #define RS_ROWS 16           // output rows per wave (<= 64: one table row per lane)
@@ -447,18 +447,22 @@ __global__ __launch_bounds__(256) void k_resize_s(const uint8_t* const* imgs, in
                                            __builtin_bit_cast(orbfe_ushort2_rs, coef[q]), 0u, false) &
                     hmask[q];
         }
-        const bool fin = r1 == s;
+        const bool fin = r1 == s;   // wave-uniform: a step that finishes no row skips the vertical pass
         uint32_t packed = 0;
+        if (fin) {
 #pragma unroll
-        for (int q = 0; q < 4; q++)
-            packed |= ((mulhi_u24(Hp[q], b0s) + mulhi_u24(Hc[q], b1s) + 2u) >> 2) << (8 * q);
-        if (!lv_all) {   // the lane holding the level's scalar-tail columns (>= simd_end)
-            const uint32_t b0 = b0s >> 8, b1 = b1s >> 8;
+            for (int q = 0; q < 4; q++)
+                packed |= ((mulhi_u24(Hp[q], b0s) + mulhi_u24(Hc[q], b1s) + 2u) >> 2) << (8 * q);
+            if (!lv_all) {   // the lane holding the level's scalar-tail columns (>= simd_end)
+                // (H0 b0 + H1 b1 + 2^21) >> 22 on the stored 16 H (unmasked for these columns):
+                // (16 H0 b0 + 16 H1 b1 + 2^25) >> 26 in 64 bits, the same floor
+                const uint64_t b0 = b0s >> 8, b1 = b1s >> 8;
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint32_t vl = (__umul24(Hp[q] >> 4, b0) + __umul24(Hc[q] >> 4, b1) + (1u << 21)) >> 22;
-                const uint32_t m = vec[q] ? 0u : 0xFFu << (8 * q);
-                packed = (packed & ~m) | ((vl << (8 * q)) & m);
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t vl = (uint32_t)(((uint64_t)Hp[q] * b0 + (uint64_t)Hc[q] * b1 + (1ull << 25)) >> 26);
+                    const uint32_t m = vec[q] ? 0u : 0xFFu << (8 * q);
+                    packed = (packed & ~m) | ((vl << (8 * q)) & m);
+                }
             }
         }
         // a whole dword even for the level's last, partial group: the bytes past the width land
@@ -480,33 +484,41 @@ __global__ __launch_bounds__(256) void k_resize_s(const uint8_t* const* imgs, in
     };
     // dword loads: the host launches this kernel only on 4-byte aligned rows (the pyramid always;
     // level 0 when the caller's images are, else k_resize builds level 1). A loop over blocks of
-    // RS_D rows, each unrolled (static buffer indices, small code). Loads run RS_D rows ahead,
-    // unconditionally (clamped to the last row); the steps past the last row finish no output row.
-    // The prologue issues the loop's (loads, store) pattern per row, in order, so the loop entry
-    // and its back edge present the same outstanding counts.
-    int doff[3];
+    // RS_D rows, each unrolled (static buffer indices, small code). A row's buffer is reloaded right
+    // after its step, RS_D rows ahead, unconditionally (clamped to the last row; the steps past the
+    // last row finish no output row), so no buffer is copied. Row address = the scalar row base +
+    // a 32-bit lane offset (the SGPR-base load form, no 64-bit address arithmetic per load). The
+    // prologue issues the loop's (store, loads) pattern per row, in order, so the loop entry and
+    // its back edge present the same outstanding counts.
+    uint32_t doff[3];
 #pragma unroll
-    for (int k = 0; k < 3; k++) doff[k] = min(base + 4 * k, spitch - 4);
+    for (int k = 0; k < 3; k++) doff[k] = (uint32_t)min(base + 4 * k, spitch - 4);
+    // buffer loads: descriptor over the source level (rows of spitch bytes, the same bytes the
+    // clamped offsets always read), row offset s * spitch in soffset
+    const uint64_t sp = (uint64_t)(uintptr_t)src;
+    const uint32_t sp_lo = __builtin_amdgcn_readfirstlane((uint32_t)sp), sp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(sp >> 32));
+    const int sbytes = __builtin_amdgcn_readfirstlane(spitch * g.lv[l - 1].h);
+    const __amdgpu_buffer_rsrc_t srd =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)sp_hi << 32) | sp_lo), (short)0, sbytes, 0x00020000);
     auto ld = [&](int s, uint32_t (&w)[3]) {
-        gptr_u8 rp = src + (size_t)s * spitch;
+        const int so = __builtin_amdgcn_readfirstlane(s * spitch);
 #pragma unroll
-        for (int k = 0; k < 3; k++) w[k] = *(const ORBFE_GLOBAL uint32_t*)(rp + doff[k]);
+        for (int k = 0; k < 3; k++) w[k] = __builtin_amdgcn_raw_buffer_load_b32(srd, (int)doff[k], so, 0);
     };
     uint32_t buf[RS_D][3];
 #pragma unroll
     for (int d = 0; d < RS_D; d++) {
-        ld(min(s_lo + d, s_hi), buf[d]);
         *slack = 0u;
+        ld(min(s_lo + d, s_hi), buf[d]);
         __builtin_amdgcn_sched_barrier(0);
     }
     for (int sb = s_lo; sb <= s_hi; sb += RS_D) {
 #pragma unroll
         for (int d = 0; d < RS_D; d++) {
-            const uint32_t w0 = buf[d][0], w1 = buf[d][1], w2 = buf[d][2];
+            step(sb + d, buf[d][0], buf[d][1], buf[d][2]);
             ld(min(sb + RS_D + d, s_hi), buf[d]);
             // keep the loads here: the scheduler would otherwise sink them next to their use
             __builtin_amdgcn_sched_barrier(0);
-            step(sb + d, w0, w1, w2);
         }
     }
 }
