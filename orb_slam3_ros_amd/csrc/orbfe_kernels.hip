@@ -378,6 +378,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
 #define RS_D 3               // rows of loads in flight per wave = RS_D - 1 (the loop body's unroll;
                              // measured: 1-6 rows within 3 %, deeper is slower)
 #endif
+#ifndef RS_X3
+#define RS_X3 1              // the lane's 12-byte source window as one dwordx3 load (0: 3 dword loads)
+#endif
 #ifndef RS_ROWS
 #define RS_ROWS 16           // output rows per wave (<= 64: one table row per lane)
 #endif
@@ -493,6 +496,7 @@ __global__ __launch_bounds__(256) void k_resize_s(const uint8_t* const* imgs, in
     uint32_t doff[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) doff[k] = (uint32_t)min(base + 4 * k, spitch - 4);
+    const uint32_t win = (uint32_t)min(base, spitch - 4);
     // buffer loads: descriptor over the source level (rows of spitch bytes, the same bytes the
     // clamped offsets always read), row offset s * spitch in soffset
     const uint64_t sp = (uint64_t)(uintptr_t)src;
@@ -502,8 +506,17 @@ __global__ __launch_bounds__(256) void k_resize_s(const uint8_t* const* imgs, in
         __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)sp_hi << 32) | sp_lo), (short)0, sbytes, 0x00020000);
     auto ld = [&](int s, uint32_t (&w)[3]) {
         const int so = __builtin_amdgcn_readfirstlane(s * spitch);
+#if RS_X3
+        // one 12-byte load from the window's first dword; a window that runs past the row's pitch
+        // reads the next row's first bytes (or zeros past the level: the descriptor's range
+        // check), which only ever meet zero coefficients
+        typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+        const u32x3 v = __builtin_bit_cast(u32x3, __builtin_amdgcn_raw_buffer_load_b96(srd, (int)win, so, 0));
+        w[0] = v.x; w[1] = v.y; w[2] = v.z;
+#else
 #pragma unroll
         for (int k = 0; k < 3; k++) w[k] = __builtin_amdgcn_raw_buffer_load_b32(srd, (int)doff[k], so, 0);
+#endif
     };
     uint32_t buf[RS_D][3];
 #pragma unroll
