@@ -83,9 +83,10 @@ __device__ __forceinline__ uint32_t remap_apply(gptr_u8 src, int sstride, const 
 #endif
 
 typedef unsigned short orbfe_ushort2_rm __attribute__((ext_vector_type(2)));
-__global__ __launch_bounds__(256) void k_remap(const uint8_t* const* srcs, int sw, int sh, int sstride,
+__global__ __launch_bounds__(256) void k_remap(const uint8_t* const* __restrict__ srcs, int sw, int sh, int sstride,
                                                const float* __restrict__ mapx, const float* __restrict__ mapy,
-                                               int dw, int dh, uint8_t* const* dsts, int dstride, int n, int src_al) {
+                                               int dw, int dh, uint8_t* const* __restrict__ dsts, int dstride, int n,
+                                               int src_al) {
 #if RM_XCD
     // XCD-aware order: the blocks one XCD runs are consecutive tiles of one image group, so the
     // source rows two adjacent tiles share are fetched into that XCD's L2 once
@@ -129,14 +130,25 @@ __global__ __launch_bounds__(256) void k_remap(const uint8_t* const* srcs, int s
     }
     fast = fast && (base - (r[0].off - (r[0].off % sstride))) + 8 <= sstride;
     const int i0 = grp * RM_IPB, i1 = min(i0 + RM_IPB, n);
-    for (int img = i0; img < i1; img++) {
+    // the fast path's two 8-byte windows of image img, as one dwordx2 load each (4-byte aligned:
+    // the hardware's unaligned global access). Every lane loads (the others from offset 0, never
+    // used), so the loads are unconditional and the next image's pair is in flight while this
+    // image is computed and stored.
+    const int woff = fast ? base : 0, woff2 = fast ? base + sstride : 0;
+    auto ldw = [&](int img, uint2& wa, uint2& wb) {
         gptr_u8 src = as_global(srcs[img]);
+        __builtin_memcpy(&wa, (const void*)(src + woff), 8);
+        __builtin_memcpy(&wb, (const void*)(src + woff2), 8);
+    };
+    uint2 na, nb;
+    ldw(i0, na, nb);
+    for (int img = i0; img < i1; img++) {
+        const uint2 wa = na, wb = nb;
+        if (img + 1 < i1) ldw(img + 1, na, nb);
         uint8_t* dst = dsts[img] + (size_t)y * dstride;
         uint32_t packed = 0;
         if (fast) {
-            const ORBFE_GLOBAL uint32_t* p0 = (const ORBFE_GLOBAL uint32_t*)(src + base);
-            const ORBFE_GLOBAL uint32_t* p1 = (const ORBFE_GLOBAL uint32_t*)(src + base + sstride);
-            const uint32_t a0 = p0[0], a1 = p0[1], b0 = p1[0], b1 = p1[1];
+            const uint32_t a0 = wa.x, a1 = wa.y, b0 = wb.x, b1 = wb.y;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const uint32_t t0 = __builtin_amdgcn_perm(a1, a0, sel[q]), t1 = __builtin_amdgcn_perm(b1, b0, sel[q]);
@@ -147,6 +159,7 @@ __global__ __launch_bounds__(256) void k_remap(const uint8_t* const* srcs, int s
                 packed |= (acc >> 15) << (8 * q);   // <= 255: the weights sum to 32768
             }
         } else {
+            gptr_u8 src = as_global(srcs[img]);
 #pragma unroll
             for (int q = 0; q < 4; q++) packed |= remap_apply(src, sstride, r[q]) << (8 * q);
         }
