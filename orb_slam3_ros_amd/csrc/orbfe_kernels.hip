@@ -1229,6 +1229,21 @@ __global__ __launch_bounds__(OCT_NT) void k_debug_block_sort(unsigned long long*
     for (int i = threadIdx.x; i < n; i += OCT_NT) a[i] = la[i];
 }
 
+// Wave-aggregated LDS increment: every active lane adds 1 to base[t]. The keys of a wave arrive in
+// cell order, so adjacent lanes mostly share a node (and quadrant); each run of equal targets adds
+// its length once from its first lane, instead of up to 64 same-address atomics serialised in the
+// LDS. Needs every lane of the wave (DPP + ballot): callers keep the trip counts wave-uniform.
+__device__ __forceinline__ void atomic_inc_runs(int* base, int t, bool act) {
+    const int lane = lane_id();
+    const int key = act ? t : -1 - lane;   // inactive lanes: distinct keys, never in a run
+    const int prev = __builtin_amdgcn_update_dpp(INT_MIN, key, 0x138, 0xf, 0xf, false);   // wave_shr:1
+    const bool head = key != prev;   // lane 0 reads INT_MIN
+    const unsigned long long hm = __ballot(head);
+    const unsigned long long above = hm & ~((2ull << lane) - 1ull);   // heads after this lane
+    const int next = above ? (int)__builtin_ctzll(above) : 64;
+    if (head && act) atomicAdd(&base[t], next - lane);
+}
+
 __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __restrict__ cellkeys,
                                                    const int* __restrict__ cellcnt, uint32_t* lkeys,
                                                    uint16_t* nodeof, uint32_t* outkeys, int* lvinfo, int* ranks,
@@ -1307,13 +1322,15 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
     for (int i = tid; i < nIni; i += OCT_NT) tmpA[i] = 0;
     for (int i = tid; i < 4 * NC; i += OCT_NT) Ccnt[i] = 0;
     SYNC();
-    for (int k0 = tid; k0 < K; k0 += OCT_NT * OCT_U) {
+    // (wave-uniform trip counts: the aggregated increments need every lane)
+    for (int kb = 0; kb < K; kb += OCT_NT * OCT_U) {
+        const int k0 = kb + tid;
         uint32_t v[OCT_U];
 #pragma unroll
         for (int u = 0; u < OCT_U; u++) v[u] = keys[min(k0 + OCT_NT * u, K - 1)];
 #pragma unroll
         for (int u = 0; u < OCT_U; u++)
-            if (k0 + OCT_NT * u < K) atomicAdd(&tmpA[(int)((float)(v[u] & 0xfff) / hX)], 1);
+            atomic_inc_runs(tmpA, (int)((float)(v[u] & 0xfff) / hX), k0 + OCT_NT * u < K);
     }
     SYNC();
     for (int i = tid; i < nIni; i += OCT_NT) tmpB[i] = tmpA[i] > 0 ? 1 : 0;
@@ -1330,19 +1347,18 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
         }
     }
     SYNC();
-    for (int k0 = tid; k0 < K; k0 += OCT_NT * OCT_U) {
+    for (int kb = 0; kb < K; kb += OCT_NT * OCT_U) {
+        const int k0 = kb + tid;
         uint32_t v[OCT_U];
 #pragma unroll
         for (int u = 0; u < OCT_U; u++) v[u] = keys[min(k0 + OCT_NT * u, K - 1)];
 #pragma unroll
         for (int u = 0; u < OCT_U; u++) {
             const int k = k0 + OCT_NT * u;
-            if (k < K) {
-                const uint32_t key = v[u];
-                const int q = tmpB[(int)((float)(key & 0xfff) / hX)];
-                nof[k] = (uint16_t)q;
-                if (Csz[q] > 1) atomicAdd(&Ccnt[4 * q + quadrant(key, Cx0[q], Cx1[q], Cy0[q], Cy1[q])], 1);
-            }
+            const uint32_t key = v[u];
+            const int q = tmpB[(int)((float)(key & 0xfff) / hX)];
+            if (k < K) nof[k] = (uint16_t)q;
+            atomic_inc_runs(Ccnt, 4 * q + quadrant(key, Cx0[q], Cx1[q], Cy0[q], Cy1[q]), k < K && Csz[q] > 1);
         }
     }
     for (int i = tid; i < NC; i += OCT_NT) divorder[i] = -1;
@@ -1454,7 +1470,8 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
         SYNC();
         OCT_STAMP();
         // key sweep: move keys to their new node positions and count the next split
-        for (int k0 = tid; k0 < K; k0 += OCT_NT * OCT_U) {
+        for (int kb = 0; kb < K; kb += OCT_NT * OCT_U) {
+            const int k0 = kb + tid;
             uint32_t v[OCT_U];
             int qv[OCT_U];
 #pragma unroll
@@ -1466,16 +1483,13 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
 #pragma unroll
             for (int u = 0; u < OCT_U; u++) {
                 const int k = k0 + OCT_NT * u;
-                if (k < K) {
-                    const uint32_t key = v[u];
-                    const int q = qv[u];
-                    int np;
-                    if (divorder[q] >= 0) np = childpos[4 * q + quadrant(key, Cx0[q], Cx1[q], Cy0[q], Cy1[q])];
-                    else np = newpos[q];
-                    nof[k] = (uint16_t)np;
-                    if (Xsz[np] > 1)
-                        atomicAdd(&Xcnt[4 * np + quadrant(key, Xx0[np], Xx1[np], Xy0[np], Xy1[np])], 1);
-                }
+                const uint32_t key = v[u];
+                const int q = qv[u];
+                int np;
+                if (divorder[q] >= 0) np = childpos[4 * q + quadrant(key, Cx0[q], Cx1[q], Cy0[q], Cy1[q])];
+                else np = newpos[q];
+                if (k < K) nof[k] = (uint16_t)np;
+                atomic_inc_runs(Xcnt, 4 * np + quadrant(key, Xx0[np], Xx1[np], Xy0[np], Xy1[np]), k < K && Xsz[np] > 1);
             }
         }
         SYNC();
