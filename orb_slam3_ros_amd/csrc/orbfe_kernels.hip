@@ -1059,7 +1059,7 @@ __device__ __forceinline__ void child_rect(int q, int x0, int x1, int y0, int y1
     *cy1 = (q & 2) ? y1 : my;
 }
 // Block-wide (OCT_NT threads) in-place exclusive scan of arr[0..n); returns the total.
-__device__ int block_excl_scan(int* arr, int n, int* s_ws) {
+__device__ __forceinline__ int block_excl_scan(int* arr, int n, int* s_ws) {
     const int lane = lane_id(), wave = threadIdx.x >> 6;
     int carry = 0;
     for (int base = 0; base < n; base += OCT_NT) {
@@ -1089,7 +1089,7 @@ __device__ int block_excl_scan(int* arr, int n, int* s_ws) {
 // depth-exhausted leaves fall back to the serial heapsort replica.
 // Scratch: fl, lpos, rpos, leaves: int[n]; tmp: u64[n]; segs: int4[ORBFE_SORT_STACK].
 // In-place exclusive scan of arr[0..n) by the calling wave only (no workgroup barrier).
-__device__ int wave_scan_lds(int* arr, int n) {
+__device__ __forceinline__ int wave_scan_lds(int* arr, int n) {
     const int lane = lane_id();
     int carry = 0;
     for (int base = 0; base < n; base += 64) {
@@ -1103,7 +1103,22 @@ __device__ int wave_scan_lds(int* arr, int n) {
     return carry;
 }
 
-__device__ void wave_introsort_impl(unsigned long long* a, int n, int* fl, int* lpos, int* rpos, int* leaves,
+// Wave-aggregated LDS increment: every active lane adds 1 to base[t]. The keys of a wave arrive in
+// cell order, so adjacent lanes mostly share a node (and quadrant); each run of equal targets adds
+// its length once from its first lane, instead of up to 64 same-address atomics serialised in the
+// LDS. Needs every lane of the wave (DPP + ballot): callers keep the trip counts wave-uniform.
+__device__ __forceinline__ void atomic_inc_runs(int* base, int t, bool act) {
+    const int lane = lane_id();
+    const int key = act ? t : -1 - lane;   // inactive lanes: distinct keys, never in a run
+    const int prev = __builtin_amdgcn_update_dpp(INT_MIN, key, 0x138, 0xf, 0xf, false);   // wave_shr:1
+    const bool head = key != prev;   // lane 0 reads INT_MIN
+    const unsigned long long hm = __ballot(head);
+    const unsigned long long above = hm & ~((2ull << lane) - 1ull);   // heads after this lane
+    const int next = above ? (int)__builtin_ctzll(above) : 64;
+    if (head && act) atomicAdd(&base[t], next - lane);
+}
+
+__device__ __forceinline__ void wave_introsort_impl(unsigned long long* a, int n, int* fl, int* lpos, int* rpos, int* leaves,
                                 unsigned long long* tmp, int4* segs, int* s_ws, int* s_ctl) {
     const int tid = lane_id();
     if (n <= 1) return;
@@ -1203,7 +1218,7 @@ __device__ void wave_introsort_impl(unsigned long long* a, int n, int* fl, int* 
 
 // Block entry: the sort runs on wave 0 only (wave-level scans, no workgroup barriers inside);
 // the other waves wait at the closing barrier.
-__device__ void block_introsort(unsigned long long* a, int n, int* fl, int* lpos, int* rpos, int* leaves,
+__device__ __forceinline__ void block_introsort(unsigned long long* a, int n, int* fl, int* lpos, int* rpos, int* leaves,
                                 unsigned long long* tmp, int4* segs, int* s_ws, int* s_ctl) {
     (void)s_ws;
     SYNC();
@@ -1227,21 +1242,6 @@ __global__ __launch_bounds__(OCT_NT) void k_debug_block_sort(unsigned long long*
     SYNC();
     block_introsort(la, n, fl, lpos, rpos, leaves, tmp, segs, s_ws, s_ctl);
     for (int i = threadIdx.x; i < n; i += OCT_NT) a[i] = la[i];
-}
-
-// Wave-aggregated LDS increment: every active lane adds 1 to base[t]. The keys of a wave arrive in
-// cell order, so adjacent lanes mostly share a node (and quadrant); each run of equal targets adds
-// its length once from its first lane, instead of up to 64 same-address atomics serialised in the
-// LDS. Needs every lane of the wave (DPP + ballot): callers keep the trip counts wave-uniform.
-__device__ __forceinline__ void atomic_inc_runs(int* base, int t, bool act) {
-    const int lane = lane_id();
-    const int key = act ? t : -1 - lane;   // inactive lanes: distinct keys, never in a run
-    const int prev = __builtin_amdgcn_update_dpp(INT_MIN, key, 0x138, 0xf, 0xf, false);   // wave_shr:1
-    const bool head = key != prev;   // lane 0 reads INT_MIN
-    const unsigned long long hm = __ballot(head);
-    const unsigned long long above = hm & ~((2ull << lane) - 1ull);   // heads after this lane
-    const int next = above ? (int)__builtin_ctzll(above) : 64;
-    if (head && act) atomicAdd(&base[t], next - lane);
 }
 
 __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __restrict__ cellkeys,

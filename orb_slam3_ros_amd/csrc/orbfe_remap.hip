@@ -145,7 +145,7 @@ __global__ __launch_bounds__(256) void k_remap(const uint8_t* const* __restrict_
     for (int img = i0; img < i1; img++) {
         const uint2 wa = na, wb = nb;
         if (img + 1 < i1) ldw(img + 1, na, nb);
-        uint8_t* dst = dsts[img] + (size_t)y * dstride;
+        ORBFE_GLOBAL uint8_t* dst = (ORBFE_GLOBAL uint8_t*)dsts[img] + (size_t)y * dstride;   // global stores, not flat
         uint32_t packed = 0;
         if (fast) {
             const uint32_t a0 = wa.x, a1 = wa.y, b0 = wb.x, b1 = wb.y;
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(256) void k_remap(const uint8_t* const* __restrict_
             for (int q = 0; q < 4; q++) packed |= remap_apply(src, sstride, r[q]) << (8 * q);
         }
         if (full && ((((uintptr_t)(dst + x0)) & 3) == 0)) {
-            *(uint32_t*)(dst + x0) = packed;
+            *(ORBFE_GLOBAL uint32_t*)(dst + x0) = packed;
         } else {
             for (int q = 0; q < 4 && x0 + q < dw; q++) dst[x0 + q] = (uint8_t)(packed >> (8 * q));
         }
