@@ -1853,10 +1853,16 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
 }
 
 #ifndef DP_KPW
-#define DP_KPW 1   // slots per wave (> 1: the next slot's patch loads overlap this slot's compute;
-                   // measured slower at 2, the extra registers cost occupancy)
+#define DP_KPW 4   // slots per wave: the next slot's patch loads overlap this slot's compute (a wave
+                   // alone is two dependent memory round trips per slot: keys, then the patch)
 #endif
-__global__ __launch_bounds__(256) void k_describe(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
+#ifndef DP_ATTR
+// 4 slots need 88 VGPRs unconstrained (5 waves per SIMD); capped for 6 waves the compiler spills
+// 40 bytes per lane and the kernel is faster: 610 -> 560 us per step (1 slot / 4 slots at 5, 6, 7
+// waves, 2, 3 and 8 slots measured, tools/gpu_variants_trace.sh)
+#define DP_ATTR __attribute__((amdgpu_waves_per_eu(6)))
+#endif
+__global__ __launch_bounds__(256) DP_ATTR void k_describe(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                                   int pyr_stride, OrbGeom g, const uint32_t* __restrict__ outkeys,
                                                   const int* __restrict__ lvinfo, const int* __restrict__ ranks,
                                                   OrbKeyPoint* kps, uint8_t* desc, int* counts, BlurKernel bk) {
