@@ -140,11 +140,11 @@ __global__ __launch_bounds__(256) void k_remap(const uint8_t* const* __restrict_
         __builtin_memcpy(&wa, (const void*)(src + woff), 8);
         __builtin_memcpy(&wb, (const void*)(src + woff2), 8);
     };
-    uint2 na, nb;
-    ldw(i0, na, nb);
+    uint2 na = {0u, 0u}, nb = {0u, 0u};
+    if (src_al) ldw(i0, na, nb);   // src_al (wave-uniform) also guarantees >= 16 bytes per source
     for (int img = i0; img < i1; img++) {
         const uint2 wa = na, wb = nb;
-        if (img + 1 < i1) ldw(img + 1, na, nb);
+        if (src_al && img + 1 < i1) ldw(img + 1, na, nb);
         ORBFE_GLOBAL uint8_t* dst = (ORBFE_GLOBAL uint8_t*)dsts[img] + (size_t)y * dstride;   // global stores, not flat
         uint32_t packed = 0;
         if (fast) {
@@ -278,7 +278,7 @@ int orbfe_remap_linear_batch(const uint8_t* const* d_src, int sw, int sh, int ss
     uint8_t* const* ddst = (uint8_t* const*)(rt.dev + n);
     const int ng = (dw + 3) >> 2;
     // the fast path's dword loads need 4-byte aligned source rows
-    bool al = (sstride & 3) == 0;
+    bool al = (sstride & 3) == 0 && (size_t)sstride * (size_t)(sh - 1) + (size_t)sw >= 16;
     for (int i = 0; al && i < n; i++) al = (((uintptr_t)d_src[i]) & 3) == 0;
     const dim3 grid((ng * dh + 255) / 256, (n + RM_IPB - 1) / RM_IPB);
     hipLaunchKernelGGL(k_remap, grid, dim3(256), 0, s, dsrc, sw, sh,
@@ -306,7 +306,8 @@ int orbfe_remap_linear(const uint8_t* src, int sw, int sh, int sstride, const fl
     hipLaunchKernelGGL(k_remap, dim3(nt, 1), dim3(256), 0, s,
                        (const uint8_t* const*)ms_ptr<uint8_t>(o_ptr), sw, sh, sstride, ms_ptr<const float>(o_mx),
                        ms_ptr<const float>(o_my), dw, dh, (uint8_t* const*)(ms_ptr<uint8_t>(o_ptr) + 8), dw, 1,
-                       (((uintptr_t)ms_ptr<uint8_t>(o_src) & 3) == 0 && (sstride & 3) == 0) ? 1 : 0);
+                       (((uintptr_t)ms_ptr<uint8_t>(o_src) & 3) == 0 && (sstride & 3) == 0 &&
+                        (size_t)sstride * (size_t)(sh - 1) + (size_t)sw >= 16) ? 1 : 0);
     HIPCHK(hipGetLastError());
     timer.end();
     HIPCHK(hipMemcpy2DAsync(dst, dstride, ms_ptr<uint8_t>(o_dst), dw, dw, dh, hipMemcpyDeviceToHost, s));

@@ -51,6 +51,26 @@ def test_remap_batch_device(gpu, oracle_lib):
         np.testing.assert_array_equal(got[i], oracle_lib.remap_linear(imgs[i], mx, my))
 
 
+@pytest.mark.parametrize("sw,sh", [(3, 2), (4, 3), (8, 2), (5, 5)])
+def test_remap_tiny_sources(gpu, oracle_lib, sw, sh):
+    """Sources of < 16 bytes take the guarded byte path (no 8-byte window loads), single and
+    batched, including batches that end in a partial image group."""
+    import torch
+    rng = np.random.default_rng(sw * 10 + sh)
+    dh, dw = 6, 9
+    mx = rng.uniform(-1.5, sw + 0.5, (dh, dw)).astype(np.float32)
+    my = rng.uniform(-1.5, sh + 0.5, (dh, dw)).astype(np.float32)
+    imgs = rng.integers(0, 256, (11, sh, sw), dtype=np.uint8)
+    np.testing.assert_array_equal(remap_linear(imgs[0], mx, my), oracle_lib.remap_linear(imgs[0], mx, my))
+    src = torch.from_numpy(imgs).cuda()
+    out = torch.zeros((11, dh, dw), dtype=torch.uint8, device="cuda")
+    remap_linear_batch(src, torch.from_numpy(mx).cuda(), torch.from_numpy(my).cuda(), out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    for i in range(11):
+        np.testing.assert_array_equal(got[i], oracle_lib.remap_linear(imgs[i], mx, my))
+
+
 @pytest.mark.parametrize("dist", [
     (-0.28340811, 0.07395907, 0.00019359, 1.76187114e-05),            # EuRoC cam0 (radial-tangential)
     (-0.28, 0.07, 2e-4, 1.8e-5, 0.01),                                 # + k3
