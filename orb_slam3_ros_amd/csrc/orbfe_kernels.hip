@@ -1962,6 +1962,9 @@ __device__ __forceinline__ int hamming32(const uint32_t* a, const uint32_t* b) {
 #define ST_LK 512   // left keypoints per block (2 blocks per frame: 256 measured 10 % slower, 1024 20 %)
 #endif
 #define ST_NT 1024
+#ifndef ST_CSORT
+#define ST_CSORT 1   // right records ordered by a counting sort over band rows (0: bitonic sort)
+#endif
 #define ST_ROFF 32    // row-start table margin (rows -32 .. height + 32)
 struct RightRec { float x; int minr, maxr, oct; };
 __global__ __launch_bounds__(ST_NT) void k_stereo(OrbGeom g, StereoSide SL, StereoSide SR, StereoArgs sa,
@@ -2008,31 +2011,52 @@ __global__ __launch_bounds__(ST_NT) void k_stereo(OrbGeom g, StereoSide SL, Ster
     }
     atomicMax(&s_maxspan, span);
     SYNC();
-    for (int k = 2; k <= P; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < P; i += blockDim.x) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const uint32_t a = s_key[i], c = s_key[ixj];
-                    if ((a > c) == ((i & k) == 0)) { s_key[i] = c; s_key[ixj] = a; }
-                }
-            }
-            SYNC();
-        }
-    // row -> first sorted record with minr >= row (rows -ST_ROFF .. height + ST_ROFF), one binary
-    // search per row for the block instead of two dependent LDS searches per left keypoint
+    // row -> first sorted record with minr >= row (rows -ST_ROFF .. height + ST_ROFF): the candidate
+    // scan of a left keypoint reads one table entry per bound instead of a binary search
     uint16_t* s_rowst = (uint16_t*)((uint8_t*)(s_key + sa.sort_cap) + (ST_NT / 64) * (512 + 128 * 4));
     const int nrow = g.height + 2 * ST_ROFF;
-    for (int r = threadIdx.x; r < nrow; r += blockDim.x) {
-        const uint32_t t = (uint32_t)max(r - ST_ROFF + 1024, 0) << 16;
-        int lo = 0, hi = Nr;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (s_key[mid] < t) lo = mid + 1; else hi = mid;
+    if (ST_CSORT && nrow + 1 <= (ST_NT / 64) * 128) {
+        // counting sort by the first row of the band (clamped into the table; a clamped record only
+        // moves towards the rows that can hold it, and the band test filters it): the order within
+        // a row is immaterial, the scan keeps the first best in iR order through its (dist, iR) key.
+        // Counts and cursors in the waves' SAD scratch, free until the keypoint loop.
+        int* s_cnt = (int*)((uint8_t*)(s_key + sa.sort_cap) + (ST_NT / 64) * 512);
+        for (int r = threadIdx.x; r <= nrow; r += blockDim.x) s_cnt[r] = 0;
+        SYNC();
+        for (int i = threadIdx.x; i < Nr; i += blockDim.x)
+            atomicAdd(&s_cnt[min(max(s_rec[i].minr + ST_ROFF, 0), nrow - 1)], 1);
+        SYNC();
+        if (wave == 0) (void)wave_scan_lds(s_cnt, nrow + 1);
+        SYNC();
+        for (int r = threadIdx.x; r < nrow; r += blockDim.x) s_rowst[r] = (uint16_t)s_cnt[r];
+        for (int i = threadIdx.x; i < Nr; i += blockDim.x) {
+            const int bin = min(max(s_rec[i].minr + ST_ROFF, 0), nrow - 1);
+            s_key[atomicAdd(&s_cnt[bin], 1)] = ((uint32_t)(bin - ST_ROFF + 1024) << 16) | (uint32_t)i;
         }
-        s_rowst[r] = (uint16_t)lo;
+        SYNC();
+    } else {
+        for (int k = 2; k <= P; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = threadIdx.x; i < P; i += blockDim.x) {
+                    const int ixj = i ^ j;
+                    if (ixj > i) {
+                        const uint32_t a = s_key[i], c = s_key[ixj];
+                        if ((a > c) == ((i & k) == 0)) { s_key[i] = c; s_key[ixj] = a; }
+                    }
+                }
+                SYNC();
+            }
+        for (int r = threadIdx.x; r < nrow; r += blockDim.x) {
+            const uint32_t t = (uint32_t)max(r - ST_ROFF + 1024, 0) << 16;
+            int lo = 0, hi = Nr;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (s_key[mid] < t) lo = mid + 1; else hi = mid;
+            }
+            s_rowst[r] = (uint16_t)lo;
+        }
+        SYNC();
     }
-    SYNC();
     const int maxspan = s_maxspan;
     float* uR_out = uright + (size_t)f * g.kp_cap;
     float* dp_out = depth + (size_t)f * g.kp_cap;
