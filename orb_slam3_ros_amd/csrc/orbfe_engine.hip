@@ -916,7 +916,7 @@ int orbfe_stereo_match_batch(orbfe_extractor* left, int lbase, int lstep, orbfe_
     StereoArgs sa{bf, fx, g.kp_cap, sort_cap};
     const size_t lds = (size_t)g.kp_cap * (32 + sizeof(RightRec)) + (size_t)sort_cap * 4 + (ST_NT / 64) * (512 + 128 * 4) +
                        (size_t)round_up(2 * (g.height + 2 * ST_ROFF), 16);
-    if (lds > 160 * 1024 - 64 || g.kp_cap > ST_SORT || g.kp_cap > 65535) return ORBFE_E_ARG;
+    if (lds > 160 * 1024 - 64 || g.kp_cap > 65535) return ORBFE_E_ARG;   // LDS: about 2700 keypoints per image
     hipStream_t s = pick_stream(left, stream);
     std::lock_guard<std::mutex> lk(left->mu_stereo);
     if (left->sdist_frames < nframes || left->sdist_kp < g.kp_cap) {

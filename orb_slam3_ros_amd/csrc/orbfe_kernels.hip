@@ -2190,48 +2190,73 @@ __global__ __launch_bounds__(ST_NT) void k_stereo(OrbGeom g, StereoSide SL, Ster
 }
 
 // Stage 2 (one block per frame): the median outlier cut of ComputeStereoMatches (Frame.cc:966-980):
-// sort the accepted (dist, iL) pairs, median = the (n/2)-th dist, drop every match with
-// dist >= 1.5f*1.4f*median. Bitonic sort of the accepted distances in LDS.
-#define ST_SORT 2048
+// median = the (n/2)-th smallest accepted SAD distance (vDistIdx sorted, index size/2), then every
+// match with dist >= 1.5f*1.4f*median is dropped. The median is selected by two histogram passes
+// (distances are < 2^16: 121 window bytes x 255), high byte then low byte, instead of a sort.
+__device__ __forceinline__ int block256_excl_scan(int v, int* s_ws, int* total) {
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    const int incl = wave_incl_scan(v);
+    if (lane == 63) s_ws[wave] = incl;
+    SYNC();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const int t = s_ws[w];
+        off += w < wave ? t : 0;
+        tot += t;
+    }
+    *total = tot;
+    return off + incl - v;
+}
 __global__ __launch_bounds__(256) void k_stereo_cut(OrbGeom g, StereoSide SL, StereoArgs sa, float* uright,
                                                     float* depth, const int* sdist, int* nmatch) {
-    __shared__ int s_v[ST_SORT];
-    __shared__ int s_n;
-    const int f = blockIdx.x;
+    __shared__ int s_h[256];
+    __shared__ int s_ws[4];
+    __shared__ int s_sel[2];
+    const int f = blockIdx.x, t = threadIdx.x;
     const int bL = SL.base + f * SL.step;
     const int N = SL.counts[2 * bL];
     const int* sd = sdist + (size_t)f * g.kp_cap;
-    if (threadIdx.x == 0) s_n = 0;
+    // pass 1: histogram of the high byte
+    s_h[t] = 0;
     SYNC();
-    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    for (int i = t; i < N; i += blockDim.x) {
         const int d = sd[i];
-        if (d >= 0) s_v[atomicAdd(&s_n, 1)] = d;
+        if (d >= 0) atomicAdd(&s_h[min(d, 65535) >> 8], 1);
     }
     SYNC();
-    const int n = s_n;
-    int P = 1;
-    while (P < n) P <<= 1;
-    for (int i = n + threadIdx.x; i < P; i += blockDim.x) s_v[i] = 0x7fffffff;
+    int n;
+    {
+        const int c = s_h[t];
+        const int ex = block256_excl_scan(c, s_ws, &n);
+        const int k = n / 2;
+        if (ex <= k && k < ex + c) { s_sel[0] = t; s_sel[1] = k - ex; }
+    }
+    if (t == 0) nmatch[f] = n;
+    if (n == 0) return;   // the reference indexes vDistIdx[size/2] unguarded here (block-uniform)
     SYNC();
-    for (int k = 2; k <= P; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < P; i += blockDim.x) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const int a = s_v[i], c = s_v[ixj];
-                    const bool up = (i & k) == 0;
-                    if ((a > c) == up) { s_v[i] = c; s_v[ixj] = a; }
-                }
-            }
-            SYNC();
-        }
-    if (threadIdx.x == 0) nmatch[f] = n;
-    if (n == 0) return;   // the reference indexes vDistIdx[size/2] unguarded here
-    const float median = (float)s_v[n / 2];
+    const int hb = s_sel[0], k2 = s_sel[1];
+    // pass 2: histogram of the low byte among the distances whose high byte is hb
+    s_h[t] = 0;
+    SYNC();
+    for (int i = t; i < N; i += blockDim.x) {
+        const int d = sd[i];
+        if (d >= 0 && (min(d, 65535) >> 8) == hb) atomicAdd(&s_h[d & 255], 1);
+    }
+    SYNC();
+    {
+        int n2;
+        const int c = s_h[t];
+        SYNC();   // s_ws is reused by the second scan
+        const int ex = block256_excl_scan(c, s_ws, &n2);
+        if (ex <= k2 && k2 < ex + c) s_sel[0] = (hb << 8) | t;
+    }
+    SYNC();
+    const float median = (float)s_sel[0];
     const float thDist = 1.5f * 1.4f * median;
     float* uR = uright + (size_t)f * g.kp_cap;
     float* dp = depth + (size_t)f * g.kp_cap;
-    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    for (int i = t; i < N; i += blockDim.x) {
         const int d = sd[i];
         if (d >= 0 && !((float)d < thDist)) { uR[i] = -1; dp[i] = -1; }
     }

@@ -296,7 +296,7 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPoi
 //       const int rc = orbfe_stereo_match(static_cast<orbfe_extractor*>(mpORBextractorLeft->mpOrbfe),
 //                                         static_cast<orbfe_extractor*>(mpORBextractorRight->mpOrbfe),
 //                                         mbf, fx, mvuRight.data(), mvDepth.data());
-//       if (rc < 0) {   // e.g. ORBFE_E_ARG: more than 2048 keypoints per image (nFeatures > ~2000)
+//       if (rc < 0) {   // e.g. ORBFE_E_ARG: more than ~2700 keypoints per image (k_stereo LDS)
 //           fprintf(stderr, "[orbfe] orbfe_stereo_match returned %d; running the CPU implementation\n", rc);
 //           mpORBextractorLeft->MaterialisePyramid();
 //           mpORBextractorRight->MaterialisePyramid();

@@ -160,11 +160,14 @@ def test_empty_image(gpu):
     assert mono == -1 and len(kp) == 0
 
 
-def test_stereo_matches_oracle(gpu, oracle_lib):
+@pytest.mark.parametrize("nfeat", [1200, 2500])
+def test_stereo_matches_oracle(gpu, oracle_lib, nfeat):
+    """ComputeStereoMatches bit-exact; 2500 features puts more than 2048 keypoints in an image
+    (the stereo kernels have no sort-size limit, only their LDS)."""
     from orb_slam3_ros_amd.extractor import ORBextractor, compute_stereo_matches
     left, right = synth_stereo(3, 752, 480)
-    el, er = ORBextractor(1200, 1.2, 8, 20, 7), ORBextractor(1200, 1.2, 8, 20, 7)
-    ol, orr = oracle_lib.OracleExtractor(1200, 1.2, 8, 20, 7), oracle_lib.OracleExtractor(1200, 1.2, 8, 20, 7)
+    el, er = ORBextractor(nfeat, 1.2, 8, 20, 7), ORBextractor(nfeat, 1.2, 8, 20, 7)
+    ol, orr = oracle_lib.OracleExtractor(nfeat, 1.2, 8, 20, 7), oracle_lib.OracleExtractor(nfeat, 1.2, 8, 20, 7)
     _, kl, dl = el(left, None, (0, 0))
     _, kr, dr = er(right, None, (0, 0))
     _, okl, odl = ol(left)
