@@ -1122,69 +1122,79 @@ __device__ __forceinline__ void wave_introsort_impl(unsigned long long* a, int n
                                 unsigned long long* tmp, int4* segs, int* s_ws, int* s_ctl) {
     const int tid = lane_id();
     if (n <= 1) return;
-    if (tid == 0) {
-        segs[0] = make_int4(0, n, 2 * st_lg(n), 0);
-        s_ctl[0] = 1;   // stack size
-        s_ctl[1] = 0;   // leaf count
-    }
+    const unsigned long long lt = (1ull << tid) - 1ull;
+    // the segment stack lives in LDS (written by lane 0), its depth and the leaf count in registers
+    // (wave-uniform): per partition step three wave hand-offs, the stops ranked by ballots
+    if (tid == 0) segs[0] = make_int4(0, n, 2 * st_lg(n), 0);
     WAVE_SYNC();
-    while (true) {
-        if (s_ctl[0] == 0) break;
-        WAVE_SYNC();
-        if (tid == 0) {
-            const int4 sg = segs[--s_ctl[0]];
-            s_ctl[2] = sg.x; s_ctl[3] = sg.y; s_ctl[4] = sg.z;
-            if (sg.y - sg.x <= 16 || sg.z == 0) {
-                leaves[s_ctl[1]++] = sg.x | ((sg.y - sg.x <= 16) ? 0 : (int)0x80000000);
-            } else {
-                unsigned long long* f = a + sg.x;
-                st_move_median_to_first(f, f + 1, f + (sg.y - sg.x) / 2, a + sg.y - 1, ExpLess64());
+    int sp = 1, nleaf = 0;
+    while (sp > 0) {
+        const int4 sg = segs[--sp];
+        const int lo = sg.x, hi = sg.y, depth = sg.z;
+        if (hi - lo <= 16 || depth == 0) {
+            if (tid == 0) leaves[nleaf] = lo | ((hi - lo <= 16) ? 0 : (int)0x80000000);
+            nleaf++;
+            continue;
+        }
+        // __move_median_to_first(first, first + 1, mid, last - 1): every lane evaluates the
+        // comparison tree on the same four values, lane 0 performs the one swap
+        {
+            const int ia = lo + 1, ib = lo + (hi - lo) / 2, ic = hi - 1;
+            const unsigned long long x0 = a[lo], xa = a[ia], xb = a[ib], xc = a[ic];
+            const ExpLess64 comp;
+            int pick;
+            if (comp(xa, xb)) pick = comp(xb, xc) ? ib : (comp(xa, xc) ? ic : ia);
+            else pick = comp(xa, xc) ? ia : (comp(xb, xc) ? ic : ib);
+            const unsigned long long xp = pick == ia ? xa : (pick == ib ? xb : xc);
+            if (tid == 0) {
+                a[lo] = xp;
+                a[pick] = x0;
             }
         }
         WAVE_SYNC();
-        const int lo = s_ctl[2], hi = s_ctl[3], depth = s_ctl[4];
-        if (hi - lo <= 16 || depth == 0) continue;
         const unsigned P = (unsigned)(a[lo] >> 32);
         const int m = hi - lo - 1;
-        // left stops (scan rightwards over [lo+1, hi)): !(x < P)
-        for (int i = tid; i < m; i += 64) fl[i] = ((unsigned)(a[lo + 1 + i] >> 32) < P) ? 0 : 1;
+        // left stops (scan rightwards over [lo+1, hi)): !(x < P); right stops (leftwards from
+        // hi-1): !(P < x); the k-th stop of each side lands at lpos[k] / rpos[k]
+        int nl = 0, nr = 0;
+        for (int b0 = 0; b0 < m; b0 += 64) {
+            const int i = b0 + tid;
+            bool lf = false, rf = false;
+            if (i < m) {
+                lf = !((unsigned)(a[lo + 1 + i] >> 32) < P);
+                rf = !(P < (unsigned)(a[hi - 1 - i] >> 32));
+            }
+            const unsigned long long lm = __ballot(lf), rm = __ballot(rf);
+            if (lf) lpos[nl + __popcll(lm & lt)] = lo + 1 + i;
+            if (rf) rpos[nr + __popcll(rm & lt)] = hi - 1 - i;
+            nl += __popcll(lm);
+            nr += __popcll(rm);
+        }
         WAVE_SYNC();
-        const int nl = wave_scan_lds(fl, m);
-        for (int i = tid; i < m; i += 64)
-            if (!((unsigned)(a[lo + 1 + i] >> 32) < P)) lpos[fl[i]] = lo + 1 + i;
-        WAVE_SYNC();
-        // right stops (scan leftwards from hi-1): !(P < x)
-        for (int j = tid; j < m; j += 64) fl[j] = (P < (unsigned)(a[hi - 1 - j] >> 32)) ? 0 : 1;
-        WAVE_SYNC();
-        const int nr = wave_scan_lds(fl, m);
-        for (int j = tid; j < m; j += 64)
-            if (!(P < (unsigned)(a[hi - 1 - j] >> 32))) rpos[fl[j]] = hi - 1 - j;
-        if (tid == 0) s_ctl[5] = 0;
-        WAVE_SYNC();
+        // lpos increasing, rpos decreasing: the pairs that swap (lpos[k] < rpos[k]) are a prefix
         const int kmax = min(nl, nr);
-        int cntk = 0;
-        for (int k = tid; k < kmax; k += 64) cntk += lpos[k] < rpos[k] ? 1 : 0;
-        cntk = wave_sum(cntk);
-        if (tid == 0) s_ctl[5] = cntk;
-        WAVE_SYNC();
-        const int sw = s_ctl[5];   // lpos increasing, rpos decreasing: the pairs that swap are a prefix
+        int sw = 0;
+        for (int b0 = 0; b0 < kmax; b0 += 64) {
+            const int k = b0 + tid;
+            sw += __popcll(__ballot(k < kmax && lpos[k] < rpos[k]));
+        }
         for (int k = tid; k < sw; k += 64) {
             const unsigned long long x = a[lpos[k]];
             a[lpos[k]] = a[rpos[k]];
             a[rpos[k]] = x;
         }
+        int cut;
+        if (sw == 0) cut = lpos[0];
+        else cut = (sw < nl && lpos[sw] < rpos[sw - 1]) ? lpos[sw] : rpos[sw - 1];
         if (tid == 0) {
-            int cut;
-            if (sw == 0) cut = lpos[0];
-            else cut = (sw < nl && lpos[sw] < rpos[sw - 1]) ? lpos[sw] : rpos[sw - 1];
-            segs[s_ctl[0]++] = make_int4(cut, hi, depth - 1, 0);
-            segs[s_ctl[0]++] = make_int4(lo, cut, depth - 1, 0);
+            segs[sp] = make_int4(cut, hi, depth - 1, 0);
+            segs[sp + 1] = make_int4(lo, cut, depth - 1, 0);
         }
+        sp += 2;
         WAVE_SYNC();
     }
     WAVE_SYNC();
     // leaves were recorded left to right; stable rank sort inside each ordinary leaf
-    const int nleaf = s_ctl[1];
     for (int i = tid; i < n; i += 64) {
         int lo_i = 0, hi_i = nleaf - 1;   // last leaf with start <= i
         while (lo_i < hi_i) {
