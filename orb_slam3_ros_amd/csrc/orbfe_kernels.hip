@@ -1035,7 +1035,9 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
 #ifndef OCT_NT
 #define OCT_NT 256
 #endif
+#ifndef OCT_U
 #define OCT_U 4
+#endif
 // expandable node: (size << 44) | (UL.x << 32) | list position; compareNodes orders by the high 32 bits
 struct ExpLess64 {
     __device__ bool operator()(const unsigned long long& a, const unsigned long long& b) const {
