@@ -1305,12 +1305,20 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
     SYNC();
     const int K = block_excl_scan(cellpre, ncell, s_ws);
     if (tid == 0) cellpre[ncell] = K;
+    const int nIni = L.n_ini;
+    const float hX = L.hx;
+    const int H = (L.h - ORBFE_MINB) - ORBFE_MINB;
+    for (int i = tid; i < nIni; i += OCT_NT) tmpA[i] = 0;
+    for (int i = tid; i < 4 * NC; i += OCT_NT) Ccnt[i] = 0;
     SYNC();
     const size_t kbase = (size_t)b * g.cellkeys_per_img + L.cellkey_off;
     uint32_t* keys = lkeys + kbase;
     uint16_t* nof = nodeof + kbase;
     const uint32_t* ck = cellkeys + kbase;
-    for (int k0 = tid; k0 < K; k0 += OCT_NT * OCT_U) {
+    // the gather also counts the keys of each initial node (ORBextractor.cc:559-601's root columns;
+    // wave-uniform trip counts: the aggregated increments need every lane)
+    for (int kb = 0; kb < K; kb += OCT_NT * OCT_U) {
+        const int k0 = kb + tid;
         uint32_t v[OCT_U];
 #pragma unroll
         for (int u = 0; u < OCT_U; u++) {
@@ -1323,27 +1331,13 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
             v[u] = ck[(size_t)lo * L.cell_cap + (k - cellpre[lo])];
         }
 #pragma unroll
-        for (int u = 0; u < OCT_U; u++)
+        for (int u = 0; u < OCT_U; u++) {
             if (k0 + OCT_NT * u < K) keys[k0 + OCT_NT * u] = v[u];
+            atomic_inc_runs(tmpA, (int)((float)(v[u] & 0xfff) / hX), k0 + OCT_NT * u < K);
+        }
     }
     OCT_STAMP();
     // ---- initial nodes (ORBextractor.cc:559-601) ----
-    const int nIni = L.n_ini;
-    const float hX = L.hx;
-    const int H = (L.h - ORBFE_MINB) - ORBFE_MINB;
-    for (int i = tid; i < nIni; i += OCT_NT) tmpA[i] = 0;
-    for (int i = tid; i < 4 * NC; i += OCT_NT) Ccnt[i] = 0;
-    SYNC();
-    // (wave-uniform trip counts: the aggregated increments need every lane)
-    for (int kb = 0; kb < K; kb += OCT_NT * OCT_U) {
-        const int k0 = kb + tid;
-        uint32_t v[OCT_U];
-#pragma unroll
-        for (int u = 0; u < OCT_U; u++) v[u] = keys[min(k0 + OCT_NT * u, K - 1)];
-#pragma unroll
-        for (int u = 0; u < OCT_U; u++)
-            atomic_inc_runs(tmpA, (int)((float)(v[u] & 0xfff) / hX), k0 + OCT_NT * u < K);
-    }
     SYNC();
     for (int i = tid; i < nIni; i += OCT_NT) tmpB[i] = tmpA[i] > 0 ? 1 : 0;
     SYNC();
