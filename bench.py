@@ -463,7 +463,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--frames", type=int, default=256, help="stereo frames per GPU per step")
+    ap.add_argument("--frames", type=int, default=512, help="stereo frames per GPU per step (512: 1024 images per launch, +3 %% over 256, tools/gpu_frames_sweep.sh)")
     ap.add_argument("--width", type=int, default=752)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--nfeatures", type=int, default=1000)

@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 D=gpurun_out/prof_round
 mkdir -p $D
 LIB=$PWD/${ISO_LIB:-variants/liborbfe_iso.so}
-PCMD="python bench.py --steps 3 --warmup 1 --stage-steps 1 --no-cpu-baseline --no-parity --matcher-steps 0 --rectify-steps 2 --no-side-configs"
+PCMD="python bench.py --frames 512 --steps 3 --warmup 1 --stage-steps 1 --no-cpu-baseline --no-parity --matcher-steps 0 --rectify-steps 2 --no-side-configs"
 ORBFE_LIB=$LIB timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o run -- $PCMD > $D/trace.log 2>&1 || { tail -20 $D/trace.log; exit 1; }
 i=0
 for grp in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES" \
@@ -19,4 +19,4 @@ for grp in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES SQ_
   i=$((i+1))
   ORBFE_LIB=$LIB timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $D/p$i -o run -- $PCMD > $D/p$i.log 2>&1 || { tail -20 $D/p$i.log; exit 1; }
 done
-python tools/pmc_round.py $D ${PREFIX:-rXX} --outdir gpurun_out
+python tools/pmc_round.py $D ${PREFIX:-rXX} --outdir gpurun_out --images 1024

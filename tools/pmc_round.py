@@ -17,7 +17,7 @@ from profiles/:
 A "step" is one bench step (one launch sequence over the batch): counts are divided by the number of
 k_octree launches (one per step); k_remap (the rectification leg) is per launch.
 
-usage: pmc_round.py <dir> <prefix> [--outdir profiles] [--images 512 --width 752 --height 480]
+usage: pmc_round.py <dir> <prefix> [--outdir profiles] [--images 1024 --width 752 --height 480]
 """
 import argparse
 import collections
@@ -45,7 +45,7 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("prefix")
     ap.add_argument("--outdir", default="profiles")
-    ap.add_argument("--images", type=int, default=512)
+    ap.add_argument("--images", type=int, default=1024)
     ap.add_argument("--width", type=int, default=752)
     ap.add_argument("--height", type=int, default=480)
     a = ap.parse_args()
