@@ -375,14 +375,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
 // dword that would cross the row pitch is read from the row's last dword instead.
 // ---------------------------------------------------------------------------------------------
 #ifndef RS_D
-#define RS_D 3               // rows of loads in flight per wave = RS_D - 1 (the loop body's unroll;
-                             // measured: 1-6 rows within 3 %, deeper is slower)
+#define RS_D 5               // rows of loads in flight per wave = RS_D - 1 (the loop body's unroll;
+                             // with the dwordx3 loads: 2 / 3 / 5 / 7 -> 729 / 676 / 637 / 675 us per
+                             // 1024 images, 7 costs a wave per SIMD)
 #endif
 #ifndef RS_X3
 #define RS_X3 1              // the lane's 12-byte source window as one dwordx3 load (0: 3 dword loads)
 #endif
 #ifndef RS_ROWS
-#define RS_ROWS 16           // output rows per wave (<= 64: one table row per lane)
+#define RS_ROWS 32           // output rows per wave (<= 64: one table row per lane; 16 -> 32 with
+                             // RS_D 5: 637 -> 615 us per 1024 images)
 #endif
 #define RS_COLS 256          // output columns per wave strip
 typedef unsigned short orbfe_ushort2_rs __attribute__((ext_vector_type(2)));
