@@ -383,8 +383,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
 #define RS_X3 1              // the lane's 12-byte source window as one dwordx3 load (0: 3 dword loads)
 #endif
 #ifndef RS_ROWS
-#define RS_ROWS 32           // output rows per wave (<= 64: one table row per lane; 16 -> 32 with
-                             // RS_D 5: 637 -> 615 us per 1024 images)
+#define RS_ROWS 48           // output rows per wave (<= 64: one table row per lane; 16 / 32 / 48 / 64
+                             // with RS_D 5: 637 / 613 / 592 / 615 us per 1024 images)
 #endif
 #define RS_COLS 256          // output columns per wave strip
 typedef unsigned short orbfe_ushort2_rs __attribute__((ext_vector_type(2)));
