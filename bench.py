@@ -261,9 +261,11 @@ def cpu_baseline(native, budget_s=4.0):
 
 
 def parity_check(fe, images_host_pairs, frame_pair, nframes, nfeat, bf, fx, stereo="rectified", lap=(0, 0)):
-    """CHECKER, outside every timed region: frames 0..nframes-1 of the last step against the CPU
-    oracle (keypoint records, descriptors, monoIndex, uRight / depth bits, nmatch or the kNN
-    candidates). Returns (ok, message)."""
+    """CHECKER, outside every timed region: EVERY frame of the last step (nframes = the whole
+    batch by default, so both ends of the launch and everything between) against the CPU oracle's
+    output for that frame's input pair (keypoint records, descriptors, monoIndex, uRight / depth
+    bits, nmatch or the kNN candidates). The batch tiles U distinct synthetic pairs, so the oracle
+    runs U times; every frame's GPU output is compared. Returns (ok, message)."""
     import concurrent.futures as cf
     from oracle import oracle
     oracle.build()
@@ -282,31 +284,41 @@ def parity_check(fe, images_host_pairs, frame_pair, nframes, nfeat, bf, fx, ster
     uniq = sorted({int(frame_pair[f]) for f in range(nframes)})
     with cf.ThreadPoolExecutor(8) as ex:
         refs = dict(zip(uniq, ex.map(ref, uniq)))
-    nmatch = fe.nmatch.cpu().numpy()
+    # one device -> host copy of the whole batch's outputs
+    counts = fe.counts[: 2 * nframes].cpu().numpy()
+    kps = fe.kps[: 2 * nframes].cpu().numpy()
+    desc = fe.desc[: 2 * nframes].cpu().numpy()
+    nmatch = fe.nmatch[:nframes].cpu().numpy()
+    if stereo == "rectified":
+        ur_all = fe.uright[:nframes].cpu().numpy().view(np.uint32)
+        dp_all = fe.depth[:nframes].cpu().numpy().view(np.uint32)
+    else:
+        l2r_all = fe.l2r[:nframes].cpu().numpy()
     for f in range(nframes):
         r = refs[int(frame_pair[f])]
         for side in (0, 1):
-            mono, kp, d = fe.host_image(2 * f + side)
+            i = 2 * f + side
+            n, mono = int(counts[i, 0]), int(counts[i, 1])
             om, ok_, od = r[side]
-            if mono != om or len(kp) != len(ok_) or not np.array_equal(kp.view(np.uint32), ok_.view(np.uint32)) \
-                    or not np.array_equal(d, od):
+            if mono != om or n != len(ok_) or not np.array_equal(kps[i, :n].reshape(-1).view(np.uint32),
+                                                                 ok_.view(np.uint32).reshape(-1)) \
+                    or not np.array_equal(desc[i, :n], od):
                 return False, f"frame {f} side {side}: keypoints / descriptors differ from the oracle"
         n = len(r[0][1])
         if stereo == "rectified":
             ur, dp, nm = r[2]
-            if int(nmatch[f]) != nm or not np.array_equal(fe.uright[f, :n].cpu().numpy().view(np.uint32),
-                                                          ur.view(np.uint32)) \
-                    or not np.array_equal(fe.depth[f, :n].cpu().numpy().view(np.uint32), dp.view(np.uint32)):
+            if int(nmatch[f]) != nm or not np.array_equal(ur_all[f, :n], ur.view(np.uint32)) \
+                    or not np.array_equal(dp_all[f, :n], dp.view(np.uint32)):
                 return False, f"frame {f}: ComputeStereoMatches output differs from the oracle"
         else:
             good, t, _ = r[2]
             ml, mr = r[0][0], r[1][0]
-            l2r = fe.l2r[f, :n].cpu().numpy()
             exp = np.full(n, -1, np.int32)
             exp[ml:][t >= 0] = t[t >= 0] + mr
-            if int(nmatch[f]) != good or not np.array_equal(l2r, exp):
+            if int(nmatch[f]) != good or not np.array_equal(l2r_all[f, :n], exp):
                 return False, f"frame {f}: fisheye kNN candidates differ from the oracle"
-    return True, f"frames 0..{nframes - 1} bit-exact vs the CPU oracle ({len(uniq)} distinct pairs)"
+    return True, (f"all {nframes} frames ({2 * nframes} images, frames 0..{nframes - 1} incl. both ends of the "
+                  f"launch) bit-exact vs the CPU oracle ({len(uniq)} distinct synthetic pairs tiled over the batch)")
 
 
 def matcher_config5(steps):
@@ -446,7 +458,7 @@ def side_leg(dev, name, W, H, nf, F, steps, warmup, stereo, lap, bf, fx, check_f
     st = stage_times(fe, images, max(3, steps // 2))
     pf = st["pyramid_fast"]
     nb = algorithmic_bytes(W, H)
-    ok, msg = parity_check(fe, pairs, fmap, min(check_frames, F), nf, bf, fx, stereo=stereo, lap=lap)
+    ok, msg = parity_check(fe, pairs, fmap, min(check_frames or F, F), nf, bf, fx, stereo=stereo, lap=lap)
     out = {"workload": name, "frames_per_step": F, "images_per_step": 2 * F, "ms_per_step": round(sec * 1e3, 4),
            "frames_per_s": round(F / sec, 2), "stage_ms": {k: round(v, 4) for k, v in st.items()},
            "pyramid_fast_roofline": {"achieved_GBps": round(2 * F * nb / (pf * 1e-3) / 1e9, 1),
@@ -467,14 +479,14 @@ def main():
     ap.add_argument("--width", type=int, default=752)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--nfeatures", type=int, default=1000)
-    ap.add_argument("--unique", type=int, default=16, help="distinct synthetic frames (tiled over the batch)")
+    ap.add_argument("--unique", type=int, default=32, help="distinct synthetic frames (tiled over the batch)")
     ap.add_argument("--path", choices=["default", "fused", "legacy"], default="default",
                     help="pyramid+FAST implementation (default: the library's)")
     ap.add_argument("--pipelines", type=int, default=1, help="sub-batches on separate HIP streams")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the post-timing oracle check (profiling runs)")
-    ap.add_argument("--parity-frames", type=int, default=16)
+    ap.add_argument("--parity-frames", type=int, default=0, help="frames checked after timing (0: the whole batch)")
     ap.add_argument("--no-side-configs", action="store_true", help="skip the config 3 / config 4 legs")
     ap.add_argument("--stage-steps", type=int, default=10, help="extra steps with per-stage HIP events")
     ap.add_argument("--matcher-steps", type=int, default=10, help="config-5 SearchByProjection calls per th (0: skip)")
@@ -560,7 +572,7 @@ def main():
     # ---- checker: the last timed step's outputs against the CPU oracle (outside the timed region)
     parity = None
     if not args.no_parity:
-        ok, msg = parity_check(fe, pairs, fmap, min(args.parity_frames, F), args.nfeatures, bf, fx)
+        ok, msg = parity_check(fe, pairs, fmap, min(args.parity_frames or F, F), args.nfeatures, bf, fx)
         parity = {"ok": ok, "detail": msg, "rank": rank}
         if not ok:
             print(json.dumps({"parity": parity}), file=sys.stderr, flush=True)
@@ -687,15 +699,15 @@ def main():
             legs, all_ok = {}, True
             legs["config3"], ok3 = side_leg(dev, "KITTI-like stereo 1241x376, nFeatures 2000 (BASELINE config 3): "
                                                  "extract L+R + ComputeStereoMatches", 1241, 376, 2000, 256,
-                                            max(3, args.steps // 2), 2, "rectified", (0, 0), KITTI_BF, KITTI_FX, 8,
+                                            max(3, args.steps // 2), 2, "rectified", (0, 0), KITTI_BF, KITTI_FX, 0,
                                             20000)
             legs["config4_step"], ok4 = side_leg(dev, "TUM-VI-like 512x512 KannalaBrandt8 stereo, per-GPU step of "
                                                       "BASELINE config 4: 8 images (4 stereo frames), vLappingArea "
                                                       "{0,511}, batched knnMatch(k=2)+ratio", 512, 512, 1000, 4,
-                                                 max(10, args.steps), 3, "fisheye", (0, 511), 0.0, 1.0, 4, 21000)
+                                                 max(10, args.steps), 3, "fisheye", (0, 511), 0.0, 1.0, 0, 21000)
             legs["config4_batch"], ok4b = side_leg(dev, "as config4_step at a 512-image batch (throughput)", 512, 512,
                                                    1000, 256, max(3, args.steps // 2), 2, "fisheye", (0, 511), 0.0,
-                                                   1.0, 4, 22000)
+                                                   1.0, 0, 22000)
             result["side_configs"] = legs
             if not (ok3 and ok4 and ok4b):
                 print(json.dumps(result), file=sys.stderr, flush=True)

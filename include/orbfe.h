@@ -51,6 +51,21 @@ int orbfe_extractor_levels(const orbfe_extractor* h);
 int orbfe_extractor_scale_info(const orbfe_extractor* h, float* scale, float* inv_scale, float* sigma2,
                                float* inv_sigma2, int* features_per_level);
 
+/* OpenCV-behaviour model of the two OpenCV primitives whose 8-bit results depend on how the
+ * OpenCV the reference links was built (the reference itself cannot be built here):
+ *   resize_simd_lanes: cv::resize INTER_LINEAR (ORBextractor.cc:1183). Columns covered by the
+ *     universal-intrinsic vertical pass (VResizeLinearVec_32s8u: blocks of `lanes` u8, then of
+ *     lanes/2) round as ((((H0>>4)*b0)>>16) + (((H1>>4)*b1)>>16) + 2) >> 2, the rest with the
+ *     scalar (H0*b0 + H1*b1 + 2^21) >> 22. 16 = SSE2/NEON baseline (default), 32 = AVX2, 64 =
+ *     AVX-512 (CV_SIMD256 / 512 builds), 8 = a half-width build, 0 = no SIMD (scalar only).
+ *   blur_variant: cv::GaussianBlur 7x7 sigma 2 8U (ORBextractor.cc:1133) Q8 kernel quantisation;
+ *     0 = error-diffusion [18,34,48,56,48,34,18] (OpenCV >= 3.4.6, default), 1 = per-tap rounding
+ *     [18,34,49,55,49,34,18] (older builds).
+ * Other values return ORBFE_E_ARG. Changing the model waits for the device, releases the handle's
+ * batch buffers (the last batch's outputs and pyramid are gone) and rebuilds them on the next call. */
+int orbfe_extractor_set_opencv_model(orbfe_extractor* h, int resize_simd_lanes, int blur_variant);
+int orbfe_extractor_get_opencv_model(const orbfe_extractor* h, int* resize_simd_lanes, int* blur_variant);
+
 /* Max keypoints one image can yield (sum over levels of the octree bound); size caller buffers with it. */
 int orbfe_extractor_capacity(orbfe_extractor* h, int width, int height);
 

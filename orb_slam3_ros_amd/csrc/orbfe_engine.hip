@@ -795,6 +795,32 @@ int orbfe_batch_outputs(orbfe_extractor* h, orbfe_keypoint** d_kps, uint8_t** d_
     return ORBFE_OK;
 }
 
+int orbfe_extractor_set_opencv_model(orbfe_extractor* h, int resize_simd_lanes, int blur_variant) {
+    if (!h || blur_variant < 0 || blur_variant > 1) return ORBFE_E_ARG;
+    if (resize_simd_lanes != 0 && resize_simd_lanes != 8 && resize_simd_lanes != 16 && resize_simd_lanes != 32 &&
+        resize_simd_lanes != 64)
+        return ORBFE_E_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    std::lock_guard<std::mutex> lk2(h->mu_stereo);   // the batch buffers the stereo calls read are released
+    if (h->resize_simd_lanes == resize_simd_lanes && h->blur_variant == blur_variant) return ORBFE_OK;
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());   // in-flight batches read the handle's tables
+    h->resize_simd_lanes = resize_simd_lanes;
+    h->blur_variant = blur_variant;
+    // the resize tables (simd_end per level) depend on the lane count: the next batch rebuilds the
+    // geometry and its buffers
+    free_buffers(h);
+    h->W = h->H = 0;
+    return ORBFE_OK;
+}
+
+int orbfe_extractor_get_opencv_model(const orbfe_extractor* h, int* resize_simd_lanes, int* blur_variant) {
+    if (!h) return ORBFE_E_ARG;
+    if (resize_simd_lanes) *resize_simd_lanes = h->resize_simd_lanes;
+    if (blur_variant) *blur_variant = h->blur_variant;
+    return ORBFE_OK;
+}
+
 int orbfe_extractor_set_path(orbfe_extractor* h, int path) {
     if (!h || path < 0 || path > 1) return ORBFE_E_ARG;
     std::lock_guard<std::mutex> lk(h->mu);

@@ -66,6 +66,19 @@ class ORBextractor:
     def handle(self) -> ctypes.c_void_p:
         return self._h
 
+    def set_opencv_model(self, resize_simd_lanes: int = 16, blur_variant: int = 0):
+        """Select the OpenCV build behaviour to reproduce (orbfe_extractor_set_opencv_model):
+        cv::resize's universal-intrinsic lane count (0, 8, 16, 32, 64) and the GaussianBlur Q8
+        kernel (0 = error diffusion, 1 = per-tap rounding)."""
+        _lib.check(self._lib.orbfe_extractor_set_opencv_model(self._h, int(resize_simd_lanes), int(blur_variant)),
+                   "orbfe_extractor_set_opencv_model")
+
+    def opencv_model(self) -> tuple[int, int]:
+        lanes, blur = ctypes.c_int(), ctypes.c_int()
+        _lib.check(self._lib.orbfe_extractor_get_opencv_model(self._h, ctypes.byref(lanes), ctypes.byref(blur)),
+                   "orbfe_extractor_get_opencv_model")
+        return lanes.value, blur.value
+
     def set_path(self, path: int):
         """0 = fused band pyramid+FAST pass (where the geometry allows), 1 = k_resize chain + k_fast
         overlapped on a side stream (the default)."""

@@ -154,6 +154,15 @@ class StereoFrontEnd:
             self._lap_key = key
         return self._lap_arr
 
+    def set_opencv_model(self, resize_simd_lanes: int = 16, blur_variant: int = 0):
+        """orbfe_extractor_set_opencv_model on every pipeline handle (see ORBextractor.set_opencv_model);
+        the handles rebuild their buffers, so the outputs are re-bound."""
+        for h in self.handles:
+            _lib.check(self.lib.orbfe_extractor_set_opencv_model(h, int(resize_simd_lanes), int(blur_variant)),
+                       "set_opencv_model")
+            self.lib.orbfe_extractor_capacity(h, self.W, self.H)
+        self.bind_outputs(self.counts, self.kps, self.desc)
+
     def set_path(self, path: int):
         """Choose the pyramid+FAST implementation (0 = fused band pass where the geometry allows it,
         1 = k_resize + k_fast) for every pipeline handle."""

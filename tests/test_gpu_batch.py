@@ -103,12 +103,12 @@ def _frame_map(nframes, nunique, seed):
 
 
 @pytest.mark.parametrize("path", [1, 0], ids=["split", "fused"])
-def test_bench_path_config2_b512(gpu, oracle_lib, path):
-    """BASELINE config 2 at bench.py's batch: 256 stereo frames = 512 images per launch, through
+def test_bench_path_config2_f512(gpu, oracle_lib, path):
+    """BASELINE config 2 at bench.py's batch: 512 stereo frames = 1024 images per launch, through
     the default split pyramid+FAST path (k_resize chain with FAST overlapped on a side stream) and
     the fused band pass."""
     from orb_slam3_ros_amd.frontend import StereoFrontEnd
-    F, U = 256, 24
+    F, U = 512, 32
     pairs = [synth_stereo(500 + i, 752, 480) for i in range(U)]
     fmap = _frame_map(F, U, 1)
     refs = _oracle_refs(oracle_lib, pairs, 1000, (0, 0), (0, 0), EUROC_BF, EUROC_FX, "rectified")
