@@ -480,8 +480,6 @@ def main():
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--nfeatures", type=int, default=1000)
     ap.add_argument("--unique", type=int, default=32, help="distinct synthetic frames (tiled over the batch)")
-    ap.add_argument("--path", choices=["default", "fused", "legacy"], default="default",
-                    help="pyramid+FAST implementation (default: the library's)")
     ap.add_argument("--pipelines", type=int, default=1, help="sub-batches on separate HIP streams")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -524,8 +522,6 @@ def main():
     bf, fx = EUROC_BF, EUROC_FX
     images, pairs, fmap = make_images(rank, W, H, F, args.unique, dev)
     fe = StereoFrontEnd(F, W, H, nfeatures=args.nfeatures, bf=bf, fx=fx, device=dev, pipelines=args.pipelines)
-    if args.path != "default":
-        fe.set_path(0 if args.path == "fused" else 1)
     gather = world > 1 and not args.no_allgather
     if gather:
         # zero-copy, double-buffered slab exchange: the extractor writes step k's outputs into slab
@@ -611,8 +607,7 @@ def main():
     if rank == 0:
         n_img = 2 * F
         pyr_fast_ms = stages["pyramid_fast"]
-        pf_kernel = ("pyramid+FAST pass, fused: k_pyrfast x8 levels (FAST of level l + resize of level l+1)"
-                     if fe.path() == 0 else "pyramid+FAST pass: k_resize_s x7 + k_fast")
+        pf_kernel = "pyramid+FAST pass: k_resize_s x7 + k_fast"
         bytes_img = algorithmic_bytes(W, H)
         achieved = n_img * bytes_img / (pyr_fast_ms * 1e-3) / 1e9 if pyr_fast_ms > 0 else 0.0
         dominant = max(stages, key=stages.get)

@@ -105,15 +105,6 @@ int orbfe_batch_outputs(orbfe_extractor* h, orbfe_keypoint** d_kps, uint8_t** d_
 int orbfe_set_batch_outputs(orbfe_extractor* h, orbfe_keypoint* d_kps, uint8_t* d_desc, int* d_counts,
                             int cap_images);
 
-/* Pyramid + FAST implementation of this handle: path 1 (default) = k_resize per level + k_fast
- * launches beside the chain; path 0 (opt-in) = the fused band pass (one launch per level: FAST
- * cells of level l and the resize of level l+1 from the same staged rows, each level read from HBM
- * once), used when the level geometry allows it, else path 1. Both are bit-exact; path 0 measured
- * 2.1x slower on MI355X. orbfe_extractor_get_path returns the path a width x height
- * batch will take (0 or 1). */
-int orbfe_extractor_set_path(orbfe_extractor* h, int path);
-int orbfe_extractor_get_path(orbfe_extractor* h, int width, int height);
-
 /* Per-kernel HIP-event timing (for bench.py's roofline). While enabled, every batch records
  * events around each stage on the stream it runs on (no host sync). orbfe_get_stage_timing waits
  * for the recorded batches, writes the MEAN ms per batch of each stage to ms[0..ORBFE_NUM_STAGES)

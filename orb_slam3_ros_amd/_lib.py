@@ -43,8 +43,6 @@ _SIGS = {
     "orbfe_extract_batch_laps": (_c_int, [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp]),
     "orbfe_batch_outputs": (_c_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp), _P_int]),
     "orbfe_set_stage_timing": (_c_int, [_vp, _c_int]),
-    "orbfe_extractor_set_path": (_c_int, [_vp, _c_int]),
-    "orbfe_extractor_get_path": (_c_int, [_vp, _c_int, _c_int]),
     "orbfe_extractor_set_opencv_model": (_c_int, [_vp, _c_int, _c_int]),
     "orbfe_extractor_get_opencv_model": (_c_int, [_vp, _P_int, _P_int]),
     "orbfe_set_batch_outputs": (_c_int, [_vp, _vp, _vp, _vp, _c_int]),

@@ -19,7 +19,6 @@
 
 // Single translation unit: the kernels are compiled together with their launchers.
 #include "orbfe_kernels.hip"
-#include "orbfe_pyrfast.hip"
 
 using namespace orbfe;
 
@@ -86,7 +85,6 @@ struct orbfe_extractor {
     uint8_t* d_pyr = nullptr;
     uint32_t* d_cellkeys = nullptr;
     int* d_cellcnt = nullptr;
-    int* d_fblist = nullptr;      // fused pass: [count, (image << 16 | cell) ...] cells for k_fallback
     uint32_t* d_lkeys = nullptr;
     uint16_t* d_nodeof = nullptr;
     uint32_t* d_outkeys = nullptr;
@@ -124,10 +122,6 @@ struct orbfe_extractor {
     uint8_t* last_desc = nullptr;
     int* last_counts = nullptr;
     std::mutex mu;
-    int path = 1;                  // 0: fused band pass when the geometry allows it; 1: k_resize + k_fast (default)
-    uint8_t* d_l0 = nullptr;       // level 0 copied to a 16-byte pitch (fused pass, unaligned input rows)
-    const uint8_t** d_l0_ptrs = nullptr;
-    int l0_cap = 0;
     unsigned long long* d_oct_ts = nullptr;   // -DORBFE_OCT_STAMPS builds: per-phase s_memtime of the octree (image 0)
 };
 
@@ -135,16 +129,11 @@ static void free_buffers(orbfe_extractor* h) {
     void** bufs[] = {(void**)&h->d_tab, (void**)&h->d_pyr, (void**)&h->d_cellkeys,
                      (void**)&h->d_cellcnt, (void**)&h->d_lkeys, (void**)&h->d_nodeof, (void**)&h->d_outkeys,
                      (void**)&h->d_lvinfo, (void**)&h->d_ranks, (void**)&h->d_kps, (void**)&h->d_desc,
-                     (void**)&h->d_counts, (void**)&h->d_ptrs, (void**)&h->d_fblist};
+                     (void**)&h->d_counts, (void**)&h->d_ptrs};
     for (void** p : bufs) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
-    if (h->d_l0) (void)hipFree(h->d_l0);
-    if (h->d_l0_ptrs) (void)hipFree(h->d_l0_ptrs);
-    h->d_l0 = nullptr;
-    h->d_l0_ptrs = nullptr;
-    h->l0_cap = 0;
     h->cap_b = 0;
     h->last_nimg = 0;   // the previous batch's intermediates are gone
     h->last_kps = nullptr;
@@ -152,94 +141,6 @@ static void free_buffers(orbfe_extractor* h) {
     h->last_counts = nullptr;
     h->last_ptrs.clear();
     h->last_laps.clear();
-}
-
-// Geometry of the fused pass for level l (orbfe_pyrfast.hip): slices (runs of whole cells that fit
-// one wave's 64 lanes x 4 columns, with the output column groups of level l+1 whose sources start in
-// them) and bands (cell rows: streamed source rows, owned output rows of level l+1), appended to tab.
-// false = the level needs the legacy k_resize + k_fast pair (clipped or skipped interior cells, a
-// cell too wide for a wave, bands taller than 255 rows, LDS).
-static bool build_bands(OrbGeom& g, int l, std::vector<int16_t>& tab, const FastLds& fl) {
-    OrbLevel& L = g.lv[l];
-    const int maxBX = L.w - ORBFE_MINB, maxBY = L.h - ORBFE_MINB;
-    const int wc = L.w_cell, hc = L.h_cell, ncols = L.n_cols, nrows = L.n_rows;
-    // the cells' detection rectangles must tile the level: no interior cell clipped at maxB, no
-    // cell skipped (ORBextractor.cc:807-822)
-    for (int j = 0; j + 1 < ncols; j++)
-        if (ORBFE_MINB + j * wc + wc + 6 > maxBX) return false;
-    for (int i = 0; i + 1 < nrows; i++)
-        if (ORBFE_MINB + i * hc + hc + 6 > maxBY) return false;
-    if (ORBFE_MINB + (ncols - 1) * wc >= maxBX - 6 || ORBFE_MINB + (nrows - 1) * hc >= maxBY - 3) return false;
-    if (ncols > 255) return false;
-    const bool has_next = l + 1 < g.nlevels;
-    const OrbLevel* L1 = has_next ? &g.lv[l + 1] : nullptr;
-    const int w1 = has_next ? L1->w : 0, ng1 = (w1 + 3) / 4;
-    const int xdet0 = ORBFE_MINB + 3, xdet1 = L.w - ORBFE_MINB - 3;
-    auto c_lo = [&](int j) { return xdet0 + j * wc; };
-    auto c_hi = [&](int j) { return j == ncols - 1 ? xdet1 : xdet0 + (j + 1) * wc; };
-    auto sx_of = [&](int dx) { return (int)tab[L1->tab_x + 3 * dx]; };
-    // slice s = cells [J[s], J[s+1]); owned output groups: sx(4g) in [S(s), S(s+1)), S(0) = 0
-    auto try_slices = [&](int n, std::vector<int16_t>& out) -> bool {
-        out.clear();
-        std::vector<int> J(n + 1);
-        for (int s = 0; s <= n; s++) J[s] = (int)((long)ncols * s / n);
-        int gcur = 0;
-        for (int s = 0; s < n; s++) {
-            const int j0 = J[s], j1 = J[s + 1];
-            if (j1 <= j0 || j1 - j0 > PF_MAXC) return false;
-            const int S1 = s + 1 < n ? c_lo(j1) : (1 << 30);
-            int g1 = gcur;
-            while (g1 < ng1 && sx_of(4 * g1) < S1) g1++;
-            int src_lo = 1 << 30, src_hi = -1;
-            if (g1 > gcur) {
-                src_lo = s == 0 ? 0 : sx_of(4 * gcur);
-                for (int dx = 4 * gcur; dx < std::min(4 * g1, w1); dx++) src_hi = std::max(src_hi, sx_of(dx) + 1);
-            }
-            const int A0 = std::max(0, std::min(c_lo(j0) - 4, src_lo)) & ~3;
-            if (c_hi(j1 - 1) > A0 + 252) return false;                     // centres in lanes 1..62
-            if (src_hi >= 0 && src_hi > A0 + 255) return false;            // resize sources in the ring
-            if (g1 - gcur > 64) return false;                              // one output group per lane
-            out.push_back((int16_t)A0);
-            out.push_back((int16_t)(j0 | (j1 << 8)));
-            out.push_back((int16_t)gcur);
-            out.push_back((int16_t)g1);
-            gcur = g1;
-        }
-        return gcur == ng1;
-    };
-    std::vector<int16_t> sl;
-    int nsl = 1;
-    while (nsl <= ncols && !try_slices(nsl, sl)) nsl++;
-    if (nsl > ncols) return false;
-    L.pf_ns = nsl;
-    L.pf_slice_tab = (int)tab.size();
-    tab.insert(tab.end(), sl.begin(), sl.end());
-    L.pf_band_tab = (int)tab.size();
-    int e = 0;
-    const int h1 = has_next ? L1->h : 0;
-    for (int i = 0; i < nrows; i++) {
-        const int iniY = ORBFE_MINB + i * hc, roi_end = std::min(iniY + hc + 6, maxBY);
-        const int Yi = i == 0 ? 0 : iniY, Yn = i == nrows - 1 ? L.h : iniY + hc;
-        const int e_lo = e;
-        while (e < h1 && tab[L1->tab_y + 4 * e] < Yn) e++;
-        const int e_hi = e;
-        int ry0 = std::min(iniY, Yi), ry1 = roi_end;
-        if (e_hi > e_lo) {
-            if (tab[L1->tab_y + 4 * e_lo] < Yi) return false;
-            ry0 = std::min(ry0, (int)tab[L1->tab_y + 4 * e_lo]);
-            ry1 = std::max(ry1, (int)tab[L1->tab_y + 4 * (e_hi - 1) + 1] + 1);
-        }
-        if (ry1 - ry0 > 255 || ry1 > L.h || e_hi - e_lo > PF_TYCAP) return false;
-        tab.push_back((int16_t)ry0);
-        tab.push_back((int16_t)ry1);
-        tab.push_back((int16_t)e_lo);
-        tab.push_back((int16_t)e_hi);
-    }
-    if (e != h1) return false;
-    const size_t lds = (size_t)PF_LDS_BYTES;
-    if (lds > 64 * 1024) return false;
-    L.pf_lds = (int)lds;
-    return true;
 }
 
 // Per-level geometry with the reference's expressions (see orbfe_types.h), derived into the
@@ -401,8 +302,6 @@ static int build_geom(const orbfe_extractor* h, int W, int H, OrbGeom& g, std::v
     fl.wave_bytes = fl.roi + fl.sc + fl.cor + FAST_ENT_BYTES;
     fast_lds = fl;
     oct_lds = octree_lds_bytes(g);
-    g.pf_ok = 1;
-    for (int l = 0; l < g.nlevels && g.pf_ok; l++) g.pf_ok = build_bands(g, l, tab, fl) ? 1 : 0;
     if (oct_lds > 160 * 1024) return ORBFE_E_ARG;
     if ((size_t)4 * fast_lds.wave_bytes > 160 * 1024) return ORBFE_E_ARG;   // k_fast: 4 waves per block
     return ORBFE_OK;
@@ -437,7 +336,6 @@ static int ensure(orbfe_extractor* h, int W, int H, int B) {
     HIPCHK(hipMalloc(&h->d_pyr, (size_t)B * g.pyr_bytes));
     HIPCHK(hipMalloc(&h->d_cellkeys, (size_t)B * g.cellkeys_per_img * 4));
     HIPCHK(hipMalloc(&h->d_cellcnt, (size_t)B * g.total_cells * 4));
-    HIPCHK(hipMalloc(&h->d_fblist, ((size_t)B * g.total_cells + 1) * 4));
     HIPCHK(hipMalloc(&h->d_lkeys, (size_t)B * g.cellkeys_per_img * 4));
     HIPCHK(hipMalloc(&h->d_nodeof, (size_t)B * g.cellkeys_per_img * 2));
     HIPCHK(hipMalloc(&h->d_outkeys, (size_t)B * g.out_per_img * 4));
@@ -492,53 +390,7 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
     OrbKeyPoint* o_kps = ext ? h->ext_kps : h->d_kps;
     uint8_t* o_desc = ext ? h->ext_desc : h->d_desc;
     int* o_counts = ext ? h->ext_counts : h->d_counts;
-    if (g.pf_ok && h->path == 0) {
-        // fused band pass (orbfe_pyrfast.hip): one launch per level; its dword row loads need
-        // 4-byte aligned rows, otherwise level 0 is first copied to a 16-byte pitch
-        bool al = (pitch & 3) == 0;
-        for (int i = 0; al && i < B; i++) al = (((uintptr_t)host_ptrs[i]) & 3) == 0;
-        const uint8_t* const* P0 = P;
-        int pitch0 = pitch;
-        if (!al) {
-            const int p16 = round_up(g.width, 16);
-            if (h->l0_cap < B) {
-                if (h->d_l0) HIPCHK(hipFree(h->d_l0));
-                if (h->d_l0_ptrs) HIPCHK(hipFree(h->d_l0_ptrs));
-                h->d_l0 = nullptr;
-                h->d_l0_ptrs = nullptr;
-                h->l0_cap = 0;
-                HIPCHK(hipMalloc(&h->d_l0, (size_t)B * g.height * p16));
-                HIPCHK(hipMalloc(&h->d_l0_ptrs, (size_t)B * sizeof(void*)));
-                std::vector<const uint8_t*> lp(B);
-                for (int i = 0; i < B; i++) lp[i] = h->d_l0 + (size_t)i * g.height * p16;
-                HIPCHK(hipMemcpy(h->d_l0_ptrs, lp.data(), (size_t)B * sizeof(void*), hipMemcpyHostToDevice));
-                h->l0_cap = B;
-            }
-            hipLaunchKernelGGL(k_repitch, dim3((g.height + 3) / 4, B), dim3(256), 0, s, P, pitch, h->d_l0, p16,
-                               g.width, g.height);
-            P0 = h->d_l0_ptrs;
-            pitch0 = p16;
-        }
-#if (PF_ABL & 2)
-        // timing-only ablation without the fused resize: the pyramid comes from k_resize instead
-        for (int l = 1; l < g.nlevels; l++) {
-            const int tiles_y = (g.lv[l].h + g.lv[l].rz_rows - 1) / g.lv[l].rz_rows;
-            dim3 grid((g.lv[l].w + g.lv[l].rz_cols - 1) / g.lv[l].rz_cols, (tiles_y + RZ_TPB - 1) / RZ_TPB, B);
-            hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, s, P, pitch, h->d_pyr, g.pyr_bytes, h->d_tab, g, l);
-        }
-        if (tm) HIPCHK(hipEventRecord(ev[0], s));   // the pyramid_fast stage then times k_pyrfast alone
-#endif
-        HIPCHK(hipMemsetAsync(h->d_fblist, 0, 4, s));
-        for (int l = 0; l < g.nlevels; l++) {
-            const OrbLevel& L = g.lv[l];
-            hipLaunchKernelGGL(k_pyrfast, dim3(L.n_rows * L.pf_ns, B), dim3(64), (size_t)L.pf_lds, s, P0, pitch0,
-                               h->d_pyr, g.pyr_bytes, h->d_tab, g, l, h->d_cellkeys, h->d_cellcnt, h->d_fblist);
-        }
-        // the listed cells' minThFAST re-run: a fixed grid of 4-wave blocks looping over the list
-        hipLaunchKernelGGL(k_fallback, dim3(std::min(256, std::max(1, B * g.total_cells / 64))), dim3(256),
-                           (size_t)4 * h->fast_lds.wave_bytes, s, P0, pitch0, h->d_pyr, g.pyr_bytes, g, h->fast_lds,
-                           h->d_cellkeys, h->d_cellcnt, h->d_fblist);
-    } else {
+    {
         // ComputePyramid's chain (level l from level l - 1) is a sequence of dependent k_resize
         // launches on the batch stream; k_fast launches (level l's cells are [lv[l].cell_base,
         // lv[l + 1].cell_base)) run beside it on the low-priority side stream as their levels
@@ -724,8 +576,6 @@ void orbfe_extractor_destroy(orbfe_extractor* h) {
     (void)hipDeviceSynchronize();
     free_buffers(h);
     if (h->d_stage) (void)hipFree(h->d_stage);
-    if (h->d_l0) (void)hipFree(h->d_l0);
-    if (h->d_l0_ptrs) (void)hipFree(h->d_l0_ptrs);
     if (h->d_uright) (void)hipFree(h->d_uright);
     if (h->d_depth) (void)hipFree(h->d_depth);
     if (h->d_nmatch) (void)hipFree(h->d_nmatch);
@@ -819,23 +669,6 @@ int orbfe_extractor_get_opencv_model(const orbfe_extractor* h, int* resize_simd_
     if (resize_simd_lanes) *resize_simd_lanes = h->resize_simd_lanes;
     if (blur_variant) *blur_variant = h->blur_variant;
     return ORBFE_OK;
-}
-
-int orbfe_extractor_set_path(orbfe_extractor* h, int path) {
-    if (!h || path < 0 || path > 1) return ORBFE_E_ARG;
-    std::lock_guard<std::mutex> lk(h->mu);
-    h->path = path;
-    return ORBFE_OK;
-}
-
-int orbfe_extractor_get_path(orbfe_extractor* h, int width, int height) {
-    if (!h) return ORBFE_E_ARG;
-    std::lock_guard<std::mutex> lk(h->mu);
-    if (width != h->W || height != h->H) {
-        int rc = ensure(h, width, height, std::max(h->cap_b, 1));
-        if (rc) return rc;
-    }
-    return (h->g.pf_ok && h->path == 0) ? 0 : 1;
 }
 
 int orbfe_set_stage_timing(orbfe_extractor* h, int enable) {
@@ -1032,17 +865,6 @@ int orbfe_debug_block_sort(uint64_t* data, int n) {
     return n;
 }
 
-#ifdef PF_STATS
-int orbfe_debug_pf_stats(unsigned long long* out, int reset) {
-    HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pf_stats), sizeof(unsigned long long) * 64));
-    if (reset) {
-        unsigned long long z[64] = {};
-        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_pf_stats), z, sizeof(z)));
-    }
-    return 64;
-}
-#endif
 
 int orbfe_descriptor_distance(const uint8_t* a, const uint8_t* b) {
     int d = 0;

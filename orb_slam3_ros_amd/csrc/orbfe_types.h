@@ -34,11 +34,6 @@ struct OrbLevel {
     int rz_rows, rz_cols;     // output rows / cols per k_resize block (fit the LDS source window)
     int rs_ok;                // k_resize_s can build this level (every lane's byte windows fit, host-checked)
     int rs_rows;              // output rows per k_resize_s wave (<= 64)
-    // fused pass (k_pyrfast): one wave per (band = cell row, slice = run of whole cells)
-    int pf_ns;                // slices per band
-    int pf_band_tab;          // int16 table offset: {ry0, ry1, e_lo, e_hi} per band
-    int pf_slice_tab;         // int16 table offset: {A0, j0 | j1 << 8, g0, g1} per slice
-    int pf_lds;               // dynamic LDS bytes of the level's launch (one wave)
 };
 
 struct OrbGeom {
@@ -52,7 +47,6 @@ struct OrbGeom {
     int pyr_bytes;            // bytes of levels >= 1 per image (padded)
     int max_cells_level;      // max cells in one level
     int node_cap;             // octree node capacity (max over levels)
-    int pf_ok;                // every level can take the fused band pass (else k_resize + k_fast)
     int pyr_slack;            // offset of a 256 B scratch area at the end of each image's pyramid slab
                               // (k_resize_s's idle lanes store there, so its store count is static)
     OrbLevel lv[ORBFE_MAX_LEVELS];

@@ -79,14 +79,6 @@ class ORBextractor:
                    "orbfe_extractor_get_opencv_model")
         return lanes.value, blur.value
 
-    def set_path(self, path: int):
-        """0 = fused band pyramid+FAST pass (where the geometry allows), 1 = k_resize chain + k_fast
-        overlapped on a side stream (the default)."""
-        _lib.check(self._lib.orbfe_extractor_set_path(self._h, int(path)), "orbfe_extractor_set_path")
-
-    def path(self, width: int, height: int) -> int:
-        return _lib.check(self._lib.orbfe_extractor_get_path(self._h, int(width), int(height)), "get_path")
-
     def capacity(self, width: int, height: int) -> int:
         return _lib.check(self._lib.orbfe_extractor_capacity(self._h, int(width), int(height)), "capacity")
 

@@ -163,16 +163,6 @@ class StereoFrontEnd:
             self.lib.orbfe_extractor_capacity(h, self.W, self.H)
         self.bind_outputs(self.counts, self.kps, self.desc)
 
-    def set_path(self, path: int):
-        """Choose the pyramid+FAST implementation (0 = fused band pass where the geometry allows it,
-        1 = k_resize + k_fast) for every pipeline handle."""
-        for h in self.handles:
-            _lib.check(self.lib.orbfe_extractor_set_path(h, int(path)), "set_path")
-
-    def path(self) -> int:
-        """Pyramid+FAST implementation the batches take (0 = fused band pass, 1 = k_resize + k_fast)."""
-        return _lib.check(self.lib.orbfe_extractor_get_path(self.h, self.W, self.H), "get_path")
-
     def set_stage_timing(self, on: bool):
         for h in self.handles:
             self.lib.orbfe_set_stage_timing(h, 1 if on else 0)

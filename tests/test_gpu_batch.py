@@ -102,11 +102,9 @@ def _frame_map(nframes, nunique, seed):
     return rng.permutation(m)[:nframes]
 
 
-@pytest.mark.parametrize("path", [1, 0], ids=["split", "fused"])
-def test_bench_path_config2_f512(gpu, oracle_lib, path):
-    """BASELINE config 2 at bench.py's batch: 512 stereo frames = 1024 images per launch, through
-    the default split pyramid+FAST path (k_resize chain with FAST overlapped on a side stream) and
-    the fused band pass."""
+def test_bench_path_config2_f512(gpu, oracle_lib):
+    """BASELINE config 2 at bench.py's batch: 512 stereo frames = 1024 images per launch (k_resize_s
+    chain with k_fast overlapped on a side stream, octree, describe, stereo)."""
     from orb_slam3_ros_amd.frontend import StereoFrontEnd
     F, U = 512, 32
     pairs = [synth_stereo(500 + i, 752, 480) for i in range(U)]
@@ -114,8 +112,6 @@ def test_bench_path_config2_f512(gpu, oracle_lib, path):
     refs = _oracle_refs(oracle_lib, pairs, 1000, (0, 0), (0, 0), EUROC_BF, EUROC_FX, "rectified")
     images = _images(pairs, fmap, gpu)
     fe = StereoFrontEnd(F, 752, 480, nfeatures=1000, bf=EUROC_BF, fx=EUROC_FX, device=gpu)
-    fe.set_path(path)
-    assert fe.path() == path
     for _ in range(2):   # a repeated run over the same buffers must give the same answer
         fe.run(images)
         _check_batch(fe, fmap, refs)

@@ -51,10 +51,9 @@ def _cell_geom(w, h):
     return ncols * nrows, ((wc + 1) // 2) * ((hc + 1) // 2)
 
 
-def _compare_extract(img, nfeat, lap, oracle_lib, check_stages=True, path=0):
+def _compare_extract(img, nfeat, lap, oracle_lib, check_stages=True):
     from orb_slam3_ros_amd.extractor import ORBextractor
     ext = ORBextractor(nfeat, 1.2, 8, 20, 7)
-    ext.set_path(path)
     ora = oracle_lib.OracleExtractor(nfeat, 1.2, 8, 20, 7)
     mono_g, kp_g, d_g = ext(img, None, lap)
     mono_o, kp_o, d_o = ora(img, lap)
@@ -91,25 +90,12 @@ def _compare_extract(img, nfeat, lap, oracle_lib, check_stages=True, path=0):
     return len(kp_g)
 
 
-@pytest.mark.parametrize("path", [0, 1])
 @pytest.mark.parametrize("w,h,nfeat", CONFIGS)
-def test_extract_matches_oracle(w, h, nfeat, path, gpu, oracle_lib):
-    """Every intermediate, both pyramid+FAST implementations (0 = fused band pass, 1 = k_resize +
-    k_fast)."""
+def test_extract_matches_oracle(w, h, nfeat, gpu, oracle_lib):
+    """Every intermediate: pyramid levels, per-cell FAST keys, octree output, final outputs."""
     img = synth_image(100 + w, w, h)
-    n = _compare_extract(img, nfeat, (0, 0), oracle_lib, path=path)
+    n = _compare_extract(img, nfeat, (0, 0), oracle_lib)
     assert n >= nfeat * 0.9
-
-
-@pytest.mark.parametrize("w,h", [(752, 480), (1241, 376), (512, 512), (640, 480), (1280, 720)])
-def test_fused_path_geometry(w, h, gpu):
-    """The fused band pass covers the BASELINE sizes (and common camera sizes)."""
-    from orb_slam3_ros_amd.extractor import ORBextractor
-    ext = ORBextractor(1000, 1.2, 8, 20, 7)
-    assert ext.path(w, h) == 1   # the split path is the default
-    ext.set_path(0)
-    assert ext.path(w, h) == 0
-    ext.close()
 
 
 @pytest.mark.parametrize("lap", [(0, 1000), (0, 511), (200, 400)])
@@ -124,15 +110,14 @@ def test_more_seeds(seed, gpu, oracle_lib):
     _compare_extract(img, 1000, (0, 1000), oracle_lib, check_stages=False)
 
 
-@pytest.mark.parametrize("path", [0, 1])
-def test_flat_and_noise_images(path, gpu, oracle_lib):
+def test_flat_and_noise_images(gpu, oracle_lib):
     flat = np.full((480, 752), 128, np.uint8)
-    _compare_extract(flat, 1000, (0, 0), oracle_lib, check_stages=False, path=path)
+    _compare_extract(flat, 1000, (0, 0), oracle_lib, check_stages=False)
     rng = np.random.default_rng(5)
     noise = rng.integers(0, 256, (480, 752), dtype=np.uint8)
-    _compare_extract(noise, 1000, (0, 0), oracle_lib, path=path)
+    _compare_extract(noise, 1000, (0, 0), oracle_lib)
     grad = np.tile(np.arange(752, dtype=np.uint8), (480, 1))
-    _compare_extract(grad, 1000, (0, 0), oracle_lib, check_stages=False, path=path)
+    _compare_extract(grad, 1000, (0, 0), oracle_lib, check_stages=False)
 
 
 def test_small_image(gpu, oracle_lib):
