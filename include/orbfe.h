@@ -336,6 +336,52 @@ int orbfe_search_local_points_device(const orbfe_frame* F, const orbfe_camera* c
                                      int32_t bFarPoints, float thFarPoints, float nnratio, int32_t* n_to_match,
                                      void* stream);
 
+/* Camera models of GeometricCamera (CameraModels/Pinhole.cpp, KannalaBrandt8.cpp): params =
+ * mvParameters, {fx, fy, cx, cy} for the pinhole model, {fx, fy, cx, cy, k0, k1, k2, k3} for
+ * KannalaBrandt8, whose project() (KannalaBrandt8.cpp:67-82) runs on the device with bit-exact ports
+ * of glibc's atan2f / cosf / sinf. */
+#define ORBFE_CAM_PINHOLE 0
+#define ORBFE_CAM_KANNALA_BRANDT8 1
+typedef struct orbfe_camera_model {
+    int32_t type;                    /* ORBFE_CAM_* */
+    float params[8];
+} orbfe_camera_model;                /* 36 bytes */
+
+/* What Frame::isInFrustum reads of a frame besides orbfe_camera's pose: mpCamera, and for a
+ * two-camera frame (orbfe_frame.two_cams: Nleft != -1) mpCamera2 and the rig (Frame.cc:1168-1242):
+ * Rrl / trl = mTrl.rotationMatrix() / translation() (row-major), tlr = mTlr.translation(), Rwc = mRwc
+ * (row-major). The right-view pose is derived in the reference's order: mR = Rrl * mRcw, mt = Rrl *
+ * mtcw + trl, twc = mRwc * tlr + mOw (Eigen 3.3 fixed-size products). */
+typedef struct orbfe_stereo_rig {
+    orbfe_camera_model left;         /* Frame::mpCamera */
+    orbfe_camera_model right;        /* Frame::mpCamera2 (two-camera frames) */
+    float Rrl[9], trl[3];
+    float tlr[3];
+    float Rwc[9];
+} orbfe_stereo_rig;
+
+/* Frame::isInFrustum for any camera model (Frame.cc:512-586): a single-camera frame takes the
+ * Nleft == -1 branch with rig->left as mpCamera (a monocular KannalaBrandt8 frame included); a
+ * two-camera frame runs isInFrustumChecks for the left and the right camera (Frame.cc:1168-1242):
+ * track[i] gets ORBFE_MP_IN_VIEW with proj_x / proj_y / scale_level / view_cos / depth (left) and
+ * ORBFE_MP_IN_VIEW_R with proj_xr / proj_yr / scale_level_r / view_cos_r (right), scale levels -1
+ * where a check fails (the reference resets mnTrackScaleLevel(R) to -1, :578-579). Returns nToMatch
+ * (points with either view). cam supplies the pose (Rcw, tcw, Ow), mfLogScaleFactor and the cosine
+ * limit; its pinhole fields are not read. A failed left check leaves depth 0 (the reference keeps the
+ * previous frame's mTrackDepth, which only bFarPoints reads). */
+int orbfe_is_in_frustum_rig(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_stereo_rig* rig,
+                            const orbfe_map_point_3d* pts, int32_t n, orbfe_map_point* track);
+/* Tracking::SearchLocalPoints (Tracking.cc:3407-3452) with the rig's camera models: the projection
+ * above, then SearchByProjection(F, points, th, bFarPoints, thFarPoints) with its two-camera branches
+ * when F->two_cams (ORBmatcher.cc:43-213). Host and device-resident forms as orbfe_search_local_points. */
+int orbfe_search_local_points_rig(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_stereo_rig* rig,
+                                  const orbfe_map_point_3d* pts, int32_t n, int32_t* mvp, const int32_t* mvp_obs,
+                                  float th, int32_t bFarPoints, float thFarPoints, float nnratio, int32_t* n_to_match);
+int orbfe_search_local_points_rig_device(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_stereo_rig* rig,
+                                         const orbfe_map_point_3d* d_pts, int32_t n, int32_t* d_mvp,
+                                         const int32_t* d_mvp_obs, float th, int32_t bFarPoints, float thFarPoints,
+                                         float nnratio, int32_t* n_to_match, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Back-end matcher pieces (LocalMapping / LoopClosing threads)
  * ------------------------------------------------------------------------------------------- */

@@ -144,6 +144,8 @@ def _match_sigs(L):
     L.oro_search_by_sim3.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, cf, vp, vp]
     L.oro_is_in_frustum.argtypes = [vp, vp, vp, ci, vp]
     L.oro_search_local_points.argtypes = [vp, vp, vp, ci, vp, vp, cf, ci, cf, cf, vp]
+    L.oro_is_in_frustum_rig.argtypes = [vp, vp, vp, vp, ci, vp]
+    L.oro_search_local_points_rig.argtypes = [vp, vp, vp, vp, ci, vp, vp, cf, ci, cf, cf, vp]
     return L
 
 
@@ -249,23 +251,25 @@ def distinctive_descriptors(desc, offsets):
     return best
 
 
-def is_in_frustum(F, cam, pts3d):
-    """(nToMatch, tracking records) — the caller passes MAP_POINT_DTYPE / MAP_POINT_3D_DTYPE arrays."""
+def is_in_frustum(F, cam, pts3d, rig=None):
+    """(nToMatch, tracking records) — the caller passes MAP_POINT_DTYPE / MAP_POINT_3D_DTYPE arrays;
+    rig: a StereoRig (camera models, right view) or None (pinhole from cam)."""
     from orb_slam3_ros_amd.matcher import MAP_POINT_DTYPE
     L = _match_sigs(lib())
     pts = np.ascontiguousarray(pts3d)
     track = np.zeros(len(pts), MAP_POINT_DTYPE)
-    n = L.oro_is_in_frustum(F.ref(), ctypes.byref(cam), pts.ctypes.data, len(pts), track.ctypes.data)
+    n = L.oro_is_in_frustum_rig(F.ref(), ctypes.byref(cam), ctypes.byref(rig) if rig is not None else None,
+                                pts.ctypes.data, len(pts), track.ctypes.data)
     return n, track
 
 
-def search_local_points(F, cam, pts3d, mvp, mvp_obs, th=1.0, bFar=False, thFar=50.0, nnratio=0.8):
+def search_local_points(F, cam, pts3d, mvp, mvp_obs, th=1.0, bFar=False, thFar=50.0, nnratio=0.8, rig=None):
     L = _match_sigs(lib())
     pts = np.ascontiguousarray(pts3d)
     ntm = ctypes.c_int32(0)
-    n = L.oro_search_local_points(F.ref(), ctypes.byref(cam), pts.ctypes.data, len(pts), mvp.ctypes.data,
-                                  mvp_obs.ctypes.data, float(th), int(bFar), float(thFar), float(nnratio),
-                                  ctypes.byref(ntm))
+    n = L.oro_search_local_points_rig(F.ref(), ctypes.byref(cam), ctypes.byref(rig) if rig is not None else None,
+                                      pts.ctypes.data, len(pts), mvp.ctypes.data, mvp_obs.ctypes.data, float(th),
+                                      int(bFar), float(thFar), float(nnratio), ctypes.byref(ntm))
     return n, int(ntm.value)
 
 

@@ -22,6 +22,9 @@
 //   ORBmatcher::ComputeThreeMaxima           ORBmatcher.cc:2012-2053     -> three_maxima()
 //   Frame::ComputeStereoFishEyeMatches kNN   Frame.cc:1126-1151          -> oro_stereo_knn_ratio()
 //   Frame::isInFrustum (pinhole)             Frame.cc:512-570            -> oro_is_in_frustum()
+//   Frame::isInFrustum (any camera model, both branches), isInFrustumChecks
+//                                            Frame.cc:512-586, 1168-1242 -> oro_is_in_frustum_rig()
+//   KannalaBrandt8::project (float)          KannalaBrandt8.cpp:67-82    -> kb8_project()
 //   MapPoint::PredictScale                   MapPoint.cc:531-546
 //   Tracking::SearchLocalPoints (projection + SearchByProjection)  Tracking.cc:3404-3453
 //                                                                        -> oro_search_local_points()
@@ -48,6 +51,12 @@ int hamming(const uint8_t* a, const uint8_t* b);
 namespace {
 
 const int TH_HIGH = 100, TH_LOW = 50, HISTO_LENGTH = 30;
+
+// Eigen 3.3's 3-term sums in fixed-size expressions (a product's coefficient, norm(), dot()): the
+// non-vectorised redux halves the range, sum(a, b, c) = a + (b + c) (Eigen/src/Core/Redux.h
+// redux_novec_unroller; ProductEvaluators.h lazy coeff = (lhs.row(i).transpose().cwiseProduct(
+// rhs.col(j))).sum()). The reference's Eigen is focal's libeigen3-dev 3.3.7 (Dockerfile:19).
+static inline float eig_sum3(float a, float b, float c) { return a + (b + c); }
 
 struct Grid {
     const orbfe_frame* F;
@@ -641,9 +650,9 @@ int oro_fuse(const orbfe_frame* KF, const orbfe_kf_camera* cam, const float* inv
         const float ur = u - KF->mbf * invz;
         const float maxDistance = 1.2f * mp.max_dist, minDistance = 0.8f * mp.min_dist;
         const float PO[3] = {mp.pos[0] - cam->Ow[0], mp.pos[1] - cam->Ow[1], mp.pos[2] - cam->Ow[2]};
-        const float dist3D = std::sqrt((PO[0] * PO[0] + PO[1] * PO[1]) + PO[2] * PO[2]);
+        const float dist3D = std::sqrt(eig_sum3(PO[0] * PO[0], PO[1] * PO[1], PO[2] * PO[2]));
         if (dist3D < minDistance || dist3D > maxDistance) continue;
-        const float dotn = (PO[0] * mp.normal[0] + PO[1] * mp.normal[1]) + PO[2] * mp.normal[2];
+        const float dotn = eig_sum3(PO[0] * mp.normal[0], PO[1] * mp.normal[1], PO[2] * mp.normal[2]);
         if (dotn < 0.5 * dist3D) continue;
         const int nPredictedLevel = predict_scale(mp.max_dist, dist3D, cam->log_scale_factor, KF->nlevels);
         const float radius = th * KF->scale_factors[nPredictedLevel];
@@ -705,9 +714,9 @@ int oro_sbp_sim3(const orbfe_frame* KF, const orbfe_kf_camera* cam, const orbfe_
         if (!kf_in_image(KF, u, v)) continue;
         const float maxDistance = 1.2f * mp.max_dist, minDistance = 0.8f * mp.min_dist;
         const float PO[3] = {mp.pos[0] - cam->Ow[0], mp.pos[1] - cam->Ow[1], mp.pos[2] - cam->Ow[2]};
-        const float dist = std::sqrt((PO[0] * PO[0] + PO[1] * PO[1]) + PO[2] * PO[2]);
+        const float dist = std::sqrt(eig_sum3(PO[0] * PO[0], PO[1] * PO[1], PO[2] * PO[2]));
         if (dist < minDistance || dist > maxDistance) continue;
-        const float dotn = (PO[0] * mp.normal[0] + PO[1] * mp.normal[1]) + PO[2] * mp.normal[2];
+        const float dotn = eig_sum3(PO[0] * mp.normal[0], PO[1] * mp.normal[1], PO[2] * mp.normal[2]);
         if (dotn < 0.5 * dist) continue;
         const int nPredictedLevel = predict_scale(mp.max_dist, dist, cam->log_scale_factor, KF->nlevels);
         const float radius = th * KF->scale_factors[nPredictedLevel];
@@ -748,7 +757,7 @@ static void sim3_side(const orbfe_frame* B, const Grid& gridB, const orbfe_map_p
         const float u = cam1->fx * x + cam1->cx, v = cam1->fy * y + cam1->cy;
         if (!kf_in_image(B, u, v)) continue;
         const float maxDistance = 1.2f * mp.max_dist, minDistance = 0.8f * mp.min_dist;
-        const float dist3D = std::sqrt((pB[0] * pB[0] + pB[1] * pB[1]) + pB[2] * pB[2]);
+        const float dist3D = std::sqrt(eig_sum3(pB[0] * pB[0], pB[1] * pB[1], pB[2] * pB[2]));
         if (dist3D < minDistance || dist3D > maxDistance) continue;
         const int nPredictedLevel = predict_scale(mp.max_dist, dist3D, logsfB, B->nlevels);
         const float radius = th * B->scale_factors[nPredictedLevel];
@@ -811,53 +820,135 @@ int oro_stereo_knn_ratio(const uint8_t* L, int32_t nl, const uint8_t* R, int32_t
     return good;
 }
 
-// Frame::isInFrustum, pinhole branch (Frame.cc:512-570), with Eigen's evaluation order spelled
-// out: (R*P)(i) = (R(i,0)*P0 + R(i,1)*P1) + R(i,2)*P2, norm = sqrt((x*x + y*y) + z*z), dot left to
-// right; Pinhole::project = fx * x / z + cx (Pinhole.cpp:43-49). PredictScale with the C library
-// logf (log(float) resolves to it through OpenCV's <math.h>).
-static bool is_in_frustum(const orbfe_frame* F, const orbfe_camera* c, const orbfe_map_point_3d& p,
-                          orbfe_map_point& t) {
-    t.flags &= ~ORBFE_MP_IN_VIEW;
-    t.proj_x = -1;
-    t.proj_y = -1;
+
+struct CamModel {
+    int type;
+    float p[8];
+};
+
+// GeometricCamera::project(const Eigen::Vector3f&): Pinhole.cpp:43-49 (fx * x / z + cx) and
+// KannalaBrandt8.cpp:67-82 (atan2f / sqrtf explicit; cos(psi) / sin(psi) of a float resolve to
+// cosf / sinf, as for computeOrbDescriptor's rotation), float arithmetic in source order.
+static void cam_project(const CamModel& m, const float* Pc, float& u, float& v) {
+    if (m.type == ORBFE_CAM_KANNALA_BRANDT8) {
+        const float x2_plus_y2 = Pc[0] * Pc[0] + Pc[1] * Pc[1];
+        const float theta = atan2f(sqrtf(x2_plus_y2), Pc[2]);
+        const float psi = atan2f(Pc[1], Pc[0]);
+        const float theta2 = theta * theta;
+        const float theta3 = theta * theta2;
+        const float theta5 = theta3 * theta2;
+        const float theta7 = theta5 * theta2;
+        const float theta9 = theta7 * theta2;
+        const float r = theta + m.p[4] * theta3 + m.p[5] * theta5 + m.p[6] * theta7 + m.p[7] * theta9;
+        u = m.p[0] * r * cosf(psi) + m.p[2];
+        v = m.p[1] * r * sinf(psi) + m.p[3];
+        return;
+    }
+    u = m.p[0] * Pc[0] / Pc[2] + m.p[2];
+    v = m.p[1] * Pc[1] / Pc[2] + m.p[3];
+}
+
+// The checks of one view (isInFrustum's Nleft == -1 branch up to its writes, or isInFrustumChecks):
+// returns the stage reached: 0 behind the camera, 1 outside the image, 2 outside the distance /
+// viewing limits, 3 in view.
+struct View {
+    float u, v, depth, invz, view_cos;
+    int level;
+};
+static int frustum_view(const orbfe_frame* F, const orbfe_camera* c, const float* R, const float* t, const float* Ow,
+                        const CamModel& m, const orbfe_map_point_3d& p, View& o) {
     const float P0 = p.pos[0], P1 = p.pos[1], P2 = p.pos[2];
     float Pc[3];
-    for (int i = 0; i < 3; i++) {
-        const float* R = c->Rcw + 3 * i;
-        Pc[i] = ((R[0] * P0 + R[1] * P1) + R[2] * P2) + c->tcw[i];
-    }
-    const float Pc_dist = std::sqrt((Pc[0] * Pc[0] + Pc[1] * Pc[1]) + Pc[2] * Pc[2]);
-    const float PcZ = Pc[2];
-    const float invz = 1.0f / PcZ;
-    if (PcZ < 0.0f) return false;
-    const float u = c->fx * Pc[0] / Pc[2] + c->cx;
-    const float v = c->fy * Pc[1] / Pc[2] + c->cy;
-    if (u < F->min_x || u > F->max_x) return false;
-    if (v < F->min_y || v > F->max_y) return false;
-    t.proj_x = u;
-    t.proj_y = v;
-    const float maxDistance = 1.2f * p.max_dist, minDistance = 0.8f * p.min_dist;
-    const float PO0 = P0 - c->Ow[0], PO1 = P1 - c->Ow[1], PO2 = P2 - c->Ow[2];
-    const float dist = std::sqrt((PO0 * PO0 + PO1 * PO1) + PO2 * PO2);
-    if (dist < minDistance || dist > maxDistance) return false;
-    const float viewCos = ((PO0 * p.normal[0] + PO1 * p.normal[1]) + PO2 * p.normal[2]) / dist;
-    if (viewCos < c->view_cos_limit) return false;
+    for (int i = 0; i < 3; i++) Pc[i] = eig_sum3(R[3 * i] * P0, R[3 * i + 1] * P1, R[3 * i + 2] * P2) + t[i];
+    o.depth = std::sqrt(eig_sum3(Pc[0] * Pc[0], Pc[1] * Pc[1], Pc[2] * Pc[2]));
+    o.invz = 1.0f / Pc[2];
+    if (Pc[2] < 0.0f) return 0;
+    cam_project(m, Pc, o.u, o.v);
+    if (o.u < F->min_x || o.u > F->max_x) return 1;
+    if (o.v < F->min_y || o.v > F->max_y) return 1;
+    const float maxDistance = 1.2f * p.max_dist, minDistance = 0.8f * p.min_dist;   // Get{Max,Min}DistanceInvariance
+    const float PO0 = P0 - Ow[0], PO1 = P1 - Ow[1], PO2 = P2 - Ow[2];
+    const float dist = std::sqrt(eig_sum3(PO0 * PO0, PO1 * PO1, PO2 * PO2));
+    if (dist < minDistance || dist > maxDistance) return 2;
+    o.view_cos = eig_sum3(PO0 * p.normal[0], PO1 * p.normal[1], PO2 * p.normal[2]) / dist;
+    if (o.view_cos < c->view_cos_limit) return 2;
+    // MapPoint::PredictScale (MapPoint.cc:531-546): log(float) resolves to logf
     const float ratio = p.max_dist / dist;
     int nScale = (int)std::ceil(logf(ratio) / c->log_scale_factor);
     if (nScale < 0) nScale = 0;
     else if (nScale >= F->nlevels) nScale = F->nlevels - 1;
-    t.flags |= ORBFE_MP_IN_VIEW;
-    t.proj_x = u;
-    t.proj_xr = u - F->mbf * invz;
-    t.depth = Pc_dist;
-    t.proj_y = v;
-    t.scale_level = nScale;
-    t.view_cos = viewCos;
-    return true;
+    o.level = nScale;
+    return 3;
 }
 
-int oro_is_in_frustum(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* pts, int32_t n,
-                      orbfe_map_point* track) {
+// Frame::isInFrustum (Frame.cc:512-586). Nleft == -1: mTrackProjX / Y = -1, then the projection
+// once it is in the image, the rest when every check passes. Nleft != -1: both views through
+// isInFrustumChecks (Frame.cc:1168-1242), levels reset to -1, each view's fields written only when
+// it passes (failed-view fields: projections -1 here; the reference leaves the previous values).
+static bool is_in_frustum(const orbfe_frame* F, const orbfe_camera* c, const orbfe_stereo_rig* rig,
+                          const orbfe_map_point_3d& p, orbfe_map_point& t) {
+    CamModel L{ORBFE_CAM_PINHOLE, {c->fx, c->fy, c->cx, c->cy, 0.f, 0.f, 0.f, 0.f}};
+    if (rig) {
+        L.type = rig->left.type;
+        memcpy(L.p, rig->left.params, sizeof(L.p));
+    }
+    View o{};
+    if (!F->two_cams) {
+        t.flags &= ~ORBFE_MP_IN_VIEW;
+        t.proj_x = -1;
+        t.proj_y = -1;
+        const int st = frustum_view(F, c, c->Rcw, c->tcw, c->Ow, L, p, o);
+        if (st >= 2) {
+            t.proj_x = o.u;
+            t.proj_y = o.v;
+        }
+        if (st < 3) return false;
+        t.flags |= ORBFE_MP_IN_VIEW;
+        t.proj_xr = o.u - F->mbf * o.invz;
+        t.depth = o.depth;
+        t.scale_level = o.level;
+        t.view_cos = o.view_cos;
+        return true;
+    }
+    t.flags &= ~(ORBFE_MP_IN_VIEW | ORBFE_MP_IN_VIEW_R);
+    t.scale_level = -1;
+    t.scale_level_r = -1;
+    t.proj_x = t.proj_y = t.proj_xr = t.proj_yr = -1;
+    bool in = false;
+    if (frustum_view(F, c, c->Rcw, c->tcw, c->Ow, L, p, o) == 3) {
+        t.flags |= ORBFE_MP_IN_VIEW;
+        t.proj_x = o.u;
+        t.proj_y = o.v;
+        t.scale_level = o.level;
+        t.view_cos = o.view_cos;
+        t.depth = o.depth;
+        in = true;
+    }
+    // right view: mR = Rrl * mRcw, mt = Rrl * mtcw + trl, twc = mRwc * mTlr.translation() + mOw
+    float R2[9], t2[3], Ow2[3];
+    const float* A = rig->Rrl;
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++)
+            R2[3 * i + j] = eig_sum3(A[3 * i] * c->Rcw[j], A[3 * i + 1] * c->Rcw[3 + j], A[3 * i + 2] * c->Rcw[6 + j]);
+        t2[i] = eig_sum3(A[3 * i] * c->tcw[0], A[3 * i + 1] * c->tcw[1], A[3 * i + 2] * c->tcw[2]) + rig->trl[i];
+        Ow2[i] = eig_sum3(rig->Rwc[3 * i] * rig->tlr[0], rig->Rwc[3 * i + 1] * rig->tlr[1], rig->Rwc[3 * i + 2] * rig->tlr[2]) +
+                 c->Ow[i];
+    }
+    CamModel Rm{rig->right.type, {}};
+    memcpy(Rm.p, rig->right.params, sizeof(Rm.p));
+    if (frustum_view(F, c, R2, t2, Ow2, Rm, p, o) == 3) {
+        t.flags |= ORBFE_MP_IN_VIEW_R;
+        t.proj_xr = o.u;
+        t.proj_yr = o.v;
+        t.scale_level_r = o.level;
+        t.view_cos_r = o.view_cos;
+        in = true;
+    }
+    return in;
+}
+
+int oro_is_in_frustum_rig(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_stereo_rig* rig,
+                          const orbfe_map_point_3d* pts, int32_t n, orbfe_map_point* track) {
     int nToMatch = 0;
     for (int i = 0; i < n; i++) {
         const orbfe_map_point_3d& p = pts[i];
@@ -867,21 +958,35 @@ int oro_is_in_frustum(const orbfe_frame* F, const orbfe_camera* cam, const orbfe
         t.observations = p.observations;
         t.id = p.id;
         memcpy(t.desc, p.desc, 32);
+        if (F->two_cams) { t.scale_level = -1; t.scale_level_r = -1; t.proj_x = t.proj_y = t.proj_xr = t.proj_yr = -1; }
+        else { t.proj_x = t.proj_y = -1; t.scale_level_r = -1; }
         if (p.flags & ORBFE_MP_SKIP) continue;   // mnLastFrameSeen == current: mbTrackInView = false
         if (p.flags & ORBFE_MP_BAD) continue;
-        if (is_in_frustum(F, cam, p, t)) nToMatch++;
+        if (is_in_frustum(F, cam, rig, p, t)) nToMatch++;
     }
     return nToMatch;
+}
+
+int oro_is_in_frustum(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* pts, int32_t n,
+                      orbfe_map_point* track) {
+    return oro_is_in_frustum_rig(F, cam, nullptr, pts, n, track);
+}
+
+int oro_search_local_points_rig(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_stereo_rig* rig,
+                                const orbfe_map_point_3d* pts, int32_t n, int32_t* mvp, const int32_t* mvp_obs, float th,
+                                int32_t bFarPoints, float thFarPoints, float nnratio, int32_t* n_to_match) {
+    std::vector<orbfe_map_point> track(n > 0 ? n : 1);
+    const int nToMatch = oro_is_in_frustum_rig(F, cam, rig, pts, n, track.data());
+    if (n_to_match) *n_to_match = nToMatch;
+    if (nToMatch <= 0) return 0;
+    return oro_sbp_local(F, mvp, mvp_obs, track.data(), n, th, bFarPoints, thFarPoints, nnratio);
 }
 
 int oro_search_local_points(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* pts, int32_t n,
                             int32_t* mvp, const int32_t* mvp_obs, float th, int32_t bFarPoints, float thFarPoints,
                             float nnratio, int32_t* n_to_match) {
-    std::vector<orbfe_map_point> track(n > 0 ? n : 1);
-    const int nToMatch = oro_is_in_frustum(F, cam, pts, n, track.data());
-    if (n_to_match) *n_to_match = nToMatch;
-    if (nToMatch <= 0) return 0;
-    return oro_sbp_local(F, mvp, mvp_obs, track.data(), n, th, bFarPoints, thFarPoints, nnratio);
+    return oro_search_local_points_rig(F, cam, nullptr, pts, n, mvp, mvp_obs, th, bFarPoints, thFarPoints, nnratio,
+                                       n_to_match);
 }
 
 }  // extern "C"

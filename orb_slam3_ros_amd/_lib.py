@@ -89,6 +89,11 @@ _SIGS = {
     "orbfe_is_in_frustum": (_c_int, [_vp, _vp, _vp, _c_int, _vp]),
     "orbfe_search_local_points": (_c_int, [_vp, _vp, _vp, _c_int, _vp, _vp, _c_float, _c_int, _c_float, _c_float, _vp]),
     "orbfe_matcher_last_ms": (_c_float, []),
+    "orbfe_is_in_frustum_rig": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _vp]),
+    "orbfe_search_local_points_rig": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _vp, _vp, _c_float, _c_int, _c_float,
+                                               _c_float, _vp]),
+    "orbfe_search_local_points_rig_device": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _vp, _vp, _c_float, _c_int,
+                                                      _c_float, _c_float, _vp, _vp]),
 }
 
 _lib = None

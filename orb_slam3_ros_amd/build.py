@@ -10,7 +10,7 @@ LIB = os.path.join(_HERE, "liborbfe.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 SOURCES = ["orbfe_engine.hip"]
 DEPS = ["orbfe_engine.hip", "orbfe_kernels.hip", "orbfe_types.h", "glibc_sincosf.h", "stl_sort.h",
-        "brief_pattern.h", "orbfe_matcher.hip", "orbfe_bow.hip", "glibc_logf.h", "orbfe_remap.hip", "orbfe_backend.hip"]
+        "brief_pattern.h", "orbfe_matcher.hip", "orbfe_bow.hip", "glibc_logf.h", "glibc_atan2f.h", "orbfe_remap.hip", "orbfe_backend.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
          "-fno-fast-math", "-Wall", "-Wno-unused-function"]
 

@@ -195,14 +195,14 @@ __global__ __launch_bounds__(MT_NT) void k_kf_geom(KfGeom g, const orbfe_map_poi
         float dist;
         float PO[3] = {0.f, 0.f, 0.f};
         if (g.dist_cam) {
-            dist = sqrtf((pc[0] * pc[0] + pc[1] * pc[1]) + pc[2] * pc[2]);
+            dist = sqrtf(eig_sum3(pc[0] * pc[0], pc[1] * pc[1], pc[2] * pc[2]));
         } else {
             PO[0] = P[0] - g.Ow[0]; PO[1] = P[1] - g.Ow[1]; PO[2] = P[2] - g.Ow[2];
-            dist = sqrtf((PO[0] * PO[0] + PO[1] * PO[1]) + PO[2] * PO[2]);
+            dist = sqrtf(eig_sum3(PO[0] * PO[0], PO[1] * PO[1], PO[2] * PO[2]));
         }
         if (dist < minDistance || dist > maxDistance) break;
         if (g.view) {
-            const float dotn = (PO[0] * mp.normal[0] + PO[1] * mp.normal[1]) + PO[2] * mp.normal[2];
+            const float dotn = eig_sum3(PO[0] * mp.normal[0], PO[1] * mp.normal[1], PO[2] * mp.normal[2]);
             if ((double)dotn < 0.5 * (double)dist) break;
         }
         const float ratio = mp.max_dist / dist;

@@ -13,6 +13,7 @@
 // keypoint index inside a cell: the grid is rebuilt with a stable (cell, index) sort), so the
 // reference's strict-< "first best wins" and best/second-best bookkeeping are reproduced verbatim.
 #pragma once
+#include "glibc_atan2f.h"
 #include "glibc_logf.h"
 
 #define MT_NT 256
@@ -588,11 +589,82 @@ __global__ __launch_bounds__(MT_NT) void k_sbp_proj2(FrameDev fr, const orbfe_pr
 // for every local map point (Tracking.cc:3407-3425): one thread per point, float arithmetic in the
 // reference's (Eigen's) order, no contraction, glibc logf port. Writes the tracking snapshot the
 // SearchByProjection kernels read and counts nToMatch.
+struct CamModelDev {
+    int type;                 // ORBFE_CAM_*
+    float fx, fy, cx, cy, k[4];
+};
 struct CamDev {
-    float R[9], t[3], Ow[3], fx, fy, cx, cy, logsf, cos_limit;
+    float R[9], t[3], Ow[3], logsf, cos_limit;
     float minx, maxx, miny, maxy, mbf;
     int nlevels;
+    int two;                  // two-camera frame (Nleft != -1): isInFrustumChecks left + right
+    CamModelDev cl, cr;       // mpCamera, mpCamera2
+    float R2[9], t2[3], Ow2[3];   // right view: Rrl * Rcw, Rrl * tcw + trl, Rwc * tlr + Ow (host-derived)
 };
+// The 3-term sums of Eigen 3.3's fixed-size expressions (products' coefficients, norm, dot): the
+// non-vectorised redux halves the range, sum(a, b, c) = a + (b + c) (Eigen/src/Core/Redux.h,
+// redux_novec_unroller; ProductEvaluators.h lazy coeff = (lhs.row(i) .* rhs.col(j)).sum()).
+__host__ __device__ __forceinline__ float eig_sum3(float a, float b, float c) { return a + (b + c); }
+// GeometricCamera::project(Eigen::Vector3f): Pinhole.cpp:43-49, KannalaBrandt8.cpp:67-82 (float
+// arithmetic in the source's order; atan2f / cos / sin of float as glibc's atan2f / cosf / sinf).
+__device__ __forceinline__ float2 mt_cam_project(const CamModelDev& m, float x, float y, float z) {
+    if (m.type == ORBFE_CAM_KANNALA_BRANDT8) {
+        const float x2_plus_y2 = x * x + y * y;
+        const float theta = glibc_atan2f(sqrtf(x2_plus_y2), z);
+        const float psi = glibc_atan2f(y, x);
+        const float theta2 = theta * theta;
+        const float theta3 = theta * theta2;
+        const float theta5 = theta3 * theta2;
+        const float theta7 = theta5 * theta2;
+        const float theta9 = theta7 * theta2;
+        const float r = theta + m.k[0] * theta3 + m.k[1] * theta5 + m.k[2] * theta7 + m.k[3] * theta9;
+        return make_float2(m.fx * r * glibc_cosf(psi) + m.cx, m.fy * r * glibc_sinf(psi) + m.cy);
+    }
+    return make_float2(m.fx * x / z + m.cx, m.fy * y / z + m.cy);
+}
+// The checks shared by isInFrustum's Nleft == -1 branch (Frame.cc:512-570) and isInFrustumChecks
+// (Frame.cc:1168-1242) for one view: pose (R, t), camera centre Ow, camera model m. stage = how far
+// the point got: 0 behind the camera, 1 outside the image, 2 outside the distance / viewing limits,
+// 3 in view (uv, depth, viewCos, level, invz valid from stage 2 / 3 on).
+struct FrustumView {
+    int stage;
+    float u, v, depth, view_cos, invz;
+    int level;
+};
+__device__ __forceinline__ FrustumView mt_frustum_view(const CamDev& c, const float* R, const float* t, const float* Ow,
+                                                       const CamModelDev& m, const orbfe_map_point_3d& p) {
+    FrustumView o{0, 0.f, 0.f, 0.f, 0.f, 0.f, 0};
+    const float P0 = p.pos[0], P1 = p.pos[1], P2 = p.pos[2];
+    float Pc[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) Pc[k] = eig_sum3(R[3 * k] * P0, R[3 * k + 1] * P1, R[3 * k + 2] * P2) + t[k];
+    o.depth = sqrtf(eig_sum3(Pc[0] * Pc[0], Pc[1] * Pc[1], Pc[2] * Pc[2]));
+    o.invz = 1.0f / Pc[2];
+    if (Pc[2] < 0.0f) return o;
+    const float2 uv = mt_cam_project(m, Pc[0], Pc[1], Pc[2]);
+    o.u = uv.x;
+    o.v = uv.y;
+    if (uv.x < c.minx || uv.x > c.maxx || uv.y < c.miny || uv.y > c.maxy) {
+        o.stage = 1;
+        return o;
+    }
+    o.stage = 2;
+    const float maxDistance = 1.2f * p.max_dist, minDistance = 0.8f * p.min_dist;
+    const float PO0 = P0 - Ow[0], PO1 = P1 - Ow[1], PO2 = P2 - Ow[2];
+    const float dist = sqrtf(eig_sum3(PO0 * PO0, PO1 * PO1, PO2 * PO2));
+    if (dist < minDistance || dist > maxDistance) return o;
+    const float viewCos = eig_sum3(PO0 * p.normal[0], PO1 * p.normal[1], PO2 * p.normal[2]) / dist;
+    if (viewCos < c.cos_limit) return o;
+    // MapPoint::PredictScale (MapPoint.cc:531-546)
+    const float ratio = p.max_dist / dist;
+    int nScale = (int)ceilf(glibc_logf(ratio) / c.logsf);
+    if (nScale < 0) nScale = 0;
+    else if (nScale >= c.nlevels) nScale = c.nlevels - 1;
+    o.view_cos = viewCos;
+    o.level = nScale;
+    o.stage = 3;
+    return o;
+}
 __global__ __launch_bounds__(MT_NT) void k_frustum(CamDev c, const orbfe_map_point_3d* pts, int n,
                                                    orbfe_map_point* track, int* n_to_match) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -609,39 +681,45 @@ __global__ __launch_bounds__(MT_NT) void k_frustum(CamDev c, const orbfe_map_poi
     t.scale_level_r = -1;
     memcpy(t.desc, p.desc, 32);
     bool in = false;
-    if (!(p.flags & (ORBFE_MP_SKIP | ORBFE_MP_BAD))) {
-        const float P0 = p.pos[0], P1 = p.pos[1], P2 = p.pos[2];
-        float Pc[3];
-#pragma unroll
-        for (int k = 0; k < 3; k++) Pc[k] = ((c.R[3 * k] * P0 + c.R[3 * k + 1] * P1) + c.R[3 * k + 2] * P2) + c.t[k];
-        const float Pc_dist = sqrtf((Pc[0] * Pc[0] + Pc[1] * Pc[1]) + Pc[2] * Pc[2]);
-        const float PcZ = Pc[2];
-        const float invz = 1.0f / PcZ;
-        if (!(PcZ < 0.0f)) {
-            const float u = c.fx * Pc[0] / Pc[2] + c.cx;
-            const float v = c.fy * Pc[1] / Pc[2] + c.cy;
-            if (!(u < c.minx || u > c.maxx) && !(v < c.miny || v > c.maxy)) {
-                t.proj_x = u;
-                t.proj_y = v;
-                const float maxDistance = 1.2f * p.max_dist, minDistance = 0.8f * p.min_dist;
-                const float PO0 = P0 - c.Ow[0], PO1 = P1 - c.Ow[1], PO2 = P2 - c.Ow[2];
-                const float dist = sqrtf((PO0 * PO0 + PO1 * PO1) + PO2 * PO2);
-                if (!(dist < minDistance || dist > maxDistance)) {
-                    const float viewCos = ((PO0 * p.normal[0] + PO1 * p.normal[1]) + PO2 * p.normal[2]) / dist;
-                    if (!(viewCos < c.cos_limit)) {
-                        const float ratio = p.max_dist / dist;
-                        int nScale = (int)ceilf(glibc_logf(ratio) / c.logsf);
-                        if (nScale < 0) nScale = 0;
-                        else if (nScale >= c.nlevels) nScale = c.nlevels - 1;
-                        t.flags |= ORBFE_MP_IN_VIEW;
-                        t.proj_xr = u - c.mbf * invz;
-                        t.depth = Pc_dist;
-                        t.scale_level = nScale;
-                        t.view_cos = viewCos;
-                        in = true;
-                    }
-                }
+    if (c.two) {
+        // Nleft != -1 (Frame.cc:575-586): both views checked, levels reset to -1, a view's fields
+        // written only when it passes (Frame.cc:1225-1239)
+        t.scale_level = -1;
+        t.proj_xr = -1.f;
+        t.proj_yr = -1.f;
+        if (!(p.flags & (ORBFE_MP_SKIP | ORBFE_MP_BAD))) {
+            const FrustumView L = mt_frustum_view(c, c.R, c.t, c.Ow, c.cl, p);
+            if (L.stage == 3) {
+                t.flags |= ORBFE_MP_IN_VIEW;
+                t.proj_x = L.u;
+                t.proj_y = L.v;
+                t.scale_level = L.level;
+                t.view_cos = L.view_cos;
+                t.depth = L.depth;
             }
+            const FrustumView Rv = mt_frustum_view(c, c.R2, c.t2, c.Ow2, c.cr, p);
+            if (Rv.stage == 3) {
+                t.flags |= ORBFE_MP_IN_VIEW_R;
+                t.proj_xr = Rv.u;
+                t.proj_yr = Rv.v;
+                t.scale_level_r = Rv.level;
+                t.view_cos_r = Rv.view_cos;
+            }
+            in = L.stage == 3 || Rv.stage == 3;
+        }
+    } else if (!(p.flags & (ORBFE_MP_SKIP | ORBFE_MP_BAD))) {
+        const FrustumView L = mt_frustum_view(c, c.R, c.t, c.Ow, c.cl, p);
+        if (L.stage >= 2) {   // mTrackProjX / Y are written once the projection is in the image
+            t.proj_x = L.u;
+            t.proj_y = L.v;
+        }
+        if (L.stage == 3) {
+            t.flags |= ORBFE_MP_IN_VIEW;
+            t.proj_xr = L.u - c.mbf * L.invz;
+            t.depth = L.depth;
+            t.scale_level = L.level;
+            t.view_cos = L.view_cos;
+            in = true;
         }
     }
     track[i] = t;
@@ -1220,7 +1298,49 @@ struct FrustumIn {
     const orbfe_camera* cam;
     const orbfe_map_point_3d* pts;
     int32_t* n_to_match;
+    const orbfe_stereo_rig* rig;   // camera models / right view (NULL: pinhole from cam, one camera)
 };
+
+// isInFrustum's per-frame constants (Frame.cc:512-586, 1168-1242): pose, bounds, camera models and,
+// for a two-camera frame, the right view's pose in the reference's Eigen order. false = bad input.
+bool make_camdev(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_stereo_rig* rig, CamDev& cd) {
+    if (!F || !cam || (F->two_cams && !rig)) return false;
+    memset(&cd, 0, sizeof(cd));
+    memcpy(cd.R, cam->Rcw, sizeof(cd.R));
+    memcpy(cd.t, cam->tcw, sizeof(cd.t));
+    memcpy(cd.Ow, cam->Ow, sizeof(cd.Ow));
+    cd.logsf = cam->log_scale_factor;
+    cd.cos_limit = cam->view_cos_limit;
+    cd.minx = F->min_x; cd.maxx = F->max_x; cd.miny = F->min_y; cd.maxy = F->max_y;
+    cd.mbf = F->mbf;
+    cd.nlevels = F->nlevels;
+    auto model = [](const orbfe_camera_model& m, CamModelDev& o) {
+        if (m.type != ORBFE_CAM_PINHOLE && m.type != ORBFE_CAM_KANNALA_BRANDT8) return false;
+        o.type = m.type;
+        o.fx = m.params[0]; o.fy = m.params[1]; o.cx = m.params[2]; o.cy = m.params[3];
+        for (int k = 0; k < 4; k++) o.k[k] = m.type == ORBFE_CAM_KANNALA_BRANDT8 ? m.params[4 + k] : 0.f;
+        return true;
+    };
+    if (rig) {
+        if (!model(rig->left, cd.cl)) return false;
+    } else {
+        cd.cl.type = ORBFE_CAM_PINHOLE;
+        cd.cl.fx = cam->fx; cd.cl.fy = cam->fy; cd.cl.cx = cam->cx; cd.cl.cy = cam->cy;
+    }
+    cd.two = F->two_cams ? 1 : 0;
+    if (cd.two) {
+        if (!model(rig->right, cd.cr)) return false;
+        const float* A = rig->Rrl;
+        for (int i = 0; i < 3; i++) {
+            for (int j = 0; j < 3; j++)   // mR = Rrl * mRcw
+                cd.R2[3 * i + j] = eig_sum3(A[3 * i] * cam->Rcw[j], A[3 * i + 1] * cam->Rcw[3 + j], A[3 * i + 2] * cam->Rcw[6 + j]);
+            cd.t2[i] = eig_sum3(A[3 * i] * cam->tcw[0], A[3 * i + 1] * cam->tcw[1], A[3 * i + 2] * cam->tcw[2]) + rig->trl[i];
+            cd.Ow2[i] = eig_sum3(rig->Rwc[3 * i] * rig->tlr[0], rig->Rwc[3 * i + 1] * rig->tlr[1],
+                                 rig->Rwc[3 * i + 2] * rig->tlr[2]) + cam->Ow[i];
+        }
+    }
+    return true;
+}
 
 // Device-resident call (the *_device entry points): F's arrays, mvp, mvp_obs and the query
 // records are device pointers produced on `caller`; the matcher's stream waits for it, results
@@ -1268,9 +1388,9 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     if (fin && (!fin->cam || (nq > 0 && !fin->pts) || mode != 0)) return ORBFE_E_ARG;
     if (mode != 2 && !mvp_obs) return ORBFE_E_ARG;
     const bool two = F->two_cams != 0;
-    // two-camera frames: the local-map search takes the snapshot's right-view fields (no device
-    // isInFrustum for the fisheye model), the last-frame search needs the right projections
-    if (two && (fin || (mode == 1 && nq > 0 && !right_uv))) return ORBFE_E_ARG;
+    // two-camera frames: a device projection needs the rig (camera models, right view); the
+    // last-frame search needs the right projections
+    if (two && ((fin && !fin->rig) || (mode == 1 && nq > 0 && !right_uv))) return ORBFE_E_ARG;
     if (two && !dev && !links_ok(F)) return ORBFE_E_ARG;
     // slot writes per query, in the reference's order (entry index = W q + b)
     const int W = !two ? 1 : mode == 0 ? 4 : mode == 1 ? 2 : 1;
@@ -1348,17 +1468,8 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     const float2* ruv = (two && mode == 1) ? (dev ? (const float2*)right_uv : ms_ptr<const float2>(o_ruv)) : nullptr;
     const uint8_t* q = dev ? (const uint8_t*)(fin ? (const void*)fin->pts : queries) : ms_ptr<const uint8_t>(o_q);
     if (fin) {   // Tracking::SearchLocalPoints: project, count nToMatch, match only if > 0
-        const orbfe_camera& c = *fin->cam;
         CamDev cd;
-        memcpy(cd.R, c.Rcw, sizeof(cd.R));
-        memcpy(cd.t, c.tcw, sizeof(cd.t));
-        memcpy(cd.Ow, c.Ow, sizeof(cd.Ow));
-        cd.fx = c.fx; cd.fy = c.fy; cd.cx = c.cx; cd.cy = c.cy;
-        cd.logsf = c.log_scale_factor;
-        cd.cos_limit = c.view_cos_limit;
-        cd.minx = F->min_x; cd.maxx = F->max_x; cd.miny = F->min_y; cd.maxy = F->max_y;
-        cd.mbf = F->mbf;
-        cd.nlevels = F->nlevels;
+        if (!make_camdev(F, fin->cam, fin->rig, cd)) return ORBFE_E_ARG;
         int* ntm = ms_ptr<int>(o_ntm);
         HIPCHK(hipMemsetAsync(ntm, 0, 4, s));
         hipLaunchKernelGGL(k_frustum, dim3((nq + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, cd,
@@ -1690,7 +1801,7 @@ int orbfe_stereo_knn_batch(orbfe_extractor* left, int lbase, int lstep, orbfe_ex
 int orbfe_search_local_points(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* pts,
                               int32_t n, int32_t* mvp, const int32_t* mvp_obs, float th, int32_t bFarPoints,
                               float thFarPoints, float nnratio, int32_t* n_to_match) {
-    const FrustumIn fin{cam, pts, n_to_match};
+    const FrustumIn fin{cam, pts, n_to_match, nullptr};
     return sbp_run(0, F, mvp, mvp_obs, nullptr, n, sizeof(orbfe_map_point), offsetof(orbfe_map_point, observations),
                    offsetof(orbfe_map_point, id), 0, offsetof(orbfe_map_point, scale_level), th, bFarPoints, 0,
                    thFarPoints, nnratio, 0, 0, &fin);
@@ -1709,7 +1820,29 @@ int orbfe_search_local_points_device(const orbfe_frame* F, const orbfe_camera* c
                                      int32_t n, int32_t* d_mvp, const int32_t* d_mvp_obs, float th,
                                      int32_t bFarPoints, float thFarPoints, float nnratio, int32_t* n_to_match,
                                      void* stream) {
-    const FrustumIn fin{cam, d_pts, n_to_match};
+    const FrustumIn fin{cam, d_pts, n_to_match, nullptr};
+    const DevIn dv{(hipStream_t)stream};
+    return sbp_run(0, F, d_mvp, d_mvp_obs, nullptr, n, sizeof(orbfe_map_point), offsetof(orbfe_map_point, observations),
+                   offsetof(orbfe_map_point, id), 0, offsetof(orbfe_map_point, scale_level), th, bFarPoints, 0,
+                   thFarPoints, nnratio, 0, 0, &fin, &dv);
+}
+
+int orbfe_search_local_points_rig(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_stereo_rig* rig,
+                                  const orbfe_map_point_3d* pts, int32_t n, int32_t* mvp, const int32_t* mvp_obs,
+                                  float th, int32_t bFarPoints, float thFarPoints, float nnratio, int32_t* n_to_match) {
+    if (!rig) return ORBFE_E_ARG;
+    const FrustumIn fin{cam, pts, n_to_match, rig};
+    return sbp_run(0, F, mvp, mvp_obs, nullptr, n, sizeof(orbfe_map_point), offsetof(orbfe_map_point, observations),
+                   offsetof(orbfe_map_point, id), 0, offsetof(orbfe_map_point, scale_level), th, bFarPoints, 0,
+                   thFarPoints, nnratio, 0, 0, &fin);
+}
+
+int orbfe_search_local_points_rig_device(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_stereo_rig* rig,
+                                         const orbfe_map_point_3d* d_pts, int32_t n, int32_t* d_mvp,
+                                         const int32_t* d_mvp_obs, float th, int32_t bFarPoints, float thFarPoints,
+                                         float nnratio, int32_t* n_to_match, void* stream) {
+    if (!rig) return ORBFE_E_ARG;
+    const FrustumIn fin{cam, d_pts, n_to_match, rig};
     const DevIn dv{(hipStream_t)stream};
     return sbp_run(0, F, d_mvp, d_mvp_obs, nullptr, n, sizeof(orbfe_map_point), offsetof(orbfe_map_point, observations),
                    offsetof(orbfe_map_point, id), 0, offsetof(orbfe_map_point, scale_level), th, bFarPoints, 0,
@@ -1718,6 +1851,12 @@ int orbfe_search_local_points_device(const orbfe_frame* F, const orbfe_camera* c
 
 int orbfe_is_in_frustum(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* pts, int32_t n,
                         orbfe_map_point* track) {
+    if (F && F->two_cams) return ORBFE_E_ARG;   // the pinhole API has no right camera
+    return orbfe_is_in_frustum_rig(F, cam, nullptr, pts, n, track);
+}
+
+int orbfe_is_in_frustum_rig(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_stereo_rig* rig,
+                            const orbfe_map_point_3d* pts, int32_t n, orbfe_map_point* track) {
     if (!F || !cam || n < 0 || (n > 0 && (!pts || !track)) || F->nlevels <= 0) return ORBFE_E_ARG;
     if (n == 0) return 0;
     Plan p;
@@ -1729,15 +1868,7 @@ int orbfe_is_in_frustum(const orbfe_frame* F, const orbfe_camera* cam, const orb
     MsTimer timer;
     hipStream_t s = t_ms.stream;
     CamDev cd;
-    memcpy(cd.R, cam->Rcw, sizeof(cd.R));
-    memcpy(cd.t, cam->tcw, sizeof(cd.t));
-    memcpy(cd.Ow, cam->Ow, sizeof(cd.Ow));
-    cd.fx = cam->fx; cd.fy = cam->fy; cd.cx = cam->cx; cd.cy = cam->cy;
-    cd.logsf = cam->log_scale_factor;
-    cd.cos_limit = cam->view_cos_limit;
-    cd.minx = F->min_x; cd.maxx = F->max_x; cd.miny = F->min_y; cd.maxy = F->max_y;
-    cd.mbf = F->mbf;
-    cd.nlevels = F->nlevels;
+    if (!make_camdev(F, cam, rig, cd)) return ORBFE_E_ARG;
     int* ntm = ms_ptr<int>(o_ntm);
     HIPCHK(hipMemsetAsync(ntm, 0, 4, s));
     hipLaunchKernelGGL(k_frustum, dim3((n + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, cd,

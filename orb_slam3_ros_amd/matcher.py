@@ -147,6 +147,44 @@ class Pose(ctypes.Structure):
         return float(sum(float(v) ** 2 for v in self.q)) if self.kind == SIM3 else 1.0
 
 
+class CameraModel(ctypes.Structure):
+    """struct orbfe_camera_model: GeometricCamera type + mvParameters (fx fy cx cy [k0 k1 k2 k3])."""
+    _fields_ = [("type", ctypes.c_int32), ("params", ctypes.c_float * 8)]
+
+    PINHOLE, KANNALA_BRANDT8 = 0, 1
+
+    @staticmethod
+    def make(kind, fx, fy, cx, cy, k=(0.0, 0.0, 0.0, 0.0)):
+        m = CameraModel()
+        m.type = CameraModel.KANNALA_BRANDT8 if kind in ("kb8", CameraModel.KANNALA_BRANDT8) else CameraModel.PINHOLE
+        m.params[:] = [float(np.float32(v)) for v in (fx, fy, cx, cy, *k)]
+        return m
+
+
+class StereoRig(ctypes.Structure):
+    """struct orbfe_stereo_rig: Frame::mpCamera / mpCamera2, mTrl (rotation row-major, translation),
+    mTlr.translation() and mRwc (row-major), as Frame::isInFrustumChecks reads them (Frame.cc:1168-1242)."""
+    _fields_ = [("left", CameraModel), ("right", CameraModel), ("Rrl", ctypes.c_float * 9), ("trl", ctypes.c_float * 3),
+                ("tlr", ctypes.c_float * 3), ("Rwc", ctypes.c_float * 9)]
+
+    @staticmethod
+    def make(left: CameraModel, right: CameraModel = None, Tlr=None, Rcw=None):
+        """Tlr: 4x4 right-to-left transform (Stereo.T_c1_c2); Rcw: the frame rotation (mRwc = Rcw^T)."""
+        r = StereoRig()
+        r.left = left
+        r.right = right if right is not None else left
+        T = np.eye(4, dtype=np.float64) if Tlr is None else np.asarray(Tlr, np.float64)
+        Rlr, tlr = T[:3, :3], T[:3, 3]
+        Rrl = Rlr.T
+        trl = -(Rrl @ tlr)
+        r.Rrl[:] = [float(v) for v in np.asarray(Rrl, np.float32).reshape(-1)]
+        r.trl[:] = [float(v) for v in np.asarray(trl, np.float32)]
+        r.tlr[:] = [float(v) for v in np.asarray(tlr, np.float32)]
+        R = np.eye(3, dtype=np.float32) if Rcw is None else np.asarray(Rcw, np.float32).reshape(3, 3)
+        r.Rwc[:] = [float(v) for v in R.T.reshape(-1)]
+        return r
+
+
 class KFCamera(ctypes.Structure):
     """struct orbfe_kf_camera: the keyframe pose (Sophus), camera centre, pinhole intrinsics and
     mfLogScaleFactor read by the back-end projections."""
@@ -485,7 +523,7 @@ def search_by_projection_local_device(F: DeviceMatchFrame, mvp, mvp_obs, mps, th
 
 
 def search_local_points_device(F: DeviceMatchFrame, cam: Camera, points3d, mvp, mvp_obs, th=1.0, bFarPoints=False,
-                               thFarPoints=50.0, nnratio=0.8):
+                               thFarPoints=50.0, nnratio=0.8, rig: StereoRig = None):
     """Tracking::SearchLocalPoints on device-resident data (points3d: CUDA uint8 tensor of
     MAP_POINT_3D_DTYPE records). Returns (nmatches, nToMatch)."""
     import torch
@@ -495,9 +533,13 @@ def search_local_points_device(F: DeviceMatchFrame, cam: Camera, points3d, mvp, 
     _dev_i32(mvp_obs, F.N, "mvp_obs")
     ntm = ctypes.c_int32(0)
     st = torch.cuda.current_stream(mvp.device).cuda_stream
-    nm = _lib.check(lib.orbfe_search_local_points_device(
-        F.ref(), ctypes.byref(cam), points3d.data_ptr(), n, mvp.data_ptr(), mvp_obs.data_ptr(), float(th),
-        int(bFarPoints), float(thFarPoints), float(nnratio), ctypes.byref(ntm), st), "search_local_points_device")
+    args = (points3d.data_ptr(), n, mvp.data_ptr(), mvp_obs.data_ptr(), float(th), int(bFarPoints), float(thFarPoints),
+            float(nnratio), ctypes.byref(ntm), st)
+    if rig is None:
+        nm = lib.orbfe_search_local_points_device(F.ref(), ctypes.byref(cam), *args)
+    else:
+        nm = lib.orbfe_search_local_points_rig_device(F.ref(), ctypes.byref(cam), ctypes.byref(rig), *args)
+    nm = _lib.check(nm, "search_local_points_device")
     return nm, int(ntm.value)
 
 
@@ -525,31 +567,38 @@ def compute_distinctive_descriptors(descriptor_sets):
     return best
 
 
-def is_in_frustum(F: MatchFrame, cam: Camera, points3d):
+def is_in_frustum(F: MatchFrame, cam: Camera, points3d, rig: StereoRig = None):
     """Frame::isInFrustum + MapPoint::PredictScale over points3d (MAP_POINT_3D_DTYPE) on the GPU.
+    rig (StereoRig): the frame's camera models (KannalaBrandt8 included) and, for a two-camera frame,
+    the right view (isInFrustumChecks, Frame.cc:1168-1242); None = pinhole from cam.
     Returns (nToMatch, tracking snapshots as MAP_POINT_DTYPE records)."""
     lib = _lib.load()
     pts = _records(points3d, MAP_POINT_3D_DTYPE, "points3d")
     track = np.zeros(len(pts), MAP_POINT_DTYPE)
-    n = _lib.check(lib.orbfe_is_in_frustum(F.ref(), ctypes.byref(cam), pts.ctypes.data, len(pts), track.ctypes.data),
-                   "is_in_frustum")
-    return n, track
+    if rig is None:
+        n = lib.orbfe_is_in_frustum(F.ref(), ctypes.byref(cam), pts.ctypes.data, len(pts), track.ctypes.data)
+    else:
+        n = lib.orbfe_is_in_frustum_rig(F.ref(), ctypes.byref(cam), ctypes.byref(rig), pts.ctypes.data, len(pts),
+                                        track.ctypes.data)
+    return _lib.check(n, "is_in_frustum"), track
 
 
 def search_local_points(F: MatchFrame, cam: Camera, points3d, mvp, mvp_obs, th: float = 1.0, bFarPoints: bool = False,
-                        thFarPoints: float = 50.0, nnratio: float = 0.8):
+                        thFarPoints: float = 50.0, nnratio: float = 0.8, rig: StereoRig = None):
     """Tracking::SearchLocalPoints' projection + SearchByProjection (Tracking.cc:3404-3453) in one
-    device pass. mvp is updated in place. Returns (nmatches, nToMatch)."""
+    device pass (rig: see is_in_frustum). mvp is updated in place. Returns (nmatches, nToMatch)."""
     lib = _lib.load()
     pts = _records(points3d, MAP_POINT_3D_DTYPE, "points3d")
     mvp = _i32(mvp, F.N, "mvp")
     mvp_obs = _i32(mvp_obs, F.N, "mvp_obs")
     ntm = ctypes.c_int32(0)
-    n = _lib.check(lib.orbfe_search_local_points(F.ref(), ctypes.byref(cam), pts.ctypes.data, len(pts),
-                                                 mvp.ctypes.data, mvp_obs.ctypes.data, float(th), int(bFarPoints),
-                                                 float(thFarPoints), float(nnratio), ctypes.byref(ntm)),
-                   "search_local_points")
-    return n, int(ntm.value)
+    args = (pts.ctypes.data, len(pts), mvp.ctypes.data, mvp_obs.ctypes.data, float(th), int(bFarPoints),
+            float(thFarPoints), float(nnratio), ctypes.byref(ntm))
+    if rig is None:
+        n = lib.orbfe_search_local_points(F.ref(), ctypes.byref(cam), *args)
+    else:
+        n = lib.orbfe_search_local_points_rig(F.ref(), ctypes.byref(cam), ctypes.byref(rig), *args)
+    return _lib.check(n, "search_local_points"), int(ntm.value)
 
 
 def stereo_knn_ratio(left_desc, right_desc, ratio: float = 0.7):

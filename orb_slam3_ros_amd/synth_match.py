@@ -495,3 +495,94 @@ def synth_proj_points_two(rng, F: MatchFrame, n: int, copy_frac: float = 0.8, fl
         p["angle"][cp] = np.mod(np.where(outl, rng.uniform(0, 360, len(cp)),
                                          F.keys["angle"][src] + rot + rng.normal(0, 4, len(cp))), 360.0)
     return p, ruv
+
+
+# ---- fisheye (KannalaBrandt8) frames: BASELINE config 4's TUM-VI rig (config/Stereo-Inertial/TUM-VI.yaml) ----
+TUMVI_LEFT = (190.97847715128717, 190.9733070521226, 254.93170605935475, 256.8974428996504,
+              (0.0034823894022493434, 0.0007150348452162257, -0.0020532361418706202, 0.00020293673591811182))
+TUMVI_RIGHT = (190.44236969414825, 190.4344384721956, 252.59949716835982, 254.91723064636983,
+               (0.0034003170790442797, 0.001766278153469831, -0.00266312569781606, 0.0003299517423931039))
+TUMVI_TLR = np.array([[0.999999445773493, 0.000791687752817, 0.000694034010224, 0.101063427414194],
+                      [-0.000823363992158, 0.998899461915674, 0.046895490788700, 0.001946204678584],
+                      [-0.000656143613644, -0.046896036240590, 0.998899560146304, 0.001015350132563],
+                      [0.0, 0.0, 0.0, 1.0]])
+
+
+def kb8_unproject(u, v, fx, fy, cx, cy, k):
+    """Unit rays of pixels under the KannalaBrandt8 model (float64 Newton on theta; the generator
+    only needs rays that land near the pixels, the parity tests project them back with the model)."""
+    px, py = (np.asarray(u, np.float64) - cx) / fx, (np.asarray(v, np.float64) - cy) / fy
+    rd = np.minimum(np.hypot(px, py), np.pi / 2)
+    th = rd.copy()
+    for _ in range(30):
+        t2 = th * th
+        f = th * (1 + k[0] * t2 + k[1] * t2 ** 2 + k[2] * t2 ** 3 + k[3] * t2 ** 4) - rd
+        df = 1 + 3 * k[0] * t2 + 5 * k[1] * t2 ** 2 + 7 * k[2] * t2 ** 3 + 9 * k[3] * t2 ** 4
+        th = th - f / df
+    psi = np.arctan2(py, px)
+    return np.stack([np.sin(th) * np.cos(psi), np.sin(th) * np.sin(psi), np.cos(th)], 1)
+
+
+def synth_rig(cam: Camera, two: bool = True):
+    """The TUM-VI KannalaBrandt8 pair as a StereoRig (mpCamera, mpCamera2, mTrl / mTlr, mRwc)."""
+    from .matcher import CameraModel, StereoRig
+    left = CameraModel.make("kb8", *TUMVI_LEFT[:4], TUMVI_LEFT[4])
+    right = CameraModel.make("kb8", *TUMVI_RIGHT[:4], TUMVI_RIGHT[4]) if two else None
+    return StereoRig.make(left, right, TUMVI_TLR, np.array(cam.Rcw[:], np.float32).reshape(3, 3))
+
+
+def synth_local_map_3d_rig(rng, F: MatchFrame, cam: Camera, n: int, two: bool = True, copy_frac: float = 0.5,
+                           flip_p: float = 0.05, nlevels: int = 8, scale_factor: float = 1.2) -> np.ndarray:
+    """synth_local_map_3d for a fisheye frame: points along the KannalaBrandt8 rays of pixels near
+    frame keypoints (left ones, and with two cameras right ones through Tlr) or anywhere around
+    the image, at 0.3-30 m; the same share of behind-camera / out-of-range / grazing / bad / seen
+    points."""
+    R = np.array(cam.Rcw[:], np.float64).reshape(3, 3)
+    t = np.array(cam.tcw[:], np.float64)
+    w, h = F.bounds[1], F.bounds[3]
+    u = rng.uniform(-40, w + 40, n)
+    v = rng.uniform(-40, h + 40, n)
+    lvl = rng.choice(nlevels, n, p=level_weights(nlevels))
+    desc = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    side = np.zeros(n, bool)
+    if F.N:
+        cp = np.nonzero(rng.random(n) < copy_frac)[0]
+        src = rng.integers(0, F.N, len(cp))
+        u[cp] = F.keys["x"][src] + rng.normal(0, 1.0, len(cp))
+        v[cp] = F.keys["y"][src] + rng.normal(0, 1.0, len(cp))
+        lvl[cp] = F.keys["octave"][src]
+        desc[cp] = flip_bits(rng, F.desc[src], flip_p)
+        if two and F.nleft is not None:
+            side[cp] = src >= F.nleft
+    s = rng.uniform(0.3, 30.0, n)
+    s[rng.random(n) < 0.02] *= -1.0
+    rays = kb8_unproject(u, v, *TUMVI_LEFT[:4], TUMVI_LEFT[4])
+    Pc = rays * s[:, None]
+    if two and side.any():
+        rr = kb8_unproject(u[side], v[side], *TUMVI_RIGHT[:4], TUMVI_RIGHT[4]) * s[side][:, None]
+        Pc[side] = rr @ TUMVI_TLR[:3, :3].T + TUMVI_TLR[:3, 3]      # right camera -> left camera
+    P = (Pc - t) @ R
+    dist = np.linalg.norm(P - np.array(cam.Ow[:], np.float64), axis=1)
+    max_d = dist * scale_factor ** (lvl - rng.uniform(0.1, 0.9, n))
+    out = rng.random(n) < 0.08
+    max_d[out] *= rng.choice([0.5, 2.5], int(out.sum()))
+    min_d = max_d / scale_factor ** (nlevels - 1)
+    view = P - np.array(cam.Ow[:], np.float64)
+    view /= np.maximum(np.linalg.norm(view, axis=1, keepdims=True), 1e-9)
+    nrm = view + rng.normal(0, 0.3, (n, 3))
+    graze = rng.random(n) < 0.05
+    nrm[graze] = -nrm[graze]
+    nrm /= np.maximum(np.linalg.norm(nrm, axis=1, keepdims=True), 1e-9)
+    m = np.zeros(n, MAP_POINT_3D_DTYPE)
+    m["pos"] = P.astype(np.float32)
+    m["normal"] = nrm.astype(np.float32)
+    m["min_dist"] = min_d.astype(np.float32)
+    m["max_dist"] = max_d.astype(np.float32)
+    fl = np.zeros(n, np.int32)
+    fl[rng.random(n) < 0.03] |= MP_BAD
+    fl[rng.random(n) < 0.03] |= MP_SKIP
+    m["flags"] = fl
+    m["observations"] = np.where(rng.random(n) < 0.1, 0, rng.integers(1, 20, n))
+    m["id"] = np.arange(n) + 30000
+    m["desc"] = desc
+    return m

@@ -423,3 +423,81 @@ def test_two_cams_rejected_where_unsupported(gpu):
         ORBmatcher(0.9).SearchByProjectionLastFrame(F, mvp, obs, pts, 7, False, False)
     with pytest.raises(OrbfeError):
         ORBmatcher(0.9).SearchForInitialization(F, F, np.zeros((F.N, 2), np.float32), np.zeros(F.N, np.int32))
+
+
+# ---- Frame::isInFrustum with KannalaBrandt8 cameras (SURVEY §8f.1 for config 4's TUM-VI rig) ----
+def _rig_case(seed, two, n_pts, nl=1000, nr=950):
+    rng = np.random.default_rng(seed)
+    F = sm.synth_frame_two(rng, nl, nr) if two else sm.synth_frame(rng, nl, 512, 512, stereo=False)
+    cam = sm.synth_camera(rng, rot_deg=20.0)
+    rig = sm.synth_rig(cam, two)
+    pts = sm.synth_local_map_3d_rig(rng, F, cam, n_pts, two=two)
+    return rng, F, cam, rig, pts
+
+
+@pytest.mark.parametrize("two", [False, True], ids=["mono_kb8", "two_cams"])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_is_in_frustum_rig(gpu, om, seed, two):
+    """isInFrustum (Nleft == -1 with a KannalaBrandt8 mpCamera, or isInFrustumChecks left + right,
+    Frame.cc:512-586, 1168-1242) on the device: flags and every field of each passing view bit-exact."""
+    from orb_slam3_ros_amd.matcher import is_in_frustum
+    _, F, cam, rig, pts = _rig_case(seed, two, 50_000)
+    ng, tg = is_in_frustum(F, cam, pts, rig)
+    no, to = om.is_in_frustum(F, cam, pts, rig)
+    assert ng == no and no > 1000
+    np.testing.assert_array_equal(tg["flags"], to["flags"])
+    inv = (to["flags"] & sm.MP_IN_VIEW) != 0
+    for f in ("proj_x", "proj_y", "depth", "view_cos") + (() if two else ("proj_xr",)):
+        np.testing.assert_array_equal(tg[f][inv].view(np.uint32), to[f][inv].view(np.uint32), err_msg=f)
+    np.testing.assert_array_equal(tg["scale_level"], to["scale_level"])
+    if two:
+        invr = (to["flags"] & sm.MP_IN_VIEW_R) != 0
+        assert invr.sum() > 1000
+        for f in ("proj_xr", "proj_yr", "view_cos_r"):
+            np.testing.assert_array_equal(tg[f][invr].view(np.uint32), to[f][invr].view(np.uint32), err_msg=f)
+        np.testing.assert_array_equal(tg["scale_level_r"], to["scale_level_r"])
+
+
+@pytest.mark.parametrize("two", [False, True], ids=["mono_kb8", "two_cams"])
+@pytest.mark.parametrize("th", [1, 3, 15])
+def test_search_local_points_rig(gpu, om, th, two):
+    """Tracking::SearchLocalPoints (Tracking.cc:3407-3452) on a fisheye frame: device projection +
+    SearchByProjection's Nleft branches (ORBmatcher.cc:43-213) == the oracle, ratio 0.8 and 0.6 with
+    bFarPoints."""
+    from orb_slam3_ros_amd.matcher import search_local_points
+    rng, F, cam, rig, pts = _rig_case(70 + th, two, 60_000)
+    mvp0, obs = sm.initial_slots(rng, F.N, 0.15)
+    for ratio, bfar in ((0.8, False), (0.6, True)):
+        a, b = mvp0.copy(), mvp0.copy()
+        ng = search_local_points(F, cam, pts, a, obs, th, bfar, 10.0, ratio, rig=rig)
+        no = om.search_local_points(F, cam, pts, b, obs, th, bfar, 10.0, ratio, rig=rig)
+        assert ng == no and no[0] > 0 and no[1] > 1000
+        np.testing.assert_array_equal(a, b)
+
+
+def test_search_local_points_rig_device_resident(gpu, om):
+    import torch
+    from orb_slam3_ros_amd.matcher import DeviceMatchFrame, search_local_points_device
+    rng, F, cam, rig, pts = _rig_case(91, True, 40_000)
+    mvp0, obs = sm.initial_slots(rng, F.N, 0.1)
+    Fd = DeviceMatchFrame(F, gpu)
+    mvp_t = torch.from_numpy(mvp0.copy()).to(gpu)
+    obs_t = torch.from_numpy(obs.copy()).to(gpu)
+    pts_t = torch.from_numpy(pts.view(np.uint8).reshape(-1).copy()).to(gpu)
+    ng, ntm_g = search_local_points_device(Fd, cam, pts_t, mvp_t, obs_t, 3.0, rig=rig)
+    mvp_o = mvp0.copy()
+    no, ntm_o = om.search_local_points(F, cam, pts, mvp_o, obs, 3.0, rig=rig)
+    assert (ng, ntm_g) == (no, ntm_o) and no > 0
+    np.testing.assert_array_equal(mvp_t.cpu().numpy(), mvp_o)
+
+
+def test_two_cams_frustum_needs_rig(gpu):
+    """A two-camera frame through the pinhole-only entry points is refused (no right camera)."""
+    from orb_slam3_ros_amd import _lib
+    from orb_slam3_ros_amd.matcher import is_in_frustum, search_local_points
+    rng, F, cam, rig, pts = _rig_case(5, True, 100)
+    mvp, obs = sm.initial_slots(rng, F.N, 0.1)
+    with pytest.raises(_lib.OrbfeError):
+        is_in_frustum(F, cam, pts)
+    with pytest.raises(_lib.OrbfeError):
+        search_local_points(F, cam, pts, mvp, obs, 1.0)

@@ -39,3 +39,11 @@ def test_glibc_logf_port_exhaustive(fma):
         pytest.skip("host libm runs the FMA ifunc variant; the SSE2 model differs from it: " + log[-200:])
     assert rc == 0, log
     assert "mismatches 0" in log
+
+
+def test_glibc_atan2f_port():
+    """KannalaBrandt8::project's atan2f (KannalaBrandt8.cpp:67-82) on the device: the port against
+    the host libm on 4e7 random / camera-like pairs plus the special values."""
+    rc, log = _build_and_run("check_atan2f.cpp", "orbfe_chk_atan2f", (), ("20000000",))
+    assert rc == 0, log
+    assert "mismatches 0" in log

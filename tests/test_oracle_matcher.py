@@ -257,9 +257,10 @@ def py_is_in_frustum(F, cam, pts):
             res.append(None)
             continue
         P = p["pos"].astype(np.float32)
-        Pc = [f32(f32(f32(R[i, 0] * P[0]) + f32(R[i, 1] * P[1])) + f32(R[i, 2] * P[2])) + t[i] for i in range(3)]
+        # Eigen 3.3 fixed-size 3-term sums: a + (b + c) (redux_novec_unroller)
+        Pc = [f32(f32(R[i, 0] * P[0]) + f32(f32(R[i, 1] * P[1]) + f32(R[i, 2] * P[2]))) + t[i] for i in range(3)]
         Pc = [f32(x) for x in Pc]
-        Pc_dist = f32(np.sqrt(f32(f32(f32(Pc[0] * Pc[0]) + f32(Pc[1] * Pc[1])) + f32(Pc[2] * Pc[2]))))
+        Pc_dist = f32(np.sqrt(f32(f32(Pc[0] * Pc[0]) + f32(f32(Pc[1] * Pc[1]) + f32(Pc[2] * Pc[2])))))
         if Pc[2] < 0:
             res.append(None)
             continue
@@ -270,12 +271,12 @@ def py_is_in_frustum(F, cam, pts):
             res.append(None)
             continue
         PO = [f32(P[i] - Ow[i]) for i in range(3)]
-        dist = f32(np.sqrt(f32(f32(f32(PO[0] * PO[0]) + f32(PO[1] * PO[1])) + f32(PO[2] * PO[2]))))
+        dist = f32(np.sqrt(f32(f32(PO[0] * PO[0]) + f32(f32(PO[1] * PO[1]) + f32(PO[2] * PO[2])))))
         if dist < f32(f32(0.8) * p["min_dist"]) or dist > f32(f32(1.2) * p["max_dist"]):
             res.append(None)
             continue
         nrm = p["normal"]
-        vc = f32(f32(f32(f32(PO[0] * nrm[0]) + f32(PO[1] * nrm[1])) + f32(PO[2] * nrm[2])) / dist)
+        vc = f32(f32(f32(PO[0] * nrm[0]) + f32(f32(PO[1] * nrm[1]) + f32(PO[2] * nrm[2]))) / dist)
         if vc < f32(cam.view_cos_limit):
             res.append(None)
             continue
@@ -446,10 +447,10 @@ def py_fuse(KF, cam, pts, th, sim3):
             continue
         ur = f32(u - f32(KF.mbf) * invz)
         PO = [f32(mp["pos"][k] - f32(cam.Ow[k])) for k in range(3)]
-        d = f32(np.sqrt(f32(f32(PO[0] * PO[0] + PO[1] * PO[1]) + PO[2] * PO[2])))
+        d = f32(np.sqrt(f32(f32(PO[0] * PO[0]) + f32(f32(PO[1] * PO[1]) + f32(PO[2] * PO[2])))))
         if d < f32(f32(0.8) * mp["min_dist"]) or d > f32(f32(1.2) * mp["max_dist"]):
             continue
-        dot = f32(f32(PO[0] * mp["normal"][0] + PO[1] * mp["normal"][1]) + PO[2] * mp["normal"][2])
+        dot = f32(f32(PO[0] * mp["normal"][0]) + f32(f32(PO[1] * mp["normal"][1]) + f32(PO[2] * mp["normal"][2])))
         if float(dot) < 0.5 * float(d):
             continue
         lvl = _py_predict(mp["max_dist"], d, cam.log_scale_factor, len(KF.scale_factors))
@@ -506,7 +507,7 @@ def py_search_by_sim3(K1, K2, p1, p2, c1, c2, S12, S21, th, m12):
             v = f32(f32(c1.fy) * f32(pB[1] * invz) + f32(c1.cy))
             if not _py_in_image(B, u, v):
                 continue
-            d = f32(np.sqrt(f32(f32(pB[0] * pB[0] + pB[1] * pB[1]) + pB[2] * pB[2])))
+            d = f32(np.sqrt(f32(f32(pB[0] * pB[0]) + f32(f32(pB[1] * pB[1]) + f32(pB[2] * pB[2])))))
             if d < f32(f32(0.8) * mp["min_dist"]) or d > f32(f32(1.2) * mp["max_dist"]):
                 continue
             lvl = _py_predict(mp["max_dist"], d, logsfB, len(B.scale_factors))
@@ -548,3 +549,102 @@ def test_oracle_search_by_sim3_vs_python(oracle_lib, scale):
     np.testing.assert_array_equal(mo, mp)
     if scale == 1.0:
         assert n > 50
+
+
+def _libm():
+    import ctypes
+    libm = ctypes.CDLL("libm.so.6")
+    for fn in ("logf", "cosf", "sinf"):
+        getattr(libm, fn).restype = ctypes.c_float
+        getattr(libm, fn).argtypes = [ctypes.c_float]
+    libm.atan2f.restype = ctypes.c_float
+    libm.atan2f.argtypes = [ctypes.c_float, ctypes.c_float]
+    return libm
+
+
+def _py_kb8(m, x, y, z, libm):
+    """KannalaBrandt8::project (KannalaBrandt8.cpp:67-82), float32 scalars in source order."""
+    p = [f32(v) for v in m.params]
+    theta = f32(libm.atan2f(float(np.sqrt(f32(f32(x * x) + f32(y * y)))), float(z)))
+    psi = f32(libm.atan2f(float(y), float(x)))
+    t2 = f32(theta * theta)
+    t3 = f32(theta * t2)
+    t5 = f32(t3 * t2)
+    t7 = f32(t5 * t2)
+    t9 = f32(t7 * t2)
+    r = f32(f32(f32(f32(theta + f32(p[4] * t3)) + f32(p[5] * t5)) + f32(p[6] * t7)) + f32(p[7] * t9))
+    return (f32(f32(f32(p[0] * r) * f32(libm.cosf(float(psi)))) + p[2]),
+            f32(f32(f32(p[1] * r) * f32(libm.sinf(float(psi)))) + p[3]))
+
+
+def _py_view(F, cam, R, t, Ow, model, p, libm):
+    """isInFrustumChecks for one view (Frame.cc:1168-1242) with Eigen 3.3's a + (b + c) sums;
+    returns (u, v, level, viewcos, depth) or None."""
+    P = p["pos"].astype(np.float32)
+    Pc = [f32(f32(f32(R[i, 0] * P[0]) + f32(f32(R[i, 1] * P[1]) + f32(R[i, 2] * P[2]))) + t[i]) for i in range(3)]
+    depth = f32(np.sqrt(f32(f32(Pc[0] * Pc[0]) + f32(f32(Pc[1] * Pc[1]) + f32(Pc[2] * Pc[2])))))
+    if Pc[2] < 0:
+        return None
+    u, v = _py_kb8(model, Pc[0], Pc[1], Pc[2], libm)
+    if u < F.bounds[0] or u > F.bounds[1] or v < F.bounds[2] or v > F.bounds[3]:
+        return None
+    PO = [f32(P[i] - Ow[i]) for i in range(3)]
+    dist = f32(np.sqrt(f32(f32(PO[0] * PO[0]) + f32(f32(PO[1] * PO[1]) + f32(PO[2] * PO[2])))))
+    if dist < f32(f32(0.8) * p["min_dist"]) or dist > f32(f32(1.2) * p["max_dist"]):
+        return None
+    nrm = p["normal"]
+    vc = f32(f32(f32(PO[0] * nrm[0]) + f32(f32(PO[1] * nrm[1]) + f32(PO[2] * nrm[2]))) / dist)
+    if vc < f32(cam.view_cos_limit):
+        return None
+    lv = int(math.ceil(f32(f32(libm.logf(float(f32(p["max_dist"] / dist)))) / f32(cam.log_scale_factor))))
+    return u, v, min(max(lv, 0), len(F.scale_factors) - 1), vc, depth
+
+
+@pytest.mark.parametrize("two", [False, True])
+def test_oracle_frustum_rig_vs_python(oracle_lib, two):
+    """Frame::isInFrustum with KannalaBrandt8 cameras (Frame.cc:512-586, 1168-1242): the C++ oracle
+    against a float32 Python restatement, a monocular fisheye frame and a two-camera frame."""
+    libm = _libm()
+    rng = np.random.default_rng(40 + two)
+    F = sm.synth_frame_two(rng, 300, 280) if two else sm.synth_frame(rng, 300, 512, 512, stereo=False)
+    cam = sm.synth_camera(rng, rot_deg=20.0)
+    rig = sm.synth_rig(cam, two)
+    pts = sm.synth_local_map_3d_rig(rng, F, cam, 600, two=two)
+    n, tr = oracle_lib.is_in_frustum(F, cam, pts, rig)
+    R = np.array(cam.Rcw[:], np.float32).reshape(3, 3)
+    t = np.array(cam.tcw[:], np.float32)
+    Ow = np.array(cam.Ow[:], np.float32)
+    # right view: mR = Rrl * mRcw, mt = Rrl * mtcw + trl, twc = mRwc * tlr + mOw (a + (b + c) sums)
+    A = np.array(rig.Rrl[:], np.float32).reshape(3, 3)
+    Rwc = np.array(rig.Rwc[:], np.float32).reshape(3, 3)
+    s3 = lambda a, b, c: f32(f32(a) + f32(f32(b) + f32(c)))   # noqa: E731
+    R2 = np.array([[s3(A[i, 0] * R[0, j], A[i, 1] * R[1, j], A[i, 2] * R[2, j]) for j in range(3)] for i in range(3)],
+                  np.float32)
+    t2 = np.array([f32(s3(A[i, 0] * t[0], A[i, 1] * t[1], A[i, 2] * t[2]) + f32(rig.trl[i])) for i in range(3)],
+                  np.float32)
+    tl = np.array(rig.tlr[:], np.float32)
+    Ow2 = np.array([f32(s3(Rwc[i, 0] * tl[0], Rwc[i, 1] * tl[1], Rwc[i, 2] * tl[2]) + Ow[i]) for i in range(3)],
+                   np.float32)
+    count = nr = 0
+    for i, p in enumerate(pts):
+        if p["flags"] & (sm.MP_SKIP | sm.MP_BAD):
+            assert not tr["flags"][i] & (sm.MP_IN_VIEW | sm.MP_IN_VIEW_R)
+            continue
+        lv = _py_view(F, cam, R, t, Ow, rig.left, p, libm)
+        rv = _py_view(F, cam, R2, t2, Ow2, rig.right, p, libm) if two else None
+        assert bool(tr["flags"][i] & sm.MP_IN_VIEW) == (lv is not None), i
+        assert bool(tr["flags"][i] & sm.MP_IN_VIEW_R) == (rv is not None), i
+        if lv is not None:
+            got = (tr["proj_x"][i], tr["proj_y"][i], int(tr["scale_level"][i]), tr["view_cos"][i], tr["depth"][i])
+            assert [np.float32(a).tobytes() for a in (got[0], got[1], got[3], got[4])] == \
+                [np.float32(b).tobytes() for b in (lv[0], lv[1], lv[3], lv[4])], i
+            assert got[2] == lv[2], i
+        if rv is not None:
+            nr += 1
+            got = (tr["proj_xr"][i], tr["proj_yr"][i], int(tr["scale_level_r"][i]), tr["view_cos_r"][i])
+            assert [np.float32(a).tobytes() for a in (got[0], got[1], got[3])] == \
+                [np.float32(b).tobytes() for b in (rv[0], rv[1], rv[3])], i
+            assert got[2] == rv[2], i
+        count += (lv is not None) or (rv is not None)
+    assert n == count and n > 150
+    assert nr > 100 or not two
