@@ -393,14 +393,27 @@ int orbfe_search_by_bow_kf(const orbfe_keypoint* keys1, const uint8_t* desc1, co
                            const int32_t* mp2, int32_t n2, const orbfe_feature_vector* fv2, int32_t* out12,
                            float nnratio, int32_t checkOri);
 
+/* The same with keyframes that have a second camera (NLeft != -1, KannalaBrandt8 stereo): nleft1 /
+ * nleft2 = NLeft (-1 = single camera). Their FeatureVector indices >= NLeft (the right keypoints,
+ * descriptor rows [NLeft, n)) are skipped as the reference does (ORBmatcher.cc:800-802, 817-819:
+ * idx >= mvKeysUn.size()); keys1 / keys2 hold n entries of which [0, NLeft) (mvKeysUn) are read. */
+int orbfe_search_by_bow_kf2(const orbfe_keypoint* keys1, const uint8_t* desc1, const int32_t* mp1, int32_t n1,
+                            int32_t nleft1, const orbfe_feature_vector* fv1, const orbfe_keypoint* keys2,
+                            const uint8_t* desc2, const int32_t* mp2, int32_t n2, int32_t nleft2,
+                            const orbfe_feature_vector* fv2, int32_t* out12, float nnratio, int32_t checkOri);
+
 /* MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:329-403) for n_points points at once: the
  * observed descriptors of point p are rows [offsets[p], offsets[p+1]) of desc (<= 2048 per point).
  * best[p] = the row (relative to offsets[p]) with the least median Hamming distance to the others
  * (median = sorted row [(N-1)/2], first on ties), -1 for a point without descriptors. */
 int orbfe_distinctive_descriptors(const uint8_t* desc, const int32_t* offsets, int32_t n_points, int32_t* best);
 
-/* SearchForTriangulation(pKF1, pKF2, vMatchedPairs, bOnlyStereo, bCoarse) (ORBmatcher.cc:907-1146,
- * pinhole keyframes without a second camera). mp1 / mp2: GetMapPoint(idx) presence (any MapPoint,
+/* SearchForTriangulation(pKF1, pKF2, vMatchedPairs, bOnlyStereo, bCoarse) (ORBmatcher.cc:907-1146).
+ * Keyframes with a second camera (two_cams: keys = mvKeys ++ mvKeysRight, the reference's kp1 / kp2
+ * selection :979-984, 1001-1006) take the NLeft branches: bStereo is false for them, KF1's epipole test
+ * is skipped; their camera-pair epipolar test (KannalaBrandt8::TriangulateMatches: Eigen JacobiSVD
+ * triangulation, :1036-1066) stays with the camera model on the host, so two-camera keyframes need
+ * bCoarse (as LocalMapping passes for inertial maps); otherwise ORBFE_E_ARG. mp1 / mp2: GetMapPoint(idx) presence (any MapPoint,
  * bad or not, -> handle >= 0; NULL -> -1); keyframe uright = mvuRight (NULL = all monocular).
  * F12 (row-major) and ep are the values the reference derives once per call:
  * F12 = K1^-T [t12]x R12 K2^-1 (Pinhole::epipolarConstrain, Pinhole.cpp:107-129) and
@@ -444,6 +457,16 @@ typedef struct orbfe_kf_camera {
 int orbfe_fuse(const orbfe_frame* KF, const orbfe_kf_camera* cam, const float* inv_level_sigma2,
                const orbfe_map_point_3d* pts, int32_t n, float th, int32_t sim3, int32_t* best_idx,
                int32_t* best_dist);
+
+/* Fuse with the keyframe's camera model and side (ORBmatcher.cc:1148-1298 with bRight, :1339-1455):
+ * model = pCamera (mpCamera, or mpCamera2 with bRight; NULL = pinhole from cam), cam->Tcw / Ow = the
+ * pose the reference uses (GetRightPose() / GetRightCameraCenter() with bRight). A keyframe with a second
+ * camera (KF->two_cams) is searched on its left grid, or with bRight on its right grid (GetFeaturesInArea(
+ * .., bRight), mvKeysRight) with best_idx reported as NLeft + the right index (:1283); its mvuRight is -1
+ * (Frame.cc:1137), so the monocular reprojection gate applies. bRight needs sim3 = 0 and two_cams. */
+int orbfe_fuse_rig(const orbfe_frame* KF, const orbfe_kf_camera* cam, const orbfe_camera_model* model,
+                   const float* inv_level_sigma2, const orbfe_map_point_3d* pts, int32_t n, float th, int32_t sim3,
+                   int32_t bRight, int32_t* best_idx, int32_t* best_dist);
 
 /* SearchByProjection(pKF, Scw, vpPoints, vpMatched, th, ratioHamming) (ORBmatcher.cc:427-523) and,
  * with point_kfs != NULL, the vpPointsKFs / vpMatchedKF overload (:525-646). cam->Tcw is the SE3

@@ -140,6 +140,8 @@ def _match_sigs(L):
     L.oro_distinctive_descriptors.argtypes = [vp, vp, ci, vp]
     L.oro_search_for_triangulation.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, vp]
     L.oro_fuse.argtypes = [vp, vp, vp, vp, ci, cf, ci, vp, vp]
+    L.oro_fuse_rig.argtypes = [vp, vp, vp, vp, vp, ci, cf, ci, ci, vp, vp]
+    L.oro_search_by_bow_kf2.argtypes = [vp, vp, vp, ci, ci, vp, vp, vp, vp, ci, ci, vp, vp, cf, ci]
     L.oro_sbp_sim3.argtypes = [vp, vp, vp, ci, vp, ci, cf, vp, vp]
     L.oro_search_by_sim3.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, cf, vp, vp]
     L.oro_is_in_frustum.argtypes = [vp, vp, vp, ci, vp]
@@ -189,16 +191,16 @@ class OracleMatcher:
                                      f_fv.ref(), out.ctypes.data, self.nnratio, self.checkOri)
         return n, out
 
-    def search_by_bow_kf(self, keys1, desc1, mp1, fv1, keys2, desc2, mp2, fv2):
+    def search_by_bow_kf(self, keys1, desc1, mp1, fv1, keys2, desc2, mp2, fv2, nleft1=-1, nleft2=-1):
         k1, k2 = np.ascontiguousarray(keys1), np.ascontiguousarray(keys2)
         d1 = np.ascontiguousarray(desc1, np.uint8)
         d2 = np.ascontiguousarray(desc2, np.uint8)
         m1 = np.ascontiguousarray(mp1, np.int32)
         m2 = np.ascontiguousarray(mp2, np.int32)
         out = np.full(len(k1), -1, np.int32)
-        n = self.L.oro_search_by_bow_kf(k1.ctypes.data, d1.ctypes.data, m1.ctypes.data, len(k1), fv1.ref(),
-                                        k2.ctypes.data, d2.ctypes.data, m2.ctypes.data, len(k2), fv2.ref(),
-                                        out.ctypes.data, self.nnratio, self.checkOri)
+        n = self.L.oro_search_by_bow_kf2(k1.ctypes.data, d1.ctypes.data, m1.ctypes.data, len(k1), int(nleft1),
+                                         fv1.ref(), k2.ctypes.data, d2.ctypes.data, m2.ctypes.data, len(k2),
+                                         int(nleft2), fv2.ref(), out.ctypes.data, self.nnratio, self.checkOri)
         return n, out
 
 
@@ -215,7 +217,7 @@ class OracleMatcher:
                                                 int(bOnlyStereo), int(bCoarse), self.checkOri, out.ctypes.data)
         return n, out
 
-    def fuse(self, KF, cam, pts, th=3.0, inv_level_sigma2=None, sim3=False):
+    def fuse(self, KF, cam, pts, th=3.0, inv_level_sigma2=None, sim3=False, model=None, bRight=False):
         if inv_level_sigma2 is None:
             sf = KF.scale_factors
             inv_level_sigma2 = (np.float32(1.0) / (sf * sf)).astype(np.float32)
@@ -223,8 +225,9 @@ class OracleMatcher:
         p = np.ascontiguousarray(pts)
         bi = np.full(len(p), -1, np.int32)
         bd = np.full(len(p), -1, np.int32)
-        n = self.L.oro_fuse(KF.ref(), ctypes.byref(cam), sig.ctypes.data, p.ctypes.data, len(p), float(th),
-                            int(bool(sim3)), bi.ctypes.data, bd.ctypes.data)
+        n = self.L.oro_fuse_rig(KF.ref(), ctypes.byref(cam), ctypes.byref(model) if model is not None else None,
+                                sig.ctypes.data, p.ctypes.data, len(p), float(th), int(bool(sim3)), int(bool(bRight)),
+                                bi.ctypes.data, bd.ctypes.data)
         return n, bi, bd
 
     def sbp_sim3(self, KF, cam, pts, matched, th=10, ratioHamming=1.0, point_kfs=None, matched_kf=None):

@@ -58,6 +58,34 @@ const int TH_HIGH = 100, TH_LOW = 50, HISTO_LENGTH = 30;
 // rhs.col(j))).sum()). The reference's Eigen is focal's libeigen3-dev 3.3.7 (Dockerfile:19).
 static inline float eig_sum3(float a, float b, float c) { return a + (b + c); }
 
+struct CamModel {
+    int type;
+    float p[8];
+};
+
+// GeometricCamera::project(const Eigen::Vector3f&): Pinhole.cpp:43-49 (fx * x / z + cx) and
+// KannalaBrandt8.cpp:67-82 (atan2f / sqrtf explicit; cos(psi) / sin(psi) of a float resolve to
+// cosf / sinf, as for computeOrbDescriptor's rotation), float arithmetic in source order.
+static void cam_project(const CamModel& m, const float* Pc, float& u, float& v) {
+    if (m.type == ORBFE_CAM_KANNALA_BRANDT8) {
+        const float x2_plus_y2 = Pc[0] * Pc[0] + Pc[1] * Pc[1];
+        const float theta = atan2f(sqrtf(x2_plus_y2), Pc[2]);
+        const float psi = atan2f(Pc[1], Pc[0]);
+        const float theta2 = theta * theta;
+        const float theta3 = theta * theta2;
+        const float theta5 = theta3 * theta2;
+        const float theta7 = theta5 * theta2;
+        const float theta9 = theta7 * theta2;
+        const float r = theta + m.p[4] * theta3 + m.p[5] * theta5 + m.p[6] * theta7 + m.p[7] * theta9;
+        u = m.p[0] * r * cosf(psi) + m.p[2];
+        v = m.p[1] * r * sinf(psi) + m.p[3];
+        return;
+    }
+    u = m.p[0] * Pc[0] / Pc[2] + m.p[2];
+    v = m.p[1] * Pc[1] / Pc[2] + m.p[3];
+}
+
+
 struct Grid {
     const orbfe_frame* F;
     float invw, invh;
@@ -449,10 +477,13 @@ int oro_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, con
 
 // vbMatched2 / vpMatches12 are indexed by keypoint; the std::map walk is the same merge-join as
 // the KF-F variant. Note the strict bestDist1 < TH_LOW here (<= in the KF-F variant).
-int oro_search_by_bow_kf(const orbfe_keypoint* keys1, const uint8_t* desc1, const int32_t* mp1, int32_t n1,
-                         const orbfe_feature_vector* fv1, const orbfe_keypoint* keys2, const uint8_t* desc2,
-                         const int32_t* mp2, int32_t n2, const orbfe_feature_vector* fv2, int32_t* out12,
-                         float nnratio, int32_t checkOri) {
+// nleft1 / nleft2: NLeft of a keyframe with a second camera (-1: none); its right indices are skipped
+// (ORBmatcher.cc:800-802, 817-819: idx >= mvKeysUn.size() == NLeft).
+int oro_search_by_bow_kf2(const orbfe_keypoint* keys1, const uint8_t* desc1, const int32_t* mp1, int32_t n1,
+                          int32_t nleft1, const orbfe_feature_vector* fv1, const orbfe_keypoint* keys2,
+                          const uint8_t* desc2, const int32_t* mp2, int32_t n2, int32_t nleft2,
+                          const orbfe_feature_vector* fv2, int32_t* out12, float nnratio, int32_t checkOri) {
+    const unsigned lim1 = (unsigned)(nleft1 >= 0 ? nleft1 : n1), lim2 = (unsigned)(nleft2 >= 0 ? nleft2 : n2);
     std::vector<int> rotHist[HISTO_LENGTH];
     std::vector<char> vbMatched2(n2 > 0 ? n2 : 1, 0);
     for (int i = 0; i < n1; i++) out12[i] = -1;
@@ -462,11 +493,13 @@ int oro_search_by_bow_kf(const orbfe_keypoint* keys1, const uint8_t* desc1, cons
         if (fv1->node_ids[a] == fv2->node_ids[b]) {
             for (int ia = fv1->offsets[a]; ia < fv1->offsets[a + 1]; ia++) {
                 const unsigned idx1 = fv1->indices[ia];
+                if (idx1 >= lim1) continue;
                 if (mp1[idx1] < 0) continue;   // !pMP1 || pMP1->isBad()
                 const uint8_t* d1 = desc1 + (size_t)idx1 * 32;
                 int bestDist1 = 256, bestIdx2 = -1, bestDist2 = 256;
                 for (int ib = fv2->offsets[b]; ib < fv2->offsets[b + 1]; ib++) {
                     const unsigned idx2 = fv2->indices[ib];
+                    if (idx2 >= lim2) continue;
                     if (vbMatched2[idx2] || mp2[idx2] < 0) continue;
                     const int dist = oracle::hamming(d1, desc2 + (size_t)idx2 * 32);
                     if (dist < bestDist1) { bestDist2 = bestDist1; bestDist1 = dist; bestIdx2 = (int)idx2; }
@@ -498,6 +531,14 @@ int oro_search_by_bow_kf(const orbfe_keypoint* keys1, const uint8_t* desc1, cons
         }
     }
     return nmatches;
+}
+
+int oro_search_by_bow_kf(const orbfe_keypoint* keys1, const uint8_t* desc1, const int32_t* mp1, int32_t n1,
+                         const orbfe_feature_vector* fv1, const orbfe_keypoint* keys2, const uint8_t* desc2,
+                         const int32_t* mp2, int32_t n2, const orbfe_feature_vector* fv2, int32_t* out12,
+                         float nnratio, int32_t checkOri) {
+    return oro_search_by_bow_kf2(keys1, desc1, mp1, n1, -1, fv1, keys2, desc2, mp2, n2, -1, fv2, out12, nnratio,
+                                 checkOri);
 }
 
 // Distances[N][N] (symmetric, zero diagonal), each row sorted, median = row[0.5 * (N - 1)] with the
@@ -581,7 +622,8 @@ int oro_search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, con
             for (int ia = fv1->offsets[a]; ia < fv1->offsets[a + 1]; ia++) {
                 const unsigned idx1 = fv1->indices[ia];
                 if (mp1[idx1] >= 0) continue;   // a MapPoint is already there
-                const bool bStereo1 = KF1->uright && KF1->uright[idx1] >= 0;
+                // keys = mvKeysUn, or mvKeys ++ mvKeysRight with a second camera (ORBmatcher.cc:979-984)
+                const bool bStereo1 = !KF1->two_cams && KF1->uright && KF1->uright[idx1] >= 0;
                 if (bOnlyStereo && !bStereo1) continue;
                 const orbfe_keypoint& kp1 = KF1->keys[idx1];
                 const uint8_t* d1 = KF1->desc + (size_t)idx1 * 32;
@@ -589,12 +631,12 @@ int oro_search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, con
                 for (int ib = fv2->offsets[b]; ib < fv2->offsets[b + 1]; ib++) {
                     const unsigned idx2 = fv2->indices[ib];
                     if (mp2[idx2] >= 0) continue;   // vbMatched2 is never set by the reference
-                    const bool bStereo2 = KF2->uright && KF2->uright[idx2] >= 0;
+                    const bool bStereo2 = !KF2->two_cams && KF2->uright && KF2->uright[idx2] >= 0;
                     if (bOnlyStereo && !bStereo2) continue;
                     const int dist = oracle::hamming(d1, KF2->desc + (size_t)idx2 * 32);
                     if (dist > TH_LOW || dist > bestDist) continue;
                     const orbfe_keypoint& kp2 = KF2->keys[idx2];
-                    if (!bStereo1 && !bStereo2) {
+                    if (!bStereo1 && !bStereo2 && !KF1->two_cams) {
                         const float distex = ep[0] - kp2.x;
                         const float distey = ep[1] - kp2.y;
                         if (distex * distex + distey * distey < 100 * KF2->scale_factors[kp2.octave]) continue;
@@ -630,9 +672,18 @@ int oro_search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, con
 }
 
 // The search half of both Fuse overloads; best_dist = -1 when no candidate survived the checks.
-int oro_fuse(const orbfe_frame* KF, const orbfe_kf_camera* cam, const float* inv_level_sigma2,
-             const orbfe_map_point_3d* pts, int32_t n, float th, int32_t sim3, int32_t* best_idx, int32_t* best_dist) {
-    const Grid grid(KF);
+// model: pCamera (mpCamera, or mpCamera2 with bRight; NULL = pinhole from cam); bRight searches the
+// right grid of a two-camera keyframe and reports global indices (idx += NLeft, ORBmatcher.cc:1283).
+int oro_fuse_rig(const orbfe_frame* KF, const orbfe_kf_camera* cam, const orbfe_camera_model* model,
+                 const float* inv_level_sigma2, const orbfe_map_point_3d* pts, int32_t n, float th, int32_t sim3,
+                 int32_t bRight, int32_t* best_idx, int32_t* best_dist) {
+    const Grid grid(KF, KF->two_cams ? (bRight ? 1 : 0) : -1);
+    CamModel M{ORBFE_CAM_PINHOLE, {cam->fx, cam->fy, cam->cx, cam->cy, 0.f, 0.f, 0.f, 0.f}};
+    if (model) {
+        M.type = model->type;
+        memcpy(M.p, model->params, sizeof(M.p));
+    }
+    const float* uright = KF->two_cams ? nullptr : KF->uright;   // KannalaBrandt8 keyframes: mvuRight == -1
     int nFused = 0;
     for (int i = 0; i < n; i++) {
         best_idx[i] = -1;
@@ -644,8 +695,8 @@ int oro_fuse(const orbfe_frame* KF, const orbfe_kf_camera* cam, const float* inv
         pose_apply(cam->Tcw, mp.pos, p3Dc);
         if (p3Dc[2] < 0.0f) continue;
         const float invz = 1 / p3Dc[2];
-        const float u = cam->fx * p3Dc[0] / p3Dc[2] + cam->cx;   // Pinhole::project
-        const float v = cam->fy * p3Dc[1] / p3Dc[2] + cam->cy;
+        float u, v;
+        cam_project(M, p3Dc, u, v);   // pCamera->project (Pinhole: fx * x / z + cx)
         if (!kf_in_image(KF, u, v)) continue;
         const float ur = u - KF->mbf * invz;
         const float maxDistance = 1.2f * mp.max_dist, minDistance = 0.8f * mp.min_dist;
@@ -664,8 +715,8 @@ int oro_fuse(const orbfe_frame* KF, const orbfe_kf_camera* cam, const float* inv
             const int kpLevel = kp.octave;
             if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
             if (!sim3) {
-                if (KF->uright && KF->uright[idx] >= 0) {
-                    const float ex = u - kp.x, ey = v - kp.y, er = ur - KF->uright[idx];
+                if (uright && uright[idx] >= 0) {
+                    const float ex = u - kp.x, ey = v - kp.y, er = ur - uright[idx];
                     const float e2 = ex * ex + ey * ey + er * er;
                     if (e2 * inv_level_sigma2[kpLevel] > 7.8) continue;
                 } else {
@@ -684,6 +735,11 @@ int oro_fuse(const orbfe_frame* KF, const orbfe_kf_camera* cam, const float* inv
         }
     }
     return nFused;
+}
+
+int oro_fuse(const orbfe_frame* KF, const orbfe_kf_camera* cam, const float* inv_level_sigma2,
+             const orbfe_map_point_3d* pts, int32_t n, float th, int32_t sim3, int32_t* best_idx, int32_t* best_dist) {
+    return oro_fuse_rig(KF, cam, nullptr, inv_level_sigma2, pts, n, th, sim3, 0, best_idx, best_dist);
 }
 
 int oro_sbp_sim3(const orbfe_frame* KF, const orbfe_kf_camera* cam, const orbfe_map_point_3d* pts, int32_t n,
@@ -820,33 +876,6 @@ int oro_stereo_knn_ratio(const uint8_t* L, int32_t nl, const uint8_t* R, int32_t
     return good;
 }
 
-
-struct CamModel {
-    int type;
-    float p[8];
-};
-
-// GeometricCamera::project(const Eigen::Vector3f&): Pinhole.cpp:43-49 (fx * x / z + cx) and
-// KannalaBrandt8.cpp:67-82 (atan2f / sqrtf explicit; cos(psi) / sin(psi) of a float resolve to
-// cosf / sinf, as for computeOrbDescriptor's rotation), float arithmetic in source order.
-static void cam_project(const CamModel& m, const float* Pc, float& u, float& v) {
-    if (m.type == ORBFE_CAM_KANNALA_BRANDT8) {
-        const float x2_plus_y2 = Pc[0] * Pc[0] + Pc[1] * Pc[1];
-        const float theta = atan2f(sqrtf(x2_plus_y2), Pc[2]);
-        const float psi = atan2f(Pc[1], Pc[0]);
-        const float theta2 = theta * theta;
-        const float theta3 = theta * theta2;
-        const float theta5 = theta3 * theta2;
-        const float theta7 = theta5 * theta2;
-        const float theta9 = theta7 * theta2;
-        const float r = theta + m.p[4] * theta3 + m.p[5] * theta5 + m.p[6] * theta7 + m.p[7] * theta9;
-        u = m.p[0] * r * cosf(psi) + m.p[2];
-        v = m.p[1] * r * sinf(psi) + m.p[3];
-        return;
-    }
-    u = m.p[0] * Pc[0] / Pc[2] + m.p[2];
-    v = m.p[1] * Pc[1] / Pc[2] + m.p[3];
-}
 
 // The checks of one view (isInFrustum's Nleft == -1 branch up to its writes, or isInFrustumChecks):
 // returns the stage reached: 0 behind the camera, 1 outside the image, 2 outside the distance /

@@ -90,6 +90,9 @@ _SIGS = {
     "orbfe_search_local_points": (_c_int, [_vp, _vp, _vp, _c_int, _vp, _vp, _c_float, _c_int, _c_float, _c_float, _vp]),
     "orbfe_matcher_last_ms": (_c_float, []),
     "orbfe_is_in_frustum_rig": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _vp]),
+    "orbfe_search_by_bow_kf2": (_c_int, [_vp, _vp, _vp, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp, _vp,
+                                         _c_float, _c_int]),
+    "orbfe_fuse_rig": (_c_int, [_vp, _vp, _vp, _vp, _vp, _c_int, _c_float, _c_int, _c_int, _vp, _vp]),
     "orbfe_search_local_points_rig": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _vp, _vp, _c_float, _c_int, _c_float,
                                                _c_float, _vp]),
     "orbfe_search_local_points_rig_device": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _vp, _vp, _c_float, _c_int,

@@ -16,12 +16,13 @@
 __global__ __launch_bounds__(MT_NT) void k_bow_kfkf(const int* pairs, int npairs, const int* off1, const uint32_t* idx1s,
                                                     const int* off2, const uint32_t* idx2s, const int32_t* mp1,
                                                     const int32_t* mp2, const uint32_t* d1, const uint32_t* d2,
-                                                    float nnratio, int* matched2, int* out_idx) {
+                                                    float nnratio, int* matched2, int* out_idx, int lim1, int lim2) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= npairs) return;
     const int a = pairs[2 * t], b = pairs[2 * t + 1];
     for (int ia = off1[a]; ia < off1[a + 1]; ia++) {
         const unsigned i1 = idx1s[ia];
+        if ((int)i1 >= lim1) continue;   // a two-camera KF's right indices (ORBmatcher.cc:800-802)
         if (mp1[i1] < 0) continue;
         uint32_t q[8];
 #pragma unroll
@@ -29,6 +30,7 @@ __global__ __launch_bounds__(MT_NT) void k_bow_kfkf(const int* pairs, int npairs
         int bestDist1 = 256, bestIdx2 = -1, bestDist2 = 256;
         for (int ib = off2[b]; ib < off2[b + 1]; ib++) {
             const unsigned i2 = idx2s[ib];
+            if ((int)i2 >= lim2) continue;   // (ORBmatcher.cc:817-819)
             if (matched2[i2] || mp2[i2] < 0) continue;
             int dist = 0;
 #pragma unroll
@@ -150,11 +152,14 @@ __device__ __forceinline__ void be_pose_apply(const orbfe_pose& P, const float p
 #define BE_PRJ_PINHOLE 0   // Pinhole::project: fx * x / z + cx
 #define BE_PRJ_INVZ_F 1    // invz = 1 / z (float); u = fx * (x * invz) + cx
 #define BE_PRJ_INVZ_D 2    // invz = (float)(1.0 / z)
+#define BE_PRJ_MODEL 3     // GeometricCamera::project of cam_type (Pinhole == BE_PRJ_PINHOLE, KannalaBrandt8)
 struct KfGeom {
     orbfe_pose T, S;
     int two;               // apply S after T (SearchBySim3)
     float Ow[3];
     float fx, fy, cx, cy, logsf, mbf;
+    float kb[4];           // BE_PRJ_MODEL with a KannalaBrandt8 camera: k0..k3
+    int cam_type;          // BE_PRJ_MODEL: ORBFE_CAM_*
     float minx, maxx, miny, maxy;
     int nlevels, proj, dist_cam, view;
     int skip_flags;        // ORBFE_MP_* flags that exclude a point (id < 0 = NULL always does)
@@ -185,6 +190,11 @@ __global__ __launch_bounds__(MT_NT) void k_kf_geom(KfGeom g, const orbfe_map_poi
         if (g.proj == BE_PRJ_PINHOLE) {
             u = g.fx * pc[0] / pc[2] + g.cx;
             v = g.fy * pc[1] / pc[2] + g.cy;
+        } else if (g.proj == BE_PRJ_MODEL) {
+            const CamModelDev m{g.cam_type, g.fx, g.fy, g.cx, g.cy, {g.kb[0], g.kb[1], g.kb[2], g.kb[3]}};
+            const float2 uv = mt_cam_project(m, pc[0], pc[1], pc[2]);
+            u = uv.x;
+            v = uv.y;
         } else {
             const float x = pc[0] * invz, y = pc[1] * invz;
             u = g.fx * x + g.cx;
@@ -222,7 +232,8 @@ __global__ __launch_bounds__(MT_NT) void k_kf_geom(KfGeom g, const orbfe_map_poi
 __global__ __launch_bounds__(MT_NT) void k_kf_search(FrameDev fr, const KfProj* pj, const orbfe_map_point_3d* pts,
                                                      int nq, float th, int reproj, const float* inv_sigma2,
                                                      int init_best, float max_acc, const int* blocked0,
-                                                     const int* first, int* assign, int* out_dist, int* changed) {
+                                                     const int* first, int* assign, int* out_dist, int* changed,
+                                                     int cell_off = 0) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nq) return;
     const KfProj p = pj[q];
@@ -230,7 +241,8 @@ __global__ __launch_bounds__(MT_NT) void k_kf_search(FrameDev fr, const KfProj* 
     if (p.level >= 0) {
         const float radius = th * fr.scale[p.level];
         const orbfe_map_point_3d& mp = pts[q];
-        mt_for_area(fr, fr.pcstart + p.level * fr.gstride_c, fr.pcidx + p.level * fr.gstride_i, p.u, p.v, radius, -1,
+        // cell_off = MT_NCELL: a two-camera keyframe's right grid (GetFeaturesInArea(.., bRight), KeyFrame.cc:707-751)
+        mt_for_area(fr, fr.pcstart + p.level * fr.gstride_c + cell_off, fr.pcidx + p.level * fr.gstride_i, p.u, p.v, radius, -1,
                     -1, [&](int idx, const OrbKeyPoint& kp) {
             if (blocked0 && (blocked0[idx] || first[idx] < q)) return;
             if (reproj) {
@@ -293,6 +305,7 @@ __global__ void k_sim3_agree(const int* vn1, int n1, const int* vn2, const orbfe
 struct TriArgs {
     float F[9], ep[2];
     int bOnlyStereo, bCoarse;
+    int two1, two2;        // KF1 / KF2 have a second camera (mpCamera2): bStereo false, no epipole test for KF1
 };
 __global__ __launch_bounds__(MT_NT) void k_tri(const int2* items, int nitems, const uint32_t* idx1s, const int* off2,
                                                const uint32_t* idx2s, const OrbKeyPoint* k1, const OrbKeyPoint* k2,
@@ -304,7 +317,7 @@ __global__ __launch_bounds__(MT_NT) void k_tri(const int2* items, int nitems, co
     const int2 it = items[t];
     const unsigned i1 = idx1s[it.x];
     if (mp1[i1] >= 0) return;
-    const bool bStereo1 = ur1 && ur1[i1] >= 0;
+    const bool bStereo1 = !a.two1 && ur1 && ur1[i1] >= 0;   // (!pKF1->mpCamera2 && mvuRight >= 0)
     if (a.bOnlyStereo && !bStereo1) return;
     const OrbKeyPoint kp1 = k1[i1];
     uint32_t q[8];
@@ -318,14 +331,14 @@ __global__ __launch_bounds__(MT_NT) void k_tri(const int2* items, int nitems, co
     for (int ib = off2[it.y]; ib < off2[it.y + 1]; ib++) {
         const unsigned i2 = idx2s[ib];
         if (mp2[i2] >= 0) continue;
-        const bool bStereo2 = ur2 && ur2[i2] >= 0;
+        const bool bStereo2 = !a.two2 && ur2 && ur2[i2] >= 0;
         if (a.bOnlyStereo && !bStereo2) continue;
         int dist = 0;
 #pragma unroll
         for (int w = 0; w < 8; w++) dist += __popc(q[w] ^ d2[8 * i2 + w]);
         if (dist > MT_TH_LOW || dist > bestDist) continue;
         const OrbKeyPoint kp2 = k2[i2];
-        if (!bStereo1 && !bStereo2) {
+        if (!bStereo1 && !bStereo2 && !a.two1) {
             const float distex = a.ep[0] - kp2.x, distey = a.ep[1] - kp2.y;
             if (distex * distex + distey * distey < 100 * scale2[kp2.octave]) continue;
         }
@@ -349,9 +362,18 @@ int orbfe_search_by_bow_kf(const orbfe_keypoint* keys1, const uint8_t* desc1, co
                            const orbfe_feature_vector* fv1, const orbfe_keypoint* keys2, const uint8_t* desc2,
                            const int32_t* mp2, int32_t n2, const orbfe_feature_vector* fv2, int32_t* out12,
                            float nnratio, int32_t checkOri) {
+    return orbfe_search_by_bow_kf2(keys1, desc1, mp1, n1, -1, fv1, keys2, desc2, mp2, n2, -1, fv2, out12, nnratio,
+                                   checkOri);
+}
+
+int orbfe_search_by_bow_kf2(const orbfe_keypoint* keys1, const uint8_t* desc1, const int32_t* mp1, int32_t n1,
+                            int32_t nleft1, const orbfe_feature_vector* fv1, const orbfe_keypoint* keys2,
+                            const uint8_t* desc2, const int32_t* mp2, int32_t n2, int32_t nleft2,
+                            const orbfe_feature_vector* fv2, int32_t* out12, float nnratio, int32_t checkOri) {
     if (n1 < 0 || n2 < 0 || !fv1 || !fv2 || (n1 > 0 && (!keys1 || !desc1 || !mp1 || !out12)) ||
-        (n2 > 0 && (!keys2 || !desc2 || !mp2)))
+        (n2 > 0 && (!keys2 || !desc2 || !mp2)) || nleft1 < -1 || nleft1 > n1 || nleft2 < -1 || nleft2 > n2)
         return ORBFE_E_ARG;
+    const int lim1 = nleft1 >= 0 ? nleft1 : n1, lim2 = nleft2 >= 0 ? nleft2 : n2;
     for (int i = 0; i < n1; i++) out12[i] = -1;
     if (n1 == 0 || n2 == 0 || fv1->n_nodes <= 0 || fv2->n_nodes <= 0) return 0;
     for (const orbfe_feature_vector* fv : {fv1, fv2}) {
@@ -403,7 +425,7 @@ int orbfe_search_by_bow_kf(const orbfe_keypoint* keys1, const uint8_t* desc1, co
                        npairs, ms_ptr<const int>(o_off1), ms_ptr<const uint32_t>(o_idx1), ms_ptr<const int>(o_off2),
                        ms_ptr<const uint32_t>(o_idx2), ms_ptr<const int32_t>(o_mp1), ms_ptr<const int32_t>(o_mp2),
                        ms_ptr<const uint32_t>(o_d1), ms_ptr<const uint32_t>(o_d2), nnratio, ms_ptr<int>(o_m2),
-                       ms_ptr<int>(o_oi));
+                       ms_ptr<int>(o_oi), lim1, lim2);
     hipLaunchKernelGGL(k_bow_kfkf_commit, dim3(1), dim3(1024), 0, s, ms_ptr<const OrbKeyPoint>(o_k1),
                        ms_ptr<const OrbKeyPoint>(o_k2), n1, ms_ptr<const int32_t>(o_mp2), checkOri,
                        ms_ptr<const int>(o_oi), ms_ptr<int>(o_out), ms_ptr<int>(o_res));
@@ -495,8 +517,11 @@ int orbfe_search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, c
                                    const orbfe_frame* KF2, const int32_t* mp2, const orbfe_feature_vector* fv2,
                                    const float* F12, const float* ep, const float* level_sigma2_2,
                                    int32_t bOnlyStereo, int32_t bCoarse, int32_t checkOri, int32_t* matches12) {
-    if (!frame1_ok(KF1) || !frame1_ok(KF2) || !F12 || !ep || !level_sigma2_2 || (KF1->n > 0 && (!mp1 || !matches12)) ||
-        (KF2->n > 0 && !mp2))
+    // keyframes with a second camera (NLeft != -1): keys = mvKeys ++ mvKeysRight (the reference's kp1 /
+    // kp2 selection, ORBmatcher.cc:979-1008); their epipolar test is KannalaBrandt8::TriangulateMatches
+    // (an Eigen JacobiSVD), which stays with the camera model on the host: bCoarse only
+    if (!frame_ok(KF1) || !frame_ok(KF2) || !F12 || !ep || !level_sigma2_2 || (KF1->n > 0 && (!mp1 || !matches12)) ||
+        (KF2->n > 0 && !mp2) || ((KF1->two_cams || KF2->two_cams) && !bCoarse))
         return ORBFE_E_ARG;
     const int n1 = KF1->n, n2 = KF2->n;
     for (int i = 0; i < n1; i++) matches12[i] = -1;
@@ -524,8 +549,9 @@ int orbfe_search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, c
     const size_t o_k1 = p.upload(KF1->keys, (size_t)n1 * sizeof(orbfe_keypoint));
     const size_t o_k2 = p.upload(KF2->keys, (size_t)n2 * sizeof(orbfe_keypoint));
     const size_t o_d1 = p.upload(KF1->desc, (size_t)n1 * 32), o_d2 = p.upload(KF2->desc, (size_t)n2 * 32);
-    const size_t o_u1 = KF1->uright ? p.upload(KF1->uright, (size_t)n1 * 4) : 0;
-    const size_t o_u2 = KF2->uright ? p.upload(KF2->uright, (size_t)n2 * 4) : 0;
+    const bool u1 = KF1->uright && !KF1->two_cams, u2 = KF2->uright && !KF2->two_cams;
+    const size_t o_u1 = u1 ? p.upload(KF1->uright, (size_t)n1 * 4) : 0;
+    const size_t o_u2 = u2 ? p.upload(KF2->uright, (size_t)n2 * 4) : 0;
     const size_t o_mp1 = p.upload(mp1, (size_t)n1 * 4), o_mp2 = p.upload(mp2, (size_t)n2 * 4);
     const size_t o_sc2 = p.upload(KF2->scale_factors, (size_t)KF2->nlevels * 4);
     const size_t o_sg2 = p.upload(level_sigma2_2, (size_t)KF2->nlevels * 4);
@@ -540,12 +566,14 @@ int orbfe_search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, c
     ta.ep[1] = ep[1];
     ta.bOnlyStereo = bOnlyStereo != 0;
     ta.bCoarse = bCoarse != 0;
+    ta.two1 = KF1->two_cams != 0;
+    ta.two2 = KF2->two_cams != 0;
     fill(ms_ptr<int>(o_oi), n1, -1);
     hipLaunchKernelGGL(k_tri, dim3((nitems + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, ms_ptr<const int2>(o_items), nitems,
                        ms_ptr<const uint32_t>(o_idx1), ms_ptr<const int>(o_off2), ms_ptr<const uint32_t>(o_idx2),
                        ms_ptr<const OrbKeyPoint>(o_k1), ms_ptr<const OrbKeyPoint>(o_k2), ms_ptr<const uint32_t>(o_d1),
-                       ms_ptr<const uint32_t>(o_d2), KF1->uright ? ms_ptr<const float>(o_u1) : nullptr,
-                       KF2->uright ? ms_ptr<const float>(o_u2) : nullptr, ms_ptr<const int32_t>(o_mp1),
+                       ms_ptr<const uint32_t>(o_d2), u1 ? ms_ptr<const float>(o_u1) : nullptr,
+                       u2 ? ms_ptr<const float>(o_u2) : nullptr, ms_ptr<const int32_t>(o_mp1),
                        ms_ptr<const int32_t>(o_mp2), ms_ptr<const float>(o_sc2), ms_ptr<const float>(o_sg2), ta,
                        ms_ptr<int>(o_oi));
     hipLaunchKernelGGL(k_bow_kfkf_commit, dim3(1), dim3(1024), 0, s, ms_ptr<const OrbKeyPoint>(o_k1),
@@ -564,8 +592,16 @@ int orbfe_search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, c
 int orbfe_fuse(const orbfe_frame* KF, const orbfe_kf_camera* cam, const float* inv_level_sigma2,
                const orbfe_map_point_3d* pts, int32_t n, float th, int32_t sim3, int32_t* best_idx,
                int32_t* best_dist) {
-    if (!frame1_ok(KF) || !cam || !pose_ok(&cam->Tcw) || n < 0 || (n > 0 && (!pts || !best_idx || !best_dist)) ||
-        (!sim3 && !inv_level_sigma2))
+    if (KF && KF->two_cams) return ORBFE_E_ARG;   // the pinhole API: no camera model / side
+    return orbfe_fuse_rig(KF, cam, nullptr, inv_level_sigma2, pts, n, th, sim3, 0, best_idx, best_dist);
+}
+
+int orbfe_fuse_rig(const orbfe_frame* KF, const orbfe_kf_camera* cam, const orbfe_camera_model* model,
+                   const float* inv_level_sigma2, const orbfe_map_point_3d* pts, int32_t n, float th, int32_t sim3,
+                   int32_t bRight, int32_t* best_idx, int32_t* best_dist) {
+    if (!frame_ok(KF) || !cam || !pose_ok(&cam->Tcw) || n < 0 || (n > 0 && (!pts || !best_idx || !best_dist)) ||
+        (!sim3 && !inv_level_sigma2) || (bRight && (sim3 || !KF->two_cams)) ||
+        (model && model->type != ORBFE_CAM_PINHOLE && model->type != ORBFE_CAM_KANNALA_BRANDT8))
         return ORBFE_E_ARG;
     for (int i = 0; i < n; i++) best_idx[i] = best_dist[i] = -1;
     if (n == 0 || KF->n == 0) return 0;
@@ -584,7 +620,13 @@ int orbfe_fuse(const orbfe_frame* KF, const orbfe_kf_camera* cam, const float* i
     hipStream_t s = t_ms.stream;
     const FrameDev fr = fp.view();
     fp.launch_grid(fr);
-    const KfGeom g = kf_geom(cam, KF, cam->log_scale_factor, BE_PRJ_PINHOLE, 0, 1);
+    KfGeom g = kf_geom(cam, KF, cam->log_scale_factor, BE_PRJ_PINHOLE, 0, 1);
+    if (model) {   // pCamera->project: mpCamera, or mpCamera2 with bRight (ORBmatcher.cc:1154-1163)
+        g.proj = BE_PRJ_MODEL;
+        g.cam_type = model->type;
+        g.fx = model->params[0]; g.fy = model->params[1]; g.cx = model->params[2]; g.cy = model->params[3];
+        for (int k = 0; k < 4; k++) g.kb[k] = model->type == ORBFE_CAM_KANNALA_BRANDT8 ? model->params[4 + k] : 0.f;
+    }
     const dim3 gq((n + MT_NT - 1) / MT_NT);
     hipLaunchKernelGGL(k_kf_geom, gq, dim3(MT_NT), 0, s, g, ms_ptr<const orbfe_map_point_3d>(o_pts), n,
                        (const uint8_t*)nullptr, ms_ptr<KfProj>(o_pj));
@@ -593,7 +635,7 @@ int orbfe_fuse(const orbfe_frame* KF, const orbfe_kf_camera* cam, const float* i
                        ms_ptr<const orbfe_map_point_3d>(o_pts), n, th, sim3 ? 0 : 1,
                        sim3 ? (const float*)nullptr : ms_ptr<const float>(o_sig), sim3 ? INT_MAX : 256,
                        (float)MT_TH_LOW, (const int*)nullptr, (const int*)nullptr, ms_ptr<int>(o_as), ms_ptr<int>(o_ds),
-                       (int*)nullptr);
+                       (int*)nullptr, bRight ? MT_NCELL : 0);
     HIPCHK(hipMemsetAsync(ms_ptr<int>(o_cnt), 0, 4, s));
     hipLaunchKernelGGL(k_count_ge0, gq, dim3(MT_NT), 0, s, ms_ptr<const int>(o_as), n, ms_ptr<int>(o_cnt));
     HIPCHK(hipGetLastError());

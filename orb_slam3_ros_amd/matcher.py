@@ -374,9 +374,11 @@ class ORBmatcher:
 
     # SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12) (:765-903)
     def SearchByBoWKF(self, keys1, desc1, map_points1, featvec1: FeatureVector, keys2, desc2, map_points2,
-                      featvec2: FeatureVector):
+                      featvec2: FeatureVector, nleft1: int = -1, nleft2: int = -1):
         """LocalMapping / LoopClosing variant. map_points* = GetMapPointMatches() handles, -1 for
-        NULL or bad points. Returns (nmatches, vpMatches12 int32 [len(keys1)]: KF2 handles or -1)."""
+        NULL or bad points; nleft1 / nleft2 = NLeft of a keyframe with a second camera (its right
+        indices are skipped, ORBmatcher.cc:800-819), -1 otherwise.
+        Returns (nmatches, vpMatches12 int32 [len(keys1)]: KF2 handles or -1)."""
         k1 = np.ascontiguousarray(keys1, KEYPOINT_DTYPE).reshape(-1)
         k2 = np.ascontiguousarray(keys2, KEYPOINT_DTYPE).reshape(-1)
         d1 = np.ascontiguousarray(desc1, np.uint8).reshape(-1, 32)
@@ -386,9 +388,9 @@ class ORBmatcher:
         m1 = _i32(np.ascontiguousarray(map_points1, np.int32), len(k1), "map_points1")
         m2 = _i32(np.ascontiguousarray(map_points2, np.int32), len(k2), "map_points2")
         out = np.full(len(k1), -1, np.int32)
-        n = _lib.check(self._lib.orbfe_search_by_bow_kf(
-            k1.ctypes.data, d1.ctypes.data, m1.ctypes.data, len(k1), featvec1.ref(), k2.ctypes.data, d2.ctypes.data,
-            m2.ctypes.data, len(k2), featvec2.ref(), out.ctypes.data, self.mfNNratio,
+        n = _lib.check(self._lib.orbfe_search_by_bow_kf2(
+            k1.ctypes.data, d1.ctypes.data, m1.ctypes.data, len(k1), int(nleft1), featvec1.ref(), k2.ctypes.data,
+            d2.ctypes.data, m2.ctypes.data, len(k2), int(nleft2), featvec2.ref(), out.ctypes.data, self.mfNNratio,
             int(self.mbCheckOrientation)), "SearchByBoW(KF, KF)")
         return n, out
 
@@ -414,9 +416,12 @@ class ORBmatcher:
         return n, out
 
     # Fuse(pKF, vpMapPoints, th) (:1148-1337) / Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (:1339-1455)
-    def Fuse(self, KF: MatchFrame, cam: KFCamera, points3d, th=3.0, inv_level_sigma2=None, sim3=False):
+    def Fuse(self, KF: MatchFrame, cam: KFCamera, points3d, th=3.0, inv_level_sigma2=None, sim3=False,
+             model: "CameraModel" = None, bRight: bool = False):
         """The search half of Fuse: (n_candidates, best_idx, best_dist) per point; the map mutation
-        (Replace / AddObservation / vpReplacePoint) is the caller's, in point order."""
+        (Replace / AddObservation / vpReplacePoint) is the caller's, in point order. model = the
+        keyframe's pCamera (mpCamera, or mpCamera2 with bRight; None = pinhole from cam); bRight
+        searches a two-camera keyframe's right grid (ORBmatcher.cc:1148-1298)."""
         pts = _records(points3d, MAP_POINT_3D_DTYPE, "points3d")
         if inv_level_sigma2 is None:
             sf = KF.scale_factors
@@ -426,8 +431,14 @@ class ORBmatcher:
             raise ValueError("inv_level_sigma2 needs one entry per level")
         bi = np.full(len(pts), -1, np.int32)
         bd = np.full(len(pts), -1, np.int32)
-        n = _lib.check(self._lib.orbfe_fuse(KF.ref(), ctypes.byref(cam), sig.ctypes.data, pts.ctypes.data, len(pts),
-                                            float(th), int(bool(sim3)), bi.ctypes.data, bd.ctypes.data), "Fuse")
+        if model is None and not bRight and KF.nleft is None:
+            n = self._lib.orbfe_fuse(KF.ref(), ctypes.byref(cam), sig.ctypes.data, pts.ctypes.data, len(pts),
+                                     float(th), int(bool(sim3)), bi.ctypes.data, bd.ctypes.data)
+        else:
+            n = self._lib.orbfe_fuse_rig(KF.ref(), ctypes.byref(cam), ctypes.byref(model) if model is not None else None,
+                                         sig.ctypes.data, pts.ctypes.data, len(pts), float(th), int(bool(sim3)),
+                                         int(bool(bRight)), bi.ctypes.data, bd.ctypes.data)
+        n = _lib.check(n, "Fuse")
         return n, bi, bd
 
     # SearchByProjection(pKF, Scw, vpPoints, vpMatched, th, ratioHamming) (:427-523) and the

@@ -586,3 +586,35 @@ def synth_local_map_3d_rig(rng, F: MatchFrame, cam: Camera, n: int, two: bool = 
     m["id"] = np.arange(n) + 30000
     m["desc"] = desc
     return m
+
+
+def synth_two_cam_kf_pair(rng, nl: int, nr: int, words: int, rot: float = 20.0, drop: float = 0.15):
+    """Two KannalaBrandt8 stereo keyframes (keys = mvKeys ++ mvKeysRight, NLeft = nl) sharing a scene:
+    KF2 a perturbed copy of KF1 (both sides), map-point handles with NULL / bad slots, and
+    FeatureVectors over every descriptor row (left and right, as the reference's mFeatVec)."""
+    K1 = synth_frame_two(rng, nl, nr)
+    P, src = perturbed_frame(rng, MatchFrame(K1.keys, K1.desc, K1.bounds, K1.scale_factors), rot=rot, flip_p=0.05,
+                             drop=drop)
+    K2 = MatchFrame(P.keys, P.desc, K1.bounds, K1.scale_factors, None, K1.mbf, nleft=nl, l2r=K1.l2r, r2l=K1.r2l)
+    mp1 = np.where(rng.random(K1.N) < 0.2, -1, np.arange(K1.N) + 10).astype(np.int32)
+    mp2 = np.where(rng.random(K2.N) < 0.2, -1, np.arange(K2.N) + 5000).astype(np.int32)
+    fv1, fv2 = synth_bow(rng, words, K1, K2, src)
+    return K1, K2, mp1, mp2, fv1, fv2, src
+
+
+def right_kf_camera(cam: Camera, rig) -> KFCamera:
+    """KeyFrame::GetRightPose() = mTrl * mTcw and GetRightCameraCenter() for a KFCamera (float64
+    composition rounded to float32, as the caller's Sophus pose holds it)."""
+    R = np.array(cam.Rcw[:], np.float64).reshape(3, 3)
+    t = np.array(cam.tcw[:], np.float64)
+    Rrl = np.array(rig.Rrl[:], np.float64).reshape(3, 3)
+    trl = np.array(rig.trl[:], np.float64)
+    Rr, tr = Rrl @ R, Rrl @ t + trl
+    k = KFCamera.make(Pose.se3(Rr, tr), *TUMVI_RIGHT[:4])
+    return k
+
+
+def left_kf_camera(cam: Camera) -> KFCamera:
+    R = np.array(cam.Rcw[:], np.float64).reshape(3, 3)
+    t = np.array(cam.tcw[:], np.float64)
+    return KFCamera.make(Pose.se3(R, t), *TUMVI_LEFT[:4])

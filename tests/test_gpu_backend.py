@@ -163,3 +163,82 @@ def test_backend_edges(gpu):
     cam2.Tcw.kind = 7
     with pytest.raises(OrbfeError):
         m.Fuse(KF, cam2, pts, 3.0)
+
+
+# ---- keyframes with a second camera (NLeft != -1, KannalaBrandt8 stereo) ----
+@pytest.mark.parametrize("sides", [(True, True), (True, False), (False, True)], ids=["two_two", "two_one", "one_two"])
+@pytest.mark.parametrize("check_ori", [True, False])
+def test_search_by_bow_kf_two_cams(gpu, oracle_lib, sides, check_ori):
+    """SearchByBoW(KF1, KF2) skips a two-camera keyframe's right indices (ORBmatcher.cc:800-802, 817-819)."""
+    rng = np.random.default_rng(21 + sides[0] + 2 * sides[1])
+    K1, K2, mp1, mp2, fv1, fv2, _ = sm.synth_two_cam_kf_pair(rng, 600, 560, 200)
+    nl1 = K1.nleft if sides[0] else -1
+    nl2 = K2.nleft if sides[1] else -1
+    for ratio in (0.75, 0.9):
+        ng, og = ORBmatcher(ratio, check_ori).SearchByBoWKF(K1.keys, K1.desc, mp1, fv1, K2.keys, K2.desc, mp2, fv2,
+                                                            nl1, nl2)
+        no, oo = oracle_lib.OracleMatcher(ratio, check_ori).search_by_bow_kf(K1.keys, K1.desc, mp1, fv1, K2.keys,
+                                                                              K2.desc, mp2, fv2, nl1, nl2)
+        assert ng == no and no > 0
+        np.testing.assert_array_equal(og, oo)
+        if sides[0]:
+            assert (og[K1.nleft:] == -1).all()
+
+
+@pytest.mark.parametrize("kinds", [(True, True), (False, True), (True, False)], ids=["two_two", "one_two", "two_one"])
+@pytest.mark.parametrize("only_stereo", [False, True])
+def test_search_for_triangulation_two_cams(gpu, oracle_lib, kinds, only_stereo):
+    """SearchForTriangulation with keyframes that have a second camera (bCoarse, as LocalMapping uses
+    for inertial maps): kp from mvKeys / mvKeysRight (ORBmatcher.cc:979-1008), bStereo false for them,
+    no epipole test when KF1 has one."""
+    rng = np.random.default_rng(31 + only_stereo)
+    K1, K2, mp1, mp2, fv1, fv2, src = sm.synth_two_cam_kf_pair(rng, 700, 650, 60)
+
+    def single(K):   # the same keypoints as a single-camera pinhole keyframe with stereo uR
+        ur = np.where(rng.random(K.N) < 0.6, K.keys["x"] - 10, -1).astype(np.float32)
+        return MatchFrame(K.keys, K.desc, K.bounds, K.scale_factors, ur, K.mbf)
+    A = K1 if kinds[0] else single(K1)
+    B = K2 if kinds[1] else single(K2)
+    mp1 = np.where(rng.random(A.N) < 0.4, 5, -1).astype(np.int32)
+    mp2 = np.where(rng.random(B.N) < 0.4, 5, -1).astype(np.int32)
+    F12 = np.eye(3, dtype=np.float32)
+    ep = np.array([256.0, 250.0], np.float32)
+    sg = (B.scale_factors * B.scale_factors).astype(np.float32)
+    m = ORBmatcher(0.6, True)
+    ng, og = m.SearchForTriangulation(A, mp1, fv1, B, mp2, fv2, F12, ep, sg, only_stereo, True)
+    no, oo = oracle_lib.OracleMatcher(0.6, True).search_for_triangulation(A, mp1, fv1, B, mp2, fv2, F12, ep, sg,
+                                                                           only_stereo, True)
+    assert ng == no
+    np.testing.assert_array_equal(og, oo)
+    assert no > 0 or (only_stereo and (kinds[0] or kinds[1]))
+    # the KannalaBrandt8 epipolar test (TriangulateMatches) stays on the host: bCoarse is required
+    with pytest.raises(OrbfeError):
+        m.SearchForTriangulation(A, mp1, fv1, B, mp2, fv2, F12, ep, sg, only_stereo, False)
+
+
+@pytest.mark.parametrize("bright", [False, True], ids=["left", "right"])
+@pytest.mark.parametrize("seed,th", [(0, 3.0), (1, 5.0)])
+def test_fuse_two_cams(gpu, oracle_lib, seed, th, bright):
+    """Fuse(pKF, vpMapPoints, th, bRight) on a KannalaBrandt8 stereo keyframe (ORBmatcher.cc:1148-1298):
+    pCamera = mpCamera / mpCamera2, GetRightPose / GetRightCameraCenter, the right grid and
+    mvKeysRight, best index NLeft + right index."""
+    rng = np.random.default_rng(50 + seed)
+    KF = sm.synth_frame_two(rng, 1000, 950)
+    cam = sm.synth_camera(rng, rot_deg=20.0)
+    rig = sm.synth_rig(cam, True)
+    pts = sm.synth_local_map_3d_rig(rng, KF, cam, 8000, two=True)
+    kcam = sm.right_kf_camera(cam, rig) if bright else sm.left_kf_camera(cam)
+    model = rig.right if bright else rig.left
+    ng, big, bdg = ORBmatcher().Fuse(KF, kcam, pts, th, model=model, bRight=bright)
+    no, bio, bdo = oracle_lib.OracleMatcher().fuse(KF, kcam, pts, th, model=model, bRight=bright)
+    assert ng == no and no > 100
+    np.testing.assert_array_equal(big, bio)
+    np.testing.assert_array_equal(bdg, bdo)
+    hit = big[big >= 0]
+    assert ((hit >= KF.nleft) == bright).all()
+    # Fuse(pKF, Scw, ...) reads the left camera of the same keyframe
+    if not bright:
+        ng, big, bdg = ORBmatcher().Fuse(KF, kcam, pts, th, sim3=True, model=model)
+        no, bio, bdo = oracle_lib.OracleMatcher().fuse(KF, kcam, pts, th, sim3=True, model=model)
+        assert ng == no and no > 0
+        np.testing.assert_array_equal(big, bio)

@@ -412,8 +412,9 @@ def test_search_by_bow_two_cams(gpu, om, seed, check_ori):
         assert (out_o[900:] >= 0).any()   # right-camera matches happened
 
 
-def test_two_cams_rejected_where_unsupported(gpu):
-    """The single-camera-only entries refuse a two-camera frame instead of mis-reading it."""
+def test_two_cams_input_rules(gpu):
+    """Two-camera frames need their right-view inputs: the last-frame search refuses one without the
+    right projections, SearchForInitialization (monocular initialisation, Nleft == -1 only) refuses it."""
     from orb_slam3_ros_amd._lib import OrbfeError
     rng = np.random.default_rng(90)
     F = sm.synth_frame_two(rng, 50, 40)
