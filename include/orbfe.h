@@ -530,7 +530,11 @@ int orbfe_vocabulary_transform(const orbfe_vocabulary* voc, const uint8_t* desc,
  * maps from initUndistortRectifyMap (System.cc:233-240, Settings.cc:506-509), BORDER_CONSTANT 0.
  * ------------------------------------------------------------------------------------------- */
 /* Batched, device-resident: n images (device pointer tables in host memory), one map pair
- * (dw x dh floats each, row-major) shared by all; stream = hipStream_t or NULL. */
+ * (dw x dh floats each, row-major) shared by all; stream = hipStream_t or NULL. A source needs
+ * sstride * (sh - 1) + sw readable bytes and a destination dstride * (dh - 1) + dw writable ones
+ * (the last rows may end at the image width). The pointer tables are uploaded asynchronously into a
+ * per-thread ring of 4 device tables keyed by the pointers, so calls that cycle through up to four
+ * buffer sets upload nothing after the first call of each. */
 int orbfe_remap_linear_batch(const uint8_t* const* d_src, int sw, int sh, int sstride, const float* d_mapx,
                              const float* d_mapy, int dw, int dh, uint8_t* const* d_dst, int dstride, int n,
                              void* stream);

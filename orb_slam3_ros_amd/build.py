@@ -23,6 +23,10 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps + [hdr])
 
 
+CAPI_SRC = os.path.join(os.path.dirname(_HERE), "tests", "native", "capi_frontend.cpp")
+CAPI_BIN = os.path.join(os.path.dirname(_HERE), "tests", "native", "capi_frontend")
+
+
 def build_library(force: bool = False, verbose: bool = False) -> str:
     deps = [os.path.join(CSRC, d) for d in DEPS]
     if force or _stale(LIB, deps):
@@ -31,6 +35,19 @@ def build_library(force: bool = False, verbose: bool = False) -> str:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
     return LIB
+
+
+def build_capi_consumer(force: bool = False, verbose: bool = False) -> str:
+    """The compiled C++ consumer of include/orbfe.h (tests/native/capi_frontend.cpp), linked against the
+    in-tree liborbfe.so by name with an $ORIGIN-relative runpath so it runs from the GPU box's copy."""
+    if force or _stale(CAPI_BIN, [CAPI_SRC, LIB]):
+        cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-I", os.path.join(os.path.dirname(_HERE), "include"),
+               "-o", CAPI_BIN, CAPI_SRC, "-L", _HERE, "-lorbfe", "-Wl,-rpath,$ORIGIN/../../orb_slam3_ros_amd",
+               "-Wl,-rpath-link,/opt/rocm/lib"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+    return CAPI_BIN
 
 
 if __name__ == "__main__":

@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) void k_remap(const uint8_t* const* __restrict_
 #pragma unroll
     for (int q = 0; q < 4; q++) r[q] = remap_setup(sw, sh, sstride, mx[q], my[q]);
     // the fast path's window: base = off_0 & ~3 (4-byte aligned when the sources' rows are), every
-    // pixel's pair at d = off - base in [0, 6], and the window's columns inside the row pitch
+    // pixel's pair at d = off - base in [0, 6], and the window's columns inside the row
     const int base = r[0].off & ~3;
     bool fast = src_al && full;
     uint32_t sel[4];
@@ -128,7 +128,8 @@ __global__ __launch_bounds__(256) void k_remap(const uint8_t* const* __restrict_
         fast = fast && (r[q].inside & 15u) == 15u && d >= 0 && d <= 6;
         sel[q] = 0x0c000c00u | (uint32_t)(d & 7) | ((uint32_t)((d + 1) & 7) << 16);
     }
-    fast = fast && (base - (r[0].off - (r[0].off % sstride))) + 8 <= sstride;
+    // (inside the image width, not the pitch: the last row of a pitched buffer may end at sw)
+    fast = fast && (base - (r[0].off - (r[0].off % sstride))) + 8 <= sw;
     const int i0 = grp * RM_IPB, i1 = min(i0 + RM_IPB, n);
     // the fast path's two 8-byte windows of image img, as one dwordx2 load each (4-byte aligned:
     // the hardware's unaligned global access). Every lane loads (the others from offset 0, never
@@ -248,34 +249,51 @@ int orbfe_remap_linear_batch(const uint8_t* const* d_src, int sw, int sh, int ss
         sstride < sw || dstride < dw)
         return n == 0 ? ORBFE_OK : ORBFE_E_ARG;
     if ((size_t)sw * sh == 0) return ORBFE_E_EMPTY;
-    // the pointer tables live in a per-thread device cache, re-uploaded only when the caller's
-    // pointers change (a rectification loop passes the same buffers every frame); the upload is
-    // ordered on s before the launch, and the previous launch that read the table was ordered on
-    // the stream it ran on, so a changed table first waits for the device to drain
-    struct RemapTables {
-        std::vector<const void*> host;
+    // the pointer tables live in a small per-thread ring of device tables keyed by the caller's
+    // pointers (a rectification loop passes the same buffers every frame, a double-buffered one
+    // alternates two sets): a hit launches without any upload; a miss takes the least recently
+    // used slot, waits only for the last launch that read it (its event), refills its pinned
+    // staging and uploads it asynchronously on s ahead of the launch
+    struct RemapSlot {
+        std::vector<const void*> key;
         void** dev = nullptr;
+        void** pinned = nullptr;
         size_t cap = 0;
+        hipEvent_t done = nullptr;
+        uint64_t used = 0;
     };
-    static thread_local RemapTables rt;
-    const bool same = rt.dev && rt.host.size() == (size_t)2 * n &&
-                      std::equal(d_src, d_src + n, rt.host.begin()) && std::equal(d_dst, d_dst + n, rt.host.begin() + n);
+    static thread_local RemapSlot ring[4];
+    static thread_local uint64_t tick = 0;
     hipStream_t s = (hipStream_t)stream;
-    if (!same) {
-        HIPCHK(hipDeviceSynchronize());
-        if (rt.cap < (size_t)2 * n) {
-            if (rt.dev) HIPCHK(hipFree(rt.dev));
-            rt.dev = nullptr;
-            rt.cap = 0;
-            HIPCHK(hipMalloc((void**)&rt.dev, (size_t)2 * n * sizeof(void*)));
-            rt.cap = (size_t)2 * n;
+    RemapSlot* slot = nullptr;
+    for (RemapSlot& r : ring)
+        if (r.dev && r.key.size() == (size_t)2 * n && std::equal(d_src, d_src + n, r.key.begin()) &&
+            std::equal(d_dst, d_dst + n, r.key.begin() + n))
+            slot = &r;
+    if (!slot) {
+        slot = &ring[0];
+        for (RemapSlot& r : ring)
+            if (r.used < slot->used) slot = &r;
+        if (slot->done) HIPCHK(hipEventSynchronize(slot->done));
+        else HIPCHK(hipEventCreateWithFlags(&slot->done, hipEventDisableTiming));
+        slot->key.clear();
+        if (slot->cap < (size_t)2 * n) {
+            if (slot->dev) HIPCHK(hipFree(slot->dev));
+            if (slot->pinned) HIPCHK(hipHostFree(slot->pinned));
+            slot->dev = slot->pinned = nullptr;
+            slot->cap = 0;
+            HIPCHK(hipMalloc((void**)&slot->dev, (size_t)2 * n * sizeof(void*)));
+            HIPCHK(hipHostMalloc((void**)&slot->pinned, (size_t)2 * n * sizeof(void*), hipHostMallocDefault));
+            slot->cap = (size_t)2 * n;
         }
-        rt.host.assign(d_src, d_src + n);
-        rt.host.insert(rt.host.end(), d_dst, d_dst + n);
-        HIPCHK(hipMemcpy(rt.dev, rt.host.data(), (size_t)2 * n * sizeof(void*), hipMemcpyHostToDevice));
+        slot->key.assign(d_src, d_src + n);
+        slot->key.insert(slot->key.end(), d_dst, d_dst + n);
+        memcpy(slot->pinned, slot->key.data(), (size_t)2 * n * sizeof(void*));
+        HIPCHK(hipMemcpyAsync(slot->dev, slot->pinned, (size_t)2 * n * sizeof(void*), hipMemcpyHostToDevice, s));
     }
-    const uint8_t* const* dsrc = (const uint8_t* const*)rt.dev;
-    uint8_t* const* ddst = (uint8_t* const*)(rt.dev + n);
+    slot->used = ++tick;
+    const uint8_t* const* dsrc = (const uint8_t* const*)slot->dev;
+    uint8_t* const* ddst = (uint8_t* const*)(slot->dev + n);
     const int ng = (dw + 3) >> 2;
     // the fast path's dword loads need 4-byte aligned source rows
     bool al = (sstride & 3) == 0 && (size_t)sstride * (size_t)(sh - 1) + (size_t)sw >= 16;
@@ -284,6 +302,7 @@ int orbfe_remap_linear_batch(const uint8_t* const* d_src, int sw, int sh, int ss
     hipLaunchKernelGGL(k_remap, grid, dim3(256), 0, s, dsrc, sw, sh,
                        sstride, d_mapx, d_mapy, dw, dh, ddst, dstride, n, al ? 1 : 0);
     HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(slot->done, s));
     return ORBFE_OK;
 }
 

@@ -1,0 +1,245 @@
+// A compiled C++ consumer of the C-ABI (include/orbfe.h only, linked against liborbfe.so): the call
+// sequence the drop-in shims make (shim/ORBextractor_orbfe.cc, shim/ORBmatcher_orbfe.cc), on plain
+// C++ stand-ins for the ORB-SLAM3 objects because OpenCV / Eigen are absent here:
+//   ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST) + getters   ORBextractor.cc:409-469
+//   ORBextractor::operator()(image, mask, keys, desc, vLappingArea)                  ORBextractor.cc:1086-1168
+//   Frame::Frame(stereo): two operator() calls, then ComputeStereoMatches             Frame.cc:101-197, 811-981
+//   ORBmatcher(0.8).SearchByProjection(F, vpMapPoints, th) through a MapPoint* <-> handle table
+//                                                                                     ORBmatcher.cc:43-213
+// usage: capi_frontend <job.bin> <out.bin>
+//   job: int32 w, h, nfeatures, n_mps, th_x100; float bf, fx; u8 left[w*h], u8 right[w*h]
+//   out: per side {int32 monoIndex, n; keypoints n x 28 B; descriptors n x 32 B}; int32 levels;
+//        float scale[levels]; stereo {int32 nmatch; float uR[nL]; float depth[nL]};
+//        map points {n_mps x orbfe_map_point}; int32 nmatches; int32 mvp[nL] (map point ids, -1)
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "orbfe.h"
+
+namespace {
+
+struct KeyPoint {   // cv::KeyPoint
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+};
+static_assert(sizeof(KeyPoint) == sizeof(orbfe_keypoint), "cv::KeyPoint layout (28 B)");
+
+void check(int rc, const char* what) {
+    if (rc < 0 && rc != ORBFE_E_EMPTY) throw std::runtime_error(std::string(what) + " failed: " + std::to_string(rc));
+}
+
+// ORB_SLAM3::ORBextractor as the shim implements it
+class ORBextractor {
+public:
+    ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST) : nlevels_(nlevels) {
+        check(orbfe_extractor_create(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, &h_), "create");
+        mvScaleFactor.resize(nlevels);
+        mvInvScaleFactor.resize(nlevels);
+        mvLevelSigma2.resize(nlevels);
+        mvInvLevelSigma2.resize(nlevels);
+        check(orbfe_extractor_scale_info(h_, mvScaleFactor.data(), mvInvScaleFactor.data(), mvLevelSigma2.data(),
+                                         mvInvLevelSigma2.data(), nullptr),
+              "scale_info");
+    }
+    ~ORBextractor() { orbfe_extractor_destroy(h_); }
+    int operator()(const uint8_t* img, int w, int h, int step, std::vector<KeyPoint>& keys, std::vector<uint8_t>& desc,
+                   const int lap[2]) {
+        const int cap = orbfe_extractor_capacity(h_, w, h);
+        check(cap, "capacity");
+        keys.resize(cap);
+        desc.resize((size_t)cap * 32);
+        int n = 0;
+        const int mono = orbfe_extract(h_, img, w, h, step, lap[0], lap[1], reinterpret_cast<orbfe_keypoint*>(keys.data()),
+                                       desc.data(), cap, &n);
+        if (mono == ORBFE_E_EMPTY) { keys.clear(); desc.clear(); return -1; }
+        check(mono, "extract");
+        keys.resize(n);
+        desc.resize((size_t)n * 32);
+        return mono;
+    }
+    int GetLevels() const { return nlevels_; }
+    orbfe_extractor* handle() const { return h_; }
+    std::vector<float> mvScaleFactor, mvInvScaleFactor, mvLevelSigma2, mvInvLevelSigma2;
+
+private:
+    orbfe_extractor* h_ = nullptr;
+    int nlevels_;
+};
+
+struct MapPoint {   // the tracking fields SearchByProjection reads (MapPoint.h:172-180)
+    float mTrackProjX, mTrackProjY, mTrackProjXR, mTrackViewCos, mTrackDepth;
+    int mnTrackScaleLevel;
+    bool mbTrackInView, bad;
+    int observations;
+    int32_t mnId;
+    uint8_t desc[32];
+};
+
+struct Frame {   // Frame(stereo): Frame.cc:101-197
+    std::vector<KeyPoint> mvKeys, mvKeysRight;
+    std::vector<uint8_t> mDescriptors, mDescriptorsRight;
+    std::vector<float> mvuRight, mvDepth;
+    std::vector<MapPoint*> mvpMapPoints;
+    int monoLeft = 0, monoRight = 0, nStereo = 0;
+    float mnMinX = 0, mnMaxX = 0, mnMinY = 0, mnMaxY = 0, mbf, mfx;
+    ORBextractor *left, *right;
+    Frame(const uint8_t* L, const uint8_t* R, int w, int h, ORBextractor* el, ORBextractor* er, float bf, float fx)
+        : mbf(bf), mfx(fx), left(el), right(er) {
+        const int lap[2] = {0, 0};
+        monoLeft = (*left)(L, w, h, w, mvKeys, mDescriptors, lap);    // ExtractORB(0, ...)
+        monoRight = (*right)(R, w, h, w, mvKeysRight, mDescriptorsRight, lap);   // ExtractORB(1, ...)
+        const int N = (int)mvKeys.size();
+        mvuRight.assign(N, -1.f);
+        mvDepth.assign(N, -1.f);
+        // ComputeStereoMatches through the library (the shim's Frame reroute, kOrbfeStereoRerouted)
+        nStereo = orbfe_stereo_match(left->handle(), right->handle(), bf, fx, mvuRight.data(), mvDepth.data());
+        check(nStereo, "stereo_match");
+        mvpMapPoints.assign(N, nullptr);
+        mnMaxX = (float)w;   // ComputeImageBounds without distortion
+        mnMaxY = (float)h;
+    }
+};
+
+// MapPoint* <-> int32 handle table of shim/ORBmatcher_orbfe.cc
+struct Handles {
+    std::vector<MapPoint*> table;
+    std::unordered_map<MapPoint*, int32_t> id;
+    int32_t of(MapPoint* p) {
+        if (!p) return -1;
+        auto it = id.find(p);
+        if (it != id.end()) return it->second;
+        const int32_t h = (int32_t)table.size();
+        table.push_back(p);
+        id.emplace(p, h);
+        return h;
+    }
+    MapPoint* at(int32_t h) const { return h < 0 ? nullptr : table[h]; }
+};
+
+// ORBmatcher(nnratio).SearchByProjection(F, vpMapPoints, th, bFarPoints, thFarPoints) as the shim does it
+int SearchByProjection(Frame& F, const std::vector<MapPoint*>& vpMapPoints, float th, float nnratio,
+                       std::vector<orbfe_map_point>& q_out) {
+    Handles H;
+    const int N = (int)F.mvKeys.size();
+    std::vector<int32_t> mvp(N), obs(N);
+    for (int i = 0; i < N; i++) {
+        mvp[i] = H.of(F.mvpMapPoints[i]);
+        obs[i] = F.mvpMapPoints[i] ? F.mvpMapPoints[i]->observations : 0;
+    }
+    std::vector<orbfe_map_point> q(vpMapPoints.size());
+    for (size_t i = 0; i < vpMapPoints.size(); i++) {
+        const MapPoint* p = vpMapPoints[i];
+        orbfe_map_point& r = q[i];
+        memset(&r, 0, sizeof(r));
+        r.proj_x = p->mTrackProjX; r.proj_y = p->mTrackProjY; r.proj_xr = p->mTrackProjXR;
+        r.view_cos = p->mTrackViewCos; r.depth = p->mTrackDepth; r.scale_level = p->mnTrackScaleLevel;
+        r.flags = (p->mbTrackInView ? ORBFE_MP_IN_VIEW : 0) | (p->bad ? ORBFE_MP_BAD : 0);
+        r.observations = p->observations;
+        r.id = H.of(const_cast<MapPoint*>(p));
+        r.scale_level_r = -1;
+        if (p->mbTrackInView && !p->bad) memcpy(r.desc, p->desc, 32);
+    }
+    orbfe_frame fr;
+    memset(&fr, 0, sizeof(fr));
+    fr.n = N;
+    fr.keys = reinterpret_cast<const orbfe_keypoint*>(F.mvKeys.data());
+    fr.desc = F.mDescriptors.data();
+    fr.uright = F.mvuRight.data();
+    fr.min_x = F.mnMinX; fr.max_x = F.mnMaxX; fr.min_y = F.mnMinY; fr.max_y = F.mnMaxY;
+    fr.nlevels = F.left->GetLevels();
+    fr.scale_factors = F.left->mvScaleFactor.data();
+    fr.mbf = F.mbf;
+    const int n = orbfe_search_by_projection_local(&fr, mvp.data(), obs.data(), q.data(), (int)q.size(), th, 0, 0.f,
+                                                   nnratio);
+    check(n, "search_by_projection_local");
+    for (int i = 0; i < N; i++) F.mvpMapPoints[i] = H.at(mvp[i]);
+    // the records with the caller's map point ids (not the call's handles) for the checker
+    for (size_t i = 0; i < q.size(); i++) q[i].id = vpMapPoints[i]->mnId;
+    q_out = q;
+    return n;
+}
+
+struct Lcg {   // deterministic map points without <random>'s implementation-defined distributions
+    uint64_t s;
+    uint32_t next() { s = s * 6364136223846793005ull + 1442695040888963407ull; return (uint32_t)(s >> 33); }
+    float unit() { return (next() & 0xFFFFFF) / 16777216.0f; }
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc != 3) { fprintf(stderr, "usage: capi_frontend job.bin out.bin\n"); return 2; }
+    try {
+        FILE* f = fopen(argv[1], "rb");
+        if (!f) throw std::runtime_error("cannot open job");
+        int32_t hdr[5];
+        float cam[2];
+        if (fread(hdr, 4, 5, f) != 5 || fread(cam, 4, 2, f) != 2) throw std::runtime_error("short job header");
+        const int w = hdr[0], h = hdr[1], nf = hdr[2], n_mps = hdr[3];
+        const float th = hdr[4] / 100.f;
+        std::vector<uint8_t> L((size_t)w * h), R((size_t)w * h);
+        if (fread(L.data(), 1, L.size(), f) != L.size() || fread(R.data(), 1, R.size(), f) != R.size())
+            throw std::runtime_error("short job images");
+        fclose(f);
+        ORBextractor el(nf, 1.2f, 8, 20, 7), er(nf, 1.2f, 8, 20, 7);   // mpORBextractorLeft / Right
+        Frame F(L.data(), R.data(), w, h, &el, &er, cam[0], cam[1]);
+        // local map: noisy copies of the frame's own keypoints (as Tracking would project them)
+        Lcg rng{12345};
+        std::vector<MapPoint> pts(n_mps);
+        std::vector<MapPoint*> vp(n_mps);
+        const int N = (int)F.mvKeys.size();
+        for (int i = 0; i < n_mps; i++) {
+            MapPoint& p = pts[i];
+            const int k = (int)(rng.next() % (uint32_t)N);
+            const KeyPoint& kp = F.mvKeys[k];
+            p.mTrackProjX = kp.x + (rng.unit() - 0.5f) * 2.f;
+            p.mTrackProjY = kp.y + (rng.unit() - 0.5f) * 2.f;
+            p.mTrackProjXR = F.mvuRight[k] >= 0 ? F.mvuRight[k] + (rng.unit() - 0.5f) : p.mTrackProjX - 20.f * rng.unit();
+            p.mTrackViewCos = 0.99f + 0.01f * rng.unit();
+            p.mTrackDepth = 1.f + 10.f * rng.unit();
+            p.mnTrackScaleLevel = kp.octave;
+            p.mbTrackInView = (rng.next() % 10) != 0;
+            p.bad = (rng.next() % 50) == 0;
+            p.observations = (int)(rng.next() % 5);
+            p.mnId = 1000 + i;
+            memcpy(p.desc, F.mDescriptors.data() + (size_t)k * 32, 32);
+            for (int b = 0; b < 12; b++) {
+                const uint32_t bit = rng.next() % 256;
+                p.desc[bit >> 3] ^= (uint8_t)(1u << (bit & 7));
+            }
+            vp[i] = &p;
+        }
+        std::vector<orbfe_map_point> q;
+        const int nmatches = SearchByProjection(F, vp, th, 0.8f, q);
+        FILE* o = fopen(argv[2], "wb");
+        if (!o) throw std::runtime_error("cannot open out");
+        auto w32 = [&](int32_t v) { fwrite(&v, 4, 1, o); };
+        for (int side = 0; side < 2; side++) {
+            const std::vector<KeyPoint>& k = side ? F.mvKeysRight : F.mvKeys;
+            const std::vector<uint8_t>& d = side ? F.mDescriptorsRight : F.mDescriptors;
+            w32(side ? F.monoRight : F.monoLeft);
+            w32((int32_t)k.size());
+            fwrite(k.data(), sizeof(KeyPoint), k.size(), o);
+            fwrite(d.data(), 1, d.size(), o);
+        }
+        w32(el.GetLevels());
+        fwrite(el.mvScaleFactor.data(), 4, el.mvScaleFactor.size(), o);
+        w32(F.nStereo);
+        fwrite(F.mvuRight.data(), 4, F.mvuRight.size(), o);
+        fwrite(F.mvDepth.data(), 4, F.mvDepth.size(), o);
+        fwrite(q.data(), sizeof(orbfe_map_point), q.size(), o);
+        w32(nmatches);
+        for (MapPoint* p : F.mvpMapPoints) w32(p ? p->mnId : -1);
+        fclose(o);
+    } catch (const std::exception& e) {
+        fprintf(stderr, "capi_frontend: %s\n", e.what());
+        return 1;
+    }
+    return 0;
+}

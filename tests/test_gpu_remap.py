@@ -86,3 +86,44 @@ def test_undistort_points(gpu, oracle_lib, dist):
     g = undistort_points(pts, K, np.array(dist, np.float32))
     o = oracle_lib.undistort_points(pts, K, np.array(dist, np.float32))
     np.testing.assert_array_equal(g.view(np.uint32), o.view(np.uint32))
+
+
+def test_remap_batch_alternating_buffer_sets(gpu, oracle_lib):
+    """The device pointer-table ring (4 slots keyed by the pointers): two double-buffered sets
+    alternated without host syncs, then six sets (more than the ring holds) cycled, each launch
+    checked against the oracle; tables re-uploaded asynchronously must never be read stale."""
+    import torch
+    w, h, n = 160, 120, 3
+    mx, my = rectify_maps(w, h, 150.0, 150.0, 80.0, 60.0, (-0.2, 0.05, 1e-4, 1e-5), R=_rot(2.0))
+    dmx, dmy = torch.from_numpy(mx).cuda(), torch.from_numpy(my).cuda()
+    imgs = [np.stack([synth_image(100 * k + i, w, h) for i in range(n)]) for k in range(6)]
+    want = [[oracle_lib.remap_linear(imgs[k][i], mx, my) for i in range(n)] for k in range(6)]
+    srcs = [torch.from_numpy(im).cuda() for im in imgs]
+    for order in ([0, 1] * 4, [0, 1, 2, 3, 4, 5, 0, 5, 1, 4, 2, 3]):
+        outs = []
+        for k in order:   # each launch writes a fresh output: every result stays checkable
+            out = torch.zeros((n, h, w), dtype=torch.uint8, device="cuda")
+            remap_linear_batch(srcs[k], dmx, dmy, out)
+            outs.append((k, out))
+        torch.cuda.synchronize()
+        for k, out in outs:
+            got = out.cpu().numpy()
+            for i in range(n):
+                np.testing.assert_array_equal(got[i], want[k][i])
+
+
+def test_remap_batch_pitched_source(gpu, oracle_lib):
+    """Sources with a row pitch above the width (padding filled with 255) and a buffer that ends at
+    the last row's width: the fast path's window stays inside the image columns."""
+    import torch
+    w, h, pitch, n = 200, 90, 256, 2
+    mx, my = rectify_maps(w, h, 180.0, 180.0, 100.0, 45.0, (-0.25, 0.06, 2e-4, -1e-4), R=_rot(-2.0))
+    imgs = np.stack([synth_image(7 + i, w, h) for i in range(n)])
+    flat = torch.full((n * h * pitch - (pitch - w),), 255, dtype=torch.uint8, device="cuda")
+    src = flat.as_strided((n, h, w), (h * pitch, pitch, 1))
+    src.copy_(torch.from_numpy(imgs).cuda())
+    out = torch.zeros((n, h, w), dtype=torch.uint8, device="cuda")
+    remap_linear_batch(src, torch.from_numpy(mx).cuda(), torch.from_numpy(my).cuda(), out)
+    torch.cuda.synchronize()
+    for i in range(n):
+        np.testing.assert_array_equal(out[i].cpu().numpy(), oracle_lib.remap_linear(imgs[i], mx, my))
