@@ -357,7 +357,9 @@ def matcher_config5(steps):
         lib.orbfe_matcher_set_timing(0)
         dms = float(np.mean(dev))
         # device-resident call (records, slots and frame already in HBM): wall time per call, which
-        # includes its single host round trip (the ordered passes converge on the device)
+        # includes its single host round trip (the ordered passes converge on the device); timed at
+        # the C-ABI (the drop-in boundary: arguments prepared, as a C++ caller holds them) and
+        # through the Python wrapper (its argument checks and stream lookup added)
         mvp_t = [torch.from_numpy(mvp0.copy()).to(dev_t) for _ in range(steps + 2)]
         for b in mvp_t[:2]:
             search_by_projection_local_device(Fd, b, obs_t, mps_t, th)
@@ -366,6 +368,19 @@ def matcher_config5(steps):
         for b in mvp_t[2:]:
             nd = search_by_projection_local_device(Fd, b, obs_t, mps_t, th)
         torch.cuda.synchronize()
+        wdt = (time.perf_counter() - t0) / steps
+        assert nd == n
+        st = torch.cuda.current_stream(dev_t).cuda_stream
+        args = [(Fd.ref(), b.data_ptr(), obs_t.data_ptr(), mps_t.data_ptr(), len(mps), float(th), 0, 50.0, 0.8, st)
+                for b in mvp_t[2:]]
+        for b in mvp_t[2:]:
+            b.copy_(mvp_t[0].new_tensor(mvp0))
+        torch.cuda.synchronize()
+        fn = lib.orbfe_search_by_projection_local_device
+        t0 = time.perf_counter()
+        for a in args:
+            nd = fn(*a)
+        torch.cuda.synchronize()
         rdt = (time.perf_counter() - t0) / steps
         assert nd == n
         out[f"th{th}"] = {"ms_per_call": round(dt * 1e3, 4), "calls_per_s": round(1.0 / dt, 2),
@@ -373,7 +388,9 @@ def matcher_config5(steps):
                           "device_queries_per_s": round(len(mps) / (dms * 1e-3), 1),
                           "resident_ms_per_call": round(rdt * 1e3, 4),
                           "resident_queries_per_s": round(len(mps) / rdt, 1),
-                          "resident_over_device": round(rdt * 1e3 / dms, 4), "nmatches": int(n)}
+                          "resident_over_device": round(rdt * 1e3 / dms, 4),
+                          "resident_wrapper_ms_per_call": round(wdt * 1e3, 4),
+                          "resident_wrapper_over_device": round(wdt * 1e3 / dms, 4), "nmatches": int(n)}
     # Tracking::SearchLocalPoints' projection (isInFrustum + PredictScale) fused with the
     # th=1 search, 100k world points, device time (HIP events)
     from orb_slam3_ros_amd.matcher import search_local_points
@@ -392,8 +409,9 @@ def matcher_config5(steps):
                         "flips) vs 1000-keypoint stereo frame, nnratio 0.8, seed 12345",
             "timing": "ms_per_call: host C-ABI call incl. 8 MB record upload and result download; "
                       "device_ms_per_call: kernels only (grid build, ordered passes, commit), HIP events; "
-                      "resident_ms_per_call: orbfe_search_by_projection_local_device wall time with the "
-                      "records, slots and frame already in HBM",
+                      "resident_ms_per_call: orbfe_search_by_projection_local_device wall time at the "
+                      "C-ABI (ctypes, arguments prepared) with the records, slots and frame already in HBM; "
+                      "resident_wrapper_ms_per_call: the same through the Python wrapper",
             "per_th": out}
 
 
@@ -487,7 +505,7 @@ def main():
     ap.add_argument("--parity-frames", type=int, default=0, help="frames checked after timing (0: the whole batch)")
     ap.add_argument("--no-side-configs", action="store_true", help="skip the config 3 / config 4 legs")
     ap.add_argument("--stage-steps", type=int, default=10, help="extra steps with per-stage HIP events")
-    ap.add_argument("--matcher-steps", type=int, default=10, help="config-5 SearchByProjection calls per th (0: skip)")
+    ap.add_argument("--matcher-steps", type=int, default=50, help="config-5 SearchByProjection calls per th (0: skip)")
     ap.add_argument("--rectify-steps", type=int, default=5,
                     help="time cv::remap rectification of the step's images (reported separately; 0: skip)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],

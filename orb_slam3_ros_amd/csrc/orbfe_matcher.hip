@@ -83,25 +83,78 @@ __device__ __forceinline__ void mt_for_area(const FrameDev& fr, const int* cs, c
     }
 }
 
+// Every per-search initialisation of sbp_run, run by the extra blocks of the grid launch (each used
+// to be its own fill / memset / kernel call): initial blocked flags of a device-resident search
+// (b0d != nullptr), the pass states of the all -1 assignment, the assignment, the change flags, the
+// rotation histogram and the commit result (resb[0] = change-flag copy, resb[1..2] = counts,
+// resb[3 + k] = -1). n == 0 and nassign == 0 with null pointers: nothing to initialise.
+#define MT_MAX_PASSES 4096
+struct SbpInit {
+    const int32_t* mvp;
+    const int32_t* obs;
+    int any_slot;
+    int* b0d;
+    int* fb0;
+    int* fb1;
+    int* assign;
+    int nassign;
+    int* changed;
+    int* hist;
+    int* resb;
+    int n;
+};
+__device__ __forceinline__ void sbp_init_elem(const SbpInit& a, int k) {
+    if (k < a.n) {
+        if (a.b0d) a.b0d[k] = a.any_slot ? (a.mvp[k] >= 0) : (a.mvp[k] >= 0 && a.obs[k] > 0);
+        a.fb0[k] = MT_INF;
+        a.fb1[k] = MT_INF;
+    }
+    if (k < a.nassign) a.assign[k] = -1;
+    if (a.changed && k < MT_MAX_PASSES) a.changed[k] = 0;
+    if (a.hist && k < MT_HISTO + 1) a.hist[k] = 0;   // + the commit's block-completion counter
+    if (a.resb && k < a.n + 3) a.resb[k] = k < 3 ? 0 : -1;
+}
+inline int sbp_init_extent(const SbpInit& a) {
+    return a.resb ? std::max(std::max(a.n + 3, a.nassign), MT_MAX_PASSES) : 0;
+}
+
 // AssignFeaturesToGrid (Frame.cc:385-416): stable (cell, index) order via a bitonic sort of
-// (cell << 16 | index) keys in LDS. One block per frame, n <= MT_GRID_MAXN. Two-camera frames
-// (nleft >= 0): rows >= nleft go to the right grid, cells MT_NCELL.. (Frame.cc:408-411).
+// (cell << 16 | index) keys (unique, so any sorting network gives the same order). One block per
+// grid, n <= MT_GRID_MAXN; each thread holds the keys i = tid + 1024 r in registers: the
+// compare-exchange stages with partner distance j < 64 stay inside a wave (lane shuffles, no
+// barrier) and only the j >= 64 stages go through LDS (14 barriers at P = 1024 instead of 55).
+// Two-camera frames (nleft >= 0): rows >= nleft go to the right grid, cells MT_NCELL..
+// (Frame.cc:408-411). Blocks >= ngrids run the search initialisation (SbpInit) instead.
 #define MT_GRID_MAXN 8192
+#define MT_GRID_R (MT_GRID_MAXN / 1024)
+__device__ __forceinline__ uint32_t bitonic_keep(uint32_t a, uint32_t c, int i, int j, int k) {
+    const bool keep_min = ((i & j) == 0) == ((i & k) == 0);   // lower of the pair == ascending
+    return keep_min ? min(a, c) : max(a, c);
+}
 __global__ __launch_bounds__(1024) void k_mt_grid(const OrbKeyPoint* keys, int n, int nleft, float minx, float miny,
                                                   float invw, float invh, int* cstart, int* cidx, int gstride_c,
-                                                  int gstride_i) {
+                                                  int gstride_i, int ngrids, SbpInit ia) {
     __shared__ uint32_t s_k[MT_GRID_MAXN];
-    // block 0: full grid; block g >= 1: keypoints with octave in [g-2, g-1] (level-(g-1) candidates)
     const int gi = blockIdx.x;
+    const int tid = threadIdx.x;
+    if (gi >= ngrids) {
+        sbp_init_elem(ia, (gi - ngrids) * blockDim.x + tid);
+        return;
+    }
+    // block 0: full grid; block g >= 1: keypoints with octave in [g-2, g-1] (level-(g-1) candidates)
     const int lvlo = gi == 0 ? INT_MIN : gi - 2, lvhi = gi == 0 ? INT_MAX : gi - 1;
     cstart += (size_t)gi * gstride_c;
     cidx += (size_t)gi * gstride_i;
-    int P = 1;
+    int P = 64;
     while (P < n) P <<= 1;
+    const int R = (P + 1023) >> 10;
     const int ncells = nleft >= 0 ? 2 * MT_NCELL : MT_NCELL;
-    for (int i = threadIdx.x; i < P; i += blockDim.x) {
+    uint32_t v[MT_GRID_R];
+#pragma unroll
+    for (int r = 0; r < MT_GRID_R; r++) {
+        const int i = tid + (r << 10);
         uint32_t key = 0xFFFFFFFFu;
-        if (i < n) {
+        if (r < R && i < n) {
             const OrbKeyPoint kp = keys[i];
             const int px = (int)roundf((kp.x - minx) * invw);
             const int py = (int)roundf((kp.y - miny) * invh);
@@ -111,12 +164,24 @@ __global__ __launch_bounds__(1024) void k_mt_grid(const OrbKeyPoint* keys, int n
                 cell = (uint32_t)(px * ORBFE_GRID_ROWS + py + (nleft >= 0 && i >= nleft ? MT_NCELL : 0));
             key = (cell << 16) | (uint32_t)i;
         }
-        s_k[i] = key;
+        v[r] = key;
     }
-    SYNC();
-    for (int k = 2; k <= P; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < P; i += blockDim.x) {
+    // the intra-wave stages j = min(k/2, 32) .. 1 of one k, on registers (elements >= P pair only
+    // among themselves: j < P keeps i ^ j on the same side of P)
+    auto wave_stages = [&](int k) {
+        for (int j = min(k >> 1, 32); j > 0; j >>= 1)
+#pragma unroll
+            for (int r = 0; r < MT_GRID_R; r++)
+                if (r < R) v[r] = bitonic_keep(v[r], (uint32_t)__shfl_xor((int)v[r], j), tid + (r << 10), j, k);
+    };
+    for (int k = 2; k <= 64; k <<= 1) wave_stages(k);
+    for (int k = 128; k <= P; k <<= 1) {
+#pragma unroll
+        for (int r = 0; r < MT_GRID_R; r++)
+            if (r < R) s_k[tid + (r << 10)] = v[r];
+        SYNC();
+        for (int j = k >> 1; j >= 64; j >>= 1) {
+            for (int i = tid; i < P; i += blockDim.x) {
                 const int ixj = i ^ j;
                 if (ixj > i) {
                     const uint32_t a = s_k[i], c = s_k[ixj];
@@ -125,8 +190,18 @@ __global__ __launch_bounds__(1024) void k_mt_grid(const OrbKeyPoint* keys, int n
             }
             SYNC();
         }
-    for (int i = threadIdx.x; i < n; i += blockDim.x) cidx[i] = (int)(s_k[i] & 0xFFFFu);
-    for (int c = threadIdx.x; c <= ncells; c += blockDim.x) {
+#pragma unroll
+        for (int r = 0; r < MT_GRID_R; r++)
+            if (r < R) v[r] = s_k[tid + (r << 10)];
+        wave_stages(k);
+        SYNC();   // every wave has read s_k before the next k (or the final copy) overwrites it
+    }
+#pragma unroll
+    for (int r = 0; r < MT_GRID_R; r++)
+        if (r < R) s_k[tid + (r << 10)] = v[r];
+    SYNC();
+    for (int i = tid; i < n; i += blockDim.x) cidx[i] = (int)(s_k[i] & 0xFFFFu);
+    for (int c = tid; c <= ncells; c += blockDim.x) {
         int lo = 0, hi = n;   // first position with cell >= c
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
@@ -805,16 +880,47 @@ __global__ __launch_bounds__(MT_NT) void k_mt_commit_drop(const OrbKeyPoint* key
     if ((threadIdx.x & 63) == 0 && m) atomicAdd(&result[1], __popcll(m));
 }
 
+// Status publication (st_host != nullptr): pinned host words {gate value, assigned count, dropped
+// count, passes needed, sequence number}; the last block to finish (done counter) stores them after
+// every block's slot writes, at system scope, the sequence number last, so a host that sees the
+// sequence number sees complete results. changed / npass: the pass change flags of this launch
+// batch (passes needed = first pass that changed nothing, + 1).
+struct CommitStatus {
+    int* st_host;
+    int* done;
+    const int* changed;
+    int npass;
+    int seq;
+};
 __global__ void k_mt_commit_write(int n, const int* qid, int q_stride_bytes, const int* result, int* mvp, int W,
-                                  const int* gate = nullptr, int* ch_out = nullptr) {
+                                  const int* gate = nullptr, int* ch_out = nullptr, CommitStatus cs = CommitStatus{}) {
     // ch_out (result[-1]): the gate's value, so one host read brings the change flag and the counts
-    if (ch_out && blockIdx.x == 0 && threadIdx.x == 0) *ch_out = gate ? *gate : 0;
-    if (gate && *gate != 0) return;
+    const int g = gate ? *gate : 0;
+    if (ch_out && blockIdx.x == 0 && threadIdx.x == 0) *ch_out = g;
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    const int w = result[2 + k];
-    if (w == -2) mvp[k] = -1;
-    else if (w >= 0) mvp[k] = *(const int*)((const uint8_t*)qid + (size_t)(w / W) * q_stride_bytes);
+    if (g == 0 && k < n) {
+        const int w = result[2 + k];
+        if (w == -2) mvp[k] = -1;
+        else if (w >= 0) mvp[k] = *(const int*)((const uint8_t*)qid + (size_t)(w / W) * q_stride_bytes);
+    }
+    if (!cs.st_host) return;
+    __threadfence_system();   // this thread's slot write, before the block is counted done
+    __syncthreads();
+    if (threadIdx.x == 0 && atomicAdd(cs.done, 1) == (int)gridDim.x - 1) {
+        __threadfence_system();
+        int need = cs.npass;
+        for (int p = 0; p < cs.npass; p++)
+            if (cs.changed[p] == 0) { need = p + 1; break; }
+        volatile int* st = cs.st_host;
+        st[0] = g;
+        st[1] = result[0];
+        st[2] = result[1];
+        st[3] = need;
+        __threadfence_system();
+        st[4] = cs.seq;
+        __threadfence_system();
+        *cs.done = 0;   // every block has counted: ready for the next batch's commit
+    }
 }
 
 // ---- SearchForInitialization (ORBmatcher.cc:648-763) ----
@@ -1124,6 +1230,9 @@ struct MatchScratch {
     uint8_t* h = nullptr;   // pinned
     size_t hcap = 0;
     int* hs = nullptr;      // pinned status words read back at the end of a call
+    int* hs_dev = nullptr;  // hs as the device addresses it (kernels store the status there)
+    int seq = 0;            // sequence number of the last published status
+    int pass_hint[3] = {4, 4, 4};   // passes the previous single-camera search of each mode needed
     // Deliberately never freed: thread_local destructors of the main thread can run after the HIP
     // runtime has been torn down at exit; the arena is reused for the thread's lifetime.
 };
@@ -1136,14 +1245,15 @@ thread_local float t_last_ms = -1.f;
 thread_local hipEvent_t t_ev[2] = {nullptr, nullptr};
 struct MsTimer {
     bool on = false, ended = false;
-    MsTimer() {
+    hipStream_t s;
+    explicit MsTimer(hipStream_t stream = t_ms.stream) : s(stream) {
         t_last_ms = -1.f;
         if (!t_timing) return;
         if (!t_ev[0] && (hipEventCreate(&t_ev[0]) != hipSuccess || hipEventCreate(&t_ev[1]) != hipSuccess)) return;
-        on = hipEventRecord(t_ev[0], t_ms.stream) == hipSuccess;
+        on = hipEventRecord(t_ev[0], s) == hipSuccess;
     }
     void end() {
-        if (on) ended = hipEventRecord(t_ev[1], t_ms.stream) == hipSuccess;
+        if (on) ended = hipEventRecord(t_ev[1], s) == hipSuccess;
     }
     ~MsTimer() {
         float ms = 0.f;
@@ -1175,7 +1285,8 @@ int ms_prepare(const Plan& p) {
         m = MatchScratch();
         m.device = dev;
         HIPCHK(hipStreamCreateWithFlags(&m.stream, hipStreamNonBlocking));
-        HIPCHK(hipHostMalloc((void**)&m.hs, 64, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc((void**)&m.hs, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostGetDevicePointer((void**)&m.hs_dev, m.hs, 0));
     }
     if (p.end > m.dcap) {
         if (m.d) HIPCHK(hipFree(m.d));
@@ -1258,9 +1369,17 @@ struct FramePlan {
         v.r2l = two ? (dev ? F->r2l : ms_ptr<const int>(r2l)) : nullptr;
         return v;
     }
-    void launch_grid(const FrameDev& v) const {
-        hipLaunchKernelGGL(k_mt_grid, dim3(ngrids), dim3(1024), 0, t_ms.stream, v.keys, v.n, v.nleft, v.minx, v.miny,
-                           v.invw, v.invh, (int*)v.cstart, (int*)v.cidx, v.gstride_c, v.gstride_i);
+    // the grids on the thread's matcher stream, or on stream s; with `init`, the same launch also
+    // runs the search initialisation in extra blocks
+    void launch_grid(const FrameDev& v) const { launch_grid_on(v, t_ms.stream, nullptr); }
+    void launch_grid_on(const FrameDev& v, hipStream_t s, const SbpInit* init) const {
+        SbpInit none;
+        memset(&none, 0, sizeof(none));
+        const SbpInit& ia = init ? *init : none;
+        const int nib = (sbp_init_extent(ia) + 1023) / 1024;
+        hipLaunchKernelGGL(k_mt_grid, dim3(ngrids + nib), dim3(1024), 0, s, v.keys, v.n, v.nleft,
+                           v.minx, v.miny, v.invw, v.invh, (int*)v.cstart, (int*)v.cidx, v.gstride_c, v.gstride_i,
+                           ngrids, ia);
     }
 };
 
@@ -1284,11 +1403,9 @@ bool links_ok(const orbfe_frame* f) {
     return true;
 }
 
-inline void fill(int* p, int n, int v) {
-    if (n > 0) hipLaunchKernelGGL(k_mt_fill, dim3((n + 255) / 256), dim3(256), 0, t_ms.stream, p, n, v);
+inline void fill(int* p, int n, int v, hipStream_t s = t_ms.stream) {
+    if (n > 0) hipLaunchKernelGGL(k_mt_fill, dim3((n + 255) / 256), dim3(256), 0, s, p, n, v);
 }
-
-#define MT_MAX_PASSES 4096
 
 // Shared driver of the three slot-assigning SearchByProjection variants.
 // mode: 0 local map, 1 last frame, 2 keyframe.
@@ -1349,37 +1466,6 @@ struct DevIn {
     hipStream_t caller;
 };
 
-// Every per-search initialisation of sbp_run in one launch (each used to be its own fill /
-// memset / kernel call): initial blocked flags of a device-resident search (b0d != nullptr), the
-// pass states of the all -1 assignment, the assignment, the change flags, the rotation histogram
-// and the commit result (resb[0] = change-flag copy, resb[1..2] = counts, resb[3 + k] = -1).
-struct SbpInit {
-    const int32_t* mvp;
-    const int32_t* obs;
-    int any_slot;
-    int* b0d;
-    int* fb0;
-    int* fb1;
-    int* assign;
-    int nassign;
-    int* changed;
-    int* hist;
-    int* resb;
-    int n;
-};
-__global__ void k_sbp_init(SbpInit a) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < a.n) {
-        if (a.b0d) a.b0d[k] = a.any_slot ? (a.mvp[k] >= 0) : (a.mvp[k] >= 0 && a.obs[k] > 0);
-        a.fb0[k] = MT_INF;
-        a.fb1[k] = MT_INF;
-    }
-    if (k < a.nassign) a.assign[k] = -1;
-    if (k < MT_MAX_PASSES) a.changed[k] = 0;
-    if (k < MT_HISTO) a.hist[k] = 0;
-    if (k < a.n + 3) a.resb[k] = k < 3 ? 0 : -1;
-}
-
 int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, const void* queries, int nq,
             size_t qstride, size_t qobs_off, size_t qid_off, size_t qangle_off, size_t qlevel_off, float th, int a0, int a1, float thFar,
             float nnratio, int maxDist, int checkOri, const FrustumIn* fin = nullptr, const DevIn* dev = nullptr,
@@ -1439,19 +1525,15 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     const size_t o_slst = buckets ? p.scratch((size_t)nq * W * 4) : 0;
     const size_t o_changed = p.scratch(MT_MAX_PASSES * 4);
     const size_t o_result = p.scratch((size_t)(n + 3) * 4);   // [change flag copy | counts | slots]
-    const size_t o_hist = p.scratch(MT_HISTO * 4);
+    const size_t o_hist = p.scratch((MT_HISTO + 1) * 4);   // rotation bins + commit completion counter
     int rc = ms_prepare(p);
     if (rc) return rc;
-    hipStream_t s = t_ms.stream;
-    if (dev) {   // order after the producer of the device inputs
-        static thread_local hipEvent_t ev = nullptr;
-        if (!ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        HIPCHK(hipEventRecord(ev, dev->caller));
-        HIPCHK(hipStreamWaitEvent(s, ev, 0));
-    }
-    MsTimer timer;
+    // a device-resident search runs on the caller's stream, after the producer of its inputs, with
+    // no cross-stream event (every call ends with a synchronisation, so the thread's scratch is free
+    // again before the next call uses it on either stream)
+    hipStream_t s = dev ? dev->caller : t_ms.stream;
+    MsTimer timer(s);
     const FrameDev fr = fp.view();
-    fp.launch_grid(fr);
     const int* b0 = dev ? ms_ptr<const int>(o_b0d) : ms_ptr<const int>(o_b0);
     int32_t* mvp_d = dev ? mvp : ms_ptr<int32_t>(o_mvp);
     int* first = ms_ptr<int>(o_first);
@@ -1459,11 +1541,10 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     int* changed = ms_ptr<int>(o_changed);
     int* resb = ms_ptr<int>(o_result);
     int* hist = ms_ptr<int>(o_hist);
-    {
+    {   // the grids and the search initialisation in one launch
         const SbpInit ia{mvp, mvp_obs, mode == 2 ? 1 : 0, dev ? ms_ptr<int>(o_b0d) : nullptr, first,
                          ms_ptr<int>(o_first1), assign, nq * W, changed, hist, resb, n};
-        const int ni = std::max(std::max(n + 3, nq * W), MT_MAX_PASSES);
-        hipLaunchKernelGGL(k_sbp_init, dim3((ni + 255) / 256), dim3(256), 0, s, ia);
+        fp.launch_grid_on(fr, s, &ia);
     }
     const float2* ruv = (two && mode == 1) ? (dev ? (const float2*)right_uv : ms_ptr<const float2>(o_ruv)) : nullptr;
     const uint8_t* q = dev ? (const uint8_t*)(fin ? (const void*)fin->pts : queries) : ms_ptr<const uint8_t>(o_q);
@@ -1486,24 +1567,28 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     const bool staged = n <= MT_STAGE_MAX;
     int* result = resb + 1;
     const dim3 ge((nq * W + MT_NT - 1) / MT_NT);
-    // the commit runs once (a gated commit that does not run leaves result / hist as k_sbp_init set them)
-    auto commit = [&](const int* gate) {
+    // the commit runs once (a gated commit that does not run leaves result / hist as the
+    // initialisation set them); st_host: where the last kernel stores the status the host reads
+    auto commit = [&](const int* gate, const CommitStatus& cs) {
         hipLaunchKernelGGL(k_mt_commit_count, ge, dim3(MT_NT), 0, s, fr.keys, assign, (const float*)(q + qangle_off),
                            (int)qstride, nq * W, checkOri, result, hist, W, gate);
         if (checkOri)
             hipLaunchKernelGGL(k_mt_commit_drop, ge, dim3(MT_NT), 0, s, fr.keys, assign,
                                (const float*)(q + qangle_off), (int)qstride, nq * W, hist, result, W, gate);
         hipLaunchKernelGGL(k_mt_commit_write, dim3((n + 255) / 256), dim3(256), 0, s, n, (const int*)(q + qid_off),
-                           (int)qstride, result, mvp_d, W, gate, resb);
+                           (int)qstride, result, mvp_d, W, gate, resb, cs);
         return ORBFE_OK;
     };
     int pass = 0;
     if (W == 1) {
         // single camera: one gated kernel per pass (PassIO), a batch of passes and the gated commit
         // per host round trip; most searches converge within the first batch (2-4 passes)
-        int* fb[3] = {first, ms_ptr<int>(o_first1), ms_ptr<int>(o_first2)};   // fb[0], fb[1] = MT_INF (k_sbp_init)
-        const int batch = 6;
+        int* fb[3] = {first, ms_ptr<int>(o_first1), ms_ptr<int>(o_first2)};   // fb[0], fb[1] = MT_INF (init)
+        // passes per round trip: as many as the previous search of this mode needed, plus one (a
+        // gated pass costs a dispatch; an extra round trip costs far more)
+        int batch = std::min(std::max(t_ms.pass_hint[mode] + 1, 2), 8);
         while (true) {
+            const int pass0 = pass;
             for (int c = 0; c < batch; c++, pass++) {
                 if (pass >= MT_MAX_PASSES) return ORBFE_E_CAPACITY;
                 PassIO io{pass ? changed + pass - 1 : nullptr, fb[(pass + 1) % 3], fb[(pass + 2) % 3], n,
@@ -1528,14 +1613,32 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
                                        mode == 1 ? 0 : 1, a0, a1, maxDist, b0, fcur, assign, changed + pass, io);
                 }
             }
-            commit(changed + pass - 1);   // runs only if the last pass changed nothing
+            // the commit (gated: runs only if the last pass changed nothing) ends with its last
+            // block storing {change flag, assigned, dropped, passes needed, sequence number} straight
+            // into the pinned host words: no copy operation, and a device-resident call waits for
+            // the sequence number instead of the stream
+            volatile int* st = t_ms.hs;
+            const int seq = ++t_ms.seq;
+            commit(changed + pass - 1, CommitStatus{t_ms.hs_dev, hist + MT_HISTO, changed + pass0, batch, seq});
             HIPCHK(hipGetLastError());
             timer.end();
-            int* st = t_ms.hs;   // change flag of the last pass, assigned count, dropped count
-            if (!dev) HIPCHK(hipMemcpyAsync(mvp, mvp_d, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipMemcpyAsync(st, resb, 12, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipStreamSynchronize(s));
-            if (st[0] == 0) return st[1] - st[2];
+            if (!dev) {
+                HIPCHK(hipMemcpyAsync(mvp, mvp_d, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipStreamSynchronize(s));
+            }
+            for (unsigned spin = 1; st[4] != seq; spin++) {
+                if ((spin & 1023) == 0) {   // bounded: a stream that finished without publishing is an error
+                    const hipError_t e = hipStreamQuery(s);
+                    if (e == hipSuccess && st[4] != seq) return ORBFE_E_DEVICE;
+                    if (e != hipSuccess && e != hipErrorNotReady) HIPCHK(e);
+                }
+                __builtin_ia32_pause();
+            }
+            if (st[0] == 0) {
+                t_ms.pass_hint[mode] = pass0 + st[3];
+                return st[1] - st[2];
+            }
+            batch = 6;
         }
     }
     const int chunk = 2;   // passes launched between host checks (two-camera frames)
@@ -1556,7 +1659,7 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
                                    nnratio, b0, (const int*)off, (const int*)lst, assign, changed + pass);
                 continue;
             }
-            fill(first, n, MT_INF);
+            fill(first, n, MT_INF, s);
             hipLaunchKernelGGL(k_mt_first_strided, gw, dim3(MT_NT), 0, s, assign, q + qobs_off, (int)qstride, nq * W,
                                mode == 2 ? 0 : 1, first, W);
             hipLaunchKernelGGL(k_sbp_proj2, gq, dim3(MT_NT), 0, s, fr, (const orbfe_proj_point*)q, ruv, nq, th, a0,
@@ -1567,7 +1670,7 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
         HIPCHK(hipStreamSynchronize(s));
         if (*ch == 0) break;
     }
-    commit(nullptr);
+    commit(nullptr, CommitStatus{});
     HIPCHK(hipGetLastError());
     timer.end();
     int* cnt = t_ms.hs;
