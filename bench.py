@@ -51,7 +51,7 @@ def algorithmic_bytes(w, h):
 
 def pmc_traffic(n_img, w, h):
     """HBM bytes per pyramid+FAST pass from the newest committed PMC summary for this workload
-    (profiles/rNN_pmc_traffic.json, written by tools/pmc_summary.py from rocprofv3 FETCH_SIZE /
+    (profiles/rNN_pmc_traffic.json, written by tools/pmc_round.py from rocprofv3 FETCH_SIZE /
     WRITE_SIZE passes of this same bench command); None when there is none."""
     import glob
     best = None
@@ -81,7 +81,7 @@ def tr_kernels(n_img, w, h):
 
 def pmc_cache(n_img, w, h):
     """Descriptor-pass L2 hit rate and LDS bank-conflict share from the newest committed cache PMC
-    summary for this workload (profiles/rNN_pmc_cache.json, tools/pmc_cache_summary.py)."""
+    summary for this workload (profiles/rNN_pmc_cache.json, tools/pmc_round.py)."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_cache.json"))):
@@ -453,7 +453,7 @@ def stage_times(fe, images, n):
 
 def pmc_valu(n_img, w, h):
     """Per-kernel VALU instruction counts and wave states from the newest committed PMC summary of
-    this workload (profiles/rNN_pmc_valu.json, tools/pmc_valu_summary.py)."""
+    this workload (profiles/rNN_pmc_valu.json, tools/pmc_round.py)."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_valu.json"))):

@@ -416,16 +416,11 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
 #ifdef FAST_NO_OVERLAP
         s2 = s;   // profiling builds: every launch in stream order (isolated kernel times)
 #endif
-#ifndef FAST_MID
-#define FAST_MID 4   // FAST of levels [1, FAST_MID) runs on the side stream once resize has built them
-#endif
-#ifndef RZ_STREAM
-#define RZ_STREAM 1  // 0: every level with the LDS-tiled k_resize (A/B builds)
-#endif
+        constexpr int kFastMid = 4;   // FAST of levels [1, kFastMid) runs on the side stream once resize has built them
         // side stream: FAST of level 0 at once, then of levels [1, lmid) when the chain has built
         // them (beside the chain's short, latency-bound top-level launches); batch stream: the
         // chain, then FAST of levels [lmid, nlevels)
-        const int lmid = std::min(std::max(FAST_MID, 1), g.nlevels);
+        const int lmid = std::min(std::max(kFastMid, 1), g.nlevels);
         HIPCHK(hipEventRecord(h->ev_fork[0], s));
         HIPCHK(hipStreamWaitEvent(s2, h->ev_fork[0], 0));
         fast_range(s2, 0, 1);
@@ -436,7 +431,7 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
         // unless the level's column windows break its rules (then the LDS-tiled k_resize)
         for (int l = 1; l < g.nlevels; l++) {
             const OrbLevel& L = g.lv[l];
-            if (RZ_STREAM && L.rs_ok && (l > 1 || al0)) {
+            if (L.rs_ok && (l > 1 || al0)) {
                 const int nstrips = (L.w + RS_COLS - 1) / RS_COLS, nitems = nstrips * ((L.h + L.rs_rows - 1) / L.rs_rows);
                 hipLaunchKernelGGL(k_resize_s, dim3((nitems + 3) / 4, B), dim3(256), 0, s, P, pitch, h->d_pyr,
                                    g.pyr_bytes, h->d_tab, g, l, nstrips, nitems);
@@ -479,9 +474,7 @@ typedef unsigned int orbfe_u32x4 __attribute__((ext_vector_type(4)));
 // Streaming copy used by bench.py as the measured HBM ceiling: CP_U independent 16-byte loads in
 // flight per lane (a block moves CP_U x 4 KB per round), non-temporal so the copy does not keep
 // either buffer in L2 / the Infinity Cache.
-#ifndef CP_U
 #define CP_U 4
-#endif
 __global__ __launch_bounds__(256) void k_copy16(const orbfe_u32x4* __restrict__ src, orbfe_u32x4* __restrict__ dst,
                                                 size_t n) {
     const size_t stride = (size_t)gridDim.x * blockDim.x * CP_U;
@@ -504,9 +497,7 @@ int orbfe_copy_stream(const void* d_src, void* d_dst, size_t bytes, void* stream
     if (!d_src || !d_dst || (bytes & 15) || (((uintptr_t)d_src | (uintptr_t)d_dst) & 15)) return ORBFE_E_ARG;
     const size_t n = bytes / 16;
     if (!n) return ORBFE_OK;
-#ifndef CP_BLOCKS
 #define CP_BLOCKS (256 * 16)
-#endif
     const unsigned blocks = (unsigned)std::min<size_t>((n + 256 * CP_U - 1) / (256 * CP_U), CP_BLOCKS);
     hipLaunchKernelGGL(k_copy16, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const orbfe_u32x4*)d_src, (orbfe_u32x4*)d_dst, n);
     HIPCHK(hipGetLastError());
@@ -770,8 +761,11 @@ int orbfe_stereo_match_batch(orbfe_extractor* left, int lbase, int lstep, orbfe_
                   left->last_counts, lbase, lstep};
     StereoSide SR{right->d_ptrs, right->last_pitch, right->d_pyr, right->g.pyr_bytes, right->last_kps,
                   right->last_desc, right->last_counts, rbase, rstep};
+    // sort keys: kp_cap for the counting sort (k_stereo's csort rule), a power of two for the
+    // bitonic fallback of images taller than 1983 rows
     int sort_cap = 1;
     while (sort_cap < g.kp_cap) sort_cap <<= 1;
+    if (g.height + 2 * ST_ROFF + 1 <= (ST_NT / 64) * 128) sort_cap = (g.kp_cap + 3) & ~3;   // 16-byte aligned tail
     StereoArgs sa{bf, fx, g.kp_cap, sort_cap};
     const size_t lds = (size_t)g.kp_cap * (32 + sizeof(RightRec)) + (size_t)sort_cap * 4 + (ST_NT / 64) * (512 + 128 * 4) +
                        (size_t)round_up(2 * (g.height + 2 * ST_ROFF), 16);

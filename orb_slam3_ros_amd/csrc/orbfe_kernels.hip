@@ -195,19 +195,13 @@ __device__ __forceinline__ uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : 
 // (B) the horizontal pass H = S[sx]*a0 + S[sx+1]*a1 (exact int) runs once per (source row,
 // output column) into LDS, (C) every thread finishes 4 adjacent output pixels of a row from two
 // 16-byte H reads and stores them with one dword store.
-#ifndef RZ_TR
 #define RZ_TR 24
 #define RZ_SR 32              // source rows of a tile window (host-checked)
-#endif
-#ifndef RZ_TC
 #define RZ_TC 128
 #define RZ_SCB 176            // source bytes of a tile window row (host-checked)
-#endif
 #define RZ_LD ((RZ_SR * RZ_SCB / 16 + 255) / 256)  // window 16-byte chunks per thread
-#ifndef RZ_TPB
 #define RZ_TPB 4              // vertically adjacent tiles per block: the next tile's window loads fly
                               // while this tile's passes run
-#endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k_resize(const uint8_t* const* imgs, int in_pitch, uint8_t* pyr, int pyr_stride,
                                                 const int16_t* __restrict__ tab, OrbGeom g, int l) {
     __shared__ __attribute__((aligned(16))) uint8_t s_src[RZ_SR][RZ_SCB];
@@ -374,18 +368,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
 // table never clips). Bytes at or past the source width only ever meet a zero coefficient, so a
 // dword that would cross the row pitch is read from the row's last dword instead.
 // ---------------------------------------------------------------------------------------------
-#ifndef RS_D
 #define RS_D 5               // rows of loads in flight per wave = RS_D - 1 (the loop body's unroll;
                              // with the dwordx3 loads: 2 / 3 / 5 / 7 -> 729 / 676 / 637 / 675 us per
                              // 1024 images, 7 costs a wave per SIMD)
-#endif
-#ifndef RS_X3
-#define RS_X3 1              // the lane's 12-byte source window as one dwordx3 load (0: 3 dword loads)
-#endif
-#ifndef RS_ROWS
 #define RS_ROWS 48           // output rows per wave (<= 64: one table row per lane; 16 / 32 / 48 / 64
                              // with RS_D 5: 637 / 613 / 592 / 615 us per 1024 images)
-#endif
 #define RS_COLS 256          // output columns per wave strip
 typedef unsigned short orbfe_ushort2_rs __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(256) void k_resize_s(const uint8_t* const* imgs, int in_pitch, uint8_t* pyr,
@@ -495,9 +482,6 @@ __global__ __launch_bounds__(256) void k_resize_s(const uint8_t* const* imgs, in
     // a 32-bit lane offset (the SGPR-base load form, no 64-bit address arithmetic per load). The
     // prologue issues the loop's (store, loads) pattern per row, in order, so the loop entry and
     // its back edge present the same outstanding counts.
-    uint32_t doff[3];
-#pragma unroll
-    for (int k = 0; k < 3; k++) doff[k] = (uint32_t)min(base + 4 * k, spitch - 4);
     const uint32_t win = (uint32_t)min(base, spitch - 4);
     // buffer loads: descriptor over the source level (rows of spitch bytes, the same bytes the
     // clamped offsets always read), row offset s * spitch in soffset
@@ -508,17 +492,12 @@ __global__ __launch_bounds__(256) void k_resize_s(const uint8_t* const* imgs, in
         __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)sp_hi << 32) | sp_lo), (short)0, sbytes, 0x00020000);
     auto ld = [&](int s, uint32_t (&w)[3]) {
         const int so = __builtin_amdgcn_readfirstlane(s * spitch);
-#if RS_X3
         // one 12-byte load from the window's first dword; a window that runs past the row's pitch
         // reads the next row's first bytes (or zeros past the level: the descriptor's range
         // check), which only ever meet zero coefficients
         typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
         const u32x3 v = __builtin_bit_cast(u32x3, __builtin_amdgcn_raw_buffer_load_b96(srd, (int)win, so, 0));
         w[0] = v.x; w[1] = v.y; w[2] = v.z;
-#else
-#pragma unroll
-        for (int k = 0; k < 3; k++) w[k] = __builtin_amdgcn_raw_buffer_load_b32(srd, (int)doff[k], so, 0);
-#endif
     };
     uint32_t buf[RS_D][3];
 #pragma unroll
@@ -594,12 +573,7 @@ __device__ __forceinline__ int fast_M(const uint8_t* im, int stride, int x, int 
     return max((int)best.x, (int)best.y);
 }
 
-#ifndef FAST_CPW
 #define FAST_CPW 4    // cells per wave (the next cell's ROI is prefetched into registers)
-#endif
-#ifndef FAST_P1_PAIR
-#define FAST_P1_PAIR 1   // pass 1 evaluates two row blocks per loop iteration
-#endif
 #define FAST_PF 4     // prefetched 16-byte chunks per lane (rows / rows-per-load: 2 at W = 35)
 struct FastCell {
     int l, local, ci, cj, r0, c0, rows, cols, pitch;
@@ -834,16 +808,12 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
                         (uint32_t)((y << 7) | (4 * lg)) | (m8 << 16);
                 ngrp += __popcll(gm);
             };
-#if FAST_P1_PAIR
             // two row blocks per iteration: both blocks' LDS reads issue before either's compute
             for (int y0 = 0; y0 < dh; y0 += 2 * rpi) {
                 const uint32_t ma = pretest(y0 + ly), mb = pretest(y0 + rpi + ly);
                 compact(y0 + ly, ma);
                 if (y0 + rpi < dh) compact(y0 + rpi + ly, mb);
             }
-#else
-            for (int y0 = 0; y0 < dh; y0 += rpi) compact(y0 + ly, pretest(y0 + ly));
-#endif
         }
         WAVE_SYNC();
         // expand the groups into entries, one per (pixel, possible sign): dy << 7 | dx, bit 14 =
@@ -1034,12 +1004,8 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
 // winner is the first max-response key in key order, i.e. max(score) then min(index)
 // (ORBextractor.cc:757-776).
 // ---------------------------------------------------------------------------------------------
-#ifndef OCT_NT
 #define OCT_NT 256
-#endif
-#ifndef OCT_U
 #define OCT_U 4
-#endif
 // expandable node: (size << 44) | (UL.x << 32) | list position; compareNodes orders by the high 32 bits
 struct ExpLess64 {
     __device__ bool operator()(const unsigned long long& a, const unsigned long long& b) const {
@@ -1860,16 +1826,12 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
     emit_kp(angle);
 }
 
-#ifndef DP_KPW
 #define DP_KPW 4   // slots per wave: the next slot's patch loads overlap this slot's compute (a wave
                    // alone is two dependent memory round trips per slot: keys, then the patch)
-#endif
-#ifndef DP_ATTR
 // 4 slots need 88 VGPRs unconstrained (5 waves per SIMD); capped for 6 waves the compiler spills
 // 40 bytes per lane and the kernel is faster: 610 -> 560 us per step (1 slot / 4 slots at 5, 6, 7
 // waves, 2, 3 and 8 slots measured, tools/gpu_variants_trace.sh)
 #define DP_ATTR __attribute__((amdgpu_waves_per_eu(6)))
-#endif
 __global__ __launch_bounds__(256) DP_ATTR void k_describe(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                                   int pyr_stride, OrbGeom g, const uint32_t* __restrict__ outkeys,
                                                   const int* __restrict__ lvinfo, const int* __restrict__ ranks,
@@ -1940,7 +1902,7 @@ __global__ __launch_bounds__(256) DP_ATTR void k_describe(const uint8_t* const* 
 struct StereoArgs {
     float bf, fx;
     int max_kp;
-    int sort_cap;   // power of two >= max_kp (LDS sort keys)
+    int sort_cap;   // LDS sort keys: >= max_kp, a power of two for the bitonic fallback
 };
 // One side (left or right camera) of a batch of frames: image f of this side is image
 // (base + f*step) of the extractor batch whose buffers are given here.
@@ -1966,13 +1928,8 @@ __device__ __forceinline__ int hamming32(const uint32_t* a, const uint32_t* b) {
 // only the records with minr in [v - maxspan, v] (the reference's vRowIndices[v] superset; the
 // first-best-in-iR-order rule is kept by the (dist, iR) key).
 // Writes per left kp: uRight, depth (-1 = none) and the SAD distance of an accepted match (-1).
-#ifndef ST_LK
 #define ST_LK 512   // left keypoints per block (2 blocks per frame: 256 measured 10 % slower, 1024 20 %)
-#endif
 #define ST_NT 1024
-#ifndef ST_CSORT
-#define ST_CSORT 1   // right records ordered by a counting sort over band rows (0: bitonic sort)
-#endif
 #define ST_ROFF 32    // row-start table margin (rows -32 .. height + 32)
 struct RightRec { float x; int minr, maxr, oct; };
 __global__ __launch_bounds__(ST_NT) void k_stereo(OrbGeom g, StereoSide SL, StereoSide SR, StereoArgs sa,
@@ -1986,8 +1943,13 @@ __global__ __launch_bounds__(ST_NT) void k_stereo(OrbGeom g, StereoSide SL, Ster
     const int N = SL.counts[2 * bL], Nr = SR.counts[2 * bR];
     const int i0 = (lb % gridDim.x) * ST_LK;
     if (i0 >= N) return;
+    // right records ordered by a counting sort over band rows when the row table fits (every image
+    // up to 1983 rows), else by a bitonic sort of P = pow2 >= Nr keys (sa.sort_cap is sized to match)
+    const int nrow = g.height + 2 * ST_ROFF;
+    const bool csort = nrow + 1 <= (ST_NT / 64) * 128;
     int P = 1;
     while (P < Nr) P <<= 1;
+    if (csort) P = Nr;
     uint32_t* s_descR = (uint32_t*)smem_st;                        // sa.max_kp * 8 words
     RightRec* s_rec = (RightRec*)(s_descR + 8 * sa.max_kp);        // sa.max_kp records
     uint32_t* s_key = (uint32_t*)(s_rec + sa.max_kp);              // sort keys, sa.sort_cap entries
@@ -2022,8 +1984,7 @@ __global__ __launch_bounds__(ST_NT) void k_stereo(OrbGeom g, StereoSide SL, Ster
     // row -> first sorted record with minr >= row (rows -ST_ROFF .. height + ST_ROFF): the candidate
     // scan of a left keypoint reads one table entry per bound instead of a binary search
     uint16_t* s_rowst = (uint16_t*)((uint8_t*)(s_key + sa.sort_cap) + (ST_NT / 64) * (512 + 128 * 4));
-    const int nrow = g.height + 2 * ST_ROFF;
-    if (ST_CSORT && nrow + 1 <= (ST_NT / 64) * 128) {
+    if (csort) {
         // counting sort by the first row of the band (clamped into the table; a clamped record only
         // moves towards the rows that can hold it, and the band test filters it): the order within
         // a row is immaterial, the scan keeps the first best in iR order through its (dist, iR) key.

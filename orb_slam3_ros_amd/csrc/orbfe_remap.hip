@@ -75,26 +75,17 @@ __device__ __forceinline__ uint32_t remap_apply(gptr_u8 src, int sstride, const 
 // v_dot2_u32_u16 against the BilinearTab_i weights, which RemapPx already packs as u16 pairs.
 // Otherwise the 16 guarded byte loads of remap_apply. Measured (512 images, 752x480): 516 ->
 // 443 us; image-group-major block order and issuing a group's loads before its stores were slower.
-#ifndef RM_IPB
 #define RM_IPB 8
-#endif
-#ifndef RM_XCD
-#define RM_XCD 1
-#endif
 
 typedef unsigned short orbfe_ushort2_rm __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(256) void k_remap(const uint8_t* const* __restrict__ srcs, int sw, int sh, int sstride,
                                                const float* __restrict__ mapx, const float* __restrict__ mapy,
                                                int dw, int dh, uint8_t* const* __restrict__ dsts, int dstride, int n,
                                                int src_al) {
-#if RM_XCD
     // XCD-aware order: the blocks one XCD runs are consecutive tiles of one image group, so the
     // source rows two adjacent tiles share are fetched into that XCD's L2 once
     const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
     const int grp = lb / gridDim.x, tile = lb - grp * gridDim.x;
-#else
-    const int grp = blockIdx.y, tile = blockIdx.x;   // tiles fastest: each image group streamed in order
-#endif
     const int ng = (dw + 3) >> 2;
     const int t = tile * blockDim.x + threadIdx.x;
     if (t >= ng * dh) return;

@@ -20,7 +20,7 @@ import torch.distributed as dist
 
 
 def shard_range(n_total: int, rank: int, world: int) -> range:
-    """Contiguous block of frame indices owned by `rank` (frame f -> rank f * world // n_total)."""
+    """Contiguous block of frame indices owned by `rank`; the first n_total % world ranks take one extra."""
     base, rem = divmod(n_total, world)
     start = rank * base + min(rank, rem)
     return range(start, start + base + (1 if rank < rem else 0))

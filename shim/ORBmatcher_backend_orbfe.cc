@@ -1,15 +1,21 @@
 // Replacement bodies for the LocalMapping / LoopClosing ORBmatcher methods
 // (orb_slam3/src/ORBmatcher.cc:427-646, 765-1674) and MapPoint::ComputeDistinctiveDescriptors
-// (MapPoint.cc:329-403) on top of liborbfe.so. Pinhole keyframes only: a keyframe
-// with a second camera (mpCamera2) keeps the original body, renamed *_cpu, which also runs (after
-// one logged line) whenever the library returns an error.
+// (MapPoint.cc:329-403) on top of liborbfe.so. Keyframes with a second camera
+// (KannalaBrandt8 stereo, NLeft != -1) go to the library's two-camera entry points
+// (orbfe_search_by_bow_kf2, orbfe_fuse_rig, orbfe_search_for_triangulation with bCoarse). The
+// original bodies, renamed *_cpu, run where the library has no device form (SearchBySim3 and the
+// Sim3 SearchByProjection with a non-pinhole camera, the fine KannalaBrandt8 epipolar test of
+// SearchForTriangulation) and, after one logged line per call site and error code, whenever the
+// library returns an error.
 // Built inside the ORB-SLAM3 tree; NOT compiled in this repository's container (no OpenCV /
 // Eigen / Sophus here). See INTEGRATION.md §4.
 #include "ORBmatcher.h"
 
-#include <atomic>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
+#include <set>
+#include <string>
 #include <unordered_map>
 
 #include <orbfe.h>
@@ -38,19 +44,38 @@ struct Handles {   // MapPoint* <-> int32 (see ORBmatcher_orbfe.cc)
     MapPoint* at(int32_t h) const { return h < 0 ? nullptr : table[h]; }
 };
 
-bool failed(int rc, const char* what) {   // see ORBmatcher_orbfe.cc
+// One log line per (call site, error code), as ORBmatcher_orbfe.cc.
+bool failed(int rc, const char* what) {
     if (rc >= 0) return false;
-    static std::atomic<int> logged{0};
-    if (logged.fetch_add(1) < 16)
-        fprintf(stderr, "[orbfe] %s returned %d; running the CPU implementation\n", what, rc);
+    static std::mutex mu;
+    static std::set<std::pair<std::string, int>> seen;
+    bool first;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        first = seen.emplace(what, rc).second;
+    }
+    if (first) fprintf(stderr, "[orbfe] %s returned %d; running the CPU implementation\n", what, rc);
     return true;
 }
 
-orbfe_frame kf_view(KeyFrame* K) {
+// Keyframe fields the matchers read. Single camera: mvKeysUn borrowed. Two cameras (NLeft != -1):
+// keys = mvKeys ++ mvKeysRight in `keys` (the reference's per-side keypoint selection), the stereo
+// links borrowed.
+orbfe_frame kf_view(KeyFrame* K, vector<cv::KeyPoint>& keys) {
     orbfe_frame f;
-    memset(&f, 0, sizeof(f));   // two_cams = 0: single-camera keyframe
+    memset(&f, 0, sizeof(f));
     f.n = K->N;
-    f.keys = reinterpret_cast<const orbfe_keypoint*>(K->mvKeysUn.data());
+    if (K->NLeft == -1) {
+        f.keys = reinterpret_cast<const orbfe_keypoint*>(K->mvKeysUn.data());
+    } else {
+        keys.assign(K->mvKeys.begin(), K->mvKeys.end());
+        keys.insert(keys.end(), K->mvKeysRight.begin(), K->mvKeysRight.end());
+        f.keys = reinterpret_cast<const orbfe_keypoint*>(keys.data());
+        f.two_cams = 1;
+        f.nleft = K->NLeft;
+        f.l2r = K->mvLeftToRightMatch.data();
+        f.r2l = K->mvRightToLeftMatch.data();
+    }
     f.desc = K->mDescriptors.data;
     f.uright = K->mvuRight.empty() ? nullptr : K->mvuRight.data();
     f.min_x = K->mnMinX; f.max_x = K->mnMaxX; f.min_y = K->mnMinY; f.max_y = K->mnMaxY;
@@ -78,6 +103,16 @@ orbfe_pose pose_of(const Sophus::Sim3f& S) {
     p.t[0] = t(0); p.t[1] = t(1); p.t[2] = t(2);
     p.kind = ORBFE_SIM3;
     return p;
+}
+
+// GeometricCamera -> orbfe_camera_model (mnType, mvParameters)
+orbfe_camera_model model_of(GeometricCamera* c) {
+    orbfe_camera_model m;
+    memset(&m, 0, sizeof(m));
+    m.type = c->GetType() == GeometricCamera::CAM_PINHOLE ? ORBFE_CAM_PINHOLE : ORBFE_CAM_KANNALA_BRANDT8;
+    const int np = m.type == ORBFE_CAM_PINHOLE ? 4 : 8;
+    for (int k = 0; k < np; k++) m.params[k] = c->getParameter(k);
+    return m;
 }
 
 orbfe_kf_camera kf_camera(KeyFrame* K, const Sophus::SE3f& Tcw, const Eigen::Vector3f& Ow) {
@@ -126,19 +161,18 @@ struct FlatFV {   // DBoW2::FeatureVector flattened (ORBmatcher_orbfe.cc has the
 }  // namespace
 
 int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12) {
-    if (pKF1->mpCamera2 || pKF2->mpCamera2) return SearchByBoW_cpu(pKF1, pKF2, vpMatches12);
     Handles H;
     const vector<MapPoint*> v1 = pKF1->GetMapPointMatches(), v2 = pKF2->GetMapPointMatches();
     vector<int32_t> m1(v1.size()), m2(v2.size()), out(v1.size());
     for (size_t i = 0; i < v1.size(); i++) m1[i] = (v1[i] && !v1[i]->isBad()) ? H.of(v1[i]) : -1;
     for (size_t i = 0; i < v2.size(); i++) m2[i] = (v2[i] && !v2[i]->isBad()) ? H.of(v2[i]) : -1;
     FlatFV f1(pKF1->mFeatVec), f2(pKF2->mFeatVec);
-    const int n = orbfe_search_by_bow_kf(reinterpret_cast<const orbfe_keypoint*>(pKF1->mvKeysUn.data()),
-                                         pKF1->mDescriptors.data, m1.data(), pKF1->N, &f1.v,
-                                         reinterpret_cast<const orbfe_keypoint*>(pKF2->mvKeysUn.data()),
-                                         pKF2->mDescriptors.data, m2.data(), pKF2->N, &f2.v, out.data(), mfNNratio,
-                                         mbCheckOrientation);
-    if (failed(n, "orbfe_search_by_bow_kf")) return SearchByBoW_cpu(pKF1, pKF2, vpMatches12);
+    vector<cv::KeyPoint> keys1, keys2;   // two cameras: the right indices are skipped (:800-819)
+    const orbfe_frame k1 = kf_view(pKF1, keys1), k2 = kf_view(pKF2, keys2);
+    const int n = orbfe_search_by_bow_kf2(k1.keys, pKF1->mDescriptors.data, m1.data(), pKF1->N, pKF1->NLeft, &f1.v,
+                                          k2.keys, pKF2->mDescriptors.data, m2.data(), pKF2->N, pKF2->NLeft, &f2.v,
+                                          out.data(), mfNNratio, mbCheckOrientation);
+    if (failed(n, "orbfe_search_by_bow_kf2")) return SearchByBoW_cpu(pKF1, pKF2, vpMatches12);
     vpMatches12.assign(v1.size(), static_cast<MapPoint*>(nullptr));
     for (size_t i = 0; i < v1.size(); i++) vpMatches12[i] = H.at(out[i]);
     return n;
@@ -146,7 +180,9 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& v
 
 int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, vector<pair<size_t, size_t>>& vMatchedPairs,
                                        const bool bOnlyStereo, const bool bCoarse) {
-    if (pKF1->mpCamera2 || pKF2->mpCamera2)
+    // two-camera keyframes: the KannalaBrandt8 pair epipolar test (TriangulateMatches) stays with the
+    // camera model, so only the bCoarse form (no epipolar test, :1036) runs on the device
+    if ((pKF1->mpCamera2 || pKF2->mpCamera2) && !bCoarse)
         return SearchForTriangulation_cpu(pKF1, pKF2, vMatchedPairs, bOnlyStereo, bCoarse);
     // the per-call constants, computed exactly as the reference does (ORBmatcher.cc:913-927,
     // Pinhole.cpp:109-112)
@@ -165,7 +201,8 @@ int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, vector<pa
     for (int i = 0; i < pKF1->N; i++) m1[i] = pKF1->GetMapPoint(i) ? 1 : -1;
     for (int i = 0; i < pKF2->N; i++) m2[i] = pKF2->GetMapPoint(i) ? 1 : -1;
     FlatFV f1(pKF1->mFeatVec), f2(pKF2->mFeatVec);
-    const orbfe_frame k1 = kf_view(pKF1), k2 = kf_view(pKF2);
+    vector<cv::KeyPoint> keys1, keys2;
+    const orbfe_frame k1 = kf_view(pKF1, keys1), k2 = kf_view(pKF2, keys2);
     const int n = orbfe_search_for_triangulation(&k1, m1.data(), &f1.v, &k2, m2.data(), &f2.v, F12, epv,
                                                  pKF2->mvLevelSigma2.data(), bOnlyStereo, bCoarse,
                                                  mbCheckOrientation, out.data());
@@ -179,17 +216,20 @@ int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, vector<pa
 }
 
 int ORBmatcher::Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, const float th, const bool bRight) {
-    if (bRight || pKF->mpCamera2) return Fuse_cpu(pKF, vpMapPoints, th, bRight);
-    const orbfe_kf_camera cam = kf_camera(pKF, pKF->GetPose(), pKF->GetCameraCenter());
+    // pCamera / Tcw / Ow as the reference selects them (:1154-1163)
+    const orbfe_camera_model model = model_of(bRight ? pKF->mpCamera2 : pKF->mpCamera);
+    const orbfe_kf_camera cam = bRight ? kf_camera(pKF, pKF->GetRightPose(), pKF->GetRightCameraCenter())
+                                       : kf_camera(pKF, pKF->GetPose(), pKF->GetCameraCenter());
     vector<orbfe_map_point_3d> q(vpMapPoints.size());
     for (size_t i = 0; i < vpMapPoints.size(); i++) {
         MapPoint* p = vpMapPoints[i];
         q[i] = point_3d(p, p ? 0 : -1, (p && p->IsInKeyFrame(pKF)) ? ORBFE_MP_SKIP : 0);
     }
-    vector<int32_t> best(q.size()), dist(q.size());
-    const orbfe_frame kf = kf_view(pKF);
-    if (orbfe_fuse(&kf, &cam, pKF->mvInvLevelSigma2.data(), q.data(), (int)q.size(), th, 0, best.data(),
-                   dist.data()) < 0)
+    vector<int32_t> best(q.size()), dist(q.size());   // best: NLeft + right index with bRight (:1283)
+    vector<cv::KeyPoint> keys;
+    const orbfe_frame kf = kf_view(pKF, keys);
+    if (failed(orbfe_fuse_rig(&kf, &cam, &model, pKF->mvInvLevelSigma2.data(), q.data(), (int)q.size(), th, 0,
+                              bRight, best.data(), dist.data()), "orbfe_fuse_rig"))
         return Fuse_cpu(pKF, vpMapPoints, th, bRight);
     // the reference's commit, in point order; the isBad / IsInKeyFrame gate is re-read because an
     // earlier commit (Replace / AddObservation) may have changed it
@@ -221,8 +261,11 @@ int ORBmatcher::Fuse(KeyFrame* pKF, Sophus::Sim3f& Scw, const vector<MapPoint*>&
     for (size_t i = 0; i < vpPoints.size(); i++)
         q[i] = point_3d(vpPoints[i], 0, spAlreadyFound.count(vpPoints[i]) ? ORBFE_MP_SKIP : 0);
     vector<int32_t> best(q.size()), dist(q.size());
-    const orbfe_frame kf = kf_view(pKF);
-    if (orbfe_fuse(&kf, &cam, nullptr, q.data(), (int)q.size(), th, 1, best.data(), dist.data()) < 0)
+    vector<cv::KeyPoint> keys;
+    const orbfe_frame kf = kf_view(pKF, keys);   // a two-camera keyframe: its left grid (:1397)
+    const orbfe_camera_model model = model_of(pKF->mpCamera);
+    if (failed(orbfe_fuse_rig(&kf, &cam, &model, nullptr, q.data(), (int)q.size(), th, 1, 0, best.data(),
+                              dist.data()), "orbfe_fuse_rig(Scw)"))
         return Fuse_cpu(pKF, Scw, vpPoints, th, vpReplacePoint);
     int nFused = 0;
     for (size_t i = 0; i < vpPoints.size(); i++) {
@@ -242,6 +285,9 @@ int ORBmatcher::Fuse(KeyFrame* pKF, Sophus::Sim3f& Scw, const vector<MapPoint*>&
 
 int ORBmatcher::SearchByProjection(KeyFrame* pKF, Sophus::Sim3f& Scw, const vector<MapPoint*>& vpPoints,
                                    vector<MapPoint*>& vpMatched, int th, float ratioHamming) {
+    // the library projects with the pinhole intrinsics (pKF->mpCamera->project, :459)
+    if (pKF->mpCamera->GetType() != GeometricCamera::CAM_PINHOLE || pKF->mpCamera2)
+        return SearchByProjection_cpu(pKF, Scw, vpPoints, vpMatched, th, ratioHamming);
     const Sophus::SE3f Tcw = Sophus::SE3f(Scw.rotationMatrix(), Scw.translation() / Scw.scale());
     const orbfe_kf_camera cam = kf_camera(pKF, Tcw, Tcw.inverse().translation());
     Handles H;
@@ -249,7 +295,8 @@ int ORBmatcher::SearchByProjection(KeyFrame* pKF, Sophus::Sim3f& Scw, const vect
     for (size_t i = 0; i < vpPoints.size(); i++) q[i] = point_3d(vpPoints[i], H.of(vpPoints[i]), 0);
     vector<int32_t> m(vpMatched.size());
     for (size_t k = 0; k < vpMatched.size(); k++) m[k] = H.of(vpMatched[k]);
-    const orbfe_frame kf = kf_view(pKF);
+    vector<cv::KeyPoint> keys;
+    const orbfe_frame kf = kf_view(pKF, keys);
     const int n = orbfe_search_by_projection_sim3(&kf, &cam, q.data(), (int)q.size(), nullptr, th, ratioHamming,
                                                   m.data(), nullptr);
     if (failed(n, "orbfe_search_by_projection_sim3"))
@@ -260,7 +307,9 @@ int ORBmatcher::SearchByProjection(KeyFrame* pKF, Sophus::Sim3f& Scw, const vect
 
 int ORBmatcher::SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12, const Sophus::Sim3f& S12,
                              const float th) {
-    if (pKF1->mpCamera2 || pKF2->mpCamera2) return SearchBySim3_cpu(pKF1, pKF2, vpMatches12, S12, th);
+    if (pKF1->mpCamera2 || pKF2->mpCamera2 || pKF1->mpCamera->GetType() != GeometricCamera::CAM_PINHOLE ||
+        pKF2->mpCamera->GetType() != GeometricCamera::CAM_PINHOLE)
+        return SearchBySim3_cpu(pKF1, pKF2, vpMatches12, S12, th);
     Handles H;
     const vector<MapPoint*> v1 = pKF1->GetMapPointMatches(), v2 = pKF2->GetMapPointMatches();
     vector<orbfe_map_point_3d> p1(v1.size()), p2(v2.size());
@@ -274,7 +323,8 @@ int ORBmatcher::SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& 
     orbfe_kf_camera c1 = kf_camera(pKF1, pKF1->GetPose(), pKF1->GetCameraCenter());
     orbfe_kf_camera c2 = kf_camera(pKF2, pKF2->GetPose(), pKF2->GetCameraCenter());
     const orbfe_pose s12 = pose_of(S12), s21 = pose_of(S12.inverse());
-    const orbfe_frame k1 = kf_view(pKF1), k2 = kf_view(pKF2);
+    vector<cv::KeyPoint> keys1, keys2;
+    const orbfe_frame k1 = kf_view(pKF1, keys1), k2 = kf_view(pKF2, keys2);
     const int n = orbfe_search_by_sim3(&k1, &k2, p1.data(), p2.data(), &c1, &c2, &s12, &s21, th, m12.data(),
                                        idx2.data());
     if (failed(n, "orbfe_search_by_sim3")) return SearchBySim3_cpu(pKF1, pKF2, vpMatches12, S12, th);

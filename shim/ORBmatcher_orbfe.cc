@@ -10,9 +10,11 @@
 // Eigen / Sophus here). See INTEGRATION.md.
 #include "ORBmatcher.h"
 
-#include <atomic>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
+#include <set>
+#include <string>
 #include <unordered_map>
 
 #include <orbfe.h>
@@ -48,11 +50,18 @@ struct Handles {
     MapPoint* at(int32_t h) const { return h < 0 ? nullptr : table[h]; }
 };
 
-// One log line per call site and error code; the caller then runs the CPU body.
+// One log line per (call site, error code): `what` names the call site; the caller then runs the
+// CPU body. A repeated failure of one method never silences the first failure of another.
 bool failed(int rc, const char* what) {
     if (rc >= 0) return false;
-    static std::atomic<int> logged{0};
-    if (logged.fetch_add(1) < 16)
+    static std::mutex mu;
+    static std::set<std::pair<std::string, int>> seen;
+    bool first;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        first = seen.emplace(what, rc).second;
+    }
+    if (first)
         fprintf(stderr, "[orbfe] %s returned %d (%s); running the CPU implementation\n", what, rc,
                 rc == ORBFE_E_ARG ? "argument / capacity limit" : rc == ORBFE_E_DEVICE ? "HIP device error"
                 : rc == ORBFE_E_CAPACITY ? "capacity" : "error");

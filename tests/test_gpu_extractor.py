@@ -165,3 +165,24 @@ def test_stereo_matches_oracle(gpu, oracle_lib, nfeat):
     assert np.array_equal(ur.view(np.uint32), our.view(np.uint32)), np.nonzero(ur != our)[0][:10]
     assert np.array_equal(dp.view(np.uint32), odp.view(np.uint32))
     assert (ur >= 0).sum() > 0.3 * len(kl)
+
+
+def test_stereo_matches_tall_image(gpu, oracle_lib):
+    """Images taller than 1983 rows take k_stereo's bitonic-sort / binary-search ordering of the
+    right records (the row-count table of the counting sort no longer fits): bit-exact too."""
+    from orb_slam3_ros_amd.extractor import ORBextractor, compute_stereo_matches
+    left, right = synth_stereo(5, 1152, 2048)   # width >= height / 2: the octree needs nIni >= 1
+    el, er = ORBextractor(1500, 1.2, 8, 20, 7), ORBextractor(1500, 1.2, 8, 20, 7)
+    ol, orr = oracle_lib.OracleExtractor(1500, 1.2, 8, 20, 7), oracle_lib.OracleExtractor(1500, 1.2, 8, 20, 7)
+    _, kl, dl = el(left, None, (0, 0))
+    _, kr, dr = er(right, None, (0, 0))
+    _, okl, odl = ol(left)
+    _, okr, odr = orr(right)
+    assert np.array_equal(kl.view(np.uint8), okl.view(np.uint8)) and np.array_equal(dr, odr)
+    bf, fx = 0.110078 * 435.2, 435.2
+    ur, dp, nm = compute_stereo_matches(el, er, bf, fx, len(kl))
+    our, odp, onm = oracle_lib.stereo_match(ol, orr, okl, odl, okr, odr, bf, fx)
+    assert nm == onm
+    assert np.array_equal(ur.view(np.uint32), our.view(np.uint32)), np.nonzero(ur != our)[0][:10]
+    assert np.array_equal(dp.view(np.uint32), odp.view(np.uint32))
+    assert (ur >= 0).sum() > 0.3 * len(kl)
