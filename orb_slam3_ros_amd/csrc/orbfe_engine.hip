@@ -401,6 +401,9 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
         // each launch sizes its per-wave LDS by the levels it covers (level 0's cells need less than
         // the tall cells of the top levels: more resident waves per CU)
         auto fast_range = [&](hipStream_t st, int l0, int l1) {
+            // cells per wave: 4 for levels 0-3 (3 / 2 measured 0-2 % slower), 2 for the top levels'
+            // smaller grids (4: +5 %, 1: +3 %; tools/gpu_variants_trace.sh, round 3)
+            const int cpw = l0 >= 4 ? 2 : 4;
             FastLds fl{0, 0, 0, 0};
             for (int l = l0; l < l1; l++) {
                 fl.roi = std::max(fl.roi, h->fast_lds_lv[l].roi);
@@ -409,9 +412,9 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
             }
             const int c0 = g.lv[l0].cell_base, c1 = l1 < g.nlevels ? g.lv[l1].cell_base : g.total_cells;
             fl.wave_bytes = fl.roi + fl.sc + fl.cor + FAST_ENT_BYTES;
-            hipLaunchKernelGGL(k_fast, dim3((c1 - c0 + 4 * FAST_CPW - 1) / (4 * FAST_CPW), B), dim3(256),
+            hipLaunchKernelGGL(k_fast, dim3((c1 - c0 + 4 * cpw - 1) / (4 * cpw), B), dim3(256),
                                (size_t)4 * fl.wave_bytes, st, P, pitch, h->d_pyr, g.pyr_bytes, g, fl, h->d_cellkeys,
-                               h->d_cellcnt, c0, c1);
+                               h->d_cellcnt, c0, c1, cpw);
         };
 #ifdef FAST_NO_OVERLAP
         s2 = s;   // profiling builds: every launch in stream order (isolated kernel times)

@@ -132,6 +132,22 @@ __device__ __forceinline__ int wave_sum_dpp(int v) {
            __builtin_amdgcn_readlane(v, 63);
 }
 
+// Number of set bits of a wave mask below this lane (v_mbcnt_lo / v_mbcnt_hi: 2 VALU).
+__device__ __forceinline__ int lanes_below(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+// Inclusive wave scan with six DPP adds: row_shr 1, 2, 4, 8 scan each 16-lane row, row_bcast 15 /
+// 31 carry rows 0 -> 1, 2 -> 3 and row 1 -> 2, 3. Every lane must be active.
+__device__ __forceinline__ int wave_incl_scan_dpp(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+    return v;
+}
+
 // In-place exclusive scan of arr[0..n) by ONE wave (the caller's block is that wave). Returns total.
 __device__ int wave_excl_scan_lds(int* arr, int n) {
     const int lane = lane_id();
@@ -573,7 +589,6 @@ __device__ __forceinline__ int fast_M(const uint8_t* im, int stride, int x, int 
     return max((int)best.x, (int)best.y);
 }
 
-#define FAST_CPW 4    // cells per wave (the next cell's ROI is prefetched into registers)
 #define FAST_PF 4     // prefetched 16-byte chunks per lane (rows / rows-per-load: 2 at W = 35)
 struct FastCell {
     int l, local, ci, cj, r0, c0, rows, cols, pitch;
@@ -834,18 +849,23 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
             {
                 const int gi = g0 + lane;
                 const uint32_t rec = gi < ngrp ? s_grp[gi] : 0u;
-                const int cnt = __popc(rec >> 16);   // <= 8: scan by bit planes
-                const unsigned long long lt = (1ull << lane) - 1ull;
-                const unsigned long long m0 = __ballot(cnt & 1), m1 = __ballot(cnt & 2), m2 = __ballot(cnt & 4),
-                                         m3 = __ballot(cnt & 8);
-                int pos = __popcll(m0 & lt) + 2 * __popcll(m1 & lt) + 4 * __popcll(m2 & lt) + 8 * __popcll(m3 & lt);
+                const int cnt = __popc(rec >> 16);   // <= 8 entries per group
+                const int incl = wave_incl_scan_dpp(cnt);
+                int pos = incl - cnt;
                 const int packed = (int)(rec & 0x3FFFu);
+                // branch-free per entry: every potential entry is stored, the absent ones to this
+                // lane's own (already read) group record slot, which nothing reads again
+                uint16_t* trash = (uint16_t*)(s_grp + gi);
+                if (rec != 0u)
+#pragma unroll
                 for (int i = 0; i < 4; i++) {
                     const uint32_t di = (rec >> (17 + 2 * i)) & 1u, bi = (rec >> (16 + 2 * i)) & 1u;
-                    if (di) s_ent[pos++] = (uint16_t)(packed + i);
-                    if (bi) s_ent[pos++] = (uint16_t)((packed + i) | 0x4000 | (di << 15));
+                    *(di ? s_ent + pos : trash) = (uint16_t)(packed + i);
+                    pos += (int)di;
+                    *(bi ? s_ent + pos : trash) = (uint16_t)((packed + i) | 0x4000 | (di << 15));
+                    pos += (int)bi;
                 }
-                nent = __popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2) + 8 * __popcll(m3);
+                nent = __builtin_amdgcn_readlane(incl, 63);
             }
             WAVE_SYNC();
             // pass 2: exact score M - 1 (corner iff M > th) of each entry for its sign only, two
@@ -875,29 +895,29 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
                     P[k] = __builtin_elementwise_fma(x2, ns, sv);
                 }
                 // M = max over the 16 arcs of the arc minimum (signed: an arc with a minimum <= 0
-                // never makes a corner, th >= 0)
-                orbfe_half2 m2[16], m4[16], m9[16];
+                // never makes a corner, th >= 0): arc k = runs k, k + 3, k + 6 of three, each
+                // minimum one v_pk_minimum3_f16
+                orbfe_half2 m3[16], m9[16];
 #pragma unroll
-                for (int k = 0; k < 16; k++) m2[k] = hmin(P[k], P[(k + 1) & 15]);
+                for (int k = 0; k < 16; k++) m3[k] = hmin(hmin(P[k], P[(k + 1) & 15]), P[(k + 2) & 15]);
 #pragma unroll
-                for (int k = 0; k < 16; k++) m4[k] = hmin(m2[k], m2[(k + 2) & 15]);
+                for (int k = 0; k < 16; k++) m9[k] = hmin(hmin(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15]);
+                // maximum of the 16 arc minima as a tree of v_pk_maximum3_f16 (8 instead of 15)
+                orbfe_half2 r[6];
 #pragma unroll
-                for (int k = 0; k < 16; k++) m9[k] = hmin(hmin(m4[k], m4[(k + 4) & 15]), P[(k + 8) & 15]);
-#pragma unroll
-                for (int w = 8; w >= 1; w >>= 1)
-#pragma unroll
-                    for (int k = 0; k < w; k++) m9[k] = hmax(m9[k], m9[k + w]);
+                for (int k = 0; k < 5; k++) r[k] = hmax(hmax(m9[3 * k], m9[3 * k + 1]), m9[3 * k + 2]);
+                r[5] = m9[15];
+                const orbfe_half2 mx = hmax(hmax(hmax(r[0], r[1]), r[2]), hmax(hmax(r[3], r[4]), r[5]));
                 // M as an integer: the bits of a non-negative denormal; negative -> no corner
-                const uint32_t mb = h2_bits(m9[0]);
+                const uint32_t mb = h2_bits(mx);
                 const int bx = (mb & 0x8000u) ? -1 : (int)(mb & 0x7fffu);
                 const int by = (mb & 0x80000000u) ? -1 : (int)((mb >> 16) & 0x7fffu);
                 const bool c0 = ok0 && bx > th, c1 = ok1 && by > th;
                 if (c0) s_sc[(((e0 >> 7) & 127) + 1) * RS + (e0 & 127) + 1] = (uint8_t)(bx - 1);
                 if (c1) s_sc[(((e1 >> 7) & 127) + 1) * RS + (e1 & 127) + 1] = (uint8_t)(by - 1);
                 const int cc = (int)c0 + (int)c1;
-                const unsigned long long lt = (1ull << lane) - 1ull;
                 const unsigned long long b0 = __ballot(cc & 1), b1 = __ballot(cc & 2);
-                int pos = ncorner + __popcll(b0 & lt) + 2 * __popcll(b1 & lt);
+                int pos = ncorner + lanes_below(b0) + 2 * lanes_below(b1);
                 if (c0) s_cor[pos++] = (uint16_t)(e0 & 0x3FFFu);
                 if (c1) s_cor[pos] = (uint16_t)(e1 & 0x3FFFu);
                 ncorner += __popcll(b0) + 2 * __popcll(b1);
@@ -923,7 +943,7 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
                        sc > q[RS - 1] && sc > q[RS] && sc > q[RS + 1];
             }
             const unsigned long long m = __ballot(surv);
-            if (surv) s_cor[nsurv + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)p;
+            if (surv) s_cor[nsurv + lanes_below(m)] = (uint16_t)p;
             nsurv += __popcll(m);
         }
         WAVE_SYNC();
@@ -947,7 +967,7 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
         }
         const bool f = i < nsurv;
         const unsigned long long m = __ballot(f);
-        const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
+        const int pos = base + lanes_below(m);
         if (f) out[pos] = (uint32_t)(xr0 + (p & 127)) | ((uint32_t)(yr0 + (p >> 7)) << 12) | ((uint32_t)sc << 24);
         base += __popcll(m);
     }
@@ -957,7 +977,7 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
 
 __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                               int pyr_stride, OrbGeom g, FastLds fl, uint32_t* cellkeys,
-                                              int* cellcnt, int c_lo, int c_hi) {
+                                              int* cellcnt, int c_lo, int c_hi, int cpw) {
     constexpr int ablate = ORBFE_ABLATE_FAST;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_fast[];
     // wave-uniform in an SGPR: the cell geometry (level search, cell row / column division, ROI
@@ -972,9 +992,11 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
     uint8_t* s_sc = s_img + fl.roi;
     uint16_t* s_cor = (uint16_t*)(s_sc + fl.sc);
     uint16_t* s_ent = (uint16_t*)((uint8_t*)s_cor + fl.cor);
-    const int cbeg = c_lo + (bx * 4 + wave) * FAST_CPW;   // the launch covers cells [c_lo, c_hi)
+    // the launch covers cells [c_lo, c_hi), cpw consecutive cells per wave (the next cell's ROI is
+    // prefetched into registers while this one is processed)
+    const int cbeg = c_lo + (bx * 4 + wave) * cpw;
     if (cbeg >= c_hi) return;
-    const int cend = min(cbeg + FAST_CPW, c_hi);
+    const int cend = min(cbeg + cpw, c_hi);
     orbfe_u32x4 pf[FAST_PF];
     FastCell cur = fast_cell(imgs, in_pitch, pyr, pyr_stride, g, b, cbeg);
     fast_prefetch(cur, lane, pf);
@@ -1667,7 +1689,7 @@ __device__ __forceinline__ void desc_stage(uint8_t* raw, int lane, const orbfe_u
 // keypoint record and the descriptor row.
 __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g, const uint8_t* raw, uint32_t* rowp,
                                              const float4 (&pat)[4], int lane, OrbKeyPoint* kps, uint8_t* desc,
-                                             const BlurKernel& bk, int ablate) {
+                                             const BlurKernel& bk, const uint4 (*icm)[3], int ablate) {
     const OrbLevel& L = g.lv[d.l];
     const int l = d.l, x = d.x, y = d.y;
     const uint32_t key = d.key;
@@ -1696,7 +1718,7 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
     int m10 = 0, m01 = 0;
     if (lane < 31) {
         const uint4* rowp = (const uint4*)(raw + (lane + DP_R - 15) * DP_RAW_S);
-        const uint4* mk = (const uint4*)c_ic_mask.m[lane];
+        const uint4* mk = icm[lane];   // the block's LDS copy of c_ic_mask
         const uint4 q0 = rowp[0], q1 = rowp[1], q2 = rowp[2];
         const uint4 k0 = mk[0], k1 = mk[1], k2 = mk[2];
         const uint32_t I[9] = {q0.y & k0.x, q0.z & k0.y, q0.w & k0.z, q1.x & k0.w, q1.y & k1.x,
@@ -1728,9 +1750,13 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
     // rounding, so this equals blurring the whole level. ----
     const uint32_t k0 = bk.k[0], k1 = bk.k[1], k2 = bk.k[2], k3 = bk.k[3];
     {
-        // output j of a 4-column group = taps 0-3 . (k0 k1 k2 k3) + taps 4-6 . (k2 k1 k0 0), each a
-        // v_dot4_u32_u8 over a byte-aligned window of the 12-byte run w0 w1 w2 (exact: <= 65280)
+        // output j of a 4-column group = bytes j .. j + 6 of the 12-byte run w0 w1 w2 times the taps
+        // (k0 k1 k2 k3 k2 k1 k0): v_dot4_u32_u8 of each dword with the kernel shifted by j bytes, no
+        // realignment (2 + 2 + 3 + 3 dot products per group; exact: <= 65280)
         const uint32_t KLO = k0 | (k1 << 8) | (k2 << 16) | (k3 << 24), KHI = k2 | (k1 << 8) | (k0 << 16);
+        const uint32_t K10 = (k0 << 8) | (k1 << 16) | (k2 << 24), K11 = k3 | (k2 << 8) | (k1 << 16) | (k0 << 24);
+        const uint32_t K20 = (k0 << 16) | (k1 << 24), K21 = k2 | (k3 << 8) | (k2 << 16) | (k1 << 24), K22 = k0;
+        const uint32_t K30 = k0 << 24, K31 = k1 | (k2 << 8) | (k3 << 16) | (k2 << 24), K32 = k1 | (k0 << 8);
         // row pairs (2 p, 2 p + 1) x 10 groups of 4 output columns: lanes 0..59 = 6 pairs x 10 groups,
         // pairs p0 + 6 i; the pair is stored as one dword per column (row 2 p low, 2 p + 1 high), one
         // 16-byte store per group. Row 43 does not exist: its half is 0 (never weighted).
@@ -1744,12 +1770,10 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
             for (int e = 0; e < 2; e++) {
                 const uint32_t* rp = (const uint32_t*)(raw + (2 * pr + e) * DP_RAW_S) + gq;
                 const uint32_t w0 = rp[0], w1 = rp[1], w2 = rp[2];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const uint32_t lo = j ? __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)j) : w0;
-                    const uint32_t hi = j ? __builtin_amdgcn_alignbyte(w2, w1, (uint32_t)j) : w1;
-                    h[e][j] = __builtin_amdgcn_udot4(hi, KHI, __builtin_amdgcn_udot4(lo, KLO, 0u, false), false);
-                }
+                h[e][0] = __builtin_amdgcn_udot4(w1, KHI, __builtin_amdgcn_udot4(w0, KLO, 0u, false), false);
+                h[e][1] = __builtin_amdgcn_udot4(w1, K11, __builtin_amdgcn_udot4(w0, K10, 0u, false), false);
+                h[e][2] = __builtin_amdgcn_udot4(w2, K22, __builtin_amdgcn_udot4(w1, K21, __builtin_amdgcn_udot4(w0, K20, 0u, false), false), false);
+                h[e][3] = __builtin_amdgcn_udot4(w2, K32, __builtin_amdgcn_udot4(w1, K31, __builtin_amdgcn_udot4(w0, K30, 0u, false), false), false);
             }
             const bool last = 2 * pr + 1 >= DP_N;
             uint4 pk;
@@ -1838,6 +1862,12 @@ __global__ __launch_bounds__(256) DP_ATTR void k_describe(const uint8_t* const* 
                                                   OrbKeyPoint* kps, uint8_t* desc, int* counts, BlurKernel bk) {
     constexpr int ablate = ORBFE_ABLATE_DESC;
     __shared__ __attribute__((aligned(16))) uint8_t s_dp[4][DP_WAVE_LDS];
+    // the IC_Angle disc masks (31 rows x 12 dwords) in LDS: per slot three ds_read_b128 instead of
+    // three vector loads from constant memory
+    __shared__ uint4 s_icm[31][3];
+    for (int i = threadIdx.x; i < 31 * 3; i += blockDim.x)
+        (&s_icm[0][0])[i] = ((const uint4*)&c_ic_mask.m[0][0])[i];
+    __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
     const int b = lb / gridDim.x;
@@ -1885,7 +1915,7 @@ __global__ __launch_bounds__(256) DP_ATTR void k_describe(const uint8_t* const* 
             nxt = desc_slot(imgs, in_pitch, pyr, pyr_stride, g, di, kv, rv, j + 1, &lvl, b, flat0 + j + 1);
             if (nxt.valid && nxt.interior) desc_load(nxt, lane, pq);
         }
-        if (cur.valid && ablate != 7) describe_one(cur, g, raw, rowp, pat, lane, kps, desc, bk, ablate);
+        if (cur.valid && ablate != 7) describe_one(cur, g, raw, rowp, pat, lane, kps, desc, bk, s_icm, ablate);
         WAVE_SYNC();   // the patch area is restaged for the next slot
         cur = nxt;
     }
