@@ -746,6 +746,8 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
     // fraction of minThFAST's.
     int nsurv = 0;
     bool stop = false;
+    uint32_t* out = cellkeys + (size_t)b * g.cellkeys_per_img + L.cellkey_off + (size_t)me.local * L.cell_cap;
+    const int xr0 = me.c0 - ORBFE_MINB + 3, yr0 = me.r0 - ORBFE_MINB + 3;
     for (int attempt = first_attempt; attempt < 2; attempt++) {
         const int th = attempt == 0 ? g.ini_th : g.min_th;
         if (attempt) {
@@ -929,49 +931,31 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
             stop = true;
             break;
         }
-        // NMS over corners (every other pixel has score 0); survivors compacted in place
+        // NMS over corners (every other pixel has score 0), fused with the emission: the corner list
+        // is in pixel order, so each chunk's survivors go straight to the cell's key list in FAST's
+        // row-major emission order. A cell whose attempt leaves no survivor has emitted nothing.
         nsurv = 0;
         for (int i0 = 0; i0 < ncorner; i0 += 64) {
             const int i = i0 + lane;
             bool surv = false;
-            int p = 0;
+            int p = 0, sc = 0;
             if (i < ncorner) {
                 p = s_cor[i];
                 const uint8_t* q = s_sc + ((p >> 7) + 1) * RS + (p & 127) + 1;
-                const int sc = q[0];
+                sc = q[0];
                 surv = sc > q[-1] && sc > q[1] && sc > q[-RS - 1] && sc > q[-RS] && sc > q[-RS + 1] &&
                        sc > q[RS - 1] && sc > q[RS] && sc > q[RS + 1];
             }
             const unsigned long long m = __ballot(surv);
-            if (surv) s_cor[nsurv + lanes_below(m)] = (uint16_t)p;
+            if (surv)
+                out[nsurv + lanes_below(m)] = (uint32_t)(xr0 + (p & 127)) | ((uint32_t)(yr0 + (p >> 7)) << 12) |
+                                              ((uint32_t)sc << 24);
             nsurv += __popcll(m);
         }
-        WAVE_SYNC();
         if (nsurv > 0) break;
+        WAVE_SYNC();   // the fallback attempt clears the score map
     }   // attempt
-    if (stop) {
-        if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = 0;
-        WAVE_SYNC();
-        return;
-    }
-    // emission of the survivors in row-major order (FAST's emission order)
-    int base = 0;
-    uint32_t* out = cellkeys + (size_t)b * g.cellkeys_per_img + L.cellkey_off + (size_t)me.local * L.cell_cap;
-    const int xr0 = me.c0 - ORBFE_MINB + 3, yr0 = me.r0 - ORBFE_MINB + 3;
-    for (int i0 = 0; i0 < nsurv; i0 += 64) {
-        const int i = i0 + lane;
-        int sc = 0, p = 0;
-        if (i < nsurv) {
-            p = s_cor[i];
-            sc = s_sc[((p >> 7) + 1) * RS + (p & 127) + 1];
-        }
-        const bool f = i < nsurv;
-        const unsigned long long m = __ballot(f);
-        const int pos = base + lanes_below(m);
-        if (f) out[pos] = (uint32_t)(xr0 + (p & 127)) | ((uint32_t)(yr0 + (p >> 7)) << 12) | ((uint32_t)sc << 24);
-        base += __popcll(m);
-    }
-    if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = base;
+    if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = stop ? 0 : nsurv;
     WAVE_SYNC();   // LDS is restaged for the next cell
 }
 
