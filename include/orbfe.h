@@ -85,7 +85,9 @@ int orbfe_pyramid_level(orbfe_extractor* h, int image, int level, uint8_t* dst, 
 
 /* Batched device path (multi-camera / multi-frame; Frame.cc:122-125 runs two extractors on two
  * threads per stereo frame — here one launch sequence covers nimg images). d_imgs: nimg device
- * pointers (host array) to width x height u8 images with row pitch `pitch`. stream: hipStream_t
+ * pointers (host array) to width x height u8 images with row pitch `pitch`; each image must have
+ * pitch * height readable bytes (the level-1 build reads whole 12-byte windows of the last row, past
+ * the width when pitch > width; a view into a larger frame satisfies this). stream: hipStream_t
  * (NULL = the handle's own stream). Outputs stay on the device: see orbfe_batch_outputs. */
 int orbfe_extract_batch(orbfe_extractor* h, int nimg, const uint8_t* const* d_imgs, int width, int height,
                         int pitch, int lap0, int lap1, void* stream);
