@@ -52,8 +52,8 @@ size_t octree_lds_bytes(const OrbGeom& g) {
     s += 2 * (4 * a16(2 * NC) + a16(4 * NC));
     s += 2 * a16(16 * NC);
     s += a16(8 * NC) + a16(2 * NC) + a16(4 * NC) * 5;
-    s += a16(8 * NC) + a16(8 * NC);
-    s += a16(4 * NC) + a16(16 * ORBFE_SORT_STACK);
+    s += a16(8 * NC);   // expv (the sort scratch and the best keys alias the next-count table)
+    s += a16(16 * ORBFE_SORT_STACK);
     return s;
 }
 
