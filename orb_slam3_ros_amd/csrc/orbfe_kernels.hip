@@ -68,15 +68,25 @@ constexpr IcMaskTab make_ic_mask() {
 }
 __constant__ IcMaskTab c_ic_mask = make_ic_mask();
 __constant__ signed char c_pattern[ORBFE_PATTERN_PAIRS * 4] = ORBFE_BRIEF_PATTERN_INIT;
-// the same pattern as floats (pair i = x0, y0, x1, y1 at 4 i): no per-sample int -> float conversion
-struct PatternF { float v[ORBFE_PATTERN_PAIRS * 4]; };
-constexpr PatternF make_pattern_f() {
+// the pattern as f16 (x0, y0), (x1, y1) pairs (pair i at 4 i): k_describe holds a lane's four pairs
+// in 8 VGPRs (as f32 they took 16 and the kernel spilled 36 bytes per lane at 6 waves per SIMD)
+struct PatternH { unsigned short v[ORBFE_PATTERN_PAIRS * 4]; };
+constexpr unsigned short f16_bits_small_int(int v) {   // |v| <= 2048: exact
+    if (v == 0) return 0;
+    const unsigned short sgn = v < 0 ? 0x8000 : 0;
+    unsigned a = (unsigned)(v < 0 ? -v : v);
+    int e = 0;
+    while ((a >> e) > 1) e++;
+    const unsigned mant = (a << (10 - e)) & 0x3FFu;
+    return (unsigned short)(sgn | ((unsigned)(e + 15) << 10) | mant);
+}
+constexpr PatternH make_pattern_h() {
     constexpr signed char p[ORBFE_PATTERN_PAIRS * 4] = ORBFE_BRIEF_PATTERN_INIT;
-    PatternF t{};
-    for (int i = 0; i < ORBFE_PATTERN_PAIRS * 4; i++) t.v[i] = (float)p[i];
+    PatternH t{};
+    for (int i = 0; i < ORBFE_PATTERN_PAIRS * 4; i++) t.v[i] = f16_bits_small_int(p[i]);
     return t;
 }
-__constant__ PatternF c_pattern_f = make_pattern_f();
+__constant__ PatternH c_pattern_h = make_pattern_h();
 constexpr int kRingDx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
 constexpr int kRingDy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
 __constant__ int c_ring_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
@@ -1676,7 +1686,7 @@ __device__ __forceinline__ void desc_stage(uint8_t* raw, int lane, const orbfe_u
 // IC_Angle + Gaussian + rBRIEF of one slot whose raw patch is staged in `raw`; writes the
 // keypoint record and the descriptor row.
 __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g, const uint8_t* raw, uint32_t* rowp,
-                                             const float4 (&pat)[4], int lane, OrbKeyPoint* kps, uint8_t* desc,
+                                             const uint2 (&pat)[4], int lane, OrbKeyPoint* kps, uint8_t* desc,
                                              const BlurKernel& bk, const uint4 (*icm)[3], int ablate) {
     const OrbLevel& L = g.lv[d.l];
     const int l = d.l, x = d.x, y = d.y;
@@ -1826,9 +1836,11 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
     unsigned long long masks[4];
 #pragma unroll
     for (int mm = 0; mm < 4; mm++) {
-        const float4 pw = pat[mm];   // pair 64 * mm + lane
-        const uint32_t t0 = blurred_at(sample_at(pw.x, pw.y));
-        const uint32_t t1 = blurred_at(sample_at(pw.z, pw.w));
+        // pair 64 * mm + lane: (x0, y0), (x1, y1) as f16 halves (the pattern's small integers are
+        // exact in f16; one v_cvt_f32_f16 per coordinate)
+        const orbfe_half2 p0 = __builtin_bit_cast(orbfe_half2, pat[mm].x), p1 = __builtin_bit_cast(orbfe_half2, pat[mm].y);
+        const uint32_t t0 = blurred_at(sample_at((float)p0.x, (float)p0.y));
+        const uint32_t t1 = blurred_at(sample_at((float)p1.x, (float)p1.y));
         masks[mm] = __ballot(t0 < t1);
     }
     if (lane < 4) {
@@ -1840,9 +1852,9 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
 
 #define DP_KPW 4   // slots per wave: the next slot's patch loads overlap this slot's compute (a wave
                    // alone is two dependent memory round trips per slot: keys, then the patch)
-// 4 slots need 88 VGPRs unconstrained (5 waves per SIMD); capped for 6 waves the compiler spills
-// 40 bytes per lane and the kernel is faster: 610 -> 560 us per step (1 slot / 4 slots at 5, 6, 7
-// waves, 2, 3 and 8 slots measured, tools/gpu_variants_trace.sh)
+// 6 waves per SIMD: 79 VGPRs, no spill since the pattern is held as f16 (at 5 waves without a spill
+// or 6 with one the kernel measured slower or equal: 1 slot / 4 slots at 5, 6, 7 waves, 2, 3 and 8
+// slots, tools/gpu_variants_trace.sh; DESIGN.md §7d, profiles/r03_kernel_ab.txt item 18)
 #define DP_ATTR __attribute__((amdgpu_waves_per_eu(6)))
 __global__ __launch_bounds__(256) DP_ATTR void k_describe(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                                   int pyr_stride, OrbGeom g, const uint32_t* __restrict__ outkeys,
@@ -1862,9 +1874,9 @@ __global__ __launch_bounds__(256) DP_ATTR void k_describe(const uint8_t* const* 
     const int flat0 = ((lb % gridDim.x) * 4 + wave) * DP_KPW;   // first of this wave's output slots
     if (flat0 >= g.out_per_img) return;
     // the rBRIEF pairs of this lane (pair 64 * mm + lane: x0, y0, x1, y1), issued first
-    float4 pat[4];
+    uint2 pat[4];
 #pragma unroll
-    for (int mm = 0; mm < 4; mm++) pat[mm] = ((const float4*)c_pattern_f.v)[64 * mm + lane];
+    for (int mm = 0; mm < 4; mm++) pat[mm] = ((const uint2*)c_pattern_h.v)[64 * mm + lane];
     // keys and ranks of the wave's slots (lane j: slot flat0 + j), one load each
     uint32_t kv = 0;
     int rv = 0;
