@@ -459,7 +459,7 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
     hipLaunchKernelGGL(k_octree, dim3(B, g.nlevels), dim3(OCT_NT), h->oct_lds, s, g, h->d_cellkeys, h->d_cellcnt,
                        h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, d_laps, h->d_oct_ts);
     if (tm) HIPCHK(hipEventRecord(ev[2], s));
-    hipLaunchKernelGGL(k_describe, dim3((g.out_per_img + 4 * DP_KPW - 1) / (4 * DP_KPW), B), dim3(256), 0, s, P, pitch, h->d_pyr,
+    hipLaunchKernelGGL(k_describe, dim3((g.out_per_img + DP_WPB * DP_KPW - 1) / (DP_WPB * DP_KPW), B), dim3(64 * DP_WPB), 0, s, P, pitch, h->d_pyr,
                        g.pyr_bytes, g, h->d_outkeys, h->d_lvinfo, h->d_ranks, o_kps, o_desc, o_counts, bk);
     if (tm) HIPCHK(hipEventRecord(ev[3], s));
     HIPCHK(hipGetLastError());

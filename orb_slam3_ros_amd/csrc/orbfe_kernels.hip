@@ -1859,12 +1859,14 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
 // or 6 with one the kernel measured slower or equal: 1 slot / 4 slots at 5, 6, 7 waves, 2, 3 and 8
 // slots, tools/gpu_variants_trace.sh; DESIGN.md §7d, profiles/r03_kernel_ab.txt items 18-19)
 #define DP_ATTR __attribute__((amdgpu_waves_per_eu(6)))
-__global__ __launch_bounds__(256) DP_ATTR void k_describe(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
+#define DP_WPB 2   // waves per block: 2 / 4 / 8 measured 1.04 / 1.06 / 1.11 ms (r03_kernel_ab.txt item 23);
+                   // 12 blocks of 12.7 KB per CU give the same 6 waves per SIMD with finer-grained refill
+__global__ __launch_bounds__(64 * DP_WPB) DP_ATTR void k_describe(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                                   int pyr_stride, OrbGeom g, const uint32_t* __restrict__ outkeys,
                                                   const int* __restrict__ lvinfo, const int* __restrict__ ranks,
                                                   OrbKeyPoint* kps, uint8_t* desc, int* counts, BlurKernel bk) {
     constexpr int ablate = ORBFE_ABLATE_DESC;
-    __shared__ __attribute__((aligned(16))) uint8_t s_dp[4][DP_WAVE_LDS];
+    __shared__ __attribute__((aligned(16))) uint8_t s_dp[DP_WPB][DP_WAVE_LDS];
     // the IC_Angle disc masks (31 rows x 12 dwords) in LDS: per slot three ds_read_b128 instead of
     // three vector loads from constant memory
     __shared__ uint4 s_icm[31][3];
@@ -1874,7 +1876,7 @@ __global__ __launch_bounds__(256) DP_ATTR void k_describe(const uint8_t* const* 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
     const int b = lb / gridDim.x;
-    const int flat0 = ((lb % gridDim.x) * 4 + wave) * DP_KPW;   // first of this wave's output slots
+    const int flat0 = ((lb % gridDim.x) * DP_WPB + wave) * DP_KPW;   // first of this wave's output slots
     if (flat0 >= g.out_per_img) return;
     // the rBRIEF pairs of this lane (pair 64 * mm + lane: x0, y0, x1, y1), issued first
     uint2 pat[4];
