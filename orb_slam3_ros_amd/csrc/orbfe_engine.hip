@@ -412,8 +412,8 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
             }
             const int c0 = g.lv[l0].cell_base, c1 = l1 < g.nlevels ? g.lv[l1].cell_base : g.total_cells;
             fl.wave_bytes = fl.roi + fl.sc + fl.cor + FAST_ENT_BYTES;
-            hipLaunchKernelGGL(k_fast, dim3((c1 - c0 + 4 * cpw - 1) / (4 * cpw), B), dim3(256),
-                               (size_t)4 * fl.wave_bytes, st, P, pitch, h->d_pyr, g.pyr_bytes, g, fl, h->d_cellkeys,
+            hipLaunchKernelGGL(k_fast, dim3((c1 - c0 + FAST_WPB * cpw - 1) / (FAST_WPB * cpw), B), dim3(64 * FAST_WPB),
+                               (size_t)FAST_WPB * fl.wave_bytes, st, P, pitch, h->d_pyr, g.pyr_bytes, g, fl, h->d_cellkeys,
                                h->d_cellcnt, c0, c1, cpw);
         };
 #ifdef FAST_NO_OVERLAP
@@ -436,7 +436,7 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
             const OrbLevel& L = g.lv[l];
             if (L.rs_ok && (l > 1 || al0)) {
                 const int nstrips = (L.w + RS_COLS - 1) / RS_COLS, nitems = nstrips * ((L.h + L.rs_rows - 1) / L.rs_rows);
-                hipLaunchKernelGGL(k_resize_s, dim3((nitems + 3) / 4, B), dim3(256), 0, s, P, pitch, h->d_pyr,
+                hipLaunchKernelGGL(k_resize_s, dim3((nitems + RS_WPB - 1) / RS_WPB, B), dim3(64 * RS_WPB), 0, s, P, pitch, h->d_pyr,
                                    g.pyr_bytes, h->d_tab, g, l, nstrips, nitems);
             } else {
                 const int tiles_y = (L.h + L.rz_rows - 1) / L.rz_rows;

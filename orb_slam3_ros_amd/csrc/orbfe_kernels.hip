@@ -401,14 +401,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
                              // with RS_D 5: 637 / 613 / 592 / 615 us per 1024 images)
 #define RS_COLS 256          // output columns per wave strip
 typedef unsigned short orbfe_ushort2_rs __attribute__((ext_vector_type(2)));
-__global__ __launch_bounds__(256) void k_resize_s(const uint8_t* const* imgs, int in_pitch, uint8_t* pyr,
+#define RS_WPB 4   // waves per block (1 / 2 / 4 measured equal: r03_kernel_ab.txt item 24)
+__global__ __launch_bounds__(64 * RS_WPB) void k_resize_s(const uint8_t* const* imgs, int in_pitch, uint8_t* pyr,
                                                   int pyr_stride, const int16_t* __restrict__ tab, OrbGeom g, int l,
                                                   int nstrips, int nitems) {
     const OrbLevel& L = g.lv[l];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
     const int bx = lb % gridDim.x, b = lb / gridDim.x;
-    const int item = bx * 4 + wave;
+    const int item = bx * RS_WPB + wave;
     if (item >= nitems) return;
     const int chunk = item / nstrips, strip = item - chunk * nstrips;
     const int y0 = chunk * L.rs_rows, y1 = min(y0 + L.rs_rows, L.h);
@@ -547,7 +548,7 @@ __global__ __launch_bounds__(256) void k_resize_s(const uint8_t* const* imgs, in
 struct BlurKernel { int k[7]; };
 
 // ---------------------------------------------------------------------------------------------
-// K3: FAST-9/16 per cell. One wave per cell (4 cells per 256-thread block). The cell ROI
+// K3: FAST-9/16 per cell. One wave per cell, single-wave blocks (FAST_WPB). The cell ROI
 // (wCell+6)x(hCell+6) is staged in LDS; the score of every detection pixel is computed ONCE at
 // minThFAST (score = M-1 where M = max over 9-arcs of the arc-min contrast, corner iff M > th),
 // and per-cell NMS is exact because the ROI ring outside the detection rect is zero. A cell
@@ -969,7 +970,10 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
     WAVE_SYNC();   // LDS is restaged for the next cell
 }
 
-__global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
+#define FAST_WPB 1   // waves per block: a block's LDS is held until its last wave retires, and the cells
+                     // of one block finish at different times; single-wave blocks return each wave's LDS
+                     // at once: 1.60 -> 1.45 ms per 1024 images against 4 (2: 1.51; r03_kernel_ab.txt item 24)
+__global__ __launch_bounds__(64 * FAST_WPB) void k_fast(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                               int pyr_stride, OrbGeom g, FastLds fl, uint32_t* cellkeys,
                                               int* cellcnt, int c_lo, int c_hi, int cpw) {
     constexpr int ablate = ORBFE_ABLATE_FAST;
@@ -988,7 +992,7 @@ __global__ __launch_bounds__(256) void k_fast(const uint8_t* const* imgs, int in
     uint16_t* s_ent = (uint16_t*)((uint8_t*)s_cor + fl.cor);
     // the launch covers cells [c_lo, c_hi), cpw consecutive cells per wave (the next cell's ROI is
     // prefetched into registers while this one is processed)
-    const int cbeg = c_lo + (bx * 4 + wave) * cpw;
+    const int cbeg = c_lo + (bx * FAST_WPB + wave) * cpw;
     if (cbeg >= c_hi) return;
     const int cend = min(cbeg + cpw, c_hi);
     orbfe_u32x4 pf[FAST_PF];
