@@ -1961,7 +1961,8 @@ __device__ __forceinline__ int hamming32(const uint32_t* a, const uint32_t* b) {
     for (int i = 0; i < 8; i++) d += __popc(a[i] ^ b[i]);
     return d;
 }
-// Stage 1: one wave per left keypoint (16 waves per block), ST_LK left keypoints per block; the right
+// Stage 1: one wave per left keypoint at a time (16 waves per block, keypoints taken from a block
+// counter), ST_LK left keypoints per block; the right
 // keypoints (x, row band, octave) and descriptors of the frame are staged in LDS once per block
 // and the records are sorted by the first row of their band, so a left keypoint on row v scans
 // only the records with minr in [v - maxspan, v] (the reference's vRowIndices[v] superset; the
@@ -1975,6 +1976,7 @@ __global__ __launch_bounds__(ST_NT) void k_stereo(OrbGeom g, StereoSide SL, Ster
                                                   float* uright, float* depth, int* sdist) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_st[];
     __shared__ int s_maxspan;
+    __shared__ int s_next;   // next left keypoint of the block (waves take them dynamically)
     const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
     const int f = lb / gridDim.x;
     const int bL = SL.base + f * SL.step, bR = SR.base + f * SR.step;
@@ -1998,7 +2000,7 @@ __global__ __launch_bounds__(ST_NT) void k_stereo(OrbGeom g, StereoSide SL, Ster
     const OrbKeyPoint* kL = SL.kps + (size_t)bL * g.kp_cap;
     const uint4* dR = (const uint4*)(SR.desc + (size_t)bR * g.kp_cap * 32);
     const uint32_t* dL = (const uint32_t*)(SL.desc + (size_t)bL * g.kp_cap * 32);
-    if (threadIdx.x == 0) s_maxspan = 0;
+    if (threadIdx.x == 0) { s_maxspan = 0; s_next = ST_NT / 64; }
     SYNC();
     for (int i = threadIdx.x; i < Nr * 2; i += blockDim.x) ((uint4*)s_descR)[i] = dR[i];
     int span = 0;
@@ -2072,7 +2074,10 @@ __global__ __launch_bounds__(ST_NT) void k_stereo(OrbGeom g, StereoSide SL, Ster
     const float mb = sa.bf / sa.fx;   // intended mb = mbf/fx (the reference reads it uninitialised)
     const float minZ = mb, minD = 0.f, maxD = sa.bf / minZ;
     const int iend = min(N, i0 + ST_LK);
-    for (int iL = i0 + wave; iL < iend; iL += ST_NT / 64) {
+    // the first keypoint of each wave is static; later ones come from a block counter, so waves whose
+    // keypoints scan few candidates take more of them and the block ends with its work, not with its
+    // slowest wave's fixed share (253 -> 236 us per 512 frames; r03_kernel_ab.txt item 29)
+    for (int iL = i0 + wave; iL < iend;) {
         float outU = -1.0f, outD = -1.0f;
         int outS = -1;
         const OrbKeyPoint kpL = kL[iL];
@@ -2194,6 +2199,9 @@ __global__ __launch_bounds__(ST_NT) void k_stereo(OrbGeom g, StereoSide SL, Ster
             }
         }
         if (lane == 0) { uR_out[iL] = outU; dp_out[iL] = outD; sd_out[iL] = outS; }
+        int nx = 0;
+        if (lane == 0) nx = atomicAdd(&s_next, 1);
+        iL = i0 + __builtin_amdgcn_readfirstlane(nx);
     }
 }
 
