@@ -304,7 +304,8 @@ typedef struct orbfe_map_point_3d {
     int32_t flags;                   /* ORBFE_MP_BAD (isBad()), ORBFE_MP_SKIP */
     int32_t observations;            /* Observations() */
     int32_t id;                      /* handle stored into mvpMapPoints */
-    int32_t reserved;
+    float track_depth;               /* mTrackDepth before this call: kept where the reference keeps it
+                                        (a two-camera point whose left view fails; bFarPoints reads it) */
     uint8_t desc[32];                /* GetDescriptor() */
 } orbfe_map_point_3d;                /* 80 bytes */
 
@@ -369,8 +370,8 @@ typedef struct orbfe_stereo_rig {
  * ORBFE_MP_IN_VIEW_R with proj_xr / proj_yr / scale_level_r / view_cos_r (right), scale levels -1
  * where a check fails (the reference resets mnTrackScaleLevel(R) to -1, :578-579). Returns nToMatch
  * (points with either view). cam supplies the pose (Rcw, tcw, Ow), mfLogScaleFactor and the cosine
- * limit; its pinhole fields are not read. A failed left check leaves depth 0 (the reference keeps the
- * previous frame's mTrackDepth, which only bFarPoints reads). */
+ * limit; its pinhole fields are not read. A failed left check keeps depth = pts[i].track_depth, the
+ * point's previous mTrackDepth, as the reference does (bFarPoints reads it). */
 int orbfe_is_in_frustum_rig(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_stereo_rig* rig,
                             const orbfe_map_point_3d* pts, int32_t n, orbfe_map_point* track);
 /* Tracking::SearchLocalPoints (Tracking.cc:3407-3452) with the rig's camera models: the projection
@@ -427,6 +428,28 @@ int orbfe_search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, c
                                    const float* F12, const float* ep, const float* level_sigma2_2,
                                    int32_t bOnlyStereo, int32_t bCoarse, int32_t checkOri, int32_t* matches12);
 
+/* The caller's epipolar test of one keypoint pair of SearchForTriangulation (bCoarse false):
+ * pCamera1->epipolarConstrain(pCamera2, kp1, kp2, R12, t12, pKF1->mvLevelSigma2[kp1.octave],
+ * pKF2->mvLevelSigma2[kp2.octave]) with the camera pair and relative pose the reference selects from
+ * the keypoints' sides (ORBmatcher.cc:1036-1074). idx1 / idx2 index KF1->keys / KF2->keys (mvKeys ++
+ * mvKeysRight for a two-camera keyframe). Nonzero = the pair passes. */
+typedef int32_t (*orbfe_epipolar_fn)(void* ctx, int32_t idx1, int32_t idx2);
+
+/* SearchForTriangulation(pKF1, pKF2, vMatchedPairs, bOnlyStereo, bCoarse = false) with the epipolar test
+ * left to the caller: the form for keyframes with a second camera, whose KannalaBrandt8::epipolarConstrain
+ * (TriangulateMatches, an Eigen JacobiSVD triangulation) runs on the host with the camera models. The
+ * device lists, per KF1 keypoint of a shared vocabulary node, the KF2 candidates that pass every other
+ * gate of the reference's loop (:1002-1033: no map point, bOnlyStereo, dist <= TH_LOW, the epipole
+ * distance to ep unless KF1 has a second camera), in ascending (dist, reverse node order); the
+ * reference keeps the last candidate of the smallest passing dist, which is the first of this order
+ * that passes, so epipolar() is called only until then (never more often than the reference calls
+ * it). Then the rotation-histogram filter with checkOri (:1114-1131). matches12 as
+ * orbfe_search_for_triangulation. Returns nmatches. */
+int orbfe_search_for_triangulation_epi(const orbfe_frame* KF1, const int32_t* mp1, const orbfe_feature_vector* fv1,
+                                       const orbfe_frame* KF2, const int32_t* mp2, const orbfe_feature_vector* fv2,
+                                       const float* ep, int32_t bOnlyStereo, int32_t checkOri,
+                                       orbfe_epipolar_fn epipolar, void* ctx, int32_t* matches12);
+
 /* A Sophus pose as the reference stores it: quaternion (x, y, z, w) + translation.
  * kind ORBFE_SE3: Sophus::SE3f, unit quaternion, p' = (p + w*uv + v x uv) + t with uv = 2 (v x p)
  *                 (sophus/so3.hpp:358-367, se3.hpp:321-324);
@@ -479,13 +502,25 @@ int orbfe_fuse_rig(const orbfe_frame* KF, const orbfe_kf_camera* cam, const orbf
 int orbfe_search_by_projection_sim3(const orbfe_frame* KF, const orbfe_kf_camera* cam, const orbfe_map_point_3d* pts,
                                     int32_t n, const int32_t* point_kfs, int32_t th, float ratioHamming,
                                     int32_t* matched, int32_t* matched_kf);
+/* The same with the keyframe's camera model (model = pKF->mpCamera; NULL = the pinhole expression on
+ * cam's intrinsics): the first overload projects with pKF->mpCamera->project (:465; KannalaBrandt8 on the
+ * device with the glibc atan2f / cosf / sinf ports), the vpPointsKFs overload (point_kfs != NULL) with
+ * fx * x * invz + cx for every camera (:571-576). A keyframe with a second camera (KF->two_cams) is
+ * searched on its left grid with mvKeys (KeyFrame::GetFeaturesInArea(.., bRight = false),
+ * KeyFrame.cc:707-751); orbfe_search_by_projection_sim3 refuses it without point_kfs. */
+int orbfe_search_by_projection_sim3_rig(const orbfe_frame* KF, const orbfe_kf_camera* cam,
+                                        const orbfe_camera_model* model, const orbfe_map_point_3d* pts, int32_t n,
+                                        const int32_t* point_kfs, int32_t th, float ratioHamming, int32_t* matched,
+                                        int32_t* matched_kf);
 
 /* SearchBySim3(pKF1, pKF2, vpMatches12, S12, th) (ORBmatcher.cc:1457-1674). pts1[KF1->n] /
  * pts2[KF2->n]: the keyframes' GetMapPointMatches() (id < 0 = NULL, flags BAD = isBad()).
  * cam1 = {T1w, pKF1 intrinsics (used for both projections), pKF1->mfLogScaleFactor};
  * cam2 = {T2w, log scale factor of pKF2}; S12 / S21 Sim3 poses. matches12 = vpMatches12 handles
  * (in/out); matched_idx2[i] = get<0>(vpMatches12[i]->GetIndexInKeyFrame(pKF2)) for the initial
- * matches (-1 otherwise). Returns nFound. */
+ * matches (-1 otherwise). Keyframes with a second camera are searched on their left grids (mvKeys);
+ * the reference projects every camera with the pinhole expression on pKF1's fx, fy, cx, cy
+ * (:1514-1519,1594-1599), so no camera model is needed. Returns nFound. */
 int orbfe_search_by_sim3(const orbfe_frame* KF1, const orbfe_frame* KF2, const orbfe_map_point_3d* pts1,
                          const orbfe_map_point_3d* pts2, const orbfe_kf_camera* cam1, const orbfe_kf_camera* cam2,
                          const orbfe_pose* S12, const orbfe_pose* S21, float th, int32_t* matches12,

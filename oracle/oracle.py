@@ -127,6 +127,10 @@ def stereo_match(ext_l: OracleExtractor, ext_r: OracleExtractor, kl, dl, kr, dr,
 
 
 # ---- ORBmatcher oracle (oracle/orb_oracle_match.cpp): same snapshot structs as the product API ----
+# int32_t (*)(void* ctx, int32_t idx1, int32_t idx2): the caller's epipolar test for a keypoint pair
+EPIPOLAR_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32)
+
+
 def _match_sigs(L):
     vp, ci, cf = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
     L.oro_sbp_local.argtypes = [vp, vp, vp, vp, ci, cf, ci, cf, cf]
@@ -143,6 +147,8 @@ def _match_sigs(L):
     L.oro_fuse_rig.argtypes = [vp, vp, vp, vp, vp, ci, cf, ci, ci, vp, vp]
     L.oro_search_by_bow_kf2.argtypes = [vp, vp, vp, ci, ci, vp, vp, vp, vp, ci, ci, vp, vp, cf, ci]
     L.oro_sbp_sim3.argtypes = [vp, vp, vp, ci, vp, ci, cf, vp, vp]
+    L.oro_sbp_sim3_rig.argtypes = [vp, vp, vp, vp, ci, vp, ci, cf, vp, vp]
+    L.oro_search_for_triangulation_epi.argtypes = [vp, vp, vp, vp, vp, vp, vp, ci, ci, EPIPOLAR_FN, vp, vp]
     L.oro_search_by_sim3.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, cf, vp, vp]
     L.oro_is_in_frustum.argtypes = [vp, vp, vp, ci, vp]
     L.oro_search_local_points.argtypes = [vp, vp, vp, ci, vp, vp, cf, ci, cf, cf, vp]
@@ -230,12 +236,26 @@ class OracleMatcher:
                                 bi.ctypes.data, bd.ctypes.data)
         return n, bi, bd
 
-    def sbp_sim3(self, KF, cam, pts, matched, th=10, ratioHamming=1.0, point_kfs=None, matched_kf=None):
+    def sbp_sim3(self, KF, cam, pts, matched, th=10, ratioHamming=1.0, point_kfs=None, matched_kf=None, model=None):
         p = np.ascontiguousarray(pts)
         pk = None if point_kfs is None else np.ascontiguousarray(point_kfs, np.int32)
-        return self.L.oro_sbp_sim3(KF.ref(), ctypes.byref(cam), p.ctypes.data, len(p),
-                                   None if pk is None else pk.ctypes.data, int(th), float(ratioHamming),
-                                   matched.ctypes.data, None if matched_kf is None else matched_kf.ctypes.data)
+        return self.L.oro_sbp_sim3_rig(KF.ref(), ctypes.byref(cam), None if model is None else ctypes.byref(model),
+                                       p.ctypes.data, len(p), None if pk is None else pk.ctypes.data, int(th),
+                                       float(ratioHamming), matched.ctypes.data,
+                                       None if matched_kf is None else matched_kf.ctypes.data)
+
+    def search_for_triangulation_epi(self, KF1, mp1, fv1, KF2, mp2, fv2, ep, epi, bOnlyStereo=False):
+        """SearchForTriangulation with bCoarse false, the epipolar test delegated to epi(idx1, idx2) -> bool
+        (pCamera1->epipolarConstrain for that keypoint pair)."""
+        m1 = np.ascontiguousarray(mp1, np.int32)
+        m2 = np.ascontiguousarray(mp2, np.int32)
+        e = np.ascontiguousarray(ep, np.float32).reshape(2)
+        out = np.full(KF1.N, -1, np.int32)
+        cb = EPIPOLAR_FN(lambda ctx, i1, i2: 1 if epi(i1, i2) else 0)
+        n = self.L.oro_search_for_triangulation_epi(KF1.ref(), m1.ctypes.data, fv1.ref(), KF2.ref(), m2.ctypes.data,
+                                                    fv2.ref(), e.ctypes.data, int(bOnlyStereo), self.checkOri, cb,
+                                                    None, out.ctypes.data)
+        return n, out
 
     def search_by_sim3(self, KF1, KF2, pts1, pts2, cam1, cam2, S12, S21, th, matches12, matched_idx2=None):
         p1, p2 = np.ascontiguousarray(pts1), np.ascontiguousarray(pts2)

@@ -609,10 +609,16 @@ static bool epipolar(const orbfe_keypoint& kp1, const orbfe_keypoint& kp2, const
     return dsqr < 3.84 * unc;
 }
 
-int oro_search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, const orbfe_feature_vector* fv1,
-                                 const orbfe_frame* KF2, const int32_t* mp2, const orbfe_feature_vector* fv2,
-                                 const float* F12, const float* ep, const float* level_sigma2_2, int32_t bOnlyStereo,
-                                 int32_t bCoarse, int32_t checkOri, int32_t* matches12) {
+typedef int32_t (*oro_epipolar_fn)(void* ctx, int32_t idx1, int32_t idx2);
+
+// epi != NULL: pCamera1->epipolarConstrain(pCamera2, kp1, kp2, R12, t12, sigma1, sigma2) as the
+// caller evaluates it for the keypoint pair (idx1, idx2) (two-camera keyframes with bCoarse false,
+// ORBmatcher.cc:1036-1074); NULL: the pinhole test on F12.
+static int search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, const orbfe_feature_vector* fv1,
+                                    const orbfe_frame* KF2, const int32_t* mp2, const orbfe_feature_vector* fv2,
+                                    const float* F12, const float* ep, const float* level_sigma2_2, int32_t bOnlyStereo,
+                                    int32_t bCoarse, int32_t checkOri, int32_t* matches12, oro_epipolar_fn epi,
+                                    void* ctx) {
     std::vector<int> rotHist[HISTO_LENGTH];
     for (int i = 0; i < KF1->n; i++) matches12[i] = -1;
     int nmatches = 0;
@@ -641,7 +647,8 @@ int oro_search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, con
                         const float distey = ep[1] - kp2.y;
                         if (distex * distex + distey * distey < 100 * KF2->scale_factors[kp2.octave]) continue;
                     }
-                    if (bCoarse || epipolar(kp1, kp2, F12, level_sigma2_2[kp2.octave])) {
+                    if (bCoarse || (epi ? epi(ctx, (int32_t)idx1, (int32_t)idx2) != 0
+                                        : epipolar(kp1, kp2, F12, level_sigma2_2[kp2.octave]))) {
                         bestIdx2 = (int)idx2;
                         bestDist = dist;
                     }
@@ -669,6 +676,22 @@ int oro_search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, con
         }
     }
     return nmatches;
+}
+
+int oro_search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, const orbfe_feature_vector* fv1,
+                                 const orbfe_frame* KF2, const int32_t* mp2, const orbfe_feature_vector* fv2,
+                                 const float* F12, const float* ep, const float* level_sigma2_2, int32_t bOnlyStereo,
+                                 int32_t bCoarse, int32_t checkOri, int32_t* matches12) {
+    return search_for_triangulation(KF1, mp1, fv1, KF2, mp2, fv2, F12, ep, level_sigma2_2, bOnlyStereo, bCoarse,
+                                    checkOri, matches12, nullptr, nullptr);
+}
+
+int oro_search_for_triangulation_epi(const orbfe_frame* KF1, const int32_t* mp1, const orbfe_feature_vector* fv1,
+                                     const orbfe_frame* KF2, const int32_t* mp2, const orbfe_feature_vector* fv2,
+                                     const float* ep, int32_t bOnlyStereo, int32_t checkOri, oro_epipolar_fn epi,
+                                     void* ctx, int32_t* matches12) {
+    return search_for_triangulation(KF1, mp1, fv1, KF2, mp2, fv2, nullptr, ep, nullptr, bOnlyStereo, 0, checkOri,
+                                    matches12, epi, ctx);
 }
 
 // The search half of both Fuse overloads; best_dist = -1 when no candidate survived the checks.
@@ -742,9 +765,19 @@ int oro_fuse(const orbfe_frame* KF, const orbfe_kf_camera* cam, const float* inv
     return oro_fuse_rig(KF, cam, nullptr, inv_level_sigma2, pts, n, th, sim3, 0, best_idx, best_dist);
 }
 
-int oro_sbp_sim3(const orbfe_frame* KF, const orbfe_kf_camera* cam, const orbfe_map_point_3d* pts, int32_t n,
-                 const int32_t* point_kfs, int32_t th, float ratioHamming, int32_t* matched, int32_t* matched_kf) {
-    const Grid grid(KF);
+// model: pKF->mpCamera for the first overload (pKF->mpCamera->project, ORBmatcher.cc:465; NULL = the
+// pinhole expression with cam's intrinsics); the vpPointsKFs overload always projects with
+// fx * x * invz + cx (:571-576). A two-camera keyframe is searched on its left grid with mvKeys
+// (KeyFrame::GetFeaturesInArea(.., bRight = false), KeyFrame.cc:707-751).
+int oro_sbp_sim3_rig(const orbfe_frame* KF, const orbfe_kf_camera* cam, const orbfe_camera_model* model,
+                     const orbfe_map_point_3d* pts, int32_t n, const int32_t* point_kfs, int32_t th,
+                     float ratioHamming, int32_t* matched, int32_t* matched_kf) {
+    const Grid grid(KF, KF->two_cams ? 0 : -1);
+    CamModel M{ORBFE_CAM_PINHOLE, {cam->fx, cam->fy, cam->cx, cam->cy, 0.f, 0.f, 0.f, 0.f}};
+    if (model) {
+        M.type = model->type;
+        memcpy(M.p, model->params, sizeof(M.p));
+    }
     std::vector<int32_t> found;
     for (int k = 0; k < KF->n; k++)
         if (matched[k] >= 0) found.push_back(matched[k]);
@@ -759,8 +792,7 @@ int oro_sbp_sim3(const orbfe_frame* KF, const orbfe_kf_camera* cam, const orbfe_
         if (p3Dc[2] < 0.0) continue;
         float u, v;
         if (!point_kfs) {
-            u = cam->fx * p3Dc[0] / p3Dc[2] + cam->cx;
-            v = cam->fy * p3Dc[1] / p3Dc[2] + cam->cy;
+            cam_project(M, p3Dc, u, v);   // pKF->mpCamera->project (Pinhole: fx * x / z + cx)
         } else {
             const float invz = 1 / p3Dc[2];
             const float x = p3Dc[0] * invz, y = p3Dc[1] * invz;
@@ -793,6 +825,11 @@ int oro_sbp_sim3(const orbfe_frame* KF, const orbfe_kf_camera* cam, const orbfe_
         }
     }
     return nmatches;
+}
+
+int oro_sbp_sim3(const orbfe_frame* KF, const orbfe_kf_camera* cam, const orbfe_map_point_3d* pts, int32_t n,
+                 const int32_t* point_kfs, int32_t th, float ratioHamming, int32_t* matched, int32_t* matched_kf) {
+    return oro_sbp_sim3_rig(KF, cam, nullptr, pts, n, point_kfs, th, ratioHamming, matched, matched_kf);
 }
 
 // One direction of SearchBySim3: points of A transformed by TAw then SBA, searched in B.
@@ -842,7 +879,9 @@ int oro_search_by_sim3(const orbfe_frame* KF1, const orbfe_frame* KF2, const orb
             const int idx2 = matched_idx2 ? matched_idx2[i] : -1;
             if (idx2 >= 0 && idx2 < N2) already2[idx2] = 1;
         }
-    const Grid g1(KF1), g2(KF2);
+    // pKF->GetFeaturesInArea(u, v, r): the left grid (mvKeys) of a two-camera keyframe; every
+    // camera projects with pKF1's fx, fy, cx, cy (ORBmatcher.cc:1459-1462,1514-1519,1594-1599)
+    const Grid g1(KF1, KF1->two_cams ? 0 : -1), g2(KF2, KF2->two_cams ? 0 : -1);
     std::vector<int> vnMatch1, vnMatch2;
     sim3_side(KF2, g2, pts1, N1, already1, cam1->Tcw, *S21, cam1, cam2->log_scale_factor, th, vnMatch1);
     sim3_side(KF1, g1, pts2, N2, already2, cam2->Tcw, *S12, cam1, cam1->log_scale_factor, th, vnMatch2);
@@ -983,6 +1022,7 @@ int oro_is_in_frustum_rig(const orbfe_frame* F, const orbfe_camera* cam, const o
         const orbfe_map_point_3d& p = pts[i];
         orbfe_map_point& t = track[i];
         memset(&t, 0, sizeof(t));
+        t.depth = p.track_depth;   // mTrackDepth persists unless a left view passes (Frame.cc:565,1237)
         t.flags = p.flags & ORBFE_MP_BAD;
         t.observations = p.observations;
         t.id = p.id;

@@ -21,6 +21,10 @@ ORBFE_NUM_STAGES = 3
 STAGE_NAMES = ("pyramid_fast", "octree", "describe")
 
 
+# orbfe_epipolar_fn: int32_t (*)(void* ctx, int32_t idx1, int32_t idx2)
+EPIPOLAR_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32)
+
+
 class OrbKeyPoint(ctypes.Structure):
     """cv::KeyPoint byte layout (28 B)."""
     _fields_ = [("x", ctypes.c_float), ("y", ctypes.c_float), ("size", ctypes.c_float),
@@ -73,6 +77,9 @@ _SIGS = {
                                                 _vp]),
     "orbfe_fuse": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _c_float, _c_int, _vp, _vp]),
     "orbfe_search_by_projection_sim3": (_c_int, [_vp, _vp, _vp, _c_int, _vp, _c_int, _c_float, _vp, _vp]),
+    "orbfe_search_by_projection_sim3_rig": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _vp, _c_int, _c_float, _vp, _vp]),
+    "orbfe_search_for_triangulation_epi": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _c_int, EPIPOLAR_FN,
+                                                    _vp, _vp]),
     "orbfe_search_by_sim3": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_float, _vp, _vp]),
     "orbfe_stereo_knn_ratio": (_c_int, [_vp, _c_int, _vp, _c_int, _c_float, _vp, _vp]),
     "orbfe_stereo_knn_batch": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp,

@@ -356,6 +356,57 @@ __global__ __launch_bounds__(MT_NT) void k_tri(const int2* items, int nitems, co
     if (bestIdx2 >= 0) out_idx[i1] = bestIdx2;
 }
 
+// SearchForTriangulation with the caller's epipolar test (bCoarse false on keyframes with a second
+// camera, whose KannalaBrandt8 test is a host-side JacobiSVD triangulation): one thread per KF1
+// keypoint of a shared node lists the node's KF2 candidates that pass every other gate of the
+// reference's loop (ORBmatcher.cc:1002-1033: no map point, bOnlyStereo, dist <= TH_LOW, the epipole
+// distance), sorted by (dist ascending, node order descending). The loop keeps a candidate when its
+// dist <= bestDist and the epipolar test passes, so its result is the LAST passing candidate of the
+// smallest passing dist: the first passing entry of this order. seg_off[t] = the item's segment (its
+// node's size), cnt[t] = candidates listed, cand = KF2 indices.
+__global__ __launch_bounds__(MT_NT) void k_tri_cand(const int2* items, int nitems, const int* seg_off,
+                                                    const uint32_t* idx1s, const int* off2, const uint32_t* idx2s,
+                                                    const OrbKeyPoint* k2, const uint32_t* d1, const uint32_t* d2,
+                                                    const float* ur1, const float* ur2, const int32_t* mp1,
+                                                    const int32_t* mp2, const float* scale2, TriArgs a, int* cnt,
+                                                    uint32_t* cand) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nitems) return;
+    const int2 it = items[t];
+    const unsigned i1 = idx1s[it.x];
+    int nc = 0;
+    const bool bStereo1 = !a.two1 && ur1 && ur1[i1] >= 0;
+    if (mp1[i1] < 0 && !(a.bOnlyStereo && !bStereo1)) {
+        uint32_t q[8];
+#pragma unroll
+        for (int w = 0; w < 8; w++) q[w] = d1[8 * i1 + w];
+        uint32_t* out = cand + seg_off[t];
+        const int base = off2[it.y];
+        for (int ib = base; ib < off2[it.y + 1]; ib++) {
+            const unsigned i2 = idx2s[ib];
+            if (mp2[i2] >= 0) continue;
+            const bool bStereo2 = !a.two2 && ur2 && ur2[i2] >= 0;
+            if (a.bOnlyStereo && !bStereo2) continue;
+            int dist = 0;
+#pragma unroll
+            for (int w = 0; w < 8; w++) dist += __popc(q[w] ^ d2[8 * i2 + w]);
+            if (dist > MT_TH_LOW) continue;
+            if (!bStereo1 && !bStereo2 && !a.two1) {
+                const OrbKeyPoint kp2 = k2[i2];
+                const float distex = a.ep[0] - kp2.x, distey = a.ep[1] - kp2.y;
+                if (distex * distex + distey * distey < 100 * scale2[kp2.octave]) continue;
+            }
+            // (dist, reverse node position): ascending order = the test order
+            const uint32_t key = ((uint32_t)dist << 20) | (0xFFFFFu - (uint32_t)(ib - base));
+            int j = nc++;
+            for (; j > 0 && out[j - 1] > key; j--) out[j] = out[j - 1];
+            out[j] = key;
+        }
+        for (int j = 0; j < nc; j++) out[j] = idx2s[base + (int)(0xFFFFFu - (out[j] & 0xFFFFFu))];
+    }
+    cnt[t] = nc;
+}
+
 extern "C" {
 
 int orbfe_search_by_bow_kf(const orbfe_keypoint* keys1, const uint8_t* desc1, const int32_t* mp1, int32_t n1,
@@ -589,6 +640,109 @@ int orbfe_search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, c
     return nm;
 }
 
+int orbfe_search_for_triangulation_epi(const orbfe_frame* KF1, const int32_t* mp1, const orbfe_feature_vector* fv1,
+                                       const orbfe_frame* KF2, const int32_t* mp2, const orbfe_feature_vector* fv2,
+                                       const float* ep, int32_t bOnlyStereo, int32_t checkOri,
+                                       orbfe_epipolar_fn epipolar, void* ctx, int32_t* matches12) {
+    if (!frame_ok(KF1) || !frame_ok(KF2) || !ep || !epipolar || (KF1->n > 0 && (!mp1 || !matches12)) ||
+        (KF2->n > 0 && !mp2))
+        return ORBFE_E_ARG;
+    const int n1 = KF1->n, n2 = KF2->n;
+    for (int i = 0; i < n1; i++) matches12[i] = -1;
+    if (!fv_ok(fv1, n1) || !fv_ok(fv2, n2)) return ORBFE_E_ARG;
+    if (n1 == 0 || n2 == 0) return 0;
+    if (!octaves_ok(KF1) || !octaves_ok(KF2)) return ORBFE_E_ARG;
+    // one item per KF1 entry of a shared node (:961-966), its candidate segment sized by the KF2 node
+    std::vector<int2> items;
+    std::vector<int> seg;
+    size_t total = 0;
+    int a = 0, b = 0;
+    while (a < fv1->n_nodes && b < fv2->n_nodes) {
+        if (fv1->node_ids[a] == fv2->node_ids[b]) {
+            const int nb = fv2->offsets[b + 1] - fv2->offsets[b];
+            if (nb >= (1 << 20)) return ORBFE_E_CAPACITY;   // k_tri_cand packs the node position in 20 bits
+            for (int ia = fv1->offsets[a]; ia < fv1->offsets[a + 1]; ia++) {
+                items.push_back(make_int2(ia, b));
+                seg.push_back((int)total);
+                total += (size_t)nb;
+            }
+            a++;
+            b++;
+        } else if (fv1->node_ids[a] < fv2->node_ids[b]) a++;
+        else b++;
+    }
+    if (items.empty()) return 0;
+    if (total > (size_t)INT_MAX / 4) return ORBFE_E_CAPACITY;
+    const int nitems = (int)items.size();
+    const int m1 = fv1->offsets[fv1->n_nodes], m2 = fv2->offsets[fv2->n_nodes];
+    Plan p;
+    const size_t o_items = p.upload(items.data(), items.size() * sizeof(int2));
+    const size_t o_seg = p.upload(seg.data(), seg.size() * 4);
+    const size_t o_idx1 = p.upload(fv1->indices, (size_t)m1 * 4);
+    const size_t o_off2 = p.upload(fv2->offsets, (size_t)(fv2->n_nodes + 1) * 4);
+    const size_t o_idx2 = p.upload(fv2->indices, (size_t)m2 * 4);
+    const size_t o_k2 = p.upload(KF2->keys, (size_t)n2 * sizeof(orbfe_keypoint));
+    const size_t o_d1 = p.upload(KF1->desc, (size_t)n1 * 32), o_d2 = p.upload(KF2->desc, (size_t)n2 * 32);
+    const bool u1 = KF1->uright && !KF1->two_cams, u2 = KF2->uright && !KF2->two_cams;
+    const size_t o_u1 = u1 ? p.upload(KF1->uright, (size_t)n1 * 4) : 0;
+    const size_t o_u2 = u2 ? p.upload(KF2->uright, (size_t)n2 * 4) : 0;
+    const size_t o_mp1 = p.upload(mp1, (size_t)n1 * 4), o_mp2 = p.upload(mp2, (size_t)n2 * 4);
+    const size_t o_sc2 = p.upload(KF2->scale_factors, (size_t)KF2->nlevels * 4);
+    const size_t o_cnt = p.scratch((size_t)nitems * 4), o_cand = p.scratch(std::max<size_t>(total, 1) * 4);
+    int rc = ms_prepare(p);
+    if (rc) return rc;
+    MsTimer timer;
+    hipStream_t s = t_ms.stream;
+    TriArgs ta;
+    memset(&ta, 0, sizeof(ta));
+    ta.ep[0] = ep[0];
+    ta.ep[1] = ep[1];
+    ta.bOnlyStereo = bOnlyStereo != 0;
+    ta.two1 = KF1->two_cams != 0;
+    ta.two2 = KF2->two_cams != 0;
+    hipLaunchKernelGGL(k_tri_cand, dim3((nitems + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, ms_ptr<const int2>(o_items),
+                       nitems, ms_ptr<const int>(o_seg), ms_ptr<const uint32_t>(o_idx1), ms_ptr<const int>(o_off2),
+                       ms_ptr<const uint32_t>(o_idx2), ms_ptr<const OrbKeyPoint>(o_k2), ms_ptr<const uint32_t>(o_d1),
+                       ms_ptr<const uint32_t>(o_d2), u1 ? ms_ptr<const float>(o_u1) : nullptr,
+                       u2 ? ms_ptr<const float>(o_u2) : nullptr, ms_ptr<const int32_t>(o_mp1),
+                       ms_ptr<const int32_t>(o_mp2), ms_ptr<const float>(o_sc2), ta, ms_ptr<int>(o_cnt),
+                       ms_ptr<uint32_t>(o_cand));
+    HIPCHK(hipGetLastError());
+    timer.end();
+    std::vector<int> cnt(nitems);
+    std::vector<uint32_t> cand(std::max<size_t>(total, 1));
+    HIPCHK(hipMemcpyAsync(cnt.data(), ms_ptr<int>(o_cnt), (size_t)nitems * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(cand.data(), ms_ptr<uint32_t>(o_cand), total * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    // the caller's test in the candidates' order; the first pass is the reference's bestIdx2
+    int nmatches = 0;
+    int hist[MT_HISTO] = {0};
+    for (int t = 0; t < nitems; t++) {
+        const int i1 = (int)fv1->indices[items[t].x];
+        for (int j = 0; j < cnt[t]; j++) {
+            const int i2 = (int)cand[(size_t)seg[t] + j];
+            if (epipolar(ctx, i1, i2)) {
+                matches12[i1] = i2;
+                nmatches++;
+                if (checkOri) hist[mt_rot_bin(KF1->keys[i1].angle, KF2->keys[i2].angle)]++;
+                break;
+            }
+        }
+    }
+    // the rotation-histogram filter (:1114-1131): entries outside the three maxima are dropped
+    if (checkOri && nmatches > 0) {
+        const unsigned keep = mt_three_maxima_keep(hist);
+        for (int i = 0; i < n1; i++) {
+            const int i2 = matches12[i];
+            if (i2 >= 0 && !((keep >> mt_rot_bin(KF1->keys[i].angle, KF2->keys[i2].angle)) & 1u)) {
+                matches12[i] = -1;
+                nmatches--;
+            }
+        }
+    }
+    return nmatches;
+}
+
 int orbfe_fuse(const orbfe_frame* KF, const orbfe_kf_camera* cam, const float* inv_level_sigma2,
                const orbfe_map_point_3d* pts, int32_t n, float th, int32_t sim3, int32_t* best_idx,
                int32_t* best_dist) {
@@ -652,8 +806,19 @@ int orbfe_fuse_rig(const orbfe_frame* KF, const orbfe_kf_camera* cam, const orbf
 int orbfe_search_by_projection_sim3(const orbfe_frame* KF, const orbfe_kf_camera* cam, const orbfe_map_point_3d* pts,
                                     int32_t n, const int32_t* point_kfs, int32_t th, float ratioHamming,
                                     int32_t* matched, int32_t* matched_kf) {
-    if (!frame1_ok(KF) || !cam || !pose_ok(&cam->Tcw) || n < 0 || (n > 0 && !pts) || (KF->n > 0 && !matched) ||
-        (point_kfs && KF->n > 0 && !matched_kf))
+    // the pinhole API: the first overload on a two-camera keyframe needs its camera model
+    if (KF && KF->two_cams && !point_kfs) return ORBFE_E_ARG;
+    return orbfe_search_by_projection_sim3_rig(KF, cam, nullptr, pts, n, point_kfs, th, ratioHamming, matched,
+                                               matched_kf);
+}
+
+int orbfe_search_by_projection_sim3_rig(const orbfe_frame* KF, const orbfe_kf_camera* cam,
+                                        const orbfe_camera_model* model, const orbfe_map_point_3d* pts, int32_t n,
+                                        const int32_t* point_kfs, int32_t th, float ratioHamming, int32_t* matched,
+                                        int32_t* matched_kf) {
+    if (!frame_ok(KF) || !cam || !pose_ok(&cam->Tcw) || n < 0 || (n > 0 && !pts) || (KF->n > 0 && !matched) ||
+        (point_kfs && KF->n > 0 && !matched_kf) ||
+        (model && model->type != ORBFE_CAM_PINHOLE && model->type != ORBFE_CAM_KANNALA_BRANDT8))
         return ORBFE_E_ARG;
     if (n == 0 || KF->n == 0) return 0;
     if (n > (1 << 24)) return ORBFE_E_CAPACITY;
@@ -688,6 +853,12 @@ int orbfe_search_by_projection_sim3(const orbfe_frame* KF, const orbfe_kf_camera
     const FrameDev fr = fp.view();
     fp.launch_grid(fr);
     KfGeom g = kf_geom(cam, KF, cam->log_scale_factor, point_kfs ? BE_PRJ_INVZ_F : BE_PRJ_PINHOLE, 0, 1);
+    if (model && !point_kfs) {   // pKF->mpCamera->project (ORBmatcher.cc:465)
+        g.proj = BE_PRJ_MODEL;
+        g.cam_type = model->type;
+        g.fx = model->params[0]; g.fy = model->params[1]; g.cx = model->params[2]; g.cy = model->params[3];
+        for (int k = 0; k < 4; k++) g.kb[k] = model->type == ORBFE_CAM_KANNALA_BRANDT8 ? model->params[4 + k] : 0.f;
+    }
     g.skip_flags = ORBFE_MP_BAD;   // spAlreadyFound is the skip array
     const dim3 gq((n + MT_NT - 1) / MT_NT);
     hipLaunchKernelGGL(k_kf_geom, gq, dim3(MT_NT), 0, s, g, ms_ptr<const orbfe_map_point_3d>(o_pts), n,
@@ -734,7 +905,9 @@ int orbfe_search_by_sim3(const orbfe_frame* KF1, const orbfe_frame* KF2, const o
                          const orbfe_map_point_3d* pts2, const orbfe_kf_camera* cam1, const orbfe_kf_camera* cam2,
                          const orbfe_pose* S12, const orbfe_pose* S21, float th, int32_t* matches12,
                          const int32_t* matched_idx2) {
-    if (!frame1_ok(KF1) || !frame1_ok(KF2) || !cam1 || !cam2 || !pose_ok(&cam1->Tcw) || !pose_ok(&cam2->Tcw) ||
+    // two-camera keyframes are searched on their left grids (mvKeys), every camera with the pinhole
+    // expression on pKF1's intrinsics as the reference does (ORBmatcher.cc:1514-1519,1594-1599)
+    if (!frame_ok(KF1) || !frame_ok(KF2) || !cam1 || !cam2 || !pose_ok(&cam1->Tcw) || !pose_ok(&cam2->Tcw) ||
         !pose_ok(S12) || !pose_ok(S21) || (KF1->n > 0 && (!pts1 || !matches12)) || (KF2->n > 0 && !pts2))
         return ORBFE_E_ARG;
     const int n1 = KF1->n, n2 = KF2->n;

@@ -303,7 +303,7 @@ static int build_geom(const orbfe_extractor* h, int W, int H, OrbGeom& g, std::v
     fast_lds = fl;
     oct_lds = octree_lds_bytes(g);
     if (oct_lds > 160 * 1024) return ORBFE_E_ARG;
-    if ((size_t)4 * fast_lds.wave_bytes > 160 * 1024) return ORBFE_E_ARG;   // k_fast: 4 waves per block
+    if ((size_t)FAST_WPB * fast_lds.wave_bytes > 160 * 1024) return ORBFE_E_ARG;   // k_fast: FAST_WPB waves per block
     return ORBFE_OK;
 }
 

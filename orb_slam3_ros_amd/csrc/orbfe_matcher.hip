@@ -746,7 +746,8 @@ __global__ __launch_bounds__(MT_NT) void k_frustum(CamDev c, const orbfe_map_poi
     if (i >= n) return;
     const orbfe_map_point_3d p = pts[i];
     orbfe_map_point t;
-    t.proj_x = -1.f; t.proj_y = -1.f; t.proj_xr = 0.f; t.view_cos = 0.f; t.depth = 0.f;
+    // mTrackDepth is only written by a passing left view: otherwise the previous value stays
+    t.proj_x = -1.f; t.proj_y = -1.f; t.proj_xr = 0.f; t.view_cos = 0.f; t.depth = p.track_depth;
     t.scale_level = 0;
     t.flags = p.flags & ORBFE_MP_BAD;
     t.observations = p.observations;
@@ -803,7 +804,7 @@ __global__ __launch_bounds__(MT_NT) void k_frustum(CamDev c, const orbfe_map_poi
 }
 
 // rotation-histogram bin of an accepted match (ORBmatcher.cc:1775-1792): round(rot * (1/30)).
-__device__ __forceinline__ int mt_rot_bin(float a1, float a2) {
+__host__ __device__ __forceinline__ int mt_rot_bin(float a1, float a2) {
     const float factor = 1.0f / MT_HISTO;
     float rot = a1 - a2;
     if (rot < 0.0) rot += 360.0f;
@@ -813,7 +814,7 @@ __device__ __forceinline__ int mt_rot_bin(float a1, float a2) {
 }
 
 // ComputeThreeMaxima (ORBmatcher.cc:2012-2053) on 30 bin counts -> keep mask.
-__device__ __forceinline__ unsigned mt_three_maxima_keep(const int* hist) {
+__host__ __device__ __forceinline__ unsigned mt_three_maxima_keep(const int* hist) {
     int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
     for (int i = 0; i < MT_HISTO; i++) {
         const int s = hist[i];
@@ -1233,6 +1234,12 @@ struct MatchScratch {
     int* hs_dev = nullptr;  // hs as the device addresses it (kernels store the status there)
     int seq = 0;            // sequence number of the last published status
     int pass_hint[3] = {4, 4, 4};   // passes the previous single-camera search of each mode needed
+    // A device-resident search returns as soon as its status words are published, before its last
+    // commit block has retired (and reset its completion counter): `tail` is recorded on its stream
+    // after the last launch, and the next call of this thread orders its own stream after it when
+    // that is a different stream (ms_after_tail), so the shared scratch is never reused early.
+    hipEvent_t tail = nullptr;
+    hipStream_t tail_stream = nullptr;
     // Deliberately never freed: thread_local destructors of the main thread can run after the HIP
     // runtime has been torn down at exit; the arena is reused for the thread's lifetime.
 };
@@ -1277,6 +1284,12 @@ struct Plan {
     size_t scratch(size_t bytes) { const size_t o = end; end += a256(bytes); return o; }
 };
 
+// order stream s after the previous device-resident search of this thread (see MatchScratch::tail)
+hipError_t ms_after_tail(hipStream_t s) {
+    if (t_ms.tail_stream && t_ms.tail_stream != s) return hipStreamWaitEvent(s, t_ms.tail, 0);
+    return hipSuccess;
+}
+
 int ms_prepare(const Plan& p) {
     MatchScratch& m = t_ms;
     int dev = 0;
@@ -1286,8 +1299,13 @@ int ms_prepare(const Plan& p) {
         m.device = dev;
         HIPCHK(hipStreamCreateWithFlags(&m.stream, hipStreamNonBlocking));
         HIPCHK(hipHostMalloc((void**)&m.hs, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        // the status words are compared against sequence numbers: start from zeros, not from
+        // whatever the allocation held
+        memset(m.hs, 0, 64);
         HIPCHK(hipHostGetDevicePointer((void**)&m.hs_dev, m.hs, 0));
+        HIPCHK(hipEventCreateWithFlags(&m.tail, hipEventDisableTiming));
     }
+    HIPCHK(ms_after_tail(m.stream));
     if (p.end > m.dcap) {
         if (m.d) HIPCHK(hipFree(m.d));
         m.d = nullptr;
@@ -1528,10 +1546,11 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     const size_t o_hist = p.scratch((MT_HISTO + 1) * 4);   // rotation bins + commit completion counter
     int rc = ms_prepare(p);
     if (rc) return rc;
-    // a device-resident search runs on the caller's stream, after the producer of its inputs, with
-    // no cross-stream event (every call ends with a synchronisation, so the thread's scratch is free
-    // again before the next call uses it on either stream)
+    // a device-resident search runs on the caller's stream, after the producer of its inputs; it
+    // returns once its status is published and records MatchScratch::tail, after which the next
+    // call of the thread orders itself (host-API calls also end with a stream synchronisation)
     hipStream_t s = dev ? dev->caller : t_ms.stream;
+    if (dev) HIPCHK(ms_after_tail(s));
     MsTimer timer(s);
     const FrameDev fr = fp.view();
     const int* b0 = dev ? ms_ptr<const int>(o_b0d) : ms_ptr<const int>(o_b0);
@@ -1621,6 +1640,10 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
             const int seq = ++t_ms.seq;
             commit(changed + pass - 1, CommitStatus{t_ms.hs_dev, hist + MT_HISTO, changed + pass0, batch, seq});
             HIPCHK(hipGetLastError());
+            if (dev) {
+                HIPCHK(hipEventRecord(t_ms.tail, s));
+                t_ms.tail_stream = s;
+            }
             timer.end();
             if (!dev) {
                 HIPCHK(hipMemcpyAsync(mvp, mvp_d, (size_t)n * 4, hipMemcpyDeviceToHost, s));

@@ -281,6 +281,11 @@ int orbfe_remap_linear_batch(const uint8_t* const* d_src, int sw, int sh, int ss
         slot->key.insert(slot->key.end(), d_dst, d_dst + n);
         memcpy(slot->pinned, slot->key.data(), (size_t)2 * n * sizeof(void*));
         HIPCHK(hipMemcpyAsync(slot->dev, slot->pinned, (size_t)2 * n * sizeof(void*), hipMemcpyHostToDevice, s));
+    } else {
+        // a hit may come on another stream than the miss that uploaded the table (or than the
+        // slot's earlier readers): order this launch after the slot's last use, whose event
+        // follows the upload and, through this same wait on every hit, every earlier reader
+        HIPCHK(hipStreamWaitEvent(s, slot->done, 0));
     }
     slot->used = ++tick;
     const uint8_t* const* dsrc = (const uint8_t* const*)slot->dev;

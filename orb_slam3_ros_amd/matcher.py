@@ -28,7 +28,7 @@ PROJ_POINT_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("invzc", "<f4"), ("oct
                              ("valid", "<i4"), ("observations", "<i4"), ("id", "<i4"), ("desc", "u1", (32,))])
 # orbfe_map_point_3d (80 B): MapPoint geometry for the local-map projection (Frame::isInFrustum)
 MAP_POINT_3D_DTYPE = np.dtype([("pos", "<f4", (3,)), ("normal", "<f4", (3,)), ("min_dist", "<f4"), ("max_dist", "<f4"),
-                               ("flags", "<i4"), ("observations", "<i4"), ("id", "<i4"), ("reserved", "<i4"),
+                               ("flags", "<i4"), ("observations", "<i4"), ("id", "<i4"), ("track_depth", "<f4"),
                                ("desc", "u1", (32,))])
 assert MAP_POINT_DTYPE.itemsize == 80 and PROJ_POINT_DTYPE.itemsize == 64 and MAP_POINT_3D_DTYPE.itemsize == 80
 MP_IN_VIEW, MP_BAD, MP_SKIP, MP_IN_VIEW_R = 1, 2, 4, 8
@@ -415,6 +415,22 @@ class ORBmatcher:
             "SearchForTriangulation")
         return n, out
 
+    # SearchForTriangulation with bCoarse = false and the caller's epipolar test (keyframes with a
+    # second camera: KannalaBrandt8::epipolarConstrain on the host, ORBmatcher.cc:1036-1074)
+    def SearchForTriangulationEpi(self, KF1: MatchFrame, mp1, fv1: FeatureVector, KF2: MatchFrame, mp2,
+                                  fv2: FeatureVector, ep, epipolar, bOnlyStereo=False):
+        """epipolar(idx1, idx2) -> bool: pCamera1->epipolarConstrain for that keypoint pair. Returns
+        (nmatches, matches12) as SearchForTriangulation."""
+        m1 = _i32(np.ascontiguousarray(mp1, np.int32), KF1.N, "mp1")
+        m2 = _i32(np.ascontiguousarray(mp2, np.int32), KF2.N, "mp2")
+        e = np.ascontiguousarray(ep, np.float32).reshape(2)
+        out = np.full(KF1.N, -1, np.int32)
+        cb = _lib.EPIPOLAR_FN(lambda ctx, i1, i2: 1 if epipolar(i1, i2) else 0)
+        n = _lib.check(self._lib.orbfe_search_for_triangulation_epi(
+            KF1.ref(), m1.ctypes.data, fv1.ref(), KF2.ref(), m2.ctypes.data, fv2.ref(), e.ctypes.data,
+            int(bOnlyStereo), int(self.mbCheckOrientation), cb, None, out.ctypes.data), "SearchForTriangulation")
+        return n, out
+
     # Fuse(pKF, vpMapPoints, th) (:1148-1337) / Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (:1339-1455)
     def Fuse(self, KF: MatchFrame, cam: KFCamera, points3d, th=3.0, inv_level_sigma2=None, sim3=False,
              model: "CameraModel" = None, bRight: bool = False):
@@ -444,14 +460,20 @@ class ORBmatcher:
     # SearchByProjection(pKF, Scw, vpPoints, vpMatched, th, ratioHamming) (:427-523) and the
     # vpPointsKFs / vpMatchedKF overload (:525-646)
     def SearchByProjectionSim3(self, KF: MatchFrame, cam: KFCamera, points3d, vpMatched, th=10, ratioHamming=1.0,
-                               point_kfs=None, vpMatchedKF=None):
-        """vpMatched (and vpMatchedKF with point_kfs) int32 [KF.N] updated in place. Returns nmatches."""
+                               point_kfs=None, vpMatchedKF=None, model: "CameraModel" = None):
+        """vpMatched (and vpMatchedKF with point_kfs) int32 [KF.N] updated in place. model: pKF->mpCamera
+        (orbfe_search_by_projection_sim3_rig; None = the pinhole expression on cam). Returns nmatches."""
         pts = _records(points3d, MAP_POINT_3D_DTYPE, "points3d")
         m = _i32(vpMatched, KF.N, "vpMatched")
         pk = mk = None
         if point_kfs is not None:
             pk = _i32(np.ascontiguousarray(point_kfs, np.int32), len(pts), "point_kfs")
             mk = _i32(vpMatchedKF, KF.N, "vpMatchedKF")
+        if model is not None:
+            return _lib.check(self._lib.orbfe_search_by_projection_sim3_rig(
+                KF.ref(), ctypes.byref(cam), ctypes.byref(model), pts.ctypes.data, len(pts),
+                None if pk is None else pk.ctypes.data, int(th), float(ratioHamming), m.ctypes.data,
+                None if mk is None else mk.ctypes.data), "SearchByProjection(Sim3)")
         return _lib.check(self._lib.orbfe_search_by_projection_sim3(
             KF.ref(), ctypes.byref(cam), pts.ctypes.data, len(pts), None if pk is None else pk.ctypes.data, int(th),
             float(ratioHamming), m.ctypes.data, None if mk is None else mk.ctypes.data), "SearchByProjection(Sim3)")

@@ -585,6 +585,9 @@ def synth_local_map_3d_rig(rng, F: MatchFrame, cam: Camera, n: int, two: bool = 
     m["observations"] = np.where(rng.random(n) < 0.1, 0, rng.integers(1, 20, n))
     m["id"] = np.arange(n) + 30000
     m["desc"] = desc
+    # the previous frame's mTrackDepth (a two-camera point seen only by the right camera keeps it,
+    # and bFarPoints reads it): 0-20 m against the tests' thFarPoints of 10 m
+    m["track_depth"] = rng.uniform(0.0, 20.0, n).astype(np.float32)
     return m
 
 

@@ -2,11 +2,12 @@
 // (orb_slam3/src/ORBmatcher.cc:427-646, 765-1674) and MapPoint::ComputeDistinctiveDescriptors
 // (MapPoint.cc:329-403) on top of liborbfe.so. Keyframes with a second camera
 // (KannalaBrandt8 stereo, NLeft != -1) go to the library's two-camera entry points
-// (orbfe_search_by_bow_kf2, orbfe_fuse_rig, orbfe_search_for_triangulation with bCoarse). The
-// original bodies, renamed *_cpu, run where the library has no device form (SearchBySim3 and the
-// Sim3 SearchByProjection with a non-pinhole camera, the fine KannalaBrandt8 epipolar test of
-// SearchForTriangulation) and, after one logged line per call site and error code, whenever the
-// library returns an error.
+// (orbfe_search_by_bow_kf2, orbfe_fuse_rig, orbfe_search_by_projection_sim3_rig, orbfe_search_by_sim3,
+// orbfe_search_for_triangulation with bCoarse, orbfe_search_for_triangulation_epi with the camera
+// models' epipolarConstrain called back on this thread). The original bodies, renamed *_cpu, run only
+// for SearchForTriangulation(bCoarse = false) between a one-camera and a two-camera keyframe (the
+// reference reads R12 / t12 uninitialised there, ORBmatcher.cc:925-940, 1036-1074) and, after one
+// logged line per call site and error code, whenever the library returns an error.
 // Built inside the ORB-SLAM3 tree; NOT compiled in this repository's container (no OpenCV /
 // Eigen / Sophus here). See INTEGRATION.md §4.
 #include "ORBmatcher.h"
@@ -136,6 +137,7 @@ orbfe_map_point_3d point_3d(MapPoint* p, int32_t id, int32_t flags) {
     m.max_dist = p->GetMaxDistance();
     m.flags = flags | (p->isBad() ? ORBFE_MP_BAD : 0);
     m.observations = p->Observations();
+    m.track_depth = p->mTrackDepth;
     memcpy(m.desc, p->GetDescriptor().data, 32);
     return m;
 }
@@ -157,6 +159,28 @@ struct FlatFV {   // DBoW2::FeatureVector flattened (ORBmatcher_orbfe.cc has the
         v.indices = idx.data();
     }
 };
+
+// SearchForTriangulation's epipolar test through the camera models: the camera pair and relative pose
+// the reference selects by the keypoints' sides (ORBmatcher.cc:925-940, 1036-1074); single-camera
+// keyframes use T12 (slot ll) and mvKeysUn.
+struct EpiCtx {
+    KeyFrame* k1;
+    KeyFrame* k2;
+    Eigen::Matrix3f R[4];   // ll, lr, rl, rr
+    Eigen::Vector3f t[4];
+};
+int32_t epipolar_cb(void* c, int32_t idx1, int32_t idx2) {
+    const EpiCtx* e = static_cast<const EpiCtx*>(c);
+    const bool s1 = e->k1->NLeft == -1, s2 = e->k2->NLeft == -1;
+    const bool r1 = !s1 && idx1 >= e->k1->NLeft, r2 = !s2 && idx2 >= e->k2->NLeft;
+    const cv::KeyPoint& kp1 = s1 ? e->k1->mvKeysUn[idx1] : r1 ? e->k1->mvKeysRight[idx1 - e->k1->NLeft] : e->k1->mvKeys[idx1];
+    const cv::KeyPoint& kp2 = s2 ? e->k2->mvKeysUn[idx2] : r2 ? e->k2->mvKeysRight[idx2 - e->k2->NLeft] : e->k2->mvKeys[idx2];
+    GeometricCamera* c1 = r1 ? e->k1->mpCamera2 : e->k1->mpCamera;
+    GeometricCamera* c2 = r2 ? e->k2->mpCamera2 : e->k2->mpCamera;
+    const int sel = (r1 ? 2 : 0) + (r2 ? 1 : 0);
+    return c1->epipolarConstrain(c2, kp1, kp2, e->R[sel], e->t[sel], e->k1->mvLevelSigma2[kp1.octave],
+                                 e->k2->mvLevelSigma2[kp2.octave]) ? 1 : 0;
+}
 
 }  // namespace
 
@@ -180,15 +204,54 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& v
 
 int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, vector<pair<size_t, size_t>>& vMatchedPairs,
                                        const bool bOnlyStereo, const bool bCoarse) {
-    // two-camera keyframes: the KannalaBrandt8 pair epipolar test (TriangulateMatches) stays with the
-    // camera model, so only the bCoarse form (no epipolar test, :1036) runs on the device
-    if ((pKF1->mpCamera2 || pKF2->mpCamera2) && !bCoarse)
+    const bool two1 = pKF1->mpCamera2 != nullptr, two2 = pKF2->mpCamera2 != nullptr;
+    // one keyframe with a second camera, the other without: the reference's fine test reads R12 / t12
+    // uninitialised (they are set only when both have one, :1036-1074); its own body keeps that
+    if (two1 != two2 && !bCoarse)
         return SearchForTriangulation_cpu(pKF1, pKF2, vMatchedPairs, bOnlyStereo, bCoarse);
-    // the per-call constants, computed exactly as the reference does (ORBmatcher.cc:913-927,
+    // the per-call constants, computed exactly as the reference does (ORBmatcher.cc:913-940,
     // Pinhole.cpp:109-112)
     const Sophus::SE3f T1w = pKF1->GetPose(), T2w = pKF2->GetPose(), Tw2 = pKF2->GetPoseInverse();
     const Eigen::Vector3f C2 = T2w * pKF1->GetCameraCenter();
     const Eigen::Vector2f ep = pKF2->mpCamera->project(C2);
+    const bool pin = pKF1->mpCamera->GetType() == GeometricCamera::CAM_PINHOLE &&
+                     pKF2->mpCamera->GetType() == GeometricCamera::CAM_PINHOLE;
+    if (!bCoarse && (two1 || !pin)) {
+        // a camera model's own test (KannalaBrandt8::epipolarConstrain -> TriangulateMatches, an
+        // Eigen JacobiSVD) runs here, called back by the library on the candidates the device lists
+        // until the first that passes
+        EpiCtx e;
+        e.k1 = pKF1;
+        e.k2 = pKF2;
+        if (two1) {
+            const Sophus::SE3f Tr1w = pKF1->GetRightPose(), Twr2 = pKF2->GetRightPoseInverse();
+            const Sophus::SE3f T[4] = {T1w * Tw2, T1w * Twr2, Tr1w * Tw2, Tr1w * Twr2};   // ll, lr, rl, rr
+            for (int k = 0; k < 4; k++) {
+                e.R[k] = T[k].rotationMatrix();
+                e.t[k] = T[k].translation();
+            }
+        } else {
+            const Sophus::SE3f T12 = T1w * Tw2;
+            e.R[0] = T12.rotationMatrix();
+            e.t[0] = T12.translation();
+        }
+        vector<int32_t> m1(pKF1->N), m2(pKF2->N), out(pKF1->N);
+        for (int i = 0; i < pKF1->N; i++) m1[i] = pKF1->GetMapPoint(i) ? 1 : -1;
+        for (int i = 0; i < pKF2->N; i++) m2[i] = pKF2->GetMapPoint(i) ? 1 : -1;
+        FlatFV f1(pKF1->mFeatVec), f2(pKF2->mFeatVec);
+        vector<cv::KeyPoint> keys1, keys2;
+        const orbfe_frame k1 = kf_view(pKF1, keys1), k2 = kf_view(pKF2, keys2);
+        const float epv[2] = {ep(0), ep(1)};
+        const int n = orbfe_search_for_triangulation_epi(&k1, m1.data(), &f1.v, &k2, m2.data(), &f2.v, epv, bOnlyStereo,
+                                                         mbCheckOrientation, epipolar_cb, &e, out.data());
+        if (failed(n, "orbfe_search_for_triangulation_epi"))
+            return SearchForTriangulation_cpu(pKF1, pKF2, vMatchedPairs, bOnlyStereo, bCoarse);
+        vMatchedPairs.clear();
+        vMatchedPairs.reserve(n);
+        for (int i = 0; i < pKF1->N; i++)
+            if (out[i] >= 0) vMatchedPairs.push_back(make_pair((size_t)i, (size_t)out[i]));
+        return n;
+    }
     const Sophus::SE3f T12 = T1w * Tw2;
     const Eigen::Matrix3f R12 = T12.rotationMatrix();
     const Eigen::Vector3f t12 = T12.translation();
@@ -285,9 +348,8 @@ int ORBmatcher::Fuse(KeyFrame* pKF, Sophus::Sim3f& Scw, const vector<MapPoint*>&
 
 int ORBmatcher::SearchByProjection(KeyFrame* pKF, Sophus::Sim3f& Scw, const vector<MapPoint*>& vpPoints,
                                    vector<MapPoint*>& vpMatched, int th, float ratioHamming) {
-    // the library projects with the pinhole intrinsics (pKF->mpCamera->project, :459)
-    if (pKF->mpCamera->GetType() != GeometricCamera::CAM_PINHOLE || pKF->mpCamera2)
-        return SearchByProjection_cpu(pKF, Scw, vpPoints, vpMatched, th, ratioHamming);
+    // pKF->mpCamera->project (:465) with the keyframe's model; a two-camera keyframe's left grid
+    const orbfe_camera_model model = model_of(pKF->mpCamera);
     const Sophus::SE3f Tcw = Sophus::SE3f(Scw.rotationMatrix(), Scw.translation() / Scw.scale());
     const orbfe_kf_camera cam = kf_camera(pKF, Tcw, Tcw.inverse().translation());
     Handles H;
@@ -297,9 +359,9 @@ int ORBmatcher::SearchByProjection(KeyFrame* pKF, Sophus::Sim3f& Scw, const vect
     for (size_t k = 0; k < vpMatched.size(); k++) m[k] = H.of(vpMatched[k]);
     vector<cv::KeyPoint> keys;
     const orbfe_frame kf = kf_view(pKF, keys);
-    const int n = orbfe_search_by_projection_sim3(&kf, &cam, q.data(), (int)q.size(), nullptr, th, ratioHamming,
-                                                  m.data(), nullptr);
-    if (failed(n, "orbfe_search_by_projection_sim3"))
+    const int n = orbfe_search_by_projection_sim3_rig(&kf, &cam, &model, q.data(), (int)q.size(), nullptr, th,
+                                                      ratioHamming, m.data(), nullptr);
+    if (failed(n, "orbfe_search_by_projection_sim3_rig"))
         return SearchByProjection_cpu(pKF, Scw, vpPoints, vpMatched, th, ratioHamming);
     for (size_t k = 0; k < vpMatched.size(); k++) vpMatched[k] = H.at(m[k]);
     return n;
@@ -307,9 +369,8 @@ int ORBmatcher::SearchByProjection(KeyFrame* pKF, Sophus::Sim3f& Scw, const vect
 
 int ORBmatcher::SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12, const Sophus::Sim3f& S12,
                              const float th) {
-    if (pKF1->mpCamera2 || pKF2->mpCamera2 || pKF1->mpCamera->GetType() != GeometricCamera::CAM_PINHOLE ||
-        pKF2->mpCamera->GetType() != GeometricCamera::CAM_PINHOLE)
-        return SearchBySim3_cpu(pKF1, pKF2, vpMatches12, S12, th);
+    // every camera with the pinhole expression on pKF1's intrinsics (:1514-1519,1594-1599); two-camera
+    // keyframes on their left grids
     Handles H;
     const vector<MapPoint*> v1 = pKF1->GetMapPointMatches(), v2 = pKF2->GetMapPointMatches();
     vector<orbfe_map_point_3d> p1(v1.size()), p2(v2.size());

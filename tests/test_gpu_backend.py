@@ -129,6 +129,69 @@ def test_search_by_projection_sim3(gpu, oracle_lib, with_kfs, seed, dup, ratio, 
         np.testing.assert_array_equal(mkg, mko)
 
 
+@pytest.mark.parametrize("two", [False, True], ids=["mono_kb8", "two_cams"])
+@pytest.mark.parametrize("seed,ratio,th", [(0, 1.0, 10), (1, 0.5, 20)])
+def test_search_by_projection_sim3_kb8(gpu, oracle_lib, two, seed, ratio, th):
+    """SearchByProjection(pKF, Scw, ...) on a KannalaBrandt8 keyframe (ORBmatcher.cc:427-523): the
+    projection is pKF->mpCamera->project (:465) on the device, a two-camera keyframe is searched on
+    its left grid (KeyFrame::GetFeaturesInArea(.., bRight = false)); the vpPointsKFs overload keeps
+    the pinhole expression (:571-576)."""
+    rng = np.random.default_rng(120 + seed + 10 * two)
+    KF = sm.synth_frame_two(rng, 1000, 950) if two else sm.synth_frame(rng, 1000, 512, 512, stereo=False)
+    cam = sm.synth_camera(rng, rot_deg=20.0)
+    rig = sm.synth_rig(cam, two)
+    pts = sm.synth_local_map_3d_rig(rng, KF, cam, 6000, two=two)
+    kcam = sm.left_kf_camera(cam)
+    matched0 = np.full(KF.N, -1, np.int32)
+    pre = rng.random(KF.N) < 0.1
+    matched0[pre] = rng.choice(pts["id"], int(pre.sum()))
+    for kfs in (None, rng.integers(0, 50, len(pts)).astype(np.int32)):
+        mk0 = np.where(pre, 99, -1).astype(np.int32)
+        mg, mo, mkg, mko = matched0.copy(), matched0.copy(), mk0.copy(), mk0.copy()
+        ng = ORBmatcher().SearchByProjectionSim3(KF, kcam, pts, mg, th, ratio, kfs, None if kfs is None else mkg,
+                                                 model=rig.left)
+        no = oracle_lib.OracleMatcher().sbp_sim3(KF, kcam, pts, mo, th, ratio, kfs, None if kfs is None else mko,
+                                                 model=rig.left)
+        assert ng == no and (no > 50 or kfs is not None)
+        np.testing.assert_array_equal(mg, mo)
+        np.testing.assert_array_equal(mkg, mko)
+        if two:
+            new = (mg >= 0) & (matched0 < 0)
+            assert not new[KF.nleft:].any()   # right keypoints are never candidates
+    if two:   # the pinhole entry point needs the camera model for the first overload
+        with pytest.raises(OrbfeError):
+            ORBmatcher().SearchByProjectionSim3(KF, kcam, pts, matched0.copy(), th, ratio)
+
+
+def _as_two_cams(K, frac):
+    """The keyframe's keypoints split into a left part [0, nleft) and a 'right' part (a two-camera
+    keyframe, NLeft != -1, no stereo links)."""
+    nl = int(K.N * frac)
+    return MatchFrame(K.keys, K.desc, K.bounds, K.scale_factors, None, K.mbf, nleft=nl)
+
+
+@pytest.mark.parametrize("kinds", [(True, True), (True, False), (False, True)], ids=["two_two", "two_one", "one_two"])
+@pytest.mark.parametrize("seed,scale,th", [(0, 1.0, 7.5), (2, 1.3, 7.5)])
+def test_search_by_sim3_two_cams(gpu, oracle_lib, kinds, seed, scale, th):
+    """SearchBySim3 with keyframes that have a second camera (ORBmatcher.cc:1457-1674): every point
+    (left and right keypoints) projects with the pinhole expression on pKF1's intrinsics, candidates
+    come from the left grid (mvKeys) of the target keyframe."""
+    rng = np.random.default_rng(300 + seed)
+    K1, K2, p1, p2, c1, c2, S12, S21, src = sm.synth_sim3_pair(rng, 2000, scale=scale)
+    A = _as_two_cams(K1, 0.6) if kinds[0] else K1
+    B = _as_two_cams(K2, 0.7) if kinds[1] else K2
+    m0 = np.full(A.N, -1, np.int32)
+    pre = np.nonzero(rng.random(A.N) < 0.05)[0]
+    m0[pre] = 123
+    mg, mo = m0.copy(), m0.copy()
+    ng = ORBmatcher().SearchBySim3(A, B, p1, p2, c1, c2, S12, S21, th, mg)
+    no = oracle_lib.OracleMatcher().search_by_sim3(A, B, p1, p2, c1, c2, S12, S21, th, mo)
+    assert ng == no
+    np.testing.assert_array_equal(mg, mo)
+    if scale == 1.0:
+        assert no > 50
+
+
 @pytest.mark.parametrize("seed,scale,th", [(0, 1.0, 7.5), (1, 1.0, 15.0), (2, 1.3, 7.5), (3, 0.8, 10.0)])
 def test_search_by_sim3(gpu, oracle_lib, seed, scale, th):
     rng = np.random.default_rng(seed)
@@ -211,9 +274,56 @@ def test_search_for_triangulation_two_cams(gpu, oracle_lib, kinds, only_stereo):
     assert ng == no
     np.testing.assert_array_equal(og, oo)
     assert no > 0 or (only_stereo and (kinds[0] or kinds[1]))
-    # the KannalaBrandt8 epipolar test (TriangulateMatches) stays on the host: bCoarse is required
+    # the KannalaBrandt8 epipolar test (TriangulateMatches) is the caller's: the bCoarse = false form
+    # is orbfe_search_for_triangulation_epi (below); the F12 entry point refuses two-camera keyframes
     with pytest.raises(OrbfeError):
         m.SearchForTriangulation(A, mp1, fv1, B, mp2, fv2, F12, ep, sg, only_stereo, False)
+
+
+def _epipolar_predicate(salt):
+    """A deterministic stand-in for pCamera1->epipolarConstrain(kp1, kp2, ...): passes about 60 % of the
+    pairs, decided by a hash of the keypoint pair. The selection logic must call it in an order that
+    yields the reference's bestIdx2 whatever the predicate; the real one is the camera model's code,
+    which the shim calls unchanged."""
+    calls = []
+
+    def epi(i1, i2):
+        calls.append((i1, i2))
+        h = (i1 * 2654435761 + i2 * 40503 + salt * 97) & 0xFFFFFFFF
+        return ((h >> 11) % 5) < 3
+    return epi, calls
+
+
+@pytest.mark.parametrize("kinds", [(True, True), (False, False), (True, False), (False, True)],
+                         ids=["two_two", "one_one", "two_one", "one_two"])
+@pytest.mark.parametrize("only_stereo,check_ori", [(False, True), (False, False), (True, True)])
+def test_search_for_triangulation_epi(gpu, oracle_lib, kinds, only_stereo, check_ori):
+    """SearchForTriangulation with bCoarse = false and the epipolar test left to the caller (the
+    KannalaBrandt8 keyframes of config 4, LocalMapping.cc:464-466 passes bCoarse = false while
+    tracking is healthy): the device lists the gated candidates in (dist, reverse order), the host
+    stops at the first that passes; matches12 and nmatches equal the oracle's literal loop
+    (ORBmatcher.cc:907-1146) run with the same predicate, which the device form never calls more
+    often than the reference does."""
+    rng = np.random.default_rng(71 + 2 * only_stereo + check_ori)
+    K1, K2, mp1, mp2, fv1, fv2, src = sm.synth_two_cam_kf_pair(rng, 700, 650, 40)
+
+    def single(K):
+        ur = np.where(rng.random(K.N) < 0.6, K.keys["x"] - 10, -1).astype(np.float32)
+        return MatchFrame(K.keys, K.desc, K.bounds, K.scale_factors, ur, K.mbf)
+    A = K1 if kinds[0] else single(K1)
+    B = K2 if kinds[1] else single(K2)
+    mp1 = np.where(rng.random(A.N) < 0.3, 5, -1).astype(np.int32)
+    mp2 = np.where(rng.random(B.N) < 0.3, 5, -1).astype(np.int32)
+    ep = np.array([256.0, 250.0], np.float32)
+    for salt in (0, 1):
+        eg, cg = _epipolar_predicate(salt)
+        eo, co = _epipolar_predicate(salt)
+        ng, og = ORBmatcher(0.6, check_ori).SearchForTriangulationEpi(A, mp1, fv1, B, mp2, fv2, ep, eg, only_stereo)
+        no, oo = oracle_lib.OracleMatcher(0.6, check_ori).search_for_triangulation_epi(A, mp1, fv1, B, mp2, fv2, ep,
+                                                                                        eo, only_stereo)
+        assert ng == no and (no > 20 or only_stereo)
+        np.testing.assert_array_equal(og, oo)
+        assert len(cg) <= len(co) and set(cg) <= set(co)
 
 
 @pytest.mark.parametrize("bright", [False, True], ids=["left", "right"])

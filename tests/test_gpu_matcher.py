@@ -451,7 +451,11 @@ def test_is_in_frustum_rig(gpu, om, seed, two):
     for f in ("proj_x", "proj_y", "depth", "view_cos") + (() if two else ("proj_xr",)):
         np.testing.assert_array_equal(tg[f][inv].view(np.uint32), to[f][inv].view(np.uint32), err_msg=f)
     np.testing.assert_array_equal(tg["scale_level"], to["scale_level"])
+    # mTrackDepth is written only by a passing left view; every other point keeps its previous value
+    # (orbfe_map_point_3d.track_depth), which bFarPoints reads for right-only points
+    np.testing.assert_array_equal(tg["depth"].view(np.uint32), to["depth"].view(np.uint32))
     if two:
+        assert (~inv & ((to["flags"] & sm.MP_IN_VIEW_R) != 0) & (to["depth"] > 10.0)).sum() > 100
         invr = (to["flags"] & sm.MP_IN_VIEW_R) != 0
         assert invr.sum() > 1000
         for f in ("proj_xr", "proj_yr", "view_cos_r"):

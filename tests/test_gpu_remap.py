@@ -127,3 +127,31 @@ def test_remap_batch_pitched_source(gpu, oracle_lib):
     torch.cuda.synchronize()
     for i in range(n):
         np.testing.assert_array_equal(out[i].cpu().numpy(), oracle_lib.remap_linear(imgs[i], mx, my))
+
+
+def test_remap_batch_two_streams(gpu, oracle_lib):
+    """The pointer-table ring used from two streams: six fixed (source, output) sets cycled over two
+    alternating streams (more sets than ring slots, so slots are refilled while the other stream may
+    still read them, and hits come on another stream than the upload). Each launch is preceded on
+    its own stream by zeroing its output, so a launch that read a stale or partly written table
+    leaves its set's output zero (or writes another set's): every final output is checked."""
+    import torch
+    w, h, n = 160, 120, 2
+    mx, my = rectify_maps(w, h, 150.0, 150.0, 80.0, 60.0, (-0.2, 0.05, 1e-4, 1e-5), R=_rot(1.0))
+    dmx, dmy = torch.from_numpy(mx).cuda(), torch.from_numpy(my).cuda()
+    imgs = [np.stack([synth_image(300 + 10 * k + i, w, h) for i in range(n)]) for k in range(6)]
+    srcs = [torch.from_numpy(im).cuda() for im in imgs]
+    outs = [torch.zeros((n, h, w), dtype=torch.uint8, device="cuda") for _ in range(6)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    order = [0, 1, 2, 3, 4, 5, 0, 0, 5, 1, 4, 2, 3, 3, 1, 0, 2, 4, 5, 1]
+    for j, k in enumerate(order):
+        s = streams[j & 1]
+        with torch.cuda.stream(s):
+            outs[k].zero_()
+            remap_linear_batch(srcs[k], dmx, dmy, outs[k], stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    for k in range(6):
+        got = outs[k].cpu().numpy()
+        for i in range(n):
+            np.testing.assert_array_equal(got[i], oracle_lib.remap_linear(imgs[k][i], mx, my))
