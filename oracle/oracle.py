@@ -25,45 +25,64 @@ def build(force: bool = False) -> str:
     return LIB
 
 
+CONTRACT_LIB = os.path.join(_HERE, "liborb_oracle_contract.so")
+
+
+def build_contract() -> str:
+    """The oracle built with the reference's own flags (-O3 -march=native, g++'s default FMA
+    contraction; the OpenCV restatements pinned uncontracted): tests/test_oracle_contraction.py."""
+    subprocess.run(["make", "-C", _HERE, "-s", "contract"], check=True)
+    return CONTRACT_LIB
+
+
 _lib = None
+_libs = {}
 
 
-def lib() -> ctypes.CDLL:
+def lib(path: str | None = None) -> ctypes.CDLL:
     global _lib
+    if path is not None:   # another build of the same sources (the contraction check)
+        if path not in _libs:
+            _libs[path] = _sigs(ctypes.CDLL(path))
+        return _libs[path]
     if _lib is None:
         if not os.path.exists(LIB):
             build()
-        L = ctypes.CDLL(LIB)
-        vp, ci, cf = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
-        L.oro_create.restype = vp
-        L.oro_create.argtypes = [ci, cf, ci, ci, ci]
-        L.oro_destroy.argtypes = [vp]
-        L.oro_set_model.argtypes = [vp, ci, ci]
-        L.oro_level_info.argtypes = [vp, vp, vp, vp, vp, vp, vp]
-        L.oro_extract.argtypes = [vp, vp, ci, ci, ci, ci, ci, vp, ci, vp, ctypes.POINTER(ci)]
-        L.oro_pyramid_level.argtypes = [vp, ci, vp, ci, ctypes.POINTER(ci), ctypes.POINTER(ci)]
-        L.oro_debug_keys.argtypes = [vp, ci, ci, vp, ci]
-        L.oro_resize.argtypes = [vp, ci, ci, vp, ci, ci, ci]
-        L.oro_blur.argtypes = [vp, ci, ci, vp, ci]
-        L.oro_fast.argtypes = [vp, ci, ci, ci, ci, vp, ci]
-        L.oro_fast_atan2.restype = cf
-        L.oro_fast_atan2.argtypes = [cf, cf]
-        L.oro_hamming.argtypes = [vp, vp]
-        L.oro_stereo_match.argtypes = [vp, vp, vp, vp, ci, vp, vp, ci, cf, cf, vp, vp]
-        L.oro_bench_extract.restype = ctypes.c_double
-        L.oro_bench_extract.argtypes = [vp, ci, ci, ci, ci, cf, ci, ci, ci, ci, ctypes.POINTER(ci)]
-        L.oro_std_sort_u64_hi.argtypes = [vp, ci]
-        L.oro_bench_stereo.restype = ctypes.c_long
-        L.oro_bench_stereo.argtypes = [vp, vp, ci, ci, ci, ci, cf, ci, ci, ci, cf, cf, ci]
-        _lib = L
+        _lib = _sigs(ctypes.CDLL(LIB))
     return _lib
+
+
+def _sigs(L: ctypes.CDLL) -> ctypes.CDLL:
+    vp, ci, cf = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    L.oro_create.restype = vp
+    L.oro_create.argtypes = [ci, cf, ci, ci, ci]
+    L.oro_destroy.argtypes = [vp]
+    L.oro_set_model.argtypes = [vp, ci, ci]
+    L.oro_level_info.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+    L.oro_extract.argtypes = [vp, vp, ci, ci, ci, ci, ci, vp, ci, vp, ctypes.POINTER(ci)]
+    L.oro_pyramid_level.argtypes = [vp, ci, vp, ci, ctypes.POINTER(ci), ctypes.POINTER(ci)]
+    L.oro_debug_keys.argtypes = [vp, ci, ci, vp, ci]
+    L.oro_resize.argtypes = [vp, ci, ci, vp, ci, ci, ci]
+    L.oro_blur.argtypes = [vp, ci, ci, vp, ci]
+    L.oro_fast.argtypes = [vp, ci, ci, ci, ci, vp, ci]
+    L.oro_fast_atan2.restype = cf
+    L.oro_fast_atan2.argtypes = [cf, cf]
+    L.oro_hamming.argtypes = [vp, vp]
+    L.oro_stereo_match.argtypes = [vp, vp, vp, vp, ci, vp, vp, ci, cf, cf, vp, vp]
+    L.oro_bench_extract.restype = ctypes.c_double
+    L.oro_bench_extract.argtypes = [vp, ci, ci, ci, ci, cf, ci, ci, ci, ci, ctypes.POINTER(ci)]
+    L.oro_std_sort_u64_hi.argtypes = [vp, ci]
+    L.oro_bench_stereo.restype = ctypes.c_long
+    L.oro_bench_stereo.argtypes = [vp, vp, ci, ci, ci, ci, cf, ci, ci, ci, cf, cf, ci]
+    return L
 
 
 class OracleExtractor:
     """CPU restatement of ORB_SLAM3::ORBextractor (see oracle/orb_oracle.cpp)."""
 
-    def __init__(self, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, resize_simd_lanes=16, blur_variant=0):
-        self._l = lib()
+    def __init__(self, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, resize_simd_lanes=16, blur_variant=0,
+                 lib_path=None):
+        self._l = lib(lib_path)
         self.h = self._l.oro_create(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
         self._l.oro_set_model(self.h, resize_simd_lanes, blur_variant)
         self.nlevels = nlevels
@@ -113,7 +132,7 @@ class OracleExtractor:
 
 
 def stereo_match(ext_l: OracleExtractor, ext_r: OracleExtractor, kl, dl, kr, dr, bf, fx):
-    L = lib()
+    L = ext_l._l
     n = len(kl)
     ur = np.zeros(max(n, 1), np.float32)
     dp = np.zeros(max(n, 1), np.float32)

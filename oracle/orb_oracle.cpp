@@ -70,12 +70,18 @@ struct Image {             // tightly packed u8 plane
     const uint8_t* row(int y) const { return px.data() + (size_t)y * w; }
 };
 
+// OpenCV's own code is compiled into libopencv_* with OpenCV's flags, not the reference's
+// -march=native: in the reference-flags build of this file (liborb_oracle_contract.so,
+// tests/test_oracle_contraction.py) these restatements stay uncontracted while the code the
+// reference owns (computeOrbDescriptor, ComputeStereoMatches, ...) is contracted as g++ does.
+#define ORO_OPENCV __attribute__((optimize("fp-contract=off")))
+
 // ---- cv::fastAtan2 (OpenCV 4.x mathfuncs atan_f32) ----
 static const float kAtanP1 = 0.9997878412794807f * (float)(180 / M_PI);
 static const float kAtanP3 = -0.3258083974640975f * (float)(180 / M_PI);
 static const float kAtanP5 = 0.1555786518463281f * (float)(180 / M_PI);
 static const float kAtanP7 = -0.04432655554792128f * (float)(180 / M_PI);
-float fast_atan2(float y, float x) {
+ORO_OPENCV float fast_atan2(float y, float x) {
     float ax = std::fabs(x), ay = std::fabs(y), a, c, c2;
     if (ax >= ay) {
         c = ay / (ax + (float)DBL_EPSILON);
@@ -92,7 +98,7 @@ float fast_atan2(float y, float x) {
 }
 
 // ---- cv::resize(src, dst, dsize, 0, 0, INTER_LINEAR), CV_8UC1 (imgproc/resize.cpp) ----
-void resize_linear(const Image& src, Image& dst, int dw, int dh, int simd_lanes) {
+ORO_OPENCV void resize_linear(const Image& src, Image& dst, int dw, int dh, int simd_lanes) {
     dst.w = dw; dst.h = dh; dst.px.assign((size_t)dw * dh, 0);
     if (dw == src.w && dh == src.h) { dst.px = src.px; return; }
     const double inv_x = (double)dw / src.w, inv_y = (double)dh / src.h;
@@ -157,7 +163,7 @@ static inline int reflect101(int p, int n) {
     while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
     return p;
 }
-void gaussian_blur7(const Image& src, Image& dst, int variant) {
+ORO_OPENCV void gaussian_blur7(const Image& src, Image& dst, int variant) {
     const int* k = variant == 1 ? kBlurRound : kBlurED;
     const int w = src.w, h = src.h;
     std::vector<uint32_t> rowq((size_t)w * h);   // Q8 row-pass values
@@ -181,7 +187,7 @@ void gaussian_blur7(const Image& src, Image& dst, int variant) {
 static const int kRing[16][2] = {{0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3, -1}, {2, -2}, {1, -3},
                                  {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
 
-static int corner_score16(const uint8_t* p, const int* pixel, int threshold) {
+ORO_OPENCV static int corner_score16(const uint8_t* p, const int* pixel, int threshold) {
     const int K = 8, N = 25;
     int v = p[0];
     int d[N];
@@ -210,7 +216,7 @@ static int corner_score16(const uint8_t* p, const int* pixel, int threshold) {
 }
 
 // roi: pointer to top-left, step = row stride, rows x cols.
-void fast9(const uint8_t* roi, int step, int rows, int cols, int threshold, std::vector<KeyPoint>& kps) {
+ORO_OPENCV void fast9(const uint8_t* roi, int step, int rows, int cols, int threshold, std::vector<KeyPoint>& kps) {
     const int K = 8, N = 25;
     int pixel[25];
     for (int k = 0; k < 16; k++) pixel[k] = kRing[k][0] + kRing[k][1] * step;

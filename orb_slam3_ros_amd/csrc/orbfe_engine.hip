@@ -193,6 +193,9 @@ static int build_geom(const orbfe_extractor* h, int W, int H, OrbGeom& g, std::v
             f.roi = round_up(rs * (L.h_cell + 6), 16);
             f.sc = round_up(rs * (L.h_cell + 2), 16);
             f.cor = round_up(std::max(2 * L.w_cell * L.h_cell, 8 * grp + 256), 16);
+#ifdef FAST_EXP_COR   // occupancy experiment only
+            f.cor = std::min(f.cor, FAST_EXP_COR);
+#endif
             f.wave_bytes = f.roi + f.sc + f.cor + FAST_ENT_BYTES;
             fl.roi = std::max(fl.roi, f.roi);
             fl.sc = std::max(fl.sc, f.sc);
