@@ -466,6 +466,35 @@ def pmc_valu(n_img, w, h):
     return best
 
 
+def dropin_leg(frames, W=752, H=480, nf=1000, bf=0.110078 * 458.654, fx=458.654):
+    """The drop-in path at batch 1 (rank 0, not part of `value`): one 752x480 stereo frame at a time
+    through the host C-ABI exactly as Tracking builds a stereo Frame (Frame.cc:122-141): two
+    ORBextractor::operator() calls on two per-frame std::threads, then ComputeStereoMatches, host
+    images in and host results out. Timed by the compiled C++ consumer (tests/native/capi_frontend.cpp
+    --latency, linked against liborbfe.so only), with the library's HIP-event split of each call
+    (upload / kernels / result copies; host = wall - the device-side critical path)."""
+    import struct
+    import subprocess
+    import tempfile
+    from orb_slam3_ros_amd import build as B
+    from orb_slam3_ros_amd.synth import synth_stereo
+    binary = B.CAPI_BIN
+    if not os.path.exists(binary):
+        return {"error": "tests/native/capi_frontend not built (run __graft_entry__.build())"}
+    left, right = synth_stereo(7, W, H)
+    with tempfile.TemporaryDirectory() as d:
+        job = os.path.join(d, "job.bin")
+        with open(job, "wb") as f:
+            f.write(struct.pack("<5i2f", W, H, nf, 0, 100, bf, fx) + left.tobytes() + right.tobytes())
+        r = subprocess.run([binary, "--latency", str(frames), job], capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        return {"error": (r.stderr or r.stdout)[-400:]}
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    out["path"] = ("host C-ABI per frame: orbfe_extract L || R on two std::threads (ExtractORB, Frame.cc:122-125), "
+                   "then orbfe_stereo_match (Frame.cc:141); medians over the frames")
+    return out
+
+
 def side_leg(dev, name, W, H, nf, F, steps, warmup, stereo, lap, bf, fx, check_frames, seed0):
     """A secondary BASELINE config on this GPU (rank 0, not part of `value`): throughput, stage
     times, the pyramid+FAST kernel roofline and a post-timing parity check."""
@@ -506,6 +535,7 @@ def main():
     ap.add_argument("--no-side-configs", action="store_true", help="skip the config 3 / config 4 legs")
     ap.add_argument("--stage-steps", type=int, default=10, help="extra steps with per-stage HIP events")
     ap.add_argument("--matcher-steps", type=int, default=50, help="config-5 SearchByProjection calls per th (0: skip)")
+    ap.add_argument("--dropin-frames", type=int, default=100, help="batch-1 drop-in latency frames (0: skip)")
     ap.add_argument("--rectify-steps", type=int, default=5,
                     help="time cv::remap rectification of the step's images (reported separately; 0: skip)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -714,9 +744,11 @@ def main():
                                                  "extract L+R + ComputeStereoMatches", 1241, 376, 2000, 256,
                                             max(3, args.steps // 2), 2, "rectified", (0, 0), KITTI_BF, KITTI_FX, 0,
                                             20000)
-            legs["config4_step"], ok4 = side_leg(dev, "TUM-VI-like 512x512 KannalaBrandt8 stereo, per-GPU step of "
-                                                      "BASELINE config 4: 8 images (4 stereo frames), vLappingArea "
-                                                      "{0,511}, batched knnMatch(k=2)+ratio", 512, 512, 1000, 4,
+            legs["config4_step"], ok4 = side_leg(dev, "TUM-VI-like 512x512 KannalaBrandt8 stereo: the whole "
+                                                      "BASELINE config 4 step (4 synthetic streams x 2 cameras = 8 "
+                                                      "images) on ONE GPU (config 4 spreads it over 8 GPUs, one "
+                                                      "image each), vLappingArea {0,511}, batched "
+                                                      "knnMatch(k=2)+ratio", 512, 512, 1000, 4,
                                                  max(10, args.steps), 3, "fisheye", (0, 511), 0.0, 1.0, 0, 21000)
             legs["config4_batch"], ok4b = side_leg(dev, "as config4_step at a 512-image batch (throughput)", 512, 512,
                                                    1000, 256, max(3, args.steps // 2), 2, "fisheye", (0, 511), 0.0,
@@ -727,8 +759,16 @@ def main():
                 sys.exit(3)
         if args.matcher_steps > 0:
             result["matcher_config5"] = matcher_config5(args.matcher_steps)
+        if args.dropin_frames > 0 and world == 1:
+            dl = dropin_leg(args.dropin_frames, nf=args.nfeatures)
+            result["dropin"] = dl
+            result["dropin_latency_ms"] = dl.get("frame_ms")
         if not args.no_cpu_baseline and world == 1:
             result["cpu_baseline"] = cpu_baseline(native)
+            lr2t = result["cpu_baseline"].get("latency_lr2t")
+            if result.get("dropin_latency_ms") and lr2t:
+                result["dropin"]["cpu_latency_lr2t_ms"] = lr2t
+                result["dropin"]["speedup_vs_cpu_latency_lr2t"] = round(lr2t / result["dropin_latency_ms"], 2)
         print(json.dumps(result), flush=True)
     fe.close()
     if world > 1:

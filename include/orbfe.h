@@ -114,6 +114,11 @@ int orbfe_set_batch_outputs(orbfe_extractor* h, orbfe_keypoint* d_kps, uint8_t* 
 #define ORBFE_NUM_STAGES 3
 int orbfe_set_stage_timing(orbfe_extractor* h, int enable);
 int orbfe_get_stage_timing(orbfe_extractor* h, float* ms);
+/* While stage timing is enabled, the host-API calls time themselves with HIP events on their stream:
+ * ms[0..2] = the last orbfe_extract's {image upload, kernels, result copies (count read-back and
+ * keypoint / descriptor copies)}, ms[3..4] = the last orbfe_stereo_match with h as the left handle
+ * {kernels, result copies}. Returns 5 (0 when timing is off: ms then holds the last timed values). */
+int orbfe_get_call_timing(orbfe_extractor* h, float* ms);
 
 /* ---------------------------------------------------------------------------------------------
  * Stereo — replaces Frame::ComputeStereoMatches (include/Frame.h:116, src/Frame.cc:811-981)

@@ -51,6 +51,7 @@ _SIGS = {
     "orbfe_extractor_get_opencv_model": (_c_int, [_vp, _P_int, _P_int]),
     "orbfe_set_batch_outputs": (_c_int, [_vp, _vp, _vp, _vp, _c_int]),
     "orbfe_get_stage_timing": (_c_int, [_vp, _vp]),
+    "orbfe_get_call_timing": (_c_int, [_vp, _vp]),
     "orbfe_stereo_match_batch": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_float, _c_float,
                                           _vp, _vp, _vp, _vp]),
     "orbfe_stereo_match": (_c_int, [_vp, _vp, _c_float, _c_float, _vp, _vp]),

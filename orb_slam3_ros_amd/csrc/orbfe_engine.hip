@@ -110,6 +110,10 @@ struct orbfe_extractor {
     // stage timing
     bool timing = false;
     hipEvent_t ev[ORBFE_NUM_STAGES + 1] = {};   // spare set (host API)
+    // host-API call timing (orbfe_get_call_timing): events around the upload, the kernels and the
+    // result copies of the last orbfe_extract / orbfe_stereo_match on this handle
+    hipEvent_t call_ev[7] = {};
+    float call_ms[5] = {};
     std::vector<std::vector<hipEvent_t>> ev_ring;  // one event set per timed batch, read lazily
     int ev_used = 0;
     float stage_ms[ORBFE_NUM_STAGES] = {};
@@ -716,11 +720,19 @@ int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int width, int height,
         HIPCHK(hipMalloc(&h->d_stage, bytes));
         h->stage_bytes = bytes;
     }
+    const bool tm = h->timing;
+    if (tm && !h->call_ev[0])
+        for (auto& e : h->call_ev) HIPCHK(hipEventCreate(&e));
+    if (tm) HIPCHK(hipEventRecord(h->call_ev[0], s));
     HIPCHK(hipMemcpy2DAsync(h->d_stage, width, img, stride, width, height, hipMemcpyHostToDevice, s));
+    if (tm) HIPCHK(hipEventRecord(h->call_ev[1], s));
     const uint8_t* ptrs[1] = {h->d_stage};
     const int laps[2] = {lap0, lap1};
+    h->timing = false;   // the call's own events bracket the kernels (the stage ring is for batches)
     rc = run_batch(h, 1, ptrs, width, laps, s, false);
+    h->timing = tm;
     if (rc) return rc;
+    if (tm) HIPCHK(hipEventRecord(h->call_ev[2], s));
     int cnt[2];
     HIPCHK(hipMemcpyAsync(cnt, h->last_counts, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -729,9 +741,21 @@ int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int width, int height,
     if (cnt[0] > 0) {
         if (kps) HIPCHK(hipMemcpyAsync(kps, h->last_kps, (size_t)cnt[0] * sizeof(OrbKeyPoint), hipMemcpyDeviceToHost, s));
         if (desc) HIPCHK(hipMemcpyAsync(desc, h->last_desc, (size_t)cnt[0] * 32, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+    }
+    if (tm) HIPCHK(hipEventRecord(h->call_ev[3], s));
+    if (cnt[0] > 0 || tm) HIPCHK(hipStreamSynchronize(s));
+    if (tm) {   // {upload, kernels, result copies (incl. the count read-back round trip)}
+        HIPCHK(hipEventElapsedTime(&h->call_ms[0], h->call_ev[0], h->call_ev[1]));
+        HIPCHK(hipEventElapsedTime(&h->call_ms[1], h->call_ev[1], h->call_ev[2]));
+        HIPCHK(hipEventElapsedTime(&h->call_ms[2], h->call_ev[2], h->call_ev[3]));
     }
     return cnt[1];
+}
+
+int orbfe_get_call_timing(orbfe_extractor* h, float* ms) {
+    if (!h || !ms) return ORBFE_E_ARG;
+    for (int i = 0; i < 5; i++) ms[i] = h->call_ms[i];
+    return h->timing ? 5 : 0;
 }
 
 int orbfe_pyramid_level(orbfe_extractor* h, int image, int level, uint8_t* dst, int dst_pitch, int* width,
@@ -809,10 +833,13 @@ int orbfe_stereo_match(orbfe_extractor* left, orbfe_extractor* right, float bf, 
         left->stereo_kp = left->g.kp_cap;
     }
     HIPCHK(hipStreamSynchronize(right->own_stream));
+    hipStream_t s = left->own_stream;
+    const bool tm = left->timing && left->call_ev[0];
+    if (tm) HIPCHK(hipEventRecord(left->call_ev[4], s));
     int rc = orbfe_stereo_match_batch(left, 0, 1, right, 0, 1, 1, bf, fx, left->d_uright, left->d_depth,
                                       left->d_nmatch, nullptr);
     if (rc) return rc;
-    hipStream_t s = left->own_stream;
+    if (tm) HIPCHK(hipEventRecord(left->call_ev[5], s));
     int cnt[2], nm = 0;
     HIPCHK(hipMemcpyAsync(cnt, left->last_counts, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(&nm, left->d_nmatch, 4, hipMemcpyDeviceToHost, s));
@@ -820,7 +847,12 @@ int orbfe_stereo_match(orbfe_extractor* left, orbfe_extractor* right, float bf, 
     if (cnt[0] > 0) {
         HIPCHK(hipMemcpyAsync(uright, left->d_uright, (size_t)cnt[0] * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(depth, left->d_depth, (size_t)cnt[0] * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+    }
+    if (tm) HIPCHK(hipEventRecord(left->call_ev[6], s));
+    if (cnt[0] > 0 || tm) HIPCHK(hipStreamSynchronize(s));
+    if (tm) {   // {kernels, result copies}
+        HIPCHK(hipEventElapsedTime(&left->call_ms[3], left->call_ev[4], left->call_ev[5]));
+        HIPCHK(hipEventElapsedTime(&left->call_ms[4], left->call_ev[5], left->call_ev[6]));
     }
     return nm;
 }

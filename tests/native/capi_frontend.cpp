@@ -7,12 +7,16 @@
 //   ORBmatcher(0.8).SearchByProjection(F, vpMapPoints, th) through a MapPoint* <-> handle table
 //                                                                                     ORBmatcher.cc:43-213
 // usage: capi_frontend <job.bin> <out.bin>
+//        capi_frontend --latency <frames> <job.bin>   (prints one JSON line: per-frame drop-in latency)
 //   job: int32 w, h, nfeatures, n_mps, th_x100; float bf, fx; u8 left[w*h], u8 right[w*h]
 //   out: per side {int32 monoIndex, n; keypoints n x 28 B; descriptors n x 32 B}; int32 levels;
 //        float scale[levels]; stereo {int32 nmatch; float uR[nL]; float depth[nL]};
 //        map points {n_mps x orbfe_map_point}; int32 nmatches; int32 mvp[nL] (map point ids, -1)
+#include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
+#include <thread>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -171,10 +175,101 @@ struct Lcg {   // deterministic map points without <random>'s implementation-def
     float unit() { return (next() & 0xFFFFFF) / 16777216.0f; }
 };
 
+double median(std::vector<double> v) {
+    std::sort(v.begin(), v.end());
+    return v.empty() ? 0.0 : v[v.size() / 2];
+}
+
+// The drop-in path at batch 1, exactly as Tracking builds a stereo Frame (Frame.cc:122-141): the left
+// and right ORBextractor::operator() on two std::threads started per frame (ExtractORB), joined,
+// then ComputeStereoMatches (orbfe_stereo_match). Host images in, host keypoints / descriptors /
+// uR / depth out. Per frame: wall time, and the library's call timing (HIP events on each handle's
+// stream: upload, kernels, result copies) for the split; host = wall - the device-side critical path.
+int latency(int frames, const char* job) {
+    FILE* f = fopen(job, "rb");
+    if (!f) throw std::runtime_error("cannot open job");
+    int32_t hdr[5];
+    float cam[2];
+    if (fread(hdr, 4, 5, f) != 5 || fread(cam, 4, 2, f) != 2) throw std::runtime_error("short job header");
+    const int w = hdr[0], h = hdr[1], nf = hdr[2];
+    std::vector<uint8_t> L((size_t)w * h), R((size_t)w * h);
+    if (fread(L.data(), 1, L.size(), f) != L.size() || fread(R.data(), 1, R.size(), f) != R.size())
+        throw std::runtime_error("short job images");
+    fclose(f);
+    ORBextractor el(nf, 1.2f, 8, 20, 7), er(nf, 1.2f, 8, 20, 7);
+    check(orbfe_set_stage_timing(el.handle(), 1), "timing");
+    check(orbfe_set_stage_timing(er.handle(), 1), "timing");
+    std::vector<double> wall, ext, st, up, ker, cp, sker, scp, host;
+    int nkp = 0, nst = 0;
+    const int warm = 5;
+    for (int it = 0; it < warm + frames; it++) {
+        std::vector<KeyPoint> kl, kr;
+        std::vector<uint8_t> dl, dr;
+        int ml = 0, mr = 0;
+        double tl = 0, tr = 0;
+        const int lap[2] = {0, 0};
+        const auto t0 = std::chrono::steady_clock::now();
+        std::thread thL([&] {
+            const auto a = std::chrono::steady_clock::now();
+            ml = el(L.data(), w, h, w, kl, dl, lap);
+            tl = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+        });
+        std::thread thR([&] {
+            const auto a = std::chrono::steady_clock::now();
+            mr = er(R.data(), w, h, w, kr, dr, lap);
+            tr = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+        });
+        thL.join();
+        thR.join();
+        const auto t1 = std::chrono::steady_clock::now();
+        std::vector<float> ur(kl.size(), -1.f), dp(kl.size(), -1.f);
+        const int ns = orbfe_stereo_match(el.handle(), er.handle(), cam[0], cam[1], ur.data(), dp.data());
+        check(ns, "stereo_match");
+        const auto t2 = std::chrono::steady_clock::now();
+        (void)ml;
+        (void)mr;
+        if (it < warm) continue;
+        float a[5], b[5];
+        check(orbfe_get_call_timing(el.handle(), a), "call_timing");
+        check(orbfe_get_call_timing(er.handle(), b), "call_timing");
+        const double fw = std::chrono::duration<double, std::milli>(t2 - t0).count();
+        const double fs = std::chrono::duration<double, std::milli>(t2 - t1).count();
+        // the extraction's critical side is the slower thread's
+        const bool lslow = tl >= tr;
+        const float* c = lslow ? a : b;
+        wall.push_back(fw);
+        ext.push_back(std::max(tl, tr));
+        st.push_back(fs);
+        up.push_back(c[0]);
+        ker.push_back(c[1]);
+        cp.push_back(c[2]);
+        sker.push_back(a[3]);
+        scp.push_back(a[4]);
+        host.push_back(fw - (c[0] + c[1] + c[2] + a[3] + a[4]));
+        nkp = (int)(kl.size() + kr.size());
+        nst = ns;
+    }
+    printf("{\"frames\": %d, \"width\": %d, \"height\": %d, \"nfeatures\": %d, \"keypoints_lr\": %d, "
+           "\"stereo_matches\": %d, \"frame_ms\": %.4f, \"frame_ms_min\": %.4f, \"extract_lr_ms\": %.4f, "
+           "\"stereo_ms\": %.4f, \"split_ms\": {\"upload\": %.4f, \"extract_kernels\": %.4f, "
+           "\"extract_copies\": %.4f, \"stereo_kernels\": %.4f, \"stereo_copies\": %.4f, \"host\": %.4f}}\n",
+           frames, w, h, nf, nkp, nst, median(wall), *std::min_element(wall.begin(), wall.end()), median(ext),
+           median(st), median(up), median(ker), median(cp), median(sker), median(scp), median(host));
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
-    if (argc != 3) { fprintf(stderr, "usage: capi_frontend job.bin out.bin\n"); return 2; }
+    if (argc == 4 && std::string(argv[1]) == "--latency") {
+        try {
+            return latency(atoi(argv[2]), argv[3]);
+        } catch (const std::exception& e) {
+            fprintf(stderr, "capi_frontend: %s\n", e.what());
+            return 1;
+        }
+    }
+    if (argc != 3) { fprintf(stderr, "usage: capi_frontend job.bin out.bin | --latency frames job.bin\n"); return 2; }
     try {
         FILE* f = fopen(argv[1], "rb");
         if (!f) throw std::runtime_error("cannot open job");
