@@ -14,6 +14,7 @@ Prints ONE JSON line (rank 0). See DESIGN.md §Measurement for the roofline byte
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import subprocess
@@ -321,6 +322,18 @@ def parity_check(fe, images_host_pairs, frame_pair, nframes, nfeat, bf, fx, ster
                   f"launch) bit-exact vs the CPU oracle ({len(uniq)} distinct synthetic pairs tiled over the batch)")
 
 
+def _matcher_pmc():
+    """Committed counters of the config-5 search kernels (tools/gpu_matcher_pmc.sh): per th, the
+    VALU issue fraction of the pass kernel."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_matcher.json")), reverse=True):
+        if os.path.exists(f):
+            with open(f) as fh:
+                d = json.load(fh)
+            return {k: dict(v, source=os.path.basename(f)) for k, v in d.get("per_th", {}).items()}
+    return None
+
+
 def matcher_config5(steps):
     """BASELINE config 5: SearchByProjection(Frame&, local map) of 100k synthetic map points against
     a 1000-keypoint stereo frame, seed 12345, th in {1, 3, 5, 15}, nnratio 0.8 (Tracking.cc:3429).
@@ -340,6 +353,7 @@ def matcher_config5(steps):
     obs_t = torch.from_numpy(obs.copy()).to(dev_t)
     mps_t = torch.from_numpy(mps.view(np.uint8).reshape(-1).copy()).to(dev_t)
     out = {}
+    matcher_pmc = _matcher_pmc()
     for th in (1, 3, 5, 15):
         for _ in range(2):
             m.SearchByProjectionLocalMap(F, mvp0.copy(), obs, mps, th)
@@ -383,7 +397,20 @@ def matcher_config5(steps):
         torch.cuda.synchronize()
         rdt = (time.perf_counter() - t0) / steps
         assert nd == n
-        out[f"th{th}"] = {"ms_per_call": round(dt * 1e3, 4), "calls_per_s": round(1.0 / dt, 2),
+        # work counters (a separate counting call: window candidates from the level grids, candidate
+        # pairs whose Hamming distance is computed, fixed-point passes) -> pairs per second of device
+        # time; the VALU issue fraction of the search kernels comes from the committed PMC pass
+        lib.orbfe_matcher_set_stats(1)
+        m.SearchByProjectionLocalMap(F, mvp0.copy(), obs, mps, th)
+        lib.orbfe_matcher_set_stats(0)
+        wst = (ctypes.c_longlong * 3)()
+        lib.orbfe_matcher_last_stats(wst)
+        kname = "k_sbp_local_wave" if th >= 6 else "k_sbp_local"
+        mp = (matcher_pmc or {}).get(f"th{th}", {})
+        out[f"th{th}"] = {"kernel": kname, "window_candidates": int(wst[0]), "pairs": int(wst[1]),
+                          "passes": int(wst[2]), "pairs_per_s": round(wst[1] / (dms * 1e-3), 1),
+                          "window_candidates_per_s": round(wst[0] / (dms * 1e-3), 1),
+                          "valu_issue_frac": mp.get("valu_issue_frac"), "pmc_source": mp.get("source"),"ms_per_call": round(dt * 1e3, 4), "calls_per_s": round(1.0 / dt, 2),
                           "queries_per_s": round(len(mps) / dt, 1), "device_ms_per_call": round(dms, 4),
                           "device_queries_per_s": round(len(mps) / (dms * 1e-3), 1),
                           "resident_ms_per_call": round(rdt * 1e3, 4),

@@ -596,6 +596,13 @@ int orbfe_undistort_points(const float* pts, int n, const float* K4, const float
  * device time of the thread's last call in ms (-1 when not timed). For bench.py. */
 int orbfe_matcher_set_timing(int enable);
 float orbfe_matcher_last_ms(void);
+/* Work counters of the single-camera SearchByProjection(local map) searches on this thread (host
+ * and device-resident forms; off by default, one extra copy and synchronisation per call when on):
+ * out[0] = window candidates enumerated from the level grids, out[1] = candidate pairs whose
+ * Hamming distance was computed, both summed over the call's fixed-point passes, out[2] = passes
+ * evaluated (the last one confirms convergence). ORBFE_E_ARG when the last call counted nothing. */
+int orbfe_matcher_set_stats(int enable);
+int orbfe_matcher_last_stats(long long* out);
 
 /* Debug/inspection (tests only): copy an intermediate of image `image`, level `level` of the last
  * batch to host memory. what: 0 = per-cell FAST key counts (int32[n_cells]),

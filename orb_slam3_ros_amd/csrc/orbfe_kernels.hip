@@ -962,9 +962,13 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
             if (i < ncorner) {
                 p = s_cor[i];
                 const uint8_t* q = s_sc + ((p >> 7) + 1) * RS + (p & 127) + 1;
+                // all nine reads issued together (a short-circuit && chain compiles to eight
+                // dependent LDS round trips with an exec-mask branch each)
+                const int n0 = q[-RS - 1], n1 = q[-RS], n2 = q[-RS + 1], n3 = q[-1], n4 = q[1];
+                const int n5 = q[RS - 1], n6 = q[RS], n7 = q[RS + 1];
                 sc = q[0];
-                surv = sc > q[-1] && sc > q[1] && sc > q[-RS - 1] && sc > q[-RS] && sc > q[-RS + 1] &&
-                       sc > q[RS - 1] && sc > q[RS] && sc > q[RS + 1];
+                const int mx = max(max(max(n0, n1), max(n2, n3)), max(max(n4, n5), max(n6, n7)));
+                surv = sc > mx;
             }
             const unsigned long long m = __ballot(surv);
 #ifdef FAST_EXP_GRP
@@ -1429,7 +1433,10 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
         for (int t = tid; t < T_div; t += OCT_NT) {
             const int q = procp[t];
             int c = 0, e = 0;
-            for (int k = 0; k < 4; k++) { const int v = Ccnt[4 * q + k]; c += v > 0; e += v > 1; }
+            const int4 cq = *(const int4*)&Ccnt[4 * q];
+            const int cv[4] = {cq.x, cq.y, cq.z, cq.w};
+#pragma unroll
+            for (int k = 0; k < 4; k++) { c += cv[k] > 0; e += cv[k] > 1; }
             tmpB[t] = c;
             tmpC[t] = e;
         }
@@ -1439,15 +1446,24 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
         // children: block of t starts at sum_{t'>t} c_t' = Ctot - (excl_t + c_t); order n4,n3,n2,n1
         for (int t = tid; t < T_div; t += OCT_NT) {
             const int q = procp[t];
+            // the four counts in one read: the child writes below may alias them for the compiler,
+            // which would otherwise re-read each count behind the previous child's stores
+            const int4 cq = *(const int4*)&Ccnt[4 * q];
+            const int cv[4] = {cq.x, cq.y, cq.z, cq.w};
             int c = 0;
-            for (int k = 0; k < 4; k++) c += Ccnt[4 * q + k] > 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) c += cv[k] > 0;
             const int start = Ctot - (tmpB[t] + c);
             int kk = 0;
             const int px0 = Cx0[q], px1 = Cx1[q], py0 = Cy0[q], py1 = Cy1[q];
+            int cpos[4];
+#pragma unroll
             for (int ch = 3; ch >= 0; ch--) {
-                const int v = Ccnt[4 * q + ch];
+                const int v = cv[ch];
+                cpos[ch] = -1;
                 if (v > 0) {
                     const int np = start + kk++;
+                    cpos[ch] = np;
                     childpos[4 * q + ch] = (int16_t)np;
                     int a0, a1, b0, b1;
                     child_rect(ch, px0, px1, py0, py1, &a0, &a1, &b0, &b1);
@@ -1459,13 +1475,14 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
                 }
             }
             int e = tmpC[t];
+#pragma unroll
             for (int ch = 0; ch < 4; ch++) {
-                const int v = Ccnt[4 * q + ch];
+                const int v = cv[ch];
                 if (v > 1) {
                     int a0, a1, b0, b1;
                     child_rect(ch, px0, px1, py0, py1, &a0, &a1, &b0, &b1);
                     expv[e] = ((unsigned long long)v << 44) | ((unsigned long long)(a0 & 0xfff) << 32) |
-                              (unsigned long long)(uint16_t)childpos[4 * q + ch];
+                              (unsigned long long)(uint16_t)cpos[ch];
                     e++;
                 }
             }

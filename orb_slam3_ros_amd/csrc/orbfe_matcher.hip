@@ -238,7 +238,16 @@ struct PassIO {
     int* first_fill;     // first_{p+2}, cleared here
     int n;               // slots
     int need_obs;        // the slot blocks later queries only if the point has observations
+    // orbfe_matcher_set_stats: [0] window candidates enumerated (grid cells of the window, octave
+    // range), [1] candidate pairs whose Hamming distance is computed; nullptr: no counting
+    unsigned long long* stats = nullptr;
 };
+__device__ __forceinline__ void pass_stats(const PassIO& io, unsigned nwin, unsigned npair) {
+    if (io.stats && (nwin | npair)) {
+        atomicAdd(&io.stats[0], (unsigned long long)nwin);
+        atomicAdd(&io.stats[1], (unsigned long long)npair);
+    }
+}
 __device__ __forceinline__ bool pass_gated(const PassIO& io) { return io.gate && *io.gate == 0; }
 __device__ __forceinline__ void pass_fill(const PassIO& io) {
     const int nt = gridDim.x * blockDim.x;
@@ -266,13 +275,16 @@ __global__ __launch_bounds__(MT_NT) void k_sbp_local(FrameDev fr, const orbfe_ma
         if (bFactor) r *= th;
         const float R = r * fr.scale[lvl];
         int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+        unsigned nwin = 0, npair = 0;
         mt_for_area(fr, fr.pcstart + lvl * fr.gstride_c, fr.pcidx + lvl * fr.gstride_i, mp.proj_x, mp.proj_y, R,
                     lvl - 1, lvl, [&](int idx, const OrbKeyPoint& kp) {
+            nwin++;
             if (blocked0[idx] || first[idx] < q) return;
             if (fr.uright && fr.uright[idx] > 0) {
                 const float er = fabsf(mp.proj_xr - fr.uright[idx]);
                 if (er > R) return;
             }
+            npair++;
             const int dist = mt_hamming(mp.desc, fr.desc + 8 * idx);
             if (dist < bestDist) {
                 bestDist2 = bestDist; bestDist = dist;
@@ -286,6 +298,7 @@ __global__ __launch_bounds__(MT_NT) void k_sbp_local(FrameDev fr, const orbfe_ma
         if (bestDist <= MT_TH_HIGH) {
             if (!(bestLevel == bestLevel2 && bestDist > nnratio * bestDist2)) result = bestIdx;
         }
+        pass_stats(io, nwin, npair);
     }
     pass_publish(io, q, result, mp.observations);
     if (result != assign[q]) {
@@ -361,6 +374,7 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wave(FrameDev fr, const or
             const int cy1 = min(ORBFE_GRID_ROWS - 1, (int)ceilf((y - fr.miny + R) * fr.invh));
             unsigned long long b1 = ~0ull, b2 = ~0ull;
             int b1idx = -1;
+            unsigned nwin = 0, npair = 0;
             if (cx0 < ORBFE_GRID_COLS && cx1 >= 0 && cy0 < ORBFE_GRID_ROWS && cy1 >= 0 && cx0 <= cx1 && cy0 <= cy1) {
                 // one contiguous CSR run per grid column of the window (<= 64 columns)
                 const int ncell = cx1 - cx0 + 1;
@@ -380,6 +394,7 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wave(FrameDev fr, const or
                     for (int j0 = 0; j0 < tot; j0 += 64) {
                         const int j = j0 + lane;
                         if (j < tot) {
+                            nwin++;
                             int lo = 0, hi = 64;   // last cell with prefix <= j
                             while (hi - lo > 1) {
                                 const int mid = (lo + hi) >> 1;
@@ -405,6 +420,7 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wave(FrameDev fr, const or
                             ok = ok && !(blocked0[idx] || first[idx] < q);
                             if (ok && ur > 0) ok = !(fabsf(xr - ur) > R);
                             if (ok) {
+                                npair++;
                                 uint4 d0, d1;
                                 if (STAGED) { d0 = s_desc[2 * idx]; d1 = s_desc[2 * idx + 1]; }
                                 else { d0 = ((const uint4*)(fr.desc + 8 * idx))[0]; d1 = ((const uint4*)(fr.desc + 8 * idx))[1]; }
@@ -424,6 +440,7 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wave(FrameDev fr, const or
                     WAVE_SYNC();
                 }
             }
+            pass_stats(io, nwin, npair);
             const unsigned long long m1 = mt_wave_min64(b1);
             const unsigned long long win = __ballot(b1 == m1 && m1 != ~0ull);
             const unsigned long long m2 = mt_wave_min64(b1 == m1 ? b2 : b1);
@@ -1248,6 +1265,9 @@ thread_local MatchScratch t_ms;
 // Optional per-thread device timing of matcher calls (orbfe_matcher_set_timing): events bracket
 // the kernels of a call on the thread's stream (after the input upload, before the result copy).
 thread_local bool t_timing = false;
+// orbfe_matcher_set_stats: window candidates / Hamming pairs / passes of the last counted search
+thread_local bool t_stats = false;
+thread_local long long t_last_stats[3] = {-1, -1, -1};
 thread_local float t_last_ms = -1.f;
 thread_local hipEvent_t t_ev[2] = {nullptr, nullptr};
 struct MsTimer {
@@ -1544,6 +1564,7 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     const size_t o_changed = p.scratch(MT_MAX_PASSES * 4);
     const size_t o_result = p.scratch((size_t)(n + 3) * 4);   // [change flag copy | counts | slots]
     const size_t o_hist = p.scratch((MT_HISTO + 1) * 4);   // rotation bins + commit completion counter
+    const size_t o_stats = t_stats ? p.scratch(16) : 0;
     int rc = ms_prepare(p);
     if (rc) return rc;
     // a device-resident search runs on the caller's stream, after the producer of its inputs; it
@@ -1551,6 +1572,9 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     // call of the thread orders itself (host-API calls also end with a stream synchronisation)
     hipStream_t s = dev ? dev->caller : t_ms.stream;
     if (dev) HIPCHK(ms_after_tail(s));
+    unsigned long long* stats = t_stats ? ms_ptr<unsigned long long>(o_stats) : nullptr;
+    t_last_stats[0] = t_last_stats[1] = t_last_stats[2] = -1;
+    if (stats) HIPCHK(hipMemsetAsync(stats, 0, 16, s));
     MsTimer timer(s);
     const FrameDev fr = fp.view();
     const int* b0 = dev ? ms_ptr<const int>(o_b0d) : ms_ptr<const int>(o_b0);
@@ -1611,7 +1635,7 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
             for (int c = 0; c < batch; c++, pass++) {
                 if (pass >= MT_MAX_PASSES) return ORBFE_E_CAPACITY;
                 PassIO io{pass ? changed + pass - 1 : nullptr, fb[(pass + 1) % 3], fb[(pass + 2) % 3], n,
-                          mode == 2 ? 0 : 1};
+                          mode == 2 ? 0 : 1, stats};
                 const int* fcur = fb[pass % 3];
                 if (mode == 0 && th >= MT_WAVE_TH) {
                     const int nb = std::min((nq + MT_WNT / 64 - 1) / (MT_WNT / 64), 512);
@@ -1659,6 +1683,14 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
             }
             if (st[0] == 0) {
                 t_ms.pass_hint[mode] = pass0 + st[3];
+                if (stats) {   // counting mode only: one more copy and synchronisation
+                    unsigned long long hst[2];
+                    HIPCHK(hipMemcpyAsync(hst, stats, 16, hipMemcpyDeviceToHost, s));
+                    HIPCHK(hipStreamSynchronize(s));
+                    t_last_stats[0] = (long long)hst[0];
+                    t_last_stats[1] = (long long)hst[1];
+                    t_last_stats[2] = pass0 + st[3];
+                }
                 return st[1] - st[2];
             }
             batch = 6;
@@ -2013,6 +2045,17 @@ int orbfe_is_in_frustum_rig(const orbfe_frame* F, const orbfe_camera* cam, const
 int orbfe_matcher_set_timing(int enable) {
     t_timing = enable != 0;
     return ORBFE_OK;
+}
+
+int orbfe_matcher_set_stats(int enable) {
+    t_stats = enable != 0;
+    return ORBFE_OK;
+}
+
+int orbfe_matcher_last_stats(long long* out) {
+    if (!out) return ORBFE_E_ARG;
+    for (int i = 0; i < 3; i++) out[i] = t_last_stats[i];
+    return t_last_stats[2] >= 0 ? ORBFE_OK : ORBFE_E_ARG;
 }
 
 float orbfe_matcher_last_ms(void) { return t_last_ms; }
