@@ -72,6 +72,9 @@ struct orbfe_extractor {
     // split path: FAST of level 0 runs on side_stream while the resize chain runs on the batch
     // stream (fork / join events)
     hipStream_t side_stream = nullptr;
+    // small batches: level 0's DistributeOctTree (the longest serial chain of a single image) starts
+    // on this stream as soon as level 0's FAST is done, beside the pyramid chain and the other levels
+    hipStream_t oct_stream = nullptr;
     hipEvent_t ev_fork[ORBFE_MAX_LEVELS + 1] = {};
     // geometry of the current allocation
     int W = 0, H = 0, cap_b = 0;
@@ -96,6 +99,10 @@ struct orbfe_extractor {
     const uint8_t** d_ptrs = nullptr;
     uint8_t* d_stage = nullptr;    // host-API input staging (one image)
     size_t stage_bytes = 0;
+    // host-API pinned staging: the image going up, then {counts, keypoints [kp_cap], descriptors
+    // [kp_cap]} coming back in one round trip (DMA from / to pinned memory, no runtime bounce)
+    uint8_t* h_pin = nullptr;
+    size_t pin_bytes = 0;
     float* d_uright = nullptr;
     float* d_depth = nullptr;
     int* d_nmatch = nullptr;
@@ -358,6 +365,13 @@ static int ensure(orbfe_extractor* h, int W, int H, int B) {
     return ORBFE_OK;
 }
 
+// Launch shapes for small batches (the drop-in host API extracts one image per call): below
+// kSmallBatch images (or stereo frames) the kernels trade per-wave work for more, shorter waves,
+// since one image cannot fill the GPU and the frame's latency is its longest chain of dependent steps.
+constexpr int kSmallBatch = 16;
+constexpr int kSmallRsRows = 8;       // k_resize_s output rows per wave (48 for large batches)
+constexpr int kSmallStereoLk = 64;    // k_stereo left keypoints per block (ST_LK = 512)
+
 static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs, int pitch, const int* laps,
                      hipStream_t s, bool use_ext) {
     const OrbGeom& g = h->g;
@@ -394,6 +408,7 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
         HIPCHK(hipEventRecord(ev[0], s));
     }
     const bool ext = use_ext && h->ext_kps;
+    const bool small = B < kSmallBatch;   // single-image launch shapes (kSmallBatch above)
     OrbKeyPoint* o_kps = ext ? h->ext_kps : h->d_kps;
     uint8_t* o_desc = ext ? h->ext_desc : h->d_desc;
     int* o_counts = ext ? h->ext_counts : h->d_counts;
@@ -410,7 +425,9 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
         auto fast_range = [&](hipStream_t st, int l0, int l1) {
             // cells per wave: 4 for levels 0-3 (3 / 2 measured 0-2 % slower), 2 for the top levels'
             // smaller grids (4: +5 %, 1: +3 %; tools/gpu_variants_trace.sh, round 3)
-            const int cpw = l0 >= 4 ? 2 : 4;
+            // small batches (the host API's single image): one cell per wave, so the launch is as
+            // many short chains as there are cells instead of a quarter as many long ones
+            const int cpw = B < kSmallBatch ? 1 : l0 >= 4 ? 2 : 4;
             FastLds fl{0, 0, 0, 0};
             for (int l = l0; l < l1; l++) {
                 fl.roi = std::max(fl.roi, h->fast_lds_lv[l].roi);
@@ -427,6 +444,11 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
         s2 = s;   // profiling builds: every launch in stream order (isolated kernel times)
 #endif
         constexpr int kFastMid = 4;   // FAST of levels [1, kFastMid) runs on the side stream once resize has built them
+        // the pyramid chain: a small batch takes short row chunks per wave (more, shorter waves: the
+        // chain of 7 launches is the frame's critical path at batch 1)
+        OrbGeom gr = g;
+        if (B < kSmallBatch)
+            for (int l = 1; l < g.nlevels; l++) gr.lv[l].rs_rows = std::min(g.lv[l].rs_rows, kSmallRsRows);
         // side stream: FAST of level 0 at once, then of levels [1, lmid) when the chain has built
         // them (beside the chain's short, latency-bound top-level launches); batch stream: the
         // chain, then FAST of levels [lmid, nlevels)
@@ -434,6 +456,17 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
         HIPCHK(hipEventRecord(h->ev_fork[0], s));
         HIPCHK(hipStreamWaitEvent(s2, h->ev_fork[0], 0));
         fast_range(s2, 0, 1);
+        if (small) {   // level 0's octree right behind its FAST, on its own stream
+            // created on first use: a process's streams share a few hardware queues, and an extra
+            // stream must not change how the large-batch path's two streams map onto them
+            if (!h->oct_stream) HIPCHK(hipStreamCreateWithFlags(&h->oct_stream, hipStreamNonBlocking));
+            HIPCHK(hipEventRecord(h->ev_fork[3], s2));
+            HIPCHK(hipStreamWaitEvent(h->oct_stream, h->ev_fork[3], 0));
+            hipLaunchKernelGGL(k_octree, dim3(B, 1), dim3(OCT_NT), h->oct_lds, h->oct_stream, g, h->d_cellkeys,
+                               h->d_cellcnt, h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, d_laps,
+                               h->d_oct_ts, 0);
+            HIPCHK(hipEventRecord(h->ev_fork[4], h->oct_stream));
+        }
         // k_resize_s reads dwords: level 0 must be 4-byte aligned (else k_resize builds level 1)
         bool al0 = (pitch & 3) == 0;
         for (int i = 0; al0 && i < B; i++) al0 = (((uintptr_t)host_ptrs[i]) & 3) == 0;
@@ -442,9 +475,10 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
         for (int l = 1; l < g.nlevels; l++) {
             const OrbLevel& L = g.lv[l];
             if (L.rs_ok && (l > 1 || al0)) {
-                const int nstrips = (L.w + RS_COLS - 1) / RS_COLS, nitems = nstrips * ((L.h + L.rs_rows - 1) / L.rs_rows);
+                const int rows = gr.lv[l].rs_rows;
+                const int nstrips = (L.w + RS_COLS - 1) / RS_COLS, nitems = nstrips * ((L.h + rows - 1) / rows);
                 hipLaunchKernelGGL(k_resize_s, dim3((nitems + RS_WPB - 1) / RS_WPB, B), dim3(64 * RS_WPB), 0, s, P, pitch, h->d_pyr,
-                                   g.pyr_bytes, h->d_tab, g, l, nstrips, nitems);
+                                   g.pyr_bytes, h->d_tab, gr, l, nstrips, nitems);
             } else {
                 const int tiles_y = (L.h + L.rz_rows - 1) / L.rz_rows;
                 dim3 grid((L.w + L.rz_cols - 1) / L.rz_cols, (tiles_y + RZ_TPB - 1) / RZ_TPB, B);
@@ -463,11 +497,25 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
     BlurKernel bk;   // the Gaussian blur is fused into k_describe
     memcpy(bk.k, h->blur_variant == 1 ? kBlurRound : kBlurED, sizeof(bk.k));
     if (tm) HIPCHK(hipEventRecord(ev[1], s));
-    hipLaunchKernelGGL(k_octree, dim3(B, g.nlevels), dim3(OCT_NT), h->oct_lds, s, g, h->d_cellkeys, h->d_cellcnt,
-                       h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, d_laps, h->d_oct_ts);
+    if (small) {
+        if (g.nlevels > 1)
+            hipLaunchKernelGGL(k_octree, dim3(B, g.nlevels - 1), dim3(OCT_NT), h->oct_lds, s, g, h->d_cellkeys,
+                               h->d_cellcnt, h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, d_laps,
+                               h->d_oct_ts, 1);
+        HIPCHK(hipStreamWaitEvent(s, h->ev_fork[4], 0));
+    } else {
+        hipLaunchKernelGGL(k_octree, dim3(B, g.nlevels), dim3(OCT_NT), h->oct_lds, s, g, h->d_cellkeys, h->d_cellcnt,
+                           h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, d_laps, h->d_oct_ts, 0);
+    }
     if (tm) HIPCHK(hipEventRecord(ev[2], s));
-    hipLaunchKernelGGL(k_describe, dim3((g.out_per_img + DP_WPB * DP_KPW - 1) / (DP_WPB * DP_KPW), B), dim3(64 * DP_WPB), 0, s, P, pitch, h->d_pyr,
-                       g.pyr_bytes, g, h->d_outkeys, h->d_lvinfo, h->d_ranks, o_kps, o_desc, o_counts, bk);
+    if (B < kSmallBatch)   // one keypoint per wave: short chains for the single-image host API
+        hipLaunchKernelGGL(k_describe<1>, dim3((g.out_per_img + DP_WPB - 1) / DP_WPB, B), dim3(64 * DP_WPB), 0, s, P,
+                           pitch, h->d_pyr, g.pyr_bytes, g, h->d_outkeys, h->d_lvinfo, h->d_ranks, o_kps, o_desc,
+                           o_counts, bk);
+    else
+        hipLaunchKernelGGL(k_describe<DP_KPW>, dim3((g.out_per_img + DP_WPB * DP_KPW - 1) / (DP_WPB * DP_KPW), B),
+                           dim3(64 * DP_WPB), 0, s, P, pitch, h->d_pyr, g.pyr_bytes, g, h->d_outkeys, h->d_lvinfo,
+                           h->d_ranks, o_kps, o_desc, o_counts, bk);
     if (tm) HIPCHK(hipEventRecord(ev[3], s));
     HIPCHK(hipGetLastError());
     h->last_kps = o_kps;
@@ -577,6 +625,7 @@ void orbfe_extractor_destroy(orbfe_extractor* h) {
     (void)hipDeviceSynchronize();
     free_buffers(h);
     if (h->d_stage) (void)hipFree(h->d_stage);
+    if (h->h_pin) (void)hipHostFree(h->h_pin);
     if (h->d_uright) (void)hipFree(h->d_uright);
     if (h->d_depth) (void)hipFree(h->d_depth);
     if (h->d_nmatch) (void)hipFree(h->d_nmatch);
@@ -586,6 +635,7 @@ void orbfe_extractor_destroy(orbfe_extractor* h) {
     for (int i = 0; i <= ORBFE_MAX_LEVELS; i++)
         if (h->ev_fork[i]) (void)hipEventDestroy(h->ev_fork[i]);
     if (h->side_stream) (void)hipStreamDestroy(h->side_stream);
+    if (h->oct_stream) (void)hipStreamDestroy(h->oct_stream);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
 }
@@ -723,8 +773,21 @@ int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int width, int height,
     const bool tm = h->timing;
     if (tm && !h->call_ev[0])
         for (auto& e : h->call_ev) HIPCHK(hipEventCreate(&e));
+    const size_t kpb = (size_t)h->g.kp_cap * sizeof(OrbKeyPoint), db = (size_t)h->g.kp_cap * 32;
+    const size_t pin_need = std::max(bytes, 16 + kpb + db);
+    if (h->pin_bytes < pin_need) {
+        if (h->h_pin) HIPCHK(hipHostFree(h->h_pin));
+        h->h_pin = nullptr;
+        h->pin_bytes = 0;
+        HIPCHK(hipHostMalloc((void**)&h->h_pin, pin_need, hipHostMallocDefault));
+        h->pin_bytes = pin_need;
+    }
+    // the previous call's result copies out of h_pin have completed (that call synchronised)
+    if (stride == width) memcpy(h->h_pin, img, bytes);
+    else
+        for (int y = 0; y < height; y++) memcpy(h->h_pin + (size_t)y * width, img + (size_t)y * stride, width);
     if (tm) HIPCHK(hipEventRecord(h->call_ev[0], s));
-    HIPCHK(hipMemcpy2DAsync(h->d_stage, width, img, stride, width, height, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(h->d_stage, h->h_pin, bytes, hipMemcpyHostToDevice, s));
     if (tm) HIPCHK(hipEventRecord(h->call_ev[1], s));
     const uint8_t* ptrs[1] = {h->d_stage};
     const int laps[2] = {lap0, lap1};
@@ -733,18 +796,23 @@ int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int width, int height,
     h->timing = tm;
     if (rc) return rc;
     if (tm) HIPCHK(hipEventRecord(h->call_ev[2], s));
-    int cnt[2];
-    HIPCHK(hipMemcpyAsync(cnt, h->last_counts, 8, hipMemcpyDeviceToHost, s));
+    // counts and the whole keypoint / descriptor capacity in one round trip (61 KB at 1000
+    // features: one transfer costs less than a second synchronisation)
+    uint8_t* hp = h->h_pin;
+    HIPCHK(hipMemcpyAsync(hp, h->last_counts, 8, hipMemcpyDeviceToHost, s));
+    if (kps) HIPCHK(hipMemcpyAsync(hp + 16, h->last_kps, kpb, hipMemcpyDeviceToHost, s));
+    if (desc) HIPCHK(hipMemcpyAsync(hp + 16 + kpb, h->last_desc, db, hipMemcpyDeviceToHost, s));
+    if (tm) HIPCHK(hipEventRecord(h->call_ev[3], s));
     HIPCHK(hipStreamSynchronize(s));
+    int cnt[2];
+    memcpy(cnt, hp, 8);
     *n = cnt[0];
     if (cnt[0] > cap) return ORBFE_E_CAPACITY;
     if (cnt[0] > 0) {
-        if (kps) HIPCHK(hipMemcpyAsync(kps, h->last_kps, (size_t)cnt[0] * sizeof(OrbKeyPoint), hipMemcpyDeviceToHost, s));
-        if (desc) HIPCHK(hipMemcpyAsync(desc, h->last_desc, (size_t)cnt[0] * 32, hipMemcpyDeviceToHost, s));
+        if (kps) memcpy(kps, hp + 16, (size_t)cnt[0] * sizeof(OrbKeyPoint));
+        if (desc) memcpy(desc, hp + 16 + kpb, (size_t)cnt[0] * 32);
     }
-    if (tm) HIPCHK(hipEventRecord(h->call_ev[3], s));
-    if (cnt[0] > 0 || tm) HIPCHK(hipStreamSynchronize(s));
-    if (tm) {   // {upload, kernels, result copies (incl. the count read-back round trip)}
+    if (tm) {   // {upload, kernels, result copies}
         HIPCHK(hipEventElapsedTime(&h->call_ms[0], h->call_ev[0], h->call_ev[1]));
         HIPCHK(hipEventElapsedTime(&h->call_ms[1], h->call_ev[1], h->call_ev[2]));
         HIPCHK(hipEventElapsedTime(&h->call_ms[2], h->call_ev[2], h->call_ev[3]));
@@ -796,7 +864,10 @@ int orbfe_stereo_match_batch(orbfe_extractor* left, int lbase, int lstep, orbfe_
     int sort_cap = 1;
     while (sort_cap < g.kp_cap) sort_cap <<= 1;
     if (g.height + 2 * ST_ROFF + 1 <= (ST_NT / 64) * 128) sort_cap = (g.kp_cap + 3) & ~3;   // 16-byte aligned tail
-    StereoArgs sa{bf, fx, g.kp_cap, sort_cap};
+    // a small batch of frames splits each frame's left keypoints over more blocks (each restages the
+    // right side: redundant work, but the frame's chain of keypoints per wave is what bounds batch 1)
+    const int lkpb = nframes < kSmallBatch ? kSmallStereoLk : ST_LK;
+    StereoArgs sa{bf, fx, g.kp_cap, sort_cap, lkpb};
     const size_t lds = (size_t)g.kp_cap * (32 + sizeof(RightRec)) + (size_t)sort_cap * 4 + (ST_NT / 64) * (512 + 128 * 4) +
                        (size_t)round_up(2 * (g.height + 2 * ST_ROFF), 16);
     if (lds > 160 * 1024 - 64 || g.kp_cap > 65535) return ORBFE_E_ARG;   // LDS: about 2700 keypoints per image
@@ -810,7 +881,7 @@ int orbfe_stereo_match_batch(orbfe_extractor* left, int lbase, int lstep, orbfe_
         left->sdist_frames = nframes;
         left->sdist_kp = g.kp_cap;
     }
-    hipLaunchKernelGGL(k_stereo, dim3((g.kp_cap + ST_LK - 1) / ST_LK, nframes), dim3(ST_NT), lds, s, g, SL, SR, sa,
+    hipLaunchKernelGGL(k_stereo, dim3((g.kp_cap + lkpb - 1) / lkpb, nframes), dim3(ST_NT), lds, s, g, SL, SR, sa,
                        d_uright, d_depth, left->d_sdist);
     hipLaunchKernelGGL(k_stereo_cut, dim3(nframes), dim3(256), 0, s, g, SL, sa, d_uright, d_depth, left->d_sdist,
                        d_nmatch);
@@ -840,16 +911,30 @@ int orbfe_stereo_match(orbfe_extractor* left, orbfe_extractor* right, float bf, 
                                       left->d_nmatch, nullptr);
     if (rc) return rc;
     if (tm) HIPCHK(hipEventRecord(left->call_ev[5], s));
-    int cnt[2], nm = 0;
-    HIPCHK(hipMemcpyAsync(cnt, left->last_counts, 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&nm, left->d_nmatch, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    if (cnt[0] > 0) {
-        HIPCHK(hipMemcpyAsync(uright, left->d_uright, (size_t)cnt[0] * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(depth, left->d_depth, (size_t)cnt[0] * 4, hipMemcpyDeviceToHost, s));
+    // counts, nmatch and the whole uR / depth capacity in one round trip through pinned memory
+    const size_t kc = (size_t)left->g.kp_cap;
+    const size_t need = 16 + 8 * kc;
+    if (left->pin_bytes < need) {
+        if (left->h_pin) HIPCHK(hipHostFree(left->h_pin));
+        left->h_pin = nullptr;
+        left->pin_bytes = 0;
+        HIPCHK(hipHostMalloc((void**)&left->h_pin, need, hipHostMallocDefault));
+        left->pin_bytes = need;
     }
+    uint8_t* hp = left->h_pin;
+    HIPCHK(hipMemcpyAsync(hp, left->last_counts, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hp + 8, left->d_nmatch, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hp + 16, left->d_uright, 4 * kc, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hp + 16 + 4 * kc, left->d_depth, 4 * kc, hipMemcpyDeviceToHost, s));
     if (tm) HIPCHK(hipEventRecord(left->call_ev[6], s));
-    if (cnt[0] > 0 || tm) HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipStreamSynchronize(s));
+    int cnt[2], nm = 0;
+    memcpy(cnt, hp, 8);
+    memcpy(&nm, hp + 8, 4);
+    if (cnt[0] > 0) {
+        memcpy(uright, hp + 16, (size_t)cnt[0] * 4);
+        memcpy(depth, hp + 16 + 4 * kc, (size_t)cnt[0] * 4);
+    }
     if (tm) {   // {kernels, result copies}
         HIPCHK(hipEventElapsedTime(&left->call_ms[3], left->call_ev[4], left->call_ev[5]));
         HIPCHK(hipEventElapsedTime(&left->call_ms[4], left->call_ev[5], left->call_ev[6]));

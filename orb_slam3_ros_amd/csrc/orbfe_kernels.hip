@@ -1272,10 +1272,11 @@ __global__ __launch_bounds__(OCT_NT) void k_debug_block_sort(unsigned long long*
 __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __restrict__ cellkeys,
                                                    const int* __restrict__ cellcnt, uint32_t* lkeys,
                                                    uint16_t* nodeof, uint32_t* outkeys, int* lvinfo, int* ranks,
-                                                   const int2* __restrict__ laps, unsigned long long* tstamp) {
+                                                   const int2* __restrict__ laps, unsigned long long* tstamp,
+                                                   int lv0) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_oct[];
-    // grid (B, nlevels): level-0 blocks (the longest) are dispatched first
-    const int b = blockIdx.x, l = blockIdx.y, tid = threadIdx.x;
+    // grid (B, levels from lv0): level-0 blocks (the longest) are dispatched first
+    const int b = blockIdx.x, l = lv0 + (int)blockIdx.y, tid = threadIdx.x;
     const int lap0 = laps[b].x, lap1 = laps[b].y;   // this image's vLappingArea
     const OrbLevel& L = g.lv[l];
     const int NC = g.node_cap;
@@ -1903,6 +1904,7 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
 #define DP_ATTR __attribute__((amdgpu_waves_per_eu(6)))
 #define DP_WPB 2   // waves per block: 2 / 4 / 8 measured 1.04 / 1.06 / 1.11 ms (r03_kernel_ab.txt item 23);
                    // 12 blocks of 12.7 KB per CU give the same 6 waves per SIMD with finer-grained refill
+template <int KPW>
 __global__ __launch_bounds__(64 * DP_WPB) DP_ATTR void k_describe(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                                   int pyr_stride, OrbGeom g, const uint32_t* __restrict__ outkeys,
                                                   const int* __restrict__ lvinfo, const int* __restrict__ ranks,
@@ -1918,7 +1920,7 @@ __global__ __launch_bounds__(64 * DP_WPB) DP_ATTR void k_describe(const uint8_t*
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
     const int b = lb / gridDim.x;
-    const int flat0 = ((lb % gridDim.x) * DP_WPB + wave) * DP_KPW;   // first of this wave's output slots
+    const int flat0 = ((lb % gridDim.x) * DP_WPB + wave) * KPW;   // first of this wave's output slots
     if (flat0 >= g.out_per_img) return;
     // the rBRIEF pairs of this lane (pair 64 * mm + lane: x0, y0, x1, y1), issued first
     uint2 pat[4];
@@ -1927,7 +1929,7 @@ __global__ __launch_bounds__(64 * DP_WPB) DP_ATTR void k_describe(const uint8_t*
     // keys and ranks of the wave's slots (lane j: slot flat0 + j), one load each
     uint32_t kv = 0;
     int rv = 0;
-    if (lane < DP_KPW && flat0 + lane < g.out_per_img) {
+    if (lane < KPW && flat0 + lane < g.out_per_img) {
         kv = outkeys[(size_t)b * g.out_per_img + flat0 + lane];
         rv = ranks[(size_t)b * g.out_per_img + flat0 + lane];
     }
@@ -1940,7 +1942,7 @@ __global__ __launch_bounds__(64 * DP_WPB) DP_ATTR void k_describe(const uint8_t*
     orbfe_u32x4 pq[3];
     if (cur.valid && cur.interior) desc_load(cur, lane, pq);
 #pragma unroll
-    for (int j = 0; j < DP_KPW; j++) {
+    for (int j = 0; j < KPW; j++) {
         // ---- stage the raw patch: raw[r][c] = level(y - 21 + r, x - 21 + c), reflect-101 outside ----
         if (cur.valid) {
             if (cur.interior) {
@@ -1958,7 +1960,7 @@ __global__ __launch_bounds__(64 * DP_WPB) DP_ATTR void k_describe(const uint8_t*
         // the next slot's patch loads fly while this one is described
         DescSlot nxt;
         nxt.valid = 0;
-        if (j + 1 < DP_KPW) {
+        if (j + 1 < KPW) {
             nxt = desc_slot(imgs, in_pitch, pyr, pyr_stride, g, di, kv, rv, j + 1, &lvl, b, flat0 + j + 1);
             if (nxt.valid && nxt.interior) desc_load(nxt, lane, pq);
         }
@@ -1980,6 +1982,7 @@ struct StereoArgs {
     float bf, fx;
     int max_kp;
     int sort_cap;   // LDS sort keys: >= max_kp, a power of two for the bitonic fallback
+    int lk;         // left keypoints per block (ST_LK; fewer for a small batch of frames)
 };
 // One side (left or right camera) of a batch of frames: image f of this side is image
 // (base + f*step) of the extractor batch whose buffers are given here.
@@ -2020,7 +2023,7 @@ __global__ __launch_bounds__(ST_NT) void k_stereo(OrbGeom g, StereoSide SL, Ster
     const int bL = SL.base + f * SL.step, bR = SR.base + f * SR.step;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     const int N = SL.counts[2 * bL], Nr = SR.counts[2 * bR];
-    const int i0 = (lb % gridDim.x) * ST_LK;
+    const int i0 = (lb % gridDim.x) * sa.lk;
     if (i0 >= N) return;
     // right records ordered by a counting sort over band rows when the row table fits (every image
     // up to 1983 rows), else by a bitonic sort of P = pow2 >= Nr keys (sa.sort_cap is sized to match)
@@ -2111,7 +2114,7 @@ __global__ __launch_bounds__(ST_NT) void k_stereo(OrbGeom g, StereoSide SL, Ster
     int* sd_out = sdist + (size_t)f * g.kp_cap;
     const float mb = sa.bf / sa.fx;   // intended mb = mbf/fx (the reference reads it uninitialised)
     const float minZ = mb, minD = 0.f, maxD = sa.bf / minZ;
-    const int iend = min(N, i0 + ST_LK);
+    const int iend = min(N, i0 + sa.lk);
     // the first keypoint of each wave is static; later ones come from a block counter, so waves whose
     // keypoints scan few candidates take more of them and the block ends with its work, not with its
     // slowest wave's fixed share (253 -> 236 us per 512 frames; r03_kernel_ab.txt item 29)
