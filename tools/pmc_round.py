@@ -29,12 +29,20 @@ import os
 VALU_PEAK = 1024 * 2.4e9 / 2
 
 
+def kname(full):
+    """'void orbfe::k_describe<4>(...)' -> 'k_describe' (template instances of a kernel pooled)."""
+    k = full.split("(")[0].replace("orbfe::", "")
+    if k.startswith("void "):
+        k = k[5:]
+    return k.split("<")[0].strip()
+
+
 def counters(d):
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     n = collections.defaultdict(set)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"].split("(")[0].replace("orbfe::", "")
+            k = kname(r["Kernel_Name"])
             acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
             n[k].add(r["Dispatch_Id"])
     return acc, {k: len(v) for k, v in n.items()}
@@ -53,7 +61,7 @@ def main():
     dur = collections.defaultdict(float)
     launches = collections.Counter()
     for r in csv.DictReader(open(tr)):
-        k = r["Kernel_Name"].split("(")[0].replace("orbfe::", "")
+        k = kname(r["Kernel_Name"])
         dur[k] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
         launches[k] += 1
     steps = launches["k_octree"] or 1
