@@ -370,7 +370,19 @@ static int ensure(orbfe_extractor* h, int W, int H, int B) {
 // since one image cannot fill the GPU and the frame's latency is its longest chain of dependent steps.
 constexpr int kSmallBatch = 16;
 constexpr int kSmallRsRows = 8;       // k_resize_s output rows per wave (48 for large batches)
-constexpr int kSmallStereoLk = 64;    // k_stereo left keypoints per block (ST_LK = 512)
+constexpr int kSmallStereoLk = 64;
+// The pyramid chain's top levels at large batches: short row chunks per wave from level kRsTopLevel
+// up. Those launches have few waves, each walking its chunk's rows in a serial chain, and they
+// share the machine with level 0's FAST on the side stream: the chain's latency is the pass's
+// critical path.
+#ifndef RS_TOP_LEVEL
+#define RS_TOP_LEVEL 99
+#endif
+#ifndef RS_TOP_ROWS
+#define RS_TOP_ROWS 48
+#endif
+constexpr int kRsTopLevel = RS_TOP_LEVEL;
+constexpr int kRsTopRows = RS_TOP_ROWS;    // k_stereo left keypoints per block (ST_LK = 512)
 
 static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs, int pitch, const int* laps,
                      hipStream_t s, bool use_ext) {
@@ -447,8 +459,9 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
         // the pyramid chain: a small batch takes short row chunks per wave (more, shorter waves: the
         // chain of 7 launches is the frame's critical path at batch 1)
         OrbGeom gr = g;
-        if (B < kSmallBatch)
-            for (int l = 1; l < g.nlevels; l++) gr.lv[l].rs_rows = std::min(g.lv[l].rs_rows, kSmallRsRows);
+        for (int l = 1; l < g.nlevels; l++)
+            if (B < kSmallBatch) gr.lv[l].rs_rows = std::min(g.lv[l].rs_rows, kSmallRsRows);
+            else if (l >= kRsTopLevel) gr.lv[l].rs_rows = std::min(g.lv[l].rs_rows, kRsTopRows);
         // side stream: FAST of level 0 at once, then of levels [1, lmid) when the chain has built
         // them (beside the chain's short, latency-bound top-level launches); batch stream: the
         // chain, then FAST of levels [lmid, nlevels)
