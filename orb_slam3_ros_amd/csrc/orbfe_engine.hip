@@ -57,6 +57,15 @@ size_t octree_lds_bytes(const OrbGeom& g) {
     return s;
 }
 
+// Output block of a batch of B images with kp_cap slots each: counts (2 ints per image) at 0,
+// keypoints from *kps, descriptors from *desc (16-byte aligned), *end bytes in all.
+void out_layout(int B, int kp_cap, size_t* kps, size_t* desc, size_t* end) {
+    auto a16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    *kps = a16((size_t)B * 8);
+    *desc = a16(*kps + (size_t)B * kp_cap * sizeof(OrbKeyPoint));
+    *end = *desc + (size_t)B * kp_cap * 32;
+}
+
 }  // namespace
 
 struct orbfe_extractor {
@@ -93,6 +102,7 @@ struct orbfe_extractor {
     uint32_t* d_outkeys = nullptr;
     int* d_lvinfo = nullptr;
     int* d_ranks = nullptr;
+    uint8_t* d_out = nullptr;      // one allocation: d_counts | d_kps | d_desc (out_layout)
     OrbKeyPoint* d_kps = nullptr;
     uint8_t* d_desc = nullptr;
     int* d_counts = nullptr;
@@ -103,6 +113,16 @@ struct orbfe_extractor {
     // [kp_cap]} coming back in one round trip (DMA from / to pinned memory, no runtime bounce)
     uint8_t* h_pin = nullptr;
     size_t pin_bytes = 0;
+    // host-API call graph: orbfe_extract's upload, launches and result copies captured once per
+    // configuration (key: width, height, lap0, lap1, keypoints / descriptors wanted) and replayed as
+    // one graph launch; dropped whenever the buffers it names go away (graph_gen)
+    bool use_graph = true;         // ORBFE_GRAPH=0 disables
+    hipGraphExec_t x_graph = nullptr;
+    int x_key[6] = {};
+    int x_calls = 0;               // consecutive plain calls with the current key
+    unsigned graph_gen = 0, x_gen = 0;
+    // host-API stereo results in one allocation {nmatch (16 B) | uR [stereo_kp] | depth [stereo_kp]}
+    uint8_t* d_st = nullptr;
     float* d_uright = nullptr;
     float* d_depth = nullptr;
     int* d_nmatch = nullptr;
@@ -136,15 +156,25 @@ struct orbfe_extractor {
     unsigned long long* d_oct_ts = nullptr;   // -DORBFE_OCT_STAMPS builds: per-phase s_memtime of the octree (image 0)
 };
 
+static void drop_graph(orbfe_extractor* h) {
+    if (h->x_graph) (void)hipGraphExecDestroy(h->x_graph);
+    h->x_graph = nullptr;
+    h->x_calls = 0;
+}
+
 static void free_buffers(orbfe_extractor* h) {
+    drop_graph(h);
+    h->graph_gen++;
     void** bufs[] = {(void**)&h->d_tab, (void**)&h->d_pyr, (void**)&h->d_cellkeys,
                      (void**)&h->d_cellcnt, (void**)&h->d_lkeys, (void**)&h->d_nodeof, (void**)&h->d_outkeys,
-                     (void**)&h->d_lvinfo, (void**)&h->d_ranks, (void**)&h->d_kps, (void**)&h->d_desc,
-                     (void**)&h->d_counts, (void**)&h->d_ptrs};
+                     (void**)&h->d_lvinfo, (void**)&h->d_ranks, (void**)&h->d_out, (void**)&h->d_ptrs};
     for (void** p : bufs) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
+    h->d_kps = nullptr;   // inside d_out
+    h->d_desc = nullptr;
+    h->d_counts = nullptr;
     h->cap_b = 0;
     h->last_nimg = 0;   // the previous batch's intermediates are gone
     h->last_kps = nullptr;
@@ -355,9 +385,14 @@ static int ensure(orbfe_extractor* h, int W, int H, int B) {
     HIPCHK(hipMalloc(&h->d_outkeys, (size_t)B * g.out_per_img * 4));
     HIPCHK(hipMalloc(&h->d_lvinfo, (size_t)B * g.nlevels * 4 * 4));
     HIPCHK(hipMalloc(&h->d_ranks, (size_t)B * g.out_per_img * 4));
-    HIPCHK(hipMalloc(&h->d_kps, (size_t)B * g.kp_cap * sizeof(OrbKeyPoint)));
-    HIPCHK(hipMalloc(&h->d_desc, (size_t)B * g.kp_cap * 32));
-    HIPCHK(hipMalloc(&h->d_counts, (size_t)B * 2 * 4));
+    // outputs in one block, {counts | keypoints | descriptors} (out_layout): for one image it is the
+    // host API's pinned result layout, so orbfe_extract brings it back in a single copy
+    size_t o_kps, o_desc, o_end;
+    out_layout(B, g.kp_cap, &o_kps, &o_desc, &o_end);
+    HIPCHK(hipMalloc(&h->d_out, o_end));
+    h->d_counts = (int*)h->d_out;
+    h->d_kps = (OrbKeyPoint*)(h->d_out + o_kps);
+    h->d_desc = h->d_out + o_desc;
     HIPCHK(hipMalloc(&h->d_ptrs, (size_t)B * (sizeof(void*) + 2 * sizeof(int))));   // image pointers, then laps
     h->cap_b = B;
     h->last_ptrs.clear();
@@ -371,18 +406,11 @@ static int ensure(orbfe_extractor* h, int W, int H, int B) {
 constexpr int kSmallBatch = 16;
 constexpr int kSmallRsRows = 8;       // k_resize_s output rows per wave (48 for large batches)
 constexpr int kSmallStereoLk = 64;
-// The pyramid chain's top levels at large batches: short row chunks per wave from level kRsTopLevel
-// up. Those launches have few waves, each walking its chunk's rows in a serial chain, and they
-// share the machine with level 0's FAST on the side stream: the chain's latency is the pass's
-// critical path.
-#ifndef RS_TOP_LEVEL
-#define RS_TOP_LEVEL 99
+#ifndef SMALL_OCT_NT
+#define SMALL_OCT_NT 1024
 #endif
-#ifndef RS_TOP_ROWS
-#define RS_TOP_ROWS 48
-#endif
-constexpr int kRsTopLevel = RS_TOP_LEVEL;
-constexpr int kRsTopRows = RS_TOP_ROWS;    // k_stereo left keypoints per block (ST_LK = 512)
+constexpr int kSmallOctNt = SMALL_OCT_NT;   // k_octree threads per (image, level) block (OCT_NT = 256)
+   // k_stereo left keypoints per block (ST_LK = 512)
 
 static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs, int pitch, const int* laps,
                      hipStream_t s, bool use_ext) {
@@ -459,9 +487,8 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
         // the pyramid chain: a small batch takes short row chunks per wave (more, shorter waves: the
         // chain of 7 launches is the frame's critical path at batch 1)
         OrbGeom gr = g;
-        for (int l = 1; l < g.nlevels; l++)
-            if (B < kSmallBatch) gr.lv[l].rs_rows = std::min(g.lv[l].rs_rows, kSmallRsRows);
-            else if (l >= kRsTopLevel) gr.lv[l].rs_rows = std::min(g.lv[l].rs_rows, kRsTopRows);
+        if (B < kSmallBatch)
+            for (int l = 1; l < g.nlevels; l++) gr.lv[l].rs_rows = std::min(g.lv[l].rs_rows, kSmallRsRows);
         // side stream: FAST of level 0 at once, then of levels [1, lmid) when the chain has built
         // them (beside the chain's short, latency-bound top-level launches); batch stream: the
         // chain, then FAST of levels [lmid, nlevels)
@@ -475,7 +502,7 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
             if (!h->oct_stream) HIPCHK(hipStreamCreateWithFlags(&h->oct_stream, hipStreamNonBlocking));
             HIPCHK(hipEventRecord(h->ev_fork[3], s2));
             HIPCHK(hipStreamWaitEvent(h->oct_stream, h->ev_fork[3], 0));
-            hipLaunchKernelGGL(k_octree, dim3(B, 1), dim3(OCT_NT), h->oct_lds, h->oct_stream, g, h->d_cellkeys,
+            hipLaunchKernelGGL(k_octree<kSmallOctNt>, dim3(B, 1), dim3(kSmallOctNt), h->oct_lds, h->oct_stream, g, h->d_cellkeys,
                                h->d_cellcnt, h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, d_laps,
                                h->d_oct_ts, 0);
             HIPCHK(hipEventRecord(h->ev_fork[4], h->oct_stream));
@@ -512,12 +539,12 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
     if (tm) HIPCHK(hipEventRecord(ev[1], s));
     if (small) {
         if (g.nlevels > 1)
-            hipLaunchKernelGGL(k_octree, dim3(B, g.nlevels - 1), dim3(OCT_NT), h->oct_lds, s, g, h->d_cellkeys,
+            hipLaunchKernelGGL(k_octree<kSmallOctNt>, dim3(B, g.nlevels - 1), dim3(kSmallOctNt), h->oct_lds, s, g, h->d_cellkeys,
                                h->d_cellcnt, h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, d_laps,
                                h->d_oct_ts, 1);
         HIPCHK(hipStreamWaitEvent(s, h->ev_fork[4], 0));
     } else {
-        hipLaunchKernelGGL(k_octree, dim3(B, g.nlevels), dim3(OCT_NT), h->oct_lds, s, g, h->d_cellkeys, h->d_cellcnt,
+        hipLaunchKernelGGL(k_octree<OCT_NT>, dim3(B, g.nlevels), dim3(OCT_NT), h->oct_lds, s, g, h->d_cellkeys, h->d_cellcnt,
                            h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, d_laps, h->d_oct_ts, 0);
     }
     if (tm) HIPCHK(hipEventRecord(ev[2], s));
@@ -620,6 +647,7 @@ int orbfe_extractor_create(int nfeatures, float scaleFactor, int nlevels, int in
     int prio_lo = 0, prio_hi = 0;   // the side stream yields to the batch stream's critical path
     if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&h->side_stream, hipStreamNonBlocking, prio_lo);
+    if (const char* v = getenv("ORBFE_GRAPH")) h->use_graph = atoi(v) != 0;
     for (int i = 0; e == hipSuccess && i <= ORBFE_MAX_LEVELS; i++)
         e = hipEventCreateWithFlags(&h->ev_fork[i], hipEventDisableTiming);
     for (int i = 0; e == hipSuccess && i <= ORBFE_NUM_STAGES; i++) e = hipEventCreate(&h->ev[i]);
@@ -636,12 +664,10 @@ void orbfe_extractor_destroy(orbfe_extractor* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     (void)hipDeviceSynchronize();
-    free_buffers(h);
+    free_buffers(h);   // (and the call graph)
     if (h->d_stage) (void)hipFree(h->d_stage);
     if (h->h_pin) (void)hipHostFree(h->h_pin);
-    if (h->d_uright) (void)hipFree(h->d_uright);
-    if (h->d_depth) (void)hipFree(h->d_depth);
-    if (h->d_nmatch) (void)hipFree(h->d_nmatch);
+    if (h->d_st) (void)hipFree(h->d_st);
     if (h->d_sdist) (void)hipFree(h->d_sdist);
     for (int i = 0; i <= ORBFE_NUM_STAGES; i++)
         if (h->ev[i]) (void)hipEventDestroy(h->ev[i]);
@@ -779,6 +805,7 @@ int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int width, int height,
     hipStream_t s = h->own_stream;
     const size_t bytes = (size_t)width * height;
     if (h->stage_bytes < bytes) {
+        drop_graph(h);
         if (h->d_stage) HIPCHK(hipFree(h->d_stage));
         HIPCHK(hipMalloc(&h->d_stage, bytes));
         h->stage_bytes = bytes;
@@ -786,9 +813,13 @@ int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int width, int height,
     const bool tm = h->timing;
     if (tm && !h->call_ev[0])
         for (auto& e : h->call_ev) HIPCHK(hipEventCreate(&e));
+    // the pinned result layout is a one-image output block (out_layout)
+    size_t o_kps, o_desc, o_end;
+    out_layout(1, h->g.kp_cap, &o_kps, &o_desc, &o_end);
     const size_t kpb = (size_t)h->g.kp_cap * sizeof(OrbKeyPoint), db = (size_t)h->g.kp_cap * 32;
-    const size_t pin_need = std::max(bytes, 16 + kpb + db);
+    const size_t pin_need = std::max(bytes, o_end);
     if (h->pin_bytes < pin_need) {
+        drop_graph(h);
         if (h->h_pin) HIPCHK(hipHostFree(h->h_pin));
         h->h_pin = nullptr;
         h->pin_bytes = 0;
@@ -799,31 +830,75 @@ int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int width, int height,
     if (stride == width) memcpy(h->h_pin, img, bytes);
     else
         for (int y = 0; y < height; y++) memcpy(h->h_pin + (size_t)y * width, img + (size_t)y * stride, width);
-    if (tm) HIPCHK(hipEventRecord(h->call_ev[0], s));
-    HIPCHK(hipMemcpyAsync(h->d_stage, h->h_pin, bytes, hipMemcpyHostToDevice, s));
-    if (tm) HIPCHK(hipEventRecord(h->call_ev[1], s));
     const uint8_t* ptrs[1] = {h->d_stage};
     const int laps[2] = {lap0, lap1};
-    h->timing = false;   // the call's own events bracket the kernels (the stage ring is for batches)
-    rc = run_batch(h, 1, ptrs, width, laps, s, false);
-    h->timing = tm;
-    if (rc) return rc;
-    if (tm) HIPCHK(hipEventRecord(h->call_ev[2], s));
-    // counts and the whole keypoint / descriptor capacity in one round trip (61 KB at 1000
-    // features: one transfer costs less than a second synchronisation)
     uint8_t* hp = h->h_pin;
-    HIPCHK(hipMemcpyAsync(hp, h->last_counts, 8, hipMemcpyDeviceToHost, s));
-    if (kps) HIPCHK(hipMemcpyAsync(hp + 16, h->last_kps, kpb, hipMemcpyDeviceToHost, s));
-    if (desc) HIPCHK(hipMemcpyAsync(hp + 16 + kpb, h->last_desc, db, hipMemcpyDeviceToHost, s));
-    if (tm) HIPCHK(hipEventRecord(h->call_ev[3], s));
+    // the whole call as stream work: upload, the batch launches, and counts plus the whole keypoint /
+    // descriptor capacity back in one round trip (61 KB at 1000 features: one transfer costs less
+    // than a second synchronisation)
+    auto enqueue = [&]() -> int {
+        if (tm) HIPCHK(hipEventRecord(h->call_ev[0], s));
+        HIPCHK(hipMemcpyAsync(h->d_stage, h->h_pin, bytes, hipMemcpyHostToDevice, s));
+        if (tm) HIPCHK(hipEventRecord(h->call_ev[1], s));
+        h->timing = false;   // the call's own events bracket the kernels (the stage ring is for batches)
+        const int r = run_batch(h, 1, ptrs, width, laps, s, false);
+        h->timing = tm;
+        if (r) return r;
+        if (tm) HIPCHK(hipEventRecord(h->call_ev[2], s));
+        if (h->cap_b == 1 && kps && desc) {   // the handle's one-image output block: one copy
+            HIPCHK(hipMemcpyAsync(hp, h->d_out, o_end, hipMemcpyDeviceToHost, s));
+        } else {
+            HIPCHK(hipMemcpyAsync(hp, h->last_counts, 8, hipMemcpyDeviceToHost, s));
+            if (kps) HIPCHK(hipMemcpyAsync(hp + o_kps, h->last_kps, kpb, hipMemcpyDeviceToHost, s));
+            if (desc) HIPCHK(hipMemcpyAsync(hp + o_desc, h->last_desc, db, hipMemcpyDeviceToHost, s));
+        }
+        if (tm) HIPCHK(hipEventRecord(h->call_ev[3], s));
+        return ORBFE_OK;
+    };
+    // graph replay needs the state the captured launches assume: this configuration's key, the same
+    // buffers (graph_gen), and the device batch description still naming the staging image (a batch
+    // call in between re-uploads it through the plain path)
+    const int key[6] = {width, height, lap0, lap1, kps != nullptr, desc != nullptr};
+    const bool key_same = memcmp(key, h->x_key, sizeof(key)) == 0;
+    const bool desc_same = h->last_nimg == 1 && h->last_ptrs.size() == 1 && h->last_ptrs[0] == h->d_stage &&
+                           h->last_laps.size() == 2 && h->last_laps[0] == lap0 && h->last_laps[1] == lap1;
+    if (h->x_graph && !(key_same && h->x_gen == h->graph_gen && desc_same)) drop_graph(h);
+    if (!h->use_graph || tm) {
+        rc = enqueue();
+        if (rc) return rc;
+    } else if (h->x_graph) {
+        HIPCHK(hipGraphLaunch(h->x_graph, s));
+    } else if (key_same && h->x_calls >= 1 && desc_same) {
+        // second plain call with this key: its launches are captured and replayed from now on
+        // (run_batch sees the same batch description, so nothing inside synchronises)
+        hipGraph_t gr = nullptr;
+        HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        rc = enqueue();
+        const hipError_t ce = hipStreamEndCapture(s, &gr);
+        if (rc) {
+            if (gr) (void)hipGraphDestroy(gr);
+            return rc;
+        }
+        HIPCHK(ce);
+        hipError_t ie = hipGraphInstantiateWithFlags(&h->x_graph, gr, 0);
+        (void)hipGraphDestroy(gr);
+        HIPCHK(ie);
+        h->x_gen = h->graph_gen;
+        HIPCHK(hipGraphLaunch(h->x_graph, s));
+    } else {
+        rc = enqueue();
+        if (rc) return rc;
+        memcpy(h->x_key, key, sizeof(key));
+        h->x_calls = key_same ? h->x_calls + 1 : 1;
+    }
     HIPCHK(hipStreamSynchronize(s));
     int cnt[2];
     memcpy(cnt, hp, 8);
     *n = cnt[0];
     if (cnt[0] > cap) return ORBFE_E_CAPACITY;
     if (cnt[0] > 0) {
-        if (kps) memcpy(kps, hp + 16, (size_t)cnt[0] * sizeof(OrbKeyPoint));
-        if (desc) memcpy(desc, hp + 16 + kpb, (size_t)cnt[0] * 32);
+        if (kps) memcpy(kps, hp + o_kps, (size_t)cnt[0] * sizeof(OrbKeyPoint));
+        if (desc) memcpy(desc, hp + o_desc, (size_t)cnt[0] * 32);
     }
     if (tm) {   // {upload, kernels, result copies}
         HIPCHK(hipEventElapsedTime(&h->call_ms[0], h->call_ev[0], h->call_ev[1]));
@@ -906,14 +981,16 @@ int orbfe_stereo_match(orbfe_extractor* left, orbfe_extractor* right, float bf, 
                        float* depth) {
     if (!left || !right) return ORBFE_E_ARG;
     std::lock_guard<std::mutex> lk(left->mu);
-    if (!left->d_uright || left->stereo_kp < left->g.kp_cap) {   // (re)size for the current geometry
-        if (left->d_uright) HIPCHK(hipFree(left->d_uright));
-        if (left->d_depth) HIPCHK(hipFree(left->d_depth));
+    if (!left->d_st || left->stereo_kp < left->g.kp_cap) {   // (re)size for the current geometry
+        if (left->d_st) HIPCHK(hipFree(left->d_st));
+        left->d_st = nullptr;
         left->d_uright = left->d_depth = nullptr;
+        left->d_nmatch = nullptr;
         left->stereo_kp = 0;
-        HIPCHK(hipMalloc(&left->d_uright, (size_t)left->g.kp_cap * 4));
-        HIPCHK(hipMalloc(&left->d_depth, (size_t)left->g.kp_cap * 4));
-        if (!left->d_nmatch) HIPCHK(hipMalloc(&left->d_nmatch, 4));
+        HIPCHK(hipMalloc(&left->d_st, 16 + (size_t)left->g.kp_cap * 8));
+        left->d_nmatch = (int*)left->d_st;
+        left->d_uright = (float*)(left->d_st + 16);
+        left->d_depth = left->d_uright + left->g.kp_cap;
         left->stereo_kp = left->g.kp_cap;
     }
     HIPCHK(hipStreamSynchronize(right->own_stream));
@@ -924,10 +1001,12 @@ int orbfe_stereo_match(orbfe_extractor* left, orbfe_extractor* right, float bf, 
                                       left->d_nmatch, nullptr);
     if (rc) return rc;
     if (tm) HIPCHK(hipEventRecord(left->call_ev[5], s));
-    // counts, nmatch and the whole uR / depth capacity in one round trip through pinned memory
-    const size_t kc = (size_t)left->g.kp_cap;
-    const size_t need = 16 + 8 * kc;
+    // counts, then {nmatch | the whole uR / depth capacity} in one copy, one round trip through
+    // pinned memory
+    const size_t kc = (size_t)left->stereo_kp;
+    const size_t need = 32 + 8 * kc;
     if (left->pin_bytes < need) {
+        drop_graph(left);   // its result copy names the old buffer
         if (left->h_pin) HIPCHK(hipHostFree(left->h_pin));
         left->h_pin = nullptr;
         left->pin_bytes = 0;
@@ -936,17 +1015,15 @@ int orbfe_stereo_match(orbfe_extractor* left, orbfe_extractor* right, float bf, 
     }
     uint8_t* hp = left->h_pin;
     HIPCHK(hipMemcpyAsync(hp, left->last_counts, 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(hp + 8, left->d_nmatch, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(hp + 16, left->d_uright, 4 * kc, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(hp + 16 + 4 * kc, left->d_depth, 4 * kc, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hp + 16, left->d_st, 16 + 8 * kc, hipMemcpyDeviceToHost, s));
     if (tm) HIPCHK(hipEventRecord(left->call_ev[6], s));
     HIPCHK(hipStreamSynchronize(s));
     int cnt[2], nm = 0;
     memcpy(cnt, hp, 8);
-    memcpy(&nm, hp + 8, 4);
+    memcpy(&nm, hp + 16, 4);
     if (cnt[0] > 0) {
-        memcpy(uright, hp + 16, (size_t)cnt[0] * 4);
-        memcpy(depth, hp + 16 + 4 * kc, (size_t)cnt[0] * 4);
+        memcpy(uright, hp + 32, (size_t)cnt[0] * 4);
+        memcpy(depth, hp + 32 + 4 * kc, (size_t)cnt[0] * 4);
     }
     if (tm) {   // {kernels, result copies}
         HIPCHK(hipEventElapsedTime(&left->call_ms[3], left->call_ev[4], left->call_ev[5]));

@@ -1073,11 +1073,12 @@ __device__ __forceinline__ void child_rect(int q, int x0, int x1, int y0, int y1
     *cy0 = (q & 2) ? my : y0;
     *cy1 = (q & 2) ? y1 : my;
 }
-// Block-wide (OCT_NT threads) in-place exclusive scan of arr[0..n); returns the total.
+// Block-wide (NT threads) in-place exclusive scan of arr[0..n); returns the total.
+template <int NT>
 __device__ __forceinline__ int block_excl_scan(int* arr, int n, int* s_ws) {
     const int lane = lane_id(), wave = threadIdx.x >> 6;
     int carry = 0;
-    for (int base = 0; base < n; base += OCT_NT) {
+    for (int base = 0; base < n; base += NT) {
         const int i = base + threadIdx.x;
         const int v = i < n ? arr[i] : 0;
         const int incl = wave_incl_scan(v);
@@ -1085,7 +1086,7 @@ __device__ __forceinline__ int block_excl_scan(int* arr, int n, int* s_ws) {
         SYNC();
         int woff = 0, tot = 0;
 #pragma unroll
-        for (int w = 0; w < OCT_NT / 64; w++) {
+        for (int w = 0; w < NT / 64; w++) {
             const int t = s_ws[w];
             woff += w < wave ? t : 0;
             tot += t;
@@ -1269,7 +1270,11 @@ __global__ __launch_bounds__(OCT_NT) void k_debug_block_sort(unsigned long long*
     for (int i = threadIdx.x; i < n; i += OCT_NT) a[i] = la[i];
 }
 
-__global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __restrict__ cellkeys,
+// NT = 256 threads per (image, level) for batches; a small batch (the host API's single image,
+// where the level-0 and level-1 blocks are the frame's long pole and nothing else competes for
+// the CUs) takes NT = 1024: the key sweeps and scans run in a quarter of the iterations.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_octree(OrbGeom g, const uint32_t* __restrict__ cellkeys,
                                                    const int* __restrict__ cellcnt, uint32_t* lkeys,
                                                    uint16_t* nodeof, uint32_t* outkeys, int* lvinfo, int* ranks,
                                                    const int2* __restrict__ laps, unsigned long long* tstamp,
@@ -1307,7 +1312,7 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
     // the last step: 12 * NC bytes less LDS (7 blocks per CU instead of 6 at EuRoC geometry; the
     // kernel time is set by the level-0 blocks' serial steps, so this measured only -0.6 %)
     int4* segs = (int4*)carve(sizeof(int4) * ORBFE_SORT_STACK);
-    __shared__ int s_ws[OCT_NT / 64];
+    __shared__ int s_ws[NT / 64];
     __shared__ int s_misc[8];
 
     // diagnostic phase stamps (image 0 of the batch, every level), tstamp == nullptr in normal runs
@@ -1317,15 +1322,15 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
     OCT_STAMP();
     // ---- gather this level's cell key lists in cell order (vToDistributeKeys order) ----
     const int* cc = cellcnt + (size_t)b * g.total_cells + L.cell_base;
-    for (int i = tid; i < ncell; i += OCT_NT) cellpre[i] = cc[i];
+    for (int i = tid; i < ncell; i += NT) cellpre[i] = cc[i];
     SYNC();
-    const int K = block_excl_scan(cellpre, ncell, s_ws);
+    const int K = block_excl_scan<NT>(cellpre, ncell, s_ws);
     if (tid == 0) cellpre[ncell] = K;
     const int nIni = L.n_ini;
     const float hX = L.hx;
     const int H = (L.h - ORBFE_MINB) - ORBFE_MINB;
-    for (int i = tid; i < nIni; i += OCT_NT) tmpA[i] = 0;
-    for (int i = tid; i < 4 * NC; i += OCT_NT) Ccnt[i] = 0;
+    for (int i = tid; i < nIni; i += NT) tmpA[i] = 0;
+    for (int i = tid; i < 4 * NC; i += NT) Ccnt[i] = 0;
     SYNC();
     const size_t kbase = (size_t)b * g.cellkeys_per_img + L.cellkey_off;
     uint32_t* keys = lkeys + kbase;
@@ -1333,12 +1338,12 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
     const uint32_t* ck = cellkeys + kbase;
     // the gather also counts the keys of each initial node (ORBextractor.cc:559-601's root columns;
     // wave-uniform trip counts: the aggregated increments need every lane)
-    for (int kb = 0; kb < K; kb += OCT_NT * OCT_U) {
+    for (int kb = 0; kb < K; kb += NT * OCT_U) {
         const int k0 = kb + tid;
         uint32_t v[OCT_U];
 #pragma unroll
         for (int u = 0; u < OCT_U; u++) {
-            const int k = min(k0 + OCT_NT * u, K - 1);
+            const int k = min(k0 + NT * u, K - 1);
             int lo = 0, hi = ncell - 1;   // largest c with cellpre[c] <= k
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
@@ -1348,17 +1353,17 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
         }
 #pragma unroll
         for (int u = 0; u < OCT_U; u++) {
-            if (k0 + OCT_NT * u < K) keys[k0 + OCT_NT * u] = v[u];
-            atomic_inc_runs(tmpA, (int)((float)(v[u] & 0xfff) / hX), k0 + OCT_NT * u < K);
+            if (k0 + NT * u < K) keys[k0 + NT * u] = v[u];
+            atomic_inc_runs(tmpA, (int)((float)(v[u] & 0xfff) / hX), k0 + NT * u < K);
         }
     }
     OCT_STAMP();
     // ---- initial nodes (ORBextractor.cc:559-601) ----
     SYNC();
-    for (int i = tid; i < nIni; i += OCT_NT) tmpB[i] = tmpA[i] > 0 ? 1 : 0;
+    for (int i = tid; i < nIni; i += NT) tmpB[i] = tmpA[i] > 0 ? 1 : 0;
     SYNC();
-    int n = block_excl_scan(tmpB, nIni, s_ws);   // position of each non-empty root
-    for (int i = tid; i < nIni; i += OCT_NT) {
+    int n = block_excl_scan<NT>(tmpB, nIni, s_ws);   // position of each non-empty root
+    for (int i = tid; i < nIni; i += NT) {
         if (tmpA[i] > 0) {
             const int q = tmpB[i];
             Cx0[q] = (int16_t)(int)(hX * (float)i);
@@ -1369,21 +1374,21 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
         }
     }
     SYNC();
-    for (int kb = 0; kb < K; kb += OCT_NT * OCT_U) {
+    for (int kb = 0; kb < K; kb += NT * OCT_U) {
         const int k0 = kb + tid;
         uint32_t v[OCT_U];
 #pragma unroll
-        for (int u = 0; u < OCT_U; u++) v[u] = keys[min(k0 + OCT_NT * u, K - 1)];
+        for (int u = 0; u < OCT_U; u++) v[u] = keys[min(k0 + NT * u, K - 1)];
 #pragma unroll
         for (int u = 0; u < OCT_U; u++) {
-            const int k = k0 + OCT_NT * u;
+            const int k = k0 + NT * u;
             const uint32_t key = v[u];
             const int q = tmpB[(int)((float)(key & 0xfff) / hX)];
             if (k < K) nof[k] = (uint16_t)q;
             atomic_inc_runs(Ccnt, 4 * q + quadrant(key, Cx0[q], Cx1[q], Cy0[q], Cy1[q]), k < K && Csz[q] > 1);
         }
     }
-    for (int i = tid; i < NC; i += OCT_NT) divorder[i] = -1;
+    for (int i = tid; i < NC; i += NT) divorder[i] = -1;
     SYNC();
     OCT_STAMP();
 
@@ -1396,11 +1401,11 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
         int T_div;   // number of divided nodes in this step
         if (!phase2) {
             // every node with >1 keys divides, in list order
-            for (int i = tid; i < n; i += OCT_NT) tmpA[i] = Csz[i] > 1 ? 1 : 0;
+            for (int i = tid; i < n; i += NT) tmpA[i] = Csz[i] > 1 ? 1 : 0;
             SYNC();
-            for (int i = tid; i < n; i += OCT_NT) divorder[i] = Csz[i] > 1 ? 1 : -1;
-            T_div = block_excl_scan(tmpA, n, s_ws);   // tmpA[i] = divider rank t (list order)
-            for (int i = tid; i < n; i += OCT_NT)
+            for (int i = tid; i < n; i += NT) divorder[i] = Csz[i] > 1 ? 1 : -1;
+            T_div = block_excl_scan<NT>(tmpA, n, s_ws);   // tmpA[i] = divider rank t (list order)
+            for (int i = tid; i < n; i += NT)
                 if (divorder[i] >= 0) { divorder[i] = tmpA[i]; procp[tmpA[i]] = i; }
             SYNC();
         } else {
@@ -1409,7 +1414,7 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
                             s_misc);
             // walk from the back until the list reaches N (ORBextractor.cc:701-748): processed node t is
             // expv[m-1-t]; the list grows by (children - 1) per division -> first t where it reaches N
-            for (int t = tid; t < m; t += OCT_NT) {
+            for (int t = tid; t < m; t += NT) {
                 const int q = (int)(expv[m - 1 - t] & 0xffffffffull);
                 const int4 cq = *(const int4*)&Ccnt[4 * q];
                 tmpA[t] = (cq.x > 0) + (cq.y > 0) + (cq.z > 0) + (cq.w > 0) - 1;
@@ -1417,8 +1422,8 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
             }
             if (tid == 0) s_misc[6] = m;
             SYNC();
-            (void)block_excl_scan(tmpA, m, s_ws);   // tmpA[t] = growth before processing t
-            for (int t = tid; t < m; t += OCT_NT) {
+            (void)block_excl_scan<NT>(tmpA, m, s_ws);   // tmpA[t] = growth before processing t
+            for (int t = tid; t < m; t += NT) {
                 const int q = procp[t];
                 const int4 cq = *(const int4*)&Ccnt[4 * q];
                 const int grow = (cq.x > 0) + (cq.y > 0) + (cq.z > 0) + (cq.w > 0) - 1;
@@ -1426,12 +1431,12 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
             }
             SYNC();
             T_div = s_misc[6];
-            for (int t = tid; t < T_div; t += OCT_NT) divorder[procp[t]] = t;
+            for (int t = tid; t < T_div; t += NT) divorder[procp[t]] = t;
             SYNC();
         }
         OCT_STAMP();
         // children counts per processed node (t order): tmpB = nonempty, tmpC = expandable (>1)
-        for (int t = tid; t < T_div; t += OCT_NT) {
+        for (int t = tid; t < T_div; t += NT) {
             const int q = procp[t];
             int c = 0, e = 0;
             const int4 cq = *(const int4*)&Ccnt[4 * q];
@@ -1442,10 +1447,10 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
             tmpC[t] = e;
         }
         SYNC();
-        const int Ctot = block_excl_scan(tmpB, T_div, s_ws);
-        const int Etot = block_excl_scan(tmpC, T_div, s_ws);
+        const int Ctot = block_excl_scan<NT>(tmpB, T_div, s_ws);
+        const int Etot = block_excl_scan<NT>(tmpC, T_div, s_ws);
         // children: block of t starts at sum_{t'>t} c_t' = Ctot - (excl_t + c_t); order n4,n3,n2,n1
-        for (int t = tid; t < T_div; t += OCT_NT) {
+        for (int t = tid; t < T_div; t += NT) {
             const int q = procp[t];
             // the four counts in one read: the child writes below may alias them for the compiler,
             // which would otherwise re-read each count behind the previous child's stores
@@ -1489,10 +1494,10 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
             }
         }
         // undivided nodes keep their relative order after the pushed children
-        for (int i = tid; i < n; i += OCT_NT) tmpA[i] = divorder[i] < 0 ? 1 : 0;
+        for (int i = tid; i < n; i += NT) tmpA[i] = divorder[i] < 0 ? 1 : 0;
         SYNC();
-        const int nKeep = block_excl_scan(tmpA, n, s_ws);
-        for (int i = tid; i < n; i += OCT_NT) {
+        const int nKeep = block_excl_scan<NT>(tmpA, n, s_ws);
+        for (int i = tid; i < n; i += NT) {
             if (divorder[i] < 0) {
                 const int np = Ctot + tmpA[i];
                 newpos[i] = (int16_t)np;
@@ -1502,23 +1507,23 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
             }
         }
         const int newN = Ctot + nKeep;
-        for (int i = tid; i < 4 * newN; i += OCT_NT) Xcnt[i] = 0;
+        for (int i = tid; i < 4 * newN; i += NT) Xcnt[i] = 0;
         SYNC();
         OCT_STAMP();
         // key sweep: move keys to their new node positions and count the next split
-        for (int kb = 0; kb < K; kb += OCT_NT * OCT_U) {
+        for (int kb = 0; kb < K; kb += NT * OCT_U) {
             const int k0 = kb + tid;
             uint32_t v[OCT_U];
             int qv[OCT_U];
 #pragma unroll
             for (int u = 0; u < OCT_U; u++) {
-                const int k = min(k0 + OCT_NT * u, K - 1);
+                const int k = min(k0 + NT * u, K - 1);
                 v[u] = keys[k];
                 qv[u] = nof[k];
             }
 #pragma unroll
             for (int u = 0; u < OCT_U; u++) {
-                const int k = k0 + OCT_NT * u;
+                const int k = k0 + NT * u;
                 const uint32_t key = v[u];
                 const int q = qv[u];
                 int np;
@@ -1529,7 +1534,7 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
             }
         }
         SYNC();
-        for (int i = tid; i < NC; i += OCT_NT) divorder[i] = -1;
+        for (int i = tid; i < NC; i += NT) divorder[i] = -1;
         {
             int16_t* t;
             int* ti;
@@ -1547,20 +1552,20 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
     OCT_STAMP();
     // ---- retain the best key per node ----
     unsigned long long* best = (unsigned long long*)Xcnt;
-    for (int i = tid; i < n; i += OCT_NT) best[i] = 0ull;
+    for (int i = tid; i < n; i += NT) best[i] = 0ull;
     SYNC();
-    for (int k0 = tid; k0 < K; k0 += OCT_NT * OCT_U) {
+    for (int k0 = tid; k0 < K; k0 += NT * OCT_U) {
         uint32_t v[OCT_U];
         int qv[OCT_U];
 #pragma unroll
         for (int u = 0; u < OCT_U; u++) {
-            const int k = min(k0 + OCT_NT * u, K - 1);
+            const int k = min(k0 + NT * u, K - 1);
             v[u] = keys[k];
             qv[u] = nof[k];
         }
 #pragma unroll
         for (int u = 0; u < OCT_U; u++) {
-            const int k = k0 + OCT_NT * u;
+            const int k = k0 + NT * u;
             if (k < K)
                 atomicMax(&best[qv[u]], ((unsigned long long)(v[u] >> 24) << 32) | (0xFFFFFFFFull - (unsigned)k));
         }
@@ -1569,7 +1574,7 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
     uint32_t* ok = outkeys + (size_t)b * g.out_per_img + L.out_off;
     int* rk = ranks + (size_t)b * g.out_per_img + L.out_off;
     // lapping flag per output node, then ranks among lapping / non-lapping keys (block scans)
-    for (int i = tid; i < n; i += OCT_NT) {
+    for (int i = tid; i < n; i += NT) {
         const unsigned k = 0xFFFFFFFFu - (unsigned)(best[i] & 0xFFFFFFFFull);
         const uint32_t key = keys[k];
         const int x = (int)(key & 0xfff) + ORBFE_MINB, y = (int)((key >> 12) & 0xfff) + ORBFE_MINB;
@@ -1580,9 +1585,9 @@ __global__ __launch_bounds__(OCT_NT) void k_octree(OrbGeom g, const uint32_t* __
         tmpB[i] = lap ? 0 : 1;
     }
     SYNC();
-    const int nlap = block_excl_scan(tmpA, n, s_ws);
-    const int nmono = block_excl_scan(tmpB, n, s_ws);
-    for (int i = tid; i < n; i += OCT_NT) {
+    const int nlap = block_excl_scan<NT>(tmpA, n, s_ws);
+    const int nmono = block_excl_scan<NT>(tmpB, n, s_ws);
+    for (int i = tid; i < n; i += NT) {
         const bool lap = (i + 1 < n ? tmpA[i + 1] : nlap) != tmpA[i];
         rk[i] = lap ? (int)(0x40000000 | tmpA[i]) : tmpB[i];
     }

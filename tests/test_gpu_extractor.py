@@ -186,3 +186,47 @@ def test_stereo_matches_tall_image(gpu, oracle_lib):
     assert np.array_equal(ur.view(np.uint32), our.view(np.uint32)), np.nonzero(ur != our)[0][:10]
     assert np.array_equal(dp.view(np.uint32), odp.view(np.uint32))
     assert (ur >= 0).sum() > 0.3 * len(kl)
+
+
+def test_host_call_graph_replay(gpu, oracle_lib):
+    """orbfe_extract captures its call (upload, launches, result copies) as a HIP graph on the second
+    call with one configuration and replays it from then on. Every call stays bit-exact across image
+    changes, a lapping-area change (a new capture), a batch call on the same handle in between (the
+    plain path re-uploads the batch description) and an OpenCV-model round trip (buffers rebuilt);
+    the pyramid getter reads the replayed call's levels."""
+    import ctypes
+
+    import torch
+    from orb_slam3_ros_amd.extractor import ORBextractor
+    ext = ORBextractor(1000, 1.2, 8, 20, 7)
+    ora = oracle_lib.OracleExtractor(1000, 1.2, 8, 20, 7)
+
+    def check(img, lap):
+        mono_g, kp_g, d_g = ext(img, None, lap)
+        mono_o, kp_o, d_o = ora(img, lap)
+        assert mono_g == mono_o and len(kp_g) == len(kp_o)
+        assert np.array_equal(kp_g.view(np.uint8), kp_o.view(np.uint8))
+        assert np.array_equal(d_g, d_o)
+
+    seeds = iter(range(300, 400))
+    for lap in [(0, 0)] * 4 + [(0, 1000)] * 3:
+        check(synth_image(next(seeds), 752, 480), lap)
+    # the last replayed call's pyramid, as Frame reads mvImagePyramid
+    img = synth_image(next(seeds), 752, 480)
+    check(img, (0, 1000))
+    for l in (0, 3, 7):
+        assert np.array_equal(ext.pyramid_level(l), ora.pyramid_level(l))
+    # a batch call on the same handle between two host calls
+    batch = torch.from_numpy(np.stack([synth_image(next(seeds), 752, 480) for _ in range(2)])).cuda()
+    ptrs = (ctypes.c_void_p * 2)(*(batch[i].data_ptr() for i in range(2)))
+    assert ext._lib.orbfe_extract_batch(ext.handle, 2, ptrs, 752, 480, 752, 0, 1000, None) == 0
+    torch.cuda.synchronize()
+    for _ in range(3):
+        check(synth_image(next(seeds), 752, 480), (0, 1000))
+    # buffers rebuilt by a model change (the replayed graph names the old ones) and back
+    for lanes in (8, 16):
+        ext.set_opencv_model(lanes, 0)
+        ora._l.oro_set_model(ora.h, lanes, 0)
+        for _ in range(3):
+            check(synth_image(next(seeds), 752, 480), (0, 1000))
+    ext.close()
