@@ -1898,17 +1898,26 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
     emit_kp(angle);
 }
 
-#define DP_KPW 4   // slots per wave: the next slot's patch loads overlap this slot's compute (a wave
-                   // alone is two dependent memory round trips per slot: keys, then the patch). 8 slots
-                   // (an 8-byte spill with the f16 pattern) ran the kernel alone 1.07 -> 1.04 ms but
-                   // doubled its HBM reads (twice the images resident per XCD overflow its L2: hit rate
-                   // 0.84 -> 0.70) and left the full step unchanged (r03_kernel_ab.txt item 19)
+// DP_KPW: slots per wave: the next slot's patch loads overlap this slot's compute (a wave alone is
+// two dependent memory round trips per slot: keys, then the patch). 8 slots (an 8-byte spill with
+// the f16 pattern) ran the kernel alone 1.07 -> 1.04 ms but doubled its HBM reads (twice the images
+// resident per XCD overflow its L2: hit rate 0.84 -> 0.70) and left the full step unchanged
+// (r03_kernel_ab.txt item 19)
+#ifndef DP_KPW
+#define DP_KPW 4
+#endif
 // 6 waves per SIMD: 79 VGPRs, no spill since the pattern is held as f16 (at 5 waves without a spill
 // or 6 with one the kernel measured slower or equal: 1 slot / 4 slots at 5, 6, 7 waves, 2, 3 and 8
 // slots, tools/gpu_variants_trace.sh; DESIGN.md §7d, profiles/r03_kernel_ab.txt items 18-19)
-#define DP_ATTR __attribute__((amdgpu_waves_per_eu(6)))
-#define DP_WPB 2   // waves per block: 2 / 4 / 8 measured 1.04 / 1.06 / 1.11 ms (r03_kernel_ab.txt item 23);
-                   // 12 blocks of 12.7 KB per CU give the same 6 waves per SIMD with finer-grained refill
+#ifndef DP_WPE
+#define DP_WPE 6
+#endif
+#define DP_ATTR __attribute__((amdgpu_waves_per_eu(DP_WPE)))
+// DP_WPB: waves per block: 2 / 4 / 8 measured 1.04 / 1.06 / 1.11 ms (r03_kernel_ab.txt item 23); 12
+// blocks of 12.7 KB per CU give the same 6 waves per SIMD with finer-grained refill
+#ifndef DP_WPB
+#define DP_WPB 2
+#endif
 template <int KPW>
 __global__ __launch_bounds__(64 * DP_WPB) DP_ATTR void k_describe(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                                   int pyr_stride, OrbGeom g, const uint32_t* __restrict__ outkeys,
