@@ -312,7 +312,9 @@ __global__ __launch_bounds__(MT_NT) void k_sbp_local(FrameDev fr, const orbfe_ma
 // flattened with a wave prefix sum) and keep the two smallest (dist, enumeration index) keys —
 // exactly the reference's sequential best / second-best (a later equal distance never displaces
 // an earlier one). Persistent blocks stage the frame's keypoints and descriptors in LDS.
+#ifndef MT_WAVE_TH
 #define MT_WAVE_TH 6.0f
+#endif
 #define MT_STAGE_MAX 1536
 __device__ __forceinline__ unsigned long long mt_wave_min64(unsigned long long v) {
 #pragma unroll
@@ -323,6 +325,36 @@ __device__ __forceinline__ unsigned long long mt_wave_min64(unsigned long long v
     }
     return v;
 }
+// The same minimum with DPP moves inside each row of 16 lanes (quad swaps, then half-row and row
+// mirrors: every lane of a row ends with the row minimum) and four readlanes across the rows: a
+// wave-uniform result with no LDS round trip (the shuffle form costs twelve dependent
+// ds_bpermutes per call, two calls per query on the wave kernel's serial per-query chain).
+template <int CTRL>
+__device__ __forceinline__ unsigned long long mt_min64_dpp_step(unsigned long long v) {
+    const unsigned hi = (unsigned)(v >> 32), lo = (unsigned)v;
+    const unsigned oh = (unsigned)__builtin_amdgcn_update_dpp((int)hi, (int)hi, CTRL, 0xf, 0xf, false);
+    const unsigned ol = (unsigned)__builtin_amdgcn_update_dpp((int)lo, (int)lo, CTRL, 0xf, 0xf, false);
+    const unsigned long long o = ((unsigned long long)oh << 32) | ol;
+    return o < v ? o : v;
+}
+__device__ __forceinline__ unsigned long long mt_wave_min64_dpp(unsigned long long v) {
+    v = mt_min64_dpp_step<0xB1>(v);    // quad_perm [1, 0, 3, 2]
+    v = mt_min64_dpp_step<0x4E>(v);    // quad_perm [2, 3, 0, 1]
+    v = mt_min64_dpp_step<0x141>(v);   // row_half_mirror
+    v = mt_min64_dpp_step<0x140>(v);   // row_mirror
+    unsigned long long m = ~0ull;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const unsigned long long x =
+            ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(v >> 32), 16 * r) << 32) |
+            (unsigned)__builtin_amdgcn_readlane((int)v, 16 * r);
+        m = x < m ? x : m;
+    }
+    return m;
+}
+#ifndef MT_WAVE_DPP
+#define MT_WAVE_DPP 1
+#endif
 #define MT_WNT 1024   // 16 waves per block share one staged copy of the frame
 template <bool STAGED>
 __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wave(FrameDev fr, const orbfe_map_point* mps, int nq, float th,
@@ -334,6 +366,9 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wave(FrameDev fr, const or
     int2* s_cell = (int2*)mt_sm;                                          // [16][64] (start, exclusive prefix)
     float4* s_key = (float4*)(mt_sm + (MT_WNT / 64) * 64 * sizeof(int2));  // x, y, octave bits, uR
     uint4* s_desc = (uint4*)(s_key + (STAGED ? fr.n : 0));         // 2 x uint4 per keypoint
+    // {blocked0, first} per keypoint (read-only during a pass): the gate of every candidate without
+    // a global round trip on the query's chain
+    int2* s_gate = (int2*)(s_desc + (STAGED ? 2 * fr.n : 0));
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     if (STAGED) {
         for (int i = tid; i < fr.n; i += MT_WNT) {
@@ -342,6 +377,7 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wave(FrameDev fr, const or
             const uint4* d = (const uint4*)(fr.desc + 8 * i);
             s_desc[2 * i] = d[0];
             s_desc[2 * i + 1] = d[1];
+            s_gate[i] = make_int2(blocked0[i], first[i]);
         }
         SYNC();
     }
@@ -349,6 +385,7 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wave(FrameDev fr, const or
     constexpr int WPB = MT_WNT / 64;
     for (int q = blockIdx.x * WPB + wave; q < nq; q += gridDim.x * WPB) {
         const orbfe_map_point& mp = mps[q];
+        const int prev = assign[q];   // issued first: read only by the publish at the chain's end
         int result = -1;
         if ((mp.flags & ORBFE_MP_IN_VIEW) && !(bFar && mp.depth > thFar) && !(mp.flags & ORBFE_MP_BAD) &&
             mp.scale_level >= 0 && mp.scale_level < fr.nlevels) {
@@ -417,7 +454,12 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wave(FrameDev fr, const or
                                 if (maxLevel >= 0 && oct > maxLevel) ok = false;
                             }
                             ok = ok && fabsf(kx - x) < R && fabsf(ky - y) < R;
-                            ok = ok && !(blocked0[idx] || first[idx] < q);
+                            if (STAGED) {
+                                const int2 gt = s_gate[idx];
+                                ok = ok && !(gt.x || gt.y < q);
+                            } else {
+                                ok = ok && !(blocked0[idx] || first[idx] < q);
+                            }
                             if (ok && ur > 0) ok = !(fabsf(xr - ur) > R);
                             if (ok) {
                                 npair++;
@@ -441,9 +483,15 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wave(FrameDev fr, const or
                 }
             }
             pass_stats(io, nwin, npair);
+#if MT_WAVE_DPP
+            const unsigned long long m1 = mt_wave_min64_dpp(b1);
+            const unsigned long long win = __ballot(b1 == m1 && m1 != ~0ull);
+            const unsigned long long m2 = mt_wave_min64_dpp(b1 == m1 ? b2 : b1);
+#else
             const unsigned long long m1 = mt_wave_min64(b1);
             const unsigned long long win = __ballot(b1 == m1 && m1 != ~0ull);
             const unsigned long long m2 = mt_wave_min64(b1 == m1 ? b2 : b1);
+#endif
             if (m1 != ~0ull) {
                 const int wl = __ffsll((long long)win) - 1;
                 const int bestIdx = __shfl(b1idx, wl, 64);
@@ -457,7 +505,7 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wave(FrameDev fr, const or
         }
         if (lane == 0) {
             pass_publish(io, q, result, mp.observations);
-            if (result != assign[q]) {
+            if (result != prev) {
                 assign[q] = result;
                 atomicAdd(changed, 1);
             }
@@ -1639,7 +1687,7 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
                 const int* fcur = fb[pass % 3];
                 if (mode == 0 && th >= MT_WAVE_TH) {
                     const int nb = std::min((nq + MT_WNT / 64 - 1) / (MT_WNT / 64), 512);
-                    const size_t lds = (MT_WNT / 64) * 64 * sizeof(int2) + (staged ? (size_t)n * 48 : 0);
+                    const size_t lds = (MT_WNT / 64) * 64 * sizeof(int2) + (staged ? (size_t)n * 56 : 0);
                     if (staged)
                         hipLaunchKernelGGL(k_sbp_local_wave<true>, dim3(nb), dim3(MT_WNT), lds, s, fr,
                                            (const orbfe_map_point*)q, nq, th, a0, thFar, nnratio, b0, fcur, assign,
