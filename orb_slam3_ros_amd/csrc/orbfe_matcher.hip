@@ -513,6 +513,187 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wave(FrameDev fr, const or
     }
 }
 
+// Several queries per wave: MT_QPW groups of 16 lanes (one DPP row each), each group running the
+// wave kernel's enumeration and (dist, enumeration index) minimum for its own query, so a wave keeps
+// MT_QPW query chains in flight instead of one (the wave kernel's time is its per-query chain).
+#ifndef MT_QPW
+#define MT_QPW 4
+#endif
+__device__ __forceinline__ int mt_row_incl_scan(int v) {   // inclusive scan within each row of 16 lanes
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    return v;
+}
+__device__ __forceinline__ unsigned long long mt_row_min64(unsigned long long v) {   // every lane: its row's min
+    v = mt_min64_dpp_step<0xB1>(v);
+    v = mt_min64_dpp_step<0x4E>(v);
+    v = mt_min64_dpp_step<0x141>(v);
+    return mt_min64_dpp_step<0x140>(v);
+}
+__device__ __forceinline__ int mt_rows_max(int v) {   // max over the four rows of a row-uniform value
+    int m = __builtin_amdgcn_readlane(v, 0);
+    m = max(m, __builtin_amdgcn_readlane(v, 16));
+    m = max(m, __builtin_amdgcn_readlane(v, 32));
+    return max(m, __builtin_amdgcn_readlane(v, 48));
+}
+template <bool STAGED>
+__global__ __launch_bounds__(MT_WNT) void k_sbp_local_wq(FrameDev fr, const orbfe_map_point* mps, int nq, float th,
+                                                      int bFar, float thFar, float nnratio, const int* blocked0,
+                                                      const int* first, int* assign, int* changed, PassIO io) {
+    static_assert(MT_QPW == 4, "one query per DPP row of 16 lanes");
+    constexpr int GL = 16;
+    extern __shared__ __attribute__((aligned(16))) uint8_t mt_sm[];
+    if (pass_gated(io)) return;
+    pass_fill(io);
+    int2* s_cell = (int2*)mt_sm;                                          // [16 waves][4 groups][16]
+    float4* s_key = (float4*)(mt_sm + (MT_WNT / 64) * 64 * sizeof(int2));  // as k_sbp_local_wave
+    uint4* s_desc = (uint4*)(s_key + (STAGED ? fr.n : 0));
+    int2* s_gate = (int2*)(s_desc + (STAGED ? 2 * fr.n : 0));
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, grp = lane >> 4, sl = lane & 15;
+    if (STAGED) {
+        for (int i = tid; i < fr.n; i += MT_WNT) {
+            const OrbKeyPoint kp = fr.keys[i];
+            s_key[i] = make_float4(kp.x, kp.y, __int_as_float(kp.octave), fr.uright ? fr.uright[i] : -1.f);
+            const uint4* d = (const uint4*)(fr.desc + 8 * i);
+            s_desc[2 * i] = d[0];
+            s_desc[2 * i + 1] = d[1];
+            s_gate[i] = make_int2(blocked0[i], first[i]);
+        }
+        SYNC();
+    }
+    int2* my_cells = s_cell + 64 * wave + GL * grp;
+    constexpr int WPB = MT_WNT / 64;
+    for (int q0 = (blockIdx.x * WPB + wave) * MT_QPW; q0 < nq; q0 += gridDim.x * WPB * MT_QPW) {
+        const int q = q0 + grp;
+        const bool qv = q < nq;
+        int prev = -1, obs = 0, lvl = 0, ncell = 0, cx0 = 0, cy0 = 0, cy1 = -1;
+        float R = 0.f, x = 0.f, y = 0.f, xr = 0.f;
+        uint32_t qd[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        if (qv) {
+            const orbfe_map_point& mp = mps[q];
+            prev = assign[q];
+            obs = mp.observations;
+            if ((mp.flags & ORBFE_MP_IN_VIEW) && !(bFar && mp.depth > thFar) && !(mp.flags & ORBFE_MP_BAD) &&
+                mp.scale_level >= 0 && mp.scale_level < fr.nlevels) {
+                lvl = mp.scale_level;
+                float r = mp.view_cos > 0.998 ? 2.5f : 4.0f;
+                if (th != 1.0f) r *= th;
+                R = r * fr.scale[lvl];
+                x = mp.proj_x;
+                y = mp.proj_y;
+                xr = mp.proj_xr;
+                memcpy(qd, mp.desc, 32);
+                cx0 = max(0, (int)floorf((x - fr.minx - R) * fr.invw));
+                const int cx1 = min(ORBFE_GRID_COLS - 1, (int)ceilf((x - fr.minx + R) * fr.invw));
+                cy0 = max(0, (int)floorf((y - fr.miny - R) * fr.invh));
+                cy1 = min(ORBFE_GRID_ROWS - 1, (int)ceilf((y - fr.miny + R) * fr.invh));
+                if (cx0 < ORBFE_GRID_COLS && cx1 >= 0 && cy0 < ORBFE_GRID_ROWS && cy1 >= 0 && cx0 <= cx1 && cy0 <= cy1)
+                    ncell = cx1 - cx0 + 1;
+            }
+        }
+        const int minLevel = lvl - 1, maxLevel = lvl;
+        const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+        const int* pcs = fr.pcstart + lvl * fr.gstride_c;
+        const int* pci = fr.pcidx + lvl * fr.gstride_i;
+        unsigned long long b1 = ~0ull, b2 = ~0ull;
+        int b1idx = -1;
+        unsigned nwin = 0, npair = 0;
+        int obase = 0;
+        const int ncmax = mt_rows_max(ncell);
+        // one contiguous CSR run per grid column of the window, 16 columns per round
+        for (int cb = 0; cb < ncmax; cb += GL) {
+            const int c = cb + sl;
+            int st = 0, cnt = 0;
+            if (c < ncell) {
+                const int ix = cx0 + c;
+                st = pcs[ix * ORBFE_GRID_ROWS + cy0];
+                cnt = pcs[ix * ORBFE_GRID_ROWS + cy1 + 1] - st;
+            }
+            const int incl = mt_row_incl_scan(cnt);
+            const int tot = __shfl(incl, lane | 15, 64);
+            my_cells[sl] = make_int2(st, incl - cnt);
+            WAVE_SYNC();
+            const int totmax = mt_rows_max(tot);
+            for (int j0 = 0; j0 < totmax; j0 += GL) {
+                const int j = j0 + sl;
+                if (j < tot) {
+                    nwin++;
+                    int lo = 0, hi = GL;   // last cell with prefix <= j
+                    while (hi - lo > 1) {
+                        const int mid = (lo + hi) >> 1;
+                        if (my_cells[mid].y <= j) lo = mid; else hi = mid;
+                    }
+                    const int2 ce = my_cells[lo];
+                    const int idx = pci[ce.x + (j - ce.y)];
+                    float kx, ky, ur;
+                    int oct;
+                    if (STAGED) {
+                        const float4 k4 = s_key[idx];
+                        kx = k4.x; ky = k4.y; oct = __float_as_int(k4.z); ur = k4.w;
+                    } else {
+                        const OrbKeyPoint kp = fr.keys[idx];
+                        kx = kp.x; ky = kp.y; oct = kp.octave; ur = fr.uright ? fr.uright[idx] : -1.f;
+                    }
+                    bool ok = true;
+                    if (bCheckLevels) {
+                        if (oct < minLevel) ok = false;
+                        if (maxLevel >= 0 && oct > maxLevel) ok = false;
+                    }
+                    ok = ok && fabsf(kx - x) < R && fabsf(ky - y) < R;
+                    if (STAGED) {
+                        const int2 gt = s_gate[idx];
+                        ok = ok && !(gt.x || gt.y < q);
+                    } else {
+                        ok = ok && !(blocked0[idx] || first[idx] < q);
+                    }
+                    if (ok && ur > 0) ok = !(fabsf(xr - ur) > R);
+                    if (ok) {
+                        npair++;
+                        uint4 d0, d1;
+                        if (STAGED) { d0 = s_desc[2 * idx]; d1 = s_desc[2 * idx + 1]; }
+                        else { d0 = ((const uint4*)(fr.desc + 8 * idx))[0]; d1 = ((const uint4*)(fr.desc + 8 * idx))[1]; }
+                        const int dist = __popc(qd[0] ^ d0.x) + __popc(qd[1] ^ d0.y) + __popc(qd[2] ^ d0.z) +
+                                         __popc(qd[3] ^ d0.w) + __popc(qd[4] ^ d1.x) + __popc(qd[5] ^ d1.y) +
+                                         __popc(qd[6] ^ d1.z) + __popc(qd[7] ^ d1.w);
+                        if (dist < 256) {
+                            const unsigned long long k = ((unsigned long long)dist << 32) |
+                                                         ((unsigned long long)(obase + j) << 4) | (unsigned)oct;
+                            if (k < b1) { b2 = b1; b1 = k; b1idx = idx; }
+                            else if (k < b2) b2 = k;
+                        }
+                    }
+                }
+            }
+            obase += tot;
+            WAVE_SYNC();
+        }
+        pass_stats(io, nwin, npair);
+        const unsigned long long m1 = mt_row_min64(b1);
+        const unsigned long long win = (__ballot(b1 == m1 && m1 != ~0ull) >> (GL * grp)) & 0xFFFFull;
+        const unsigned long long m2 = mt_row_min64(b1 == m1 ? b2 : b1);
+        const int wl = win ? GL * grp + __ffsll((long long)win) - 1 : lane;
+        const int bestIdx = __shfl(b1idx, wl, 64);   // every lane takes part
+        int result = -1;
+        if (m1 != ~0ull) {
+            const int bestDist = (int)(m1 >> 32), bestLevel = (int)(m1 & 15);
+            const int bestDist2 = m2 != ~0ull ? (int)(m2 >> 32) : 256;
+            const int bestLevel2 = m2 != ~0ull ? (int)(m2 & 15) : -1;
+            if (bestDist <= MT_TH_HIGH) {
+                if (!(bestLevel == bestLevel2 && bestDist > nnratio * bestDist2)) result = bestIdx;
+            }
+        }
+        if (sl == 0 && qv) {
+            pass_publish(io, q, result, obs);
+            if (result != prev) {
+                assign[q] = result;
+                atomicAdd(changed, 1);
+            }
+        }
+    }
+}
+
 // ---- SearchByProjection(CurrentFrame, LastFrame, ...) (ORBmatcher.cc:1676-1887) and
 //      SearchByProjection(CurrentFrame, pKF, ...) (:1889-2010): single best, then rotation filter ----
 __global__ __launch_bounds__(MT_NT) void k_sbp_proj(FrameDev fr, const orbfe_proj_point* pts, int nq, float th,
@@ -1685,7 +1866,19 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
                 PassIO io{pass ? changed + pass - 1 : nullptr, fb[(pass + 1) % 3], fb[(pass + 2) % 3], n,
                           mode == 2 ? 0 : 1, stats};
                 const int* fcur = fb[pass % 3];
-                if (mode == 0 && th >= MT_WAVE_TH) {
+                if (mode == 0 && th >= MT_WAVE_TH && MT_QPW > 1) {
+                    const int qpb = (MT_WNT / 64) * MT_QPW;   // queries per block and round
+                    const int nb = std::min((nq + qpb - 1) / qpb, 512);
+                    const size_t lds = (MT_WNT / 64) * 64 * sizeof(int2) + (staged ? (size_t)n * 56 : 0);
+                    if (staged)
+                        hipLaunchKernelGGL(k_sbp_local_wq<true>, dim3(nb), dim3(MT_WNT), lds, s, fr,
+                                           (const orbfe_map_point*)q, nq, th, a0, thFar, nnratio, b0, fcur, assign,
+                                           changed + pass, io);
+                    else
+                        hipLaunchKernelGGL(k_sbp_local_wq<false>, dim3(nb), dim3(MT_WNT), lds, s, fr,
+                                           (const orbfe_map_point*)q, nq, th, a0, thFar, nnratio, b0, fcur, assign,
+                                           changed + pass, io);
+                } else if (mode == 0 && th >= MT_WAVE_TH) {
                     const int nb = std::min((nq + MT_WNT / 64 - 1) / (MT_WNT / 64), 512);
                     const size_t lds = (MT_WNT / 64) * 64 * sizeof(int2) + (staged ? (size_t)n * 56 : 0);
                     if (staged)
