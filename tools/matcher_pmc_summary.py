@@ -19,7 +19,8 @@ for th in (1, 3, 5, 15):
             seen = set()
             for r in csv.DictReader(open(f)):
                 cnt[r["Counter_Name"]] += float(r["Counter_Value"])
-                names.add(r["Kernel_Name"].split("(")[0].split("<")[0])
+                k = r["Kernel_Name"].split("(")[0].split("<")[0]
+                names.add(k[5:] if k.startswith("void ") else k)
         if i == 1:
             for f in glob.glob(os.path.join(root, f"mp_th{th}_{i}", "**", "*kernel_trace.csv"), recursive=True):
                 for r in csv.DictReader(open(f)):
