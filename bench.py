@@ -405,8 +405,10 @@ def matcher_config5(steps):
         lib.orbfe_matcher_set_stats(0)
         wst = (ctypes.c_longlong * 3)()
         lib.orbfe_matcher_last_stats(wst)
-        kname = "k_sbp_local_wave" if th >= 6 else "k_sbp_local"
         mp = (matcher_pmc or {}).get(f"th{th}", {})
+        # the pass kernel: the PMC pass's name when it covers this th, else by the library's switch
+        # (th >= 6: the wide-window kernel, four queries per wave)
+        kname = mp.get("kernel") or ("k_sbp_local_wq" if th >= 6 else "k_sbp_local")
         out[f"th{th}"] = {"kernel": kname, "window_candidates": int(wst[0]), "pairs": int(wst[1]),
                           "passes": int(wst[2]), "pairs_per_s": round(wst[1] / (dms * 1e-3), 1),
                           "window_candidates_per_s": round(wst[0] / (dms * 1e-3), 1),
