@@ -74,11 +74,7 @@ int orbfe_extractor_capacity(orbfe_extractor* h, int width, int height);
  * Host buffers: img is width x height u8 with row stride `stride` bytes. The mask is ignored, as in
  * the reference. lap0/lap1 = vLappingArea[0..1]. On success returns monoIndex (>= 0) and writes
  * *n keypoints / descriptors; returns ORBFE_E_EMPTY for an empty image.
- * Per call: one pinned upload, the handle's launches, one result copy, one synchronisation. From the
- * second consecutive call with one configuration (size, lap0/lap1, which outputs are wanted) the
- * upload, launches and result copy are a captured HIP graph replayed as one launch; any change of
- * configuration or buffers (a batch call, set_opencv_model, a new size) falls back to the plain path
- * and recaptures. Environment ORBFE_GRAPH=0 (read at handle creation) keeps the plain path. */
+ * Per call: one pinned upload, the handle's launches, one result copy, one synchronisation. */
 int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int width, int height, int stride, int lap0, int lap1,
                   orbfe_keypoint* kps, uint8_t* desc, int cap, int* n);
 

@@ -113,14 +113,6 @@ struct orbfe_extractor {
     // [kp_cap]} coming back in one round trip (DMA from / to pinned memory, no runtime bounce)
     uint8_t* h_pin = nullptr;
     size_t pin_bytes = 0;
-    // host-API call graph: orbfe_extract's upload, launches and result copies captured once per
-    // configuration (key: width, height, lap0, lap1, keypoints / descriptors wanted) and replayed as
-    // one graph launch; dropped whenever the buffers it names go away (graph_gen)
-    bool use_graph = true;         // ORBFE_GRAPH=0 disables
-    hipGraphExec_t x_graph = nullptr;
-    int x_key[6] = {};
-    int x_calls = 0;               // consecutive plain calls with the current key
-    unsigned graph_gen = 0, x_gen = 0;
     // host-API stereo results in one allocation {nmatch (16 B) | uR [stereo_kp] | depth [stereo_kp]}
     uint8_t* d_st = nullptr;
     float* d_uright = nullptr;
@@ -156,15 +148,7 @@ struct orbfe_extractor {
     unsigned long long* d_oct_ts = nullptr;   // -DORBFE_OCT_STAMPS builds: per-phase s_memtime of the octree (image 0)
 };
 
-static void drop_graph(orbfe_extractor* h) {
-    if (h->x_graph) (void)hipGraphExecDestroy(h->x_graph);
-    h->x_graph = nullptr;
-    h->x_calls = 0;
-}
-
 static void free_buffers(orbfe_extractor* h) {
-    drop_graph(h);
-    h->graph_gen++;
     void** bufs[] = {(void**)&h->d_tab, (void**)&h->d_pyr, (void**)&h->d_cellkeys,
                      (void**)&h->d_cellcnt, (void**)&h->d_lkeys, (void**)&h->d_nodeof, (void**)&h->d_outkeys,
                      (void**)&h->d_lvinfo, (void**)&h->d_ranks, (void**)&h->d_out, (void**)&h->d_ptrs};
@@ -647,7 +631,6 @@ int orbfe_extractor_create(int nfeatures, float scaleFactor, int nlevels, int in
     int prio_lo = 0, prio_hi = 0;   // the side stream yields to the batch stream's critical path
     if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&h->side_stream, hipStreamNonBlocking, prio_lo);
-    if (const char* v = getenv("ORBFE_GRAPH")) h->use_graph = atoi(v) != 0;
     for (int i = 0; e == hipSuccess && i <= ORBFE_MAX_LEVELS; i++)
         e = hipEventCreateWithFlags(&h->ev_fork[i], hipEventDisableTiming);
     for (int i = 0; e == hipSuccess && i <= ORBFE_NUM_STAGES; i++) e = hipEventCreate(&h->ev[i]);
@@ -664,7 +647,7 @@ void orbfe_extractor_destroy(orbfe_extractor* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     (void)hipDeviceSynchronize();
-    free_buffers(h);   // (and the call graph)
+    free_buffers(h);
     if (h->d_stage) (void)hipFree(h->d_stage);
     if (h->h_pin) (void)hipHostFree(h->h_pin);
     if (h->d_st) (void)hipFree(h->d_st);
@@ -805,7 +788,6 @@ int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int width, int height,
     hipStream_t s = h->own_stream;
     const size_t bytes = (size_t)width * height;
     if (h->stage_bytes < bytes) {
-        drop_graph(h);
         if (h->d_stage) HIPCHK(hipFree(h->d_stage));
         HIPCHK(hipMalloc(&h->d_stage, bytes));
         h->stage_bytes = bytes;
@@ -819,7 +801,6 @@ int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int width, int height,
     const size_t kpb = (size_t)h->g.kp_cap * sizeof(OrbKeyPoint), db = (size_t)h->g.kp_cap * 32;
     const size_t pin_need = std::max(bytes, o_end);
     if (h->pin_bytes < pin_need) {
-        drop_graph(h);
         if (h->h_pin) HIPCHK(hipHostFree(h->h_pin));
         h->h_pin = nullptr;
         h->pin_bytes = 0;
@@ -855,42 +836,8 @@ int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int width, int height,
         if (tm) HIPCHK(hipEventRecord(h->call_ev[3], s));
         return ORBFE_OK;
     };
-    // graph replay needs the state the captured launches assume: this configuration's key, the same
-    // buffers (graph_gen), and the device batch description still naming the staging image (a batch
-    // call in between re-uploads it through the plain path)
-    const int key[6] = {width, height, lap0, lap1, kps != nullptr, desc != nullptr};
-    const bool key_same = memcmp(key, h->x_key, sizeof(key)) == 0;
-    const bool desc_same = h->last_nimg == 1 && h->last_ptrs.size() == 1 && h->last_ptrs[0] == h->d_stage &&
-                           h->last_laps.size() == 2 && h->last_laps[0] == lap0 && h->last_laps[1] == lap1;
-    if (h->x_graph && !(key_same && h->x_gen == h->graph_gen && desc_same)) drop_graph(h);
-    if (!h->use_graph || tm) {
-        rc = enqueue();
-        if (rc) return rc;
-    } else if (h->x_graph) {
-        HIPCHK(hipGraphLaunch(h->x_graph, s));
-    } else if (key_same && h->x_calls >= 1 && desc_same) {
-        // second plain call with this key: its launches are captured and replayed from now on
-        // (run_batch sees the same batch description, so nothing inside synchronises)
-        hipGraph_t gr = nullptr;
-        HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-        rc = enqueue();
-        const hipError_t ce = hipStreamEndCapture(s, &gr);
-        if (rc) {
-            if (gr) (void)hipGraphDestroy(gr);
-            return rc;
-        }
-        HIPCHK(ce);
-        hipError_t ie = hipGraphInstantiateWithFlags(&h->x_graph, gr, 0);
-        (void)hipGraphDestroy(gr);
-        HIPCHK(ie);
-        h->x_gen = h->graph_gen;
-        HIPCHK(hipGraphLaunch(h->x_graph, s));
-    } else {
-        rc = enqueue();
-        if (rc) return rc;
-        memcpy(h->x_key, key, sizeof(key));
-        h->x_calls = key_same ? h->x_calls + 1 : 1;
-    }
+    rc = enqueue();
+    if (rc) return rc;
     HIPCHK(hipStreamSynchronize(s));
     int cnt[2];
     memcpy(cnt, hp, 8);
@@ -1006,7 +953,6 @@ int orbfe_stereo_match(orbfe_extractor* left, orbfe_extractor* right, float bf, 
     const size_t kc = (size_t)left->stereo_kp;
     const size_t need = 32 + 8 * kc;
     if (left->pin_bytes < need) {
-        drop_graph(left);   // its result copy names the old buffer
         if (left->h_pin) HIPCHK(hipHostFree(left->h_pin));
         left->h_pin = nullptr;
         left->pin_bytes = 0;

@@ -188,12 +188,12 @@ def test_stereo_matches_tall_image(gpu, oracle_lib):
     assert (ur >= 0).sum() > 0.3 * len(kl)
 
 
-def test_host_call_graph_replay(gpu, oracle_lib):
-    """orbfe_extract captures its call (upload, launches, result copies) as a HIP graph on the second
-    call with one configuration and replays it from then on. Every call stays bit-exact across image
-    changes, a lapping-area change (a new capture), a batch call on the same handle in between (the
-    plain path re-uploads the batch description) and an OpenCV-model round trip (buffers rebuilt);
-    the pyramid getter reads the replayed call's levels."""
+def test_host_call_sequence(gpu, oracle_lib):
+    """A sequence of orbfe_extract calls on one handle, as Tracking makes them (one-image output block,
+    single result copy): every call stays bit-exact across image changes, a lapping-area change, a
+    batch call on the same handle in between (the next host call re-uploads the batch description)
+    and an OpenCV-model round trip (buffers rebuilt); the pyramid getter reads the last call's
+    levels."""
     import ctypes
 
     import torch
@@ -211,7 +211,7 @@ def test_host_call_graph_replay(gpu, oracle_lib):
     seeds = iter(range(300, 400))
     for lap in [(0, 0)] * 4 + [(0, 1000)] * 3:
         check(synth_image(next(seeds), 752, 480), lap)
-    # the last replayed call's pyramid, as Frame reads mvImagePyramid
+    # the last call's pyramid, as Frame reads mvImagePyramid
     img = synth_image(next(seeds), 752, 480)
     check(img, (0, 1000))
     for l in (0, 3, 7):
@@ -223,7 +223,7 @@ def test_host_call_graph_replay(gpu, oracle_lib):
     torch.cuda.synchronize()
     for _ in range(3):
         check(synth_image(next(seeds), 752, 480), (0, 1000))
-    # buffers rebuilt by a model change (the replayed graph names the old ones) and back
+    # buffers rebuilt by a model change and back
     for lanes in (8, 16):
         ext.set_opencv_model(lanes, 0)
         ora._l.oro_set_model(ora.h, lanes, 0)

@@ -7,13 +7,11 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/dropin_trace
 python3 tools/dropin_job.py gpurun_out/dropin_trace/job.bin
-# latency, twice each: the in-tree library with the host-call graph (default) and without
-# (ORBFE_GRAPH=0), then every variants_lat/<name>/liborbfe.so (LD_LIBRARY_PATH beats the RUNPATH)
+# latency, twice each: the in-tree library, then every variants_lat/<name>/liborbfe.so
+# (LD_LIBRARY_PATH beats the RUNPATH)
 for rep in 1 2; do
-  for gflag in 1 0; do
-    echo -n "tree graph=$gflag "
-    ORBFE_GRAPH=$gflag timeout -k 10 60 tests/native/capi_frontend --latency 200 gpurun_out/dropin_trace/job.bin || exit 1
-  done
+  echo -n "tree "
+  timeout -k 10 60 tests/native/capi_frontend --latency 200 gpurun_out/dropin_trace/job.bin || exit 1
   for d in variants_lat/*/; do
     [ -f $d/liborbfe.so ] || continue
     echo -n "$(basename $d) "
