@@ -81,9 +81,6 @@ struct orbfe_extractor {
     // split path: FAST of level 0 runs on side_stream while the resize chain runs on the batch
     // stream (fork / join events)
     hipStream_t side_stream = nullptr;
-    // small batches: level 0's DistributeOctTree (the longest serial chain of a single image) starts
-    // on this stream as soon as level 0's FAST is done, beside the pyramid chain and the other levels
-    hipStream_t oct_stream = nullptr;
     hipEvent_t ev_fork[ORBFE_MAX_LEVELS + 1] = {};
     // geometry of the current allocation
     int W = 0, H = 0, cap_b = 0;
@@ -393,7 +390,8 @@ constexpr int kSmallStereoLk = 64;
 #ifndef SMALL_OCT_NT
 #define SMALL_OCT_NT 1024
 #endif
-constexpr int kSmallOctNt = SMALL_OCT_NT;   // k_octree threads per (image, level) block (OCT_NT = 256)
+constexpr int kSmallOctNt = SMALL_OCT_NT;
+   // k_octree threads per (image, level) block (OCT_NT = 256)
    // k_stereo left keypoints per block (ST_LK = 512)
 
 static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs, int pitch, const int* laps,
@@ -467,6 +465,10 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
 #ifdef FAST_NO_OVERLAP
         s2 = s;   // profiling builds: every launch in stream order (isolated kernel times)
 #endif
+        // a small batch runs every launch in stream order: at one image the device has room for all
+        // of them anyway, and a cross-stream event wait costs more than the overlap it buys (a stereo
+        // frame through the host API: 0.43 -> 0.33 ms, profiles/r04_kernel_ab.txt item 13)
+        if (small) s2 = s;
         constexpr int kFastMid = 4;   // FAST of levels [1, kFastMid) runs on the side stream once resize has built them
         // the pyramid chain: a small batch takes short row chunks per wave (more, shorter waves: the
         // chain of 7 launches is the frame's critical path at batch 1)
@@ -477,20 +479,12 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
         // them (beside the chain's short, latency-bound top-level launches); batch stream: the
         // chain, then FAST of levels [lmid, nlevels)
         const int lmid = std::min(std::max(kFastMid, 1), g.nlevels);
-        HIPCHK(hipEventRecord(h->ev_fork[0], s));
-        HIPCHK(hipStreamWaitEvent(s2, h->ev_fork[0], 0));
-        fast_range(s2, 0, 1);
-        if (small) {   // level 0's octree right behind its FAST, on its own stream
-            // created on first use: a process's streams share a few hardware queues, and an extra
-            // stream must not change how the large-batch path's two streams map onto them
-            if (!h->oct_stream) HIPCHK(hipStreamCreateWithFlags(&h->oct_stream, hipStreamNonBlocking));
-            HIPCHK(hipEventRecord(h->ev_fork[3], s2));
-            HIPCHK(hipStreamWaitEvent(h->oct_stream, h->ev_fork[3], 0));
-            hipLaunchKernelGGL(k_octree<kSmallOctNt>, dim3(B, 1), dim3(kSmallOctNt), h->oct_lds, h->oct_stream, g, h->d_cellkeys,
-                               h->d_cellcnt, h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, d_laps,
-                               h->d_oct_ts, 0);
-            HIPCHK(hipEventRecord(h->ev_fork[4], h->oct_stream));
+        const bool fork = s2 != s;   // (profiling / one-stream builds: no fork or join)
+        if (fork) {
+            HIPCHK(hipEventRecord(h->ev_fork[0], s));
+            HIPCHK(hipStreamWaitEvent(s2, h->ev_fork[0], 0));
         }
+        fast_range(s2, 0, 1);
         // k_resize_s reads dwords: level 0 must be 4-byte aligned (else k_resize builds level 1)
         bool al0 = (pitch & 3) == 0;
         for (int i = 0; al0 && i < B; i++) al0 = (((uintptr_t)host_ptrs[i]) & 3) == 0;
@@ -509,24 +503,24 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
                 hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, s, P, pitch, h->d_pyr, g.pyr_bytes, h->d_tab, g, l);
             }
             if (l + 1 == lmid) {
-                HIPCHK(hipEventRecord(h->ev_fork[2], s));
-                HIPCHK(hipStreamWaitEvent(s2, h->ev_fork[2], 0));
+                if (fork) {
+                    HIPCHK(hipEventRecord(h->ev_fork[2], s));
+                    HIPCHK(hipStreamWaitEvent(s2, h->ev_fork[2], 0));
+                }
                 fast_range(s2, 1, lmid);
             }
         }
-        HIPCHK(hipEventRecord(h->ev_fork[1], s2));
+        if (fork) HIPCHK(hipEventRecord(h->ev_fork[1], s2));
         if (lmid < g.nlevels) fast_range(s, lmid, g.nlevels);
-        HIPCHK(hipStreamWaitEvent(s, h->ev_fork[1], 0));
+        if (fork) HIPCHK(hipStreamWaitEvent(s, h->ev_fork[1], 0));
     }
     BlurKernel bk;   // the Gaussian blur is fused into k_describe
     memcpy(bk.k, h->blur_variant == 1 ? kBlurRound : kBlurED, sizeof(bk.k));
     if (tm) HIPCHK(hipEventRecord(ev[1], s));
     if (small) {
-        if (g.nlevels > 1)
-            hipLaunchKernelGGL(k_octree<kSmallOctNt>, dim3(B, g.nlevels - 1), dim3(kSmallOctNt), h->oct_lds, s, g, h->d_cellkeys,
-                               h->d_cellcnt, h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, d_laps,
-                               h->d_oct_ts, 1);
-        HIPCHK(hipStreamWaitEvent(s, h->ev_fork[4], 0));
+        hipLaunchKernelGGL(k_octree<kSmallOctNt>, dim3(B, g.nlevels), dim3(kSmallOctNt), h->oct_lds, s, g,
+                           h->d_cellkeys, h->d_cellcnt, h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo,
+                           h->d_ranks, d_laps, h->d_oct_ts, 0);
     } else {
         hipLaunchKernelGGL(k_octree<OCT_NT>, dim3(B, g.nlevels), dim3(OCT_NT), h->oct_lds, s, g, h->d_cellkeys, h->d_cellcnt,
                            h->d_lkeys, h->d_nodeof, h->d_outkeys, h->d_lvinfo, h->d_ranks, d_laps, h->d_oct_ts, 0);
@@ -657,7 +651,6 @@ void orbfe_extractor_destroy(orbfe_extractor* h) {
     for (int i = 0; i <= ORBFE_MAX_LEVELS; i++)
         if (h->ev_fork[i]) (void)hipEventDestroy(h->ev_fork[i]);
     if (h->side_stream) (void)hipStreamDestroy(h->side_stream);
-    if (h->oct_stream) (void)hipStreamDestroy(h->oct_stream);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
 }
