@@ -500,8 +500,8 @@ def dropin_leg(frames, W=752, H=480, nf=1000, bf=0.110078 * 458.654, fx=458.654)
     through the host C-ABI exactly as Tracking builds a stereo Frame (Frame.cc:122-141): two
     ORBextractor::operator() calls on two per-frame std::threads, then ComputeStereoMatches, host
     images in and host results out. Timed by the compiled C++ consumer (tests/native/capi_frontend.cpp
-    --latency, linked against liborbfe.so only): frame_ms as an application runs it (no event timing,
-    so the library replays its host-call graphs), then a second run with the library's HIP-event split
+    --latency, linked against liborbfe.so only): frame_ms as an application runs it (no event timing),
+    then a second run with the library's HIP-event split
     of each call (upload / kernels / result copies; host = wall - the device-side critical path) and
     its own wall time, frame_ms_timed."""
     import struct
@@ -522,8 +522,8 @@ def dropin_leg(frames, W=752, H=480, nf=1000, bf=0.110078 * 458.654, fx=458.654)
         return {"error": (r.stderr or r.stdout)[-400:]}
     out = json.loads(r.stdout.strip().splitlines()[-1])
     out["path"] = ("host C-ABI per frame: orbfe_extract L || R on two std::threads (ExtractORB, Frame.cc:122-125), "
-                   "then orbfe_stereo_match (Frame.cc:141); medians over the frames; split_ms from the timed "
-                   "run (events on, graph replay off)")
+                   "then orbfe_stereo_match (Frame.cc:141); medians over the frames; split_ms from a second, "
+                   "timed run (per-call HIP events on)")
     return out
 
 

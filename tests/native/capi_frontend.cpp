@@ -198,9 +198,9 @@ int latency(int frames, const char* job) {
         throw std::runtime_error("short job images");
     fclose(f);
     ORBextractor el(nf, 1.2f, 8, 20, 7), er(nf, 1.2f, 8, 20, 7);
-    // two runs of `frames` frames: first as an application runs (no event timing: the library replays
-    // its host-call graphs), giving frame_ms; then with the per-call HIP-event timing on (plain path,
-    // events around the upload / kernels / copies), giving the split and frame_ms_timed
+    // two runs of `frames` frames: first as an application runs (no event timing), giving frame_ms;
+    // then with the per-call HIP-event timing on (events around the upload / kernels / copies), giving
+    // the split and frame_ms_timed
     std::vector<double> wall_plain, wall, ext, st, up, ker, cp, sker, scp, host;
     int nkp = 0, nst = 0;
     const int warm = 5;
