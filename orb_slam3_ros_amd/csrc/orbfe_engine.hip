@@ -484,7 +484,9 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
             HIPCHK(hipEventRecord(h->ev_fork[0], s));
             HIPCHK(hipStreamWaitEvent(s2, h->ev_fork[0], 0));
         }
-        fast_range(s2, 0, 1);
+        // a small batch: the chain first, then FAST of every level in one launch (in one stream, a
+        // FAST launch ahead of or inside the chain would only lengthen it)
+        if (!small) fast_range(s2, 0, 1);
         // k_resize_s reads dwords: level 0 must be 4-byte aligned (else k_resize builds level 1)
         bool al0 = (pitch & 3) == 0;
         for (int i = 0; al0 && i < B; i++) al0 = (((uintptr_t)host_ptrs[i]) & 3) == 0;
@@ -502,7 +504,7 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
                 dim3 grid((L.w + L.rz_cols - 1) / L.rz_cols, (tiles_y + RZ_TPB - 1) / RZ_TPB, B);
                 hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, s, P, pitch, h->d_pyr, g.pyr_bytes, h->d_tab, g, l);
             }
-            if (l + 1 == lmid) {
+            if (l + 1 == lmid && !small) {
                 if (fork) {
                     HIPCHK(hipEventRecord(h->ev_fork[2], s));
                     HIPCHK(hipStreamWaitEvent(s2, h->ev_fork[2], 0));
@@ -510,9 +512,13 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
                 fast_range(s2, 1, lmid);
             }
         }
-        if (fork) HIPCHK(hipEventRecord(h->ev_fork[1], s2));
-        if (lmid < g.nlevels) fast_range(s, lmid, g.nlevels);
-        if (fork) HIPCHK(hipStreamWaitEvent(s, h->ev_fork[1], 0));
+        if (small) {
+            fast_range(s, 0, g.nlevels);
+        } else {
+            if (fork) HIPCHK(hipEventRecord(h->ev_fork[1], s2));
+            if (lmid < g.nlevels) fast_range(s, lmid, g.nlevels);
+            if (fork) HIPCHK(hipStreamWaitEvent(s, h->ev_fork[1], 0));
+        }
     }
     BlurKernel bk;   // the Gaussian blur is fused into k_describe
     memcpy(bk.k, h->blur_variant == 1 ? kBlurRound : kBlurED, sizeof(bk.k));
