@@ -385,8 +385,14 @@ static int ensure(orbfe_extractor* h, int W, int H, int B) {
 // kSmallBatch images (or stereo frames) the kernels trade per-wave work for more, shorter waves,
 // since one image cannot fill the GPU and the frame's latency is its longest chain of dependent steps.
 constexpr int kSmallBatch = 16;
-constexpr int kSmallRsRows = 8;       // k_resize_s output rows per wave (48 for large batches)
-constexpr int kSmallStereoLk = 64;
+#ifndef SMALL_RS_ROWS
+#define SMALL_RS_ROWS 4
+#endif
+constexpr int kSmallRsRows = SMALL_RS_ROWS;       // k_resize_s output rows per wave (48 for large batches)
+#ifndef SMALL_STEREO_LK
+#define SMALL_STEREO_LK 32
+#endif
+constexpr int kSmallStereoLk = SMALL_STEREO_LK;
 #ifndef SMALL_OCT_NT
 #define SMALL_OCT_NT 1024
 #endif
