@@ -215,9 +215,6 @@ static int build_geom(const orbfe_extractor* h, int W, int H, OrbGeom& g, std::v
             f.roi = round_up(rs * (L.h_cell + 6), 16);
             f.sc = round_up(rs * (L.h_cell + 2), 16);
             f.cor = round_up(std::max(2 * L.w_cell * L.h_cell, 8 * grp + 256), 16);
-#ifdef FAST_EXP_COR   // occupancy experiment only
-            f.cor = std::min(f.cor, FAST_EXP_COR);
-#endif
             f.wave_bytes = f.roi + f.sc + f.cor + FAST_ENT_BYTES;
             fl.roi = std::max(fl.roi, f.roi);
             fl.sc = std::max(fl.sc, f.sc);
@@ -385,20 +382,9 @@ static int ensure(orbfe_extractor* h, int W, int H, int B) {
 // kSmallBatch images (or stereo frames) the kernels trade per-wave work for more, shorter waves,
 // since one image cannot fill the GPU and the frame's latency is its longest chain of dependent steps.
 constexpr int kSmallBatch = 16;
-#ifndef SMALL_RS_ROWS
-#define SMALL_RS_ROWS 4
-#endif
-constexpr int kSmallRsRows = SMALL_RS_ROWS;       // k_resize_s output rows per wave (48 for large batches)
-#ifndef SMALL_STEREO_LK
-#define SMALL_STEREO_LK 32
-#endif
-constexpr int kSmallStereoLk = SMALL_STEREO_LK;
-#ifndef SMALL_OCT_NT
-#define SMALL_OCT_NT 1024
-#endif
-constexpr int kSmallOctNt = SMALL_OCT_NT;
-   // k_octree threads per (image, level) block (OCT_NT = 256)
-   // k_stereo left keypoints per block (ST_LK = 512)
+constexpr int kSmallRsRows = 4;       // k_resize_s output rows per wave (48 for large batches)
+constexpr int kSmallStereoLk = 32;    // k_stereo left keypoints per block (ST_LK = 512)
+constexpr int kSmallOctNt = 1024;     // k_octree threads per (image, level) block (OCT_NT = 256)
 
 static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs, int pitch, const int* laps,
                      hipStream_t s, bool use_ext) {

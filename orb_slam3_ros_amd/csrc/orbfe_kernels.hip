@@ -600,9 +600,7 @@ __device__ __forceinline__ int fast_M(const uint8_t* im, int stride, int x, int 
     return max((int)best.x, (int)best.y);
 }
 
-#ifndef FAST_PF
 #define FAST_PF 4
-#endif
 //             prefetched 16-byte chunks per lane (rows / rows-per-load: 2 at W = 35)
 struct FastCell {
     int l, local, ci, cj, r0, c0, rows, cols, pitch;
@@ -734,9 +732,7 @@ __device__ __forceinline__ void fast_stage_cell(const FastCell& cur, const orbfe
 struct FastLds {
     int roi, sc, cor, wave_bytes;   // bytes per wave: ROI image, score map, corner list (+ entries)
 };
-#ifndef FAST_ENT_BYTES
 #define FAST_ENT_BYTES 1024     // entry chunk: 64 groups x <= 8 entries x 2 B
-#endif
 
 // Detection of one staged cell (both attempts, NMS, emission). NDC = the LDS row stride in dwords
 // when known at compile time (0: runtime): every LDS offset of the ring / neighbour reads is then
@@ -776,11 +772,7 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
         // arithmetic (even bytes / odd bytes); candidates compacted row-major as (dy << 8 | dx).
         int ngrp = 0;
         // group records at the tail of the corner list: <= ng * dh of them
-#ifdef FAST_EXP_GRP   // occupancy experiment (invalid outputs for dense cells): a fixed record tail
-        uint32_t* s_grp = (uint32_t*)((uint8_t*)s_cor + fl.cor) - FAST_EXP_GRP;
-#else
         uint32_t* s_grp = (uint32_t*)((uint8_t*)s_cor + fl.cor) - ng * dh;
-#endif
         if (ng) {
             const int rpi = 64 / ng;
             const int ly = small_div(lane, ng), lg = lane - ly * ng;
@@ -971,11 +963,7 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
                 surv = sc > mx;
             }
             const unsigned long long m = __ballot(surv);
-#ifdef FAST_EXP_GRP
-            if (surv && nsurv + lanes_below(m) < L.cell_cap)
-#else
             if (surv)
-#endif
                 out[nsurv + lanes_below(m)] = (uint32_t)(xr0 + (p & 127)) | ((uint32_t)(yr0 + (p >> 7)) << 12) |
                                               ((uint32_t)sc << 24);
             nsurv += __popcll(m);
@@ -983,9 +971,6 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
         if (nsurv > 0) break;
         WAVE_SYNC();   // the fallback attempt clears the score map
     }   // attempt
-#ifdef FAST_EXP_GRP
-    nsurv = min(nsurv, L.cell_cap);
-#endif
     if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = stop ? 0 : nsurv;
     WAVE_SYNC();   // LDS is restaged for the next cell
 }
@@ -993,12 +978,7 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
 #define FAST_WPB 1   // waves per block: a block's LDS is held until its last wave retires, and the cells
                      // of one block finish at different times; single-wave blocks return each wave's LDS
                      // at once: 1.60 -> 1.45 ms per 1024 images against 4 (2: 1.51; r03_kernel_ab.txt item 24)
-#ifdef FAST_WPE
-#define FAST_ATTR __attribute__((amdgpu_waves_per_eu(FAST_WPE)))
-#else
-#define FAST_ATTR
-#endif
-__global__ __launch_bounds__(64 * FAST_WPB) FAST_ATTR void k_fast(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
+__global__ __launch_bounds__(64 * FAST_WPB) void k_fast(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                               int pyr_stride, OrbGeom g, FastLds fl, uint32_t* cellkeys,
                                               int* cellcnt, int c_lo, int c_hi, int cpw) {
     constexpr int ablate = ORBFE_ABLATE_FAST;
@@ -1903,21 +1883,14 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
 // the f16 pattern) ran the kernel alone 1.07 -> 1.04 ms but doubled its HBM reads (twice the images
 // resident per XCD overflow its L2: hit rate 0.84 -> 0.70) and left the full step unchanged
 // (r03_kernel_ab.txt item 19)
-#ifndef DP_KPW
 #define DP_KPW 4
-#endif
 // 6 waves per SIMD: 79 VGPRs, no spill since the pattern is held as f16 (at 5 waves without a spill
 // or 6 with one the kernel measured slower or equal: 1 slot / 4 slots at 5, 6, 7 waves, 2, 3 and 8
 // slots, tools/gpu_variants_trace.sh; DESIGN.md §7d, profiles/r03_kernel_ab.txt items 18-19)
-#ifndef DP_WPE
-#define DP_WPE 6
-#endif
-#define DP_ATTR __attribute__((amdgpu_waves_per_eu(DP_WPE)))
+#define DP_ATTR __attribute__((amdgpu_waves_per_eu(6)))
 // DP_WPB: waves per block: 2 / 4 / 8 measured 1.04 / 1.06 / 1.11 ms (r03_kernel_ab.txt item 23); 12
 // blocks of 12.7 KB per CU give the same 6 waves per SIMD with finer-grained refill
-#ifndef DP_WPB
 #define DP_WPB 2
-#endif
 template <int KPW>
 __global__ __launch_bounds__(64 * DP_WPB) DP_ATTR void k_describe(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                                   int pyr_stride, OrbGeom g, const uint32_t* __restrict__ outkeys,

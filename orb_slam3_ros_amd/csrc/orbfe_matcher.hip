@@ -307,28 +307,20 @@ __global__ __launch_bounds__(MT_NT) void k_sbp_local(FrameDev fr, const orbfe_ma
     }
 }
 
-// Wave-per-query form of k_sbp_local for wide search windows (th >= MT_WAVE_TH): the 64 lanes of
-// a wave enumerate the query's candidates in GetFeaturesInArea order (cells ix-outer / iy-inner,
-// flattened with a wave prefix sum) and keep the two smallest (dist, enumeration index) keys —
-// exactly the reference's sequential best / second-best (a later equal distance never displaces
-// an earlier one). Persistent blocks stage the frame's keypoints and descriptors in LDS.
-#ifndef MT_WAVE_TH
+// Wide search windows (th >= MT_WAVE_TH): four queries per wave, one per DPP row of 16 lanes. A row
+// enumerates its query's candidates in GetFeaturesInArea order (cells ix-outer / iy-inner, 16 grid
+// columns at a time flattened with a row prefix sum) and keeps the two smallest (dist, enumeration
+// index) keys, exactly the reference's sequential best / second-best (a later equal distance never
+// displaces an earlier one). Four query chains per wave in flight: one query per wave ran 0.77 ms at
+// config 5 th = 15 against 0.51 (profiles/r04_kernel_ab.txt items 10-11), its time being the
+// per-query chain (record -> grid columns -> candidates), not the window. Persistent blocks stage the
+// frame's keypoints, descriptors and per-keypoint gates in LDS.
 #define MT_WAVE_TH 6.0f
-#endif
 #define MT_STAGE_MAX 1536
-__device__ __forceinline__ unsigned long long mt_wave_min64(unsigned long long v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const unsigned long long o = ((unsigned long long)(unsigned)__shfl_xor((int)(v >> 32), d, 64) << 32) |
-                                     (unsigned)__shfl_xor((int)(v & 0xffffffffu), d, 64);
-        v = o < v ? o : v;
-    }
-    return v;
-}
-// The same minimum with DPP moves inside each row of 16 lanes (quad swaps, then half-row and row
-// mirrors: every lane of a row ends with the row minimum) and four readlanes across the rows: a
-// wave-uniform result with no LDS round trip (the shuffle form costs twelve dependent
-// ds_bpermutes per call, two calls per query on the wave kernel's serial per-query chain).
+#define MT_WNT 1024   // 16 waves per block share one staged copy of the frame
+#define MT_QPW 4      // queries per wave: one per row of 16 lanes
+// 64-bit minimum by DPP moves inside each row of 16 lanes (quad swaps, then half-row and row
+// mirrors: every lane of a row ends with the row minimum), no LDS round trip
 template <int CTRL>
 __device__ __forceinline__ unsigned long long mt_min64_dpp_step(unsigned long long v) {
     const unsigned hi = (unsigned)(v >> 32), lo = (unsigned)v;
@@ -337,188 +329,6 @@ __device__ __forceinline__ unsigned long long mt_min64_dpp_step(unsigned long lo
     const unsigned long long o = ((unsigned long long)oh << 32) | ol;
     return o < v ? o : v;
 }
-__device__ __forceinline__ unsigned long long mt_wave_min64_dpp(unsigned long long v) {
-    v = mt_min64_dpp_step<0xB1>(v);    // quad_perm [1, 0, 3, 2]
-    v = mt_min64_dpp_step<0x4E>(v);    // quad_perm [2, 3, 0, 1]
-    v = mt_min64_dpp_step<0x141>(v);   // row_half_mirror
-    v = mt_min64_dpp_step<0x140>(v);   // row_mirror
-    unsigned long long m = ~0ull;
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const unsigned long long x =
-            ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(v >> 32), 16 * r) << 32) |
-            (unsigned)__builtin_amdgcn_readlane((int)v, 16 * r);
-        m = x < m ? x : m;
-    }
-    return m;
-}
-#ifndef MT_WAVE_DPP
-#define MT_WAVE_DPP 1
-#endif
-#define MT_WNT 1024   // 16 waves per block share one staged copy of the frame
-template <bool STAGED>
-__global__ __launch_bounds__(MT_WNT) void k_sbp_local_wave(FrameDev fr, const orbfe_map_point* mps, int nq, float th,
-                                                        int bFar, float thFar, float nnratio, const int* blocked0,
-                                                        const int* first, int* assign, int* changed, PassIO io) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t mt_sm[];
-    if (pass_gated(io)) return;
-    pass_fill(io);
-    int2* s_cell = (int2*)mt_sm;                                          // [16][64] (start, exclusive prefix)
-    float4* s_key = (float4*)(mt_sm + (MT_WNT / 64) * 64 * sizeof(int2));  // x, y, octave bits, uR
-    uint4* s_desc = (uint4*)(s_key + (STAGED ? fr.n : 0));         // 2 x uint4 per keypoint
-    // {blocked0, first} per keypoint (read-only during a pass): the gate of every candidate without
-    // a global round trip on the query's chain
-    int2* s_gate = (int2*)(s_desc + (STAGED ? 2 * fr.n : 0));
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    if (STAGED) {
-        for (int i = tid; i < fr.n; i += MT_WNT) {
-            const OrbKeyPoint kp = fr.keys[i];
-            s_key[i] = make_float4(kp.x, kp.y, __int_as_float(kp.octave), fr.uright ? fr.uright[i] : -1.f);
-            const uint4* d = (const uint4*)(fr.desc + 8 * i);
-            s_desc[2 * i] = d[0];
-            s_desc[2 * i + 1] = d[1];
-            s_gate[i] = make_int2(blocked0[i], first[i]);
-        }
-        SYNC();
-    }
-    int2* my_cells = s_cell + 64 * wave;
-    constexpr int WPB = MT_WNT / 64;
-    for (int q = blockIdx.x * WPB + wave; q < nq; q += gridDim.x * WPB) {
-        const orbfe_map_point& mp = mps[q];
-        const int prev = assign[q];   // issued first: read only by the publish at the chain's end
-        int result = -1;
-        if ((mp.flags & ORBFE_MP_IN_VIEW) && !(bFar && mp.depth > thFar) && !(mp.flags & ORBFE_MP_BAD) &&
-            mp.scale_level >= 0 && mp.scale_level < fr.nlevels) {
-            const int lvl = mp.scale_level;
-            float r = mp.view_cos > 0.998 ? 2.5f : 4.0f;
-            if (th != 1.0f) r *= th;
-            const float R = r * fr.scale[lvl];
-            const float x = mp.proj_x, y = mp.proj_y, xr = mp.proj_xr;
-            uint32_t qd[8];
-#pragma unroll
-            for (int w = 0; w < 8; w++) {
-                uint32_t t;
-                memcpy(&t, mp.desc + 4 * w, 4);
-                qd[w] = __builtin_amdgcn_readfirstlane(t);
-            }
-            const int minLevel = lvl - 1, maxLevel = lvl;
-            const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
-            const int* pcs = fr.pcstart + lvl * fr.gstride_c;
-            const int* pci = fr.pcidx + lvl * fr.gstride_i;
-            const int cx0 = max(0, (int)floorf((x - fr.minx - R) * fr.invw));
-            const int cx1 = min(ORBFE_GRID_COLS - 1, (int)ceilf((x - fr.minx + R) * fr.invw));
-            const int cy0 = max(0, (int)floorf((y - fr.miny - R) * fr.invh));
-            const int cy1 = min(ORBFE_GRID_ROWS - 1, (int)ceilf((y - fr.miny + R) * fr.invh));
-            unsigned long long b1 = ~0ull, b2 = ~0ull;
-            int b1idx = -1;
-            unsigned nwin = 0, npair = 0;
-            if (cx0 < ORBFE_GRID_COLS && cx1 >= 0 && cy0 < ORBFE_GRID_ROWS && cy1 >= 0 && cx0 <= cx1 && cy0 <= cy1) {
-                // one contiguous CSR run per grid column of the window (<= 64 columns)
-                const int ncell = cx1 - cx0 + 1;
-                int obase = 0;
-                for (int cb = 0; cb < ncell; cb += 64) {
-                    const int c = cb + lane;
-                    int st = 0, cnt = 0;
-                    if (c < ncell) {
-                        const int ix = cx0 + c;
-                        st = pcs[ix * ORBFE_GRID_ROWS + cy0];
-                        cnt = pcs[ix * ORBFE_GRID_ROWS + cy1 + 1] - st;
-                    }
-                    const int incl = wave_incl_scan(cnt);
-                    const int tot = __shfl(incl, 63, 64);
-                    my_cells[lane] = make_int2(st, incl - cnt);
-                    WAVE_SYNC();
-                    for (int j0 = 0; j0 < tot; j0 += 64) {
-                        const int j = j0 + lane;
-                        if (j < tot) {
-                            nwin++;
-                            int lo = 0, hi = 64;   // last cell with prefix <= j
-                            while (hi - lo > 1) {
-                                const int mid = (lo + hi) >> 1;
-                                if (my_cells[mid].y <= j) lo = mid; else hi = mid;
-                            }
-                            const int2 ce = my_cells[lo];
-                            const int idx = pci[ce.x + (j - ce.y)];
-                            float kx, ky, ur;
-                            int oct;
-                            if (STAGED) {
-                                const float4 k4 = s_key[idx];
-                                kx = k4.x; ky = k4.y; oct = __float_as_int(k4.z); ur = k4.w;
-                            } else {
-                                const OrbKeyPoint kp = fr.keys[idx];
-                                kx = kp.x; ky = kp.y; oct = kp.octave; ur = fr.uright ? fr.uright[idx] : -1.f;
-                            }
-                            bool ok = true;
-                            if (bCheckLevels) {
-                                if (oct < minLevel) ok = false;
-                                if (maxLevel >= 0 && oct > maxLevel) ok = false;
-                            }
-                            ok = ok && fabsf(kx - x) < R && fabsf(ky - y) < R;
-                            if (STAGED) {
-                                const int2 gt = s_gate[idx];
-                                ok = ok && !(gt.x || gt.y < q);
-                            } else {
-                                ok = ok && !(blocked0[idx] || first[idx] < q);
-                            }
-                            if (ok && ur > 0) ok = !(fabsf(xr - ur) > R);
-                            if (ok) {
-                                npair++;
-                                uint4 d0, d1;
-                                if (STAGED) { d0 = s_desc[2 * idx]; d1 = s_desc[2 * idx + 1]; }
-                                else { d0 = ((const uint4*)(fr.desc + 8 * idx))[0]; d1 = ((const uint4*)(fr.desc + 8 * idx))[1]; }
-                                const int dist = __popc(qd[0] ^ d0.x) + __popc(qd[1] ^ d0.y) + __popc(qd[2] ^ d0.z) +
-                                                 __popc(qd[3] ^ d0.w) + __popc(qd[4] ^ d1.x) + __popc(qd[5] ^ d1.y) +
-                                                 __popc(qd[6] ^ d1.z) + __popc(qd[7] ^ d1.w);
-                                if (dist < 256) {
-                                    const unsigned long long k = ((unsigned long long)dist << 32) |
-                                                                 ((unsigned long long)(obase + j) << 4) | (unsigned)oct;
-                                    if (k < b1) { b2 = b1; b1 = k; b1idx = idx; }
-                                    else if (k < b2) b2 = k;
-                                }
-                            }
-                        }
-                    }
-                    obase += tot;
-                    WAVE_SYNC();
-                }
-            }
-            pass_stats(io, nwin, npair);
-#if MT_WAVE_DPP
-            const unsigned long long m1 = mt_wave_min64_dpp(b1);
-            const unsigned long long win = __ballot(b1 == m1 && m1 != ~0ull);
-            const unsigned long long m2 = mt_wave_min64_dpp(b1 == m1 ? b2 : b1);
-#else
-            const unsigned long long m1 = mt_wave_min64(b1);
-            const unsigned long long win = __ballot(b1 == m1 && m1 != ~0ull);
-            const unsigned long long m2 = mt_wave_min64(b1 == m1 ? b2 : b1);
-#endif
-            if (m1 != ~0ull) {
-                const int wl = __ffsll((long long)win) - 1;
-                const int bestIdx = __shfl(b1idx, wl, 64);
-                const int bestDist = (int)(m1 >> 32), bestLevel = (int)(m1 & 15);
-                const int bestDist2 = m2 != ~0ull ? (int)(m2 >> 32) : 256;
-                const int bestLevel2 = m2 != ~0ull ? (int)(m2 & 15) : -1;
-                if (bestDist <= MT_TH_HIGH) {
-                    if (!(bestLevel == bestLevel2 && bestDist > nnratio * bestDist2)) result = bestIdx;
-                }
-            }
-        }
-        if (lane == 0) {
-            pass_publish(io, q, result, mp.observations);
-            if (result != prev) {
-                assign[q] = result;
-                atomicAdd(changed, 1);
-            }
-        }
-    }
-}
-
-// Several queries per wave: MT_QPW groups of 16 lanes (one DPP row each), each group running the
-// wave kernel's enumeration and (dist, enumeration index) minimum for its own query, so a wave keeps
-// MT_QPW query chains in flight instead of one (the wave kernel's time is its per-query chain).
-#ifndef MT_QPW
-#define MT_QPW 4
-#endif
 __device__ __forceinline__ int mt_row_incl_scan(int v) {   // inclusive scan within each row of 16 lanes
     v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
     v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
@@ -542,15 +352,14 @@ template <bool STAGED>
 __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wq(FrameDev fr, const orbfe_map_point* mps, int nq, float th,
                                                       int bFar, float thFar, float nnratio, const int* blocked0,
                                                       const int* first, int* assign, int* changed, PassIO io) {
-    static_assert(MT_QPW == 4, "one query per DPP row of 16 lanes");
     constexpr int GL = 16;
     extern __shared__ __attribute__((aligned(16))) uint8_t mt_sm[];
     if (pass_gated(io)) return;
     pass_fill(io);
-    int2* s_cell = (int2*)mt_sm;                                          // [16 waves][4 groups][16]
-    float4* s_key = (float4*)(mt_sm + (MT_WNT / 64) * 64 * sizeof(int2));  // as k_sbp_local_wave
-    uint4* s_desc = (uint4*)(s_key + (STAGED ? fr.n : 0));
-    int2* s_gate = (int2*)(s_desc + (STAGED ? 2 * fr.n : 0));
+    int2* s_cell = (int2*)mt_sm;                                          // [16 waves][4 rows][16] (start, prefix)
+    float4* s_key = (float4*)(mt_sm + (MT_WNT / 64) * 64 * sizeof(int2));  // x, y, octave bits, uR
+    uint4* s_desc = (uint4*)(s_key + (STAGED ? fr.n : 0));         // 2 x uint4 per keypoint
+    int2* s_gate = (int2*)(s_desc + (STAGED ? 2 * fr.n : 0));      // {blocked0, first}, read-only in a pass
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, grp = lane >> 4, sl = lane & 15;
     if (STAGED) {
         for (int i = tid; i < fr.n; i += MT_WNT) {
@@ -1866,7 +1675,7 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
                 PassIO io{pass ? changed + pass - 1 : nullptr, fb[(pass + 1) % 3], fb[(pass + 2) % 3], n,
                           mode == 2 ? 0 : 1, stats};
                 const int* fcur = fb[pass % 3];
-                if (mode == 0 && th >= MT_WAVE_TH && MT_QPW > 1) {
+                if (mode == 0 && th >= MT_WAVE_TH) {
                     const int qpb = (MT_WNT / 64) * MT_QPW;   // queries per block and round
                     const int nb = std::min((nq + qpb - 1) / qpb, 512);
                     const size_t lds = (MT_WNT / 64) * 64 * sizeof(int2) + (staged ? (size_t)n * 56 : 0);
@@ -1876,17 +1685,6 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
                                            changed + pass, io);
                     else
                         hipLaunchKernelGGL(k_sbp_local_wq<false>, dim3(nb), dim3(MT_WNT), lds, s, fr,
-                                           (const orbfe_map_point*)q, nq, th, a0, thFar, nnratio, b0, fcur, assign,
-                                           changed + pass, io);
-                } else if (mode == 0 && th >= MT_WAVE_TH) {
-                    const int nb = std::min((nq + MT_WNT / 64 - 1) / (MT_WNT / 64), 512);
-                    const size_t lds = (MT_WNT / 64) * 64 * sizeof(int2) + (staged ? (size_t)n * 56 : 0);
-                    if (staged)
-                        hipLaunchKernelGGL(k_sbp_local_wave<true>, dim3(nb), dim3(MT_WNT), lds, s, fr,
-                                           (const orbfe_map_point*)q, nq, th, a0, thFar, nnratio, b0, fcur, assign,
-                                           changed + pass, io);
-                    else
-                        hipLaunchKernelGGL(k_sbp_local_wave<false>, dim3(nb), dim3(MT_WNT), lds, s, fr,
                                            (const orbfe_map_point*)q, nq, th, a0, thFar, nnratio, b0, fcur, assign,
                                            changed + pass, io);
                 } else if (mode == 0) {

@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU: counters of the config-5 search kernels per th (k_sbp_local for th < 6, k_sbp_local_wave
+# GPU: counters of the config-5 search kernels per th (k_sbp_local for th < 6, k_sbp_local_wq
 # above; one rocprofv3 --pmc pass per counter group), summarised into
 # gpurun_out/${PREFIX}_pmc_matcher.json by tools/matcher_pmc_summary.py.
 set -o pipefail
