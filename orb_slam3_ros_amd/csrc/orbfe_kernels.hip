@@ -1119,14 +1119,16 @@ __device__ __forceinline__ void wave_introsort_impl(unsigned long long* a, int n
     const int tid = lane_id();
     if (n <= 1) return;
     const unsigned long long lt = (1ull << tid) - 1ull;
-    // the segment stack lives in LDS (written by lane 0), its depth and the leaf count in registers
-    // (wave-uniform): per partition step three wave hand-offs, the stops ranked by ballots
-    if (tid == 0) segs[0] = make_int4(0, n, 2 * st_lg(n), 0);
-    WAVE_SYNC();
+    // the segment stack lives in registers, entry k in lane k (ORBFE_SORT_STACK = 64 = the wave;
+    // pop = three readlanes, push = the owning lane's moves), its depth and the leaf count
+    // wave-uniform: per partition step two wave hand-offs through LDS, the stops ranked by ballots
+    (void)segs;
+    int sg_lo = 0, sg_hi = tid == 0 ? n : 0, sg_dp = tid == 0 ? 2 * st_lg(n) : 0;
     int sp = 1, nleaf = 0;
     while (sp > 0) {
-        const int4 sg = segs[--sp];
-        const int lo = sg.x, hi = sg.y, depth = sg.z;
+        --sp;
+        const int lo = __builtin_amdgcn_readlane(sg_lo, sp), hi = __builtin_amdgcn_readlane(sg_hi, sp);
+        const int depth = __builtin_amdgcn_readlane(sg_dp, sp);
         if (hi - lo <= 16 || depth == 0) {
             if (tid == 0) leaves[nleaf] = lo | ((hi - lo <= 16) ? 0 : (int)0x80000000);
             nleaf++;
@@ -1182,10 +1184,8 @@ __device__ __forceinline__ void wave_introsort_impl(unsigned long long* a, int n
         int cut;
         if (sw == 0) cut = lpos[0];
         else cut = (sw < nl && lpos[sw] < rpos[sw - 1]) ? lpos[sw] : rpos[sw - 1];
-        if (tid == 0) {
-            segs[sp] = make_int4(cut, hi, depth - 1, 0);
-            segs[sp + 1] = make_int4(lo, cut, depth - 1, 0);
-        }
+        if (tid == sp) { sg_lo = cut; sg_hi = hi; sg_dp = depth - 1; }
+        if (tid == sp + 1) { sg_lo = lo; sg_hi = cut; sg_dp = depth - 1; }
         sp += 2;
         WAVE_SYNC();
     }
