@@ -1136,6 +1136,7 @@ __device__ __forceinline__ void wave_introsort_impl(unsigned long long* a, int n
         }
         // __move_median_to_first(first, first + 1, mid, last - 1): every lane evaluates the
         // comparison tree on the same four values, lane 0 performs the one swap
+        unsigned long long xpiv;
         {
             const int ia = lo + 1, ib = lo + (hi - lo) / 2, ic = hi - 1;
             const unsigned long long x0 = a[lo], xa = a[ia], xb = a[ib], xc = a[ic];
@@ -1143,14 +1144,14 @@ __device__ __forceinline__ void wave_introsort_impl(unsigned long long* a, int n
             int pick;
             if (comp(xa, xb)) pick = comp(xb, xc) ? ib : (comp(xa, xc) ? ic : ia);
             else pick = comp(xa, xc) ? ia : (comp(xb, xc) ? ic : ib);
-            const unsigned long long xp = pick == ia ? xa : (pick == ib ? xb : xc);
+            xpiv = pick == ia ? xa : (pick == ib ? xb : xc);
             if (tid == 0) {
-                a[lo] = xp;
+                a[lo] = xpiv;
                 a[pick] = x0;
             }
         }
         WAVE_SYNC();
-        const unsigned P = (unsigned)(a[lo] >> 32);
+        const unsigned P = (unsigned)(xpiv >> 32);   // the pivot every lane already holds
         const int m = hi - lo - 1;
         // left stops (scan rightwards over [lo+1, hi)): !(x < P); right stops (leftwards from
         // hi-1): !(P < x); the k-th stop of each side lands at lpos[k] / rpos[k]
