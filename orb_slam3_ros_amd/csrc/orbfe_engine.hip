@@ -383,7 +383,7 @@ static int ensure(orbfe_extractor* h, int W, int H, int B) {
 // since one image cannot fill the GPU and the frame's latency is its longest chain of dependent steps.
 constexpr int kSmallBatch = 16;
 constexpr int kSmallRsRows = 4;       // k_resize_s output rows per wave (48 for large batches)
-constexpr int kSmallStereoLk = 32;    // k_stereo left keypoints per block (ST_LK = 512)
+constexpr int kSmallStereoLk = 16;    // k_stereo left keypoints per block (ST_LK = 512)
 constexpr int kSmallOctNt = 1024;     // k_octree threads per (image, level) block (OCT_NT = 256)
 
 static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs, int pitch, const int* laps,
