@@ -151,9 +151,9 @@ def start_native_oracle_build():
     extractor + stereo restatement for THIS host in the background (a few seconds) while the GPU
     legs run. Returns (process, path) or (None, None)."""
     out = os.path.join(tempfile.gettempdir(), f"orbfe_oracle_native_{os.getpid()}.so")
-    src = os.path.join(ROOT, "oracle", "orb_oracle.cpp")
+    srcs = [os.path.join(ROOT, "oracle", f) for f in ("orb_oracle.cpp", "orb_oracle_match.cpp", "orb_oracle_bench.cpp")]
     cmd = ["g++", "-O3", "-march=native", "-ffp-contract=off", "-fno-fast-math", "-std=c++17", "-fPIC", "-shared",
-           "-o", out, src, "-lpthread"]
+           "-o", out] + srcs + ["-lpthread"]
     try:
         return subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE), out
     except OSError:
@@ -182,6 +182,11 @@ def _oracle_cdll(native):
     L.oro_bench_stereo_latency.argtypes = [vp, vp, ci, ci, ci, ci, cf, ci, ci, ci, cf, cf, ci, cd]
     L.oro_bench_mono.restype = ctypes.c_long
     L.oro_bench_mono.argtypes = [vp, ci, ci, ci, ci, cf, ci, ci, ci, ci, ci, ci, cd]
+    L.oro_bench_fisheye_latency.restype = ctypes.c_long
+    L.oro_bench_fisheye_latency.argtypes = [vp, vp, ci, ci, ci, ci, cf, ci, ci, ci, ci, ci, ci, cd]
+    L.oro_bench_fisheye.restype = ctypes.c_long
+    L.oro_bench_fisheye.argtypes = [vp, vp, ci, ci, ci, ci, cf, ci, ci, ci, ci, ci, ci, cd]
+    oracle._match_sigs(L)
     return L, flags
 
 
@@ -246,10 +251,70 @@ def cpu_baseline(native, budget_s=4.0):
                      "sample": f"{n1} frames latency, {nt} frames throughput ({U} distinct synthetic {W}x{H} "
                                f"images, nFeatures {nf}, vLappingArea {{0, 1000}} as the mono Frame passes)"}
 
+    def fisheye_cfg(name, W, H, nf, lap, seed):
+        # BASELINE config 4's per-frame CPU path: ExtractORB L || R (lapping {0, 511}) + the fisheye
+        # stereo descriptor stage (knnMatch k=2 + ratio 0.7, Frame.cc:1126-1151)
+        U = 8
+        pairs = [synth_stereo(seed + i, W, H) for i in range(U)]
+        Ls = np.ascontiguousarray(np.stack([p[0] for p in pairs]))
+        Rs = np.ascontiguousarray(np.stack([p[1] for p in pairs]))
+        L.oro_bench_fisheye_latency(Ls.ctypes.data, Rs.ctypes.data, 1, W, H, nf, 1.2, 8, 20, 7, lap[0], lap[1], 0,
+                                    ctypes.byref(ms))
+        est = max(ms.value, 1.0)
+        n1 = int(min(400, max(8, budget_s * 1e3 / est)))
+        idx = [i % U for i in range(n1)]
+        Ln, Rn = np.ascontiguousarray(Ls[idx]), np.ascontiguousarray(Rs[idx])
+        L.oro_bench_fisheye_latency(Ln.ctypes.data, Rn.ctypes.data, n1, W, H, nf, 1.2, 8, 20, 7, lap[0], lap[1], 0,
+                                    ctypes.byref(ms))
+        lat1 = ms.value
+        L.oro_bench_fisheye_latency(Ln.ctypes.data, Rn.ctypes.data, n1, W, H, nf, 1.2, 8, 20, 7, lap[0], lap[1], 1,
+                                    ctypes.byref(ms))
+        lat2 = ms.value
+        nt = int(min(20000, max(2 * threads, budget_s * 1e3 * threads / est)))
+        idx = [i % U for i in range(nt)]
+        Ln, Rn = np.ascontiguousarray(Ls[idx]), np.ascontiguousarray(Rs[idx])
+        L.oro_bench_fisheye(Ln.ctypes.data, Rn.ctypes.data, nt, W, H, nf, 1.2, 8, 20, 7, lap[0], lap[1], threads,
+                            ctypes.byref(ms))
+        out[name] = {"latency_1t_ms": round(lat1, 3), "latency_lr2t_ms": round(lat2, 3),
+                     "throughput_frames_per_s": round(nt / (ms.value * 1e-3), 2), "throughput_threads": threads,
+                     "images_per_s": round(2 * nt / (ms.value * 1e-3), 2),
+                     "sample": f"{n1} frames per latency mode, {nt} frames for throughput ({U} distinct synthetic "
+                               f"{W}x{H} pairs, nFeatures {nf}, vLappingArea {{{lap[0]},{lap[1]}}}); extract L+R + "
+                               f"knnMatch(k=2)+ratio of the lapping rows (TriangulateMatches not timed)"}
+
+    def sbp_config5():
+        # BASELINE config 5 on the CPU restatement: the same synthetic frame / 100k map points / slots as
+        # matcher_config5 (seed 12345). The search is ordered over the map points (later points see
+        # earlier assignments, ORBmatcher.cc:88-90), so the reference runs it on one thread.
+        from orb_slam3_ros_amd import synth_match as sm
+        rng = np.random.default_rng(12345)
+        F = sm.synth_frame(rng, 1000)
+        mps = sm.synth_local_map(rng, F, 100_000)
+        mvp0, obs = sm.initial_slots(rng, F.N)
+        res = {}
+        for th in (1, 3, 5, 15):
+            times, n = [], 0
+            t_end = time.perf_counter() + budget_s / 4
+            while time.perf_counter() < t_end or len(times) < 3:
+                mvp = mvp0.copy()
+                t0 = time.perf_counter()
+                n = L.oro_sbp_local(F.ref(), mvp.ctypes.data, obs.ctypes.data, mps.ctypes.data, len(mps), float(th), 0,
+                                    50.0, 0.8)
+                times.append(time.perf_counter() - t0)
+            m = float(np.median(times))
+            res[f"th{th}"] = {"ms_per_call": round(m * 1e3, 3), "queries_per_s": round(len(mps) / m, 1),
+                              "calls": len(times), "nmatches": int(n)}
+        out["config5_search_by_projection_100k"] = {
+            "per_th": res, "threads": 1,
+            "sample": "SearchByProjection(F, 100k local map points, th) of matcher_config5's workload (seed 12345), "
+                      "median over >= 3 calls per th; ordered over the points, one thread as in the reference"}
+
     t0 = time.perf_counter()
     stereo_cfg("config2_euroc_stereo_752x480", 752, 480, 1000, EUROC_BF, EUROC_FX, 9000)
     mono_cfg("config1_euroc_mono_752x480", 752, 480, 1000, 9100)
     stereo_cfg("config3_kitti_stereo_1241x376", 1241, 376, 2000, KITTI_BF, KITTI_FX, 9200)
+    fisheye_cfg("config4_tumvi_fisheye_512x512", 512, 512, 1000, (0, 511), 9300)
+    sbp_config5()
     total = time.perf_counter() - t0
     c2 = out["config2_euroc_stereo_752x480"]
     return {"value": c2["throughput_frames_per_s"], "unit": "frames/s", "cores": threads, "kind": "port",
@@ -495,35 +560,84 @@ def pmc_valu(n_img, w, h):
     return best
 
 
-def dropin_leg(frames, W=752, H=480, nf=1000, bf=0.110078 * 458.654, fx=458.654):
-    """The drop-in path at batch 1 (rank 0, not part of `value`): one 752x480 stereo frame at a time
-    through the host C-ABI exactly as Tracking builds a stereo Frame (Frame.cc:122-141): two
-    ORBextractor::operator() calls on two per-frame std::threads, then ComputeStereoMatches, host
-    images in and host results out. Timed by the compiled C++ consumer (tests/native/capi_frontend.cpp
-    --latency, linked against liborbfe.so only): frame_ms as an application runs it (no event timing),
-    then a second run with the library's HIP-event split
-    of each call (upload / kernels / result copies; host = wall - the device-side critical path) and
-    its own wall time, frame_ms_timed."""
+def write_sequence_job(path, frames, W=752, H=480, nf=1000, window=20, seed=21):
+    """The drop-in harness's input (tests/native/capi_frontend.cpp SeqJob): a seeded synthetic stereo
+    sequence (synth.synth_stereo_sequence: a planar scene at disparity SEQ_DISP, the rig moving SEQ_SHIFT
+    px per frame, every frame distinct) with the EuRoC MH_01 pinhole intrinsics and the per-frame
+    translation that makes the constant-velocity motion model exact."""
     import struct
+    from orb_slam3_ros_amd.synth import SEQ_DISP, SEQ_SHIFT, synth_stereo_sequence
+    fx, fy, cx, cy = EUROC_FX, 457.296, 367.215, 248.375
+    bf = EUROC_BF
+    tx = SEQ_SHIFT * (bf / SEQ_DISP) / fx
+    seq = synth_stereo_sequence(seed, frames, W, H)
+    with open(path, "wb") as f:
+        f.write(struct.pack("<6i6f", 0x5342524F, W, H, nf, frames, window, fx, fy, cx, cy, bf, tx))
+        for left, right in seq:
+            f.write(left.tobytes())
+            f.write(right.tobytes())
+    return path
+
+
+def dropin_leg(frames, W=752, H=480, nf=1000, tracking_frames=60, cpu=True):
+    """The drop-in path at batch 1 (rank 0, not part of `value`), timed by the compiled C++ consumer of
+    the C-ABI (tests/native/capi_frontend.cpp, linked against liborbfe.so only) over a seeded synthetic
+    stereo SEQUENCE (every frame a distinct pair, small per-frame shifts), host images in and host
+    results out:
+      frame_call: orbfe_frame_stereo, Frame::Frame(stereo) in one call (Frame.cc:101-141);
+      threads:    two ORBextractor::operator() calls on two per-frame std::threads, then
+                  ComputeStereoMatches (Frame.cc:122-141), the way the reference builds the Frame;
+      tracking:   a whole Tracking frame (tests/native/tracking_loop.h): Frame(stereo), then
+                  SearchByProjection(CurrentFrame, LastFrame, th 7) (Tracking.cc:2925) and
+                  SearchLocalPoints (isInFrustum + SearchByProjection(F, local map, th 1),
+                  Tracking.cc:3382-3452), with the same loop run on the CPU restatement beside it
+                  (tests/native/tracking_cpu.cpp) and the two runs' per-frame results compared.
+    frame_ms = median wall time per frame without event timing; split_ms from a second, timed pass."""
     import subprocess
     import tempfile
     from orb_slam3_ros_amd import build as B
-    from orb_slam3_ros_amd.synth import synth_stereo
     binary = B.CAPI_BIN
     if not os.path.exists(binary):
         return {"error": "tests/native/capi_frontend not built (run __graft_entry__.build())"}
-    left, right = synth_stereo(7, W, H)
+    n_seq = max(frames, tracking_frames)
+    out = {}
     with tempfile.TemporaryDirectory() as d:
-        job = os.path.join(d, "job.bin")
-        with open(job, "wb") as f:
-            f.write(struct.pack("<5i2f", W, H, nf, 0, 100, bf, fx) + left.tobytes() + right.tobytes())
+        job = write_sequence_job(os.path.join(d, "seq.bin"), n_seq, W, H, nf)
         r = subprocess.run([binary, "--latency", str(frames), job], capture_output=True, text=True, timeout=300)
-    if r.returncode != 0:
-        return {"error": (r.stderr or r.stdout)[-400:]}
-    out = json.loads(r.stdout.strip().splitlines()[-1])
-    out["path"] = ("host C-ABI per frame: orbfe_extract L || R on two std::threads (ExtractORB, Frame.cc:122-125), "
-                   "then orbfe_stereo_match (Frame.cc:141); medians over the frames; split_ms from a second, "
-                   "timed run (per-call HIP events on)")
+        if r.returncode != 0:
+            return {"error": (r.stderr or r.stdout)[-400:]}
+        lat = json.loads(r.stdout.strip().splitlines()[-1])
+        out.update(lat["frame_call"])
+        out["threads"] = lat["threads"]
+        out["frames"], out["distinct_pairs"] = lat["frames"], lat["distinct_pairs"]
+        out["path"] = ("host C-ABI per frame over a seeded stereo sequence: orbfe_frame_stereo (Frame(stereo) in one "
+                       "call: one upload, one two-image launch chain with the stereo kernels, one result copy); "
+                       "`threads` = orbfe_extract L || R on two std::threads + orbfe_stereo_match")
+        if tracking_frames > 0:
+            g_out, c_out = os.path.join(d, "gpu.out"), os.path.join(d, "cpu.out")
+            r = subprocess.run([binary, "--tracking", str(tracking_frames), job, g_out], capture_output=True, text=True,
+                               timeout=300)
+            if r.returncode != 0:
+                out["tracking"] = {"error": (r.stderr or r.stdout)[-400:]}
+            else:
+                tr = json.loads(r.stdout.strip().splitlines()[-1])
+                if cpu and os.path.exists(B.TRACK_CPU_BIN):
+                    # CHECKER + CPU baseline: the same loop on the oracle restatement
+                    rc = subprocess.run([B.TRACK_CPU_BIN, str(tracking_frames), job, c_out], capture_output=True,
+                                        text=True, timeout=600)
+                    if rc.returncode == 0:
+                        tc = json.loads(rc.stdout.strip().splitlines()[-1])
+                        same = open(g_out, "rb").read() == open(c_out, "rb").read()
+                        tr["cpu"] = {"tracking_frame_ms": tc["tracking_frame_ms"], "split_ms": tc["split_ms"],
+                                     "path": tc["path"]}
+                        tr["speedup_vs_cpu"] = round(tc["tracking_frame_ms"] / tr["tracking_frame_ms"], 2)
+                        tr["parity"] = ("every frame's counts and mvpMapPoints identical to the CPU restatement's run"
+                                        if same else "MISMATCH against the CPU restatement's run")
+                        tr["parity_ok"] = same
+                    else:
+                        tr["cpu"] = {"error": (rc.stderr or rc.stdout)[-400:]}
+                out["tracking"] = tr
+                out["tracking_frame_ms"] = tr["tracking_frame_ms"]
     return out
 
 
@@ -792,7 +906,7 @@ def main():
         if args.matcher_steps > 0:
             result["matcher_config5"] = matcher_config5(args.matcher_steps)
         if args.dropin_frames > 0 and world == 1:
-            dl = dropin_leg(args.dropin_frames, nf=args.nfeatures)
+            dl = dropin_leg(args.dropin_frames, nf=args.nfeatures, cpu=not args.no_cpu_baseline)
             result["dropin"] = dl
             result["dropin_latency_ms"] = dl.get("frame_ms")
         if not args.no_cpu_baseline and world == 1:

@@ -139,6 +139,23 @@ int orbfe_stereo_match_batch(orbfe_extractor* left, int lbase, int lstep, orbfe_
 int orbfe_stereo_match(orbfe_extractor* left, orbfe_extractor* right, float bf, float fx, float* uright,
                        float* depth);
 
+/* Frame::Frame(stereo) (src/Frame.cc:101-141) in one call: ExtractORB(0, imLeft) and ExtractORB(1,
+ * imRight) (:122-125, ORBextractor::operator() with vLappingArea {0, 0}), then ComputeStereoMatches
+ * (:141), with host images in and host results out. Replaces the two per-frame std::threads plus
+ * orbfe_extract x 2 + orbfe_stereo_match: both images go up in one pinned copy, run as ONE two-image
+ * batch on `left` (image 0 = left, image 1 = right: orbfe_pyramid_level(left, 1, ...) is the right
+ * extractor's mvImagePyramid afterwards) with the stereo kernels on the same stream, and every result
+ * comes back before one synchronisation. `right` must have left's parameters (Tracking builds both
+ * extractors from the same settings, Tracking.cc:637-645; else ORBFE_E_ARG); it is not written.
+ * Outputs as orbfe_extract for each side (n_*, mono_* = monoIndex) and orbfe_stereo_match
+ * (uright / depth [n_left]). Returns the pre-cut stereo match count. orbfe_get_call_timing(left)
+ * then holds {upload, extraction kernels, result copies, stereo kernels, 0}. */
+int orbfe_frame_stereo(orbfe_extractor* left, orbfe_extractor* right, const uint8_t* img_left,
+                       const uint8_t* img_right, int width, int height, int stride, float bf, float fx,
+                       orbfe_keypoint* kps_left, uint8_t* desc_left, int cap_left, int* n_left, int* mono_left,
+                       orbfe_keypoint* kps_right, uint8_t* desc_right, int cap_right, int* n_right,
+                       int* mono_right, float* uright, float* depth);
+
 /* ---------------------------------------------------------------------------------------------
  * ORBmatcher — replaces the Tracking-thread methods of ORB_SLAM3::ORBmatcher (include/ORBmatcher.h)
  * and Frame::ComputeStereoFishEyeMatches' brute-force kNN. Stateless and re-entrant; every call
@@ -450,7 +467,8 @@ typedef int32_t (*orbfe_epipolar_fn)(void* ctx, int32_t idx1, int32_t idx2);
  * reference keeps the last candidate of the smallest passing dist, which is the first of this order
  * that passes, so epipolar() is called only until then (never more often than the reference calls
  * it). Then the rotation-histogram filter with checkOri (:1114-1131). matches12 as
- * orbfe_search_for_triangulation. Returns nmatches. */
+ * orbfe_search_for_triangulation. Returns nmatches, or ORBFE_E_CAPACITY when the candidate slots (the sum
+ * over KF1 entries of their shared KF2 node's size) exceed 16 M: the caller then keeps its CPU body. */
 int orbfe_search_for_triangulation_epi(const orbfe_frame* KF1, const int32_t* mp1, const orbfe_feature_vector* fv1,
                                        const orbfe_frame* KF2, const int32_t* mp2, const orbfe_feature_vector* fv2,
                                        const float* ep, int32_t bOnlyStereo, int32_t checkOri,

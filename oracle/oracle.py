@@ -19,7 +19,7 @@ KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle"
 
 
 def build(force: bool = False) -> str:
-    srcs = [os.path.join(_HERE, f) for f in ("orb_oracle.cpp", "orb_oracle_match.cpp", "orb_oracle_bow.cpp", "orb_oracle_remap.cpp", "Makefile")]
+    srcs = [os.path.join(_HERE, f) for f in ("orb_oracle.cpp", "orb_oracle_match.cpp", "orb_oracle_bow.cpp", "orb_oracle_remap.cpp", "orb_oracle_bench.cpp", "Makefile")]
     if force or not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in srcs):
         subprocess.run(["make", "-C", _HERE, "-B" if force else "-s"], check=True)
     return LIB

@@ -55,6 +55,8 @@ _SIGS = {
     "orbfe_stereo_match_batch": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_float, _c_float,
                                           _vp, _vp, _vp, _vp]),
     "orbfe_stereo_match": (_c_int, [_vp, _vp, _c_float, _c_float, _vp, _vp]),
+    "orbfe_frame_stereo": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _c_float,
+                                    _vp, _vp, _c_int, _P_int, _P_int, _vp, _vp, _c_int, _P_int, _P_int, _vp, _vp]),
     "orbfe_descriptor_distance": (_c_int, [_vp, _vp]),
     "orbfe_debug_copy": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _c_int]),
     "orbfe_debug_block_sort": (_c_int, [_vp, _c_int]),
@@ -137,9 +139,10 @@ def load(path: str | None = None) -> ctypes.CDLL:
         try:
             fn = getattr(lib, name)
         except AttributeError:
-            # an older ORBFE_LIB build (kernel A/B baseline) may predate an entry point: using it
-            # raises; the product library is checked to export every symbol (tests/test_capi.py)
-            if p == LIB_PATH:
+            # an older build (a kernel A/B baseline) may predate an entry point, but only when that
+            # is asked for explicitly (ORBFE_LIB_PARTIAL=1); the product library, reached by any
+            # path, must export every symbol (tests/test_capi.py)
+            if os.environ.get("ORBFE_LIB_PARTIAL") != "1" or os.path.realpath(p) == os.path.realpath(LIB_PATH):
                 raise
             continue
         fn.restype = res

@@ -640,6 +640,8 @@ int orbfe_search_for_triangulation(const orbfe_frame* KF1, const int32_t* mp1, c
     return nm;
 }
 
+static constexpr size_t kTriEpiMaxSlots = (size_t)1 << 24;
+
 int orbfe_search_for_triangulation_epi(const orbfe_frame* KF1, const int32_t* mp1, const orbfe_feature_vector* fv1,
                                        const orbfe_frame* KF2, const int32_t* mp2, const orbfe_feature_vector* fv2,
                                        const float* ep, int32_t bOnlyStereo, int32_t checkOri,
@@ -672,7 +674,10 @@ int orbfe_search_for_triangulation_epi(const orbfe_frame* KF1, const int32_t* mp
         else b++;
     }
     if (items.empty()) return 0;
-    if (total > (size_t)INT_MAX / 4) return ORBFE_E_CAPACITY;
+    // candidate slots = sum over items of the KF2 node size: a pair of keyframes with very coarse
+    // vocabulary nodes would need a large scratch (and k_tri_cand's per-item insertion is O(nb^2));
+    // beyond 16 M slots (64 MB) the call reports capacity and the caller keeps its CPU body
+    if (total > kTriEpiMaxSlots) return ORBFE_E_CAPACITY;
     const int nitems = (int)items.size();
     const int m1 = fv1->offsets[fv1->n_nodes], m2 = fv2->offsets[fv2->n_nodes];
     Plan p;

@@ -848,6 +848,8 @@ int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int width, int height,
 
 int orbfe_get_call_timing(orbfe_extractor* h, float* ms) {
     if (!h || !ms) return ORBFE_E_ARG;
+    // the calls write call_ms and toggle `timing` under the handle's mutex
+    std::lock_guard<std::mutex> lk(h->mu);
     for (int i = 0; i < 5; i++) ms[i] = h->call_ms[i];
     return h->timing ? 5 : 0;
 }
@@ -965,6 +967,125 @@ int orbfe_stereo_match(orbfe_extractor* left, orbfe_extractor* right, float bf, 
     if (tm) {   // {kernels, result copies}
         HIPCHK(hipEventElapsedTime(&left->call_ms[3], left->call_ev[4], left->call_ev[5]));
         HIPCHK(hipEventElapsedTime(&left->call_ms[4], left->call_ev[5], left->call_ev[6]));
+    }
+    return nm;
+}
+
+// Frame::Frame(stereo) in one call (Frame.cc:120-141): both ExtractORB calls (:122-125) as ONE
+// two-image batch on the left handle (left image 0, right image 1), ComputeStereoMatches (:141) on
+// the same stream, one pinned upload of both images and one synchronisation for all results. The
+// right handle only supplies (and must equal) the extractor parameters, as Tracking constructs both
+// extractors from the same settings (Tracking.cc:637-645); it is not written.
+int orbfe_frame_stereo(orbfe_extractor* left, orbfe_extractor* right, const uint8_t* img_left,
+                       const uint8_t* img_right, int width, int height, int stride, float bf, float fx,
+                       orbfe_keypoint* kps_left, uint8_t* desc_left, int cap_left, int* n_left, int* mono_left,
+                       orbfe_keypoint* kps_right, uint8_t* desc_right, int cap_right, int* n_right,
+                       int* mono_right, float* uright, float* depth) {
+    if (!left || !right || !n_left || !n_right || !mono_left || !mono_right) return ORBFE_E_ARG;
+    *n_left = *n_right = 0;
+    *mono_left = *mono_right = -1;
+    if (!img_left || !img_right || width <= 0 || height <= 0) return ORBFE_E_EMPTY;
+    if (stride < width || !kps_left || !desc_left || !kps_right || !desc_right || !uright || !depth) return ORBFE_E_ARG;
+    if (left != right && (left->nfeatures != right->nfeatures || left->nlevels != right->nlevels ||
+                          left->scale_factor_f != right->scale_factor_f || left->ini_th != right->ini_th ||
+                          left->min_th != right->min_th || left->resize_simd_lanes != right->resize_simd_lanes ||
+                          left->blur_variant != right->blur_variant))
+        return ORBFE_E_ARG;
+    orbfe_extractor* h = left;
+    std::lock_guard<std::mutex> lk(h->mu);
+    int rc = ensure(h, width, height, 2);
+    if (rc) return rc;
+    hipStream_t s = h->own_stream;
+    const size_t bytes = (size_t)width * height;
+    if (h->stage_bytes < 2 * bytes) {
+        if (h->d_stage) HIPCHK(hipFree(h->d_stage));
+        h->d_stage = nullptr;
+        h->stage_bytes = 0;
+        HIPCHK(hipMalloc(&h->d_stage, 2 * bytes));
+        h->stage_bytes = 2 * bytes;
+    }
+    const int kc = h->g.kp_cap;
+    if (!h->d_st || h->stereo_kp < kc) {   // {nmatch (16 B) | uR [kc] | depth [kc]}
+        if (h->d_st) HIPCHK(hipFree(h->d_st));
+        h->d_st = nullptr;
+        h->d_uright = h->d_depth = nullptr;
+        h->d_nmatch = nullptr;
+        h->stereo_kp = 0;
+        HIPCHK(hipMalloc(&h->d_st, 16 + (size_t)kc * 8));
+        h->d_nmatch = (int*)h->d_st;
+        h->d_uright = (float*)(h->d_st + 16);
+        h->d_depth = h->d_uright + kc;
+        h->stereo_kp = kc;
+    }
+    // pinned: both images going up; coming back {counts [2][2] | keypoints [2][kc] | descriptors
+    // [2][kc]} (the two-image output block) then {nmatch | uR | depth}
+    size_t o_kps, o_desc, o_end;
+    out_layout(2, kc, &o_kps, &o_desc, &o_end);
+    const size_t o_st = (o_end + 15) & ~(size_t)15, st_bytes = 16 + (size_t)h->stereo_kp * 8;
+    const size_t pin_need = std::max(2 * bytes, o_st + st_bytes);
+    if (h->pin_bytes < pin_need) {
+        if (h->h_pin) HIPCHK(hipHostFree(h->h_pin));
+        h->h_pin = nullptr;
+        h->pin_bytes = 0;
+        HIPCHK(hipHostMalloc((void**)&h->h_pin, pin_need, hipHostMallocDefault));
+        h->pin_bytes = pin_need;
+    }
+    uint8_t* hp = h->h_pin;
+    const uint8_t* src[2] = {img_left, img_right};
+    for (int i = 0; i < 2; i++) {
+        if (stride == width) memcpy(hp + i * bytes, src[i], bytes);
+        else
+            for (int y = 0; y < height; y++)
+                memcpy(hp + i * bytes + (size_t)y * width, src[i] + (size_t)y * stride, width);
+    }
+    const bool tm = h->timing;
+    if (tm && !h->call_ev[0])
+        for (auto& e : h->call_ev) HIPCHK(hipEventCreate(&e));
+    const uint8_t* ptrs[2] = {h->d_stage, h->d_stage + bytes};
+    const int laps[4] = {0, 0, 0, 0};   // the pinhole stereo Frame passes vLappingArea {0, 0} (Frame.cc:122-123)
+    if (tm) HIPCHK(hipEventRecord(h->call_ev[0], s));
+    HIPCHK(hipMemcpyAsync(h->d_stage, hp, 2 * bytes, hipMemcpyHostToDevice, s));
+    if (tm) HIPCHK(hipEventRecord(h->call_ev[1], s));
+    h->timing = false;   // the call's own events bracket the kernels (the stage ring is for batches)
+    rc = run_batch(h, 2, ptrs, width, laps, s, false);
+    h->timing = tm;
+    if (rc) return rc;
+    if (tm) HIPCHK(hipEventRecord(h->call_ev[2], s));
+    rc = orbfe_stereo_match_batch(h, 0, 1, h, 1, 1, 1, bf, fx, h->d_uright, h->d_depth, h->d_nmatch, s);
+    if (rc) return rc;
+    if (tm) HIPCHK(hipEventRecord(h->call_ev[4], s));
+    if (h->cap_b == 2) {   // the handle's two-image output block: one copy
+        HIPCHK(hipMemcpyAsync(hp, h->d_out, o_end, hipMemcpyDeviceToHost, s));
+    } else {
+        HIPCHK(hipMemcpyAsync(hp, h->last_counts, 16, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(hp + o_kps, h->last_kps, (size_t)2 * kc * sizeof(OrbKeyPoint), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(hp + o_desc, h->last_desc, (size_t)2 * kc * 32, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipMemcpyAsync(hp + o_st, h->d_st, st_bytes, hipMemcpyDeviceToHost, s));
+    if (tm) HIPCHK(hipEventRecord(h->call_ev[5], s));
+    HIPCHK(hipStreamSynchronize(s));
+    int cnt[4], nm = 0;
+    memcpy(cnt, hp, 16);
+    memcpy(&nm, hp + o_st, 4);
+    *n_left = cnt[0];
+    *n_right = cnt[2];
+    *mono_left = cnt[1];
+    *mono_right = cnt[3];
+    if (cnt[0] > cap_left || cnt[2] > cap_right) return ORBFE_E_CAPACITY;
+    const OrbKeyPoint* hk = (const OrbKeyPoint*)(hp + o_kps);
+    const uint8_t* hd = hp + o_desc;
+    memcpy(kps_left, hk, (size_t)cnt[0] * sizeof(OrbKeyPoint));
+    memcpy(desc_left, hd, (size_t)cnt[0] * 32);
+    memcpy(kps_right, hk + kc, (size_t)cnt[2] * sizeof(OrbKeyPoint));
+    memcpy(desc_right, hd + (size_t)kc * 32, (size_t)cnt[2] * 32);
+    memcpy(uright, hp + o_st + 16, (size_t)cnt[0] * 4);
+    memcpy(depth, hp + o_st + 16 + (size_t)h->stereo_kp * 4, (size_t)cnt[0] * 4);
+    if (tm) {   // {upload, extract kernels, stereo kernels, result copies}
+        HIPCHK(hipEventElapsedTime(&h->call_ms[0], h->call_ev[0], h->call_ev[1]));
+        HIPCHK(hipEventElapsedTime(&h->call_ms[1], h->call_ev[1], h->call_ev[2]));
+        HIPCHK(hipEventElapsedTime(&h->call_ms[3], h->call_ev[2], h->call_ev[4]));
+        HIPCHK(hipEventElapsedTime(&h->call_ms[2], h->call_ev[4], h->call_ev[5]));
+        h->call_ms[4] = 0.f;
     }
     return nm;
 }

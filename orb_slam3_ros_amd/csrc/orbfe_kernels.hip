@@ -968,7 +968,7 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
                                               ((uint32_t)sc << 24);
             nsurv += __popcll(m);
         }
-        if (nsurv > 0) break;
+        if (nsurv > 0 || ablate == 4) break;
         WAVE_SYNC();   // the fallback attempt clears the score map
     }   // attempt
     if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = stop ? 0 : nsurv;

@@ -131,24 +131,43 @@ __device__ __forceinline__ uint32_t bitonic_keep(uint32_t a, uint32_t c, int i, 
     const bool keep_min = ((i & j) == 0) == ((i & k) == 0);   // lower of the pair == ascending
     return keep_min ? min(a, c) : max(a, c);
 }
+// The band index of k_sbp_band (single-camera local-map search): keypoints in (octave, 8-row band of
+// y) buckets, index order inside a bucket; bucket = octave * NB + min(max(floor(y / 8), 0), NB - 1),
+// octaves outside [0, nlev) in no bucket. bstart == nullptr: not built.
+#define MT_BAND_ROWS 8
+struct BandGrid {
+    int* bstart;   // nlev * NB + 1 bucket starts
+    int* bidx;     // keypoint indices sorted by (bucket, index)
+    int NB, nlev;
+};
+__device__ __forceinline__ int mt_band_of(float y, int NB) {
+    return min(max((int)floorf(y * (1.0f / MT_BAND_ROWS)), 0), NB - 1);
+}
 __global__ __launch_bounds__(1024) void k_mt_grid(const OrbKeyPoint* keys, int n, int nleft, float minx, float miny,
                                                   float invw, float invh, int* cstart, int* cidx, int gstride_c,
-                                                  int gstride_i, int ngrids, SbpInit ia) {
+                                                  int gstride_i, int ngrids, SbpInit ia, BandGrid band) {
     __shared__ uint32_t s_k[MT_GRID_MAXN];
     const int gi = blockIdx.x;
     const int tid = threadIdx.x;
-    if (gi >= ngrids) {
-        sbp_init_elem(ia, (gi - ngrids) * blockDim.x + tid);
+    const int nband = band.bstart ? 1 : 0;
+    if (gi >= ngrids + nband) {
+        sbp_init_elem(ia, (gi - ngrids - nband) * blockDim.x + tid);
         return;
     }
+    const bool is_band = gi == ngrids;
     // block 0: full grid; block g >= 1: keypoints with octave in [g-2, g-1] (level-(g-1) candidates)
     const int lvlo = gi == 0 ? INT_MIN : gi - 2, lvhi = gi == 0 ? INT_MAX : gi - 1;
-    cstart += (size_t)gi * gstride_c;
-    cidx += (size_t)gi * gstride_i;
+    if (is_band) {
+        cstart = band.bstart;
+        cidx = band.bidx;
+    } else {
+        cstart += (size_t)gi * gstride_c;
+        cidx += (size_t)gi * gstride_i;
+    }
     int P = 64;
     while (P < n) P <<= 1;
     const int R = (P + 1023) >> 10;
-    const int ncells = nleft >= 0 ? 2 * MT_NCELL : MT_NCELL;
+    const int ncells = is_band ? band.nlev * band.NB : nleft >= 0 ? 2 * MT_NCELL : MT_NCELL;
     uint32_t v[MT_GRID_R];
 #pragma unroll
     for (int r = 0; r < MT_GRID_R; r++) {
@@ -156,12 +175,16 @@ __global__ __launch_bounds__(1024) void k_mt_grid(const OrbKeyPoint* keys, int n
         uint32_t key = 0xFFFFFFFFu;
         if (r < R && i < n) {
             const OrbKeyPoint kp = keys[i];
-            const int px = (int)roundf((kp.x - minx) * invw);
-            const int py = (int)roundf((kp.y - miny) * invh);
             uint32_t cell = (uint32_t)ncells;   // outside the grid: never a candidate (PosInGrid false)
-            if (!(px < 0 || px >= ORBFE_GRID_COLS || py < 0 || py >= ORBFE_GRID_ROWS) && kp.octave >= lvlo &&
-                kp.octave <= lvhi)
-                cell = (uint32_t)(px * ORBFE_GRID_ROWS + py + (nleft >= 0 && i >= nleft ? MT_NCELL : 0));
+            if (is_band) {
+                if (kp.octave >= 0 && kp.octave < band.nlev) cell = (uint32_t)(kp.octave * band.NB + mt_band_of(kp.y, band.NB));
+            } else {
+                const int px = (int)roundf((kp.x - minx) * invw);
+                const int py = (int)roundf((kp.y - miny) * invh);
+                if (!(px < 0 || px >= ORBFE_GRID_COLS || py < 0 || py >= ORBFE_GRID_ROWS) && kp.octave >= lvlo &&
+                    kp.octave <= lvhi)
+                    cell = (uint32_t)(px * ORBFE_GRID_ROWS + py + (nleft >= 0 && i >= nleft ? MT_NCELL : 0));
+            }
             key = (cell << 16) | (uint32_t)i;
         }
         v[r] = key;
@@ -494,6 +517,133 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wq(FrameDev fr, const orbf
             }
         }
         if (sl == 0 && qv) {
+            pass_publish(io, q, result, obs);
+            if (result != prev) {
+                assign[q] = result;
+                atomicAdd(changed, 1);
+            }
+        }
+    }
+}
+
+// SearchByProjection(Frame&, vector<MapPoint*>, ...) (ORBmatcher.cc:43-213) for a single-camera frame
+// of at most MT_BAND_MAXN keypoints, every th: the frame lives in LDS in (octave, 8-row band)
+// order (BandGrid), so a query's candidates are two contiguous LDS runs (octaves lvl - 1 and lvl,
+// the bands its y window touches, one band of margin each side) that the 16 lanes of its DPP row
+// read in order: no grid walk, no per-candidate search. GetFeaturesInArea's candidates are exactly the
+// in-grid keypoints of those octaves with |dx| < r and |dy| < r (a keypoint inside the box lies in a
+// cell of the reference's window: round() of a value inside [floor(lo), ceil(hi)]), and its
+// enumeration order (cell ix, iy, then index, Frame.cc:691-719) is the rank (cell << 13 | index)
+// carried in each candidate's key, so the two smallest (dist, rank) keys are the reference's
+// best / second best whatever order the lanes visit them in. Four queries per wave, one per row.
+#define MT_BAND_MAXN 2048
+#define MT_BNT 1024
+__global__ __launch_bounds__(MT_BNT) void k_sbp_band(FrameDev fr, BandGrid bg, const orbfe_map_point* mps, int nq,
+                                                     float th, int bFar, float thFar, float nnratio,
+                                                     const int* blocked0, const int* first, int* assign, int* changed,
+                                                     PassIO io) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t mt_sm[];
+    if (pass_gated(io)) return;
+    pass_fill(io);
+    const int n = fr.n;
+    const int nbk = bg.nlev * bg.NB;
+    float4* s_kp = (float4*)mt_sm;                 // {x, y, rank bits, uR} per band position
+    uint4* s_desc = (uint4*)(s_kp + n);            // 2 x uint4 per band position
+    int* s_gate = (int*)(s_desc + 2 * n);          // -1: blocked initially, else first[] (MT_INF: free)
+    int* s_bs = s_gate + n;                        // bucket starts [nbk + 1]
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, grp = lane >> 4, sl = lane & 15;
+    for (int p = tid; p < n; p += MT_BNT) {
+        const int idx = bg.bidx[p];
+        const OrbKeyPoint kp = fr.keys[idx];
+        const int px = (int)roundf((kp.x - fr.minx) * fr.invw);   // PosInGrid (Frame.cc:725-735)
+        const int py = (int)roundf((kp.y - fr.miny) * fr.invh);
+        const bool in_grid = !(px < 0 || px >= ORBFE_GRID_COLS || py < 0 || py >= ORBFE_GRID_ROWS);
+        const uint32_t rank = ((uint32_t)(px * ORBFE_GRID_ROWS + py) << 13) | (uint32_t)idx;
+        s_kp[p] = make_float4(in_grid ? kp.x : __builtin_nanf(""), kp.y, __uint_as_float(rank),
+                              fr.uright ? fr.uright[idx] : -1.f);
+        const uint4* d = (const uint4*)(fr.desc + 8 * idx);
+        s_desc[2 * p] = d[0];
+        s_desc[2 * p + 1] = d[1];
+        s_gate[p] = blocked0[idx] ? -1 : first[idx];
+    }
+    for (int b = tid; b <= nbk; b += MT_BNT) s_bs[b] = bg.bstart[b];
+    SYNC();
+    constexpr int WPB = MT_BNT / 64;
+    for (int q0 = (blockIdx.x * WPB + wave) * MT_QPW; q0 < nq; q0 += gridDim.x * WPB * MT_QPW) {
+        const int q = q0 + grp;
+        int prev = -1, obs = 0, lvl = 0, s1 = 0, n1 = 0, s2 = 0, n2 = 0;
+        float R = 0.f, x = 0.f, y = 0.f, xr = 0.f;
+        uint32_t qd[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        if (q < nq) {
+            const orbfe_map_point& mp = mps[q];
+            prev = assign[q];
+            obs = mp.observations;
+            if ((mp.flags & ORBFE_MP_IN_VIEW) && !(bFar && mp.depth > thFar) && !(mp.flags & ORBFE_MP_BAD) &&
+                mp.scale_level >= 0 && mp.scale_level < fr.nlevels) {
+                lvl = mp.scale_level;
+                float r = mp.view_cos > 0.998 ? 2.5f : 4.0f;   // RadiusByViewingCos (ORBmatcher.cc:215-221)
+                if (th != 1.0f) r *= th;
+                R = r * fr.scale[lvl];
+                x = mp.proj_x;
+                y = mp.proj_y;
+                xr = mp.proj_xr;
+                memcpy(qd, mp.desc, 32);
+                // the bands of (y - R, y + R), one band of margin for the rounding of y -+ R
+                const int b0 = max(mt_band_of(y - R, bg.NB) - 1, 0), b1 = min(mt_band_of(y + R, bg.NB) + 1, bg.NB - 1);
+                if (lvl < bg.nlev) {
+                    s2 = s_bs[lvl * bg.NB + b0];
+                    n2 = s_bs[lvl * bg.NB + b1 + 1] - s2;
+                    if (lvl >= 1) {
+                        s1 = s_bs[(lvl - 1) * bg.NB + b0];
+                        n1 = s_bs[(lvl - 1) * bg.NB + b1 + 1] - s1;
+                    }
+                }
+            }
+        }
+        const int tot = n1 + n2;
+        unsigned long long b1k = ~0ull, b2k = ~0ull;
+        unsigned nwin = 0, npair = 0;
+        const int totmax = mt_rows_max(tot);
+        for (int j0 = 0; j0 < totmax; j0 += 16) {
+            const int j = j0 + sl;
+            if (j < tot) {
+                const bool lo = j < n1;
+                const int p = lo ? s1 + j : s2 + (j - n1);
+                const int oct = lo ? lvl - 1 : lvl;
+                const float4 k4 = s_kp[p];
+                bool ok = fabsf(k4.x - x) < R && fabsf(k4.y - y) < R;
+                if (ok) {
+                    nwin++;
+                    ok = s_gate[p] >= q;
+                    if (ok && k4.w > 0) ok = !(fabsf(xr - k4.w) > R);
+                }
+                if (ok) {
+                    npair++;
+                    const uint4 d0 = s_desc[2 * p], d1 = s_desc[2 * p + 1];
+                    const int dist = __popc(qd[0] ^ d0.x) + __popc(qd[1] ^ d0.y) + __popc(qd[2] ^ d0.z) +
+                                     __popc(qd[3] ^ d0.w) + __popc(qd[4] ^ d1.x) + __popc(qd[5] ^ d1.y) +
+                                     __popc(qd[6] ^ d1.z) + __popc(qd[7] ^ d1.w);
+                    const unsigned long long k = ((unsigned long long)dist << 40) |
+                                                 ((unsigned long long)__float_as_uint(k4.z) << 4) | (unsigned)oct;
+                    if (k < b1k) { b2k = b1k; b1k = k; }
+                    else if (k < b2k) b2k = k;
+                }
+            }
+        }
+        pass_stats(io, nwin, npair);
+        const unsigned long long m1 = mt_row_min64(b1k);
+        const unsigned long long m2 = mt_row_min64(b1k == m1 ? b2k : b1k);
+        int result = -1;
+        if (m1 != ~0ull) {
+            const int bestDist = (int)(m1 >> 40), bestLevel = (int)(m1 & 15);
+            const int bestDist2 = m2 != ~0ull ? (int)(m2 >> 40) : 256;
+            const int bestLevel2 = m2 != ~0ull ? (int)(m2 & 15) : -1;
+            if (bestDist <= MT_TH_HIGH) {
+                if (!(bestLevel == bestLevel2 && bestDist > nnratio * bestDist2))
+                    result = (int)((m1 >> 4) & 0x1FFFu);   // the keypoint index carried in the rank
+            }
+        }
+        if (sl == 0 && q < nq) {
             pass_publish(io, q, result, obs);
             if (result != prev) {
                 assign[q] = result;
@@ -1407,6 +1557,16 @@ struct FramePlan {
         (void)want_grid;
     }
     int ngrids = 1;
+    // k_sbp_band's (octave, band) index, built by the grid launch when planned (plan_band)
+    bool band = false;
+    int band_nb = 0;
+    size_t bstart = 0, bidx = 0;
+    void plan_band(Plan& p) {
+        band = true;
+        band_nb = std::min(std::max((int)std::floor(F->max_y * (1.0f / MT_BAND_ROWS)) + 2, 1), 4096);
+        bstart = p.scratch((size_t)(F->nlevels * band_nb + 1) * 4);
+        bidx = p.scratch((size_t)std::max(F->n, 1) * 4);
+    }
     int cells() const { return (two ? 2 : 1) * MT_NCELL; }
     void plan_grid(Plan& p, int grids) {   // grids = 1 (full) + level-restricted grids
         ngrids = grids;
@@ -1453,9 +1613,11 @@ struct FramePlan {
         memset(&none, 0, sizeof(none));
         const SbpInit& ia = init ? *init : none;
         const int nib = (sbp_init_extent(ia) + 1023) / 1024;
-        hipLaunchKernelGGL(k_mt_grid, dim3(ngrids + nib), dim3(1024), 0, s, v.keys, v.n, v.nleft,
+        BandGrid bg{nullptr, nullptr, 0, 0};
+        if (band) bg = BandGrid{ms_ptr<int>(bstart), ms_ptr<int>(bidx), band_nb, F->nlevels};
+        hipLaunchKernelGGL(k_mt_grid, dim3(ngrids + (band ? 1 : 0) + nib), dim3(1024), 0, s, v.keys, v.n, v.nleft,
                            v.minx, v.miny, v.invw, v.invh, (int*)v.cstart, (int*)v.cidx, v.gstride_c, v.gstride_i,
-                           ngrids, ia);
+                           ngrids, ia, bg);
     }
 };
 
@@ -1588,6 +1750,12 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     const size_t o_mvp = dev ? 0 : p.upload(mvp, (size_t)n * 4);
     const size_t o_b0d = dev ? p.scratch((size_t)n * 4) : 0;
     fp.plan_grid(p, mode == 0 ? F->nlevels + 1 : 1);
+    // the single-camera local-map search of a frame that fits in LDS: the band kernel
+    bool use_band = mode == 0 && W == 1 && n <= MT_BAND_MAXN;
+    if (use_band) {
+        fp.plan_band(p);
+        if ((size_t)F->nlevels * fp.band_nb >= 65535) use_band = fp.band = false;   // 16-bit bucket keys
+    }
     const size_t o_track = fin ? p.scratch((size_t)nq * sizeof(orbfe_map_point)) : 0;
     const size_t o_ntm = fin ? p.scratch(16) : 0;
     const size_t o_ruv = (two && mode == 1 && !dev) ? p.upload(right_uv, (size_t)nq * 8) : 0;
@@ -1675,7 +1843,14 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
                 PassIO io{pass ? changed + pass - 1 : nullptr, fb[(pass + 1) % 3], fb[(pass + 2) % 3], n,
                           mode == 2 ? 0 : 1, stats};
                 const int* fcur = fb[pass % 3];
-                if (mode == 0 && th >= MT_WAVE_TH) {
+                if (use_band) {
+                    const int qpb = (MT_BNT / 64) * MT_QPW;
+                    const int nb = std::min((nq + qpb - 1) / qpb, 512);
+                    const BandGrid bg{ms_ptr<int>(fp.bstart), ms_ptr<int>(fp.bidx), fp.band_nb, F->nlevels};
+                    const size_t lds = ((size_t)n * 52 + (size_t)(F->nlevels * fp.band_nb + 1) * 4 + 15) & ~(size_t)15;
+                    hipLaunchKernelGGL(k_sbp_band, dim3(nb), dim3(MT_BNT), lds, s, fr, bg, (const orbfe_map_point*)q, nq,
+                                       th, a0, thFar, nnratio, b0, fcur, assign, changed + pass, io);
+                } else if (mode == 0 && th >= MT_WAVE_TH) {
                     const int qpb = (MT_WNT / 64) * MT_QPW;   // queries per block and round
                     const int nb = std::min((nq + qpb - 1) / qpb, 512);
                     const size_t lds = (MT_WNT / 64) * 64 * sizeof(int2) + (staged ? (size_t)n * 56 : 0);

@@ -144,3 +144,34 @@ def compute_stereo_matches(left: ORBextractor, right: ORBextractor, bf: float, f
                                         dp.ctypes.data)
     _lib.check(rc, "orbfe_stereo_match")
     return ur[:n_left], dp[:n_left], rc
+
+
+def frame_stereo(left: ORBextractor, right: ORBextractor, imLeft, imRight, bf: float, fx: float):
+    """Frame::Frame(stereo) (Frame.cc:101-141) in one library call: ExtractORB on both images (the
+    reference's two per-frame threads, :122-125) as one two-image batch on `left`, then
+    ComputeStereoMatches (:141). Returns ((monoLeft, kpsLeft, descLeft), (monoRight, kpsRight,
+    descRight), mvuRight, mvDepth, n_matches_before_cut)."""
+    L = np.ascontiguousarray(np.asarray(imLeft))
+    R = np.ascontiguousarray(np.asarray(imRight))
+    if L.size == 0 or R.size == 0:
+        raise _lib.OrbfeError("Frame(stereo) needs two non-empty images")
+    for im in (L, R):
+        if im.dtype != np.uint8 or im.ndim != 2:
+            raise _lib.OrbfeError("ORBextractor expects a single-channel uint8 image (CV_8UC1)")
+    if L.shape != R.shape:
+        raise _lib.OrbfeError("left and right images differ in size")
+    h, w = L.shape
+    cap = left.capacity(w, h)
+    kl, kr = np.zeros(cap, KEYPOINT_DTYPE), np.zeros(cap, KEYPOINT_DTYPE)
+    dl, dr = np.zeros((cap, 32), np.uint8), np.zeros((cap, 32), np.uint8)
+    ur, dp = np.zeros(cap, np.float32), np.zeros(cap, np.float32)
+    nl, nr, ml, mr = (ctypes.c_int() for _ in range(4))
+    rc = _lib.load().orbfe_frame_stereo(left.handle, right.handle, L.ctypes.data, R.ctypes.data, w, h, w,
+                                        float(bf), float(fx), kl.ctypes.data, dl.ctypes.data, cap,
+                                        ctypes.byref(nl), ctypes.byref(ml), kr.ctypes.data, dr.ctypes.data, cap,
+                                        ctypes.byref(nr), ctypes.byref(mr), ur.ctypes.data, dp.ctypes.data)
+    _lib.check(rc, "orbfe_frame_stereo")
+    left._last_shape = (h, w)
+    n, m = nl.value, nr.value
+    return ((ml.value, kl[:n].copy(), dl[:n].copy()), (mr.value, kr[:m].copy(), dr[:m].copy()),
+            ur[:n].copy(), dp[:n].copy(), rc)

@@ -425,10 +425,25 @@ class ORBmatcher:
         m2 = _i32(np.ascontiguousarray(mp2, np.int32), KF2.N, "mp2")
         e = np.ascontiguousarray(ep, np.float32).reshape(2)
         out = np.full(KF1.N, -1, np.int32)
-        cb = _lib.EPIPOLAR_FN(lambda ctx, i1, i2: 1 if epipolar(i1, i2) else 0)
+        # ctypes swallows an exception raised inside a callback (prints it, returns 0): record the
+        # first one and re-raise it after the call, so a failing predicate cannot change the matches
+        err = []
+
+        def pred(ctx, i1, i2):
+            if err:
+                return 0
+            try:
+                return 1 if epipolar(i1, i2) else 0
+            except BaseException as ex:  # noqa: BLE001 - re-raised below
+                err.append(ex)
+                return 0
+
+        cb = _lib.EPIPOLAR_FN(pred)
         n = _lib.check(self._lib.orbfe_search_for_triangulation_epi(
             KF1.ref(), m1.ctypes.data, fv1.ref(), KF2.ref(), m2.ctypes.data, fv2.ref(), e.ctypes.data,
             int(bOnlyStereo), int(self.mbCheckOrientation), cb, None, out.ctypes.data), "SearchForTriangulation")
+        if err:
+            raise err[0]
         return n, out
 
     # Fuse(pKF, vpMapPoints, th) (:1148-1337) / Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (:1339-1455)

@@ -82,3 +82,29 @@ def synth_stereo(seed: int, w: int = 752, h: int = 480, max_disp: float = 48.0,
 def synth_batch(seed: int, n: int, w: int = 752, h: int = 480) -> np.ndarray:
     """n independent images, shape (n, h, w)."""
     return np.stack([synth_image(seed + i, w, h) for i in range(n)])
+
+
+# The stereo sequence's geometry: a fronto-parallel textured plane at depth Z = bf / SEQ_DISP seen by
+# a rectified pinhole stereo rig translating along +x by SEQ_SHIFT * Z / fx per frame, so the image
+# content moves SEQ_SHIFT px left per frame and every scene point has disparity SEQ_DISP: the frames,
+# their stereo depths and a constant-velocity motion model agree exactly (Tracking's
+# TrackWithMotionModel / SearchLocalPoints find their points where the projection puts them).
+SEQ_DISP = 16
+SEQ_SHIFT = 2
+
+
+def synth_stereo_sequence(seed: int, n: int, w: int = 752, h: int = 480, shift: int = SEQ_SHIFT,
+                          disp: int = SEQ_DISP, noise: float = 3.0) -> list[tuple[np.ndarray, np.ndarray]]:
+    """n seeded rectified stereo pairs of a camera moving along x over one planar scene: frame k's
+    left image is scene columns [k * shift, k * shift + w), its right image columns [k * shift +
+    disp, ...) (disparity `disp` everywhere), each with its own sensor noise."""
+    rng = np.random.default_rng(seed)
+    scene = _scene(rng, h, w + (n - 1) * shift + disp)
+    to_u8 = lambda a: np.clip(np.rint(a), 0, 255).astype(np.uint8)   # noqa: E731
+    out = []
+    for k in range(n):
+        c = k * shift
+        left = scene[:, c:c + w] + rng.normal(0.0, noise, (h, w))
+        right = scene[:, c + disp:c + disp + w] + rng.normal(0.0, noise, (h, w))
+        out.append((np.ascontiguousarray(to_u8(left)), np.ascontiguousarray(to_u8(right))))
+    return out

@@ -7,7 +7,8 @@
 //   ORBmatcher(0.8).SearchByProjection(F, vpMapPoints, th) through a MapPoint* <-> handle table
 //                                                                                     ORBmatcher.cc:43-213
 // usage: capi_frontend <job.bin> <out.bin>
-//        capi_frontend --latency <frames> <job.bin>   (prints one JSON line: per-frame drop-in latency)
+//        capi_frontend --latency <frames> <seq.bin>   (one JSON line: per-frame drop-in latency, both forms)
+//        capi_frontend --tracking <frames> <seq.bin> [out.bin]   (one JSON line: a Tracking frame, split)
 //   job: int32 w, h, nfeatures, n_mps, th_x100; float bf, fx; u8 left[w*h], u8 right[w*h]
 //   out: per side {int32 monoIndex, n; keypoints n x 28 B; descriptors n x 32 B}; int32 levels;
 //        float scale[levels]; stereo {int32 nmatch; float uR[nL]; float depth[nL]};
@@ -25,6 +26,7 @@
 #include <vector>
 
 #include "orbfe.h"
+#include "tracking_loop.h"
 
 namespace {
 
@@ -180,101 +182,226 @@ double median(std::vector<double> v) {
     return v.empty() ? 0.0 : v[v.size() / 2];
 }
 
-// The drop-in path at batch 1, exactly as Tracking builds a stereo Frame (Frame.cc:122-141): the left
-// and right ORBextractor::operator() on two std::threads started per frame (ExtractORB), joined,
-// then ComputeStereoMatches (orbfe_stereo_match). Host images in, host keypoints / descriptors /
-// uR / depth out. Per frame: wall time without event timing (frame_ms), then wall time with the
-// library's call timing (HIP events on each handle's stream: upload, kernels, result copies) for the
-// split (frame_ms_timed); host = timed wall - the device-side critical path.
-int latency(int frames, const char* job) {
+// Sequence job (bench.py dropin leg): int32 magic 'ORBS', w, h, nfeatures, npairs, window; float fx,
+// fy, cx, cy, bf, tx; then npairs x (u8 left[w*h], u8 right[w*h]) of synth_stereo_sequence.
+struct SeqJob {
+    int w = 0, h = 0, nf = 0, npairs = 0, window = 6;
+    trk::Cam cam{};
+    std::vector<uint8_t> px;
+    const uint8_t* left(int k) const { return px.data() + (size_t)(k % npairs) * 2 * w * h; }
+    const uint8_t* right(int k) const { return left(k) + (size_t)w * h; }
+};
+
+SeqJob read_seq(const char* job) {
     FILE* f = fopen(job, "rb");
     if (!f) throw std::runtime_error("cannot open job");
-    int32_t hdr[5];
-    float cam[2];
-    if (fread(hdr, 4, 5, f) != 5 || fread(cam, 4, 2, f) != 2) throw std::runtime_error("short job header");
-    const int w = hdr[0], h = hdr[1], nf = hdr[2];
-    std::vector<uint8_t> L((size_t)w * h), R((size_t)w * h);
-    if (fread(L.data(), 1, L.size(), f) != L.size() || fread(R.data(), 1, R.size(), f) != R.size())
-        throw std::runtime_error("short job images");
+    int32_t hdr[6];
+    float c[6];
+    if (fread(hdr, 4, 6, f) != 6 || fread(c, 4, 6, f) != 6) throw std::runtime_error("short job header");
+    if (hdr[0] != 0x5342524f) throw std::runtime_error("not a sequence job");
+    SeqJob j;
+    j.w = hdr[1];
+    j.h = hdr[2];
+    j.nf = hdr[3];
+    j.npairs = hdr[4];
+    j.window = hdr[5];
+    j.cam = trk::Cam{c[0], c[1], c[2], c[3], c[4], c[5]};
+    j.px.resize((size_t)j.npairs * 2 * j.w * j.h);
+    if (j.npairs <= 0 || fread(j.px.data(), 1, j.px.size(), f) != j.px.size()) throw std::runtime_error("short job images");
     fclose(f);
+    return j;
+}
+
+// The drop-in path at batch 1, a stereo Frame at a time over the job's sequence (frame k = pair k mod
+// npairs), in the two forms the shim can take:
+//   frame call: orbfe_frame_stereo, Frame::Frame(stereo) in one library call (Frame.cc:101-141);
+//   threads:    exactly as Tracking builds a stereo Frame (Frame.cc:122-141): the left and right
+//               ORBextractor::operator() on two std::threads started per frame (ExtractORB), joined,
+//               then ComputeStereoMatches (orbfe_stereo_match).
+// Host images in, host keypoints / descriptors / uR / depth out. Per form: wall time per frame without
+// event timing (medians), then a second pass with the library's call timing (HIP events on the
+// stream: upload / kernels / result copies) for the split; host = timed wall - the device-side path.
+int latency(int frames, const char* job) {
+    const SeqJob J = read_seq(job);
+    const int w = J.w, h = J.h, nf = J.nf;
     ORBextractor el(nf, 1.2f, 8, 20, 7), er(nf, 1.2f, 8, 20, 7);
-    // two runs of `frames` frames: first as an application runs (no event timing), giving frame_ms;
-    // then with the per-call HIP-event timing on (events around the upload / kernels / copies), giving
-    // the split and frame_ms_timed
-    std::vector<double> wall_plain, wall, ext, st, up, ker, cp, sker, scp, host;
-    int nkp = 0, nst = 0;
+    const int cap = orbfe_extractor_capacity(el.handle(), w, h);
+    check(cap, "capacity");
     const int warm = 5;
-    for (int it = 0; it < 2 * (warm + frames); it++) {
-        const bool timed = it >= warm + frames;
-        if (it == warm + frames) {
-            check(orbfe_set_stage_timing(el.handle(), 1), "timing");
-            check(orbfe_set_stage_timing(er.handle(), 1), "timing");
+    std::string out = "{";
+    for (int form = 0; form < 2; form++) {   // 0 = frame call, 1 = threads
+        std::vector<double> wall_plain, wall, ext, st, up, ker, cp, sker, scp, host;
+        int nkp = 0, nst = 0;
+        for (int it = 0; it < 2 * (warm + frames); it++) {
+            const bool timed = it >= warm + frames;
+            if (it == 0 || it == warm + frames) {
+                check(orbfe_set_stage_timing(el.handle(), timed), "timing");
+                check(orbfe_set_stage_timing(er.handle(), timed), "timing");
+            }
+            const int k = timed ? it - (warm + frames) : it;
+            const uint8_t* L = J.left(k);
+            const uint8_t* R = J.right(k);
+            std::vector<KeyPoint> kl, kr;
+            std::vector<uint8_t> dl, dr;
+            std::vector<float> ur, dp;
+            double tl = 0, tr = 0;
+            int ns = 0;
+            const auto t0 = std::chrono::steady_clock::now();
+            auto t1 = t0;
+            if (form == 0) {
+                kl.resize(cap);
+                kr.resize(cap);
+                dl.resize((size_t)cap * 32);
+                dr.resize((size_t)cap * 32);
+                ur.resize(cap);
+                dp.resize(cap);
+                int nl = 0, nr = 0, ml = 0, mr = 0;
+                ns = orbfe_frame_stereo(el.handle(), er.handle(), L, R, w, h, w, J.cam.bf, J.cam.fx,
+                                        reinterpret_cast<orbfe_keypoint*>(kl.data()), dl.data(), cap, &nl, &ml,
+                                        reinterpret_cast<orbfe_keypoint*>(kr.data()), dr.data(), cap, &nr, &mr,
+                                        ur.data(), dp.data());
+                check(ns, "frame_stereo");
+                kl.resize(nl);
+                kr.resize(nr);
+                t1 = std::chrono::steady_clock::now();
+            } else {
+                const int lap[2] = {0, 0};
+                std::thread thL([&] {
+                    const auto a = std::chrono::steady_clock::now();
+                    el(L, w, h, w, kl, dl, lap);
+                    tl = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+                });
+                std::thread thR([&] {
+                    const auto a = std::chrono::steady_clock::now();
+                    er(R, w, h, w, kr, dr, lap);
+                    tr = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+                });
+                thL.join();
+                thR.join();
+                t1 = std::chrono::steady_clock::now();
+                ur.assign(kl.size(), -1.f);
+                dp.assign(kl.size(), -1.f);
+                ns = orbfe_stereo_match(el.handle(), er.handle(), J.cam.bf, J.cam.fx, ur.data(), dp.data());
+                check(ns, "stereo_match");
+            }
+            const auto t2 = std::chrono::steady_clock::now();
+            if (k < warm) continue;
+            if (!timed) {
+                wall_plain.push_back(std::chrono::duration<double, std::milli>(t2 - t0).count());
+                continue;
+            }
+            float a[5], b[5];
+            check(orbfe_get_call_timing(el.handle(), a), "call_timing");
+            check(orbfe_get_call_timing(er.handle(), b), "call_timing");
+            const double fw = std::chrono::duration<double, std::milli>(t2 - t0).count();
+            wall.push_back(fw);
+            if (form == 0) {   // {upload, extraction kernels, result copies, stereo kernels}
+                ext.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+                st.push_back(0.0);
+                up.push_back(a[0]);
+                ker.push_back(a[1]);
+                cp.push_back(a[2]);
+                sker.push_back(a[3]);
+                scp.push_back(0.0);
+                host.push_back(fw - (a[0] + a[1] + a[2] + a[3]));
+            } else {
+                const bool lslow = tl >= tr;   // the extraction's critical side is the slower thread's
+                const float* c = lslow ? a : b;
+                ext.push_back(std::max(tl, tr));
+                st.push_back(std::chrono::duration<double, std::milli>(t2 - t1).count());
+                up.push_back(c[0]);
+                ker.push_back(c[1]);
+                cp.push_back(c[2]);
+                sker.push_back(a[3]);
+                scp.push_back(a[4]);
+                host.push_back(fw - (c[0] + c[1] + c[2] + a[3] + a[4]));
+            }
+            nkp = (int)(kl.size() + kr.size());
+            nst = ns;
         }
-        const int k = timed ? it - (warm + frames) : it;
-        std::vector<KeyPoint> kl, kr;
-        std::vector<uint8_t> dl, dr;
-        int ml = 0, mr = 0;
-        double tl = 0, tr = 0;
-        const int lap[2] = {0, 0};
-        const auto t0 = std::chrono::steady_clock::now();
-        std::thread thL([&] {
-            const auto a = std::chrono::steady_clock::now();
-            ml = el(L.data(), w, h, w, kl, dl, lap);
-            tl = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
-        });
-        std::thread thR([&] {
-            const auto a = std::chrono::steady_clock::now();
-            mr = er(R.data(), w, h, w, kr, dr, lap);
-            tr = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
-        });
-        thL.join();
-        thR.join();
-        const auto t1 = std::chrono::steady_clock::now();
-        std::vector<float> ur(kl.size(), -1.f), dp(kl.size(), -1.f);
-        const int ns = orbfe_stereo_match(el.handle(), er.handle(), cam[0], cam[1], ur.data(), dp.data());
-        check(ns, "stereo_match");
-        const auto t2 = std::chrono::steady_clock::now();
-        (void)ml;
-        (void)mr;
-        if (k < warm) continue;
-        if (!timed) {
-            wall_plain.push_back(std::chrono::duration<double, std::milli>(t2 - t0).count());
-            continue;
-        }
-        float a[5], b[5];
-        check(orbfe_get_call_timing(el.handle(), a), "call_timing");
-        check(orbfe_get_call_timing(er.handle(), b), "call_timing");
-        const double fw = std::chrono::duration<double, std::milli>(t2 - t0).count();
-        const double fs = std::chrono::duration<double, std::milli>(t2 - t1).count();
-        // the extraction's critical side is the slower thread's
-        const bool lslow = tl >= tr;
-        const float* c = lslow ? a : b;
-        wall.push_back(fw);
-        ext.push_back(std::max(tl, tr));
-        st.push_back(fs);
-        up.push_back(c[0]);
-        ker.push_back(c[1]);
-        cp.push_back(c[2]);
-        sker.push_back(a[3]);
-        scp.push_back(a[4]);
-        host.push_back(fw - (c[0] + c[1] + c[2] + a[3] + a[4]));
-        nkp = (int)(kl.size() + kr.size());
-        nst = ns;
+        char buf[1024];
+        snprintf(buf, sizeof(buf),
+                 "%s\"%s\": {\"frame_ms\": %.4f, \"frame_ms_min\": %.4f, \"frame_ms_timed\": %.4f, "
+                 "\"extract_lr_ms\": %.4f, \"stereo_ms\": %.4f, \"keypoints_lr\": %d, \"stereo_matches\": %d, "
+                 "\"split_ms\": {\"upload\": %.4f, \"extract_kernels\": %.4f, \"result_copies\": %.4f, "
+                 "\"stereo_kernels\": %.4f, \"stereo_copies\": %.4f, \"host\": %.4f}}",
+                 form ? ", " : "", form ? "threads" : "frame_call", median(wall_plain),
+                 *std::min_element(wall_plain.begin(), wall_plain.end()), median(wall), median(ext), median(st), nkp,
+                 nst, median(up), median(ker), median(cp), median(sker), median(scp), median(host));
+        out += buf;
     }
-    printf("{\"frames\": %d, \"width\": %d, \"height\": %d, \"nfeatures\": %d, \"keypoints_lr\": %d, "
-           "\"stereo_matches\": %d, \"frame_ms\": %.4f, \"frame_ms_min\": %.4f, \"frame_ms_timed\": %.4f, "
-           "\"extract_lr_ms\": %.4f, "
-           "\"stereo_ms\": %.4f, \"split_ms\": {\"upload\": %.4f, \"extract_kernels\": %.4f, "
-           "\"extract_copies\": %.4f, \"stereo_kernels\": %.4f, \"stereo_copies\": %.4f, \"host\": %.4f}}\n",
-           frames, w, h, nf, nkp, nst, median(wall_plain), *std::min_element(wall_plain.begin(), wall_plain.end()),
-           median(wall), median(ext), median(st), median(up), median(ker), median(cp), median(sker), median(scp),
-           median(host));
+    char tail[256];
+    snprintf(tail, sizeof(tail), ", \"frames\": %d, \"distinct_pairs\": %d, \"width\": %d, \"height\": %d, \"nfeatures\": %d}",
+             frames, J.npairs, w, h, nf);
+    printf("%s%s\n", out.c_str(), tail);
     return 0;
 }
 
+// The library as trk::Tracker's Api (tests/native/tracking_loop.h)
+struct GpuApi {
+    ORBextractor& el;
+    ORBextractor& er;
+    int w, h, cap;
+    float bf, fx;
+    int frame(const uint8_t* L, const uint8_t* R, trk::FrameData& f) {
+        f.keys.resize(cap);
+        f.keys_r.resize(cap);
+        f.desc.resize((size_t)cap * 32);
+        f.desc_r.resize((size_t)cap * 32);
+        f.ur.resize(cap);
+        f.depth.resize(cap);
+        int nl = 0, nr = 0;
+        const int ns = orbfe_frame_stereo(el.handle(), er.handle(), L, R, w, h, w, bf, fx, f.keys.data(), f.desc.data(),
+                                          cap, &nl, &f.mono_l, f.keys_r.data(), f.desc_r.data(), cap, &nr, &f.mono_r,
+                                          f.ur.data(), f.depth.data());
+        check(ns, "frame_stereo");
+        f.keys.resize(nl);
+        f.desc.resize((size_t)nl * 32);
+        f.keys_r.resize(nr);
+        f.desc_r.resize((size_t)nr * 32);
+        f.ur.resize(nl);
+        f.depth.resize(nl);
+        f.nstereo = ns;
+        return ns;
+    }
+    int sbp_last(const orbfe_frame* F, int32_t* mvp, const int32_t* obs, const orbfe_proj_point* pts, int n, float th,
+                 int fwd, int bwd, int ori) {
+        const int r = orbfe_search_by_projection_lastframe(F, mvp, obs, pts, n, th, fwd, bwd, ori);
+        check(r, "search_by_projection_lastframe");
+        return r;
+    }
+    int local_points(const orbfe_frame* F, const orbfe_camera* c, const orbfe_map_point_3d* pts, int n, int32_t* mvp,
+                     const int32_t* obs, float th, int bFar, float thFar, float ratio, int32_t* ntm) {
+        const int r = orbfe_search_local_points(F, c, pts, n, mvp, obs, th, bFar, thFar, ratio, ntm);
+        check(r, "search_local_points");
+        return r;
+    }
+};
+
 }  // namespace
 
+int tracking(int frames, const char* job, const char* out_path) {
+    const SeqJob J = read_seq(job);
+    ORBextractor el(J.nf, 1.2f, 8, 20, 7), er(J.nf, 1.2f, 8, 20, 7);
+    const int cap = orbfe_extractor_capacity(el.handle(), J.w, J.h);
+    check(cap, "capacity");
+    GpuApi api{el, er, J.w, J.h, cap, J.cam.bf, J.cam.fx};
+    return trk::run_sequence(api, J.cam, J.w, J.h, el.mvScaleFactor, J.window, frames, J.npairs,
+                             [&](int k) { return J.left(k); }, [&](int k) { return J.right(k); }, out_path,
+                             "gpu: liborbfe.so C-ABI (orbfe_frame_stereo, orbfe_search_by_projection_lastframe, "
+                             "orbfe_search_local_points)");
+}
+
+
 int main(int argc, char** argv) {
+    if ((argc == 4 || argc == 5) && std::string(argv[1]) == "--tracking") {
+        try {
+            return tracking(atoi(argv[2]), argv[3], argc == 5 ? argv[4] : nullptr);
+        } catch (const std::exception& e) {
+            fprintf(stderr, "capi_frontend: %s\n", e.what());
+            return 1;
+        }
+    }
     if (argc == 4 && std::string(argv[1]) == "--latency") {
         try {
             return latency(atoi(argv[2]), argv[3]);

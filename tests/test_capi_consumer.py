@@ -126,3 +126,77 @@ def test_consumer_extract_golden(consumer, oracle_lib, tmp_path, th):
         np.testing.assert_array_equal(kp.view(np.uint8).reshape(-1, 28), g["euroc_stereo_l_kp"])
         np.testing.assert_array_equal(desc, g["euroc_stereo_l_desc"])
     _check_sbp(oracle_lib, sides, scale, ur, mps, nsbp, mvp, w, h, 48.0, th)
+
+
+@pytest.fixture(scope="module")
+def seq_job(tmp_path_factory):
+    import bench
+    p = tmp_path_factory.mktemp("seq") / "seq.bin"
+    return str(bench.write_sequence_job(str(p), 24, nf=1000, window=20))
+
+
+@pytest.fixture(scope="module")
+def tracking_cpu_bin(oracle_lib):
+    return B.build_tracking_cpu()
+
+
+def _tracking_records(buf):
+    """Per frame {n_left, n_right, n_stereo, sbp_th, sbp_matches, n_to_match, local_matches, mvp[n_left]}."""
+    a = np.frombuffer(buf, "<i4")
+    out, o = [], 0
+    while o < len(a):
+        rec = a[o:o + 7]
+        mvp = a[o + 7:o + 7 + rec[0]]
+        out.append((rec.copy(), mvp.copy()))
+        o += 7 + rec[0]
+    return out
+
+
+def test_tracking_cpu_sequence_deterministic(tracking_cpu_bin, seq_job, tmp_path):
+    """The CPU Tracking-frame loop (oracle restatement) is deterministic and does real work: the motion
+    model finds most last-frame points, SearchLocalPoints projects a growing local map."""
+    import json
+    outs = []
+    for i in range(2):
+        o = tmp_path / f"cpu{i}.out"
+        r = subprocess.run([tracking_cpu_bin, "12", seq_job, str(o)], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        outs.append(o.read_bytes())
+    assert outs[0] == outs[1]
+    recs = _tracking_records(outs[0])
+    assert len(recs) == 12
+    st = json.loads(r.stdout.strip().splitlines()[-1])
+    assert st["mean"]["last_frame_matches"] > 0.5 * st["mean"]["last_frame_points"] > 200
+    assert st["mean"]["local_to_match"] > 100 and st["mean"]["local_matches"] > 10
+    for rec, mvp in recs[1:]:
+        assert rec[4] == (mvp >= 0).sum() - rec[6] or rec[4] >= 20
+
+
+@pytest.mark.gpu
+def test_tracking_sequence_matches_cpu(consumer, tracking_cpu_bin, seq_job, tmp_path):
+    """A whole Tracking frame through the C-ABI (orbfe_frame_stereo, SearchByProjection(CurrentFrame,
+    LastFrame, 7), SearchLocalPoints) over a 24-frame sequence, against the same loop on the CPU
+    restatement: every frame's counts and mvpMapPoints identical (the loop feeds each frame's results
+    into the next frame's inputs, so one difference would propagate)."""
+    g, c = tmp_path / "gpu.out", tmp_path / "cpu.out"
+    r = subprocess.run([consumer, "--tracking", "24", seq_job, str(g)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    rc = subprocess.run([tracking_cpu_bin, "24", seq_job, str(c)], capture_output=True, text=True, timeout=600)
+    assert rc.returncode == 0, rc.stderr
+    gr, cr = _tracking_records(g.read_bytes()), _tracking_records(c.read_bytes())
+    assert len(gr) == len(cr) == 24
+    for k, ((ga, gm), (ca, cm)) in enumerate(zip(gr, cr)):
+        np.testing.assert_array_equal(ga, ca, err_msg=f"frame {k} counts")
+        np.testing.assert_array_equal(gm, cm, err_msg=f"frame {k} mvpMapPoints")
+
+
+@pytest.mark.gpu
+def test_latency_mode_sequence(consumer, seq_job):
+    """The drop-in latency harness over the sequence: both forms run and report the same work."""
+    import json
+    r = subprocess.run([consumer, "--latency", "10", seq_job], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["distinct_pairs"] == 24 and d["frames"] == 10
+    assert d["frame_call"]["keypoints_lr"] > 1800 and d["frame_call"]["stereo_matches"] > 300
+    assert d["frame_call"]["frame_ms"] > 0 and d["threads"]["frame_ms"] > 0

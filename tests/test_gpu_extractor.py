@@ -230,3 +230,44 @@ def test_host_call_sequence(gpu, oracle_lib):
         for _ in range(3):
             check(synth_image(next(seeds), 752, 480), (0, 1000))
     ext.close()
+
+
+@pytest.mark.parametrize("nfeat,size", [(1000, (752, 480)), (2000, (1241, 376))])
+def test_frame_stereo_entry(gpu, oracle_lib, nfeat, size):
+    """orbfe_frame_stereo (Frame::Frame(stereo), Frame.cc:101-141, in one call) against the oracle's
+    two extractions + ComputeStereoMatches: keypoints, descriptors, monoIndex, uR / depth bits and
+    the match count, over a seeded sequence of frames on the same handles (one handle reused after
+    a host orbfe_extract call in between, and the right image's pyramid read back from the left
+    handle's image 1)."""
+    from orb_slam3_ros_amd.extractor import ORBextractor, frame_stereo
+    from orb_slam3_ros_amd.synth import synth_stereo_sequence
+    w, h = size
+    bf, fx = 0.110078 * 458.654, 458.654
+    el, er = ORBextractor(nfeat, 1.2, 8, 20, 7), ORBextractor(nfeat, 1.2, 8, 20, 7)
+    seq = synth_stereo_sequence(11, 3, w, h)
+    for k, (left, right) in enumerate(seq):
+        if k == 1:   # a plain host call on the left handle in between
+            el(left, None, (0, 0))
+        (ml, kl, dl), (mr, kr, dr), ur, dp, nm = frame_stereo(el, er, left, right, bf, fx)
+        ol, orr = oracle_lib.OracleExtractor(nfeat, 1.2, 8, 20, 7), oracle_lib.OracleExtractor(nfeat, 1.2, 8, 20, 7)
+        oml, okl, odl = ol(left)
+        omr, okr, odr = orr(right)
+        assert (ml, mr) == (oml, omr)
+        assert np.array_equal(kl.view(np.uint8), okl.view(np.uint8)) and np.array_equal(dl, odl)
+        assert np.array_equal(kr.view(np.uint8), okr.view(np.uint8)) and np.array_equal(dr, odr)
+        our, odp, onm = oracle_lib.stereo_match(ol, orr, okl, odl, okr, odr, bf, fx)
+        assert nm == onm
+        assert np.array_equal(ur.view(np.uint32), our.view(np.uint32)), np.nonzero(ur != our)[0][:10]
+        assert np.array_equal(dp.view(np.uint32), odp.view(np.uint32))
+        assert (ur >= 0).sum() > 0.3 * len(kl)
+        for lv in (0, 3, 7):
+            assert np.array_equal(el.pyramid_level(lv, image=1), orr.pyramid_level(lv))
+
+
+def test_frame_stereo_rejects_mismatched_handles(gpu):
+    from orb_slam3_ros_amd import _lib
+    from orb_slam3_ros_amd.extractor import ORBextractor, frame_stereo
+    left, right = synth_stereo(4, 752, 480)
+    el, er = ORBextractor(1000, 1.2, 8, 20, 7), ORBextractor(1200, 1.2, 8, 20, 7)
+    with pytest.raises(_lib.OrbfeError):
+        frame_stereo(el, er, left, right, 50.0, 458.0)

@@ -3,6 +3,7 @@
 # then the kernel-trace A/B of all of them (tools/gpu_variants_trace.sh).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
+export ORBFE_LIB_PARTIAL=1   # A/B baselines built from older commits may predate entry points
 mkdir -p gpurun_out
 for so in variants/liborbfe_*.so; do
   v=$(basename $so .so)

@@ -3,6 +3,7 @@
 # pass per group, --kernel-include-regex), summed per variant. usage: KREGEX=k_fast bash tools/gpu_kernel_pmc.sh
 set -o pipefail
 cd $GRAFT_REPO_ROOT
+export ORBFE_LIB_PARTIAL=1   # A/B baselines built from older commits may predate entry points
 export TMPDIR=/tmp
 K=${KREGEX:-k_fast}
 PCMD="python bench.py --frames 512 --steps 2 --warmup 1 --stage-steps 1 --no-cpu-baseline --no-parity --matcher-steps 0 --rectify-steps 0 --no-side-configs"

@@ -3,6 +3,7 @@
 # for each variants/liborbfe_*.so on the default bench workload (one --pmc pass per counter group).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
+export ORBFE_LIB_PARTIAL=1   # A/B baselines built from older commits may predate entry points
 export TMPDIR=/tmp
 PCMD="python bench.py --frames 512 --steps 3 --warmup 1 --stage-steps 1 --no-cpu-baseline --no-parity --matcher-steps 0 --rectify-steps 0 --no-side-configs"
 for so in variants/liborbfe_*.so; do

@@ -6,6 +6,7 @@
 # Summarise with: python tools/pmc_round.py gpurun_out/prof_round <prefix>
 set -o pipefail
 cd $GRAFT_REPO_ROOT
+export ORBFE_LIB_PARTIAL=1   # A/B baselines built from older commits may predate entry points
 export TMPDIR=/tmp
 D=gpurun_out/prof_round
 mkdir -p $D

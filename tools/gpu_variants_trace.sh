@@ -3,6 +3,7 @@
 # per-kernel mean durations (kernel A/B experiments; ablated variants produce invalid outputs).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
+export ORBFE_LIB_PARTIAL=1   # A/B baselines built from older commits may predate entry points
 export TMPDIR=/tmp
 for rep in $(seq 1 ${REPS:-2}); do
 for so in variants/liborbfe_*.so; do
