@@ -641,6 +641,92 @@ def dropin_leg(frames, W=752, H=480, nf=1000, tracking_frames=60, cpu=True):
     return out
 
 
+def config4_dist_leg(dev, rank, world, gloo, K=64, steps=10, warmup=3):
+    """BASELINE config 4's own multi-GPU layout (world even, every rank): 512x512 KannalaBrandt8-like
+    stereo, stream s's left / right camera on ranks 2s / 2s + 1 (distributed.rig_role), K frames of
+    the rank's camera extracted per step (vLappingArea {0, 511}), one slab all-gather per step (K
+    steps batched per collective), the fisheye kNN + ratio of the step's K frames on
+    the left rank against the partner's gathered slots, one step behind so the gather overlaps the
+    next extraction. Frames/s = streams x K x steps / max-rank time. The left ranks' last step is
+    checked against the CPU oracle afterwards (4 frames)."""
+    import torch
+    import torch.distributed as dist
+    from orb_slam3_ros_amd import distributed as odist
+    from orb_slam3_ros_amd.synth import synth_stereo
+    stream, cam = odist.rig_role(rank)
+    U = 8   # distinct synthetic pairs per stream, tiled over the K frames
+    rig, err = None, None
+    try:
+        pairs = [synth_stereo(31000 + 100 * stream + i, 512, 512) for i in range(U)]
+        imgs = torch.from_numpy(np.stack([pairs[f % U][cam] for f in range(K)])).to(dev)
+        rig = odist.StereoRigExchange(K, 512, 512, device=dev)
+    except Exception as e:  # noqa: BLE001 - every rank learns of it below, so none waits in a collective
+        err = f"{type(e).__name__}: {e}"[:400]
+    ready = torch.tensor([0 if err else 1], dtype=torch.int32, device="cpu" if gloo else dev)
+    dist.all_reduce(ready, op=dist.ReduceOp.MIN)
+    if not int(ready.item()):
+        if rig is not None:
+            rig.close()
+        return {"error": err or "set-up failed on another rank"}
+    it = [0]
+
+    def step():
+        k = it[0]
+        it[0] += 1
+        rig.extract(imgs, k)
+        if k:
+            rig.match(k - 1)
+
+    def finish():
+        rig.match(it[0] - 1)
+        rig.drain()
+
+    for _ in range(warmup):
+        step()
+    finish()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    finish()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cpu" if gloo else dev)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = float(el.item())
+    ok, detail = True, "right-camera rank (no kNN)"
+    if cam == 0:   # CHECKER, outside the timed region
+        from oracle import oracle
+        oracle.build()
+        l2r = rig.l2r.cpu().numpy()
+        ngood = rig.ngood.cpu().numpy()
+        for f in range(min(4, K)):
+            left, right = pairs[f % U]
+            ol, orr = oracle.OracleExtractor(1000, 1.2, 8, 20, 7), oracle.OracleExtractor(1000, 1.2, 8, 20, 7)
+            ml, kl, dl = ol(left, (0, 511))
+            mr, kr, dr = orr(right, (0, 511))
+            g, t, _ = oracle.stereo_knn_ratio(dl[ml:], dr[mr:], 0.7)
+            exp = np.full(rig.cap, -1, np.int32)
+            exp[ml:len(kl)][t >= 0] = t[t >= 0] + mr
+            if int(ngood[f]) != g or not np.array_equal(l2r[f], exp):
+                ok, detail = False, f"stream {stream} frame {f}: kNN candidates differ from the oracle"
+                break
+        else:
+            detail = f"stream {stream}: frames 0..3 of the last step bit-exact vs the CPU oracle"
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device="cpu" if gloo else dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    rig.close()
+    streams = world // 2
+    return {"workload": "TUM-VI-like 512x512 KannalaBrandt8 stereo (BASELINE config 4): one camera per rank, "
+                        f"{streams} stream(s) x 2 cameras, K={K} frames per step and collective, vLappingArea "
+                        "{0,511}, slot all-gather + batched knnMatch(k=2)+ratio on the left-camera rank",
+            "frames_per_s": round(streams * K * steps / el, 2), "images_per_s": round(world * K * steps / el, 2),
+            "ms_per_step": round(1000.0 * el / steps, 4), "steps": steps, "warmup": warmup, "K": K,
+            "allgather_bytes_per_rank_per_step": odist.slab_bytes(K, rig.cap), "backend": "gloo" if gloo else "nccl",
+            "parity": {"ok": bool(int(flag.item())), "detail_rank0": detail}}
+
+
 def side_leg(dev, name, W, H, nf, F, steps, warmup, stereo, lap, bf, fx, check_frames, seed0):
     """A secondary BASELINE config on this GPU (rank 0, not part of `value`): throughput, stage
     times, the pyramid+FAST kernel roofline and a post-timing parity check."""
@@ -797,6 +883,13 @@ def main():
         del rout
     counts = fe.counts.cpu().numpy()
     nm = fe.nmatch.cpu().numpy()
+    c4 = None
+    if world > 1 and world % 2 == 0 and not args.no_side_configs:
+        # config 4's own layout over the same ranks (after the config-2 measurement, not part of `value`)
+        try:
+            c4 = config4_dist_leg(dev, rank, world, gloo)
+        except Exception as e:  # noqa: BLE001 - reported, never fatal to the config-2 line
+            c4 = {"error": f"{type(e).__name__}: {e}"[:400]}
 
     if rank == 0:
         n_img = 2 * F
@@ -884,6 +977,8 @@ def main():
                 rk = tr_kernels(n_img, W, H)["k_remap"]
                 rect["pmc_traffic_bytes_per_step"] = rk["read_bytes_per_step"] + rk["write_bytes_per_step"]
             result["rectify_remap"] = rect
+        if c4 is not None:
+            result["config4_multi_gpu"] = c4
         if world == 1 and not args.no_side_configs:
             legs, all_ok = {}, True
             legs["config3"], ok3 = side_leg(dev, "KITTI-like stereo 1241x376, nFeatures 2000 (BASELINE config 3): "

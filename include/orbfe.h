@@ -314,6 +314,16 @@ int orbfe_stereo_knn_ratio(const uint8_t* left_desc, int32_t nl, const uint8_t* 
 int orbfe_stereo_knn_batch(orbfe_extractor* left, int lbase, int lstep, orbfe_extractor* right, int rbase, int rstep,
                            int nframes, float ratio, int32_t* d_l2r, int32_t* d_dist, int32_t* d_ngood, void* stream);
 
+/* The same stage over explicit device output blocks instead of extractor handles: the layout of
+ * orbfe_batch_outputs / orbfe_set_batch_outputs (counts [image][2] = {n, monoIndex}, descriptors
+ * [image][cap][32]), e.g. the slots an all-gather brought from the rank that extracted the other
+ * camera (BASELINE config 4 over several GPUs: the left and right image of a stream on two ranks,
+ * SURVEY.md §8(e)). Frame f pairs left image (lbase + f*lstep) with right image (rbase + f*rstep).
+ * Outputs and stream as orbfe_stereo_knn_batch. */
+int orbfe_stereo_knn_slabs(const int32_t* d_counts_l, const uint8_t* d_desc_l, int lbase, int lstep,
+                           const int32_t* d_counts_r, const uint8_t* d_desc_r, int rbase, int rstep, int cap,
+                           int nframes, float ratio, int32_t* d_l2r, int32_t* d_dist, int32_t* d_ngood, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Local-map projection (the step before SearchByProjection in Tracking::SearchLocalPoints,
  * Tracking.cc:3407-3452): Frame::isInFrustum (pinhole branch, Frame.cc:512-570) and

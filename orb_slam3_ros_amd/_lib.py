@@ -85,6 +85,8 @@ _SIGS = {
                                                     _vp, _vp]),
     "orbfe_search_by_sim3": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_float, _vp, _vp]),
     "orbfe_stereo_knn_ratio": (_c_int, [_vp, _c_int, _vp, _c_int, _c_float, _vp, _vp]),
+    "orbfe_stereo_knn_slabs": (_c_int, [_vp, _vp, _c_int, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float,
+                                        _vp, _vp, _vp, _vp]),
     "orbfe_stereo_knn_batch": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _vp,
                                         _vp]),
     "orbfe_matcher_set_timing": (_c_int, [_c_int]),

@@ -264,7 +264,7 @@ __global__ __launch_bounds__(MT_NT) void k_kf_search(FrameDev fr, const KfProj* 
     if (out_dist) out_dist[q] = bestIdx >= 0 ? bestDist : -1;
     if (result != assign[q]) {
         assign[q] = result;
-        if (changed) atomicAdd(changed, 1);
+        if (changed) mt_flag_changed(changed);
     }
 }
 

@@ -21,16 +21,6 @@
 #include "orbfe_types.h"
 #include "stl_sort.h"
 
-// Timing-only ablation builds (tools/build_variant.sh -DORBFE_ABLATE_FAST=n / -DORBFE_ABLATE_DESC=n):
-// nonzero values cut k_fast / k_describe short and leave their outputs INVALID. The product build
-// (orb_slam3_ros_amd/build.py) never defines them.
-#ifndef ORBFE_ABLATE_FAST
-#define ORBFE_ABLATE_FAST 0
-#endif
-#ifndef ORBFE_ABLATE_DESC
-#define ORBFE_ABLATE_DESC 0
-#endif
-
 namespace orbfe {
 
 #define SYNC() __syncthreads()
@@ -741,23 +731,16 @@ template <int NDC>
 __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds& fl, const FastCell& me, int ng,
                                                  int nd_rt, int dw, int dh, uint8_t* s_img, uint8_t* s_sc,
                                                  uint16_t* s_cor, uint16_t* s_ent, uint32_t* cellkeys, int* cellcnt,
-                                                 int b, int c, int lane, int ablate, int first_attempt = 0) {
+                                                 int b, int c, int lane, int first_attempt = 0) {
     const int nd = NDC ? NDC : fast_rsd(nd_rt);   // row stride in dwords (>= the nd_rt dwords read)
     const int RS = 4 * nd;
     const OrbLevel& L = g.lv[me.l];
-    if (ablate == 1) {
-        asm volatile("" ::"v"((int)s_img[lane]));
-        if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = 0;
-        WAVE_SYNC();
-        return;
-    }
     const uint8_t* s_px = s_img + 1;   // ROI pixel (y, x) = s_px[y * RS + x]
     // attempt 0 = FAST at iniThFAST; attempt 1 (only when attempt 0 leaves no NMS survivor) =
     // FAST at minThFAST over a cleared score map: the reference's per-cell fallback
     // (ORBextractor.cc:826-846). Most cells stop after attempt 0, whose candidate set is a
     // fraction of minThFAST's.
     int nsurv = 0;
-    bool stop = false;
     uint32_t* out = cellkeys + (size_t)b * g.cellkeys_per_img + L.cellkey_off + (size_t)me.local * L.cell_cap;
     const int xr0 = me.c0 - ORBFE_MINB + 3, yr0 = me.r0 - ORBFE_MINB + 3;
     for (int attempt = first_attempt; attempt < 2; attempt++) {
@@ -845,13 +828,6 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
             }
         }
         WAVE_SYNC();
-        // expand the groups into entries, one per (pixel, possible sign): dy << 7 | dx, bit 14 =
-        // bright, bit 15 = second entry of a pixel (both signs passed; at most one can be a corner)
-        if (ablate == 2) {
-            asm volatile("" ::"v"(ngrp));
-            stop = true;
-            break;
-        }
         // per chunk of 64 groups: expand into entries, one per (pixel, possible sign): dy << 7 |
         // dx, bit 14 = bright, bit 15 = second entry of a pixel (both signs passed; at most one
         // can be a corner); then the exact score of the chunk's entries. Corners are appended in
@@ -938,11 +914,6 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
             }
             WAVE_SYNC();   // s_ent is refilled by the next chunk
         }
-        if (ablate == 3) {
-            asm volatile("" ::"v"((int)s_sc[lane]));
-            stop = true;
-            break;
-        }
         // NMS over corners (every other pixel has score 0), fused with the emission: the corner list
         // is in pixel order, so each chunk's survivors go straight to the cell's key list in FAST's
         // row-major emission order. A cell whose attempt leaves no survivor has emitted nothing.
@@ -968,10 +939,10 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
                                               ((uint32_t)sc << 24);
             nsurv += __popcll(m);
         }
-        if (nsurv > 0 || ablate == 4) break;
+        if (nsurv > 0) break;
         WAVE_SYNC();   // the fallback attempt clears the score map
     }   // attempt
-    if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = stop ? 0 : nsurv;
+    if (lane == 0) cellcnt[(size_t)b * g.total_cells + c] = nsurv;
     WAVE_SYNC();   // LDS is restaged for the next cell
 }
 
@@ -981,7 +952,6 @@ __device__ __forceinline__ void fast_cell_detect(const OrbGeom& g, const FastLds
 __global__ __launch_bounds__(64 * FAST_WPB) void k_fast(const uint8_t* const* imgs, int in_pitch, const uint8_t* pyr,
                                               int pyr_stride, OrbGeom g, FastLds fl, uint32_t* cellkeys,
                                               int* cellcnt, int c_lo, int c_hi, int cpw) {
-    constexpr int ablate = ORBFE_ABLATE_FAST;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_fast[];
     // wave-uniform in an SGPR: the cell geometry (level search, cell row / column division, ROI
     // bounds, row bases) is then scalar code instead of per-lane VALU divisions
@@ -1014,9 +984,9 @@ __global__ __launch_bounds__(64 * FAST_WPB) void k_fast(const uint8_t* const* im
             fast_prefetch(cur, lane, pf);
         }
         if (fast_rsd(nd) == 12)
-            fast_cell_detect<12>(g, fl, me, ng, nd, dw, dh, s_img, s_sc, s_cor, s_ent, cellkeys, cellcnt, b, c, lane, ablate);
+            fast_cell_detect<12>(g, fl, me, ng, nd, dw, dh, s_img, s_sc, s_cor, s_ent, cellkeys, cellcnt, b, c, lane);
         else
-            fast_cell_detect<0>(g, fl, me, ng, nd, dw, dh, s_img, s_sc, s_cor, s_ent, cellkeys, cellcnt, b, c, lane, ablate);
+            fast_cell_detect<0>(g, fl, me, ng, nd, dw, dh, s_img, s_sc, s_cor, s_ent, cellkeys, cellcnt, b, c, lane);
     }
 }
 
@@ -1716,7 +1686,7 @@ __device__ __forceinline__ void desc_stage(uint8_t* raw, int lane, const orbfe_u
 // keypoint record and the descriptor row.
 __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g, const uint8_t* raw, uint32_t* rowp,
                                              const uint2 (&pat)[4], int lane, OrbKeyPoint* kps, uint8_t* desc,
-                                             const BlurKernel& bk, const uint4 (*icm)[3], int ablate) {
+                                             const BlurKernel& bk, const uint4 (*icm)[3]) {
     const OrbLevel& L = g.lv[d.l];
     const int l = d.l, x = d.x, y = d.y;
     const uint32_t key = d.key;
@@ -1734,11 +1704,6 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
             kps[o] = kp;
         }
     };
-    if (ablate == 1) {   // timing-only (descriptors invalid, keypoint records valid): staging
-        asm volatile("" ::"v"((int)raw[lane]));
-        emit_kp(0.f);
-        return;
-    }
     // ---- IC_Angle on the unblurred patch, centre (21, 21): lane v + 15 sums disc row v with
     // two v_dot4 per dword: m10 = sum (u + 16) I - 16 sum I, m01 = sum v * sum I (exact integers,
     // the reference's sums in another order) ----
@@ -1766,11 +1731,6 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
     m10 = wave_sum_dpp(m10);
     m01 = wave_sum_dpp(m01);
     const float angle = fast_atan2_dev((float)m01, (float)m10);
-    if (ablate == 2) {   // + IC_Angle
-        asm volatile("" ::"v"(angle));
-        emit_kp(angle);
-        return;
-    }
     // ---- 7x7 Gaussian: row pass (Q8, exact) over the 43x37 region in packed u16x2 (every
     // partial sum fits 16 bits: sum(k) * 255 <= 65535); the column pass (Q16, rounded) runs only
     // at the 512 points rBRIEF samples. Both passes are exact integer sums before the final
@@ -1812,11 +1772,6 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
         }
     }
     WAVE_SYNC();
-    if (ablate == 3) {   // + Gaussian row pass
-        asm volatile("" ::"v"(rowp[lane]), "v"(angle));
-        emit_kp(angle);
-        return;
-    }
     // ---- rBRIEF, centre (18, 18) of the blurred window ----
     const float factorPI = (float)(M_PI / 180.f);
     const float ang = angle * factorPI;
@@ -1897,7 +1852,6 @@ __global__ __launch_bounds__(64 * DP_WPB) DP_ATTR void k_describe(const uint8_t*
                                                   int pyr_stride, OrbGeom g, const uint32_t* __restrict__ outkeys,
                                                   const int* __restrict__ lvinfo, const int* __restrict__ ranks,
                                                   OrbKeyPoint* kps, uint8_t* desc, int* counts, BlurKernel bk) {
-    constexpr int ablate = ORBFE_ABLATE_DESC;
     __shared__ __attribute__((aligned(16))) uint8_t s_dp[DP_WPB][DP_WAVE_LDS];
     // the IC_Angle disc masks (31 rows x 12 dwords) in LDS: per slot three ds_read_b128 instead of
     // three vector loads from constant memory
@@ -1952,7 +1906,7 @@ __global__ __launch_bounds__(64 * DP_WPB) DP_ATTR void k_describe(const uint8_t*
             nxt = desc_slot(imgs, in_pitch, pyr, pyr_stride, g, di, kv, rv, j + 1, &lvl, b, flat0 + j + 1);
             if (nxt.valid && nxt.interior) desc_load(nxt, lane, pq);
         }
-        if (cur.valid && ablate != 7) describe_one(cur, g, raw, rowp, pat, lane, kps, desc, bk, s_icm, ablate);
+        if (cur.valid) describe_one(cur, g, raw, rowp, pat, lane, kps, desc, bk, s_icm);
         WAVE_SYNC();   // the patch area is restaged for the next slot
         cur = nxt;
     }

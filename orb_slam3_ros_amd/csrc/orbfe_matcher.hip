@@ -177,7 +177,10 @@ __global__ __launch_bounds__(1024) void k_mt_grid(const OrbKeyPoint* keys, int n
             const OrbKeyPoint kp = keys[i];
             uint32_t cell = (uint32_t)ncells;   // outside the grid: never a candidate (PosInGrid false)
             if (is_band) {
-                if (kp.octave >= 0 && kp.octave < band.nlev) cell = (uint32_t)(kp.octave * band.NB + mt_band_of(kp.y, band.NB));
+                // a two-camera frame's single-camera searches (SearchByProjection(CurrentFrame, pKF))
+                // read its left grid only: the right rows [nleft, n) are in no bucket
+                if (kp.octave >= 0 && kp.octave < band.nlev && (nleft < 0 || i < nleft))
+                    cell = (uint32_t)(kp.octave * band.NB + mt_band_of(kp.y, band.NB));
             } else {
                 const int px = (int)roundf((kp.x - minx) * invw);
                 const int py = (int)roundf((kp.y - miny) * invh);
@@ -272,12 +275,24 @@ __device__ __forceinline__ void pass_stats(const PassIO& io, unsigned nwin, unsi
     }
 }
 __device__ __forceinline__ bool pass_gated(const PassIO& io) { return io.gate && *io.gate == 0; }
+// A pass's change word is only ever tested against zero (the next pass's gate, the commit, the host):
+// one plain store of 1 per wave that changed something. A counting atomicAdd from every changing
+// query put tens of thousands of same-address atomics into one pass (one per wave of four queries
+// in the wave-per-four-queries kernels) and serialised them at the memory side. Call from the lanes
+// that changed (a ballot over the active lanes picks one writer).
+__device__ __forceinline__ void mt_flag_changed(int* changed) {
+    const unsigned long long m = __ballot(true);
+    if ((int)(threadIdx.x & 63) == __ffsll((long long)m) - 1) *changed = 1;
+}
 __device__ __forceinline__ void pass_fill(const PassIO& io) {
     const int nt = gridDim.x * blockDim.x;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < io.n; i += nt) io.first_fill[i] = MT_INF;
 }
 __device__ __forceinline__ void pass_publish(const PassIO& io, int q, int result, int obs) {
-    if (result >= 0 && (!io.need_obs || obs > 0)) atomicMin(&io.first_next[result], q);
+    // first_next only decreases during the pass: a query that already sees a smaller index skips its
+    // atomic (most of the queries that pick one keypoint come after its first picker)
+    if (result >= 0 && (!io.need_obs || obs > 0) && q < __atomic_load_n(&io.first_next[result], __ATOMIC_RELAXED))
+        atomicMin(&io.first_next[result], q);
 }
 
 // ---- SearchByProjection(Frame&, vector<MapPoint*>, th, bFarPoints, thFar) (ORBmatcher.cc:43-213) ----
@@ -326,7 +341,7 @@ __global__ __launch_bounds__(MT_NT) void k_sbp_local(FrameDev fr, const orbfe_ma
     pass_publish(io, q, result, mp.observations);
     if (result != assign[q]) {
         assign[q] = result;
-        atomicAdd(changed, 1);
+        mt_flag_changed(changed);
     }
 }
 
@@ -520,7 +535,7 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wq(FrameDev fr, const orbf
             pass_publish(io, q, result, obs);
             if (result != prev) {
                 assign[q] = result;
-                atomicAdd(changed, 1);
+                mt_flag_changed(changed);
             }
         }
     }
@@ -647,9 +662,387 @@ __global__ __launch_bounds__(MT_BNT) void k_sbp_band(FrameDev fr, BandGrid bg, c
             pass_publish(io, q, result, obs);
             if (result != prev) {
                 assign[q] = result;
-                atomicAdd(changed, 1);
+                mt_flag_changed(changed);
             }
         }
+    }
+}
+
+// Small single-camera searches (nq <= MT_BLOCK_MAXQ: the per-frame Tracking calls, a few hundred to a
+// few thousand queries) in ONE workgroup: the frame in LDS as for k_sbp_band, one thread per query,
+// and the whole fixed point (ORBmatcher's ordered "later queries see earlier assignments", see the
+// top of this file) iterated inside the block, the first[] states in LDS and a barrier between
+// passes. A multi-block pass costs a launch and a round trip through memory per pass and its
+// one-thread-per-query grid walk is a chain of dependent global loads; a Tracking call's dependency
+// chains need up to ~10 passes (SearchByProjection(CurrentFrame, LastFrame): duplicated corners of
+// neighbouring octaves compete for the same keypoints), which here are a few microseconds each.
+//   MODE 0: SearchByProjection(F, vpMapPoints, th, bFarPoints, thFar) (ORBmatcher.cc:43-213): best and
+//           second best with their levels, ratio test; records orbfe_map_point.
+//   MODE 1: SearchByProjection(CurrentFrame, LastFrame, th, bMono) (:1676-1887), MODE 2:
+//           SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) (:1889-2010): single
+//           best (strict <, the first minimum in GetFeaturesInArea order = the smallest (dist, rank)
+//           key) within maxDist; records orbfe_proj_point.
+// Candidates: the in-grid keypoints of the octave range with |dx| < r and |dy| < r (k_sbp_band's
+// argument), read from the (octave, band) runs of the bands (y - r, y + r) touches.
+#define MT_BLOCK_MAXQ 2048
+#define MT_BLK_NT 1024
+#define MT_BLK_QPT (MT_BLOCK_MAXQ / MT_BLK_NT)
+__host__ __device__ __forceinline__ int mt_rot_bin(float a1, float a2);
+__host__ __device__ __forceinline__ unsigned mt_three_maxima_keep(const int* hist);
+// What k_sbp_block reads besides the frame and the records, and where it reports: the slot state
+// (F.mvpMapPoints handles and their Observations(), blocked0 = a held slot that blocks, any held slot
+// for the keyframe variant), the record fields the commit needs, and the pinned status words the
+// host waits on ({0, assigned, dropped, passes, sequence number, nToMatch}, as k_mt_commit_write).
+struct BlkIO {
+    const int32_t* mvp_in;     // slots before the search (device)
+    const int32_t* obs_in;     // Observations() per slot (nullptr: any held slot blocks)
+    int32_t* mvp_out;          // slots after the search (may alias mvp_in)
+    int q_stride, qid_off, qangle_off, checkOri;
+    const int* ntm;            // k_frustum's nToMatch (nullptr: none)
+    int* st_host;              // pinned status words
+    int seq;
+    unsigned long long* stats;   // [3]: window candidates, Hamming pairs, passes (nullptr: off)
+};
+// A query of k_sbp_block: its window and descriptor (from its record, pass 0 and fallbacks only)
+struct BlkQuery {
+    float x, y, R, xr;
+    int olo, ohi, obs;
+    bool ok;
+    uint32_t qd[8];
+};
+template <int MODE>
+__device__ __forceinline__ BlkQuery blk_load(const FrameDev& fr, const BandGrid& bg, const void* recs, int q, float th,
+                                             int a0, int a1, float thFar) {
+    BlkQuery Q;
+    Q.x = Q.y = Q.R = Q.xr = 0.f;
+    Q.olo = 0;
+    Q.ohi = -1;
+    if (MODE == 0) {
+        const orbfe_map_point& mp = ((const orbfe_map_point*)recs)[q];
+        Q.obs = mp.observations;
+        Q.ok = (mp.flags & ORBFE_MP_IN_VIEW) && !(a0 && mp.depth > thFar) && !(mp.flags & ORBFE_MP_BAD) &&
+               mp.scale_level >= 0 && mp.scale_level < fr.nlevels;
+        if (Q.ok) {
+            const int lvl = mp.scale_level;
+            float r = mp.view_cos > 0.998 ? 2.5f : 4.0f;   // RadiusByViewingCos (ORBmatcher.cc:215-221)
+            if (th != 1.0f) r *= th;
+            Q.R = r * fr.scale[lvl];
+            Q.x = mp.proj_x;
+            Q.y = mp.proj_y;
+            Q.xr = mp.proj_xr;
+            Q.olo = max(lvl - 1, 0);
+            Q.ohi = lvl;
+            memcpy(Q.qd, mp.desc, 32);
+        }
+    } else {
+        const orbfe_proj_point& pp = ((const orbfe_proj_point*)recs)[q];
+        Q.obs = pp.observations;
+        Q.ok = pp.valid != 0 && pp.octave >= 0 && pp.octave < fr.nlevels;
+        if (Q.ok && MODE == 1) {   // ORBmatcher.cc:1718-1736
+            if (pp.invzc < 0) Q.ok = false;
+            else if (pp.u < fr.minx || pp.u > fr.maxx) Q.ok = false;
+            else if (pp.v < fr.miny || pp.v > fr.maxy) Q.ok = false;
+        }
+        if (Q.ok) {
+            const int oct = pp.octave;
+            Q.R = th * fr.scale[oct];
+            Q.x = pp.u;
+            Q.y = pp.v;
+            Q.xr = MODE == 1 ? pp.u - fr.mbf * pp.invzc : 0.f;   // ur of :1752
+            // GetFeaturesInArea's level filter (Frame.cc:689,704-711: bCheckLevels)
+            int minL, maxL;
+            if (MODE == 2) { minL = oct - 1; maxL = oct + 1; }
+            else if (a0) { minL = oct; maxL = -1; }
+            else if (a1) { minL = 0; maxL = oct; }
+            else { minL = oct - 1; maxL = oct + 1; }
+            const bool chk = (minL > 0) || (maxL >= 0);
+            Q.olo = chk ? max(minL, 0) : 0;
+            Q.ohi = (chk && maxL >= 0) ? min(maxL, bg.nlev - 1) : bg.nlev - 1;
+            memcpy(Q.qd, pp.desc, 32);
+        }
+    }
+    if (Q.ohi >= bg.nlev) Q.ok = false;
+    return Q;
+}
+// Q's candidates that pass every gate-independent test (box, octave range, stereo), f(key, idx):
+// key = dist << 40 | rank << 4 | octave (the reference's enumeration order breaks distance ties)
+template <int MODE, typename Fn>
+__device__ __forceinline__ void blk_enum(const BlkQuery& Q, const BandGrid& bg, const float4* s_kp, const uint4* s_desc,
+                                         const int* s_bs, const uint8_t* s_blk, Fn&& f) {
+    if (!Q.ok || Q.olo > Q.ohi) return;
+    const int b0 = max(mt_band_of(Q.y - Q.R, bg.NB) - 1, 0), b1 = min(mt_band_of(Q.y + Q.R, bg.NB) + 1, bg.NB - 1);
+    for (int o = Q.olo; o <= Q.ohi; o++) {
+        const int pe = s_bs[o * bg.NB + b1 + 1];
+        // four positions per step, their box reads issued together (a thread's run is a chain of
+        // LDS round trips otherwise)
+        for (int p0 = s_bs[o * bg.NB + b0]; p0 < pe; p0 += 4) {
+            float4 kk[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) kk[u] = s_kp[min(p0 + u, pe - 1)];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+            const int p = p0 + u;
+            const float4 k4 = kk[u];
+            if (p >= pe || !(fabsf(k4.x - Q.x) < Q.R && fabsf(k4.y - Q.y) < Q.R)) continue;
+            const int idx = (int)(__float_as_uint(k4.z) & 0x1FFFu);
+            if (s_blk[idx]) continue;
+            if (MODE != 2 && k4.w > 0 && fabsf(Q.xr - k4.w) > Q.R) continue;
+            const uint4 d0 = s_desc[2 * p], d1 = s_desc[2 * p + 1];
+            const int dist = __popc(Q.qd[0] ^ d0.x) + __popc(Q.qd[1] ^ d0.y) + __popc(Q.qd[2] ^ d0.z) +
+                             __popc(Q.qd[3] ^ d0.w) + __popc(Q.qd[4] ^ d1.x) + __popc(Q.qd[5] ^ d1.y) +
+                             __popc(Q.qd[6] ^ d1.z) + __popc(Q.qd[7] ^ d1.w);
+            f(((unsigned long long)dist << 40) | ((unsigned long long)__float_as_uint(k4.z) << 4) | (unsigned)o, idx);
+            }
+        }
+    }
+}
+// the reference's acceptance from the best / second-best (dist, octave) of a query
+template <int MODE>
+__device__ __forceinline__ int blk_accept(int bestIdx, int bestDist, int bestLevel, int bestDist2, int bestLevel2,
+                                          float nnratio, int maxDist) {
+    if (bestIdx < 0) return -1;
+    if (MODE == 0)
+        return bestDist <= MT_TH_HIGH && !(bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) ? bestIdx : -1;
+    return bestDist <= maxDist ? bestIdx : -1;
+}
+
+#define MT_BLK_LIST 8   // candidates kept per query: the smallest keys, as u32 idx | octave << 13 | dist << 16
+template <int MODE>
+__global__ __launch_bounds__(MT_BLK_NT) void k_sbp_block(FrameDev fr, int NB, const void* recs, int nq, float th,
+                                                         int a0, int a1, float thFar, float nnratio, int maxDist,
+                                                         int need_obs, BlkIO io) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t mt_sm[];
+    const int n = fr.n;
+    const int nlev = fr.nlevels;
+    const int nbk = nlev * NB;
+    const BandGrid bg{nullptr, nullptr, NB, nlev};
+    float4* s_kp = (float4*)mt_sm;                 // {x (NaN: outside the grid), y, rank bits, uR}
+    uint4* s_desc = (uint4*)(s_kp + n);            // 2 x uint4 per band position
+    int* s_first = (int*)(s_desc + 2 * n);         // two first[] states by keypoint index (then the commit's slots)
+    int* s_bs = s_first + 2 * n;                   // bucket starts [nbk + 1]
+    int* s_cur = s_bs + nbk + 1;                   // bucket cursors [nbk]
+    uint8_t* s_blk = (uint8_t*)(s_cur + nbk);      // blocked initially, by keypoint index
+    __shared__ int s_flag, s_ws[MT_BLK_NT / 64], s_hist[MT_HISTO], s_cnt[2];
+    __shared__ unsigned s_keep;
+    const int tid = threadIdx.x;
+    // ---- the (octave, band) index in LDS: bucket counts, scan, placement (the order inside a bucket
+    // is irrelevant: every candidate carries its enumeration rank) ----
+    for (int b = tid; b <= nbk; b += MT_BLK_NT) s_bs[b] = 0;
+    if (tid < MT_HISTO) s_hist[tid] = 0;
+    if (tid < 2) s_cnt[tid] = 0;
+    SYNC();
+    auto bucket_of = [&](const OrbKeyPoint& kp, int idx) {
+        // a two-camera frame's single-camera searches read its left grid only (rows [0, nleft))
+        return (kp.octave >= 0 && kp.octave < nlev && (fr.nleft < 0 || idx < fr.nleft))
+                   ? kp.octave * NB + mt_band_of(kp.y, NB) : -1;
+    };
+    // every keypoint's data is read from memory ONCE, into registers (n <= 2 x MT_BLK_NT), before the
+    // bucket counts: one round trip for the whole staging
+    constexpr int KPT = (MT_BAND_MAXN + MT_BLK_NT - 1) / MT_BLK_NT;
+    OrbKeyPoint rk[KPT];
+    uint4 rd0[KPT], rd1[KPT];
+    float rur[KPT];
+    int rblk[KPT], rb[KPT];
+#pragma unroll
+    for (int u = 0; u < KPT; u++) {
+        const int idx = tid + u * MT_BLK_NT;
+        rb[u] = -1;
+        if (idx >= n) continue;
+        rk[u] = fr.keys[idx];
+        const uint4* d = (const uint4*)(fr.desc + 8 * idx);
+        rd0[u] = d[0];
+        rd1[u] = d[1];
+        rur[u] = fr.uright ? fr.uright[idx] : -1.f;
+        const int hb = io.mvp_in[idx] >= 0;
+        rblk[u] = io.obs_in ? (hb && io.obs_in[idx] > 0) : hb;
+    }
+#pragma unroll
+    for (int u = 0; u < KPT; u++) {
+        const int idx = tid + u * MT_BLK_NT;
+        if (idx >= n) continue;
+        rb[u] = bucket_of(rk[u], idx);
+        if (rb[u] >= 0) atomicAdd(&s_bs[rb[u]], 1);
+    }
+    SYNC();
+    const int nin = block_excl_scan<MT_BLK_NT>(s_bs, nbk, s_ws);
+    if (tid == 0) s_bs[nbk] = nin;
+    for (int b = tid; b < nbk; b += MT_BLK_NT) s_cur[b] = s_bs[b];
+    SYNC();
+#pragma unroll
+    for (int u = 0; u < KPT; u++) {
+        const int idx = tid + u * MT_BLK_NT;
+        if (idx >= n) continue;
+        s_blk[idx] = (uint8_t)rblk[u];
+        s_first[idx] = MT_INF;
+        if (rb[u] < 0) continue;
+        const int p = atomicAdd(&s_cur[rb[u]], 1);
+        const int px = (int)roundf((rk[u].x - fr.minx) * fr.invw);   // PosInGrid (Frame.cc:725-735)
+        const int py = (int)roundf((rk[u].y - fr.miny) * fr.invh);
+        const bool in_grid = !(px < 0 || px >= ORBFE_GRID_COLS || py < 0 || py >= ORBFE_GRID_ROWS);
+        const uint32_t rank = ((uint32_t)(px * ORBFE_GRID_ROWS + py) << 13) | (uint32_t)idx;
+        s_kp[p] = make_float4(in_grid ? rk[u].x : __builtin_nanf(""), rk[u].y, __uint_as_float(rank), rur[u]);
+        s_desc[2 * p] = rd0[u];
+        s_desc[2 * p + 1] = rd1[u];
+    }
+    SYNC();
+    // pass-independent part, once: each query's gate-independent candidates, the MT_BLK_LIST smallest
+    // keys sorted (registers) and their count; a pass then only walks the list past the keypoints
+    // that earlier queries hold (first[idx] < q). A query whose list runs out while more candidates
+    // exist re-enumerates its window with the pass's gates (exact, rare).
+    uint32_t L[MT_BLK_QPT][MT_BLK_LIST];
+    int cnt[MT_BLK_QPT], obs[MT_BLK_QPT], res[MT_BLK_QPT];
+    unsigned long long npair = 0;
+#pragma unroll
+    for (int i = 0; i < MT_BLK_QPT; i++) {
+        cnt[i] = 0;
+        obs[i] = 0;
+        res[i] = -1;
+        const int q = tid + i * MT_BLK_NT;
+#pragma unroll
+        for (int k = 0; k < MT_BLK_LIST; k++) L[i][k] = 0xFFFFFFFFu;
+        if (q >= nq) continue;
+        const BlkQuery Q = blk_load<MODE>(fr, bg, recs, q, th, a0, a1, thFar);
+        obs[i] = Q.obs;
+        unsigned long long K[MT_BLK_LIST];
+#pragma unroll
+        for (int k = 0; k < MT_BLK_LIST; k++) K[k] = ~0ull;
+        int c = 0;
+        blk_enum<MODE>(Q, bg, s_kp, s_desc, s_bs, s_blk, [&](unsigned long long key, int) {
+            c++;
+#pragma unroll
+            for (int k = 0; k < MT_BLK_LIST; k++) {   // sorted insertion (a compare-swap chain)
+                const bool lt = key < K[k];
+                const unsigned long long t = K[k];
+                K[k] = lt ? key : t;
+                key = lt ? t : key;
+            }
+        });
+        npair += (unsigned)c;
+        cnt[i] = c;
+#pragma unroll
+        for (int k = 0; k < MT_BLK_LIST; k++)
+            L[i][k] = K[k] == ~0ull ? 0xFFFFFFFFu
+                                    : (uint32_t)((K[k] >> 4) & 0x1FFFu) | (uint32_t)((K[k] & 15) << 13) |
+                                          (uint32_t)((K[k] >> 40) << 16);
+    }
+    int pass = 0;
+    for (;; pass++) {
+        const int* fcur = s_first + (pass & 1) * n;
+        int* fnext = s_first + ((pass + 1) & 1) * n;
+        for (int k = tid; k < n; k += MT_BLK_NT) fnext[k] = MT_INF;
+        if (tid == 0) s_flag = 0;
+        SYNC();
+        bool ch = false;
+#pragma unroll
+        for (int i = 0; i < MT_BLK_QPT; i++) {
+            const int q = tid + i * MT_BLK_NT;
+            if (q >= nq) continue;   // (not break: the loop must unroll so the per-slot arrays stay in registers)
+            // the first (and, MODE 0, second) list entries that no earlier query holds
+            // (the eight gate reads issued together, the selection in registers)
+            bool free_[MT_BLK_LIST];
+#pragma unroll
+            for (int k = 0; k < MT_BLK_LIST; k++)
+                free_[k] = L[i][k] != 0xFFFFFFFFu && fcur[L[i][k] & 0x1FFFu] >= q;
+            uint32_t e1 = 0xFFFFFFFFu, e2 = 0xFFFFFFFFu;
+            int found = 0;
+#pragma unroll
+            for (int k = 0; k < MT_BLK_LIST; k++) {
+                if (!free_[k] || found >= (MODE == 0 ? 2 : 1)) continue;
+                if (found == 0) e1 = L[i][k];
+                else e2 = L[i][k];
+                found++;
+            }
+            int result;
+            if (found < (MODE == 0 ? 2 : 1) && cnt[i] > MT_BLK_LIST) {
+                // the list ran out: the window again, with this pass's gates
+                const BlkQuery Q = blk_load<MODE>(fr, bg, recs, q, th, a0, a1, thFar);
+                unsigned long long k1 = ~0ull, k2 = ~0ull;
+                blk_enum<MODE>(Q, bg, s_kp, s_desc, s_bs, s_blk, [&](unsigned long long key, int idx) {
+                    if (fcur[idx] < q) return;
+                    const bool lt1 = key < k1, lt2 = key < k2;   // selects, not a store through a chosen pointer
+                    k2 = lt1 ? k1 : (lt2 ? key : k2);
+                    k1 = lt1 ? key : k1;
+                });
+                result = blk_accept<MODE>(k1 != ~0ull ? (int)((k1 >> 4) & 0x1FFFu) : -1, (int)(k1 >> 40),
+                                          (int)(k1 & 15), k2 != ~0ull ? (int)(k2 >> 40) : 256,
+                                          k2 != ~0ull ? (int)(k2 & 15) : -1, nnratio, maxDist);
+            } else {
+                result = blk_accept<MODE>(e1 != 0xFFFFFFFFu ? (int)(e1 & 0x1FFFu) : -1, (int)(e1 >> 16),
+                                          (int)((e1 >> 13) & 7), e2 != 0xFFFFFFFFu ? (int)(e2 >> 16) : 256,
+                                          e2 != 0xFFFFFFFFu ? (int)((e2 >> 13) & 7) : -1, nnratio, maxDist);
+            }
+            if (result >= 0 && (!need_obs || obs[i] > 0)) atomicMin(&fnext[result], q);
+            if (result != res[i]) {
+                res[i] = result;
+                ch = true;
+            }
+        }
+        if (__ballot(ch) && (tid & 63) == 0) s_flag = 1;
+        SYNC();
+        // after pass t the first t queries are final, so at most nq + 1 passes change anything
+        if (s_flag == 0 || pass > nq) break;
+    }
+    // ---- the commit (k_mt_commit_count / _drop / _write in one block): the last writer of a slot
+    // wins, every assignment enters the rotation histogram, ComputeThreeMaxima's dropped bins clear
+    // their slots and count once per entry (ORBmatcher.cc:1775-1792,1864-1884) ----
+    int* s_res = s_first;   // the pass states are dead
+    for (int k = tid; k < n; k += MT_BLK_NT) s_res[k] = -1;
+    SYNC();
+    int nas = 0;
+    int bins[MT_BLK_QPT];
+#pragma unroll
+    for (int i = 0; i < MT_BLK_QPT; i++) {
+        const int q = tid + i * MT_BLK_NT;
+        bins[i] = 0;
+        if (q >= nq || res[i] < 0) continue;
+        atomicMax(&s_res[res[i]], q);
+        nas++;
+        if (io.checkOri) {
+            const float qa = *(const float*)((const uint8_t*)recs + (size_t)q * io.q_stride + io.qangle_off);
+            bins[i] = mt_rot_bin(qa, fr.keys[res[i]].angle);
+            atomicAdd(&s_hist[bins[i]], 1);
+        }
+    }
+    if (nas) atomicAdd(&s_cnt[0], nas);
+    SYNC();
+    if (tid == 0) s_keep = io.checkOri ? mt_three_maxima_keep(s_hist) : 0xFFFFFFFFu;
+    SYNC();
+    int ndrop = 0;
+#pragma unroll
+    for (int i = 0; i < MT_BLK_QPT; i++) {
+        const int q = tid + i * MT_BLK_NT;
+        if (q >= nq || res[i] < 0 || ((s_keep >> bins[i]) & 1u)) continue;
+        s_res[res[i]] = -2;
+        ndrop++;
+    }
+    if (ndrop) atomicAdd(&s_cnt[1], ndrop);
+    SYNC();
+    for (int k = tid; k < n; k += MT_BLK_NT) {
+        const int w = s_res[k];
+        if (w == -2) io.mvp_out[k] = -1;
+        else if (w >= 0) io.mvp_out[k] = *(const int*)((const uint8_t*)recs + (size_t)w * io.q_stride + io.qid_off);
+    }
+    if (io.stats && npair) {
+        atomicAdd(&io.stats[0], npair);
+        atomicAdd(&io.stats[1], npair);
+    }
+    // every wave's slot writes complete (vmcnt 0), the barrier, then ONE system-scope release before the
+    // status words (MI355X_MICROARCH.md, correctness boundaries): a release per thread wrote back the
+    // L2 sixteen times and cost more than the search
+    __builtin_amdgcn_s_waitcnt(0);
+    SYNC();
+    if (tid == 0) {
+        __threadfence_system();
+        if (io.stats) io.stats[2] = (unsigned long long)(pass + 1);
+        volatile int* st = io.st_host;
+        st[0] = 0;
+        st[1] = s_cnt[0];
+        st[2] = s_cnt[1];
+        st[3] = pass + 1;
+        st[5] = io.ntm ? *io.ntm : 0;
+        __threadfence_system();
+        st[4] = io.seq;
+        __threadfence_system();
     }
 }
 
@@ -695,7 +1088,7 @@ __global__ __launch_bounds__(MT_NT) void k_sbp_proj(FrameDev fr, const orbfe_pro
     pass_publish(io, q, result, p.observations);
     if (result != assign[q]) {
         assign[q] = result;
-        atomicAdd(changed, 1);
+        mt_flag_changed(changed);
     }
 }
 
@@ -813,7 +1206,7 @@ __global__ __launch_bounds__(MT_NT) void k_sbp_local2(FrameDev fr, const orbfe_m
 #pragma unroll
     for (int b = 0; b < 4; b++)
         if (res[b] != assign[e0 + b]) { assign[e0 + b] = res[b]; ch = 1; }
-    if (ch) atomicAdd(changed, 1);
+    if (ch) mt_flag_changed(changed);
 }
 
 // SearchByProjection(CurrentFrame, LastFrame, th, bMono) with CurrentFrame.Nleft != -1
@@ -861,7 +1254,7 @@ __global__ __launch_bounds__(MT_NT) void k_sbp_proj2(FrameDev fr, const orbfe_pr
     if (ch) {
         assign[2 * q] = res[0];
         assign[2 * q + 1] = res[1];
-        atomicAdd(changed, 1);
+        mt_flag_changed(changed);
     }
 }
 
@@ -1110,8 +1503,11 @@ __global__ void k_mt_commit_write(int n, const int* qid, int q_stride_bytes, con
         else if (w >= 0) mvp[k] = *(const int*)((const uint8_t*)qid + (size_t)(w / W) * q_stride_bytes);
     }
     if (!cs.st_host) return;
-    __threadfence_system();   // this thread's slot write, before the block is counted done
+    // this block's slot writes complete (every wave's vmcnt 0, the barrier), then one release by the
+    // thread that counts the block done (a release per thread wrote back the L2 once per wave)
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
+    if (threadIdx.x == 0) __threadfence_system();
     if (threadIdx.x == 0 && atomicAdd(cs.done, 1) == (int)gridDim.x - 1) {
         __threadfence_system();
         int need = cs.npass;
@@ -1209,7 +1605,7 @@ __global__ __launch_bounds__(MT_NT) void k_init_eval(FrameDev f1, FrameDev f2, c
     if (result != assign[q] || (result >= 0 && rdist != adist[q])) {
         assign[q] = result;
         adist[q] = rdist;
-        atomicAdd(changed, 1);
+        mt_flag_changed(changed);
     }
 }
 
@@ -1435,6 +1831,10 @@ struct MatchScratch {
     size_t dcap = 0;
     uint8_t* h = nullptr;   // pinned
     size_t hcap = 0;
+    uint8_t* hd = nullptr;  // h as the device addresses it (mapped): the zero-copy inputs of k_sbp_block
+    int32_t* ho = nullptr;  // pinned, mapped: k_sbp_block's slot results
+    int32_t* ho_dev = nullptr;
+    size_t ocap = 0;
     int* hs = nullptr;      // pinned status words read back at the end of a call
     int* hs_dev = nullptr;  // hs as the device addresses it (kernels store the status there)
     int seq = 0;            // sequence number of the last published status
@@ -1498,7 +1898,7 @@ hipError_t ms_after_tail(hipStream_t s) {
     return hipSuccess;
 }
 
-int ms_prepare(const Plan& p) {
+int ms_prepare(const Plan& p, bool zero_copy = false) {
     MatchScratch& m = t_ms;
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
@@ -1525,16 +1925,21 @@ int ms_prepare(const Plan& p) {
         if (m.h) HIPCHK(hipHostFree(m.h));
         m.h = nullptr;
         const size_t cap = std::max<size_t>(p.up_end + p.up_end / 2, 1 << 20);
-        HIPCHK(hipHostMalloc((void**)&m.h, cap, hipHostMallocDefault));
+        // mapped and fine-grained as well: the one-workgroup searches read their inputs from here
+        // directly, uncached, so a later call never sees an earlier call's lines
+        HIPCHK(hipHostMalloc((void**)&m.h, cap, hipHostMallocMapped | hipHostMallocCoherent));
         m.hcap = cap;
+        HIPCHK(hipHostGetDevicePointer((void**)&m.hd, m.h, 0));
     }
     for (const auto& u : p.ups)
         if (u.bytes) memcpy(m.h + u.off, u.src, u.bytes);
-    if (p.up_end) HIPCHK(hipMemcpyAsync(m.d, m.h, p.up_end, hipMemcpyHostToDevice, m.stream));
+    if (p.up_end && !zero_copy) HIPCHK(hipMemcpyAsync(m.d, m.h, p.up_end, hipMemcpyHostToDevice, m.stream));
     return ORBFE_OK;
 }
 
 template <typename T> T* ms_ptr(size_t off) { return reinterpret_cast<T*>(t_ms.d + off); }
+// an uploaded input: the device arena copy, or (zero copy) the mapped pinned staging itself
+template <typename T> T* up_ptr(size_t off, bool zc) { return reinterpret_cast<T*>((zc ? t_ms.hd : t_ms.d) + off); }
 
 // Upload a frame and plan its grid; returns the device view after ms_prepare (fill_frame).
 struct FramePlan {
@@ -1581,19 +1986,20 @@ struct FramePlan {
         two = f->two_cams != 0;
         has_uright = !two && want_uright && f->uright != nullptr;
     }
+    bool zc = false;   // uploads read in place from the mapped pinned staging (no DMA)
     FrameDev view() const {
         FrameDev v;
         v.n = F->n;
-        v.keys = dev ? (const OrbKeyPoint*)F->keys : ms_ptr<const OrbKeyPoint>(keys);
-        v.desc = dev ? (const uint32_t*)F->desc : ms_ptr<const uint32_t>(desc);
-        v.uright = has_uright ? (dev ? F->uright : ms_ptr<const float>(uright)) : nullptr;
+        v.keys = dev ? (const OrbKeyPoint*)F->keys : up_ptr<const OrbKeyPoint>(keys, zc);
+        v.desc = dev ? (const uint32_t*)F->desc : up_ptr<const uint32_t>(desc, zc);
+        v.uright = has_uright ? (dev ? F->uright : up_ptr<const float>(uright, zc)) : nullptr;
         v.minx = F->min_x; v.maxx = F->max_x; v.miny = F->min_y; v.maxy = F->max_y;
         // mfGridElementWidthInv / HeightInv (Frame.cc:163-164)
         v.invw = static_cast<float>(ORBFE_GRID_COLS) / (F->max_x - F->min_x);
         v.invh = static_cast<float>(ORBFE_GRID_ROWS) / (F->max_y - F->min_y);
         v.mbf = F->mbf;
         v.nlevels = F->nlevels;
-        v.scale = dev ? F->scale_factors : ms_ptr<const float>(scale);
+        v.scale = dev ? F->scale_factors : up_ptr<const float>(scale, zc);
         v.cstart = ms_ptr<const int>(cstart);
         v.cidx = ms_ptr<const int>(cidx);
         v.gstride_c = cells() + 1;
@@ -1601,8 +2007,8 @@ struct FramePlan {
         v.pcstart = v.cstart + v.gstride_c;
         v.pcidx = v.cidx + v.gstride_i;
         v.nleft = two ? F->nleft : -1;
-        v.l2r = two ? (dev ? F->l2r : ms_ptr<const int>(l2r)) : nullptr;
-        v.r2l = two ? (dev ? F->r2l : ms_ptr<const int>(r2l)) : nullptr;
+        v.l2r = two ? (dev ? F->l2r : up_ptr<const int>(l2r, zc)) : nullptr;
+        v.r2l = two ? (dev ? F->r2l : up_ptr<const int>(r2l, zc)) : nullptr;
         return v;
     }
     // the grids on the thread's matcher stream, or on stream s; with `init`, the same launch also
@@ -1704,6 +2110,104 @@ struct DevIn {
     hipStream_t caller;
 };
 
+// sbp_run's one-launch form (k_sbp_block): arguments already validated by sbp_run.
+int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, const void* queries, int nq,
+                  size_t qstride, size_t qid_off, size_t qangle_off, float th, int a0, int a1, float thFar,
+                  float nnratio, int maxDist, int checkOri, int band_nb, const FrustumIn* fin, const DevIn* dev) {
+    const int n = F->n;
+    Plan p;
+    FramePlan fp;
+    if (dev) fp.plan_dev(F, mode != 2);
+    else fp.plan(p, F, true, mode != 2);
+    const size_t o_q = dev ? 0 : fin ? p.upload(fin->pts, (size_t)nq * sizeof(orbfe_map_point_3d))
+                                     : p.upload(queries, (size_t)nq * qstride);
+    const size_t o_mvp = dev ? 0 : p.upload(mvp, (size_t)n * 4);
+    const size_t o_obs = (dev || mode == 2) ? 0 : p.upload(mvp_obs, (size_t)n * 4);
+    const size_t o_track = fin ? p.scratch((size_t)nq * sizeof(orbfe_map_point)) : 0;
+    const size_t o_ntm = fin ? p.scratch(16) : 0;
+    const size_t o_stats = t_stats ? p.scratch(24) : 0;
+    // host-API calls: zero copy both ways. The kernel reads its inputs straight from the mapped pinned
+    // staging and writes the slots into mapped pinned memory; the host waits for the status words
+    // only (no DMA, no stream synchronisation: the call is one launch).
+    const bool zc = !dev;
+    int rc = ms_prepare(p, zc);
+    if (rc) return rc;
+    MatchScratch& m = t_ms;
+    if (zc && m.ocap < (size_t)n) {
+        if (m.ho) HIPCHK(hipHostFree(m.ho));
+        m.ho = nullptr;
+        m.ocap = 0;
+        const size_t cap = std::max<size_t>((size_t)n, 2048);
+        HIPCHK(hipHostMalloc((void**)&m.ho, cap * 4, hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostGetDevicePointer((void**)&m.ho_dev, m.ho, 0));
+        m.ocap = cap;
+    }
+    fp.zc = zc;
+    hipStream_t s = dev ? dev->caller : t_ms.stream;
+    if (dev) HIPCHK(ms_after_tail(s));
+    unsigned long long* stats = t_stats ? ms_ptr<unsigned long long>(o_stats) : nullptr;
+    t_last_stats[0] = t_last_stats[1] = t_last_stats[2] = -1;
+    if (stats) HIPCHK(hipMemsetAsync(stats, 0, 24, s));
+    MsTimer timer(s);
+    const FrameDev fr = fp.view();
+    const uint8_t* q = dev ? (const uint8_t*)(fin ? (const void*)fin->pts : queries) : up_ptr<const uint8_t>(o_q, zc);
+    int* ntm = fin ? ms_ptr<int>(o_ntm) : nullptr;
+    if (fin) {   // Tracking::SearchLocalPoints' isInFrustum, then the search (nothing in view: no match)
+        CamDev cd;
+        if (!make_camdev(F, fin->cam, fin->rig, cd)) return ORBFE_E_ARG;
+        HIPCHK(hipMemsetAsync(ntm, 0, 4, s));
+        hipLaunchKernelGGL(k_frustum, dim3((nq + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, cd,
+                           (const orbfe_map_point_3d*)q, nq, ms_ptr<orbfe_map_point>(o_track), ntm);
+        q = ms_ptr<const uint8_t>(o_track);
+        qstride = sizeof(orbfe_map_point);
+        qid_off = offsetof(orbfe_map_point, id);
+    }
+    const int32_t* mvp_in = dev ? mvp : up_ptr<const int32_t>(o_mvp, zc);
+    int32_t* mvp_out = dev ? mvp : m.ho_dev;
+    const int32_t* obs_d = mode == 2 ? nullptr : dev ? mvp_obs : up_ptr<const int32_t>(o_obs, zc);
+    const int seq = ++t_ms.seq;
+    if (zc) memcpy(m.ho, mvp, (size_t)n * 4);   // the slots the search leaves alone keep their value
+    const BlkIO io{mvp_in, obs_d, mvp_out, (int)qstride, (int)qid_off, (int)qangle_off, checkOri, ntm, t_ms.hs_dev, seq,
+                   stats};
+    const int nbk = F->nlevels * band_nb;
+    const size_t lds = ((size_t)n * 57 + (size_t)nbk * 8 + 4 + 15) & ~(size_t)15;
+    if (mode == 0)
+        hipLaunchKernelGGL(k_sbp_block<0>, dim3(1), dim3(MT_BLK_NT), lds, s, fr, band_nb, (const void*)q, nq, th, a0, a1,
+                           thFar, nnratio, maxDist, 1, io);
+    else if (mode == 1)
+        hipLaunchKernelGGL(k_sbp_block<1>, dim3(1), dim3(MT_BLK_NT), lds, s, fr, band_nb, (const void*)q, nq, th, a0, a1,
+                           thFar, nnratio, maxDist, 1, io);
+    else
+        hipLaunchKernelGGL(k_sbp_block<2>, dim3(1), dim3(MT_BLK_NT), lds, s, fr, band_nb, (const void*)q, nq, th, a0, a1,
+                           thFar, nnratio, maxDist, 0, io);
+    HIPCHK(hipGetLastError());
+    if (dev) {
+        HIPCHK(hipEventRecord(t_ms.tail, s));
+        t_ms.tail_stream = s;
+    }
+    timer.end();
+    volatile int* st = t_ms.hs;
+    for (unsigned spin = 1; st[4] != seq; spin++) {
+        if ((spin & 1023) == 0) {   // bounded: a stream that finished without publishing is an error
+            const hipError_t e = hipStreamQuery(s);
+            if (e == hipSuccess && st[4] != seq) return ORBFE_E_DEVICE;
+            if (e != hipSuccess && e != hipErrorNotReady) HIPCHK(e);
+        }
+        __builtin_ia32_pause();
+    }
+    if (zc) memcpy(mvp, m.ho, (size_t)n * 4);   // complete: the status words come after the slot writes
+    if (fin && fin->n_to_match) *fin->n_to_match = st[5];
+    if (stats) {   // counting mode only: one more copy and synchronisation
+        unsigned long long hst[3];
+        HIPCHK(hipMemcpyAsync(hst, stats, 24, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        t_last_stats[0] = (long long)hst[0];
+        t_last_stats[1] = (long long)hst[1];
+        t_last_stats[2] = (long long)hst[2];
+    }
+    return st[1] - st[2];
+}
+
 int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, const void* queries, int nq,
             size_t qstride, size_t qobs_off, size_t qid_off, size_t qangle_off, size_t qlevel_off, float th, int a0, int a1, float thFar,
             float nnratio, int maxDist, int checkOri, const FrustumIn* fin = nullptr, const DevIn* dev = nullptr,
@@ -1738,6 +2242,14 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
                 return ORBFE_E_ARG;
         }
     }
+    // single-camera searches of a frame that fits in LDS run on its (octave, band) index: a small
+    // search (the per-frame Tracking calls) entirely in one workgroup, one launch (k_sbp_block), a
+    // large local-map search as one multi-block pass per fixed-point step (k_sbp_band)
+    const int band_nb = std::min(std::max((int)std::floor(F->max_y * (1.0f / MT_BAND_ROWS)) + 2, 1), 4096);
+    const bool band_ok = (size_t)F->nlevels * band_nb < 65535;   // 16-bit bucket keys
+    if (W == 1 && n <= MT_BAND_MAXN && nq <= MT_BLOCK_MAXQ && band_ok)
+        return sbp_block_run(mode, F, mvp, mvp_obs, queries, nq, qstride, qid_off, qangle_off, th, a0, a1, thFar,
+                             nnratio, maxDist, checkOri, band_nb, fin, dev);
     std::vector<int32_t> blocked0(dev ? 0 : n);
     for (int k = 0; !dev && k < n; k++) blocked0[k] = mode == 2 ? (mvp[k] >= 0) : (mvp[k] >= 0 && mvp_obs[k] > 0);
     Plan p;
@@ -1750,11 +2262,13 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     const size_t o_mvp = dev ? 0 : p.upload(mvp, (size_t)n * 4);
     const size_t o_b0d = dev ? p.scratch((size_t)n * 4) : 0;
     fp.plan_grid(p, mode == 0 ? F->nlevels + 1 : 1);
-    // the single-camera local-map search of a frame that fits in LDS: the band kernel
-    bool use_band = mode == 0 && W == 1 && n <= MT_BAND_MAXN;
+    // single-camera searches of a frame that fits in LDS run on its (octave, band) index: a small
+    // search (the per-frame Tracking calls) entirely in one workgroup (k_sbp_block), a large local-map
+    // search as one multi-block pass per fixed-point step (k_sbp_band)
+    bool use_band = mode == 0 && W == 1 && n <= MT_BAND_MAXN && band_ok;
     if (use_band) {
         fp.plan_band(p);
-        if ((size_t)F->nlevels * fp.band_nb >= 65535) use_band = fp.band = false;   // 16-bit bucket keys
+        fp.ngrids = 0;   // the cell grids are not read
     }
     const size_t o_track = fin ? p.scratch((size_t)nq * sizeof(orbfe_map_point)) : 0;
     const size_t o_ntm = fin ? p.scratch(16) : 0;
@@ -1770,7 +2284,7 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     const size_t o_changed = p.scratch(MT_MAX_PASSES * 4);
     const size_t o_result = p.scratch((size_t)(n + 3) * 4);   // [change flag copy | counts | slots]
     const size_t o_hist = p.scratch((MT_HISTO + 1) * 4);   // rotation bins + commit completion counter
-    const size_t o_stats = t_stats ? p.scratch(16) : 0;
+    const size_t o_stats = t_stats ? p.scratch(24) : 0;
     int rc = ms_prepare(p);
     if (rc) return rc;
     // a device-resident search runs on the caller's stream, after the producer of its inputs; it
@@ -1780,7 +2294,7 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     if (dev) HIPCHK(ms_after_tail(s));
     unsigned long long* stats = t_stats ? ms_ptr<unsigned long long>(o_stats) : nullptr;
     t_last_stats[0] = t_last_stats[1] = t_last_stats[2] = -1;
-    if (stats) HIPCHK(hipMemsetAsync(stats, 0, 16, s));
+    if (stats) HIPCHK(hipMemsetAsync(stats, 0, 24, s));
     MsTimer timer(s);
     const FrameDev fr = fp.view();
     const int* b0 = dev ? ms_ptr<const int>(o_b0d) : ms_ptr<const int>(o_b0);
@@ -1898,8 +2412,8 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
             if (st[0] == 0) {
                 t_ms.pass_hint[mode] = pass0 + st[3];
                 if (stats) {   // counting mode only: one more copy and synchronisation
-                    unsigned long long hst[2];
-                    HIPCHK(hipMemcpyAsync(hst, stats, 16, hipMemcpyDeviceToHost, s));
+                    unsigned long long hst[3];
+                    HIPCHK(hipMemcpyAsync(hst, stats, 24, hipMemcpyDeviceToHost, s));
                     HIPCHK(hipStreamSynchronize(s));
                     t_last_stats[0] = (long long)hst[0];
                     t_last_stats[1] = (long long)hst[1];
@@ -2145,6 +2659,24 @@ int orbfe_stereo_knn_ratio(const uint8_t* left_desc, int32_t nl, const uint8_t* 
     int good = 0;
     for (int i = 0; i < nl; i++) good += out_train[i] >= 0;
     return good;
+}
+
+int orbfe_stereo_knn_slabs(const int32_t* d_counts_l, const uint8_t* d_desc_l, int lbase, int lstep,
+                           const int32_t* d_counts_r, const uint8_t* d_desc_r, int rbase, int rstep, int cap,
+                           int nframes, float ratio, int32_t* d_l2r, int32_t* d_dist, int32_t* d_ngood, void* stream) {
+    if (!d_counts_l || !d_desc_l || !d_counts_r || !d_desc_r || nframes <= 0 || cap <= 0 || !d_l2r || !d_dist ||
+        !d_ngood || lbase < 0 || rbase < 0 || lstep < 0 || rstep < 0)
+        return ORBFE_E_ARG;
+    const size_t lds = (size_t)cap * 32;
+    if (lds > 128 * 1024) return ORBFE_E_ARG;
+    StereoSide SL{nullptr, 0, nullptr, 0, nullptr, d_desc_l, d_counts_l, lbase, lstep};
+    StereoSide SR{nullptr, 0, nullptr, 0, nullptr, d_desc_r, d_counts_r, rbase, rstep};
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipMemsetAsync(d_ngood, 0, (size_t)nframes * 4, s));
+    hipLaunchKernelGGL(k_knn2_batch, dim3((cap + KNN_Q - 1) / KNN_Q, nframes), dim3(256), lds, s, SL, SR, cap, ratio,
+                       (int*)d_l2r, (int*)d_dist, (int*)d_ngood);
+    HIPCHK(hipGetLastError());
+    return ORBFE_OK;
 }
 
 int orbfe_stereo_knn_batch(orbfe_extractor* left, int lbase, int lstep, orbfe_extractor* right, int rbase, int rstep,

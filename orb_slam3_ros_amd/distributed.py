@@ -120,3 +120,98 @@ class SlabExchange:
         nb = slab_bytes(self.n, self.cap)
         g = self.gathered[k % len(self.gathered)]
         return slab_views(g[r * nb:(r + 1) * nb], self.n, self.cap)
+
+
+def rig_role(rank: int) -> tuple[int, int]:
+    """BASELINE config 4 over 2 x streams ranks (one image per GPU): stream s's
+    left camera on rank 2s, its right camera on rank 2s + 1. Returns (stream, camera)."""
+    return rank // 2, rank % 2
+
+
+class StereoRigExchange:
+    """Config 4's multi-GPU layout (TUM-VI KannalaBrandt8 stereo, Frame.cc:1034-1166): each rank
+    extracts its camera of its stream for K consecutive frames per step (one launch, vLappingArea
+    `lap`), the step's slots are all-gathered once (K steps of one image batched per collective,
+    SURVEY.md §8(e)), and the left-camera rank runs ComputeStereoFishEyeMatches' descriptor stage
+    (knnMatch k=2 + ratio over the lapping rows, Frame.cc:1126-1151) for those K frames against the
+    right-camera slots its partner rank produced (orbfe_stereo_knn_slabs). Every rank ends a step
+    holding every stream's keypoints and descriptors (the gathered slab).
+
+    Step k writes slab k % 2; match(k) makes the caller's stream wait for step k's gather and
+    enqueues the kNN, so calling match(k - 1) after extract(k) overlaps the gather with the next
+    step's kernels. gloo (CPU rehearsal) exchanges host copies synchronously."""
+
+    def __init__(self, K: int, width: int, height: int, nfeatures: int = 1000, lap=(0, 511), ratio: float = 0.7,
+                 device=None, group=None):
+        import ctypes
+
+        from . import _lib
+        self.lib, self._lib = _lib.load(), _lib
+        self.K, self.W, self.H = int(K), int(width), int(height)
+        self.lap, self.ratio = (int(lap[0]), int(lap[1])), float(ratio)
+        self.group = group
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        if self.world % 2:
+            raise ValueError("config 4's rig layout needs an even number of ranks (two cameras per stream)")
+        self.stream_id, self.camera = rig_role(self.rank)
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.orbfe_extractor_create(nfeatures, 1.2, 8, 20, 7, ctypes.byref(h)), "create")
+        self.h = h
+        self.cap = _lib.check(self.lib.orbfe_extractor_capacity(h, self.W, self.H), "capacity")
+        self.xchg = SlabExchange(self.K, self.cap, self.device, group)
+        self.l2r = torch.full((self.K, self.cap), -1, dtype=torch.int32, device=self.device)
+        self.dist = torch.full((self.K, self.cap), -1, dtype=torch.int32, device=self.device)
+        self.ngood = torch.zeros(self.K, dtype=torch.int32, device=self.device)
+        self._ptr_key, self._ptrs = None, None
+        self._partner = None   # gloo: device copy of the partner's gathered slab
+
+    def extract(self, images, k: int):
+        """images: [K, H, W] u8 device tensor, this rank's camera for the step's K frames."""
+        import ctypes
+        assert images.shape == (self.K, self.H, self.W) and images.dtype == torch.uint8 and images.is_cuda
+        self.xchg.acquire(k)
+        counts, kps, desc = self.xchg.views(k)
+        _ = self._lib.check(self.lib.orbfe_set_batch_outputs(self.h, kps.data_ptr(), desc.data_ptr(),
+                                                             counts.data_ptr(), self.K), "set_batch_outputs")
+        key = (images.data_ptr(), images.stride(0))
+        if key != self._ptr_key:
+            self._ptrs = (ctypes.c_void_p * self.K)(*[images.data_ptr() + i * images.stride(0) for i in range(self.K)])
+            self._ptr_key = key
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        self._lib.check(self.lib.orbfe_extract_batch(self.h, self.K, self._ptrs, self.W, self.H, images.stride(1),
+                                                     self.lap[0], self.lap[1], s), "extract_batch")
+        self.xchg.post(k)
+
+    def match(self, k: int):
+        """Left-camera ranks: the fisheye kNN of step k's K frames (own slab x the partner's gathered
+        slab) into l2r / dist / ngood; right-camera ranks: nothing."""
+        i = k % len(self.xchg.local)
+        if self.xchg.pending[i] is not None:   # the caller's stream waits for step k's gather
+            self.xchg.pending[i].wait()
+            self.xchg.pending[i] = None
+        if self.camera != 0:
+            return
+        cl, _, dl = self.xchg.views(k)
+        cr, _, dr = self.xchg.rank_views(k, self.rank + 1)
+        if cr.device != self.device:   # gloo rehearsal: the gathered slab is a host tensor
+            if self._partner is None:
+                self._partner = torch.empty(slab_bytes(self.K, self.cap), dtype=torch.uint8, device=self.device)
+            nb = slab_bytes(self.K, self.cap)
+            g = self.xchg.gathered[i]
+            self._partner.copy_(g[(self.rank + 1) * nb:(self.rank + 2) * nb])
+            cr, _, dr = slab_views(self._partner, self.K, self.cap)
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        self._lib.check(self.lib.orbfe_stereo_knn_slabs(cl.data_ptr(), dl.data_ptr(), 0, 1, cr.data_ptr(),
+                                                        dr.data_ptr(), 0, 1, self.cap, self.K, self.ratio,
+                                                        self.l2r.data_ptr(), self.dist.data_ptr(),
+                                                        self.ngood.data_ptr(), s), "stereo_knn_slabs")
+
+    def drain(self):
+        self.xchg.drain()
+
+    def close(self):
+        if self.h:
+            self.lib.orbfe_set_batch_outputs(self.h, None, None, None, 0)
+            self.lib.orbfe_extractor_destroy(self.h)
+            self.h = None

@@ -364,39 +364,67 @@ struct GpuApi {
         f.nstereo = ns;
         return ns;
     }
+    // diagnostic run (--tracking-diag): device time (HIP events around the call's kernels) and the
+    // fixed-point passes of every matcher call
+    bool diag = false;
+    std::vector<double> d_sbp, d_loc, p_sbp, p_loc, w_sbp, w_loc;
+    void note(std::vector<double>& dv, std::vector<double>& pv) {
+        if (!diag) return;
+        dv.push_back(orbfe_matcher_last_ms());
+        long long st[3];
+        orbfe_matcher_last_stats(st);
+        pv.push_back((double)st[2]);
+    }
     int sbp_last(const orbfe_frame* F, int32_t* mvp, const int32_t* obs, const orbfe_proj_point* pts, int n, float th,
                  int fwd, int bwd, int ori) {
+        const auto t0 = std::chrono::steady_clock::now();
         const int r = orbfe_search_by_projection_lastframe(F, mvp, obs, pts, n, th, fwd, bwd, ori);
+        if (diag) w_sbp.push_back(trk::ms_since(t0));
         check(r, "search_by_projection_lastframe");
+        note(d_sbp, p_sbp);
         return r;
     }
     int local_points(const orbfe_frame* F, const orbfe_camera* c, const orbfe_map_point_3d* pts, int n, int32_t* mvp,
                      const int32_t* obs, float th, int bFar, float thFar, float ratio, int32_t* ntm) {
+        const auto t0 = std::chrono::steady_clock::now();
         const int r = orbfe_search_local_points(F, c, pts, n, mvp, obs, th, bFar, thFar, ratio, ntm);
+        if (diag) w_loc.push_back(trk::ms_since(t0));
         check(r, "search_local_points");
+        note(d_loc, p_loc);
         return r;
     }
 };
 
 }  // namespace
 
-int tracking(int frames, const char* job, const char* out_path) {
+int tracking(int frames, const char* job, const char* out_path, bool diag) {
     const SeqJob J = read_seq(job);
     ORBextractor el(J.nf, 1.2f, 8, 20, 7), er(J.nf, 1.2f, 8, 20, 7);
     const int cap = orbfe_extractor_capacity(el.handle(), J.w, J.h);
     check(cap, "capacity");
     GpuApi api{el, er, J.w, J.h, cap, J.cam.bf, J.cam.fx};
-    return trk::run_sequence(api, J.cam, J.w, J.h, el.mvScaleFactor, J.window, frames, J.npairs,
-                             [&](int k) { return J.left(k); }, [&](int k) { return J.right(k); }, out_path,
-                             "gpu: liborbfe.so C-ABI (orbfe_frame_stereo, orbfe_search_by_projection_lastframe, "
-                             "orbfe_search_local_points)");
+    api.diag = diag;
+    if (diag) {
+        orbfe_matcher_set_timing(1);
+        orbfe_matcher_set_stats(1);
+    }
+    const int rc = trk::run_sequence(api, J.cam, J.w, J.h, el.mvScaleFactor, J.window, frames, J.npairs,
+                                     [&](int k) { return J.left(k); }, [&](int k) { return J.right(k); }, out_path,
+                                     "gpu: liborbfe.so C-ABI (orbfe_frame_stereo, orbfe_search_by_projection_lastframe, "
+                                     "orbfe_search_local_points)");
+    if (diag)
+        printf("{\"diag\": {\"sbp_last_wall_ms\": %.4f, \"sbp_last_device_ms\": %.4f, \"sbp_last_passes\": %.1f, "
+               "\"local_wall_ms\": %.4f, \"local_device_ms\": %.4f, \"local_passes\": %.1f}}\n",
+               median(api.w_sbp), median(api.d_sbp), median(api.p_sbp), median(api.w_loc), median(api.d_loc),
+               median(api.p_loc));
+    return rc;
 }
 
 
 int main(int argc, char** argv) {
-    if ((argc == 4 || argc == 5) && std::string(argv[1]) == "--tracking") {
+    if ((argc == 4 || argc == 5) && (std::string(argv[1]) == "--tracking" || std::string(argv[1]) == "--tracking-diag")) {
         try {
-            return tracking(atoi(argv[2]), argv[3], argc == 5 ? argv[4] : nullptr);
+            return tracking(atoi(argv[2]), argv[3], argc == 5 ? argv[4] : nullptr, std::string(argv[1]) == "--tracking-diag");
         } catch (const std::exception& e) {
             fprintf(stderr, "capi_frontend: %s\n", e.what());
             return 1;

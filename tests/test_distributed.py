@@ -6,6 +6,7 @@ import socket
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+import pytest
 
 from orb_slam3_ros_amd import distributed as odist
 
@@ -137,4 +138,108 @@ def test_allgather_real_features_gloo():
     world, nframes, cap = 2, 4, 600
     out = mp.Manager().dict()
     mp.spawn(_real_worker, args=(world, _free_port(), nframes, cap, out), nprocs=world, join=True)
+    assert dict(out) == {0: 1, 1: 1}
+
+
+def _rig_frames(stream, K):
+    """K consecutive synthetic TUM-VI-like 512x512 stereo pairs of one stream (seeded by stream)."""
+    from orb_slam3_ros_amd.synth import synth_stereo
+    return [synth_stereo(5000 + 100 * stream + f, 512, 512) for f in range(K)]
+
+
+def _rig_worker(rank, world, port, K, cap, out):
+    """BASELINE config 4's layout on the CPU: each rank extracts its camera of its stream (the oracle
+    stands in for the device extractor), the slabs are all-gathered, and the left rank runs the
+    fisheye kNN + ratio on its own slots against the partner's gathered ones."""
+    import numpy as np
+    from oracle import oracle
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    stream, cam = odist.rig_role(rank)
+    frames = _rig_frames(stream, K)
+    ex = oracle.OracleExtractor(1000, 1.2, 8, 20, 7)
+    x = odist.SlabExchange(K, cap, "cpu")
+    counts, kps, desc = x.views(0)
+    for f, pair in enumerate(frames):
+        mono, k, d = ex(pair[cam], (0, 511))
+        n = len(k)
+        counts[f] = torch.tensor([n, mono], dtype=torch.int32)
+        kps[f, :n] = torch.from_numpy(np.ascontiguousarray(k).view(np.int32).reshape(n, 7).copy())
+        desc[f, :n] = torch.from_numpy(d)
+    x.post(0)
+    x.drain()
+    ok = True
+    if cam == 0:
+        cr, _, dr = x.rank_views(0, rank + 1)
+        exr = oracle.OracleExtractor(1000, 1.2, 8, 20, 7)
+        for f, (left, right) in enumerate(frames):
+            ml, nl = int(counts[f, 1]), int(counts[f, 0])
+            mr, nr = int(cr[f, 1]), int(cr[f, 0])
+            g, t, dd = oracle.stereo_knn_ratio(desc[f, ml:nl].numpy(), dr[f, mr:nr].numpy(), 0.7)
+            omr, _, odr = exr(right, (0, 511))
+            oml, _, odl = ex(left, (0, 511))
+            g2, t2, d2 = oracle.stereo_knn_ratio(odl[oml:], odr[omr:], 0.7)
+            ok = ok and g == g2 and np.array_equal(t, t2) and np.array_equal(dd, d2) and g > 0
+    out[rank] = int(ok)
+    dist.destroy_process_group()
+
+
+def test_rig_layout_gloo():
+    """Config 4 over 2 ranks (one stream: left camera on rank 0, right on rank 1): the right camera's
+    slots reach the left rank through the slab all-gather intact, and the kNN there equals the one
+    computed from both images directly."""
+    from oracle import oracle
+    oracle.build()
+    assert [odist.rig_role(r) for r in range(4)] == [(0, 0), (0, 1), (1, 0), (1, 1)]
+    world, K, cap = 2, 2, 1100
+    out = mp.Manager().dict()
+    mp.spawn(_rig_worker, args=(world, _free_port(), K, cap, out), nprocs=world, join=True)
+    assert dict(out) == {0: 1, 1: 1}
+
+
+def _rig_gpu_worker(rank, world, port, K, out):
+    import numpy as np
+    from oracle import oracle
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    stream, cam = odist.rig_role(rank)
+    frames = _rig_frames(stream, K)
+    imgs = torch.from_numpy(np.stack([p[cam] for p in frames])).cuda()
+    rig = odist.StereoRigExchange(K, 512, 512, device=torch.device("cuda", 0))
+    for k in range(3):   # three steps over the two slabs, the match lagging one step
+        rig.extract(imgs, k)
+        if k:
+            rig.match(k - 1)
+    rig.match(2)
+    rig.drain()
+    torch.cuda.synchronize()
+    ok = True
+    if cam == 0:
+        l2r = rig.l2r.cpu().numpy()
+        ngood = rig.ngood.cpu().numpy()
+        for f, (left, right) in enumerate(frames):
+            ol, orr = oracle.OracleExtractor(1000, 1.2, 8, 20, 7), oracle.OracleExtractor(1000, 1.2, 8, 20, 7)
+            ml, kl, dl = ol(left, (0, 511))
+            mr, kr, dr = orr(right, (0, 511))
+            g, t, _ = oracle.stereo_knn_ratio(dl[ml:], dr[mr:], 0.7)
+            exp = np.full(rig.cap, -1, np.int32)
+            exp[ml:len(kl)][t >= 0] = t[t >= 0] + mr
+            ok = ok and int(ngood[f]) == g and np.array_equal(l2r[f], exp)
+    rig.close()
+    out[rank] = int(ok)
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rig_exchange_gpu_gloo():
+    """StereoRigExchange (config 4's multi-GPU layout) with two ranks sharing cuda:0 over gloo: the
+    left rank's batched kNN from the partner's gathered slots is bit-exact against the oracle."""
+    from oracle import oracle
+    oracle.build()
+    world, K = 2, 3
+    out = mp.Manager().dict()
+    mp.spawn(_rig_gpu_worker, args=(world, _free_port(), K, out), nprocs=world, join=True)
     assert dict(out) == {0: 1, 1: 1}

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 from orb_slam3_ros_amd import synth_match as sm
-from orb_slam3_ros_amd.matcher import ORBmatcher, stereo_knn_ratio
+from orb_slam3_ros_amd.matcher import MatchFrame, ORBmatcher, stereo_knn_ratio
 
 pytestmark = pytest.mark.gpu
 
@@ -506,3 +506,64 @@ def test_two_cams_frustum_needs_rig(gpu):
         is_in_frustum(F, cam, pts)
     with pytest.raises(_lib.OrbfeError):
         search_local_points(F, cam, pts, mvp, obs, 1.0)
+
+
+@pytest.mark.parametrize("n_kp", [2048, 2049])
+@pytest.mark.parametrize("th", [1, 5])
+def test_sbp_local_band_edges(gpu, om, n_kp, th):
+    """k_sbp_band's (octave, 8-row band) candidate runs against the reference's GetFeaturesInArea:
+    keypoints and projections on integer and band-boundary rows (y = 8k, y +- R exactly on a band
+    edge), keypoints outside the grid's bounds (PosInGrid false: never candidates), tied distances
+    (duplicated descriptors: the enumeration order decides), at the band kernel's size limit (2048
+    keypoints) and one past it (the grid-walk kernels)."""
+    rng = np.random.default_rng(4242 + n_kp + th)
+    F0 = sm.synth_frame(rng, n_kp)
+    k = F0.keys.copy()
+    k["y"][: n_kp // 3] = (8.0 * rng.integers(0, 60, n_kp // 3)).astype(np.float32)     # on band edges
+    k["x"][: n_kp // 4] = np.round(k["x"][: n_kp // 4]).astype(np.float32)
+    k["x"][-20:] = np.float32(751.5)   # round((x - minx) * 64 / 747) = 64: outside the grid
+    desc = F0.desc.copy()
+    desc[1::7] = desc[0::7][: len(desc[1::7])]   # exact duplicates: distance ties
+    F = MatchFrame(k, desc, (0.0, 747.0, 0.0, 480.0), F0.scale_factors, F0.uright, F0.mbf)
+    mps = sm.synth_local_map(rng, F, 30000, copy_frac=0.5)
+    # projections exactly on band rows, and y +- R on a band edge for level-0 radius 2.5 * th
+    sel = rng.random(len(mps)) < 0.3
+    mps["proj_y"][sel] = (8.0 * rng.integers(0, 60, int(sel.sum()))).astype(np.float32)
+    sel2 = rng.random(len(mps)) < 0.1
+    mps["proj_y"][sel2] = (8.0 * rng.integers(1, 59, int(sel2.sum())) + 2.5 * th).astype(np.float32)
+    mps["view_cos"][sel2] = 0.9995
+    mps["scale_level"][sel2] = 0
+    mvp0, obs = sm.initial_slots(rng, F.N, 0.1)
+    a, b = mvp0.copy(), mvp0.copy()
+    ng = ORBmatcher(0.8).SearchByProjectionLocalMap(F, a, obs, mps, th)
+    no = om.OracleMatcher(0.8).sbp_local(F, b, obs, mps, th)
+    assert ng == no and no > 0
+    np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("nq", [2048, 2049])
+def test_sbp_block_limit(gpu, om, nq):
+    """The single-workgroup fixed point (k_sbp_block, up to 2048 queries) and the multi-block passes
+    one query past it, for the three SearchByProjection variants on one dense case (duplicated
+    descriptors and map points: long "later points see earlier assignments" chains)."""
+    rng = np.random.default_rng(900 + nq)
+    F = sm.synth_frame(rng, 1800)
+    F.desc[1::5] = F.desc[0::5][: len(F.desc[1::5])]
+    mps = sm.synth_local_map(rng, F, nq, copy_frac=0.8, flip_p=0.02)
+    pts = sm.synth_proj_points(rng, F, nq, copy_frac=0.8)
+    mvp0, obs = sm.initial_slots(rng, F.N, 0.15)
+    for th in (1, 5):
+        a, b = mvp0.copy(), mvp0.copy()
+        assert ORBmatcher(0.8).SearchByProjectionLocalMap(F, a, obs, mps, th) == \
+            om.OracleMatcher(0.8).sbp_local(F, b, obs, mps, th)
+        np.testing.assert_array_equal(a, b)
+    for mode in ("none", "forward", "backward"):
+        a, b = mvp0.copy(), mvp0.copy()
+        fw, bw = mode == "forward", mode == "backward"
+        assert ORBmatcher(0.9, True).SearchByProjectionLastFrame(F, a, obs, pts, 7, fw, bw) == \
+            om.OracleMatcher(0.9, True).sbp_lastframe(F, b, obs, pts, 7, fw, bw)
+        np.testing.assert_array_equal(a, b)
+    a, b = mvp0.copy(), mvp0.copy()
+    assert ORBmatcher(0.9, True).SearchByProjectionKeyFrame(F, a, pts, 10, 100) == \
+        om.OracleMatcher(0.9, True).sbp_kf(F, b, pts, 10, 100)
+    np.testing.assert_array_equal(a, b)

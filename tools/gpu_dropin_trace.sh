@@ -21,3 +21,5 @@ done
 timeout -k 10 120 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/dropin_trace -o run -- tests/native/capi_frontend --latency 60 gpurun_out/dropin_trace/job.bin > gpurun_out/dropin_trace/log 2>&1 || { tail -20 gpurun_out/dropin_trace/log; exit 1; }
 tail -1 gpurun_out/dropin_trace/log
 python3 tools/dropin_timeline.py gpurun_out/dropin_trace
+# the raw traces exceed what gpurun copies back: keep the summaries only
+rm -rf gpurun_out/dropin_trace/*/ gpurun_out/dropin_trace/*.csv gpurun_out/dropin_trace/job.bin
