@@ -392,15 +392,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k
 #define RS_COLS 256          // output columns per wave strip
 typedef unsigned short orbfe_ushort2_rs __attribute__((ext_vector_type(2)));
 #define RS_WPB 4   // waves per block (1 / 2 / 4 measured equal: r03_kernel_ab.txt item 24)
-__global__ __launch_bounds__(64 * RS_WPB) void k_resize_s(const uint8_t* const* imgs, int in_pitch, uint8_t* pyr,
-                                                  int pyr_stride, const int16_t* __restrict__ tab, OrbGeom g, int l,
-                                                  int nstrips, int nitems) {
+// one wave's item of k_resize_s (image b, level l, item = chunk * nstrips + strip)
+__device__ __forceinline__ void resize_s_item(const uint8_t* const* imgs, int in_pitch, uint8_t* pyr, int pyr_stride,
+                                              const int16_t* __restrict__ tab, const OrbGeom& g, int l, int nstrips,
+                                              int item, int b) {
     const OrbLevel& L = g.lv[l];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
-    const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
-    const int bx = lb % gridDim.x, b = lb / gridDim.x;
-    const int item = bx * RS_WPB + wave;
-    if (item >= nitems) return;
+    const int lane = lane_id();
     const int chunk = item / nstrips, strip = item - chunk * nstrips;
     const int y0 = chunk * L.rs_rows, y1 = min(y0 + L.rs_rows, L.h);
     int spitch;
@@ -532,6 +529,16 @@ __global__ __launch_bounds__(64 * RS_WPB) void k_resize_s(const uint8_t* const* 
             __builtin_amdgcn_sched_barrier(0);
         }
     }
+}
+__global__ __launch_bounds__(64 * RS_WPB) void k_resize_s(const uint8_t* const* imgs, int in_pitch, uint8_t* pyr,
+                                                  int pyr_stride, const int16_t* __restrict__ tab, OrbGeom g, int l,
+                                                  int nstrips, int nitems) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
+    const int bx = lb % gridDim.x, b = lb / gridDim.x;
+    const int item = bx * RS_WPB + wave;
+    if (item >= nitems) return;
+    resize_s_item(imgs, in_pitch, pyr, pyr_stride, tab, g, l, nstrips, item, b);
 }
 
 // Gaussian 7x7 quantised kernel taps (the blur itself is fused into k_describe, K5).

@@ -685,6 +685,7 @@ __global__ __launch_bounds__(MT_BNT) void k_sbp_band(FrameDev fr, BandGrid bg, c
 // Candidates: the in-grid keypoints of the octave range with |dx| < r and |dy| < r (k_sbp_band's
 // argument), read from the (octave, band) runs of the bands (y - r, y + r) touches.
 #define MT_BLOCK_MAXQ 2048
+#define MT_LDS_MAX (160 * 1024 - 1024)   // dynamic LDS of k_sbp_block (the static part is < 1 KB)
 #define MT_BLK_NT 1024
 #define MT_BLK_QPT (MT_BLOCK_MAXQ / MT_BLK_NT)
 __host__ __device__ __forceinline__ int mt_rot_bin(float a1, float a2);
@@ -703,6 +704,15 @@ struct BlkIO {
     int seq;
     unsigned long long* stats;   // [3]: window candidates, Hamming pairs, passes (nullptr: off)
 };
+// k_sbp_block's LDS index: buckets (octave, band of br rows, strip of sw columns), bucket
+// c = (octave * NB + band) * NS + strip (the strips of a band are consecutive, so a query's window is one
+// contiguous run per (octave, band)); be[c] .. be[c + 1] is bucket c's run of band positions.
+struct BlkGeom {
+    int NB, NS;
+    float inv_br, inv_sw;
+    __device__ __forceinline__ int band(float y) const { return min(max((int)floorf(y * inv_br), 0), NB - 1); }
+    __device__ __forceinline__ int strip(float x) const { return min(max((int)floorf(x * inv_sw), 0), NS - 1); }
+};
 // A query of k_sbp_block: its window and descriptor (from its record, pass 0 and fallbacks only)
 struct BlkQuery {
     float x, y, R, xr;
@@ -711,8 +721,8 @@ struct BlkQuery {
     uint32_t qd[8];
 };
 template <int MODE>
-__device__ __forceinline__ BlkQuery blk_load(const FrameDev& fr, const BandGrid& bg, const void* recs, int q, float th,
-                                             int a0, int a1, float thFar) {
+__device__ __forceinline__ BlkQuery blk_load(const FrameDev& fr, const void* recs, int q, float th, int a0, int a1,
+                                             float thFar) {
     BlkQuery Q;
     Q.x = Q.y = Q.R = Q.xr = 0.f;
     Q.olo = 0;
@@ -757,25 +767,30 @@ __device__ __forceinline__ BlkQuery blk_load(const FrameDev& fr, const BandGrid&
             else { minL = oct - 1; maxL = oct + 1; }
             const bool chk = (minL > 0) || (maxL >= 0);
             Q.olo = chk ? max(minL, 0) : 0;
-            Q.ohi = (chk && maxL >= 0) ? min(maxL, bg.nlev - 1) : bg.nlev - 1;
+            Q.ohi = (chk && maxL >= 0) ? min(maxL, fr.nlevels - 1) : fr.nlevels - 1;
             memcpy(Q.qd, pp.desc, 32);
         }
     }
-    if (Q.ohi >= bg.nlev) Q.ok = false;
+    if (Q.ohi >= fr.nlevels) Q.ok = false;
     return Q;
 }
 // Q's candidates that pass every gate-independent test (box, octave range, stereo), f(key, idx):
 // key = dist << 40 | rank << 4 | octave (the reference's enumeration order breaks distance ties)
 template <int MODE, typename Fn>
-__device__ __forceinline__ void blk_enum(const BlkQuery& Q, const BandGrid& bg, const float4* s_kp, const uint4* s_desc,
-                                         const int* s_bs, const uint8_t* s_blk, Fn&& f) {
+__device__ __forceinline__ void blk_enum(const BlkQuery& Q, const BlkGeom& gm, const float4* s_kp, const uint4* s_desc,
+                                         const int* s_be, const uint8_t* s_blk, Fn&& f) {
     if (!Q.ok || Q.olo > Q.ohi) return;
-    const int b0 = max(mt_band_of(Q.y - Q.R, bg.NB) - 1, 0), b1 = min(mt_band_of(Q.y + Q.R, bg.NB) + 1, bg.NB - 1);
-    for (int o = Q.olo; o <= Q.ohi; o++) {
-        const int pe = s_bs[o * bg.NB + b1 + 1];
+    // the buckets of (x -+ (r + 1), y -+ (r + 1)): a keypoint that passes the box test lies inside (one
+    // pixel of margin is far beyond the rounding of the bounds); out-of-grid keypoints are in no bucket
+    const int b0 = gm.band(Q.y - Q.R - 1.f), b1 = gm.band(Q.y + Q.R + 1.f);
+    const int s0 = gm.strip(Q.x - Q.R - 1.f), s1 = gm.strip(Q.x + Q.R + 1.f);
+    for (int o = Q.olo; o <= Q.ohi; o++)
+    for (int b = b0; b <= b1; b++) {
+        const int c = (o * gm.NB + b) * gm.NS;
+        const int pe = s_be[c + s1 + 1];
         // four positions per step, their box reads issued together (a thread's run is a chain of
         // LDS round trips otherwise)
-        for (int p0 = s_bs[o * bg.NB + b0]; p0 < pe; p0 += 4) {
+        for (int p0 = s_be[c + s0]; p0 < pe; p0 += 4) {
             float4 kk[4];
 #pragma unroll
             for (int u = 0; u < 4; u++) kk[u] = s_kp[min(p0 + u, pe - 1)];
@@ -807,123 +822,184 @@ __device__ __forceinline__ int blk_accept(int bestIdx, int bestDist, int bestLev
 }
 
 #define MT_BLK_LIST 8   // candidates kept per query: the smallest keys, as u32 idx | octave << 13 | dist << 16
-template <int MODE>
-__global__ __launch_bounds__(MT_BLK_NT) void k_sbp_block(FrameDev fr, int NB, const void* recs, int nq, float th,
-                                                         int a0, int a1, float thFar, float nnratio, int maxDist,
-                                                         int need_obs, BlkIO io) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t mt_sm[];
-    const int n = fr.n;
-    const int nlev = fr.nlevels;
-    const int nbk = nlev * NB;
-    const BandGrid bg{nullptr, nullptr, NB, nlev};
-    float4* s_kp = (float4*)mt_sm;                 // {x (NaN: outside the grid), y, rank bits, uR}
-    uint4* s_desc = (uint4*)(s_kp + n);            // 2 x uint4 per band position
-    int* s_first = (int*)(s_desc + 2 * n);         // two first[] states by keypoint index (then the commit's slots)
-    int* s_bs = s_first + 2 * n;                   // bucket starts [nbk + 1]
-    int* s_cur = s_bs + nbk + 1;                   // bucket cursors [nbk]
-    uint8_t* s_blk = (uint8_t*)(s_cur + nbk);      // blocked initially, by keypoint index
-    __shared__ int s_flag, s_ws[MT_BLK_NT / 64], s_hist[MT_HISTO], s_cnt[2];
-    __shared__ unsigned s_keep;
-    const int tid = threadIdx.x;
-    // ---- the (octave, band) index in LDS: bucket counts, scan, placement (the order inside a bucket
-    // is irrelevant: every candidate carries its enumeration rank) ----
-    for (int b = tid; b <= nbk; b += MT_BLK_NT) s_bs[b] = 0;
-    if (tid < MT_HISTO) s_hist[tid] = 0;
-    if (tid < 2) s_cnt[tid] = 0;
+// k_sbp_block's / k_sbp_multi0's LDS frame: the (octave, band, strip) bucket index (counts, scan,
+// placement; the order inside a bucket is irrelevant: every candidate carries its enumeration rank),
+// keypoints {x, y, rank bits, uR} and descriptors by bucket position, blocked flags (and angles, the
+// first[] state, when given) by keypoint index. Ends with a barrier.
+template <int NT>
+__device__ __forceinline__ void blk_stage(const FrameDev& fr, const BlkGeom& gm, const int32_t* mvp_in,
+                                          const int32_t* obs_in, float4* s_kp, uint4* s_desc, int* s_be,
+                                          uint8_t* s_blk, float* s_ang, int* s_first, int* s_ws) {
+    const int n = fr.n, nlev = fr.nlevels, nbk = nlev * gm.NB * gm.NS, tid = threadIdx.x;
+    for (int b = tid; b <= nbk; b += NT) s_be[b] = 0;
     SYNC();
-    auto bucket_of = [&](const OrbKeyPoint& kp, int idx) {
-        // a two-camera frame's single-camera searches read its left grid only (rows [0, nleft))
-        return (kp.octave >= 0 && kp.octave < nlev && (fr.nleft < 0 || idx < fr.nleft))
-                   ? kp.octave * NB + mt_band_of(kp.y, NB) : -1;
+    auto bucket_of = [&](float x, float y, int oct, int idx) {
+        // a two-camera frame's single-camera searches read its left grid only (rows [0, nleft)); a
+        // keypoint outside the grid (PosInGrid, Frame.cc:725-735) is in no cell of the reference
+        const int px = (int)roundf((x - fr.minx) * fr.invw);
+        const int py = (int)roundf((y - fr.miny) * fr.invh);
+        const bool in_grid = !(px < 0 || px >= ORBFE_GRID_COLS || py < 0 || py >= ORBFE_GRID_ROWS);
+        return (in_grid && oct >= 0 && oct < nlev && (fr.nleft < 0 || idx < fr.nleft))
+                   ? (oct * gm.NB + gm.band(y)) * gm.NS + gm.strip(x) : -1;
     };
-    // every keypoint's data is read from memory ONCE, into registers (n <= 2 x MT_BLK_NT), before the
-    // bucket counts: one round trip for the whole staging
-    constexpr int KPT = (MT_BAND_MAXN + MT_BLK_NT - 1) / MT_BLK_NT;
-    OrbKeyPoint rk[KPT];
+    // every keypoint's data is read from memory ONCE, into registers (n <= 2 x NT), before the bucket
+    // counts: one round trip for the whole staging (the fields, not the struct: a struct array
+    // copy is not promoted to registers)
+    constexpr int KPT = (MT_BAND_MAXN + NT - 1) / NT;
+    float kx[KPT], ky[KPT], kang[KPT];
+    int koct[KPT];
     uint4 rd0[KPT], rd1[KPT];
     float rur[KPT];
     int rblk[KPT], rb[KPT];
 #pragma unroll
     for (int u = 0; u < KPT; u++) {
-        const int idx = tid + u * MT_BLK_NT;
+        const int idx = tid + u * NT;
         rb[u] = -1;
+        kx[u] = ky[u] = kang[u] = rur[u] = 0.f;
+        koct[u] = rblk[u] = 0;
+        rd0[u] = rd1[u] = make_uint4(0u, 0u, 0u, 0u);
         if (idx >= n) continue;
-        rk[u] = fr.keys[idx];
+        const OrbKeyPoint& kp = fr.keys[idx];
+        kx[u] = kp.x;
+        ky[u] = kp.y;
+        kang[u] = kp.angle;
+        koct[u] = kp.octave;
         const uint4* d = (const uint4*)(fr.desc + 8 * idx);
         rd0[u] = d[0];
         rd1[u] = d[1];
         rur[u] = fr.uright ? fr.uright[idx] : -1.f;
-        const int hb = io.mvp_in[idx] >= 0;
-        rblk[u] = io.obs_in ? (hb && io.obs_in[idx] > 0) : hb;
+        const int hb = mvp_in[idx] >= 0;
+        rblk[u] = obs_in ? (hb && obs_in[idx] > 0) : hb;
     }
 #pragma unroll
     for (int u = 0; u < KPT; u++) {
-        const int idx = tid + u * MT_BLK_NT;
+        const int idx = tid + u * NT;
         if (idx >= n) continue;
-        rb[u] = bucket_of(rk[u], idx);
-        if (rb[u] >= 0) atomicAdd(&s_bs[rb[u]], 1);
+        rb[u] = bucket_of(kx[u], ky[u], koct[u], idx);
+        if (rb[u] >= 0) atomicAdd(&s_be[rb[u] + 1], 1);
     }
     SYNC();
-    const int nin = block_excl_scan<MT_BLK_NT>(s_bs, nbk, s_ws);
-    if (tid == 0) s_bs[nbk] = nin;
-    for (int b = tid; b < nbk; b += MT_BLK_NT) s_cur[b] = s_bs[b];
+    // counts -> starts (be[c + 1] = start of c); the placement's atomic increments then leave be[c + 1]
+    // at the end of bucket c, i.e. the start of c + 1, with be[0] = 0. One segment of consecutive
+    // buckets per thread: one barrier instead of one pair per NT buckets.
+    {
+        int* a = s_be + 1;
+        const int per = (nbk + NT - 1) / NT, b0 = tid * per, b1 = min(b0 + per, nbk);
+        int sum = 0;
+        for (int b = b0; b < b1; b++) sum += a[b];
+        const int incl = wave_incl_scan_dpp(sum);
+        if ((tid & 63) == 63) s_ws[tid >> 6] = incl;
+        SYNC();
+        int run = incl - sum;
+#pragma unroll
+        for (int w = 0; w < NT / 64; w++) run += w < (tid >> 6) ? s_ws[w] : 0;
+        for (int b = b0; b < b1; b++) {
+            const int v = a[b];
+            a[b] = run;
+            run += v;
+        }
+    }
     SYNC();
 #pragma unroll
     for (int u = 0; u < KPT; u++) {
-        const int idx = tid + u * MT_BLK_NT;
+        const int idx = tid + u * NT;
         if (idx >= n) continue;
         s_blk[idx] = (uint8_t)rblk[u];
-        s_first[idx] = MT_INF;
+        if (s_first) s_first[idx] = MT_INF;
+        if (s_ang) s_ang[idx] = kang[u];
         if (rb[u] < 0) continue;
-        const int p = atomicAdd(&s_cur[rb[u]], 1);
-        const int px = (int)roundf((rk[u].x - fr.minx) * fr.invw);   // PosInGrid (Frame.cc:725-735)
-        const int py = (int)roundf((rk[u].y - fr.miny) * fr.invh);
-        const bool in_grid = !(px < 0 || px >= ORBFE_GRID_COLS || py < 0 || py >= ORBFE_GRID_ROWS);
+        const int p = atomicAdd(&s_be[rb[u] + 1], 1);
+        const int px = (int)roundf((kx[u] - fr.minx) * fr.invw);   // PosInGrid (Frame.cc:725-735)
+        const int py = (int)roundf((ky[u] - fr.miny) * fr.invh);
         const uint32_t rank = ((uint32_t)(px * ORBFE_GRID_ROWS + py) << 13) | (uint32_t)idx;
-        s_kp[p] = make_float4(in_grid ? rk[u].x : __builtin_nanf(""), rk[u].y, __uint_as_float(rank), rur[u]);
+        s_kp[p] = make_float4(kx[u], ky[u], __uint_as_float(rank), rur[u]);
         s_desc[2 * p] = rd0[u];
         s_desc[2 * p + 1] = rd1[u];
     }
     SYNC();
+}
+// A query's gate-independent candidates: the MT_BLK_LIST smallest keys, sorted, packed as
+// idx | octave << 13 | dist << 16 (0xFFFFFFFF: none); returns the candidate count
+template <int MODE>
+__device__ __forceinline__ int blk_list(const BlkQuery& Q, const BlkGeom& gm, const float4* kp, const uint4* desc,
+                                        const int* be, const uint8_t* blk, uint32_t (&L)[MT_BLK_LIST]) {
+    unsigned long long K[MT_BLK_LIST];
+#pragma unroll
+    for (int k = 0; k < MT_BLK_LIST; k++) K[k] = ~0ull;
+    int c = 0;
+    blk_enum<MODE>(Q, gm, kp, desc, be, blk, [&](unsigned long long key, int) {
+        c++;
+#pragma unroll
+        for (int k = 0; k < MT_BLK_LIST; k++) {   // sorted insertion (a compare-swap chain)
+            const bool lt = key < K[k];
+            const unsigned long long t = K[k];
+            K[k] = lt ? key : t;
+            key = lt ? t : key;
+        }
+    });
+#pragma unroll
+    for (int k = 0; k < MT_BLK_LIST; k++)
+        L[k] = K[k] == ~0ull ? 0xFFFFFFFFu
+                             : (uint32_t)((K[k] >> 4) & 0x1FFFu) | (uint32_t)((K[k] & 15) << 13) |
+                                   (uint32_t)((K[k] >> 40) << 16);
+    return c;
+}
+template <int MODE>
+__global__ __launch_bounds__(MT_BLK_NT) void k_sbp_block(FrameDev fr, BlkGeom gm, const void* recs, int nq, float th,
+                                                         int a0, int a1, float thFar, float nnratio, int maxDist,
+                                                         int need_obs, BlkIO io) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t mt_sm[];
+    const int n = fr.n;
+    const int nlev = fr.nlevels;
+    const int nbk = nlev * gm.NB * gm.NS;
+    float4* s_kp = (float4*)mt_sm;                 // {x, y, rank bits, uR} per bucket position
+    uint4* s_desc = (uint4*)(s_kp + n);            // 2 x uint4 per bucket position
+    int* s_first = (int*)(s_desc + 2 * n);         // two first[] states by keypoint index (then the commit's slots)
+    float* s_ang = (float*)(s_first + 2 * n);      // keypoint angles by index (the rotation check)
+    int* s_be = (int*)(s_ang + n);                 // bucket bounds [nbk + 1]
+    uint8_t* s_blk = (uint8_t*)(s_be + nbk + 1);   // blocked initially, by keypoint index
+    __shared__ int s_flag, s_ws[MT_BLK_NT / 64], s_hist[MT_HISTO], s_cnt[2];
+    __shared__ unsigned s_keep;
+    const int tid = threadIdx.x;
     // pass-independent part, once: each query's gate-independent candidates, the MT_BLK_LIST smallest
     // keys sorted (registers) and their count; a pass then only walks the list past the keypoints
     // that earlier queries hold (first[idx] < q). A query whose list runs out while more candidates
     // exist re-enumerates its window with the pass's gates (exact, rare).
     uint32_t L[MT_BLK_QPT][MT_BLK_LIST];
-    int cnt[MT_BLK_QPT], obs[MT_BLK_QPT], res[MT_BLK_QPT];
+    int cnt[MT_BLK_QPT], obs[MT_BLK_QPT], res[MT_BLK_QPT], qid[MT_BLK_QPT];
+    float qang[MT_BLK_QPT];
     unsigned long long npair = 0;
+    // every record of the thread read first, before the frame is staged (the two memory round trips
+    // overlap: from host memory they are ~7 us each), with the fields the commit needs
+    BlkQuery QS[MT_BLK_QPT];
 #pragma unroll
     for (int i = 0; i < MT_BLK_QPT; i++) {
         cnt[i] = 0;
-        obs[i] = 0;
         res[i] = -1;
+        qid[i] = -1;
+        qang[i] = 0.f;
+        QS[i].ok = false;
+        QS[i].obs = 0;
         const int q = tid + i * MT_BLK_NT;
+        if (q >= nq) continue;
+        const uint8_t* rec = (const uint8_t*)recs + (size_t)q * io.q_stride;
+        qid[i] = *(const int*)(rec + io.qid_off);
+        if (io.checkOri) qang[i] = *(const float*)(rec + io.qangle_off);
+        QS[i] = blk_load<MODE>(fr, recs, q, th, a0, a1, thFar);
+    }
+    if (tid < MT_HISTO) s_hist[tid] = 0;
+    if (tid < 2) s_cnt[tid] = 0;
+    blk_stage<MT_BLK_NT>(fr, gm, io.mvp_in, io.obs_in, s_kp, s_desc, s_be, s_blk, s_ang, s_first, s_ws);
+#pragma unroll
+    for (int i = 0; i < MT_BLK_QPT; i++) {
+        const int q = tid + i * MT_BLK_NT;
+        obs[i] = QS[i].obs;
 #pragma unroll
         for (int k = 0; k < MT_BLK_LIST; k++) L[i][k] = 0xFFFFFFFFu;
         if (q >= nq) continue;
-        const BlkQuery Q = blk_load<MODE>(fr, bg, recs, q, th, a0, a1, thFar);
-        obs[i] = Q.obs;
-        unsigned long long K[MT_BLK_LIST];
-#pragma unroll
-        for (int k = 0; k < MT_BLK_LIST; k++) K[k] = ~0ull;
-        int c = 0;
-        blk_enum<MODE>(Q, bg, s_kp, s_desc, s_bs, s_blk, [&](unsigned long long key, int) {
-            c++;
-#pragma unroll
-            for (int k = 0; k < MT_BLK_LIST; k++) {   // sorted insertion (a compare-swap chain)
-                const bool lt = key < K[k];
-                const unsigned long long t = K[k];
-                K[k] = lt ? key : t;
-                key = lt ? t : key;
-            }
-        });
+        const int c = blk_list<MODE>(QS[i], gm, s_kp, s_desc, s_be, s_blk, L[i]);
         npair += (unsigned)c;
         cnt[i] = c;
-#pragma unroll
-        for (int k = 0; k < MT_BLK_LIST; k++)
-            L[i][k] = K[k] == ~0ull ? 0xFFFFFFFFu
-                                    : (uint32_t)((K[k] >> 4) & 0x1FFFu) | (uint32_t)((K[k] & 15) << 13) |
-                                          (uint32_t)((K[k] >> 40) << 16);
     }
     int pass = 0;
     for (;; pass++) {
@@ -955,9 +1031,9 @@ __global__ __launch_bounds__(MT_BLK_NT) void k_sbp_block(FrameDev fr, int NB, co
             int result;
             if (found < (MODE == 0 ? 2 : 1) && cnt[i] > MT_BLK_LIST) {
                 // the list ran out: the window again, with this pass's gates
-                const BlkQuery Q = blk_load<MODE>(fr, bg, recs, q, th, a0, a1, thFar);
+                const BlkQuery Q = blk_load<MODE>(fr, recs, q, th, a0, a1, thFar);
                 unsigned long long k1 = ~0ull, k2 = ~0ull;
-                blk_enum<MODE>(Q, bg, s_kp, s_desc, s_bs, s_blk, [&](unsigned long long key, int idx) {
+                blk_enum<MODE>(Q, gm, s_kp, s_desc, s_be, s_blk, [&](unsigned long long key, int idx) {
                     if (fcur[idx] < q) return;
                     const bool lt1 = key < k1, lt2 = key < k2;   // selects, not a store through a chosen pointer
                     k2 = lt1 ? k1 : (lt2 ? key : k2);
@@ -993,17 +1069,28 @@ __global__ __launch_bounds__(MT_BLK_NT) void k_sbp_block(FrameDev fr, int NB, co
 #pragma unroll
     for (int i = 0; i < MT_BLK_QPT; i++) {
         const int q = tid + i * MT_BLK_NT;
-        bins[i] = 0;
+        bins[i] = -1;
         if (q >= nq || res[i] < 0) continue;
         atomicMax(&s_res[res[i]], q);
         nas++;
-        if (io.checkOri) {
-            const float qa = *(const float*)((const uint8_t*)recs + (size_t)q * io.q_stride + io.qangle_off);
-            bins[i] = mt_rot_bin(qa, fr.keys[res[i]].angle);
-            atomicAdd(&s_hist[bins[i]], 1);
+        if (io.checkOri) bins[i] = mt_rot_bin(qang[i], s_ang[res[i]]);
+    }
+    // per-wave counts, one LDS atomic per wave and distinct bin (the assignments of a frame fall in
+    // a few bins: same-address atomics from every lane serialise)
+    nas = wave_sum_dpp(nas);
+    if ((tid & 63) == 0 && nas) atomicAdd(&s_cnt[0], nas);
+    if (io.checkOri) {
+#pragma unroll
+        for (int i = 0; i < MT_BLK_QPT; i++) {
+            int b = bins[i];
+            for (unsigned long long act = __ballot(b >= 0); act; act = __ballot(b >= 0)) {
+                const int lead = __builtin_amdgcn_readlane(b, (int)__builtin_ctzll(act));
+                const unsigned long long same = __ballot(b == lead);
+                if ((tid & 63) == (int)__builtin_ctzll(same)) atomicAdd(&s_hist[lead], (int)__popcll(same));
+                if (b == lead) b = -1;
+            }
         }
     }
-    if (nas) atomicAdd(&s_cnt[0], nas);
     SYNC();
     if (tid == 0) s_keep = io.checkOri ? mt_three_maxima_keep(s_hist) : 0xFFFFFFFFu;
     SYNC();
@@ -1011,16 +1098,19 @@ __global__ __launch_bounds__(MT_BLK_NT) void k_sbp_block(FrameDev fr, int NB, co
 #pragma unroll
     for (int i = 0; i < MT_BLK_QPT; i++) {
         const int q = tid + i * MT_BLK_NT;
-        if (q >= nq || res[i] < 0 || ((s_keep >> bins[i]) & 1u)) continue;
+        if (q >= nq || res[i] < 0 || bins[i] < 0 || ((s_keep >> bins[i]) & 1u)) continue;
         s_res[res[i]] = -2;
+        io.mvp_out[res[i]] = -1;
         ndrop++;
     }
-    if (ndrop) atomicAdd(&s_cnt[1], ndrop);
+    ndrop = wave_sum_dpp(ndrop);
+    if ((tid & 63) == 0 && ndrop) atomicAdd(&s_cnt[1], ndrop);
     SYNC();
-    for (int k = tid; k < n; k += MT_BLK_NT) {
-        const int w = s_res[k];
-        if (w == -2) io.mvp_out[k] = -1;
-        else if (w >= 0) io.mvp_out[k] = *(const int*)((const uint8_t*)recs + (size_t)w * io.q_stride + io.qid_off);
+    // the last writer of each slot that no dropped entry cleared stores its record's id
+#pragma unroll
+    for (int i = 0; i < MT_BLK_QPT; i++) {
+        const int q = tid + i * MT_BLK_NT;
+        if (q < nq && res[i] >= 0 && s_res[res[i]] == q) io.mvp_out[res[i]] = qid[i];
     }
     if (io.stats && npair) {
         atomicAdd(&io.stats[0], npair);
@@ -1044,6 +1134,253 @@ __global__ __launch_bounds__(MT_BLK_NT) void k_sbp_block(FrameDev fr, int NB, co
         st[4] = io.seq;
         __threadfence_system();
     }
+}
+
+// ---- Large single-camera local-map searches (nq > MT_BLOCK_MAXQ, frame in LDS): k_sbp_block's design
+// over many workgroups. Pass 0 (k_sbp_multi0, one query per thread, every block stages the frame in
+// LDS) enumerates each query's window ONCE and keeps its MT_BLK_LIST smallest keys in memory, with
+// the queries that have any candidate in an active list; a later pass (k_sbp_multi) walks only the
+// active queries' lists past the keypoints earlier queries hold (a list that runs out re-enumerates
+// the window over block 0's copy of the LDS frame in memory: exact, rare) and needs no frame at all.
+// The first[] states, last writers and change flags carry the pass's generation (a per-call base +
+// the pass), so nothing is cleared between passes or calls. The last block of a pass to finish
+// commits when the pass changed nothing (slot writes, status words) and otherwise reports "not
+// converged" when it ends the host's batch.
+struct MultiIO {
+    const int32_t* mvp_in;     // slots before the search (device)
+    const int32_t* obs_in;     // Observations() per slot
+    int32_t* mvp_out;          // slots after the search (device; may alias mvp_in)
+    int q_stride, qid_off;
+    const int* ntm;            // k_frustum's nToMatch (nullptr: none)
+    int* assign;               // [nq] result of the latest pass that ran the query
+    uint32_t* lists;           // [nq][MT_BLK_LIST]
+    int* lcnt;                 // [nq] candidate count | (Observations() > 0) << 31
+    int* active;               // queries with candidates
+    int* nactive;
+    unsigned long long* first[2];   // generation-tagged first[] states (pass parity)
+    unsigned long long* lastw;      // generation-tagged last assigner per slot
+    unsigned long long* changed;    // [MT_MAX_PASSES] generation of a pass that changed something
+    int* done;                 // [MT_MAX_PASSES] finished blocks (reset by the last one)
+    int* cnt;                  // [MT_MAX_PASSES] assigned queries (reset by the last block)
+    float4* g_kp;              // block 0's LDS frame, for the re-enumerations
+    uint4* g_desc;
+    int* g_be;
+    uint8_t* g_blk;
+    int* st_host;
+    int seq;
+    unsigned long long gen0;   // generation of pass 0
+    unsigned long long* stats;
+};
+// first[]: gen << 24 | (2^24 - 1 - q), atomicMax keeps the newest generation's smallest query; an
+// entry of another generation reads as free (MT_INF). Last writer: gen << 24 | q.
+__device__ __forceinline__ unsigned long long mt_ftag(unsigned long long gen, int q) {
+    return (gen << 24) | (unsigned long long)(0xFFFFFF - q);
+}
+__device__ __forceinline__ int mt_fget(unsigned long long v, unsigned long long gen) {
+    return (v >> 24) == gen ? 0xFFFFFF - (int)(v & 0xFFFFFFull) : MT_INF;
+}
+__device__ __forceinline__ void multi_publish(const MultiIO& io, unsigned long long* fnext, unsigned long long gen,
+                                              int q, int result, bool hasobs) {
+    if (hasobs) {
+        const unsigned long long t = mt_ftag(gen + 1, q);
+        if (t > __atomic_load_n(&fnext[result], __ATOMIC_RELAXED)) atomicMax(&fnext[result], t);
+    }
+    atomicMax(&io.lastw[result], (gen << 24) | (unsigned long long)q);
+}
+// end of pass p: this block's counts and flag, then the last block to finish commits or reports
+template <int NT>
+__device__ void multi_pass_end(const MultiIO& io, const orbfe_map_point* recs, int n, int p, int final_, int nas,
+                               bool ch, unsigned long long npair) {
+    __shared__ int s_last, s_nas, s_ch;
+    const int tid = threadIdx.x;
+    const unsigned long long gen = io.gen0 + (unsigned long long)p;
+    // everything the last block reads is an atomic (performed device-wide, no cache write-back
+    // needed): counts, the change flag, the last writers; a device-scope release per block wrote
+    // back a whole L2 each time and cost more than the pass. The block's counts are summed in LDS
+    // first: same-address global atomics serialise at the memory side (one per wave was thousands
+    // per pass)
+    if (tid == 0) s_nas = s_ch = 0;
+    SYNC();
+    nas = wave_sum_dpp(nas);
+    if ((tid & 63) == 0 && nas) atomicAdd(&s_nas, nas);
+    if (__ballot(ch) && (tid & 63) == 0) s_ch = 1;
+    if (io.stats && npair) atomicAdd(&io.stats[1], npair);
+    // every wave's atomics acknowledged, the barrier, the block's counts, the ticket
+    __builtin_amdgcn_s_waitcnt(0);
+    SYNC();
+    if (tid == 0) {
+        if (s_nas) atomicAdd(&io.cnt[p], s_nas);
+        if (s_ch) atomicMax(&io.changed[p], gen);
+        __builtin_amdgcn_s_waitcnt(0);
+        s_last = atomicAdd(&io.done[p], 1) == (int)gridDim.x - 1;
+    }
+    SYNC();
+    if (!s_last) return;
+    // agent-scope loads (sc1): the atomics' values, not this XCD's cached lines
+    const bool conv = __hip_atomic_load(&io.changed[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen;
+    if (conv)
+#pragma unroll 4
+        for (int k = tid; k < n; k += NT) {
+            const unsigned long long v = __hip_atomic_load(&io.lastw[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((v >> 24) == gen)
+                io.mvp_out[k] = *(const int*)((const uint8_t*)recs + (size_t)(v & 0xFFFFFFull) * io.q_stride + io.qid_off);
+        }
+    __builtin_amdgcn_s_waitcnt(0);
+    SYNC();
+    if (tid == 0) {
+        if (conv || final_) {
+            __threadfence_system();
+            if (io.stats) io.stats[2] = (unsigned long long)(p + 1);
+            volatile int* st = io.st_host;
+            st[0] = conv ? 0 : 1;
+            st[1] = __hip_atomic_load(&io.cnt[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            st[2] = 0;
+            st[3] = p + 1;
+            st[5] = io.ntm ? *io.ntm : 0;
+            __threadfence_system();
+            st[4] = io.seq;
+            __threadfence_system();
+        }
+        __hip_atomic_store(&io.done[p], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&io.cnt[p], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (conv) __hip_atomic_store(io.nactive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+__global__ __launch_bounds__(MT_BLK_NT) void k_sbp_multi0(FrameDev fr, BlkGeom gm, const orbfe_map_point* recs, int nq,
+                                                          float th, int bFar, float thFar, float nnratio, int final_,
+                                                          MultiIO io) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t mt_sm[];
+    const int n = fr.n, nbk = fr.nlevels * gm.NB * gm.NS, tid = threadIdx.x;
+    float4* s_kp = (float4*)mt_sm;
+    uint4* s_desc = (uint4*)(s_kp + n);
+    int* s_be = (int*)(s_desc + 2 * n);
+    uint8_t* s_blk = (uint8_t*)(s_be + nbk + 1);
+    __shared__ int s_ws[MT_BLK_NT / 64];
+    // the first round's records are read before the frame is staged: both memory round trips overlap
+    BlkQuery Q0;
+    Q0.ok = false;
+    Q0.obs = 0;
+    if (blockIdx.x * MT_BLK_NT + tid < nq) Q0 = blk_load<0>(fr, recs, blockIdx.x * MT_BLK_NT + tid, th, bFar, 0, thFar);
+    blk_stage<MT_BLK_NT>(fr, gm, io.mvp_in, io.obs_in, s_kp, s_desc, s_be, s_blk, nullptr, nullptr, s_ws);
+    if (blockIdx.x == 0) {   // the frame as staged, for later passes' re-enumerations
+        for (int i = tid; i < n; i += MT_BLK_NT) {
+            io.g_kp[i] = s_kp[i];
+            io.g_desc[2 * i] = s_desc[2 * i];
+            io.g_desc[2 * i + 1] = s_desc[2 * i + 1];
+            io.g_blk[i] = s_blk[i];
+        }
+        for (int b = tid; b <= nbk; b += MT_BLK_NT) io.g_be[b] = s_be[b];
+    }
+    const unsigned long long gen = io.gen0;
+    int nas = 0;
+    bool ch = false;
+    unsigned long long npair = 0;
+    __shared__ int s_acnt, s_abase;
+    // block-uniform trip count (the active list is compacted per block: one global atomic per block
+    // and round instead of one per wave)
+    for (int q0 = blockIdx.x * MT_BLK_NT; q0 < nq; q0 += gridDim.x * MT_BLK_NT) {
+        const int q = q0 + tid;
+        BlkQuery Q = Q0;
+        if (q0 != blockIdx.x * MT_BLK_NT) {
+            Q.ok = false;
+            Q.obs = 0;
+            if (q < nq) Q = blk_load<0>(fr, recs, q, th, bFar, 0, thFar);
+        }
+        uint32_t L[MT_BLK_LIST];
+        const int c = blk_list<0>(Q, gm, s_kp, s_desc, s_be, s_blk, L);
+        int result = -1;
+        if (c > 0) {
+            uint4* lp = (uint4*)(io.lists + (size_t)q * MT_BLK_LIST);
+            lp[0] = make_uint4(L[0], L[1], L[2], L[3]);
+            lp[1] = make_uint4(L[4], L[5], L[6], L[7]);
+            io.lcnt[q] = c | (Q.obs > 0 ? (int)0x80000000 : 0);
+            // pass 0: no earlier query holds anything, the list's head decides
+            result = blk_accept<0>((int)(L[0] & 0x1FFFu), (int)(L[0] >> 16), (int)((L[0] >> 13) & 7),
+                                   L[1] != 0xFFFFFFFFu ? (int)(L[1] >> 16) : 256,
+                                   L[1] != 0xFFFFFFFFu ? (int)((L[1] >> 13) & 7) : -1, nnratio, 0);
+            npair += (unsigned)c;
+        }
+        // the active list: wave offsets from an LDS counter, one global reservation per block
+        if (tid == 0) s_acnt = 0;
+        SYNC();
+        const unsigned long long am = __ballot(c > 0);
+        int woff = 0;
+        if ((tid & 63) == 0 && am) woff = atomicAdd(&s_acnt, (int)__popcll(am));
+        woff = __shfl(woff, 0);
+        SYNC();
+        if (tid == 0) s_abase = s_acnt ? atomicAdd(io.nactive, s_acnt) : 0;
+        SYNC();
+        if (c > 0) io.active[s_abase + woff + lanes_below(am)] = q;
+        if (q < nq) io.assign[q] = result;
+        if (result >= 0) {
+            nas++;
+            ch = true;
+            multi_publish(io, io.first[1], gen, q, result, Q.obs > 0);
+        }
+    }
+    multi_pass_end<MT_BLK_NT>(io, recs, n, 0, final_, nas, ch, npair);
+}
+#define MT_MULTI_NT 256
+#define MT_MULTI_TH 4.0f   // k_sbp_multi0 / k_sbp_multi below this th
+__global__ __launch_bounds__(MT_MULTI_NT) void k_sbp_multi(FrameDev fr, BlkGeom gm, const orbfe_map_point* recs,
+                                                           float th, int bFar, float thFar, float nnratio, int p,
+                                                           int final_, MultiIO io) {
+    const unsigned long long gen = io.gen0 + (unsigned long long)p;
+    if (__atomic_load_n(&io.changed[p - 1], __ATOMIC_RELAXED) != gen - 1) return;   // converged at p - 1
+    const unsigned long long* fcur = io.first[p & 1];
+    unsigned long long* fnext = io.first[(p + 1) & 1];
+    const int na = __hip_atomic_load(io.nactive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int nas = 0;
+    bool ch = false;
+    for (int i = blockIdx.x * MT_MULTI_NT + threadIdx.x; i < na; i += gridDim.x * MT_MULTI_NT) {
+        const int q = io.active[i];
+        const int prev = io.assign[q];
+        const int lc = io.lcnt[q];
+        const int c = lc & 0x7FFFFFFF;
+        const uint4* lp = (const uint4*)(io.lists + (size_t)q * MT_BLK_LIST);
+        const uint4 l0 = lp[0], l1 = lp[1];
+        const uint32_t L[MT_BLK_LIST] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+        bool free_[MT_BLK_LIST];
+#pragma unroll
+        for (int k = 0; k < MT_BLK_LIST; k++)
+            free_[k] = L[k] != 0xFFFFFFFFu && mt_fget(fcur[L[k] & 0x1FFFu], gen) >= q;
+        uint32_t e1 = 0xFFFFFFFFu, e2 = 0xFFFFFFFFu;
+        int found = 0;
+#pragma unroll
+        for (int k = 0; k < MT_BLK_LIST; k++) {
+            if (!free_[k] || found >= 2) continue;
+            if (found == 0) e1 = L[k];
+            else e2 = L[k];
+            found++;
+        }
+        int result;
+        if (found < 2 && c > MT_BLK_LIST) {
+            // the list ran out: the window again, over block 0's frame copy, with this pass's gates
+            const BlkQuery Q = blk_load<0>(fr, recs, q, th, bFar, 0, thFar);
+            unsigned long long k1 = ~0ull, k2 = ~0ull;
+            blk_enum<0>(Q, gm, io.g_kp, io.g_desc, io.g_be, io.g_blk, [&](unsigned long long key, int idx) {
+                if (mt_fget(fcur[idx], gen) < q) return;
+                const bool lt1 = key < k1, lt2 = key < k2;
+                k2 = lt1 ? k1 : (lt2 ? key : k2);
+                k1 = lt1 ? key : k1;
+            });
+            result = blk_accept<0>(k1 != ~0ull ? (int)((k1 >> 4) & 0x1FFFu) : -1, (int)(k1 >> 40), (int)(k1 & 15),
+                                   k2 != ~0ull ? (int)(k2 >> 40) : 256, k2 != ~0ull ? (int)(k2 & 15) : -1, nnratio, 0);
+        } else {
+            result = blk_accept<0>(e1 != 0xFFFFFFFFu ? (int)(e1 & 0x1FFFu) : -1, (int)(e1 >> 16), (int)((e1 >> 13) & 7),
+                                   e2 != 0xFFFFFFFFu ? (int)(e2 >> 16) : 256,
+                                   e2 != 0xFFFFFFFFu ? (int)((e2 >> 13) & 7) : -1, nnratio, 0);
+        }
+        if (result != prev) {
+            io.assign[q] = result;
+            ch = true;
+        }
+        if (result >= 0) {
+            nas++;
+            multi_publish(io, fnext, gen, q, result, lc < 0);
+        }
+    }
+    multi_pass_end<MT_MULTI_NT>(io, recs, fr.n, p, final_, nas, ch, 0);
 }
 
 // ---- SearchByProjection(CurrentFrame, LastFrame, ...) (ORBmatcher.cc:1676-1887) and
@@ -1845,6 +2182,11 @@ struct MatchScratch {
     // that is a different stream (ms_after_tail), so the shared scratch is never reused early.
     hipEvent_t tail = nullptr;
     hipStream_t tail_stream = nullptr;
+    // sbp_multi_run's persistent state (MultiBuf), the generation of the next call's pass 0 (tags of
+    // 0 never match) and whether an unfinished call may have left its counters set
+    uint8_t* mbuf = nullptr;
+    unsigned long long gen = MT_MAX_PASSES;
+    bool mdirty = false;
     // Deliberately never freed: thread_local destructors of the main thread can run after the HIP
     // runtime has been torn down at exit; the arena is reused for the thread's lifetime.
 };
@@ -1906,10 +2248,10 @@ int ms_prepare(const Plan& p, bool zero_copy = false) {
         m = MatchScratch();
         m.device = dev;
         HIPCHK(hipStreamCreateWithFlags(&m.stream, hipStreamNonBlocking));
-        HIPCHK(hipHostMalloc((void**)&m.hs, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostMalloc((void**)&m.hs, 128, hipHostMallocMapped | hipHostMallocCoherent));
         // the status words are compared against sequence numbers: start from zeros, not from
         // whatever the allocation held
-        memset(m.hs, 0, 64);
+        memset(m.hs, 0, 128);
         HIPCHK(hipHostGetDevicePointer((void**)&m.hs_dev, m.hs, 0));
         HIPCHK(hipEventCreateWithFlags(&m.tail, hipEventDisableTiming));
     }
@@ -2110,10 +2452,28 @@ struct DevIn {
     hipStream_t caller;
 };
 
+// k_sbp_block's bucket geometry for a frame: bands of 16 rows, then as many column strips (<= 32, >= 24
+// columns wide) as 8192 buckets and the LDS allow; false: the frame does not fit the block form
+size_t blk_lds(int n, int nlev, const BlkGeom& gm) {
+    return ((size_t)n * 61 + (size_t)(nlev * gm.NB * gm.NS + 1) * 4 + 15) & ~(size_t)15;
+}
+bool blk_geom(const orbfe_frame* F, BlkGeom& gm) {
+    constexpr int BR = 16;
+    if (!(F->max_y > 0.f && F->max_y < 65536.f && F->max_x > 0.f && F->max_x < 65536.f)) return false;
+    gm.NB = (int)std::floor(F->max_y / BR) + 2;
+    gm.inv_br = 1.0f / BR;
+    const int lev_bands = F->nlevels * gm.NB;
+    const long budget = std::min<long>(8192, ((long)MT_LDS_MAX - 61L * F->n - 4) / 4);
+    gm.NS = (int)std::min<long>(std::min<long>(32, budget / std::max(lev_bands, 1)), (long)std::ceil(F->max_x / 24.f));
+    if (gm.NS < 1) return false;
+    gm.inv_sw = (float)gm.NS / (F->max_x + 1.f);
+    return blk_lds(F->n, F->nlevels, gm) <= MT_LDS_MAX;
+}
+
 // sbp_run's one-launch form (k_sbp_block): arguments already validated by sbp_run.
 int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, const void* queries, int nq,
                   size_t qstride, size_t qid_off, size_t qangle_off, float th, int a0, int a1, float thFar,
-                  float nnratio, int maxDist, int checkOri, int band_nb, const FrustumIn* fin, const DevIn* dev) {
+                  float nnratio, int maxDist, int checkOri, const BlkGeom& gm, const FrustumIn* fin, const DevIn* dev) {
     const int n = F->n;
     Plan p;
     FramePlan fp;
@@ -2169,16 +2529,15 @@ int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* m
     if (zc) memcpy(m.ho, mvp, (size_t)n * 4);   // the slots the search leaves alone keep their value
     const BlkIO io{mvp_in, obs_d, mvp_out, (int)qstride, (int)qid_off, (int)qangle_off, checkOri, ntm, t_ms.hs_dev, seq,
                    stats};
-    const int nbk = F->nlevels * band_nb;
-    const size_t lds = ((size_t)n * 57 + (size_t)nbk * 8 + 4 + 15) & ~(size_t)15;
+    const size_t lds = blk_lds(n, F->nlevels, gm);
     if (mode == 0)
-        hipLaunchKernelGGL(k_sbp_block<0>, dim3(1), dim3(MT_BLK_NT), lds, s, fr, band_nb, (const void*)q, nq, th, a0, a1,
+        hipLaunchKernelGGL(k_sbp_block<0>, dim3(1), dim3(MT_BLK_NT), lds, s, fr, gm, (const void*)q, nq, th, a0, a1,
                            thFar, nnratio, maxDist, 1, io);
     else if (mode == 1)
-        hipLaunchKernelGGL(k_sbp_block<1>, dim3(1), dim3(MT_BLK_NT), lds, s, fr, band_nb, (const void*)q, nq, th, a0, a1,
+        hipLaunchKernelGGL(k_sbp_block<1>, dim3(1), dim3(MT_BLK_NT), lds, s, fr, gm, (const void*)q, nq, th, a0, a1,
                            thFar, nnratio, maxDist, 1, io);
     else
-        hipLaunchKernelGGL(k_sbp_block<2>, dim3(1), dim3(MT_BLK_NT), lds, s, fr, band_nb, (const void*)q, nq, th, a0, a1,
+        hipLaunchKernelGGL(k_sbp_block<2>, dim3(1), dim3(MT_BLK_NT), lds, s, fr, gm, (const void*)q, nq, th, a0, a1,
                            thFar, nnratio, maxDist, 0, io);
     HIPCHK(hipGetLastError());
     if (dev) {
@@ -2206,6 +2565,172 @@ int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* m
         t_last_stats[2] = (long long)hst[2];
     }
     return st[1] - st[2];
+}
+
+// the multi-block local-map search's persistent state (MatchScratch::mbuf): generation-tagged arrays
+// and self-resetting counters, zeroed once at allocation
+struct MultiBuf {
+    static constexpr size_t kFirst = (size_t)MT_BAND_MAXN * 8;
+    static constexpr size_t off_first0 = 0, off_first1 = kFirst, off_lastw = 2 * kFirst;
+    static constexpr size_t off_changed = 3 * kFirst;
+    static constexpr size_t off_done = off_changed + (size_t)MT_MAX_PASSES * 8;
+    static constexpr size_t off_cnt = off_done + (size_t)MT_MAX_PASSES * 4;
+    static constexpr size_t off_nactive = off_cnt + (size_t)MT_MAX_PASSES * 4;
+    static constexpr size_t counters = off_done, counters_bytes = off_nactive + 256 - off_done;
+    static constexpr size_t bytes = off_nactive + 256;
+};
+size_t multi_lds(int n, int nlev, const BlkGeom& gm) {
+    return ((size_t)n * 49 + (size_t)(nlev * gm.NB * gm.NS + 1) * 4 + 15) & ~(size_t)15;
+}
+
+// sbp_run's multi-block form for single-camera local-map searches of more than MT_BLOCK_MAXQ points
+// (k_sbp_multi0 / k_sbp_multi): arguments already validated by sbp_run.
+int sbp_multi_run(const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, const void* queries, int nq,
+                  size_t qstride, size_t qid_off, float th, int a0, float thFar, float nnratio, const BlkGeom& gm,
+                  const FrustumIn* fin, const DevIn* dev) {
+    const int n = F->n;
+    const int nbk = F->nlevels * gm.NB * gm.NS;
+    Plan p;
+    FramePlan fp;
+    if (dev) fp.plan_dev(F, true);
+    else fp.plan(p, F, true, true);
+    const size_t o_q = dev ? 0 : fin ? p.upload(fin->pts, (size_t)nq * sizeof(orbfe_map_point_3d))
+                                     : p.upload(queries, (size_t)nq * qstride);
+    const size_t o_mvp = dev ? 0 : p.upload(mvp, (size_t)n * 4);
+    const size_t o_obs = dev ? 0 : p.upload(mvp_obs, (size_t)n * 4);
+    const size_t o_track = fin ? p.scratch((size_t)nq * sizeof(orbfe_map_point)) : 0;
+    const size_t o_ntm = fin ? p.scratch(16) : 0;
+    const size_t o_assign = p.scratch((size_t)nq * 4);
+    const size_t o_lists = p.scratch((size_t)nq * MT_BLK_LIST * 4);
+    const size_t o_lcnt = p.scratch((size_t)nq * 4);
+    const size_t o_active = p.scratch((size_t)nq * 4);
+    const size_t o_gkp = p.scratch((size_t)n * 16);
+    const size_t o_gdesc = p.scratch((size_t)n * 32);
+    const size_t o_gbe = p.scratch((size_t)(nbk + 1) * 4);
+    const size_t o_gblk = p.scratch((size_t)n);
+    const size_t o_stats = t_stats ? p.scratch(24) : 0;
+    int rc = ms_prepare(p);
+    if (rc) return rc;
+    MatchScratch& m = t_ms;
+    hipStream_t s = dev ? dev->caller : m.stream;
+    if (dev) HIPCHK(ms_after_tail(s));
+    if (!m.mbuf) {   // zeroed on the search's stream (a non-blocking stream does not wait for the null stream)
+        HIPCHK(hipMalloc(&m.mbuf, MultiBuf::bytes));
+        HIPCHK(hipMemsetAsync(m.mbuf, 0, MultiBuf::bytes, s));
+        m.mdirty = false;
+    }
+    if (m.mdirty) {   // an earlier call ended early: its counters may not have been reset
+        HIPCHK(hipMemsetAsync(m.mbuf + MultiBuf::counters, 0, MultiBuf::counters_bytes, s));
+        m.mdirty = false;
+    }
+    unsigned long long* stats = t_stats ? ms_ptr<unsigned long long>(o_stats) : nullptr;
+    t_last_stats[0] = t_last_stats[1] = t_last_stats[2] = -1;
+    if (stats) HIPCHK(hipMemsetAsync(stats, 0, 24, s));
+    MsTimer timer(s);
+    const FrameDev fr = fp.view();
+    const uint8_t* q = dev ? (const uint8_t*)(fin ? (const void*)fin->pts : queries) : ms_ptr<const uint8_t>(o_q);
+    int* ntm = fin ? ms_ptr<int>(o_ntm) : nullptr;
+    if (fin) {   // Tracking::SearchLocalPoints' isInFrustum, then the search
+        CamDev cd;
+        if (!make_camdev(F, fin->cam, fin->rig, cd)) return ORBFE_E_ARG;
+        HIPCHK(hipMemsetAsync(ntm, 0, 4, s));
+        hipLaunchKernelGGL(k_frustum, dim3((nq + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, cd,
+                           (const orbfe_map_point_3d*)q, nq, ms_ptr<orbfe_map_point>(o_track), ntm);
+        q = ms_ptr<const uint8_t>(o_track);
+        qstride = sizeof(orbfe_map_point);
+        qid_off = offsetof(orbfe_map_point, id);
+    }
+    uint8_t* mb = m.mbuf;
+    MultiIO io;
+    io.mvp_in = dev ? mvp : ms_ptr<const int32_t>(o_mvp);
+    io.obs_in = dev ? mvp_obs : ms_ptr<const int32_t>(o_obs);
+    io.mvp_out = dev ? mvp : ms_ptr<int32_t>(o_mvp);
+    io.q_stride = (int)qstride;
+    io.qid_off = (int)qid_off;
+    io.ntm = ntm;
+    io.assign = ms_ptr<int>(o_assign);
+    io.lists = ms_ptr<uint32_t>(o_lists);
+    io.lcnt = ms_ptr<int>(o_lcnt);
+    io.active = ms_ptr<int>(o_active);
+    io.nactive = (int*)(mb + MultiBuf::off_nactive);
+    io.first[0] = (unsigned long long*)(mb + MultiBuf::off_first0);
+    io.first[1] = (unsigned long long*)(mb + MultiBuf::off_first1);
+    io.lastw = (unsigned long long*)(mb + MultiBuf::off_lastw);
+    io.changed = (unsigned long long*)(mb + MultiBuf::off_changed);
+    io.done = (int*)(mb + MultiBuf::off_done);
+    io.cnt = (int*)(mb + MultiBuf::off_cnt);
+    io.g_kp = ms_ptr<float4>(o_gkp);
+    io.g_desc = ms_ptr<uint4>(o_gdesc);
+    io.g_be = ms_ptr<int>(o_gbe);
+    io.g_blk = ms_ptr<uint8_t>(o_gblk);
+    io.st_host = m.hs_dev;
+    io.stats = stats;
+    io.gen0 = m.gen;
+    m.gen += MT_MAX_PASSES;
+    const orbfe_map_point* recs = (const orbfe_map_point*)q;
+    const int nb0 = std::min((nq + MT_BLK_NT - 1) / MT_BLK_NT, 1024);
+    // later passes walk the active queries (a fraction of nq): each thread's chain of dependent
+    // loads (list -> gates) is the pass's latency, so more blocks (32: 10.8 us per pass, 128: 8.1)
+    const int nb1 = std::min((nq + MT_MULTI_NT - 1) / MT_MULTI_NT, 256);
+    const size_t lds = multi_lds(n, F->nlevels, gm);
+    // passes per round trip: as many as the previous search needed, plus one (a gated pass is one
+    // short dispatch; another round trip costs far more)
+    int batch = std::min(std::max(m.pass_hint[0] + 1, 2), 8);
+    int pass = 0;
+    volatile int* st = m.hs;
+    while (true) {
+        io.seq = ++m.seq;
+        for (int c = 0; c < batch; c++, pass++) {
+            if (pass >= MT_MAX_PASSES) {
+                m.mdirty = true;
+                return ORBFE_E_CAPACITY;
+            }
+            const int final_ = c == batch - 1;
+            if (pass == 0)
+                hipLaunchKernelGGL(k_sbp_multi0, dim3(nb0), dim3(MT_BLK_NT), lds, s, fr, gm, recs, nq, th, a0, thFar,
+                                   nnratio, final_, io);
+            else
+                hipLaunchKernelGGL(k_sbp_multi, dim3(nb1), dim3(MT_MULTI_NT), 0, s, fr, gm, recs, th, a0, thFar,
+                                   nnratio, pass, final_, io);
+        }
+        HIPCHK(hipGetLastError());
+        if (dev) {
+            HIPCHK(hipEventRecord(m.tail, s));
+            m.tail_stream = s;
+        }
+        timer.end();
+        for (unsigned spin = 1; st[4] != io.seq; spin++) {
+            if ((spin & 1023) == 0) {   // bounded: a stream that finished without publishing is an error
+                const hipError_t e = hipStreamQuery(s);
+                if (e == hipSuccess && st[4] != io.seq) {
+                    m.mdirty = true;
+                    return ORBFE_E_DEVICE;
+                }
+                if (e != hipSuccess && e != hipErrorNotReady) {
+                    m.mdirty = true;
+                    HIPCHK(e);
+                }
+            }
+            __builtin_ia32_pause();
+        }
+        if (st[0] == 0) break;
+        batch = 6;
+    }
+    m.pass_hint[0] = st[3];
+    if (!dev) {
+        HIPCHK(hipMemcpyAsync(mvp, io.mvp_out, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    if (fin && fin->n_to_match) *fin->n_to_match = st[5];
+    if (stats) {   // counting mode only: one more copy and synchronisation
+        unsigned long long hst[3];
+        HIPCHK(hipMemcpyAsync(hst, stats, 24, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        t_last_stats[0] = (long long)hst[1];
+        t_last_stats[1] = (long long)hst[1];
+        t_last_stats[2] = (long long)hst[2];
+    }
+    return st[1];
 }
 
 int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, const void* queries, int nq,
@@ -2247,9 +2772,16 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     // large local-map search as one multi-block pass per fixed-point step (k_sbp_band)
     const int band_nb = std::min(std::max((int)std::floor(F->max_y * (1.0f / MT_BAND_ROWS)) + 2, 1), 4096);
     const bool band_ok = (size_t)F->nlevels * band_nb < 65535;   // 16-bit bucket keys
-    if (W == 1 && n <= MT_BAND_MAXN && nq <= MT_BLOCK_MAXQ && band_ok)
-        return sbp_block_run(mode, F, mvp, mvp_obs, queries, nq, qstride, qid_off, qangle_off, th, a0, a1, thFar,
-                             nnratio, maxDist, checkOri, band_nb, fin, dev);
+    BlkGeom gm;
+    if (W == 1 && n <= MT_BAND_MAXN && blk_geom(F, gm)) {
+        if (nq <= MT_BLOCK_MAXQ)
+            return sbp_block_run(mode, F, mvp, mvp_obs, queries, nq, qstride, qid_off, qangle_off, th, a0, a1, thFar,
+                                 nnratio, maxDist, checkOri, gm, fin, dev);
+        // narrow windows only: a wide window is a long serial walk for one thread, where k_sbp_band's
+        // sixteen lanes per query win (config 5: th 1 / 3 here, th 5 / 15 there; r05_kernel_ab.txt)
+        if (mode == 0 && th < MT_MULTI_TH)
+            return sbp_multi_run(F, mvp, mvp_obs, queries, nq, qstride, qid_off, th, a0, thFar, nnratio, gm, fin, dev);
+    }
     std::vector<int32_t> blocked0(dev ? 0 : n);
     for (int k = 0; !dev && k < n; k++) blocked0[k] = mode == 2 ? (mvp[k] >= 0) : (mvp[k] >= 0 && mvp_obs[k] > 0);
     Plan p;

@@ -2,7 +2,9 @@
 """Summarise a kernel (+ memory copy) trace of capi_frontend --latency: mean duration per kernel
 and the GPU timeline of one late frame (start offsets from the frame's first GPU op, durations,
 idle gaps), so the batch-1 critical path and its launch gaps can be read off.
-usage: dropin_timeline.py <rocprofv3 output dir>"""
+usage: dropin_timeline.py <rocprofv3 output dir> [--frame-after KERNEL]
+(--frame-after: a frame starts at the first host-to-device copy after KERNEL, e.g. k_sbp_block<0> for
+capi_frontend --tracking; default: after >= 100 us of GPU idleness)"""
 import collections
 import csv
 import glob
@@ -14,11 +16,12 @@ def kname(full):
     k = full.split("(")[0].replace("orbfe::", "")
     if k.startswith("void "):
         k = k[5:]
-    return k.split("<")[0].strip()
+    return k.strip()
 
 
 def main():
     d = sys.argv[1]
+    after = sys.argv[3] if len(sys.argv) > 3 and sys.argv[2] == "--frame-after" else None
     ops = []
     for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
@@ -35,8 +38,11 @@ def main():
     for k, v in sorted(per.items(), key=lambda x: -sum(x[1])):
         print(f"{k:16s} n={len(v):5d} mean={sum(v) / len(v):8.1f} us")
     # frames: a frame starts at an H2D copy that follows >= 100 us of GPU idleness
-    starts = [i for i, o in enumerate(ops) if o[2].startswith("copy_") and "HOST_TO_DEVICE" in o[2].upper()
-              and (i == 0 or o[0] - max(x[1] for x in ops[max(0, i - 40):i]) > 100e3)]
+    h2d = [i for i, o in enumerate(ops) if o[2].startswith("copy_") and "HOST_TO_DEVICE" in o[2].upper()]
+    if after:
+        starts = [i for i in h2d if i > 0 and ops[i - 1][2] == after]
+    else:
+        starts = [i for i in h2d if i == 0 or ops[i][0] - max(x[1] for x in ops[max(0, i - 40):i]) > 100e3]
     if len(starts) < 3:
         print("frames not found")
         return
