@@ -471,13 +471,15 @@ def matcher_config5(steps):
         wst = (ctypes.c_longlong * 3)()
         lib.orbfe_matcher_last_stats(wst)
         mp = (matcher_pmc or {}).get(f"th{th}", {})
-        # the pass kernel: the PMC pass's name when it covers this th, else by the library's switch
-        # (th >= 6: the wide-window kernel, four queries per wave)
-        kname = mp.get("kernel") or ("k_sbp_local_wq" if th >= 6 else "k_sbp_local")
+        # the search kernels: the PMC pass's names when it covers this th, else by the library's switch
+        # (th < 4: k_sbp_multi0 + k_sbp_multi, the list-based passes; wider windows: k_sbp_band)
+        kname = mp.get("kernel") or ("k_sbp_multi0+k_sbp_multi" if th < 4 else "k_sbp_band")
         out[f"th{th}"] = {"kernel": kname, "window_candidates": int(wst[0]), "pairs": int(wst[1]),
                           "passes": int(wst[2]), "pairs_per_s": round(wst[1] / (dms * 1e-3), 1),
                           "window_candidates_per_s": round(wst[0] / (dms * 1e-3), 1),
-                          "valu_issue_frac": mp.get("valu_issue_frac"), "pmc_source": mp.get("source"),"ms_per_call": round(dt * 1e3, 4), "calls_per_s": round(1.0 / dt, 2),
+                          "valu_issue_frac": mp.get("valu_issue_frac"), "pmc_source": mp.get("source"),
+                          "valu_per_pair": (round(mp["valu_per_call"] / max(int(wst[1]), 1), 2)
+                                            if mp.get("valu_per_call") else None),"ms_per_call": round(dt * 1e3, 4), "calls_per_s": round(1.0 / dt, 2),
                           "queries_per_s": round(len(mps) / dt, 1), "device_ms_per_call": round(dms, 4),
                           "device_queries_per_s": round(len(mps) / (dms * 1e-3), 1),
                           "resident_ms_per_call": round(rdt * 1e3, 4),

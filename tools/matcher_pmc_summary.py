@@ -24,7 +24,7 @@ for th in (1, 3, 5, 15):
         if i == 1:
             for f in glob.glob(os.path.join(root, f"mp_th{th}_{i}", "**", "*kernel_trace.csv"), recursive=True):
                 for r in csv.DictReader(open(f)):
-                    if "k_sbp_local" in r["Kernel_Name"]:
+                    if any(k in r["Kernel_Name"] for k in ("k_sbp_local", "k_sbp_band", "k_sbp_multi")):
                         dur += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
                         ndisp += 1
     if not dur:
