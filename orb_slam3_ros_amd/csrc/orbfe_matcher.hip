@@ -822,16 +822,26 @@ __device__ __forceinline__ int blk_accept(int bestIdx, int bestDist, int bestLev
 }
 
 #define MT_BLK_LIST 8   // candidates kept per query: the smallest keys, as u32 idx | octave << 13 | dist << 16
+// Bucket bounds region: 4 zero words, then one counter per bucket padded to a multiple of 4 NT (each
+// thread scans a run of whole int4s); after the placement, word 4 + c = end of bucket c, so the
+// enumeration's bounds array ("be", be[c] = start of c, be[c + 1] = end) is region + 3.
+__host__ __device__ __forceinline__ int blk_be_words(int nbk, int nt) {
+    const int per = ((nbk + nt - 1) / nt + 3) & ~3;
+    return per * nt + 4;
+}
 // k_sbp_block's / k_sbp_multi0's LDS frame: the (octave, band, strip) bucket index (counts, scan,
 // placement; the order inside a bucket is irrelevant: every candidate carries its enumeration rank),
 // keypoints {x, y, rank bits, uR} and descriptors by bucket position, blocked flags (and angles, the
-// first[] state, when given) by keypoint index. Ends with a barrier.
+// first[] state, when given) by keypoint index. s_be: the 16-byte aligned bounds region
+// (blk_be_words). Ends with a barrier.
 template <int NT>
 __device__ __forceinline__ void blk_stage(const FrameDev& fr, const BlkGeom& gm, const int32_t* mvp_in,
                                           const int32_t* obs_in, float4* s_kp, uint4* s_desc, int* s_be,
                                           uint8_t* s_blk, float* s_ang, int* s_first, int* s_ws) {
     const int n = fr.n, nlev = fr.nlevels, nbk = nlev * gm.NB * gm.NS, tid = threadIdx.x;
-    for (int b = tid; b <= nbk; b += NT) s_be[b] = 0;
+    const int per = ((nbk + NT - 1) / NT + 3) & ~3;   // buckets per thread in the scan (whole int4s)
+    for (int b = tid; b < (per * NT + 4) / 4; b += NT) ((int4*)s_be)[b] = make_int4(0, 0, 0, 0);
+    int* a = s_be + 4;   // counters, then starts, then ends
     SYNC();
     auto bucket_of = [&](float x, float y, int oct, int idx) {
         // a two-camera frame's single-camera searches read its left grid only (rows [0, nleft)); a
@@ -876,27 +886,33 @@ __device__ __forceinline__ void blk_stage(const FrameDev& fr, const BlkGeom& gm,
         const int idx = tid + u * NT;
         if (idx >= n) continue;
         rb[u] = bucket_of(kx[u], ky[u], koct[u], idx);
-        if (rb[u] >= 0) atomicAdd(&s_be[rb[u] + 1], 1);
+        if (rb[u] >= 0) atomicAdd(&a[rb[u]], 1);
     }
     SYNC();
-    // counts -> starts (be[c + 1] = start of c); the placement's atomic increments then leave be[c + 1]
-    // at the end of bucket c, i.e. the start of c + 1, with be[0] = 0. One segment of consecutive
-    // buckets per thread: one barrier instead of one pair per NT buckets.
+    // counts -> starts (a[c] = start of c); the placement's atomic increments then leave a[c] at the
+    // end of bucket c, i.e. the start of c + 1, with a[-1] = 0. One run of whole int4s per thread:
+    // one barrier, and 16-byte LDS accesses instead of per-word strided ones.
     {
-        int* a = s_be + 1;
-        const int per = (nbk + NT - 1) / NT, b0 = tid * per, b1 = min(b0 + per, nbk);
+        int4* a4 = (int4*)a + tid * (per >> 2);
         int sum = 0;
-        for (int b = b0; b < b1; b++) sum += a[b];
+        for (int j = 0; j < (per >> 2); j++) {
+            const int4 v = a4[j];
+            sum += v.x + v.y + v.z + v.w;
+        }
         const int incl = wave_incl_scan_dpp(sum);
         if ((tid & 63) == 63) s_ws[tid >> 6] = incl;
         SYNC();
         int run = incl - sum;
 #pragma unroll
         for (int w = 0; w < NT / 64; w++) run += w < (tid >> 6) ? s_ws[w] : 0;
-        for (int b = b0; b < b1; b++) {
-            const int v = a[b];
-            a[b] = run;
-            run += v;
+        for (int j = 0; j < (per >> 2); j++) {
+            const int4 v = a4[j];
+            int4 o;
+            o.x = run; run += v.x;
+            o.y = run; run += v.y;
+            o.z = run; run += v.z;
+            o.w = run; run += v.w;
+            a4[j] = o;
         }
     }
     SYNC();
@@ -908,7 +924,7 @@ __device__ __forceinline__ void blk_stage(const FrameDev& fr, const BlkGeom& gm,
         if (s_first) s_first[idx] = MT_INF;
         if (s_ang) s_ang[idx] = kang[u];
         if (rb[u] < 0) continue;
-        const int p = atomicAdd(&s_be[rb[u] + 1], 1);
+        const int p = atomicAdd(&a[rb[u]], 1);
         const int px = (int)roundf((kx[u] - fr.minx) * fr.invw);   // PosInGrid (Frame.cc:725-735)
         const int py = (int)roundf((ky[u] - fr.miny) * fr.invh);
         const uint32_t rank = ((uint32_t)(px * ORBFE_GRID_ROWS + py) << 13) | (uint32_t)idx;
@@ -954,10 +970,11 @@ __global__ __launch_bounds__(MT_BLK_NT) void k_sbp_block(FrameDev fr, BlkGeom gm
     const int nbk = nlev * gm.NB * gm.NS;
     float4* s_kp = (float4*)mt_sm;                 // {x, y, rank bits, uR} per bucket position
     uint4* s_desc = (uint4*)(s_kp + n);            // 2 x uint4 per bucket position
-    int* s_first = (int*)(s_desc + 2 * n);         // two first[] states by keypoint index (then the commit's slots)
+    int* s_ber = (int*)(s_desc + 2 * n);           // bucket bounds region (blk_be_words)
+    const int* s_be = s_ber + 3;                   // be[c] = start of bucket c, be[c + 1] = its end
+    int* s_first = s_ber + blk_be_words(nbk, MT_BLK_NT);   // two first[] states by keypoint index (then the commit's slots)
     float* s_ang = (float*)(s_first + 2 * n);      // keypoint angles by index (the rotation check)
-    int* s_be = (int*)(s_ang + n);                 // bucket bounds [nbk + 1]
-    uint8_t* s_blk = (uint8_t*)(s_be + nbk + 1);   // blocked initially, by keypoint index
+    uint8_t* s_blk = (uint8_t*)(s_ang + n);        // blocked initially, by keypoint index
     __shared__ int s_flag, s_ws[MT_BLK_NT / 64], s_hist[MT_HISTO], s_cnt[2];
     __shared__ unsigned s_keep;
     const int tid = threadIdx.x;
@@ -989,7 +1006,7 @@ __global__ __launch_bounds__(MT_BLK_NT) void k_sbp_block(FrameDev fr, BlkGeom gm
     }
     if (tid < MT_HISTO) s_hist[tid] = 0;
     if (tid < 2) s_cnt[tid] = 0;
-    blk_stage<MT_BLK_NT>(fr, gm, io.mvp_in, io.obs_in, s_kp, s_desc, s_be, s_blk, s_ang, s_first, s_ws);
+    blk_stage<MT_BLK_NT>(fr, gm, io.mvp_in, io.obs_in, s_kp, s_desc, s_ber, s_blk, s_ang, s_first, s_ws);
 #pragma unroll
     for (int i = 0; i < MT_BLK_QPT; i++) {
         const int q = tid + i * MT_BLK_NT;
@@ -1253,15 +1270,16 @@ __global__ __launch_bounds__(MT_BLK_NT) void k_sbp_multi0(FrameDev fr, BlkGeom g
     const int n = fr.n, nbk = fr.nlevels * gm.NB * gm.NS, tid = threadIdx.x;
     float4* s_kp = (float4*)mt_sm;
     uint4* s_desc = (uint4*)(s_kp + n);
-    int* s_be = (int*)(s_desc + 2 * n);
-    uint8_t* s_blk = (uint8_t*)(s_be + nbk + 1);
+    int* s_ber = (int*)(s_desc + 2 * n);           // bucket bounds region (blk_be_words)
+    const int* s_be = s_ber + 3;
+    uint8_t* s_blk = (uint8_t*)(s_ber + blk_be_words(nbk, MT_BLK_NT));
     __shared__ int s_ws[MT_BLK_NT / 64];
     // the first round's records are read before the frame is staged: both memory round trips overlap
     BlkQuery Q0;
     Q0.ok = false;
     Q0.obs = 0;
     if (blockIdx.x * MT_BLK_NT + tid < nq) Q0 = blk_load<0>(fr, recs, blockIdx.x * MT_BLK_NT + tid, th, bFar, 0, thFar);
-    blk_stage<MT_BLK_NT>(fr, gm, io.mvp_in, io.obs_in, s_kp, s_desc, s_be, s_blk, nullptr, nullptr, s_ws);
+    blk_stage<MT_BLK_NT>(fr, gm, io.mvp_in, io.obs_in, s_kp, s_desc, s_ber, s_blk, nullptr, nullptr, s_ws);
     if (blockIdx.x == 0) {   // the frame as staged, for later passes' re-enumerations
         for (int i = tid; i < n; i += MT_BLK_NT) {
             io.g_kp[i] = s_kp[i];
@@ -2455,7 +2473,7 @@ struct DevIn {
 // k_sbp_block's bucket geometry for a frame: bands of 16 rows, then as many column strips (<= 32, >= 24
 // columns wide) as 8192 buckets and the LDS allow; false: the frame does not fit the block form
 size_t blk_lds(int n, int nlev, const BlkGeom& gm) {
-    return ((size_t)n * 61 + (size_t)(nlev * gm.NB * gm.NS + 1) * 4 + 15) & ~(size_t)15;
+    return (size_t)n * 61 + (size_t)blk_be_words(nlev * gm.NB * gm.NS, MT_BLK_NT) * 4 + 16;
 }
 bool blk_geom(const orbfe_frame* F, BlkGeom& gm) {
     constexpr int BR = 16;
@@ -2466,6 +2484,7 @@ bool blk_geom(const orbfe_frame* F, BlkGeom& gm) {
     const long budget = std::min<long>(8192, ((long)MT_LDS_MAX - 61L * F->n - 4) / 4);
     gm.NS = (int)std::min<long>(std::min<long>(32, budget / std::max(lev_bands, 1)), (long)std::ceil(F->max_x / 24.f));
     if (gm.NS < 1) return false;
+    while (gm.NS > 1 && blk_lds(F->n, F->nlevels, gm) > MT_LDS_MAX) gm.NS--;   // the scan's padding
     gm.inv_sw = (float)gm.NS / (F->max_x + 1.f);
     return blk_lds(F->n, F->nlevels, gm) <= MT_LDS_MAX;
 }
@@ -2580,7 +2599,7 @@ struct MultiBuf {
     static constexpr size_t bytes = off_nactive + 256;
 };
 size_t multi_lds(int n, int nlev, const BlkGeom& gm) {
-    return ((size_t)n * 49 + (size_t)(nlev * gm.NB * gm.NS + 1) * 4 + 15) & ~(size_t)15;
+    return (size_t)n * 49 + (size_t)blk_be_words(nlev * gm.NB * gm.NS, MT_BLK_NT) * 4 + 16;
 }
 
 // sbp_run's multi-block form for single-camera local-map searches of more than MT_BLOCK_MAXQ points
