@@ -1233,8 +1233,24 @@ __device__ void multi_pass_end(const MultiIO& io, const orbfe_map_point* recs, i
     }
     SYNC();
     if (!s_last) return;
-    // agent-scope loads (sc1): the atomics' values, not this XCD's cached lines
-    const bool conv = __hip_atomic_load(&io.changed[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen;
+    // agent-scope loads (sc1): the atomics' values, not this XCD's cached lines. Converged when this
+    // pass changed no result, or when the first[] state it built for the next pass equals the one it
+    // read: the next pass would then compute exactly this pass's results (every result is a function
+    // of first[] and fixed data), so the pass that would only confirm it is never run
+    bool same = true;
+    {
+        const unsigned long long* fcur = io.first[p & 1];
+        const unsigned long long* fnext = io.first[(p + 1) & 1];
+        for (int k = tid; k < n && same; k += NT)
+            same = mt_fget(__hip_atomic_load(&fnext[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), gen + 1) ==
+                   mt_fget(__hip_atomic_load(&fcur[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), gen);
+    }
+    same = __syncthreads_and(same);
+    const bool conv = same || __hip_atomic_load(&io.changed[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen;
+    // the batch's later passes are gated on this pass's change word: clear it, or a pass that
+    // converged by the first[] test (its results did change) would let the next pass run and publish
+    // a second status for the same sequence number
+    if (conv && tid == 0) __hip_atomic_store(&io.changed[p], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (conv)
 #pragma unroll 4
         for (int k = tid; k < n; k += NT) {
