@@ -1168,22 +1168,29 @@ __device__ __forceinline__ void wave_introsort_impl(unsigned long long* a, int n
         WAVE_SYNC();
     }
     WAVE_SYNC();
-    // leaves were recorded left to right; stable rank sort inside each ordinary leaf
+    // leaves were recorded left to right; stable rank sort inside each ordinary leaf. Each leaf's
+    // lane first writes {start, end | heap flag} over its positions (fl), so an element finds its
+    // leaf in one read instead of a binary search of dependent reads
+    for (int L = tid; L < nleaf; L += 64) {
+        const int ls = leaves[L] & 0x7fffffff;
+        const int le = L + 1 < nleaf ? (leaves[L + 1] & 0x7fffffff) : n;
+        const int tag = ls | (le << 16) | (leaves[L] & 0x80000000);
+        for (int i = ls; i < le; i++) fl[i] = tag;
+    }
+    WAVE_SYNC();
     for (int i = tid; i < n; i += 64) {
-        int lo_i = 0, hi_i = nleaf - 1;   // last leaf with start <= i
-        while (lo_i < hi_i) {
-            const int mid = (lo_i + hi_i + 1) >> 1;
-            if ((leaves[mid] & 0x7fffffff) <= i) lo_i = mid; else hi_i = mid - 1;
-        }
-        const int ls = leaves[lo_i] & 0x7fffffff;
-        const int le = lo_i + 1 < nleaf ? (leaves[lo_i + 1] & 0x7fffffff) : n;
+        const int tag = fl[i];
+        const int ls = tag & 0xffff, le = (tag >> 16) & 0x7fff;
         const unsigned long long x = a[i];
-        if (leaves[lo_i] & 0x80000000) { tmp[i] = x; continue; }
+        if (tag & 0x80000000) { tmp[i] = x; continue; }
         const unsigned kx = (unsigned)(x >> 32);
+        // an ordinary leaf holds <= 16 elements: the reads issued together
         int r = 0;
-        for (int j = ls; j < le; j++) {
-            const unsigned kj = (unsigned)(a[j] >> 32);
-            r += (kj < kx || (kj == kx && j < i)) ? 1 : 0;
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            const int j = ls + u;
+            const unsigned kj = (unsigned)(a[min(j, n - 1)] >> 32);
+            r += (j < le && (kj < kx || (kj == kx && j < i))) ? 1 : 0;
         }
         tmp[ls + r] = x;
     }
@@ -1370,6 +1377,7 @@ __global__ __launch_bounds__(NT) void k_octree(OrbGeom g, const uint32_t* __rest
             // std::sort(vPrevSizeAndPointerToNode, compareNodes) (ORBextractor.cc:700), exact replica
             block_introsort(expv, m, tmpC, tmpA, tmpB, Xcnt + 2 * NC, (unsigned long long*)Xcnt, segs, s_ws,
                             s_misc);
+            OCT_STAMP();
             // walk from the back until the list reaches N (ORBextractor.cc:701-748): processed node t is
             // expv[m-1-t]; the list grows by (children - 1) per division -> first t where it reaches N
             for (int t = tid; t < m; t += NT) {

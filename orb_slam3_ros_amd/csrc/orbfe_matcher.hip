@@ -945,6 +945,7 @@ __device__ __forceinline__ int blk_list(const BlkQuery& Q, const BlkGeom& gm, co
     int c = 0;
     blk_enum<MODE>(Q, gm, kp, desc, be, blk, [&](unsigned long long key, int) {
         c++;
+        if (key >= K[MT_BLK_LIST - 1]) return;   // not among the 8 smallest so far (keys are unique)
 #pragma unroll
         for (int k = 0; k < MT_BLK_LIST; k++) {   // sorted insertion (a compare-swap chain)
             const bool lt = key < K[k];

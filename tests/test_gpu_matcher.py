@@ -567,3 +567,91 @@ def test_sbp_block_limit(gpu, om, nq):
     assert ORBmatcher(0.9, True).SearchByProjectionKeyFrame(F, a, pts, 10, 100) == \
         om.OracleMatcher(0.9, True).sbp_kf(F, b, pts, 10, 100)
     np.testing.assert_array_equal(a, b)
+
+
+def _crowded_case(seed, n_kp=1200, n_mps=6000, per=12):
+    """Clusters of `per` keypoints within a few pixels whose descriptors form a ladder (keypoint i
+    differs from keypoint 0 in 6 i bits) on alternating octaves 0 / 1, and per cluster `per` + 4
+    map points (level 1, Observations() > 0) with keypoint 0's descriptor: the j-th of them takes
+    keypoint j (alternating octaves skip the ratio test), so from the 9th on every point's 8-key
+    candidate list is taken by earlier points and k_sbp_multi re-enumerates its window."""
+    rng = np.random.default_rng(seed)
+    F = sm.synth_frame(rng, n_kp)
+    k = F.keys.copy()
+    desc = F.desc.copy()
+    ncl = n_kp // per
+    cx = rng.uniform(40, 700, ncl).astype(np.float32)
+    cy = rng.uniform(40, 440, ncl).astype(np.float32)
+    for c in range(ncl):
+        sl = slice(c * per, (c + 1) * per)
+        k["x"][sl] = cx[c] + rng.uniform(-2.0, 2.0, per).astype(np.float32)
+        k["y"][sl] = cy[c] + rng.uniform(-2.0, 2.0, per).astype(np.float32)
+        k["octave"][sl] = np.arange(per) % 2
+        bits = np.unpackbits(desc[c * per])
+        order = rng.permutation(256)
+        for i in range(per):
+            b = bits.copy()
+            b[order[:6 * i]] ^= 1
+            desc[c * per + i] = np.packbits(b)
+    F = MatchFrame(k, desc, F.bounds, F.scale_factors, None, F.mbf)
+    mps = sm.synth_local_map(rng, F, n_mps, copy_frac=0.0)
+    m = min(n_mps, ncl * (per + 4))
+    cl = np.arange(m) // (per + 4)
+    mps["proj_x"][:m] = cx[cl]
+    mps["proj_y"][:m] = cy[cl]
+    mps["scale_level"][:m] = 1
+    mps["view_cos"][:m] = 0.995            # radius 4 * th * scale[1]
+    mps["flags"][:m] = sm.MP_IN_VIEW
+    mps["observations"][:m] = rng.integers(1, 9, m)
+    mps["desc"][:m] = desc[cl * per]
+    perm = rng.permutation(n_mps)           # interleave the crowded points with the rest
+    return F, mps[perm]
+
+
+@pytest.mark.parametrize("th", [1, 3])
+def test_sbp_multi_lists_run_out(gpu, om, th):
+    """k_sbp_multi0 / k_sbp_multi (more than 2048 points, th < 4) when candidate lists run out: the
+    passes re-enumerate over block 0's frame copy with their gates. Host and device-resident calls
+    against the oracle."""
+    import torch
+    from orb_slam3_ros_amd.matcher import DeviceMatchFrame, search_by_projection_local_device
+    F, mps = _crowded_case(77 + th)
+    rng = np.random.default_rng(5)
+    mvp0, obs = sm.initial_slots(rng, F.N, 0.05)
+    a, b = mvp0.copy(), mvp0.copy()
+    ng = ORBmatcher(0.8).SearchByProjectionLocalMap(F, a, obs, mps, th)
+    no = om.OracleMatcher(0.8).sbp_local(F, b, obs, mps, th)
+    assert ng == no and no > 0
+    np.testing.assert_array_equal(a, b)
+    Fd = DeviceMatchFrame(F, gpu)
+    mvp_t = torch.from_numpy(mvp0.copy()).to(gpu)
+    nd = search_by_projection_local_device(Fd, mvp_t, torch.from_numpy(obs.copy()).to(gpu),
+                                           torch.from_numpy(mps.view(np.uint8).reshape(-1).copy()).to(gpu), th)
+    torch.cuda.synchronize()
+    assert nd == no
+    np.testing.assert_array_equal(mvp_t.cpu().numpy(), b)
+
+
+def test_sbp_multi_degenerate(gpu, om):
+    """The multi-block search with nothing to do: every keypoint held by a point with observations
+    (all blocked), and no point in view; both converge at pass 0 and leave the slots alone."""
+    rng = np.random.default_rng(31)
+    F = sm.synth_frame(rng, 1000)
+    mps = sm.synth_local_map(rng, F, 5000, copy_frac=0.5)
+    mvp = np.arange(F.N, dtype=np.int32) + 1
+    obs = np.full(F.N, 3, np.int32)
+    a = mvp.copy()
+    assert ORBmatcher(0.8).SearchByProjectionLocalMap(F, a, obs, mps, 1) == 0
+    np.testing.assert_array_equal(a, mvp)
+    mvp0, obs0 = sm.initial_slots(rng, F.N, 0.1)
+    off = mps.copy()
+    off["flags"] = 0
+    a, b = mvp0.copy(), mvp0.copy()
+    assert ORBmatcher(0.8).SearchByProjectionLocalMap(F, a, obs0, off, 1) == \
+        om.OracleMatcher(0.8).sbp_local(F, b, obs0, off, 1) == 0
+    np.testing.assert_array_equal(a, b)
+    # and a normal search right after (the counters the degenerate calls used are reset)
+    a, b = mvp0.copy(), mvp0.copy()
+    assert ORBmatcher(0.8).SearchByProjectionLocalMap(F, a, obs0, mps, 1) == \
+        om.OracleMatcher(0.8).sbp_local(F, b, obs0, mps, 1)
+    np.testing.assert_array_equal(a, b)
