@@ -1127,6 +1127,20 @@ int orbfe_debug_block_sort(uint64_t* data, int n) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(data, d, (size_t)n * 8, hipMemcpyDeviceToHost));
     HIPCHK(hipFree(d));
+#if ORBFE_OCT_STAMPS
+    {
+        unsigned long long ts[16 * 16];
+        HIPCHK(hipMemcpyFromSymbol(ts, HIP_SYMBOL(g_sort_ts), sizeof(ts)));
+        fprintf(stderr, "sortts n=%d", n);
+        for (int w = 0; w < OCT_NT / 64; w++) {
+            fprintf(stderr, " | w%d:", w);
+            for (int k = 1; k < (int)ts[w * 16 + 15] && k < 15; k++) fprintf(stderr, " %lld", (long long)(ts[w * 16 + k] - ts[0]));
+        }
+        fprintf(stderr, " | s64:");
+        for (int k = 1; k < (int)ts[8 * 16 + 15] && k < 15; k++) fprintf(stderr, " %lld", (long long)(ts[8 * 16 + k] - ts[8 * 16 + k - 1]));
+        fprintf(stderr, "\n");
+    }
+#endif
     return n;
 }
 

@@ -155,9 +155,9 @@ __device__ int wave_excl_scan_lds(int* arr, int n) {
     for (int base = 0; base < n; base += 64) {
         const int i = base + lane;
         const int v = i < n ? arr[i] : 0;
-        const int incl = wave_incl_scan(v);
+        const int incl = wave_incl_scan_dpp(v);
         if (i < n) arr[i] = carry + incl - v;
-        carry += __shfl(incl, 63, 64);
+        carry += __builtin_amdgcn_readlane(incl, 63);
     }
     SYNC();
     return carry;
@@ -1038,7 +1038,7 @@ __device__ __forceinline__ int block_excl_scan(int* arr, int n, int* s_ws) {
     for (int base = 0; base < n; base += NT) {
         const int i = base + threadIdx.x;
         const int v = i < n ? arr[i] : 0;
-        const int incl = wave_incl_scan(v);
+        const int incl = wave_incl_scan_dpp(v);
         if (lane == 63) s_ws[wave] = incl;
         SYNC();
         int woff = 0, tot = 0;
@@ -1055,12 +1055,34 @@ __device__ __forceinline__ int block_excl_scan(int* arr, int n, int* s_ws) {
     return carry;
 }
 
+// Block-wide exclusive scan of two per-thread values (thread = element, one element per thread):
+// one barrier. s_w2 must not be reused before the caller's next barrier.
+template <int NT>
+__device__ __forceinline__ void block_scan2(int a, int b, int2* s_w2, int& exa, int& exb, int& tota, int& totb) {
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    const int ia = wave_incl_scan_dpp(a), ib = wave_incl_scan_dpp(b);
+    if (lane == 63) s_w2[wave] = make_int2(ia, ib);
+    SYNC();
+    int oa = 0, ob = 0, ta = 0, tb = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; w++) {
+        const int2 t = s_w2[w];
+        oa += w < wave ? t.x : 0;
+        ob += w < wave ? t.y : 0;
+        ta += t.x;
+        tb += t.y;
+    }
+    exa = oa + ia - a;
+    exb = ob + ib - b;
+    tota = ta;
+    totb = tb;
+}
+
 // Block-parallel, element-for-element replica of libstdc++ std::sort on u64 elements ordered by
-// their high 32 bits (see stl_sort.h "Data-parallel formulation"). Segments are processed one at
-// a time by the whole block: median-of-three on one thread, then the unguarded partition as
-// stop-pairing with block scans; leaves (<= 16 elements) are stably sorted in parallel by rank;
-// depth-exhausted leaves fall back to the serial heapsort replica.
-// Scratch: fl, lpos, rpos, leaves: int[n]; tmp: u64[n]; segs: int4[ORBFE_SORT_STACK].
+// their high 32 bits (see stl_sort.h "Data-parallel formulation"): every wave of the block
+// partitions its own segments (median-of-three, then the unguarded partition as stop pairing by
+// ballots); leaves (<= 16 elements) are stably sorted by rank as soon as they are cut;
+// depth-exhausted leaves fall back to the serial heapsort replica. block_introsort below.
 // In-place exclusive scan of arr[0..n) by the calling wave only (no workgroup barrier).
 __device__ __forceinline__ int wave_scan_lds(int* arr, int n) {
     const int lane = lane_id();
@@ -1068,9 +1090,9 @@ __device__ __forceinline__ int wave_scan_lds(int* arr, int n) {
     for (int base = 0; base < n; base += 64) {
         const int i = base + lane;
         const int v = i < n ? arr[i] : 0;
-        const int incl = wave_incl_scan(v);
+        const int incl = wave_incl_scan_dpp(v);
         if (i < n) arr[i] = carry + incl - v;
-        carry += __shfl(incl, 63, 64);
+        carry += __builtin_amdgcn_readlane(incl, 63);
     }
     WAVE_SYNC();
     return carry;
@@ -1091,130 +1113,333 @@ __device__ __forceinline__ void atomic_inc_runs(int* base, int t, bool act) {
     if (head && act) atomicAdd(&base[t], next - lane);
 }
 
-__device__ __forceinline__ void wave_introsort_impl(unsigned long long* a, int n, int* fl, int* lpos, int* rpos, int* leaves,
-                                unsigned long long* tmp, int4* segs, int* s_ws, int* s_ctl) {
+// One unguarded partition of a[lo, hi) by the calling wave (hi - lo > 16): __move_median_to_first
+// then __unguarded_partition (stl_sort.h). Returns the cut. The stops are ranked by ballots; the k-th
+// left / right stop of the segment lands at lpos[lo + k] / rpos[lo + k] (segments are disjoint, so
+// waves partitioning different segments share the scratch).
+__device__ __forceinline__ int wave_partition(unsigned long long* a, int lo, int hi, int* lpos, int* rpos) {
     const int tid = lane_id();
-    if (n <= 1) return;
     const unsigned long long lt = (1ull << tid) - 1ull;
-    // the segment stack lives in registers, entry k in lane k (ORBFE_SORT_STACK = 64 = the wave;
-    // pop = three readlanes, push = the owning lane's moves), its depth and the leaf count
-    // wave-uniform: per partition step two wave hand-offs through LDS, the stops ranked by ballots
-    (void)segs;
-    int sg_lo = 0, sg_hi = tid == 0 ? n : 0, sg_dp = tid == 0 ? 2 * st_lg(n) : 0;
-    int sp = 1, nleaf = 0;
+    // __move_median_to_first(first, first + 1, mid, last - 1): every lane evaluates the
+    // comparison tree on the same four values, lane 0 performs the one swap
+    unsigned long long xpiv;
+    {
+        const int ia = lo + 1, ib = lo + (hi - lo) / 2, ic = hi - 1;
+        const unsigned long long x0 = a[lo], xa = a[ia], xb = a[ib], xc = a[ic];
+        const ExpLess64 comp;
+        int pick;
+        if (comp(xa, xb)) pick = comp(xb, xc) ? ib : (comp(xa, xc) ? ic : ia);
+        else pick = comp(xa, xc) ? ia : (comp(xb, xc) ? ic : ib);
+        xpiv = pick == ia ? xa : (pick == ib ? xb : xc);
+        if (tid == 0) {
+            a[lo] = xpiv;
+            a[pick] = x0;
+        }
+    }
+    WAVE_SYNC();
+    const unsigned P = (unsigned)(xpiv >> 32);   // the pivot every lane already holds
+    const int m = hi - lo - 1;
+    int* lp = lpos + lo;
+    int* rp = rpos + lo;
+    // left stops (scan rightwards over [lo+1, hi)): !(x < P); right stops (leftwards from hi-1): !(P < x)
+    int nl = 0, nr = 0;
+    for (int b0 = 0; b0 < m; b0 += 64) {
+        const int i = b0 + tid;
+        bool lf = false, rf = false;
+        if (i < m) {
+            lf = !((unsigned)(a[lo + 1 + i] >> 32) < P);
+            rf = !(P < (unsigned)(a[hi - 1 - i] >> 32));
+        }
+        const unsigned long long lm = __ballot(lf), rm = __ballot(rf);
+        if (lf) lp[nl + __popcll(lm & lt)] = lo + 1 + i;
+        if (rf) rp[nr + __popcll(rm & lt)] = hi - 1 - i;
+        nl += __popcll(lm);
+        nr += __popcll(rm);
+    }
+    WAVE_SYNC();
+    // lpos increasing, rpos decreasing: the pairs that swap (lpos[k] < rpos[k]) are a prefix
+    const int kmax = min(nl, nr);
+    int sw = 0;
+    for (int b0 = 0; b0 < kmax; b0 += 64) {
+        const int k = b0 + tid;
+        sw += __popcll(__ballot(k < kmax && lp[k] < rp[k]));
+    }
+    for (int k = tid; k < sw; k += 64) {
+        const unsigned long long x = a[lp[k]];
+        a[lp[k]] = a[rp[k]];
+        a[rp[k]] = x;
+    }
+    int cut;
+    if (sw == 0) cut = lp[0];
+    else cut = (sw < nl && lp[sw] < rp[sw - 1]) ? lp[sw] : rp[sw - 1];
+    WAVE_SYNC();
+    return cut;
+}
+
+// A finished introsort leaf a[lo, hi), sorted at once by the wave that cut it: the final insertion
+// sort never moves an element across a partition boundary, so it equals a stable sort of each leaf
+// (<= 16 elements: ranks from the keys broadcast by readlane); a depth-exhausted leaf (> 16) is the
+// serial heapsort replica (__partial_sort) on lane 0.
+__device__ __forceinline__ void wave_leaf(unsigned long long* a, int lo, int hi) {
+    const int lane = lane_id();
+    const int len = hi - lo;
+    if (len <= 1) return;
+    if (len > 16) {
+        if (lane == 0) st_heap_sort(a + lo, len, ExpLess64());
+        WAVE_SYNC();
+        return;
+    }
+    const unsigned long long x = a[lo + min(lane, len - 1)];
+    const unsigned kx = (unsigned)(x >> 32);
+    int r = 0;
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+        const unsigned ku = (unsigned)__builtin_amdgcn_readlane((int)kx, u);
+        r += (u < len && (ku < kx || (ku == kx && u < lane))) ? 1 : 0;
+    }
+    WAVE_SYNC();
+    if (lane < len) a[lo + r] = x;
+    WAVE_SYNC();
+}
+
+#if ORBFE_OCT_STAMPS
+__device__ unsigned long long g_sort_ts[16 * 16];   // diagnostic: per-wave phase stamps of the last block sort
+#endif
+__device__ __forceinline__ unsigned long long rl64(unsigned long long x, int l) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)x, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(x >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
+// gather: lane i gets x of lane src(i)
+__device__ __forceinline__ unsigned long long bp64(unsigned long long x, int src) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_ds_bpermute(src << 2, (int)(unsigned)x);
+    const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(src << 2, (int)(unsigned)(x >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
+// scatter: lane dst(i) gets x of lane i
+__device__ __forceinline__ unsigned long long pm64(unsigned long long x, int dst) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_ds_permute(dst << 2, (int)(unsigned)x);
+    const unsigned hi = (unsigned)__builtin_amdgcn_ds_permute(dst << 2, (int)(unsigned)(x >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+// __introsort_loop of a segment a[lo0, lo0 + len) of <= 64 elements in the calling wave's registers
+// (element i in lane i), then the final insertion sort of all its leaves at once; the same
+// partitions as wave_partition. Per partition: the median of three by readlane; left stops
+// !(x < P) and right stops !(P < x) by ballot, ranked by popcount (left ascending, right
+// descending); the k-th left stop swaps with the k-th right stop iff it lies below it, i.e. iff
+// more than k right stops lie above it, so the swap count is one more ballot; the pairs exchange
+// values through two crossbar scatters (ds_permute) and gathers (ds_bpermute). No LDS round trip.
+__device__ __forceinline__ void wave_sort64(unsigned long long* a, int lo0, int len, int d0) {
+    const int lane = lane_id();
+#if ORBFE_OCT_STAMPS
+    int s64i = 0;
+#define S64_STAMP() do { if (lane == 0 && s64i < 15 && (threadIdx.x >> 6) == 0) g_sort_ts[8 * 16 + s64i] = __builtin_amdgcn_s_memtime(); s64i++; } while (0)
+#else
+#define S64_STAMP() do { } while (0)
+#endif
+    S64_STAMP();
+    unsigned long long x = a[lo0 + min(lane, len - 1)];
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const unsigned long long above = lane == 63 ? 0ull : (~0ull << (lane + 1));
+    unsigned long long leafm = 0, heapm = 0;   // leaf starts (wave-uniform); depth-exhausted leaves
+    int sg_lo = 0, sg_hi = lane == 0 ? len : 0, sg_dp = lane == 0 ? d0 : 0;
+    int sp = 1;
+    while (sp > 0) {
+        --sp;
+        const int lo = __builtin_amdgcn_readlane(sg_lo, sp), hi = __builtin_amdgcn_readlane(sg_hi, sp);
+        const int dp = __builtin_amdgcn_readlane(sg_dp, sp);
+        if (hi - lo <= 16 || dp == 0) {
+            leafm |= 1ull << lo;
+            if (hi - lo > 16) heapm |= 1ull << lo;
+            continue;
+        }
+        // __move_median_to_first(first, first + 1, mid, last - 1)
+        const int ia = lo + 1, ib = lo + (hi - lo) / 2, ic = hi - 1;
+        const unsigned kx = (unsigned)(x >> 32);
+        const unsigned ka = (unsigned)__builtin_amdgcn_readlane((int)kx, ia);
+        const unsigned kb = (unsigned)__builtin_amdgcn_readlane((int)kx, ib);
+        const unsigned kc = (unsigned)__builtin_amdgcn_readlane((int)kx, ic);
+        int pick;
+        if (ka < kb) pick = kb < kc ? ib : (ka < kc ? ic : ia);
+        else pick = ka < kc ? ia : (kb < kc ? ic : ib);
+        const unsigned long long x0 = rl64(x, lo), xp = rl64(x, pick);
+        if (lane == lo) x = xp;
+        else if (lane == pick) x = x0;
+        const unsigned P = (unsigned)(xp >> 32);
+        // __unguarded_partition(first + 1, last, first)
+        const unsigned k = (unsigned)(x >> 32);
+        const bool inr = lane > lo && lane < hi;
+        const bool lf = inr && !(k < P), rf = inr && !(P < k);
+        const unsigned long long LM = __ballot(lf), RM = __ballot(rf);
+        const int rl = __popcll(LM & below), rr = __popcll(RM & above);
+        const bool sL = lf && __popcll(RM & above) > rl;
+        const int sw = __popcll(__ballot(sL));
+        const bool sR = rf && rr < sw;
+        int cut;
+        if (sw == 0) {
+            cut = __builtin_ctzll(LM);
+        } else {
+            const int rp = __builtin_ctzll(__ballot(rf && rr == sw - 1));
+            const int lp = sw < __popcll(LM) ? __builtin_ctzll(__ballot(lf && rl == sw)) : 64;
+            cut = lp < rp ? lp : rp;
+            // lane k of vR / vL holds the k-th right / left stop's value (other lanes park on 63,
+            // never read: sw <= 31)
+            const unsigned long long vR = pm64(x, sR ? rr : 63);
+            const unsigned long long vL = pm64(x, sL ? rl : 63);
+            const unsigned long long fromR = bp64(vR, rl & 63), fromL = bp64(vL, rr & 63);
+            if (sL) x = fromR;
+            else if (sR) x = fromL;
+        }
+        if (lane == sp) { sg_lo = cut; sg_hi = hi; sg_dp = dp - 1; }
+        if (lane == sp + 1) { sg_lo = lo; sg_hi = cut; sg_dp = dp - 1; }
+        sp += 2;
+        S64_STAMP();
+    }
+    S64_STAMP();
+    // final insertion sort = a stable sort of each ordinary leaf: rank among the leaf's keys, scatter
+    const unsigned long long upto = leafm & ~above;
+    const int ls = 63 - __builtin_clzll(upto | 1ull);
+    const unsigned long long after = leafm & above;
+    const int le = after ? __builtin_ctzll(after) : len;
+    const bool heap = (heapm >> ls) & 1ull;
+    const unsigned kx = (unsigned)(x >> 32);
+    // the 16 gathers issued back to back, then the compares (branch-free)
+    unsigned kj[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) kj[u] = (unsigned)__builtin_amdgcn_ds_bpermute(min(ls + u, 63) << 2, (int)kx);
+    int r = 0;
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+        const int j = ls + u;
+        r += (int)((j < le) & ((kj[u] < kx) | ((kj[u] == kx) & (j < lane))));
+    }
+    x = pm64(x, (lane < len && !heap) ? ls + r : lane);
+    if (lane < len) a[lo0 + lane] = x;
+    if (heapm) {
+        WAVE_SYNC();
+        if (lane == 0) {
+            unsigned long long hm = heapm;
+            while (hm) {
+                const int hs = __builtin_ctzll(hm);
+                hm &= hm - 1ull;
+                const unsigned long long nx = leafm & (hs == 63 ? 0ull : (~0ull << (hs + 1)));
+                const int he = nx ? __builtin_ctzll(nx) : len;
+                st_heap_sort(a + lo0 + hs, he - hs, ExpLess64());
+            }
+        }
+    }
+    WAVE_SYNC();
+    S64_STAMP();
+#if ORBFE_OCT_STAMPS
+    if (lane == 0 && (threadIdx.x >> 6) == 0) g_sort_ts[8 * 16 + 15] = s64i;
+#endif
+#undef S64_STAMP
+}
+
+// __introsort_loop of one segment by the calling wave, depth first. The segment stack lives in
+// registers, entry k in lane k (ORBFE_SORT_STACK = 64 = the wave; pop = three readlanes).
+__device__ __forceinline__ void wave_sort_seg(unsigned long long* a, int lo0, int hi0, int dp0, int* lpos, int* rpos) {
+    const int tid = lane_id();
+    int sg_lo = lo0, sg_hi = tid == 0 ? hi0 : 0, sg_dp = tid == 0 ? dp0 : 0;
+    int sp = 1;
     while (sp > 0) {
         --sp;
         const int lo = __builtin_amdgcn_readlane(sg_lo, sp), hi = __builtin_amdgcn_readlane(sg_hi, sp);
         const int depth = __builtin_amdgcn_readlane(sg_dp, sp);
-        if (hi - lo <= 16 || depth == 0) {
-            if (tid == 0) leaves[nleaf] = lo | ((hi - lo <= 16) ? 0 : (int)0x80000000);
-            nleaf++;
+        if (hi - lo <= 64 && depth > 0) {
+            if (hi - lo > 1) wave_sort64(a, lo, hi - lo, depth);
             continue;
         }
-        // __move_median_to_first(first, first + 1, mid, last - 1): every lane evaluates the
-        // comparison tree on the same four values, lane 0 performs the one swap
-        unsigned long long xpiv;
-        {
-            const int ia = lo + 1, ib = lo + (hi - lo) / 2, ic = hi - 1;
-            const unsigned long long x0 = a[lo], xa = a[ia], xb = a[ib], xc = a[ic];
-            const ExpLess64 comp;
-            int pick;
-            if (comp(xa, xb)) pick = comp(xb, xc) ? ib : (comp(xa, xc) ? ic : ia);
-            else pick = comp(xa, xc) ? ia : (comp(xb, xc) ? ic : ib);
-            xpiv = pick == ia ? xa : (pick == ib ? xb : xc);
-            if (tid == 0) {
-                a[lo] = xpiv;
-                a[pick] = x0;
-            }
+        if (depth == 0) {
+            wave_leaf(a, lo, hi);
+            continue;
         }
-        WAVE_SYNC();
-        const unsigned P = (unsigned)(xpiv >> 32);   // the pivot every lane already holds
-        const int m = hi - lo - 1;
-        // left stops (scan rightwards over [lo+1, hi)): !(x < P); right stops (leftwards from
-        // hi-1): !(P < x); the k-th stop of each side lands at lpos[k] / rpos[k]
-        int nl = 0, nr = 0;
-        for (int b0 = 0; b0 < m; b0 += 64) {
-            const int i = b0 + tid;
-            bool lf = false, rf = false;
-            if (i < m) {
-                lf = !((unsigned)(a[lo + 1 + i] >> 32) < P);
-                rf = !(P < (unsigned)(a[hi - 1 - i] >> 32));
-            }
-            const unsigned long long lm = __ballot(lf), rm = __ballot(rf);
-            if (lf) lpos[nl + __popcll(lm & lt)] = lo + 1 + i;
-            if (rf) rpos[nr + __popcll(rm & lt)] = hi - 1 - i;
-            nl += __popcll(lm);
-            nr += __popcll(rm);
-        }
-        WAVE_SYNC();
-        // lpos increasing, rpos decreasing: the pairs that swap (lpos[k] < rpos[k]) are a prefix
-        const int kmax = min(nl, nr);
-        int sw = 0;
-        for (int b0 = 0; b0 < kmax; b0 += 64) {
-            const int k = b0 + tid;
-            sw += __popcll(__ballot(k < kmax && lpos[k] < rpos[k]));
-        }
-        for (int k = tid; k < sw; k += 64) {
-            const unsigned long long x = a[lpos[k]];
-            a[lpos[k]] = a[rpos[k]];
-            a[rpos[k]] = x;
-        }
-        int cut;
-        if (sw == 0) cut = lpos[0];
-        else cut = (sw < nl && lpos[sw] < rpos[sw - 1]) ? lpos[sw] : rpos[sw - 1];
+        const int cut = wave_partition(a, lo, hi, lpos, rpos);
         if (tid == sp) { sg_lo = cut; sg_hi = hi; sg_dp = depth - 1; }
         if (tid == sp + 1) { sg_lo = lo; sg_hi = cut; sg_dp = depth - 1; }
         sp += 2;
-        WAVE_SYNC();
     }
-    WAVE_SYNC();
-    // leaves were recorded left to right; stable rank sort inside each ordinary leaf. Each leaf's
-    // lane first writes {start, end | heap flag} over its positions (fl), so an element finds its
-    // leaf in one read instead of a binary search of dependent reads
-    for (int L = tid; L < nleaf; L += 64) {
-        const int ls = leaves[L] & 0x7fffffff;
-        const int le = L + 1 < nleaf ? (leaves[L + 1] & 0x7fffffff) : n;
-        const int tag = ls | (le << 16) | (leaves[L] & 0x80000000);
-        for (int i = ls; i < le; i++) fl[i] = tag;
-    }
-    WAVE_SYNC();
-    for (int i = tid; i < n; i += 64) {
-        const int tag = fl[i];
-        const int ls = tag & 0xffff, le = (tag >> 16) & 0x7fff;
-        const unsigned long long x = a[i];
-        if (tag & 0x80000000) { tmp[i] = x; continue; }
-        const unsigned kx = (unsigned)(x >> 32);
-        // an ordinary leaf holds <= 16 elements: the reads issued together
-        int r = 0;
-#pragma unroll
-        for (int u = 0; u < 16; u++) {
-            const int j = ls + u;
-            const unsigned kj = (unsigned)(a[min(j, n - 1)] >> 32);
-            r += (j < le && (kj < kx || (kj == kx && j < i))) ? 1 : 0;
-        }
-        tmp[ls + r] = x;
-    }
-    WAVE_SYNC();
-    for (int i = tid; i < n; i += 64) a[i] = tmp[i];
-    WAVE_SYNC();
-    if (tid == 0)
-        for (int L = 0; L < nleaf; L++)
-            if (leaves[L] & 0x80000000) {
-                const int ls = leaves[L] & 0x7fffffff;
-                const int le = L + 1 < nleaf ? (leaves[L + 1] & 0x7fffffff) : n;
-                st_heap_sort(a + ls, le - ls, ExpLess64());
-            }
-    WAVE_SYNC();
 }
 
-// Block entry: the sort runs on wave 0 only (wave-level scans, no workgroup barriers inside);
-// the other waves wait at the closing barrier.
+// segment list entry: lo | hi << 16 | depth << 32
+__device__ __forceinline__ unsigned long long seg_pack(int lo, int hi, int d) {
+    return (unsigned long long)(unsigned)lo | ((unsigned long long)(unsigned)hi << 16) | ((unsigned long long)d << 32);
+}
+
+// Block entry: every wave of the block sorts. Partitions of disjoint segments are independent, so
+// the order they run in does not change the result: breadth-first rounds (wave w takes list entries
+// w, w + nw, ...; an entry's two children go to entries 2s and 2s + 1 of the next list, empty when
+// the child was a leaf and sorted at once; block barrier between rounds) until the list has at least
+// as many entries as there are waves, then each wave finishes its entries depth first. No atomics:
+// the compiler's lane-serial expansion of a wave's LDS atomic cost ~5 k cycles per push or pop.
+// Scratch: lpos, rpos int[n]; tmp u64[n] (two segment lists); s_ctl[8] (non-empty flags).
+// fl, leaves, segs, s_ws unused.
 __device__ __forceinline__ void block_introsort(unsigned long long* a, int n, int* fl, int* lpos, int* rpos, int* leaves,
                                 unsigned long long* tmp, int4* segs, int* s_ws, int* s_ctl) {
-    (void)s_ws;
+    (void)fl; (void)leaves; (void)segs; (void)s_ws;
+    const int lane = lane_id(), wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#if ORBFE_OCT_STAMPS
+    int sti = 0;
+#define SORT_STAMP() do { if (lane == 0 && sti < 15) g_sort_ts[wave * 16 + sti] = __builtin_amdgcn_s_memtime(); sti++; } while (0)
+#else
+#define SORT_STAMP() do { } while (0)
+#endif
+    SORT_STAMP();
+    if (threadIdx.x == 0) {
+        tmp[0] = seg_pack(0, n, 2 * st_lg(n));
+#pragma unroll
+        for (int k = 0; k < 8; k++) s_ctl[k] = 0;
+    }
     SYNC();
-    if ((threadIdx.x >> 6) == 0) wave_introsort_impl(a, n, fl, lpos, rpos, leaves, tmp, segs, s_ws, s_ctl);
+    SORT_STAMP();
+    if (n <= 1) return;
+    // a list holds at most 2 * nw - 2 entries (it doubles while below nw): tmp needs 4 * nw entries
+    // (k_octree: the 2 * NC of the next-count table; the debug entry: its LDS tail)
+    unsigned long long* cur = tmp;
+    unsigned long long* nxt = tmp + 2 * nw;
+    int S = 1, r = 0;
+    while (S > 0 && S < nw && r < 7) {
+        bool any = false;
+        for (int s = wave; s < S; s += nw) {
+            const unsigned long long e = cur[s];
+            const int lo = (int)(e & 0xffff), hi = (int)((e >> 16) & 0xffff), d = (int)(e >> 32);
+            unsigned long long c0 = 0, c1 = 0;
+            if (hi - lo <= 16 || d == 0) {
+                wave_leaf(a, lo, hi);
+            } else if (hi - lo <= 64) {
+                wave_sort64(a, lo, hi - lo, d);
+            } else {
+                const int cut = wave_partition(a, lo, hi, lpos, rpos);
+                if (hi - cut <= 16 || d == 1) wave_leaf(a, cut, hi);
+                else c0 = seg_pack(cut, hi, d - 1);
+                if (cut - lo <= 16 || d == 1) wave_leaf(a, lo, cut);
+                else c1 = seg_pack(lo, cut, d - 1);
+            }
+            if (lane == 0) {
+                nxt[2 * s] = c0;
+                nxt[2 * s + 1] = c1;
+            }
+            any = any || c0 != 0 || c1 != 0;
+        }
+        if (any && lane == 0) s_ctl[r] = 1;   // plain stores of one value: no atomic needed
+        SYNC();
+        SORT_STAMP();
+        S = s_ctl[r] ? 2 * S : 0;
+        r++;
+        unsigned long long* t = cur; cur = nxt; nxt = t;
+    }
+    for (int s = wave; s < S; s += nw) {
+        const unsigned long long e = cur[s];
+        if (e) wave_sort_seg(a, (int)(e & 0xffff), (int)((e >> 16) & 0xffff), (int)(e >> 32), lpos, rpos);
+    }
+    SORT_STAMP();
     SYNC();
+    SORT_STAMP();
+#if ORBFE_OCT_STAMPS
+    if (lane == 0) g_sort_ts[wave * 16 + 15] = sti;
+#endif
+#undef SORT_STAMP
 }
 
 // Debug/test entry: sort one array with the block sort (single block).
@@ -1279,6 +1504,7 @@ __global__ __launch_bounds__(NT) void k_octree(OrbGeom g, const uint32_t* __rest
     int4* segs = (int4*)carve(sizeof(int4) * ORBFE_SORT_STACK);
     __shared__ int s_ws[NT / 64];
     __shared__ int s_misc[8];
+    __shared__ int2 s_ws2[NT / 64];
 
     // diagnostic phase stamps (image 0 of the batch, every level), tstamp == nullptr in normal runs
     unsigned long long* ts = (tstamp && b == 0) ? tstamp + 64 * l : nullptr;
@@ -1363,119 +1589,189 @@ __global__ __launch_bounds__(NT) void k_octree(OrbGeom g, const uint32_t* __rest
     int guard = 0;
     while (!finish && guard++ < 100000) {
         const int prevN = n;
-        int T_div;   // number of divided nodes in this step
-        if (!phase2) {
-            // every node with >1 keys divides, in list order
-            for (int i = tid; i < n; i += NT) tmpA[i] = Csz[i] > 1 ? 1 : 0;
-            SYNC();
-            for (int i = tid; i < n; i += NT) divorder[i] = Csz[i] > 1 ? 1 : -1;
-            T_div = block_excl_scan<NT>(tmpA, n, s_ws);   // tmpA[i] = divider rank t (list order)
-            for (int i = tid; i < n; i += NT)
-                if (divorder[i] >= 0) { divorder[i] = tmpA[i]; procp[tmpA[i]] = i; }
-            SYNC();
-        } else {
-            // std::sort(vPrevSizeAndPointerToNode, compareNodes) (ORBextractor.cc:700), exact replica
-            block_introsort(expv, m, tmpC, tmpA, tmpB, Xcnt + 2 * NC, (unsigned long long*)Xcnt, segs, s_ws,
-                            s_misc);
-            OCT_STAMP();
-            // walk from the back until the list reaches N (ORBextractor.cc:701-748): processed node t is
-            // expv[m-1-t]; the list grows by (children - 1) per division -> first t where it reaches N
-            for (int t = tid; t < m; t += NT) {
-                const int q = (int)(expv[m - 1 - t] & 0xffffffffull);
-                const int4 cq = *(const int4*)&Ccnt[4 * q];
-                tmpA[t] = (cq.x > 0) + (cq.y > 0) + (cq.z > 0) + (cq.w > 0) - 1;
-                procp[t] = q;
-            }
-            if (tid == 0) s_misc[6] = m;
-            SYNC();
-            (void)block_excl_scan<NT>(tmpA, m, s_ws);   // tmpA[t] = growth before processing t
-            for (int t = tid; t < m; t += NT) {
-                const int q = procp[t];
-                const int4 cq = *(const int4*)&Ccnt[4 * q];
-                const int grow = (cq.x > 0) + (cq.y > 0) + (cq.z > 0) + (cq.w > 0) - 1;
-                if (n + tmpA[t] + grow >= N) atomicMin(&s_misc[6], t + 1);
-            }
-            SYNC();
-            T_div = s_misc[6];
-            for (int t = tid; t < T_div; t += NT) divorder[procp[t]] = t;
-            SYNC();
-        }
-        OCT_STAMP();
-        // children counts per processed node (t order): tmpB = nonempty, tmpC = expandable (>1)
-        for (int t = tid; t < T_div; t += NT) {
-            const int q = procp[t];
-            int c = 0, e = 0;
-            const int4 cq = *(const int4*)&Ccnt[4 * q];
+        int newN, Etot;
+        if (!phase2 && n <= NT) {
+            // Phase-1 step fused (one node per thread): every node with > 1 keys divides, in list order,
+            // so the divider rank t, the children / expandable-children offsets and the kept-node rank
+            // are one packed two-value block scan over the list (counts < 2^16: n <= NT <= 1024)
+            const int i = tid;
+            const bool live = i < n;
+            const int csz = live ? Csz[i] : 0;
+            const bool div = csz > 1;
+            int4 cq = make_int4(0, 0, 0, 0);
+            if (div) cq = *(const int4*)&Ccnt[4 * i];
             const int cv[4] = {cq.x, cq.y, cq.z, cq.w};
+            int c = 0, e = 0;
 #pragma unroll
             for (int k = 0; k < 4; k++) { c += cv[k] > 0; e += cv[k] > 1; }
-            tmpB[t] = c;
-            tmpC[t] = e;
-        }
-        SYNC();
-        const int Ctot = block_excl_scan<NT>(tmpB, T_div, s_ws);
-        const int Etot = block_excl_scan<NT>(tmpC, T_div, s_ws);
-        // children: block of t starts at sum_{t'>t} c_t' = Ctot - (excl_t + c_t); order n4,n3,n2,n1
-        for (int t = tid; t < T_div; t += NT) {
-            const int q = procp[t];
-            // the four counts in one read: the child writes below may alias them for the compiler,
-            // which would otherwise re-read each count behind the previous child's stores
-            const int4 cq = *(const int4*)&Ccnt[4 * q];
-            const int cv[4] = {cq.x, cq.y, cq.z, cq.w};
-            int c = 0;
+            int exA, exB, totA, totB;
+            block_scan2<NT>(live ? (div ? 1 : 0x10000) : 0, c | (e << 16), s_ws2, exA, exB, totA, totB);
+            const int Ctot = totB & 0xffff;
+            Etot = totB >> 16;
+            newN = Ctot + (totA >> 16);
+            if (div) {
+                divorder[i] = exA & 0xffff;
+                // children: block of t starts at sum_{t'>t} c_t'; order n4,n3,n2,n1 (push_front)
+                const int start = Ctot - ((exB & 0xffff) + c);
+                int kk = 0;
+                const int px0 = Cx0[i], px1 = Cx1[i], py0 = Cy0[i], py1 = Cy1[i];
+                int cpos[4];
 #pragma unroll
-            for (int k = 0; k < 4; k++) c += cv[k] > 0;
-            const int start = Ctot - (tmpB[t] + c);
-            int kk = 0;
-            const int px0 = Cx0[q], px1 = Cx1[q], py0 = Cy0[q], py1 = Cy1[q];
-            int cpos[4];
-#pragma unroll
-            for (int ch = 3; ch >= 0; ch--) {
-                const int v = cv[ch];
-                cpos[ch] = -1;
-                if (v > 0) {
-                    const int np = start + kk++;
-                    cpos[ch] = np;
-                    childpos[4 * q + ch] = (int16_t)np;
-                    int a0, a1, b0, b1;
-                    child_rect(ch, px0, px1, py0, py1, &a0, &a1, &b0, &b1);
-                    Xx0[np] = (int16_t)a0; Xx1[np] = (int16_t)a1;
-                    Xy0[np] = (int16_t)b0; Xy1[np] = (int16_t)b1;
-                    Xsz[np] = v;
-                } else {
-                    childpos[4 * q + ch] = -1;
+                for (int ch = 3; ch >= 0; ch--) {
+                    const int v = cv[ch];
+                    cpos[ch] = -1;
+                    if (v > 0) {
+                        const int np = start + kk++;
+                        cpos[ch] = np;
+                        childpos[4 * i + ch] = (int16_t)np;
+                        int a0, a1, b0, b1;
+                        child_rect(ch, px0, px1, py0, py1, &a0, &a1, &b0, &b1);
+                        Xx0[np] = (int16_t)a0; Xx1[np] = (int16_t)a1;
+                        Xy0[np] = (int16_t)b0; Xy1[np] = (int16_t)b1;
+                        Xsz[np] = v;
+                    } else {
+                        childpos[4 * i + ch] = -1;
+                    }
                 }
-            }
-            int e = tmpC[t];
+                int ei = exB >> 16;
 #pragma unroll
-            for (int ch = 0; ch < 4; ch++) {
-                const int v = cv[ch];
-                if (v > 1) {
-                    int a0, a1, b0, b1;
-                    child_rect(ch, px0, px1, py0, py1, &a0, &a1, &b0, &b1);
-                    expv[e] = ((unsigned long long)v << 44) | ((unsigned long long)(a0 & 0xfff) << 32) |
-                              (unsigned long long)(uint16_t)cpos[ch];
-                    e++;
+                for (int ch = 0; ch < 4; ch++) {
+                    const int v = cv[ch];
+                    if (v > 1) {
+                        int a0, a1, b0, b1;
+                        child_rect(ch, px0, px1, py0, py1, &a0, &a1, &b0, &b1);
+                        expv[ei] = ((unsigned long long)v << 44) | ((unsigned long long)(a0 & 0xfff) << 32) |
+                                   (unsigned long long)(uint16_t)cpos[ch];
+                        ei++;
+                    }
                 }
-            }
-        }
-        // undivided nodes keep their relative order after the pushed children
-        for (int i = tid; i < n; i += NT) tmpA[i] = divorder[i] < 0 ? 1 : 0;
-        SYNC();
-        const int nKeep = block_excl_scan<NT>(tmpA, n, s_ws);
-        for (int i = tid; i < n; i += NT) {
-            if (divorder[i] < 0) {
-                const int np = Ctot + tmpA[i];
+            } else if (live) {
+                // undivided nodes keep their relative order after the pushed children
+                divorder[i] = -1;
+                const int np = Ctot + (exA >> 16);
                 newpos[i] = (int16_t)np;
                 Xx0[np] = Cx0[i]; Xx1[np] = Cx1[i];
                 Xy0[np] = Cy0[i]; Xy1[np] = Cy1[i];
-                Xsz[np] = Csz[i];
+                Xsz[np] = csz;
             }
+            for (int j = tid; j < 4 * newN; j += NT) Xcnt[j] = 0;
+            SYNC();
+            OCT_STAMP();
+        } else {
+            int T_div;   // number of divided nodes in this step
+            if (!phase2) {
+                // every node with >1 keys divides, in list order
+                for (int i = tid; i < n; i += NT) tmpA[i] = Csz[i] > 1 ? 1 : 0;
+                SYNC();
+                for (int i = tid; i < n; i += NT) divorder[i] = Csz[i] > 1 ? 1 : -1;
+                T_div = block_excl_scan<NT>(tmpA, n, s_ws);   // tmpA[i] = divider rank t (list order)
+                for (int i = tid; i < n; i += NT)
+                    if (divorder[i] >= 0) { divorder[i] = tmpA[i]; procp[tmpA[i]] = i; }
+                SYNC();
+            } else {
+                // std::sort(vPrevSizeAndPointerToNode, compareNodes) (ORBextractor.cc:700), exact replica
+                block_introsort(expv, m, tmpC, tmpA, tmpB, Xcnt + 2 * NC, (unsigned long long*)Xcnt, segs, s_ws,
+                                s_misc);
+                OCT_STAMP();
+                // walk from the back until the list reaches N (ORBextractor.cc:701-748): processed node t is
+                // expv[m-1-t]; the list grows by (children - 1) per division -> first t where it reaches N
+                for (int t = tid; t < m; t += NT) {
+                    const int q = (int)(expv[m - 1 - t] & 0xffffffffull);
+                    const int4 cq = *(const int4*)&Ccnt[4 * q];
+                    tmpA[t] = (cq.x > 0) + (cq.y > 0) + (cq.z > 0) + (cq.w > 0) - 1;
+                    procp[t] = q;
+                }
+                if (tid == 0) s_misc[6] = m;
+                SYNC();
+                (void)block_excl_scan<NT>(tmpA, m, s_ws);   // tmpA[t] = growth before processing t
+                for (int t = tid; t < m; t += NT) {
+                    const int q = procp[t];
+                    const int4 cq = *(const int4*)&Ccnt[4 * q];
+                    const int grow = (cq.x > 0) + (cq.y > 0) + (cq.z > 0) + (cq.w > 0) - 1;
+                    if (n + tmpA[t] + grow >= N) atomicMin(&s_misc[6], t + 1);
+                }
+                SYNC();
+                T_div = s_misc[6];
+                for (int t = tid; t < T_div; t += NT) divorder[procp[t]] = t;
+                SYNC();
+            }
+            OCT_STAMP();
+            // children counts per processed node (t order): tmpB = nonempty, tmpC = expandable (>1)
+            for (int t = tid; t < T_div; t += NT) {
+                const int q = procp[t];
+                int c = 0, e = 0;
+                const int4 cq = *(const int4*)&Ccnt[4 * q];
+                const int cv[4] = {cq.x, cq.y, cq.z, cq.w};
+    #pragma unroll
+                for (int k = 0; k < 4; k++) { c += cv[k] > 0; e += cv[k] > 1; }
+                tmpB[t] = c;
+                tmpC[t] = e;
+            }
+            SYNC();
+            const int Ctot = block_excl_scan<NT>(tmpB, T_div, s_ws);
+            Etot = block_excl_scan<NT>(tmpC, T_div, s_ws);
+            // children: block of t starts at sum_{t'>t} c_t' = Ctot - (excl_t + c_t); order n4,n3,n2,n1
+            for (int t = tid; t < T_div; t += NT) {
+                const int q = procp[t];
+                // the four counts in one read: the child writes below may alias them for the compiler,
+                // which would otherwise re-read each count behind the previous child's stores
+                const int4 cq = *(const int4*)&Ccnt[4 * q];
+                const int cv[4] = {cq.x, cq.y, cq.z, cq.w};
+                int c = 0;
+    #pragma unroll
+                for (int k = 0; k < 4; k++) c += cv[k] > 0;
+                const int start = Ctot - (tmpB[t] + c);
+                int kk = 0;
+                const int px0 = Cx0[q], px1 = Cx1[q], py0 = Cy0[q], py1 = Cy1[q];
+                int cpos[4];
+    #pragma unroll
+                for (int ch = 3; ch >= 0; ch--) {
+                    const int v = cv[ch];
+                    cpos[ch] = -1;
+                    if (v > 0) {
+                        const int np = start + kk++;
+                        cpos[ch] = np;
+                        childpos[4 * q + ch] = (int16_t)np;
+                        int a0, a1, b0, b1;
+                        child_rect(ch, px0, px1, py0, py1, &a0, &a1, &b0, &b1);
+                        Xx0[np] = (int16_t)a0; Xx1[np] = (int16_t)a1;
+                        Xy0[np] = (int16_t)b0; Xy1[np] = (int16_t)b1;
+                        Xsz[np] = v;
+                    } else {
+                        childpos[4 * q + ch] = -1;
+                    }
+                }
+                int e = tmpC[t];
+    #pragma unroll
+                for (int ch = 0; ch < 4; ch++) {
+                    const int v = cv[ch];
+                    if (v > 1) {
+                        int a0, a1, b0, b1;
+                        child_rect(ch, px0, px1, py0, py1, &a0, &a1, &b0, &b1);
+                        expv[e] = ((unsigned long long)v << 44) | ((unsigned long long)(a0 & 0xfff) << 32) |
+                                  (unsigned long long)(uint16_t)cpos[ch];
+                        e++;
+                    }
+                }
+            }
+            // undivided nodes keep their relative order after the pushed children
+            for (int i = tid; i < n; i += NT) tmpA[i] = divorder[i] < 0 ? 1 : 0;
+            SYNC();
+            const int nKeep = block_excl_scan<NT>(tmpA, n, s_ws);
+            for (int i = tid; i < n; i += NT) {
+                if (divorder[i] < 0) {
+                    const int np = Ctot + tmpA[i];
+                    newpos[i] = (int16_t)np;
+                    Xx0[np] = Cx0[i]; Xx1[np] = Cx1[i];
+                    Xy0[np] = Cy0[i]; Xy1[np] = Cy1[i];
+                    Xsz[np] = Csz[i];
+                }
+            }
+            newN = Ctot + nKeep;
+            for (int i = tid; i < 4 * newN; i += NT) Xcnt[i] = 0;
+            SYNC();
+            OCT_STAMP();
         }
-        const int newN = Ctot + nKeep;
-        for (int i = tid; i < 4 * newN; i += NT) Xcnt[i] = 0;
-        SYNC();
-        OCT_STAMP();
         // key sweep: move keys to their new node positions and count the next split
         for (int kb = 0; kb < K; kb += NT * OCT_U) {
             const int k0 = kb + tid;
@@ -1500,6 +1796,8 @@ __global__ __launch_bounds__(NT) void k_octree(OrbGeom g, const uint32_t* __rest
             }
         }
         SYNC();
+        // no barrier after the reset: the next step touches divorder only behind its own barriers
+        // (the fused step's scan, the sort's entry), and nothing else here is shared
         for (int i = tid; i < NC; i += NT) divorder[i] = -1;
         {
             int16_t* t;
@@ -1508,7 +1806,6 @@ __global__ __launch_bounds__(NT) void k_octree(OrbGeom g, const uint32_t* __rest
             t = Cy0; Cy0 = Xy0; Xy0 = t; t = Cy1; Cy1 = Xy1; Xy1 = t;
             ti = Csz; Csz = Xsz; Xsz = ti; ti = Ccnt; Ccnt = Xcnt; Xcnt = ti;
         }
-        SYNC();
         n = newN;
         m = Etot;
         if (n > NC - 4) { n = NC - 4; finish = true; }   // capacity guard (bound: n <= max(N+2, 4*nIni) = NC-8-1)
