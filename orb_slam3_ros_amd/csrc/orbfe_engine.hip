@@ -73,6 +73,7 @@ struct orbfe_extractor {
     float scale_factor_f;
     double scale_factor;
     int resize_simd_lanes = 16;
+    bool no_fused_pyramid = getenv("ORBFE_NO_FUSED_PYRAMID") != nullptr;   // A/B: the chained launches
     int blur_variant = 0;
     std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
     std::vector<int> per_level;
@@ -89,8 +90,13 @@ struct orbfe_extractor {
     FastLds fast_lds{};   // k_fast per-wave LDS layout (max over levels)
     FastLds fast_lds_lv[ORBFE_MAX_LEVELS] = {};   // per level: a launch over levels [a, b] sizes its LDS by their max
     size_t oct_lds = 0;
+    // k_pyramid tile records (small batches); pt_n = 0 when the geometry does not fit its limits
+    std::vector<uint32_t> ptile;
+    int pt_n = 0, pt_stride = 0, pt_cap = 0;
+    size_t pt_lds = 0;
     // device buffers
     int16_t* d_tab = nullptr;
+    uint32_t* d_ptile = nullptr;
     uint8_t* d_pyr = nullptr;
     uint32_t* d_cellkeys = nullptr;
     int* d_cellcnt = nullptr;
@@ -146,7 +152,7 @@ struct orbfe_extractor {
 };
 
 static void free_buffers(orbfe_extractor* h) {
-    void** bufs[] = {(void**)&h->d_tab, (void**)&h->d_pyr, (void**)&h->d_cellkeys,
+    void** bufs[] = {(void**)&h->d_tab, (void**)&h->d_ptile, (void**)&h->d_pyr, (void**)&h->d_cellkeys,
                      (void**)&h->d_cellcnt, (void**)&h->d_lkeys, (void**)&h->d_nodeof, (void**)&h->d_outkeys,
                      (void**)&h->d_lvinfo, (void**)&h->d_ranks, (void**)&h->d_out, (void**)&h->d_ptrs};
     for (void** p : bufs) {
@@ -329,6 +335,134 @@ static int build_geom(const orbfe_extractor* h, int W, int H, OrbGeom& g, std::v
     return ORBFE_OK;
 }
 
+// k_pyramid tiles (orbfe_kernels.hip K1c): TX x TY tiles, tile (i, j) owning columns
+// [4 floor(i W_l / 4 TX), ...) and rows [floor(j H_l / TY), ...) of every level l >= 1, and the
+// rectangle it needs at each level: its own plus the source cone of its needs one level up
+// (columns sx, sx + 1 and rows s0, s1 of the level's tables), from the top level down to the
+// level-0 window. Returns false when a limit of the kernel is exceeded (then the chained launches run).
+static bool build_pyr_tiles(const OrbGeom& g, const std::vector<int16_t>& tab, std::vector<uint32_t>& out, int& ntiles,
+                            int& stride, int& cap, size_t& lds) {
+    const int nl = g.nlevels;
+    out.clear();
+    ntiles = stride = cap = 0;
+    lds = 0;
+    if (nl < 2) return false;
+    const int W1 = g.lv[1].w, H1 = g.lv[1].h;
+    int TX = std::max(1, (W1 + 79) / 80), TY = std::max(1, (H1 + 63) / 64);
+    struct R { int x0, x1, y0, y1; };
+    auto own = [&](int l, int i, int j, int TXn, int TYn) {
+        const OrbLevel& L = g.lv[l];
+        R r;
+        r.x0 = i == 0 ? 0 : (int)((long long)i * L.w / TXn) & ~3;
+        r.x1 = i + 1 == TXn ? L.w : (int)((long long)(i + 1) * L.w / TXn) & ~3;
+        r.y0 = (int)((long long)j * L.h / TYn);
+        r.y1 = j + 1 == TYn ? L.h : (int)((long long)(j + 1) * L.h / TYn);
+        return r;
+    };
+    for (;;) {   // every tile must own a non-empty rectangle of every level
+        bool ok = true;
+        for (int l = 1; l < nl && ok; l++)
+            for (int i = 0; i < TX && ok; i++) {
+                const R r = own(l, i, 0, TX, TY);
+                if (r.x1 <= r.x0) ok = false;
+            }
+        for (int l = 1; l < nl && ok; l++)
+            for (int j = 0; j < TY && ok; j++) {
+                const R r = own(l, 0, j, TX, TY);
+                if (r.y1 <= r.y0) ok = false;
+            }
+        if (ok) break;
+        if (TX == 1 && TY == 1) return false;
+        if (TX >= TY && TX > 1) TX--; else TY--;
+    }
+    std::vector<std::vector<uint32_t>> recs;
+    for (int j = 0; j < TY; j++)
+        for (int i = 0; i < TX; i++) {
+            std::vector<R> need(nl), ow(nl);
+            for (int l = 1; l < nl; l++) ow[l] = own(l, i, j, TX, TY);
+            // top level: its own rectangle, columns rounded out to whole dwords
+            need[nl - 1] = {ow[nl - 1].x0, round_up(ow[nl - 1].x1, 4), ow[nl - 1].y0, ow[nl - 1].y1};
+            for (int l = nl - 1; l >= 1; l--) {
+                const OrbLevel& L = g.lv[l];
+                const OrbLevel& P = g.lv[l - 1];
+                const int16_t* tx = tab.data() + L.tab_x;
+                const int16_t* ty = tab.data() + L.tab_y;
+                int c0 = 1 << 30, c1 = -1, r0 = 1 << 30, r1 = -1;
+                for (int x = need[l].x0; x < need[l].x1; x++) {
+                    const int xi = std::min(x, L.w - 1), sx = tx[3 * xi];
+                    c0 = std::min(c0, sx);
+                    c1 = std::max(c1, std::min(sx + 1, P.w - 1));
+                }
+                for (int y = need[l].y0; y < need[l].y1; y++) {
+                    r0 = std::min(r0, (int)ty[4 * y]);
+                    r1 = std::max(r1, (int)ty[4 * y + 1]);
+                }
+                R n{c0 & ~3, round_up(c1 + 1, 4), r0, r1 + 1};
+                if (l - 1 >= 1) {
+                    const R& o = ow[l - 1];
+                    n.x0 = std::min(n.x0, o.x0);
+                    n.x1 = std::max(n.x1, round_up(o.x1, 4));
+                    n.y0 = std::min(n.y0, o.y0);
+                    n.y1 = std::max(n.y1, o.y1);
+                    n.x1 = std::min(n.x1, round_up(P.w, 4));
+                }
+                need[l - 1] = n;
+            }
+            std::vector<uint32_t> rc(5 * nl + (nl & 1 ? 1 : 0), 0u);   // header (body starts on an even dword)
+            for (int l = 0; l < nl; l++) {
+                const R& n = need[l];
+                if (n.x1 > 65535 || n.y1 > 65535) return false;
+                cap = std::max(cap, (n.x1 - n.x0) * (n.y1 - n.y0));
+                rc[5 * l + 0] = (uint32_t)n.x0 | ((uint32_t)n.x1 << 16);
+                rc[5 * l + 1] = (uint32_t)n.y0 | ((uint32_t)n.y1 << 16);
+                if (l >= 1) {
+                    rc[5 * l + 2] = (uint32_t)ow[l].x0 | ((uint32_t)ow[l].x1 << 16);
+                    rc[5 * l + 3] = (uint32_t)ow[l].y0 | ((uint32_t)ow[l].y1 << 16);
+                }
+            }
+            for (int l = 1; l < nl; l++) {
+                const OrbLevel& L = g.lv[l];
+                const R& n = need[l];
+                const R& p = need[l - 1];
+                const int16_t* tx = tab.data() + L.tab_x;
+                const int16_t* ty = tab.data() + L.tab_y;
+                const size_t coloff = rc.size();
+                for (int x = n.x0; x < n.x1; x++) {
+                    const int xi = std::min(x, L.w - 1);
+                    const int sx = tx[3 * xi];
+                    const bool lin = xi < L.xmax;
+                    const int a0 = lin ? tx[3 * xi + 1] : 2048, a1 = lin ? tx[3 * xi + 2] : 0;
+                    const int s0 = sx - p.x0, s1 = std::min(sx + 1, p.x1 - 1) - p.x0;
+                    if (s0 < 0 || s1 >= p.x1 - p.x0 || s0 > 0x7fff || a0 < 0 || a1 < 0) return false;
+                    rc.push_back((uint32_t)s0 | ((uint32_t)s1 << 15) | ((x < L.simd_end ? 1u : 0u) << 30));
+                    rc.push_back((uint32_t)a0 | ((uint32_t)a1 << 16));
+                }
+                const size_t rowoff = rc.size();
+                for (int y = n.y0; y < n.y1; y++) {
+                    const int s0 = ty[4 * y] - p.y0, s1 = ty[4 * y + 1] - p.y0;
+                    const int b0 = ty[4 * y + 2], b1 = ty[4 * y + 3];
+                    if (s0 < 0 || s1 >= p.y1 - p.y0 || b0 < 0 || b1 < 0) return false;
+                    rc.push_back((uint32_t)s0 | ((uint32_t)s1 << 16));
+                    rc.push_back((uint32_t)b0 | ((uint32_t)b1 << 16));
+                }
+                if (rowoff > 65535) return false;
+                rc[5 * l + 4] = (uint32_t)coloff | ((uint32_t)rowoff << 16);
+            }
+            const R& w0 = need[0];
+            if (((w0.x1 - w0.x0) >> 2) * (w0.y1 - w0.y0) > PYR_NT * PYR_U0) return false;
+            recs.push_back(std::move(rc));
+        }
+    for (auto& r : recs) stride = std::max(stride, round_up((int)r.size(), 4));
+    if (stride / 4 > PYR_NT * PYR_RU) return false;
+    cap = round_up(cap, 16);
+    lds = (size_t)stride * 4 + 2 * (size_t)cap;
+    if (lds > 64 * 1024) return false;
+    ntiles = (int)recs.size();
+    out.assign((size_t)ntiles * stride, 0u);
+    for (int t = 0; t < ntiles; t++) std::copy(recs[t].begin(), recs[t].end(), out.begin() + (size_t)t * stride);
+    return true;
+}
+
 static int ensure(orbfe_extractor* h, int W, int H, int B) {
     if (W == h->W && H == h->H && B <= h->cap_b) return ORBFE_OK;
     HIPCHK(hipSetDevice(h->device));
@@ -346,6 +480,7 @@ static int ensure(orbfe_extractor* h, int W, int H, int B) {
         h->fast_lds = fl;
         memcpy(h->fast_lds_lv, fl_lv, sizeof(fl_lv));
         h->oct_lds = oct;
+        if (!build_pyr_tiles(h->g, h->tab, h->ptile, h->pt_n, h->pt_stride, h->pt_cap, h->pt_lds)) h->pt_n = 0;
         h->W = W;
         h->H = H;
     } else {
@@ -355,6 +490,10 @@ static int ensure(orbfe_extractor* h, int W, int H, int B) {
     const OrbGeom& g = h->g;
     HIPCHK(hipMalloc(&h->d_tab, std::max<size_t>(2, h->tab.size() * 2)));
     HIPCHK(hipMemcpy(h->d_tab, h->tab.data(), h->tab.size() * 2, hipMemcpyHostToDevice));
+    if (h->pt_n > 0) {
+        HIPCHK(hipMalloc(&h->d_ptile, h->ptile.size() * 4));
+        HIPCHK(hipMemcpy(h->d_ptile, h->ptile.data(), h->ptile.size() * 4, hipMemcpyHostToDevice));
+    }
     HIPCHK(hipMalloc(&h->d_pyr, (size_t)B * g.pyr_bytes));
     HIPCHK(hipMalloc(&h->d_cellkeys, (size_t)B * g.cellkeys_per_img * 4));
     HIPCHK(hipMalloc(&h->d_cellcnt, (size_t)B * g.total_cells * 4));
@@ -484,7 +623,12 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
         for (int i = 0; al0 && i < B; i++) al0 = (((uintptr_t)host_ptrs[i]) & 3) == 0;
         // ComputePyramid: one launch per level (level l from level l - 1); the row-streamed k_resize_s
         // unless the level's column windows break its rules (then the LDS-tiled k_resize)
-        for (int l = 1; l < g.nlevels; l++) {
+        // a small batch: the whole pyramid in one launch (k_pyramid) when the tiles fit its limits
+        const bool fused_pyr = small && h->pt_n > 0 && !h->no_fused_pyramid;
+        if (fused_pyr)
+            hipLaunchKernelGGL(k_pyramid, dim3(h->pt_n, B), dim3(PYR_NT), h->pt_lds, s, P, pitch, h->d_pyr, g.pyr_bytes, g,
+                               h->d_ptile, h->pt_stride, h->pt_cap, al0 ? 1 : 0);
+        for (int l = 1; l < g.nlevels && !fused_pyr; l++) {
             const OrbLevel& L = g.lv[l];
             if (L.rs_ok && (l > 1 || al0)) {
                 const int rows = gr.lv[l].rs_rows;
@@ -1116,6 +1260,13 @@ int orbfe_debug_copy(orbfe_extractor* h, int what, int image, int level, void* d
     return count;
 }
 
+#if ORBFE_OCT_STAMPS
+// diagnostic builds: the per-wave stamps of the last block sort of block (0, 0)
+int orbfe_debug_sort_stamps(uint64_t* out) {
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sort_ts), (16 * 16 + 16) * 8));
+    return 272;
+}
+#endif
 int orbfe_debug_block_sort(uint64_t* data, int n) {
     if (!data || n < 0 || n > 4096) return ORBFE_E_ARG;
     if (n == 0) return 0;
@@ -1129,7 +1280,7 @@ int orbfe_debug_block_sort(uint64_t* data, int n) {
     HIPCHK(hipFree(d));
 #if ORBFE_OCT_STAMPS
     {
-        unsigned long long ts[16 * 16];
+        unsigned long long ts[16 * 16 + 16];
         HIPCHK(hipMemcpyFromSymbol(ts, HIP_SYMBOL(g_sort_ts), sizeof(ts)));
         fprintf(stderr, "sortts n=%d", n);
         for (int w = 0; w < OCT_NT / 64; w++) {
@@ -1137,7 +1288,7 @@ int orbfe_debug_block_sort(uint64_t* data, int n) {
             for (int k = 1; k < (int)ts[w * 16 + 15] && k < 15; k++) fprintf(stderr, " %lld", (long long)(ts[w * 16 + k] - ts[0]));
         }
         fprintf(stderr, " | s64:");
-        for (int k = 1; k < (int)ts[8 * 16 + 15] && k < 15; k++) fprintf(stderr, " %lld", (long long)(ts[8 * 16 + k] - ts[8 * 16 + k - 1]));
+        for (int k = 1; k < (int)ts[256 + 15] && k < 15; k++) fprintf(stderr, " %lld", (long long)(ts[256 + k] - ts[256 + k - 1]));
         fprintf(stderr, "\n");
     }
 #endif

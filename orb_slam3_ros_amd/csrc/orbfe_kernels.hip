@@ -541,6 +541,120 @@ __global__ __launch_bounds__(64 * RS_WPB) void k_resize_s(const uint8_t* const* 
     resize_s_item(imgs, in_pitch, pyr, pyr_stride, tab, g, l, nstrips, item, b);
 }
 
+// ---------------------------------------------------------------------------------------------
+// K1c: the whole pyramid (levels 1 .. nlevels-1) in ONE launch for small batches, where the chain
+// of per-level launches is latency-bound (each ~5 us for a few thousand pixels). One block per
+// (tile, image): a tile owns a rectangle of every level (the same fraction of each level, columns
+// on multiples of 4) and builds the rectangle it NEEDS at each level (what it owns plus the source
+// cone of its higher levels, computed on the host from the same coefficient tables), level by
+// level in LDS; only owned dwords are stored. Per pixel the arithmetic is k_resize's (H = S[sx]
+// a0 + S[sx+1] a1, a0 = 2048 / a1 = 0 past xmax; the universal-intrinsic rounding below simd_end,
+// the >> 22 form above), so the levels are bit-identical to the chained launches. The block reads
+// its tile record (header + relative column / row tables) and its level-0 window in one batch of
+// loads, then touches global memory only to store.
+// Record (dwords): per level l a 5-dword header {ax0 | ax1 << 16, ny0 | ny1 << 16, ox0 | ox1 << 16,
+// oy0 | oy1 << 16, coloff | rowoff << 16}; per level >= 1 the needed columns (sx - ax0(l-1) |
+// min(sx + 1, last) - ax0(l-1) << 15 | simd << 30, a0 | a1 << 16) and rows (s0 - ny0(l-1) |
+// s1 - ny0(l-1) << 16, b0 | b1 << 16).
+// ---------------------------------------------------------------------------------------------
+#define PYR_NT 512
+#define PYR_RU 4     // record 16-byte chunks per thread
+#define PYR_U0 8     // level-0 window dwords per thread
+__global__ __launch_bounds__(PYR_NT) void k_pyramid(const uint8_t* const* imgs, int in_pitch, uint8_t* pyr, int pyr_stride,
+                                                    OrbGeom g, const uint32_t* __restrict__ ptile, int pt_stride, int cap,
+                                                    int al0) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_pyr[];
+    const int lb = xcd_logical(block_linear(), gridDim.x * gridDim.y);
+    const int tile = lb % gridDim.x, b = lb / gridDim.x;
+    const int tid = threadIdx.x;
+    uint32_t* srec = (uint32_t*)smem_pyr;
+    uint8_t* buf0 = smem_pyr + (size_t)pt_stride * 4;
+    uint8_t* buf1 = buf0 + cap;
+    const uint32_t* rec = ptile + (size_t)tile * pt_stride;
+    const uint32_t hx = rec[0], hy = rec[1];
+    const int ax0 = (int)(hx & 0xffff), ax1 = (int)(hx >> 16), ny0 = (int)(hy & 0xffff), ny1 = (int)(hy >> 16);
+    const int dpr = (ax1 - ax0) >> 2, items0 = dpr * (ny1 - ny0);
+    const int W0 = g.lv[0].w;
+    gptr_u8 src = as_global(imgs[b]);
+    // every load of the block issued before any store
+    orbfe_u32x4 rv[PYR_RU];
+#pragma unroll
+    for (int u = 0; u < PYR_RU; u++) {
+        const int i = tid + PYR_NT * u;
+        if (i < (pt_stride >> 2)) rv[u] = ((const ORBFE_GLOBAL orbfe_u32x4*)rec)[i];
+    }
+    uint32_t wv[PYR_U0];
+#pragma unroll
+    for (int u = 0; u < PYR_U0; u++) {
+        const int i = tid + PYR_NT * u;
+        wv[u] = 0u;
+        if (i < items0) {
+            const int r = small_div(i, dpr), c = i - r * dpr;
+            const int x = ax0 + 4 * c;
+            gptr_u8 sp = src + (size_t)(ny0 + r) * in_pitch + x;
+            if (al0 && x + 4 <= W0) {
+                wv[u] = *(const ORBFE_GLOBAL uint32_t*)sp;
+            } else {
+                uint32_t w = 0u;
+                for (int k = 0; k < 4; k++)
+                    if (x + k < W0) w |= (uint32_t)sp[k] << (8 * k);
+                wv[u] = w;
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < PYR_RU; u++) {
+        const int i = tid + PYR_NT * u;
+        if (i < (pt_stride >> 2)) ((orbfe_u32x4*)srec)[i] = rv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < PYR_U0; u++) {
+        const int i = tid + PYR_NT * u;
+        if (i < items0) ((uint32_t*)buf0)[i] = wv[u];   // rows of (ax1 - ax0) bytes, dword-packed
+    }
+    SYNC();
+    for (int l = 1; l < g.nlevels; l++) {
+        const OrbLevel& L = g.lv[l];
+        const uint32_t* hp = srec + 5 * (l - 1);
+        const uint32_t* hl = srec + 5 * l;
+        const int sw = (int)(hp[0] >> 16) - (int)(hp[0] & 0xffff);
+        const int dx0 = (int)(hl[0] & 0xffff), dw = (int)(hl[0] >> 16) - dx0;
+        const int dy0 = (int)(hl[1] & 0xffff), drows = (int)(hl[1] >> 16) - dy0;
+        const int ox0 = (int)(hl[2] & 0xffff), ox1 = (int)(hl[2] >> 16);
+        const int oy0 = (int)(hl[3] & 0xffff), oy1 = (int)(hl[3] >> 16);
+        const uint2* cols = (const uint2*)(srec + (hl[4] & 0xffff));
+        const uint2* rows = (const uint2*)(srec + (hl[4] >> 16));
+        const uint8_t* sb = (l & 1) ? buf0 : buf1;   // level l - 1
+        uint8_t* db = (l & 1) ? buf1 : buf0;
+        uint8_t* gdst = pyr + (size_t)b * pyr_stride + L.pyr_off;
+        const int ngr = dw >> 2, items = ngr * drows;
+        for (int i = tid; i < items; i += PYR_NT) {
+            const int r = small_div(i, ngr), gi = i - r * ngr;
+            const uint2 rw = rows[r];
+            const uint8_t* s0 = sb + (int)(rw.x & 0xffff) * sw;
+            const uint8_t* s1 = sb + (int)(rw.x >> 16) * sw;
+            const uint32_t b0 = rw.y & 0xffff, b1 = rw.y >> 16;
+            uint32_t packed = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint2 cw = cols[4 * gi + q];
+                const int x0 = (int)(cw.x & 0x7fff), x1 = (int)((cw.x >> 15) & 0x7fff);
+                const uint32_t a0 = cw.y & 0xffff, a1 = cw.y >> 16;
+                const uint32_t H0 = (uint32_t)s0[x0] * a0 + (uint32_t)s0[x1] * a1;
+                const uint32_t H1 = (uint32_t)s1[x0] * a0 + (uint32_t)s1[x1] * a1;
+                const uint32_t v = (cw.x >> 30)
+                                       ? (mulhi_u24((H0 << 4) & 0xFFFF00u, b0 << 8) + mulhi_u24((H1 << 4) & 0xFFFF00u, b1 << 8) + 2u) >> 2
+                                       : (H0 * b0 + H1 * b1 + (1u << 21)) >> 22;
+                packed |= v << (8 * q);
+            }
+            *(uint32_t*)(db + r * dw + 4 * gi) = packed;
+            const int x = dx0 + 4 * gi, y = dy0 + r;
+            if (x >= ox0 && x < ox1 && y >= oy0 && y < oy1) *(uint32_t*)(gdst + (size_t)y * L.pitch + x) = packed;
+        }
+        SYNC();
+    }
+}
+
 // Gaussian 7x7 quantised kernel taps (the blur itself is fused into k_describe, K5).
 struct BlurKernel { int k[7]; };
 
@@ -1203,7 +1317,11 @@ __device__ __forceinline__ void wave_leaf(unsigned long long* a, int lo, int hi)
 }
 
 #if ORBFE_OCT_STAMPS
-__device__ unsigned long long g_sort_ts[16 * 16];   // diagnostic: per-wave phase stamps of the last block sort
+// diagnostic builds: per-wave phase stamps of the last block sort of block (0, 0) (16 waves x 16)
+// and of wave 0's last register sort (16 more), buffered in LDS (a global store would make the
+// next barrier wait for it) and flushed at the end of the sort
+__device__ unsigned long long g_sort_ts[16 * 16 + 16];
+__shared__ unsigned long long s_dbg_ts[16 * 16 + 16];
 #endif
 __device__ __forceinline__ unsigned long long rl64(unsigned long long x, int l) {
     const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)x, l);
@@ -1234,7 +1352,7 @@ __device__ __forceinline__ void wave_sort64(unsigned long long* a, int lo0, int 
     const int lane = lane_id();
 #if ORBFE_OCT_STAMPS
     int s64i = 0;
-#define S64_STAMP() do { if (lane == 0 && s64i < 15 && (threadIdx.x >> 6) == 0) g_sort_ts[8 * 16 + s64i] = __builtin_amdgcn_s_memtime(); s64i++; } while (0)
+#define S64_STAMP() do { if (lane == 0 && s64i < 15 && (threadIdx.x >> 6) == 0 && blockIdx.x == 0 && blockIdx.y == 0) s_dbg_ts[256 + s64i] = __builtin_amdgcn_s_memtime(); s64i++; } while (0)
 #else
 #define S64_STAMP() do { } while (0)
 #endif
@@ -1332,7 +1450,7 @@ __device__ __forceinline__ void wave_sort64(unsigned long long* a, int lo0, int 
     WAVE_SYNC();
     S64_STAMP();
 #if ORBFE_OCT_STAMPS
-    if (lane == 0 && (threadIdx.x >> 6) == 0) g_sort_ts[8 * 16 + 15] = s64i;
+    if (lane == 0 && (threadIdx.x >> 6) == 0 && blockIdx.x == 0 && blockIdx.y == 0) s_dbg_ts[256 + 15] = s64i;
 #endif
 #undef S64_STAMP
 }
@@ -1381,7 +1499,7 @@ __device__ __forceinline__ void block_introsort(unsigned long long* a, int n, in
     const int lane = lane_id(), wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
 #if ORBFE_OCT_STAMPS
     int sti = 0;
-#define SORT_STAMP() do { if (lane == 0 && sti < 15) g_sort_ts[wave * 16 + sti] = __builtin_amdgcn_s_memtime(); sti++; } while (0)
+#define SORT_STAMP() do { if (lane == 0 && sti < 15 && blockIdx.x == 0 && blockIdx.y == 0) s_dbg_ts[wave * 16 + sti] = __builtin_amdgcn_s_memtime(); sti++; } while (0)
 #else
 #define SORT_STAMP() do { } while (0)
 #endif
@@ -1437,7 +1555,10 @@ __device__ __forceinline__ void block_introsort(unsigned long long* a, int n, in
     SYNC();
     SORT_STAMP();
 #if ORBFE_OCT_STAMPS
-    if (lane == 0) g_sort_ts[wave * 16 + 15] = sti;
+    if (lane == 0 && blockIdx.x == 0 && blockIdx.y == 0) s_dbg_ts[wave * 16 + 15] = sti;
+    SYNC();
+    if (blockIdx.x == 0 && blockIdx.y == 0)
+        for (int i = threadIdx.x; i < 16 * 16 + 16; i += blockDim.x) g_sort_ts[i] = s_dbg_ts[i];
 #endif
 #undef SORT_STAMP
 }
@@ -1509,7 +1630,14 @@ __global__ __launch_bounds__(NT) void k_octree(OrbGeom g, const uint32_t* __rest
     // diagnostic phase stamps (image 0 of the batch, every level), tstamp == nullptr in normal runs
     unsigned long long* ts = (tstamp && b == 0) ? tstamp + 64 * l : nullptr;
     int tsi = 0;
-#define OCT_STAMP() do { if (ts && tid == 0 && tsi < 62) ts[tsi] = __builtin_amdgcn_s_memtime(); tsi++; } while (0)
+    (void)ts;
+    (void)tsi;
+#if ORBFE_OCT_STAMPS
+    __shared__ unsigned long long s_octts[64];
+#define OCT_STAMP() do { if (ts && tid == 0 && tsi < 62) s_octts[tsi] = __builtin_amdgcn_s_memtime(); tsi++; } while (0)
+#else
+#define OCT_STAMP() do { } while (0)
+#endif
     OCT_STAMP();
     // ---- gather this level's cell key lists in cell order (vToDistributeKeys order) ----
     const int* cc = cellcnt + (size_t)b * g.total_cells + L.cell_base;
@@ -1527,13 +1655,22 @@ __global__ __launch_bounds__(NT) void k_octree(OrbGeom g, const uint32_t* __rest
     uint32_t* keys = lkeys + kbase;
     uint16_t* nof = nodeof + kbase;
     const uint32_t* ck = cellkeys + kbase;
+    // Keys of this level held in registers for the whole kernel when they fit (key k = tid + NT * u
+    // in rkv[u], its node in rq[u]): no key / node-index round trips through global memory, and no
+    // barrier waiting on their stores. Otherwise the global lists (lkeys, nodeof) carry them.
+    constexpr int OU = NT >= 1024 ? 8 : OCT_U;
+    const bool regk = K <= NT * OU;
+    uint32_t rkv[OU];
+    int rq[OU];
     // the gather also counts the keys of each initial node (ORBextractor.cc:559-601's root columns;
     // wave-uniform trip counts: the aggregated increments need every lane)
-    for (int kb = 0; kb < K; kb += NT * OCT_U) {
+    for (int kb = 0; kb < K; kb += NT * OU) {
         const int k0 = kb + tid;
-        uint32_t v[OCT_U];
+        uint32_t v[OU];
 #pragma unroll
-        for (int u = 0; u < OCT_U; u++) {
+        for (int u = 0; u < OU; u++) {
+            if ((u & 3) == 0 && kb + NT * u >= K) break;   // block-uniform, per group of 4 slots (the
+                                                             // group's chains interleave)
             const int k = min(k0 + NT * u, K - 1);
             int lo = 0, hi = ncell - 1;   // largest c with cellpre[c] <= k
             while (lo < hi) {
@@ -1543,8 +1680,10 @@ __global__ __launch_bounds__(NT) void k_octree(OrbGeom g, const uint32_t* __rest
             v[u] = ck[(size_t)lo * L.cell_cap + (k - cellpre[lo])];
         }
 #pragma unroll
-        for (int u = 0; u < OCT_U; u++) {
-            if (k0 + NT * u < K) keys[k0 + NT * u] = v[u];
+        for (int u = 0; u < OU; u++) {
+            if ((u & 3) == 0 && kb + NT * u >= K) break;
+            if (regk) rkv[u] = v[u];   // regk: this loop runs once
+            else if (k0 + NT * u < K) keys[k0 + NT * u] = v[u];
             atomic_inc_runs(tmpA, (int)((float)(v[u] & 0xfff) / hX), k0 + NT * u < K);
         }
     }
@@ -1565,17 +1704,19 @@ __global__ __launch_bounds__(NT) void k_octree(OrbGeom g, const uint32_t* __rest
         }
     }
     SYNC();
-    for (int kb = 0; kb < K; kb += NT * OCT_U) {
+    for (int kb = 0; kb < K; kb += NT * OU) {
         const int k0 = kb + tid;
-        uint32_t v[OCT_U];
+        uint32_t v[OU];
 #pragma unroll
-        for (int u = 0; u < OCT_U; u++) v[u] = keys[min(k0 + NT * u, K - 1)];
+        for (int u = 0; u < OU; u++) v[u] = regk ? rkv[u] : keys[min(k0 + NT * u, K - 1)];
 #pragma unroll
-        for (int u = 0; u < OCT_U; u++) {
+        for (int u = 0; u < OU; u++) {
+            if ((u & 3) == 0 && kb + NT * u >= K) break;
             const int k = k0 + NT * u;
             const uint32_t key = v[u];
             const int q = tmpB[(int)((float)(key & 0xfff) / hX)];
-            if (k < K) nof[k] = (uint16_t)q;
+            if (regk) rq[u] = q;
+            else if (k < K) nof[k] = (uint16_t)q;
             atomic_inc_runs(Ccnt, 4 * q + quadrant(key, Cx0[q], Cx1[q], Cy0[q], Cy1[q]), k < K && Csz[q] > 1);
         }
     }
@@ -1670,6 +1811,9 @@ __global__ __launch_bounds__(NT) void k_octree(OrbGeom g, const uint32_t* __rest
                 SYNC();
             } else {
                 // std::sort(vPrevSizeAndPointerToNode, compareNodes) (ORBextractor.cc:700), exact replica
+#if ORBFE_OCT_STAMPS
+                if (ts && tid == 0) s_octts[62] = (unsigned long long)m | ((unsigned long long)n << 16) | ((unsigned long long)K << 32);
+#endif
                 block_introsort(expv, m, tmpC, tmpA, tmpB, Xcnt + 2 * NC, (unsigned long long*)Xcnt, segs, s_ws,
                                 s_misc);
                 OCT_STAMP();
@@ -1773,25 +1917,27 @@ __global__ __launch_bounds__(NT) void k_octree(OrbGeom g, const uint32_t* __rest
             OCT_STAMP();
         }
         // key sweep: move keys to their new node positions and count the next split
-        for (int kb = 0; kb < K; kb += NT * OCT_U) {
+        for (int kb = 0; kb < K; kb += NT * OU) {
             const int k0 = kb + tid;
-            uint32_t v[OCT_U];
-            int qv[OCT_U];
+            uint32_t v[OU];
+            int qv[OU];
 #pragma unroll
-            for (int u = 0; u < OCT_U; u++) {
+            for (int u = 0; u < OU; u++) {
                 const int k = min(k0 + NT * u, K - 1);
-                v[u] = keys[k];
-                qv[u] = nof[k];
+                v[u] = regk ? rkv[u] : keys[k];
+                qv[u] = regk ? rq[u] : nof[k];
             }
 #pragma unroll
-            for (int u = 0; u < OCT_U; u++) {
+            for (int u = 0; u < OU; u++) {
+                if ((u & 3) == 0 && kb + NT * u >= K) break;
                 const int k = k0 + NT * u;
                 const uint32_t key = v[u];
                 const int q = qv[u];
                 int np;
                 if (divorder[q] >= 0) np = childpos[4 * q + quadrant(key, Cx0[q], Cx1[q], Cy0[q], Cy1[q])];
                 else np = newpos[q];
-                if (k < K) nof[k] = (uint16_t)np;
+                if (regk) rq[u] = np;
+                else if (k < K) nof[k] = (uint16_t)np;
                 atomic_inc_runs(Xcnt, 4 * np + quadrant(key, Xx0[np], Xx1[np], Xy0[np], Xy1[np]), k < K && Xsz[np] > 1);
             }
         }
@@ -1817,18 +1963,19 @@ __global__ __launch_bounds__(NT) void k_octree(OrbGeom g, const uint32_t* __rest
     unsigned long long* best = (unsigned long long*)Xcnt;
     for (int i = tid; i < n; i += NT) best[i] = 0ull;
     SYNC();
-    for (int k0 = tid; k0 < K; k0 += NT * OCT_U) {
-        uint32_t v[OCT_U];
-        int qv[OCT_U];
+    for (int k0 = tid; k0 < K; k0 += NT * OU) {
+        uint32_t v[OU];
+        int qv[OU];
 #pragma unroll
-        for (int u = 0; u < OCT_U; u++) {
+        for (int u = 0; u < OU; u++) {
             const int k = min(k0 + NT * u, K - 1);
-            v[u] = keys[k];
-            qv[u] = nof[k];
+            v[u] = regk ? rkv[u] : keys[k];
+            qv[u] = regk ? rq[u] : nof[k];
         }
 #pragma unroll
-        for (int u = 0; u < OCT_U; u++) {
+        for (int u = 0; u < OU; u++) {
             const int k = k0 + NT * u;
+            if ((u & 3) == 0 && k0 - tid + NT * u >= K) break;
             if (k < K)
                 atomicMax(&best[qv[u]], ((unsigned long long)(v[u] >> 24) << 32) | (0xFFFFFFFFull - (unsigned)k));
         }
@@ -1836,26 +1983,51 @@ __global__ __launch_bounds__(NT) void k_octree(OrbGeom g, const uint32_t* __rest
     SYNC();
     uint32_t* ok = outkeys + (size_t)b * g.out_per_img + L.out_off;
     int* rk = ranks + (size_t)b * g.out_per_img + L.out_off;
-    // lapping flag per output node, then ranks among lapping / non-lapping keys (block scans)
-    for (int i = tid; i < n; i += NT) {
-        const unsigned k = 0xFFFFFFFFu - (unsigned)(best[i] & 0xFFFFFFFFull);
-        const uint32_t key = keys[k];
+    // the output key of each node and its lapping flag: written by the thread holding the node's
+    // winning key (registers), or read back from the global key list
+    auto emit = [&](int i, uint32_t key) {
         const int x = (int)(key & 0xfff) + ORBFE_MINB, y = (int)((key >> 12) & 0xfff) + ORBFE_MINB;
         ok[i] = (uint32_t)x | ((uint32_t)y << 12) | (key & 0xff000000u);
         const float sx = (l == 0) ? (float)x : (float)x * L.scale;
-        const bool lap = sx >= (float)lap0 && sx <= (float)lap1;
-        tmpA[i] = lap ? 1 : 0;
-        tmpB[i] = lap ? 0 : 1;
+        tmpA[i] = (sx >= (float)lap0 && sx <= (float)lap1) ? 1 : 0;
+    };
+    if (regk) {
+#pragma unroll
+        for (int u = 0; u < OU; u++) {
+            const int k = tid + NT * u;
+            if ((u & 3) == 0 && NT * u >= K) break;
+            if (k < K && best[rq[u]] == (((unsigned long long)(rkv[u] >> 24) << 32) | (0xFFFFFFFFull - (unsigned)k)))
+                emit(rq[u], rkv[u]);
+        }
+    } else {
+        for (int i = tid; i < n; i += NT) emit(i, keys[0xFFFFFFFFu - (unsigned)(best[i] & 0xFFFFFFFFull)]);
     }
     SYNC();
-    const int nlap = block_excl_scan<NT>(tmpA, n, s_ws);
-    const int nmono = block_excl_scan<NT>(tmpB, n, s_ws);
-    for (int i = tid; i < n; i += NT) {
-        const bool lap = (i + 1 < n ? tmpA[i + 1] : nlap) != tmpA[i];
-        rk[i] = lap ? (int)(0x40000000 | tmpA[i]) : tmpB[i];
+    // ranks among lapping / non-lapping keys
+    int nlap, nmono;
+    if (n <= NT) {
+        const int f = tid < n ? tmpA[tid] : 0;
+        int exl, exm;
+        block_scan2<NT>(f, tid < n ? 1 - f : 0, s_ws2, exl, exm, nlap, nmono);
+        if (tid < n) rk[tid] = f ? (int)(0x40000000 | exl) : exm;
+    } else {
+        for (int i = tid; i < n; i += NT) tmpB[i] = 1 - tmpA[i];
+        SYNC();
+        nlap = block_excl_scan<NT>(tmpA, n, s_ws);
+        nmono = block_excl_scan<NT>(tmpB, n, s_ws);
+        for (int i = tid; i < n; i += NT) {
+            const bool lap = (i + 1 < n ? tmpA[i + 1] : nlap) != tmpA[i];
+            rk[i] = lap ? (int)(0x40000000 | tmpA[i]) : tmpB[i];
+        }
     }
     OCT_STAMP();
-    if (ts && tid == 0) ts[63] = (unsigned long long)tsi;
+#if ORBFE_OCT_STAMPS
+    if (ts && tid == 0) {
+        for (int i = 0; i < min(tsi, 62); i++) ts[i] = s_octts[i];
+        ts[62] = s_octts[62];
+        ts[63] = (unsigned long long)tsi;
+    }
+#endif
 #undef OCT_STAMP
     if (tid == 0) {
         int* inf = lvinfo + ((size_t)b * g.nlevels + l) * 4;

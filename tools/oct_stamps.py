@@ -40,7 +40,19 @@ def main():
             return 1
         k = int(ts[63])
         d = np.diff(ts[:min(k, 62)].astype(np.int64))
-        print(f"level {l}: {k} stamps, total {int(ts[min(k, 62) - 1] - ts[0])} cycles: {d.tolist()}")
+        info = int(ts[62])
+        print(f"level {l}: {k} stamps, total {int(ts[min(k, 62) - 1] - ts[0])} cycles: {d.tolist()}"
+              f" (last sort m={info & 0xffff} n={(info >> 16) & 0xffff} K={info >> 32})")
+    if hasattr(fe.lib, "orbfe_debug_sort_stamps"):
+        st = np.zeros(272, np.uint64)
+        fe.lib.orbfe_debug_sort_stamps(ctypes.c_void_p(st.ctypes.data))
+        t0 = int(st[0])
+        for w in range(16):
+            k = int(st[w * 16 + 15])
+            if k:
+                print(f"sort w{w}:", [int(st[w * 16 + j]) - t0 for j in range(1, min(k, 15))])
+        k = int(st[256 + 15])
+        print("s64 (wave 0, last call):", np.diff(st[256:256 + min(k, 15)].astype(np.int64)).tolist())
     return 0
 
 
