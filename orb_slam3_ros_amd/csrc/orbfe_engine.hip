@@ -348,7 +348,14 @@ static bool build_pyr_tiles(const OrbGeom& g, const std::vector<int16_t>& tab, s
     lds = 0;
     if (nl < 2) return false;
     const int W1 = g.lv[1].w, H1 = g.lv[1].h;
-    int TX = std::max(1, (W1 + 79) / 80), TY = std::max(1, (H1 + 63) / 64);
+    // level-1 tile target (ORBFE_PYR_TILE=WxH overrides, for A/B runs): 48x40 at 752x480 makes
+    // 13 x 10 tiles; 80x64 / 64x48 measured +10 % / +8 % (tools/gpu_pyr_ab.sh)
+    int tw = 48, th = 40;
+    if (const char* e = getenv("ORBFE_PYR_TILE")) {
+        int a = 0, c = 0;
+        if (sscanf(e, "%dx%d", &a, &c) == 2 && a >= 8 && c >= 8) { tw = a; th = c; }
+    }
+    int TX = std::max(1, (W1 + tw - 1) / tw), TY = std::max(1, (H1 + th - 1) / th);
     struct R { int x0, x1, y0, y1; };
     auto own = [&](int l, int i, int j, int TXn, int TYn) {
         const OrbLevel& L = g.lv[l];

@@ -557,9 +557,13 @@ __global__ __launch_bounds__(64 * RS_WPB) void k_resize_s(const uint8_t* const* 
 // min(sx + 1, last) - ax0(l-1) << 15 | simd << 30, a0 | a1 << 16) and rows (s0 - ny0(l-1) |
 // s1 - ny0(l-1) << 16, b0 | b1 << 16).
 // ---------------------------------------------------------------------------------------------
-#define PYR_NT 512
-#define PYR_RU 4     // record 16-byte chunks per thread
-#define PYR_U0 8     // level-0 window dwords per thread
+#ifndef PYR_NT
+#define PYR_NT 1024   // threads per tile block (512 / 256: +7 % / +29 % at 48x40 tiles, tools/gpu_pyr_ab.sh)
+#endif
+#define PYR_RU 2     // record 16-byte chunks per thread
+#ifndef PYR_U0
+#define PYR_U0 4     // level-0 window dwords per thread
+#endif
 __global__ __launch_bounds__(PYR_NT) void k_pyramid(const uint8_t* const* imgs, int in_pitch, uint8_t* pyr, int pyr_stride,
                                                     OrbGeom g, const uint32_t* __restrict__ ptile, int pt_stride, int cap,
                                                     int al0) {
