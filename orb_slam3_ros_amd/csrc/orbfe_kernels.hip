@@ -1589,7 +1589,7 @@ __global__ __launch_bounds__(OCT_NT) void k_debug_block_sort(unsigned long long*
 // where the level-0 and level-1 blocks are the frame's long pole and nothing else competes for
 // the CUs) takes NT = 1024: the key sweeps and scans run in a quarter of the iterations.
 template <int NT>
-__global__ __launch_bounds__(NT) void k_octree(OrbGeom g, const uint32_t* __restrict__ cellkeys,
+__global__ __launch_bounds__(NT, NT <= 256 ? 6 : 1) void k_octree(OrbGeom g, const uint32_t* __restrict__ cellkeys,
                                                    const int* __restrict__ cellcnt, uint32_t* lkeys,
                                                    uint16_t* nodeof, uint32_t* outkeys, int* lvinfo, int* ranks,
                                                    const int2* __restrict__ laps, unsigned long long* tstamp,
@@ -1663,7 +1663,9 @@ __global__ __launch_bounds__(NT) void k_octree(OrbGeom g, const uint32_t* __rest
     // in rkv[u], its node in rq[u]): no key / node-index round trips through global memory, and no
     // barrier waiting on their stores. Otherwise the global lists (lkeys, nodeof) carry them.
     constexpr int OU = NT >= 1024 ? 8 : OCT_U;
-    const bool regk = K <= NT * OU;
+    // (the 1024-thread small-batch instance only: at 256 threads the batch fills the CUs, and the
+    // registers would cost resident blocks)
+    const bool regk = NT >= 1024 && K <= NT * OU;
     uint32_t rkv[OU];
     int rq[OU];
     // the gather also counts the keys of each initial node (ORBextractor.cc:559-601's root columns;
