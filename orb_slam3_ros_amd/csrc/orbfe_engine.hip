@@ -74,6 +74,7 @@ struct orbfe_extractor {
     double scale_factor;
     int resize_simd_lanes = 16;
     bool no_fused_pyramid = getenv("ORBFE_NO_FUSED_PYRAMID") != nullptr;   // A/B: the chained launches
+    bool fused_pyramid_batch = getenv("ORBFE_FUSED_PYR_BATCH") != nullptr;  // A/B: k_pyramid for large batches too
     int blur_variant = 0;
     std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
     std::vector<int> per_level;
@@ -631,7 +632,7 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
         // ComputePyramid: one launch per level (level l from level l - 1); the row-streamed k_resize_s
         // unless the level's column windows break its rules (then the LDS-tiled k_resize)
         // a small batch: the whole pyramid in one launch (k_pyramid) when the tiles fit its limits
-        const bool fused_pyr = small && h->pt_n > 0 && !h->no_fused_pyramid;
+        const bool fused_pyr = h->pt_n > 0 && !h->no_fused_pyramid && (small || h->fused_pyramid_batch);
         if (fused_pyr)
             hipLaunchKernelGGL(k_pyramid, dim3(h->pt_n, B), dim3(PYR_NT), h->pt_lds, s, P, pitch, h->d_pyr, g.pyr_bytes, g,
                                h->d_ptile, h->pt_stride, h->pt_cap, al0 ? 1 : 0);
@@ -659,7 +660,8 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
             fast_range(s, 0, g.nlevels);
         } else {
             if (fork) HIPCHK(hipEventRecord(h->ev_fork[1], s2));
-            if (lmid < g.nlevels) fast_range(s, lmid, g.nlevels);
+            if (fused_pyr) fast_range(s, 1, g.nlevels);   // level 0's FAST ran beside the pyramid
+            else if (lmid < g.nlevels) fast_range(s, lmid, g.nlevels);
             if (fork) HIPCHK(hipStreamWaitEvent(s, h->ev_fork[1], 0));
         }
     }
