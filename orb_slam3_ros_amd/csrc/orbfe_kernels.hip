@@ -1804,6 +1804,96 @@ __global__ __launch_bounds__(NT, NT <= 256 ? 6 : 1) void k_octree(OrbGeom g, con
             for (int j = tid; j < 4 * newN; j += NT) Xcnt[j] = 0;
             SYNC();
             OCT_STAMP();
+        } else if (phase2 && m <= NT && n <= NT) {
+            // Phase-2 step fused: std::sort(vPrevSizeAndPointerToNode, compareNodes) (ORBextractor.cc:700),
+            // exact replica, then the walk from the back (ORBextractor.cc:701-748) and the rebuild with
+            // three scans in two packed block scans: sorted position t = thread (node expv[m-1-t])
+#if ORBFE_OCT_STAMPS
+            if (ts && tid == 0) s_octts[62] = (unsigned long long)m | ((unsigned long long)n << 16) | ((unsigned long long)K << 32);
+#endif
+            block_introsort(expv, m, tmpC, tmpA, tmpB, Xcnt + 2 * NC, (unsigned long long*)Xcnt, segs, s_ws,
+                            s_misc);
+            OCT_STAMP();
+            const int t = tid;
+            const bool live = t < m;
+            int q = 0;
+            int4 cq = make_int4(0, 0, 0, 0);
+            if (live) {
+                q = (int)(expv[m - 1 - t] & 0xffffffffull);
+                cq = *(const int4*)&Ccnt[4 * q];
+            }
+            const int cv[4] = {cq.x, cq.y, cq.z, cq.w};
+            int c = 0, e = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) { c += cv[k] > 0; e += cv[k] > 1; }
+            const int grow = live ? c - 1 : 0;   // the list grows by (children - 1) per division
+            if (tid == 0) s_misc[6] = m;
+            int exG, exCE, totG, totCE;
+            block_scan2<NT>(grow, c | (e << 16), s_ws2, exG, exCE, totG, totCE);
+            // first t at which the list reaches N: nodes [0, T_div) of the walk divide
+            if (live && n + exG + grow >= N) atomicMin(&s_misc[6], t + 1);
+            if (live) tmpB[t] = exCE + (c | (e << 16));   // inclusive (children | expandable << 16)
+            SYNC();
+            const int T_div = s_misc[6];
+            const int tot = T_div > 0 ? tmpB[T_div - 1] : 0;
+            const int Ctot = tot & 0xffff;
+            Etot = tot >> 16;
+            if (t < T_div) {
+                divorder[q] = t;
+                // children: block of t starts at sum_{t'>t} c_t'; order n4,n3,n2,n1 (push_front)
+                const int start = Ctot - ((exCE & 0xffff) + c);
+                int kk = 0;
+                const int px0 = Cx0[q], px1 = Cx1[q], py0 = Cy0[q], py1 = Cy1[q];
+                int cpos[4];
+#pragma unroll
+                for (int ch = 3; ch >= 0; ch--) {
+                    const int v = cv[ch];
+                    cpos[ch] = -1;
+                    if (v > 0) {
+                        const int np = start + kk++;
+                        cpos[ch] = np;
+                        childpos[4 * q + ch] = (int16_t)np;
+                        int a0, a1, b0, b1;
+                        child_rect(ch, px0, px1, py0, py1, &a0, &a1, &b0, &b1);
+                        Xx0[np] = (int16_t)a0; Xx1[np] = (int16_t)a1;
+                        Xy0[np] = (int16_t)b0; Xy1[np] = (int16_t)b1;
+                        Xsz[np] = v;
+                    } else {
+                        childpos[4 * q + ch] = -1;
+                    }
+                }
+                int ei = exCE >> 16;
+#pragma unroll
+                for (int ch = 0; ch < 4; ch++) {
+                    const int v = cv[ch];
+                    if (v > 1) {
+                        int a0, a1, b0, b1;
+                        child_rect(ch, px0, px1, py0, py1, &a0, &a1, &b0, &b1);
+                        expv[ei] = ((unsigned long long)v << 44) | ((unsigned long long)(a0 & 0xfff) << 32) |
+                                   (unsigned long long)(uint16_t)cpos[ch];
+                        ei++;
+                    }
+                }
+            }
+            SYNC();
+            // undivided nodes keep their relative order after the pushed children
+            const int i = tid;
+            const bool keep = i < n && divorder[i] < 0;
+            int exK, exZ, nKeep, totZ;
+            block_scan2<NT>(keep ? 1 : 0, 0, s_ws2, exK, exZ, nKeep, totZ);
+            (void)exZ;
+            (void)totZ;
+            if (keep) {
+                const int np = Ctot + exK;
+                newpos[i] = (int16_t)np;
+                Xx0[np] = Cx0[i]; Xx1[np] = Cx1[i];
+                Xy0[np] = Cy0[i]; Xy1[np] = Cy1[i];
+                Xsz[np] = Csz[i];
+            }
+            newN = Ctot + nKeep;
+            for (int j = tid; j < 4 * newN; j += NT) Xcnt[j] = 0;
+            SYNC();
+            OCT_STAMP();
         } else {
             int T_div;   // number of divided nodes in this step
             if (!phase2) {
