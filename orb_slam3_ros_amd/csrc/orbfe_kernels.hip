@@ -1652,7 +1652,13 @@ __global__ __launch_bounds__(NT, NT <= 256 ? 6 : 1) void k_octree(OrbGeom g, con
     const int nIni = L.n_ini;
     const float hX = L.hx;
     const int H = (L.h - ORBFE_MINB) - ORBFE_MINB;
+    // registers hold the keys (below) and the initial columns fit one per thread: the gather also
+    // counts each key's root quadrant by column (a root's rectangle is its column's), so the
+    // initial nodes need no second pass over the keys
+    const bool fini = NT >= 1024 && K <= NT * (NT >= 1024 ? 8 : OCT_U) && nIni <= NT;
     for (int i = tid; i < nIni; i += NT) tmpA[i] = 0;
+    if (fini)
+        for (int i = tid; i < 4 * nIni; i += NT) tmpC[i] = 0;
     for (int i = tid; i < 4 * NC; i += NT) Ccnt[i] = 0;
     SYNC();
     const size_t kbase = (size_t)b * g.cellkeys_per_img + L.cellkey_off;
@@ -1690,15 +1696,49 @@ __global__ __launch_bounds__(NT, NT <= 256 ? 6 : 1) void k_octree(OrbGeom g, con
             if ((u & 3) == 0 && kb + NT * u >= K) break;
             if (regk) rkv[u] = v[u];   // regk: this loop runs once
             else if (k0 + NT * u < K) keys[k0 + NT * u] = v[u];
-            atomic_inc_runs(tmpA, (int)((float)(v[u] & 0xfff) / hX), k0 + NT * u < K);
+            const int col = (int)((float)(v[u] & 0xfff) / hX);
+            atomic_inc_runs(tmpA, col, k0 + NT * u < K);
+            if (fini) {
+                rq[u] = col;   // remapped to the root's list position below
+                atomic_inc_runs(tmpC, 4 * col + quadrant(v[u], (int)(hX * (float)col), (int)(hX * (float)(col + 1)), 0, H),
+                                k0 + NT * u < K);
+            }
         }
     }
     OCT_STAMP();
     // ---- initial nodes (ORBextractor.cc:559-601) ----
     SYNC();
+    int n;
+    if (fini) {
+        // one thread per column: the non-empty columns in order are the initial list; their counts
+        // and quadrant counts come from the gather; each key's column becomes its node position
+        const int i = tid;
+        const bool f = i < nIni && tmpA[i] > 0;
+        int ex, exZ, totZ;
+        block_scan2<NT>(f ? 1 : 0, 0, s_ws2, ex, exZ, n, totZ);
+        (void)exZ;
+        (void)totZ;
+        if (f) {
+            Cx0[ex] = (int16_t)(int)(hX * (float)i);
+            Cx1[ex] = (int16_t)(int)(hX * (float)(i + 1));
+            Cy0[ex] = 0;
+            Cy1[ex] = (int16_t)H;
+            Csz[ex] = tmpA[i];
+            *(int4*)&Ccnt[4 * ex] = *(const int4*)&tmpC[4 * i];
+        }
+        if (i < nIni) tmpB[i] = ex;
+        for (int j = tid; j < NC; j += NT) divorder[j] = -1;
+        SYNC();
+#pragma unroll
+        for (int u = 0; u < (NT >= 1024 ? 8 : OCT_U); u++) {
+            if ((u & 3) == 0 && NT * u >= K) break;   // the slots the gather filled
+            rq[u] = tmpB[rq[u]];
+        }
+        OCT_STAMP();
+    } else {
     for (int i = tid; i < nIni; i += NT) tmpB[i] = tmpA[i] > 0 ? 1 : 0;
     SYNC();
-    int n = block_excl_scan<NT>(tmpB, nIni, s_ws);   // position of each non-empty root
+    n = block_excl_scan<NT>(tmpB, nIni, s_ws);   // position of each non-empty root
     for (int i = tid; i < nIni; i += NT) {
         if (tmpA[i] > 0) {
             const int q = tmpB[i];
@@ -1729,6 +1769,7 @@ __global__ __launch_bounds__(NT, NT <= 256 ? 6 : 1) void k_octree(OrbGeom g, con
     for (int i = tid; i < NC; i += NT) divorder[i] = -1;
     SYNC();
     OCT_STAMP();
+    }
 
     const int N = L.budget;
     bool phase2 = false, finish = false;
