@@ -2464,7 +2464,10 @@ __device__ __forceinline__ void describe_one(const DescSlot& d, const OrbGeom& g
 // 6 waves per SIMD: 79 VGPRs, no spill since the pattern is held as f16 (at 5 waves without a spill
 // or 6 with one the kernel measured slower or equal: 1 slot / 4 slots at 5, 6, 7 waves, 2, 3 and 8
 // slots, tools/gpu_variants_trace.sh; DESIGN.md §7d, profiles/r03_kernel_ab.txt items 18-19)
-#define DP_ATTR __attribute__((amdgpu_waves_per_eu(6)))
+#ifndef DP_WAVES
+#define DP_WAVES 6
+#endif
+#define DP_ATTR __attribute__((amdgpu_waves_per_eu(DP_WAVES)))
 // DP_WPB: waves per block: 2 / 4 / 8 measured 1.04 / 1.06 / 1.11 ms (r03_kernel_ab.txt item 23); 12
 // blocks of 12.7 KB per CU give the same 6 waves per SIMD with finer-grained refill
 #define DP_WPB 2
