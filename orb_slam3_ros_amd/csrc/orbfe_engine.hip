@@ -75,6 +75,7 @@ struct orbfe_extractor {
     int resize_simd_lanes = 16;
     bool no_fused_pyramid = getenv("ORBFE_NO_FUSED_PYRAMID") != nullptr;   // A/B: the chained launches
     bool fused_pyramid_batch = getenv("ORBFE_FUSED_PYR_BATCH") != nullptr;  // A/B: k_pyramid for large batches too
+    bool no_pull = getenv("ORBFE_NO_PULL") != nullptr;   // A/B: the frame call's results by DMA copies
     int blur_variant = 0;
     std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
     std::vector<int> per_level;
@@ -716,6 +717,16 @@ __global__ __launch_bounds__(256) void k_copy16(const orbfe_u32x4* __restrict__ 
     for (; i < n; i += blockDim.x) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
 }
 
+// The stereo frame call's results written straight into the caller-side pinned block (mapped,
+// coherent) by the launch stream: no copy-engine start-up between the last kernel and the results
+// (a DMA started ~13 us after the stereo kernels in the drop-in trace). 16-byte items.
+__global__ __launch_bounds__(256) void k_pull2(const orbfe_u32x4* __restrict__ s0, orbfe_u32x4* d0, int n0,
+                                               const orbfe_u32x4* __restrict__ s1, orbfe_u32x4* d1, int n1) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n0) d0[i] = s0[i];
+    else if (i - n0 < n1) d1[i - n0] = s1[i - n0];
+}
+
 extern "C" {
 
 const char* orbfe_version(void) { return "orbfe 0.1 (gfx950, HIP)"; }
@@ -948,7 +959,7 @@ int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int width, int height,
         if (h->h_pin) HIPCHK(hipHostFree(h->h_pin));
         h->h_pin = nullptr;
         h->pin_bytes = 0;
-        HIPCHK(hipHostMalloc((void**)&h->h_pin, pin_need, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc((void**)&h->h_pin, pin_need, hipHostMallocMapped | hipHostMallocCoherent));
         h->pin_bytes = pin_need;
     }
     // the previous call's result copies out of h_pin have completed (that call synchronised)
@@ -1102,7 +1113,7 @@ int orbfe_stereo_match(orbfe_extractor* left, orbfe_extractor* right, float bf, 
         if (left->h_pin) HIPCHK(hipHostFree(left->h_pin));
         left->h_pin = nullptr;
         left->pin_bytes = 0;
-        HIPCHK(hipHostMalloc((void**)&left->h_pin, need, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc((void**)&left->h_pin, need, hipHostMallocMapped | hipHostMallocCoherent));
         left->pin_bytes = need;
     }
     uint8_t* hp = left->h_pin;
@@ -1164,7 +1175,7 @@ int orbfe_frame_stereo(orbfe_extractor* left, orbfe_extractor* right, const uint
         h->d_uright = h->d_depth = nullptr;
         h->d_nmatch = nullptr;
         h->stereo_kp = 0;
-        HIPCHK(hipMalloc(&h->d_st, 16 + (size_t)kc * 8));
+        HIPCHK(hipMalloc(&h->d_st, (16 + (size_t)kc * 8 + 15) & ~(size_t)15));   // whole 16-byte items (k_pull2)
         h->d_nmatch = (int*)h->d_st;
         h->d_uright = (float*)(h->d_st + 16);
         h->d_depth = h->d_uright + kc;
@@ -1175,12 +1186,13 @@ int orbfe_frame_stereo(orbfe_extractor* left, orbfe_extractor* right, const uint
     size_t o_kps, o_desc, o_end;
     out_layout(2, kc, &o_kps, &o_desc, &o_end);
     const size_t o_st = (o_end + 15) & ~(size_t)15, st_bytes = 16 + (size_t)h->stereo_kp * 8;
-    const size_t pin_need = std::max(2 * bytes, o_st + st_bytes);
+    const size_t st16 = (st_bytes + 15) & ~(size_t)15;
+    const size_t pin_need = std::max(2 * bytes, o_st + st16);
     if (h->pin_bytes < pin_need) {
         if (h->h_pin) HIPCHK(hipHostFree(h->h_pin));
         h->h_pin = nullptr;
         h->pin_bytes = 0;
-        HIPCHK(hipHostMalloc((void**)&h->h_pin, pin_need, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc((void**)&h->h_pin, pin_need, hipHostMallocMapped | hipHostMallocCoherent));
         h->pin_bytes = pin_need;
     }
     uint8_t* hp = h->h_pin;
@@ -1207,14 +1219,23 @@ int orbfe_frame_stereo(orbfe_extractor* left, orbfe_extractor* right, const uint
     rc = orbfe_stereo_match_batch(h, 0, 1, h, 1, 1, 1, bf, fx, h->d_uright, h->d_depth, h->d_nmatch, s);
     if (rc) return rc;
     if (tm) HIPCHK(hipEventRecord(h->call_ev[4], s));
-    if (h->cap_b == 2) {   // the handle's two-image output block: one copy
-        HIPCHK(hipMemcpyAsync(hp, h->d_out, o_end, hipMemcpyDeviceToHost, s));
+    if (h->cap_b == 2 && !h->no_pull) {   // the two-image output block and the stereo results: one kernel
+        uint8_t* hpd = nullptr;
+        HIPCHK(hipHostGetDevicePointer((void**)&hpd, hp, 0));
+        const int n0 = (int)(o_end / 16), n1 = (int)(st16 / 16);
+        hipLaunchKernelGGL(k_pull2, dim3((n0 + n1 + 255) / 256), dim3(256), 0, s, (const orbfe_u32x4*)h->d_out,
+                           (orbfe_u32x4*)hpd, n0, (const orbfe_u32x4*)h->d_st, (orbfe_u32x4*)(hpd + o_st), n1);
+        HIPCHK(hipGetLastError());
     } else {
-        HIPCHK(hipMemcpyAsync(hp, h->last_counts, 16, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(hp + o_kps, h->last_kps, (size_t)2 * kc * sizeof(OrbKeyPoint), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(hp + o_desc, h->last_desc, (size_t)2 * kc * 32, hipMemcpyDeviceToHost, s));
+        if (h->cap_b == 2) {   // the handle's two-image output block: one copy
+            HIPCHK(hipMemcpyAsync(hp, h->d_out, o_end, hipMemcpyDeviceToHost, s));
+        } else {
+            HIPCHK(hipMemcpyAsync(hp, h->last_counts, 16, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(hp + o_kps, h->last_kps, (size_t)2 * kc * sizeof(OrbKeyPoint), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(hp + o_desc, h->last_desc, (size_t)2 * kc * 32, hipMemcpyDeviceToHost, s));
+        }
+        HIPCHK(hipMemcpyAsync(hp + o_st, h->d_st, st_bytes, hipMemcpyDeviceToHost, s));
     }
-    HIPCHK(hipMemcpyAsync(hp + o_st, h->d_st, st_bytes, hipMemcpyDeviceToHost, s));
     if (tm) HIPCHK(hipEventRecord(h->call_ev[5], s));
     HIPCHK(hipStreamSynchronize(s));
     int cnt[4], nm = 0;
