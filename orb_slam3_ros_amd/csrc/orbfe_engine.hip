@@ -76,6 +76,7 @@ struct orbfe_extractor {
     bool no_fused_pyramid = getenv("ORBFE_NO_FUSED_PYRAMID") != nullptr;   // A/B: the chained launches
     bool fused_pyramid_batch = getenv("ORBFE_FUSED_PYR_BATCH") != nullptr;  // A/B: k_pyramid for large batches too
     bool no_pull = getenv("ORBFE_NO_PULL") != nullptr;   // A/B: the frame call's results by DMA copies
+    bool no_push = getenv("ORBFE_NO_PUSH") != nullptr;   // A/B: the frame call's images by a DMA copy
     int blur_variant = 0;
     std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
     std::vector<int> per_level;
@@ -727,6 +728,16 @@ __global__ __launch_bounds__(256) void k_pull2(const orbfe_u32x4* __restrict__ s
     else if (i - n0 < n1) d1[i - n0] = s1[i - n0];
 }
 
+// The stereo frame call's two images read from the mapped pinned staging block by the launch
+// stream (16-byte items, then a byte tail): the host-to-device copy without a copy-engine start-up.
+__global__ __launch_bounds__(256) void k_push(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, size_t bytes) {
+    const size_t n16 = bytes / 16;
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n16) ((orbfe_u32x4*)dst)[i] = ((const orbfe_u32x4*)src)[i];
+    else if (i == n16)
+        for (size_t k = n16 * 16; k < bytes; k++) dst[k] = src[k];
+}
+
 extern "C" {
 
 const char* orbfe_version(void) { return "orbfe 0.1 (gfx950, HIP)"; }
@@ -1209,7 +1220,16 @@ int orbfe_frame_stereo(orbfe_extractor* left, orbfe_extractor* right, const uint
     const uint8_t* ptrs[2] = {h->d_stage, h->d_stage + bytes};
     const int laps[4] = {0, 0, 0, 0};   // the pinhole stereo Frame passes vLappingArea {0, 0} (Frame.cc:122-123)
     if (tm) HIPCHK(hipEventRecord(h->call_ev[0], s));
-    HIPCHK(hipMemcpyAsync(h->d_stage, hp, 2 * bytes, hipMemcpyHostToDevice, s));
+    if (!h->no_push) {
+        uint8_t* hpd = nullptr;
+        HIPCHK(hipHostGetDevicePointer((void**)&hpd, hp, 0));
+        const size_t n16 = 2 * bytes / 16;
+        hipLaunchKernelGGL(k_push, dim3((unsigned)((n16 + 1 + 255) / 256)), dim3(256), 0, s, (const uint8_t*)hpd,
+                           h->d_stage, 2 * bytes);
+        HIPCHK(hipGetLastError());
+    } else {
+        HIPCHK(hipMemcpyAsync(h->d_stage, hp, 2 * bytes, hipMemcpyHostToDevice, s));
+    }
     if (tm) HIPCHK(hipEventRecord(h->call_ev[1], s));
     h->timing = false;   // the call's own events bracket the kernels (the stage ring is for batches)
     rc = run_batch(h, 2, ptrs, width, laps, s, false);
