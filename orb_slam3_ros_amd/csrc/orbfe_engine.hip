@@ -1208,27 +1208,36 @@ int orbfe_frame_stereo(orbfe_extractor* left, orbfe_extractor* right, const uint
     }
     uint8_t* hp = h->h_pin;
     const uint8_t* src[2] = {img_left, img_right};
+    const bool tm = h->timing;
+    if (tm && !h->call_ev[0])
+        for (auto& e : h->call_ev) HIPCHK(hipEventCreate(&e));
+    uint8_t* hpd = nullptr;
+    if (!h->no_push) HIPCHK(hipHostGetDevicePointer((void**)&hpd, hp, 0));
+    // whole 16-byte items per image: the left image's push runs while the right one is packed
+    const bool split = !h->no_push && (bytes % 16) == 0;
     for (int i = 0; i < 2; i++) {
         if (stride == width) memcpy(hp + i * bytes, src[i], bytes);
         else
             for (int y = 0; y < height; y++)
                 memcpy(hp + i * bytes + (size_t)y * width, src[i] + (size_t)y * stride, width);
+        if (split) {
+            if (i == 0 && tm) HIPCHK(hipEventRecord(h->call_ev[0], s));
+            hipLaunchKernelGGL(k_push, dim3((unsigned)((bytes / 16 + 1 + 255) / 256)), dim3(256), 0, s,
+                               (const uint8_t*)hpd + i * bytes, h->d_stage + i * bytes, bytes);
+            HIPCHK(hipGetLastError());
+        }
     }
-    const bool tm = h->timing;
-    if (tm && !h->call_ev[0])
-        for (auto& e : h->call_ev) HIPCHK(hipEventCreate(&e));
     const uint8_t* ptrs[2] = {h->d_stage, h->d_stage + bytes};
     const int laps[4] = {0, 0, 0, 0};   // the pinhole stereo Frame passes vLappingArea {0, 0} (Frame.cc:122-123)
-    if (tm) HIPCHK(hipEventRecord(h->call_ev[0], s));
-    if (!h->no_push) {
-        uint8_t* hpd = nullptr;
-        HIPCHK(hipHostGetDevicePointer((void**)&hpd, hp, 0));
-        const size_t n16 = 2 * bytes / 16;
-        hipLaunchKernelGGL(k_push, dim3((unsigned)((n16 + 1 + 255) / 256)), dim3(256), 0, s, (const uint8_t*)hpd,
-                           h->d_stage, 2 * bytes);
-        HIPCHK(hipGetLastError());
-    } else {
-        HIPCHK(hipMemcpyAsync(h->d_stage, hp, 2 * bytes, hipMemcpyHostToDevice, s));
+    if (!split) {   // both images in one push (an image size that is not whole 16-byte items), or by DMA
+        if (tm) HIPCHK(hipEventRecord(h->call_ev[0], s));
+        if (!h->no_push) {
+            hipLaunchKernelGGL(k_push, dim3((unsigned)((2 * bytes / 16 + 1 + 255) / 256)), dim3(256), 0, s,
+                               (const uint8_t*)hpd, h->d_stage, 2 * bytes);
+            HIPCHK(hipGetLastError());
+        } else {
+            HIPCHK(hipMemcpyAsync(h->d_stage, hp, 2 * bytes, hipMemcpyHostToDevice, s));
+        }
     }
     if (tm) HIPCHK(hipEventRecord(h->call_ev[1], s));
     h->timing = false;   // the call's own events bracket the kernels (the stage ring is for batches)
