@@ -983,16 +983,30 @@ int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int width, int height,
     // the whole call as stream work: upload, the batch launches, and counts plus the whole keypoint /
     // descriptor capacity back in one round trip (61 KB at 1000 features: one transfer costs less
     // than a second synchronisation)
+    // (the mapped pinned block read / written by kernels on the stream, as in orbfe_frame_stereo)
+    uint8_t* hpd = nullptr;
+    if (!h->no_push || !h->no_pull) HIPCHK(hipHostGetDevicePointer((void**)&hpd, hp, 0));
     auto enqueue = [&]() -> int {
         if (tm) HIPCHK(hipEventRecord(h->call_ev[0], s));
-        HIPCHK(hipMemcpyAsync(h->d_stage, h->h_pin, bytes, hipMemcpyHostToDevice, s));
+        if (!h->no_push) {
+            hipLaunchKernelGGL(k_push, dim3((unsigned)((bytes / 16 + 1 + 255) / 256)), dim3(256), 0, s,
+                               (const uint8_t*)hpd, h->d_stage, bytes);
+            HIPCHK(hipGetLastError());
+        } else {
+            HIPCHK(hipMemcpyAsync(h->d_stage, h->h_pin, bytes, hipMemcpyHostToDevice, s));
+        }
         if (tm) HIPCHK(hipEventRecord(h->call_ev[1], s));
         h->timing = false;   // the call's own events bracket the kernels (the stage ring is for batches)
         const int r = run_batch(h, 1, ptrs, width, laps, s, false);
         h->timing = tm;
         if (r) return r;
         if (tm) HIPCHK(hipEventRecord(h->call_ev[2], s));
-        if (h->cap_b == 1 && kps && desc) {   // the handle's one-image output block: one copy
+        if (h->cap_b == 1 && kps && desc && !h->no_pull) {   // the one-image output block, by one kernel
+            const int n0 = (int)(o_end / 16);
+            hipLaunchKernelGGL(k_pull2, dim3((n0 + 255) / 256), dim3(256), 0, s, (const orbfe_u32x4*)h->d_out,
+                               (orbfe_u32x4*)hpd, n0, (const orbfe_u32x4*)nullptr, (orbfe_u32x4*)nullptr, 0);
+            HIPCHK(hipGetLastError());
+        } else if (h->cap_b == 1 && kps && desc) {   // the handle's one-image output block: one copy
             HIPCHK(hipMemcpyAsync(hp, h->d_out, o_end, hipMemcpyDeviceToHost, s));
         } else {
             HIPCHK(hipMemcpyAsync(hp, h->last_counts, 8, hipMemcpyDeviceToHost, s));
