@@ -351,9 +351,10 @@ static bool build_pyr_tiles(const OrbGeom& g, const std::vector<int16_t>& tab, s
     lds = 0;
     if (nl < 2) return false;
     const int W1 = g.lv[1].w, H1 = g.lv[1].h;
-    // level-1 tile target (ORBFE_PYR_TILE=WxH overrides, for A/B runs): 48x40 at 752x480 makes
-    // 13 x 10 tiles; 80x64 / 64x48 measured +10 % / +8 % (tools/gpu_pyr_ab.sh)
-    int tw = 48, th = 40;
+    // level-1 tile target (ORBFE_PYR_TILE=WxH overrides, for A/B runs): 56x40 at 752x480 makes
+    // 12 x 10 tiles; k_pyramid at B=2, 1024 threads: 32x32 14.0 us, 48x40 11.7-12.1, 56x40 10.6,
+    // 56x48 10.6-10.7, 64x48 10.9-11.0, 72x56 11.4 (r05_kernel_ab.txt item 12)
+    int tw = 56, th = 40;
     if (const char* e = getenv("ORBFE_PYR_TILE")) {
         int a = 0, c = 0;
         if (sscanf(e, "%dx%d", &a, &c) == 2 && a >= 8 && c >= 8) { tw = a; th = c; }
