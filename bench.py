@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import argparse
 import ctypes
+import datetime
 import json
 import os
 import subprocess
@@ -683,41 +684,58 @@ def config4_dist_leg(dev, rank, world, gloo, K=64, steps=10, warmup=3):
         rig.match(it[0] - 1)
         rig.drain()
 
-    for _ in range(warmup):
-        step()
-    finish()
-    torch.cuda.synchronize()
-    dist.barrier()
+    # Every rank reaches the same collectives in the same order whatever fails locally:
+    # a rank whose loop or checker raises records the error, skips only local work, and still joins
+    # the barrier / all_reduce(el) / all_reduce(flag) below. A failure INSIDE a step's own all-gather
+    # cannot be bridged this way; the process group's timeout (init in main) ends that case.
+    err = None
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    finish()
-    torch.cuda.synchronize()
+    try:
+        for _ in range(warmup):
+            step()
+        finish()
+        torch.cuda.synchronize()
+    except Exception as e:  # noqa: BLE001 - reported in the leg's result
+        err = f"warmup: {type(e).__name__}: {e}"[:400]
+    dist.barrier()
+    if err is None:
+        t0 = time.perf_counter()
+        try:
+            for _ in range(steps):
+                step()
+            finish()
+            torch.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001
+            err = f"timed loop: {type(e).__name__}: {e}"[:400]
     dist.barrier()
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cpu" if gloo else dev)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     el = float(el.item())
-    ok, detail = True, "right-camera rank (no kNN)"
-    if cam == 0:   # CHECKER, outside the timed region
-        from oracle import oracle
-        oracle.build()
-        l2r = rig.l2r.cpu().numpy()
-        ngood = rig.ngood.cpu().numpy()
-        for f in range(min(4, K)):
-            left, right = pairs[f % U]
-            ol, orr = oracle.OracleExtractor(1000, 1.2, 8, 20, 7), oracle.OracleExtractor(1000, 1.2, 8, 20, 7)
-            ml, kl, dl = ol(left, (0, 511))
-            mr, kr, dr = orr(right, (0, 511))
-            g, t, _ = oracle.stereo_knn_ratio(dl[ml:], dr[mr:], 0.7)
-            exp = np.full(rig.cap, -1, np.int32)
-            exp[ml:len(kl)][t >= 0] = t[t >= 0] + mr
-            if int(ngood[f]) != g or not np.array_equal(l2r[f], exp):
-                ok, detail = False, f"stream {stream} frame {f}: kNN candidates differ from the oracle"
-                break
-        else:
-            detail = f"stream {stream}: frames 0..3 of the last step bit-exact vs the CPU oracle"
-    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device="cpu" if gloo else dev)
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    ok, detail = err is None, err or "right-camera rank (no kNN)"
+    try:
+        if cam == 0 and err is None:   # CHECKER, outside the timed region
+            from oracle import oracle
+            oracle.build()
+            l2r = rig.l2r.cpu().numpy()
+            ngood = rig.ngood.cpu().numpy()
+            for f in range(min(4, K)):
+                left, right = pairs[f % U]
+                ol, orr = oracle.OracleExtractor(1000, 1.2, 8, 20, 7), oracle.OracleExtractor(1000, 1.2, 8, 20, 7)
+                ml, kl, dl = ol(left, (0, 511))
+                mr, kr, dr = orr(right, (0, 511))
+                g, t, _ = oracle.stereo_knn_ratio(dl[ml:], dr[mr:], 0.7)
+                exp = np.full(rig.cap, -1, np.int32)
+                exp[ml:len(kl)][t >= 0] = t[t >= 0] + mr
+                if int(ngood[f]) != g or not np.array_equal(l2r[f], exp):
+                    ok, detail = False, f"stream {stream} frame {f}: kNN candidates differ from the oracle"
+                    break
+            else:
+                detail = f"stream {stream}: frames 0..3 of the last step bit-exact vs the CPU oracle"
+    except Exception as e:  # noqa: BLE001
+        ok, detail = False, f"checker: {type(e).__name__}: {e}"[:400]
+    finally:
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device="cpu" if gloo else dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     rig.close()
     streams = world // 2
     return {"workload": "TUM-VI-like 512x512 KannalaBrandt8 stereo (BASELINE config 4): one camera per rank, "
@@ -751,6 +769,63 @@ def side_leg(dev, name, W, H, nf, F, steps, warmup, stereo, lap, bf, fx, check_f
     return out, ok
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_command(argv, gpus, port, python=sys.executable, script=None):
+    """The torchrun command line that runs this bench as `gpus` ranks on one node (one process per
+    GPU, rendezvous on 127.0.0.1), forwarding argv unchanged so every rank parses the same flags."""
+    return [python, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", script or os.path.abspath(__file__)] + list(argv)
+
+
+def maybe_launch(gpus, argv, env=None):
+    """`bench.py --gpus N` without an outer torchrun: spawn N ranks as a CHILD process (never exec:
+    nothing here has touched the GPU yet, and the parent never will) and return its exit code, the
+    rank-0 JSON line reaching our stdout through the inherited descriptor. Returns None when this
+    process is itself a rank (WORLD_SIZE set, equal to --gpus) or N = 1. A WORLD_SIZE that disagrees
+    with --gpus is an error: the line must never report fewer GPUs than were asked for."""
+    env = os.environ if env is None else env
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            print(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws}", file=sys.stderr, flush=True)
+            return 2
+        return None
+    if gpus <= 1:
+        return None
+    child_env = dict(env)
+    child_env.setdefault("MASTER_ADDR", "127.0.0.1")
+    child_env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    r = subprocess.run(launch_command(argv, gpus, _free_port()), env=child_env)
+    return r.returncode
+
+
+def launch_dry_run(args):
+    """--launch-dry-run: the rank plumbing alone (no GPU call): every rank joins a gloo group,
+    all-reduces its rank, and rank 0 prints the line's n_gpus. The CPU test of maybe_launch."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.tensor([rank], dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "rank_sum": int(t.item()), "gpus_flag": args.gpus, "dry_run": True}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -776,7 +851,16 @@ def main():
                     help="nccl = RCCL over xGMI (the measured path); gloo = CPU rehearsal of the multi-rank path")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank uses cuda:0 (rehearse N ranks on a 1-GPU box with --dist-backend gloo)")
+    ap.add_argument("--launch-dry-run", action="store_true",
+                    help="only the rank plumbing of --gpus N (gloo, no GPU): rank 0 prints n_gpus")
     args = ap.parse_args()
+
+    rc = maybe_launch(args.gpus, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
+    if args.launch_dry_run:
+        launch_dry_run(args)
+        return
 
     native = (None, None)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -796,9 +880,9 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if gloo:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=300))
 
     W, H, F = args.width, args.height, args.frames
     bf, fx = EUROC_BF, EUROC_FX

@@ -149,7 +149,8 @@ int orbfe_stereo_match(orbfe_extractor* left, orbfe_extractor* right, float bf, 
  * extractors from the same settings, Tracking.cc:637-645; else ORBFE_E_ARG); it is not written.
  * Outputs as orbfe_extract for each side (n_*, mono_* = monoIndex) and orbfe_stereo_match
  * (uright / depth [n_left]). Returns the pre-cut stereo match count. orbfe_get_call_timing(left)
- * then holds {upload, extraction kernels, result copies, stereo kernels, 0}. */
+ * then holds {upload, extraction kernels, result copies, stereo kernels, 0}; the upload slot runs
+ * from the left image's push to the right image's, so it includes the right image's host packing. */
 int orbfe_frame_stereo(orbfe_extractor* left, orbfe_extractor* right, const uint8_t* img_left,
                        const uint8_t* img_right, int width, int height, int stride, float bf, float fx,
                        orbfe_keypoint* kps_left, uint8_t* desc_left, int cap_left, int* n_left, int* mono_left,

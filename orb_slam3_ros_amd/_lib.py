@@ -120,6 +120,12 @@ class OrbfeError(RuntimeError):
     pass
 
 
+class OrbfeCapacityError(OrbfeError):
+    """ORBFE_E_CAPACITY: the call's inputs exceed a documented device limit (include/orbfe.h). No
+    device work ran and no output was written; the caller keeps its CPU body for this call, as the
+    C++ shim does (shim/ORBmatcher_backend_orbfe.cc). The library never falls back by itself."""
+
+
 def load(path: str | None = None) -> ctypes.CDLL:
     """Load liborbfe.so (raises OrbfeError if it is missing: there is no fallback path)."""
     global _lib
@@ -157,5 +163,6 @@ def load(path: str | None = None) -> ctypes.CDLL:
 def check(rc: int, what: str) -> int:
     if rc < 0 and rc != ORBFE_E_EMPTY:
         names = {ORBFE_E_ARG: "bad argument", ORBFE_E_DEVICE: "HIP device error", ORBFE_E_CAPACITY: "capacity"}
-        raise OrbfeError(f"{what} failed: {names.get(rc, rc)}")
+        cls = OrbfeCapacityError if rc == ORBFE_E_CAPACITY else OrbfeError
+        raise cls(f"{what} failed: {names.get(rc, rc)}")
     return rc

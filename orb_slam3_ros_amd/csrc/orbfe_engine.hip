@@ -66,6 +66,21 @@ void out_layout(int B, int kp_cap, size_t* kps, size_t* desc, size_t* end) {
     *end = *desc + (size_t)B * kp_cap * 32;
 }
 
+// A/B switches (tools/gpu_pyr_ab.sh) are read from the environment only by a diagnostic build
+// (tools/build_variant.sh NAME -DORBFE_AB_KNOBS=1); the product library's kernels, launch shapes
+// and transfer paths never depend on the caller's environment.
+#ifndef ORBFE_AB_KNOBS
+#define ORBFE_AB_KNOBS 0
+#endif
+inline bool ab_knob(const char* name) {
+#if ORBFE_AB_KNOBS
+    return getenv(name) != nullptr;
+#else
+    (void)name;
+    return false;
+#endif
+}
+
 }  // namespace
 
 struct orbfe_extractor {
@@ -73,10 +88,10 @@ struct orbfe_extractor {
     float scale_factor_f;
     double scale_factor;
     int resize_simd_lanes = 16;
-    bool no_fused_pyramid = getenv("ORBFE_NO_FUSED_PYRAMID") != nullptr;   // A/B: the chained launches
-    bool fused_pyramid_batch = getenv("ORBFE_FUSED_PYR_BATCH") != nullptr;  // A/B: k_pyramid for large batches too
-    bool no_pull = getenv("ORBFE_NO_PULL") != nullptr;   // A/B: the frame call's results by DMA copies
-    bool no_push = getenv("ORBFE_NO_PUSH") != nullptr;   // A/B: the frame call's images by a DMA copy
+    bool no_fused_pyramid = ab_knob("ORBFE_NO_FUSED_PYRAMID");   // A/B: the chained launches
+    bool fused_pyramid_batch = ab_knob("ORBFE_FUSED_PYR_BATCH");  // A/B: k_pyramid for large batches too
+    bool no_pull = ab_knob("ORBFE_NO_PULL");   // A/B: the frame call's results by DMA copies
+    bool no_push = ab_knob("ORBFE_NO_PUSH");   // A/B: the frame call's images by a DMA copy
     int blur_variant = 0;
     std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
     std::vector<int> per_level;
@@ -351,14 +366,16 @@ static bool build_pyr_tiles(const OrbGeom& g, const std::vector<int16_t>& tab, s
     lds = 0;
     if (nl < 2) return false;
     const int W1 = g.lv[1].w, H1 = g.lv[1].h;
-    // level-1 tile target (ORBFE_PYR_TILE=WxH overrides, for A/B runs): 56x40 at 752x480 makes
+    // level-1 tile target (ORBFE_PYR_TILE=WxH overrides it in an -DORBFE_AB_KNOBS=1 build): 56x40 at 752x480 makes
     // 12 x 10 tiles; k_pyramid at B=2, 1024 threads: 32x32 14.0 us, 48x40 11.7-12.1, 56x40 10.6,
     // 56x48 10.6-10.7, 64x48 10.9-11.0, 72x56 11.4 (r05_kernel_ab.txt item 12)
     int tw = 56, th = 40;
+#if ORBFE_AB_KNOBS
     if (const char* e = getenv("ORBFE_PYR_TILE")) {
         int a = 0, c = 0;
         if (sscanf(e, "%dx%d", &a, &c) == 2 && a >= 8 && c >= 8) { tw = a; th = c; }
     }
+#endif
     int TX = std::max(1, (W1 + tw - 1) / tw), TY = std::max(1, (H1 + th - 1) / th);
     struct R { int x0, x1, y0, y1; };
     auto own = [&](int l, int i, int j, int TXn, int TYn) {
@@ -1298,7 +1315,10 @@ int orbfe_frame_stereo(orbfe_extractor* left, orbfe_extractor* right, const uint
     memcpy(desc_right, hd + (size_t)kc * 32, (size_t)cnt[2] * 32);
     memcpy(uright, hp + o_st + 16, (size_t)cnt[0] * 4);
     memcpy(depth, hp + o_st + 16 + (size_t)h->stereo_kp * 4, (size_t)cnt[0] * 4);
-    if (tm) {   // {upload, extract kernels, stereo kernels, result copies}
+    // slots as the header documents: {upload, extraction kernels, result copies, stereo kernels}. On the
+    // split path the upload slot starts at the left image's push and so also counts the host packing
+    // of the right image (the GPU waits for it): it is push + packing, not a pure transfer time.
+    if (tm) {
         HIPCHK(hipEventElapsedTime(&h->call_ms[0], h->call_ev[0], h->call_ev[1]));
         HIPCHK(hipEventElapsedTime(&h->call_ms[1], h->call_ev[1], h->call_ev[2]));
         HIPCHK(hipEventElapsedTime(&h->call_ms[3], h->call_ev[2], h->call_ev[4]));

@@ -2196,6 +2196,12 @@ __global__ __launch_bounds__(256) void k_knn2_batch(StereoSide SL, StereoSide SR
 // =============================================================================================
 namespace {
 
+// The zero-copy status words: a commit kernel stores the slots and st[0..3,5], fences at system
+// scope, then stores the sequence word st[4]. The host spin reads st[4] with ACQUIRE semantics, so
+// neither the compiler nor the CPU may move the later reads of the slots (memcpy from the mapped
+// block) or of st[0..5] above the read that saw the new sequence number.
+inline int host_seq_acquire(volatile int* st) { return __atomic_load_n((int*)&st[4], __ATOMIC_ACQUIRE); }
+
 struct MatchScratch {
     int device = -1;
     hipStream_t stream = nullptr;
@@ -2582,10 +2588,10 @@ int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* m
     }
     timer.end();
     volatile int* st = t_ms.hs;
-    for (unsigned spin = 1; st[4] != seq; spin++) {
+    for (unsigned spin = 1; host_seq_acquire(st) != seq; spin++) {
         if ((spin & 1023) == 0) {   // bounded: a stream that finished without publishing is an error
             const hipError_t e = hipStreamQuery(s);
-            if (e == hipSuccess && st[4] != seq) return ORBFE_E_DEVICE;
+            if (e == hipSuccess && host_seq_acquire(st) != seq) return ORBFE_E_DEVICE;
             if (e != hipSuccess && e != hipErrorNotReady) HIPCHK(e);
         }
         __builtin_ia32_pause();
@@ -2735,10 +2741,10 @@ int sbp_multi_run(const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, co
             m.tail_stream = s;
         }
         timer.end();
-        for (unsigned spin = 1; st[4] != io.seq; spin++) {
+        for (unsigned spin = 1; host_seq_acquire(st) != io.seq; spin++) {
             if ((spin & 1023) == 0) {   // bounded: a stream that finished without publishing is an error
                 const hipError_t e = hipStreamQuery(s);
-                if (e == hipSuccess && st[4] != io.seq) {
+                if (e == hipSuccess && host_seq_acquire(st) != io.seq) {
                     m.mdirty = true;
                     return ORBFE_E_DEVICE;
                 }
@@ -2969,10 +2975,10 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
                 HIPCHK(hipMemcpyAsync(mvp, mvp_d, (size_t)n * 4, hipMemcpyDeviceToHost, s));
                 HIPCHK(hipStreamSynchronize(s));
             }
-            for (unsigned spin = 1; st[4] != seq; spin++) {
+            for (unsigned spin = 1; host_seq_acquire(st) != seq; spin++) {
                 if ((spin & 1023) == 0) {   // bounded: a stream that finished without publishing is an error
                     const hipError_t e = hipStreamQuery(s);
-                    if (e == hipSuccess && st[4] != seq) return ORBFE_E_DEVICE;
+                    if (e == hipSuccess && host_seq_acquire(st) != seq) return ORBFE_E_DEVICE;
                     if (e != hipSuccess && e != hipErrorNotReady) HIPCHK(e);
                 }
                 __builtin_ia32_pause();

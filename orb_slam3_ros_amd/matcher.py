@@ -420,7 +420,9 @@ class ORBmatcher:
     def SearchForTriangulationEpi(self, KF1: MatchFrame, mp1, fv1: FeatureVector, KF2: MatchFrame, mp2,
                                   fv2: FeatureVector, ep, epipolar, bOnlyStereo=False):
         """epipolar(idx1, idx2) -> bool: pCamera1->epipolarConstrain for that keypoint pair. Returns
-        (nmatches, matches12) as SearchForTriangulation."""
+        (nmatches, matches12) as SearchForTriangulation. Raises _lib.OrbfeCapacityError when the
+        shared vocabulary nodes need more than 16 M candidate slots (orbfe.h): the caller then runs its
+        own CPU body for this keyframe pair, as the C++ shim does."""
         m1 = _i32(np.ascontiguousarray(mp1, np.int32), KF1.N, "mp1")
         m2 = _i32(np.ascontiguousarray(mp2, np.int32), KF2.N, "mp2")
         e = np.ascontiguousarray(ep, np.float32).reshape(2)

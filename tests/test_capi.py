@@ -32,3 +32,24 @@ def test_descriptor_distance_host_entry(orbfe_lib):
     b = np.zeros(32, np.uint8)
     b[0], b[31] = 0xFF, 0x01
     assert orbfe_lib.orbfe_descriptor_distance(a.ctypes.data, b.ctypes.data) == 9
+
+
+def test_triangulation_epi_capacity_is_reported():
+    """ORBFE_E_CAPACITY of orbfe_search_for_triangulation_epi (> 16 M candidate slots: one shared
+    vocabulary node of 4100 x 4100 entries) reaches a Python caller as OrbfeCapacityError, before any
+    device work (this runs without a GPU), so the caller can keep its CPU body."""
+    import numpy as np
+    import pytest
+    from orb_slam3_ros_amd import synth_match as sm
+    from orb_slam3_ros_amd._lib import OrbfeCapacityError
+    from orb_slam3_ros_amd.matcher import FeatureVector, ORBmatcher
+    rng = np.random.default_rng(3)
+    n = 4100
+    A, B = sm.synth_frame(rng, n, stereo=False), sm.synth_frame(rng, n, stereo=False)
+    fv = FeatureVector({7: list(range(n))})
+    mp = np.full(n, -1, np.int32)
+    calls = []
+    with pytest.raises(OrbfeCapacityError):
+        ORBmatcher(0.6, True).SearchForTriangulationEpi(A, mp, fv, B, mp.copy(), fv, np.zeros(2, np.float32),
+                                                        lambda i, j: calls.append((i, j)) or True)
+    assert not calls

@@ -198,36 +198,46 @@ def test_rig_layout_gloo():
     assert dict(out) == {0: 1, 1: 1}
 
 
-def _rig_gpu_worker(rank, world, port, K, out):
+def _rig_gpu_worker(rank, world, port, K, steps, out):
     import numpy as np
     from oracle import oracle
+    from orb_slam3_ros_amd.synth import synth_stereo
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     stream, cam = odist.rig_role(rank)
-    frames = _rig_frames(stream, K)
-    imgs = torch.from_numpy(np.stack([p[cam] for p in frames])).cuda()
+    # a distinct stereo pair for every (step, frame): a wrong slab index, or a gather overwritten by
+    # a later extraction, shows up as another step's kNN
+    frames = [[synth_stereo(7000 + 1000 * k + 100 * stream + f, 512, 512) for f in range(K)] for k in range(steps)]
+    imgs = [torch.from_numpy(np.stack([p[cam] for p in fr])).cuda() for fr in frames]
     rig = odist.StereoRigExchange(K, 512, 512, device=torch.device("cuda", 0))
-    for k in range(3):   # three steps over the two slabs, the match lagging one step
-        rig.extract(imgs, k)
+    got = []
+
+    def take():
+        torch.cuda.synchronize()
+        got.append((rig.l2r.cpu().numpy().copy(), rig.ngood.cpu().numpy().copy()))
+
+    for k in range(steps):   # steps >= 3: slabs 0 and 1 are both reused, the match lagging one step
+        rig.extract(imgs[k], k)
         if k:
             rig.match(k - 1)
-    rig.match(2)
+            take()
+    rig.match(steps - 1)
     rig.drain()
-    torch.cuda.synchronize()
+    take()
     ok = True
     if cam == 0:
-        l2r = rig.l2r.cpu().numpy()
-        ngood = rig.ngood.cpu().numpy()
-        for f, (left, right) in enumerate(frames):
-            ol, orr = oracle.OracleExtractor(1000, 1.2, 8, 20, 7), oracle.OracleExtractor(1000, 1.2, 8, 20, 7)
-            ml, kl, dl = ol(left, (0, 511))
-            mr, kr, dr = orr(right, (0, 511))
-            g, t, _ = oracle.stereo_knn_ratio(dl[ml:], dr[mr:], 0.7)
-            exp = np.full(rig.cap, -1, np.int32)
-            exp[ml:len(kl)][t >= 0] = t[t >= 0] + mr
-            ok = ok and int(ngood[f]) == g and np.array_equal(l2r[f], exp)
+        for k in range(steps):
+            l2r, ngood = got[k]
+            for f, (left, right) in enumerate(frames[k]):
+                ol, orr = oracle.OracleExtractor(1000, 1.2, 8, 20, 7), oracle.OracleExtractor(1000, 1.2, 8, 20, 7)
+                ml, kl, dl = ol(left, (0, 511))
+                mr, kr, dr = orr(right, (0, 511))
+                g, t, _ = oracle.stereo_knn_ratio(dl[ml:], dr[mr:], 0.7)
+                exp = np.full(rig.cap, -1, np.int32)
+                exp[ml:len(kl)][t >= 0] = t[t >= 0] + mr
+                ok = ok and int(ngood[f]) == g and np.array_equal(l2r[f], exp)
     rig.close()
     out[rank] = int(ok)
     dist.destroy_process_group()
@@ -235,11 +245,12 @@ def _rig_gpu_worker(rank, world, port, K, out):
 
 @pytest.mark.gpu
 def test_rig_exchange_gpu_gloo():
-    """StereoRigExchange (config 4's multi-GPU layout) with two ranks sharing cuda:0 over gloo: the
-    left rank's batched kNN from the partner's gathered slots is bit-exact against the oracle."""
+    """StereoRigExchange (config 4's multi-GPU layout) with two ranks sharing cuda:0 over gloo: every
+    step's (distinct images, both slabs reused) batched kNN on the left rank, from the partner's
+    gathered slots, read right after that step's match, is bit-exact against the oracle."""
     from oracle import oracle
     oracle.build()
-    world, K = 2, 3
+    world, K, steps = 2, 2, 4
     out = mp.Manager().dict()
-    mp.spawn(_rig_gpu_worker, args=(world, _free_port(), K, out), nprocs=world, join=True)
+    mp.spawn(_rig_gpu_worker, args=(world, _free_port(), K, steps, out), nprocs=world, join=True)
     assert dict(out) == {0: 1, 1: 1}

@@ -1,5 +1,6 @@
 #!/bin/bash
-# GPU: k_pyramid duration (kernel trace of the drop-in latency run) per tile size (ORBFE_PYR_TILE)
+# GPU: k_pyramid duration (kernel trace of the drop-in latency run) per tile size (ORBFE_PYR_TILE; the
+# knob is read only by a variant built with tools/build_variant.sh NAME -DORBFE_AB_KNOBS=1)
 # and block size (variants/liborbfe_pyr{256,1024}.so via ORBFE_LIB; the in-tree library is 512).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
