@@ -89,7 +89,8 @@ int orbfe_pyramid_level(orbfe_extractor* h, int image, int level, uint8_t* dst, 
  * pointers (host array) to width x height u8 images with row pitch `pitch`; each image must have
  * pitch * height readable bytes (the level-1 build reads whole 12-byte windows of the last row, past
  * the width when pitch > width; a view into a larger frame satisfies this). stream: hipStream_t
- * (NULL = the handle's own stream). Outputs stay on the device: see orbfe_batch_outputs. */
+ * (NULL = the legacy default stream, as for every stream argument here). Outputs stay on the device:
+ * see orbfe_batch_outputs. */
 int orbfe_extract_batch(orbfe_extractor* h, int nimg, const uint8_t* const* d_imgs, int width, int height,
                         int pitch, int lap0, int lap1, void* stream);
 /* orbfe_extract_batch with a vLappingArea per image: laps[2*i], laps[2*i+1] (host array) for image i,

@@ -713,8 +713,14 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
     return ORBFE_OK;
 }
 
+// The batched entry points run on the caller's stream; NULL is the legacy default (null) stream, as
+// for every other stream argument of the C-ABI, so a caller's default-stream work (torch's default
+// stream, a collective ordered after it) is ordered with the batch. (Until round 6 NULL selected the
+// handle's own non-blocking stream, which nothing of the caller's waited for: a slab all-gather on
+// the default stream could read the outputs before the kernels wrote them.)
 static hipStream_t pick_stream(orbfe_extractor* h, void* stream) {
-    return stream ? (hipStream_t)stream : h->own_stream;
+    (void)h;
+    return (hipStream_t)stream;
 }
 
 typedef unsigned int orbfe_u32x4 __attribute__((ext_vector_type(4)));

@@ -139,7 +139,10 @@ class StereoRigExchange:
 
     Step k writes slab k % 2; match(k) makes the caller's stream wait for step k's gather and
     enqueues the kNN, so calling match(k - 1) after extract(k) overlaps the gather with the next
-    step's kernels. gloo (CPU rehearsal) exchanges host copies synchronously."""
+    step's kernels. gloo (CPU rehearsal) exchanges host copies synchronously. Every launch goes to
+    the caller's current torch stream (the default stream is handle 0 = the legacy null stream,
+    which the C-ABI takes as such), so the gather that post(k) orders after that stream sees the
+    finished slab (tests/test_distributed.py::test_rig_exchange_gpu_gloo checks every step)."""
 
     def __init__(self, K: int, width: int, height: int, nfeatures: int = 1000, lap=(0, 511), ratio: float = 0.7,
                  device=None, group=None):
