@@ -1151,7 +1151,7 @@ int orbfe_stereo_match(orbfe_extractor* left, orbfe_extractor* right, float bf, 
     const bool tm = left->timing && left->call_ev[0];
     if (tm) HIPCHK(hipEventRecord(left->call_ev[4], s));
     int rc = orbfe_stereo_match_batch(left, 0, 1, right, 0, 1, 1, bf, fx, left->d_uright, left->d_depth,
-                                      left->d_nmatch, nullptr);
+                                      left->d_nmatch, s);
     if (rc) return rc;
     if (tm) HIPCHK(hipEventRecord(left->call_ev[5], s));
     // counts, then {nmatch | the whole uR / depth capacity} in one copy, one round trip through
