@@ -420,6 +420,16 @@ int orbfe_search_local_points_rig_device(const orbfe_frame* F, const orbfe_camer
                                          const int32_t* d_mvp_obs, float th, int32_t bFarPoints, float thFarPoints,
                                          float nnratio, int32_t* n_to_match, void* stream);
 
+/* Tracking::SearchLocalPoints as the drop-in shim calls it (shim/Tracking_orbfe.cc): the fused search
+ * above (rig may be NULL: pinhole from cam, one camera) that also returns each point's isInFrustum
+ * record in track[n] (as orbfe_is_in_frustum_rig writes it), from which the caller applies the
+ * loop's side effects on its MapPoints (mbTrackInView(R), mTrackProj*, mnTrackScaleLevel(R),
+ * mTrackViewCos(R), IncreaseVisible for points in view, Tracking.cc:3407-3425). */
+int orbfe_search_local_points_track(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_stereo_rig* rig,
+                                    const orbfe_map_point_3d* pts, int32_t n, int32_t* mvp, const int32_t* mvp_obs,
+                                    float th, int32_t bFarPoints, float thFarPoints, float nnratio,
+                                    int32_t* n_to_match, orbfe_map_point* track);
+
 /* ---------------------------------------------------------------------------------------------
  * Back-end matcher pieces (LocalMapping / LoopClosing threads)
  * ------------------------------------------------------------------------------------------- */

@@ -111,6 +111,8 @@ _SIGS = {
                                                _c_float, _vp]),
     "orbfe_search_local_points_rig_device": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _vp, _vp, _c_float, _c_int,
                                                       _c_float, _c_float, _vp, _vp]),
+    "orbfe_search_local_points_track": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _vp, _vp, _c_float, _c_int, _c_float,
+                                                 _c_float, _vp, _vp]),
 }
 
 _lib = None

@@ -2204,6 +2204,10 @@ inline int host_seq_acquire(volatile int* st) { return __atomic_load_n((int*)&st
 
 struct MatchScratch {
     int device = -1;
+    // the last fused local-map search's isInFrustum records (device arena) and their count, for
+    // orbfe_search_local_points_track's read-back
+    const orbfe_map_point* last_track = nullptr;
+    int last_track_n = 0;
     hipStream_t stream = nullptr;
     uint8_t* d = nullptr;
     size_t dcap = 0;
@@ -2560,6 +2564,8 @@ int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* m
         HIPCHK(hipMemsetAsync(ntm, 0, 4, s));
         hipLaunchKernelGGL(k_frustum, dim3((nq + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, cd,
                            (const orbfe_map_point_3d*)q, nq, ms_ptr<orbfe_map_point>(o_track), ntm);
+        t_ms.last_track = ms_ptr<const orbfe_map_point>(o_track);
+        t_ms.last_track_n = nq;
         q = ms_ptr<const uint8_t>(o_track);
         qstride = sizeof(orbfe_map_point);
         qid_off = offsetof(orbfe_map_point, id);
@@ -2678,6 +2684,8 @@ int sbp_multi_run(const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, co
         HIPCHK(hipMemsetAsync(ntm, 0, 4, s));
         hipLaunchKernelGGL(k_frustum, dim3((nq + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, cd,
                            (const orbfe_map_point_3d*)q, nq, ms_ptr<orbfe_map_point>(o_track), ntm);
+        t_ms.last_track = ms_ptr<const orbfe_map_point>(o_track);
+        t_ms.last_track_n = nq;
         q = ms_ptr<const uint8_t>(o_track);
         qstride = sizeof(orbfe_map_point);
         qid_off = offsetof(orbfe_map_point, id);
@@ -2892,6 +2900,8 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
         HIPCHK(hipMemsetAsync(ntm, 0, 4, s));
         hipLaunchKernelGGL(k_frustum, dim3((nq + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, cd,
                            (const orbfe_map_point_3d*)q, nq, ms_ptr<orbfe_map_point>(o_track), ntm);
+        t_ms.last_track = ms_ptr<const orbfe_map_point>(o_track);
+        t_ms.last_track_n = nq;
         int h_ntm = 0;
         HIPCHK(hipMemcpyAsync(t_ms.hs, ntm, 4, hipMemcpyDeviceToHost, s));   // pinned
         HIPCHK(hipStreamSynchronize(s));
@@ -3276,9 +3286,22 @@ int orbfe_stereo_knn_batch(orbfe_extractor* left, int lbase, int lstep, orbfe_ex
     return ORBFE_OK;
 }
 
+// A frame without keypoints matches nothing, but Tracking::SearchLocalPoints still runs isInFrustum
+// over every point (Tracking.cc:3407-3425), so nToMatch is the projection's count.
+static int empty_frame_n_to_match(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_stereo_rig* rig,
+                                  const orbfe_map_point_3d* pts, int32_t n, int32_t* n_to_match) {
+    std::vector<orbfe_map_point> track((size_t)n);
+    const int k = orbfe_is_in_frustum_rig(F, cam, rig, pts, n, track.data());
+    if (k < 0) return k;
+    if (n_to_match) *n_to_match = k;
+    return 0;
+}
+
 int orbfe_search_local_points(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* pts,
                               int32_t n, int32_t* mvp, const int32_t* mvp_obs, float th, int32_t bFarPoints,
                               float thFarPoints, float nnratio, int32_t* n_to_match) {
+    if (F && F->n == 0 && n > 0 && pts && cam && !F->two_cams)
+        return empty_frame_n_to_match(F, cam, nullptr, pts, n, n_to_match);
     const FrustumIn fin{cam, pts, n_to_match, nullptr};
     return sbp_run(0, F, mvp, mvp_obs, nullptr, n, sizeof(orbfe_map_point), offsetof(orbfe_map_point, observations),
                    offsetof(orbfe_map_point, id), 0, offsetof(orbfe_map_point, scale_level), th, bFarPoints, 0,
@@ -3309,6 +3332,7 @@ int orbfe_search_local_points_rig(const orbfe_frame* F, const orbfe_camera* cam,
                                   const orbfe_map_point_3d* pts, int32_t n, int32_t* mvp, const int32_t* mvp_obs,
                                   float th, int32_t bFarPoints, float thFarPoints, float nnratio, int32_t* n_to_match) {
     if (!rig) return ORBFE_E_ARG;
+    if (F && F->n == 0 && n > 0 && pts && cam) return empty_frame_n_to_match(F, cam, rig, pts, n, n_to_match);
     const FrustumIn fin{cam, pts, n_to_match, rig};
     return sbp_run(0, F, mvp, mvp_obs, nullptr, n, sizeof(orbfe_map_point), offsetof(orbfe_map_point, observations),
                    offsetof(orbfe_map_point, id), 0, offsetof(orbfe_map_point, scale_level), th, bFarPoints, 0,
@@ -3325,6 +3349,32 @@ int orbfe_search_local_points_rig_device(const orbfe_frame* F, const orbfe_camer
     return sbp_run(0, F, d_mvp, d_mvp_obs, nullptr, n, sizeof(orbfe_map_point), offsetof(orbfe_map_point, observations),
                    offsetof(orbfe_map_point, id), 0, offsetof(orbfe_map_point, scale_level), th, bFarPoints, 0,
                    thFarPoints, nnratio, 0, 0, &fin, &dv);
+}
+
+int orbfe_search_local_points_track(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_stereo_rig* rig,
+                                    const orbfe_map_point_3d* pts, int32_t n, int32_t* mvp, const int32_t* mvp_obs,
+                                    float th, int32_t bFarPoints, float thFarPoints, float nnratio,
+                                    int32_t* n_to_match, orbfe_map_point* track) {
+    if (n < 0 || (n > 0 && !track)) return ORBFE_E_ARG;
+    t_ms.last_track = nullptr;
+    t_ms.last_track_n = 0;
+    const int r = rig ? orbfe_search_local_points_rig(F, cam, rig, pts, n, mvp, mvp_obs, th, bFarPoints, thFarPoints,
+                                                      nnratio, n_to_match)
+                      : orbfe_search_local_points(F, cam, pts, n, mvp, mvp_obs, th, bFarPoints, thFarPoints, nnratio,
+                                                  n_to_match);
+    if (r < 0 || n == 0) return r;
+    if (t_ms.last_track && t_ms.last_track_n == n) {
+        // the search has completed (its status word was seen): the records are final in the arena
+        HIPCHK(hipMemcpyAsync(track, t_ms.last_track, (size_t)n * sizeof(orbfe_map_point), hipMemcpyDeviceToHost,
+                              t_ms.stream));
+        HIPCHK(hipStreamSynchronize(t_ms.stream));
+        t_ms.last_track = nullptr;
+        return r;
+    }
+    // the search returned before projecting (a frame without keypoints): the reference still runs
+    // isInFrustum over every point, so the records come from the projection alone
+    const int k = rig ? orbfe_is_in_frustum_rig(F, cam, rig, pts, n, track) : orbfe_is_in_frustum(F, cam, pts, n, track);
+    return k < 0 ? k : r;
 }
 
 int orbfe_is_in_frustum(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* pts, int32_t n,

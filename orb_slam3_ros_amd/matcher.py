@@ -634,9 +634,11 @@ def is_in_frustum(F: MatchFrame, cam: Camera, points3d, rig: StereoRig = None):
 
 
 def search_local_points(F: MatchFrame, cam: Camera, points3d, mvp, mvp_obs, th: float = 1.0, bFarPoints: bool = False,
-                        thFarPoints: float = 50.0, nnratio: float = 0.8, rig: StereoRig = None):
+                        thFarPoints: float = 50.0, nnratio: float = 0.8, rig: StereoRig = None, track: bool = False):
     """Tracking::SearchLocalPoints' projection + SearchByProjection (Tracking.cc:3404-3453) in one
-    device pass (rig: see is_in_frustum). mvp is updated in place. Returns (nmatches, nToMatch)."""
+    device pass (rig: see is_in_frustum). mvp is updated in place. Returns (nmatches, nToMatch), and
+    with track=True (nmatches, nToMatch, the isInFrustum records as MAP_POINT_DTYPE): the
+    orbfe_search_local_points_track form the C++ shim calls (shim/Tracking_orbfe.cc)."""
     lib = _lib.load()
     pts = _records(points3d, MAP_POINT_3D_DTYPE, "points3d")
     mvp = _i32(mvp, F.N, "mvp")
@@ -644,6 +646,11 @@ def search_local_points(F: MatchFrame, cam: Camera, points3d, mvp, mvp_obs, th: 
     ntm = ctypes.c_int32(0)
     args = (pts.ctypes.data, len(pts), mvp.ctypes.data, mvp_obs.ctypes.data, float(th), int(bFarPoints),
             float(thFarPoints), float(nnratio), ctypes.byref(ntm))
+    if track:
+        rec = np.zeros(len(pts), MAP_POINT_DTYPE)
+        n = lib.orbfe_search_local_points_track(F.ref(), ctypes.byref(cam), ctypes.byref(rig) if rig is not None else None,
+                                                *args, rec.ctypes.data)
+        return _lib.check(n, "search_local_points_track"), int(ntm.value), rec
     if rig is None:
         n = lib.orbfe_search_local_points(F.ref(), ctypes.byref(cam), *args)
     else:

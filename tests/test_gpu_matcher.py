@@ -264,6 +264,36 @@ def test_search_local_points(gpu, om, th, seed):
     np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("npts,th", [(1500, 1), (100_000, 1), (100_000, 15), (0, 1)],
+                         ids=["block", "multi", "band", "empty"])
+def test_search_local_points_track(gpu, om, npts, th):
+    """orbfe_search_local_points_track (the shim's SearchLocalPoints): the same slots and counts as
+    the fused search, plus every point's isInFrustum record bit-exact against the oracle's
+    projection, whichever search kernel ran (one workgroup, multi-block lists, bands); a frame with no
+    keypoints still projects every point (the reference's loop runs regardless)."""
+    from orb_slam3_ros_amd.matcher import search_local_points
+    rng = np.random.default_rng(90 + npts % 7 + th)
+    F = sm.synth_frame(rng, 1000)
+    cam = sm.synth_camera(rng)
+    pts = sm.synth_local_map_3d(rng, F, cam, max(npts, 800))[:npts] if npts else sm.synth_local_map_3d(rng, F, cam, 800)
+    mvp0, obs = sm.initial_slots(rng, F.N)
+    if npts == 0:   # no keypoints in the frame, 800 points
+        F = sm.synth_frame(rng, 0)
+        mvp0, obs = np.zeros(0, np.int32), np.zeros(0, np.int32)
+    a, b = mvp0.copy(), mvp0.copy()
+    ng, tg, rec = search_local_points(F, cam, pts, a, obs, th, track=True)
+    no, to = om.search_local_points(F, cam, pts, b, obs, th)
+    assert (ng, tg) == (no, to)
+    np.testing.assert_array_equal(a, b)
+    n2, ref = om.is_in_frustum(F, cam, pts)
+    assert n2 == tg and len(rec) == len(pts)
+    inv = (ref["flags"] & sm.MP_IN_VIEW) != 0
+    np.testing.assert_array_equal(rec["flags"], ref["flags"])
+    for f in ("proj_x", "proj_y", "proj_xr", "depth", "view_cos"):
+        np.testing.assert_array_equal(rec[f][inv].view(np.uint32), ref[f][inv].view(np.uint32), err_msg=f)
+    np.testing.assert_array_equal(rec["scale_level"][inv], ref["scale_level"][inv])
+
+
 @pytest.mark.parametrize("th", [1, 3, 15])
 def test_sbp_local_device_resident(gpu, om, th):
     """orbfe_search_by_projection_local_device (records, slots and frame in HBM) == the oracle."""
