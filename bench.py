@@ -283,13 +283,13 @@ def cpu_baseline(native, budget_s=4.0):
                                f"{W}x{H} pairs, nFeatures {nf}, vLappingArea {{{lap[0]},{lap[1]}}}); extract L+R + "
                                f"knnMatch(k=2)+ratio of the lapping rows (TriangulateMatches not timed)"}
 
-    def sbp_config5():
+    def sbp_config5(n_kp=1000, name="config5_search_by_projection_100k"):
         # BASELINE config 5 on the CPU restatement: the same synthetic frame / 100k map points / slots as
         # matcher_config5 (seed 12345). The search is ordered over the map points (later points see
         # earlier assignments, ORBmatcher.cc:88-90), so the reference runs it on one thread.
         from orb_slam3_ros_amd import synth_match as sm
         rng = np.random.default_rng(12345)
-        F = sm.synth_frame(rng, 1000)
+        F = sm.synth_frame(rng, n_kp)
         mps = sm.synth_local_map(rng, F, 100_000)
         mvp0, obs = sm.initial_slots(rng, F.N)
         res = {}
@@ -305,17 +305,20 @@ def cpu_baseline(native, budget_s=4.0):
             m = float(np.median(times))
             res[f"th{th}"] = {"ms_per_call": round(m * 1e3, 3), "queries_per_s": round(len(mps) / m, 1),
                               "calls": len(times), "nmatches": int(n)}
-        out["config5_search_by_projection_100k"] = {
+        out[name] = {
             "per_th": res, "threads": 1,
-            "sample": "SearchByProjection(F, 100k local map points, th) of matcher_config5's workload (seed 12345), "
-                      "median over >= 3 calls per th; ordered over the points, one thread as in the reference"}
+            "sample": f"SearchByProjection(F of {n_kp} keypoints, 100k local map points, th) of the matcher_config5 "
+                      "workload (seed 12345), median over >= 3 calls per th; ordered over the points, one thread as "
+                      "in the reference"}
 
     t0 = time.perf_counter()
     stereo_cfg("config2_euroc_stereo_752x480", 752, 480, 1000, EUROC_BF, EUROC_FX, 9000)
+    stereo_cfg("config2_euroc_stereo_752x480_nf1200", 752, 480, 1200, EUROC_BF, EUROC_FX, 9050)
     mono_cfg("config1_euroc_mono_752x480", 752, 480, 1000, 9100)
     stereo_cfg("config3_kitti_stereo_1241x376", 1241, 376, 2000, KITTI_BF, KITTI_FX, 9200)
     fisheye_cfg("config4_tumvi_fisheye_512x512", 512, 512, 1000, (0, 511), 9300)
     sbp_config5()
+    sbp_config5(5000, "config5_search_by_projection_100k_n5000")
     total = time.perf_counter() - t0
     c2 = out["config2_euroc_stereo_752x480"]
     return {"value": c2["throughput_frames_per_s"], "unit": "frames/s", "cores": threads, "kind": "port",
@@ -510,6 +513,49 @@ def matcher_config5(steps):
                       "C-ABI (ctypes, arguments prepared) with the records, slots and frame already in HBM; "
                       "resident_wrapper_ms_per_call: the same through the Python wrapper",
             "per_th": out}
+
+
+def matcher_config5_n(steps, n_kp):
+    """BASELINE config 5 at another frame size (N = 1000 and 5000): the same 100k-point
+    local map construction (seed 12345) against an n_kp-keypoint frame, th in {1, 3, 5, 15}. Per th:
+    the host C-ABI call (records packed + uploaded, slots back) and its device time (HIP events), and
+    a parity check of the slots and count against the CPU oracle (outside the timed loop)."""
+    from oracle import oracle
+    from orb_slam3_ros_amd import synth_match as sm
+    from orb_slam3_ros_amd.matcher import ORBmatcher
+    oracle.build()
+    rng = np.random.default_rng(12345)
+    F = sm.synth_frame(rng, n_kp)
+    mps = sm.synth_local_map(rng, F, 100_000)
+    mvp0, obs = sm.initial_slots(rng, F.N)
+    m = ORBmatcher(0.8)
+    lib = m._lib
+    out, all_ok = {}, True
+    for th in (1, 3, 5, 15):
+        a = mvp0.copy()
+        n = m.SearchByProjectionLocalMap(F, a, obs, mps, th)
+        b = mvp0.copy()
+        no = oracle.OracleMatcher(0.8).sbp_local(F, b, obs, mps, th)
+        ok = n == no and np.array_equal(a, b)
+        all_ok = all_ok and ok
+        bufs = [mvp0.copy() for _ in range(steps)]
+        t0 = time.perf_counter()
+        for bb in bufs:
+            m.SearchByProjectionLocalMap(F, bb, obs, mps, th)
+        dt = (time.perf_counter() - t0) / steps
+        lib.orbfe_matcher_set_timing(1)
+        dev = []
+        for _ in range(steps):
+            m.SearchByProjectionLocalMap(F, mvp0.copy(), obs, mps, th)
+            dev.append(lib.orbfe_matcher_last_ms())
+        lib.orbfe_matcher_set_timing(0)
+        dms = float(np.mean(dev))
+        out[f"th{th}"] = {"ms_per_call": round(dt * 1e3, 4), "device_ms_per_call": round(dms, 4),
+                          "queries_per_s": round(len(mps) / dt, 1), "device_queries_per_s": round(len(mps) / (dms * 1e-3), 1),
+                          "nmatches": int(n), "parity_ok": bool(ok)}
+    return {"workload": f"SearchByProjection local map: 100k map points vs a {n_kp}-keypoint stereo frame "
+                        "(BASELINE config 5's second frame size), nnratio 0.8, seed 12345",
+            "per_th": out, "parity": {"ok": all_ok, "detail": "slots + nmatches identical to the CPU oracle per th"}}
 
 
 def make_images(rank, W, H, F, U, dev, seed0=0):
@@ -1080,12 +1126,23 @@ def main():
             legs["config4_batch"], ok4b = side_leg(dev, "as config4_step at a 512-image batch (throughput)", 512, 512,
                                                    1000, 256, max(3, args.steps // 2), 2, "fisheye", (0, 511), 0.0,
                                                    1.0, 0, 22000)
+            legs["config2_nf1200"], ok2b = side_leg(dev, "EuRoC-like stereo 752x480, nFeatures 1200 (config/Stereo/"
+                                                         "EuRoC.yaml; BASELINE config 2's secondary size): extract L+R "
+                                                         "+ ComputeStereoMatches", 752, 480, 1200, 512,
+                                                    max(3, args.steps // 2), 2, "rectified", (0, 0), EUROC_BF, EUROC_FX,
+                                                    0, 23000)
             result["side_configs"] = legs
-            if not (ok3 and ok4 and ok4b):
+            if not (ok3 and ok4 and ok4b and ok2b):
                 print(json.dumps(result), file=sys.stderr, flush=True)
                 sys.exit(3)
         if args.matcher_steps > 0:
             result["matcher_config5"] = matcher_config5(args.matcher_steps)
+            if world == 1 and not args.no_side_configs:
+                c5b = matcher_config5_n(max(5, args.matcher_steps // 5), 5000)
+                result["matcher_config5_n5000"] = c5b
+                if not c5b["parity"]["ok"]:
+                    print(json.dumps(result), file=sys.stderr, flush=True)
+                    sys.exit(3)
         if args.dropin_frames > 0 and world == 1:
             dl = dropin_leg(args.dropin_frames, nf=args.nfeatures, cpu=not args.no_cpu_baseline)
             result["dropin"] = dl

@@ -29,6 +29,7 @@ TRACK_HDR = os.path.join(os.path.dirname(_HERE), "tests", "native", "tracking_lo
 TRACK_CPU_SRC = os.path.join(os.path.dirname(_HERE), "tests", "native", "tracking_cpu.cpp")
 TRACK_CPU_BIN = os.path.join(os.path.dirname(_HERE), "tests", "native", "tracking_cpu")
 ORACLE_LIB = os.path.join(os.path.dirname(_HERE), "oracle", "liborb_oracle.so")
+GLUE_HDR = os.path.join(os.path.dirname(_HERE), "shim", "orbfe_glue.h")
 
 
 def build_library(force: bool = False, verbose: bool = False) -> str:
@@ -44,8 +45,9 @@ def build_library(force: bool = False, verbose: bool = False) -> str:
 def build_capi_consumer(force: bool = False, verbose: bool = False) -> str:
     """The compiled C++ consumer of include/orbfe.h (tests/native/capi_frontend.cpp), linked against the
     in-tree liborbfe.so by name with an $ORIGIN-relative runpath so it runs from the GPU box's copy."""
-    if force or _stale(CAPI_BIN, [CAPI_SRC, TRACK_HDR, LIB]):
+    if force or _stale(CAPI_BIN, [CAPI_SRC, TRACK_HDR, LIB, GLUE_HDR]):
         cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-I", os.path.join(os.path.dirname(_HERE), "include"),
+               "-I", os.path.join(os.path.dirname(_HERE), "shim"),
                "-o", CAPI_BIN, CAPI_SRC, "-L", _HERE, "-lorbfe", "-Wl,-rpath,$ORIGIN/../../orb_slam3_ros_amd",
                "-Wl,-rpath-link,/opt/rocm/lib"]
         if verbose:

@@ -1711,7 +1711,8 @@ __device__ __forceinline__ FrustumView mt_frustum_view(const CamDev& c, const fl
     return o;
 }
 __global__ __launch_bounds__(MT_NT) void k_frustum(CamDev c, const orbfe_map_point_3d* pts, int n,
-                                                   orbfe_map_point* track, int* n_to_match) {
+                                                   orbfe_map_point* track, int* n_to_match,
+                                                   orbfe_map_point* track_host = nullptr) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const orbfe_map_point_3d p = pts[i];
@@ -1769,6 +1770,13 @@ __global__ __launch_bounds__(MT_NT) void k_frustum(CamDev c, const orbfe_map_poi
         }
     }
     track[i] = t;
+    // the caller's copy of the records (orbfe_search_local_points_track): vector stores into mapped,
+    // coherent host memory, fenced at system scope before the search that follows in the stream
+    // publishes its status word, so the host sees them when it sees that word
+    if (track_host) {
+        track_host[i] = t;
+        __threadfence_system();
+    }
     const unsigned long long m = __ballot(in);
     if ((threadIdx.x & 63) == 0 && m) atomicAdd(n_to_match, __popcll(m));
 }
@@ -2208,6 +2216,9 @@ struct MatchScratch {
     // orbfe_search_local_points_track's read-back
     const orbfe_map_point* last_track = nullptr;
     int last_track_n = 0;
+    orbfe_map_point* th = nullptr;       // mapped pinned track records (orbfe_search_local_points_track)
+    orbfe_map_point* th_dev = nullptr;
+    size_t th_cap = 0;
     hipStream_t stream = nullptr;
     uint8_t* d = nullptr;
     size_t dcap = 0;
@@ -2447,6 +2458,7 @@ struct FrustumIn {
     const orbfe_map_point_3d* pts;
     int32_t* n_to_match;
     const orbfe_stereo_rig* rig;   // camera models / right view (NULL: pinhole from cam, one camera)
+    orbfe_map_point* track_dev = nullptr;   // mapped host copy of the isInFrustum records (device view)
 };
 
 // isInFrustum's per-frame constants (Frame.cc:512-586, 1168-1242): pose, bounds, camera models and,
@@ -2563,7 +2575,7 @@ int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* m
         if (!make_camdev(F, fin->cam, fin->rig, cd)) return ORBFE_E_ARG;
         HIPCHK(hipMemsetAsync(ntm, 0, 4, s));
         hipLaunchKernelGGL(k_frustum, dim3((nq + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, cd,
-                           (const orbfe_map_point_3d*)q, nq, ms_ptr<orbfe_map_point>(o_track), ntm);
+                           (const orbfe_map_point_3d*)q, nq, ms_ptr<orbfe_map_point>(o_track), ntm, fin->track_dev);
         t_ms.last_track = ms_ptr<const orbfe_map_point>(o_track);
         t_ms.last_track_n = nq;
         q = ms_ptr<const uint8_t>(o_track);
@@ -2683,7 +2695,7 @@ int sbp_multi_run(const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, co
         if (!make_camdev(F, fin->cam, fin->rig, cd)) return ORBFE_E_ARG;
         HIPCHK(hipMemsetAsync(ntm, 0, 4, s));
         hipLaunchKernelGGL(k_frustum, dim3((nq + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, cd,
-                           (const orbfe_map_point_3d*)q, nq, ms_ptr<orbfe_map_point>(o_track), ntm);
+                           (const orbfe_map_point_3d*)q, nq, ms_ptr<orbfe_map_point>(o_track), ntm, fin->track_dev);
         t_ms.last_track = ms_ptr<const orbfe_map_point>(o_track);
         t_ms.last_track_n = nq;
         q = ms_ptr<const uint8_t>(o_track);
@@ -2899,7 +2911,7 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
         int* ntm = ms_ptr<int>(o_ntm);
         HIPCHK(hipMemsetAsync(ntm, 0, 4, s));
         hipLaunchKernelGGL(k_frustum, dim3((nq + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, cd,
-                           (const orbfe_map_point_3d*)q, nq, ms_ptr<orbfe_map_point>(o_track), ntm);
+                           (const orbfe_map_point_3d*)q, nq, ms_ptr<orbfe_map_point>(o_track), ntm, fin->track_dev);
         t_ms.last_track = ms_ptr<const orbfe_map_point>(o_track);
         t_ms.last_track_n = nq;
         int h_ntm = 0;
@@ -3356,25 +3368,45 @@ int orbfe_search_local_points_track(const orbfe_frame* F, const orbfe_camera* ca
                                     float th, int32_t bFarPoints, float thFarPoints, float nnratio,
                                     int32_t* n_to_match, orbfe_map_point* track) {
     if (n < 0 || (n > 0 && !track)) return ORBFE_E_ARG;
-    t_ms.last_track = nullptr;
-    t_ms.last_track_n = 0;
-    const int r = rig ? orbfe_search_local_points_rig(F, cam, rig, pts, n, mvp, mvp_obs, th, bFarPoints, thFarPoints,
-                                                      nnratio, n_to_match)
-                      : orbfe_search_local_points(F, cam, pts, n, mvp, mvp_obs, th, bFarPoints, thFarPoints, nnratio,
-                                                  n_to_match);
-    if (r < 0 || n == 0) return r;
-    if (t_ms.last_track && t_ms.last_track_n == n) {
-        // the search has completed (its status word was seen): the records are final in the arena
-        HIPCHK(hipMemcpyAsync(track, t_ms.last_track, (size_t)n * sizeof(orbfe_map_point), hipMemcpyDeviceToHost,
-                              t_ms.stream));
-        HIPCHK(hipStreamSynchronize(t_ms.stream));
-        t_ms.last_track = nullptr;
-        return r;
+    if (n == 0 || !F || F->n == 0 || !pts || !cam) {
+        // no projection inside the search (a frame without keypoints, nothing to project): the
+        // reference still runs isInFrustum over every point, so the records come from it alone
+        int r = rig ? orbfe_search_local_points_rig(F, cam, rig, pts, n, mvp, mvp_obs, th, bFarPoints, thFarPoints,
+                                                    nnratio, n_to_match)
+                    : orbfe_search_local_points(F, cam, pts, n, mvp, mvp_obs, th, bFarPoints, thFarPoints, nnratio,
+                                                n_to_match);
+        if (r < 0 || n == 0) return r;
+        const int k = rig ? orbfe_is_in_frustum_rig(F, cam, rig, pts, n, track) : orbfe_is_in_frustum(F, cam, pts, n, track);
+        return k < 0 ? k : r;
     }
-    // the search returned before projecting (a frame without keypoints): the reference still runs
-    // isInFrustum over every point, so the records come from the projection alone
-    const int k = rig ? orbfe_is_in_frustum_rig(F, cam, rig, pts, n, track) : orbfe_is_in_frustum(F, cam, pts, n, track);
-    return k < 0 ? k : r;
+    // the records come back zero-copy: k_frustum stores them into mapped pinned memory as well, and
+    // the host copies them out once the search's status word has arrived
+    {   // this thread's scratch on the current device first (a first call or a device switch resets it)
+        Plan p0;
+        const int rc0 = ms_prepare(p0);
+        if (rc0) return rc0;
+    }
+    MatchScratch& m = t_ms;
+    if (m.th_cap < (size_t)n) {
+        if (m.th) HIPCHK(hipHostFree(m.th));
+        m.th = nullptr;
+        m.th_cap = 0;
+        const size_t cap = std::max<size_t>((size_t)n, 4096);
+        HIPCHK(hipHostMalloc((void**)&m.th, cap * sizeof(orbfe_map_point), hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostGetDevicePointer((void**)&m.th_dev, m.th, 0));
+        m.th_cap = cap;
+    }
+    if (rig == nullptr && F->two_cams) return ORBFE_E_ARG;   // the pinhole API has no right camera
+    FrustumIn fin{cam, pts, n_to_match, rig};
+    fin.track_dev = m.th_dev;
+    const orbfe_map_point* th_host = m.th;
+    const int r = sbp_run(0, F, mvp, mvp_obs, nullptr, n, sizeof(orbfe_map_point), offsetof(orbfe_map_point, observations),
+                          offsetof(orbfe_map_point, id), 0, offsetof(orbfe_map_point, scale_level), th, bFarPoints, 0,
+                          thFarPoints, nnratio, 0, 0, &fin);
+    if (r < 0) return r;
+    std::atomic_thread_fence(std::memory_order_acquire);
+    memcpy(track, th_host, (size_t)n * sizeof(orbfe_map_point));
+    return r;
 }
 
 int orbfe_is_in_frustum(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* pts, int32_t n,

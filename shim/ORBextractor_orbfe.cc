@@ -1,9 +1,10 @@
 // Drop-in replacement for orb_slam3/src/ORBextractor.cc on top of liborbfe.so (include/orbfe.h).
-// Built inside the ORB-SLAM3 tree (needs OpenCV 4.2 and the ORB-SLAM3 headers, which this
-// repository's container does not have — it is NOT compiled here).
-// ORBextractor.h keeps its public interface; the only header change is one private member
+// Built inside the ORB-SLAM3 tree (OpenCV 4.2 and the ORB-SLAM3 headers); this repository compiles
+// it with -fsyntax-only against stand-in headers (tests/shim_stubs/, tests/test_shim_compile.py).
+// ORBextractor.h keeps its public interface; the header changes are one private member
 //     void* mpOrbfe = nullptr;   // orbfe_extractor*
-// and a non-inline destructor declaration.
+// its public accessor void* OrbfeHandle() const { return mpOrbfe; } (the Frame shim's handle), a
+// non-inline destructor declaration and void MaterialisePyramid().
 #include "ORBextractor.h"
 
 #include <cassert>
@@ -18,7 +19,7 @@ using namespace std;
 
 namespace ORB_SLAM3 {
 
-// Defined by shim/ORBmatcher_orbfe.cc next to the ComputeStereoMatches replacement: the only
+// Defined by shim/Frame_orbfe.cc next to the ComputeStereoMatches replacement: the only
 // reader of mvImagePyramid in the reference (Frame.cc:818-923), which this file no longer fills.
 // Replacing ORBextractor.cc without that rerouting is a link error, not a silent wrong read.
 extern const int kOrbfeStereoRerouted;

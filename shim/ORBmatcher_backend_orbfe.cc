@@ -8,8 +8,8 @@
 // for SearchForTriangulation(bCoarse = false) between a one-camera and a two-camera keyframe (the
 // reference reads R12 / t12 uninitialised there, ORBmatcher.cc:925-940, 1036-1074) and, after one
 // logged line per call site and error code, whenever the library returns an error.
-// Built inside the ORB-SLAM3 tree; NOT compiled in this repository's container (no OpenCV /
-// Eigen / Sophus here). See INTEGRATION.md §4.
+// Built inside the ORB-SLAM3 tree; this repository compiles it with -fsyntax-only against stand-in
+// headers (tests/shim_stubs/, tests/test_shim_compile.py). See INTEGRATION.md §4.
 #include "ORBmatcher.h"
 
 #include <cstdio>

@@ -1,13 +1,14 @@
-// Replacement bodies for the Tracking-thread ORBmatcher methods (orb_slam3/src/ORBmatcher.cc)
-// and Frame::ComputeStereoMatches (Frame.cc:811-981) on top of liborbfe.so. The original bodies
+// Replacement bodies for the Tracking-thread ORBmatcher methods (orb_slam3/src/ORBmatcher.cc) on
+// top of liborbfe.so (Frame::ComputeStereoMatches and the stereo Frame's one-call extraction are in
+// shim/Frame_orbfe.cc, Tracking::SearchLocalPoints in shim/Tracking_orbfe.cc). The original bodies
 // of the replaced methods stay in ORBmatcher.cc / Frame.cc renamed *_cpu: every replacement checks
 // the library's return code and, on an error (no device, a capacity or argument limit), logs the
 // reason once and runs the *_cpu body instead, so a failure never reaches Tracking as a negative
 // nmatches or a silently monocular frame. Both camera layouts are handled on the device: Nleft ==
 // -1 frames and the KannalaBrandt8 two-camera frames (Nleft != -1: keys mvKeys ++ mvKeysRight,
 // mvLeftToRightMatch / mvRightToLeftMatch).
-// Built inside the ORB-SLAM3 tree; NOT compiled in this repository's container (no OpenCV /
-// Eigen / Sophus here). See INTEGRATION.md.
+// Built inside the ORB-SLAM3 tree; this repository compiles it with -fsyntax-only against stand-in
+// headers (tests/shim_stubs/, tests/test_shim_compile.py). See INTEGRATION.md.
 #include "ORBmatcher.h"
 
 #include <cstdio>
@@ -26,11 +27,6 @@
 using namespace std;
 
 namespace ORB_SLAM3 {
-
-// Defined here, referenced by shim/ORBextractor_orbfe.cc: an ORBextractor.cc replaced without this
-// file (and the ComputeStereoMatches body below) fails to link instead of leaving Frame.cc reading
-// the mvImagePyramid the shim no longer fills.
-extern const int kOrbfeStereoRerouted = 1;
 
 namespace {
 
@@ -296,21 +292,5 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPoi
     for (int i = 0; i < F.N; i++) vpMapPointMatches[i] = H.at(out[i]);
     return n;
 }
-
-// Frame.cc:811-981: the body of Frame::ComputeStereoMatches becomes (it lives in Frame.cc, with
-// the original body renamed ComputeStereoMatches_cpu):
-//   void Frame::ComputeStereoMatches() {
-//       mvuRight = vector<float>(N, -1.0f);
-//       mvDepth = vector<float>(N, -1.0f);
-//       const int rc = orbfe_stereo_match(static_cast<orbfe_extractor*>(mpORBextractorLeft->mpOrbfe),
-//                                         static_cast<orbfe_extractor*>(mpORBextractorRight->mpOrbfe),
-//                                         mbf, fx, mvuRight.data(), mvDepth.data());
-//       if (rc < 0) {   // e.g. ORBFE_E_ARG: more than ~2700 keypoints per image (k_stereo LDS)
-//           fprintf(stderr, "[orbfe] orbfe_stereo_match returned %d; running the CPU implementation\n", rc);
-//           mpORBextractorLeft->MaterialisePyramid();
-//           mpORBextractorRight->MaterialisePyramid();
-//           ComputeStereoMatches_cpu();
-//       }
-//   }
 
 }  // namespace ORB_SLAM3

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "orbfe.h"
+#include "orbfe_glue.h"   // shim/: the drop-in shim's own call sequence (Frame(stereo), SearchLocalPoints)
 #include "tracking_loop.h"
 
 namespace {
@@ -35,6 +36,16 @@ struct KeyPoint {   // cv::KeyPoint
     int32_t octave, class_id;
 };
 static_assert(sizeof(KeyPoint) == sizeof(orbfe_keypoint), "cv::KeyPoint layout (28 B)");
+
+// std::vector descriptor sink for orbfe_glue::frame_stereo (the shim's is a cv::Mat)
+struct VecRows {
+    std::vector<uint8_t>& v;
+    uint8_t* rows(int cap) {
+        v.resize((size_t)cap * 32);
+        return v.data();
+    }
+    void keep(int n) { v.resize((size_t)n * 32); }
+};
 
 void check(int rc, const char* what) {
     if (rc < 0 && rc != ORBFE_E_EMPTY) throw std::runtime_error(std::string(what) + " failed: " + std::to_string(rc));
@@ -248,21 +259,12 @@ int latency(int frames, const char* job) {
             int ns = 0;
             const auto t0 = std::chrono::steady_clock::now();
             auto t1 = t0;
-            if (form == 0) {
-                kl.resize(cap);
-                kr.resize(cap);
-                dl.resize((size_t)cap * 32);
-                dr.resize((size_t)cap * 32);
-                ur.resize(cap);
-                dp.resize(cap);
-                int nl = 0, nr = 0, ml = 0, mr = 0;
-                ns = orbfe_frame_stereo(el.handle(), er.handle(), L, R, w, h, w, J.cam.bf, J.cam.fx,
-                                        reinterpret_cast<orbfe_keypoint*>(kl.data()), dl.data(), cap, &nl, &ml,
-                                        reinterpret_cast<orbfe_keypoint*>(kr.data()), dr.data(), cap, &nr, &mr,
-                                        ur.data(), dp.data());
+            if (form == 0) {   // the shim's Frame(stereo) (shim/Frame_orbfe.cc -> orbfe_glue::frame_stereo)
+                int ml = 0, mr = 0;
+                VecRows sl{dl}, sr{dr};
+                ns = orbfe_glue::frame_stereo(el.handle(), er.handle(), L, R, w, h, w, J.cam.bf, J.cam.fx, kl, sl, &ml, kr,
+                                              sr, &mr, ur, dp);
                 check(ns, "frame_stereo");
-                kl.resize(nl);
-                kr.resize(nr);
                 t1 = std::chrono::steady_clock::now();
             } else {
                 const int lap[2] = {0, 0};
@@ -343,24 +345,12 @@ struct GpuApi {
     ORBextractor& er;
     int w, h, cap;
     float bf, fx;
+    // Frame(stereo) as the shim builds it (shim/Frame_orbfe.cc: orbfe_glue::frame_stereo)
     int frame(const uint8_t* L, const uint8_t* R, trk::FrameData& f) {
-        f.keys.resize(cap);
-        f.keys_r.resize(cap);
-        f.desc.resize((size_t)cap * 32);
-        f.desc_r.resize((size_t)cap * 32);
-        f.ur.resize(cap);
-        f.depth.resize(cap);
-        int nl = 0, nr = 0;
-        const int ns = orbfe_frame_stereo(el.handle(), er.handle(), L, R, w, h, w, bf, fx, f.keys.data(), f.desc.data(),
-                                          cap, &nl, &f.mono_l, f.keys_r.data(), f.desc_r.data(), cap, &nr, &f.mono_r,
-                                          f.ur.data(), f.depth.data());
+        VecRows sl{f.desc}, sr{f.desc_r};
+        const int ns = orbfe_glue::frame_stereo(el.handle(), er.handle(), L, R, w, h, w, bf, fx, f.keys, sl, &f.mono_l,
+                                                f.keys_r, sr, &f.mono_r, f.ur, f.depth);
         check(ns, "frame_stereo");
-        f.keys.resize(nl);
-        f.desc.resize((size_t)nl * 32);
-        f.keys_r.resize(nr);
-        f.desc_r.resize((size_t)nr * 32);
-        f.ur.resize(nl);
-        f.depth.resize(nl);
         f.nstereo = ns;
         return ns;
     }
@@ -368,6 +358,7 @@ struct GpuApi {
     // fixed-point passes of every matcher call
     bool diag = false;
     std::vector<double> d_sbp, d_loc, p_sbp, p_loc, w_sbp, w_loc;
+    std::vector<orbfe_map_point> track;   // SearchLocalPoints' isInFrustum records
     void note(std::vector<double>& dv, std::vector<double>& pv) {
         if (!diag) return;
         dv.push_back(orbfe_matcher_last_ms());
@@ -387,7 +378,10 @@ struct GpuApi {
     int local_points(const orbfe_frame* F, const orbfe_camera* c, const orbfe_map_point_3d* pts, int n, int32_t* mvp,
                      const int32_t* obs, float th, int bFar, float thFar, float ratio, int32_t* ntm) {
         const auto t0 = std::chrono::steady_clock::now();
-        const int r = orbfe_search_local_points(F, c, pts, n, mvp, obs, th, bFar, thFar, ratio, ntm);
+        // SearchLocalPoints as the shim calls it (shim/Tracking_orbfe.cc: orbfe_glue::local_points, the
+        // isInFrustum records returned for the MapPoint side effects); nnratio is the reference's 0.8
+        (void)ratio;
+        const int r = orbfe_glue::local_points(F, c, nullptr, pts, n, mvp, obs, th, bFar != 0, thFar, track, ntm);
         if (diag) w_loc.push_back(trk::ms_since(t0));
         check(r, "search_local_points");
         note(d_loc, p_loc);
@@ -410,8 +404,8 @@ int tracking(int frames, const char* job, const char* out_path, bool diag) {
     }
     const int rc = trk::run_sequence(api, J.cam, J.w, J.h, el.mvScaleFactor, J.window, frames, J.npairs,
                                      [&](int k) { return J.left(k); }, [&](int k) { return J.right(k); }, out_path,
-                                     "gpu: liborbfe.so C-ABI (orbfe_frame_stereo, orbfe_search_by_projection_lastframe, "
-                                     "orbfe_search_local_points)");
+                                     "gpu: liborbfe.so C-ABI through the shim glue (shim/orbfe_glue.h: orbfe_frame_stereo, "
+                                     "orbfe_search_local_points_track) + orbfe_search_by_projection_lastframe");
     if (diag)
         printf("{\"diag\": {\"sbp_last_wall_ms\": %.4f, \"sbp_last_device_ms\": %.4f, \"sbp_last_passes\": %.1f, "
                "\"local_wall_ms\": %.4f, \"local_device_ms\": %.4f, \"local_passes\": %.1f}}\n",
