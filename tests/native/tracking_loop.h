@@ -130,20 +130,26 @@ public:
             }
         }
         st.sbp_ms = ms_since(t1);
-        // SearchLocalPoints: the local map = the points held by any of the last `window` frames (the
-        // reference takes the points of the covisible keyframes, Tracking.cc:UpdateLocalPoints)
+        // UpdateLocalPoints (untimed, Tracking.cc:3496-3527, a separate step of TrackLocalMap): the
+        // local map = the points held by any of the last `window` frames (the reference takes the
+        // points of the covisible keyframes)
+        std::vector<int32_t> local_ids;
+        for (size_t j = 0; j < points_.size(); j++)
+            if (points_[j].last_seen >= k_ - window_) local_ids.push_back((int32_t)j);
+        // SearchLocalPoints (Tracking.cc:3382-3452): the frame's matched points skipped, the local
+        // points snapshotted (isInFrustum's inputs), the projection + search
+        std::vector<uint8_t> held(points_.size(), 0);
         const auto t2 = std::chrono::steady_clock::now();
         {
-            std::vector<uint8_t> held(points_.size(), 0);
             for (int i = 0; i < N; i++)
                 if (cur.mvp[i] >= 0) {
                     held[cur.mvp[i]] = 1;   // mnLastFrameSeen = current frame: not projected
                     obs[i] = points_[cur.mvp[i]].obs;
                 }
             std::vector<orbfe_map_point_3d> lm;
-            for (size_t j = 0; j < points_.size(); j++) {
+            lm.reserve(local_ids.size());
+            for (const int32_t j : local_ids) {
                 const MapPoint& p = points_[j];
-                if (p.last_seen < k_ - window_) continue;
                 orbfe_map_point_3d r;
                 memset(&r, 0, sizeof(r));
                 memcpy(r.pos, p.pos, 12);
