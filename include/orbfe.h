@@ -194,7 +194,22 @@ typedef struct orbfe_frame {
     int32_t nleft;                   /* Nleft, 0 <= nleft <= n */
     const int32_t* l2r;              /* mvLeftToRightMatch [nleft] (right index or -1) */
     const int32_t* r2l;              /* mvRightToLeftMatch [n - nleft] (left index or -1) */
+    int32_t device;                  /* 1: keys / desc / uright / scale_factors are device pointers
+                                        (orbfe_frame_device_view); 0: host memory */
 } orbfe_frame;
+
+/* The current frame kept on the device for Tracking's searches. orbfe_extractor_frame_id(h) counts
+ * h's extractions; read it right after orbfe_frame_stereo (the shim keeps it in the Frame).
+ * orbfe_frame_device_view(left, id, F) then fills F with the DEVICE view of that call's left image
+ * (mvKeysUn / mDescriptors / mvuRight of the pinhole stereo Frame, Frame.cc:101-141): n, keys, desc,
+ * uright, nlevels, scale_factors, device = 1 (the caller sets the bounds and mbf as for a host view).
+ * ORBFE_E_ARG when h has extracted since (the view would show another frame). The host-API
+ * single-camera searches (orbfe_search_by_projection_local / _lastframe / _kf,
+ * orbfe_search_local_points(_track)) take such a view for frames of <= 2048 keypoints and <= 2048
+ * queries and read the frame from HBM instead of the caller's copy (no per-call upload of ~64 KB);
+ * other shapes return ORBFE_E_ARG (pass the host view). Valid until h's next extraction. */
+uint64_t orbfe_extractor_frame_id(orbfe_extractor* h);
+int orbfe_frame_device_view(orbfe_extractor* left, uint64_t frame_id, orbfe_frame* F);
 
 /* MapPoint tracking snapshot for SearchByProjection(Frame&, vector<MapPoint*>, ...)
  * (MapPoint.h:172-180; filled by Frame::isInFrustum, Tracking.cc:3407-3425). 80 bytes. */

@@ -113,6 +113,8 @@ _SIGS = {
                                                       _c_float, _c_float, _vp, _vp]),
     "orbfe_search_local_points_track": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _vp, _vp, _c_float, _c_int, _c_float,
                                                  _c_float, _vp, _vp]),
+    "orbfe_extractor_frame_id": (ctypes.c_uint64, [_vp]),
+    "orbfe_frame_device_view": (_c_int, [_vp, ctypes.c_uint64, _vp]),
 }
 
 _lib = None

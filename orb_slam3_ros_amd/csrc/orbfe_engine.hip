@@ -146,6 +146,11 @@ struct orbfe_extractor {
     std::mutex mu_stereo;
     // last batch description
     int last_nimg = 0, last_pitch = 0;
+    // extraction counter (every run_batch) and the matcher view of the last orbfe_frame_stereo call:
+    // its id, left keypoint count, and the scale factors on the device (orbfe_frame_device_view)
+    uint64_t frame_id = 0, fs_id = 0;
+    int fs_n = 0;
+    float* d_scale = nullptr;
     std::vector<const uint8_t*> last_ptrs;
     std::vector<int> last_laps;   // vLappingArea {lap0, lap1} per image of the last batch
     // stage timing
@@ -575,6 +580,7 @@ static int run_batch(orbfe_extractor* h, int B, const uint8_t* const* host_ptrs,
         HIPCHK(hipStreamSynchronize(s));
     }
     h->last_nimg = B;
+    h->frame_id++;
     h->last_pitch = pitch;
     const uint8_t* const* P = h->d_ptrs;
     const bool tm = h->timing;
@@ -843,6 +849,7 @@ void orbfe_extractor_destroy(orbfe_extractor* h) {
     if (h->d_stage) (void)hipFree(h->d_stage);
     if (h->h_pin) (void)hipHostFree(h->h_pin);
     if (h->d_st) (void)hipFree(h->d_st);
+    if (h->d_scale) (void)hipFree(h->d_scale);
     if (h->d_sdist) (void)hipFree(h->d_sdist);
     for (int i = 0; i <= ORBFE_NUM_STAGES; i++)
         if (h->ev[i]) (void)hipEventDestroy(h->ev[i]);
@@ -1314,6 +1321,8 @@ int orbfe_frame_stereo(orbfe_extractor* left, orbfe_extractor* right, const uint
     *mono_left = cnt[1];
     *mono_right = cnt[3];
     if (cnt[0] > cap_left || cnt[2] > cap_right) return ORBFE_E_CAPACITY;
+    h->fs_id = h->frame_id;   // the left image's records stay in the handle's output block
+    h->fs_n = cnt[0];
     const OrbKeyPoint* hk = (const OrbKeyPoint*)(hp + o_kps);
     const uint8_t* hd = hp + o_desc;
     memcpy(kps_left, hk, (size_t)cnt[0] * sizeof(OrbKeyPoint));
@@ -1333,6 +1342,31 @@ int orbfe_frame_stereo(orbfe_extractor* left, orbfe_extractor* right, const uint
         h->call_ms[4] = 0.f;
     }
     return nm;
+}
+
+uint64_t orbfe_extractor_frame_id(orbfe_extractor* h) { return h ? h->frame_id : 0; }
+
+int orbfe_frame_device_view(orbfe_extractor* left, uint64_t frame_id, orbfe_frame* F) {
+    if (!left || !F) return ORBFE_E_ARG;
+    std::lock_guard<std::mutex> lk(left->mu);
+    if (frame_id == 0 || left->fs_id != frame_id || left->frame_id != frame_id || !left->last_kps || !left->d_st)
+        return ORBFE_E_ARG;   // no frame call, or the handle has extracted since
+    if (!left->d_scale) {
+        HIPCHK(hipSetDevice(left->device));
+        HIPCHK(hipMalloc(&left->d_scale, ORBFE_MAX_LEVELS * sizeof(float)));
+        HIPCHK(hipMemcpy(left->d_scale, left->scale.data(), left->nlevels * sizeof(float), hipMemcpyHostToDevice));
+    }
+    F->n = left->fs_n;
+    F->keys = (const orbfe_keypoint*)left->last_kps;   // image 0 of the last batch = the left image
+    F->desc = left->last_desc;
+    F->uright = left->d_uright;
+    F->nlevels = left->nlevels;
+    F->scale_factors = left->d_scale;
+    F->two_cams = 0;
+    F->nleft = 0;
+    F->l2r = F->r2l = nullptr;
+    F->device = 1;
+    return ORBFE_OK;
 }
 
 int orbfe_debug_copy(orbfe_extractor* h, int what, int image, int level, void* dst, int cap_bytes) {

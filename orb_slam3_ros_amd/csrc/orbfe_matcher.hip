@@ -2425,8 +2425,9 @@ struct FramePlan {
     }
 };
 
+// device views (orbfe_frame_device_view) are taken by sbp_run's one-workgroup path only
 bool frame_ok(const orbfe_frame* f) {
-    return f && f->n >= 0 && f->n <= MT_GRID_MAXN && (f->n == 0 || (f->keys && f->desc)) && f->scale_factors &&
+    return f && !f->device && f->n >= 0 && f->n <= MT_GRID_MAXN && (f->n == 0 || (f->keys && f->desc)) && f->scale_factors &&
            f->nlevels > 0 &&
            (!f->two_cams || (f->nleft >= 0 && f->nleft <= f->n && (f->nleft == 0 || f->l2r) &&
                              (f->nleft == f->n || f->r2l)));
@@ -2535,7 +2536,7 @@ int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* m
     const int n = F->n;
     Plan p;
     FramePlan fp;
-    if (dev) fp.plan_dev(F, mode != 2);
+    if (dev || F->device) fp.plan_dev(F, mode != 2);   // a device frame: read in place
     else fp.plan(p, F, true, mode != 2);
     const size_t o_q = dev ? 0 : fin ? p.upload(fin->pts, (size_t)nq * sizeof(orbfe_map_point_3d))
                                      : p.upload(queries, (size_t)nq * qstride);
@@ -2799,7 +2800,17 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
             size_t qstride, size_t qobs_off, size_t qid_off, size_t qangle_off, size_t qlevel_off, float th, int a0, int a1, float thFar,
             float nnratio, int maxDist, int checkOri, const FrustumIn* fin = nullptr, const DevIn* dev = nullptr,
             const float* right_uv = nullptr) {
-    if (!frame_ok(F) || !mvp || nq < 0 || (nq > 0 && !queries && !fin)) return ORBFE_E_ARG;
+    // a device view of the current frame (orbfe_frame_device_view): the frame's arrays are read in HBM
+    // by k_sbp_block; any other path would read them on the host, so other shapes are refused
+    const bool fdev = F && F->device != 0;
+    orbfe_frame Fchk;
+    if (fdev) {
+        Fchk = *F;
+        Fchk.device = 0;
+        BlkGeom g0;
+        if (F->two_cams || F->n > MT_BAND_MAXN || nq > MT_BLOCK_MAXQ || !blk_geom(F, g0)) return ORBFE_E_ARG;
+    }
+    if (!frame_ok(fdev ? &Fchk : F) || !mvp || nq < 0 || (nq > 0 && !queries && !fin)) return ORBFE_E_ARG;
     if (fin && (!fin->cam || (nq > 0 && !fin->pts) || mode != 0)) return ORBFE_E_ARG;
     if (mode != 2 && !mvp_obs) return ORBFE_E_ARG;
     const bool two = F->two_cams != 0;

@@ -41,7 +41,8 @@ class CFrame(ctypes.Structure):
                 ("uright", ctypes.c_void_p), ("min_x", ctypes.c_float), ("max_x", ctypes.c_float),
                 ("min_y", ctypes.c_float), ("max_y", ctypes.c_float), ("nlevels", ctypes.c_int32),
                 ("scale_factors", ctypes.c_void_p), ("mbf", ctypes.c_float), ("two_cams", ctypes.c_int32),
-                ("nleft", ctypes.c_int32), ("l2r", ctypes.c_void_p), ("r2l", ctypes.c_void_p)]
+                ("nleft", ctypes.c_int32), ("l2r", ctypes.c_void_p), ("r2l", ctypes.c_void_p),
+                ("device", ctypes.c_int32)]
 
 
 class CFeatureVector(ctypes.Structure):
@@ -669,3 +670,22 @@ def stereo_knn_ratio(left_desc, right_desc, ratio: float = 0.7):
     g = _lib.check(lib.orbfe_stereo_knn_ratio(L.ctypes.data, len(L), R.ctypes.data, len(R), float(ratio),
                                               t.ctypes.data, d.ctypes.data), "stereo_knn_ratio")
     return g, t, d
+
+
+def current_frame_view(F: MatchFrame, left, frame_id: int):
+    """The device view (orbfe_frame_device_view) of the frame the last orbfe_frame_stereo on extractor
+    `left` produced, with F's bounds and mbf: a CFrame whose keys / desc / uR / scale factors are in
+    HBM, for the host-API single-camera searches (SearchByProjectionLocalMap / LastFrame /
+    search_local_points take it through MatchFrame-compatible `.ref()`). None when stale."""
+    c = CFrame()
+    ctypes.memmove(ctypes.byref(c), F.ref(), ctypes.sizeof(CFrame))
+    if _lib.load().orbfe_frame_device_view(left.handle, int(frame_id), ctypes.byref(c)) != 0:
+        return None
+
+    class _View:   # what the search wrappers read of a MatchFrame
+        pass
+    v = _View()
+    v.c, v.N, v.nleft, v.scale_factors, v.bounds, v.keys = c, int(c.n), None, F.scale_factors, F.bounds, F.keys
+    v.ref = lambda: ctypes.byref(c)
+    return v
+

@@ -63,7 +63,7 @@ orbfe_extractor* handle_of(ORBextractor* e) { return static_cast<orbfe_extractor
 
 }  // namespace
 
-// Frame.cc:122-141 in one call (the member INTEGRATION.md §2 adds to Frame.h). Fills mvKeys,
+// Frame.cc:122-141 in one call (the members INTEGRATION.md §2 adds to Frame.h). Fills mvKeys,
 // mvKeysRight, mDescriptors, mDescriptorsRight, mvuRight and mvDepth exactly as the two ExtractORB
 // threads and ComputeStereoMatches do, with mb = mbf / fx taken from mK (the reference's body reads
 // the member mb before the constructor assigns it, Frame.cc:141 vs :174). Returns false
@@ -84,6 +84,9 @@ bool Frame::ExtractStereoOrbfe(const cv::Mat& imLeft, const cv::Mat& imRight) {
     }
     mDescriptors = dl.m;
     mDescriptorsRight = dr.m;
+    // Tracking's searches on this frame read it in HBM while the left handle still holds it
+    // (orbfe_frame_device_view); rectified stereo only: mvKeysUn == mvKeys (no distortion)
+    mnOrbfeFrameId = mDistCoef.at<float>(0) == 0.f ? orbfe_extractor_frame_id(handle_of(mpORBextractorLeft)) : 0;
     mpORBextractorLeft->mvImagePyramid.clear();
     mpORBextractorRight->mvImagePyramid.clear();
     return true;

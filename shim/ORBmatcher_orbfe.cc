@@ -20,8 +20,11 @@
 
 #include <orbfe.h>
 
+#include "orbfe_glue.h"
+
 #include "Frame.h"
 #include "KeyFrame.h"
+#include "ORBextractor.h"
 #include "MapPoint.h"
 
 using namespace std;
@@ -104,6 +107,11 @@ void slots_of(const Frame& F, Handles& H, vector<int32_t>& mvp, vector<int32_t>*
 void copy_desc(const cv::Mat& d, uint8_t out[32]) { memcpy(out, d.ptr<uint8_t>(0), 32); }
 
 // keypoint i of a frame / keyframe in the reference's side-aware lookup
+// the left extractor's handle (the device view of the frame it produced last)
+orbfe_extractor* handle_of(const Frame& F) {
+    return F.mpORBextractorLeft ? static_cast<orbfe_extractor*>(F.mpORBextractorLeft->OrbfeHandle()) : nullptr;
+}
+
 const cv::KeyPoint& key_of(const Frame& F, int i) {
     return F.Nleft == -1 ? F.mvKeysUn[i] : i < F.Nleft ? F.mvKeys[i] : F.mvKeysRight[i - F.Nleft];
 }
@@ -137,8 +145,12 @@ int ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoint
     }
     vector<cv::KeyPoint> keys;
     const orbfe_frame fr = frame_view(F, keys);
-    const int n = orbfe_search_by_projection_local(&fr, mvp.data(), obs.data(), q.data(), (int)q.size(),
-                                                   th, bFarPoints, thFarPoints, mfNNratio);
+    // the current frame in HBM when its extractor still holds it (single camera)
+    const int n = orbfe_glue::on_current_frame(handle_of(F), F.Nleft == -1 ? F.mnOrbfeFrameId : 0, fr,
+                                               [&](const orbfe_frame* V) {
+        return orbfe_search_by_projection_local(V, mvp.data(), obs.data(), q.data(), (int)q.size(), th, bFarPoints,
+                                                thFarPoints, mfNNratio);
+    });
     if (failed(n, "orbfe_search_by_projection_local"))
         return SearchByProjection_cpu(F, vpMapPoints, th, bFarPoints, thFarPoints);
     for (int i = 0; i < F.N; i++) F.mvpMapPoints[i] = H.at(mvp[i]);
@@ -184,9 +196,12 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, 
     }
     vector<cv::KeyPoint> keys;
     const orbfe_frame fr = frame_view(CurrentFrame, keys);
-    const int n = orbfe_search_by_projection_lastframe_stereo(&fr, mvp.data(), obs.data(), q.data(),
-                                                              two ? ruv.data() : nullptr, (int)q.size(), th,
-                                                              bForward, bBackward, mbCheckOrientation);
+    const int n = orbfe_glue::on_current_frame(handle_of(CurrentFrame), two ? 0 : CurrentFrame.mnOrbfeFrameId, fr,
+                                               [&](const orbfe_frame* V) {
+        return orbfe_search_by_projection_lastframe_stereo(V, mvp.data(), obs.data(), q.data(),
+                                                           two ? ruv.data() : nullptr, (int)q.size(), th, bForward,
+                                                           bBackward, mbCheckOrientation);
+    });
     if (failed(n, "orbfe_search_by_projection_lastframe_stereo"))
         return SearchByProjection_cpu(CurrentFrame, LastFrame, th, bMono);
     for (int i = 0; i < CurrentFrame.N; i++) CurrentFrame.mvpMapPoints[i] = H.at(mvp[i]);

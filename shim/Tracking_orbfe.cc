@@ -22,6 +22,7 @@
 #include "Frame.h"
 #include "LocalMapping.h"
 #include "MapPoint.h"
+#include "ORBextractor.h"
 #include "ORBmatcher.h"
 #include "orbfe_glue.h"
 
@@ -173,9 +174,13 @@ void Tracking::SearchLocalPoints() {
     }
     vector<orbfe_map_point> track;
     int32_t nToMatch = 0;
-    const int n = orbfe_glue::local_points(&fr, &cam, &rig, recs.data(), (int32_t)recs.size(), mvp.data(), obs.data(),
-                                           (float)th, mpLocalMapper->mbFarPoints, mpLocalMapper->mThFarPoints, track,
-                                           &nToMatch);
+    // the current frame in HBM while its extractor still holds it (single camera, Frame_orbfe.cc)
+    orbfe_extractor* hl = F.mpORBextractorLeft ? static_cast<orbfe_extractor*>(F.mpORBextractorLeft->OrbfeHandle()) : nullptr;
+    const int n = orbfe_glue::on_current_frame(hl, F.Nleft == -1 ? F.mnOrbfeFrameId : 0, fr, [&](const orbfe_frame* V) {
+        return orbfe_glue::local_points(V, &cam, &rig, recs.data(), (int32_t)recs.size(), mvp.data(), obs.data(),
+                                        (float)th, mpLocalMapper->mbFarPoints, mpLocalMapper->mThFarPoints, track,
+                                        &nToMatch);
+    });
     if (n < 0) {
         // the frustum loop and the matcher call of the reference (:3404-3452); the first loop's
         // side effects above have already happened

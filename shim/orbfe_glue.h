@@ -85,4 +85,21 @@ inline int local_points(const orbfe_frame* F, const orbfe_camera* cam, const orb
                                            n_to_match, track.data());
 }
 
+// Tracking's searches on the CURRENT frame read it in HBM when the extractor still holds it: call(F)
+// runs with the device view of the frame the last orbfe_frame_stereo on `left` produced
+// (orbfe_frame_device_view; `frame_id` = orbfe_extractor_frame_id(left) right after that call, 0 =
+// none), the bounds and mbf taken from `host`; a view the library cannot take for this call (a
+// stale id, a search shape outside the one-workgroup path) falls back to call(&host), the host view.
+template <class Call>
+int on_current_frame(orbfe_extractor* left, uint64_t frame_id, const orbfe_frame& host, Call&& call) {
+    if (left && frame_id) {
+        orbfe_frame dv = host;
+        if (orbfe_frame_device_view(left, frame_id, &dv) == ORBFE_OK) {
+            const int r = call(&dv);
+            if (r != ORBFE_E_ARG) return r;
+        }
+    }
+    return call(&host);
+}
+
 }  // namespace orbfe_glue

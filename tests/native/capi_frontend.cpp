@@ -352,8 +352,11 @@ struct GpuApi {
                                                 f.keys_r, sr, &f.mono_r, f.ur, f.depth);
         check(ns, "frame_stereo");
         f.nstereo = ns;
+        frame_id = host_view ? 0 : orbfe_extractor_frame_id(el.handle());   // the shim keeps it in the Frame
         return ns;
     }
+    uint64_t frame_id = 0;   // the current frame's id: its searches read it in HBM (orbfe_frame_device_view)
+    bool host_view = false;  // --tracking-hostview: the searches read the caller's copy (A/B)
     // diagnostic run (--tracking-diag): device time (HIP events around the call's kernels) and the
     // fixed-point passes of every matcher call
     bool diag = false;
@@ -369,7 +372,9 @@ struct GpuApi {
     int sbp_last(const orbfe_frame* F, int32_t* mvp, const int32_t* obs, const orbfe_proj_point* pts, int n, float th,
                  int fwd, int bwd, int ori) {
         const auto t0 = std::chrono::steady_clock::now();
-        const int r = orbfe_search_by_projection_lastframe(F, mvp, obs, pts, n, th, fwd, bwd, ori);
+        const int r = orbfe_glue::on_current_frame(el.handle(), frame_id, *F, [&](const orbfe_frame* V) {
+            return orbfe_search_by_projection_lastframe(V, mvp, obs, pts, n, th, fwd, bwd, ori);
+        });
         if (diag) w_sbp.push_back(trk::ms_since(t0));
         check(r, "search_by_projection_lastframe");
         note(d_sbp, p_sbp);
@@ -381,7 +386,9 @@ struct GpuApi {
         // SearchLocalPoints as the shim calls it (shim/Tracking_orbfe.cc: orbfe_glue::local_points, the
         // isInFrustum records returned for the MapPoint side effects); nnratio is the reference's 0.8
         (void)ratio;
-        const int r = orbfe_glue::local_points(F, c, nullptr, pts, n, mvp, obs, th, bFar != 0, thFar, track, ntm);
+        const int r = orbfe_glue::on_current_frame(el.handle(), frame_id, *F, [&](const orbfe_frame* V) {
+            return orbfe_glue::local_points(V, c, nullptr, pts, n, mvp, obs, th, bFar != 0, thFar, track, ntm);
+        });
         if (diag) w_loc.push_back(trk::ms_since(t0));
         check(r, "search_local_points");
         note(d_loc, p_loc);
@@ -391,13 +398,14 @@ struct GpuApi {
 
 }  // namespace
 
-int tracking(int frames, const char* job, const char* out_path, bool diag) {
+int tracking(int frames, const char* job, const char* out_path, bool diag, bool host_view = false) {
     const SeqJob J = read_seq(job);
     ORBextractor el(J.nf, 1.2f, 8, 20, 7), er(J.nf, 1.2f, 8, 20, 7);
     const int cap = orbfe_extractor_capacity(el.handle(), J.w, J.h);
     check(cap, "capacity");
     GpuApi api{el, er, J.w, J.h, cap, J.cam.bf, J.cam.fx};
     api.diag = diag;
+    api.host_view = host_view;
     if (diag) {
         orbfe_matcher_set_timing(1);
         orbfe_matcher_set_stats(1);
@@ -416,9 +424,11 @@ int tracking(int frames, const char* job, const char* out_path, bool diag) {
 
 
 int main(int argc, char** argv) {
-    if ((argc == 4 || argc == 5) && (std::string(argv[1]) == "--tracking" || std::string(argv[1]) == "--tracking-diag")) {
+    if ((argc == 4 || argc == 5) && (std::string(argv[1]) == "--tracking" || std::string(argv[1]) == "--tracking-diag" ||
+                                     std::string(argv[1]) == "--tracking-hostview")) {
         try {
-            return tracking(atoi(argv[2]), argv[3], argc == 5 ? argv[4] : nullptr, std::string(argv[1]) == "--tracking-diag");
+            return tracking(atoi(argv[2]), argv[3], argc == 5 ? argv[4] : nullptr, std::string(argv[1]) == "--tracking-diag",
+                            std::string(argv[1]) == "--tracking-hostview");
         } catch (const std::exception& e) {
             fprintf(stderr, "capi_frontend: %s\n", e.what());
             return 1;

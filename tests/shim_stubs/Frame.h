@@ -19,6 +19,8 @@ public:
     Sophus::SE3<float> GetPose() const;
     ORBextractor *mpORBextractorLeft, *mpORBextractorRight;
     cv::Mat mK;
+    cv::Mat mDistCoef;
+    uint64_t mnOrbfeFrameId = 0;   // orbfe_extractor_frame_id after ExtractStereoOrbfe
     float mbf, mb;
     int N;
     std::vector<cv::KeyPoint> mvKeys, mvKeysRight, mvKeysUn;

@@ -47,6 +47,8 @@ public:
     void release();
     template <class T> T* ptr(int row = 0);
     template <class T> const T* ptr(int row = 0) const;
+    template <class T> T& at(int i0);
+    template <class T> const T& at(int i0) const;
     template <class T> T& at(int r, int c);
     template <class T> const T& at(int r, int c) const;
 };

@@ -271,3 +271,45 @@ def test_frame_stereo_rejects_mismatched_handles(gpu):
     el, er = ORBextractor(1000, 1.2, 8, 20, 7), ORBextractor(1200, 1.2, 8, 20, 7)
     with pytest.raises(_lib.OrbfeError):
         frame_stereo(el, er, left, right, 50.0, 458.0)
+
+
+def test_frame_device_view_searches(gpu):
+    """Tracking's searches on the current frame read it in HBM (orbfe_frame_device_view of the last
+    orbfe_frame_stereo): SearchByProjection(F, local map) and SearchByProjection(CurrentFrame,
+    LastFrame) give the same slots and counts through the device view as through the host copy; a
+    stale id (the handle extracted since) and a shape outside the one-workgroup path are refused."""
+    from orb_slam3_ros_amd import _lib
+    from orb_slam3_ros_amd import synth_match as sm
+    from orb_slam3_ros_amd.extractor import ORBextractor, frame_stereo
+    from orb_slam3_ros_amd.matcher import MatchFrame, ORBmatcher, current_frame_view
+    from orb_slam3_ros_amd.synth import synth_stereo
+    bf, fx = 0.110078 * 458.654, 458.654
+    el, er = ORBextractor(1000, 1.2, 8, 20, 7), ORBextractor(1000, 1.2, 8, 20, 7)
+    left, right = synth_stereo(5, 752, 480)
+    (ml, kl, dl), _, ur, _, _ = frame_stereo(el, er, left, right, bf, fx)
+    lib = _lib.load()
+    fid = lib.orbfe_extractor_frame_id(el.handle)
+    F = MatchFrame(kl, dl, (0.0, 752.0, 0.0, 480.0), np.asarray(el.GetScaleFactors(), np.float32), ur, bf)
+    V = current_frame_view(F, el, fid)
+    assert V is not None and V.N == F.N
+    rng = np.random.default_rng(3)
+    mps = sm.synth_local_map(rng, F, 1500)
+    mvp0, obs = sm.initial_slots(rng, F.N)
+    m = ORBmatcher(0.8)
+    for th in (1.0, 3.0):
+        a, b = mvp0.copy(), mvp0.copy()
+        assert m.SearchByProjectionLocalMap(V, a, obs, mps, th) == m.SearchByProjectionLocalMap(F, b, obs, mps, th)
+        np.testing.assert_array_equal(a, b)
+    pts = sm.synth_proj_points(rng, F, 900)
+    for fwd, bwd in ((0, 0), (1, 0)):
+        a, b = mvp0.copy(), mvp0.copy()
+        ga = m.SearchByProjectionLastFrame(V, a, obs, pts, 7.0, fwd, bwd)
+        gb = m.SearchByProjectionLastFrame(F, b, obs, pts, 7.0, fwd, bwd)
+        assert ga == gb
+        np.testing.assert_array_equal(a, b)
+    big = sm.synth_local_map(rng, F, 5000)   # > 2048 queries: not the one-workgroup path
+    with pytest.raises(_lib.OrbfeError):
+        m.SearchByProjectionLocalMap(V, mvp0.copy(), obs, big, 1.0)
+    el(left, None, (0, 0))   # the handle extracts again: the view is stale
+    assert current_frame_view(F, el, fid) is None
+

@@ -213,10 +213,30 @@ def test_record_layouts():
     import ctypes
     from orb_slam3_ros_amd.matcher import CFeatureVector, CFrame
     assert sm.MAP_POINT_DTYPE.itemsize == 80 and sm.PROJ_POINT_DTYPE.itemsize == 64
-    assert ctypes.sizeof(CFrame) == 96 and CFrame.mbf.offset == 64
+    assert ctypes.sizeof(CFrame) == 104 and CFrame.mbf.offset == 64
     assert CFrame.two_cams.offset == 68 and CFrame.nleft.offset == 72 and CFrame.l2r.offset == 80
+    assert CFrame.device.offset == 96
     assert sm.MAP_POINT_DTYPE.fields["proj_yr"][1] == 36 and sm.MAP_POINT_DTYPE.fields["scale_level_r"][1] == 44
     assert ctypes.sizeof(CFeatureVector) == 32
+
+
+def test_frame_layout_matches_header(tmp_path):
+    """struct orbfe_frame as the C compiler lays it out (include/orbfe.h) == the ctypes mirror."""
+    import ctypes
+    import os
+    import shutil
+    import subprocess
+    from orb_slam3_ros_amd.matcher import CFrame
+    if shutil.which("gcc") is None:
+        pytest.skip("needs gcc")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = tmp_path / "lay.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "orbfe.h"\nint main(void){printf("%zu %zu %zu",'
+                   ' sizeof(orbfe_frame), offsetof(orbfe_frame, device), offsetof(orbfe_frame, r2l));return 0;}\n')
+    exe = tmp_path / "lay"
+    subprocess.run(["gcc", "-I", os.path.join(root, "include"), "-o", str(exe), str(src)], check=True)
+    size, dev, r2l = map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split())
+    assert (size, dev, r2l) == (ctypes.sizeof(CFrame), CFrame.device.offset, CFrame.r2l.offset)
 
 
 def _golden_cases():
