@@ -609,7 +609,7 @@ def pmc_valu(n_img, w, h):
     return best
 
 
-def write_sequence_job(path, frames, W=752, H=480, nf=1000, window=20, seed=21):
+def write_sequence_job(path, frames, W=752, H=480, nf=1000, window=20, seed=21, cxy=None):
     """The drop-in harness's input (tests/native/capi_frontend.cpp SeqJob): a seeded synthetic stereo
     sequence (synth.synth_stereo_sequence: a planar scene at disparity SEQ_DISP, the rig moving SEQ_SHIFT
     px per frame, every frame distinct) with the EuRoC MH_01 pinhole intrinsics and the per-frame
@@ -617,6 +617,8 @@ def write_sequence_job(path, frames, W=752, H=480, nf=1000, window=20, seed=21):
     import struct
     from orb_slam3_ros_amd.synth import SEQ_DISP, SEQ_SHIFT, synth_stereo_sequence
     fx, fy, cx, cy = EUROC_FX, 457.296, 367.215, 248.375
+    if cxy is not None:   # a principal point for another image size (the 512x512 two-camera rig)
+        cx, cy = float(cxy[0]), float(cxy[1])
     bf = EUROC_BF
     tx = SEQ_SHIFT * (bf / SEQ_DISP) / fx
     seq = synth_stereo_sequence(seed, frames, W, H)
@@ -687,6 +689,32 @@ def dropin_leg(frames, W=752, H=480, nf=1000, tracking_frames=60, cpu=True):
                         tr["cpu"] = {"error": (rc.stderr or rc.stdout)[-400:]}
                 out["tracking"] = tr
                 out["tracking_frame_ms"] = tr["tracking_frame_ms"]
+            # BASELINE config 4 per frame: the KannalaBrandt8 two-camera Tracking frame (tests/native/
+            # tracking_kb8.h) over a 512x512 sequence, with the CPU restatement beside it as checker
+            kjob = write_sequence_job(os.path.join(d, "seq_kb8.bin"), tracking_frames, 512, 512, nf, 20, 31,
+                                      (256.0, 256.0))
+            gk, ck = os.path.join(d, "gpu_kb8.out"), os.path.join(d, "cpu_kb8.out")
+            r = subprocess.run([binary, "--tracking-kb8", str(tracking_frames), kjob, gk], capture_output=True,
+                               text=True, timeout=300)
+            if r.returncode != 0:
+                out["tracking_kb8"] = {"error": (r.stderr or r.stdout)[-400:]}
+            else:
+                tk = json.loads(r.stdout.strip().splitlines()[-1])
+                if cpu and os.path.exists(B.TRACK_CPU_BIN):
+                    rc = subprocess.run([B.TRACK_CPU_BIN, "--kb8", str(tracking_frames), kjob, ck], capture_output=True,
+                                        text=True, timeout=600)
+                    if rc.returncode == 0:
+                        tc = json.loads(rc.stdout.strip().splitlines()[-1])
+                        same = open(gk, "rb").read() == open(ck, "rb").read()
+                        tk["cpu"] = {"tracking_frame_ms": tc["tracking_frame_ms"], "split_ms": tc["split_ms"],
+                                     "path": tc["path"]}
+                        tk["speedup_vs_cpu"] = round(tc["tracking_frame_ms"] / tk["tracking_frame_ms"], 2)
+                        tk["parity_ok"] = same
+                        tk["parity"] = ("every frame's counts and both cameras' mvpMapPoints identical to the CPU "
+                                        "restatement's run" if same else "MISMATCH against the CPU restatement's run")
+                    else:
+                        tk["cpu"] = {"error": (rc.stderr or rc.stdout)[-400:]}
+                out["tracking_kb8"] = tk
     return out
 
 

@@ -26,6 +26,7 @@ def _stale(target: str, deps: list[str]) -> bool:
 CAPI_SRC = os.path.join(os.path.dirname(_HERE), "tests", "native", "capi_frontend.cpp")
 CAPI_BIN = os.path.join(os.path.dirname(_HERE), "tests", "native", "capi_frontend")
 TRACK_HDR = os.path.join(os.path.dirname(_HERE), "tests", "native", "tracking_loop.h")
+TRACK_KB8_HDR = os.path.join(os.path.dirname(_HERE), "tests", "native", "tracking_kb8.h")
 TRACK_CPU_SRC = os.path.join(os.path.dirname(_HERE), "tests", "native", "tracking_cpu.cpp")
 TRACK_CPU_BIN = os.path.join(os.path.dirname(_HERE), "tests", "native", "tracking_cpu")
 ORACLE_LIB = os.path.join(os.path.dirname(_HERE), "oracle", "liborb_oracle.so")
@@ -45,7 +46,7 @@ def build_library(force: bool = False, verbose: bool = False) -> str:
 def build_capi_consumer(force: bool = False, verbose: bool = False) -> str:
     """The compiled C++ consumer of include/orbfe.h (tests/native/capi_frontend.cpp), linked against the
     in-tree liborbfe.so by name with an $ORIGIN-relative runpath so it runs from the GPU box's copy."""
-    if force or _stale(CAPI_BIN, [CAPI_SRC, TRACK_HDR, LIB, GLUE_HDR]):
+    if force or _stale(CAPI_BIN, [CAPI_SRC, TRACK_HDR, TRACK_KB8_HDR, LIB, GLUE_HDR]):
         cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-I", os.path.join(os.path.dirname(_HERE), "include"),
                "-I", os.path.join(os.path.dirname(_HERE), "shim"),
                "-o", CAPI_BIN, CAPI_SRC, "-L", _HERE, "-lorbfe", "-Wl,-rpath,$ORIGIN/../../orb_slam3_ros_amd",
@@ -60,7 +61,7 @@ def build_tracking_cpu(force: bool = False, verbose: bool = False) -> str:
     """TEST INFRASTRUCTURE: the CPU Tracking-frame timer / parity reference (tests/native/tracking_cpu.cpp),
     tests/native/tracking_loop.h over the oracle's restatement (oracle/liborb_oracle.so, built first by
     oracle/Makefile). Only the CPU-baseline leg of bench.py and the tests run it."""
-    if force or _stale(TRACK_CPU_BIN, [TRACK_CPU_SRC, TRACK_HDR, ORACLE_LIB]):
+    if force or _stale(TRACK_CPU_BIN, [TRACK_CPU_SRC, TRACK_HDR, TRACK_KB8_HDR, ORACLE_LIB]):
         cmd = ["g++", "-O3", "-march=x86-64-v3", "-std=c++17", "-Wall", "-pthread", "-I",
                os.path.join(os.path.dirname(_HERE), "include"), "-o", TRACK_CPU_BIN, TRACK_CPU_SRC, ORACLE_LIB,
                "-Wl,-rpath,$ORIGIN/../../oracle"]

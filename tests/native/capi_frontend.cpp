@@ -27,6 +27,7 @@
 
 #include "orbfe.h"
 #include "orbfe_glue.h"   // shim/: the drop-in shim's own call sequence (Frame(stereo), SearchLocalPoints)
+#include "tracking_kb8.h"
 #include "tracking_loop.h"
 
 namespace {
@@ -396,7 +397,69 @@ struct GpuApi {
     }
 };
 
+// The library as trk::TrackerKB8's Api (tests/native/tracking_kb8.h): Frame(stereo, KB8) the way the
+// reference builds it (two ExtractORB threads with vLappingArea {0, 511}, then the kNN + ratio stage of
+// ComputeStereoFishEyeMatches over the lapping rows), the two-camera SearchByProjection(LastFrame) and
+// SearchLocalPoints through the shim glue with the rig
+struct GpuApiKB8 {
+    ORBextractor& el;
+    ORBextractor& er;
+    int w, h;
+    std::vector<orbfe_map_point> track;
+    int frame_kb8(const uint8_t* L, const uint8_t* R, trk::FrameKB8& f) {
+        std::vector<KeyPoint> kl, kr;
+        std::vector<uint8_t> dl, dr;
+        const int lap[2] = {0, 511};
+        std::thread tl([&] { f.mono_l = el(L, w, h, w, kl, dl, lap); });
+        std::thread tr([&] { f.mono_r = er(R, w, h, w, kr, dr, lap); });
+        tl.join();
+        tr.join();
+        f.nl = (int)kl.size();
+        f.nr = (int)kr.size();
+        f.mono_l = std::max(f.mono_l, 0);
+        f.mono_r = std::max(f.mono_r, 0);
+        const int ql = f.nl - f.mono_l, qr = f.nr - f.mono_r;
+        std::vector<int32_t> train(std::max(ql, 0), -1), dist(std::max(ql, 0), -1);
+        if (ql > 0 && qr > 0)
+            check(orbfe_stereo_knn_ratio(dl.data() + (size_t)f.mono_l * 32, ql, dr.data() + (size_t)f.mono_r * 32, qr,
+                                         0.7f, train.data(), dist.data()),
+                  "stereo_knn_ratio");
+        f.keys.resize(f.nl + f.nr);
+        memcpy(f.keys.data(), kl.data(), kl.size() * sizeof(KeyPoint));
+        memcpy(f.keys.data() + f.nl, kr.data(), kr.size() * sizeof(KeyPoint));
+        f.desc.resize((size_t)(f.nl + f.nr) * 32);
+        memcpy(f.desc.data(), dl.data(), dl.size());
+        memcpy(f.desc.data() + dl.size(), dr.data(), dr.size());
+        f.nstereo = trk::fisheye_links(f, train);
+        return f.nstereo;
+    }
+    int sbp_last_stereo(const orbfe_frame* F, int32_t* mvp, const int32_t* obs, const orbfe_proj_point* pts,
+                        const float* ruv, int n, float th) {
+        const int r = orbfe_search_by_projection_lastframe_stereo(F, mvp, obs, pts, ruv, n, th, 0, 0, 1);
+        check(r, "search_by_projection_lastframe_stereo");
+        return r;
+    }
+    int local_points_rig(const orbfe_frame* F, const orbfe_camera* c, const orbfe_stereo_rig* rig,
+                         const orbfe_map_point_3d* pts, int n, int32_t* mvp, const int32_t* obs, float th,
+                         int32_t* ntm) {
+        const int r = orbfe_glue::local_points(F, c, rig, pts, n, mvp, obs, th, false, 50.f, track, ntm);
+        check(r, "search_local_points_track (rig)");
+        return r;
+    }
+};
+
 }  // namespace
+
+int tracking_kb8(int frames, const char* job, const char* out_path) {
+    const SeqJob J = read_seq(job);
+    ORBextractor el(J.nf, 1.2f, 8, 20, 7), er(J.nf, 1.2f, 8, 20, 7);
+    GpuApiKB8 api{el, er, J.w, J.h, {}};
+    return trk::run_sequence_kb8(api, J.cam, J.w, J.h, el.mvScaleFactor, J.window, frames, J.npairs,
+                                 [&](int k) { return J.left(k); }, [&](int k) { return J.right(k); }, out_path,
+                                 "gpu: liborbfe.so C-ABI, KannalaBrandt8 two-camera frame (orbfe_extract x 2 threads, "
+                                 "orbfe_stereo_knn_ratio, orbfe_search_by_projection_lastframe_stereo, "
+                                 "orbfe_search_local_points_track with the rig)");
+}
 
 int tracking(int frames, const char* job, const char* out_path, bool diag, bool host_view = false) {
     const SeqJob J = read_seq(job);
@@ -429,6 +492,14 @@ int main(int argc, char** argv) {
         try {
             return tracking(atoi(argv[2]), argv[3], argc == 5 ? argv[4] : nullptr, std::string(argv[1]) == "--tracking-diag",
                             std::string(argv[1]) == "--tracking-hostview");
+        } catch (const std::exception& e) {
+            fprintf(stderr, "capi_frontend: %s\n", e.what());
+            return 1;
+        }
+    }
+    if ((argc == 4 || argc == 5) && std::string(argv[1]) == "--tracking-kb8") {
+        try {
+            return tracking_kb8(atoi(argv[2]), argv[3], argc == 5 ? argv[4] : nullptr);
         } catch (const std::exception& e) {
             fprintf(stderr, "capi_frontend: %s\n", e.what());
             return 1;

@@ -4,12 +4,15 @@
 // std::threads started per frame, as Frame.cc:122-125 does, then runs ComputeStereoMatches (:141).
 // usage: tracking_cpu <frames> <seq.bin> [out.bin]   (seq.bin: the sequence job of capi_frontend)
 #include <cstdio>
+#include <algorithm>
 #include <cstdlib>
+#include <string>
 #include <stdexcept>
 #include <thread>
 #include <vector>
 
 #include "orbfe.h"
+#include "tracking_kb8.h"
 #include "tracking_loop.h"
 
 // oracle/orb_oracle.cpp, orb_oracle_match.cpp (KeyPoint records are the 28-byte cv::KeyPoint layout)
@@ -27,6 +30,14 @@ int oro_sbp_lastframe(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_o
 int oro_search_local_points(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_map_point_3d* pts, int32_t n,
                             int32_t* mvp, const int32_t* mvp_obs, float th, int32_t bFarPoints, float thFarPoints,
                             float nnratio, int32_t* n_to_match);
+int oro_stereo_knn_ratio(const uint8_t* L, int32_t nl, const uint8_t* R, int32_t nr, float ratio, int32_t* out_train,
+                         int32_t* out_dist);
+int oro_sbp_lastframe_stereo(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_obs_in,
+                             const orbfe_proj_point* pts, const float* right_uv, int32_t n_pts, float th,
+                             int32_t bForward, int32_t bBackward, int32_t checkOri);
+int oro_search_local_points_rig(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_stereo_rig* rig,
+                                const orbfe_map_point_3d* pts, int32_t n, int32_t* mvp, const int32_t* mvp_obs, float th,
+                                int32_t bFarPoints, float thFarPoints, float nnratio, int32_t* n_to_match);
 }
 
 namespace {
@@ -65,13 +76,54 @@ struct CpuApi {
                      const int32_t* obs, float th, int bFar, float thFar, float ratio, int32_t* ntm) {
         return oro_search_local_points(F, c, pts, n, mvp, obs, th, bFar, thFar, ratio, ntm);
     }
+    // the two-camera Tracking frame (tests/native/tracking_kb8.h) on the restatement
+    int frame_kb8(const uint8_t* L, const uint8_t* R, trk::FrameKB8& f) {
+        std::vector<orbfe_keypoint> kl(cap), kr(cap);
+        std::vector<uint8_t> dl((size_t)cap * 32), dr((size_t)cap * 32);
+        int nl = 0, nr = 0;
+        std::thread tl([&] { f.mono_l = oro_extract(el, L, w, h, w, 0, 511, kl.data(), cap, dl.data(), &nl); });
+        std::thread tr([&] { f.mono_r = oro_extract(er, R, w, h, w, 0, 511, kr.data(), cap, dr.data(), &nr); });
+        tl.join();
+        tr.join();
+        if (nl > cap || nr > cap) throw std::runtime_error("keypoint capacity");
+        f.nl = nl;
+        f.nr = nr;
+        f.mono_l = std::max(f.mono_l, 0);
+        f.mono_r = std::max(f.mono_r, 0);
+        const int ql = nl - f.mono_l, qr = nr - f.mono_r;
+        std::vector<int32_t> train(std::max(ql, 0), -1), dist(std::max(ql, 0), -1);
+        if (ql > 0 && qr > 0)
+            oro_stereo_knn_ratio(dl.data() + (size_t)f.mono_l * 32, ql, dr.data() + (size_t)f.mono_r * 32, qr, 0.7f,
+                                 train.data(), dist.data());
+        f.keys.assign(kl.begin(), kl.begin() + nl);
+        f.keys.insert(f.keys.end(), kr.begin(), kr.begin() + nr);
+        f.desc.assign(dl.begin(), dl.begin() + (size_t)nl * 32);
+        f.desc.insert(f.desc.end(), dr.begin(), dr.begin() + (size_t)nr * 32);
+        f.nstereo = trk::fisheye_links(f, train);
+        return f.nstereo;
+    }
+    int sbp_last_stereo(const orbfe_frame* F, int32_t* mvp, const int32_t* obs, const orbfe_proj_point* pts,
+                        const float* ruv, int n, float th) {
+        return oro_sbp_lastframe_stereo(F, mvp, obs, pts, ruv, n, th, 0, 0, 1);
+    }
+    int local_points_rig(const orbfe_frame* F, const orbfe_camera* c, const orbfe_stereo_rig* rig,
+                         const orbfe_map_point_3d* pts, int n, int32_t* mvp, const int32_t* obs, float th,
+                         int32_t* ntm) {
+        return oro_search_local_points_rig(F, c, rig, pts, n, mvp, obs, th, 0, 50.f, 0.8f, ntm);
+    }
 };
 
 }  // namespace
 
 int main(int argc, char** argv) {
+    // --kb8: the KannalaBrandt8 two-camera Tracking frame (tests/native/tracking_kb8.h)
+    const bool kb8 = argc >= 2 && std::string(argv[1]) == "--kb8";
+    if (kb8) {
+        argv++;
+        argc--;
+    }
     if (argc != 3 && argc != 4) {
-        fprintf(stderr, "usage: tracking_cpu <frames> <seq.bin> [out.bin]\n");
+        fprintf(stderr, "usage: tracking_cpu [--kb8] <frames> <seq.bin> [out.bin]\n");
         return 2;
     }
     try {
@@ -94,10 +146,14 @@ int main(int argc, char** argv) {
         const trk::Cam cam{c[0], c[1], c[2], c[3], c[4], c[5]};
         auto L = [&](int k) { return px.data() + (size_t)(k % npairs) * 2 * w * h; };
         auto R = [&](int k) { return px.data() + (size_t)(k % npairs) * 2 * w * h + (size_t)w * h; };
-        const int rc = trk::run_sequence(api, cam, w, h, scale, window, atoi(argv[1]), npairs, L, R,
-                                         argc == 4 ? argv[3] : nullptr,
-                                         "cpu: oracle restatement (2 extraction threads per frame, then the matchers "
-                                         "on the calling thread)");
+        const int rc = kb8 ? trk::run_sequence_kb8(api, cam, w, h, scale, window, atoi(argv[1]), npairs, L, R,
+                                                   argc == 4 ? argv[3] : nullptr,
+                                                   "cpu: oracle restatement, KannalaBrandt8 two-camera frame (2 "
+                                                   "extraction threads, kNN + ratio, then the matchers)")
+                           : trk::run_sequence(api, cam, w, h, scale, window, atoi(argv[1]), npairs, L, R,
+                                               argc == 4 ? argv[3] : nullptr,
+                                               "cpu: oracle restatement (2 extraction threads per frame, then the "
+                                               "matchers on the calling thread)");
         oro_destroy(el);
         oro_destroy(er);
         return rc;

@@ -140,16 +140,66 @@ def tracking_cpu_bin(oracle_lib):
     return B.build_tracking_cpu()
 
 
-def _tracking_records(buf):
-    """Per frame {n_left, n_right, n_stereo, sbp_th, sbp_matches, n_to_match, local_matches, mvp[n_left]}."""
+def _tracking_records(buf, two_cams=False):
+    """Per frame {n_left, n_right, n_stereo, sbp_th, sbp_matches, n_to_match, local_matches, mvp[n_left]}
+    (two-camera frames: mvp[n_left + n_right], both cameras' slots)."""
     a = np.frombuffer(buf, "<i4")
     out, o = [], 0
     while o < len(a):
         rec = a[o:o + 7]
-        mvp = a[o + 7:o + 7 + rec[0]]
+        n = rec[0] + (rec[1] if two_cams else 0)
+        mvp = a[o + 7:o + 7 + n]
         out.append((rec.copy(), mvp.copy()))
-        o += 7 + rec[0]
+        o += 7 + n
     return out
+
+
+@pytest.fixture(scope="module")
+def seq_job_kb8(tmp_path_factory):
+    import bench
+    p = tmp_path_factory.mktemp("seqkb8") / "seq.bin"
+    return str(bench.write_sequence_job(str(p), 24, 512, 512, 1000, 20, 31, (256.0, 256.0)))
+
+
+def test_tracking_kb8_cpu_sequence(tracking_cpu_bin, seq_job_kb8, tmp_path):
+    """The KannalaBrandt8 two-camera Tracking loop on the CPU restatement (tests/native/tracking_kb8.h):
+    deterministic, and every call does real work (ratio-test stereo pairs, a last-frame search over
+    both cameras' slots, a local map projected into both cameras)."""
+    import json
+    outs = []
+    for i in range(2):
+        o = tmp_path / f"k{i}.out"
+        r = subprocess.run([tracking_cpu_bin, "--kb8", "10", seq_job_kb8, str(o)], capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr
+        outs.append(o.read_bytes())
+    assert outs[0] == outs[1]
+    recs = _tracking_records(outs[0], two_cams=True)
+    assert len(recs) == 10
+    st = json.loads(r.stdout.strip().splitlines()[-1])
+    assert st["mean"]["stereo_matches"] > 200 and st["mean"]["last_frame_matches"] > 0.5 * st["mean"]["last_frame_points"]
+    assert st["mean"]["local_to_match"] > 50 and st["mean"]["local_matches"] > 10
+    assert any((mvp[rec[0]:] >= 0).any() for rec, mvp in recs[1:])   # right-camera slots matched too
+
+
+@pytest.mark.gpu
+def test_tracking_kb8_sequence_matches_cpu(consumer, tracking_cpu_bin, seq_job_kb8, tmp_path):
+    """The two-camera Tracking frame through the C-ABI (two orbfe_extract threads with vLappingArea
+    {0, 511}, orbfe_stereo_knn_ratio, orbfe_search_by_projection_lastframe_stereo,
+    orbfe_search_local_points_track with a KannalaBrandt8 rig) over 24 frames, against the same loop
+    on the CPU restatement: every frame's counts and both cameras' slots identical."""
+    g, c = tmp_path / "gpu.out", tmp_path / "cpu.out"
+    r = subprocess.run([consumer, "--tracking-kb8", "24", seq_job_kb8, str(g)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    rc = subprocess.run([tracking_cpu_bin, "--kb8", "24", seq_job_kb8, str(c)], capture_output=True, text=True,
+                        timeout=600)
+    assert rc.returncode == 0, rc.stderr
+    gr, cr = _tracking_records(g.read_bytes(), True), _tracking_records(c.read_bytes(), True)
+    assert len(gr) == len(cr) == 24
+    for k, ((ga, gm), (ca, cm)) in enumerate(zip(gr, cr)):
+        np.testing.assert_array_equal(ga, ca, err_msg=f"frame {k} counts")
+        np.testing.assert_array_equal(gm, cm, err_msg=f"frame {k} mvpMapPoints")
 
 
 def test_tracking_cpu_sequence_deterministic(tracking_cpu_bin, seq_job, tmp_path):
