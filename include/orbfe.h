@@ -158,6 +158,20 @@ int orbfe_frame_stereo(orbfe_extractor* left, orbfe_extractor* right, const uint
                        orbfe_keypoint* kps_right, uint8_t* desc_right, int cap_right, int* n_right,
                        int* mono_right, float* uright, float* depth);
 
+/* Frame::Frame(imLeft, imRight, ..., KannalaBrandt8 rig) (src/Frame.cc:1034-1105) up to its descriptor
+ * matching, in one call like orbfe_frame_stereo: ExtractORB(0, imLeft) and ExtractORB(1, imRight)
+ * with vLappingArea {lap0, lap1} (:1059-1062; TUM-VI overlappingBegin/End), then
+ * ComputeStereoFishEyeMatches' knnMatch(k = 2) + ratio test of the lapping rows (:1126-1151), as ONE
+ * two-image launch chain on `left`. l2r[n_left]: the right keypoint index (mvKeysRight numbering) of
+ * each left keypoint whose ratio test passes, -1 otherwise (the mvLeftToRightMatch candidates that
+ * the camera model's TriangulateMatches then confirms on the host, :1152-1160); dist[n_left] their
+ * Hamming distance or -1. Returns the passing query count (the kNN stage's good matches). */
+int orbfe_frame_fisheye(orbfe_extractor* left, orbfe_extractor* right, const uint8_t* img_left,
+                        const uint8_t* img_right, int width, int height, int stride, int lap0, int lap1, float ratio,
+                        orbfe_keypoint* kps_left, uint8_t* desc_left, int cap_left, int* n_left, int* mono_left,
+                        orbfe_keypoint* kps_right, uint8_t* desc_right, int cap_right, int* n_right,
+                        int* mono_right, int32_t* l2r, int32_t* dist);
+
 /* ---------------------------------------------------------------------------------------------
  * ORBmatcher — replaces the Tracking-thread methods of ORB_SLAM3::ORBmatcher (include/ORBmatcher.h)
  * and Frame::ComputeStereoFishEyeMatches' brute-force kNN. Stateless and re-entrant; every call

@@ -57,6 +57,8 @@ _SIGS = {
     "orbfe_stereo_match": (_c_int, [_vp, _vp, _c_float, _c_float, _vp, _vp]),
     "orbfe_frame_stereo": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _c_float,
                                     _vp, _vp, _c_int, _P_int, _P_int, _vp, _vp, _c_int, _P_int, _P_int, _vp, _vp]),
+    "orbfe_frame_fisheye": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float,
+                                     _vp, _vp, _c_int, _P_int, _P_int, _vp, _vp, _c_int, _P_int, _P_int, _vp, _vp]),
     "orbfe_descriptor_distance": (_c_int, [_vp, _vp]),
     "orbfe_debug_copy": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _c_int]),
     "orbfe_debug_block_sort": (_c_int, [_vp, _c_int]),

@@ -1197,16 +1197,20 @@ int orbfe_stereo_match(orbfe_extractor* left, orbfe_extractor* right, float bf, 
 // the same stream, one pinned upload of both images and one synchronisation for all results. The
 // right handle only supplies (and must equal) the extractor parameters, as Tracking constructs both
 // extractors from the same settings (Tracking.cc:637-645); it is not written.
-int orbfe_frame_stereo(orbfe_extractor* left, orbfe_extractor* right, const uint8_t* img_left,
-                       const uint8_t* img_right, int width, int height, int stride, float bf, float fx,
-                       orbfe_keypoint* kps_left, uint8_t* desc_left, int cap_left, int* n_left, int* mono_left,
-                       orbfe_keypoint* kps_right, uint8_t* desc_right, int cap_right, int* n_right,
-                       int* mono_right, float* uright, float* depth) {
+// The two-image frame call behind orbfe_frame_stereo (pinhole: vLappingArea {0, 0}, then
+// ComputeStereoMatches) and orbfe_frame_fisheye (KannalaBrandt8: the caller's vLappingArea, then the
+// kNN + ratio stage): one upload through a mapped pinned block, one launch chain, one result pull.
+// The per-left-keypoint results (uR / depth floats, or l2r / dist ints) share the d_st region.
+static int frame_pair(orbfe_extractor* left, orbfe_extractor* right, const uint8_t* img_left, const uint8_t* img_right,
+                      int width, int height, int stride, bool fisheye, int lap0, int lap1, float bf, float fx,
+                      float ratio, orbfe_keypoint* kps_left, uint8_t* desc_left, int cap_left, int* n_left,
+                      int* mono_left, orbfe_keypoint* kps_right, uint8_t* desc_right, int cap_right, int* n_right,
+                      int* mono_right, void* res_a, void* res_b) {
     if (!left || !right || !n_left || !n_right || !mono_left || !mono_right) return ORBFE_E_ARG;
     *n_left = *n_right = 0;
     *mono_left = *mono_right = -1;
     if (!img_left || !img_right || width <= 0 || height <= 0) return ORBFE_E_EMPTY;
-    if (stride < width || !kps_left || !desc_left || !kps_right || !desc_right || !uright || !depth) return ORBFE_E_ARG;
+    if (stride < width || !kps_left || !desc_left || !kps_right || !desc_right || !res_a || !res_b) return ORBFE_E_ARG;
     if (left != right && (left->nfeatures != right->nfeatures || left->nlevels != right->nlevels ||
                           left->scale_factor_f != right->scale_factor_f || left->ini_th != right->ini_th ||
                           left->min_th != right->min_th || left->resize_simd_lanes != right->resize_simd_lanes ||
@@ -1274,7 +1278,9 @@ int orbfe_frame_stereo(orbfe_extractor* left, orbfe_extractor* right, const uint
         }
     }
     const uint8_t* ptrs[2] = {h->d_stage, h->d_stage + bytes};
-    const int laps[4] = {0, 0, 0, 0};   // the pinhole stereo Frame passes vLappingArea {0, 0} (Frame.cc:122-123)
+    // the pinhole stereo Frame passes vLappingArea {0, 0} (Frame.cc:122-123), the KB8 one its
+    // overlapping area (:1059-1060)
+    const int laps[4] = {fisheye ? lap0 : 0, fisheye ? lap1 : 0, fisheye ? lap0 : 0, fisheye ? lap1 : 0};
     if (!split) {   // both images in one push (an image size that is not whole 16-byte items), or by DMA
         if (tm) HIPCHK(hipEventRecord(h->call_ev[0], s));
         if (!h->no_push) {
@@ -1291,7 +1297,11 @@ int orbfe_frame_stereo(orbfe_extractor* left, orbfe_extractor* right, const uint
     h->timing = tm;
     if (rc) return rc;
     if (tm) HIPCHK(hipEventRecord(h->call_ev[2], s));
-    rc = orbfe_stereo_match_batch(h, 0, 1, h, 1, 1, 1, bf, fx, h->d_uright, h->d_depth, h->d_nmatch, s);
+    if (fisheye)   // ComputeStereoFishEyeMatches' descriptor stage (Frame.cc:1126-1151): l2r / dist in d_st
+        rc = orbfe_stereo_knn_batch(h, 0, 1, h, 1, 1, 1, ratio, (int32_t*)h->d_uright, (int32_t*)h->d_depth,
+                                    h->d_nmatch, s);
+    else
+        rc = orbfe_stereo_match_batch(h, 0, 1, h, 1, 1, 1, bf, fx, h->d_uright, h->d_depth, h->d_nmatch, s);
     if (rc) return rc;
     if (tm) HIPCHK(hipEventRecord(h->call_ev[4], s));
     if (h->cap_b == 2 && !h->no_pull) {   // the two-image output block and the stereo results: one kernel
@@ -1321,16 +1331,18 @@ int orbfe_frame_stereo(orbfe_extractor* left, orbfe_extractor* right, const uint
     *mono_left = cnt[1];
     *mono_right = cnt[3];
     if (cnt[0] > cap_left || cnt[2] > cap_right) return ORBFE_E_CAPACITY;
-    h->fs_id = h->frame_id;   // the left image's records stay in the handle's output block
-    h->fs_n = cnt[0];
+    if (!fisheye) {   // the left image's records stay in the handle's output block (orbfe_frame_device_view)
+        h->fs_id = h->frame_id;
+        h->fs_n = cnt[0];
+    }
     const OrbKeyPoint* hk = (const OrbKeyPoint*)(hp + o_kps);
     const uint8_t* hd = hp + o_desc;
     memcpy(kps_left, hk, (size_t)cnt[0] * sizeof(OrbKeyPoint));
     memcpy(desc_left, hd, (size_t)cnt[0] * 32);
     memcpy(kps_right, hk + kc, (size_t)cnt[2] * sizeof(OrbKeyPoint));
     memcpy(desc_right, hd + (size_t)kc * 32, (size_t)cnt[2] * 32);
-    memcpy(uright, hp + o_st + 16, (size_t)cnt[0] * 4);
-    memcpy(depth, hp + o_st + 16 + (size_t)h->stereo_kp * 4, (size_t)cnt[0] * 4);
+    memcpy(res_a, hp + o_st + 16, (size_t)cnt[0] * 4);   // uR or l2r
+    memcpy(res_b, hp + o_st + 16 + (size_t)h->stereo_kp * 4, (size_t)cnt[0] * 4);   // depth or dist
     // slots as the header documents: {upload, extraction kernels, result copies, stereo kernels}. On the
     // split path the upload slot starts at the left image's push and so also counts the host packing
     // of the right image (the GPU waits for it): it is push + packing, not a pure transfer time.
@@ -1342,6 +1354,26 @@ int orbfe_frame_stereo(orbfe_extractor* left, orbfe_extractor* right, const uint
         h->call_ms[4] = 0.f;
     }
     return nm;
+}
+
+int orbfe_frame_stereo(orbfe_extractor* left, orbfe_extractor* right, const uint8_t* img_left,
+                       const uint8_t* img_right, int width, int height, int stride, float bf, float fx,
+                       orbfe_keypoint* kps_left, uint8_t* desc_left, int cap_left, int* n_left, int* mono_left,
+                       orbfe_keypoint* kps_right, uint8_t* desc_right, int cap_right, int* n_right,
+                       int* mono_right, float* uright, float* depth) {
+    return frame_pair(left, right, img_left, img_right, width, height, stride, false, 0, 0, bf, fx, 0.f, kps_left,
+                      desc_left, cap_left, n_left, mono_left, kps_right, desc_right, cap_right, n_right, mono_right,
+                      uright, depth);
+}
+
+int orbfe_frame_fisheye(orbfe_extractor* left, orbfe_extractor* right, const uint8_t* img_left,
+                        const uint8_t* img_right, int width, int height, int stride, int lap0, int lap1, float ratio,
+                        orbfe_keypoint* kps_left, uint8_t* desc_left, int cap_left, int* n_left, int* mono_left,
+                        orbfe_keypoint* kps_right, uint8_t* desc_right, int cap_right, int* n_right,
+                        int* mono_right, int32_t* l2r, int32_t* dist) {
+    return frame_pair(left, right, img_left, img_right, width, height, stride, true, lap0, lap1, 0.f, 1.f, ratio,
+                      kps_left, desc_left, cap_left, n_left, mono_left, kps_right, desc_right, cap_right, n_right,
+                      mono_right, l2r, dist);
 }
 
 uint64_t orbfe_extractor_frame_id(orbfe_extractor* h) { return h ? h->frame_id : 0; }

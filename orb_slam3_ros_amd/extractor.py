@@ -175,3 +175,36 @@ def frame_stereo(left: ORBextractor, right: ORBextractor, imLeft, imRight, bf: f
     n, m = nl.value, nr.value
     return ((ml.value, kl[:n].copy(), dl[:n].copy()), (mr.value, kr[:m].copy(), dr[:m].copy()),
             ur[:n].copy(), dp[:n].copy(), rc)
+
+
+def frame_fisheye(left: ORBextractor, right: ORBextractor, imLeft, imRight, lap=(0, 511), ratio: float = 0.7):
+    """Frame::Frame(stereo, KannalaBrandt8) (Frame.cc:1034-1105) up to the descriptor stage in one library
+    call: ExtractORB on both images with vLappingArea `lap` (:1059-1062) as one two-image batch on `left`,
+    then ComputeStereoFishEyeMatches' knnMatch(k=2) + ratio over the lapping rows (:1126-1151).
+    Returns ((monoLeft, kpsLeft, descLeft), (monoRight, kpsRight, descRight), l2r, dist, n_good):
+    l2r[i] = the right keypoint index of left keypoint i whose ratio test passes, else -1."""
+    L = np.ascontiguousarray(np.asarray(imLeft))
+    R = np.ascontiguousarray(np.asarray(imRight))
+    if L.size == 0 or R.size == 0:
+        raise _lib.OrbfeError("Frame(stereo) needs two non-empty images")
+    for im in (L, R):
+        if im.dtype != np.uint8 or im.ndim != 2:
+            raise _lib.OrbfeError("ORBextractor expects a single-channel uint8 image (CV_8UC1)")
+    if L.shape != R.shape:
+        raise _lib.OrbfeError("left and right images differ in size")
+    h, w = L.shape
+    cap = left.capacity(w, h)
+    kl, kr = np.zeros(cap, KEYPOINT_DTYPE), np.zeros(cap, KEYPOINT_DTYPE)
+    dl, dr = np.zeros((cap, 32), np.uint8), np.zeros((cap, 32), np.uint8)
+    l2r, dist = np.zeros(cap, np.int32), np.zeros(cap, np.int32)
+    nl, nr, ml, mr = (ctypes.c_int() for _ in range(4))
+    rc = _lib.load().orbfe_frame_fisheye(left.handle, right.handle, L.ctypes.data, R.ctypes.data, w, h, w,
+                                         int(lap[0]), int(lap[1]), float(ratio), kl.ctypes.data, dl.ctypes.data, cap,
+                                         ctypes.byref(nl), ctypes.byref(ml), kr.ctypes.data, dr.ctypes.data, cap,
+                                         ctypes.byref(nr), ctypes.byref(mr), l2r.ctypes.data, dist.ctypes.data)
+    _lib.check(rc, "orbfe_frame_fisheye")
+    left._last_shape = (h, w)
+    n, m = nl.value, nr.value
+    return ((ml.value, kl[:n].copy(), dl[:n].copy()), (mr.value, kr[:m].copy(), dr[:m].copy()), l2r[:n].copy(),
+            dist[:n].copy(), rc)
+

@@ -55,6 +55,46 @@ int frame_stereo(orbfe_extractor* hl, orbfe_extractor* hr, const uint8_t* img_l,
     return ns;
 }
 
+// Frame::Frame(imLeft, imRight, ..., KannalaBrandt8) (Frame.cc:1034-1105) up to the descriptor stage
+// of ComputeStereoFishEyeMatches (:1126-1151): the two ExtractORB threads with each camera's
+// vLappingArea (:1059-1062; one pair for both images here, as the batched engine) and knnMatch(k = 2)
+// + ratio over the lapping rows as ONE orbfe_frame_fisheye call. On success l2r[i] is the right
+// keypoint (absolute index) left keypoint i's ratio test keeps, -1 otherwise, dist[i] its Hamming
+// distance; the return value is the number kept. The triangulation and depth checks that follow in
+// the reference (:1153-1176) need the camera models and stay with the caller.
+template <class Key, class Desc>
+int frame_fisheye(orbfe_extractor* hl, orbfe_extractor* hr, const uint8_t* img_l, const uint8_t* img_r, int width,
+                  int height, int stride, int lap0, int lap1, float ratio, std::vector<Key>& kl, Desc& dl, int* mono_l,
+                  std::vector<Key>& kr, Desc& dr, int* mono_r, std::vector<int32_t>& l2r,
+                  std::vector<int32_t>& dist) {
+    static_assert(sizeof(Key) == sizeof(orbfe_keypoint), "cv::KeyPoint layout (28 B) expected");
+    if (width <= 0 || height <= 0 || !img_l || !img_r) {
+        kl.clear(); kr.clear(); l2r.clear(); dist.clear();
+        dl.keep(0); dr.keep(0);
+        *mono_l = *mono_r = -1;
+        return 0;
+    }
+    const int cap = orbfe_extractor_capacity(hl, width, height);
+    if (cap < 0) return cap;
+    kl.resize(cap);
+    kr.resize(cap);
+    l2r.resize(cap);
+    dist.resize(cap);
+    int nl = 0, nr = 0;
+    const int ng = orbfe_frame_fisheye(hl, hr, img_l, img_r, width, height, stride, lap0, lap1, ratio,
+                                       reinterpret_cast<orbfe_keypoint*>(kl.data()), dl.rows(cap), cap, &nl, mono_l,
+                                       reinterpret_cast<orbfe_keypoint*>(kr.data()), dr.rows(cap), cap, &nr, mono_r,
+                                       l2r.data(), dist.data());
+    if (ng < 0) return ng;
+    kl.resize(nl);
+    kr.resize(nr);
+    dl.keep(nl);
+    dr.keep(nr);
+    l2r.resize(nl);
+    dist.resize(nl);
+    return ng;
+}
+
 // The pose part of Frame::isInFrustum's inputs (Frame.cc:512-586): Rcw row-major, tcw, Ow = the
 // camera centre; fx..cy the pinhole parameters (unused with a rig), mfLogScaleFactor, and the
 // viewing-cosine limit SearchLocalPoints passes (0.5, Tracking.cc:3415).

@@ -407,29 +407,27 @@ struct GpuApiKB8 {
     int w, h;
     std::vector<orbfe_map_point> track;
     int frame_kb8(const uint8_t* L, const uint8_t* R, trk::FrameKB8& f) {
+        // both extractions (vLappingArea {0, 511}) and the kNN ratio test in one library call
         std::vector<KeyPoint> kl, kr;
         std::vector<uint8_t> dl, dr;
-        const int lap[2] = {0, 511};
-        std::thread tl([&] { f.mono_l = el(L, w, h, w, kl, dl, lap); });
-        std::thread tr([&] { f.mono_r = er(R, w, h, w, kr, dr, lap); });
-        tl.join();
-        tr.join();
+        std::vector<int32_t> l2r, dist;
+        VecRows sl{dl}, sr{dr};
+        check(orbfe_glue::frame_fisheye(el.handle(), er.handle(), L, R, w, h, w, 0, 511, 0.7f, kl, sl, &f.mono_l, kr,
+                                        sr, &f.mono_r, l2r, dist),
+              "frame_fisheye");
         f.nl = (int)kl.size();
         f.nr = (int)kr.size();
         f.mono_l = std::max(f.mono_l, 0);
         f.mono_r = std::max(f.mono_r, 0);
-        const int ql = f.nl - f.mono_l, qr = f.nr - f.mono_r;
-        std::vector<int32_t> train(std::max(ql, 0), -1), dist(std::max(ql, 0), -1);
-        if (ql > 0 && qr > 0)
-            check(orbfe_stereo_knn_ratio(dl.data() + (size_t)f.mono_l * 32, ql, dr.data() + (size_t)f.mono_r * 32, qr,
-                                         0.7f, train.data(), dist.data()),
-                  "stereo_knn_ratio");
+        std::vector<int32_t> train(std::max(f.nl - f.mono_l, 0), -1);
+        for (int q = 0; q < (int)train.size(); q++)
+            if (l2r[q + f.mono_l] >= 0) train[q] = l2r[q + f.mono_l] - f.mono_r;
         f.keys.resize(f.nl + f.nr);
         memcpy(f.keys.data(), kl.data(), kl.size() * sizeof(KeyPoint));
         memcpy(f.keys.data() + f.nl, kr.data(), kr.size() * sizeof(KeyPoint));
         f.desc.resize((size_t)(f.nl + f.nr) * 32);
-        memcpy(f.desc.data(), dl.data(), dl.size());
-        memcpy(f.desc.data() + dl.size(), dr.data(), dr.size());
+        memcpy(f.desc.data(), dl.data(), (size_t)f.nl * 32);
+        memcpy(f.desc.data() + (size_t)f.nl * 32, dr.data(), (size_t)f.nr * 32);
         f.nstereo = trk::fisheye_links(f, train);
         return f.nstereo;
     }
@@ -456,8 +454,8 @@ int tracking_kb8(int frames, const char* job, const char* out_path) {
     GpuApiKB8 api{el, er, J.w, J.h, {}};
     return trk::run_sequence_kb8(api, J.cam, J.w, J.h, el.mvScaleFactor, J.window, frames, J.npairs,
                                  [&](int k) { return J.left(k); }, [&](int k) { return J.right(k); }, out_path,
-                                 "gpu: liborbfe.so C-ABI, KannalaBrandt8 two-camera frame (orbfe_extract x 2 threads, "
-                                 "orbfe_stereo_knn_ratio, orbfe_search_by_projection_lastframe_stereo, "
+                                 "gpu: liborbfe.so C-ABI, KannalaBrandt8 two-camera frame (orbfe_frame_fisheye, "
+                                 "orbfe_search_by_projection_lastframe_stereo, "
                                  "orbfe_search_local_points_track with the rig)");
 }
 

@@ -313,3 +313,31 @@ def test_frame_device_view_searches(gpu):
     el(left, None, (0, 0))   # the handle extracts again: the view is stale
     assert current_frame_view(F, el, fid) is None
 
+
+@pytest.mark.parametrize("lap", [(0, 511), (100, 400)])
+def test_frame_fisheye_entry(gpu, oracle_lib, lap):
+    """orbfe_frame_fisheye (Frame(stereo, KannalaBrandt8) up to its descriptor stage, Frame.cc:1034-1151,
+    in one call) against the oracle's two extractions with the same vLappingArea + knnMatch(k=2) +
+    ratio 0.7 over the lapping rows: keypoints, descriptors, monoIndex, the l2r candidates and their
+    count, over a seeded sequence on the same handles."""
+    from orb_slam3_ros_amd.extractor import ORBextractor, frame_fisheye
+    el, er = ORBextractor(1000, 1.2, 8, 20, 7), ORBextractor(1000, 1.2, 8, 20, 7)
+    for seed in (31, 32, 33):
+        left, right = synth_stereo(seed, 512, 512)
+        (ml, kl, dl), (mr, kr, dr), l2r, dist, ng = frame_fisheye(el, er, left, right, lap, 0.7)
+        ol, orr = oracle_lib.OracleExtractor(1000, 1.2, 8, 20, 7), oracle_lib.OracleExtractor(1000, 1.2, 8, 20, 7)
+        oml, okl, odl = ol(left, lap)
+        omr, okr, odr = orr(right, lap)
+        assert (ml, mr) == (oml, omr)
+        assert np.array_equal(kl.view(np.uint8), okl.view(np.uint8)) and np.array_equal(dl, odl)
+        assert np.array_equal(kr.view(np.uint8), okr.view(np.uint8)) and np.array_equal(dr, odr)
+        g, t, d = oracle_lib.stereo_knn_ratio(odl[oml:], odr[omr:], 0.7)
+        exp, expd = np.full(len(okl), -1, np.int32), np.full(len(okl), -1, np.int32)
+        exp[oml:][t >= 0] = t[t >= 0] + omr
+        expd[oml:][t >= 0] = d[t >= 0]
+        assert ng == g and g > 50
+        np.testing.assert_array_equal(l2r, exp)
+        np.testing.assert_array_equal(dist, expd)
+        ol.close()
+        orr.close()
+
