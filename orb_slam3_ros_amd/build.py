@@ -47,7 +47,8 @@ def build_capi_consumer(force: bool = False, verbose: bool = False) -> str:
     """The compiled C++ consumer of include/orbfe.h (tests/native/capi_frontend.cpp), linked against the
     in-tree liborbfe.so by name with an $ORIGIN-relative runpath so it runs from the GPU box's copy."""
     if force or _stale(CAPI_BIN, [CAPI_SRC, TRACK_HDR, TRACK_KB8_HDR, LIB, GLUE_HDR]):
-        cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-I", os.path.join(os.path.dirname(_HERE), "include"),
+        # no contraction: the harness's host-side projections must round as the CPU twin's do
+        cmd = ["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-Wall", "-I", os.path.join(os.path.dirname(_HERE), "include"),
                "-I", os.path.join(os.path.dirname(_HERE), "shim"),
                "-o", CAPI_BIN, CAPI_SRC, "-L", _HERE, "-lorbfe", "-Wl,-rpath,$ORIGIN/../../orb_slam3_ros_amd",
                "-Wl,-rpath-link,/opt/rocm/lib"]
@@ -62,7 +63,9 @@ def build_tracking_cpu(force: bool = False, verbose: bool = False) -> str:
     tests/native/tracking_loop.h over the oracle's restatement (oracle/liborb_oracle.so, built first by
     oracle/Makefile). Only the CPU-baseline leg of bench.py and the tests run it."""
     if force or _stale(TRACK_CPU_BIN, [TRACK_CPU_SRC, TRACK_HDR, TRACK_KB8_HDR, ORACLE_LIB]):
-        cmd = ["g++", "-O3", "-march=x86-64-v3", "-std=c++17", "-Wall", "-pthread", "-I",
+        # -ffp-contract=off: -march=x86-64-v3 has FMA, and g++ would contract the host-side projections
+        # and pose arithmetic of tests/native/tracking_*.h differently from the GPU consumer's build
+        cmd = ["g++", "-O3", "-march=x86-64-v3", "-ffp-contract=off", "-std=c++17", "-Wall", "-pthread", "-I",
                os.path.join(os.path.dirname(_HERE), "include"), "-o", TRACK_CPU_BIN, TRACK_CPU_SRC, ORACLE_LIB,
                "-Wl,-rpath,$ORIGIN/../../oracle"]
         if verbose:
