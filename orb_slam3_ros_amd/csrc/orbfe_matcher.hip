@@ -703,7 +703,17 @@ struct BlkIO {
     int* st_host;              // pinned status words
     int seq;
     unsigned long long* stats;   // [3]: window candidates, Hamming pairs, passes (nullptr: off)
+    uint4* qdev;               // device copy of host-memory records for the re-enumerations (nullptr: records in HBM)
 };
+// Records in mapped host memory are read once over PCIe: the block copies them into HBM scratch
+// (before the frame staging, whose barriers publish it), and a list that runs out re-reads its record
+// from there instead of paying another PCIe round trip inside a pass.
+__device__ __forceinline__ const void* blk_qcopy(const BlkIO& io, const void* recs, int nq) {
+    if (!io.qdev) return recs;
+    const int nv = nq * io.q_stride / 16;
+    for (int i = threadIdx.x; i < nv; i += blockDim.x) io.qdev[i] = ((const uint4*)recs)[i];
+    return io.qdev;
+}
 // k_sbp_block's LDS index: buckets (octave, band of br rows, strip of sw columns), bucket
 // c = (octave * NB + band) * NS + strip (the strips of a band are consecutive, so a query's window is one
 // contiguous run per (octave, band)); be[c] .. be[c + 1] is bucket c's run of band positions.
@@ -776,9 +786,14 @@ __device__ __forceinline__ BlkQuery blk_load(const FrameDev& fr, const void* rec
 }
 // Q's candidates that pass every gate-independent test (box, octave range, stereo), f(key, idx):
 // key = dist << 40 | rank << 4 | octave (the reference's enumeration order breaks distance ties)
+// cbase: the first bucket of the camera searched (k_sbp_block2: nlev * NB * NS for the right grid);
+// nwin: when given, counts every keypoint of the window (GetFeaturesInArea's result, blocked or not).
+// MODE 3 = a two-camera frame's last-frame search (k_sbp_block2): MODE 1's gates without the stereo
+// test (ORBmatcher.cc:1747-1760 runs for Nleft == -1 only).
 template <int MODE, typename Fn>
 __device__ __forceinline__ void blk_enum(const BlkQuery& Q, const BlkGeom& gm, const float4* s_kp, const uint4* s_desc,
-                                         const int* s_be, const uint8_t* s_blk, Fn&& f) {
+                                         const int* s_be, const uint8_t* s_blk, Fn&& f, int cbase = 0,
+                                         int* nwin = nullptr) {
     if (!Q.ok || Q.olo > Q.ohi) return;
     // the buckets of (x -+ (r + 1), y -+ (r + 1)): a keypoint that passes the box test lies inside (one
     // pixel of margin is far beyond the rounding of the bounds); out-of-grid keypoints are in no bucket
@@ -786,7 +801,7 @@ __device__ __forceinline__ void blk_enum(const BlkQuery& Q, const BlkGeom& gm, c
     const int s0 = gm.strip(Q.x - Q.R - 1.f), s1 = gm.strip(Q.x + Q.R + 1.f);
     for (int o = Q.olo; o <= Q.ohi; o++)
     for (int b = b0; b <= b1; b++) {
-        const int c = (o * gm.NB + b) * gm.NS;
+        const int c = cbase + (o * gm.NB + b) * gm.NS;
         const int pe = s_be[c + s1 + 1];
         // four positions per step, their box reads issued together (a thread's run is a chain of
         // LDS round trips otherwise)
@@ -799,9 +814,10 @@ __device__ __forceinline__ void blk_enum(const BlkQuery& Q, const BlkGeom& gm, c
             const int p = p0 + u;
             const float4 k4 = kk[u];
             if (p >= pe || !(fabsf(k4.x - Q.x) < Q.R && fabsf(k4.y - Q.y) < Q.R)) continue;
+            if (nwin) ++*nwin;
             const int idx = (int)(__float_as_uint(k4.z) & 0x1FFFu);
             if (s_blk[idx]) continue;
-            if (MODE != 2 && k4.w > 0 && fabsf(Q.xr - k4.w) > Q.R) continue;
+            if (MODE != 2 && MODE != 3 && k4.w > 0 && fabsf(Q.xr - k4.w) > Q.R) continue;
             const uint4 d0 = s_desc[2 * p], d1 = s_desc[2 * p + 1];
             const int dist = __popc(Q.qd[0] ^ d0.x) + __popc(Q.qd[1] ^ d0.y) + __popc(Q.qd[2] ^ d0.z) +
                              __popc(Q.qd[3] ^ d0.w) + __popc(Q.qd[4] ^ d1.x) + __popc(Q.qd[5] ^ d1.y) +
@@ -834,11 +850,14 @@ __host__ __device__ __forceinline__ int blk_be_words(int nbk, int nt) {
 // keypoints {x, y, rank bits, uR} and descriptors by bucket position, blocked flags (and angles, the
 // first[] state, when given) by keypoint index. s_be: the 16-byte aligned bounds region
 // (blk_be_words). Ends with a barrier.
+// ncam = 2 (k_sbp_block2): a two-camera frame's right keypoints [nleft, n) in a second bucket set
+// after the left one (bucket + nlev * NB * NS); ncam = 1: its single-camera searches read the left
+// grid only.
 template <int NT>
 __device__ __forceinline__ void blk_stage(const FrameDev& fr, const BlkGeom& gm, const int32_t* mvp_in,
                                           const int32_t* obs_in, float4* s_kp, uint4* s_desc, int* s_be,
-                                          uint8_t* s_blk, float* s_ang, int* s_first, int* s_ws) {
-    const int n = fr.n, nlev = fr.nlevels, nbk = nlev * gm.NB * gm.NS, tid = threadIdx.x;
+                                          uint8_t* s_blk, float* s_ang, int* s_first, int* s_ws, int ncam = 1) {
+    const int n = fr.n, nlev = fr.nlevels, nbk = ncam * nlev * gm.NB * gm.NS, tid = threadIdx.x;
     const int per = ((nbk + NT - 1) / NT + 3) & ~3;   // buckets per thread in the scan (whole int4s)
     for (int b = tid; b < (per * NT + 4) / 4; b += NT) ((int4*)s_be)[b] = make_int4(0, 0, 0, 0);
     int* a = s_be + 4;   // counters, then starts, then ends
@@ -849,8 +868,9 @@ __device__ __forceinline__ void blk_stage(const FrameDev& fr, const BlkGeom& gm,
         const int px = (int)roundf((x - fr.minx) * fr.invw);
         const int py = (int)roundf((y - fr.miny) * fr.invh);
         const bool in_grid = !(px < 0 || px >= ORBFE_GRID_COLS || py < 0 || py >= ORBFE_GRID_ROWS);
-        return (in_grid && oct >= 0 && oct < nlev && (fr.nleft < 0 || idx < fr.nleft))
-                   ? (oct * gm.NB + gm.band(y)) * gm.NS + gm.strip(x) : -1;
+        const int cam = (fr.nleft >= 0 && idx >= fr.nleft) ? 1 : 0;
+        return (in_grid && oct >= 0 && oct < nlev && cam < ncam)
+                   ? ((cam * nlev + oct) * gm.NB + gm.band(y)) * gm.NS + gm.strip(x) : -1;
     };
     // every keypoint's data is read from memory ONCE, into registers (n <= 2 x NT), before the bucket
     // counts: one round trip for the whole staging (the fields, not the struct: a struct array
@@ -936,26 +956,27 @@ __device__ __forceinline__ void blk_stage(const FrameDev& fr, const BlkGeom& gm,
 }
 // A query's gate-independent candidates: the MT_BLK_LIST smallest keys, sorted, packed as
 // idx | octave << 13 | dist << 16 (0xFFFFFFFF: none); returns the candidate count
-template <int MODE>
+template <int MODE, int LEN = MT_BLK_LIST>
 __device__ __forceinline__ int blk_list(const BlkQuery& Q, const BlkGeom& gm, const float4* kp, const uint4* desc,
-                                        const int* be, const uint8_t* blk, uint32_t (&L)[MT_BLK_LIST]) {
-    unsigned long long K[MT_BLK_LIST];
+                                        const int* be, const uint8_t* blk, uint32_t (&L)[LEN], int cbase = 0,
+                                        int* nwin = nullptr) {
+    unsigned long long K[LEN];
 #pragma unroll
-    for (int k = 0; k < MT_BLK_LIST; k++) K[k] = ~0ull;
+    for (int k = 0; k < LEN; k++) K[k] = ~0ull;
     int c = 0;
     blk_enum<MODE>(Q, gm, kp, desc, be, blk, [&](unsigned long long key, int) {
         c++;
-        if (key >= K[MT_BLK_LIST - 1]) return;   // not among the 8 smallest so far (keys are unique)
+        if (key >= K[LEN - 1]) return;   // not among the LEN smallest so far (keys are unique)
 #pragma unroll
-        for (int k = 0; k < MT_BLK_LIST; k++) {   // sorted insertion (a compare-swap chain)
+        for (int k = 0; k < LEN; k++) {   // sorted insertion (a compare-swap chain)
             const bool lt = key < K[k];
             const unsigned long long t = K[k];
             K[k] = lt ? key : t;
             key = lt ? t : key;
         }
-    });
+    }, cbase, nwin);
 #pragma unroll
-    for (int k = 0; k < MT_BLK_LIST; k++)
+    for (int k = 0; k < LEN; k++)
         L[k] = K[k] == ~0ull ? 0xFFFFFFFFu
                              : (uint32_t)((K[k] >> 4) & 0x1FFFu) | (uint32_t)((K[k] & 15) << 13) |
                                    (uint32_t)((K[k] >> 40) << 16);
@@ -1007,6 +1028,7 @@ __global__ __launch_bounds__(MT_BLK_NT) void k_sbp_block(FrameDev fr, BlkGeom gm
     }
     if (tid < MT_HISTO) s_hist[tid] = 0;
     if (tid < 2) s_cnt[tid] = 0;
+    const void* rq = blk_qcopy(io, recs, nq);
     blk_stage<MT_BLK_NT>(fr, gm, io.mvp_in, io.obs_in, s_kp, s_desc, s_ber, s_blk, s_ang, s_first, s_ws);
 #pragma unroll
     for (int i = 0; i < MT_BLK_QPT; i++) {
@@ -1049,7 +1071,7 @@ __global__ __launch_bounds__(MT_BLK_NT) void k_sbp_block(FrameDev fr, BlkGeom gm
             int result;
             if (found < (MODE == 0 ? 2 : 1) && cnt[i] > MT_BLK_LIST) {
                 // the list ran out: the window again, with this pass's gates
-                const BlkQuery Q = blk_load<MODE>(fr, recs, q, th, a0, a1, thFar);
+                const BlkQuery Q = blk_load<MODE>(fr, rq, q, th, a0, a1, thFar);
                 unsigned long long k1 = ~0ull, k2 = ~0ull;
                 blk_enum<MODE>(Q, gm, s_kp, s_desc, s_be, s_blk, [&](unsigned long long key, int idx) {
                     if (fcur[idx] < q) return;
@@ -1152,6 +1174,237 @@ __global__ __launch_bounds__(MT_BLK_NT) void k_sbp_block(FrameDev fr, BlkGeom gm
         st[4] = io.seq;
         __threadfence_system();
     }
+}
+
+// SearchByProjection(CurrentFrame, LastFrame, th, bMono) for a two-camera frame (Nleft != -1,
+// ORBmatcher.cc:1695-1858) in ONE workgroup, k_sbp_block's design with two entries per point: entry
+// 2 q = the best left keypoint of point q's window (left grid), entry 2 q + 1 = the best right keypoint
+// around the caller's right-camera projection right_uv[q] (right grid), searched only when the left
+// window holds any keypoint (:1740-1741, blocked ones included). Both cameras' keypoints are staged in
+// LDS (two bucket sets); an entry's gate is first[k] < entry (the slot was written by an earlier entry
+// of a point with Observations() > 0: such a write is never overwritten, so the earliest one is the
+// one that blocks). Each entry keeps its MT_BLK2_LIST smallest gate-independent keys in registers;
+// the fixed point, the last-writer commit and the rotation histogram over all entries
+// (:1860-1884) run in the block as in k_sbp_block<1>. Up to MT_BLOCK_MAXQ points: two per thread,
+// four entries.
+#define MT_BLK2_LIST 8
+#ifdef ORBFE_BLK2_STAMPS   // diagnostic build (tools/build_variant.sh): phase times of thread 0, printed
+#define BLK2_STAMP(k) do { if (threadIdx.x == 0) t_st[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define BLK2_STAMP(k) do { } while (0)
+#endif
+__global__ __launch_bounds__(MT_BLK_NT) void k_sbp_block2(FrameDev fr, BlkGeom gm, const orbfe_proj_point* recs,
+                                                          const float2* right_uv, int nq, float th, int a0, int a1,
+                                                          int maxDist, BlkIO io) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t mt_sm[];
+    const int n = fr.n;
+    const int nbk1 = fr.nlevels * gm.NB * gm.NS;   // buckets of one camera
+    float4* s_kp = (float4*)mt_sm;
+    uint4* s_desc = (uint4*)(s_kp + n);
+    int* s_ber = (int*)(s_desc + 2 * n);
+    const int* s_be = s_ber + 3;
+    int* s_first = s_ber + blk_be_words(2 * nbk1, MT_BLK_NT);
+    float* s_ang = (float*)(s_first + 2 * n);
+    uint8_t* s_blk = (uint8_t*)(s_ang + n);
+    __shared__ int s_flag, s_ws[MT_BLK_NT / 64], s_hist[MT_HISTO], s_cnt[2];
+    __shared__ unsigned s_keep;
+    const int tid = threadIdx.x;
+#ifdef ORBFE_BLK2_STAMPS
+    unsigned long long t_st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+    BLK2_STAMP(0);
+    constexpr int QPT = MT_BLK_QPT, EPT = 2 * MT_BLK_QPT;   // points / entries per thread (entry j: point j / 2, side j & 1)
+    uint32_t L[EPT][MT_BLK2_LIST];
+    int cnt[EPT], res[EPT];
+    int obs[QPT], qid[QPT];
+    float qang[QPT];
+    unsigned long long npair = 0;
+    BlkQuery QS[QPT];
+    float2 uv[QPT];
+#pragma unroll
+    for (int i = 0; i < QPT; i++) {
+        qid[i] = -1;
+        qang[i] = 0.f;
+        uv[i] = make_float2(0.f, 0.f);
+        QS[i].ok = false;
+        QS[i].obs = 0;
+        const int q = tid + i * MT_BLK_NT;
+        if (q >= nq) continue;
+        uv[i] = right_uv[q];
+    }
+    if (tid < MT_HISTO) s_hist[tid] = 0;
+    if (tid < 2) s_cnt[tid] = 0;
+    BLK2_STAMP(1);
+    // the records cross PCIe once, into HBM (their loads in flight during the staging); the points'
+    // windows are read from that copy after the staging's barriers
+    const orbfe_proj_point* rq = (const orbfe_proj_point*)blk_qcopy(io, recs, nq);
+    blk_stage<MT_BLK_NT>(fr, gm, io.mvp_in, io.obs_in, s_kp, s_desc, s_ber, s_blk, s_ang, s_first, s_ws, 2);
+    BLK2_STAMP(2);
+#pragma unroll
+    for (int i = 0; i < QPT; i++) {
+        const int q = tid + i * MT_BLK_NT;
+        if (q >= nq) continue;
+        const uint8_t* rec = (const uint8_t*)rq + (size_t)q * io.q_stride;
+        qid[i] = *(const int*)(rec + io.qid_off);
+        if (io.checkOri) qang[i] = *(const float*)(rec + io.qangle_off);
+        QS[i] = blk_load<1>(fr, rq, q, th, a0, a1, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < QPT; i++) {
+        const int q = tid + i * MT_BLK_NT;
+        obs[i] = QS[i].obs;
+#pragma unroll
+        for (int sd = 0; sd < 2; sd++) {
+            cnt[2 * i + sd] = 0;
+#pragma unroll
+            for (int k = 0; k < MT_BLK2_LIST; k++) L[2 * i + sd][k] = 0xFFFFFFFFu;
+        }
+        if (q >= nq) continue;
+        int nwin = 0;
+        cnt[2 * i] = blk_list<3, MT_BLK2_LIST>(QS[i], gm, s_kp, s_desc, s_be, s_blk, L[2 * i], 0, &nwin);
+        if (nwin > 0) {   // the right camera only after a non-empty left window
+            BlkQuery QR = QS[i];
+            QR.x = uv[i].x;
+            QR.y = uv[i].y;
+            cnt[2 * i + 1] = blk_list<3, MT_BLK2_LIST>(QR, gm, s_kp, s_desc, s_be, s_blk, L[2 * i + 1], nbk1);
+        }
+        npair += (unsigned)(cnt[2 * i] + cnt[2 * i + 1]);
+    }
+#pragma unroll
+    for (int j = 0; j < EPT; j++) res[j] = -1;
+    SYNC();
+    BLK2_STAMP(3);
+    int pass = 0;
+    for (;; pass++) {
+        const int* fcur = s_first + (pass & 1) * n;
+        int* fnext = s_first + ((pass + 1) & 1) * n;
+        for (int k = tid; k < n; k += MT_BLK_NT) fnext[k] = MT_INF;
+        if (tid == 0) s_flag = 0;
+        SYNC();
+        bool ch = false;
+#pragma unroll
+        for (int j = 0; j < EPT; j++) {
+            const int i = j >> 1, sd = j & 1;
+            const int q = tid + i * MT_BLK_NT;
+            if (q >= nq) continue;
+            const int e = 2 * q + sd;
+            // the first list entry no earlier entry holds (the gate reads issued together)
+            bool free_[MT_BLK2_LIST];
+#pragma unroll
+            for (int k = 0; k < MT_BLK2_LIST; k++)
+                free_[k] = L[j][k] != 0xFFFFFFFFu && fcur[L[j][k] & 0x1FFFu] >= e;
+            uint32_t e1 = 0xFFFFFFFFu;
+#pragma unroll
+            for (int k = MT_BLK2_LIST - 1; k >= 0; k--)
+                if (free_[k]) e1 = L[j][k];
+            int result;
+            if (e1 == 0xFFFFFFFFu && cnt[j] > MT_BLK2_LIST) {
+                // the list ran out: the window again, with this pass's gates (the smallest key = the
+                // first strict minimum in GetFeaturesInArea order)
+                BlkQuery Q = blk_load<1>(fr, rq, q, th, a0, a1, 0.f);
+                if (sd) {
+                    const float2 u = right_uv[q];
+                    Q.x = u.x;
+                    Q.y = u.y;
+                }
+                unsigned long long k1 = ~0ull;
+                blk_enum<3>(Q, gm, s_kp, s_desc, s_be, s_blk, [&](unsigned long long key, int idx) {
+                    if (fcur[idx] < e) return;
+                    k1 = key < k1 ? key : k1;
+                }, sd ? nbk1 : 0);
+                result = blk_accept<1>(k1 != ~0ull ? (int)((k1 >> 4) & 0x1FFFu) : -1, (int)(k1 >> 40), 0, 256, -1,
+                                       0.f, maxDist);
+            } else {
+                result = blk_accept<1>(e1 != 0xFFFFFFFFu ? (int)(e1 & 0x1FFFu) : -1, (int)(e1 >> 16), 0, 256, -1, 0.f,
+                                       maxDist);
+            }
+            if (result >= 0 && obs[i] > 0) atomicMin(&fnext[result], e);
+            if (result != res[j]) {
+                res[j] = result;
+                ch = true;
+            }
+        }
+        if (__ballot(ch) && (tid & 63) == 0) s_flag = 1;
+        SYNC();
+        if (s_flag == 0 || pass > 2 * nq) break;
+    }
+    BLK2_STAMP(4);
+    // ---- the commit: the last entry writing a slot wins, every assignment enters the rotation
+    // histogram, the dropped bins clear their slots and count once per entry ----
+    int* s_res = s_first;
+    for (int k = tid; k < n; k += MT_BLK_NT) s_res[k] = -1;
+    SYNC();
+    int nas = 0;
+    int bins[EPT];
+#pragma unroll
+    for (int j = 0; j < EPT; j++) {
+        const int i = j >> 1, q = tid + i * MT_BLK_NT;
+        bins[j] = -1;
+        if (q >= nq || res[j] < 0) continue;
+        atomicMax(&s_res[res[j]], 2 * q + (j & 1));
+        nas++;
+        if (io.checkOri) bins[j] = mt_rot_bin(qang[i], s_ang[res[j]]);
+    }
+    nas = wave_sum_dpp(nas);
+    if ((tid & 63) == 0 && nas) atomicAdd(&s_cnt[0], nas);
+    if (io.checkOri) {
+#pragma unroll
+        for (int j = 0; j < EPT; j++) {
+            int b = bins[j];
+            for (unsigned long long act = __ballot(b >= 0); act; act = __ballot(b >= 0)) {
+                const int lead = __builtin_amdgcn_readlane(b, (int)__builtin_ctzll(act));
+                const unsigned long long same = __ballot(b == lead);
+                if ((tid & 63) == (int)__builtin_ctzll(same)) atomicAdd(&s_hist[lead], (int)__popcll(same));
+                if (b == lead) b = -1;
+            }
+        }
+    }
+    SYNC();
+    if (tid == 0) s_keep = io.checkOri ? mt_three_maxima_keep(s_hist) : 0xFFFFFFFFu;
+    SYNC();
+    int ndrop = 0;
+#pragma unroll
+    for (int j = 0; j < EPT; j++) {
+        const int q = tid + (j >> 1) * MT_BLK_NT;
+        if (q >= nq || res[j] < 0 || bins[j] < 0 || ((s_keep >> bins[j]) & 1u)) continue;
+        s_res[res[j]] = -2;
+        io.mvp_out[res[j]] = -1;
+        ndrop++;
+    }
+    ndrop = wave_sum_dpp(ndrop);
+    if ((tid & 63) == 0 && ndrop) atomicAdd(&s_cnt[1], ndrop);
+    SYNC();
+#pragma unroll
+    for (int j = 0; j < EPT; j++) {
+        const int i = j >> 1, q = tid + i * MT_BLK_NT;
+        if (q < nq && res[j] >= 0 && s_res[res[j]] == 2 * q + (j & 1)) io.mvp_out[res[j]] = qid[i];
+    }
+    if (io.stats && npair) {
+        atomicAdd(&io.stats[0], npair);
+        atomicAdd(&io.stats[1], npair);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    SYNC();
+    if (tid == 0) {
+        __threadfence_system();
+        if (io.stats) io.stats[2] = (unsigned long long)(pass + 1);
+        volatile int* st = io.st_host;
+        st[0] = 0;
+        st[1] = s_cnt[0];
+        st[2] = s_cnt[1];
+        st[3] = pass + 1;
+        st[5] = 0;
+        __threadfence_system();
+        st[4] = io.seq;
+        __threadfence_system();
+    }
+#ifdef ORBFE_BLK2_STAMPS
+    BLK2_STAMP(5);
+    if (tid == 0)   // s_memrealtime ticks at 100 MHz
+        printf("blk2 nq %d n %d passes %d  load %.1f stage %.1f lists %.1f passes %.1f commit %.1f us\n", nq, n, pass + 1,
+               (t_st[1] - t_st[0]) * 0.01, (t_st[2] - t_st[1]) * 0.01, (t_st[3] - t_st[2]) * 0.01,
+               (t_st[4] - t_st[3]) * 0.01, (t_st[5] - t_st[4]) * 0.01);
+#endif
 }
 
 // ---- Large single-camera local-map searches (nq > MT_BLOCK_MAXQ, frame in LDS): k_sbp_block's design
@@ -2512,21 +2765,22 @@ struct DevIn {
 
 // k_sbp_block's bucket geometry for a frame: bands of 16 rows, then as many column strips (<= 32, >= 24
 // columns wide) as 8192 buckets and the LDS allow; false: the frame does not fit the block form
-size_t blk_lds(int n, int nlev, const BlkGeom& gm) {
-    return (size_t)n * 61 + (size_t)blk_be_words(nlev * gm.NB * gm.NS, MT_BLK_NT) * 4 + 16;
+// (ncam = 2: both cameras' bucket sets, k_sbp_block2)
+size_t blk_lds(int n, int nlev, const BlkGeom& gm, int ncam = 1) {
+    return (size_t)n * 61 + (size_t)blk_be_words(ncam * nlev * gm.NB * gm.NS, MT_BLK_NT) * 4 + 16;
 }
-bool blk_geom(const orbfe_frame* F, BlkGeom& gm) {
+bool blk_geom(const orbfe_frame* F, BlkGeom& gm, int ncam = 1) {
     constexpr int BR = 16;
     if (!(F->max_y > 0.f && F->max_y < 65536.f && F->max_x > 0.f && F->max_x < 65536.f)) return false;
     gm.NB = (int)std::floor(F->max_y / BR) + 2;
     gm.inv_br = 1.0f / BR;
-    const int lev_bands = F->nlevels * gm.NB;
+    const int lev_bands = ncam * F->nlevels * gm.NB;
     const long budget = std::min<long>(8192, ((long)MT_LDS_MAX - 61L * F->n - 4) / 4);
     gm.NS = (int)std::min<long>(std::min<long>(32, budget / std::max(lev_bands, 1)), (long)std::ceil(F->max_x / 24.f));
     if (gm.NS < 1) return false;
-    while (gm.NS > 1 && blk_lds(F->n, F->nlevels, gm) > MT_LDS_MAX) gm.NS--;   // the scan's padding
+    while (gm.NS > 1 && blk_lds(F->n, F->nlevels, gm, ncam) > MT_LDS_MAX) gm.NS--;   // the scan's padding
     gm.inv_sw = (float)gm.NS / (F->max_x + 1.f);
-    return blk_lds(F->n, F->nlevels, gm) <= MT_LDS_MAX;
+    return blk_lds(F->n, F->nlevels, gm, ncam) <= MT_LDS_MAX;
 }
 
 // sbp_run's one-launch form (k_sbp_block): arguments already validated by sbp_run.
@@ -2545,6 +2799,7 @@ int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* m
     const size_t o_track = fin ? p.scratch((size_t)nq * sizeof(orbfe_map_point)) : 0;
     const size_t o_ntm = fin ? p.scratch(16) : 0;
     const size_t o_stats = t_stats ? p.scratch(24) : 0;
+    const size_t o_qdev = (!dev && !fin) ? p.scratch((size_t)nq * qstride) : 0;
     // host-API calls: zero copy both ways. The kernel reads its inputs straight from the mapped pinned
     // staging and writes the slots into mapped pinned memory; the host waits for the status words
     // only (no DMA, no stream synchronisation: the call is one launch).
@@ -2589,7 +2844,7 @@ int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* m
     const int seq = ++t_ms.seq;
     if (zc) memcpy(m.ho, mvp, (size_t)n * 4);   // the slots the search leaves alone keep their value
     const BlkIO io{mvp_in, obs_d, mvp_out, (int)qstride, (int)qid_off, (int)qangle_off, checkOri, ntm, t_ms.hs_dev, seq,
-                   stats};
+                   stats, (!dev && !fin) ? ms_ptr<uint4>(o_qdev) : nullptr};
     const size_t lds = blk_lds(n, F->nlevels, gm);
     if (mode == 0)
         hipLaunchKernelGGL(k_sbp_block<0>, dim3(1), dim3(MT_BLK_NT), lds, s, fr, gm, (const void*)q, nq, th, a0, a1,
@@ -2618,6 +2873,73 @@ int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* m
     if (zc) memcpy(mvp, m.ho, (size_t)n * 4);   // complete: the status words come after the slot writes
     if (fin && fin->n_to_match) *fin->n_to_match = st[5];
     if (stats) {   // counting mode only: one more copy and synchronisation
+        unsigned long long hst[3];
+        HIPCHK(hipMemcpyAsync(hst, stats, 24, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        t_last_stats[0] = (long long)hst[0];
+        t_last_stats[1] = (long long)hst[1];
+        t_last_stats[2] = (long long)hst[2];
+    }
+    return st[1] - st[2];
+}
+
+// sbp_run's one-launch form for a two-camera frame's last-frame search (k_sbp_block2): host buffers
+// read in place from the mapped pinned staging, slots written to mapped pinned memory, the status
+// words awaited (as sbp_block_run); arguments already validated by sbp_run.
+int sbp_block2_run(const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, const orbfe_proj_point* pts,
+                   const float* right_uv, int nq, float th, int a0, int a1, int maxDist, int checkOri,
+                   const BlkGeom& gm) {
+    const int n = F->n;
+    Plan p;
+    FramePlan fp;
+    fp.plan(p, F, true, false);
+    const size_t o_q = p.upload(pts, (size_t)nq * sizeof(orbfe_proj_point));
+    const size_t o_ruv = p.upload(right_uv, (size_t)nq * 8);
+    const size_t o_mvp = p.upload(mvp, (size_t)n * 4);
+    const size_t o_obs = p.upload(mvp_obs, (size_t)n * 4);
+    const size_t o_stats = t_stats ? p.scratch(24) : 0;
+    const size_t o_qdev = p.scratch((size_t)nq * sizeof(orbfe_proj_point));
+    int rc = ms_prepare(p, true);
+    if (rc) return rc;
+    MatchScratch& m = t_ms;
+    if (m.ocap < (size_t)n) {
+        if (m.ho) HIPCHK(hipHostFree(m.ho));
+        m.ho = nullptr;
+        m.ocap = 0;
+        const size_t cap = std::max<size_t>((size_t)n, 2048);
+        HIPCHK(hipHostMalloc((void**)&m.ho, cap * 4, hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostGetDevicePointer((void**)&m.ho_dev, m.ho, 0));
+        m.ocap = cap;
+    }
+    fp.zc = true;
+    hipStream_t s = t_ms.stream;
+    unsigned long long* stats = t_stats ? ms_ptr<unsigned long long>(o_stats) : nullptr;
+    t_last_stats[0] = t_last_stats[1] = t_last_stats[2] = -1;
+    if (stats) HIPCHK(hipMemsetAsync(stats, 0, 24, s));
+    MsTimer timer(s);
+    const FrameDev fr = fp.view();
+    const int seq = ++t_ms.seq;
+    memcpy(m.ho, mvp, (size_t)n * 4);   // the slots the search leaves alone keep their value
+    const BlkIO io{up_ptr<const int32_t>(o_mvp, true), up_ptr<const int32_t>(o_obs, true), m.ho_dev,
+                   (int)sizeof(orbfe_proj_point), (int)offsetof(orbfe_proj_point, id),
+                   (int)offsetof(orbfe_proj_point, angle), checkOri, nullptr, t_ms.hs_dev, seq, stats,
+                   ms_ptr<uint4>(o_qdev)};
+    hipLaunchKernelGGL(k_sbp_block2, dim3(1), dim3(MT_BLK_NT), blk_lds(n, F->nlevels, gm, 2), s, fr, gm,
+                       up_ptr<const orbfe_proj_point>(o_q, true), up_ptr<const float2>(o_ruv, true), nq, th, a0, a1,
+                       maxDist, io);
+    HIPCHK(hipGetLastError());
+    timer.end();
+    volatile int* st = t_ms.hs;
+    for (unsigned spin = 1; host_seq_acquire(st) != seq; spin++) {
+        if ((spin & 1023) == 0) {   // bounded: a stream that finished without publishing is an error
+            const hipError_t e = hipStreamQuery(s);
+            if (e == hipSuccess && host_seq_acquire(st) != seq) return ORBFE_E_DEVICE;
+            if (e != hipSuccess && e != hipErrorNotReady) HIPCHK(e);
+        }
+        __builtin_ia32_pause();
+    }
+    memcpy(mvp, m.ho, (size_t)n * 4);
+    if (stats) {
         unsigned long long hst[3];
         HIPCHK(hipMemcpyAsync(hst, stats, 24, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
@@ -2855,6 +3177,11 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
         if (mode == 0 && th < MT_MULTI_TH)
             return sbp_multi_run(F, mvp, mvp_obs, queries, nq, qstride, qid_off, th, a0, thFar, nnratio, gm, fin, dev);
     }
+    // a two-camera frame's last-frame search (the per-frame Tracking call of a KannalaBrandt8 rig) in
+    // one workgroup as well: both cameras' keypoints in LDS, two entries per point
+    if (two && mode == 1 && !dev && n <= MT_BAND_MAXN && nq <= MT_BLOCK_MAXQ && blk_geom(F, gm, 2))
+        return sbp_block2_run(F, mvp, mvp_obs, (const orbfe_proj_point*)queries, right_uv, nq, th, a0, a1, maxDist,
+                              checkOri, gm);
     std::vector<int32_t> blocked0(dev ? 0 : n);
     for (int k = 0; !dev && k < n; k++) blocked0[k] = mode == 2 ? (mvp[k] >= 0) : (mvp[k] >= 0 && mvp_obs[k] > 0);
     Plan p;

@@ -402,6 +402,29 @@ def test_sbp_lastframe_two_cams(gpu, om, seed, mode, check_ori):
         np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("nl,nr,npts,copy_frac", [
+    (1000, 900, 1500, 0.8),    # the one-workgroup path (k_sbp_block2): n <= 2048, <= 2048 points
+    (1024, 1024, 2048, 0.8),   # its limits
+    (300, 280, 2000, 0.97),    # ~7 points per keypoint: entry lists (4 keys) run out, re-enumeration
+    (1100, 1000, 2049, 0.8),   # one point past the block form: the multi-launch passes
+    (1030, 1019, 1200, 0.8),   # one keypoint past it
+])
+def test_sbp_lastframe_two_cams_block(gpu, om, nl, nr, npts, copy_frac):
+    """SearchByProjection(CurrentFrame, LastFrame) for a two-camera frame through the one-workgroup
+    search (k_sbp_block2) and across its size limits, against the oracle's literal loop
+    (ORBmatcher.cc:1695-1884): th 7 / 15, checkOri on and off, all three level filters."""
+    rng = np.random.default_rng(nl + nr + npts)
+    F = sm.synth_frame_two(rng, nl, nr)
+    pts, ruv = sm.synth_proj_points_two(rng, F, npts, copy_frac=copy_frac)
+    mvp0, obs = sm.initial_slots(rng, F.N, 0.2)
+    for th, check_ori, fw, bw in [(7, True, False, False), (15, False, True, False), (7, True, False, True)]:
+        a, b = mvp0.copy(), mvp0.copy()
+        ng = ORBmatcher(0.9, check_ori).SearchByProjectionLastFrameStereo(F, a, obs, pts, ruv, th, fw, bw)
+        no = om.OracleMatcher(0.9, check_ori).sbp_lastframe_stereo(F, b, obs, pts, ruv, th, fw, bw)
+        assert ng == no and no > 0, (th, ng, no)
+        np.testing.assert_array_equal(a, b)
+
+
 def test_sbp_two_cams_keyframe_left_grid(gpu, om):
     """SearchByProjection(CurrentFrame, pKF) has no right-camera branch: a two-camera frame is
     searched through its left grid only (GetFeaturesInArea's default bRight = false)."""
