@@ -789,7 +789,9 @@ __device__ __forceinline__ BlkQuery blk_load(const FrameDev& fr, const void* rec
 // cbase: the first bucket of the camera searched (k_sbp_block2: nlev * NB * NS for the right grid);
 // nwin: when given, counts every keypoint of the window (GetFeaturesInArea's result, blocked or not).
 // MODE 3 = a two-camera frame's last-frame search (k_sbp_block2): MODE 1's gates without the stereo
-// test (ORBmatcher.cc:1747-1760 runs for Nleft == -1 only).
+// test (ORBmatcher.cc:1747-1760 runs for Nleft == -1 only). MODE 4 = a two-camera frame's local-map
+// search (k_sbp_block4): no stereo test, and a slot held before the search is NOT skipped here (an
+// earlier point's unguarded partner write can replace its holder: the pass gates decide).
 template <int MODE, typename Fn>
 __device__ __forceinline__ void blk_enum(const BlkQuery& Q, const BlkGeom& gm, const float4* s_kp, const uint4* s_desc,
                                          const int* s_be, const uint8_t* s_blk, Fn&& f, int cbase = 0,
@@ -816,8 +818,8 @@ __device__ __forceinline__ void blk_enum(const BlkQuery& Q, const BlkGeom& gm, c
             if (p >= pe || !(fabsf(k4.x - Q.x) < Q.R && fabsf(k4.y - Q.y) < Q.R)) continue;
             if (nwin) ++*nwin;
             const int idx = (int)(__float_as_uint(k4.z) & 0x1FFFu);
-            if (s_blk[idx]) continue;
-            if (MODE != 2 && MODE != 3 && k4.w > 0 && fabsf(Q.xr - k4.w) > Q.R) continue;
+            if (MODE != 4 && s_blk[idx]) continue;
+            if (MODE < 2 && k4.w > 0 && fabsf(Q.xr - k4.w) > Q.R) continue;
             const uint4 d0 = s_desc[2 * p], d1 = s_desc[2 * p + 1];
             const int dist = __popc(Q.qd[0] ^ d0.x) + __popc(Q.qd[1] ^ d0.y) + __popc(Q.qd[2] ^ d0.z) +
                              __popc(Q.qd[3] ^ d0.w) + __popc(Q.qd[4] ^ d1.x) + __popc(Q.qd[5] ^ d1.y) +
@@ -1405,6 +1407,241 @@ __global__ __launch_bounds__(MT_BLK_NT) void k_sbp_block2(FrameDev fr, BlkGeom g
                (t_st[1] - t_st[0]) * 0.01, (t_st[2] - t_st[1]) * 0.01, (t_st[3] - t_st[2]) * 0.01,
                (t_st[4] - t_st[3]) * 0.01, (t_st[5] - t_st[4]) * 0.01);
 #endif
+}
+
+// SearchByProjection(F, vpMapPoints, th, bFarPoints, thFarPoints) for a two-camera frame (Nleft != -1,
+// ORBmatcher.cc:43-213; the per-frame SearchLocalPoints call of a KannalaBrandt8 rig) in ONE
+// workgroup. Point q writes up to four slots in the reference's order: entry 4 q = the left best,
+// 4 q + 1 = its right partner (mvLeftToRightMatch, written without a check), 4 q + 2 = the right best's
+// left partner (mvRightToLeftMatch), 4 q + 3 = the right best; a failed left ratio test skips the right
+// search (:124-125). A keypoint is taken for point q when the LAST write to its slot before entry 4 q
+// holds a point with Observations() > 0 (no write: the slot's holder before the search); the right
+// search sees the point's own partner write as the latest (:158-160). Partner writes are unguarded, so a
+// slot's writers are kept per pass: every slot's writer entries (<= MT_B4_WCAP, tagged with their
+// point's Observations() > 0) in LDS, rebuilt from the previous pass's results at the start of each
+// pass; more writers than that abort the search (status 2) and the caller runs the multi-launch form.
+// Each search keeps its MT_BLK_LIST smallest gate-independent keys; the last writer of each slot wins
+// (no rotation check in this search), nmatches counts every write (:130-137,196-204).
+#define MT_B4_WCAP 6
+#define MT_B4_LIST 4   // keys kept per search (registers: two searches per point, two points per thread)
+__host__ __device__ constexpr int blk4_bytes_per_kp() { return 16 + 32 + 4 + 2 * MT_B4_WCAP + 2 + 1; }
+__device__ __forceinline__ bool b4_taken(const uint16_t* wl, const int* wcnt, const uint8_t* blk0, int k, int e) {
+    const int c = min(wcnt[k], MT_B4_WCAP);
+    int last = -1;
+    for (int j = 0; j < c; j++) {
+        const int w = wl[k * MT_B4_WCAP + j];
+        if ((w >> 1) < e && w > last) last = w;
+    }
+    return last < 0 ? blk0[k] != 0 : (last & 1) != 0;
+}
+// the right-camera search of a point (its record's IN_VIEW_R fields, radius not scaled by th)
+__device__ __forceinline__ BlkQuery b4_right(const FrameDev& fr, const orbfe_map_point& mp, int bFar, float thFar) {
+    BlkQuery Q;
+    Q.x = Q.y = Q.R = Q.xr = 0.f;
+    Q.olo = 0;
+    Q.ohi = -1;
+    Q.obs = mp.observations;
+    const int lvl = mp.scale_level_r;
+    Q.ok = (mp.flags & ORBFE_MP_IN_VIEW_R) && !(bFar && mp.depth > thFar) && !(mp.flags & ORBFE_MP_BAD) &&
+           lvl != -1 && lvl >= 0 && lvl < fr.nlevels;
+    if (Q.ok) {
+        Q.R = (mp.view_cos_r > 0.998 ? 2.5f : 4.0f) * fr.scale[lvl];   // RadiusByViewingCos, :143-147
+        Q.x = mp.proj_xr;
+        Q.y = mp.proj_yr;
+        Q.olo = max(lvl - 1, 0);
+        Q.ohi = lvl;
+        memcpy(Q.qd, mp.desc, 32);
+    }
+    return Q;
+}
+__global__ __launch_bounds__(MT_BLK_NT) void k_sbp_block4(FrameDev fr, BlkGeom gm, const orbfe_map_point* recs, int nq,
+                                                          float th, int bFar, float thFar, float nnratio, BlkIO io) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t mt_sm[];
+    const int n = fr.n, nl = fr.nleft;
+    const int nbk1 = fr.nlevels * gm.NB * gm.NS;
+    float4* s_kp = (float4*)mt_sm;
+    uint4* s_desc = (uint4*)(s_kp + n);
+    int* s_ber = (int*)(s_desc + 2 * n);
+    const int* s_be = s_ber + 3;
+    int* s_wcnt = s_ber + blk_be_words(2 * nbk1, MT_BLK_NT);                  // writers per slot (this pass)
+    uint16_t* s_wl = (uint16_t*)(s_wcnt + n);                                  // their entries << 1 | Observations() > 0
+    int16_t* s_link = (int16_t*)(s_wl + (size_t)MT_B4_WCAP * n);              // l2r (left) / r2l (right) partner
+    uint8_t* s_blk = (uint8_t*)(s_link + n);                                   // held before the search
+    __shared__ int s_flag, s_ovf, s_ws[MT_BLK_NT / 64], s_cnt;
+    const int tid = threadIdx.x;
+    constexpr int QPT = MT_BLK_QPT;
+    uint32_t L[2 * QPT][MT_B4_LIST];   // [2 i]: point i's left list, [2 i + 1]: its right list
+    int cnt[2 * QPT], res[QPT][4];
+    int obs[QPT];
+    bool gl[QPT], gr[QPT];              // the left / right search runs (record flags)
+    unsigned long long npair = 0;
+    if (tid == 0) { s_cnt = 0; s_ovf = 0; }
+    const orbfe_map_point* rq = (const orbfe_map_point*)blk_qcopy(io, recs, nq);
+    blk_stage<MT_BLK_NT>(fr, gm, io.mvp_in, io.obs_in, s_kp, s_desc, s_ber, s_blk, nullptr, nullptr, s_ws, 2);
+    for (int k = tid; k < n; k += MT_BLK_NT) {
+        int p = k < nl ? fr.l2r[k] : fr.r2l[k - nl];
+        if (k < nl ? !(p >= 0 && nl + p < n) : !(p >= 0 && p < nl)) p = -1;   // range-guarded links
+        s_link[k] = (int16_t)(p < 0 ? -1 : (k < nl ? nl + p : p));
+    }
+#pragma unroll
+    for (int i = 0; i < QPT; i++) {
+        const int q = tid + i * MT_BLK_NT;
+        obs[i] = 0;
+        gl[i] = gr[i] = false;
+#pragma unroll
+        for (int b = 0; b < 4; b++) res[i][b] = -1;
+#pragma unroll
+        for (int sd = 0; sd < 2; sd++) {
+            cnt[2 * i + sd] = 0;
+#pragma unroll
+            for (int k = 0; k < MT_B4_LIST; k++) L[2 * i + sd][k] = 0xFFFFFFFFu;
+        }
+        if (q >= nq) continue;
+        const orbfe_map_point& mp = rq[q];
+        obs[i] = mp.observations;
+        const BlkQuery QL = blk_load<0>(fr, rq, q, th, bFar, 0, thFar);   // mbTrackInView, th-scaled radius
+        const BlkQuery QR = b4_right(fr, mp, bFar, thFar);
+        gl[i] = QL.ok;
+        gr[i] = QR.ok;
+        cnt[2 * i] = blk_list<4, MT_B4_LIST>(QL, gm, s_kp, s_desc, s_be, s_blk, L[2 * i]);
+        cnt[2 * i + 1] = blk_list<4, MT_B4_LIST>(QR, gm, s_kp, s_desc, s_be, s_blk, L[2 * i + 1], nbk1);
+        npair += (unsigned)(cnt[2 * i] + cnt[2 * i + 1]);
+    }
+    int pass = 0;
+    for (;; pass++) {
+        // the slots' writers, from the previous pass's results (none in pass 0)
+        for (int k = tid; k < n; k += MT_BLK_NT) s_wcnt[k] = 0;
+        if (tid == 0) s_flag = 0;
+        SYNC();
+        bool ovf = false;
+#pragma unroll
+        for (int i = 0; i < QPT; i++) {
+            const int q = tid + i * MT_BLK_NT;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const int k = res[i][b];
+                if (k < 0) continue;
+                const int pos = atomicAdd(&s_wcnt[k], 1);
+                if (pos < MT_B4_WCAP) s_wl[k * MT_B4_WCAP + pos] = (uint16_t)(((4 * q + b) << 1) | (obs[i] > 0 ? 1 : 0));
+                else ovf = true;
+            }
+        }
+        if (__ballot(ovf) && (tid & 63) == 0) s_ovf = 1;
+        SYNC();
+        if (s_ovf) break;
+        bool ch = false;
+#pragma unroll
+        for (int i = 0; i < QPT; i++) {
+            const int q = tid + i * MT_BLK_NT;
+            if (q >= nq) continue;
+            const int e0 = 4 * q;
+            int r[4] = {-1, -1, -1, -1};
+            bool go = true;
+#pragma unroll
+            for (int sd = 0; sd < 2; sd++) {
+                const int j = 2 * i + sd;
+                if (!(sd ? (go && gr[i]) : gl[i])) continue;
+                const int own = r[1];   // the right search sees this point's own partner write
+                auto taken = [&](int k) {
+                    return (sd && k == own) ? obs[i] > 0 : b4_taken(s_wl, s_wcnt, s_blk, k, e0);
+                };
+                bool free_[MT_B4_LIST];
+#pragma unroll
+                for (int k = 0; k < MT_B4_LIST; k++) free_[k] = L[j][k] != 0xFFFFFFFFu && !taken((int)(L[j][k] & 0x1FFFu));
+                uint32_t e1 = 0xFFFFFFFFu, e2 = 0xFFFFFFFFu;
+                int found = 0;
+#pragma unroll
+                for (int k = 0; k < MT_B4_LIST; k++) {
+                    if (!free_[k] || found >= 2) continue;
+                    if (found == 0) e1 = L[j][k];
+                    else e2 = L[j][k];
+                    found++;
+                }
+                int bi = -1, bd = 256, bl = -1, bd2 = 256, bl2 = -1;
+                if (found < 2 && cnt[j] > MT_B4_LIST) {
+                    // the list ran out: the window again, with this pass's gates
+                    const BlkQuery Q = sd ? b4_right(fr, rq[q], bFar, thFar) : blk_load<0>(fr, rq, q, th, bFar, 0, thFar);
+                    unsigned long long k1 = ~0ull, k2 = ~0ull;
+                    blk_enum<4>(Q, gm, s_kp, s_desc, s_be, s_blk, [&](unsigned long long key, int idx) {
+                        if (taken(idx)) return;
+                        const bool lt1 = key < k1, lt2 = key < k2;
+                        k2 = lt1 ? k1 : (lt2 ? key : k2);
+                        k1 = lt1 ? key : k1;
+                    }, sd ? nbk1 : 0);
+                    if (k1 != ~0ull) { bi = (int)((k1 >> 4) & 0x1FFFu); bd = (int)(k1 >> 40); bl = (int)(k1 & 15); }
+                    if (k2 != ~0ull) { bd2 = (int)(k2 >> 40); bl2 = (int)(k2 & 15); }
+                } else {
+                    if (e1 != 0xFFFFFFFFu) { bi = (int)(e1 & 0x1FFFu); bd = (int)(e1 >> 16); bl = (int)((e1 >> 13) & 7); }
+                    if (e2 != 0xFFFFFFFFu) { bd2 = (int)(e2 >> 16); bl2 = (int)((e2 >> 13) & 7); }
+                }
+                if (bi < 0 || bd > MT_TH_HIGH) continue;
+                if (bl == bl2 && bd > nnratio * bd2) {   // :124-125 / :190-191: `continue` to the next point
+                    go = false;
+                    continue;
+                }
+                const int p = s_link[bi];
+                if (sd == 0) { r[0] = bi; r[1] = p; }
+                else { r[2] = p; r[3] = bi; }
+            }
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                if (r[b] != res[i][b]) ch = true;
+                res[i][b] = r[b];
+            }
+        }
+        if (__ballot(ch) && (tid & 63) == 0) s_flag = 1;
+        SYNC();
+        // after pass t the first t points are final
+        if (s_flag == 0 || pass > nq) break;
+    }
+    const bool aborted = s_ovf != 0;
+    // ---- the commit: the last entry writing a slot wins; nmatches counts every write ----
+    int* s_res = s_wcnt;
+    for (int k = tid; k < n; k += MT_BLK_NT) s_res[k] = -1;
+    SYNC();
+    int nas = 0;
+    if (!aborted) {
+#pragma unroll
+        for (int i = 0; i < QPT; i++) {
+            const int q = tid + i * MT_BLK_NT;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                if (q >= nq || res[i][b] < 0) continue;
+                atomicMax(&s_res[res[i][b]], 4 * q + b);
+                nas++;
+            }
+        }
+    }
+    nas = wave_sum_dpp(nas);
+    if ((tid & 63) == 0 && nas) atomicAdd(&s_cnt, nas);
+    SYNC();
+    if (!aborted)
+#pragma unroll
+        for (int i = 0; i < QPT; i++) {
+            const int q = tid + i * MT_BLK_NT;
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                if (q < nq && res[i][b] >= 0 && s_res[res[i][b]] == 4 * q + b) io.mvp_out[res[i][b]] = rq[q].id;
+        }
+    if (io.stats && npair) {
+        atomicAdd(&io.stats[0], npair);
+        atomicAdd(&io.stats[1], npair);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    SYNC();
+    if (tid == 0) {
+        __threadfence_system();
+        if (io.stats) io.stats[2] = (unsigned long long)(pass + 1);
+        volatile int* st = io.st_host;
+        st[0] = aborted ? 2 : 0;
+        st[1] = s_cnt;
+        st[2] = 0;
+        st[3] = pass + 1;
+        st[5] = io.ntm ? *io.ntm : 0;
+        __threadfence_system();
+        st[4] = io.seq;
+        __threadfence_system();
+    }
 }
 
 // ---- Large single-camera local-map searches (nq > MT_BLOCK_MAXQ, frame in LDS): k_sbp_block's design
@@ -2765,25 +3002,28 @@ struct DevIn {
 
 // k_sbp_block's bucket geometry for a frame: bands of 16 rows, then as many column strips (<= 32, >= 24
 // columns wide) as 8192 buckets and the LDS allow; false: the frame does not fit the block form
-// (ncam = 2: both cameras' bucket sets, k_sbp_block2)
-size_t blk_lds(int n, int nlev, const BlkGeom& gm, int ncam = 1) {
-    return (size_t)n * 61 + (size_t)blk_be_words(ncam * nlev * gm.NB * gm.NS, MT_BLK_NT) * 4 + 16;
+// (ncam = 2: both cameras' bucket sets, k_sbp_block2 / k_sbp_block4; bpk: LDS bytes per keypoint)
+size_t blk_lds(int n, int nlev, const BlkGeom& gm, int ncam = 1, int bpk = 61) {
+    return (size_t)n * bpk + (size_t)blk_be_words(ncam * nlev * gm.NB * gm.NS, MT_BLK_NT) * 4 + 16;
 }
-bool blk_geom(const orbfe_frame* F, BlkGeom& gm, int ncam = 1) {
+bool blk_geom(const orbfe_frame* F, BlkGeom& gm, int ncam = 1, int bpk = 61) {
     constexpr int BR = 16;
     if (!(F->max_y > 0.f && F->max_y < 65536.f && F->max_x > 0.f && F->max_x < 65536.f)) return false;
     gm.NB = (int)std::floor(F->max_y / BR) + 2;
     gm.inv_br = 1.0f / BR;
     const int lev_bands = ncam * F->nlevels * gm.NB;
-    const long budget = std::min<long>(8192, ((long)MT_LDS_MAX - 61L * F->n - 4) / 4);
+    const long budget = std::min<long>(8192, ((long)MT_LDS_MAX - (long)bpk * F->n - 4) / 4);
     gm.NS = (int)std::min<long>(std::min<long>(32, budget / std::max(lev_bands, 1)), (long)std::ceil(F->max_x / 24.f));
     if (gm.NS < 1) return false;
-    while (gm.NS > 1 && blk_lds(F->n, F->nlevels, gm, ncam) > MT_LDS_MAX) gm.NS--;   // the scan's padding
+    while (gm.NS > 1 && blk_lds(F->n, F->nlevels, gm, ncam, bpk) > MT_LDS_MAX) gm.NS--;   // the scan's padding
     gm.inv_sw = (float)gm.NS / (F->max_x + 1.f);
-    return blk_lds(F->n, F->nlevels, gm, ncam) <= MT_LDS_MAX;
+    return blk_lds(F->n, F->nlevels, gm, ncam, bpk) <= MT_LDS_MAX;
 }
 
-// sbp_run's one-launch form (k_sbp_block): arguments already validated by sbp_run.
+// sbp_run's one-launch form (k_sbp_block, k_sbp_block4): arguments already validated by sbp_run.
+// kBlockAborted: k_sbp_block4 gave up (more writers of one slot than it tracks) before writing
+// anything; the caller runs the multi-launch form.
+constexpr int kBlockAborted = -1000;
 int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, const void* queries, int nq,
                   size_t qstride, size_t qid_off, size_t qangle_off, float th, int a0, int a1, float thFar,
                   float nnratio, int maxDist, int checkOri, const BlkGeom& gm, const FrustumIn* fin, const DevIn* dev) {
@@ -2845,8 +3085,12 @@ int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* m
     if (zc) memcpy(m.ho, mvp, (size_t)n * 4);   // the slots the search leaves alone keep their value
     const BlkIO io{mvp_in, obs_d, mvp_out, (int)qstride, (int)qid_off, (int)qangle_off, checkOri, ntm, t_ms.hs_dev, seq,
                    stats, (!dev && !fin) ? ms_ptr<uint4>(o_qdev) : nullptr};
-    const size_t lds = blk_lds(n, F->nlevels, gm);
-    if (mode == 0)
+    const bool two4 = F->two_cams && mode == 0;
+    const size_t lds = two4 ? blk_lds(n, F->nlevels, gm, 2, blk4_bytes_per_kp()) : blk_lds(n, F->nlevels, gm);
+    if (two4)
+        hipLaunchKernelGGL(k_sbp_block4, dim3(1), dim3(MT_BLK_NT), lds, s, fr, gm, (const orbfe_map_point*)q, nq, th, a0,
+                           thFar, nnratio, io);
+    else if (mode == 0)
         hipLaunchKernelGGL(k_sbp_block<0>, dim3(1), dim3(MT_BLK_NT), lds, s, fr, gm, (const void*)q, nq, th, a0, a1,
                            thFar, nnratio, maxDist, 1, io);
     else if (mode == 1)
@@ -2870,6 +3114,7 @@ int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* m
         }
         __builtin_ia32_pause();
     }
+    if (st[0] == 2) return kBlockAborted;   // k_sbp_block4: a slot with too many writers, nothing written
     if (zc) memcpy(mvp, m.ho, (size_t)n * 4);   // complete: the status words come after the slot writes
     if (fin && fin->n_to_match) *fin->n_to_match = st[5];
     if (stats) {   // counting mode only: one more copy and synchronisation
@@ -3176,6 +3421,13 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
         // sixteen lanes per query win (config 5: th 1 / 3 here, th 5 / 15 there; r05_kernel_ab.txt)
         if (mode == 0 && th < MT_MULTI_TH)
             return sbp_multi_run(F, mvp, mvp_obs, queries, nq, qstride, qid_off, th, a0, thFar, nnratio, gm, fin, dev);
+    }
+    // a two-camera frame's local-map search (SearchLocalPoints of a KannalaBrandt8 rig) in one
+    // workgroup: four slot writes per point, the slots' writers tracked per pass (k_sbp_block4)
+    if (two && mode == 0 && n <= MT_BAND_MAXN && nq <= MT_BLOCK_MAXQ && blk_geom(F, gm, 2, blk4_bytes_per_kp())) {
+        const int r = sbp_block_run(0, F, mvp, mvp_obs, queries, nq, qstride, qid_off, qangle_off, th, a0, a1, thFar,
+                                    nnratio, maxDist, 0, gm, fin, dev);
+        if (r != kBlockAborted) return r;
     }
     // a two-camera frame's last-frame search (the per-frame Tracking call of a KannalaBrandt8 rig) in
     // one workgroup as well: both cameras' keypoints in LDS, two entries per point

@@ -369,6 +369,70 @@ def test_sbp_local_two_cams_dense(gpu, om):
         np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("nl,nr,n_mps,th", [
+    (1000, 950, 1500, 1),     # the one-workgroup path (k_sbp_block4): <= 2048 keypoints and points
+    (1000, 950, 2000, 3),
+    (1000, 950, 1200, 15),
+    (1024, 1024, 2048, 3),    # its limits
+    (1000, 950, 2049, 3),     # one point past them: the multi-launch passes
+])
+def test_sbp_local_two_cams_block(gpu, om, nl, nr, n_mps, th):
+    """SearchByProjection(F, vpMapPoints) with Nleft != -1 (ORBmatcher.cc:62-209) through the
+    one-workgroup search and across its size limits, against the oracle: ratio 0.8 / 0.6, bFarPoints."""
+    _, F, mps, mvp0, obs = _two_case(nl + nr + n_mps + th, nl, nr, n_mps)
+    for ratio, bfar in ((0.8, False), (0.6, True)):
+        a, b = mvp0.copy(), mvp0.copy()
+        ng = ORBmatcher(ratio).SearchByProjectionLocalMap(F, a, obs, mps, th, bfar, 20.0)
+        no = om.OracleMatcher(ratio).sbp_local(F, b, obs, mps, th, bfar, 20.0)
+        assert ng == no and no > 0
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("n_mps", [600, 2000])
+def test_sbp_local_two_cams_block_dense(gpu, om, n_mps):
+    """k_sbp_block4 under competition: few keypoints, dense stereo links, half the points with
+    Observations() == 0 (their slots stay open to later points, partner writes replace holders); at
+    2000 points a slot can collect more writers in a pass than the block tracks, which must hand the
+    search to the multi-launch form with nothing written."""
+    rng = np.random.default_rng(67 + n_mps)
+    F = sm.synth_frame_two(rng, 150, 140, w=120, h=90, stereo_frac=0.9)
+    mps = sm.synth_local_map_two(rng, F, n_mps, copy_frac=0.9, flip_p=0.02)
+    mps["observations"] = np.where(rng.random(len(mps)) < 0.5, 0, mps["observations"])
+    mvp0, obs = sm.initial_slots(rng, F.N, 0.2)
+    for th in (1, 3):
+        a, b = mvp0.copy(), mvp0.copy()
+        ng = ORBmatcher(0.8).SearchByProjectionLocalMap(F, a, obs, mps, th)
+        no = om.OracleMatcher(0.8).sbp_local(F, b, obs, mps, th)
+        assert ng == no
+        np.testing.assert_array_equal(a, b)
+
+
+def test_search_local_points_rig_block(gpu, om):
+    """Tracking::SearchLocalPoints on a two-camera fisheye frame with a Tracking-sized local map
+    (<= 2048 points): the device projection, then k_sbp_block4."""
+    from orb_slam3_ros_amd.matcher import search_local_points
+    rng, F, cam, rig, pts = _rig_case(93, True, 1800)
+    mvp0, obs = sm.initial_slots(rng, F.N, 0.15)
+    for th, ratio, bfar in ((1, 0.8, False), (3, 0.6, True)):
+        a, b = mvp0.copy(), mvp0.copy()
+        ng = search_local_points(F, cam, pts, a, obs, th, bfar, 10.0, ratio, rig=rig)
+        no = om.search_local_points(F, cam, pts, b, obs, th, bfar, 10.0, ratio, rig=rig)
+        assert ng == no and no[0] > 0
+        np.testing.assert_array_equal(a, b)
+    # the device-resident form (frame, slots and points in HBM)
+    import torch
+    from orb_slam3_ros_amd.matcher import DeviceMatchFrame, search_local_points_device
+    Fd = DeviceMatchFrame(F, gpu)
+    mvp_t = torch.from_numpy(mvp0.copy()).to(gpu)
+    obs_t = torch.from_numpy(obs.copy()).to(gpu)
+    pts_t = torch.from_numpy(pts.view(np.uint8).reshape(-1).copy()).to(gpu)
+    ng, ntm_g = search_local_points_device(Fd, cam, pts_t, mvp_t, obs_t, 3.0, rig=rig)
+    mvp_o = mvp0.copy()
+    no, ntm_o = om.search_local_points(F, cam, pts, mvp_o, obs, 3.0, rig=rig)
+    assert (ng, ntm_g) == (no, ntm_o) and no > 0
+    np.testing.assert_array_equal(mvp_t.cpu().numpy(), mvp_o)
+
+
 def test_sbp_local_two_cams_device_resident(gpu, om):
     import torch
     from orb_slam3_ros_amd.matcher import DeviceMatchFrame, search_by_projection_local_device
