@@ -546,6 +546,31 @@ typedef struct orbfe_kf_camera {
     float log_scale_factor;          /* mfLogScaleFactor */
 } orbfe_kf_camera;
 
+/* A last-frame point for the device-projected motion-model search (ORBmatcher.cc:1695-1712): the
+ * MapPoint's world position, nLastOctave and the keypoint angle of LastFrame (mvKeys / mvKeysRight),
+ * Observations(), the caller's handle, and valid = pMP && !LastFrame.mvbOutlier[i]. */
+typedef struct orbfe_last_point {
+    float pos[3];                    /* pMP->GetWorldPos() */
+    int32_t octave;                  /* nLastOctave */
+    float angle;                     /* LastFrame keypoint angle (rotation check) */
+    int32_t observations;
+    int32_t id;
+    int32_t valid;
+    uint8_t desc[32];                /* pMP->GetDescriptor() */
+} orbfe_last_point;                  /* 64 bytes */
+
+/* SearchByProjection(CurrentFrame, LastFrame, th, bMono) with the projection on the device
+ * (ORBmatcher.cc:1702-1718, 1794-1796): x3Dc = Tcw * x3Dw (Sophus SE3f action, Tcw = CurrentFrame.
+ * GetPose()), invzc = 1.0 / x3Dc(2) (double, then float), uv = cam->project(x3Dc) (CurrentFrame.
+ * mpCamera: pinhole or KannalaBrandt8), and for a two-camera cur the right-camera search around
+ * cam->project(Trl * x3Dc) (Trl = GetRelativePoseTrl(); the reference projects it with mpCamera);
+ * then exactly orbfe_search_by_projection_lastframe(_stereo). Trl is ignored (may be NULL) for a
+ * single-camera cur. bForward / bBackward as the reference computes them from the poses. */
+int orbfe_search_by_projection_lastframe_pose(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_obs,
+                                              const orbfe_last_point* pts, int32_t n_pts, const orbfe_pose* Tcw,
+                                              const orbfe_pose* Trl, const orbfe_camera_model* cam, float th,
+                                              int32_t bForward, int32_t bBackward, int32_t checkOri);
+
 /* The matching half of Fuse (ORBmatcher.cc:1148-1337 with sim3 = 0; :1339-1455, Fuse(pKF, Scw, ...)
  * with sim3 = 1; pinhole, bRight = false): for every point with id >= 0 not flagged BAD / SKIP (SKIP =
  * IsInKeyFrame(pKF), resp. already in pKF->GetMapPoints()), project, check and search the keyframe

@@ -155,6 +155,7 @@ def _match_sigs(L):
     L.oro_sbp_local.argtypes = [vp, vp, vp, vp, ci, cf, ci, cf, cf]
     L.oro_sbp_lastframe.argtypes = [vp, vp, vp, vp, ci, cf, ci, ci, ci]
     L.oro_sbp_lastframe_stereo.argtypes = [vp, vp, vp, vp, vp, ci, cf, ci, ci, ci]
+    L.oro_sbp_lastframe_pose.argtypes = [vp, vp, vp, vp, ci, vp, vp, vp, cf, ci, ci, ci]
     L.oro_sbp_kf.argtypes = [vp, vp, vp, ci, cf, ci, ci]
     L.oro_search_for_init.argtypes = [vp, vp, vp, vp, ci, cf, ci]
     L.oro_search_by_bow.argtypes = [vp, vp, vp, ci, vp, vp, vp, vp, cf, ci]
@@ -192,6 +193,14 @@ class OracleMatcher:
     def sbp_lastframe(self, F, mvp, mvp_obs, pts, th, bForward, bBackward):
         return self.L.oro_sbp_lastframe(F.ref(), mvp.ctypes.data, mvp_obs.ctypes.data, pts.ctypes.data, len(pts),
                                         float(th), int(bForward), int(bBackward), self.checkOri)
+
+    def sbp_lastframe_pose(self, F, mvp, mvp_obs, pts, Tcw, cam, th, bForward, bBackward, Trl=None):
+        """pts: LAST_POINT records; Tcw / Trl: orbfe_pose structures; cam: orbfe_camera_model."""
+        import ctypes
+        return self.L.oro_sbp_lastframe_pose(F.ref(), mvp.ctypes.data, mvp_obs.ctypes.data, pts.ctypes.data, len(pts),
+                                             ctypes.addressof(Tcw), ctypes.addressof(Trl) if Trl is not None else None,
+                                             ctypes.addressof(cam), float(th), int(bForward), int(bBackward),
+                                             self.checkOri)
 
     def sbp_lastframe_stereo(self, F, mvp, mvp_obs, pts, right_uv, th, bForward, bBackward):
         ruv = np.ascontiguousarray(right_uv, np.float32)

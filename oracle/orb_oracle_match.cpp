@@ -585,6 +585,50 @@ static void pose_apply(const orbfe_pose& P, const float p[3], float o[3]) {
     }
 }
 
+// SearchByProjection(CurrentFrame, LastFrame, th, bMono) with its projection (ORBmatcher.cc:1695-1718,
+// 1794-1796): x3Dc = Tcw * x3Dw (Sophus SE3f action), invzc = 1.0 / x3Dc(2) (the double literal makes
+// the division double), uv = mpCamera->project(x3Dc); a two-camera frame's right-camera window around
+// mpCamera->project(Trl * x3Dc); then the host-projected search above.
+int oro_sbp_lastframe_pose(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_obs_in, const orbfe_last_point* lp,
+                           int32_t n_pts, const orbfe_pose* Tcw, const orbfe_pose* Trl, const orbfe_camera_model* cam,
+                           float th, int32_t bForward, int32_t bBackward, int32_t checkOri) {
+    const bool two = cur->two_cams != 0;
+    CamModel M{cam->type, {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}};
+    for (int k = 0; k < 8; k++) M.p[k] = cam->params[k];
+    orbfe_pose T = *Tcw, R;
+    T.kind = ORBFE_SE3;
+    if (two) {
+        R = *Trl;
+        R.kind = ORBFE_SE3;
+    }
+    std::vector<orbfe_proj_point> pts((size_t)n_pts);
+    std::vector<float> ruv((size_t)n_pts * 2, 0.f);
+    for (int i = 0; i < n_pts; i++) {
+        const orbfe_last_point& p = lp[i];
+        orbfe_proj_point& q = pts[i];
+        memset(&q, 0, sizeof(q));
+        q.octave = p.octave;
+        q.angle = p.angle;
+        q.observations = p.observations;
+        q.id = p.id;
+        memcpy(q.desc, p.desc, 32);
+        if (!p.valid) continue;   // pMP == NULL or an outlier
+        q.valid = 1;
+        float c[3];
+        pose_apply(T, p.pos, c);
+        q.invzc = (float)(1.0 / (double)c[2]);
+        if (q.invzc < 0) continue;   // skipped by the search as the reference's `continue`
+        cam_project(M, c, q.u, q.v);
+        if (two) {
+            float cr[3];
+            pose_apply(R, c, cr);
+            cam_project(M, cr, ruv[2 * i], ruv[2 * i + 1]);
+        }
+    }
+    return oro_sbp_lastframe_stereo(cur, mvp, mvp_obs_in, pts.data(), two ? ruv.data() : nullptr, n_pts, th, bForward,
+                                    bBackward, checkOri);
+}
+
 static bool kf_in_image(const orbfe_frame* F, float x, float y) {   // KeyFrame::IsInImage (KeyFrame.cc:753-756)
     return x >= F->min_x && x < F->max_x && y >= F->min_y && y < F->max_y;
 }

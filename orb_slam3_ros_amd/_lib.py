@@ -67,6 +67,8 @@ _SIGS = {
     "orbfe_search_by_projection_lastframe": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _c_float, _c_int, _c_int, _c_int]),
     "orbfe_search_by_projection_lastframe_stereo": (_c_int, [_vp, _vp, _vp, _vp, _vp, _c_int, _c_float, _c_int, _c_int,
                                                              _c_int]),
+    "orbfe_search_by_projection_lastframe_pose": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _c_float, _c_int,
+                                                           _c_int, _c_int]),
     "orbfe_search_by_projection_kf": (_c_int, [_vp, _vp, _vp, _c_int, _c_float, _c_int, _c_int]),
     "orbfe_search_for_initialization": (_c_int, [_vp, _vp, _vp, _vp, _c_int, _c_float, _c_int]),
     "orbfe_search_by_bow": (_c_int, [_vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_float, _c_int]),

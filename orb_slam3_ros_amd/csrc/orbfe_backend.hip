@@ -131,23 +131,7 @@ __global__ __launch_bounds__(256) void k_distinctive(const uint32_t* desc, const
 }
 
 // ---- back-end projections ----
-// Sophus point action in Eigen's order, no contraction; RxSO3 scale = squaredNorm() reduced as one
-// SSE packet, (x*x + z*z) + (y*y + w*w) (Eigen's predux<Packet4f>).
-__device__ __forceinline__ void be_pose_apply(const orbfe_pose& P, const float p[3], float o[3]) {
-    const float vx = P.q[0], vy = P.q[1], vz = P.q[2], w = P.q[3];
-    float uv[3] = {vy * p[2] - vz * p[1], vz * p[0] - vx * p[2], vx * p[1] - vy * p[0]};
-#pragma unroll
-    for (int k = 0; k < 3; k++) uv[k] += uv[k];
-    const float c[3] = {vy * uv[2] - vz * uv[1], vz * uv[0] - vx * uv[2], vx * uv[1] - vy * uv[0]};
-    if (P.kind == ORBFE_SIM3) {
-        const float sc = (vx * vx + vz * vz) + (vy * vy + w * w);
-#pragma unroll
-        for (int k = 0; k < 3; k++) o[k] = (sc * p[k] + (w * uv[k] + c[k])) + P.t[k];
-    } else {
-#pragma unroll
-        for (int k = 0; k < 3; k++) o[k] = ((p[k] + w * uv[k]) + c[k]) + P.t[k];
-    }
-}
+// (be_pose_apply, the Sophus point action, lives in orbfe_matcher.hip: the last-frame search uses it too)
 
 #define BE_PRJ_PINHOLE 0   // Pinhole::project: fx * x / z + cx
 #define BE_PRJ_INVZ_F 1    // invz = 1 / z (float); u = fx * (x * invz) + cx

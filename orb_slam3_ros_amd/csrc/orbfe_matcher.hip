@@ -2140,6 +2140,24 @@ struct CamDev {
 // non-vectorised redux halves the range, sum(a, b, c) = a + (b + c) (Eigen/src/Core/Redux.h,
 // redux_novec_unroller; ProductEvaluators.h lazy coeff = (lhs.row(i) .* rhs.col(j)).sum()).
 __host__ __device__ __forceinline__ float eig_sum3(float a, float b, float c) { return a + (b + c); }
+// Sophus point action in Eigen's order, no contraction; RxSO3 scale = squaredNorm() reduced as one
+// SSE packet, (x*x + z*z) + (y*y + w*w) (Eigen's predux<Packet4f>).
+__device__ __forceinline__ void be_pose_apply(const orbfe_pose& P, const float p[3], float o[3]) {
+    const float vx = P.q[0], vy = P.q[1], vz = P.q[2], w = P.q[3];
+    float uv[3] = {vy * p[2] - vz * p[1], vz * p[0] - vx * p[2], vx * p[1] - vy * p[0]};
+#pragma unroll
+    for (int k = 0; k < 3; k++) uv[k] += uv[k];
+    const float c[3] = {vy * uv[2] - vz * uv[1], vz * uv[0] - vx * uv[2], vx * uv[1] - vy * uv[0]};
+    if (P.kind == ORBFE_SIM3) {
+        const float sc = (vx * vx + vz * vz) + (vy * vy + w * w);
+#pragma unroll
+        for (int k = 0; k < 3; k++) o[k] = (sc * p[k] + (w * uv[k] + c[k])) + P.t[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; k++) o[k] = ((p[k] + w * uv[k]) + c[k]) + P.t[k];
+    }
+}
+
 // GeometricCamera::project(Eigen::Vector3f): Pinhole.cpp:43-49, KannalaBrandt8.cpp:67-82 (float
 // arithmetic in the source's order; atan2f / cos / sin of float as glibc's atan2f / cosf / sinf).
 __device__ __forceinline__ float2 mt_cam_project(const CamModelDev& m, float x, float y, float z) {
@@ -2156,6 +2174,51 @@ __device__ __forceinline__ float2 mt_cam_project(const CamModelDev& m, float x, 
         return make_float2(m.fx * r * glibc_cosf(psi) + m.cx, m.fy * r * glibc_sinf(psi) + m.cy);
     }
     return make_float2(m.fx * x / z + m.cx, m.fy * y / z + m.cy);
+}
+// SearchByProjection(CurrentFrame, LastFrame)'s projection (ORBmatcher.cc:1702-1718, 1794-1796) for
+// orbfe_search_by_projection_lastframe_pose: one thread per last-frame point, x3Dc = Tcw * x3Dw (Sophus
+// SE3f action), invzc = 1.0 / x3Dc(2) in double as the reference's double literal makes it, uv =
+// mpCamera->project(x3Dc), and for a two-camera frame the right-camera window centre mpCamera->project(
+// Trl * x3Dc). Writes the orbfe_proj_point records the searches read (a point behind the camera keeps
+// its negative invzc: the search skips it as the reference's `continue` does).
+struct LastProjIn {
+    const orbfe_last_point* pts;   // host points (staged by the runner)
+    orbfe_pose T, Trl;
+    CamModelDev cam;
+    int two;
+};
+__global__ __launch_bounds__(MT_NT) void k_last_proj(LastProjIn g, const orbfe_last_point* pts, int n,
+                                                     orbfe_proj_point* out, float2* ruv) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const orbfe_last_point p = pts[i];
+    orbfe_proj_point r;
+    r.u = r.v = r.invzc = 0.f;
+    r.octave = p.octave;
+    r.angle = p.angle;
+    r.valid = 0;
+    r.observations = p.observations;
+    r.id = p.id;
+    memcpy(r.desc, p.desc, 32);
+    float2 uvr = make_float2(0.f, 0.f);
+    if (p.valid) {
+        float c[3];
+        be_pose_apply(g.T, p.pos, c);
+        r.invzc = (float)(1.0 / (double)c[2]);
+        r.valid = 1;
+        if (!(r.invzc < 0)) {
+            const float2 uv = mt_cam_project(g.cam, c[0], c[1], c[2]);
+            r.u = uv.x;
+            r.v = uv.y;
+            if (g.two) {
+                float cr[3];
+                be_pose_apply(g.Trl, c, cr);
+                uvr = mt_cam_project(g.cam, cr[0], cr[1], cr[2]);
+            }
+        }
+    }
+    out[i] = r;
+    if (g.two) ruv[i] = uvr;
 }
 // The checks shared by isInFrustum's Nleft == -1 branch (Frame.cc:512-570) and isInFrustumChecks
 // (Frame.cc:1168-1242) for one view: pose (R, t), camera centre Ow, camera model m. stage = how far
@@ -3026,20 +3089,23 @@ bool blk_geom(const orbfe_frame* F, BlkGeom& gm, int ncam = 1, int bpk = 61) {
 constexpr int kBlockAborted = -1000;
 int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, const void* queries, int nq,
                   size_t qstride, size_t qid_off, size_t qangle_off, float th, int a0, int a1, float thFar,
-                  float nnratio, int maxDist, int checkOri, const BlkGeom& gm, const FrustumIn* fin, const DevIn* dev) {
+                  float nnratio, int maxDist, int checkOri, const BlkGeom& gm, const FrustumIn* fin, const DevIn* dev,
+                  const LastProjIn* lp = nullptr) {
     const int n = F->n;
     Plan p;
     FramePlan fp;
     if (dev || F->device) fp.plan_dev(F, mode != 2);   // a device frame: read in place
     else fp.plan(p, F, true, mode != 2);
     const size_t o_q = dev ? 0 : fin ? p.upload(fin->pts, (size_t)nq * sizeof(orbfe_map_point_3d))
-                                     : p.upload(queries, (size_t)nq * qstride);
+                                     : lp ? p.upload(lp->pts, (size_t)nq * sizeof(orbfe_last_point))
+                                          : p.upload(queries, (size_t)nq * qstride);
+    const size_t o_rec = lp ? p.scratch((size_t)nq * sizeof(orbfe_proj_point)) : 0;   // device-projected records
     const size_t o_mvp = dev ? 0 : p.upload(mvp, (size_t)n * 4);
     const size_t o_obs = (dev || mode == 2) ? 0 : p.upload(mvp_obs, (size_t)n * 4);
     const size_t o_track = fin ? p.scratch((size_t)nq * sizeof(orbfe_map_point)) : 0;
     const size_t o_ntm = fin ? p.scratch(16) : 0;
     const size_t o_stats = t_stats ? p.scratch(24) : 0;
-    const size_t o_qdev = (!dev && !fin) ? p.scratch((size_t)nq * qstride) : 0;
+    const size_t o_qdev = (!dev && !fin && !lp) ? p.scratch((size_t)nq * qstride) : 0;
     // host-API calls: zero copy both ways. The kernel reads its inputs straight from the mapped pinned
     // staging and writes the slots into mapped pinned memory; the host waits for the status words
     // only (no DMA, no stream synchronisation: the call is one launch).
@@ -3078,13 +3144,18 @@ int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* m
         qstride = sizeof(orbfe_map_point);
         qid_off = offsetof(orbfe_map_point, id);
     }
+    if (lp) {   // SearchByProjection(CurrentFrame, LastFrame)'s projection on the device
+        hipLaunchKernelGGL(k_last_proj, dim3((nq + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, *lp,
+                           up_ptr<const orbfe_last_point>(o_q, zc), nq, ms_ptr<orbfe_proj_point>(o_rec), (float2*)nullptr);
+        q = ms_ptr<const uint8_t>(o_rec);
+    }
     const int32_t* mvp_in = dev ? mvp : up_ptr<const int32_t>(o_mvp, zc);
     int32_t* mvp_out = dev ? mvp : m.ho_dev;
     const int32_t* obs_d = mode == 2 ? nullptr : dev ? mvp_obs : up_ptr<const int32_t>(o_obs, zc);
     const int seq = ++t_ms.seq;
     if (zc) memcpy(m.ho, mvp, (size_t)n * 4);   // the slots the search leaves alone keep their value
     const BlkIO io{mvp_in, obs_d, mvp_out, (int)qstride, (int)qid_off, (int)qangle_off, checkOri, ntm, t_ms.hs_dev, seq,
-                   stats, (!dev && !fin) ? ms_ptr<uint4>(o_qdev) : nullptr};
+                   stats, (!dev && !fin && !lp) ? ms_ptr<uint4>(o_qdev) : nullptr};
     const bool two4 = F->two_cams && mode == 0;
     const size_t lds = two4 ? blk_lds(n, F->nlevels, gm, 2, blk4_bytes_per_kp()) : blk_lds(n, F->nlevels, gm);
     if (two4)
@@ -3133,17 +3204,19 @@ int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* m
 // words awaited (as sbp_block_run); arguments already validated by sbp_run.
 int sbp_block2_run(const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, const orbfe_proj_point* pts,
                    const float* right_uv, int nq, float th, int a0, int a1, int maxDist, int checkOri,
-                   const BlkGeom& gm) {
+                   const BlkGeom& gm, const LastProjIn* lp = nullptr) {
     const int n = F->n;
     Plan p;
     FramePlan fp;
     fp.plan(p, F, true, false);
-    const size_t o_q = p.upload(pts, (size_t)nq * sizeof(orbfe_proj_point));
-    const size_t o_ruv = p.upload(right_uv, (size_t)nq * 8);
+    const size_t o_q = lp ? p.upload(lp->pts, (size_t)nq * sizeof(orbfe_last_point))
+                          : p.upload(pts, (size_t)nq * sizeof(orbfe_proj_point));
+    const size_t o_ruv = lp ? p.scratch((size_t)nq * 8) : p.upload(right_uv, (size_t)nq * 8);
+    const size_t o_rec = lp ? p.scratch((size_t)nq * sizeof(orbfe_proj_point)) : 0;
     const size_t o_mvp = p.upload(mvp, (size_t)n * 4);
     const size_t o_obs = p.upload(mvp_obs, (size_t)n * 4);
     const size_t o_stats = t_stats ? p.scratch(24) : 0;
-    const size_t o_qdev = p.scratch((size_t)nq * sizeof(orbfe_proj_point));
+    const size_t o_qdev = lp ? 0 : p.scratch((size_t)nq * sizeof(orbfe_proj_point));
     int rc = ms_prepare(p, true);
     if (rc) return rc;
     MatchScratch& m = t_ms;
@@ -3168,10 +3241,18 @@ int sbp_block2_run(const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, c
     const BlkIO io{up_ptr<const int32_t>(o_mvp, true), up_ptr<const int32_t>(o_obs, true), m.ho_dev,
                    (int)sizeof(orbfe_proj_point), (int)offsetof(orbfe_proj_point, id),
                    (int)offsetof(orbfe_proj_point, angle), checkOri, nullptr, t_ms.hs_dev, seq, stats,
-                   ms_ptr<uint4>(o_qdev)};
-    hipLaunchKernelGGL(k_sbp_block2, dim3(1), dim3(MT_BLK_NT), blk_lds(n, F->nlevels, gm, 2), s, fr, gm,
-                       up_ptr<const orbfe_proj_point>(o_q, true), up_ptr<const float2>(o_ruv, true), nq, th, a0, a1,
-                       maxDist, io);
+                   lp ? nullptr : ms_ptr<uint4>(o_qdev)};
+    const orbfe_proj_point* recs = up_ptr<const orbfe_proj_point>(o_q, true);
+    const float2* ruv = up_ptr<const float2>(o_ruv, true);
+    if (lp) {   // the projection into both cameras on the device; records and right centres in HBM
+        recs = ms_ptr<const orbfe_proj_point>(o_rec);
+        ruv = ms_ptr<const float2>(o_ruv);
+        hipLaunchKernelGGL(k_last_proj, dim3((nq + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, *lp,
+                           up_ptr<const orbfe_last_point>(o_q, true), nq, ms_ptr<orbfe_proj_point>(o_rec),
+                           ms_ptr<float2>(o_ruv));
+    }
+    hipLaunchKernelGGL(k_sbp_block2, dim3(1), dim3(MT_BLK_NT), blk_lds(n, F->nlevels, gm, 2), s, fr, gm, recs, ruv, nq,
+                       th, a0, a1, maxDist, io);
     HIPCHK(hipGetLastError());
     timer.end();
     volatile int* st = t_ms.hs;
@@ -3363,10 +3444,31 @@ int sbp_multi_run(const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, co
     return st[1];
 }
 
+// k_last_proj for the multi-launch forms: records and right-camera centres back to the host
+int last_proj_host(const LastProjIn& lp, int nq, std::vector<orbfe_proj_point>& rec, std::vector<float>& ruv) {
+    Plan p;
+    const size_t o_in = p.upload(lp.pts, (size_t)nq * sizeof(orbfe_last_point));
+    const size_t o_rec = p.scratch((size_t)nq * sizeof(orbfe_proj_point));
+    const size_t o_ruv = p.scratch((size_t)nq * 8);
+    int rc = ms_prepare(p);
+    if (rc) return rc;
+    hipStream_t s = t_ms.stream;
+    hipLaunchKernelGGL(k_last_proj, dim3((nq + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, lp,
+                       ms_ptr<const orbfe_last_point>(o_in), nq, ms_ptr<orbfe_proj_point>(o_rec), ms_ptr<float2>(o_ruv));
+    HIPCHK(hipGetLastError());
+    rec.resize(nq);
+    ruv.assign((size_t)nq * 2, 0.f);
+    HIPCHK(hipMemcpyAsync(rec.data(), ms_ptr<orbfe_proj_point>(o_rec), (size_t)nq * sizeof(orbfe_proj_point),
+                          hipMemcpyDeviceToHost, s));
+    if (lp.two) HIPCHK(hipMemcpyAsync(ruv.data(), ms_ptr<float2>(o_ruv), (size_t)nq * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+}
+
 int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs, const void* queries, int nq,
             size_t qstride, size_t qobs_off, size_t qid_off, size_t qangle_off, size_t qlevel_off, float th, int a0, int a1, float thFar,
             float nnratio, int maxDist, int checkOri, const FrustumIn* fin = nullptr, const DevIn* dev = nullptr,
-            const float* right_uv = nullptr) {
+            const float* right_uv = nullptr, const LastProjIn* lp = nullptr) {
     // a device view of the current frame (orbfe_frame_device_view): the frame's arrays are read in HBM
     // by k_sbp_block; any other path would read them on the host, so other shapes are refused
     const bool fdev = F && F->device != 0;
@@ -3377,13 +3479,13 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
         BlkGeom g0;
         if (F->two_cams || F->n > MT_BAND_MAXN || nq > MT_BLOCK_MAXQ || !blk_geom(F, g0)) return ORBFE_E_ARG;
     }
-    if (!frame_ok(fdev ? &Fchk : F) || !mvp || nq < 0 || (nq > 0 && !queries && !fin)) return ORBFE_E_ARG;
+    if (!frame_ok(fdev ? &Fchk : F) || !mvp || nq < 0 || (nq > 0 && !queries && !fin && !lp)) return ORBFE_E_ARG;
     if (fin && (!fin->cam || (nq > 0 && !fin->pts) || mode != 0)) return ORBFE_E_ARG;
     if (mode != 2 && !mvp_obs) return ORBFE_E_ARG;
     const bool two = F->two_cams != 0;
     // two-camera frames: a device projection needs the rig (camera models, right view); the
     // last-frame search needs the right projections
-    if (two && ((fin && !fin->rig) || (mode == 1 && nq > 0 && !right_uv))) return ORBFE_E_ARG;
+    if (two && ((fin && !fin->rig) || (mode == 1 && nq > 0 && !right_uv && !lp))) return ORBFE_E_ARG;
     if (two && !dev && !links_ok(F)) return ORBFE_E_ARG;
     // slot writes per query, in the reference's order (entry index = W q + b)
     const int W = !two ? 1 : mode == 0 ? 4 : mode == 1 ? 2 : 1;
@@ -3394,7 +3496,7 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     // level indices address mvScaleFactors: reject out-of-range ones instead of reading past it
     // (frustum-produced levels are clamped to [0, nlevels) by PredictScale; device-resident
     // records are not visible to the host: the kernels skip out-of-range levels instead)
-    for (int j = 0; !fin && !dev && j < nq; j++) {
+    for (int j = 0; !fin && !dev && !lp && j < nq; j++) {
         const uint8_t* rec = (const uint8_t*)queries + (size_t)j * qstride;
         const bool used = mode == 0 ? (((const orbfe_map_point*)rec)->flags & ORBFE_MP_IN_VIEW) != 0
                                     : ((const orbfe_proj_point*)rec)->valid != 0;
@@ -3416,7 +3518,7 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     if (W == 1 && n <= MT_BAND_MAXN && blk_geom(F, gm)) {
         if (nq <= MT_BLOCK_MAXQ)
             return sbp_block_run(mode, F, mvp, mvp_obs, queries, nq, qstride, qid_off, qangle_off, th, a0, a1, thFar,
-                                 nnratio, maxDist, checkOri, gm, fin, dev);
+                                 nnratio, maxDist, checkOri, gm, fin, dev, lp);
         // narrow windows only: a wide window is a long serial walk for one thread, where k_sbp_band's
         // sixteen lanes per query win (config 5: th 1 / 3 here, th 5 / 15 there; r05_kernel_ab.txt)
         if (mode == 0 && th < MT_MULTI_TH)
@@ -3433,7 +3535,17 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     // one workgroup as well: both cameras' keypoints in LDS, two entries per point
     if (two && mode == 1 && !dev && n <= MT_BAND_MAXN && nq <= MT_BLOCK_MAXQ && blk_geom(F, gm, 2))
         return sbp_block2_run(F, mvp, mvp_obs, (const orbfe_proj_point*)queries, right_uv, nq, th, a0, a1, maxDist,
-                              checkOri, gm);
+                              checkOri, gm, lp);
+    // the multi-launch forms read host records: a device-projected search projects first and brings the
+    // records back (searches beyond the one-workgroup limits only)
+    std::vector<orbfe_proj_point> lp_rec;
+    std::vector<float> lp_ruv;
+    if (lp) {
+        const int rc = last_proj_host(*lp, nq, lp_rec, lp_ruv);
+        if (rc) return rc;
+        queries = lp_rec.data();
+        right_uv = lp_ruv.data();
+    }
     std::vector<int32_t> blocked0(dev ? 0 : n);
     for (int k = 0; !dev && k < n; k++) blocked0[k] = mode == 2 ? (mvp[k] >= 0) : (mvp[k] >= 0 && mvp_obs[k] > 0);
     Plan p;
@@ -3666,6 +3778,36 @@ int orbfe_search_by_projection_lastframe_stereo(const orbfe_frame* cur, int32_t*
     return sbp_run(1, cur, mvp, mvp_obs, pts, n_pts, sizeof(orbfe_proj_point), offsetof(orbfe_proj_point, observations),
                    offsetof(orbfe_proj_point, id), offsetof(orbfe_proj_point, angle), offsetof(orbfe_proj_point, octave),
                    th, bForward, bBackward, 0.f, 0.f, MT_TH_HIGH, checkOri, nullptr, nullptr, right_uv);
+}
+
+int orbfe_search_by_projection_lastframe_pose(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_obs,
+                                              const orbfe_last_point* pts, int32_t n_pts, const orbfe_pose* Tcw,
+                                              const orbfe_pose* Trl, const orbfe_camera_model* cam, float th,
+                                              int32_t bForward, int32_t bBackward, int32_t checkOri) {
+    if (!cur || !Tcw || !cam || n_pts < 0 || (n_pts > 0 && !pts)) return ORBFE_E_ARG;
+    const bool two = cur->two_cams != 0;
+    if (two && !Trl) return ORBFE_E_ARG;
+    if (cam->type != ORBFE_CAM_PINHOLE && cam->type != ORBFE_CAM_KANNALA_BRANDT8) return ORBFE_E_ARG;
+    // nLastOctave addresses mvScaleFactors (as the host-projected entry points check)
+    for (int j = 0; j < n_pts; j++)
+        if (pts[j].valid && (pts[j].octave < 0 || pts[j].octave >= cur->nlevels)) return ORBFE_E_ARG;
+    LastProjIn lp;
+    memset(&lp, 0, sizeof(lp));
+    lp.pts = pts;
+    lp.T = *Tcw;
+    lp.T.kind = ORBFE_SE3;
+    if (two) {
+        lp.Trl = *Trl;
+        lp.Trl.kind = ORBFE_SE3;
+    }
+    lp.two = two ? 1 : 0;
+    lp.cam.type = cam->type;
+    lp.cam.fx = cam->params[0]; lp.cam.fy = cam->params[1]; lp.cam.cx = cam->params[2]; lp.cam.cy = cam->params[3];
+    for (int k = 0; k < 4; k++) lp.cam.k[k] = cam->type == ORBFE_CAM_KANNALA_BRANDT8 ? cam->params[4 + k] : 0.f;
+    return sbp_run(1, cur, mvp, mvp_obs, nullptr, n_pts, sizeof(orbfe_proj_point),
+                   offsetof(orbfe_proj_point, observations), offsetof(orbfe_proj_point, id),
+                   offsetof(orbfe_proj_point, angle), offsetof(orbfe_proj_point, octave), th, bForward, bBackward, 0.f, 0.f,
+                   MT_TH_HIGH, checkOri, nullptr, nullptr, nullptr, &lp);
 }
 
 int orbfe_search_by_projection_lastframe(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_obs,

@@ -30,7 +30,11 @@ PROJ_POINT_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("invzc", "<f4"), ("oct
 MAP_POINT_3D_DTYPE = np.dtype([("pos", "<f4", (3,)), ("normal", "<f4", (3,)), ("min_dist", "<f4"), ("max_dist", "<f4"),
                                ("flags", "<i4"), ("observations", "<i4"), ("id", "<i4"), ("track_depth", "<f4"),
                                ("desc", "u1", (32,))])
+# orbfe_last_point (64 B): a last-frame point for the device-projected motion-model search
+LAST_POINT_DTYPE = np.dtype([("pos", "<f4", (3,)), ("octave", "<i4"), ("angle", "<f4"), ("observations", "<i4"),
+                             ("id", "<i4"), ("valid", "<i4"), ("desc", "u1", (32,))])
 assert MAP_POINT_DTYPE.itemsize == 80 and PROJ_POINT_DTYPE.itemsize == 64 and MAP_POINT_3D_DTYPE.itemsize == 80
+assert LAST_POINT_DTYPE.itemsize == 64
 MP_IN_VIEW, MP_BAD, MP_SKIP, MP_IN_VIEW_R = 1, 2, 4, 8
 TH_HIGH, TH_LOW, HISTO_LENGTH = 100, 50, 30   # ORBmatcher.cc:33-35
 
@@ -330,6 +334,20 @@ class ORBmatcher:
         return _lib.check(self._lib.orbfe_search_by_projection_lastframe_stereo(
             cur.ref(), mvp.ctypes.data, mvp_obs.ctypes.data, pts.ctypes.data, ruv.ctypes.data, len(pts), float(th),
             int(bForward), int(bBackward), int(self.mbCheckOrientation)), "SearchByProjection(last frame, stereo)")
+
+    def SearchByProjectionLastFramePose(self, cur: MatchFrame, mvp, mvp_obs, points, Tcw: "Pose", cam: "CameraModel",
+                                        th: float, bForward: bool, bBackward: bool, Trl: "Pose" = None) -> int:
+        """SearchByProjection(CurrentFrame, LastFrame, th, bMono) with its projection on the device
+        (ORBmatcher.cc:1695-1718, 1794-1796): points = LAST_POINT records (world positions), Tcw =
+        CurrentFrame.GetPose(), cam = CurrentFrame.mpCamera, Trl = GetRelativePoseTrl() for a
+        two-camera frame."""
+        mvp = _i32(mvp, cur.N, "mvp")
+        mvp_obs = _i32(mvp_obs, cur.N, "mvp_obs")
+        pts = _records(points, LAST_POINT_DTYPE, "points")
+        return _lib.check(self._lib.orbfe_search_by_projection_lastframe_pose(
+            cur.ref(), mvp.ctypes.data, mvp_obs.ctypes.data, pts.ctypes.data, len(pts), ctypes.byref(Tcw),
+            ctypes.byref(Trl) if Trl is not None else None, ctypes.byref(cam), float(th), int(bForward),
+            int(bBackward), int(self.mbCheckOrientation)), "SearchByProjection(last frame, device projection)")
 
     # SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist) (:1889-2010)
     def SearchByProjectionKeyFrame(self, cur: MatchFrame, mvp, points, th: float, ORBdist: int) -> int:

@@ -621,3 +621,53 @@ def left_kf_camera(cam: Camera) -> KFCamera:
     R = np.array(cam.Rcw[:], np.float64).reshape(3, 3)
     t = np.array(cam.tcw[:], np.float64)
     return KFCamera.make(Pose.se3(R, t), *TUMVI_LEFT[:4])
+
+
+def synth_pose(rng, rot_deg=10.0, t_scale=0.5):
+    """A random rotation (up to rot_deg about a random axis) and translation, as float64 (R, t)."""
+    axis = rng.normal(size=3)
+    axis /= np.linalg.norm(axis)
+    ang = np.deg2rad(rng.uniform(-rot_deg, rot_deg))
+    K = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    R = np.eye(3) + np.sin(ang) * K + (1 - np.cos(ang)) * K @ K
+    return R, rng.normal(scale=t_scale, size=3)
+
+
+def synth_last_points(rng, F: MatchFrame, model, R, t, n: int, copy_frac: float = 0.8, flip_p: float = 0.05,
+                      rot: float = 15.0, nlevels: int = 8) -> np.ndarray:
+    """Last-frame points in the world for the device-projected motion-model search (LAST_POINT
+    records): copies of the frame's (left) keypoints sit on the keypoint's ray under `model` (pinhole
+    or KannalaBrandt8) at a random depth for the pose x_c = R x_w + t, with flipped descriptor bits,
+    the keypoint's octave +-1 and its angle + rot; the rest are random points in front of the camera.
+    Some are invalid (no point / outlier), a few behind the camera."""
+    from .matcher import LAST_POINT_DTYPE, CameraModel
+    p = np.zeros(n, LAST_POINT_DTYPE)
+    nl = F.nleft if F.nleft is not None else F.N
+    fx, fy, cx, cy = (float(v) for v in model.params[:4])
+    w, h = F.bounds[1], F.bounds[3]
+    u = rng.uniform(0, w, n)
+    v = rng.uniform(0, h, n)
+    p["desc"] = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    p["octave"] = rng.integers(0, nlevels, n)
+    p["angle"] = rng.uniform(0, 360, n)
+    if nl:
+        cp = np.nonzero(rng.random(n) < copy_frac)[0]
+        src = rng.integers(0, nl, len(cp))
+        u[cp] = F.keys["x"][src] + rng.normal(0, 1.5, len(cp))
+        v[cp] = F.keys["y"][src] + rng.normal(0, 1.5, len(cp))
+        p["desc"][cp] = flip_bits(rng, F.desc[src], flip_p)
+        p["octave"][cp] = np.clip(F.keys["octave"][src] + rng.integers(-1, 2, len(cp)), 0, nlevels - 1)
+        p["angle"][cp] = np.mod(F.keys["angle"][src] + rot + rng.normal(0, 4, len(cp)), 360.0)
+    if model.type == CameraModel.KANNALA_BRANDT8:
+        rays = kb8_unproject(u, v, fx, fy, cx, cy, [float(k) for k in model.params[4:8]])
+    else:
+        rays = np.stack([(u - cx) / fx, (v - cy) / fy, np.ones(n)], 1)
+    depth = rng.uniform(1.0, 12.0, n)
+    depth[rng.random(n) < 0.02] *= -1.0   # behind the camera
+    c = rays * depth[:, None]
+    p["pos"] = ((c - np.asarray(t)[None, :]) @ np.asarray(R)).astype(np.float32)   # R^T (c - t)
+    p["observations"] = np.where(rng.random(n) < 0.1, 0, rng.integers(1, 20, n))
+    p["id"] = np.arange(n) + 5000
+    p["valid"] = (rng.random(n) > 0.05).astype(np.int32)
+    return p
+

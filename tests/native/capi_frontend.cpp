@@ -431,10 +431,10 @@ struct GpuApiKB8 {
         f.nstereo = trk::fisheye_links(f, train);
         return f.nstereo;
     }
-    int sbp_last_stereo(const orbfe_frame* F, int32_t* mvp, const int32_t* obs, const orbfe_proj_point* pts,
-                        const float* ruv, int n, float th) {
-        const int r = orbfe_search_by_projection_lastframe_stereo(F, mvp, obs, pts, ruv, n, th, 0, 0, 1);
-        check(r, "search_by_projection_lastframe_stereo");
+    int sbp_last_pose(const orbfe_frame* F, int32_t* mvp, const int32_t* obs, const orbfe_last_point* pts, int n,
+                      const orbfe_pose* Tcw, const orbfe_pose* Trl, const orbfe_camera_model* cam, float th) {
+        const int r = orbfe_search_by_projection_lastframe_pose(F, mvp, obs, pts, n, Tcw, Trl, cam, th, 0, 0, 1);
+        check(r, "search_by_projection_lastframe_pose");
         return r;
     }
     int local_points_rig(const orbfe_frame* F, const orbfe_camera* c, const orbfe_stereo_rig* rig,
@@ -455,7 +455,7 @@ int tracking_kb8(int frames, const char* job, const char* out_path) {
     return trk::run_sequence_kb8(api, J.cam, J.w, J.h, el.mvScaleFactor, J.window, frames, J.npairs,
                                  [&](int k) { return J.left(k); }, [&](int k) { return J.right(k); }, out_path,
                                  "gpu: liborbfe.so C-ABI, KannalaBrandt8 two-camera frame (orbfe_frame_fisheye, "
-                                 "orbfe_search_by_projection_lastframe_stereo, "
+                                 "orbfe_search_by_projection_lastframe_pose, "
                                  "orbfe_search_local_points_track with the rig)");
 }
 

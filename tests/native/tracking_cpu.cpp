@@ -35,6 +35,9 @@ int oro_stereo_knn_ratio(const uint8_t* L, int32_t nl, const uint8_t* R, int32_t
 int oro_sbp_lastframe_stereo(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_obs_in,
                              const orbfe_proj_point* pts, const float* right_uv, int32_t n_pts, float th,
                              int32_t bForward, int32_t bBackward, int32_t checkOri);
+int oro_sbp_lastframe_pose(const orbfe_frame* cur, int32_t* mvp, const int32_t* mvp_obs_in, const orbfe_last_point* lp,
+                           int32_t n_pts, const orbfe_pose* Tcw, const orbfe_pose* Trl, const orbfe_camera_model* cam,
+                           float th, int32_t bForward, int32_t bBackward, int32_t checkOri);
 int oro_search_local_points_rig(const orbfe_frame* F, const orbfe_camera* cam, const orbfe_stereo_rig* rig,
                                 const orbfe_map_point_3d* pts, int32_t n, int32_t* mvp, const int32_t* mvp_obs, float th,
                                 int32_t bFarPoints, float thFarPoints, float nnratio, int32_t* n_to_match);
@@ -102,9 +105,9 @@ struct CpuApi {
         f.nstereo = trk::fisheye_links(f, train);
         return f.nstereo;
     }
-    int sbp_last_stereo(const orbfe_frame* F, int32_t* mvp, const int32_t* obs, const orbfe_proj_point* pts,
-                        const float* ruv, int n, float th) {
-        return oro_sbp_lastframe_stereo(F, mvp, obs, pts, ruv, n, th, 0, 0, 1);
+    int sbp_last_pose(const orbfe_frame* F, int32_t* mvp, const int32_t* obs, const orbfe_last_point* pts, int n,
+                      const orbfe_pose* Tcw, const orbfe_pose* Trl, const orbfe_camera_model* cam, float th) {
+        return oro_sbp_lastframe_pose(F, mvp, obs, pts, n, Tcw, Trl, cam, th, 0, 0, 1);
     }
     int local_points_rig(const orbfe_frame* F, const orbfe_camera* c, const orbfe_stereo_rig* rig,
                          const orbfe_map_point_3d* pts, int n, int32_t* mvp, const int32_t* obs, float th,

@@ -123,46 +123,45 @@ public:
         fr.r2l = cur.r2l.data();
         cur.mvp.assign(N, -1);
         std::vector<int32_t> obs(N, 0);
-        // TrackWithMotionModel: the last frame's points (both cameras' slots) projected with the
-        // motion-model pose into the left camera and, for the right-camera branch, through Trl with
-        // mpCamera (ORBmatcher.cc:1795-1796 projects with mpCamera)
+        // TrackWithMotionModel: the last frame's points (both cameras' slots), projected by the search
+        // itself (orbfe_search_by_projection_lastframe_pose: x3Dc = Tcw * x3Dw, mpCamera->project for the
+        // left window and for Trl * x3Dc, ORBmatcher.cc:1702-1718, 1794-1796); Rcw = I here, so Tcw is
+        // the quaternion (0, 0, 0, 1) with tcw = -Ow, and Trl the rig's baseline
         const auto t1 = std::chrono::steady_clock::now();
         if (have_last_) {
-            std::vector<orbfe_proj_point> pts;
-            std::vector<float> ruv;
-            const int NL = last_.nl;
+            std::vector<orbfe_last_point> pts;
             for (int i = 0; i < (int)last_.mvp.size(); i++) {
                 const int32_t id = last_.mvp[i];
                 if (id < 0) continue;
                 const MapPoint& p = points_[id];
-                orbfe_proj_point q;
+                orbfe_last_point q;
                 memset(&q, 0, sizeof(q));
-                const float xc = p.pos[0] - Ox, yc = p.pos[1], zc = p.pos[2];
-                q.invzc = 1.0f / zc;
-                kb8_project(kb_, xc, yc, zc, &q.u, &q.v);
-                q.valid = q.invzc >= 0;
+                memcpy(q.pos, p.pos, 12);
                 const orbfe_keypoint& kp = last_.keys[i];   // mvKeys[i] or mvKeysRight[i - Nleft]
                 q.octave = kp.octave;
                 q.angle = kp.angle;
                 q.observations = p.obs;
                 q.id = id;
+                q.valid = 1;
                 memcpy(q.desc, p.desc, 32);
-                float ur = 0.f, vr = 0.f;
-                if (q.valid) kb8_project(kb_, xc - b_, yc, zc, &ur, &vr);
-                ruv.push_back(ur);
-                ruv.push_back(vr);
                 pts.push_back(q);
-                (void)NL;
             }
+            orbfe_pose Tcw, Trl;
+            memset(&Tcw, 0, sizeof(Tcw));
+            memset(&Trl, 0, sizeof(Trl));
+            Tcw.q[3] = Trl.q[3] = 1.f;
+            Tcw.t[0] = -Ox;
+            Trl.t[0] = -b_;
+            const orbfe_camera_model cam = kb8_model(kb_);
             st.n_last_pts = (int)pts.size();
             st.sbp_th = 7;
-            st.sbp_matches = api_.sbp_last_stereo(&fr, cur.mvp.data(), obs.data(), pts.data(), ruv.data(),
-                                                  (int)pts.size(), 7.f);
+            st.sbp_matches = api_.sbp_last_pose(&fr, cur.mvp.data(), obs.data(), pts.data(), (int)pts.size(), &Tcw,
+                                                &Trl, &cam, 7.f);
             if (st.sbp_matches < 20) {
                 std::fill(cur.mvp.begin(), cur.mvp.end(), -1);
                 st.sbp_th = 14;
-                st.sbp_matches = api_.sbp_last_stereo(&fr, cur.mvp.data(), obs.data(), pts.data(), ruv.data(),
-                                                      (int)pts.size(), 14.f);
+                st.sbp_matches = api_.sbp_last_pose(&fr, cur.mvp.data(), obs.data(), pts.data(), (int)pts.size(),
+                                                    &Tcw, &Trl, &cam, 14.f);
             }
         }
         st.sbp_ms = ms_since(t1);

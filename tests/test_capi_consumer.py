@@ -184,8 +184,8 @@ def test_tracking_kb8_cpu_sequence(tracking_cpu_bin, seq_job_kb8, tmp_path):
 
 @pytest.mark.gpu
 def test_tracking_kb8_sequence_matches_cpu(consumer, tracking_cpu_bin, seq_job_kb8, tmp_path):
-    """The two-camera Tracking frame through the C-ABI (two orbfe_extract threads with vLappingArea
-    {0, 511}, orbfe_stereo_knn_ratio, orbfe_search_by_projection_lastframe_stereo,
+    """The two-camera Tracking frame through the C-ABI (both extractions with vLappingArea
+    {0, 511} and the kNN in one orbfe_frame_fisheye call, orbfe_search_by_projection_lastframe_pose,
     orbfe_search_local_points_track with a KannalaBrandt8 rig) over 24 frames, against the same loop
     on the CPU restatement: every frame's counts and both cameras' slots identical."""
     g, c = tmp_path / "gpu.out", tmp_path / "cpu.out"

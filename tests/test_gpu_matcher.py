@@ -489,6 +489,41 @@ def test_sbp_lastframe_two_cams_block(gpu, om, nl, nr, npts, copy_frac):
         np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("kind,nl,nr,npts", [
+    ("pinhole", 1000, 0, 1500),   # k_sbp_block<1> on device-projected records
+    ("pinhole", 1000, 0, 2100),   # beyond the block form: projected, then the multi-launch passes
+    ("kb8", 1000, 950, 1500),     # two cameras: k_sbp_block2 with both cameras' projections on the device
+    ("kb8", 1000, 950, 2100),
+])
+def test_sbp_lastframe_pose(gpu, om, kind, nl, nr, npts):
+    """SearchByProjection(CurrentFrame, LastFrame) with the projection on the device
+    (orbfe_search_by_projection_lastframe_pose, ORBmatcher.cc:1695-1718, 1794-1796: Sophus Tcw * x3Dw,
+    invzc in double, mpCamera->project for both cameras) against the oracle's projection + loop."""
+    from orb_slam3_ros_amd.matcher import CameraModel, Pose
+    rng = np.random.default_rng(nl + nr + npts + (7 if kind == "kb8" else 0))
+    if kind == "kb8":
+        F = sm.synth_frame_two(rng, nl, nr)
+        model = CameraModel.make("kb8", *sm.TUMVI_LEFT[:4], sm.TUMVI_LEFT[4])
+        Trl = Pose.se3(*sm.synth_pose(rng, 1.0, 0.05))
+    else:
+        F = sm.synth_frame(rng, nl)
+        model = CameraModel.make("pinhole", 458.654, 457.296, 367.215, 248.375)
+        Trl = None
+    R, t = sm.synth_pose(rng)
+    Tcw = Pose.se3(R, t)
+    pts = sm.synth_last_points(rng, F, model, R, t, npts)
+    mvp0, obs = sm.initial_slots(rng, F.N, 0.2)
+    total = 0
+    for th, check_ori, fw, bw in [(7, True, False, False), (15, False, True, False), (7, True, False, True)]:
+        a, b = mvp0.copy(), mvp0.copy()
+        ng = ORBmatcher(0.9, check_ori).SearchByProjectionLastFramePose(F, a, obs, pts, Tcw, model, th, fw, bw, Trl)
+        no = om.OracleMatcher(0.9, check_ori).sbp_lastframe_pose(F, b, obs, pts, Tcw, model, th, fw, bw, Trl)
+        assert ng == no, (th, ng, no)
+        np.testing.assert_array_equal(a, b)
+        total += no
+    assert total > 100
+
+
 def test_sbp_two_cams_keyframe_left_grid(gpu, om):
     """SearchByProjection(CurrentFrame, pKF) has no right-camera branch: a two-camera frame is
     searched through its left grid only (GetFeaturesInArea's default bRight = false)."""

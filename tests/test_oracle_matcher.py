@@ -668,3 +668,37 @@ def test_oracle_frustum_rig_vs_python(oracle_lib, two):
         count += (lv is not None) or (rv is not None)
     assert n == count and n > 150
     assert nr > 100 or not two
+
+
+@pytest.mark.parametrize("seed", [31, 32])
+def test_oracle_lastframe_pose_identity(oracle_lib, seed):
+    """The oracle's device-projection restatement (oro_sbp_lastframe_pose) with the identity rotation
+    and a pinhole camera, where Sophus' action reduces to x + t exactly: the projected records rebuilt
+    in numpy float32 (u = fx * x / z + cx, invzc = float(1.0 / double(z))) give the same search
+    through the host-projected entry point, slots included."""
+    from orb_slam3_ros_amd.matcher import PROJ_POINT_DTYPE, CameraModel, Pose
+    rng = np.random.default_rng(seed)
+    F = sm.synth_frame(rng, 800)
+    model = CameraModel.make("pinhole", 458.654, 457.296, 367.215, 248.375)
+    t = rng.normal(scale=0.3, size=3).astype(np.float32)
+    pts = sm.synth_last_points(rng, F, model, np.eye(3), t.astype(np.float64), 900)
+    Tcw = Pose.se3(np.eye(3), t)
+    assert list(Tcw.q) == [0.0, 0.0, 0.0, 1.0]
+    c = (pts["pos"] + t[None, :]).astype(np.float32)
+    rec = np.zeros(len(pts), PROJ_POINT_DTYPE)
+    for f in ("octave", "angle", "observations", "id", "valid", "desc"):
+        rec[f] = pts[f]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        rec["invzc"] = (1.0 / c[:, 2].astype(np.float64)).astype(np.float32)
+        fx, fy, cx, cy = (np.float32(v) for v in model.params[:4])
+        rec["u"] = np.where(rec["valid"] != 0, fx * c[:, 0] / c[:, 2] + cx, 0).astype(np.float32)
+        rec["v"] = np.where(rec["valid"] != 0, fy * c[:, 1] / c[:, 2] + cy, 0).astype(np.float32)
+    mvp0, obs = sm.initial_slots(rng, F.N, 0.2)
+    om = oracle_lib.OracleMatcher(0.9, True)
+    for th, fw, bw in [(7, False, False), (15, True, False)]:
+        a, b = mvp0.copy(), mvp0.copy()
+        na = om.sbp_lastframe_pose(F, a, obs, pts, Tcw, model, th, fw, bw)
+        nb = om.sbp_lastframe(F, b, obs, rec, th, fw, bw)
+        assert na == nb and na > 20
+        np.testing.assert_array_equal(a, b)
+
