@@ -21,6 +21,7 @@
 #include <orbfe.h>
 
 #include "orbfe_glue.h"
+#include "orbfe_slam_types.h"
 
 #include "Frame.h"
 #include "KeyFrame.h"
@@ -157,7 +158,8 @@ int ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoint
     return n;
 }
 
-// ORBmatcher.cc:1676-1887 (projection with Tcw stays on the host, as in the reference)
+// ORBmatcher.cc:1676-1887: the projection (Tcw * x3Dw, mpCamera->project for the left window and for
+// GetRelativePoseTrl() * x3Dc, :1702-1718, 1794-1796) runs on the device with the search
 int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, const float th, const bool bMono) {
     const Sophus::SE3f Tcw = CurrentFrame.GetPose();
     const Eigen::Vector3f twc = Tcw.inverse().translation();
@@ -168,17 +170,14 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, 
     Handles H;
     vector<int32_t> mvp, obs;
     slots_of(CurrentFrame, H, mvp, &obs);
-    vector<orbfe_proj_point> q(LastFrame.N);
-    vector<float> ruv(two ? 2 * (size_t)LastFrame.N : 0, 0.f);
+    vector<orbfe_last_point> q(LastFrame.N);
     for (int i = 0; i < LastFrame.N; i++) {
-        orbfe_proj_point& r = q[i];
+        orbfe_last_point& r = q[i];
         memset(&r, 0, sizeof(r));
         MapPoint* p = LastFrame.mvpMapPoints[i];
         if (!p || LastFrame.mvbOutlier[i]) continue;   // valid = 0
-        const Eigen::Vector3f x3Dc = Tcw * p->GetWorldPos();
-        r.invzc = 1.0 / x3Dc(2);
-        const Eigen::Vector2f uv = CurrentFrame.mpCamera->project(x3Dc);
-        r.u = uv(0); r.v = uv(1);
+        const Eigen::Vector3f x3Dw = p->GetWorldPos();
+        r.pos[0] = x3Dw(0); r.pos[1] = x3Dw(1); r.pos[2] = x3Dw(2);
         // nLastOctave and kpLF (:1721-1722, :1765-1767)
         r.octave = (LastFrame.Nleft == -1 || i < LastFrame.Nleft) ? LastFrame.mvKeys[i].octave
                                                                    : LastFrame.mvKeysRight[i - LastFrame.Nleft].octave;
@@ -187,22 +186,19 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, 
         r.observations = p->Observations();
         r.id = H.of(p);
         copy_desc(p->GetDescriptor(), r.desc);
-        if (two && !(r.invzc < 0)) {   // :1795-1796: the reference projects with mpCamera here too
-            const Eigen::Vector3f x3Dr = CurrentFrame.GetRelativePoseTrl() * x3Dc;
-            const Eigen::Vector2f uvr = CurrentFrame.mpCamera->project(x3Dr);
-            ruv[2 * i] = uvr(0);
-            ruv[2 * i + 1] = uvr(1);
-        }
     }
+    const orbfe_pose pcw = orbfe_shim::pose_of(Tcw);
+    const orbfe_pose prl = two ? orbfe_shim::pose_of(CurrentFrame.GetRelativePoseTrl()) : pcw;
+    const orbfe_camera_model cam = orbfe_shim::model_of(CurrentFrame.mpCamera);
     vector<cv::KeyPoint> keys;
     const orbfe_frame fr = frame_view(CurrentFrame, keys);
     const int n = orbfe_glue::on_current_frame(handle_of(CurrentFrame), two ? 0 : CurrentFrame.mnOrbfeFrameId, fr,
                                                [&](const orbfe_frame* V) {
-        return orbfe_search_by_projection_lastframe_stereo(V, mvp.data(), obs.data(), q.data(),
-                                                           two ? ruv.data() : nullptr, (int)q.size(), th, bForward,
-                                                           bBackward, mbCheckOrientation);
+        return orbfe_search_by_projection_lastframe_pose(V, mvp.data(), obs.data(), q.data(), (int)q.size(), &pcw,
+                                                         two ? &prl : nullptr, &cam, th, bForward, bBackward,
+                                                         mbCheckOrientation);
     });
-    if (failed(n, "orbfe_search_by_projection_lastframe_stereo"))
+    if (failed(n, "orbfe_search_by_projection_lastframe_pose"))
         return SearchByProjection_cpu(CurrentFrame, LastFrame, th, bMono);
     for (int i = 0; i < CurrentFrame.N; i++) CurrentFrame.mvpMapPoints[i] = H.at(mvp[i]);
     return n;

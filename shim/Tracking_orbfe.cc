@@ -25,6 +25,7 @@
 #include "ORBextractor.h"
 #include "ORBmatcher.h"
 #include "orbfe_glue.h"
+#include "orbfe_slam_types.h"
 
 using namespace std;
 
@@ -58,15 +59,6 @@ struct Handles {
     }
     MapPoint* at(int32_t h) const { return h < 0 ? nullptr : table[h]; }
 };
-
-orbfe_camera_model model_of(GeometricCamera* c) {   // GeometricCamera -> (mnType, mvParameters)
-    orbfe_camera_model m;
-    memset(&m, 0, sizeof(m));
-    m.type = c->GetType() == GeometricCamera::CAM_PINHOLE ? ORBFE_CAM_PINHOLE : ORBFE_CAM_KANNALA_BRANDT8;
-    const int np = m.type == ORBFE_CAM_PINHOLE ? 4 : 8;
-    for (int k = 0; k < np; k++) m.params[k] = c->getParameter(k);
-    return m;
-}
 
 void rowmajor(const Eigen::Matrix3f& R, float* out) {
     for (int r = 0; r < 3; r++)
@@ -163,9 +155,9 @@ void Tracking::SearchLocalPoints() {
     const orbfe_camera cam = orbfe_glue::camera(Rcw, tcw, Ow, 0.f, 0.f, 0.f, 0.f, F.mfLogScaleFactor, 0.5f);
     orbfe_stereo_rig rig;
     memset(&rig, 0, sizeof(rig));
-    rig.left = model_of(F.mpCamera);
+    rig.left = orbfe_shim::model_of(F.mpCamera);
     if (F.Nleft != -1) {
-        rig.right = model_of(F.mpCamera2);
+        rig.right = orbfe_shim::model_of(F.mpCamera2);
         const Sophus::SE3f Trl = F.GetRelativePoseTrl(), Tlr = F.GetRelativePoseTlr();
         rowmajor(Trl.rotationMatrix(), rig.Rrl);
         const Eigen::Vector3f trl = Trl.translation(), tlr = Tlr.translation();
