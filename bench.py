@@ -725,7 +725,8 @@ def config4_dist_leg(dev, rank, world, gloo, K=64, steps=10, warmup=3):
     steps batched per collective), the fisheye kNN + ratio of the step's K frames on
     the left rank against the partner's gathered slots, one step behind so the gather overlaps the
     next extraction. Frames/s = streams x K x steps / max-rank time. The left ranks' last step is
-    checked against the CPU oracle afterwards (4 frames)."""
+    checked against the CPU oracle afterwards (4 frames). With K = 1, ms_per_step is the per-frame
+    step time of the rig (a frame's kNN completes one step after its extraction)."""
     import torch
     import torch.distributed as dist
     from orb_slam3_ros_amd import distributed as odist
@@ -1043,13 +1044,19 @@ def main():
         del rout
     counts = fe.counts.cpu().numpy()
     nm = fe.nmatch.cpu().numpy()
-    c4 = None
+    c4 = c4k1 = None
     if world > 1 and world % 2 == 0 and not args.no_side_configs:
-        # config 4's own layout over the same ranks (after the config-2 measurement, not part of `value`)
+        # config 4's own layout over the same ranks (after the config-2 measurement, not part of `value`):
+        # K = 64 frames per collective (throughput), then K = 1 (one frame per step and all-gather: the
+        # per-frame cadence a live rig runs at)
         try:
             c4 = config4_dist_leg(dev, rank, world, gloo)
         except Exception as e:  # noqa: BLE001 - reported, never fatal to the config-2 line
             c4 = {"error": f"{type(e).__name__}: {e}"[:400]}
+        try:
+            c4k1 = config4_dist_leg(dev, rank, world, gloo, K=1, steps=60, warmup=5)
+        except Exception as e:  # noqa: BLE001
+            c4k1 = {"error": f"{type(e).__name__}: {e}"[:400]}
 
     if rank == 0:
         n_img = 2 * F
@@ -1139,6 +1146,8 @@ def main():
             result["rectify_remap"] = rect
         if c4 is not None:
             result["config4_multi_gpu"] = c4
+        if c4k1 is not None:
+            result["config4_multi_gpu_k1"] = c4k1
         if world == 1 and not args.no_side_configs:
             legs, all_ok = {}, True
             legs["config3"], ok3 = side_leg(dev, "KITTI-like stereo 1241x376, nFeatures 2000 (BASELINE config 3): "
