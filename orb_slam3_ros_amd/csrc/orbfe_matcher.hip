@@ -2689,11 +2689,14 @@ __global__ __launch_bounds__(MT_NT) void k_knn2(const uint32_t* L, int nl, const
 // the earlier train row (cv::BFMatcher's strict-less insertion). Outputs in the frame's full keypoint
 // numbering: l2r[f][i] = right keypoint index (trainIdx + monoRight) when Lowe's test passes, else -1;
 // dist[f][i] its Hamming distance or -1; ngood[f] += passed queries (zeroed by the launcher).
+// W waves per block split the train rows: 4 for batches (the grid fills the machine), 16 for a few
+// frames (the one-frame fisheye Frame: 16 blocks would otherwise leave each lane a 250-row chain)
 #define KNN_Q 64
-__global__ __launch_bounds__(256) void k_knn2_batch(StereoSide SL, StereoSide SR, int cap, float ratio,
-                                                    int* __restrict__ l2r, int* __restrict__ dist, int* ngood) {
+template <int W>
+__global__ __launch_bounds__(64 * W) void k_knn2_batch(StereoSide SL, StereoSide SR, int cap, float ratio,
+                                                       int* __restrict__ l2r, int* __restrict__ dist, int* ngood) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_train[];   // [cap][8]
-    __shared__ int s_part[4][KNN_Q][3];
+    __shared__ int s_part[W][KNN_Q][3];
     const int f = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int li = SL.base + f * SL.step, ri = SR.base + f * SR.step;
     const int nL = SL.counts[2 * li], monoL = SL.counts[2 * li + 1];
@@ -2708,14 +2711,14 @@ __global__ __launch_bounds__(256) void k_knn2_batch(StereoSide SL, StereoSide SR
     }
     const int nt = max(nR - monoR, 0);
     const uint32_t* rdesc = (const uint32_t*)(SR.desc + ((size_t)ri * cap + monoR) * 32);
-    for (int k = threadIdx.x; k < nt * 8; k += 256) s_train[k] = rdesc[k];
+    for (int k = threadIdx.x; k < nt * 8; k += 64 * W) s_train[k] = rdesc[k];
     const bool valid = q >= monoL && q < nL;
     uint32_t d[8];
     const uint32_t* ld = (const uint32_t*)(SL.desc + ((size_t)li * cap + (valid ? q : q0)) * 32);
 #pragma unroll
     for (int w = 0; w < 8; w++) d[w] = ld[w];
     SYNC();
-    const int j0 = (int)(((long)nt * wave) >> 2), j1 = (int)(((long)nt * (wave + 1)) >> 2);
+    const int j0 = (int)((long)nt * wave / W), j1 = (int)((long)nt * (wave + 1) / W);
     int d0 = MT_INF, d1 = MT_INF, t0 = -1;
     for (int j = j0; j < j1; j++) {
         const uint4 a = *(const uint4*)&s_train[8 * j];
@@ -2731,7 +2734,7 @@ __global__ __launch_bounds__(256) void k_knn2_batch(StereoSide SL, StereoSide SR
     SYNC();
     if (wave == 0) {
         // merge the later ranges into the running top-2: a later row wins only when strictly closer
-        for (int w = 1; w < 4; w++) {
+        for (int w = 1; w < W; w++) {
             const int b0 = s_part[w][lane][0], b1 = s_part[w][lane][1], bt = s_part[w][lane][2];
             if (b0 < d0) { d1 = min(d0, b1); d0 = b0; t0 = bt; }
             else d1 = min(d1, b0);
@@ -3989,6 +3992,18 @@ int orbfe_stereo_knn_ratio(const uint8_t* left_desc, int32_t nl, const uint8_t* 
     return good;
 }
 
+static void knn2_batch_launch(const StereoSide& SL, const StereoSide& SR, int cap, int nframes, float ratio,
+                              int32_t* d_l2r, int32_t* d_dist, int32_t* d_ngood, hipStream_t s) {
+    const size_t lds = (size_t)cap * 32;
+    const dim3 grid((cap + KNN_Q - 1) / KNN_Q, nframes);
+    if (nframes < 16)   // a few frames: the whole CU on each block's 64 queries
+        hipLaunchKernelGGL(k_knn2_batch<16>, grid, dim3(1024), lds, s, SL, SR, cap, ratio, (int*)d_l2r, (int*)d_dist,
+                           (int*)d_ngood);
+    else
+        hipLaunchKernelGGL(k_knn2_batch<4>, grid, dim3(256), lds, s, SL, SR, cap, ratio, (int*)d_l2r, (int*)d_dist,
+                           (int*)d_ngood);
+}
+
 int orbfe_stereo_knn_slabs(const int32_t* d_counts_l, const uint8_t* d_desc_l, int lbase, int lstep,
                            const int32_t* d_counts_r, const uint8_t* d_desc_r, int rbase, int rstep, int cap,
                            int nframes, float ratio, int32_t* d_l2r, int32_t* d_dist, int32_t* d_ngood, void* stream) {
@@ -4001,8 +4016,7 @@ int orbfe_stereo_knn_slabs(const int32_t* d_counts_l, const uint8_t* d_desc_l, i
     StereoSide SR{nullptr, 0, nullptr, 0, nullptr, d_desc_r, d_counts_r, rbase, rstep};
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipMemsetAsync(d_ngood, 0, (size_t)nframes * 4, s));
-    hipLaunchKernelGGL(k_knn2_batch, dim3((cap + KNN_Q - 1) / KNN_Q, nframes), dim3(256), lds, s, SL, SR, cap, ratio,
-                       (int*)d_l2r, (int*)d_dist, (int*)d_ngood);
+    knn2_batch_launch(SL, SR, cap, nframes, ratio, d_l2r, d_dist, d_ngood, s);
     HIPCHK(hipGetLastError());
     return ORBFE_OK;
 }
@@ -4024,8 +4038,7 @@ int orbfe_stereo_knn_batch(orbfe_extractor* left, int lbase, int lstep, orbfe_ex
                   right->last_desc, right->last_counts, rbase, rstep};
     hipStream_t s = pick_stream(left, stream);
     HIPCHK(hipMemsetAsync(d_ngood, 0, (size_t)nframes * 4, s));
-    hipLaunchKernelGGL(k_knn2_batch, dim3((cap + KNN_Q - 1) / KNN_Q, nframes), dim3(256), lds, s, SL, SR, cap, ratio,
-                       (int*)d_l2r, (int*)d_dist, (int*)d_ngood);
+    knn2_batch_launch(SL, SR, cap, nframes, ratio, d_l2r, d_dist, d_ngood, s);
     HIPCHK(hipGetLastError());
     return ORBFE_OK;
 }
