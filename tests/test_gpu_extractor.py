@@ -307,6 +307,16 @@ def test_frame_device_view_searches(gpu):
         gb = m.SearchByProjectionLastFrame(F, b, obs, pts, 7.0, fwd, bwd)
         assert ga == gb
         np.testing.assert_array_equal(a, b)
+    # the device-projected last-frame search (the shim's form) on the view as well
+    from orb_slam3_ros_amd.matcher import CameraModel, Pose
+    model = CameraModel.make("pinhole", fx, 457.296, 367.215, 248.375)
+    R, t = sm.synth_pose(rng)
+    lp = sm.synth_last_points(rng, F, model, R, t, 900)
+    a, b = mvp0.copy(), mvp0.copy()
+    ga = m.SearchByProjectionLastFramePose(V, a, obs, lp, Pose.se3(R, t), model, 7.0, False, False)
+    gb = m.SearchByProjectionLastFramePose(F, b, obs, lp, Pose.se3(R, t), model, 7.0, False, False)
+    assert ga == gb and ga > 0
+    np.testing.assert_array_equal(a, b)
     big = sm.synth_local_map(rng, F, 5000)   # > 2048 queries: not the one-workgroup path
     with pytest.raises(_lib.OrbfeError):
         m.SearchByProjectionLocalMap(V, mvp0.copy(), obs, big, 1.0)
