@@ -556,7 +556,7 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wq(FrameDev fr, const orbf
 __global__ __launch_bounds__(MT_BNT) void k_sbp_band(FrameDev fr, BandGrid bg, const orbfe_map_point* mps, int nq,
                                                      float th, int bFar, float thFar, float nnratio,
                                                      const int* blocked0, const int* first, int* assign, int* changed,
-                                                     PassIO io) {
+                                                     PassIO io, const int* fprev, int qshift) {
     extern __shared__ __attribute__((aligned(16))) uint8_t mt_sm[];
     if (pass_gated(io)) return;
     pass_fill(io);
@@ -566,6 +566,10 @@ __global__ __launch_bounds__(MT_BNT) void k_sbp_band(FrameDev fr, BandGrid bg, c
     uint4* s_desc = (uint4*)(s_kp + n);            // 2 x uint4 per band position
     int* s_gate = (int*)(s_desc + 2 * n);          // -1: blocked initially, else first[] (MT_INF: free)
     int* s_bs = s_gate + n;                        // bucket starts [nbk + 1]
+    // per bucket: the query bins (q >> qshift, 128 of them, two words) whose view of some keypoint of
+    // the bucket changed since the previous pass (fprev: that pass's first[]; nullptr: no skipping)
+    unsigned long long* s_cm = (unsigned long long*)(((uintptr_t)(s_bs + nbk + 1) + 7) & ~(uintptr_t)7);
+    int* s_gprev = (int*)(s_cm + 2 * nbk);         // fprev[] per band position
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, grp = lane >> 4, sl = lane & 15;
     for (int p = tid; p < n; p += MT_BNT) {
         const int idx = bg.bidx[p];
@@ -580,13 +584,42 @@ __global__ __launch_bounds__(MT_BNT) void k_sbp_band(FrameDev fr, BandGrid bg, c
         s_desc[2 * p] = d[0];
         s_desc[2 * p + 1] = d[1];
         s_gate[p] = blocked0[idx] ? -1 : first[idx];
+        if (fprev) s_gprev[p] = fprev[idx];
     }
     for (int b = tid; b <= nbk; b += MT_BNT) s_bs[b] = bg.bstart[b];
     SYNC();
+    // Passes >= 1 skip the queries whose candidates all kept their gate: candidate k is open to query q
+    // iff gate_k >= q, so a gate that moved from a to b changes it exactly for q in (min, max]. A
+    // query none of whose window buckets holds such a change in its bin computes the previous pass's
+    // result again (the same candidates, descriptors and gates), which assign[q] still holds.
+    if (fprev) {
+        for (int b = tid; b < nbk; b += MT_BNT) {
+            unsigned long long m0 = 0ull, m1 = 0ull;
+            for (int p = s_bs[b]; p < s_bs[b + 1]; p++) {
+                const int gc = s_gate[p];
+                if (gc < 0) continue;   // blocked in every pass
+                const int gp = s_gprev[p];
+                if (gp == gc) continue;
+                const int lo = min(gp, gc) + 1, hi = min(max(gp, gc), nq - 1);
+                if (lo > hi) continue;
+                const int blo = lo >> qshift, bhi = hi >> qshift;   // bins blo .. bhi of 0 .. 127
+                auto bits = [](int a, int z) -> unsigned long long {   // bits a .. z of one word, clipped
+                    if (z < 0 || a > 63) return 0ull;
+                    a = max(a, 0);
+                    return (z >= 63 ? ~0ull : ((2ull << z) - 1ull)) & ~((1ull << a) - 1ull);
+                };
+                m0 |= bits(blo, bhi);
+                m1 |= bits(blo - 64, bhi - 64);
+            }
+            s_cm[2 * b] = m0;
+            s_cm[2 * b + 1] = m1;
+        }
+        SYNC();
+    }
     constexpr int WPB = MT_BNT / 64;
     for (int q0 = (blockIdx.x * WPB + wave) * MT_QPW; q0 < nq; q0 += gridDim.x * WPB * MT_QPW) {
         const int q = q0 + grp;
-        int prev = -1, obs = 0, lvl = 0, s1 = 0, n1 = 0, s2 = 0, n2 = 0;
+        int prev = -1, obs = 0, lvl = 0, s1 = 0, n1 = 0, s2 = 0, n2 = 0, bk0 = 0, nbd = 0;
         float R = 0.f, x = 0.f, y = 0.f, xr = 0.f;
         uint32_t qd[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
         if (q < nq) {
@@ -612,10 +645,22 @@ __global__ __launch_bounds__(MT_BNT) void k_sbp_band(FrameDev fr, BandGrid bg, c
                         s1 = s_bs[(lvl - 1) * bg.NB + b0];
                         n1 = s_bs[(lvl - 1) * bg.NB + b1 + 1] - s1;
                     }
+                    nbd = b1 - b0 + 1;
+                    bk0 = (lvl >= 1 ? lvl - 1 : lvl) * bg.NB + b0;
                 }
             }
         }
-        const int tot = n1 + n2;
+        bool skip = false;
+        if (fprev) {   // the row's lanes test the window's buckets (both octaves) for a change in q's bin
+            const int nbt = lvl >= 1 ? 2 * nbd : nbd, bin = q >> qshift;
+            bool hit = false;
+            for (int i = sl; i < nbt; i += 16) {
+                const int bk = i < nbd ? bk0 + i : bk0 + bg.NB + (i - nbd);
+                hit = hit || ((s_cm[2 * bk + (bin >> 6)] >> (bin & 63)) & 1ull);
+            }
+            skip = ((__ballot(hit) >> (16 * grp)) & 0xFFFFull) == 0ull;
+        }
+        const int tot = skip ? 0 : n1 + n2;
         unsigned long long b1k = ~0ull, b2k = ~0ull;
         unsigned nwin = 0, npair = 0;
         const int totmax = mt_rows_max(tot);
@@ -658,6 +703,7 @@ __global__ __launch_bounds__(MT_BNT) void k_sbp_band(FrameDev fr, BandGrid bg, c
                     result = (int)((m1 >> 4) & 0x1FFFu);   // the keypoint index carried in the rank
             }
         }
+        if (skip) result = prev;
         if (sl == 0 && q < nq) {
             pass_publish(io, q, result, obs);
             if (result != prev) {
@@ -3516,7 +3562,9 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     // search (the per-frame Tracking calls) entirely in one workgroup, one launch (k_sbp_block), a
     // large local-map search as one multi-block pass per fixed-point step (k_sbp_band)
     const int band_nb = std::min(std::max((int)std::floor(F->max_y * (1.0f / MT_BAND_ROWS)) + 2, 1), 4096);
-    const bool band_ok = (size_t)F->nlevels * band_nb < 65535;   // 16-bit bucket keys
+    // 16-bit bucket keys, and k_sbp_band's LDS (frame, bucket starts, change bins) within 160 KB
+    const bool band_ok = (size_t)F->nlevels * band_nb < 65535 &&
+                         (size_t)n * 56 + (size_t)F->nlevels * band_nb * 20 + 32 <= 160 * 1024;
     BlkGeom gm;
     if (W == 1 && n <= MT_BAND_MAXN && blk_geom(F, gm)) {
         if (nq <= MT_BLOCK_MAXQ)
@@ -3575,6 +3623,7 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     const size_t o_first = p.scratch((size_t)n * 4);
     const size_t o_first1 = p.scratch((size_t)n * 4);   // rotating pass states (W == 1)
     const size_t o_first2 = p.scratch((size_t)n * 4);
+    const size_t o_first3 = p.scratch((size_t)n * 4);
     const size_t o_assign = p.scratch((size_t)nq * W * 4);
     const bool buckets = two && mode == 0;
     const size_t o_soff = buckets ? p.scratch((size_t)(n + 1) * 4) : 0;
@@ -3647,7 +3696,9 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
     if (W == 1) {
         // single camera: one gated kernel per pass (PassIO), a batch of passes and the gated commit
         // per host round trip; most searches converge within the first batch (2-4 passes)
-        int* fb[3] = {first, ms_ptr<int>(o_first1), ms_ptr<int>(o_first2)};   // fb[0], fb[1] = MT_INF (init)
+        // fb[0], fb[1] = MT_INF (init); four states so that pass p still sees its predecessor's
+        // (k_sbp_band's skip of unchanged queries) while it clears the state of pass p + 2
+        int* fb[4] = {first, ms_ptr<int>(o_first1), ms_ptr<int>(o_first2), ms_ptr<int>(o_first3)};
         // passes per round trip: as many as the previous search of this mode needed, plus one (a
         // gated pass costs a dispatch; an extra round trip costs far more)
         int batch = std::min(std::max(t_ms.pass_hint[mode] + 1, 2), 8);
@@ -3655,16 +3706,21 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
             const int pass0 = pass;
             for (int c = 0; c < batch; c++, pass++) {
                 if (pass >= MT_MAX_PASSES) return ORBFE_E_CAPACITY;
-                PassIO io{pass ? changed + pass - 1 : nullptr, fb[(pass + 1) % 3], fb[(pass + 2) % 3], n,
+                PassIO io{pass ? changed + pass - 1 : nullptr, fb[(pass + 1) % 4], fb[(pass + 2) % 4], n,
                           mode == 2 ? 0 : 1, stats};
-                const int* fcur = fb[pass % 3];
+                const int* fcur = fb[pass % 4];
+                // pass 1 sees nearly every gate move (free -> first claimer): skipping from pass 2 on
+                const int* fprev = pass >= 2 ? fb[(pass + 3) % 4] : nullptr;
                 if (use_band) {
                     const int qpb = (MT_BNT / 64) * MT_QPW;
                     const int nb = std::min((nq + qpb - 1) / qpb, 512);
                     const BandGrid bg{ms_ptr<int>(fp.bstart), ms_ptr<int>(fp.bidx), fp.band_nb, F->nlevels};
-                    const size_t lds = ((size_t)n * 52 + (size_t)(F->nlevels * fp.band_nb + 1) * 4 + 15) & ~(size_t)15;
+                    const size_t nbk = (size_t)F->nlevels * fp.band_nb;
+                    const size_t lds = ((size_t)n * 56 + (nbk + 1) * 4 + 8 + nbk * 16 + 15) & ~(size_t)15;
+                    int qshift = 0;
+                    while ((((nq - 1) >> qshift) >> 7) > 0) qshift++;   // 128 query bins
                     hipLaunchKernelGGL(k_sbp_band, dim3(nb), dim3(MT_BNT), lds, s, fr, bg, (const orbfe_map_point*)q, nq,
-                                       th, a0, thFar, nnratio, b0, fcur, assign, changed + pass, io);
+                                       th, a0, thFar, nnratio, b0, fcur, assign, changed + pass, io, fprev, qshift);
                 } else if (mode == 0 && th >= MT_WAVE_TH) {
                     const int qpb = (MT_WNT / 64) * MT_QPW;   // queries per block and round
                     const int nb = std::min((nq + qpb - 1) / qpb, 512);
