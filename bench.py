@@ -558,6 +558,96 @@ def matcher_config5_n(steps, n_kp):
             "per_th": out, "parity": {"ok": all_ok, "detail": "slots + nmatches identical to the CPU oracle per th"}}
 
 
+def matcher_calls(steps):
+    """The Tracking thread's other per-frame matcher calls at their own sizes, one host C-ABI call each
+    through the Python wrapper (inputs packed and uploaded, results back), with the kernels' device
+    time (HIP events), the CPU oracle's single-thread time on the same inputs and a parity check:
+      - MonocularInitialization: ORBmatcher(0.9, true).SearchForInitialization(mInitialFrame,
+        mCurrentFrame, mvbPrevMatched, mvIniMatches, 100) (Tracking.cc:2386) on 5000-feature frames
+        (the initial extractor's 5 x nFeatures);
+      - TrackReferenceKeyFrame: ORBmatcher(0.7, true).SearchByBoW(mpReferenceKF, mCurrentFrame)
+        (Tracking.cc:2836);
+      - Relocalization: ORBmatcher(0.75, true).SearchByBoW(pKF, mCurrentFrame) per candidate
+        (Tracking.cc:3765), then ORBmatcher(0.9, true).SearchByProjection(mCurrentFrame, pKF, sFound,
+        10, 100) (Tracking.cc:3818) and (..., 3, 64) (Tracking.cc:3838)."""
+    from oracle import oracle
+    from orb_slam3_ros_amd import synth_match as sm
+    from orb_slam3_ros_amd.matcher import ORBmatcher
+    oracle.build()
+    lib = ORBmatcher()._lib
+    rng = np.random.default_rng(4242)
+
+    def timed(gpu_call, cpu_call, check):
+        gpu_call()   # warm-up (buffers, grids)
+        t, dev = [], []
+        lib.orbfe_matcher_set_timing(1)
+        for _ in range(steps):
+            t0 = time.perf_counter()
+            g = gpu_call()
+            t.append(time.perf_counter() - t0)
+            dev.append(lib.orbfe_matcher_last_ms())
+        lib.orbfe_matcher_set_timing(0)
+        tc = []
+        for _ in range(max(3, min(steps, 10))):
+            t0 = time.perf_counter()
+            c = cpu_call()
+            tc.append(time.perf_counter() - t0)
+        ms, cms = 1e3 * float(np.median(t)), 1e3 * float(np.median(tc))
+        return {"ms_per_call": round(ms, 4), "device_ms_per_call": round(float(np.median(dev)), 4),
+                "cpu_ms_per_call": round(cms, 4), "speedup_vs_cpu": round(cms / ms, 2),
+                "parity_ok": bool(check(g, c))}
+
+    out = {}
+    # monocular initialisation, 5000 features, window 100
+    F1 = sm.synth_frame(rng, 5000, stereo=False)
+    F2, _ = sm.perturbed_frame(rng, F1, shift=(6.0, -4.0), jitter=2.0, rot=12.0, flip_p=0.06, drop=0.2)
+    prev0 = np.stack([F1.keys["x"], F1.keys["y"]], 1).astype(np.float32)
+
+    def sfi(m):
+        pv, m12 = prev0.copy(), np.zeros(F1.N, np.int32)
+        return m.SearchForInitialization(F1, F2, pv, m12, 100), pv, m12
+    og, oo = ORBmatcher(0.9, True), oracle.OracleMatcher(0.9, True)
+    out["search_for_initialization_5000"] = dict(
+        timed(lambda: sfi(og), lambda: (lambda pv, m12: (oo.search_for_init(F1, F2, pv, m12, 100), pv, m12))(
+            prev0.copy(), np.zeros(F1.N, np.int32)),
+              lambda g, c: g[0] == c[0] and np.array_equal(g[1], c[1]) and np.array_equal(g[2], c[2])),
+        features=int(F1.N), window=100)
+    # SearchByBoW(KF, F): reference keyframe (0.7) and relocalisation candidate (0.75), 1000 features
+    KF = sm.synth_frame(rng, 1000, stereo=False)
+    F, src = sm.perturbed_frame(rng, KF, rot=20.0, flip_p=0.05, drop=0.15)
+    kf_mp = np.where(rng.random(KF.N) < 0.25, -1, np.arange(KF.N) + 100).astype(np.int32)
+    fk, ff = sm.synth_bow(rng, 400, KF, F, src)
+    for name, ratio in (("search_by_bow_track_reference_kf", 0.7), ("search_by_bow_relocalisation", 0.75)):
+        g_m, o_m = ORBmatcher(ratio, True), oracle.OracleMatcher(ratio, True)
+        out[name] = dict(timed(lambda: g_m.SearchByBoW(KF.keys, KF.desc, kf_mp, fk, F, ff),
+                               lambda: o_m.search_by_bow(KF.keys, KF.desc, kf_mp, fk, F, ff),
+                               lambda g, c: g[0] == c[0] and np.array_equal(g[1], c[1])),
+                         kf_features=int(KF.N), frame_features=int(F.N), bow_nodes=400)
+    # relocalisation's SearchByProjection(F, KF, sFound, th, ORBdist): the candidate keyframe's points
+    Fr = sm.synth_frame(rng, 1000, stereo=False)
+    pts = sm.synth_proj_points(rng, Fr, 1200, copy_frac=0.7)
+    mvp0, _ = sm.initial_slots(rng, Fr.N, 0.25)
+    g_m, o_m = ORBmatcher(0.9, True), oracle.OracleMatcher(0.9, True)
+    for th, orbdist in ((10, 100), (3, 64)):
+        def gk():
+            a = mvp0.copy()
+            return g_m.SearchByProjectionKeyFrame(Fr, a, pts, th, orbdist), a
+
+        def ck():
+            b = mvp0.copy()
+            return o_m.sbp_kf(Fr, b, pts, th, orbdist), b
+        out[f"search_by_projection_keyframe_th{th}"] = dict(
+            timed(gk, ck, lambda g, c: g[0] == c[0] and np.array_equal(g[1], c[1])),
+            frame_features=int(Fr.N), kf_points=int(len(pts)), ORBdist=orbdist)
+    return {"workload": "synthetic Tracking-sized inputs, seed 4242 (sm.synth_frame / perturbed_frame / synth_bow / "
+                        "synth_proj_points)",
+            "timing": "median over the calls: ms_per_call = the wrapper's host C-ABI call (inputs packed and "
+                      "uploaded, results back); device_ms_per_call = its kernels (HIP events); cpu_ms_per_call = the "
+                      "oracle restatement on one host thread, same inputs",
+            "calls": out, "parity": {"ok": all(v["parity_ok"] for v in out.values()),
+                                     "detail": "counts and outputs identical to the CPU oracle per call"}}
+
+
 def make_images(rank, W, H, F, U, dev, seed0=0):
     """Interleaved [2F, H, W] device tensor of U distinct synthetic stereo pairs tiled over F frames
     (frame f = pair f % U); returns (images, host pairs, frame -> pair map)."""
@@ -1177,7 +1267,9 @@ def main():
             if world == 1 and not args.no_side_configs:
                 c5b = matcher_config5_n(max(5, args.matcher_steps // 5), 5000)
                 result["matcher_config5_n5000"] = c5b
-                if not c5b["parity"]["ok"]:
+                mc = matcher_calls(max(10, args.matcher_steps // 2))
+                result["matcher_calls"] = mc
+                if not (c5b["parity"]["ok"] and mc["parity"]["ok"]):
                     print(json.dumps(result), file=sys.stderr, flush=True)
                     sys.exit(3)
         if args.dropin_frames > 0 and world == 1:

@@ -145,9 +145,13 @@ __device__ __forceinline__ int mt_band_of(float y, int NB) {
 }
 __global__ __launch_bounds__(1024) void k_mt_grid(const OrbKeyPoint* keys, int n, int nleft, float minx, float miny,
                                                   float invw, float invh, int* cstart, int* cidx, int gstride_c,
-                                                  int gstride_i, int ngrids, SbpInit ia, BandGrid band) {
+                                                  int gstride_i, int ngrids, SbpInit ia, BandGrid band, int gfirst) {
     __shared__ uint32_t s_k[MT_GRID_MAXN];
-    const int gi = blockIdx.x;
+    __shared__ int s_m;
+    // blocks: grids gfirst .. ngrids - 1 (a search that reads only level grids skips the full one), the
+    // band index, then the search initialisation
+    const int nbg = ngrids - gfirst;
+    const int gi = (int)blockIdx.x < nbg ? (int)blockIdx.x + gfirst : (int)blockIdx.x - nbg + ngrids;
     const int tid = threadIdx.x;
     const int nband = band.bstart ? 1 : 0;
     if (gi >= ngrids + nband) {
@@ -164,18 +168,18 @@ __global__ __launch_bounds__(1024) void k_mt_grid(const OrbKeyPoint* keys, int n
         cstart += (size_t)gi * gstride_c;
         cidx += (size_t)gi * gstride_i;
     }
-    int P = 64;
-    while (P < n) P <<= 1;
-    const int R = (P + 1023) >> 10;
     const int ncells = is_band ? band.nlev * band.NB : nleft >= 0 ? 2 * MT_NCELL : MT_NCELL;
-    uint32_t v[MT_GRID_R];
-#pragma unroll
-    for (int r = 0; r < MT_GRID_R; r++) {
-        const int i = tid + (r << 10);
-        uint32_t key = 0xFFFFFFFFu;
-        if (r < R && i < n) {
+    // the keys of the grid's keypoints, appended in any order (the (cell, index) sort restores it);
+    // a level grid holds a fraction of the frame, so it sorts fewer keys. The band index keeps every
+    // keypoint (k_sbp_band stages all n positions).
+    if (tid == 0) s_m = 0;
+    SYNC();
+    // wave-aggregated appends (one LDS atomic per wave and round, positions by mbcnt)
+    for (int i0 = 0; i0 < n; i0 += blockDim.x) {
+        const int i = i0 + tid;
+        uint32_t cell = (uint32_t)ncells;   // outside the grid: never a candidate (PosInGrid false)
+        if (i < n) {
             const OrbKeyPoint kp = keys[i];
-            uint32_t cell = (uint32_t)ncells;   // outside the grid: never a candidate (PosInGrid false)
             if (is_band) {
                 // a two-camera frame's single-camera searches (SearchByProjection(CurrentFrame, pKF))
                 // read its left grid only: the right rows [nleft, n) are in no bucket
@@ -188,10 +192,27 @@ __global__ __launch_bounds__(1024) void k_mt_grid(const OrbKeyPoint* keys, int n
                     kp.octave <= lvhi)
                     cell = (uint32_t)(px * ORBFE_GRID_ROWS + py + (nleft >= 0 && i >= nleft ? MT_NCELL : 0));
             }
-            key = (cell << 16) | (uint32_t)i;
         }
-        v[r] = key;
+        const bool keep = i < n && (is_band || cell < (uint32_t)ncells);
+        const unsigned long long bm = __ballot(keep);
+        const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+        int base = 0;
+        if ((threadIdx.x & 63) == 0 && bm) base = atomicAdd(&s_m, __popcll(bm));
+        base = __shfl(base, 0, 64);
+        if (keep) s_k[base + below] = (cell << 16) | (uint32_t)i;
     }
+    SYNC();
+    const int m = s_m;
+    int P = 64;
+    while (P < m) P <<= 1;
+    const int R = (P + 1023) >> 10;
+    uint32_t v[MT_GRID_R];
+#pragma unroll
+    for (int r = 0; r < MT_GRID_R; r++) {
+        const int i = tid + (r << 10);
+        v[r] = (r < R && i < m) ? s_k[i] : 0xFFFFFFFFu;
+    }
+    SYNC();   // every key is in registers before the sort's first LDS round overwrites s_k
     // the intra-wave stages j = min(k/2, 32) .. 1 of one k, on registers (elements >= P pair only
     // among themselves: j < P keeps i ^ j on the same side of P)
     auto wave_stages = [&](int k) {
@@ -226,9 +247,9 @@ __global__ __launch_bounds__(1024) void k_mt_grid(const OrbKeyPoint* keys, int n
     for (int r = 0; r < MT_GRID_R; r++)
         if (r < R) s_k[tid + (r << 10)] = v[r];
     SYNC();
-    for (int i = tid; i < n; i += blockDim.x) cidx[i] = (int)(s_k[i] & 0xFFFFu);
+    for (int i = tid; i < m; i += blockDim.x) cidx[i] = (int)(s_k[i] & 0xFFFFu);
     for (int c = tid; c <= ncells; c += blockDim.x) {
-        int lo = 0, hi = n;   // first position with cell >= c
+        int lo = 0, hi = m;   // first position with cell >= c
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
             if ((int)(s_k[mid] >> 16) < c) lo = mid + 1; else hi = mid;
@@ -2510,11 +2531,14 @@ __global__ void k_mt_commit_write(int n, const int* qid, int q_stride_bytes, con
 // minimum). The state table is rebuilt every pass: (i2 << 16 | j) keys sorted + segmented
 // prefix-min of the selecting distances.
 #define MT_INIT_MAXQ 8192
+// Per candidate i2 the table also keeps its segment (seg_off, seg_cnt; n2 entries, cleared here), so a
+// query walks the few selectors of its candidate instead of a binary search over the whole table.
 __global__ __launch_bounds__(1024) void k_init_state(const int* assign, const int* adist, int nq, uint32_t* skey,
-                                                     int* spmin, int* nsel) {
+                                                     int* spmin, int* nsel, int n2, int* seg_off, int* seg_cnt) {
     __shared__ uint32_t s_k[MT_INIT_MAXQ];
     __shared__ int s_cnt;
     if (threadIdx.x == 0) s_cnt = 0;
+    for (int i = threadIdx.x; i < n2; i += blockDim.x) seg_cnt[i] = 0;
     SYNC();
     for (int j = threadIdx.x; j < nq; j += blockDim.x)
         if (assign[j] >= 0) s_k[atomicAdd(&s_cnt, 1)] = ((uint32_t)assign[j] << 16) | (uint32_t)j;
@@ -2539,47 +2563,96 @@ __global__ __launch_bounds__(1024) void k_init_state(const int* assign, const in
     for (int i = threadIdx.x; i < m; i += blockDim.x) {
         skey[i] = s_k[i];
         if (i == 0 || (s_k[i - 1] >> 16) != (s_k[i] >> 16)) {
-            int cur = MT_INF;
-            for (int t = i; t < m && (s_k[t] >> 16) == (s_k[i] >> 16); t++) {
+            int cur = MT_INF, t = i;
+            for (; t < m && (s_k[t] >> 16) == (s_k[i] >> 16); t++) {
                 cur = min(cur, adist[s_k[t] & 0xFFFFu]);
                 spmin[t] = cur;
             }
+            seg_off[s_k[i] >> 16] = i;
+            seg_cnt[s_k[i] >> 16] = t - i;
         }
     }
     if (threadIdx.x == 0) *nsel = m;
 }
 
-__global__ __launch_bounds__(MT_NT) void k_init_eval(FrameDev f1, FrameDev f2, const float* prev, int windowSize,
-                                                     float nnratio, const uint32_t* skey, const int* spmin,
-                                                     const int* nsel, int* assign, int* adist, int* changed) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= f1.n) return;
-    int result = -1, rdist = 0;
-    const int m = *nsel;
-    const OrbKeyPoint kp1 = f1.keys[q];
-    if (kp1.octave <= 0) {
-        const int level1 = kp1.octave;
-        uint8_t d1[32];
-        memcpy(d1, f1.desc + 8 * q, 32);
-        int bestDist = MT_INF, bestDist2 = MT_INF, bestIdx2 = -1;
-        // only level-0 queries reach here: the octave-0 grid holds exactly the level-0 candidates
-        mt_for_area(f2, f2.pcstart, f2.pcidx, prev[2 * q], prev[2 * q + 1], (float)windowSize, level1, level1,
-                    [&](int i2, const OrbKeyPoint&) {
-            const int dist = mt_hamming(d1, f2.desc + 8 * i2);
-            // vMatchedDistance[i2] as seen by query q: last selector j < q of i2
-            int lo = 0, hi = m;   // first key >= (i2 << 16 | q)
-            const uint32_t target = ((uint32_t)i2 << 16) | (uint32_t)q;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (skey[mid] < target) lo = mid + 1; else hi = mid;
+// One query per DPP row of 16 lanes (four per wave): lane l walks the window's grid columns
+// nMinCellX + l, + l + 16, ... (GetFeaturesInArea, Frame.cc:657-723, one contiguous CSR run per column)
+// and keeps its two smallest (dist, CSR position) keys; the CSR position is the reference's
+// enumeration order, so the row minimum is its first best and the second minimum its bestDist2.
+// A thread per query left most of the machine idle (5,000 queries = 20 blocks) behind a chain of
+// dependent loads per candidate.
+#define MT_INIT_WNT 256
+__global__ __launch_bounds__(MT_INIT_WNT) void k_init_eval(FrameDev f1, FrameDev f2, const float* prev, int windowSize,
+                                                           float nnratio, const uint32_t* skey, const int* spmin,
+                                                           const int* seg_off, const int* seg_cnt, int* assign,
+                                                           int* adist, int* changed) {
+    const int lane = threadIdx.x & 63, grp = lane >> 4, sl = lane & 15;
+    const int q = (blockIdx.x * (MT_INIT_WNT / 64) + (threadIdx.x >> 6)) * 4 + grp;
+    const bool qv = q < f1.n;
+    int level1 = 1;
+    float x = 0.f, y = 0.f;
+    uint32_t d1[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    if (qv) {
+        level1 = f1.keys[q].octave;
+        if (level1 <= 0) {
+            x = prev[2 * q];
+            y = prev[2 * q + 1];
+#pragma unroll
+            for (int w = 0; w < 8; w++) d1[w] = f1.desc[8 * q + w];
+        }
+    }
+    const float r = (float)windowSize;
+    int cx0 = 0, cx1 = -1, cy0 = 0, cy1 = -1;
+    if (qv && level1 <= 0) {
+        cx0 = max(0, (int)floorf((x - f2.minx - r) * f2.invw));
+        cx1 = min(ORBFE_GRID_COLS - 1, (int)ceilf((x - f2.minx + r) * f2.invw));
+        cy0 = max(0, (int)floorf((y - f2.miny - r) * f2.invh));
+        cy1 = min(ORBFE_GRID_ROWS - 1, (int)ceilf((y - f2.miny + r) * f2.invh));
+        if (cx0 >= ORBFE_GRID_COLS || cx1 < 0 || cy0 >= ORBFE_GRID_ROWS || cy1 < 0) cx1 = cx0 - 1;
+    }
+    const bool bCheckLevels = (level1 > 0) || (level1 >= 0);
+    // only level-0 queries search: the octave-0 grid (pcstart) holds exactly the level-0 candidates
+    const int* cs = f2.pcstart;
+    const int* ci = f2.pcidx;
+    unsigned long long b1 = ~0ull, b2 = ~0ull;
+    for (int ix = cx0 + sl; ix <= cx1; ix += 16) {
+        const int j1 = cs[ix * ORBFE_GRID_ROWS + cy1 + 1];
+        for (int j = cs[ix * ORBFE_GRID_ROWS + cy0]; j < j1; j++) {
+            const int i2 = ci[j];
+            const OrbKeyPoint kp = f2.keys[i2];
+            if (bCheckLevels) {
+                if (kp.octave < level1) continue;
+                if (level1 >= 0 && kp.octave > level1) continue;
             }
+            if (!(fabsf(kp.x - x) < r && fabsf(kp.y - y) < r)) continue;
+            int dist = 0;
+#pragma unroll
+            for (int w = 0; w < 8; w++) dist += __popc(d1[w] ^ f2.desc[8 * i2 + w]);
+            // vMatchedDistance[i2] as seen by query q: the prefix minimum at the last selector j < q of
+            // i2 (its segment lists the selectors in j order; most candidates have none or one)
             int md = MT_INF;
-            if (lo > 0 && (skey[lo - 1] >> 16) == (uint32_t)i2) md = spmin[lo - 1];
-            if (md <= dist) return;
-            if (dist < bestDist) { bestDist2 = bestDist; bestDist = dist; bestIdx2 = i2; }
-            else if (dist < bestDist2) bestDist2 = dist;
-        });
-        if (bestDist <= MT_TH_LOW && bestDist < (float)bestDist2 * nnratio) { result = bestIdx2; rdist = bestDist; }
+            const int sc = seg_cnt[i2];
+            if (sc) {
+                const int so = seg_off[i2];
+                for (int t = so; t < so + sc && (int)(skey[t] & 0xFFFFu) < q; t++) md = spmin[t];
+            }
+            if (md <= dist) continue;
+            const unsigned long long k = ((unsigned long long)dist << 32) | (unsigned)j;
+            if (k < b1) { b2 = b1; b1 = k; }
+            else if (k < b2) b2 = k;
+        }
+    }
+    const unsigned long long m1 = mt_row_min64(b1);
+    const unsigned long long m2 = mt_row_min64(b1 == m1 ? b2 : b1);
+    if (sl != 0 || !qv) return;
+    int result = -1, rdist = 0;
+    if (m1 != ~0ull) {
+        const int bestDist = (int)(m1 >> 32);
+        const int bestDist2 = m2 != ~0ull ? (int)(m2 >> 32) : MT_INF;
+        if (bestDist <= MT_TH_LOW && bestDist < (float)bestDist2 * nnratio) {
+            result = ci[(int)(m1 & 0xFFFFFFFFu)];
+            rdist = bestDist;
+        }
     }
     if (result != assign[q] || (result >= 0 && rdist != adist[q])) {
         assign[q] = result;
@@ -2695,6 +2768,114 @@ __global__ __launch_bounds__(1024) void k_bow_commit(const OrbKeyPoint* kf_keys,
     atomicAdd(&s_n, cnt);
     SYNC();
     if (threadIdx.x == 0) result[0] = s_n;
+}
+
+// SearchByBoW(KF, F) in ONE workgroup (the Tracking thread's TrackReferenceKeyFrame / Relocalization
+// calls, Tracking.cc:2836,3765): both descriptor sets, the node lists and the match state in LDS, the
+// node walks of k_bow_nodes (same order, same two-camera rule) reading LDS only, and k_bow_commit's
+// rotation histogram in the same block. One launch; the multi-launch pair above serves the sets
+// that do not fit.
+#define MT_BOW_NT 1024
+struct BowBlockIn {
+    const int* pairs;
+    int npairs;
+    const int* kf_off;
+    const uint32_t* kf_idx;
+    int kf_nodes, nki;
+    const int* f_off;
+    const uint32_t* f_idx;
+    int f_nodes, nfi;
+    const int32_t* kf_mp;
+    const uint4* kf_desc;
+    const uint4* f_desc;
+    const OrbKeyPoint* kf_keys;
+    const OrbKeyPoint* f_keys;
+    int kf_n, fn, nleft, checkOri;
+    float nnratio;
+};
+__host__ __device__ inline size_t bow_block_lds(int kf_n, int fn, int kf_nodes, int nki, int f_nodes, int nfi, int npairs) {
+    return (size_t)(kf_n + fn) * 32 + (size_t)(fn + kf_n) * 4 +
+           (size_t)(kf_nodes + 1 + nki + f_nodes + 1 + nfi + 2 * npairs) * 4 + 16;
+}
+__global__ __launch_bounds__(MT_BOW_NT) void k_bow_block(BowBlockIn in, int* out, int* result) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t bw_sm[];
+    __shared__ int s_hist[MT_HISTO];
+    __shared__ unsigned s_keep;
+    __shared__ int s_n;
+    const int tid = threadIdx.x;
+    uint4* s_kd = (uint4*)bw_sm;                 // KF descriptors [kf_n][2]
+    uint4* s_fd = s_kd + 2 * in.kf_n;            // F descriptors [fn][2]
+    int* s_src = (int*)(s_fd + 2 * in.fn);       // F index -> matched KF index (-1)
+    int* s_mp = s_src + in.fn;                   // KF map point slot
+    int* s_kfo = s_mp + in.kf_n;
+    int* s_kfi = s_kfo + in.kf_nodes + 1;
+    int* s_fo = s_kfi + in.nki;
+    int* s_fi = s_fo + in.f_nodes + 1;
+    int* s_pr = s_fi + in.nfi;
+    for (int i = tid; i < 2 * in.kf_n; i += MT_BOW_NT) s_kd[i] = in.kf_desc[i];
+    for (int i = tid; i < 2 * in.fn; i += MT_BOW_NT) s_fd[i] = in.f_desc[i];
+    for (int i = tid; i < in.fn; i += MT_BOW_NT) s_src[i] = -1;
+    for (int i = tid; i < in.kf_n; i += MT_BOW_NT) s_mp[i] = in.kf_mp[i];
+    for (int i = tid; i <= in.kf_nodes; i += MT_BOW_NT) s_kfo[i] = in.kf_off[i];
+    for (int i = tid; i < in.nki; i += MT_BOW_NT) s_kfi[i] = (int)in.kf_idx[i];
+    for (int i = tid; i <= in.f_nodes; i += MT_BOW_NT) s_fo[i] = in.f_off[i];
+    for (int i = tid; i < in.nfi; i += MT_BOW_NT) s_fi[i] = (int)in.f_idx[i];
+    for (int i = tid; i < 2 * in.npairs; i += MT_BOW_NT) s_pr[i] = in.pairs[i];
+    if (tid < MT_HISTO) s_hist[tid] = 0;
+    if (tid == 0) s_n = 0;
+    SYNC();
+    // one thread per node present in both vectors (ORBmatcher.cc:244-371): an F index belongs to one
+    // node only, so the "already matched" skip stays inside the thread's own walk
+    for (int t = tid; t < in.npairs; t += MT_BOW_NT) {
+        const int a = s_pr[2 * t], b = s_pr[2 * t + 1];
+        const int fb0 = s_fo[b], fb1 = s_fo[b + 1];
+        for (int ia = s_kfo[a]; ia < s_kfo[a + 1]; ia++) {
+            const int realIdxKF = s_kfi[ia];
+            if (s_mp[realIdxKF] < 0) continue;
+            const uint4 k0 = s_kd[2 * realIdxKF], k1 = s_kd[2 * realIdxKF + 1];
+            int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
+            int bestDist1R = 256, bestIdxFR = -1;
+            for (int ib = fb0; ib < fb1; ib++) {
+                const int realIdxF = s_fi[ib];
+                if (s_src[realIdxF] >= 0) continue;
+                const uint4 f0 = s_fd[2 * realIdxF], f1 = s_fd[2 * realIdxF + 1];
+                const int dist = __popc(k0.x ^ f0.x) + __popc(k0.y ^ f0.y) + __popc(k0.z ^ f0.z) + __popc(k0.w ^ f0.w) +
+                                 __popc(k1.x ^ f1.x) + __popc(k1.y ^ f1.y) + __popc(k1.z ^ f1.z) + __popc(k1.w ^ f1.w);
+                if (in.nleft < 0 || realIdxF < in.nleft) {
+                    if (dist < bestDist1) { bestDist2 = bestDist1; bestDist1 = dist; bestIdxF = realIdxF; }
+                    else if (dist < bestDist2) bestDist2 = dist;
+                } else if (dist < bestDist1R) {
+                    bestDist1R = dist;
+                    bestIdxFR = realIdxF;
+                }
+            }
+            if (bestDist1 <= MT_TH_LOW) {
+                if (static_cast<float>(bestDist1) < in.nnratio * static_cast<float>(bestDist2)) s_src[bestIdxF] = realIdxKF;
+                if (bestDist1R <= MT_TH_LOW) s_src[bestIdxFR] = realIdxKF;
+            }
+        }
+    }
+    SYNC();
+    // rotation consistency (ORBmatcher.cc:373-395) and the output (k_bow_commit)
+    for (int i = tid; i < in.fn; i += MT_BOW_NT) {
+        const int sidx = s_src[i];
+        if (sidx >= 0 && in.checkOri) atomicAdd(&s_hist[mt_rot_bin(in.kf_keys[sidx].angle, in.f_keys[i].angle)], 1);
+    }
+    SYNC();
+    if (tid == 0) s_keep = in.checkOri ? mt_three_maxima_keep(s_hist) : 0xFFFFFFFFu;
+    SYNC();
+    int cnt = 0;
+    for (int i = tid; i < in.fn; i += MT_BOW_NT) {
+        const int sidx = s_src[i];
+        int o = -1;
+        if (sidx >= 0 && (!in.checkOri || ((s_keep >> mt_rot_bin(in.kf_keys[sidx].angle, in.f_keys[i].angle)) & 1u)))
+            o = s_mp[sidx];
+        out[i] = o;
+        cnt += o >= 0 ? 1 : 0;
+    }
+    atomicAdd(&s_n, cnt);
+    SYNC();
+    if (tid == 0) result[0] = s_n;
 }
 
 // ---- ComputeStereoFishEyeMatches' knnMatch(k=2) + ratio (Frame.cc:1144-1151) ----
@@ -2962,6 +3143,7 @@ struct FramePlan {
         (void)want_grid;
     }
     int ngrids = 1;
+    int gfirst = 0;   // grids below gfirst are not built (a search that reads only level grids)
     // k_sbp_band's (octave, band) index, built by the grid launch when planned (plan_band)
     bool band = false;
     int band_nb = 0;
@@ -3021,9 +3203,9 @@ struct FramePlan {
         const int nib = (sbp_init_extent(ia) + 1023) / 1024;
         BandGrid bg{nullptr, nullptr, 0, 0};
         if (band) bg = BandGrid{ms_ptr<int>(bstart), ms_ptr<int>(bidx), band_nb, F->nlevels};
-        hipLaunchKernelGGL(k_mt_grid, dim3(ngrids + (band ? 1 : 0) + nib), dim3(1024), 0, s, v.keys, v.n, v.nleft,
-                           v.minx, v.miny, v.invw, v.invh, (int*)v.cstart, (int*)v.cidx, v.gstride_c, v.gstride_i,
-                           ngrids, ia, bg);
+        hipLaunchKernelGGL(k_mt_grid, dim3(ngrids - gfirst + (band ? 1 : 0) + nib), dim3(1024), 0, s, v.keys, v.n,
+                           v.nleft, v.minx, v.miny, v.invw, v.invh, (int*)v.cstart, (int*)v.cidx, v.gstride_c,
+                           v.gstride_i, ngrids, ia, bg, gfirst);
     }
 };
 
@@ -3900,11 +4082,14 @@ int orbfe_search_for_initialization(const orbfe_frame* F1, const orbfe_frame* F2
     const size_t o_prev = p.upload(prev_matched, (size_t)n1 * 8);
     f1p.cstart = f1p.cidx = 0;
     f2p.plan_grid(p, 2);
+    f2p.gfirst = 1;   // k_init_eval reads the octave-0 grid only
     const size_t o_assign = p.scratch((size_t)n1 * 4);
     const size_t o_adist = p.scratch((size_t)n1 * 4);
     const size_t o_skey = p.scratch((size_t)n1 * 4);
     const size_t o_spmin = p.scratch((size_t)n1 * 4);
     const size_t o_nsel = p.scratch(4);
+    const size_t o_segoff = p.scratch((size_t)F2->n * 4);
+    const size_t o_segcnt = p.scratch((size_t)F2->n * 4);
     const size_t o_changed = p.scratch(MT_MAX_PASSES * 4);
     const size_t o_m12 = p.scratch((size_t)n1 * 4);
     const size_t o_result = p.scratch(16);
@@ -3920,16 +4105,17 @@ int orbfe_search_for_initialization(const orbfe_frame* F1, const orbfe_frame* F2
     HIPCHK(hipMemsetAsync(changed, 0, MT_MAX_PASSES * 4, s));
     fill(assign, n1, -1);
     fill(adist, n1, 0);
-    const dim3 gq((n1 + MT_NT - 1) / MT_NT);
+    const dim3 gq((n1 + MT_INIT_WNT / 16 - 1) / (MT_INIT_WNT / 16));   // four queries per wave
     int pass = 0;
     while (true) {
         for (int c = 0; c < 2; c++, pass++) {
             if (pass >= MT_MAX_PASSES) return ORBFE_E_CAPACITY;
             hipLaunchKernelGGL(k_init_state, dim3(1), dim3(1024), 0, s, assign, adist, n1, ms_ptr<uint32_t>(o_skey),
-                               ms_ptr<int>(o_spmin), ms_ptr<int>(o_nsel));
-            hipLaunchKernelGGL(k_init_eval, gq, dim3(MT_NT), 0, s, v1, v2, ms_ptr<const float>(o_prev), windowSize,
+                               ms_ptr<int>(o_spmin), ms_ptr<int>(o_nsel), F2->n, ms_ptr<int>(o_segoff),
+                               ms_ptr<int>(o_segcnt));
+            hipLaunchKernelGGL(k_init_eval, gq, dim3(MT_INIT_WNT), 0, s, v1, v2, ms_ptr<const float>(o_prev), windowSize,
                                nnratio, ms_ptr<const uint32_t>(o_skey), ms_ptr<const int>(o_spmin),
-                               ms_ptr<const int>(o_nsel), assign, adist, changed + pass);
+                               ms_ptr<const int>(o_segoff), ms_ptr<const int>(o_segcnt), assign, adist, changed + pass);
         }
         int ch = 0;
         HIPCHK(hipMemcpyAsync(t_ms.hs, changed + pass - 1, 4, hipMemcpyDeviceToHost, s));   // pinned
@@ -4004,6 +4190,15 @@ int orbfe_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, c
     if (rc) return rc;
     MsTimer timer;
     hipStream_t s = t_ms.stream;
+    const size_t blds = bow_block_lds(kf_n, fn, kf_fv->n_nodes, nki, f_fv->n_nodes, nfi, npairs);
+    if (blds <= 150 * 1024) {   // one workgroup, everything in LDS
+        BowBlockIn in{ms_ptr<const int>(o_pairs), npairs, ms_ptr<const int>(o_kfoff), ms_ptr<const uint32_t>(o_kfidx),
+                      kf_fv->n_nodes, nki, ms_ptr<const int>(o_foff), ms_ptr<const uint32_t>(o_fidx), f_fv->n_nodes,
+                      nfi, ms_ptr<const int32_t>(o_kfmp), ms_ptr<const uint4>(o_kfdesc), ms_ptr<const uint4>(o_fdesc),
+                      ms_ptr<const OrbKeyPoint>(o_kfkeys), ms_ptr<const OrbKeyPoint>(o_fkeys), kf_n, fn,
+                      F->two_cams ? F->nleft : -1, checkOri, nnratio};
+        hipLaunchKernelGGL(k_bow_block, dim3(1), dim3(MT_BOW_NT), blds, s, in, ms_ptr<int>(o_out), ms_ptr<int>(o_result));
+    } else {
     fill(ms_ptr<int>(o_src), fn, -1);
     hipLaunchKernelGGL(k_bow_nodes, dim3((npairs + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, ms_ptr<const int>(o_pairs),
                        npairs, ms_ptr<const int>(o_kfoff), ms_ptr<const uint32_t>(o_kfidx), ms_ptr<const int>(o_foff),
@@ -4012,6 +4207,7 @@ int orbfe_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, c
     hipLaunchKernelGGL(k_bow_commit, dim3(1), dim3(1024), 0, s, ms_ptr<const OrbKeyPoint>(o_kfkeys),
                        ms_ptr<const OrbKeyPoint>(o_fkeys), fn, ms_ptr<const int32_t>(o_kfmp), checkOri,
                        ms_ptr<const int>(o_src), ms_ptr<int>(o_out), ms_ptr<int>(o_result));
+    }
     HIPCHK(hipGetLastError());
     timer.end();
     int nm = 0;
