@@ -2776,106 +2776,219 @@ __global__ __launch_bounds__(1024) void k_bow_commit(const OrbKeyPoint* kf_keys,
 // rotation histogram in the same block. One launch; the multi-launch pair above serves the sets
 // that do not fit.
 #define MT_BOW_NT 1024
+#define MT_BOW_FR 4   // F features per thread in the commit (fn <= 4096)
+// The call's uploads are one contiguous device range (Plan), node pairs first and the F descriptors
+// last: the block copies that range into LDS with one flat 16-byte loop (independent loads in flight
+// together; a copy loop per array waited one memory latency per array) and addresses every array
+// at its byte offset inside the copy. F's keypoints (after the range) are read from memory.
 struct BowBlockIn {
-    const int* pairs;
-    int npairs;
-    const int* kf_off;
-    const uint32_t* kf_idx;
-    int kf_nodes, nki;
-    const int* f_off;
-    const uint32_t* f_idx;
-    int f_nodes, nfi;
-    const int32_t* kf_mp;
-    const uint4* kf_desc;
-    const uint4* f_desc;
-    const OrbKeyPoint* kf_keys;
+    const uint4* region;   // the contiguous uploads (the mapped pinned staging: read over the link once)
+    int nvec;              // 16-byte words copied
+    int o_pairs, o_kfoff, o_kfidx, o_foff, o_fidx, o_kfmp, o_kfdesc, o_kfkeys, o_fdesc;   // byte offsets
     const OrbKeyPoint* f_keys;
-    int kf_n, fn, nleft, checkOri;
+    int npairs, kf_n, fn, nleft, checkOri;
     float nnratio;
+    volatile int* st_host;   // status words: [1] = matches, [4] = seq (after the outputs)
+    int seq;
 };
-__host__ __device__ inline size_t bow_block_lds(int kf_n, int fn, int kf_nodes, int nki, int f_nodes, int nfi, int npairs) {
-    return (size_t)(kf_n + fn) * 32 + (size_t)(fn + kf_n) * 4 +
-           (size_t)(kf_nodes + 1 + nki + f_nodes + 1 + nfi + 2 * npairs) * 4 + 16;
-}
+#ifdef ORBFE_BOW_STAMPS   // diagnostic build (tools/build_variant.sh): phase times of thread 0, printed
+#define BOW_STAMP(k) do { if (threadIdx.x == 0) t_st[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define BOW_STAMP(k) do { } while (0)
+#endif
 __global__ __launch_bounds__(MT_BOW_NT) void k_bow_block(BowBlockIn in, int* out, int* result) {
     extern __shared__ __attribute__((aligned(16))) uint8_t bw_sm[];
     __shared__ int s_hist[MT_HISTO];
     __shared__ unsigned s_keep;
     __shared__ int s_n;
     const int tid = threadIdx.x;
-    uint4* s_kd = (uint4*)bw_sm;                 // KF descriptors [kf_n][2]
-    uint4* s_fd = s_kd + 2 * in.kf_n;            // F descriptors [fn][2]
-    int* s_src = (int*)(s_fd + 2 * in.fn);       // F index -> matched KF index (-1)
-    int* s_mp = s_src + in.fn;                   // KF map point slot
-    int* s_kfo = s_mp + in.kf_n;
-    int* s_kfi = s_kfo + in.kf_nodes + 1;
-    int* s_fo = s_kfi + in.nki;
-    int* s_fi = s_fo + in.f_nodes + 1;
-    int* s_pr = s_fi + in.nfi;
-    for (int i = tid; i < 2 * in.kf_n; i += MT_BOW_NT) s_kd[i] = in.kf_desc[i];
-    for (int i = tid; i < 2 * in.fn; i += MT_BOW_NT) s_fd[i] = in.f_desc[i];
+#ifdef ORBFE_BOW_STAMPS
+    unsigned long long t_st[5] = {0, 0, 0, 0, 0};
+#endif
+    BOW_STAMP(0);
+    // F's angles for the commit, loaded now (their latency hides under the staging and the walks)
+    float fang[MT_BOW_FR];
+#pragma unroll
+    for (int u = 0; u < MT_BOW_FR; u++) {
+        const int i = tid + u * MT_BOW_NT;
+        fang[u] = i < in.fn ? in.f_keys[i].angle : 0.f;
+    }
+    uint4* s_reg = (uint4*)bw_sm;
+    int* s_src = (int*)(s_reg + in.nvec);        // F index -> matched KF index (-1)
+#pragma unroll 4
+    for (int i = tid; i < in.nvec; i += MT_BOW_NT) s_reg[i] = in.region[i];
     for (int i = tid; i < in.fn; i += MT_BOW_NT) s_src[i] = -1;
-    for (int i = tid; i < in.kf_n; i += MT_BOW_NT) s_mp[i] = in.kf_mp[i];
-    for (int i = tid; i <= in.kf_nodes; i += MT_BOW_NT) s_kfo[i] = in.kf_off[i];
-    for (int i = tid; i < in.nki; i += MT_BOW_NT) s_kfi[i] = (int)in.kf_idx[i];
-    for (int i = tid; i <= in.f_nodes; i += MT_BOW_NT) s_fo[i] = in.f_off[i];
-    for (int i = tid; i < in.nfi; i += MT_BOW_NT) s_fi[i] = (int)in.f_idx[i];
-    for (int i = tid; i < 2 * in.npairs; i += MT_BOW_NT) s_pr[i] = in.pairs[i];
     if (tid < MT_HISTO) s_hist[tid] = 0;
     if (tid == 0) s_n = 0;
     SYNC();
-    // one thread per node present in both vectors (ORBmatcher.cc:244-371): an F index belongs to one
-    // node only, so the "already matched" skip stays inside the thread's own walk
-    for (int t = tid; t < in.npairs; t += MT_BOW_NT) {
+    BOW_STAMP(1);
+    const int* s_pr = (const int*)(bw_sm + in.o_pairs);
+    const int* s_kfo = (const int*)(bw_sm + in.o_kfoff);
+    const int* s_kfi = (const int*)(bw_sm + in.o_kfidx);
+    const int* s_fo = (const int*)(bw_sm + in.o_foff);
+    const int* s_fi = (const int*)(bw_sm + in.o_fidx);
+    const int* s_mp = (const int*)(bw_sm + in.o_kfmp);
+    const uint4* s_kd = (const uint4*)(bw_sm + in.o_kfdesc);
+    const OrbKeyPoint* s_kk = (const OrbKeyPoint*)(bw_sm + in.o_kfkeys);
+    const uint4* s_fd = (const uint4*)(bw_sm + in.o_fdesc);
+    // one quad of lanes per node present in both vectors (ORBmatcher.cc:244-371). The node's KF
+    // features run in the reference's order; for each, the quad's lanes score the node's F features
+    // (lane l: l, l + 4, ...) and the quad minimum of (dist, position) keys is the reference's first
+    // best, the second minimum its bestDist2. An F index belongs to one node only, so the "already
+    // matched" state is private to the quad. One thread per node walked the longest node's KF x F
+    // pairs alone (16-18 us of the kernel's 26); a row of 16 lanes per node spent more on its
+    // reductions than it saved at ~2.5 features per node (28 us).
+    const int sl = tid & 3;
+    auto quad_min64 = [](unsigned long long v) {
+        v = mt_min64_dpp_step<0xB1>(v);
+        return mt_min64_dpp_step<0x4E>(v);
+    };
+    constexpr int FQ = 4;   // F features per lane held in registers (nodes of <= 16 F features)
+    for (int t = tid >> 2; t < in.npairs; t += MT_BOW_NT / 4) {
         const int a = s_pr[2 * t], b = s_pr[2 * t + 1];
         const int fb0 = s_fo[b], fb1 = s_fo[b + 1];
-        for (int ia = s_kfo[a]; ia < s_kfo[a + 1]; ia++) {
+        const int ka0 = s_kfo[a], ka1 = s_kfo[a + 1];
+        if (fb1 - fb0 <= 4 * FQ) {
+            // the node's F features in registers (position p = 4 c + lane: the reference's order), the
+            // "already matched" flags as a bit mask: no LDS round trip inside the KF walk
+            uint4 fd0[FQ], fd1[FQ];
+            int fidx[FQ];
+            unsigned taken = 0u, isleft = 0u;
+#pragma unroll
+            for (int c = 0; c < FQ; c++) {
+                const int ib = fb0 + sl + 4 * c;
+                fidx[c] = ib < fb1 ? s_fi[ib] : 0;
+                if (ib < fb1) {
+                    fd0[c] = s_fd[2 * fidx[c]];
+                    fd1[c] = s_fd[2 * fidx[c] + 1];
+                    if (in.nleft < 0 || fidx[c] < in.nleft) isleft |= 1u << c;
+                } else {
+                    fd0[c] = fd1[c] = make_uint4(0u, 0u, 0u, 0u);
+                    taken |= 1u << c;
+                }
+            }
+            for (int ia = ka0; ia < ka1; ia++) {
+                const int realIdxKF = s_kfi[ia];
+                if (s_mp[realIdxKF] < 0) continue;
+                const uint4 k0 = s_kd[2 * realIdxKF], k1 = s_kd[2 * realIdxKF + 1];
+                unsigned long long b1 = ~0ull, b2 = ~0ull, r1 = ~0ull;
+#pragma unroll
+                for (int c = 0; c < FQ; c++) {
+                    if ((taken >> c) & 1u) continue;
+                    const int dist = __popc(k0.x ^ fd0[c].x) + __popc(k0.y ^ fd0[c].y) + __popc(k0.z ^ fd0[c].z) +
+                                     __popc(k0.w ^ fd0[c].w) + __popc(k1.x ^ fd1[c].x) + __popc(k1.y ^ fd1[c].y) +
+                                     __popc(k1.z ^ fd1[c].z) + __popc(k1.w ^ fd1[c].w);
+                    const unsigned long long key = ((unsigned long long)dist << 32) | (unsigned)(4 * c + sl);
+                    if ((isleft >> c) & 1u) {
+                        if (key < b1) { b2 = b1; b1 = key; }
+                        else if (key < b2) b2 = key;
+                    } else if (key < r1) {
+                        r1 = key;
+                    }
+                }
+                const unsigned long long m1 = quad_min64(b1);
+                const unsigned long long m2 = quad_min64(b1 == m1 ? b2 : b1);
+                const unsigned long long mr = quad_min64(r1);
+                const int bestDist1 = m1 != ~0ull ? (int)(m1 >> 32) : 256;
+                const int bestDist2 = m2 != ~0ull ? (int)(m2 >> 32) : 256;
+                const int bestDist1R = mr != ~0ull ? (int)(mr >> 32) : 256;
+                int w1 = -1, wr = -1;   // winning positions
+                if (bestDist1 <= MT_TH_LOW) {
+                    if (static_cast<float>(bestDist1) < in.nnratio * static_cast<float>(bestDist2)) w1 = (int)(m1 & 0xFFFFFFFFu);
+                    if (bestDist1R <= MT_TH_LOW) wr = (int)(mr & 0xFFFFFFFFu);
+                }
+#pragma unroll
+                for (int c = 0; c < FQ; c++) {
+                    if (w1 == 4 * c + sl || wr == 4 * c + sl) {
+                        taken |= 1u << c;
+                        s_src[fidx[c]] = realIdxKF;
+                    }
+                }
+            }
+            continue;
+        }
+        // larger nodes: the F features and their flags read from LDS per KF feature
+        for (int ia = ka0; ia < ka1; ia++) {
             const int realIdxKF = s_kfi[ia];
             if (s_mp[realIdxKF] < 0) continue;
             const uint4 k0 = s_kd[2 * realIdxKF], k1 = s_kd[2 * realIdxKF + 1];
-            int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
-            int bestDist1R = 256, bestIdxFR = -1;
-            for (int ib = fb0; ib < fb1; ib++) {
+            unsigned long long b1 = ~0ull, b2 = ~0ull, r1 = ~0ull;
+            for (int ib = fb0 + sl; ib < fb1; ib += 4) {
                 const int realIdxF = s_fi[ib];
                 if (s_src[realIdxF] >= 0) continue;
                 const uint4 f0 = s_fd[2 * realIdxF], f1 = s_fd[2 * realIdxF + 1];
                 const int dist = __popc(k0.x ^ f0.x) + __popc(k0.y ^ f0.y) + __popc(k0.z ^ f0.z) + __popc(k0.w ^ f0.w) +
                                  __popc(k1.x ^ f1.x) + __popc(k1.y ^ f1.y) + __popc(k1.z ^ f1.z) + __popc(k1.w ^ f1.w);
+                const unsigned long long key = ((unsigned long long)dist << 32) | (unsigned)ib;
                 if (in.nleft < 0 || realIdxF < in.nleft) {
-                    if (dist < bestDist1) { bestDist2 = bestDist1; bestDist1 = dist; bestIdxF = realIdxF; }
-                    else if (dist < bestDist2) bestDist2 = dist;
-                } else if (dist < bestDist1R) {
-                    bestDist1R = dist;
-                    bestIdxFR = realIdxF;
+                    if (key < b1) { b2 = b1; b1 = key; }
+                    else if (key < b2) b2 = key;
+                } else if (key < r1) {
+                    r1 = key;
                 }
             }
-            if (bestDist1 <= MT_TH_LOW) {
-                if (static_cast<float>(bestDist1) < in.nnratio * static_cast<float>(bestDist2)) s_src[bestIdxF] = realIdxKF;
-                if (bestDist1R <= MT_TH_LOW) s_src[bestIdxFR] = realIdxKF;
+            const unsigned long long m1 = quad_min64(b1);
+            const unsigned long long m2 = quad_min64(b1 == m1 ? b2 : b1);
+            const unsigned long long mr = quad_min64(r1);
+            if (sl == 0) {
+                const int bestDist1 = m1 != ~0ull ? (int)(m1 >> 32) : 256;
+                const int bestDist2 = m2 != ~0ull ? (int)(m2 >> 32) : 256;
+                const int bestDist1R = mr != ~0ull ? (int)(mr >> 32) : 256;
+                if (bestDist1 <= MT_TH_LOW) {
+                    if (static_cast<float>(bestDist1) < in.nnratio * static_cast<float>(bestDist2))
+                        s_src[s_fi[(int)(m1 & 0xFFFFFFFFu)]] = realIdxKF;
+                    if (bestDist1R <= MT_TH_LOW) s_src[s_fi[(int)(mr & 0xFFFFFFFFu)]] = realIdxKF;
+                }
             }
+            WAVE_SYNC();   // the quad's next KF feature sees the taken F features
         }
     }
     SYNC();
-    // rotation consistency (ORBmatcher.cc:373-395) and the output (k_bow_commit)
-    for (int i = tid; i < in.fn; i += MT_BOW_NT) {
-        const int sidx = s_src[i];
-        if (sidx >= 0 && in.checkOri) atomicAdd(&s_hist[mt_rot_bin(in.kf_keys[sidx].angle, in.f_keys[i].angle)], 1);
+    BOW_STAMP(2);
+    // rotation consistency (ORBmatcher.cc:373-395) and the output (k_bow_commit); F's angles were
+    // loaded at the start
+    int sidx[MT_BOW_FR], bin[MT_BOW_FR];
+#pragma unroll
+    for (int u = 0; u < MT_BOW_FR; u++) {
+        const int i = tid + u * MT_BOW_NT;
+        sidx[u] = i < in.fn ? s_src[i] : -1;
+        bin[u] = sidx[u] >= 0 ? mt_rot_bin(s_kk[sidx[u]].angle, fang[u]) : 0;
+        if (sidx[u] >= 0 && in.checkOri) atomicAdd(&s_hist[bin[u]], 1);
     }
     SYNC();
     if (tid == 0) s_keep = in.checkOri ? mt_three_maxima_keep(s_hist) : 0xFFFFFFFFu;
     SYNC();
     int cnt = 0;
-    for (int i = tid; i < in.fn; i += MT_BOW_NT) {
-        const int sidx = s_src[i];
+#pragma unroll
+    for (int u = 0; u < MT_BOW_FR; u++) {
+        const int i = tid + u * MT_BOW_NT;
+        if (i >= in.fn) continue;
         int o = -1;
-        if (sidx >= 0 && (!in.checkOri || ((s_keep >> mt_rot_bin(in.kf_keys[sidx].angle, in.f_keys[i].angle)) & 1u)))
-            o = s_mp[sidx];
+        if (sidx[u] >= 0 && (!in.checkOri || ((s_keep >> bin[u]) & 1u))) o = s_mp[sidx[u]];
         out[i] = o;
         cnt += o >= 0 ? 1 : 0;
     }
     atomicAdd(&s_n, cnt);
+    // every wave's output stores complete (vmcnt 0), the barrier, then one system-scope release before
+    // the status words the host waits for (as k_sbp_block)
+    __builtin_amdgcn_s_waitcnt(0);
     SYNC();
-    if (tid == 0) result[0] = s_n;
+    if (tid == 0) {
+        result[0] = s_n;
+        __threadfence_system();
+        volatile int* st = in.st_host;
+        st[0] = 0;
+        st[1] = s_n;
+        __threadfence_system();
+        st[4] = in.seq;
+        __threadfence_system();
+    }
+#ifdef ORBFE_BOW_STAMPS
+    BOW_STAMP(3);
+    if (tid == 0)   // s_memrealtime ticks at 100 MHz
+        printf("bow npairs %d kf %d f %d nvec %d  stage %.1f walk %.1f commit %.1f us\n", in.npairs, in.kf_n, in.fn,
+               in.nvec, (t_st[1] - t_st[0]) * 0.01, (t_st[2] - t_st[1]) * 0.01, (t_st[3] - t_st[2]) * 0.01);
+#endif
 }
 
 // ---- ComputeStereoFishEyeMatches' knnMatch(k=2) + ratio (Frame.cc:1144-1151) ----
@@ -4186,19 +4299,50 @@ int orbfe_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, c
     const size_t o_src = p.scratch((size_t)fn * 4);
     const size_t o_out = p.scratch((size_t)fn * 4);
     const size_t o_result = p.scratch(16);
-    int rc = ms_prepare(p);
+    // the uploads from the node pairs to the F descriptors, in Plan order (k_bow_block copies them whole)
+    const size_t reg_bytes = o_fdesc + (size_t)fn * 32 - o_pairs;
+    const size_t blds = ((reg_bytes + 15) & ~(size_t)15) + (size_t)fn * 4 + 16;
+    const bool block = o_pairs < o_kfoff && o_kfoff < o_kfidx && o_kfidx < o_foff && o_foff < o_fidx &&
+                       o_fidx < o_kfmp && o_kfmp < o_kfdesc && o_kfdesc < o_kfkeys && o_kfkeys < o_fdesc &&
+                       blds <= 150 * 1024 && fn <= MT_BOW_FR * MT_BOW_NT;
+    // one workgroup: zero copy both ways (inputs read in place from the mapped pinned staging, the
+    // output written to mapped pinned memory, the status words awaited: no DMA, no stream sync)
+    int rc = ms_prepare(p, block);
     if (rc) return rc;
     MsTimer timer;
     hipStream_t s = t_ms.stream;
-    const size_t blds = bow_block_lds(kf_n, fn, kf_fv->n_nodes, nki, f_fv->n_nodes, nfi, npairs);
-    if (blds <= 150 * 1024) {   // one workgroup, everything in LDS
-        BowBlockIn in{ms_ptr<const int>(o_pairs), npairs, ms_ptr<const int>(o_kfoff), ms_ptr<const uint32_t>(o_kfidx),
-                      kf_fv->n_nodes, nki, ms_ptr<const int>(o_foff), ms_ptr<const uint32_t>(o_fidx), f_fv->n_nodes,
-                      nfi, ms_ptr<const int32_t>(o_kfmp), ms_ptr<const uint4>(o_kfdesc), ms_ptr<const uint4>(o_fdesc),
-                      ms_ptr<const OrbKeyPoint>(o_kfkeys), ms_ptr<const OrbKeyPoint>(o_fkeys), kf_n, fn,
-                      F->two_cams ? F->nleft : -1, checkOri, nnratio};
-        hipLaunchKernelGGL(k_bow_block, dim3(1), dim3(MT_BOW_NT), blds, s, in, ms_ptr<int>(o_out), ms_ptr<int>(o_result));
-    } else {
+    if (block) {
+        MatchScratch& m = t_ms;
+        if (m.ocap < (size_t)fn) {
+            if (m.ho) HIPCHK(hipHostFree(m.ho));
+            m.ho = nullptr;
+            m.ocap = 0;
+            const size_t cap = std::max<size_t>((size_t)fn, 2048);
+            HIPCHK(hipHostMalloc((void**)&m.ho, cap * 4, hipHostMallocMapped | hipHostMallocCoherent));
+            HIPCHK(hipHostGetDevicePointer((void**)&m.ho_dev, m.ho, 0));
+            m.ocap = cap;
+        }
+        auto rel = [&](size_t o) { return (int)(o - o_pairs); };
+        const int seq = ++t_ms.seq;
+        BowBlockIn in{up_ptr<const uint4>(o_pairs, true), (int)((reg_bytes + 15) / 16), rel(o_pairs), rel(o_kfoff),
+                      rel(o_kfidx), rel(o_foff), rel(o_fidx), rel(o_kfmp), rel(o_kfdesc), rel(o_kfkeys), rel(o_fdesc),
+                      up_ptr<const OrbKeyPoint>(o_fkeys, true), npairs, kf_n, fn, F->two_cams ? F->nleft : -1,
+                      checkOri, nnratio, t_ms.hs_dev, seq};
+        hipLaunchKernelGGL(k_bow_block, dim3(1), dim3(MT_BOW_NT), blds, s, in, m.ho_dev, ms_ptr<int>(o_result));
+        HIPCHK(hipGetLastError());
+        timer.end();
+        volatile int* st = t_ms.hs;
+        for (unsigned spin = 1; host_seq_acquire(st) != seq; spin++) {
+            if ((spin & 1023) == 0) {   // bounded: a stream that finished without publishing is an error
+                const hipError_t e = hipStreamQuery(s);
+                if (e == hipSuccess && host_seq_acquire(st) != seq) return ORBFE_E_DEVICE;
+                if (e != hipSuccess && e != hipErrorNotReady) HIPCHK(e);
+            }
+            __builtin_ia32_pause();
+        }
+        memcpy(out, m.ho, (size_t)fn * 4);   // complete: the status words come after the output stores
+        return st[1];
+    }
     fill(ms_ptr<int>(o_src), fn, -1);
     hipLaunchKernelGGL(k_bow_nodes, dim3((npairs + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, ms_ptr<const int>(o_pairs),
                        npairs, ms_ptr<const int>(o_kfoff), ms_ptr<const uint32_t>(o_kfidx), ms_ptr<const int>(o_foff),
@@ -4207,7 +4351,6 @@ int orbfe_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, c
     hipLaunchKernelGGL(k_bow_commit, dim3(1), dim3(1024), 0, s, ms_ptr<const OrbKeyPoint>(o_kfkeys),
                        ms_ptr<const OrbKeyPoint>(o_fkeys), fn, ms_ptr<const int32_t>(o_kfmp), checkOri,
                        ms_ptr<const int>(o_src), ms_ptr<int>(o_out), ms_ptr<int>(o_result));
-    }
     HIPCHK(hipGetLastError());
     timer.end();
     int nm = 0;
