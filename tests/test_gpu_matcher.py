@@ -154,6 +154,41 @@ def test_search_by_bow(gpu, om, seed, check_ori):
         assert no > 0
 
 
+@pytest.mark.parametrize("n_kf,n_f,words", [
+    (1000, 1000, 1),      # one node: a 1000 x 1000 walk through the LDS form of k_bow_block
+    (3000, 3000, 400),    # beyond k_bow_block's LDS (the multi-launch k_bow_nodes + k_bow_commit)
+    (1200, 1100, 5000),   # mostly single-feature nodes, many without a partner node
+])
+def test_search_by_bow_sizes(gpu, om, n_kf, n_f, words):
+    rng = np.random.default_rng(n_kf + 7 * words)
+    KF = sm.synth_frame(rng, n_kf, stereo=False)
+    F, src = sm.perturbed_frame(rng, KF, rot=20.0, flip_p=0.05, drop=0.15)
+    F = MatchFrame(F.keys[:n_f].copy(), F.desc[:n_f].copy(), F.bounds, F.scale_factors)
+    src = src[:n_f]
+    kf_mp = np.where(rng.random(KF.N) < 0.25, -1, np.arange(KF.N) + 100).astype(np.int32)
+    fk, ff = sm.synth_bow(rng, words, KF, F, src)
+    for check_ori in (True, False):
+        ng, out_g = ORBmatcher(0.75, check_ori).SearchByBoW(KF.keys, KF.desc, kf_mp, fk, F, ff)
+        no, out_o = om.OracleMatcher(0.75, check_ori).search_by_bow(KF.keys, KF.desc, kf_mp, fk, F, ff)
+        assert ng == no
+        np.testing.assert_array_equal(out_g, out_o)
+
+
+def test_search_for_initialization_5000(gpu, om):
+    """The monocular initialiser's size (5 x nFeatures): one query row of 16 lanes per F1 feature."""
+    rng = np.random.default_rng(4242)
+    F1 = sm.synth_frame(rng, 5000, stereo=False)
+    F2, _ = sm.perturbed_frame(rng, F1, shift=(6.0, -4.0), jitter=2.0, rot=12.0, flip_p=0.06, drop=0.2)
+    prev0 = np.stack([F1.keys["x"], F1.keys["y"]], 1).astype(np.float32)
+    pa, pb = prev0.copy(), prev0.copy()
+    ma, mb = np.zeros(F1.N, np.int32), np.zeros(F1.N, np.int32)
+    ng = ORBmatcher(0.9, True).SearchForInitialization(F1, F2, pa, ma, 100)
+    no = om.OracleMatcher(0.9, True).search_for_init(F1, F2, pb, mb, 100)
+    assert ng == no and no > 0
+    np.testing.assert_array_equal(ma, mb)
+    np.testing.assert_array_equal(pa, pb)
+
+
 @pytest.mark.parametrize("nl,nr", [(1000, 1000), (1, 2), (333, 517), (700, 1)])
 def test_stereo_knn_ratio(gpu, om, nl, nr):
     rng = np.random.default_rng(nl * 7 + nr)
