@@ -169,30 +169,101 @@ __global__ __launch_bounds__(1024) void k_mt_grid(const OrbKeyPoint* keys, int n
         cidx += (size_t)gi * gstride_i;
     }
     const int ncells = is_band ? band.nlev * band.NB : nleft >= 0 ? 2 * MT_NCELL : MT_NCELL;
+    // cell of keypoint i (ncells: outside the grid, never a candidate: PosInGrid false)
+    auto cell_of = [&](int i) -> uint32_t {
+        const OrbKeyPoint kp = keys[i];
+        uint32_t cell = (uint32_t)ncells;
+        if (is_band) {
+            // a two-camera frame's single-camera searches (SearchByProjection(CurrentFrame, pKF))
+            // read its left grid only: the right rows [nleft, n) are in no bucket
+            if (kp.octave >= 0 && kp.octave < band.nlev && (nleft < 0 || i < nleft))
+                cell = (uint32_t)(kp.octave * band.NB + mt_band_of(kp.y, band.NB));
+        } else {
+            const int px = (int)roundf((kp.x - minx) * invw);
+            const int py = (int)roundf((kp.y - miny) * invh);
+            if (!(px < 0 || px >= ORBFE_GRID_COLS || py < 0 || py >= ORBFE_GRID_ROWS) && kp.octave >= lvlo &&
+                kp.octave <= lvhi)
+                cell = (uint32_t)(px * ORBFE_GRID_ROWS + py + (nleft >= 0 && i >= nleft ? MT_NCELL : 0));
+        }
+        return cell;
+    };
+    // Stable counting sort by cell when the cells fit in LDS and none is crowded: counts, an exclusive
+    // scan (the cell starts), atomic placement, then each cell's few indices put back in index order
+    // by one thread (insertion sort). The bitonic network below (about 40 barrier stages at 2,048
+    // keys) stays for crowded cells and very many buckets.
+    constexpr int CS_MAX = 2 * MT_NCELL;
+    __shared__ int s_cnt[CS_MAX + 1];
+    __shared__ int s_ws[16], s_maxc;
+    uint32_t cr[MT_GRID_R];
+#pragma unroll
+    for (int r = 0; r < MT_GRID_R; r++) {
+        const int i = tid + (r << 10);
+        cr[r] = i < n ? cell_of(i) : 0xFFFFFFFFu;
+    }
+    if (ncells <= CS_MAX) {
+        const int nb = ncells + 1;   // + the outside cell (its keys go last)
+        for (int c = tid; c < nb; c += blockDim.x) s_cnt[c] = 0;
+        if (tid == 0) s_maxc = 0;
+        SYNC();
+#pragma unroll
+        for (int r = 0; r < MT_GRID_R; r++)
+            if (cr[r] != 0xFFFFFFFFu) atomicAdd(&s_cnt[cr[r]], 1);
+        SYNC();
+        const int per = (nb + (int)blockDim.x - 1) / (int)blockDim.x, c0 = tid * per;
+        int sum = 0, mx = 0;
+        for (int u = 0; u < per; u++) {
+            const int c = c0 + u;
+            const int v = c < nb ? s_cnt[c] : 0;
+            sum += v;
+            if (c < ncells) mx = max(mx, v);
+        }
+        const int incl = wave_incl_scan_dpp(sum);
+        if ((tid & 63) == 63) s_ws[tid >> 6] = incl;
+        if (mx > 32) atomicMax(&s_maxc, mx);
+        SYNC();
+        if (s_maxc <= 32) {   // block-uniform
+            int run = incl - sum;
+            for (int w = 0; w < (int)(blockDim.x >> 6); w++) run += w < (tid >> 6) ? s_ws[w] : 0;
+            for (int u = 0; u < per; u++) {
+                const int c = c0 + u;
+                if (c >= nb) break;
+                const int v = s_cnt[c];
+                s_cnt[c] = run;   // cursor of the placement
+                if (c <= ncells) cstart[c] = run;
+                run += v;
+            }
+            SYNC();
+#pragma unroll
+            for (int r = 0; r < MT_GRID_R; r++)
+                if (cr[r] != 0xFFFFFFFFu) s_k[atomicAdd(&s_cnt[cr[r]], 1)] = (uint32_t)(tid + (r << 10));
+            SYNC();
+            // s_cnt[c] is now the end of cell c: restore index order inside each cell
+            for (int c = tid; c < ncells; c += blockDim.x) {
+                const int a = c ? s_cnt[c - 1] : 0, b = s_cnt[c];
+                for (int x = a + 1; x < b; x++) {
+                    const uint32_t v = s_k[x];
+                    int y = x - 1;
+                    while (y >= a && s_k[y] > v) { s_k[y + 1] = s_k[y]; y--; }
+                    s_k[y + 1] = v;
+                }
+            }
+            SYNC();
+            // positions past cstart[ncells] (the outside cell) are never read by a search; the band
+            // index keeps them as k_sbp_band stages all n positions
+            for (int p = tid; p < n; p += blockDim.x) cidx[p] = (int)s_k[p];
+            return;
+        }
+    }
     // the keys of the grid's keypoints, appended in any order (the (cell, index) sort restores it);
     // a level grid holds a fraction of the frame, so it sorts fewer keys. The band index keeps every
     // keypoint (k_sbp_band stages all n positions).
     if (tid == 0) s_m = 0;
     SYNC();
     // wave-aggregated appends (one LDS atomic per wave and round, positions by mbcnt)
-    for (int i0 = 0; i0 < n; i0 += blockDim.x) {
-        const int i = i0 + tid;
-        uint32_t cell = (uint32_t)ncells;   // outside the grid: never a candidate (PosInGrid false)
-        if (i < n) {
-            const OrbKeyPoint kp = keys[i];
-            if (is_band) {
-                // a two-camera frame's single-camera searches (SearchByProjection(CurrentFrame, pKF))
-                // read its left grid only: the right rows [nleft, n) are in no bucket
-                if (kp.octave >= 0 && kp.octave < band.nlev && (nleft < 0 || i < nleft))
-                    cell = (uint32_t)(kp.octave * band.NB + mt_band_of(kp.y, band.NB));
-            } else {
-                const int px = (int)roundf((kp.x - minx) * invw);
-                const int py = (int)roundf((kp.y - miny) * invh);
-                if (!(px < 0 || px >= ORBFE_GRID_COLS || py < 0 || py >= ORBFE_GRID_ROWS) && kp.octave >= lvlo &&
-                    kp.octave <= lvhi)
-                    cell = (uint32_t)(px * ORBFE_GRID_ROWS + py + (nleft >= 0 && i >= nleft ? MT_NCELL : 0));
-            }
-        }
+#pragma unroll
+    for (int r = 0; r < MT_GRID_R; r++) {
+        const int i = tid + (r << 10);
+        const uint32_t cell = cr[r];
         const bool keep = i < n && (is_band || cell < (uint32_t)ncells);
         const unsigned long long bm = __ballot(keep);
         const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
@@ -4179,9 +4250,58 @@ int orbfe_search_by_projection_kf(const orbfe_frame* cur, int32_t* mvp, const or
                    offsetof(orbfe_proj_point, angle), offsetof(orbfe_proj_point, octave), th, 0, 0, 0.f, 0.f, ORBdist, checkOri);
 }
 
+static int sfi_core(const orbfe_frame* F1, const orbfe_frame* F2, float* prev_matched, int32_t* matches12,
+                    int32_t windowSize, float nnratio, int32_t checkOri);
+
 int orbfe_search_for_initialization(const orbfe_frame* F1, const orbfe_frame* F2, float* prev_matched,
                                     int32_t* matches12, int32_t windowSize, float nnratio, int32_t checkOri) {
     if (!frame1_ok(F1) || !frame1_ok(F2) || !prev_matched || !matches12) return ORBFE_E_ARG;
+    // Only F1's level-0 features search (ORBmatcher.cc:661-663: level1 > 0 continues), and their
+    // windows read F2's level-0 features only (GetFeaturesInArea(.., level1, level1)). The call runs
+    // on those two subsets (order-preserving, so "earlier query" and the enumeration order are
+    // unchanged) and scatters the results back: a fifth of the monocular initialiser's 5 x nFeatures
+    // to pack, upload and grid. A negative octave (no level filter in the reference) keeps the
+    // whole frames.
+    bool neg = false;
+    for (int i = 0; i < F1->n && !neg; i++) neg = F1->keys[i].octave < 0;
+    if (neg || F1->n == 0 || F2->n == 0)
+        return sfi_core(F1, F2, prev_matched, matches12, windowSize, nnratio, checkOri);
+    std::vector<int32_t> i1, i2;
+    for (int i = 0; i < F1->n; i++)
+        if (F1->keys[i].octave == 0) i1.push_back(i);
+    for (int i = 0; i < F2->n; i++)
+        if (F2->keys[i].octave == 0) i2.push_back(i);
+    const int m1 = (int)i1.size(), m2 = (int)i2.size();
+    std::vector<orbfe_keypoint> k1(std::max(m1, 1)), k2(std::max(m2, 1));
+    std::vector<uint8_t> d1((size_t)std::max(m1, 1) * 32), d2((size_t)std::max(m2, 1) * 32);
+    std::vector<float> pv((size_t)std::max(m1, 1) * 2);
+    for (int j = 0; j < m1; j++) {
+        k1[j] = F1->keys[i1[j]];
+        memcpy(&d1[(size_t)j * 32], F1->desc + (size_t)i1[j] * 32, 32);
+        pv[2 * j] = prev_matched[2 * i1[j]];
+        pv[2 * j + 1] = prev_matched[2 * i1[j] + 1];
+    }
+    for (int j = 0; j < m2; j++) {
+        k2[j] = F2->keys[i2[j]];
+        memcpy(&d2[(size_t)j * 32], F2->desc + (size_t)i2[j] * 32, 32);
+    }
+    orbfe_frame c1 = *F1, c2 = *F2;
+    c1.n = m1; c1.keys = k1.data(); c1.desc = d1.data(); c1.uright = nullptr;
+    c2.n = m2; c2.keys = k2.data(); c2.desc = d2.data(); c2.uright = nullptr;
+    std::vector<int32_t> mc((size_t)std::max(m1, 1));
+    const int r = sfi_core(&c1, &c2, pv.data(), mc.data(), windowSize, nnratio, checkOri);
+    if (r < 0) return r;
+    for (int i = 0; i < F1->n; i++) matches12[i] = -1;
+    for (int j = 0; j < m1; j++) {
+        matches12[i1[j]] = mc[j] >= 0 ? i2[mc[j]] : -1;
+        prev_matched[2 * i1[j]] = pv[2 * j];
+        prev_matched[2 * i1[j] + 1] = pv[2 * j + 1];
+    }
+    return r;
+}
+
+static int sfi_core(const orbfe_frame* F1, const orbfe_frame* F2, float* prev_matched, int32_t* matches12,
+                    int32_t windowSize, float nnratio, int32_t checkOri) {
     const int n1 = F1->n;
     if (n1 == 0) return 0;
     if (F2->n == 0) {
