@@ -118,11 +118,12 @@ inline int sbp_init_extent(const SbpInit& a) {
     return a.resb ? std::max(std::max(a.n + 3, a.nassign), MT_MAX_PASSES) : 0;
 }
 
-// AssignFeaturesToGrid (Frame.cc:385-416): stable (cell, index) order via a bitonic sort of
-// (cell << 16 | index) keys (unique, so any sorting network gives the same order). One block per
-// grid, n <= MT_GRID_MAXN; each thread holds the keys i = tid + 1024 r in registers: the
-// compare-exchange stages with partner distance j < 64 stay inside a wave (lane shuffles, no
-// barrier) and only the j >= 64 stages go through LDS (14 barriers at P = 1024 instead of 55).
+// AssignFeaturesToGrid (Frame.cc:385-416): stable (cell, index) order. One block per grid,
+// n <= MT_GRID_MAXN. Normally a counting sort by cell (see below); crowded cells fall back to a
+// bitonic sort of (cell << 16 | index) keys (unique, so any sorting network gives the same order):
+// each thread holds the keys i = tid + 1024 r in registers, the compare-exchange stages with partner
+// distance j < 64 stay inside a wave (lane shuffles, no barrier) and only the j >= 64 stages go
+// through LDS.
 // Two-camera frames (nleft >= 0): rows >= nleft go to the right grid, cells MT_NCELL..
 // (Frame.cc:408-411). Blocks >= ngrids run the search initialisation (SbpInit) instead.
 #define MT_GRID_MAXN 8192
