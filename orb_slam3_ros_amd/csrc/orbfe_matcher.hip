@@ -445,8 +445,14 @@ __global__ __launch_bounds__(MT_NT) void k_sbp_local(FrameDev fr, const orbfe_ma
 // displaces an earlier one). Four query chains per wave in flight: one query per wave ran 0.77 ms at
 // config 5 th = 15 against 0.51 (profiles/r04_kernel_ab.txt items 10-11), its time being the
 // per-query chain (record -> grid columns -> candidates), not the window. Persistent blocks stage the
-// frame's keypoints, descriptors and per-keypoint gates in LDS.
-#define MT_WAVE_TH 6.0f
+// frame's keypoints, descriptors and per-keypoint gates in LDS (a frame beyond MT_STAGE_MAX: keypoints
+// and gates only). Frames of <= 2048 keypoints use the LDS-indexed forms instead (k_sbp_block /
+// k_sbp_multi / k_sbp_band), so the threshold only splits larger frames: config 5 at N = 5000 measured
+// th 3 / 5 at 0.192 / 0.267 ms here against 0.273 / 0.58 one thread per query, th 1 at 0.141 against
+// 0.118 (r06_kernel_ab.txt item 20).
+#ifndef MT_WAVE_TH
+#define MT_WAVE_TH 2.5f
+#endif
 #define MT_STAGE_MAX 1536
 #define MT_WNT 1024   // 16 waves per block share one staged copy of the frame
 #define MT_QPW 4      // queries per wave: one per row of 16 lanes
@@ -479,7 +485,11 @@ __device__ __forceinline__ int mt_rows_max(int v) {   // max over the four rows 
     m = max(m, __builtin_amdgcn_readlane(v, 32));
     return max(m, __builtin_amdgcn_readlane(v, 48));
 }
-template <bool STAGED>
+// ST = 1: the frame's keypoints, descriptors and gates staged in LDS (n <= MT_STAGE_MAX); ST = 2: the
+// keypoints and gates only (larger frames, e.g. BASELINE config 5's 5,000 keypoints: the box, octave
+// and gate tests of every window candidate from LDS, descriptors from memory for the candidates that
+// pass them); ST = 0: nothing staged.
+template <int ST>
 __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wq(FrameDev fr, const orbfe_map_point* mps, int nq, float th,
                                                       int bFar, float thFar, float nnratio, const int* blocked0,
                                                       const int* first, int* assign, int* changed, PassIO io) {
@@ -489,16 +499,18 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wq(FrameDev fr, const orbf
     pass_fill(io);
     int2* s_cell = (int2*)mt_sm;                                          // [16 waves][4 rows][16] (start, prefix)
     float4* s_key = (float4*)(mt_sm + (MT_WNT / 64) * 64 * sizeof(int2));  // x, y, octave bits, uR
-    uint4* s_desc = (uint4*)(s_key + (STAGED ? fr.n : 0));         // 2 x uint4 per keypoint
-    int2* s_gate = (int2*)(s_desc + (STAGED ? 2 * fr.n : 0));      // {blocked0, first}, read-only in a pass
+    uint4* s_desc = (uint4*)(s_key + (ST ? fr.n : 0));             // 2 x uint4 per keypoint (ST == 1)
+    int2* s_gate = (int2*)(s_desc + (ST == 1 ? 2 * fr.n : 0));     // {blocked0, first}, read-only in a pass
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, grp = lane >> 4, sl = lane & 15;
-    if (STAGED) {
+    if (ST) {
         for (int i = tid; i < fr.n; i += MT_WNT) {
             const OrbKeyPoint kp = fr.keys[i];
             s_key[i] = make_float4(kp.x, kp.y, __int_as_float(kp.octave), fr.uright ? fr.uright[i] : -1.f);
-            const uint4* d = (const uint4*)(fr.desc + 8 * i);
-            s_desc[2 * i] = d[0];
-            s_desc[2 * i + 1] = d[1];
+            if (ST == 1) {
+                const uint4* d = (const uint4*)(fr.desc + 8 * i);
+                s_desc[2 * i] = d[0];
+                s_desc[2 * i + 1] = d[1];
+            }
             s_gate[i] = make_int2(blocked0[i], first[i]);
         }
         SYNC();
@@ -569,7 +581,7 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wq(FrameDev fr, const orbf
                     const int idx = pci[ce.x + (j - ce.y)];
                     float kx, ky, ur;
                     int oct;
-                    if (STAGED) {
+                    if (ST) {
                         const float4 k4 = s_key[idx];
                         kx = k4.x; ky = k4.y; oct = __float_as_int(k4.z); ur = k4.w;
                     } else {
@@ -582,7 +594,7 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wq(FrameDev fr, const orbf
                         if (maxLevel >= 0 && oct > maxLevel) ok = false;
                     }
                     ok = ok && fabsf(kx - x) < R && fabsf(ky - y) < R;
-                    if (STAGED) {
+                    if (ST) {
                         const int2 gt = s_gate[idx];
                         ok = ok && !(gt.x || gt.y < q);
                     } else {
@@ -592,7 +604,7 @@ __global__ __launch_bounds__(MT_WNT) void k_sbp_local_wq(FrameDev fr, const orbf
                     if (ok) {
                         npair++;
                         uint4 d0, d1;
-                        if (STAGED) { d0 = s_desc[2 * idx]; d1 = s_desc[2 * idx + 1]; }
+                        if (ST == 1) { d0 = s_desc[2 * idx]; d1 = s_desc[2 * idx + 1]; }
                         else { d0 = ((const uint4*)(fr.desc + 8 * idx))[0]; d1 = ((const uint4*)(fr.desc + 8 * idx))[1]; }
                         const int dist = __popc(qd[0] ^ d0.x) + __popc(qd[1] ^ d0.y) + __popc(qd[2] ^ d0.z) +
                                          __popc(qd[3] ^ d0.w) + __popc(qd[4] ^ d1.x) + __popc(qd[5] ^ d1.y) +
@@ -4091,13 +4103,19 @@ int sbp_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* mvp_obs
                 } else if (mode == 0 && th >= MT_WAVE_TH) {
                     const int qpb = (MT_WNT / 64) * MT_QPW;   // queries per block and round
                     const int nb = std::min((nq + qpb - 1) / qpb, 512);
-                    const size_t lds = (MT_WNT / 64) * 64 * sizeof(int2) + (staged ? (size_t)n * 56 : 0);
-                    if (staged)
-                        hipLaunchKernelGGL(k_sbp_local_wq<true>, dim3(nb), dim3(MT_WNT), lds, s, fr,
+                    const size_t cellb = (MT_WNT / 64) * 64 * sizeof(int2);
+                    const int st = staged ? 1 : (cellb + (size_t)n * 24 <= 150 * 1024 ? 2 : 0);
+                    const size_t lds = cellb + (st == 1 ? (size_t)n * 56 : st == 2 ? (size_t)n * 24 : 0);
+                    if (st == 1)
+                        hipLaunchKernelGGL(k_sbp_local_wq<1>, dim3(nb), dim3(MT_WNT), lds, s, fr,
+                                           (const orbfe_map_point*)q, nq, th, a0, thFar, nnratio, b0, fcur, assign,
+                                           changed + pass, io);
+                    else if (st == 2)
+                        hipLaunchKernelGGL(k_sbp_local_wq<2>, dim3(nb), dim3(MT_WNT), lds, s, fr,
                                            (const orbfe_map_point*)q, nq, th, a0, thFar, nnratio, b0, fcur, assign,
                                            changed + pass, io);
                     else
-                        hipLaunchKernelGGL(k_sbp_local_wq<false>, dim3(nb), dim3(MT_WNT), lds, s, fr,
+                        hipLaunchKernelGGL(k_sbp_local_wq<0>, dim3(nb), dim3(MT_WNT), lds, s, fr,
                                            (const orbfe_map_point*)q, nq, th, a0, thFar, nnratio, b0, fcur, assign,
                                            changed + pass, io);
                 } else if (mode == 0) {
