@@ -2618,9 +2618,11 @@ __global__ void k_mt_commit_write(int n, const int* qid, int q_stride_bytes, con
 // Per candidate i2 the table also keeps its segment (seg_off, seg_cnt; n2 entries, cleared here), so a
 // query walks the few selectors of its candidate instead of a binary search over the whole table.
 __global__ __launch_bounds__(1024) void k_init_state(const int* assign, const int* adist, int nq, uint32_t* skey,
-                                                     int* spmin, int* nsel, int n2, int* seg_off, int* seg_cnt) {
+                                                     int* spmin, int* nsel, int n2, int* seg_off, int* seg_cnt,
+                                                     const int* gate) {
     __shared__ uint32_t s_k[MT_INIT_MAXQ];
     __shared__ int s_cnt;
+    if (gate && *gate == 0) return;   // the previous pass changed nothing: converged
     if (threadIdx.x == 0) s_cnt = 0;
     for (int i = threadIdx.x; i < n2; i += blockDim.x) seg_cnt[i] = 0;
     SYNC();
@@ -2669,7 +2671,8 @@ __global__ __launch_bounds__(1024) void k_init_state(const int* assign, const in
 __global__ __launch_bounds__(MT_INIT_WNT) void k_init_eval(FrameDev f1, FrameDev f2, const float* prev, int windowSize,
                                                            float nnratio, const uint32_t* skey, const int* spmin,
                                                            const int* seg_off, const int* seg_cnt, int* assign,
-                                                           int* adist, int* changed) {
+                                                           int* adist, int* changed, const int* gate) {
+    if (gate && *gate == 0) return;   // the previous pass changed nothing: converged
     const int lane = threadIdx.x & 63, grp = lane >> 4, sl = lane & 15;
     const int q = (blockIdx.x * (MT_INIT_WNT / 64) + (threadIdx.x >> 6)) * 4 + grp;
     const bool qv = q < f1.n;
@@ -2745,43 +2748,60 @@ __global__ __launch_bounds__(MT_INIT_WNT) void k_init_eval(FrameDev f1, FrameDev
     }
 }
 
+// The commit runs only once the last pass changed nothing (gate == 0). Its outputs (matches12 and
+// the updated prevMatched, the latter pre-filled with the input by the host) go straight into mapped
+// pinned memory, then {converged, matches, -, -, sequence number} into the status words the host
+// waits on; a gated-off commit publishes "not converged" only (the host enqueues more passes).
 __global__ __launch_bounds__(1024) void k_init_commit(FrameDev f1, FrameDev f2, const int* assign, int checkOri,
-                                                      float* prev, int* m12, int* result) {
+                                                      float* prev, int* m12, const int* gate, int* st_host, int seq) {
     __shared__ int s_hist[MT_HISTO];
     __shared__ unsigned s_keep;
     __shared__ int s_n;
     __shared__ int s_owner[MT_INIT_MAXQ];
-    if (threadIdx.x < MT_HISTO) s_hist[threadIdx.x] = 0;
-    if (threadIdx.x == 0) s_n = 0;
-    for (int i = threadIdx.x; i < f2.n && i < MT_INIT_MAXQ; i += blockDim.x) s_owner[i] = -1;
-    SYNC();
-    for (int j = threadIdx.x; j < f1.n; j += blockDim.x) {
-        const int a = assign[j];
-        if (a < 0) continue;
-        atomicMax(&s_owner[a], j);   // the last selector keeps i2; earlier ones were stolen
-        if (checkOri) atomicAdd(&s_hist[mt_rot_bin(f1.keys[j].angle, f2.keys[a].angle)], 1);
-    }
-    SYNC();
-    if (threadIdx.x == 0) s_keep = checkOri ? mt_three_maxima_keep(s_hist) : 0xFFFFFFFFu;
-    SYNC();
-    int cnt = 0;
-    for (int j = threadIdx.x; j < f1.n; j += blockDim.x) {
-        const int a = assign[j];
-        int out = -1;
-        if (a >= 0 && s_owner[a] == j) {
-            out = a;
-            if (checkOri && !((s_keep >> mt_rot_bin(f1.keys[j].angle, f2.keys[a].angle)) & 1u)) out = -1;
+    const bool run = !gate || *gate == 0;
+    if (run) {
+        if (threadIdx.x < MT_HISTO) s_hist[threadIdx.x] = 0;
+        if (threadIdx.x == 0) s_n = 0;
+        for (int i = threadIdx.x; i < f2.n && i < MT_INIT_MAXQ; i += blockDim.x) s_owner[i] = -1;
+        SYNC();
+        for (int j = threadIdx.x; j < f1.n; j += blockDim.x) {
+            const int a = assign[j];
+            if (a < 0) continue;
+            atomicMax(&s_owner[a], j);   // the last selector keeps i2; earlier ones were stolen
+            if (checkOri) atomicAdd(&s_hist[mt_rot_bin(f1.keys[j].angle, f2.keys[a].angle)], 1);
         }
-        m12[j] = out;
-        if (out >= 0) {
-            cnt++;
-            prev[2 * j] = f2.keys[out].x;
-            prev[2 * j + 1] = f2.keys[out].y;
+        SYNC();
+        if (threadIdx.x == 0) s_keep = checkOri ? mt_three_maxima_keep(s_hist) : 0xFFFFFFFFu;
+        SYNC();
+        int cnt = 0;
+        for (int j = threadIdx.x; j < f1.n; j += blockDim.x) {
+            const int a = assign[j];
+            int out = -1;
+            if (a >= 0 && s_owner[a] == j) {
+                out = a;
+                if (checkOri && !((s_keep >> mt_rot_bin(f1.keys[j].angle, f2.keys[a].angle)) & 1u)) out = -1;
+            }
+            m12[j] = out;
+            if (out >= 0) {
+                cnt++;
+                prev[2 * j] = f2.keys[out].x;
+                prev[2 * j + 1] = f2.keys[out].y;
+            }
         }
+        atomicAdd(&s_n, cnt);
     }
-    atomicAdd(&s_n, cnt);
+    // every wave's output stores complete, the barrier, one system-scope release, then the status
+    __builtin_amdgcn_s_waitcnt(0);
     SYNC();
-    if (threadIdx.x == 0) result[0] = s_n;
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        volatile int* st = st_host;
+        st[0] = run ? 0 : 1;
+        st[1] = run ? s_n : 0;
+        __threadfence_system();
+        st[4] = seq;
+        __threadfence_system();
+    }
 }
 
 // ---- SearchByBoW(KF, F) (ORBmatcher.cc:223-425): one thread per node present in both vectors.
@@ -4343,8 +4363,6 @@ static int sfi_core(const orbfe_frame* F1, const orbfe_frame* F2, float* prev_ma
     const size_t o_segoff = p.scratch((size_t)F2->n * 4);
     const size_t o_segcnt = p.scratch((size_t)F2->n * 4);
     const size_t o_changed = p.scratch(MT_MAX_PASSES * 4);
-    const size_t o_m12 = p.scratch((size_t)n1 * 4);
-    const size_t o_result = p.scratch(16);
     int rc = ms_prepare(p);
     if (rc) return rc;
     MsTimer timer;
@@ -4358,34 +4376,55 @@ static int sfi_core(const orbfe_frame* F1, const orbfe_frame* F2, float* prev_ma
     fill(assign, n1, -1);
     fill(adist, n1, 0);
     const dim3 gq((n1 + MT_INIT_WNT / 16 - 1) / (MT_INIT_WNT / 16));   // four queries per wave
-    int pass = 0;
+    // outputs in mapped pinned memory: matches12, then prevMatched (the input, updated by the commit)
+    MatchScratch& m = t_ms;
+    if (m.ocap < (size_t)n1 * 3) {
+        if (m.ho) HIPCHK(hipHostFree(m.ho));
+        m.ho = nullptr;
+        m.ocap = 0;
+        const size_t cap = std::max<size_t>((size_t)n1 * 3, 2048);
+        HIPCHK(hipHostMalloc((void**)&m.ho, cap * 4, hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostGetDevicePointer((void**)&m.ho_dev, m.ho, 0));
+        m.ocap = cap;
+    }
+    memcpy(m.ho + n1, prev_matched, (size_t)n1 * 8);
+    // gated passes (a pass after an unchanged one returns at once) and a gated commit per round trip:
+    // the host waits for the commit's status words, and enqueues more passes only when the last one
+    // still changed something
+    int pass = 0, batch = 3;
     while (true) {
-        for (int c = 0; c < 2; c++, pass++) {
+        for (int c = 0; c < batch; c++, pass++) {
             if (pass >= MT_MAX_PASSES) return ORBFE_E_CAPACITY;
+            const int* gate = pass ? changed + pass - 1 : nullptr;
             hipLaunchKernelGGL(k_init_state, dim3(1), dim3(1024), 0, s, assign, adist, n1, ms_ptr<uint32_t>(o_skey),
                                ms_ptr<int>(o_spmin), ms_ptr<int>(o_nsel), F2->n, ms_ptr<int>(o_segoff),
-                               ms_ptr<int>(o_segcnt));
+                               ms_ptr<int>(o_segcnt), gate);
             hipLaunchKernelGGL(k_init_eval, gq, dim3(MT_INIT_WNT), 0, s, v1, v2, ms_ptr<const float>(o_prev), windowSize,
                                nnratio, ms_ptr<const uint32_t>(o_skey), ms_ptr<const int>(o_spmin),
-                               ms_ptr<const int>(o_segoff), ms_ptr<const int>(o_segcnt), assign, adist, changed + pass);
+                               ms_ptr<const int>(o_segoff), ms_ptr<const int>(o_segcnt), assign, adist, changed + pass,
+                               gate);
         }
-        int ch = 0;
-        HIPCHK(hipMemcpyAsync(t_ms.hs, changed + pass - 1, 4, hipMemcpyDeviceToHost, s));   // pinned
-        HIPCHK(hipStreamSynchronize(s));
-        ch = t_ms.hs[0];
-        if (ch == 0) break;
+        const int seq = ++t_ms.seq;
+        hipLaunchKernelGGL(k_init_commit, dim3(1), dim3(1024), 0, s, v1, v2, assign, checkOri,
+                           (float*)(m.ho_dev + n1), m.ho_dev, changed + pass - 1, t_ms.hs_dev, seq);
+        HIPCHK(hipGetLastError());
+        timer.end();
+        volatile int* st = t_ms.hs;
+        for (unsigned spin = 1; host_seq_acquire(st) != seq; spin++) {
+            if ((spin & 1023) == 0) {   // bounded: a stream that finished without publishing is an error
+                const hipError_t e = hipStreamQuery(s);
+                if (e == hipSuccess && host_seq_acquire(st) != seq) return ORBFE_E_DEVICE;
+                if (e != hipSuccess && e != hipErrorNotReady) HIPCHK(e);
+            }
+            __builtin_ia32_pause();
+        }
+        if (st[0] == 0) {   // converged and committed: the outputs precede the status words
+            memcpy(matches12, m.ho, (size_t)n1 * 4);
+            memcpy(prev_matched, m.ho + n1, (size_t)n1 * 8);
+            return st[1];
+        }
+        batch = 4;
     }
-    hipLaunchKernelGGL(k_init_commit, dim3(1), dim3(1024), 0, s, v1, v2, assign, checkOri, ms_ptr<float>(o_prev),
-                       ms_ptr<int>(o_m12), ms_ptr<int>(o_result));
-    HIPCHK(hipGetLastError());
-    timer.end();
-    int nm = 0;
-    HIPCHK(hipMemcpyAsync(matches12, ms_ptr<int>(o_m12), (size_t)n1 * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(prev_matched, ms_ptr<float>(o_prev), (size_t)n1 * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(t_ms.hs, ms_ptr<int>(o_result), 4, hipMemcpyDeviceToHost, s));   // pinned
-    HIPCHK(hipStreamSynchronize(s));
-    nm = t_ms.hs[0];
-    return nm;
 }
 
 int orbfe_search_by_bow(const orbfe_keypoint* kf_keys, const uint8_t* kf_desc, const int32_t* kf_mp, int32_t kf_n,
