@@ -2620,45 +2620,64 @@ __global__ void k_mt_commit_write(int n, const int* qid, int q_stride_bytes, con
 __global__ __launch_bounds__(1024) void k_init_state(const int* assign, const int* adist, int nq, uint32_t* skey,
                                                      int* spmin, int* nsel, int n2, int* seg_off, int* seg_cnt,
                                                      const int* gate) {
+    // The selections (i2 << 16 | j) in (i2, j) order as a counting sort by i2: counts, one scan (the
+    // segment starts and lengths, written for every i2), atomic placement, then each segment's few
+    // selectors put back in j order by one thread (a bitonic network over the selections took ~10 us
+    // of barrier stages)
     __shared__ uint32_t s_k[MT_INIT_MAXQ];
-    __shared__ int s_cnt;
+    __shared__ int s_c[MT_INIT_MAXQ];
+    __shared__ int s_ws[16];
     if (gate && *gate == 0) return;   // the previous pass changed nothing: converged
-    if (threadIdx.x == 0) s_cnt = 0;
-    for (int i = threadIdx.x; i < n2; i += blockDim.x) seg_cnt[i] = 0;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    for (int i = tid; i < n2; i += nt) s_c[i] = 0;
     SYNC();
-    for (int j = threadIdx.x; j < nq; j += blockDim.x)
-        if (assign[j] >= 0) s_k[atomicAdd(&s_cnt, 1)] = ((uint32_t)assign[j] << 16) | (uint32_t)j;
+    for (int j = tid; j < nq; j += nt) {
+        const int a = assign[j];
+        if (a >= 0) atomicAdd(&s_c[a], 1);
+    }
     SYNC();
-    const int m = s_cnt;
-    int P = 1;
-    while (P < m) P <<= 1;
-    for (int i = m + threadIdx.x; i < P; i += blockDim.x) s_k[i] = 0xFFFFFFFFu;
+    const int per = (n2 + nt - 1) / nt, c0 = tid * per;
+    int sum = 0;
+    for (int u = 0; u < per; u++) sum += c0 + u < n2 ? s_c[c0 + u] : 0;
+    const int incl = wave_incl_scan_dpp(sum);
+    if ((tid & 63) == 63) s_ws[tid >> 6] = incl;
     SYNC();
-    for (int k = 2; k <= P; k <<= 1)
-        for (int jj = k >> 1; jj > 0; jj >>= 1) {
-            for (int i = threadIdx.x; i < P; i += blockDim.x) {
-                const int ixj = i ^ jj;
-                if (ixj > i) {
-                    const uint32_t a = s_k[i], c = s_k[ixj];
-                    if ((a > c) == ((i & k) == 0)) { s_k[i] = c; s_k[ixj] = a; }
-                }
-            }
-            SYNC();
+    int run = incl - sum;
+    for (int w = 0; w < (nt >> 6); w++) run += w < (tid >> 6) ? s_ws[w] : 0;
+    for (int u = 0; u < per; u++) {
+        const int c = c0 + u;
+        if (c >= n2) break;
+        const int v = s_c[c];
+        seg_off[c] = run;
+        seg_cnt[c] = v;
+        s_c[c] = run;   // placement cursor
+        run += v;
+    }
+    SYNC();
+    for (int j = tid; j < nq; j += nt) {
+        const int a = assign[j];
+        if (a >= 0) s_k[atomicAdd(&s_c[a], 1)] = ((uint32_t)a << 16) | (uint32_t)j;
+    }
+    SYNC();
+    // s_c[i2] is now the end of i2's segment: j order inside it, then the segmented prefix-min of
+    // the selecting distances
+    for (int c = tid; c < n2; c += nt) {
+        const int b = s_c[c], a0 = b - seg_cnt[c];
+        if (b <= a0) continue;
+        for (int x = a0 + 1; x < b; x++) {
+            const uint32_t v = s_k[x];
+            int y = x - 1;
+            while (y >= a0 && s_k[y] > v) { s_k[y + 1] = s_k[y]; y--; }
+            s_k[y + 1] = v;
         }
-    // segmented prefix-min of distances (segments = equal i2); sequential per segment start
-    for (int i = threadIdx.x; i < m; i += blockDim.x) {
-        skey[i] = s_k[i];
-        if (i == 0 || (s_k[i - 1] >> 16) != (s_k[i] >> 16)) {
-            int cur = MT_INF, t = i;
-            for (; t < m && (s_k[t] >> 16) == (s_k[i] >> 16); t++) {
-                cur = min(cur, adist[s_k[t] & 0xFFFFu]);
-                spmin[t] = cur;
-            }
-            seg_off[s_k[i] >> 16] = i;
-            seg_cnt[s_k[i] >> 16] = t - i;
+        int cur = MT_INF;
+        for (int t = a0; t < b; t++) {
+            cur = min(cur, adist[s_k[t] & 0xFFFFu]);
+            spmin[t] = cur;
+            skey[t] = s_k[t];
         }
     }
-    if (threadIdx.x == 0) *nsel = m;
+    if (tid == nt - 1) *nsel = run;   // the last thread's running sum: every count
 }
 
 // One query per DPP row of 16 lanes (four per wave): lane l walks the window's grid columns
