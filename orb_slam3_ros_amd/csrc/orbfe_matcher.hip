@@ -3572,12 +3572,16 @@ int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* m
     const size_t o_track = fin ? p.scratch((size_t)nq * sizeof(orbfe_map_point)) : 0;
     const size_t o_ntm = fin ? p.scratch(16) : 0;
     const size_t o_stats = t_stats ? p.scratch(24) : 0;
-    const size_t o_qdev = (!dev && !fin && !lp) ? p.scratch((size_t)nq * qstride) : 0;
+#ifndef ORBFE_BLK_DMA
+#define ORBFE_BLK_DMA 0
+#endif
     // host-API calls: zero copy both ways. The kernel reads its inputs straight from the mapped pinned
     // staging and writes the slots into mapped pinned memory; the host waits for the status words
-    // only (no DMA, no stream synchronisation: the call is one launch).
-    const bool zc = !dev;
-    int rc = ms_prepare(p, zc);
+    // only (no DMA, no stream synchronisation: the call is one launch). (ORBFE_BLK_DMA: inputs by one
+    // DMA instead, an A/B build.)
+    const bool zc = !dev, zin = zc && !ORBFE_BLK_DMA;
+    const size_t o_qdev = (!dev && !fin && !lp && zin) ? p.scratch((size_t)nq * qstride) : 0;
+    int rc = ms_prepare(p, zin);
     if (rc) return rc;
     MatchScratch& m = t_ms;
     if (zc && m.ocap < (size_t)n) {
@@ -3589,7 +3593,7 @@ int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* m
         HIPCHK(hipHostGetDevicePointer((void**)&m.ho_dev, m.ho, 0));
         m.ocap = cap;
     }
-    fp.zc = zc;
+    fp.zc = zin;
     hipStream_t s = dev ? dev->caller : t_ms.stream;
     if (dev) HIPCHK(ms_after_tail(s));
     unsigned long long* stats = t_stats ? ms_ptr<unsigned long long>(o_stats) : nullptr;
@@ -3597,7 +3601,7 @@ int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* m
     if (stats) HIPCHK(hipMemsetAsync(stats, 0, 24, s));
     MsTimer timer(s);
     const FrameDev fr = fp.view();
-    const uint8_t* q = dev ? (const uint8_t*)(fin ? (const void*)fin->pts : queries) : up_ptr<const uint8_t>(o_q, zc);
+    const uint8_t* q = dev ? (const uint8_t*)(fin ? (const void*)fin->pts : queries) : up_ptr<const uint8_t>(o_q, zin);
     int* ntm = fin ? ms_ptr<int>(o_ntm) : nullptr;
     if (fin) {   // Tracking::SearchLocalPoints' isInFrustum, then the search (nothing in view: no match)
         CamDev cd;
@@ -3613,16 +3617,16 @@ int sbp_block_run(int mode, const orbfe_frame* F, int32_t* mvp, const int32_t* m
     }
     if (lp) {   // SearchByProjection(CurrentFrame, LastFrame)'s projection on the device
         hipLaunchKernelGGL(k_last_proj, dim3((nq + MT_NT - 1) / MT_NT), dim3(MT_NT), 0, s, *lp,
-                           up_ptr<const orbfe_last_point>(o_q, zc), nq, ms_ptr<orbfe_proj_point>(o_rec), (float2*)nullptr);
+                           up_ptr<const orbfe_last_point>(o_q, zin), nq, ms_ptr<orbfe_proj_point>(o_rec), (float2*)nullptr);
         q = ms_ptr<const uint8_t>(o_rec);
     }
-    const int32_t* mvp_in = dev ? mvp : up_ptr<const int32_t>(o_mvp, zc);
+    const int32_t* mvp_in = dev ? mvp : up_ptr<const int32_t>(o_mvp, zin);
     int32_t* mvp_out = dev ? mvp : m.ho_dev;
-    const int32_t* obs_d = mode == 2 ? nullptr : dev ? mvp_obs : up_ptr<const int32_t>(o_obs, zc);
+    const int32_t* obs_d = mode == 2 ? nullptr : dev ? mvp_obs : up_ptr<const int32_t>(o_obs, zin);
     const int seq = ++t_ms.seq;
     if (zc) memcpy(m.ho, mvp, (size_t)n * 4);   // the slots the search leaves alone keep their value
     const BlkIO io{mvp_in, obs_d, mvp_out, (int)qstride, (int)qid_off, (int)qangle_off, checkOri, ntm, t_ms.hs_dev, seq,
-                   stats, (!dev && !fin && !lp) ? ms_ptr<uint4>(o_qdev) : nullptr};
+                   stats, (!dev && !fin && !lp && zin) ? ms_ptr<uint4>(o_qdev) : nullptr};
     const bool two4 = F->two_cams && mode == 0;
     const size_t lds = two4 ? blk_lds(n, F->nlevels, gm, 2, blk4_bytes_per_kp()) : blk_lds(n, F->nlevels, gm);
     if (two4)

@@ -4,7 +4,7 @@
 # run's per-frame slots compared with the CPU twin's (tests/native/tracking_cpu).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-D=gpurun_out/enum_ab
+D=/tmp/enum_ab
 mkdir -p $D
 python3 -c "import bench; bench.write_sequence_job('$D/seq.bin', 60); bench.write_sequence_job('$D/kb8.bin', 60, 512, 512, 1000, 20, 31, (256.0, 256.0))" || exit 1
 timeout -k 10 300 tests/native/tracking_cpu 60 $D/seq.bin $D/cpu.out > /dev/null || exit 1
@@ -22,3 +22,10 @@ t = json.loads(open('$D/t.json').read().strip().splitlines()[-1]); k = json.load
 print('$n', 'pinhole', t['tracking_frame_ms'], t['split_ms'], '$a', '| kb8', k['tracking_frame_ms'], k['split_ms'], '$b')"
   done
 done
+# the host-API KF search (bench.matcher_calls) with each variant
+for r in 1 2; do for d in variants_lat/*/; do
+  ORBFE_LIB_PARTIAL=1 ORBFE_LIB=$PWD/$d/liborbfe.so timeout -k 10 120 python3 -c "
+import bench
+r = bench.matcher_calls(20)['calls']
+print('$(basename $d)', {k: (v['ms_per_call'], v['device_ms_per_call'], v['parity_ok']) for k, v in r.items() if 'keyframe' in k})" || exit 1
+done; done
