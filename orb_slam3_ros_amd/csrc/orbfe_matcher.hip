@@ -1340,7 +1340,9 @@ __global__ __launch_bounds__(MT_BLK_NT) void k_sbp_block(FrameDev fr, BlkGeom gm
 // the fixed point, the last-writer commit and the rotation histogram over all entries
 // (:1860-1884) run in the block as in k_sbp_block<1>. Up to MT_BLOCK_MAXQ points: two per thread,
 // four entries.
+#ifndef MT_BLK2_LIST
 #define MT_BLK2_LIST 8
+#endif
 #ifdef ORBFE_BLK2_STAMPS   // diagnostic build (tools/build_variant.sh): phase times of thread 0, printed
 #define BLK2_STAMP(k) do { if (threadIdx.x == 0) t_st[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
