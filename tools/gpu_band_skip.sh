@@ -19,5 +19,8 @@ rows = list(csv.reader(open(f)))[1:]
 tot = sum(float(r[2]) for r in rows if "k_sbp_band" in r[0])
 cnt = sum(int(r[1]) for r in rows if "k_sbp_band" in r[0])
 print(f"{sys.argv[2]:5s} th {sys.argv[3]:>2s}: k_sbp_band {cnt} launches, {tot / 1e3 / 30:.1f} us per call")
+allk = sum(float(r[2]) for r in rows if not r[0].startswith("__amd"))
+cw = [float(r[3]) / 1e3 for r in rows if "k_mt_commit_write" in r[0]]
+print(f"      all kernels {allk / 1e3 / 30:.1f} us per call; k_mt_commit_write mean {cw[0] if cw else 0:.2f} us")
 PY
 done; done; done
