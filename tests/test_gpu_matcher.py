@@ -842,3 +842,45 @@ def test_sbp_multi_degenerate(gpu, om):
     assert ORBmatcher(0.8).SearchByProjectionLocalMap(F, a, obs0, mps, 1) == \
         om.OracleMatcher(0.8).sbp_local(F, b, obs0, mps, 1)
     np.testing.assert_array_equal(a, b)
+
+
+def _crowd(F, rng, k, x, y, octave=0):
+    """k of F's keypoints moved into one grid cell / band bucket (within a pixel of (x, y))."""
+    idx = rng.choice(F.N, k, replace=False)
+    F.keys["x"][idx] = x + rng.uniform(-0.4, 0.4, k)
+    F.keys["y"][idx] = y + rng.uniform(-0.4, 0.4, k)
+    F.keys["octave"][idx] = octave
+    return MatchFrame(F.keys, F.desc, F.bounds, F.scale_factors, F.uright, F.mbf)
+
+
+def test_search_for_initialization_crowded_cell(gpu, om):
+    """More than 32 of F2's level-0 keypoints in one grid cell: k_mt_grid's bitonic fallback (the
+    counting sort keeps at most 32 per cell in index order)."""
+    rng = np.random.default_rng(77)
+    F1 = sm.synth_frame(rng, 2000, stereo=False)
+    F2, _ = sm.perturbed_frame(rng, F1, shift=(3.0, -2.0), jitter=1.0, rot=8.0, flip_p=0.05, drop=0.1)
+    F2 = _crowd(F2, rng, 120, 300.0, 200.0)
+    prev0 = np.stack([F1.keys["x"], F1.keys["y"]], 1).astype(np.float32)
+    pa, pb = prev0.copy(), prev0.copy()
+    ma, mb = np.zeros(F1.N, np.int32), np.zeros(F1.N, np.int32)
+    ng = ORBmatcher(0.9, True).SearchForInitialization(F1, F2, pa, ma, 100)
+    no = om.OracleMatcher(0.9, True).search_for_init(F1, F2, pb, mb, 100)
+    assert ng == no
+    np.testing.assert_array_equal(ma, mb)
+    np.testing.assert_array_equal(pa, pb)
+
+
+@pytest.mark.parametrize("th", [5, 15])
+def test_sbp_local_band_crowded_bucket(gpu, om, th):
+    """k_sbp_band over a band index with one (octave, band) bucket of 150 keypoints (the index's
+    bitonic fallback) against the oracle; 5,000 points, so the multi-block band passes run."""
+    rng = np.random.default_rng(91 + th)
+    F = sm.synth_frame(rng, 1000)
+    F = _crowd(F, rng, 150, 400.0, 243.0, octave=1)
+    mps = sm.synth_local_map(rng, F, 5000)
+    mvp0, obs = sm.initial_slots(rng, F.N)
+    a, b = mvp0.copy(), mvp0.copy()
+    ng = ORBmatcher(0.8).SearchByProjectionLocalMap(F, a, obs, mps, th)
+    no = om.OracleMatcher(0.8).sbp_local(F, b, obs, mps, th)
+    assert ng == no
+    np.testing.assert_array_equal(a, b)
