@@ -22,3 +22,10 @@ t = json.loads(open('$D/t.json').read().strip().splitlines()[-1]); k = json.load
 print('$n', 'pinhole', t['tracking_frame_ms'], t['split_ms'], '$a', '| kb8', k['tracking_frame_ms'], k['split_ms'], '$b')"
   done
 done
+# the host-API calls (bench.matcher_calls) with each variant
+for r in 1 2; do for d in variants_lat/*/; do
+  ORBFE_LIB_PARTIAL=1 ORBFE_LIB=$PWD/$d/liborbfe.so timeout -k 10 120 python3 -c "
+import bench
+r = bench.matcher_calls(20)['calls']
+print('$(basename $d)', {k[:24]: (v['ms_per_call'], v['device_ms_per_call'], v['parity_ok']) for k, v in r.items()})" || exit 1
+done; done
